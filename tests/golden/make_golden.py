@@ -1,0 +1,461 @@
+"""Generate the golden parity fixtures by running the REFERENCE env core in this container.
+
+This script is the only place that imports the reference (read-only, /root/reference).  It runs
+here, never on the GPU box; only its outputs (``tests/golden/*.npz``, ``*.json``) travel.  The
+fixtures are data: inputs and the reference's outputs for them.
+
+Recipe:
+  * ``PYTHONPATH=<stubdir>:/root/reference/server``, ``TZ=UTC``;
+  * ``<stubdir>/perlin_noise`` is an import-only stub whose ``noise()`` raises, so perlin mode can
+    never silently produce a fixture (perlin parity is unpinned);
+  * three ``sys.modules`` shims let the controller modules import without the server stack
+    (``app.core.agents.controllers`` package init pulls cvxpy/v0; ``parser_service`` and
+    ``app.utils.logger`` pull pydantic-v1 ``BaseSettings``).
+
+Fixtures (names follow SURVEY §8(c) F1..F9):
+  F1 lockout.npz       HVAC.step sequences, L in {12, 40}, dt in {4, 3}, random action strings
+  F2 thermal.npz       Building.update_temperature over a random grid (Ua ~1 and 218, on/off, dt)
+  F3 solar.npz         compute_solar_gain over a (month, day, hour, minute) sweep
+  F4 signal.npz        flat / sinusoidals / regular_steps signals over a datetime sweep
+  F5 rewards.npz       RewardsCalculator in all 4 penalty modes
+  F6 traj_*.npz        seeded end-to-end trajectories (Environment.reset/step + norm_state_dict)
+  F7 greedy.npz        GreedyMyopic decisions along a trajectory
+  F8 comm.json         neighbour tables for the deterministic comm modes (+ random_fixed seeded)
+  F9 rng_order.npz     population after 1 and 3 resets for seeds {0, 4, 123}
+
+Usage:  python tests/golden/make_golden.py   (writes next to this file)
+"""
+from __future__ import annotations
+
+import copy
+import datetime as dt
+import json
+import os
+import random
+import sys
+import tempfile
+import types
+
+import numpy as np
+
+REF = "/root/reference/server"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _install_stubs() -> None:
+    os.environ["TZ"] = "UTC"
+    os.environ.setdefault("MPLBACKEND", "Agg")
+    stub = tempfile.mkdtemp(prefix="mdr_refstub_")
+    os.makedirs(os.path.join(stub, "perlin_noise"))
+    with open(os.path.join(stub, "perlin_noise", "__init__.py"), "w") as f:
+        f.write(
+            "class PerlinNoise:\n"
+            "    def __init__(self, octaves=1, seed=None):\n"
+            "        self.octaves, self.seed = octaves, seed\n"
+            "    def noise(self, *a, **k):\n"
+            "        raise RuntimeError('perlin_noise is absent: perlin parity is unpinned')\n"
+        )
+    sys.path[:0] = [stub, REF]
+    import logging
+
+    lg = types.ModuleType("app.utils.logger")
+    lg.logger = logging.getLogger("ref")
+    sys.modules["app.utils.logger"] = lg
+    ps = types.ModuleType("app.services.parser_service")
+    ps.MarlConfig = object
+    sys.modules["app.services.parser_service"] = ps
+    ctl = types.ModuleType("app.core.agents.controllers")
+    ctl.__path__ = [os.path.join(REF, "app/core/agents/controllers")]
+    sys.modules["app.core.agents.controllers"] = ctl
+
+
+_install_stubs()
+
+from app.core.environment.environment import Environment  # noqa: E402
+from app.core.environment.environment_properties import EnvironmentProperties  # noqa: E402
+from app.core.environment.cluster.hvac import HVAC  # noqa: E402
+from app.core.environment.cluster.building import Building  # noqa: E402
+from app.core.environment.environment_properties import (  # noqa: E402
+    BuildingProperties,
+    HvacProperties,
+    RewardProperties,
+)
+from app.core.environment.power_grid.signal_calculator import SignalCalculator  # noqa: E402
+from app.core.environment.power_grid.power_grid_properties import SignalProperties  # noqa: E402
+from app.core.environment.rewards_calculator import RewardsCalculator  # noqa: E402
+from app.core.environment.cluster.agent_communication_builder import (  # noqa: E402
+    AgentCommunicationBuilder,
+)
+from app.core.environment.cluster.cluster_properties import (  # noqa: E402
+    AgentsCommunicationProperties,
+)
+from app.utils.utils import compute_solar_gain  # noqa: E402
+from app.utils.norm import norm_state_dict  # noqa: E402
+from app.core.agents.controllers.bangbang_controllers import (  # noqa: E402
+    DeadbandBangBangController,
+    BangBangController,
+)
+from app.core.agents.controllers import greedy_myopic_controller as greedy_mod  # noqa: E402
+
+MARL_JSON = os.path.join(REF, "app/core/config/MARLconfig.json")
+
+
+def env_prop_json() -> dict:
+    with open(MARL_JSON) as f:
+        return json.load(f)["env_prop"]
+
+
+def make_props(overrides: dict) -> EnvironmentProperties:
+    d = copy.deepcopy(env_prop_json())
+    for path, val in overrides.items():
+        cur = d
+        keys = path.split(".")
+        for k in keys[:-1]:
+            cur = cur[k]
+        cur[keys[-1]] = val
+    return EnvironmentProperties.parse_obj(d)
+
+
+def epoch(t: dt.datetime) -> float:
+    return (t - dt.datetime(1970, 1, 1)).total_seconds()
+
+
+# ---------------------------------------------------------------------------------------- F1
+def gen_lockout() -> None:
+    rs = np.random.RandomState(11)
+    out = {}
+    cases = [(12, 4), (40, 4), (40, 3), (10, 4)]
+    for ci, (L, step) in enumerate(cases):
+        hv = HVAC(HvacProperties(lockout_duration=L))
+        T = 300
+        acts = rs.randint(0, 2, size=T).astype(np.uint8)
+        # bias some strings toward long on / off runs
+        if ci % 2 == 1:
+            acts = np.repeat(rs.randint(0, 2, size=T // 10), 10).astype(np.uint8)
+        on = np.zeros(T, np.uint8)
+        lock = np.zeros(T, np.uint8)
+        sso = np.zeros(T, np.int64)
+        for t in range(T):
+            hv.step(bool(acts[t]), dt.timedelta(seconds=step))
+            on[t], lock[t], sso[t] = bool(hv.turned_on), bool(hv.lockout), hv.seconds_since_off
+        out[f"c{ci}_L"] = np.int64(L)
+        out[f"c{ci}_dt"] = np.int64(step)
+        out[f"c{ci}_action"] = acts
+        out[f"c{ci}_on"] = on
+        out[f"c{ci}_lock"] = lock
+        out[f"c{ci}_sso"] = sso
+    out["ncases"] = np.int64(len(cases))
+    np.savez_compressed(os.path.join(OUT, "lockout.npz"), **out)
+
+
+# ---------------------------------------------------------------------------------------- F2
+def gen_thermal() -> None:
+    rs = np.random.RandomState(12)
+    M = 600
+    cols = {k: np.zeros(M) for k in
+            ("Ua", "Ca", "Cm", "Hm", "T", "Tm", "Tod", "cap", "solar_gain", "T_new", "Tm_new")}
+    on = np.zeros(M, np.uint8)
+    step = np.zeros(M, np.int64)
+    stamp = np.zeros(M, np.float64)
+    solar_flag = np.zeros(M, np.uint8)
+    base = dt.datetime(2021, 1, 1)
+    for i in range(M):
+        bp = BuildingProperties()
+        b = Building(bp)
+        ua = rs.uniform(0.9, 1.1) if i % 2 == 0 else 218.0 * rs.uniform(0.9, 1.1)
+        b.init_props.Ua = ua
+        b.init_props.Ca = 9.08e5 * rs.uniform(0.9, 1.1)
+        b.init_props.Cm = 3.45e6 * rs.uniform(0.9, 1.1)
+        b.init_props.Hm = 2.84e3 * rs.uniform(0.9, 1.1)
+        b.init_props.solar_gain = bool(i % 5 != 4)
+        b.indoor_temp = rs.uniform(10, 35)
+        b.current_mass_temp = rs.uniform(10, 35)
+        b.hvac.turned_on = bool(rs.randint(0, 2))
+        b.hvac.init_props.cooling_capacity = float(rs.choice([12500, 15000, 17500]))
+        s = int(rs.choice([1, 4, 4, 4, 60]))
+        when = base + dt.timedelta(days=int(rs.randint(0, 364)), seconds=int(rs.randint(0, 86400)))
+        tod = rs.uniform(10, 40)
+        cols["Ua"][i], cols["Ca"][i] = b.init_props.Ua, b.init_props.Ca
+        cols["Cm"][i], cols["Hm"][i] = b.init_props.Cm, b.init_props.Hm
+        cols["T"][i], cols["Tm"][i], cols["Tod"][i] = b.indoor_temp, b.current_mass_temp, tod
+        cols["cap"][i] = b.hvac.init_props.cooling_capacity
+        on[i], step[i], stamp[i] = b.hvac.turned_on, s, epoch(when)
+        solar_flag[i] = b.init_props.solar_gain
+        b.update_temperature(tod, dt.timedelta(seconds=s), when)
+        cols["T_new"][i], cols["Tm_new"][i] = b.indoor_temp, b.current_mass_temp
+        cols["solar_gain"][i] = b.current_solar_gain
+    np.savez_compressed(os.path.join(OUT, "thermal.npz"), on=on, dt=step, epoch=stamp,
+                        solar_flag=solar_flag, **cols)
+
+
+# ---------------------------------------------------------------------------------------- F3
+def gen_solar() -> None:
+    stamps, vals = [], []
+    for month in range(1, 13):
+        for day in (1, 9, 15, 28):
+            for minute_of_day in range(0, 24 * 60, 7):
+                t = dt.datetime(2021, month, day, minute_of_day // 60, minute_of_day % 60)
+                stamps.append(epoch(t))
+                vals.append(compute_solar_gain(t, 7.175, 0.67))
+    np.savez_compressed(os.path.join(OUT, "solar.npz"), epoch=np.array(stamps),
+                        gain=np.array(vals, np.float64))
+
+
+# ---------------------------------------------------------------------------------------- F4
+def gen_signal() -> None:
+    out = {}
+    t0 = dt.datetime(2021, 3, 7, 0, 0, 0)
+    stamps = [t0 + dt.timedelta(seconds=4 * k + (k % 7)) for k in range(0, 24 * 900, 9)]
+    out["epoch"] = np.array([epoch(t) for t in stamps])
+    for mode in ("flat", "sinusoidals", "regular_steps"):
+        for nb in (50, 1000):
+            sp = SignalProperties(mode=mode)
+            sc = SignalCalculator(sp, nb)
+            base = 4200.0 * nb
+            out[f"{mode}_{nb}"] = np.array([float(sc.compute_signal(base, t)) for t in stamps])
+    # non-default amplitude / period settings
+    sp = SignalProperties(mode="sinusoidals", amplitude_ratios=[0.2, 0.05, 0.1],
+                          periods=[300, 900, 3600])
+    sc = SignalCalculator(sp, 77)
+    out["sinusoidals_custom_77"] = np.array([float(sc.compute_signal(77 * 3900.0, t)) for t in stamps])
+    sp = SignalProperties(mode="regular_steps", amplitude_per_hvac=5000, period=600)
+    sc = SignalCalculator(sp, 77)
+    out["regular_steps_custom_77"] = np.array([float(sc.compute_signal(77 * 3900.0, t)) for t in stamps])
+    np.savez_compressed(os.path.join(OUT, "signal.npz"), **out)
+
+
+# ---------------------------------------------------------------------------------------- F5
+def gen_rewards() -> None:
+    rs = np.random.RandomState(15)
+    out = {}
+    N = 8
+    bp = BuildingProperties(target_temp=19.0, deadband=0.5)
+    buildings = []
+    for i in range(N):
+        b = Building(bp)
+        b.init_props.target_temp = 19.0 + abs(rs.normal())
+        b.indoor_temp = rs.uniform(16, 24)
+        buildings.append(b)
+    out["target"] = np.array([b.init_props.target_temp for b in buildings])
+    out["T"] = np.array([b.indoor_temp for b in buildings])
+    out["deadband"] = np.float64(0.5)
+    out["P"] = np.float64(41000.0)
+    out["S"] = np.float64(36517.25)
+    for mode in ("individual_L2", "common_L2", "common_max_error", "mixture"):
+        rp = RewardProperties()
+        rp.penalty_props.mode = mode
+        rp.penalty_props.alpha_common_max = 0.5 if mode == "mixture" else 0.0
+        rc = RewardsCalculator(rp, bp)
+        r = rc.compute_rewards(buildings, 41000.0, 36517.25)
+        out[f"reward_{mode}"] = np.array([r[i] for i in range(N)])
+    np.savez_compressed(os.path.join(OUT, "rewards.npz"), **out)
+
+
+# ---------------------------------------------------------------------------------------- F6
+POP_KEYS = ("Ua", "Ca", "Cm", "Hm", "target_temp", "cooling_capacity")
+
+
+def population(env) -> dict:
+    bs = env.cluster.buildings
+    return {
+        "Ua": np.array([b.init_props.Ua for b in bs]),
+        "Ca": np.array([b.init_props.Ca for b in bs]),
+        "Cm": np.array([b.init_props.Cm for b in bs]),
+        "Hm": np.array([b.init_props.Hm for b in bs]),
+        "target_temp": np.array([b.init_props.target_temp for b in bs]),
+        "cooling_capacity": np.array([float(b.hvac.init_props.cooling_capacity) for b in bs]),
+        "init_air_temp_noised": np.array([b.init_props.init_air_temp for b in bs]),
+    }
+
+
+def record_obs(obs: dict, N: int) -> dict:
+    o = [obs[i] for i in range(N)]
+    return {
+        "T": np.array([x["indoor_temp"] for x in o], np.float64),
+        "Tm": np.array([x["mass_temp"] for x in o], np.float64),
+        "on": np.array([bool(x["turned_on"]) for x in o], np.uint8),
+        "lock": np.array([bool(x["lockout"]) for x in o], np.uint8),
+        "sso": np.array([x["seconds_since_off"] for x in o], np.int64),
+        "P": np.float64(o[0]["cluster_hvac_power"]),
+        "S": np.float64(o[0]["reg_signal"]),
+        "Tod": np.float64(o[0]["OD_temp"]),
+        "G": np.float64(o[0]["solar_gain"]),
+        "epoch": np.float64(epoch(o[0]["datetime"])),
+        # one neighbour message per house, first in comm order (checks message fields)
+        "msg0_diff": np.array([x["message"][0]["current_temp_diff_to_target"] if x["message"] else 0.0
+                               for x in o], np.float64),
+        "msg0_curr": np.array([x["message"][0]["curr_consumption"] if x["message"] else 0.0
+                               for x in o], np.float64),
+    }
+
+
+def gen_traj(name: str, overrides: dict, N: int, T: int, seed: int, controller: str,
+             norm_ticks=(0, 1, 2, 50), resets: int = 3, action_seed: int = 1234) -> None:
+    overrides = dict(overrides)
+    overrides["cluster_prop.nb_agents"] = N
+    props = make_props(overrides)
+    random.seed(seed)
+    env = Environment(props)
+    obs = None
+    for _ in range(resets - 1):
+        obs = env.reset()
+    if obs is None:
+        obs = env.get_obs()
+    pop = population(env)
+    rs = np.random.RandomState(action_seed)
+    if controller == "random":
+        actions = rs.randint(0, 2, size=(T, N)).astype(np.uint8)
+    else:
+        actions = np.zeros((T, N), np.uint8)
+    ctl = None
+    if controller == "deadband_bbc":
+        ctl = [DeadbandBangBangController({"id": i}, None) for i in range(N)]
+    elif controller == "bbc":
+        ctl = [BangBangController({"id": i}, None) for i in range(N)]
+    rec = {k: [] for k in record_obs(obs, N)}
+    rec["reward"] = []
+    o0 = record_obs(obs, N)
+    norms = {}
+    if 0 in norm_ticks:
+        norms["norm_t0"] = np.array(norm_state_dict(obs, env.init_props))
+    for t in range(T):
+        if ctl is not None:
+            a = {i: ctl[i].act(obs) for i in range(N)}
+            actions[t] = [bool(a[i]) for i in range(N)]
+        else:
+            a = {i: bool(actions[t, i]) for i in range(N)}
+        obs, rew = env.step(a)
+        r = record_obs(obs, N)
+        for k, v in r.items():
+            rec[k].append(v)
+        rec["reward"].append(np.array([rew[i] for i in range(N)], np.float64))
+        if (t + 1) in norm_ticks:
+            norms[f"norm_t{t + 1}"] = np.array(norm_state_dict(obs, env.init_props))
+    out = {f"pop_{k}": v for k, v in pop.items()}
+    out.update({f"init_{k}": v for k, v in o0.items()})
+    out.update({f"traj_{k}": np.stack(v) if np.ndim(v[0]) else np.array(v) for k, v in rec.items()})
+    out.update(norms)
+    out["actions"] = actions
+    out["N"], out["T"], out["seed"], out["resets"] = np.int64(N), np.int64(T), np.int64(seed), np.int64(resets)
+    meta = {"overrides": overrides, "controller": controller, "N": N, "T": T, "seed": seed,
+            "resets": resets, "action_seed": action_seed, "norm_ticks": list(norm_ticks)}
+    out["meta_json"] = np.frombuffer(json.dumps(meta).encode(), np.uint8)
+    np.savez_compressed(os.path.join(OUT, f"traj_{name}.npz"), **out)
+
+
+# ---------------------------------------------------------------------------------------- F7
+def gen_greedy() -> None:
+    N, T = 120, 25
+    props = make_props({"cluster_prop.nb_agents": N,
+                        "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    random.seed(7)
+    env = Environment(props)
+    obs = env.reset()
+    greedy_mod.global_myopic_memory[0] = None
+    greedy_mod.global_myopic_memory[1] = None
+    ctl = [greedy_mod.GreedyMyopic({"id": i}, None) for i in range(N)]
+    rec = {"T": [], "target": [], "cap": [], "lock": [], "S": [], "action": []}
+    for t in range(T):
+        a = {i: int(ctl[i].act(obs)) for i in range(N)}
+        rec["T"].append([obs[i]["indoor_temp"] for i in range(N)])
+        rec["target"].append([obs[i]["target_temp"] for i in range(N)])
+        rec["cap"].append([float(obs[i]["cooling_capacity"]) for i in range(N)])
+        rec["lock"].append([bool(obs[i]["lockout"]) for i in range(N)])
+        rec["S"].append(float(obs[0]["reg_signal"]))
+        rec["action"].append([a[i] for i in range(N)])
+        obs, _ = env.step(a)
+    out = {k: np.array(v) for k, v in rec.items()}
+    out["cop"] = np.float64(2.5)
+    np.savez_compressed(os.path.join(OUT, "greedy.npz"), **out)
+
+
+# ---------------------------------------------------------------------------------------- F8
+def gen_comm() -> None:
+    out = {}
+    for mode, ns in (("neighbours", (2, 3, 7, 11, 50)), ("closed_groups", (7, 11, 25, 50, 53)),
+                     ("neighbours_2D", (25, 50, 100))):
+        for n in ns:
+            for kmax in (10, 4):
+                p = AgentsCommunicationProperties(mode=mode, max_nb_agents_communication=kmax,
+                                                  row_size=5 if n != 100 else 10,
+                                                  max_communication_distance=2 if n != 25 else 1)
+                try:
+                    links = AgentCommunicationBuilder(p, n).get_comm_link_list()
+                    out[f"{mode}_{n}_{kmax}"] = [[int(j) for j in links[i]] for i in range(n)]
+                except ValueError as e:
+                    out[f"{mode}_{n}_{kmax}"] = "ValueError: " + str(e)
+    random.seed(99)
+    p = AgentsCommunicationProperties(mode="random_fixed", max_nb_agents_communication=4)
+    links = AgentCommunicationBuilder(p, 12).get_comm_link_list()
+    out["random_fixed_12_4_seed99"] = [[int(j) for j in links[i]] for i in range(12)]
+    with open(os.path.join(OUT, "comm.json"), "w") as f:
+        json.dump(out, f)
+
+
+# ---------------------------------------------------------------------------------------- F9
+def gen_rng_order() -> None:
+    out = {}
+    for seed in (0, 4, 123):
+        for mode in ("random", "fixed"):
+            props = make_props({"cluster_prop.nb_agents": 20, "start_datetime_mode": mode,
+                                "power_grid_prop.signal_properties.mode": "flat"})
+            random.seed(seed)
+            env = Environment(props)
+            p1 = population(env)
+            e1 = epoch(env.date_time)
+            env.reset()
+            env.reset()
+            p3 = population(env)
+            e3 = epoch(env.date_time)
+            for k, v in p1.items():
+                out[f"s{seed}_{mode}_r1_{k}"] = v
+            for k, v in p3.items():
+                out[f"s{seed}_{mode}_r3_{k}"] = v
+            out[f"s{seed}_{mode}_r1_epoch"] = np.float64(e1)
+            out[f"s{seed}_{mode}_r3_epoch"] = np.float64(e3)
+            out[f"s{seed}_{mode}_r3_Tod"] = np.float64(env.current_od_temp)
+            out[f"s{seed}_{mode}_r3_next_random"] = np.float64(random.random())
+    np.savez_compressed(os.path.join(OUT, "rng_order.npz"), **out)
+
+
+def main() -> None:
+    with open(os.path.join(OUT, "marl_env_prop.json"), "w") as f:
+        json.dump(env_prop_json(), f, indent=1, sort_keys=True)
+    gen_lockout()
+    gen_thermal()
+    gen_solar()
+    gen_signal()
+    gen_rewards()
+    sig = "power_grid_prop.signal_properties.mode"
+    gen_traj("c1_sin_dbbc", {sig: "sinusoidals"}, N=50, T=200, seed=4, controller="deadband_bbc")
+    gen_traj("c1_flat_random", {sig: "flat"}, N=50, T=200, seed=4, controller="random")
+    gen_traj("fixed_steps_bbc", {sig: "regular_steps", "start_datetime_mode": "fixed",
+                                 "cluster_prop.house_prop.deadband": 0.5},
+             N=37, T=150, seed=123, controller="bbc", resets=1)
+    gen_traj("n400_random_common", {sig: "sinusoidals",
+                                    "reward_prop.penalty_props.mode": "common_L2"},
+             N=400, T=40, seed=0, controller="random", norm_ticks=(0, 40))
+    gen_traj("n64_mixture_2d", {sig: "flat", "reward_prop.penalty_props.mode": "mixture",
+                                "reward_prop.penalty_props.alpha_common_max": 0.5,
+                                "cluster_prop.agents_comm_prop.mode": "neighbours_2D",
+                                "cluster_prop.agents_comm_prop.row_size": 8,
+                                "cluster_prop.house_prop.solar_gain": False,
+                                "time_step": 60},
+             N=64, T=60, seed=5, controller="deadband_bbc", norm_ticks=(0, 60))
+    gen_traj("n30_maxerr_groups_hvacmsg", {sig: "sinusoidals",
+                                           "reward_prop.penalty_props.mode": "common_max_error",
+                                           "cluster_prop.agents_comm_prop.mode": "closed_groups",
+                                           "cluster_prop.agents_comm_prop.max_nb_agents_communication": 4,
+                                           "cluster_prop.message_prop.thermal": True,
+                                           "cluster_prop.message_prop.hvac": True,
+                                           "state_prop.hvac": True, "state_prop.thermal": True,
+                                           "state_prop.solar_gain": True},
+             N=30, T=50, seed=9, controller="random", norm_ticks=(0, 1, 50))
+    gen_greedy()
+    gen_comm()
+    gen_rng_order()
+    print("golden fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()

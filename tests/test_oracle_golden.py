@@ -1,0 +1,188 @@
+"""Pin the CPU oracle (oracle/env_np.py) against the reference's own outputs (tests/golden).
+
+Bar: bit-exact for integer / boolean state (lockout FSM, on/off masks, seconds-since-off,
+neighbour tables, RNG-order populations); float64 within 1e-12 relative for temperatures, powers,
+rewards and observation vectors (only libm exp / pow rounding can differ).
+"""
+import datetime as dt
+import json
+import random
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+from oracle import env_np as O
+
+RTOL = 1e-12
+
+
+def test_lockout_kat_v0_sequence():
+    # Known-answer sequence of server/v0/env/unit_tests_MA_DemandResponse.py:39-70
+    # (L = 12 s, dt = 4 s), which the app's HVAC.step reproduces.
+    on, lock, sso = np.array([True]), np.array([False]), np.array([0])
+    exp = [(True, True, False, 0), (False, False, True, None), (True, False, True, 4),
+           (True, False, True, 8), (True, True, False, 0), (True, True, False, 0)]
+    for act, e_on, e_lock, e_sso in exp:
+        on, lock, sso = O.hvac_step(on, lock, sso, np.array([act]), 12, 4)
+        assert bool(on[0]) == e_on and bool(lock[0]) == e_lock
+        if e_sso is not None:
+            assert int(sso[0]) == e_sso
+
+
+def test_lockout_golden():
+    d = gu.load("lockout.npz")
+    for c in range(int(d["ncases"])):
+        L, step = int(d[f"c{c}_L"]), int(d[f"c{c}_dt"])
+        on, lock, sso = np.array([True]), np.array([False]), np.array([0])
+        for t, a in enumerate(d[f"c{c}_action"]):
+            on, lock, sso = O.hvac_step(on, lock, sso, np.array([bool(a)]), L, step)
+            assert (on[0], lock[0], sso[0]) == (bool(d[f"c{c}_on"][t]), bool(d[f"c{c}_lock"][t]),
+                                                d[f"c{c}_sso"][t]), (c, t)
+
+
+def test_thermal_golden():
+    d = gu.load("thermal.npz")
+    hp_lcf = 0.35
+    G = np.array([O.solar_gain(gu.from_epoch(e), 7.175, 0.67) if f else 0.0
+                  for e, f in zip(d["epoch"], d["solar_flag"])])
+    np.testing.assert_array_equal(G, d["solar_gain"])
+    q = O.heat_transfer(d["on"].astype(bool), d["cap"], hp_lcf)
+    T, Tm = O.update_temperature(d["T"], d["Tm"], d["Ua"], d["Ca"], d["Cm"], d["Hm"], q, G,
+                                 d["Tod"], d["dt"].astype(np.float64))
+    np.testing.assert_allclose(T, d["T_new"], rtol=RTOL, atol=0)
+    np.testing.assert_allclose(Tm, d["Tm_new"], rtol=RTOL, atol=0)
+
+
+def test_solar_golden_exact():
+    d = gu.load("solar.npz")
+    got = np.array([O.solar_gain(gu.from_epoch(e), 7.175, 0.67) for e in d["epoch"]])
+    np.testing.assert_array_equal(got, d["gain"])
+
+
+def test_signal_golden_exact():
+    from mdr_amd.config import SignalProperties
+
+    d = gu.load("signal.npz")
+    stamps = [gu.from_epoch(e) for e in d["epoch"]]
+    for mode in ("flat", "sinusoidals", "regular_steps"):
+        for nb in (50, 1000):
+            sp = SignalProperties(mode=mode)
+            got = [float(O.signal(mode, sp, 4200.0 * nb, t, nb)) for t in stamps]
+            np.testing.assert_array_equal(got, d[f"{mode}_{nb}"])
+    sp = SignalProperties(mode="sinusoidals", amplitude_ratios=[0.2, 0.05, 0.1], periods=[300, 900, 3600])
+    got = [float(O.signal("sinusoidals", sp, 77 * 3900.0, t, 77)) for t in stamps]
+    np.testing.assert_array_equal(got, d["sinusoidals_custom_77"])
+    sp = SignalProperties(mode="regular_steps", amplitude_per_hvac=5000, period=600)
+    got = [float(O.signal("regular_steps", sp, 77 * 3900.0, t, 77)) for t in stamps]
+    np.testing.assert_array_equal(got, d["regular_steps_custom_77"])
+
+
+@pytest.mark.parametrize("mode", ["individual_L2", "common_L2", "common_max_error", "mixture"])
+def test_rewards_golden(mode):
+    from mdr_amd.config import RewardProperties
+
+    d = gu.load("rewards.npz")
+    rp = RewardProperties()
+    rp.penalty_props.mode = mode
+    rp.penalty_props.alpha_common_max = 0.5 if mode == "mixture" else 0.0
+    got = O.rewards(d["T"], d["target"], float(d["deadband"]), float(d["P"]), float(d["S"]), rp, 19.0)
+    np.testing.assert_allclose(got, d[f"reward_{mode}"], rtol=RTOL, atol=0)
+
+
+def test_comm_golden():
+    from mdr_amd.config import AgentsCommunicationProperties, ClusterPropreties
+
+    with open(gu.path("comm.json")) as f:
+        g = json.load(f)
+    for key, val in g.items():
+        if key.startswith("random_fixed"):
+            continue
+        mode, n, kmax = key.rsplit("_", 2)
+        n, kmax = int(n), int(kmax)
+        cp = ClusterPropreties(nb_agents=n, agents_comm_prop=AgentsCommunicationProperties(
+            mode=mode, max_nb_agents_communication=kmax, row_size=5 if n != 100 else 10,
+            max_communication_distance=2 if n != 25 else 1))
+        if isinstance(val, str):
+            with pytest.raises(ValueError):
+                O.comm_links(cp, random)
+        else:
+            assert O.comm_links(cp, random) == val, key
+    cp = ClusterPropreties(nb_agents=12, agents_comm_prop=AgentsCommunicationProperties(
+        mode="random_fixed", max_nb_agents_communication=4))
+    rng = random.Random(99)
+    assert O.comm_links(cp, rng) == g["random_fixed_12_4_seed99"]
+
+
+@pytest.mark.parametrize("seed", [0, 4, 123])
+@pytest.mark.parametrize("mode", ["random", "fixed"])
+def test_rng_order_golden(seed, mode):
+    d = gu.load("rng_order.npz")
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": 20, "start_datetime_mode": mode,
+                                     "power_grid_prop.signal_properties.mode": "flat"})
+    rng = random.Random(seed)
+    env = O.OracleEnv(props, rng)
+    key = f"s{seed}_{mode}"
+    np.testing.assert_array_equal(env.pop["Ua"], d[f"{key}_r1_Ua"])
+    env.reset()
+    env.reset()
+    for k, gk in (("Ua", "Ua"), ("Ca", "Ca"), ("Cm", "Cm"), ("Hm", "Hm"), ("target", "target_temp"),
+                  ("cap", "cooling_capacity"), ("init_air", "init_air_temp_noised")):
+        np.testing.assert_array_equal(env.pop[k], d[f"{key}_r3_{gk}"], err_msg=k)
+    assert (env.date - gu.EPOCH0).total_seconds() == float(d[f"{key}_r3_epoch"])
+    assert env.Tod == float(d[f"{key}_r3_Tod"])
+    assert rng.random() == float(d[f"{key}_r3_next_random"])
+
+
+def run_oracle_traj(name):
+    d, meta = gu.traj(name)
+    props = gu.props_from_overrides(meta["overrides"])
+    rng = random.Random(meta["seed"])
+    env = O.OracleEnv(props, rng)
+    for _ in range(meta["resets"] - 1):
+        env.reset()
+    return d, meta, props, env
+
+
+@pytest.mark.parametrize("name", gu.TRAJ_NAMES)
+def test_trajectory_golden(name):
+    d, meta, props, env = run_oracle_traj(name)
+    for k, gk in (("Ua", "Ua"), ("Ca", "Ca"), ("Cm", "Cm"), ("Hm", "Hm"), ("target", "target_temp"),
+                  ("cap", "cooling_capacity")):
+        np.testing.assert_array_equal(env.pop[k], d[f"pop_{gk}"], err_msg=k)
+    o = env.obs()
+    assert o["P"] == float(d["init_P"]) and o["S"] == float(d["init_S"]) and o["Tod"] == float(d["init_Tod"])
+    if "norm_t0" in d:
+        np.testing.assert_allclose(env.norm_vector(), d["norm_t0"], rtol=RTOL, atol=1e-15)
+    acts = d["actions"]
+    hp = props.cluster_prop.house_prop
+    for t in range(meta["T"]):
+        if meta["controller"] == "deadband_bbc":
+            a = O.deadband_bangbang(env.T, env.pop["target"], hp.deadband, env.on)
+            np.testing.assert_array_equal(a, acts[t].astype(bool))
+        elif meta["controller"] == "bbc":
+            a = O.bangbang(env.T, env.pop["target"])
+            np.testing.assert_array_equal(a, acts[t].astype(bool))
+        else:
+            a = acts[t].astype(bool)
+        o, r = env.step(a)
+        np.testing.assert_array_equal(o["on"], d["traj_on"][t].astype(bool), err_msg=f"on t={t}")
+        np.testing.assert_array_equal(o["lock"], d["traj_lock"][t].astype(bool), err_msg=f"lock t={t}")
+        np.testing.assert_array_equal(o["sso"], d["traj_sso"][t], err_msg=f"sso t={t}")
+        np.testing.assert_allclose(o["T"], d["traj_T"][t], rtol=RTOL, atol=0, err_msg=f"T t={t}")
+        np.testing.assert_allclose(o["Tm"], d["traj_Tm"][t], rtol=RTOL, atol=0, err_msg=f"Tm t={t}")
+        np.testing.assert_allclose(r, d["traj_reward"][t], rtol=RTOL, atol=1e-14, err_msg=f"r t={t}")
+        assert o["P"] == float(d["traj_P"][t])
+        assert o["S"] == float(d["traj_S"][t]) and o["Tod"] == float(d["traj_Tod"][t])
+        assert o["G"] == float(d["traj_G"][t])
+        assert (o["date"] - gu.EPOCH0).total_seconds() == float(d["traj_epoch"][t])
+        if f"norm_t{t + 1}" in d:
+            np.testing.assert_allclose(env.norm_vector(), d[f"norm_t{t + 1}"], rtol=RTOL, atol=1e-15)
+
+
+def test_greedy_golden():
+    d = gu.load("greedy.npz")
+    for t in range(d["action"].shape[0]):
+        a = O.greedy(d["T"][t], d["target"][t], d["cap"][t], float(d["cop"]), d["lock"][t].astype(bool),
+                     float(d["S"][t]))
+        np.testing.assert_array_equal(a, d["action"][t].astype(bool), err_msg=f"t={t}")
