@@ -1,0 +1,251 @@
+/*
+ * mdr.h — C ABI of the MI355X-native vectorised environment step (libmdr_hip.so).
+ *
+ * Drop-in boundary for the reference's per-tick environment step, ALLabMTL/marl-demandresponse
+ * v2 (file:line relative to /root/reference):
+ *
+ *   Environment.step               server/app/core/environment/environment.py:72-108
+ *     Cluster.step (house loop)    server/app/core/environment/cluster/cluster.py:73-89
+ *       HVAC.step (lockout FSM)    server/app/core/environment/cluster/hvac.py:43-64
+ *       Building.update_temperature server/app/core/environment/cluster/building.py:141-222
+ *       get_power_consumption      server/app/core/environment/cluster/hvac.py:101-111
+ *     RewardsCalculator            server/app/core/environment/rewards_calculator.py:135-203
+ *     Cluster.get_obs / messages   server/app/core/environment/cluster/cluster.py:91-121
+ *   norm_state_dict (obs vector)   server/app/utils/norm.py:178-218
+ *   controllers                    server/app/core/agents/controllers/bangbang_controllers.py:25-89,
+ *                                  server/app/core/agents/controllers/greedy_myopic_controller.py:67-104
+ *   Environment.reset / noise      server/app/core/environment/environment.py:49-70,161-194
+ *
+ * The reference has no FFI: its boundary is a Python object (Environment.reset/step).  The
+ * Python layer mdr_amd.Environment keeps that object surface and binds these symbols with ctypes
+ * (INTEGRATION.md shows the binding).  Per-tick scalar drivers (outdoor temperature, solar gain,
+ * regulation signal, datetime) stay on the host in the reference's own arithmetic and RNG order
+ * and are passed in as mdr_tick; everything per house runs on the GPU.
+ *
+ * Conventions
+ *   - All device pointers are caller-owned (PyTorch tensors in mdr_amd); the library owns only
+ *     small scratch (per-tick power counts, penalty partials, graph cache).
+ *   - Every call is asynchronous on the caller's hipStream_t (passed as void*; NULL = legacy
+ *     default stream) and returns 0 on success, a negative MDR_E* code otherwise;
+ *     mdr_last_error() gives the text (thread-local).
+ *   - A context maps to ONE device and ONE contiguous shard of houses [global_offset,
+ *     global_offset + n_local) of a cluster of n_global houses; it is not thread-safe.
+ *
+ * Per-house state layout (SoA, length n_local):
+ *   t_air, t_mass : double   indoor air / mass temperature (Celsius)
+ *   hvac          : uint32   bits 0..29 seconds_since_off (saturating), bit 30 lockout, bit 31 on
+ *   ua, ca, cm, hm, target : double  (noised per-house parameters)
+ *   cap_idx       : uint8    index into the cooling-capacity table (mdr_config.cap_table)
+ */
+#ifndef MDR_H_
+#define MDR_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDR_ABI_VERSION 1
+#define MDR_MAX_CAP 64
+
+enum {
+  MDR_OK = 0,
+  MDR_EARG = -1,   /* bad argument / shape / unbound context */
+  MDR_EHIP = -2,   /* HIP runtime error */
+  MDR_ERCCL = -3,  /* RCCL error */
+  MDR_ENOMEM = -4,
+  MDR_ESTATE = -5, /* call out of order (e.g. step before bind) */
+};
+
+/* penalty modes, rewards_calculator.py:46-133 */
+enum { MDR_PEN_INDIVIDUAL_L2 = 0, MDR_PEN_COMMON_L2 = 1, MDR_PEN_COMMON_MAX = 2, MDR_PEN_MIXTURE = 3 };
+
+/* where a tick's actions come from */
+enum {
+  MDR_ACT_BUFFER = 0,     /* uint8 action[n_local] (non-zero = turn on), the Dict[int,bool] of step() */
+  MDR_ACT_RANDOM = 1,     /* Bernoulli(0.5) from Philox4x32-10(seed, global house id, tick) */
+  MDR_ACT_ALWAYS_ON = 2,  /* AlwaysOnController, bangbang_controllers.py:7-16 */
+  MDR_ACT_BANGBANG = 16,  /* BangBangController on the pre-step state, bangbang_controllers.py:54-65 */
+  MDR_ACT_DEADBAND_BANGBANG = 17 /* DeadbandBangBangController, bangbang_controllers.py:25-42 */
+};
+
+/* controller evaluated on the post-step state, written as the NEXT tick's action buffer */
+enum { MDR_CTRL_NONE = 0, MDR_CTRL_BANGBANG = 1, MDR_CTRL_DEADBAND_BANGBANG = 2 };
+
+/* communication (message) topology, agent_communication_builder.py:36-203 */
+enum { MDR_COMM_RING = 0, MDR_COMM_TABLE = 1 };
+
+typedef struct mdr_config {
+  int32_t abi_version;      /* = MDR_ABI_VERSION */
+  int32_t device;           /* HIP device ordinal */
+  int64_t n_local;          /* houses in this shard */
+  int64_t global_offset;    /* global id of the shard's first house */
+  int64_t n_global;         /* cluster size N (signal penalty, obs normalisation) */
+  int32_t dt;               /* time_step.seconds */
+  int32_t lockout_duration; /* L (hvac_prop.lockout_duration) */
+  double cop;               /* hvac_prop.cop */
+  double lcf;               /* hvac_prop.latent_cooling_fraction */
+  double deadband;          /* house_prop.deadband */
+  int32_t n_cap;            /* entries in cap_table (<= MDR_MAX_CAP) */
+  int32_t penalty_mode;     /* MDR_PEN_* */
+  double cap_table[MDR_MAX_CAP]; /* cooling capacities (W) the population draws from */
+  double alpha_temp, alpha_sig;  /* reward_prop */
+  double norm_temp, norm_sig;    /* deadbandL2 normalisers, computed by the caller */
+  double alpha_ind_l2, alpha_common_l2, alpha_common_max;
+  uint64_t seed;                 /* Philox key for MDR_ACT_RANDOM and synthetic populations */
+} mdr_config;
+
+typedef struct mdr_soa {
+  double* t_air;
+  double* t_mass;
+  uint32_t* hvac;
+  const double* ua;
+  const double* ca;
+  const double* cm;
+  const double* hm;
+  const double* target;
+  const uint8_t* cap_idx;
+} mdr_soa;
+
+/* host-side per-tick drivers (environment.py:86-106 ordering) */
+typedef struct mdr_tick {
+  double t_od_prev; /* outdoor temperature BEFORE this step (used by the thermal update) */
+  double solar;     /* compute_solar_gain at the NEW datetime, 0 if house_prop.solar_gain is off */
+  double s_prev;    /* regulation signal before this step (the reward uses the old signal) */
+  uint64_t tick;    /* tick counter (Philox stream for MDR_ACT_RANDOM) */
+} mdr_tick;
+
+typedef struct mdr_ctx mdr_ctx;
+
+/* ---- lifecycle ------------------------------------------------------------------------- */
+int mdr_abi_version(void);
+/* sizeof of the ABI structs, for binding checks: out[0..5] = mdr_config, mdr_soa, mdr_tick,
+ * mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars; returns the number written */
+int mdr_abi_sizes(int64_t* out, int n);
+const char* mdr_last_error(void);
+int mdr_create(mdr_ctx** out, const mdr_config* cfg);
+int mdr_destroy(mdr_ctx* ctx);
+/* Bind the caller-owned SoA arrays (Environment.reset, environment.py:49-70). */
+int mdr_bind(mdr_ctx* ctx, const mdr_soa* soa);
+
+/* ---- population ------------------------------------------------------------------------ */
+/* Synthetic population drawn on device from Philox4x32-10(seed, global house id): the reference
+ * noise model (building.py:224-267, hvac.py:66-70: target = target_temp + |N(0, std_target)|,
+ * Ua = Tri(lo, hi, 1) (the reference ASSIGNS the factor), Cm/Ca/Hm = cfg * Tri(lo, hi, 1), cap =
+ * uniform over cap_table) with a counter-based RNG instead of MT19937, so a population is
+ * identical for any sharding.  Initial state as Building.reset/HVAC.reset: T = init temps, on,
+ * no lockout, sso = 0.  Writes every bound array. */
+typedef struct mdr_pop_spec {
+  double target_temp, std_target;   /* house_prop.target_temp, noise_prop.std_target_temp */
+  double thermo_lo, thermo_hi;      /* noise_prop.factor_thermo_low / _high */
+  double ca, cm, hm;                /* house_prop.Ca, Cm, Hm */
+  double init_air, init_mass;       /* house_prop.init_air_temp, init_mass_temp */
+} mdr_pop_spec;
+int mdr_populate(mdr_ctx* ctx, const mdr_pop_spec* spec, void* stream);
+
+/* ---- tick: phase 1 (cluster power) ------------------------------------------------------ */
+/* Lockout FSM on the current state + this tick's actions -> ON houses per capacity class,
+ * accumulated into the context's count slab for this tick (int64[kCountShards * n_cap], sharded
+ * to spread atomics).  P = sum_k count_k * cap_k / cop is exact and order independent.  State
+ * is not modified.  (cluster.py:82-88)  Not needed when the previous mdr_step ran with a
+ * lookahead action source. */
+int mdr_power_counts(mdr_ctx* ctx, const uint8_t* action, int action_mode, uint64_t tick,
+                     void* stream);
+/* Device pointer + element count of the current tick's count slab: the buffer a multi-GPU caller
+ * sum-allreduces (int64) between phase 1 and phase 2. */
+int mdr_counts_buffer(mdr_ctx* ctx, int64_t** dev_ptr, int* len);
+
+/* ---- tick: phase 2 (fused step) -------------------------------------------------------- */
+/* FSM + RC thermal update + per-house reward with this tick's GLOBAL cluster power; updates the
+ * state in place and writes reward[n_local] (double).
+ *   action_mode : MDR_ACT_* (BUFFER reads action[]), or MDR_ACT_BANGBANG / _DEADBAND_BANGBANG to
+ *                 evaluate that controller on the pre-step state (the obs the caller would act on)
+ *   lookahead   : 0, or the action source of the NEXT tick (MDR_ACT_RANDOM / _ALWAYS_ON /
+ *                 _BANGBANG / _DEADBAND_BANGBANG): its ON counts are accumulated here on the new
+ *                 state, so the next tick needs no phase-1 launch
+ *   ctrl_out    : if non-NULL, the bang-bang (ctrl = MDR_CTRL_*) decision on the new state
+ *   p_out       : if non-NULL, device double receiving the tick's cluster power
+ * For common penalty modes reward holds the raw penalty until mdr_reward_finalize. */
+int mdr_step(mdr_ctx* ctx, const uint8_t* action, int action_mode, const mdr_tick* tick,
+             double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
+             void* stream);
+
+/* Common penalty modes (common_L2 / common_max_error / mixture): per-shard {sum pen/N, max pen}
+ * into the context's partial buffer (device double[2]; sum-/max-allreduce it on multi-GPU), then
+ * the rewards are finalised in place. */
+int mdr_penalty_partials(mdr_ctx* ctx, void* stream);
+int mdr_penalty_buffer(mdr_ctx* ctx, double** dev_ptr);
+int mdr_reward_finalize(mdr_ctx* ctx, const mdr_tick* tick, double* reward, void* stream);
+
+/* ---- several ticks in one call (single GPU) --------------------------------------------- */
+/* n_ticks consecutive steps; ticks[] in host memory.  action / reward advance by act_stride /
+ * rew_stride elements per tick (0 = reuse one buffer).  With an in-kernel action source
+ * (MDR_ACT_RANDOM / _ALWAYS_ON / _BANGBANG / _DEADBAND_BANGBANG) every tick is ONE launch (the
+ * counts of tick t+1 come from tick t's lookahead); with MDR_ACT_BUFFER two.  use_graph != 0
+ * captures the sequence in a hipGraph (cached per shape) and replays it. */
+int mdr_rollout(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t* action,
+                int64_t act_stride, int action_mode, double* reward, int64_t rew_stride,
+                int use_graph, void* stream);
+
+/* ---- observation vector (norm_state_dict, norm.py:178-218) ----------------------------- */
+typedef struct mdr_obs_spec {
+  int32_t n_feat;        /* features per house written (row length of obs) */
+  int32_t hvac_state;    /* state_prop.hvac */
+  int32_t solar_state;   /* state_prop.solar_gain */
+  int32_t thermal_state; /* state_prop.thermal */
+  int32_t msg_thermal;   /* message_prop.thermal */
+  int32_t msg_hvac;      /* message_prop.hvac */
+  int32_t n_comm;        /* messages per house (nb_comm) */
+  int32_t comm_mode;     /* MDR_COMM_RING (neighbours, arithmetic) or MDR_COMM_TABLE */
+  const int32_t* comm_table; /* TABLE mode: [n_local, n_comm] local house indices */
+  const float* halo_msg;     /* RING mode, multi-GPU: [lo + hi][msg_w] message features of the
+                                houses before / after the shard (mdr_halo_pack of the neighbours);
+                                NULL = single shard, ring wraps around locally */
+  double norm_reg_sig;   /* R */
+  double cfg_ua, cfg_ca, cfg_cm, cfg_hm; /* house_prop (un-noised) for the thermal ratios */
+  double cfg_cap;        /* hvac_prop.cooling_capacity (message hvac feature) */
+} mdr_obs_spec;
+
+typedef struct mdr_obs_scalars {
+  double p;       /* cluster power of the tick (obs cluster_hvac_power) */
+  double s;       /* regulation signal after the step (obs reg_signal) */
+  double solar;   /* obs solar_gain */
+  double t_od;    /* obs OD_temp */
+} mdr_obs_scalars;
+
+/* message feature width for a spec (4, +4 thermal, +3 hvac) */
+int mdr_msg_width(const mdr_obs_spec* spec);
+/* float32 obs[n_local, n_feat].  p_dev, when non-NULL, overrides sc->p with a device scalar
+ * (the value mdr_step wrote), so no host round trip is needed. */
+int mdr_obs(mdr_ctx* ctx, const mdr_obs_spec* spec, const mdr_obs_scalars* sc,
+            const double* p_dev, float* obs, void* stream);
+/* message features of this shard's first hi and last lo houses -> out[(hi + lo) * msg_w] floats:
+ * rows [0, hi) = first hi houses, rows [hi, hi + lo) = last lo houses. */
+int mdr_halo_pack(mdr_ctx* ctx, const mdr_obs_spec* spec, float* out, void* stream);
+
+/* ---- greedy-myopic controller (greedy_myopic_controller.py:67-104) --------------------- */
+/* Next actions for the whole shard (single GPU: shard = cluster) from the current state: order
+ * by -(T - target) ascending, then the reference's sequential take rule with budget S. */
+int mdr_ctrl_greedy(mdr_ctx* ctx, double budget, uint8_t* action, void* stream);
+
+/* ---- multi-GPU (RCCL over xGMI) --------------------------------------------------------- */
+/* ncclUniqueId is 128 bytes; rank 0 creates it, the caller broadcasts it (torch.distributed). */
+int mdr_rccl_unique_id(uint8_t* id128);
+int mdr_rccl_init(mdr_ctx* ctx, const uint8_t* id128, int world, int rank);
+/* in-place allreduce on `stream`: dtype 0 = int64 sum, 1 = double sum, 2 = double max */
+int mdr_rccl_allreduce(mdr_ctx* ctx, void* buf, int64_t count, int dtype, void* stream);
+/* sharded multi-tick rollout, RCCL allreduce of the count slab inside the loop:
+ * per tick  [phase 1 if BUFFER] -> allreduce(counts) -> phase 2 (with lookahead when possible) */
+int mdr_rollout_sharded(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t* action,
+                        int64_t act_stride, int action_mode, double* reward, int64_t rew_stride,
+                        void* stream);
+
+/* ---- timing helpers for bench.py (HIP events on the given stream) ---------------------- */
+int mdr_event_record(mdr_ctx* ctx, int slot, void* stream);
+int mdr_event_elapsed_ms(mdr_ctx* ctx, int slot0, int slot1, float* ms);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MDR_H_ */

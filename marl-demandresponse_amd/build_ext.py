@@ -1,0 +1,57 @@
+"""Build libmdr_hip.so in-tree for gfx950 (hipcc, no JIT cache): ``python build_ext.py``.
+
+Flags that matter for parity: ``-ffp-contract=off`` (no a*b+c fusion: the reference evaluates every
+operation with its own rounding) and no fast-math (correctly rounded fp64 division / sqrt).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+SRC = [os.path.join(HERE, "csrc", f) for f in ("mdr_kernels.hip", "mdr_capi.hip")]
+HDR = [os.path.join(HERE, "csrc", f) for f in ("mdr_kernels.h", "mdr_device.h")] + [
+    os.path.join(ROOT, "include", "mdr.h")]
+OUT = os.path.join(HERE, "mdr_amd", "libmdr_hip.so")
+ARCH = os.environ.get("MDR_OFFLOAD_ARCH", "gfx950")
+
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+         f"--offload-arch={ARCH}", "-Wno-unused-value", "-Wno-unused-result",
+         "-I" + os.path.join(ROOT, "include"), "-I" + os.path.join(HERE, "csrc")]
+
+
+def hipcc() -> str:
+    for c in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if c and os.path.exists(c):
+            return c
+    raise RuntimeError("hipcc not found")
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(OUT):
+        return False
+    t = os.path.getmtime(OUT)
+    return all(os.path.getmtime(s) <= t for s in SRC + HDR + [__file__])
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return OUT
+    tmp = OUT + ".tmp"
+    cmd = [hipcc()] + FLAGS + SRC + ["-o", tmp, "-L/opt/rocm/lib", "-lrccl",
+                                     "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"hipcc failed ({r.returncode})")
+    os.replace(tmp, OUT)
+    return OUT
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,612 @@
+// mdr_capi.hip — C-ABI host runtime: contexts, launches, graph cache, greedy scratch, RCCL.
+//
+// The C ABI (include/mdr.h) is what the Python layer (mdr_amd, via ctypes) and any other host
+// binds.  It owns only small scratch; every launch goes to the caller's stream.
+#include <hip/hip_runtime.h>
+#include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <vector>
+
+#include "mdr_kernels.h"
+
+using namespace mdr;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(MDR_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_));            \
+  } while (0)
+
+#define RCCL_TRY(expr)                                                                     \
+  do {                                                                                     \
+    ncclResult_t r_ = (expr);                                                              \
+    if (r_ != ncclSuccess) return fail(MDR_ERCCL, std::string(#expr) + ": " + ncclGetErrorString(r_)); \
+  } while (0)
+
+#define LAUNCH_CHECK(what)                                                                 \
+  do {                                                                                     \
+    hipError_t e_ = hipGetLastError();                                                     \
+    if (e_ != hipSuccess) return fail(MDR_EHIP, std::string(what) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+inline unsigned blocks(int64_t n, int b) { return (unsigned)((n + b - 1) / b); }
+
+struct GraphKey {
+  int n_ticks, mode;
+  const void* act;
+  int64_t act_stride;
+  void* rew;
+  int64_t rew_stride;
+  void* stream;
+  bool operator<(const GraphKey& o) const {
+    return std::tie(n_ticks, mode, act, act_stride, rew, rew_stride, stream) <
+           std::tie(o.n_ticks, o.mode, o.act, o.act_stride, o.rew, o.rew_stride, o.stream);
+  }
+};
+
+}  // namespace
+
+struct mdr_ctx {
+  mdr_config cfg{};
+  KParams kp{};
+  bool bound = false;
+  double* d_tables = nullptr;           // q_on[MDR_MAX_CAP] | p_on[MDR_MAX_CAP]
+  unsigned long long* d_slab = nullptr;  // 3 x kCountShards x n_cap ring of count slabs
+  int slab_len = 0;
+  int ring = 0;                          // slab of the current tick
+  bool counts_ready = false;             // current slab filled (phase 1 or previous lookahead)
+  double* d_pen_partial = nullptr;       // 2 per block of k_step
+  double* d_partial2 = nullptr;
+  int pen_blocks = 0;
+  // rollout tick drivers
+  TickArgs* d_ticks = nullptr;
+  TickArgs* h_ticks = nullptr;  // pinned staging
+  int ticks_cap = 0;
+  hipEvent_t ticks_free = nullptr;
+  std::map<GraphKey, std::pair<hipGraphExec_t, int>> graphs;  // exec, ring phase at end
+  // greedy scratch
+  int64_t g_cap = 0;
+  double *g_key = nullptr, *g_key2 = nullptr, *g_ps = nullptr, *g_incl = nullptr;
+  int *g_idx = nullptr, *g_idx2 = nullptr;
+  uint8_t* g_ls = nullptr;
+  void* g_tmp = nullptr;
+  size_t g_tmp_bytes = 0;
+  int64_t* g_kpos = nullptr;
+  int64_t* g_extra = nullptr;
+  // multi-GPU
+  ncclComm_t comm = nullptr;
+  int world = 1, rank = 0;
+  hipEvent_t ev[16] = {};
+};
+
+namespace {
+
+unsigned long long* slab_at(mdr_ctx* c, int r) { return c->d_slab + (size_t)((r % 3 + 3) % 3) * c->slab_len; }
+
+int check_mode(int m) {
+  return m == MDR_ACT_BUFFER || m == MDR_ACT_RANDOM || m == MDR_ACT_ALWAYS_ON ||
+         m == MDR_ACT_BANGBANG || m == MDR_ACT_DEADBAND_BANGBANG;
+}
+
+bool lookahead_ok(int m) { return m != MDR_ACT_BUFFER; }
+
+TickArgs to_tick(const mdr_tick* t) { return TickArgs{t->t_od_prev, t->solar, t->s_prev, t->tick}; }
+
+// phase 1 into the current slab
+int launch_counts(mdr_ctx* c, const uint8_t* action, int mode, uint64_t tick, const TickArgs* tkp,
+                  hipStream_t st) {
+  int m = mode;
+  if (m == MDR_ACT_BANGBANG || m == MDR_ACT_DEADBAND_BANGBANG)
+    return fail(MDR_EARG, "phase 1 with a bang-bang action source: use mdr_step lookahead or a BUFFER");
+  hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, action, m,
+                     tick, tkp, slab_at(c, c->ring));
+  LAUNCH_CHECK("k_power_counts");
+  return MDR_OK;
+}
+
+int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const TickArgs* tkp,
+                double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
+                hipStream_t st) {
+  unsigned long long* cur = slab_at(c, c->ring);
+  unsigned long long* nxt = slab_at(c, c->ring + 1);
+  unsigned long long* zer = slab_at(c, c->ring + 2);
+  hipLaunchKernelGGL(k_step, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, action, mode, tk,
+                     tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer, c->d_pen_partial);
+  LAUNCH_CHECK("k_step");
+  c->ring = (c->ring + 1) % 3;
+  c->counts_ready = lookahead != 0;
+  return MDR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mdr_abi_version(void) { return MDR_ABI_VERSION; }
+
+int mdr_abi_sizes(int64_t* out, int n) {
+  const int64_t v[6] = {(int64_t)sizeof(mdr_config), (int64_t)sizeof(mdr_soa), (int64_t)sizeof(mdr_tick),
+                        (int64_t)sizeof(mdr_pop_spec), (int64_t)sizeof(mdr_obs_spec),
+                        (int64_t)sizeof(mdr_obs_scalars)};
+  int k = 0;
+  for (; out && k < n && k < 6; ++k) out[k] = v[k];
+  return k;
+}
+
+const char* mdr_last_error(void) { return g_err.c_str(); }
+
+int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
+  if (!out || !cfg) return fail(MDR_EARG, "mdr_create: null argument");
+  if (cfg->abi_version != MDR_ABI_VERSION) return fail(MDR_EARG, "mdr_create: ABI version mismatch");
+  if (cfg->n_local < 1 || cfg->n_global < cfg->n_local || cfg->global_offset < 0 ||
+      cfg->global_offset + cfg->n_local > cfg->n_global)
+    return fail(MDR_EARG, "mdr_create: bad shard geometry");
+  if (cfg->n_local > (int64_t)INT32_MAX) return fail(MDR_EARG, "mdr_create: n_local exceeds int32 (greedy indices)");
+  if (cfg->n_cap < 1 || cfg->n_cap > MDR_MAX_CAP) return fail(MDR_EARG, "mdr_create: n_cap out of range");
+  if (cfg->dt < 0) return fail(MDR_EARG, "mdr_create: negative dt");
+  if (cfg->penalty_mode < 0 || cfg->penalty_mode > 3) return fail(MDR_EARG, "mdr_create: bad penalty mode");
+  HIP_TRY(hipSetDevice(cfg->device));
+  mdr_ctx* c = new mdr_ctx();
+  c->cfg = *cfg;
+  KParams& k = c->kp;
+  k.n = cfg->n_local;
+  k.goff = cfg->global_offset;
+  k.n_global = cfg->n_global;
+  k.dt = cfg->dt;
+  k.L = cfg->lockout_duration;
+  k.n_cap = cfg->n_cap;
+  k.penalty_mode = cfg->penalty_mode;
+  k.deadband = cfg->deadband;
+  k.alpha_temp = cfg->alpha_temp;
+  k.alpha_sig = cfg->alpha_sig;
+  k.norm_temp = cfg->norm_temp;
+  k.norm_sig = cfg->norm_sig;
+  k.alpha_ind_l2 = cfg->alpha_ind_l2;
+  k.alpha_common_l2 = cfg->alpha_common_l2;
+  k.alpha_common_max = cfg->alpha_common_max;
+  k.seed = cfg->seed;
+  // capacity tables with the reference's expressions: hvac.py:94-97 and
+  // environment_properties.py:92-98  (-1 * cap / (1 + lcf), cap / cop)
+  double tab[2 * MDR_MAX_CAP] = {};
+  for (int i = 0; i < cfg->n_cap; ++i) {
+    tab[i] = (-1.0 * cfg->cap_table[i]) / (1.0 + cfg->lcf);
+    tab[MDR_MAX_CAP + i] = cfg->cap_table[i] / cfg->cop;
+  }
+  auto cleanup = [&](int rc) { mdr_destroy(c); return rc; };
+  if (hipMalloc(&c->d_tables, sizeof(tab)) != hipSuccess) return cleanup(fail(MDR_ENOMEM, "tables"));
+  if (hipMemcpy(c->d_tables, tab, sizeof(tab), hipMemcpyHostToDevice) != hipSuccess)
+    return cleanup(fail(MDR_EHIP, "tables copy"));
+  k.q_on = c->d_tables;
+  k.p_on = c->d_tables + MDR_MAX_CAP;
+  c->slab_len = kCountShards * cfg->n_cap;
+  if (hipMalloc(&c->d_slab, 3 * c->slab_len * sizeof(unsigned long long)) != hipSuccess)
+    return cleanup(fail(MDR_ENOMEM, "count slabs"));
+  if (hipMemset(c->d_slab, 0, 3 * c->slab_len * sizeof(unsigned long long)) != hipSuccess)
+    return cleanup(fail(MDR_EHIP, "count slabs memset"));
+  c->pen_blocks = (int)blocks(cfg->n_local, 256);
+  if (hipMalloc(&c->d_pen_partial, 2 * sizeof(double) * c->pen_blocks) != hipSuccess ||
+      hipMalloc(&c->d_partial2, 2 * sizeof(double)) != hipSuccess)
+    return cleanup(fail(MDR_ENOMEM, "penalty partials"));
+  if (hipEventCreateWithFlags(&c->ticks_free, hipEventDisableTiming) != hipSuccess)
+    return cleanup(fail(MDR_EHIP, "event"));
+  for (auto& e : c->ev)
+    if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(MDR_EHIP, "event"));
+  *out = c;
+  return MDR_OK;
+}
+
+int mdr_destroy(mdr_ctx* c) {
+  if (!c) return MDR_OK;
+  hipSetDevice(c->cfg.device);
+  hipDeviceSynchronize();
+  for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
+  hipFree(c->d_tables);
+  hipFree(c->d_slab);
+  hipFree(c->d_pen_partial);
+  hipFree(c->d_partial2);
+  hipFree(c->d_ticks);
+  if (c->h_ticks) hipHostFree(c->h_ticks);
+  if (c->ticks_free) hipEventDestroy(c->ticks_free);
+  for (auto& e : c->ev)
+    if (e) hipEventDestroy(e);
+  hipFree(c->g_key); hipFree(c->g_key2); hipFree(c->g_ps); hipFree(c->g_incl);
+  hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
+  hipFree(c->g_kpos); hipFree(c->g_extra);
+  if (c->comm) ncclCommDestroy(c->comm);
+  delete c;
+  return MDR_OK;
+}
+
+int mdr_bind(mdr_ctx* c, const mdr_soa* s) {
+  if (!c || !s) return fail(MDR_EARG, "mdr_bind: null argument");
+  if (!s->t_air || !s->t_mass || !s->hvac || !s->ua || !s->ca || !s->cm || !s->hm || !s->target ||
+      !s->cap_idx)
+    return fail(MDR_EARG, "mdr_bind: null array");
+  KParams& k = c->kp;
+  k.t_air = s->t_air;
+  k.t_mass = s->t_mass;
+  k.hvac = s->hvac;
+  k.ua = s->ua;
+  k.ca = s->ca;
+  k.cm = s->cm;
+  k.hm = s->hm;
+  k.target = s->target;
+  k.cap_idx = s->cap_idx;
+  c->bound = true;
+  c->counts_ready = false;
+  for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
+  c->graphs.clear();
+  return MDR_OK;
+}
+
+int mdr_populate(mdr_ctx* c, const mdr_pop_spec* sp, void* stream) {
+  if (!c || !sp) return fail(MDR_EARG, "mdr_populate: null argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_populate: context not bound");
+  PopArgs a{sp->target_temp, sp->std_target, sp->thermo_lo, sp->thermo_hi, sp->ca, sp->cm, sp->hm,
+            sp->init_air, sp->init_mass};
+  hipLaunchKernelGGL(k_populate, dim3(blocks(c->kp.n, 256)), dim3(256), 0, S(stream), c->kp, a);
+  LAUNCH_CHECK("k_populate");
+  c->counts_ready = false;
+  return MDR_OK;
+}
+
+int mdr_power_counts(mdr_ctx* c, const uint8_t* action, int mode, uint64_t tick, void* stream) {
+  if (!c) return fail(MDR_EARG, "mdr_power_counts: null ctx");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_power_counts: context not bound");
+  if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action))
+    return fail(MDR_EARG, "mdr_power_counts: bad action source");
+  // (re)compute this tick's counts from zero (a previous lookahead may have filled the slab)
+  HIP_TRY(hipMemsetAsync(slab_at(c, c->ring), 0, c->slab_len * sizeof(unsigned long long), S(stream)));
+  int rc = launch_counts(c, action, mode, tick, nullptr, S(stream));
+  if (rc) return rc;
+  c->counts_ready = true;
+  return MDR_OK;
+}
+
+int mdr_counts_buffer(mdr_ctx* c, int64_t** ptr, int* len) {
+  if (!c || !ptr || !len) return fail(MDR_EARG, "mdr_counts_buffer: null argument");
+  *ptr = reinterpret_cast<int64_t*>(slab_at(c, c->ring));
+  *len = c->slab_len;
+  return MDR_OK;
+}
+
+int mdr_step(mdr_ctx* c, const uint8_t* action, int mode, const mdr_tick* tick, double* reward,
+             int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out, void* stream) {
+  if (!c || !tick || !reward) return fail(MDR_EARG, "mdr_step: null argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_step: context not bound");
+  if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action))
+    return fail(MDR_EARG, "mdr_step: bad action source");
+  if (lookahead && (!check_mode(lookahead) || !lookahead_ok(lookahead)))
+    return fail(MDR_EARG, "mdr_step: bad lookahead source");
+  if (ctrl < MDR_CTRL_NONE || ctrl > MDR_CTRL_DEADBAND_BANGBANG) return fail(MDR_EARG, "mdr_step: bad ctrl");
+  if (!c->counts_ready) return fail(MDR_ESTATE, "mdr_step: no cluster-power counts for this tick (call mdr_power_counts)");
+  return launch_step(c, action, mode, to_tick(tick), nullptr, reward, lookahead, ctrl, ctrl_out, p_out,
+                     S(stream));
+}
+
+int mdr_penalty_partials(mdr_ctx* c, void* stream) {
+  if (!c) return fail(MDR_EARG, "mdr_penalty_partials: null ctx");
+  hipLaunchKernelGGL(k_pen_reduce, dim3(1), dim3(256), 0, S(stream), c->d_pen_partial, c->pen_blocks,
+                     c->d_partial2);
+  LAUNCH_CHECK("k_pen_reduce");
+  return MDR_OK;
+}
+
+int mdr_penalty_buffer(mdr_ctx* c, double** ptr) {
+  if (!c || !ptr) return fail(MDR_EARG, "mdr_penalty_buffer: null argument");
+  *ptr = c->d_partial2;
+  return MDR_OK;
+}
+
+int mdr_reward_finalize(mdr_ctx* c, const mdr_tick* tick, double* reward, void* stream) {
+  if (!c || !tick || !reward) return fail(MDR_EARG, "mdr_reward_finalize: null argument");
+  // the tick's counts are in the slab just before the current one
+  hipLaunchKernelGGL(k_reward_finalize, dim3(blocks(c->kp.n, 256)), dim3(256), 0, S(stream), c->kp,
+                     to_tick(tick), slab_at(c, c->ring - 1), c->d_partial2, reward);
+  LAUNCH_CHECK("k_reward_finalize");
+  return MDR_OK;
+}
+
+// ------------------------------------------------------------------------------------ rollout
+static int stage_ticks(mdr_ctx* c, int n, const mdr_tick* ticks, hipStream_t st) {
+  if (n > c->ticks_cap) {
+    HIP_TRY(hipEventSynchronize(c->ticks_free));
+    hipFree(c->d_ticks);
+    if (c->h_ticks) hipHostFree(c->h_ticks);
+    c->d_ticks = nullptr;
+    c->h_ticks = nullptr;
+    int cap = n < 64 ? 64 : n;
+    HIP_TRY(hipMalloc(&c->d_ticks, cap * sizeof(TickArgs)));
+    HIP_TRY(hipHostMalloc(&c->h_ticks, cap * sizeof(TickArgs), hipHostMallocDefault));
+    c->ticks_cap = cap;
+    for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
+    c->graphs.clear();
+  }
+  HIP_TRY(hipEventSynchronize(c->ticks_free));  // previous H2D of the staging buffer done
+  for (int i = 0; i < n; ++i) c->h_ticks[i] = to_tick(&ticks[i]);
+  HIP_TRY(hipMemcpyAsync(c->d_ticks, c->h_ticks, n * sizeof(TickArgs), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipEventRecord(c->ticks_free, st));
+  return MDR_OK;
+}
+
+// The launch sequence of a rollout; tick args come from d_ticks so a captured graph is reusable.
+static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t act_stride, int mode,
+                            double* reward, int64_t rew_stride, hipStream_t st) {
+  HIP_TRY(hipMemsetAsync(c->d_slab, 0, 3 * c->slab_len * sizeof(unsigned long long), st));
+  c->ring = 0;
+  const bool la = lookahead_ok(mode);
+  for (int t = 0; t < n; ++t) {
+    const uint8_t* a = action ? action + (int64_t)t * act_stride : nullptr;
+    double* r = reward + (int64_t)t * rew_stride;
+    if (!la || t == 0) {
+      int m = mode;
+      if (t == 0 && (mode == MDR_ACT_BANGBANG || mode == MDR_ACT_DEADBAND_BANGBANG)) {
+        // first tick under a bang-bang source: phase 1 needs the decision on the current state;
+        // write it into the context's scratch via a zero-reward dry step is not possible, so the
+        // caller must provide the first actions: handled by the caller (mode remapped to BUFFER)
+        return fail(MDR_EARG, "rollout: bang-bang sources need a BUFFER first tick (use mdr_step)");
+      }
+      hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, a, m,
+                         (uint64_t)0, c->d_ticks + t, slab_at(c, c->ring));
+      LAUNCH_CHECK("k_power_counts");
+    }
+    int rc = launch_step(c, a, mode, TickArgs{}, c->d_ticks + t, r, la ? mode : 0, MDR_CTRL_NONE,
+                         nullptr, nullptr, st);
+    if (rc) return rc;
+  }
+  return MDR_OK;
+}
+
+int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action, int64_t act_stride,
+                int mode, double* reward, int64_t rew_stride, int use_graph, void* stream) {
+  if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout: bad argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout: context not bound");
+  if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout: bad action source");
+  if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
+    return fail(MDR_EARG, "mdr_rollout: common penalty modes need the per-step API");
+  hipStream_t st = S(stream);
+  int rc = stage_ticks(c, n, ticks, st);
+  if (rc) return rc;
+  if (!use_graph) {
+    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, st);
+    c->counts_ready = false;
+    return rc;
+  }
+  GraphKey key{n, mode, action, act_stride, reward, rew_stride, stream};
+  auto it = c->graphs.find(key);
+  if (it == c->graphs.end()) {
+    if (st == nullptr) return fail(MDR_EARG, "mdr_rollout: graph capture needs a non-default stream");
+    hipGraph_t g;
+    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, st);
+    hipError_t e = hipStreamEndCapture(st, &g);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(MDR_EHIP, std::string("capture: ") + hipGetErrorString(e));
+    hipGraphExec_t ex;
+    e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    if (e != hipSuccess) return fail(MDR_EHIP, std::string("instantiate: ") + hipGetErrorString(e));
+    it = c->graphs.emplace(key, std::make_pair(ex, c->ring)).first;
+  }
+  HIP_TRY(hipGraphLaunch(it->second.first, st));
+  c->ring = it->second.second;
+  c->counts_ready = false;
+  return MDR_OK;
+}
+
+// ------------------------------------------------------------------------------------ obs
+static ObsArgs obs_args(const mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc) {
+  ObsArgs o{};
+  o.n_feat = sp->n_feat;
+  o.msg_w = mdr_msg_width(sp);
+  o.n_comm = sp->n_comm;
+  o.comm_mode = sp->comm_mode;
+  o.hvac_state = sp->hvac_state;
+  o.solar_state = sp->solar_state;
+  o.thermal_state = sp->thermal_state;
+  o.msg_thermal = sp->msg_thermal;
+  o.msg_hvac = sp->msg_hvac;
+  o.comm_table = sp->comm_table;
+  o.halo_msg = sp->halo_msg;
+  o.norm_reg_sig = sp->norm_reg_sig;
+  o.cfg_ua = sp->cfg_ua;
+  o.cfg_ca = sp->cfg_ca;
+  o.cfg_cm = sp->cfg_cm;
+  o.cfg_hm = sp->cfg_hm;
+  o.cfg_cop = c->cfg.cop;
+  o.cfg_lcf = c->cfg.lcf;
+  o.cfg_cap = sp->cfg_cap;
+  if (sc) { o.p = sc->p; o.s = sc->s; o.solar = sc->solar; o.t_od = sc->t_od; }
+  return o;
+}
+
+int mdr_msg_width(const mdr_obs_spec* sp) {
+  if (!sp) return 0;
+  return 4 + (sp->msg_thermal ? 4 : 0) + (sp->msg_hvac ? 3 : 0);
+}
+
+static int expected_feat(const mdr_obs_spec* sp) {
+  int base = 10 + (sp->hvac_state ? 2 : 0) + (sp->solar_state ? 1 : 0) + (sp->thermal_state ? 5 : 0);
+  return base + sp->n_comm * mdr_msg_width(sp);
+}
+
+int mdr_obs(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc, const double* p_dev,
+            float* obs, void* stream) {
+  if (!c || !sp || !sc || !obs) return fail(MDR_EARG, "mdr_obs: null argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_obs: context not bound");
+  if (sp->n_feat != expected_feat(sp)) return fail(MDR_EARG, "mdr_obs: n_feat does not match the flags");
+  if (sp->n_comm < 0 || sp->n_comm > 64) return fail(MDR_EARG, "mdr_obs: n_comm out of range");
+  if (sp->comm_mode == MDR_COMM_TABLE && sp->n_comm > 0 && !sp->comm_table)
+    return fail(MDR_EARG, "mdr_obs: TABLE mode without a table");
+  if (sp->comm_mode == MDR_COMM_TABLE && mdr_msg_width(sp) > 16) return fail(MDR_EARG, "mdr_obs: msg width");
+  ObsArgs o = obs_args(c, sp, sc);
+  const int lo = sp->n_comm / 2, hi = (sp->n_comm + 1) / 2;
+  size_t tile = ((size_t)kObsBlock * sp->n_feat + 3) & ~(size_t)3;
+  size_t msg = (size_t)(lo + kObsBlock + hi) * o.msg_w;
+  size_t bytes = (tile + msg) * sizeof(float);
+  if (bytes > 160 * 1024) return fail(MDR_EARG, "mdr_obs: obs row too wide for one LDS tile");
+  hipLaunchKernelGGL(k_obs, dim3(blocks(c->kp.n, kObsBlock)), dim3(kObsBlock), bytes, S(stream), c->kp, o,
+                     p_dev, obs);
+  LAUNCH_CHECK("k_obs");
+  return MDR_OK;
+}
+
+int mdr_halo_pack(mdr_ctx* c, const mdr_obs_spec* sp, float* out, void* stream) {
+  if (!c || !sp || !out) return fail(MDR_EARG, "mdr_halo_pack: null argument");
+  ObsArgs o = obs_args(c, sp, nullptr);
+  const int lo = sp->n_comm / 2, hi = (sp->n_comm + 1) / 2;
+  if (lo + hi == 0) return MDR_OK;
+  hipLaunchKernelGGL(k_halo_pack, dim3(1), dim3(64), 0, S(stream), c->kp, o, lo, hi, out);
+  LAUNCH_CHECK("k_halo_pack");
+  return MDR_OK;
+}
+
+// ------------------------------------------------------------------------------------ greedy
+static int greedy_scratch(mdr_ctx* c) {
+  const int64_t n = c->kp.n;
+  if (c->g_cap >= n) return MDR_OK;
+  hipFree(c->g_key); hipFree(c->g_key2); hipFree(c->g_ps); hipFree(c->g_incl);
+  hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
+  hipFree(c->g_kpos); hipFree(c->g_extra);
+  HIP_TRY(hipMalloc(&c->g_key, n * sizeof(double)));
+  HIP_TRY(hipMalloc(&c->g_key2, n * sizeof(double)));
+  HIP_TRY(hipMalloc(&c->g_ps, n * sizeof(double)));
+  HIP_TRY(hipMalloc(&c->g_incl, n * sizeof(double)));
+  HIP_TRY(hipMalloc(&c->g_idx, n * sizeof(int)));
+  HIP_TRY(hipMalloc(&c->g_idx2, n * sizeof(int)));
+  HIP_TRY(hipMalloc(&c->g_ls, n));
+  HIP_TRY(hipMalloc(&c->g_kpos, 2 * sizeof(int64_t)));
+  HIP_TRY(hipMalloc(&c->g_extra, 64 * sizeof(int64_t)));
+  size_t b1 = 0, b2 = 0;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, c->g_key, c->g_key2, c->g_idx, c->g_idx2, (int)n));
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b2, c->g_ps, c->g_incl, (int)n));
+  c->g_tmp_bytes = b1 > b2 ? b1 : b2;
+  HIP_TRY(hipMalloc(&c->g_tmp, c->g_tmp_bytes));
+  c->g_cap = n;
+  return MDR_OK;
+}
+
+int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
+  if (!c || !action) return fail(MDR_EARG, "mdr_ctrl_greedy: null argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_ctrl_greedy: context not bound");
+  int rc = greedy_scratch(c);
+  if (rc) return rc;
+  hipStream_t st = S(stream);
+  const int n = (int)c->kp.n;
+  hipLaunchKernelGGL(k_greedy_keys, dim3(blocks(n, 256)), dim3(256), 0, st, c->kp, c->g_key, c->g_idx);
+  LAUNCH_CHECK("k_greedy_keys");
+  size_t b = c->g_tmp_bytes;
+  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->g_tmp, b, c->g_key, c->g_key2, c->g_idx, c->g_idx2, n,
+                                             0, 64, st));
+  hipLaunchKernelGGL(k_greedy_gather, dim3(blocks(n, 256)), dim3(256), 0, st, c->kp, c->g_idx2, c->g_ps,
+                     c->g_ls);
+  LAUNCH_CHECK("k_greedy_gather");
+  b = c->g_tmp_bytes;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(c->g_tmp, b, c->g_ps, c->g_incl, n, st));
+  double pmin = INFINITY;
+  for (int k = 0; k < c->cfg.n_cap; ++k) pmin = fmin(pmin, c->cfg.cap_table[k] / c->cfg.cop);
+  hipLaunchKernelGGL(k_greedy_walk, dim3(1), dim3(256), 0, st, (int64_t)n, c->g_incl, c->g_ps, c->g_ls,
+                     budget, pmin, c->g_kpos, c->g_extra, 64);
+  LAUNCH_CHECK("k_greedy_walk");
+  hipLaunchKernelGGL(k_greedy_apply, dim3(blocks(n, 256)), dim3(256), 0, st, (int64_t)n, c->g_idx2,
+                     c->g_kpos, c->g_extra, action);
+  LAUNCH_CHECK("k_greedy_apply");
+  return MDR_OK;
+}
+
+// ------------------------------------------------------------------------------------ RCCL
+int mdr_rccl_unique_id(uint8_t* id128) {
+  if (!id128) return fail(MDR_EARG, "mdr_rccl_unique_id: null");
+  ncclUniqueId id;
+  RCCL_TRY(ncclGetUniqueId(&id));
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId size");
+  memcpy(id128, &id, 128);
+  return MDR_OK;
+}
+
+int mdr_rccl_init(mdr_ctx* c, const uint8_t* id128, int world, int rank) {
+  if (!c || !id128 || world < 1 || rank < 0 || rank >= world) return fail(MDR_EARG, "mdr_rccl_init: bad argument");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  ncclUniqueId id;
+  memcpy(&id, id128, 128);
+  RCCL_TRY(ncclCommInitRank(&c->comm, world, id, rank));
+  c->world = world;
+  c->rank = rank;
+  return MDR_OK;
+}
+
+int mdr_rccl_allreduce(mdr_ctx* c, void* buf, int64_t count, int dtype, void* stream) {
+  if (!c || !buf || count < 0) return fail(MDR_EARG, "mdr_rccl_allreduce: bad argument");
+  if (!c->comm) return fail(MDR_ESTATE, "mdr_rccl_allreduce: RCCL not initialised");
+  ncclDataType_t t = dtype == 0 ? ncclInt64 : ncclFloat64;
+  ncclRedOp_t op = dtype == 2 ? ncclMax : ncclSum;
+  RCCL_TRY(ncclAllReduce(buf, buf, (size_t)count, t, op, c->comm, S(stream)));
+  return MDR_OK;
+}
+
+int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
+                        int64_t act_stride, int mode, double* reward, int64_t rew_stride, void* stream) {
+  if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout_sharded: bad argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout_sharded: context not bound");
+  if (!c->comm) return fail(MDR_ESTATE, "mdr_rollout_sharded: RCCL not initialised");
+  if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout_sharded: bad action source");
+  if (mode == MDR_ACT_BANGBANG || mode == MDR_ACT_DEADBAND_BANGBANG)
+    return fail(MDR_EARG, "mdr_rollout_sharded: bang-bang sources need the per-step API");
+  if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
+    return fail(MDR_EARG, "mdr_rollout_sharded: common penalty modes need the per-step API");
+  hipStream_t st = S(stream);
+  int rc = stage_ticks(c, n, ticks, st);
+  if (rc) return rc;
+  HIP_TRY(hipMemsetAsync(c->d_slab, 0, 3 * c->slab_len * sizeof(unsigned long long), st));
+  c->ring = 0;
+  const bool la = lookahead_ok(mode);
+  for (int t = 0; t < n; ++t) {
+    const uint8_t* a = action ? action + (int64_t)t * act_stride : nullptr;
+    if (!la || t == 0) {
+      hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, a, mode,
+                         (uint64_t)0, c->d_ticks + t, slab_at(c, c->ring));
+      LAUNCH_CHECK("k_power_counts");
+    }
+    RCCL_TRY(ncclAllReduce(slab_at(c, c->ring), slab_at(c, c->ring), c->slab_len, ncclUint64, ncclSum,
+                           c->comm, st));
+    rc = launch_step(c, a, mode, TickArgs{}, c->d_ticks + t, reward + (int64_t)t * rew_stride,
+                     la ? mode : 0, MDR_CTRL_NONE, nullptr, nullptr, st);
+    if (rc) return rc;
+  }
+  c->counts_ready = false;
+  return MDR_OK;
+}
+
+// ------------------------------------------------------------------------------------ events
+int mdr_event_record(mdr_ctx* c, int slot, void* stream) {
+  if (!c || slot < 0 || slot >= 16) return fail(MDR_EARG, "mdr_event_record: bad slot");
+  HIP_TRY(hipEventRecord(c->ev[slot], S(stream)));
+  return MDR_OK;
+}
+
+int mdr_event_elapsed_ms(mdr_ctx* c, int s0, int s1, float* ms) {
+  if (!c || !ms || s0 < 0 || s1 < 0 || s0 >= 16 || s1 >= 16) return fail(MDR_EARG, "mdr_event_elapsed_ms: bad slot");
+  HIP_TRY(hipEventSynchronize(c->ev[s1]));
+  HIP_TRY(hipEventElapsedTime(ms, c->ev[s0], c->ev[s1]));
+  return MDR_OK;
+}
+
+}  // extern "C"

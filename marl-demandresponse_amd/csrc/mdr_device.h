@@ -1,0 +1,124 @@
+// mdr_device.h — per-house device math for the vectorised environment step (gfx950).
+//
+// Every floating-point expression keeps the reference's operation order (Python evaluates
+// left to right, one IEEE-754 rounding per operation); the library is compiled with
+// -ffp-contract=off so no a*b+c is fused into an FMA.  Division and sqrt are correctly rounded
+// on gfx950 (v_div_scale/v_div_fmas/v_div_fixup; v_sqrt_f64 + refinement), exp is ocml's
+// (<= 1 ulp), so a tick agrees with the reference to ~1e-13 relative and integer state is
+// bit-exact.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mdr {
+
+constexpr uint32_t kOnBit = 1u << 31;
+constexpr uint32_t kLockBit = 1u << 30;
+constexpr uint32_t kSsoMask = (1u << 30) - 1u;  // seconds_since_off saturates at 2^30-1 s (34 y)
+
+// ---------------------------------------------------------------------------- lockout FSM
+// HVAC.step, server/app/core/environment/cluster/hvac.py:43-64:
+//   if not on: sso += dt
+//   lockout = not (on or sso >= L)
+//   if lockout: on = False
+//   else: on = action; if on: sso = 0 elif sso + dt < L: lockout = True
+__device__ __forceinline__ uint32_t hvac_fsm(uint32_t w, bool action, int dt, int L) {
+  const bool on = (w & kOnBit) != 0;
+  int64_t sso = (int64_t)(w & kSsoMask);
+  if (!on) sso += dt;
+  const bool locked = !(on || sso >= (int64_t)L);
+  bool non = false, nlock = locked;
+  if (!locked) {
+    non = action;
+    if (non) sso = 0;
+    else if (sso + dt < (int64_t)L) nlock = true;
+  }
+  if (sso > (int64_t)kSsoMask) sso = kSsoMask;
+  if (sso < 0) sso = 0;
+  return (uint32_t)sso | (nlock ? kLockBit : 0u) | (non ? kOnBit : 0u);
+}
+
+__device__ __forceinline__ bool hv_on(uint32_t w) { return (w & kOnBit) != 0; }
+__device__ __forceinline__ bool hv_lock(uint32_t w) { return (w & kLockBit) != 0; }
+__device__ __forceinline__ uint32_t hv_sso(uint32_t w) { return w & kSsoMask; }
+
+// ---------------------------------------------------------------------------- RC thermal
+// Building.update_temperature, server/app/core/environment/cluster/building.py:141-222
+// (GridLAB-D 2-node analytic solution).  q_hvac = HVAC.get_heat_transfer (hvac.py:85-99),
+// solar = compute_solar_gain (per-tick scalar), t_od = previous tick's outdoor temperature.
+__device__ __forceinline__ void rc_update(double T, double Tm, double Ua, double Ca, double Cm,
+                                          double Hm, double q_hvac, double solar, double t_od,
+                                          double dt, double& T_out, double& Tm_out) {
+  const double od_k = t_od + 273.0;
+  const double t_k = T + 273.0;
+  const double tm_k = Tm + 273.0;
+  const double Qa = q_hvac + solar;
+  const double a = Cm * Ca / Hm;
+  const double UaHm = Ua + Hm;
+  const double b = Cm * UaHm / Hm + Ca;
+  const double c = Ua;
+  const double d = Qa + Ua * od_k;  // Qm (= 0) + Qa + Ua * od_k
+  const double disc = __builtin_sqrt(b * b - 4.0 * a * c);
+  const double two_a = 2.0 * a;
+  const double r1 = (-b + disc) / two_a;
+  const double r2 = (-b - disc) / two_a;
+  const double dTA0dt = Hm * tm_k / Ca - UaHm * t_k / Ca + Ua * od_k / Ca + Qa / Ca;
+  const double d_c = d / c;
+  const double A1 = (r2 * t_k - dTA0dt - r2 * d / c) / (r2 - r1);
+  const double A2 = t_k - d_c - A1;
+  const double UaHm_Hm = UaHm / Hm;
+  const double A3 = r1 * Ca / Hm + UaHm_Hm;
+  const double A4 = r2 * Ca / Hm + UaHm_Hm;
+  const double e1 = exp(r1 * dt);
+  const double e2 = exp(r2 * dt);
+  const double t_new = A1 * e1 + A2 * e2 + d_c;
+  const double tm_new = A1 * A3 * e1 + A2 * A4 * e2 + 0.0 + d_c;  // + g (= Qm/Hm = 0)
+  T_out = t_new - 273.0;
+  Tm_out = tm_new - 273.0;
+}
+
+// deadbandL2, server/app/utils/utils.py:4-23  (x**2 evaluated as x*x)
+__device__ __forceinline__ double deadband_l2(double target, double deadband, double value) {
+  const double hi = target + deadband / 2.0;
+  const double lo = target - deadband / 2.0;
+  if (hi < value) { const double x = value - hi; return x * x; }
+  if (lo > value) { const double x = lo - value; return x * x; }
+  return 0.0;
+}
+
+// ---------------------------------------------------------------------------- controllers
+// BangBangController.act (bangbang_controllers.py:54-65): on iff T > target.
+__device__ __forceinline__ bool ctrl_bangbang(double T, double target) { return T > target; }
+// DeadbandBangBangController.act (bangbang_controllers.py:25-42).
+__device__ __forceinline__ bool ctrl_deadband(double T, double target, double deadband, bool on) {
+  if (T < target - deadband / 2.0) return false;
+  if (T > target + deadband / 2.0) return true;
+  return on;
+}
+
+// ---------------------------------------------------------------------------- Philox4x32-10
+struct u32x4 { uint32_t x, y, z, w; };
+
+__device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    const uint32_t lo0 = 0xD2511F53u * c.x, hi0 = __umulhi(0xD2511F53u, c.x);
+    const uint32_t lo1 = 0xCD9E8D57u * c.z, hi1 = __umulhi(0xCD9E8D57u, c.z);
+    c = u32x4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+    k0 += 0x9E3779B9u;
+    k1 += 0xBB67AE85u;
+  }
+  return c;
+}
+
+// Random controller: Bernoulli(0.5) per (house, tick)
+__device__ __forceinline__ bool random_action(uint64_t seed, uint64_t gid, uint64_t tick) {
+  const u32x4 r = philox4x32_10(u32x4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)tick,
+                                      (uint32_t)(tick >> 32) ^ 0x5A17u},
+                                (uint32_t)seed, (uint32_t)(seed >> 32));
+  return (r.x & 1u) != 0;
+}
+
+__device__ __forceinline__ double u01(uint32_t x) { return ((double)x + 0.5) * 2.3283064365386963e-10; }
+
+}  // namespace mdr

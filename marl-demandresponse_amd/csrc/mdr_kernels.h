@@ -1,0 +1,74 @@
+// mdr_kernels.h — kernel parameter blocks shared by the kernels and the C-ABI host runtime.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/mdr.h"
+
+namespace mdr {
+
+constexpr int kCountShards = 64;  // atomic shards for the per-class ON counts
+constexpr int kObsBlock = 128;    // houses per obs tile
+constexpr int kActBangBang = 16;  // internal action modes: controller evaluated on the loaded state
+constexpr int kActDeadband = 17;
+
+// Everything per-context a kernel needs, by value (one 256-B kernel argument).
+struct KParams {
+  int64_t n, goff, n_global;
+  int dt, L, n_cap, penalty_mode;
+  double deadband, alpha_temp, alpha_sig, norm_temp, norm_sig;
+  double alpha_ind_l2, alpha_common_l2, alpha_common_max;
+  uint64_t seed;
+  double* t_air;
+  double* t_mass;
+  uint32_t* hvac;
+  const double* ua;
+  const double* ca;
+  const double* cm;
+  const double* hm;
+  const double* target;
+  const uint8_t* cap_idx;
+  const double* q_on;  // [n_cap] -cap/(1+lcf)      (device, context-owned)
+  const double* p_on;  // [n_cap] cap/cop
+};
+
+struct TickArgs {
+  double t_od_prev, solar, s_prev;
+  uint64_t tick;
+};
+
+struct PopArgs {
+  double target_temp, std_target, lo, hi, ca0, cm0, hm0, init_air, init_mass;
+};
+
+struct ObsArgs {
+  int n_feat, msg_w, n_comm, comm_mode;
+  int hvac_state, solar_state, thermal_state, msg_thermal, msg_hvac;
+  const int32_t* comm_table;
+  const float* halo_msg;  // [lo + hi][msg_w] or null
+  double norm_reg_sig, cfg_ua, cfg_ca, cfg_cm, cfg_hm, cfg_cop, cfg_lcf, cfg_cap;
+  double p, s, solar, t_od;
+};
+
+__global__ void k_power_counts(KParams p, const uint8_t* action, int action_mode, uint64_t tick,
+                               const TickArgs* tkp, unsigned long long* slab);
+__global__ void k_step(KParams p, const uint8_t* action, int action_mode, TickArgs tk,
+                       const TickArgs* tkp,
+                       const unsigned long long* counts, double* reward, int ctrl, uint8_t* ctrl_out,
+                       double* p_out, int lookahead, unsigned long long* next_slab,
+                       unsigned long long* zero_slab, double* pen_partial);
+__global__ void k_pen_reduce(const double* pen_partial, int nblk, double* partial2);
+__global__ void k_reward_finalize(KParams p, TickArgs tk, const unsigned long long* counts,
+                                  const double* partial2, double* reward);
+__global__ void k_populate(KParams p, PopArgs a);
+__global__ void k_obs(KParams p, ObsArgs o, const double* p_dev, float* obs);
+__global__ void k_halo_pack(KParams p, ObsArgs o, int lo, int hi, float* out);
+__global__ void k_greedy_keys(KParams p, double* key, int* idx);
+__global__ void k_greedy_gather(KParams p, const int* perm, double* psorted, uint8_t* lsorted);
+__global__ void k_greedy_walk(int64_t n, const double* incl, const double* psorted,
+                              const uint8_t* lsorted, double S, double pmin, int64_t* kpos,
+                              int64_t* extra, int max_extra);
+__global__ void k_greedy_apply(int64_t n, const int* perm, const int64_t* kpos, const int64_t* extra,
+                               uint8_t* action);
+
+}  // namespace mdr

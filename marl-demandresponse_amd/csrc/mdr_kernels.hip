@@ -1,0 +1,470 @@
+// mdr_kernels.hip — house-parallel kernels of the vectorised environment step (gfx950 / CDNA4).
+//
+// Bandwidth-bound elementwise work: one thread per house, SoA fp64 state/params loaded with
+// coalesced 8-B-per-lane accesses, the per-context cooling-capacity tables staged in LDS, the
+// cluster power reduced with wave ballots + LDS histogram + sharded global atomics (integer
+// counts per capacity class, so the sum is exact and order independent).  No MFMA: there is
+// no contraction on this path.
+#include "mdr_kernels.h"
+
+#include "mdr_device.h"
+
+namespace mdr {
+
+// --------------------------------------------------------------------------------------- helpers
+
+// Per-block histogram of ON houses per capacity class, flushed to the sharded slab with at most
+// n_cap atomics per block: slab[(blockIdx % kCountShards) * MDR_MAX_CAP + k].
+__device__ __forceinline__ void count_on(bool on, int cls, int n_cap, unsigned* hist,
+                                         unsigned long long* slab) {
+  const int lane = threadIdx.x & 63;
+  for (int k = 0; k < n_cap; ++k) {
+    const unsigned long long m = __ballot(on && cls == k);
+    if (lane == 0 && m) atomicAdd(&hist[k], (unsigned)__popcll(m));
+  }
+  __syncthreads();
+  if ((int)threadIdx.x < n_cap) {
+    const unsigned v = hist[threadIdx.x];
+    if (v) atomicAdd(&slab[(blockIdx.x % kCountShards) * n_cap + threadIdx.x],
+                     (unsigned long long)v);
+  }
+}
+
+// Cluster power of a tick from the (global) per-class counts: P = sum_k counts[k] * p_on[k].
+// cap/cop of the reference's capacity list are integers at the default config, so the sum is
+// exactly the reference's sequential float sum (cluster.py:82-88).
+__device__ __forceinline__ double power_from_counts(const unsigned long long* counts,
+                                                    const double* p_on, int n_cap) {
+  double P = 0.0;
+  for (int k = 0; k < n_cap; ++k) P += (double)counts[k] * p_on[k];
+  return P;
+}
+
+__device__ __forceinline__ bool tick_action(int mode, const uint8_t* action, int64_t i,
+                                            uint64_t seed, uint64_t gid, uint64_t tick) {
+  if (mode == MDR_ACT_BUFFER) return action[i] != 0;
+  if (mode == MDR_ACT_RANDOM) return random_action(seed, gid, tick);
+  return true;  // MDR_ACT_ALWAYS_ON
+}
+
+// --------------------------------------------------------------------------------------- K0
+// Phase 1: FSM only -> ON count per capacity class (cluster.py:82-88).  Reads 6 B per house.
+__global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* __restrict__ action,
+                                                      int action_mode, uint64_t tick0,
+                                                      const TickArgs* tkp,
+                                                      unsigned long long* __restrict__ slab) {
+  const uint64_t tick = tkp ? tkp->tick : tick0;
+  __shared__ unsigned hist[MDR_MAX_CAP];
+  if ((int)threadIdx.x < p.n_cap) hist[threadIdx.x] = 0;
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  bool on = false;
+  int cls = 0;
+  if (i < p.n) {
+    const bool a = tick_action(action_mode, action, i, p.seed, p.goff + i, tick);
+    on = hv_on(hvac_fsm(p.hvac[i], a, p.dt, p.L));
+    cls = p.cap_idx[i];
+  }
+  count_on(on, cls, p.n_cap, hist, slab);
+}
+
+// --------------------------------------------------------------------------------------- K1
+// Phase 2: fused FSM + RC thermal + reward (environment.py:86-101) for one tick.
+//   counts    : the tick's GLOBAL per-class ON counts (kCountShards x MDR_MAX_CAP slab, summed here)
+//   next_slab : when lookahead != 0, ON counts of tick+1 under the in-kernel action source
+//               (random / always-on / bang-bang on the new state) are accumulated here, so the
+//               next tick needs no phase-1 launch.
+__global__ void __launch_bounds__(256) k_step(KParams p, const uint8_t* __restrict__ action,
+                                              int action_mode, TickArgs tk0, const TickArgs* tkp,
+                                              const unsigned long long* __restrict__ counts,
+                                              double* __restrict__ reward, int ctrl,
+                                              uint8_t* __restrict__ ctrl_out, double* p_out,
+                                              int lookahead, unsigned long long* next_slab,
+                                              unsigned long long* zero_slab,
+                                              double* __restrict__ pen_partial) {
+  __shared__ double s_q_on[MDR_MAX_CAP];
+  __shared__ double s_p_on[MDR_MAX_CAP];
+  __shared__ unsigned long long s_cnt[MDR_MAX_CAP];
+  __shared__ unsigned hist[MDR_MAX_CAP];
+  __shared__ double s_red[2][4];
+  const int tid = threadIdx.x;
+  const TickArgs tk = tkp ? *tkp : tk0;
+  if (tid < p.n_cap) {
+    s_q_on[tid] = p.q_on[tid];
+    s_p_on[tid] = p.p_on[tid];
+    unsigned long long c = 0;
+    for (int s = 0; s < kCountShards; ++s) c += counts[s * p.n_cap + tid];
+    s_cnt[tid] = c;
+    hist[tid] = 0;
+  }
+  if (zero_slab && blockIdx.x == 0)
+    for (int j = tid; j < kCountShards * p.n_cap; j += blockDim.x) zero_slab[j] = 0ull;
+  __syncthreads();
+
+  // per-tick signal penalty (rewards_calculator.py:183-203), identical in every thread
+  const double P = power_from_counts(s_cnt, s_p_on, p.n_cap);
+  const double x = (P - tk.s_prev) / (double)p.n_global;
+  const double sig_term = p.alpha_sig * (x * x) / p.norm_sig;
+  if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
+
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
+  bool on1 = false;
+  int cls = 0;
+  double pen = 0.0;
+  if (i < p.n) {
+    const uint64_t gid = p.goff + i;
+    const uint32_t w0 = p.hvac[i];
+    const double T = p.t_air[i], Tm = p.t_mass[i];
+    const double tgt = p.target[i];
+    cls = p.cap_idx[i];
+    bool a;
+    if (action_mode == MDR_ACT_BUFFER) a = action[i] != 0;
+    else if (action_mode == MDR_ACT_RANDOM) a = random_action(p.seed, gid, tk.tick);
+    else if (action_mode == MDR_ACT_ALWAYS_ON) a = true;
+    else if (action_mode == kActBangBang) a = ctrl_bangbang(T, tgt);
+    else a = ctrl_deadband(T, tgt, p.deadband, hv_on(w0));
+    const uint32_t w = hvac_fsm(w0, a, p.dt, p.L);
+    const bool on = hv_on(w);
+    const double q = on ? s_q_on[cls] : 0.0;
+    double Tn, Tmn;
+    rc_update(T, Tm, p.ua[i], p.ca[i], p.cm[i], p.hm[i], q, tk.solar, tk.t_od_prev, (double)p.dt, Tn, Tmn);
+    p.t_air[i] = Tn;
+    p.t_mass[i] = Tmn;
+    p.hvac[i] = w;
+    pen = deadband_l2(tgt, p.deadband, Tn);
+    if (p.penalty_mode == MDR_PEN_INDIVIDUAL_L2) {
+      reward[i] = -(p.alpha_temp * pen / p.norm_temp + sig_term);
+    } else {
+      reward[i] = pen;  // finalised by k_reward_finalize once the cluster reduction is known
+    }
+    if (ctrl != MDR_CTRL_NONE && ctrl_out) {
+      const bool a1 = ctrl == MDR_CTRL_BANGBANG ? ctrl_bangbang(Tn, tgt)
+                                                 : ctrl_deadband(Tn, tgt, p.deadband, on);
+      ctrl_out[i] = a1 ? 1 : 0;
+    }
+    if (lookahead) {
+      bool an;
+      if (lookahead == MDR_ACT_RANDOM) an = random_action(p.seed, gid, tk.tick + 1);
+      else if (lookahead == MDR_ACT_ALWAYS_ON) an = true;
+      else if (lookahead == kActBangBang) an = ctrl_bangbang(Tn, tgt);
+      else an = ctrl_deadband(Tn, tgt, p.deadband, on);
+      on1 = hv_on(hvac_fsm(w, an, p.dt, p.L));
+    }
+  }
+  if (lookahead) count_on(on1, cls, p.n_cap, hist, next_slab);
+  if (p.penalty_mode != MDR_PEN_INDIVIDUAL_L2) {
+    // block partials of sum(pen/N) and max(pen) for the common penalty modes
+    double s = (i < p.n) ? pen / (double)p.n_global : 0.0;
+    double m = pen;
+    for (int off = 32; off > 0; off >>= 1) {
+      s += __shfl_xor(s, off);
+      m = fmax(m, __shfl_xor(m, off));
+    }
+    if ((tid & 63) == 0) { s_red[0][tid >> 6] = s; s_red[1][tid >> 6] = m; }
+    __syncthreads();
+    if (tid == 0) {
+      double bs = 0.0, bm = 0.0;
+      for (int w2 = 0; w2 < (int)(blockDim.x >> 6); ++w2) { bs += s_red[0][w2]; bm = fmax(bm, s_red[1][w2]); }
+      pen_partial[2 * blockIdx.x] = bs;
+      pen_partial[2 * blockIdx.x + 1] = bm;
+    }
+  }
+}
+
+// Fixed-order reduction of the per-block penalty partials -> partial2 = {sum pen/N, max pen}.
+__global__ void __launch_bounds__(256) k_pen_reduce(const double* __restrict__ pen_partial, int nblk,
+                                                    double* __restrict__ partial2) {
+  __shared__ double ss[256], sm[256];
+  double s = 0.0, m = 0.0;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) { s += pen_partial[2 * b]; m = fmax(m, pen_partial[2 * b + 1]); }
+  ss[threadIdx.x] = s;
+  sm[threadIdx.x] = m;
+  __syncthreads();
+  for (int w = blockDim.x / 2; w > 0; w >>= 1) {
+    if ((int)threadIdx.x < w) {
+      ss[threadIdx.x] += ss[threadIdx.x + w];
+      sm[threadIdx.x] = fmax(sm[threadIdx.x], sm[threadIdx.x + w]);
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) { partial2[0] = ss[0]; partial2[1] = sm[0]; }
+}
+
+// rewards for common_L2 / common_max_error / mixture (rewards_calculator.py:46-181)
+__global__ void __launch_bounds__(256) k_reward_finalize(KParams p, TickArgs tk,
+                                                         const unsigned long long* __restrict__ counts,
+                                                         const double* __restrict__ partial2,
+                                                         double* __restrict__ reward) {
+  __shared__ double s_p_on[MDR_MAX_CAP];
+  __shared__ unsigned long long s_cnt[MDR_MAX_CAP];
+  const int tid = threadIdx.x;
+  if (tid < p.n_cap) {
+    s_p_on[tid] = p.p_on[tid];
+    unsigned long long c = 0;
+    for (int s = 0; s < kCountShards; ++s) c += counts[s * p.n_cap + tid];
+    s_cnt[tid] = c;
+  }
+  __syncthreads();
+  const double P = power_from_counts(s_cnt, s_p_on, p.n_cap);
+  const double x = (P - tk.s_prev) / (double)p.n_global;
+  const double sig_term = p.alpha_sig * (x * x) / p.norm_sig;
+  const double common_l2 = partial2[0], common_max = partial2[1];
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
+  if (i >= p.n) return;
+  const double pen = reward[i];
+  double tp;
+  if (p.penalty_mode == MDR_PEN_COMMON_L2) tp = common_l2;
+  else if (p.penalty_mode == MDR_PEN_COMMON_MAX) tp = common_max;
+  else tp = (p.alpha_ind_l2 * pen + p.alpha_common_l2 * common_l2 + p.alpha_common_max * common_max) /
+            (p.alpha_ind_l2 + p.alpha_common_l2 + p.alpha_common_max);
+  reward[i] = -(p.alpha_temp * tp / p.norm_temp + sig_term);
+}
+
+// --------------------------------------------------------------------------------------- population
+// Synthetic population: the reference noise model (building.py:224-267, hvac.py:66-70) drawn
+// from Philox4x32-10 keyed by (seed, global house id) — identical for any sharding.
+__device__ __forceinline__ double triangular(double u, double lo, double hi, double mode) {
+  // random.triangular's inverse CDF
+  double c = (mode - lo) / (hi - lo);
+  if (u > c) { u = 1.0 - u; c = 1.0 - c; const double t = lo; lo = hi; hi = t; }
+  return lo + (hi - lo) * sqrt(u * c);
+}
+
+__global__ void __launch_bounds__(256) k_populate(KParams p, PopArgs a) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const uint64_t gid = p.goff + i;
+  const u32x4 r0 = philox4x32_10(u32x4{(uint32_t)gid, (uint32_t)(gid >> 32), 0x9090u, 0u},
+                                 (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+  const u32x4 r1 = philox4x32_10(u32x4{(uint32_t)gid, (uint32_t)(gid >> 32), 0x9090u, 1u},
+                                 (uint32_t)p.seed, (uint32_t)(p.seed >> 32));
+  const double g = sqrt(-2.0 * log(u01(r0.x))) * cos(6.283185307179586 * u01(r0.y));
+  double* pt = const_cast<double*>(p.target);
+  pt[i] = a.target_temp + fabs(g * a.std_target);
+  const_cast<double*>(p.ua)[i] = triangular(u01(r0.z), a.lo, a.hi, 1.0);
+  const_cast<double*>(p.cm)[i] = a.cm0 * triangular(u01(r0.w), a.lo, a.hi, 1.0);
+  const_cast<double*>(p.ca)[i] = a.ca0 * triangular(u01(r1.x), a.lo, a.hi, 1.0);
+  const_cast<double*>(p.hm)[i] = a.hm0 * triangular(u01(r1.y), a.lo, a.hi, 1.0);
+  const_cast<uint8_t*>(p.cap_idx)[i] = (uint8_t)(((uint64_t)r1.z * (uint64_t)p.n_cap) >> 32);
+  p.t_air[i] = a.init_air;
+  p.t_mass[i] = a.init_mass;
+  p.hvac[i] = kOnBit;
+}
+
+// --------------------------------------------------------------------------------------- obs
+// norm_state_dict (norm.py:178-218) as float32 rows, staged through LDS and flushed with
+// 16-B coalesced stores.  Message sources for a block [b0, b0+B) of the ring topology are the
+// houses [b0 - lo, b0 + B + hi); their message features are computed once into LDS.
+__device__ __forceinline__ void msg_features(const KParams& p, const ObsArgs& o, int64_t j,
+                                             float* dst) {
+  const uint32_t w = p.hvac[j];
+  const int cls = p.cap_idx[j];
+  const double pmax = p.p_on[cls];
+  const double R = o.norm_reg_sig;
+  dst[0] = (float)((p.t_air[j] - p.target[j]) / 5.0);
+  dst[1] = (float)trunc((double)hv_sso(w) / (double)p.L);
+  dst[2] = (float)((hv_on(w) ? pmax : 0.0) / R);
+  dst[3] = (float)(pmax / R);
+  int f = 4;
+  if (o.msg_thermal) {
+    dst[f++] = (float)(p.ua[j] / o.cfg_ua);
+    dst[f++] = (float)(p.ca[j] / o.cfg_ca);
+    dst[f++] = (float)(p.cm[j] / o.cfg_cm);
+    dst[f++] = (float)(p.hm[j] / o.cfg_hm);
+  }
+  if (o.msg_hvac) {
+    dst[f++] = (float)o.cfg_cop;
+    dst[f++] = (float)o.cfg_lcf;
+    dst[f++] = (float)o.cfg_cap;
+  }
+}
+
+__global__ void __launch_bounds__(kObsBlock) k_obs(KParams p, ObsArgs o, const double* p_dev,
+                                                   float* __restrict__ obs) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int F = o.n_feat, M = o.msg_w, K = o.n_comm;
+  const int lo = K / 2, hi = (K + 1) / 2;
+  const int64_t b0 = (int64_t)blockIdx.x * kObsBlock;
+  const int nb = (int)min((int64_t)kObsBlock, p.n - b0);
+  float* tile = smem;                                  // [kObsBlock][F]
+  float* msg = smem + ((kObsBlock * F + 3) & ~3);      // [lo + kObsBlock + hi][M]
+  const double P = p_dev ? *p_dev : o.p;
+  const double R = o.norm_reg_sig;
+
+  if (o.comm_mode == MDR_COMM_RING && K > 0) {
+    const int nsrc = lo + nb + hi;
+    for (int s = threadIdx.x; s < nsrc; s += kObsBlock) {
+      int64_t j = b0 - lo + s;              // local index, may fall outside the shard
+      if (o.halo_msg && (j < 0 || j >= p.n)) {
+        // multi-GPU ring: [0, lo) = houses before the shard, [lo, lo+hi) = houses after it
+        const int h = j < 0 ? (int)(j + lo) : (int)(lo + (j - p.n));
+        for (int m = 0; m < M; ++m) msg[s * M + m] = o.halo_msg[h * M + m];
+      } else {
+        j %= p.n;
+        if (j < 0) j += p.n;
+        msg_features(p, o, j, msg + s * M);
+      }
+    }
+  }
+  __syncthreads();
+  const int t = threadIdx.x;
+  if (t < nb) {
+    const int64_t i = b0 + t;
+    float* row = tile + t * F;
+    const uint32_t w = p.hvac[i];
+    int f = 0;
+    row[f++] = hv_on(w) ? 1.f : 0.f;
+    row[f++] = hv_lock(w) ? 1.f : 0.f;
+    row[f++] = (float)trunc((double)hv_sso(w) / (double)p.L);
+    row[f++] = 1.f;  // int(lockout_duration / lockout_duration)
+    if (o.hvac_state) { row[f++] = (float)(o.cfg_cop / o.cfg_cop); row[f++] = (float)(o.cfg_lcf / o.cfg_lcf); }
+    row[f++] = (float)(P / R);
+    row[f++] = (float)(o.s / (R * (double)p.n_global));
+    row[f++] = (float)p.deadband;
+    const double tgt = p.target[i];
+    row[f++] = (float)((p.t_air[i] - 20.0) / 5.0);
+    row[f++] = (float)((p.t_mass[i] - 20.0) / 5.0);
+    row[f++] = (float)((tgt - 20.0) / 5.0);
+    if (o.solar_state) row[f++] = (float)(o.solar / 1000.0);
+    if (o.thermal_state) {
+      row[f++] = (float)(p.ua[i] / o.cfg_ua);
+      row[f++] = (float)(p.ca[i] / o.cfg_ca);
+      row[f++] = (float)(p.cm[i] / o.cfg_cm);
+      row[f++] = (float)(p.hm[i] / o.cfg_hm);
+      row[f++] = (float)((o.t_od - 20.0) / 5.0);
+    }
+    if (K > 0) {
+      if (o.comm_mode == MDR_COMM_RING) {
+        // neighbours [i-lo .. i-1, i+1 .. i+hi] (agent_communication_builder.py:65-83)
+        for (int k = 0; k < K; ++k) {
+          const int s = k < lo ? (t + k) : (t + lo + 1 + (k - lo));
+          for (int m = 0; m < M; ++m) row[f++] = msg[s * M + m];
+        }
+      } else {
+        float tmp[16];
+        for (int k = 0; k < K; ++k) {
+          const int64_t j = o.comm_table[i * K + k];
+          msg_features(p, o, j, tmp);
+          for (int m = 0; m < M; ++m) row[f++] = tmp[m];
+        }
+      }
+    }
+  }
+  __syncthreads();
+  // coalesced flush of the contiguous tile obs[b0 .. b0+nb) rows
+  const int64_t nflt = (int64_t)nb * F;
+  float* dst = obs + b0 * F;
+  if ((((uintptr_t)dst) & 15) == 0) {
+    const int64_t n4 = nflt >> 2;
+    for (int64_t q = threadIdx.x; q < n4; q += kObsBlock)
+      reinterpret_cast<float4*>(dst)[q] = reinterpret_cast<const float4*>(tile)[q];
+    for (int64_t q = (n4 << 2) + threadIdx.x; q < nflt; q += kObsBlock) dst[q] = tile[q];
+  } else {
+    for (int64_t q = threadIdx.x; q < nflt; q += kObsBlock) dst[q] = tile[q];
+  }
+}
+
+// message features of the first `lo` (tail) / last `hi` (head) houses of this shard, for the
+// neighbouring shards' ring halos: out[0..hi) = first hi houses, out[hi..hi+lo) = last lo houses
+__global__ void k_halo_pack(KParams p, ObsArgs o, int lo, int hi, float* out) {
+  const int t = threadIdx.x;
+  const int M = o.msg_w;
+  if (t < hi) msg_features(p, o, t % p.n, out + t * M);
+  else if (t < hi + lo) {
+    int64_t j = p.n - lo + (t - hi);
+    if (j < 0) j = ((j % p.n) + p.n) % p.n;
+    msg_features(p, o, j, out + t * M);
+  }
+}
+
+// --------------------------------------------------------------------------------------- greedy
+// GreedyMyopic.get_action (greedy_myopic_controller.py:67-104), device form:
+//   key_i = -(T_i - target_i), sorted ascending (stable radix sort; pandas' quicksort tie order
+//   is implementation-defined, parity on exact key ties is unpinned).  Then the sequential rule
+//   take_j  iff  P_j + tot < S  or  (|P_j + tot - S| < |tot - S| and not lockout_j)
+// is evaluated as: a prefix of the sorted order is taken while the inclusive prefix sum of P is
+// < S (k = first index where it is not); from k on, with gap g = S - tot, item j is taken iff
+// P_j < g or (P_j < 2g and not lockout_j) — gap-dependent, so a single workgroup walks the
+// remaining order with 256-wide ballots until g can no longer admit any class (2g <= min P).
+__global__ void k_greedy_keys(KParams p, double* __restrict__ key, int* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  key[i] = -(p.t_air[i] - p.target[i]);
+  idx[i] = (int)i;
+}
+
+__global__ void k_greedy_gather(KParams p, const int* __restrict__ perm, double* __restrict__ psorted,
+                                uint8_t* __restrict__ lsorted) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= p.n) return;
+  const int i = perm[j];
+  psorted[j] = p.p_on[p.cap_idx[i]];
+  lsorted[j] = hv_lock(p.hvac[i]) ? 1 : 0;
+}
+
+// single workgroup: k from the inclusive prefix sums, then the gap walk; writes the take flag
+// for sorted positions >= k into flag_sorted (positions < k are implied) and kpos[0] = k.
+__global__ void __launch_bounds__(256) k_greedy_walk(int64_t n, const double* __restrict__ incl,
+                                                     const double* __restrict__ psorted,
+                                                     const uint8_t* __restrict__ lsorted, double S,
+                                                     double pmin, int64_t* kpos,
+                                                     int64_t* extra, int max_extra) {
+  __shared__ int64_t s_k;
+  __shared__ int s_ne;
+  __shared__ double s_tot;
+  if (threadIdx.x == 0) {
+    // first k with incl[k] >= S  (all earlier items satisfy P + tot < S); binary search
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const int64_t mid = (lo + hi) / 2;
+      if (incl[mid] < S) lo = mid + 1; else hi = mid;
+    }
+    s_k = lo;
+    s_tot = lo > 0 ? incl[lo - 1] : 0.0;
+    s_ne = 0;
+  }
+  __syncthreads();
+  int64_t pos = s_k;
+  while (pos < n) {
+    const double tot = s_tot;
+    // once tot >= S nothing is taken (P > 0); with gap g = S - tot an item needs P < 2g
+    // (conservative margin: the exact predicate below decides)
+    if (!(tot < S) || 2.0 * (S - tot) < pmin * (1.0 - 1e-9)) break;
+    const int64_t j = pos + threadIdx.x;
+    bool take = false;
+    if (j < n) {
+      const double pj = psorted[j];
+      take = (pj + tot < S) || (fabs(pj + tot - S) < fabs(tot - S) && !lsorted[j]);
+    }
+    __shared__ unsigned long long s_bal[4];
+    const unsigned long long b = __ballot(take);
+    if ((threadIdx.x & 63) == 0) s_bal[threadIdx.x >> 6] = b;
+    __syncthreads();
+    int first = -1;
+    for (int w = 0; w < 4; ++w)
+      if (s_bal[w]) { first = w * 64 + __ffsll((long long)s_bal[w]) - 1; break; }
+    __syncthreads();
+    if (first < 0) { pos += blockDim.x; continue; }
+    if (threadIdx.x == 0) {
+      const int64_t jj = pos + first;
+      if (s_ne < max_extra) extra[s_ne] = jj;
+      s_ne++;
+      s_tot = tot + psorted[jj];
+    }
+    __syncthreads();
+    pos += first + 1;
+  }
+  if (threadIdx.x == 0) { kpos[0] = s_k; kpos[1] = s_ne < max_extra ? s_ne : max_extra; }
+}
+
+__global__ void k_greedy_apply(int64_t n, const int* __restrict__ perm, const int64_t* kpos,
+                               const int64_t* extra, uint8_t* __restrict__ action) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  bool take = j < kpos[0];
+  const int64_t ne = kpos[1];
+  for (int64_t e = 0; e < ne; ++e) take |= (extra[e] == j);
+  action[perm[j]] = take ? 1 : 0;
+}
+
+}  // namespace mdr

@@ -1,0 +1,160 @@
+"""ctypes binding of the C ABI in include/mdr.h (libmdr_hip.so, built in-tree for gfx950).
+
+There is no fallback: if the library is missing or fails to load, ``load()`` raises
+:class:`MdrLibraryError`.  The product path never computes the step on the CPU.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MDR_LIB", os.path.join(HERE, "libmdr_hip.so"))
+
+ABI_VERSION = 1
+MAX_CAP = 64
+
+# enums (mdr.h)
+ACT_BUFFER, ACT_RANDOM, ACT_ALWAYS_ON, ACT_BANGBANG, ACT_DEADBAND_BANGBANG = 0, 1, 2, 16, 17
+CTRL_NONE, CTRL_BANGBANG, CTRL_DEADBAND_BANGBANG = 0, 1, 2
+COMM_RING, COMM_TABLE = 0, 1
+PEN_MODES = {"individual_L2": 0, "common_L2": 1, "common_max_error": 2, "mixture": 3}
+ERRORS = {-1: "MDR_EARG", -2: "MDR_EHIP", -3: "MDR_ERCCL", -4: "MDR_ENOMEM", -5: "MDR_ESTATE"}
+
+
+class MdrLibraryError(RuntimeError):
+    """libmdr_hip.so is missing or unusable (no CPU fallback exists)."""
+
+
+class MdrError(RuntimeError):
+    pass
+
+
+class mdr_config(C.Structure):
+    _fields_ = [
+        ("abi_version", C.c_int32), ("device", C.c_int32),
+        ("n_local", C.c_int64), ("global_offset", C.c_int64), ("n_global", C.c_int64),
+        ("dt", C.c_int32), ("lockout_duration", C.c_int32),
+        ("cop", C.c_double), ("lcf", C.c_double), ("deadband", C.c_double),
+        ("n_cap", C.c_int32), ("penalty_mode", C.c_int32),
+        ("cap_table", C.c_double * MAX_CAP),
+        ("alpha_temp", C.c_double), ("alpha_sig", C.c_double),
+        ("norm_temp", C.c_double), ("norm_sig", C.c_double),
+        ("alpha_ind_l2", C.c_double), ("alpha_common_l2", C.c_double), ("alpha_common_max", C.c_double),
+        ("seed", C.c_uint64),
+    ]
+
+
+class mdr_soa(C.Structure):
+    _fields_ = [(k, C.c_void_p) for k in
+                ("t_air", "t_mass", "hvac", "ua", "ca", "cm", "hm", "target", "cap_idx")]
+
+
+class mdr_tick(C.Structure):
+    _fields_ = [("t_od_prev", C.c_double), ("solar", C.c_double), ("s_prev", C.c_double),
+                ("tick", C.c_uint64)]
+
+
+class mdr_pop_spec(C.Structure):
+    _fields_ = [(k, C.c_double) for k in
+                ("target_temp", "std_target", "thermo_lo", "thermo_hi", "ca", "cm", "hm",
+                 "init_air", "init_mass")]
+
+
+class mdr_obs_spec(C.Structure):
+    _fields_ = [
+        ("n_feat", C.c_int32), ("hvac_state", C.c_int32), ("solar_state", C.c_int32),
+        ("thermal_state", C.c_int32), ("msg_thermal", C.c_int32), ("msg_hvac", C.c_int32),
+        ("n_comm", C.c_int32), ("comm_mode", C.c_int32),
+        ("comm_table", C.c_void_p), ("halo_msg", C.c_void_p),
+        ("norm_reg_sig", C.c_double), ("cfg_ua", C.c_double), ("cfg_ca", C.c_double),
+        ("cfg_cm", C.c_double), ("cfg_hm", C.c_double), ("cfg_cap", C.c_double),
+    ]
+
+
+class mdr_obs_scalars(C.Structure):
+    _fields_ = [("p", C.c_double), ("s", C.c_double), ("solar", C.c_double), ("t_od", C.c_double)]
+
+
+P, VP, I, I64, U64, D = C.POINTER, C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_double
+
+# name -> (restype, argtypes); every symbol declared in include/mdr.h
+SIGNATURES = {
+    "mdr_abi_version": (I, []),
+    "mdr_abi_sizes": (I, [P(I64), I]),
+    "mdr_last_error": (C.c_char_p, []),
+    "mdr_create": (I, [P(VP), P(mdr_config)]),
+    "mdr_destroy": (I, [VP]),
+    "mdr_bind": (I, [VP, P(mdr_soa)]),
+    "mdr_populate": (I, [VP, P(mdr_pop_spec), VP]),
+    "mdr_power_counts": (I, [VP, VP, I, U64, VP]),
+    "mdr_counts_buffer": (I, [VP, P(VP), P(I)]),
+    "mdr_step": (I, [VP, VP, I, P(mdr_tick), VP, I, I, VP, VP, VP]),
+    "mdr_penalty_partials": (I, [VP, VP]),
+    "mdr_penalty_buffer": (I, [VP, P(VP)]),
+    "mdr_reward_finalize": (I, [VP, P(mdr_tick), VP, VP]),
+    "mdr_rollout": (I, [VP, I, P(mdr_tick), VP, I64, I, VP, I64, I, VP]),
+    "mdr_msg_width": (I, [P(mdr_obs_spec)]),
+    "mdr_obs": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, VP, VP]),
+    "mdr_halo_pack": (I, [VP, P(mdr_obs_spec), VP, VP]),
+    "mdr_ctrl_greedy": (I, [VP, D, VP, VP]),
+    "mdr_rccl_unique_id": (I, [VP]),
+    "mdr_rccl_init": (I, [VP, VP, I, I]),
+    "mdr_rccl_allreduce": (I, [VP, VP, I64, I, VP]),
+    "mdr_rollout_sharded": (I, [VP, I, P(mdr_tick), VP, I64, I, VP, I64, VP]),
+    "mdr_event_record": (I, [VP, I, VP]),
+    "mdr_event_elapsed_ms": (I, [VP, I, I, P(C.c_float)]),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libmdr_hip.so (after torch, so one HIP runtime serves both) and bind SIGNATURES."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        import torch  # noqa: F401  (torch's libamdhip64 / librccl must be the process's copies)
+
+        if not os.path.exists(path):
+            raise MdrLibraryError(
+                f"{path} not found: build it with `python marl-demandresponse_amd/build_ext.py` "
+                "(or __graft_entry__.build()); there is no CPU fallback")
+        try:
+            lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+        except OSError as e:
+            raise MdrLibraryError(f"cannot load {path}: {e}") from e
+        for name, (res, args) in SIGNATURES.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.mdr_abi_version() != ABI_VERSION:
+            raise MdrLibraryError("libmdr_hip.so ABI version mismatch; rebuild it")
+        sizes = (C.c_int64 * 6)()
+        lib.mdr_abi_sizes(sizes, 6)
+        want = [C.sizeof(t) for t in (mdr_config, mdr_soa, mdr_tick, mdr_pop_spec, mdr_obs_spec,
+                                      mdr_obs_scalars)]
+        if list(sizes) != want:
+            raise MdrLibraryError(f"ABI struct sizes differ: library {list(sizes)} vs binding {want}")
+        _lib = lib
+        return lib
+
+
+def check(rc: int, what: str = "") -> None:
+    if rc != 0:
+        msg = _lib.mdr_last_error().decode() if _lib is not None else ""
+        raise MdrError(f"{what or 'mdr call'} failed: {ERRORS.get(rc, rc)}: {msg}")
+
+
+def ptr(t) -> int:
+    """Raw device pointer of a torch tensor (None -> NULL)."""
+    return 0 if t is None else t.data_ptr()
+
+
+def stream_handle(device) -> int:
+    import torch
+
+    return torch.cuda.current_stream(device).cuda_stream

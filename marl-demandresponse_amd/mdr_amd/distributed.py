@@ -1,0 +1,107 @@
+"""Multi-GPU: one process per GPU, houses sharded contiguously, RCCL over xGMI for the exchanges.
+
+The path partitions naturally: every house is independent except for ONE scalar
+coupling per tick, the cluster power (and, for the common penalty modes, the cluster penalty
+sum/max).  Per tick each rank runs phase 1 on its shard, the tiny per-class ON-count slab is
+sum-allreduced with RCCL (exact integer counts, so every rank derives the identical P), then
+phase 2.  Scalar drivers (outdoor temperature, solar gain, signal) are replicated: every rank
+draws them from the same host RNG stream, so nothing is broadcast.  Messages of the
+``neighbours`` ring cross shard edges: ``ring_halo`` exchanges the lo/hi edge houses' message
+features (all-gather of 2*5 rows per rank).
+
+The RCCL communicator is created by libmdr_hip (ncclCommInitRank) from a unique id that rank 0
+draws and ``torch.distributed`` broadcasts, so the per-tick allreduces are issued from C on the
+compute stream (``mdr_rollout_sharded``) without a Python round trip per tick.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+
+class RcclComm:
+    """Collectives of a sharded Environment, over the libmdr_hip RCCL communicator."""
+
+    def __init__(self):
+        import torch.distributed as dist
+
+        if not dist.is_initialized():
+            raise RuntimeError("init torch.distributed (backend 'nccl' = RCCL) before RcclComm()")
+        self.dist = dist
+        self.rank = dist.get_rank()
+        self.world = dist.get_world_size()
+        self._attached = set()
+
+    def attach(self, shard) -> None:
+        import torch
+
+        if id(shard) in self._attached:
+            return
+        lib = shard.lib
+        uid = torch.zeros(128, dtype=torch.uint8)
+        if self.rank == 0:
+            buf = (C.c_uint8 * 128)()
+            L.check(lib.mdr_rccl_unique_id(buf), "mdr_rccl_unique_id")
+            uid = torch.tensor(list(bytes(buf)), dtype=torch.uint8)
+        dev_uid = uid.to(shard.device)
+        self.dist.broadcast(dev_uid, src=0)
+        host = bytes(dev_uid.cpu().tolist())
+        arr = (C.c_uint8 * 128).from_buffer_copy(host)
+        L.check(lib.mdr_rccl_init(shard.ctx, arr, self.world, self.rank), "mdr_rccl_init")
+        self._attached.add(id(shard))
+
+    def allreduce_counts(self, shard) -> None:
+        ptr, n = shard.counts_buffer()
+        L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, ptr, n, 0, shard.stream()), "allreduce counts")
+
+    def allreduce_penalty(self, shard) -> None:
+        p = C.c_void_p()
+        L.check(shard.lib.mdr_penalty_buffer(shard.ctx, C.byref(p)), "mdr_penalty_buffer")
+        L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, p.value, 1, 1, shard.stream()), "allreduce pen sum")
+        L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, p.value + 8, 1, 2, shard.stream()), "allreduce pen max")
+
+    def rollout(self, shard, ticks, actions, mode, rewards) -> None:
+        arr = (L.mdr_tick * len(ticks))(*ticks)
+        n = shard.n
+        L.check(shard.lib.mdr_rollout_sharded(shard.ctx, len(ticks), arr, L.ptr(actions),
+                                              n if actions is not None else 0, mode, L.ptr(rewards), n,
+                                              shard.stream()), "mdr_rollout_sharded")
+
+    def ring_halo(self, shard, spec):
+        """Message features of the houses just before / after this shard on the global ring."""
+        import torch
+
+        k = spec.n_comm
+        lo, hi = k // 2, (k + 1) // 2
+        m = shard.lib.mdr_msg_width(C.byref(spec))
+        if shard.n < max(lo, hi):
+            raise NotImplementedError("shards smaller than the ring half-width")
+        mine = torch.empty((hi + lo, m), dtype=torch.float32, device=shard.device)
+        shard.halo_pack(spec, mine)
+        allh = [torch.empty_like(mine) for _ in range(self.world)]
+        self.dist.all_gather(allh, mine)
+        prev, nxt = allh[(self.rank - 1) % self.world], allh[(self.rank + 1) % self.world]
+        # rows [hi, hi+lo) of a pack = that shard's last lo houses; rows [0, hi) = its first hi
+        return torch.cat([prev[hi:hi + lo], nxt[:hi]]).contiguous()
+
+    def allgather_state(self, shard, st: dict, prm: dict, n: int):
+        """Full-cluster host copies of the state/params (dict obs of a sharded env: messages
+        reference houses on other shards)."""
+        import torch
+
+        out_st, out_prm = {}, {}
+        for src, dst, keys in ((st, out_st, ("T", "Tm", "on", "lock", "sso")),
+                               (prm, out_prm, ("ua", "ca", "cm", "hm", "target", "cap_idx"))):
+            for key in keys:
+                a = np.asarray(src[key])
+                t = torch.from_numpy(np.ascontiguousarray(a.astype(np.float64))).to(shard.device)
+                sizes = [None] * self.world
+                self.dist.all_gather_object(sizes, int(t.numel()))
+                parts = [torch.empty(s, dtype=torch.float64, device=shard.device) for s in sizes]
+                self.dist.all_gather(parts, t)
+                full = torch.cat(parts).cpu().numpy()
+                dst[key] = full.astype(a.dtype) if a.dtype != np.float64 else full
+        return out_st, out_prm

@@ -1,0 +1,160 @@
+"""Per-tick scalar drivers, computed on the host in the reference's own arithmetic and RNG order.
+
+These are O(1) per tick (the same value for every house), so they stay on the host and reach the
+kernels as ``mdr_tick`` arguments.  Each function keeps the reference's expression order so the
+values are bit-identical (pinned by tests/test_drivers_golden.py):
+
+  solar_gain      server/app/utils/utils.py:42-117
+  od_temp         server/app/core/environment/environment.py:132-159
+  Signal          server/app/core/environment/power_grid/signal_calculator.py:11-129
+  GridSignal      server/app/core/environment/power_grid/power_grid.py:21-161
+  deadband_l2     server/app/utils/utils.py:4-23 (scalar, for the reward normalisers)
+"""
+from __future__ import annotations
+
+import datetime as _dt
+import math
+import random as _random
+
+import numpy as np
+
+# CIBSE solar cooling load regression: (coefficient, x power, y power), summed in this order
+SOLAR_TERMS = (
+    (4.36579418e01, 0, 0), (1.58055357e02, 1, 0), (8.76635241e01, 0, 1), (-4.55944821e01, 2, 0),
+    (3.24275366e00, 2, 1), (-4.56096472e-01, 2, 2), (-1.47795612e01, 0, 2), (4.68950855e00, 1, 2),
+    (-3.73313090e01, 1, 1), (5.78827663e00, 3, 0), (1.04354810e00, 0, 3), (2.12969604e-02, 3, 1),
+    (2.58881400e-03, 3, 2), (-5.11397219e-04, 3, 3), (1.56398008e-02, 2, 3),
+    (-1.18302764e-01, 1, 3), (-2.71446436e-01, 4, 0), (-3.97855577e-02, 0, 4),
+)
+
+
+def _powf(v: float, k: int) -> float:
+    return v if k == 1 else v ** k
+
+
+def solar_gain(t: _dt.datetime, window_area: float, shading_coeff: float) -> float:
+    """Solar heat gain through the windows (W) at time t; identical for every house."""
+    x = t.hour + t.minute / 60 - 7.5
+    if x < 0 or x > 10:
+        load = 0
+    else:
+        y = t.month + t.day / 30 - 1
+        load = SOLAR_TERMS[0][0]
+        for c, i, j in SOLAR_TERMS[1:]:
+            if i and j:
+                load = load + _powf(x, i) * _powf(y, j) * c
+            elif i:
+                load = load + _powf(x, i) * c
+            else:
+                load = load + _powf(y, j) * c
+    return window_area * shading_coeff * load
+
+
+def od_temp(t: _dt.datetime, temp_prop, rng=_random):
+    """Sinusoidal daily outdoor temperature + one gauss(0, temp_std) draw (consumes the RNG)."""
+    amplitude = (temp_prop.day_temp - temp_prop.night_temp) / 2.0
+    bias = (temp_prop.day_temp + temp_prop.night_temp) / 2.0
+    delay = -6.0 + temp_prop.phase
+    time_day = t.hour + t.minute / 60.0
+    temperature = amplitude * np.sin(2 * np.pi * (time_day + delay) / 24.0) + bias
+    temperature += rng.gauss(0, temp_prop.temp_std)
+    return temperature
+
+
+def deadband_l2(target, deadband, value):
+    if target + deadband / 2 < value:
+        return (value - (target + deadband / 2)) ** 2
+    if target - deadband / 2 > value:
+        return ((target - deadband / 2) - value) ** 2
+    return 0.0
+
+
+def reward_normalisers(reward_prop, house_prop):
+    """(norm_temp, norm_sig) exactly as RewardsCalculator.compute_rewards computes them."""
+    norm_t = deadband_l2(house_prop.target_temp, 0, house_prop.target_temp + 1)
+    R = reward_prop.norm_reg_sig
+    norm_s = deadband_l2(R, 0, 0.75 * R)
+    return float(norm_t), float(norm_s)
+
+
+def _seconds_of_day(t: _dt.datetime) -> int:
+    return t.hour * 3600 + t.minute * 60 + t.second
+
+
+class Signal:
+    """Regulation-signal shape (signal_calculator.py), without the base-power part."""
+
+    def __init__(self, signal_props, nb_agents: int, rng=_random):
+        self.sp = signal_props
+        self.nb_agents = nb_agents
+        self.mode = signal_props.mode
+        if self.mode == "perlin":
+            from .perlin import Perlin
+
+            # SignalCalculator draws the perlin seed from the global RNG (signal_calculator.py:24-31)
+            self.perlin = Perlin(1, signal_props.nb_octaves, signal_props.octaves_step,
+                                 signal_props.period, rng.random())
+        elif self.mode not in ("flat", "sinusoidals", "regular_steps"):
+            raise ValueError(f"unknown signal mode {self.mode!r}")
+
+    def __call__(self, base_power, t: _dt.datetime):
+        sp = self.sp
+        if self.mode == "flat":
+            return base_power
+        if self.mode == "sinusoidals":
+            amplitudes = [base_power * r for r in sp.amplitude_ratios]
+            if len(sp.periods) != len(amplitudes):
+                raise ValueError("Power grid signal parameters: periods and amplitude_ratios lists "
+                                 "should have the same length.")
+            ts = _seconds_of_day(t)
+            s = base_power
+            for k, period in enumerate(sp.periods):
+                s += amplitudes[k] * np.sin(2 * np.pi * ts / period)
+            return s
+        if self.mode == "regular_steps":
+            amplitude = sp.amplitude_per_hvac * self.nb_agents
+            ratio = base_power / amplitude
+            return amplitude * np.heaviside((_seconds_of_day(t) % sp.period) - (1 - ratio) * sp.period, 1)
+        # perlin: max(0, base * (1 + amplitude * noise(mktime(t) mod 86400)))
+        import time
+
+        stamp = time.mktime(t.timetuple()) % 86400
+        return np.maximum(0, base_power + (base_power * sp.amplitude_ratios[0] * self.perlin.calculate_noise(stamp)))
+
+
+class GridSignal:
+    """PowerGrid (power_grid.py:21-161): base power x signal shape x artificial ratio, capped.
+
+    ``grid_props`` is mutated like the reference's (its artificial_ratio compounds across resets,
+    power_grid.py:44-49) because the reference does not copy it.
+    """
+
+    def __init__(self, grid_props, nb_agents: int, max_power: float, rng=_random, signal_fn=None):
+        self.gp = grid_props
+        self.nb_agents = nb_agents
+        self.max_power = max_power
+        grid_props.artificial_ratio = grid_props.artificial_ratio * \
+            grid_props.artificial_signal_ratio_range ** (rng.random() * 2 - 1)
+        self.current_signal = 0.0
+        self.signal = Signal(grid_props.signal_properties, nb_agents, rng)
+        self.signal_fn = signal_fn
+        bp = grid_props.base_power_props
+        if bp.mode == "interpolation":
+            raise NotImplementedError(
+                "base_power_props.mode='interpolation' needs the Monte-Carlo table "
+                "(mergedGridSearchResultFinal.npy), which the reference does not ship (SURVEY §8(f))")
+        if bp.mode != "constant":
+            raise ValueError(f"unknown base power mode {bp.mode!r}")
+
+    def base_power(self):
+        return self.gp.base_power_props.avg_power_per_hvac * self.nb_agents
+
+    def step(self, t: _dt.datetime):
+        base = self.base_power()
+        s = self.signal_fn(base, t) if self.signal_fn is not None else self.signal(base, t)
+        s = s * self.gp.artificial_ratio
+        self.current_signal = np.minimum(s, self.max_power)
+        return self.current_signal
+
+    def get_obs(self):
+        return {"reg_signal": self.current_signal}

@@ -1,0 +1,489 @@
+"""Drop-in ``Environment`` on MI355X: the reference's reset/step object surface, HIP underneath.
+
+Reference: server/app/core/environment/environment.py:23-194 (and the collaborators it calls,
+cited per method).  Same constructor argument (an ``EnvironmentProperties``: ours from
+``mdr_amd.config`` or the reference's own pydantic object), same ``reset() -> Dict[int, obs]``
+and ``step(Dict[int, bool]) -> (Dict[int, obs], Dict[int, float])``, same attributes the server
+reads (``init_props``, ``date_time``, ``current_od_temp``, ``cluster.current_power_consumption``,
+``cluster.max_power``, ``cluster.buildings``, ``power_grid.current_signal``), same global-``random``
+call order, so a seeded caller gets the reference's trajectory (tests/test_env_parity_gpu.py).
+
+Fast paths (no per-house Python): ``step_tensor`` (device actions -> device rewards),
+``obs_tensor`` (the ``norm_state_dict`` vector, float32 [N, F] on device) and ``rollout``
+(many ticks per call, hipGraph-captured).
+"""
+from __future__ import annotations
+
+import copy
+import datetime as _dt
+import random as _random
+from types import SimpleNamespace
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import _lib as L
+from . import config as cfgmod
+from . import population as popmod
+from .drivers import GridSignal, od_temp, reward_normalisers, solar_gain
+from .shard import HipShard, encode_hvac
+
+ACTION_MODES = {"buffer": L.ACT_BUFFER, "random": L.ACT_RANDOM, "always_on": L.ACT_ALWAYS_ON,
+                "bangbang": L.ACT_BANGBANG, "deadband_bangbang": L.ACT_DEADBAND_BANGBANG}
+
+
+def shard_range(n: int, rank: int, world: int):
+    """Contiguous house range of a rank: [r*n//w, (r+1)*n//w)."""
+    lo = rank * n // world
+    hi = (rank + 1) * n // world
+    return lo, hi - lo
+
+
+class _ClusterView:
+    """The parts of ``Cluster`` (cluster.py:17-126) the server and controllers read."""
+
+    def __init__(self, env: "Environment"):
+        self._env = env
+
+    @property
+    def init_props(self):
+        return self._env.init_props.cluster_prop
+
+    @property
+    def max_power(self) -> float:
+        return self._env._max_power
+
+    @property
+    def current_power_consumption(self) -> float:
+        return self._env._cluster_power()
+
+    @property
+    def buildings(self):
+        return self._env._building_views()
+
+    @property
+    def agent_communicators(self):
+        links = self._env._obs_links
+        return {self._env._offset + i: [int(j) for j in row] for i, row in enumerate(links)} if links is not None else {}
+
+
+class Environment:
+    """Vectorised environment for N houses (one shard of them per process on multi-GPU)."""
+
+    def __init__(self, env_props, device=None, rng=None, population: str = "reference",
+                 seed: int = 0, signal_fn=None, rank: int = 0, world: int = 1, comm=None,
+                 _shard_factory=None):
+        self.init_props = copy.deepcopy(env_props)
+        cfgmod.validate(self.init_props)
+        if population not in ("reference", "synthetic"):
+            raise ValueError("population must be 'reference' (host RNG, reference stream) or 'synthetic'")
+        self.rng = rng if rng is not None else _random
+        self._population = population
+        self._seed = int(seed)
+        self._signal_fn = signal_fn
+        self.rank, self.world = int(rank), int(world)
+        if world > 1 and comm is None:
+            raise ValueError("a multi-shard Environment needs a comm (mdr_amd.distributed)")
+        self._comm = comm
+        self._device = device
+        self._shard_factory = _shard_factory
+        self._shard: Optional[HipShard] = None
+        self.cluster = _ClusterView(self)
+        self.reset(return_obs=False)  # the reference's __init__ resets and discards the obs
+
+    # ------------------------------------------------------------------ geometry
+    @property
+    def n(self) -> int:
+        return self.init_props.cluster_prop.nb_agents
+
+    @property
+    def n_local(self) -> int:
+        return self._n_local
+
+    @property
+    def shard(self) -> HipShard:
+        return self._shard
+
+    # ------------------------------------------------------------------ reset
+    def reset(self, return_obs: bool = True):
+        """environment.py:49-70 (RNG order: SURVEY Appendix B).  ``return_obs=False`` skips the
+        host-side dict materialisation (it draws nothing from the RNG) for tensor-API callers."""
+        p = self.init_props
+        cp, hp = p.cluster_prop, p.cluster_prop.house_prop
+        hv = hp.hvac_prop
+        rng = self.rng
+        n = cp.nb_agents
+        self._offset, self._n_local = shard_range(n, self.rank, self.world)
+        # Cluster.reset (cluster.py:49-69): pre-noise power / max power, comm graph, get_obs()
+        pre = hv.cooling_capacity / hv.cop
+        seq = float(np.cumsum(np.full(n, pre, np.float64))[-1])  # sequential float sum
+        self._max_power = seq
+        self._P_host = seq
+        self._P_dev_valid = False
+        self._links = popmod.comm_links(cp, rng)
+        if self._links is None:
+            popmod.random_links(cp, rng)  # Cluster.reset() -> get_obs() draws in random_sample mode
+        # Environment.apply_noise: randomize_date then per-building noise
+        self.date_time = p.start_datetime
+        if p.start_datetime_mode == "random":
+            days = rng.randrange(364)
+            secs = rng.randrange(86400)
+            self.date_time = p.start_datetime + _dt.timedelta(days=days, seconds=secs)
+        lo, nl = self._offset, self._n_local
+        if self._population == "reference":
+            pop = popmod.draw_reference(cp, rng)
+            table, idx = popmod.cap_table(hv, pop["cap"][lo:lo + nl])
+            local = {k: pop[k][lo:lo + nl] for k in ("ua", "ca", "cm", "hm", "target")}
+        else:
+            table, idx = popmod.cap_table(hv, ())
+            local = None
+        self._cap_values = table
+        # outdoor temperature, grid, rewards calculator, first signal (environment.py:59-69)
+        self.current_od_temp = od_temp(self.date_time, p.temp_prop, rng)
+        self.power_grid = GridSignal(p.power_grid_prop, n, self._max_power, rng, self._signal_fn)
+        self._norm_temp, self._norm_sig = reward_normalisers(p.reward_prop, hp)
+        self.power_grid.step(self.date_time)
+        # device state (Building.reset / HVAC.reset: init temps, on, no lockout, sso = 0)
+        self._ensure_shard(table)
+        sh = self._shard
+        if local is not None:
+            sh.upload(local, idx, np.full(nl, float(hp.init_air_temp)), np.full(nl, float(hp.init_mass_temp)),
+                      encode_hvac(np.ones(nl, bool), np.zeros(nl, bool), np.zeros(nl, np.int64)))
+        else:
+            sh.populate(hp)
+        self._host_params = None
+        self._solar = 0.0
+        self._tick = 0
+        self._counts_ready = 0
+        self._obs_links = self._links if self._links is not None else popmod.random_links(cp, rng)
+        return self.get_obs() if return_obs else None
+
+    def _ensure_shard(self, cap_values):
+        key = (tuple(cap_values), self._n_local)
+        if self._shard is not None and self._shard_key == key:
+            return
+        if self._shard is not None:
+            self._shard.close()
+        factory = self._shard_factory or HipShard
+        dev = self._device
+        if dev is None:
+            import torch
+
+            dev = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else "cuda"
+        self._shard = factory(self.init_props, self._n_local, self._offset, self.n, dev, cap_values,
+                              seed=self._seed)
+        self._shard_key = key
+        if self._comm is not None and hasattr(self._comm, "attach"):
+            self._comm.attach(self._shard)
+
+    # ------------------------------------------------------------------ step
+    def _tick_args(self) -> L.mdr_tick:
+        return L.mdr_tick(float(self._tod_prev), float(self._solar), float(self._s_prev), self._tick)
+
+    def step_tensor(self, actions=None, action_mode: str = "buffer", lookahead: Optional[str] = None,
+                    ctrl: Optional[str] = None, ctrl_out=None):
+        """One tick on device.  ``actions``: uint8/bool tensor [n_local] on the shard's device
+        (``action_mode='buffer'``) or None with an in-kernel source ('random', 'always_on',
+        'bangbang', 'deadband_bangbang').  Returns the device reward tensor (float64 [n_local]).
+
+        ``lookahead`` names the NEXT tick's in-kernel action source: its cluster-power counts
+        are computed by this launch, so the next tick is a single kernel.
+        """
+        p = self.init_props
+        hp = p.cluster_prop.house_prop
+        sh = self._shard
+        mode = ACTION_MODES[action_mode]
+        if mode == L.ACT_BUFFER:
+            if actions is None:
+                raise ValueError("action_mode='buffer' needs an actions tensor")
+            if actions.dtype != sh.action.dtype:
+                actions = actions.to(sh.action.dtype)
+            if actions.numel() != self._n_local:
+                raise ValueError(f"actions must have {self._n_local} elements")
+            actions = actions.contiguous()
+        # environment.py:86-91: time advances, the cluster steps with the previous OD temp
+        self.date_time = self.date_time + p.time_step
+        self._solar = solar_gain(self.date_time, hp.window_area, hp.shading_coeff) if hp.solar_gain else 0.0
+        self._tod_prev = self.current_od_temp
+        self._s_prev = self.power_grid.current_signal
+        tick = self._tick_args()
+        if mode == L.ACT_BUFFER or self._counts_ready != mode:
+            # phase 1 (unless the previous launch already counted this tick under the same source)
+            if mode in (L.ACT_BUFFER, L.ACT_RANDOM, L.ACT_ALWAYS_ON):
+                sh.power_counts(actions, mode, self._tick)
+            else:
+                self._bangbang_counts(mode)
+        if self._comm is not None:
+            self._comm.allreduce_counts(sh)
+        la = ACTION_MODES[lookahead] if lookahead else 0
+        cm = {None: 0, "bangbang": L.CTRL_BANGBANG, "deadband_bangbang": L.CTRL_DEADBAND_BANGBANG}[ctrl]
+        reward = sh.step(actions, mode, tick, lookahead=la, ctrl=cm, ctrl_out=ctrl_out)
+        if sh.penalty_mode != 0:
+            sh.penalty_partials()
+            if self._comm is not None:
+                self._comm.allreduce_penalty(sh)
+            sh.reward_finalize(tick)
+        self._counts_ready = la
+        self._P_dev_valid = True
+        cp = p.cluster_prop
+        if self._links is None:
+            popmod.random_links(cp, self.rng)  # the discarded Cluster.get_obs() (cluster.py:89)
+        self.current_od_temp = od_temp(self.date_time, p.temp_prop, self.rng)
+        self.power_grid.step(self.date_time)
+        self._obs_links = self._links if self._links is not None else popmod.random_links(cp, self.rng)
+        self._tick += 1
+        return reward
+
+    def _bangbang_counts(self, mode):
+        # phase 1 for a bang-bang source: evaluate the controller on the current state on device
+        import torch
+
+        sh = self._shard
+        T, tgt = sh.t_air, sh.target
+        if mode == L.ACT_BANGBANG:
+            a = T > tgt
+        else:
+            db = self.init_props.cluster_prop.house_prop.deadband
+            on = (sh.hvac < 0)  # bit 31
+            a = torch.where(T < tgt - db / 2, torch.zeros_like(on), torch.where(T > tgt + db / 2, torch.ones_like(on), on))
+        sh.action.copy_(a.to(torch.uint8))
+        sh.power_counts(sh.action, L.ACT_BUFFER, self._tick)
+
+    def step(self, action_dict):
+        """environment.py:72-108 — dict in, (obs dict, rewards dict) out."""
+        import torch
+
+        a = np.zeros(self._n_local, np.uint8)
+        lo, nl = self._offset, self._n_local
+        if isinstance(action_dict, dict):
+            for k, v in action_dict.items():
+                try:
+                    j = int(k) - lo
+                except (TypeError, ValueError):
+                    continue
+                if 0 <= j < nl and v:
+                    a[j] = 1
+        else:
+            a[:] = np.asarray(action_dict, bool)[lo:lo + nl] if len(action_dict) == self.n else np.asarray(action_dict, bool)
+        sh = self._shard
+        sh.action.copy_(torch.from_numpy(a).to(sh.device))
+        reward = self.step_tensor(sh.action)
+        r = reward.cpu().numpy()
+        rewards = {lo + i: float(r[i]) for i in range(nl)}
+        return self.get_obs(), rewards
+
+    # ------------------------------------------------------------------ many ticks per call
+    def driver_window(self, n_ticks: int):
+        """Advance the host drivers n_ticks ahead (same RNG order as n calls of step) and return
+        the per-tick ``mdr_tick`` list for a rollout.  Valid when nothing else draws from the RNG
+        between ticks (random_sample comm mode draws, so it is excluded)."""
+        if self._links is None:
+            raise NotImplementedError("random_sample comm mode draws per tick; use step()")
+        p = self.init_props
+        hp = p.cluster_prop.house_prop
+        ticks = []
+        for _ in range(n_ticks):
+            self.date_time = self.date_time + p.time_step
+            self._solar = solar_gain(self.date_time, hp.window_area, hp.shading_coeff) if hp.solar_gain else 0.0
+            self._tod_prev = self.current_od_temp
+            self._s_prev = self.power_grid.current_signal
+            ticks.append(self._tick_args())
+            self.current_od_temp = od_temp(self.date_time, p.temp_prop, self.rng)
+            self.power_grid.step(self.date_time)
+            self._tick += 1
+        return ticks
+
+    def rollout(self, n_ticks: int, actions=None, action_mode: str = "random", rewards=None,
+                use_graph: bool = True):
+        """n_ticks steps in one C call (hipGraph-captured).  ``actions``: uint8 [n_ticks, N]
+        (buffer mode) or None; ``rewards``: float64 [n_ticks, N] output (allocated if None)."""
+        import torch
+
+        sh = self._shard
+        if sh.penalty_mode != 0:
+            raise NotImplementedError("rollout supports individual_L2; use step_tensor for common penalties")
+        mode = ACTION_MODES[action_mode]
+        if mode in (L.ACT_BANGBANG, L.ACT_DEADBAND_BANGBANG):
+            raise NotImplementedError("bang-bang rollouts: use step_tensor(action_mode=..., lookahead=...)")
+        if rewards is None:
+            rewards = torch.empty((n_ticks, self._n_local), dtype=torch.float64, device=sh.device)
+        ticks = self.driver_window(n_ticks)
+        if self._comm is not None:
+            self._comm.rollout(sh, ticks, actions, mode, rewards)
+        else:
+            sh.rollout(ticks, actions, self._n_local if actions is not None else 0, mode, rewards,
+                       self._n_local, use_graph)
+        self._counts_ready = 0
+        self._P_dev_valid = True
+        return rewards
+
+    # ------------------------------------------------------------------ observations
+    def _cluster_power(self) -> float:
+        if self._P_dev_valid:
+            return float(self._shard.p_dev.item())
+        return self._P_host
+
+    def obs_spec(self):
+        """mdr_obs_spec for the norm_state_dict layout of this config (norm.py:178-218)."""
+        p = self.init_props
+        cp, hp = p.cluster_prop, p.cluster_prop.house_prop
+        sp, mp = p.state_prop, cp.message_prop
+        k = popmod.nb_comm(cp)
+        msg_w = 4 + (4 if mp.thermal else 0) + (3 if mp.hvac else 0)
+        n_feat = 10 + (2 if sp.hvac else 0) + (1 if sp.solar_gain else 0) + (5 if sp.thermal else 0) + k * msg_w
+        spec = L.mdr_obs_spec()
+        spec.n_feat = n_feat
+        spec.hvac_state, spec.solar_state, spec.thermal_state = int(sp.hvac), int(sp.solar_gain), int(sp.thermal)
+        spec.msg_thermal, spec.msg_hvac = int(mp.thermal), int(mp.hvac)
+        spec.n_comm = k
+        ring = cp.agents_comm_prop.mode == "neighbours"
+        spec.comm_mode = L.COMM_RING if ring else L.COMM_TABLE
+        spec.norm_reg_sig = float(p.reward_prop.norm_reg_sig)
+        spec.cfg_ua, spec.cfg_ca, spec.cfg_cm, spec.cfg_hm = hp.Ua, hp.Ca, hp.Cm, hp.Hm
+        spec.cfg_cap = float(hp.hvac_prop.cooling_capacity)
+        return spec
+
+    def obs_tensor(self, out=None):
+        """``norm_state_dict`` for every local house as float32 [n_local, F] on device."""
+        import torch
+
+        sh = self._shard
+        spec = self.obs_spec()
+        if out is None:
+            out = torch.empty((self._n_local, spec.n_feat), dtype=torch.float32, device=sh.device)
+        keep = []
+        if spec.comm_mode == L.COMM_TABLE and spec.n_comm > 0:
+            if self.world > 1:
+                raise NotImplementedError("non-ring comm modes are single-shard for the device obs")
+            tab = torch.from_numpy(np.ascontiguousarray(self._obs_links, np.int32)).to(sh.device)
+            keep.append(tab)
+            spec.comm_table = L.ptr(tab)
+        if spec.comm_mode == L.COMM_RING and self.world > 1 and spec.n_comm > 0:
+            halo = self._comm.ring_halo(sh, spec)
+            keep.append(halo)
+            spec.halo_msg = L.ptr(halo)
+        sc = L.mdr_obs_scalars(float(self._P_host), float(self.power_grid.current_signal),
+                               float(self._solar), float(self.current_od_temp))
+        sh.obs(spec, sc, out, use_p_dev=self._P_dev_valid)
+        if keep:
+            torch.cuda.current_stream(sh.device).synchronize()
+        return out
+
+    def _params_host(self):
+        if self._host_params is None:
+            self._host_params = self._shard.host_params()
+        return self._host_params
+
+    def get_obs(self) -> Dict[int, dict]:
+        """environment.py:110-130 — one 21-key dict per (local) house, with its messages."""
+        p = self.init_props
+        cp, hp = p.cluster_prop, p.cluster_prop.house_prop
+        hv = hp.hvac_prop
+        st = self._shard.host_state()
+        prm = self._params_host()
+        lo, nl = self._offset, self._n_local
+        if self.world > 1:  # messages need neighbours on other shards: gather the cluster state
+            st, prm = self._comm.allgather_state(self._shard, st, prm, self.n)
+        else:
+            lo = 0
+        caps = [self._cap_values[j] for j in prm["cap_idx"].tolist()]
+        maxc = [c / hv.cop for c in caps]
+        T, Tm = st["T"].tolist(), st["Tm"].tolist()
+        on, lock, sso = st["on"].tolist(), st["lock"].tolist(), st["sso"].tolist()
+        tgt = prm["target"].tolist()
+        ua, ca, cm, hm = (prm[k].tolist() for k in ("ua", "ca", "cm", "hm"))
+        P = self._cluster_power()
+        G = self._solar
+        od, dt_, S = self.current_od_temp, self.date_time, self.power_grid.current_signal
+        L_, cop, lcf, db = hv.lockout_duration, hv.cop, hv.latent_cooling_fraction, hp.deadband
+        mp = cp.message_prop
+        links = self._obs_links
+
+        def message(j):
+            m = {"seconds_since_off": sso[j], "curr_consumption": maxc[j] if on[j] else 0.0,
+                 "max_consumption": maxc[j], "lockout_duration": L_,
+                 "current_temp_diff_to_target": T[j] - tgt[j]}
+            if mp.hvac:
+                m.update({"cop": cop, "latent_cooling_fraction": lcf, "cooling_capacity": caps[j]})
+            if mp.thermal:
+                m.update({"Ca": ca[j], "Ua": ua[j], "Cm": cm[j], "Hm": hm[j]})
+            return m
+
+        obs = {}
+        for g in range(lo, lo + nl):  # arrays are indexed by global house id from here on
+            row = links[g] if links is not None else ()
+            obs[g] = {
+                "turned_on": on[g], "seconds_since_off": sso[g], "lockout": lock[g], "cop": cop,
+                "cooling_capacity": caps[g], "latent_cooling_fraction": lcf, "lockout_duration": L_,
+                "target_temp": tgt[g], "deadband": db, "Ua": ua[g], "Ca": ca[g], "Cm": cm[g],
+                "Hm": hm[g], "indoor_temp": T[g], "mass_temp": Tm[g], "solar_gain": G,
+                "cluster_hvac_power": P, "message": [message(int(j)) for j in row],
+                "OD_temp": od, "datetime": dt_, "reg_signal": S,
+            }
+        return obs
+
+    # ------------------------------------------------------------------ server-facing views
+    def _building_views(self):
+        st = self._shard.host_state()
+        prm = self._params_host()
+        hp = self.init_props.cluster_prop.house_prop
+        out = []
+        for i in range(self._n_local):
+            cap = self._cap_values[int(prm["cap_idx"][i])]
+            hv = SimpleNamespace(turned_on=bool(st["on"][i]), lockout=bool(st["lock"][i]),
+                                 seconds_since_off=int(st["sso"][i]),
+                                 init_props=SimpleNamespace(cooling_capacity=cap, cop=hp.hvac_prop.cop,
+                                                            max_consumption=cap / hp.hvac_prop.cop,
+                                                            lockout_duration=hp.hvac_prop.lockout_duration))
+            ip = SimpleNamespace(Ua=float(prm["ua"][i]), Ca=float(prm["ca"][i]), Cm=float(prm["cm"][i]),
+                                 Hm=float(prm["hm"][i]), target_temp=float(prm["target"][i]),
+                                 deadband=hp.deadband)
+            out.append(SimpleNamespace(indoor_temp=float(st["T"][i]), current_mass_temp=float(st["Tm"][i]),
+                                       current_solar_gain=self._solar, init_props=ip, hvac=hv))
+        return out
+
+    # ------------------------------------------------------------------ checkpoint / deepcopy
+    def state_dict(self) -> dict:
+        sh = self._shard
+        host = {k: getattr(sh, k).detach().cpu().clone() for k in
+                ("t_air", "t_mass", "hvac", "ua", "ca", "cm", "hm", "target", "cap_idx")}
+        host.update(date_time=self.date_time, current_od_temp=self.current_od_temp,
+                    current_signal=self.power_grid.current_signal, solar=self._solar, tick=self._tick,
+                    P=self._cluster_power(), cap_values=list(self._cap_values),
+                    links=None if self._links is None else self._links.copy(),
+                    obs_links=None if self._obs_links is None else np.array(self._obs_links))
+        return host
+
+    def load_state_dict(self, sd: dict) -> None:
+        sh = self._shard
+        if list(sd["cap_values"]) != list(self._cap_values):
+            self._ensure_shard(sd["cap_values"])
+            self._cap_values = list(sd["cap_values"])
+            sh = self._shard
+        for k in ("t_air", "t_mass", "hvac", "ua", "ca", "cm", "hm", "target", "cap_idx"):
+            getattr(sh, k).copy_(sd[k].to(sh.device))
+        self.date_time = sd["date_time"]
+        self.current_od_temp = sd["current_od_temp"]
+        self.power_grid.current_signal = sd["current_signal"]
+        self._solar, self._tick = sd["solar"], sd["tick"]
+        self._P_host, self._P_dev_valid = sd["P"], False
+        self._links = sd["links"]
+        self._obs_links = sd["obs_links"]
+        self._host_params = None
+        self._counts_ready = 0
+
+    def __deepcopy__(self, memo):
+        """TrainingManager.test deep-copies the env (training_manager.py:269): clone the device
+        state into a fresh context; the RNG is shared like the reference's global random."""
+        new = object.__new__(Environment)
+        memo[id(self)] = new
+        for k, v in self.__dict__.items():
+            if k in ("_shard", "cluster", "rng", "_comm", "_shard_factory"):
+                continue
+            new.__dict__[k] = copy.deepcopy(v, memo)
+        new.rng, new._comm, new._shard_factory = self.rng, self._comm, self._shard_factory
+        new.cluster = _ClusterView(new)
+        new._shard = None
+        new._ensure_shard(self._cap_values)
+        new.load_state_dict(self.state_dict())
+        return new

@@ -1,0 +1,195 @@
+"""Device shard: the SoA state of a contiguous range of houses + the libmdr_hip context.
+
+``HipShard`` owns the PyTorch-ROCm tensors (the device container) and issues the C-ABI calls on
+the current torch stream.  ``Environment`` drives one shard per process; multi-GPU runs add a
+collective (``comm``) between phase 1 and phase 2 of every tick.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib as L
+
+ON_BIT = np.uint32(1 << 31)
+LOCK_BIT = np.uint32(1 << 30)
+SSO_MASK = np.uint32((1 << 30) - 1)
+
+
+def decode_hvac(words: np.ndarray):
+    w = words.view(np.uint32)
+    return (w & ON_BIT) != 0, (w & LOCK_BIT) != 0, (w & SSO_MASK).astype(np.int64)
+
+
+def encode_hvac(on, lock, sso) -> np.ndarray:
+    w = np.minimum(np.asarray(sso, np.int64), int(SSO_MASK)).astype(np.uint32)
+    w |= np.where(np.asarray(on, bool), ON_BIT, np.uint32(0))
+    w |= np.where(np.asarray(lock, bool), LOCK_BIT, np.uint32(0))
+    return w.view(np.int32)
+
+
+class HipShard:
+    """Houses [offset, offset + n) of a cluster of n_global, on one GPU."""
+
+    def __init__(self, props, n: int, offset: int, n_global: int, device, cap_values, seed: int = 0):
+        import torch
+
+        from .drivers import reward_normalisers
+
+        self.lib = L.load()
+        if not torch.cuda.is_available():
+            raise L.MdrLibraryError("no ROCm GPU visible: the HIP step has no CPU fallback")
+        self.torch = torch
+        self.device = torch.device(device)
+        self.n, self.offset, self.n_global = int(n), int(offset), int(n_global)
+        hp = props.cluster_prop.house_prop
+        hv = hp.hvac_prop
+        rp = props.reward_prop
+        pp = rp.penalty_props
+        cfg = L.mdr_config()
+        cfg.abi_version = L.ABI_VERSION
+        cfg.device = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        cfg.n_local, cfg.global_offset, cfg.n_global = self.n, self.offset, self.n_global
+        cfg.dt = props.time_step.seconds
+        cfg.lockout_duration = hv.lockout_duration
+        cfg.cop, cfg.lcf, cfg.deadband = hv.cop, hv.latent_cooling_fraction, hp.deadband
+        cfg.n_cap = len(cap_values)
+        cfg.penalty_mode = L.PEN_MODES[pp.mode]
+        for i, v in enumerate(cap_values):
+            cfg.cap_table[i] = float(v)
+        cfg.alpha_temp, cfg.alpha_sig = rp.alpha_temp, rp.alpha_sig
+        cfg.norm_temp, cfg.norm_sig = reward_normalisers(rp, hp)
+        cfg.alpha_ind_l2, cfg.alpha_common_l2, cfg.alpha_common_max = (
+            pp.alpha_ind_l2, pp.alpha_common_l2, pp.alpha_common_max)
+        cfg.seed = seed & 0xFFFFFFFFFFFFFFFF
+        self.cfg = cfg
+        self.penalty_mode = cfg.penalty_mode
+        ctx = C.c_void_p()
+        L.check(self.lib.mdr_create(C.byref(ctx), C.byref(cfg)), "mdr_create")
+        self.ctx = ctx
+        f64 = dict(dtype=torch.float64, device=self.device)
+        self.t_air = torch.empty(self.n, **f64)
+        self.t_mass = torch.empty(self.n, **f64)
+        self.hvac = torch.empty(self.n, dtype=torch.int32, device=self.device)
+        self.ua = torch.empty(self.n, **f64)
+        self.ca = torch.empty(self.n, **f64)
+        self.cm = torch.empty(self.n, **f64)
+        self.hm = torch.empty(self.n, **f64)
+        self.target = torch.empty(self.n, **f64)
+        self.cap_idx = torch.empty(self.n, dtype=torch.uint8, device=self.device)
+        self.reward = torch.zeros(self.n, **f64)
+        self.action = torch.zeros(self.n, dtype=torch.uint8, device=self.device)
+        self.p_dev = torch.zeros(1, **f64)
+        self._bind()
+
+    # ------------------------------------------------------------------ plumbing
+    def _bind(self):
+        soa = L.mdr_soa(*(L.ptr(t) for t in (self.t_air, self.t_mass, self.hvac, self.ua, self.ca,
+                                             self.cm, self.hm, self.target, self.cap_idx)))
+        L.check(self.lib.mdr_bind(self.ctx, C.byref(soa)), "mdr_bind")
+
+    def stream(self):
+        return L.stream_handle(self.device)
+
+    def close(self):
+        if getattr(self, "ctx", None):
+            self.lib.mdr_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ------------------------------------------------------------------ population / state
+    def upload(self, pop: dict, cap_idx: np.ndarray, t_air, t_mass, hvac_words):
+        t = self.torch
+        dev = self.device
+        for name in ("ua", "ca", "cm", "hm", "target"):
+            getattr(self, name).copy_(t.from_numpy(np.ascontiguousarray(pop[name], np.float64)).to(dev))
+        self.cap_idx.copy_(t.from_numpy(np.ascontiguousarray(cap_idx, np.uint8)).to(dev))
+        self.t_air.copy_(t.from_numpy(np.ascontiguousarray(t_air, np.float64)).to(dev))
+        self.t_mass.copy_(t.from_numpy(np.ascontiguousarray(t_mass, np.float64)).to(dev))
+        self.hvac.copy_(t.from_numpy(np.ascontiguousarray(hvac_words, np.int32)).to(dev))
+
+    def populate(self, hp):
+        nz = hp.noise_prop
+        spec = L.mdr_pop_spec(hp.target_temp, nz.std_target_temp, nz.factor_thermo_low,
+                              nz.factor_thermo_high, hp.Ca, hp.Cm, hp.Hm, hp.init_air_temp,
+                              hp.init_mass_temp)
+        L.check(self.lib.mdr_populate(self.ctx, C.byref(spec), self.stream()), "mdr_populate")
+
+    # ------------------------------------------------------------------ tick
+    def power_counts(self, action, mode: int, tick: int):
+        L.check(self.lib.mdr_power_counts(self.ctx, L.ptr(action), mode, tick, self.stream()),
+                "mdr_power_counts")
+
+    def counts_buffer(self):
+        p = C.c_void_p()
+        n = C.c_int()
+        L.check(self.lib.mdr_counts_buffer(self.ctx, C.byref(p), C.byref(n)), "mdr_counts_buffer")
+        return p.value, n.value
+
+    def step(self, action, mode: int, tick: L.mdr_tick, lookahead: int = 0, ctrl: int = 0,
+             ctrl_out=None, reward=None):
+        reward = self.reward if reward is None else reward
+        L.check(self.lib.mdr_step(self.ctx, L.ptr(action), mode, C.byref(tick), L.ptr(reward),
+                                  lookahead, ctrl, L.ptr(ctrl_out), L.ptr(self.p_dev), self.stream()),
+                "mdr_step")
+        return reward
+
+    def penalty_partials(self):
+        L.check(self.lib.mdr_penalty_partials(self.ctx, self.stream()), "mdr_penalty_partials")
+        p = C.c_void_p()
+        L.check(self.lib.mdr_penalty_buffer(self.ctx, C.byref(p)), "mdr_penalty_buffer")
+        return p.value
+
+    def reward_finalize(self, tick: L.mdr_tick, reward=None):
+        reward = self.reward if reward is None else reward
+        L.check(self.lib.mdr_reward_finalize(self.ctx, C.byref(tick), L.ptr(reward), self.stream()),
+                "mdr_reward_finalize")
+
+    def rollout(self, ticks, action, act_stride, mode, reward, rew_stride, use_graph=True):
+        """Many ticks in one C call.  Graph capture needs a non-default stream: the rollout runs
+        on the shard's own stream, ordered after / before the caller's current stream."""
+        arr = (L.mdr_tick * len(ticks))(*ticks)
+        torch = self.torch
+        cur = torch.cuda.current_stream(self.device)
+        if use_graph:
+            if getattr(self, "_side", None) is None:
+                self._side = torch.cuda.Stream(self.device)
+            s = self._side
+            s.wait_stream(cur)
+            handle = s.cuda_stream
+        else:
+            handle = cur.cuda_stream
+        L.check(self.lib.mdr_rollout(self.ctx, len(ticks), arr, L.ptr(action), act_stride, mode,
+                                     L.ptr(reward), rew_stride, int(use_graph), handle),
+                "mdr_rollout")
+        if use_graph:
+            cur.wait_stream(self._side)
+
+    def greedy(self, budget: float, action):
+        L.check(self.lib.mdr_ctrl_greedy(self.ctx, float(budget), L.ptr(action), self.stream()),
+                "mdr_ctrl_greedy")
+
+    def obs(self, spec, scalars, out, use_p_dev=True):
+        L.check(self.lib.mdr_obs(self.ctx, C.byref(spec), C.byref(scalars),
+                                 L.ptr(self.p_dev) if use_p_dev else 0, L.ptr(out), self.stream()),
+                "mdr_obs")
+
+    def halo_pack(self, spec, out):
+        L.check(self.lib.mdr_halo_pack(self.ctx, C.byref(spec), L.ptr(out), self.stream()), "mdr_halo_pack")
+
+    # ------------------------------------------------------------------ host views
+    def host_state(self):
+        t = self.torch
+        t.cuda.current_stream(self.device).synchronize()
+        on, lock, sso = decode_hvac(self.hvac.cpu().numpy())
+        return {"T": self.t_air.cpu().numpy(), "Tm": self.t_mass.cpu().numpy(), "on": on, "lock": lock,
+                "sso": sso}
+
+    def host_params(self):
+        return {k: getattr(self, k).cpu().numpy() for k in ("ua", "ca", "cm", "hm", "target", "cap_idx")}

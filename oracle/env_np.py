@@ -284,10 +284,14 @@ def draw_population(cp, rng):
 class OracleEnv:
     """Vectorised restatement of ``Environment`` (environment.py:23-194), SoA state."""
 
-    def __init__(self, props, rng=None):
+    def __init__(self, props, rng=None, population: Optional[dict] = None):
+        """``population`` (keys Ua, Ca, Cm, Hm, target, cap) replaces the RNG draw of the
+        per-building noise (used for synthetic bench populations); everything else is as the
+        reference."""
         self.p = props
         self.rng = rng if rng is not None else _random
         self.n = props.cluster_prop.nb_agents
+        self._pop0 = population
         self.reset()
 
     # environment.py:49-70
@@ -308,7 +312,8 @@ class OracleEnv:
             days = self.rng.randrange(364)
             secs = self.rng.randrange(86400)
             self.date = p.start_datetime + _dt.timedelta(days=days, seconds=secs)
-        self.pop = draw_population(cp, self.rng)
+        self.pop = draw_population(cp, self.rng) if self._pop0 is None else \
+            {k: np.array(v, np.float64) for k, v in self._pop0.items()}
         self.T = np.full(n, float(hp.init_air_temp))
         self.Tm = np.full(n, float(hp.init_mass_temp))
         self.on = np.ones(n, bool)

@@ -1,0 +1,294 @@
+"""HIP path (libmdr_hip.so through mdr_amd.Environment) vs the reference goldens and the oracle.
+
+Tolerances (BASELINE.json north_star): lockout counters, on/off masks and seconds-since-off
+bit-exact; temperatures, cluster power and rewards within 1e-5 relative — asserted here much
+tighter (1e-10) since the kernels keep the reference's fp64 operation order; float32 observation
+vectors within 2 float32 ulps of the float64 reference values cast to float32.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+from oracle import env_np as O
+
+pytestmark = pytest.mark.gpu
+
+TEMP_RTOL = 1e-10
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def make_env(props, seed, resets, **kw):
+    from mdr_amd.environment import Environment
+
+    rng = random.Random(seed)
+    env = Environment(props, rng=rng, **kw)
+    obs = None
+    for _ in range(resets - 1):
+        obs = env.reset()
+    return env, rng, obs
+
+
+@pytest.mark.parametrize("name", gu.TRAJ_NAMES)
+def test_golden_trajectory_dict_api(torch_gpu, name):
+    """Environment.reset/step (dict API) on the GPU reproduces the reference trajectory."""
+    d, meta = gu.traj(name)
+    props = gu.props_from_overrides(meta["overrides"])
+    env, rng, obs = make_env(props, meta["seed"], meta["resets"])
+    if obs is None:
+        obs = env.get_obs()
+    N, T = meta["N"], meta["T"]
+    assert obs[0]["cluster_hvac_power"] == float(d["init_P"])
+    assert obs[0]["reg_signal"] == float(d["init_S"])
+    np.testing.assert_array_equal([obs[i]["Ua"] for i in range(N)], d["pop_Ua"])
+    np.testing.assert_array_equal([obs[i]["target_temp"] for i in range(N)], d["pop_target_temp"])
+    hp = props.cluster_prop.house_prop
+    for t in range(T):
+        if meta["controller"] == "deadband_bbc":
+            acts = {i: obs[i]["indoor_temp"] > obs[i]["target_temp"] + hp.deadband / 2 or
+                    (not obs[i]["indoor_temp"] < obs[i]["target_temp"] - hp.deadband / 2 and obs[i]["turned_on"])
+                    for i in range(N)}
+            np.testing.assert_array_equal([bool(acts[i]) for i in range(N)], d["actions"][t].astype(bool))
+        elif meta["controller"] == "bbc":
+            acts = {i: obs[i]["indoor_temp"] > obs[i]["target_temp"] for i in range(N)}
+            np.testing.assert_array_equal([bool(acts[i]) for i in range(N)], d["actions"][t].astype(bool))
+        else:
+            acts = {i: bool(d["actions"][t, i]) for i in range(N)}
+        obs, rew = env.step(acts)
+        on = np.array([obs[i]["turned_on"] for i in range(N)])
+        lock = np.array([obs[i]["lockout"] for i in range(N)])
+        sso = np.array([obs[i]["seconds_since_off"] for i in range(N)])
+        np.testing.assert_array_equal(on, d["traj_on"][t].astype(bool), err_msg=f"on t={t}")
+        np.testing.assert_array_equal(lock, d["traj_lock"][t].astype(bool), err_msg=f"lock t={t}")
+        np.testing.assert_array_equal(sso, d["traj_sso"][t], err_msg=f"sso t={t}")
+        Tn = np.array([obs[i]["indoor_temp"] for i in range(N)])
+        Tmn = np.array([obs[i]["mass_temp"] for i in range(N)])
+        np.testing.assert_allclose(Tn, d["traj_T"][t], rtol=TEMP_RTOL, atol=0, err_msg=f"T t={t}")
+        np.testing.assert_allclose(Tmn, d["traj_Tm"][t], rtol=TEMP_RTOL, atol=0, err_msg=f"Tm t={t}")
+        np.testing.assert_allclose([rew[i] for i in range(N)], d["traj_reward"][t], rtol=1e-9, atol=1e-12)
+        assert obs[0]["cluster_hvac_power"] == float(d["traj_P"][t])
+        assert obs[0]["reg_signal"] == float(d["traj_S"][t])
+        assert obs[0]["OD_temp"] == float(d["traj_Tod"][t])
+        assert obs[0]["solar_gain"] == float(d["traj_G"][t])
+        m0 = np.array([obs[i]["message"][0]["current_temp_diff_to_target"] for i in range(N)])
+        np.testing.assert_allclose(m0, d["traj_msg0_diff"][t], rtol=1e-9, atol=1e-12)
+        np.testing.assert_array_equal([obs[i]["message"][0]["curr_consumption"] for i in range(N)],
+                                      d["traj_msg0_curr"][t])
+
+
+@pytest.mark.parametrize("name", gu.TRAJ_NAMES)
+def test_golden_obs_vector(torch_gpu, name):
+    """The device norm_state_dict vector (obs_tensor) matches the reference's at the goldens' ticks."""
+    d, meta = gu.traj(name)
+    props = gu.props_from_overrides(meta["overrides"])
+    env, rng, _ = make_env(props, meta["seed"], meta["resets"])
+    N = meta["N"]
+    ticks = sorted(int(k[6:]) for k in d.keys() if k.startswith("norm_t"))
+
+    def check(t):
+        got = env.obs_tensor().cpu().numpy()
+        ref = d[f"norm_t{t}"].astype(np.float32)
+        np.testing.assert_array_max_ulp(got, ref, maxulp=2)
+
+    if 0 in ticks:
+        check(0)
+    for t in range(max(ticks)):
+        acts = torch_gpu.from_numpy(d["actions"][t]).to("cuda")
+        env.step_tensor(acts)
+        if t + 1 in ticks:
+            check(t + 1)
+
+
+def oracle_and_env(props, seed, **kw):
+    from mdr_amd.environment import Environment
+
+    env = Environment(props, rng=random.Random(seed), **kw)
+    ora = O.OracleEnv(props, random.Random(seed))
+    return env, ora
+
+
+@pytest.mark.parametrize("n", [1, 2, 257, 4099])
+def test_random_actions_vs_oracle(torch_gpu, n):
+    """Edge sizes (1 house, ragged last block) against the oracle over 60 ticks."""
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env, ora = oracle_and_env(props, 31)
+    rs = np.random.RandomState(n)
+    for t in range(60):
+        a = rs.randint(0, 2, n).astype(np.uint8)
+        r = env.step_tensor(torch_gpu.from_numpy(a).to("cuda")).cpu().numpy()
+        o, rr = ora.step(a.astype(bool))
+        st = env.shard.host_state()
+        np.testing.assert_array_equal(st["on"], o["on"])
+        np.testing.assert_array_equal(st["lock"], o["lock"])
+        np.testing.assert_array_equal(st["sso"], o["sso"])
+        np.testing.assert_allclose(st["T"], o["T"], rtol=TEMP_RTOL, atol=0)
+        np.testing.assert_allclose(st["Tm"], o["Tm"], rtol=TEMP_RTOL, atol=0)
+        np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12)
+        assert env.cluster.current_power_consumption == o["P"]
+
+
+@pytest.mark.parametrize("mode", ["common_L2", "common_max_error", "mixture"])
+def test_common_penalty_modes_vs_oracle(torch_gpu, mode):
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": 3001,
+                                     "power_grid_prop.signal_properties.mode": "flat",
+                                     "reward_prop.penalty_props.mode": mode,
+                                     "reward_prop.penalty_props.alpha_common_max": 0.5,
+                                     "cluster_prop.house_prop.deadband": 0.4})
+    env, ora = oracle_and_env(props, 5)
+    rs = np.random.RandomState(2)
+    for t in range(25):
+        a = rs.randint(0, 2, 3001).astype(np.uint8)
+        r = env.step_tensor(torch_gpu.from_numpy(a).to("cuda")).cpu().numpy()
+        _, rr = ora.step(a.astype(bool))
+        np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12)
+
+
+@pytest.mark.parametrize("ctrl", ["bangbang", "deadband_bangbang"])
+def test_fused_bangbang_matches_dict_controller(torch_gpu, ctrl):
+    """In-kernel controller (+ lookahead counts) == the reference controller applied per tick."""
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": 777,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals",
+                                     "cluster_prop.house_prop.deadband": 0.5})
+    env, ora = oracle_and_env(props, 8)
+    hp = props.cluster_prop.house_prop
+    for t in range(80):
+        if ctrl == "bangbang":
+            a = O.bangbang(ora.T, ora.pop["target"])
+        else:
+            a = O.deadband_bangbang(ora.T, ora.pop["target"], hp.deadband, ora.on)
+        r = env.step_tensor(None, action_mode=ctrl, lookahead=ctrl).cpu().numpy()
+        o, rr = ora.step(a)
+        st = env.shard.host_state()
+        np.testing.assert_array_equal(st["on"], o["on"])
+        np.testing.assert_array_equal(st["lock"], o["lock"])
+        np.testing.assert_allclose(st["T"], o["T"], rtol=TEMP_RTOL, atol=0)
+        np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12)
+
+
+def test_rollout_equals_steps(torch_gpu):
+    """mdr_rollout (graph-captured, lookahead counts) == the same ticks via step_tensor."""
+    torch = torch_gpu
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": 20000,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    from mdr_amd.environment import Environment
+
+    e1 = Environment(props, rng=random.Random(3), population="synthetic", seed=77)
+    e2 = Environment(props, rng=random.Random(3), population="synthetic", seed=77)
+    R = e1.rollout(50, action_mode="random")
+    R2 = e1.rollout(50, action_mode="random")  # graph replay
+    rews = []
+    for t in range(100):
+        rews.append(e2.step_tensor(None, action_mode="random").clone())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(torch.cat([R, R2]).cpu().numpy(), torch.stack(rews).cpu().numpy())
+    s1, s2 = e1.shard.host_state(), e2.shard.host_state()
+    for k in s1:
+        np.testing.assert_array_equal(s1[k], s2[k])
+
+
+def test_rollout_buffer_actions_vs_oracle(torch_gpu):
+    torch = torch_gpu
+    n, T = 3000, 40
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "flat"})
+    env, ora = oracle_and_env(props, 12)
+    acts = np.random.RandomState(0).randint(0, 2, (T, n)).astype(np.uint8)
+    R = env.rollout(T, actions=torch.from_numpy(acts).cuda(), action_mode="buffer").cpu().numpy()
+    for t in range(T):
+        o, rr = ora.step(acts[t].astype(bool))
+        np.testing.assert_allclose(R[t], rr, rtol=1e-9, atol=1e-12)
+    st = env.shard.host_state()
+    np.testing.assert_array_equal(st["sso"], o["sso"])
+    np.testing.assert_allclose(st["T"], o["T"], rtol=TEMP_RTOL, atol=0)
+
+
+def test_greedy_golden(torch_gpu):
+    """mdr_ctrl_greedy on the reference's greedy inputs (F7) picks the reference's houses."""
+    torch = torch_gpu
+    from mdr_amd.environment import Environment
+
+    d = gu.load("greedy.npz")
+    Tn, N = d["action"].shape
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": N,
+                                     "power_grid_prop.signal_properties.mode": "flat"})
+    env = Environment(props, rng=random.Random(1))
+    sh = env.shard
+    from mdr_amd.shard import encode_hvac
+
+    for t in range(Tn):
+        caps = [int(c) for c in d["cap"][t]]
+        idx = np.array([env._cap_values.index(c) for c in caps], np.uint8)
+        sh.cap_idx.copy_(torch.from_numpy(idx).cuda())
+        sh.t_air.copy_(torch.from_numpy(d["T"][t]).cuda())
+        sh.target.copy_(torch.from_numpy(d["target"][t]).cuda())
+        sh.hvac.copy_(torch.from_numpy(encode_hvac(np.ones(N, bool), d["lock"][t], np.zeros(N))).cuda())
+        out = torch.zeros(N, dtype=torch.uint8, device="cuda")
+        sh.greedy(float(d["S"][t]), out)
+        np.testing.assert_array_equal(out.cpu().numpy().astype(bool), d["action"][t].astype(bool), err_msg=f"t={t}")
+
+
+def test_greedy_vs_oracle_large(torch_gpu):
+    torch = torch_gpu
+    from mdr_amd.environment import Environment
+
+    n = 200_000
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "flat"})
+    env = Environment(props, rng=random.Random(1), population="synthetic", seed=5)
+    for t in range(5):
+        env.step_tensor(None, action_mode="random")
+    sh = env.shard
+    st, prm = sh.host_state(), sh.host_params()
+    caps = np.array(env._cap_values, np.float64)[prm["cap_idx"]]
+    for S in (0.0, 3000.0, 1.0e8, float(env.power_grid.current_signal), 1e12):
+        out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        sh.greedy(S, out)
+        ref = O.greedy(st["T"], prm["target"], caps, props.cluster_prop.house_prop.hvac_prop.cop, st["lock"], S)
+        np.testing.assert_array_equal(out.cpu().numpy().astype(bool), ref)
+
+
+def test_one_million_houses_properties(torch_gpu):
+    """Full-size (1,048,576 houses) size-independent checks: FSM bit-exact vs the oracle on the
+    same input state, temperatures within tolerance, P == sum of ON power (exact integers)."""
+    torch = torch_gpu
+    from mdr_amd.environment import Environment
+
+    n = 1 << 20
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env = Environment(props, rng=random.Random(9), population="synthetic", seed=9)
+    for _ in range(30):
+        env.step_tensor(None, action_mode="random", lookahead="random")
+    sh = env.shard
+    st0, prm = sh.host_state(), sh.host_params()
+    a = (torch.rand(n, device="cuda") < 0.5).to(torch.uint8)
+    tick_tod, tick_S = env.current_od_temp, env.power_grid.current_signal
+    r = env.step_tensor(a).cpu().numpy()
+    st1 = sh.host_state()
+    hv = props.cluster_prop.house_prop.hvac_prop
+    on, lock, sso = O.hvac_step(st0["on"], st0["lock"], st0["sso"], a.cpu().numpy().astype(bool),
+                                hv.lockout_duration, props.time_step.seconds)
+    np.testing.assert_array_equal(st1["on"], on)
+    np.testing.assert_array_equal(st1["lock"], lock)
+    np.testing.assert_array_equal(st1["sso"], sso)
+    caps = np.array(env._cap_values, np.float64)[prm["cap_idx"]]
+    q = O.heat_transfer(on, caps, hv.latent_cooling_fraction)
+    T, Tm = O.update_temperature(st0["T"], st0["Tm"], prm["ua"], prm["ca"], prm["cm"], prm["hm"], q,
+                                 env._solar, tick_tod, float(props.time_step.seconds))
+    np.testing.assert_allclose(st1["T"], T, rtol=TEMP_RTOL, atol=0)
+    np.testing.assert_allclose(st1["Tm"], Tm, rtol=TEMP_RTOL, atol=0)
+    P = float(np.sum(np.where(on, caps / hv.cop, 0.0)))
+    assert env.cluster.current_power_consumption == P
+    rr = O.rewards(T, prm["target"], props.cluster_prop.house_prop.deadband, P, tick_S,
+                   props.reward_prop, props.cluster_prop.house_prop.target_temp)
+    np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12)
+    assert np.all(np.isfinite(r))
