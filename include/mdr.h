@@ -241,6 +241,11 @@ int mdr_rollout_sharded(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const 
                         int64_t act_stride, int action_mode, double* reward, int64_t rew_stride,
                         void* stream);
 
+/* ---- diagnostics ------------------------------------------------------------------------ */
+/* Memory-floor probe: the loads/stores of one mdr_step over the bound arrays with no arithmetic
+ * (writes the state back unchanged, garbage into reward).  Roofline calibration only. */
+int mdr_probe_stream(mdr_ctx* ctx, double* reward, void* stream);
+
 /* ---- timing helpers for bench.py (HIP events on the given stream) ---------------------- */
 int mdr_event_record(mdr_ctx* ctx, int slot, void* stream);
 int mdr_event_elapsed_ms(mdr_ctx* ctx, int slot0, int slot1, float* ms);

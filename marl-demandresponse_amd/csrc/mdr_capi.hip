@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -76,6 +77,7 @@ struct mdr_ctx {
   double* d_pen_partial = nullptr;       // 2 per block of k_step
   double* d_partial2 = nullptr;
   int pen_blocks = 0;
+  int hpt = 2;                           // houses per thread of k_step (MDR_HPT env overrides)
   // rollout tick drivers
   TickArgs* d_ticks = nullptr;
   TickArgs* h_ticks = nullptr;  // pinned staging
@@ -128,8 +130,13 @@ int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const 
   unsigned long long* cur = slab_at(c, c->ring);
   unsigned long long* nxt = slab_at(c, c->ring + 1);
   unsigned long long* zer = slab_at(c, c->ring + 2);
-  hipLaunchKernelGGL(k_step, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, action, mode, tk,
-                     tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer, c->d_pen_partial);
+  if (c->hpt == 2) {
+    hipLaunchKernelGGL(k_step_t<2>, dim3(blocks(c->kp.n, 512)), dim3(256), 0, st, c->kp, action, mode,
+                       tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer, c->d_pen_partial);
+  } else {
+    hipLaunchKernelGGL(k_step_t<1>, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, action, mode,
+                       tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer, c->d_pen_partial);
+  }
   LAUNCH_CHECK("k_step");
   c->ring = (c->ring + 1) % 3;
   c->counts_ready = lookahead != 0;
@@ -201,7 +208,8 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
     return cleanup(fail(MDR_ENOMEM, "count slabs"));
   if (hipMemset(c->d_slab, 0, 3 * c->slab_len * sizeof(unsigned long long)) != hipSuccess)
     return cleanup(fail(MDR_EHIP, "count slabs memset"));
-  c->pen_blocks = (int)blocks(cfg->n_local, 256);
+  if (const char* e = getenv("MDR_HPT")) c->hpt = atoi(e) == 1 ? 1 : 2;
+  c->pen_blocks = (int)blocks(cfg->n_local, 256 * c->hpt);  // = k_step grid
   if (hipMalloc(&c->d_pen_partial, 2 * sizeof(double) * c->pen_blocks) != hipSuccess ||
       hipMalloc(&c->d_partial2, 2 * sizeof(double)) != hipSuccess)
     return cleanup(fail(MDR_ENOMEM, "penalty partials"));
@@ -592,6 +600,15 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
     if (rc) return rc;
   }
   c->counts_ready = false;
+  return MDR_OK;
+}
+
+// ------------------------------------------------------------------------------------ diagnostics
+int mdr_probe_stream(mdr_ctx* c, double* reward, void* stream) {
+  if (!c || !reward) return fail(MDR_EARG, "mdr_probe_stream: null argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_probe_stream: context not bound");
+  hipLaunchKernelGGL(k_probe_stream, dim3(blocks(c->kp.n, 512)), dim3(256), 0, S(stream), c->kp, reward);
+  LAUNCH_CHECK("k_probe_stream");
   return MDR_OK;
 }
 

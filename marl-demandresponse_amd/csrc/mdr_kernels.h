@@ -52,11 +52,13 @@ struct ObsArgs {
 
 __global__ void k_power_counts(KParams p, const uint8_t* action, int action_mode, uint64_t tick,
                                const TickArgs* tkp, unsigned long long* slab);
-__global__ void k_step(KParams p, const uint8_t* action, int action_mode, TickArgs tk,
-                       const TickArgs* tkp,
-                       const unsigned long long* counts, double* reward, int ctrl, uint8_t* ctrl_out,
-                       double* p_out, int lookahead, unsigned long long* next_slab,
-                       unsigned long long* zero_slab, double* pen_partial);
+template <int HPT>
+__global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, TickArgs tk,
+                         const TickArgs* tkp, const unsigned long long* counts, double* reward,
+                         int ctrl, uint8_t* ctrl_out, double* p_out, int lookahead,
+                         unsigned long long* next_slab, unsigned long long* zero_slab,
+                         double* pen_partial);
+__global__ void k_probe_stream(KParams p, double* reward);
 __global__ void k_pen_reduce(const double* pen_partial, int nblk, double* partial2);
 __global__ void k_reward_finalize(KParams p, TickArgs tk, const unsigned long long* counts,
                                   const double* partial2, double* reward);

@@ -30,16 +30,6 @@ __device__ __forceinline__ void count_on(bool on, int cls, int n_cap, unsigned* 
   }
 }
 
-// Cluster power of a tick from the (global) per-class counts: P = sum_k counts[k] * p_on[k].
-// cap/cop of the reference's capacity list are integers at the default config, so the sum is
-// exactly the reference's sequential float sum (cluster.py:82-88).
-__device__ __forceinline__ double power_from_counts(const unsigned long long* counts,
-                                                    const double* p_on, int n_cap) {
-  double P = 0.0;
-  for (int k = 0; k < n_cap; ++k) P += (double)counts[k] * p_on[k];
-  return P;
-}
-
 __device__ __forceinline__ bool tick_action(int mode, const uint8_t* action, int64_t i,
                                             uint64_t seed, uint64_t gid, uint64_t tick) {
   if (mode == MDR_ACT_BUFFER) return action[i] != 0;
@@ -69,98 +59,173 @@ __global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* 
 }
 
 // --------------------------------------------------------------------------------------- K1
-// Phase 2: fused FSM + RC thermal + reward (environment.py:86-101) for one tick.
-//   counts    : the tick's GLOBAL per-class ON counts (kCountShards x MDR_MAX_CAP slab, summed here)
+// Phase 2: fused FSM + RC thermal + reward (environment.py:86-101) for one tick, HPT houses per
+// thread (HPT = 2: 16-B-per-lane loads/stores of the fp64 SoA arrays, two independent fp64
+// dependency chains per thread).
+//   counts    : the tick's GLOBAL per-class ON counts, slab [kCountShards][n_cap]; every wave
+//               reduces it itself (lane l reads shard l), so no block barrier precedes the work
 //   next_slab : when lookahead != 0, ON counts of tick+1 under the in-kernel action source
 //               (random / always-on / bang-bang on the new state) are accumulated here, so the
 //               next tick needs no phase-1 launch.
-__global__ void __launch_bounds__(256) k_step(KParams p, const uint8_t* __restrict__ action,
-                                              int action_mode, TickArgs tk0, const TickArgs* tkp,
-                                              const unsigned long long* __restrict__ counts,
-                                              double* __restrict__ reward, int ctrl,
-                                              uint8_t* __restrict__ ctrl_out, double* p_out,
-                                              int lookahead, unsigned long long* next_slab,
-                                              unsigned long long* zero_slab,
-                                              double* __restrict__ pen_partial) {
-  __shared__ double s_q_on[MDR_MAX_CAP];
-  __shared__ double s_p_on[MDR_MAX_CAP];
-  __shared__ unsigned long long s_cnt[MDR_MAX_CAP];
+
+__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  return v;
+}
+
+// cluster power of the tick from the sharded count slab (uniform in the wave)
+__device__ __forceinline__ double wave_power(const unsigned long long* __restrict__ counts,
+                                             const double* __restrict__ p_on, int n_cap) {
+  static_assert(kCountShards == 64, "one shard per lane");
+  const int lane = threadIdx.x & 63;
+  double P = 0.0;
+  for (int k = 0; k < n_cap; ++k) {
+    const unsigned long long c = wave_sum_u64(counts[lane * n_cap + k]);
+    P += (double)c * p_on[k];
+  }
+  return P;
+}
+
+__device__ __forceinline__ bool pick_action(int mode, const uint8_t* action, int64_t i, uint64_t seed,
+                                            uint64_t gid, uint64_t tick, double T, double tgt,
+                                            double deadband, uint32_t w0) {
+  if (mode == MDR_ACT_BUFFER) return action[i] != 0;
+  if (mode == MDR_ACT_RANDOM) return random_action(seed, gid, tick);
+  if (mode == MDR_ACT_ALWAYS_ON) return true;
+  if (mode == kActBangBang) return ctrl_bangbang(T, tgt);
+  return ctrl_deadband(T, tgt, deadband, hv_on(w0));
+}
+
+template <int HPT>
+__global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __restrict__ action,
+                                                int action_mode, TickArgs tk0, const TickArgs* tkp,
+                                                const unsigned long long* __restrict__ counts,
+                                                double* __restrict__ reward, int ctrl,
+                                                uint8_t* __restrict__ ctrl_out, double* p_out,
+                                                int lookahead, unsigned long long* next_slab,
+                                                unsigned long long* zero_slab,
+                                                double* __restrict__ pen_partial) {
   __shared__ unsigned hist[MDR_MAX_CAP];
   __shared__ double s_red[2][4];
   const int tid = threadIdx.x;
-  const TickArgs tk = tkp ? *tkp : tk0;
-  if (tid < p.n_cap) {
-    s_q_on[tid] = p.q_on[tid];
-    s_p_on[tid] = p.p_on[tid];
-    unsigned long long c = 0;
-    for (int s = 0; s < kCountShards; ++s) c += counts[s * p.n_cap + tid];
-    s_cnt[tid] = c;
-    hist[tid] = 0;
+  const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + tid) * HPT;
+  bool valid[HPT];
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) valid[h] = i0 + h < p.n;
+
+  // ---- all per-house loads first (one round trip)
+  uint32_t w0[HPT];
+  double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
+  int cls[HPT];
+  if (HPT == 2 && valid[HPT - 1]) {
+    const double2 vT = *reinterpret_cast<const double2*>(p.t_air + i0);
+    const double2 vTm = *reinterpret_cast<const double2*>(p.t_mass + i0);
+    const double2 vua = *reinterpret_cast<const double2*>(p.ua + i0);
+    const double2 vca = *reinterpret_cast<const double2*>(p.ca + i0);
+    const double2 vcm = *reinterpret_cast<const double2*>(p.cm + i0);
+    const double2 vhm = *reinterpret_cast<const double2*>(p.hm + i0);
+    const double2 vtg = *reinterpret_cast<const double2*>(p.target + i0);
+    const uint2 vw = *reinterpret_cast<const uint2*>(p.hvac + i0);
+    const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
+    T[0] = vT.x; T[HPT - 1] = vT.y; Tm[0] = vTm.x; Tm[HPT - 1] = vTm.y;
+    ua[0] = vua.x; ua[HPT - 1] = vua.y; ca[0] = vca.x; ca[HPT - 1] = vca.y;
+    cm[0] = vcm.x; cm[HPT - 1] = vcm.y; hm[0] = vhm.x; hm[HPT - 1] = vhm.y;
+    tg[0] = vtg.x; tg[HPT - 1] = vtg.y; w0[0] = vw.x; w0[HPT - 1] = vw.y;
+    cls[0] = vc & 0xFF; cls[HPT - 1] = vc >> 8;
+  } else {
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) {
+      const int64_t i = valid[h] ? i0 + h : 0;
+      T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i]; cm[h] = p.cm[i];
+      hm[h] = p.hm[i]; tg[h] = p.target[i]; w0[h] = p.hvac[i]; cls[h] = p.cap_idx[i];
+    }
   }
   if (zero_slab && blockIdx.x == 0)
     for (int j = tid; j < kCountShards * p.n_cap; j += blockDim.x) zero_slab[j] = 0ull;
-  __syncthreads();
+  if (tid < p.n_cap) hist[tid] = 0;
 
-  // per-tick signal penalty (rewards_calculator.py:183-203), identical in every thread
-  const double P = power_from_counts(s_cnt, s_p_on, p.n_cap);
+  const TickArgs tk = tkp ? *tkp : tk0;
+  // per-tick signal penalty (rewards_calculator.py:183-203), uniform in the wave
+  const double P = wave_power(counts, p.p_on, p.n_cap);
   const double x = (P - tk.s_prev) / (double)p.n_global;
   const double sig_term = p.alpha_sig * (x * x) / p.norm_sig;
   if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
 
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
-  bool on1 = false;
-  int cls = 0;
-  double pen = 0.0;
-  if (i < p.n) {
+  double Tn[HPT], Tmn[HPT], rw[HPT], pen[HPT];
+  uint32_t w[HPT];
+  bool on[HPT], on1[HPT];
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) {
+    const int64_t i = i0 + h;
     const uint64_t gid = p.goff + i;
-    const uint32_t w0 = p.hvac[i];
-    const double T = p.t_air[i], Tm = p.t_mass[i];
-    const double tgt = p.target[i];
-    cls = p.cap_idx[i];
-    bool a;
-    if (action_mode == MDR_ACT_BUFFER) a = action[i] != 0;
-    else if (action_mode == MDR_ACT_RANDOM) a = random_action(p.seed, gid, tk.tick);
-    else if (action_mode == MDR_ACT_ALWAYS_ON) a = true;
-    else if (action_mode == kActBangBang) a = ctrl_bangbang(T, tgt);
-    else a = ctrl_deadband(T, tgt, p.deadband, hv_on(w0));
-    const uint32_t w = hvac_fsm(w0, a, p.dt, p.L);
-    const bool on = hv_on(w);
-    const double q = on ? s_q_on[cls] : 0.0;
-    double Tn, Tmn;
-    rc_update(T, Tm, p.ua[i], p.ca[i], p.cm[i], p.hm[i], q, tk.solar, tk.t_od_prev, (double)p.dt, Tn, Tmn);
-    p.t_air[i] = Tn;
-    p.t_mass[i] = Tmn;
-    p.hvac[i] = w;
-    pen = deadband_l2(tgt, p.deadband, Tn);
-    if (p.penalty_mode == MDR_PEN_INDIVIDUAL_L2) {
-      reward[i] = -(p.alpha_temp * pen / p.norm_temp + sig_term);
-    } else {
-      reward[i] = pen;  // finalised by k_reward_finalize once the cluster reduction is known
-    }
-    if (ctrl != MDR_CTRL_NONE && ctrl_out) {
-      const bool a1 = ctrl == MDR_CTRL_BANGBANG ? ctrl_bangbang(Tn, tgt)
-                                                 : ctrl_deadband(Tn, tgt, p.deadband, on);
-      ctrl_out[i] = a1 ? 1 : 0;
-    }
-    if (lookahead) {
+    const bool a = valid[h] && pick_action(action_mode, action, i, p.seed, gid, tk.tick, T[h], tg[h],
+                                           p.deadband, w0[h]);
+    w[h] = hvac_fsm(w0[h], a, p.dt, p.L);
+    on[h] = hv_on(w[h]);
+    const double q = on[h] ? p.q_on[cls[h]] : 0.0;
+    rc_update(T[h], Tm[h], ua[h], ca[h], cm[h], hm[h], q, tk.solar, tk.t_od_prev, (double)p.dt, Tn[h], Tmn[h]);
+    pen[h] = deadband_l2(tg[h], p.deadband, Tn[h]);
+    rw[h] = p.penalty_mode == MDR_PEN_INDIVIDUAL_L2 ? -(p.alpha_temp * pen[h] / p.norm_temp + sig_term)
+                                                    : pen[h];  // finalised by k_reward_finalize
+    on1[h] = false;
+    if (valid[h] && lookahead) {
       bool an;
       if (lookahead == MDR_ACT_RANDOM) an = random_action(p.seed, gid, tk.tick + 1);
       else if (lookahead == MDR_ACT_ALWAYS_ON) an = true;
-      else if (lookahead == kActBangBang) an = ctrl_bangbang(Tn, tgt);
-      else an = ctrl_deadband(Tn, tgt, p.deadband, on);
-      on1 = hv_on(hvac_fsm(w, an, p.dt, p.L));
+      else if (lookahead == kActBangBang) an = ctrl_bangbang(Tn[h], tg[h]);
+      else an = ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
+      on1[h] = hv_on(hvac_fsm(w[h], an, p.dt, p.L));
     }
   }
-  if (lookahead) count_on(on1, cls, p.n_cap, hist, next_slab);
-  if (p.penalty_mode != MDR_PEN_INDIVIDUAL_L2) {
-    // block partials of sum(pen/N) and max(pen) for the common penalty modes
-    double s = (i < p.n) ? pen / (double)p.n_global : 0.0;
-    double m = pen;
-    for (int off = 32; off > 0; off >>= 1) {
-      s += __shfl_xor(s, off);
-      m = fmax(m, __shfl_xor(m, off));
+
+  // ---- stores
+  if (HPT == 2 && valid[HPT - 1]) {
+    *reinterpret_cast<double2*>(p.t_air + i0) = make_double2(Tn[0], Tn[HPT - 1]);
+    *reinterpret_cast<double2*>(p.t_mass + i0) = make_double2(Tmn[0], Tmn[HPT - 1]);
+    *reinterpret_cast<uint2*>(p.hvac + i0) = make_uint2(w[0], w[HPT - 1]);
+    *reinterpret_cast<double2*>(reward + i0) = make_double2(rw[0], rw[HPT - 1]);
+  } else {
+#pragma unroll
+    for (int h = 0; h < HPT; ++h)
+      if (valid[h]) {
+        p.t_air[i0 + h] = Tn[h]; p.t_mass[i0 + h] = Tmn[h]; p.hvac[i0 + h] = w[h]; reward[i0 + h] = rw[h];
+      }
+  }
+  if (ctrl != MDR_CTRL_NONE && ctrl_out) {
+#pragma unroll
+    for (int h = 0; h < HPT; ++h)
+      if (valid[h]) {
+        const bool a1 = ctrl == MDR_CTRL_BANGBANG ? ctrl_bangbang(Tn[h], tg[h])
+                                                   : ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
+        ctrl_out[i0 + h] = a1 ? 1 : 0;
+      }
+  }
+
+  // ---- cluster reductions for the next launch / the common penalty modes
+  if (lookahead) {
+    __syncthreads();  // hist zeroed
+    const int lane = tid & 63;
+    for (int k = 0; k < p.n_cap; ++k) {
+      unsigned c = 0;
+#pragma unroll
+      for (int h = 0; h < HPT; ++h) c += (unsigned)__popcll(__ballot(on1[h] && cls[h] == k));
+      if (lane == 0 && c) atomicAdd(&hist[k], c);
     }
-    if ((tid & 63) == 0) { s_red[0][tid >> 6] = s; s_red[1][tid >> 6] = m; }
+    __syncthreads();
+    if (tid < p.n_cap && hist[tid])
+      atomicAdd(&next_slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)hist[tid]);
+  }
+  if (p.penalty_mode != MDR_PEN_INDIVIDUAL_L2) {
+    double sacc = 0.0, macc = 0.0;
+#pragma unroll
+    for (int h = 0; h < HPT; ++h)
+      if (valid[h]) { sacc += pen[h] / (double)p.n_global; macc = fmax(macc, pen[h]); }
+    for (int off = 32; off > 0; off >>= 1) {
+      sacc += __shfl_xor(sacc, off);
+      macc = fmax(macc, __shfl_xor(macc, off));
+    }
+    if ((tid & 63) == 0) { s_red[0][tid >> 6] = sacc; s_red[1][tid >> 6] = macc; }
     __syncthreads();
     if (tid == 0) {
       double bs = 0.0, bm = 0.0;
@@ -169,6 +234,35 @@ __global__ void __launch_bounds__(256) k_step(KParams p, const uint8_t* __restri
       pen_partial[2 * blockIdx.x + 1] = bm;
     }
   }
+}
+
+template __global__ void k_step_t<1>(KParams, const uint8_t*, int, TickArgs, const TickArgs*,
+                                     const unsigned long long*, double*, int, uint8_t*, double*, int,
+                                     unsigned long long*, unsigned long long*, double*);
+template __global__ void k_step_t<2>(KParams, const uint8_t*, int, TickArgs, const TickArgs*,
+                                     const unsigned long long*, double*, int, uint8_t*, double*, int,
+                                     unsigned long long*, unsigned long long*, double*);
+
+// Memory-floor probe for k_step's access pattern: the same loads and stores, trivial arithmetic
+// (roofline diagnostics only; never on the product path).
+__global__ void __launch_bounds__(256) k_probe_stream(KParams p, double* __restrict__ reward) {
+  const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) * 2;
+  if (i0 + 1 >= p.n) return;
+  const double2 vT = *reinterpret_cast<const double2*>(p.t_air + i0);
+  const double2 vTm = *reinterpret_cast<const double2*>(p.t_mass + i0);
+  const double2 vua = *reinterpret_cast<const double2*>(p.ua + i0);
+  const double2 vca = *reinterpret_cast<const double2*>(p.ca + i0);
+  const double2 vcm = *reinterpret_cast<const double2*>(p.cm + i0);
+  const double2 vhm = *reinterpret_cast<const double2*>(p.hm + i0);
+  const double2 vtg = *reinterpret_cast<const double2*>(p.target + i0);
+  const uint2 vw = *reinterpret_cast<const uint2*>(p.hvac + i0);
+  const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
+  const double s0 = vua.x + vca.x + vcm.x + vhm.x + vtg.x + (double)(vc & 0xFF);
+  const double s1 = vua.y + vca.y + vcm.y + vhm.y + vtg.y + (double)(vc >> 8);
+  *reinterpret_cast<double2*>(p.t_air + i0) = make_double2(vT.x * 1.0, vT.y * 1.0);
+  *reinterpret_cast<double2*>(p.t_mass + i0) = make_double2(vTm.x * 1.0, vTm.y * 1.0);
+  *reinterpret_cast<uint2*>(p.hvac + i0) = vw;
+  *reinterpret_cast<double2*>(reward + i0) = make_double2(s0, s1);
 }
 
 // Fixed-order reduction of the per-block penalty partials -> partial2 = {sum pen/N, max pen}.
@@ -195,21 +289,11 @@ __global__ void __launch_bounds__(256) k_reward_finalize(KParams p, TickArgs tk,
                                                          const unsigned long long* __restrict__ counts,
                                                          const double* __restrict__ partial2,
                                                          double* __restrict__ reward) {
-  __shared__ double s_p_on[MDR_MAX_CAP];
-  __shared__ unsigned long long s_cnt[MDR_MAX_CAP];
-  const int tid = threadIdx.x;
-  if (tid < p.n_cap) {
-    s_p_on[tid] = p.p_on[tid];
-    unsigned long long c = 0;
-    for (int s = 0; s < kCountShards; ++s) c += counts[s * p.n_cap + tid];
-    s_cnt[tid] = c;
-  }
-  __syncthreads();
-  const double P = power_from_counts(s_cnt, s_p_on, p.n_cap);
+  const double P = wave_power(counts, p.p_on, p.n_cap);
   const double x = (P - tk.s_prev) / (double)p.n_global;
   const double sig_term = p.alpha_sig * (x * x) / p.norm_sig;
   const double common_l2 = partial2[0], common_max = partial2[1];
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + tid;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n) return;
   const double pen = reward[i];
   double tp;

@@ -63,12 +63,12 @@ class RcclComm:
         L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, p.value, 1, 1, shard.stream()), "allreduce pen sum")
         L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, p.value + 8, 1, 2, shard.stream()), "allreduce pen max")
 
-    def rollout(self, shard, ticks, actions, mode, rewards) -> None:
+    def rollout(self, shard, ticks, actions, mode, rewards, rew_stride) -> None:
         arr = (L.mdr_tick * len(ticks))(*ticks)
         n = shard.n
         L.check(shard.lib.mdr_rollout_sharded(shard.ctx, len(ticks), arr, L.ptr(actions),
-                                              n if actions is not None else 0, mode, L.ptr(rewards), n,
-                                              shard.stream()), "mdr_rollout_sharded")
+                                              n if actions is not None else 0, mode, L.ptr(rewards),
+                                              rew_stride, shard.stream()), "mdr_rollout_sharded")
 
     def ring_halo(self, shard, spec):
         """Message features of the houses just before / after this shard on the global ring."""

@@ -296,7 +296,8 @@ class Environment:
     def rollout(self, n_ticks: int, actions=None, action_mode: str = "random", rewards=None,
                 use_graph: bool = True):
         """n_ticks steps in one C call (hipGraph-captured).  ``actions``: uint8 [n_ticks, N]
-        (buffer mode) or None; ``rewards``: float64 [n_ticks, N] output (allocated if None)."""
+        (buffer mode) or None; ``rewards``: float64 [n_ticks, N] output (allocated if None), or a
+        1-D [N] buffer that every tick overwrites."""
         import torch
 
         sh = self._shard
@@ -307,12 +308,13 @@ class Environment:
             raise NotImplementedError("bang-bang rollouts: use step_tensor(action_mode=..., lookahead=...)")
         if rewards is None:
             rewards = torch.empty((n_ticks, self._n_local), dtype=torch.float64, device=sh.device)
+        rew_stride = 0 if rewards.dim() == 1 else self._n_local  # 1-D: every tick overwrites it
         ticks = self.driver_window(n_ticks)
         if self._comm is not None:
-            self._comm.rollout(sh, ticks, actions, mode, rewards)
+            self._comm.rollout(sh, ticks, actions, mode, rewards, rew_stride)
         else:
             sh.rollout(ticks, actions, self._n_local if actions is not None else 0, mode, rewards,
-                       self._n_local, use_graph)
+                       rew_stride, use_graph)
         self._counts_ready = 0
         self._P_dev_valid = True
         return rewards
@@ -328,7 +330,8 @@ class Environment:
         p = self.init_props
         cp, hp = p.cluster_prop, p.cluster_prop.house_prop
         sp, mp = p.state_prop, cp.message_prop
-        k = popmod.nb_comm(cp)
+        links = self._obs_links
+        k = int(links.shape[1]) if links is not None and links.ndim == 2 else popmod.nb_comm(cp)
         msg_w = 4 + (4 if mp.thermal else 0) + (3 if mp.hvac else 0)
         n_feat = 10 + (2 if sp.hvac else 0) + (1 if sp.solar_gain else 0) + (5 if sp.thermal else 0) + k * msg_w
         spec = L.mdr_obs_spec()
