@@ -129,6 +129,12 @@ int mdr_destroy(mdr_ctx* ctx);
 /* Bind the caller-owned SoA arrays (Environment.reset, environment.py:49-70). */
 int mdr_bind(mdr_ctx* ctx, const mdr_soa* soa);
 
+/* The caller rewrote ua/ca/cm/hm (or dt changed): derived per-house coefficients the context may
+ * cache (the CACHED step variant keeps r1, r2, A3, A4, exp(r1 dt), exp(r2 dt) of every house,
+ * bit-identical to recomputing them per tick) are refreshed before the next step.  mdr_bind and
+ * mdr_populate imply it. */
+int mdr_params_changed(mdr_ctx* ctx);
+
 /* ---- population ------------------------------------------------------------------------ */
 /* Synthetic population drawn on device from Philox4x32-10(seed, global house id): the reference
  * noise model (building.py:224-267, hvac.py:66-70: target = target_temp + |N(0, std_target)|,

@@ -78,6 +78,9 @@ struct mdr_ctx {
   double* d_partial2 = nullptr;
   int pen_blocks = 0;
   int hpt = 2;                           // houses per thread of k_step (MDR_HPT env overrides)
+  bool cached = false;                   // cached param-only thermal coefficients (MDR_VARIANT=coef)
+  bool coef_dirty = true;
+  double* d_coef = nullptr;              // [6][n] r1, r2, A3, A4, e1, e2
   // rollout tick drivers
   TickArgs* d_ticks = nullptr;
   TickArgs* h_ticks = nullptr;  // pinned staging
@@ -130,13 +133,22 @@ int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const 
   unsigned long long* cur = slab_at(c, c->ring);
   unsigned long long* nxt = slab_at(c, c->ring + 1);
   unsigned long long* zer = slab_at(c, c->ring + 2);
-  if (c->hpt == 2) {
-    hipLaunchKernelGGL(k_step_t<2>, dim3(blocks(c->kp.n, 512)), dim3(256), 0, st, c->kp, action, mode,
-                       tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer, c->d_pen_partial);
-  } else {
-    hipLaunchKernelGGL(k_step_t<1>, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, action, mode,
-                       tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer, c->d_pen_partial);
+  if (c->cached && c->coef_dirty) {
+    hipLaunchKernelGGL(k_coeffs, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, c->d_coef);
+    LAUNCH_CHECK("k_coeffs");
+    c->coef_dirty = false;
   }
+  KParams kp = c->kp;
+  kp.coef = c->cached ? c->d_coef : nullptr;
+#define MDR_LAUNCH_STEP(H, C)                                                                        \
+  hipLaunchKernelGGL((k_step_t<H, C>), dim3(blocks(kp.n, 256 * H)), dim3(256), 0, st, kp, action, mode, \
+                     tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer, c->d_pen_partial)
+  if (c->hpt == 2) {
+    if (c->cached) MDR_LAUNCH_STEP(2, true); else MDR_LAUNCH_STEP(2, false);
+  } else {
+    if (c->cached) MDR_LAUNCH_STEP(1, true); else MDR_LAUNCH_STEP(1, false);
+  }
+#undef MDR_LAUNCH_STEP
   LAUNCH_CHECK("k_step");
   c->ring = (c->ring + 1) % 3;
   c->counts_ready = lookahead != 0;
@@ -209,6 +221,12 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   if (hipMemset(c->d_slab, 0, 3 * c->slab_len * sizeof(unsigned long long)) != hipSuccess)
     return cleanup(fail(MDR_EHIP, "count slabs memset"));
   if (const char* e = getenv("MDR_HPT")) c->hpt = atoi(e) == 1 ? 1 : 2;
+  if (const char* e = getenv("MDR_VARIANT")) c->cached = strcmp(e, "coef") == 0;
+  if (c->cached) {
+    k.coef_stride = cfg->n_local;
+    if (hipMalloc(&c->d_coef, 6 * sizeof(double) * cfg->n_local) != hipSuccess)
+      return cleanup(fail(MDR_ENOMEM, "coefficients"));
+  }
   c->pen_blocks = (int)blocks(cfg->n_local, 256 * c->hpt);  // = k_step grid
   if (hipMalloc(&c->d_pen_partial, 2 * sizeof(double) * c->pen_blocks) != hipSuccess ||
       hipMalloc(&c->d_partial2, 2 * sizeof(double)) != hipSuccess)
@@ -227,6 +245,7 @@ int mdr_destroy(mdr_ctx* c) {
   hipDeviceSynchronize();
   for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
   hipFree(c->d_tables);
+  hipFree(c->d_coef);
   hipFree(c->d_slab);
   hipFree(c->d_pen_partial);
   hipFree(c->d_partial2);
@@ -260,6 +279,7 @@ int mdr_bind(mdr_ctx* c, const mdr_soa* s) {
   k.cap_idx = s->cap_idx;
   c->bound = true;
   c->counts_ready = false;
+  c->coef_dirty = true;
   for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
   c->graphs.clear();
   return MDR_OK;
@@ -273,6 +293,7 @@ int mdr_populate(mdr_ctx* c, const mdr_pop_spec* sp, void* stream) {
   hipLaunchKernelGGL(k_populate, dim3(blocks(c->kp.n, 256)), dim3(256), 0, S(stream), c->kp, a);
   LAUNCH_CHECK("k_populate");
   c->counts_ready = false;
+  c->coef_dirty = true;
   return MDR_OK;
 }
 
@@ -600,6 +621,12 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
     if (rc) return rc;
   }
   c->counts_ready = false;
+  return MDR_OK;
+}
+
+int mdr_params_changed(mdr_ctx* c) {
+  if (!c) return fail(MDR_EARG, "mdr_params_changed: null ctx");
+  c->coef_dirty = true;
   return MDR_OK;
 }
 

@@ -44,37 +44,57 @@ __device__ __forceinline__ uint32_t hv_sso(uint32_t w) { return w & kSsoMask; }
 
 // ---------------------------------------------------------------------------- RC thermal
 // Building.update_temperature, server/app/core/environment/cluster/building.py:141-222
-// (GridLAB-D 2-node analytic solution).  q_hvac = HVAC.get_heat_transfer (hvac.py:85-99),
-// solar = compute_solar_gain (per-tick scalar), t_od = previous tick's outdoor temperature.
-__device__ __forceinline__ void rc_update(double T, double Tm, double Ua, double Ca, double Cm,
-                                          double Hm, double q_hvac, double solar, double t_od,
-                                          double dt, double& T_out, double& Tm_out) {
-  const double od_k = t_od + 273.0;
-  const double t_k = T + 273.0;
-  const double tm_k = Tm + 273.0;
-  const double Qa = q_hvac + solar;
+// (GridLAB-D 2-node analytic solution), split into the part that depends only on the house's
+// parameters (rc_coeffs: roots r1, r2 of the characteristic polynomial, mass/air ratios A3, A4
+// and the decay factors exp(r dt)) and the per-tick part (rc_apply).  Both keep the reference's
+// operation order, so a cached RcCoef gives bit-identical results to recomputing it every tick.
+// q_hvac = HVAC.get_heat_transfer (hvac.py:85-99), solar = compute_solar_gain (per-tick scalar),
+// t_od = previous tick's outdoor temperature.
+struct RcCoef { double r1, r2, A3, A4, e1, e2; };
+
+__device__ __forceinline__ RcCoef rc_coeffs(double Ua, double Ca, double Cm, double Hm, double dt) {
+  RcCoef k;
   const double a = Cm * Ca / Hm;
   const double UaHm = Ua + Hm;
   const double b = Cm * UaHm / Hm + Ca;
   const double c = Ua;
-  const double d = Qa + Ua * od_k;  // Qm (= 0) + Qa + Ua * od_k
   const double disc = __builtin_sqrt(b * b - 4.0 * a * c);
   const double two_a = 2.0 * a;
-  const double r1 = (-b + disc) / two_a;
-  const double r2 = (-b - disc) / two_a;
+  k.r1 = (-b + disc) / two_a;
+  k.r2 = (-b - disc) / two_a;
+  const double UaHm_Hm = UaHm / Hm;
+  k.A3 = k.r1 * Ca / Hm + UaHm_Hm;
+  k.A4 = k.r2 * Ca / Hm + UaHm_Hm;
+  k.e1 = exp(k.r1 * dt);
+  k.e2 = exp(k.r2 * dt);
+  return k;
+}
+
+__device__ __forceinline__ void rc_apply(double T, double Tm, double Ua, double Ca, double Hm,
+                                         const RcCoef& k, double q_hvac, double solar, double t_od,
+                                         double& T_out, double& Tm_out) {
+  const double od_k = t_od + 273.0;
+  const double t_k = T + 273.0;
+  const double tm_k = Tm + 273.0;
+  const double Qa = q_hvac + solar;
+  const double UaHm = Ua + Hm;
+  const double c = Ua;
+  const double d = Qa + Ua * od_k;  // Qm (= 0) + Qa + Ua * od_k
   const double dTA0dt = Hm * tm_k / Ca - UaHm * t_k / Ca + Ua * od_k / Ca + Qa / Ca;
   const double d_c = d / c;
-  const double A1 = (r2 * t_k - dTA0dt - r2 * d / c) / (r2 - r1);
+  const double A1 = (k.r2 * t_k - dTA0dt - k.r2 * d / c) / (k.r2 - k.r1);
   const double A2 = t_k - d_c - A1;
-  const double UaHm_Hm = UaHm / Hm;
-  const double A3 = r1 * Ca / Hm + UaHm_Hm;
-  const double A4 = r2 * Ca / Hm + UaHm_Hm;
-  const double e1 = exp(r1 * dt);
-  const double e2 = exp(r2 * dt);
-  const double t_new = A1 * e1 + A2 * e2 + d_c;
-  const double tm_new = A1 * A3 * e1 + A2 * A4 * e2 + 0.0 + d_c;  // + g (= Qm/Hm = 0)
+  const double t_new = A1 * k.e1 + A2 * k.e2 + d_c;
+  const double tm_new = A1 * k.A3 * k.e1 + A2 * k.A4 * k.e2 + 0.0 + d_c;  // + g (= Qm/Hm = 0)
   T_out = t_new - 273.0;
   Tm_out = tm_new - 273.0;
+}
+
+__device__ __forceinline__ void rc_update(double T, double Tm, double Ua, double Ca, double Cm,
+                                          double Hm, double q_hvac, double solar, double t_od,
+                                          double dt, double& T_out, double& Tm_out) {
+  const RcCoef k = rc_coeffs(Ua, Ca, Cm, Hm, dt);
+  rc_apply(T, Tm, Ua, Ca, Hm, k, q_hvac, solar, t_od, T_out, Tm_out);
 }
 
 // deadbandL2, server/app/utils/utils.py:4-23  (x**2 evaluated as x*x)

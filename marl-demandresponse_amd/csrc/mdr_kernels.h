@@ -30,6 +30,8 @@ struct KParams {
   const uint8_t* cap_idx;
   const double* q_on;  // [n_cap] -cap/(1+lcf)      (device, context-owned)
   const double* p_on;  // [n_cap] cap/cop
+  const double* coef;  // [6][coef_stride] cached rc_coeffs (r1, r2, A3, A4, e1, e2) or null
+  int64_t coef_stride;
 };
 
 struct TickArgs {
@@ -52,13 +54,14 @@ struct ObsArgs {
 
 __global__ void k_power_counts(KParams p, const uint8_t* action, int action_mode, uint64_t tick,
                                const TickArgs* tkp, unsigned long long* slab);
-template <int HPT>
+template <int HPT, bool CACHED>
 __global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, TickArgs tk,
                          const TickArgs* tkp, const unsigned long long* counts, double* reward,
                          int ctrl, uint8_t* ctrl_out, double* p_out, int lookahead,
                          unsigned long long* next_slab, unsigned long long* zero_slab,
                          double* pen_partial);
 __global__ void k_probe_stream(KParams p, double* reward);
+__global__ void k_coeffs(KParams p, double* coef);
 __global__ void k_pen_reduce(const double* pen_partial, int nblk, double* partial2);
 __global__ void k_reward_finalize(KParams p, TickArgs tk, const unsigned long long* counts,
                                   const double* partial2, double* reward);

@@ -97,7 +97,7 @@ __device__ __forceinline__ bool pick_action(int mode, const uint8_t* action, int
   return ctrl_deadband(T, tgt, deadband, hv_on(w0));
 }
 
-template <int HPT>
+template <int HPT, bool CACHED>
 __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __restrict__ action,
                                                 int action_mode, TickArgs tk0, const TickArgs* tkp,
                                                 const unsigned long long* __restrict__ counts,
@@ -117,28 +117,41 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   // ---- all per-house loads first (one round trip)
   uint32_t w0[HPT];
   double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
+  RcCoef kc[HPT];
   int cls[HPT];
+  const int64_t cs = p.coef_stride;
   if (HPT == 2 && valid[HPT - 1]) {
-    const double2 vT = *reinterpret_cast<const double2*>(p.t_air + i0);
-    const double2 vTm = *reinterpret_cast<const double2*>(p.t_mass + i0);
-    const double2 vua = *reinterpret_cast<const double2*>(p.ua + i0);
-    const double2 vca = *reinterpret_cast<const double2*>(p.ca + i0);
-    const double2 vcm = *reinterpret_cast<const double2*>(p.cm + i0);
-    const double2 vhm = *reinterpret_cast<const double2*>(p.hm + i0);
-    const double2 vtg = *reinterpret_cast<const double2*>(p.target + i0);
+    auto ld2 = [&](const double* a) { return *reinterpret_cast<const double2*>(a + i0); };
+    const double2 vT = ld2(p.t_air), vTm = ld2(p.t_mass), vua = ld2(p.ua), vca = ld2(p.ca);
+    const double2 vhm = ld2(p.hm), vtg = ld2(p.target);
     const uint2 vw = *reinterpret_cast<const uint2*>(p.hvac + i0);
     const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
     T[0] = vT.x; T[HPT - 1] = vT.y; Tm[0] = vTm.x; Tm[HPT - 1] = vTm.y;
     ua[0] = vua.x; ua[HPT - 1] = vua.y; ca[0] = vca.x; ca[HPT - 1] = vca.y;
-    cm[0] = vcm.x; cm[HPT - 1] = vcm.y; hm[0] = vhm.x; hm[HPT - 1] = vhm.y;
+    hm[0] = vhm.x; hm[HPT - 1] = vhm.y;
     tg[0] = vtg.x; tg[HPT - 1] = vtg.y; w0[0] = vw.x; w0[HPT - 1] = vw.y;
     cls[0] = vc & 0xFF; cls[HPT - 1] = vc >> 8;
+    if (CACHED) {
+      const double2 r1 = ld2(p.coef), r2 = ld2(p.coef + cs), A3 = ld2(p.coef + 2 * cs);
+      const double2 A4 = ld2(p.coef + 3 * cs), e1 = ld2(p.coef + 4 * cs), e2 = ld2(p.coef + 5 * cs);
+      kc[0] = RcCoef{r1.x, r2.x, A3.x, A4.x, e1.x, e2.x};
+      kc[HPT - 1] = RcCoef{r1.y, r2.y, A3.y, A4.y, e1.y, e2.y};
+    } else {
+      const double2 vcm = ld2(p.cm);
+      cm[0] = vcm.x; cm[HPT - 1] = vcm.y;
+    }
   } else {
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
       const int64_t i = valid[h] ? i0 + h : 0;
-      T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i]; cm[h] = p.cm[i];
+      T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i];
       hm[h] = p.hm[i]; tg[h] = p.target[i]; w0[h] = p.hvac[i]; cls[h] = p.cap_idx[i];
+      if (CACHED) {
+        const double* c = p.coef + i;
+        kc[h] = RcCoef{c[0], c[cs], c[2 * cs], c[3 * cs], c[4 * cs], c[5 * cs]};
+      } else {
+        cm[h] = p.cm[i];
+      }
     }
   }
   if (zero_slab && blockIdx.x == 0)
@@ -164,7 +177,8 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
     w[h] = hvac_fsm(w0[h], a, p.dt, p.L);
     on[h] = hv_on(w[h]);
     const double q = on[h] ? p.q_on[cls[h]] : 0.0;
-    rc_update(T[h], Tm[h], ua[h], ca[h], cm[h], hm[h], q, tk.solar, tk.t_od_prev, (double)p.dt, Tn[h], Tmn[h]);
+    if (!CACHED) kc[h] = rc_coeffs(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+    rc_apply(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
     pen[h] = deadband_l2(tg[h], p.deadband, Tn[h]);
     rw[h] = p.penalty_mode == MDR_PEN_INDIVIDUAL_L2 ? -(p.alpha_temp * pen[h] / p.norm_temp + sig_term)
                                                     : pen[h];  // finalised by k_reward_finalize
@@ -236,12 +250,25 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   }
 }
 
-template __global__ void k_step_t<1>(KParams, const uint8_t*, int, TickArgs, const TickArgs*,
-                                     const unsigned long long*, double*, int, uint8_t*, double*, int,
-                                     unsigned long long*, unsigned long long*, double*);
-template __global__ void k_step_t<2>(KParams, const uint8_t*, int, TickArgs, const TickArgs*,
-                                     const unsigned long long*, double*, int, uint8_t*, double*, int,
-                                     unsigned long long*, unsigned long long*, double*);
+#define MDR_INST_STEP(H, C)                                                                       \
+  template __global__ void k_step_t<H, C>(KParams, const uint8_t*, int, TickArgs, const TickArgs*, \
+                                          const unsigned long long*, double*, int, uint8_t*,      \
+                                          double*, int, unsigned long long*, unsigned long long*, \
+                                          double*);
+MDR_INST_STEP(1, false)
+MDR_INST_STEP(2, false)
+MDR_INST_STEP(1, true)
+MDR_INST_STEP(2, true)
+
+// Param-only thermal coefficients (rc_coeffs) of every house, for the CACHED step variant.
+__global__ void __launch_bounds__(256) k_coeffs(KParams p, double* __restrict__ coef) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const RcCoef k = rc_coeffs(p.ua[i], p.ca[i], p.cm[i], p.hm[i], (double)p.dt);
+  const int64_t cs = p.coef_stride;
+  coef[i] = k.r1; coef[i + cs] = k.r2; coef[i + 2 * cs] = k.A3;
+  coef[i + 3 * cs] = k.A4; coef[i + 4 * cs] = k.e1; coef[i + 5 * cs] = k.e2;
+}
 
 // Memory-floor probe for k_step's access pattern: the same loads and stores, trivial arithmetic
 // (roofline diagnostics only; never on the product path).

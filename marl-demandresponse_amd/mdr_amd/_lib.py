@@ -87,6 +87,7 @@ SIGNATURES = {
     "mdr_create": (I, [P(VP), P(mdr_config)]),
     "mdr_destroy": (I, [VP]),
     "mdr_bind": (I, [VP, P(mdr_soa)]),
+    "mdr_params_changed": (I, [VP]),
     "mdr_populate": (I, [VP, P(mdr_pop_spec), VP]),
     "mdr_power_counts": (I, [VP, VP, I, U64, VP]),
     "mdr_counts_buffer": (I, [VP, P(VP), P(I)]),

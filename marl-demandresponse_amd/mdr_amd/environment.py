@@ -465,6 +465,7 @@ class Environment:
             sh = self._shard
         for k in ("t_air", "t_mass", "hvac", "ua", "ca", "cm", "hm", "target", "cap_idx"):
             getattr(sh, k).copy_(sd[k].to(sh.device))
+        sh.params_changed()
         self.date_time = sd["date_time"]
         self.current_od_temp = sd["current_od_temp"]
         self.power_grid.current_signal = sd["current_signal"]

@@ -113,6 +113,10 @@ class HipShard:
         self.t_air.copy_(t.from_numpy(np.ascontiguousarray(t_air, np.float64)).to(dev))
         self.t_mass.copy_(t.from_numpy(np.ascontiguousarray(t_mass, np.float64)).to(dev))
         self.hvac.copy_(t.from_numpy(np.ascontiguousarray(hvac_words, np.int32)).to(dev))
+        self.params_changed()
+
+    def params_changed(self):
+        L.check(self.lib.mdr_params_changed(self.ctx), "mdr_params_changed")
 
     def populate(self, hp):
         nz = hp.noise_prop
