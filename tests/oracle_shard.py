@@ -1,0 +1,158 @@
+"""Test doubles for the multi-process path on CPU (gloo): a shard that computes with the oracle
+and a comm over torch.distributed/gloo.  They implement the interface mdr_amd.Environment drives
+(HipShard / RcclComm), so the sharding, replicated drivers and per-tick exchanges of the product
+orchestration are exercised without a GPU.  Never used by the product path."""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from mdr_amd import _lib as L
+from mdr_amd.drivers import reward_normalisers
+from mdr_amd.shard import decode_hvac, encode_hvac
+from oracle import env_np as O
+
+
+class OracleShard:
+    def __init__(self, props, n, offset, n_global, device, cap_values, seed=0):
+        self.props = props
+        self.n, self.offset, self.n_global = int(n), int(offset), int(n_global)
+        self.device = torch.device("cpu")
+        self.cap_values = [float(c) for c in cap_values]
+        self.penalty_mode = L.PEN_MODES[props.reward_prop.penalty_props.mode]
+        f64 = dict(dtype=torch.float64)
+        self.t_air = torch.zeros(self.n, **f64)
+        self.t_mass = torch.zeros(self.n, **f64)
+        self.hvac = torch.zeros(self.n, dtype=torch.int32)
+        for k in ("ua", "ca", "cm", "hm", "target"):
+            setattr(self, k, torch.zeros(self.n, **f64))
+        self.cap_idx = torch.zeros(self.n, dtype=torch.uint8)
+        self.reward = torch.zeros(self.n, **f64)
+        self.action = torch.zeros(self.n, dtype=torch.uint8)
+        self.p_dev = torch.zeros(1, **f64)
+        self.counts = torch.zeros(len(cap_values), dtype=torch.int64)
+        self.partial2 = torch.zeros(2, **f64)
+
+    def close(self):
+        pass
+
+    def params_changed(self):
+        pass
+
+    def upload(self, pop, cap_idx, t_air, t_mass, hvac_words):
+        for k in ("ua", "ca", "cm", "hm", "target"):
+            getattr(self, k).copy_(torch.from_numpy(np.asarray(pop[k], np.float64)))
+        self.cap_idx.copy_(torch.from_numpy(np.asarray(cap_idx, np.uint8)))
+        self.t_air.copy_(torch.from_numpy(np.asarray(t_air, np.float64)))
+        self.t_mass.copy_(torch.from_numpy(np.asarray(t_mass, np.float64)))
+        self.hvac.copy_(torch.from_numpy(np.asarray(hvac_words, np.int32)))
+
+    def _caps(self):
+        return np.asarray(self.cap_values)[self.cap_idx.numpy()]
+
+    def _actions(self, action, mode):
+        if mode == L.ACT_BUFFER:
+            return action.numpy().astype(bool)
+        if mode == L.ACT_ALWAYS_ON:
+            return np.ones(self.n, bool)
+        raise NotImplementedError("oracle shard: buffer / always-on actions only")
+
+    def power_counts(self, action, mode, tick):
+        on, lock, sso = decode_hvac(self.hvac.numpy())
+        hv = self.props.cluster_prop.house_prop.hvac_prop
+        on1, _, _ = O.hvac_step(on, lock, sso, self._actions(action, mode), hv.lockout_duration,
+                                self.props.time_step.seconds)
+        idx = self.cap_idx.numpy()
+        self.counts.copy_(torch.from_numpy(np.bincount(idx[on1], minlength=len(self.cap_values)).astype(np.int64)))
+
+    def step(self, action, mode, tick, lookahead=0, ctrl=0, ctrl_out=None, reward=None):
+        p = self.props
+        hp = p.cluster_prop.house_prop
+        hv = hp.hvac_prop
+        on, lock, sso = decode_hvac(self.hvac.numpy())
+        on, lock, sso = O.hvac_step(on, lock, sso, self._actions(action, mode), hv.lockout_duration,
+                                    p.time_step.seconds)
+        caps = self._caps()
+        q = O.heat_transfer(on, caps, hv.latent_cooling_fraction)
+        T, Tm = O.update_temperature(self.t_air.numpy(), self.t_mass.numpy(), self.ua.numpy(), self.ca.numpy(),
+                                     self.cm.numpy(), self.hm.numpy(), q, tick.solar, tick.t_od_prev,
+                                     float(p.time_step.seconds))
+        self.t_air.copy_(torch.from_numpy(T))
+        self.t_mass.copy_(torch.from_numpy(Tm))
+        self.hvac.copy_(torch.from_numpy(encode_hvac(on, lock, sso)))
+        P = 0.0
+        for k, c in enumerate(self.counts.tolist()):
+            P += float(c) * (self.cap_values[k] / hv.cop)
+        self.p_dev[0] = P
+        pen = O.deadband_l2(self.target.numpy(), hp.deadband, T)
+        self._pen = pen
+        x = (P - tick.s_prev) / self.n_global
+        norm_t, norm_s = reward_normalisers(p.reward_prop, hp)
+        rp = p.reward_prop
+        self._sig = rp.alpha_sig * (x * x) / norm_s
+        self._norm_t = norm_t
+        r = -(rp.alpha_temp * pen / norm_t + self._sig)
+        out = self.reward if reward is None else reward
+        out.copy_(torch.from_numpy(r if self.penalty_mode == 0 else pen))
+        return out
+
+    def penalty_partials(self):
+        s = 0.0
+        for v in self._pen:
+            s += v / self.n_global
+        self.partial2[0] = s
+        self.partial2[1] = float(np.max(self._pen, initial=0.0))
+
+    def reward_finalize(self, tick, reward=None):
+        pp = self.props.reward_prop.penalty_props
+        cl2, cmax = float(self.partial2[0]), float(self.partial2[1])
+        pen = self._pen
+        if pp.mode == "common_L2":
+            tp = np.full_like(pen, cl2)
+        elif pp.mode == "common_max_error":
+            tp = np.full_like(pen, cmax)
+        else:
+            tp = (pp.alpha_ind_l2 * pen + pp.alpha_common_l2 * cl2 + pp.alpha_common_max * cmax) / (
+                pp.alpha_ind_l2 + pp.alpha_common_l2 + pp.alpha_common_max)
+        r = -(self.props.reward_prop.alpha_temp * tp / self._norm_t + self._sig)
+        (self.reward if reward is None else reward).copy_(torch.from_numpy(r))
+
+    def host_state(self):
+        on, lock, sso = decode_hvac(self.hvac.numpy().copy())
+        return {"T": self.t_air.numpy().copy(), "Tm": self.t_mass.numpy().copy(), "on": on,
+                "lock": lock, "sso": sso}
+
+    def host_params(self):
+        return {k: getattr(self, k).numpy().copy() for k in ("ua", "ca", "cm", "hm", "target", "cap_idx")}
+
+
+class GlooComm:
+    def __init__(self):
+        import torch.distributed as dist
+
+        self.dist = dist
+        self.rank, self.world = dist.get_rank(), dist.get_world_size()
+
+    def attach(self, shard):
+        pass
+
+    def allreduce_counts(self, shard):
+        self.dist.all_reduce(shard.counts)
+
+    def allreduce_penalty(self, shard):
+        s = shard.partial2[:1].clone()
+        m = shard.partial2[1:].clone()
+        self.dist.all_reduce(s)
+        self.dist.all_reduce(m, op=self.dist.ReduceOp.MAX)
+        shard.partial2[0], shard.partial2[1] = s[0], m[0]
+
+    def allgather_state(self, shard, st, prm, n):
+        out_st, out_prm = {}, {}
+        for src, dst, keys in ((st, out_st, ("T", "Tm", "on", "lock", "sso")),
+                               (prm, out_prm, ("ua", "ca", "cm", "hm", "target", "cap_idx"))):
+            for key in keys:
+                a = np.asarray(src[key])
+                parts = [None] * self.world
+                self.dist.all_gather_object(parts, a)
+                dst[key] = np.concatenate(parts)
+        return out_st, out_prm

@@ -1,0 +1,91 @@
+"""Multi-process (world_size 2, gloo, CPU) test of the sharded Environment orchestration.
+
+Each rank runs mdr_amd.Environment over its contiguous house range with the oracle-backed test
+shard (tests/oracle_shard.py) and a gloo comm; the per-tick cluster-power counts and the common
+penalty reductions go through all_reduce exactly where the RCCL path exchanges them.  The
+sharded run must equal the single-process oracle run bit for bit (integers) and to 1e-12."""
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import golden_util as gu
+from oracle import env_np as O
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def _worker(rank, world, port, overrides, seed, actions, out_dir):
+    import torch.distributed as dist
+
+    sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "marl-demandresponse_amd"), os.path.dirname(HERE)]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import golden_util as g
+    from oracle_shard import GlooComm, OracleShard
+
+    from mdr_amd.environment import Environment
+
+    props = g.props_from_overrides(overrides)
+    env = Environment(props, rng=random.Random(seed), rank=rank, world=world, comm=GlooComm(),
+                      _shard_factory=OracleShard)
+    import torch
+
+    lo, nl = env._offset, env.n_local
+    rewards, Ts, ons = [], [], []
+    obs_msgs = None
+    for t in range(actions.shape[0]):
+        r = env.step_tensor(torch.from_numpy(actions[t, lo:lo + nl].copy()))
+        rewards.append(r.numpy().copy())
+        st = env.shard.host_state()
+        Ts.append(st["T"])
+        ons.append(st["on"])
+    obs = env.get_obs()
+    obs_msgs = np.array([[m["current_temp_diff_to_target"] for m in obs[g_]["message"]] for g_ in sorted(obs)])
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), lo=lo, rewards=np.array(rewards), T=np.array(Ts),
+             on=np.array(ons), msgs=obs_msgs, P=env.cluster.current_power_consumption,
+             S=float(env.power_grid.current_signal), tod=float(env.current_od_temp))
+    dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("mode,n", [("individual_L2", 101), ("common_L2", 64), ("mixture", 37)])
+def test_sharded_env_equals_oracle(tmp_path, mode, n):
+    world, T, seed = 2, 12, 21
+    overrides = {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals",
+                 "reward_prop.penalty_props.mode": mode, "reward_prop.penalty_props.alpha_common_max": 0.5,
+                 "cluster_prop.house_prop.deadband": 0.3}
+    actions = np.random.RandomState(n).randint(0, 2, (T, n)).astype(np.uint8)
+    mp.start_processes(_worker, args=(world, _free_port(), overrides, seed, actions, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    parts = [np.load(tmp_path / f"rank{r}.npz") for r in range(world)]
+    props = gu.props_from_overrides(overrides)
+    ora = O.OracleEnv(props, random.Random(seed))
+    for t in range(T):
+        o, rr = ora.step(actions[t].astype(bool))
+        got_r = np.concatenate([p["rewards"][t] for p in parts])
+        got_T = np.concatenate([p["T"][t] for p in parts])
+        got_on = np.concatenate([p["on"][t] for p in parts])
+        np.testing.assert_array_equal(got_on, o["on"])
+        np.testing.assert_array_equal(got_T, o["T"])  # same arithmetic: bit-exact
+        np.testing.assert_allclose(got_r, rr, rtol=1e-12, atol=1e-15)
+    for p in parts:
+        assert float(p["P"]) == ora.P and float(p["S"]) == float(ora.S) and float(p["tod"]) == ora.Tod
+    # dict obs of a sharded env: messages cross the shard edge (ring neighbours of house 0 wrap)
+    msgs = np.concatenate([p["msgs"] for p in parts])
+    links = O.comm_links(props.cluster_prop, random)
+    ref = np.array([[ora.T[j] - ora.pop["target"][j] for j in row] for row in links])
+    np.testing.assert_array_equal(msgs, ref)
