@@ -331,7 +331,10 @@ class Environment:
         cp, hp = p.cluster_prop, p.cluster_prop.house_prop
         sp, mp = p.state_prop, cp.message_prop
         links = self._obs_links
-        k = int(links.shape[1]) if links is not None and links.ndim == 2 else popmod.nb_comm(cp)
+        if links is not None and not isinstance(links, np.ndarray):
+            raise ValueError("ragged closed_groups neighbour lists (nb_comm < max_nb_agents_communication) "
+                             "have no fixed-width observation vector")
+        k = int(links.shape[1]) if links is not None else popmod.nb_comm(cp)
         msg_w = 4 + (4 if mp.thermal else 0) + (3 if mp.hvac else 0)
         n_feat = 10 + (2 if sp.hvac else 0) + (1 if sp.solar_gain else 0) + (5 if sp.thermal else 0) + k * msg_w
         spec = L.mdr_obs_spec()
@@ -453,8 +456,7 @@ class Environment:
         host.update(date_time=self.date_time, current_od_temp=self.current_od_temp,
                     current_signal=self.power_grid.current_signal, solar=self._solar, tick=self._tick,
                     P=self._cluster_power(), cap_values=list(self._cap_values),
-                    links=None if self._links is None else self._links.copy(),
-                    obs_links=None if self._obs_links is None else np.array(self._obs_links))
+                    links=copy.deepcopy(self._links), obs_links=copy.deepcopy(self._obs_links))
         return host
 
     def load_state_dict(self, sd: dict) -> None:

@@ -63,7 +63,7 @@ def comm_links(cluster_prop, rng=_random):
         off = np.concatenate([np.arange(-lo, 0), np.arange(1, hi + 1)])
         return ((ids + off[None, :]) % n).astype(np.int32)
     if mode == "closed_groups":
-        out = np.empty((n, k), np.int32)
+        out = []
         for i in range(n):
             base = i - i % (k + 1)
             if base + k <= n:
@@ -71,7 +71,11 @@ def comm_links(cluster_prop, rng=_random):
             else:
                 grp = [n - k - 1 + j for j in range(k + 1)]
             grp.remove(i)
-            out[i] = grp
+            out.append(grp)
+        # with nb_comm < max_nb_agents_communication (small clusters) the reference builds ragged
+        # groups that may name houses >= N (its get_obs then raises IndexError): keep them as is
+        if len({len(g) for g in out}) == 1:
+            return np.array(out, np.int32).reshape(n, len(out[0]))
         return out
     if mode == "random_sample":
         return None
