@@ -131,12 +131,48 @@ __device__ __forceinline__ u32x4 philox4x32_10(u32x4 c, uint32_t k0, uint32_t k1
   return c;
 }
 
-// Random controller: Bernoulli(0.5) per (house, tick)
-__device__ __forceinline__ bool random_action(uint64_t seed, uint64_t gid, uint64_t tick) {
-  const u32x4 r = philox4x32_10(u32x4{(uint32_t)gid, (uint32_t)(gid >> 32), (uint32_t)tick,
-                                      (uint32_t)(tick >> 32) ^ 0x5A17u},
+// Random controller: Bernoulli(0.5) per (house, tick).  The bit of global house gid at tick t is
+// bit (gid & 63) of the first 64 bits of Philox4x32-10(seed; counter = (gid >> 6, t)), so it does
+// not depend on sharding or on how houses map to threads.  One wave evaluates the generator ONCE
+// for all its houses and both ticks it needs (t and t + 1): lanes 0..31 take the 64-house groups
+// starting at the wave's first id for tick t, lanes 32..63 the same groups for t + 1, and every
+// house fetches its word from the owning lane (4 cross-lane reads).  All lanes of the wave must
+// call it with the same wave-uniform gbase (first id of the wave) and tick; a wave may span at
+// most 32 groups (here <= 3).
+__device__ __forceinline__ void philox_words(uint64_t seed, uint64_t grp, uint64_t t, uint32_t& lo,
+                                             uint32_t& hi) {
+  const u32x4 r = philox4x32_10(u32x4{(uint32_t)grp, (uint32_t)(grp >> 32), (uint32_t)t,
+                                      (uint32_t)(t >> 32) ^ 0x5A17u},
                                 (uint32_t)seed, (uint32_t)(seed >> 32));
-  return (r.x & 1u) != 0;
+  lo = r.x;
+  hi = r.y;
+}
+
+__device__ __forceinline__ bool bit_of(uint32_t lo, uint32_t hi, uint64_t gid) {
+  const int b = (int)(gid & 63);
+  return ((b < 32 ? (lo >> b) : (hi >> (b - 32))) & 1u) != 0;
+}
+
+struct WaveRandom {
+  uint32_t lo, hi;  // this lane's generator words
+  uint64_t g0;      // first 64-house group of the wave
+  __device__ __forceinline__ WaveRandom(uint64_t seed, uint64_t gbase, uint64_t t) {
+    const int lane = threadIdx.x & 63;
+    g0 = gbase >> 6;
+    philox_words(seed, g0 + (lane & 31), t + (lane >> 5), lo, hi);
+  }
+  // action of house gid at tick t (next = false) or t + 1 (next = true)
+  __device__ __forceinline__ bool get(uint64_t gid, bool next) const {
+    const int src = (int)((gid >> 6) - g0) + (next ? 32 : 0);
+    return bit_of((uint32_t)__shfl((int)lo, src), (uint32_t)__shfl((int)hi, src), gid);
+  }
+};
+
+// the same bit evaluated for one house alone (host-side checks / slow paths)
+__device__ __forceinline__ bool random_action(uint64_t seed, uint64_t gid, uint64_t tick) {
+  uint32_t lo, hi;
+  philox_words(seed, gid >> 6, tick, lo, hi);
+  return bit_of(lo, hi, gid);
 }
 
 __device__ __forceinline__ double u01(uint32_t x) { return ((double)x + 0.5) * 2.3283064365386963e-10; }

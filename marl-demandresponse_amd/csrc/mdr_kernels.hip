@@ -30,13 +30,6 @@ __device__ __forceinline__ void count_on(bool on, int cls, int n_cap, unsigned* 
   }
 }
 
-__device__ __forceinline__ bool tick_action(int mode, const uint8_t* action, int64_t i,
-                                            uint64_t seed, uint64_t gid, uint64_t tick) {
-  if (mode == MDR_ACT_BUFFER) return action[i] != 0;
-  if (mode == MDR_ACT_RANDOM) return random_action(seed, gid, tick);
-  return true;  // MDR_ACT_ALWAYS_ON
-}
-
 // --------------------------------------------------------------------------------------- K0
 // Phase 1: FSM only -> ON count per capacity class (cluster.py:82-88).  Reads 6 B per house.
 __global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* __restrict__ action,
@@ -48,10 +41,16 @@ __global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* 
   if ((int)threadIdx.x < p.n_cap) hist[threadIdx.x] = 0;
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t wave0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
+  bool a = action_mode == MDR_ACT_ALWAYS_ON;
+  if (action_mode == MDR_ACT_RANDOM) {
+    const WaveRandom wr(p.seed, p.goff + wave0, tick);  // whole wave, before any divergence
+    a = wr.get(p.goff + i, false);
+  }
   bool on = false;
   int cls = 0;
   if (i < p.n) {
-    const bool a = tick_action(action_mode, action, i, p.seed, p.goff + i, tick);
+    if (action_mode == MDR_ACT_BUFFER) a = action[i] != 0;
     on = hv_on(hvac_fsm(p.hvac[i], a, p.dt, p.L));
     cls = p.cap_idx[i];
   }
@@ -68,9 +67,11 @@ __global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* 
 //               (random / always-on / bang-bang on the new state) are accumulated here, so the
 //               next tick needs no phase-1 launch.
 
-__device__ __forceinline__ unsigned long long wave_sum_u64(unsigned long long v) {
+// sum over the 64 lanes; 32-bit partial sums are exact while the cluster has < 2^32 houses
+__device__ __forceinline__ unsigned long long wave_sum_counts(unsigned long long v64) {
+  unsigned v = (unsigned)v64;
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  for (int off = 32; off > 0; off >>= 1) v += (unsigned)__shfl_xor((int)v, off);
   return v;
 }
 
@@ -81,17 +82,16 @@ __device__ __forceinline__ double wave_power(const unsigned long long* __restric
   const int lane = threadIdx.x & 63;
   double P = 0.0;
   for (int k = 0; k < n_cap; ++k) {
-    const unsigned long long c = wave_sum_u64(counts[lane * n_cap + k]);
+    const unsigned long long c = wave_sum_counts(counts[lane * n_cap + k]);
     P += (double)c * p_on[k];
   }
   return P;
 }
 
-__device__ __forceinline__ bool pick_action(int mode, const uint8_t* action, int64_t i, uint64_t seed,
-                                            uint64_t gid, uint64_t tick, double T, double tgt,
-                                            double deadband, uint32_t w0) {
+__device__ __forceinline__ bool pick_action(int mode, const uint8_t* action, int64_t i, bool rnd,
+                                            double T, double tgt, double deadband, uint32_t w0) {
   if (mode == MDR_ACT_BUFFER) return action[i] != 0;
-  if (mode == MDR_ACT_RANDOM) return random_action(seed, gid, tick);
+  if (mode == MDR_ACT_RANDOM) return rnd;
   if (mode == MDR_ACT_ALWAYS_ON) return true;
   if (mode == kActBangBang) return ctrl_bangbang(T, tgt);
   return ctrl_deadband(T, tgt, deadband, hv_on(w0));
@@ -165,27 +165,43 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   const double sig_term = p.alpha_sig * (x * x) / p.norm_sig;
   if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
 
+  // random controller bits of this tick (and the next, for the lookahead) for the whole wave
+  bool rnd[HPT], rnd1[HPT];
+  if (action_mode == MDR_ACT_RANDOM || lookahead == MDR_ACT_RANDOM) {
+    const int64_t wave0 = (((int64_t)blockIdx.x * blockDim.x) + (tid & ~63)) * HPT;
+    const WaveRandom wr(p.seed, p.goff + wave0, tk.tick);
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) {
+      rnd[h] = wr.get(p.goff + i0 + h, false);
+      rnd1[h] = wr.get(p.goff + i0 + h, true);
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) rnd[h] = rnd1[h] = false;
+  }
+
   double Tn[HPT], Tmn[HPT], rw[HPT], pen[HPT];
   uint32_t w[HPT];
   bool on[HPT], on1[HPT];
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
     const int64_t i = i0 + h;
-    const uint64_t gid = p.goff + i;
-    const bool a = valid[h] && pick_action(action_mode, action, i, p.seed, gid, tk.tick, T[h], tg[h],
-                                           p.deadband, w0[h]);
+    const bool a = valid[h] && pick_action(action_mode, action, i, rnd[h], T[h], tg[h], p.deadband, w0[h]);
     w[h] = hvac_fsm(w0[h], a, p.dt, p.L);
     on[h] = hv_on(w[h]);
     const double q = on[h] ? p.q_on[cls[h]] : 0.0;
     if (!CACHED) kc[h] = rc_coeffs(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
     rc_apply(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
     pen[h] = deadband_l2(tg[h], p.deadband, Tn[h]);
-    rw[h] = p.penalty_mode == MDR_PEN_INDIVIDUAL_L2 ? -(p.alpha_temp * pen[h] / p.norm_temp + sig_term)
-                                                    : pen[h];  // finalised by k_reward_finalize
+    // x / 1.0 == x exactly: the default normaliser (integer target) costs no division
+    const double tpen = p.alpha_temp * pen[h];
+    rw[h] = p.penalty_mode == MDR_PEN_INDIVIDUAL_L2
+                ? -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig_term)
+                : pen[h];  // finalised by k_reward_finalize
     on1[h] = false;
     if (valid[h] && lookahead) {
       bool an;
-      if (lookahead == MDR_ACT_RANDOM) an = random_action(p.seed, gid, tk.tick + 1);
+      if (lookahead == MDR_ACT_RANDOM) an = rnd1[h];
       else if (lookahead == MDR_ACT_ALWAYS_ON) an = true;
       else if (lookahead == kActBangBang) an = ctrl_bangbang(Tn[h], tg[h]);
       else an = ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
