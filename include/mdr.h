@@ -251,6 +251,9 @@ int mdr_rollout_sharded(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const 
 /* Memory-floor probe: the loads/stores of one mdr_step over the bound arrays with no arithmetic
  * (writes the state back unchanged, garbage into reward).  Roofline calibration only. */
 int mdr_probe_stream(mdr_ctx* ctx, double* reward, void* stream);
+/* Exact-division self-check: counts (into *mismatches, device int64) the i where the
+ * shared-reciprocal division sequence of the step kernels differs bitwise from a[i] / b[i]. */
+int mdr_div_check(const double* a, const double* b, int64_t n, int64_t* mismatches, void* stream);
 
 /* ---- timing helpers for bench.py (HIP events on the given stream) ---------------------- */
 int mdr_event_record(mdr_ctx* ctx, int slot, void* stream);

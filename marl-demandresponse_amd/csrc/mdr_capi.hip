@@ -79,6 +79,7 @@ struct mdr_ctx {
   int pen_blocks = 0;
   int hpt = 2;                           // houses per thread of k_step (MDR_HPT env overrides)
   bool cached = false;                   // cached param-only thermal coefficients (MDR_VARIANT=coef)
+  bool fastdiv = false;                  // shared-reciprocal exact division (MDR_FASTDIV=1)
   bool coef_dirty = true;
   double* d_coef = nullptr;              // [6][n] r1, r2, A3, A4, e1, e2
   // rollout tick drivers
@@ -140,13 +141,18 @@ int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const 
   }
   KParams kp = c->kp;
   kp.coef = c->cached ? c->d_coef : nullptr;
-#define MDR_LAUNCH_STEP(H, C)                                                                        \
-  hipLaunchKernelGGL((k_step_t<H, C>), dim3(blocks(kp.n, 256 * H)), dim3(256), 0, st, kp, action, mode, \
-                     tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer, c->d_pen_partial)
+#define MDR_LAUNCH_STEP(H, C, F)                                                                      \
+  hipLaunchKernelGGL((k_step_t<H, C, F>), dim3(blocks(kp.n, 256 * H)), dim3(256), 0, st, kp, action,      \
+                     mode, tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer,              \
+                     c->d_pen_partial)
   if (c->hpt == 2) {
-    if (c->cached) MDR_LAUNCH_STEP(2, true); else MDR_LAUNCH_STEP(2, false);
+    if (c->fastdiv) {
+      if (c->cached) MDR_LAUNCH_STEP(2, true, true); else MDR_LAUNCH_STEP(2, false, true);
+    } else {
+      if (c->cached) MDR_LAUNCH_STEP(2, true, false); else MDR_LAUNCH_STEP(2, false, false);
+    }
   } else {
-    if (c->cached) MDR_LAUNCH_STEP(1, true); else MDR_LAUNCH_STEP(1, false);
+    if (c->cached) MDR_LAUNCH_STEP(1, true, false); else MDR_LAUNCH_STEP(1, false, false);
   }
 #undef MDR_LAUNCH_STEP
   LAUNCH_CHECK("k_step");
@@ -222,6 +228,7 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
     return cleanup(fail(MDR_EHIP, "count slabs memset"));
   if (const char* e = getenv("MDR_HPT")) c->hpt = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("MDR_VARIANT")) c->cached = strcmp(e, "coef") == 0;
+  if (const char* e = getenv("MDR_FASTDIV")) c->fastdiv = atoi(e) != 0;
   if (c->cached) {
     k.coef_stride = cfg->n_local;
     if (hipMalloc(&c->d_coef, 6 * sizeof(double) * cfg->n_local) != hipSuccess)
@@ -636,6 +643,15 @@ int mdr_probe_stream(mdr_ctx* c, double* reward, void* stream) {
   if (!c->bound) return fail(MDR_ESTATE, "mdr_probe_stream: context not bound");
   hipLaunchKernelGGL(k_probe_stream, dim3(blocks(c->kp.n, 512)), dim3(256), 0, S(stream), c->kp, reward);
   LAUNCH_CHECK("k_probe_stream");
+  return MDR_OK;
+}
+
+int mdr_div_check(const double* a, const double* b, int64_t n, int64_t* mismatches, void* stream) {
+  if (!a || !b || !mismatches || n < 0) return fail(MDR_EARG, "mdr_div_check: bad argument");
+  HIP_TRY(hipMemsetAsync(mismatches, 0, sizeof(int64_t), S(stream)));
+  hipLaunchKernelGGL(k_div_check, dim3(blocks(n, 256)), dim3(256), 0, S(stream), a, b, n,
+                     reinterpret_cast<unsigned long long*>(mismatches));
+  LAUNCH_CHECK("k_div_check");
   return MDR_OK;
 }
 

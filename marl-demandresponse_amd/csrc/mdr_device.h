@@ -50,29 +50,89 @@ __device__ __forceinline__ uint32_t hv_sso(uint32_t w) { return w & kSsoMask; }
 // operation order, so a cached RcCoef gives bit-identical results to recomputing it every tick.
 // q_hvac = HVAC.get_heat_transfer (hvac.py:85-99), solar = compute_solar_gain (per-tick scalar),
 // t_od = previous tick's outdoor temperature.
+// ---------------------------------------------------------------------------- exact division
+// a / b correctly rounded with the reciprocal shared by every quotient that has the same
+// divisor.  This is the gfx950 IEEE division sequence LLVM emits for fdiv f64 (v_rcp_f64, two
+// Newton steps, q0 = a*y, r = fma(-b, q0, a), q = fma(r, y, q0); Markstein's theorem makes the
+// final correction exact) minus v_div_scale / v_div_fixup, which only act for denormals, zero /
+// inf / nan operands or operand exponents 768+ apart.  Callers check `Recip::safe` (divisor and
+// numerators within [2^-300, 2^300]) and fall back to the plain operator otherwise, so results
+// are bit-identical to `a / b` (tests/test_division_gpu.py checks this on 10^8 random pairs).
+struct Recip {
+  double b, nb, y;
+};
+
+__device__ __forceinline__ Recip recip(double b) {
+  Recip r;
+  r.b = b;
+  r.nb = -b;
+  double y = __builtin_amdgcn_rcp(b);
+  const double e0 = __builtin_fma(r.nb, y, 1.0);
+  y = __builtin_fma(y, e0, y);
+  const double e1 = __builtin_fma(r.nb, y, 1.0);
+  r.y = __builtin_fma(y, e1, y);
+  return r;
+}
+
+__device__ __forceinline__ double div_by(double a, const Recip& r) {
+  const double q0 = a * r.y;
+  const double rem = __builtin_fma(r.nb, q0, a);
+  return __builtin_fma(rem, r.y, q0);
+}
+
+// |x| in [2^-300, 2^300] (zero excluded): no scaling can trigger in the hardware sequence
+__device__ __forceinline__ bool div_safe(double x) {
+  const uint32_t e = (uint32_t)(__double_as_longlong(x) >> 52) & 0x7FF;
+  return e >= 1023 - 300 && e <= 1023 + 300;
+}
+
+// ---------------------------------------------------------------------------- RC coefficients
 struct RcCoef { double r1, r2, A3, A4, e1, e2; };
 
-__device__ __forceinline__ RcCoef rc_coeffs(double Ua, double Ca, double Cm, double Hm, double dt) {
+// FAST = shared-reciprocal division (callers guarantee div_safe operands)
+template <bool FAST>
+__device__ __forceinline__ RcCoef rc_coeffs_t(double Ua, double Ca, double Cm, double Hm, double dt) {
   RcCoef k;
-  const double a = Cm * Ca / Hm;
   const double UaHm = Ua + Hm;
-  const double b = Cm * UaHm / Hm + Ca;
   const double c = Ua;
-  const double disc = __builtin_sqrt(b * b - 4.0 * a * c);
-  const double two_a = 2.0 * a;
-  k.r1 = (-b + disc) / two_a;
-  k.r2 = (-b - disc) / two_a;
-  const double UaHm_Hm = UaHm / Hm;
-  k.A3 = k.r1 * Ca / Hm + UaHm_Hm;
-  k.A4 = k.r2 * Ca / Hm + UaHm_Hm;
+  double a, b, UaHm_Hm, r1Ca_Hm, r2Ca_Hm;
+  if (FAST) {
+    const Recip rH = recip(Hm);
+    a = div_by(Cm * Ca, rH);
+    b = div_by(Cm * UaHm, rH) + Ca;
+    const double disc = __builtin_sqrt(b * b - 4.0 * a * c);
+    const Recip r2a = recip(2.0 * a);
+    k.r1 = div_by(-b + disc, r2a);
+    k.r2 = div_by(-b - disc, r2a);
+    UaHm_Hm = div_by(UaHm, rH);
+    r1Ca_Hm = div_by(k.r1 * Ca, rH);
+    r2Ca_Hm = div_by(k.r2 * Ca, rH);
+  } else {
+    a = Cm * Ca / Hm;
+    b = Cm * UaHm / Hm + Ca;
+    const double disc = __builtin_sqrt(b * b - 4.0 * a * c);
+    const double two_a = 2.0 * a;
+    k.r1 = (-b + disc) / two_a;
+    k.r2 = (-b - disc) / two_a;
+    UaHm_Hm = UaHm / Hm;
+    r1Ca_Hm = k.r1 * Ca / Hm;
+    r2Ca_Hm = k.r2 * Ca / Hm;
+  }
+  k.A3 = r1Ca_Hm + UaHm_Hm;
+  k.A4 = r2Ca_Hm + UaHm_Hm;
   k.e1 = exp(k.r1 * dt);
   k.e2 = exp(k.r2 * dt);
   return k;
 }
 
-__device__ __forceinline__ void rc_apply(double T, double Tm, double Ua, double Ca, double Hm,
-                                         const RcCoef& k, double q_hvac, double solar, double t_od,
-                                         double& T_out, double& Tm_out) {
+__device__ __forceinline__ RcCoef rc_coeffs(double Ua, double Ca, double Cm, double Hm, double dt) {
+  return rc_coeffs_t<false>(Ua, Ca, Cm, Hm, dt);
+}
+
+template <bool FAST>
+__device__ __forceinline__ void rc_apply_t(double T, double Tm, double Ua, double Ca, double Hm,
+                                           const RcCoef& k, double q_hvac, double solar, double t_od,
+                                           double& T_out, double& Tm_out) {
   const double od_k = t_od + 273.0;
   const double t_k = T + 273.0;
   const double tm_k = Tm + 273.0;
@@ -80,14 +140,31 @@ __device__ __forceinline__ void rc_apply(double T, double Tm, double Ua, double 
   const double UaHm = Ua + Hm;
   const double c = Ua;
   const double d = Qa + Ua * od_k;  // Qm (= 0) + Qa + Ua * od_k
-  const double dTA0dt = Hm * tm_k / Ca - UaHm * t_k / Ca + Ua * od_k / Ca + Qa / Ca;
-  const double d_c = d / c;
-  const double A1 = (k.r2 * t_k - dTA0dt - k.r2 * d / c) / (k.r2 - k.r1);
+  double dTA0dt, d_c, r2d_c, A1;
+  if (FAST) {
+    const Recip rCa = recip(Ca);
+    const Recip rc = recip(c);
+    dTA0dt = div_by(Hm * tm_k, rCa) - div_by(UaHm * t_k, rCa) + div_by(Ua * od_k, rCa) + div_by(Qa, rCa);
+    d_c = div_by(d, rc);
+    r2d_c = div_by(k.r2 * d, rc);
+    A1 = div_by(k.r2 * t_k - dTA0dt - r2d_c, recip(k.r2 - k.r1));
+  } else {
+    dTA0dt = Hm * tm_k / Ca - UaHm * t_k / Ca + Ua * od_k / Ca + Qa / Ca;
+    d_c = d / c;
+    r2d_c = k.r2 * d / c;
+    A1 = (k.r2 * t_k - dTA0dt - r2d_c) / (k.r2 - k.r1);
+  }
   const double A2 = t_k - d_c - A1;
   const double t_new = A1 * k.e1 + A2 * k.e2 + d_c;
   const double tm_new = A1 * k.A3 * k.e1 + A2 * k.A4 * k.e2 + 0.0 + d_c;  // + g (= Qm/Hm = 0)
   T_out = t_new - 273.0;
   Tm_out = tm_new - 273.0;
+}
+
+__device__ __forceinline__ void rc_apply(double T, double Tm, double Ua, double Ca, double Hm,
+                                         const RcCoef& k, double q_hvac, double solar, double t_od,
+                                         double& T_out, double& Tm_out) {
+  rc_apply_t<false>(T, Tm, Ua, Ca, Hm, k, q_hvac, solar, t_od, T_out, Tm_out);
 }
 
 __device__ __forceinline__ void rc_update(double T, double Tm, double Ua, double Ca, double Cm,

@@ -54,7 +54,7 @@ struct ObsArgs {
 
 __global__ void k_power_counts(KParams p, const uint8_t* action, int action_mode, uint64_t tick,
                                const TickArgs* tkp, unsigned long long* slab);
-template <int HPT, bool CACHED>
+template <int HPT, bool CACHED, bool FAST>
 __global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, TickArgs tk,
                          const TickArgs* tkp, const unsigned long long* counts, double* reward,
                          int ctrl, uint8_t* ctrl_out, double* p_out, int lookahead,
@@ -62,6 +62,7 @@ __global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, Tick
                          double* pen_partial);
 __global__ void k_probe_stream(KParams p, double* reward);
 __global__ void k_coeffs(KParams p, double* coef);
+__global__ void k_div_check(const double* a, const double* b, int64_t n, unsigned long long* mismatches);
 __global__ void k_pen_reduce(const double* pen_partial, int nblk, double* partial2);
 __global__ void k_reward_finalize(KParams p, TickArgs tk, const unsigned long long* counts,
                                   const double* partial2, double* reward);

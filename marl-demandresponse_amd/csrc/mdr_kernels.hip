@@ -97,7 +97,7 @@ __device__ __forceinline__ bool pick_action(int mode, const uint8_t* action, int
   return ctrl_deadband(T, tgt, deadband, hv_on(w0));
 }
 
-template <int HPT, bool CACHED>
+template <int HPT, bool CACHED, bool FAST>
 __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __restrict__ action,
                                                 int action_mode, TickArgs tk0, const TickArgs* tkp,
                                                 const unsigned long long* __restrict__ counts,
@@ -190,8 +190,8 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
     w[h] = hvac_fsm(w0[h], a, p.dt, p.L);
     on[h] = hv_on(w[h]);
     const double q = on[h] ? p.q_on[cls[h]] : 0.0;
-    if (!CACHED) kc[h] = rc_coeffs(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
-    rc_apply(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
+    if (!CACHED) kc[h] = rc_coeffs_t<FAST>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+    rc_apply_t<FAST>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
     pen[h] = deadband_l2(tg[h], p.deadband, Tn[h]);
     // x / 1.0 == x exactly: the default normaliser (integer target) costs no division
     const double tpen = p.alpha_temp * pen[h];
@@ -266,15 +266,28 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   }
 }
 
-#define MDR_INST_STEP(H, C)                                                                       \
-  template __global__ void k_step_t<H, C>(KParams, const uint8_t*, int, TickArgs, const TickArgs*, \
-                                          const unsigned long long*, double*, int, uint8_t*,      \
-                                          double*, int, unsigned long long*, unsigned long long*, \
-                                          double*);
-MDR_INST_STEP(1, false)
-MDR_INST_STEP(2, false)
-MDR_INST_STEP(1, true)
-MDR_INST_STEP(2, true)
+#define MDR_INST_STEP(H, C, F)                                                                    \
+  template __global__ void k_step_t<H, C, F>(KParams, const uint8_t*, int, TickArgs, const TickArgs*, \
+                                             const unsigned long long*, double*, int, uint8_t*,   \
+                                             double*, int, unsigned long long*, unsigned long long*, \
+                                             double*);
+MDR_INST_STEP(1, false, false)
+MDR_INST_STEP(2, false, false)
+MDR_INST_STEP(1, true, false)
+MDR_INST_STEP(2, true, false)
+MDR_INST_STEP(2, false, true)
+MDR_INST_STEP(2, true, true)
+
+// Division self-check: q_fast = shared-reciprocal sequence, q_ieee = the / operator.
+__global__ void k_div_check(const double* __restrict__ a, const double* __restrict__ b, int64_t n,
+                            unsigned long long* __restrict__ mismatches) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const double x = a[i], y = b[i];
+  const double f = div_by(x, recip(y));
+  const double q = x / y;
+  if (__double_as_longlong(f) != __double_as_longlong(q)) atomicAdd(mismatches, 1ull);
+}
 
 // Param-only thermal coefficients (rc_coeffs) of every house, for the CACHED step variant.
 __global__ void __launch_bounds__(256) k_coeffs(KParams p, double* __restrict__ coef) {

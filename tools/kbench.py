@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--houses", default="1048576,4194304,16777216")
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="hpt1,hpt2,coef1,coef2,probe")
+    ap.add_argument("--variants", default="hpt2,fast2,coef2,fcoef2,probe")
     a = ap.parse_args()
     import torch
 
@@ -31,7 +31,8 @@ def main():
         envs = {}
         for v in a.variants.split(","):
             os.environ["MDR_HPT"] = "1" if v.endswith("1") else "2"
-            os.environ["MDR_VARIANT"] = "coef" if v.startswith("coef") else "raw"
+            os.environ["MDR_VARIANT"] = "coef" if "coef" in v else "raw"
+            os.environ["MDR_FASTDIV"] = "1" if v.startswith("f") else "0"
             envs[v] = Environment(env_props(n), device="cuda:0", rng=random.Random(1),
                                   population="synthetic", seed=5)
             rews = torch.empty(n, dtype=torch.float64, device="cuda:0")
