@@ -77,11 +77,13 @@ struct mdr_ctx {
   double* d_pen_partial = nullptr;       // 2 per block of k_step
   double* d_partial2 = nullptr;
   int pen_blocks = 0;
+  unsigned step_grid = 0;                // k_step grid: min(tiles, resident blocks x oversub)
   int hpt = 2;                           // houses per thread of k_step (MDR_HPT env overrides)
   bool cached = false;                   // cached param-only thermal coefficients (MDR_VARIANT=coef)
-  bool fastdiv = false;                  // shared-reciprocal exact division (MDR_FASTDIV=1)
+  bool fastdiv = true;                   // shared-reciprocal exact division (MDR_FASTDIV=0 disables)
   bool coef_dirty = true;
   double* d_coef = nullptr;              // [6][n] r1, r2, A3, A4, e1, e2
+  int* d_flags = nullptr;                // [0] params_bad
   // rollout tick drivers
   TickArgs* d_ticks = nullptr;
   TickArgs* h_ticks = nullptr;  // pinned staging
@@ -128,21 +130,29 @@ int launch_counts(mdr_ctx* c, const uint8_t* action, int mode, uint64_t tick, co
   return MDR_OK;
 }
 
+// parameter-derived state (fast-division range flag, cached coefficients) after a change;
+// called before any launch sequence is captured, so graphs never contain it
+int refresh_if_dirty(mdr_ctx* c, hipStream_t st) {
+  if (!c->coef_dirty) return MDR_OK;
+  HIP_TRY(hipMemsetAsync(c->d_flags, 0, sizeof(int), st));
+  hipLaunchKernelGGL(k_refresh, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp,
+                     c->cached ? c->d_coef : nullptr, c->d_flags);
+  LAUNCH_CHECK("k_refresh");
+  c->coef_dirty = false;
+  return MDR_OK;
+}
+
 int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const TickArgs* tkp,
                 double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
                 hipStream_t st) {
   unsigned long long* cur = slab_at(c, c->ring);
   unsigned long long* nxt = slab_at(c, c->ring + 1);
   unsigned long long* zer = slab_at(c, c->ring + 2);
-  if (c->cached && c->coef_dirty) {
-    hipLaunchKernelGGL(k_coeffs, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, c->d_coef);
-    LAUNCH_CHECK("k_coeffs");
-    c->coef_dirty = false;
-  }
+  if (int rc = refresh_if_dirty(c, st)) return rc;
   KParams kp = c->kp;
   kp.coef = c->cached ? c->d_coef : nullptr;
 #define MDR_LAUNCH_STEP(H, C, F)                                                                      \
-  hipLaunchKernelGGL((k_step_t<H, C, F>), dim3(blocks(kp.n, 256 * H)), dim3(256), 0, st, kp, action,      \
+  hipLaunchKernelGGL((k_step_t<H, C, F>), dim3(c->step_grid), dim3(256), 0, st, kp, action,               \
                      mode, tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer,              \
                      c->d_pen_partial)
   if (c->hpt == 2) {
@@ -221,6 +231,14 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
     return cleanup(fail(MDR_EHIP, "tables copy"));
   k.q_on = c->d_tables;
   k.p_on = c->d_tables + MDR_MAX_CAP;
+  if (hipMalloc(&c->d_flags, 16) != hipSuccess) return cleanup(fail(MDR_ENOMEM, "flags"));
+  k.params_bad = c->d_flags;
+  {
+    // the fast division is provably exact for dt < 2^20 s and |q_on| < 2^40 W (mdr_device.h)
+    bool ok = cfg->dt < (1 << 20);
+    for (int i = 0; i < cfg->n_cap; ++i) ok = ok && fabs(tab[i]) < 1099511627776.0;
+    k.fast_tick_ok = ok ? 1 : 0;
+  }
   c->slab_len = kCountShards * cfg->n_cap;
   if (hipMalloc(&c->d_slab, 3 * c->slab_len * sizeof(unsigned long long)) != hipSuccess)
     return cleanup(fail(MDR_ENOMEM, "count slabs"));
@@ -234,7 +252,24 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
     if (hipMalloc(&c->d_coef, 6 * sizeof(double) * cfg->n_local) != hipSuccess)
       return cleanup(fail(MDR_ENOMEM, "coefficients"));
   }
-  c->pen_blocks = (int)blocks(cfg->n_local, 256 * c->hpt);  // = k_step grid
+  {
+    // resident-grid sizing for the grid-stride step kernel
+    const void* fn = c->hpt == 2 ? (c->cached ? (c->fastdiv ? (const void*)k_step_t<2, true, true> : (const void*)k_step_t<2, true, false>)
+                                              : (c->fastdiv ? (const void*)k_step_t<2, false, true> : (const void*)k_step_t<2, false, false>))
+                                 : (c->cached ? (const void*)k_step_t<1, true, false> : (const void*)k_step_t<1, false, false>);
+    int per_cu = 0, cus = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess) cus = prop.multiProcessorCount;
+    if (cus < 1) cus = 256;
+    int oversub = 1;
+    if (const char* e = getenv("MDR_GRID_OVERSUB")) oversub = atoi(e) > 0 ? atoi(e) : 1;
+    const int64_t tiles_blocks = blocks(cfg->n_local, 256 * c->hpt);
+    const int64_t resident = (int64_t)per_cu * cus * oversub;
+    c->step_grid = (unsigned)(tiles_blocks < resident ? tiles_blocks : resident);
+    if (const char* e = getenv("MDR_GRID")) if (atoi(e) > 0) c->step_grid = (unsigned)atoi(e);
+  }
+  c->pen_blocks = (int)c->step_grid;  // one penalty partial per k_step block
   if (hipMalloc(&c->d_pen_partial, 2 * sizeof(double) * c->pen_blocks) != hipSuccess ||
       hipMalloc(&c->d_partial2, 2 * sizeof(double)) != hipSuccess)
     return cleanup(fail(MDR_ENOMEM, "penalty partials"));
@@ -253,6 +288,7 @@ int mdr_destroy(mdr_ctx* c) {
   for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
   hipFree(c->d_tables);
   hipFree(c->d_coef);
+  hipFree(c->d_flags);
   hipFree(c->d_slab);
   hipFree(c->d_pen_partial);
   hipFree(c->d_partial2);
@@ -419,7 +455,9 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
     return fail(MDR_EARG, "mdr_rollout: common penalty modes need the per-step API");
   hipStream_t st = S(stream);
-  int rc = stage_ticks(c, n, ticks, st);
+  int rc = refresh_if_dirty(c, st);
+  if (rc) return rc;
+  rc = stage_ticks(c, n, ticks, st);
   if (rc) return rc;
   if (!use_graph) {
     rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, st);
@@ -609,7 +647,9 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
   if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
     return fail(MDR_EARG, "mdr_rollout_sharded: common penalty modes need the per-step API");
   hipStream_t st = S(stream);
-  int rc = stage_ticks(c, n, ticks, st);
+  int rc = refresh_if_dirty(c, st);
+  if (rc) return rc;
+  rc = stage_ticks(c, n, ticks, st);
   if (rc) return rc;
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, 3 * c->slab_len * sizeof(unsigned long long), st));
   c->ring = 0;

@@ -32,6 +32,8 @@ struct KParams {
   const double* p_on;  // [n_cap] cap/cop
   const double* coef;  // [6][coef_stride] cached rc_coeffs (r1, r2, A3, A4, e1, e2) or null
   int64_t coef_stride;
+  const int* params_bad;  // device flag: some house's parameters are outside the fast-division range
+  int fast_tick_ok;       // host-checked: dt and the capacity table are inside that range
 };
 
 struct TickArgs {
@@ -61,7 +63,7 @@ __global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, Tick
                          unsigned long long* next_slab, unsigned long long* zero_slab,
                          double* pen_partial);
 __global__ void k_probe_stream(KParams p, double* reward);
-__global__ void k_coeffs(KParams p, double* coef);
+__global__ void k_refresh(KParams p, double* coef, int* params_bad);
 __global__ void k_div_check(const double* a, const double* b, int64_t n, unsigned long long* mismatches);
 __global__ void k_pen_reduce(const double* pen_partial, int nblk, double* partial2);
 __global__ void k_reward_finalize(KParams p, TickArgs tk, const unsigned long long* counts,

@@ -109,153 +109,174 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   __shared__ unsigned hist[MDR_MAX_CAP];
   __shared__ double s_red[2][4];
   const int tid = threadIdx.x;
-  const int64_t i0 = ((int64_t)blockIdx.x * blockDim.x + tid) * HPT;
-  bool valid[HPT];
-#pragma unroll
-  for (int h = 0; h < HPT; ++h) valid[h] = i0 + h < p.n;
-
-  // ---- all per-house loads first (one round trip)
-  uint32_t w0[HPT];
-  double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
-  RcCoef kc[HPT];
-  int cls[HPT];
-  const int64_t cs = p.coef_stride;
-  if (HPT == 2 && valid[HPT - 1]) {
-    auto ld2 = [&](const double* a) { return *reinterpret_cast<const double2*>(a + i0); };
-    const double2 vT = ld2(p.t_air), vTm = ld2(p.t_mass), vua = ld2(p.ua), vca = ld2(p.ca);
-    const double2 vhm = ld2(p.hm), vtg = ld2(p.target);
-    const uint2 vw = *reinterpret_cast<const uint2*>(p.hvac + i0);
-    const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
-    T[0] = vT.x; T[HPT - 1] = vT.y; Tm[0] = vTm.x; Tm[HPT - 1] = vTm.y;
-    ua[0] = vua.x; ua[HPT - 1] = vua.y; ca[0] = vca.x; ca[HPT - 1] = vca.y;
-    hm[0] = vhm.x; hm[HPT - 1] = vhm.y;
-    tg[0] = vtg.x; tg[HPT - 1] = vtg.y; w0[0] = vw.x; w0[HPT - 1] = vw.y;
-    cls[0] = vc & 0xFF; cls[HPT - 1] = vc >> 8;
-    if (CACHED) {
-      const double2 r1 = ld2(p.coef), r2 = ld2(p.coef + cs), A3 = ld2(p.coef + 2 * cs);
-      const double2 A4 = ld2(p.coef + 3 * cs), e1 = ld2(p.coef + 4 * cs), e2 = ld2(p.coef + 5 * cs);
-      kc[0] = RcCoef{r1.x, r2.x, A3.x, A4.x, e1.x, e2.x};
-      kc[HPT - 1] = RcCoef{r1.y, r2.y, A3.y, A4.y, e1.y, e2.y};
-    } else {
-      const double2 vcm = ld2(p.cm);
-      cm[0] = vcm.x; cm[HPT - 1] = vcm.y;
-    }
-  } else {
-#pragma unroll
-    for (int h = 0; h < HPT; ++h) {
-      const int64_t i = valid[h] ? i0 + h : 0;
-      T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i];
-      hm[h] = p.hm[i]; tg[h] = p.target[i]; w0[h] = p.hvac[i]; cls[h] = p.cap_idx[i];
-      if (CACHED) {
-        const double* c = p.coef + i;
-        kc[h] = RcCoef{c[0], c[cs], c[2 * cs], c[3 * cs], c[4 * cs], c[5 * cs]};
-      } else {
-        cm[h] = p.cm[i];
-      }
-    }
-  }
+  const int lane = tid & 63;
+  if (tid < p.n_cap) hist[tid] = 0;
   if (zero_slab && blockIdx.x == 0)
     for (int j = tid; j < kCountShards * p.n_cap; j += blockDim.x) zero_slab[j] = 0ull;
-  if (tid < p.n_cap) hist[tid] = 0;
 
   const TickArgs tk = tkp ? *tkp : tk0;
-  // per-tick signal penalty (rewards_calculator.py:183-203), uniform in the wave
+  // per-tick signal penalty (rewards_calculator.py:183-203), uniform; once per wave
   const double P = wave_power(counts, p.p_on, p.n_cap);
   const double x = (P - tk.s_prev) / (double)p.n_global;
   const double sig_term = p.alpha_sig * (x * x) / p.norm_sig;
   if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
+  __syncthreads();  // hist zeroed before any wave adds to it
 
-  // random controller bits of this tick (and the next, for the lookahead) for the whole wave
-  bool rnd[HPT], rnd1[HPT];
-  if (action_mode == MDR_ACT_RANDOM || lookahead == MDR_ACT_RANDOM) {
-    const int64_t wave0 = (((int64_t)blockIdx.x * blockDim.x) + (tid & ~63)) * HPT;
-    const WaveRandom wr(p.seed, p.goff + wave0, tk.tick);
+  const bool want_rnd = action_mode == MDR_ACT_RANDOM || lookahead == MDR_ACT_RANDOM;
+  // shared-reciprocal division only where it is provably the IEEE quotient (mdr_device.h)
+  const bool fast_ok = FAST && !*p.params_bad && p.fast_tick_ok && fabs(tk.t_od_prev) < 1048576.0 &&
+                       fabs(tk.solar) < 1099511627776.0;
+  const int64_t cs = p.coef_stride;
+  double pen_sum = 0.0, pen_max = 0.0;
+  // grid-stride over wave tiles of 64*HPT houses (the grid is sized to the resident capacity;
+  // the trip count is wave-uniform, so the cross-lane random-bit exchange stays convergent)
+  const int64_t tiles = (p.n + 64 * HPT - 1) / (64 * HPT);
+  for (int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6); tile < tiles;
+       tile += (int64_t)gridDim.x * (blockDim.x >> 6)) {
+    const int64_t i0 = tile * 64 * HPT + (int64_t)lane * HPT;
+    bool valid[HPT];
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) valid[h] = i0 + h < p.n;
+
+    // ---- all per-house loads first (one round trip)
+    uint32_t w0[HPT];
+    double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
+    RcCoef kc[HPT];
+    int cls[HPT];
+    if (HPT == 2 && valid[HPT - 1]) {
+      auto ld2 = [&](const double* a) { return *reinterpret_cast<const double2*>(a + i0); };
+      const double2 vT = ld2(p.t_air), vTm = ld2(p.t_mass), vua = ld2(p.ua), vca = ld2(p.ca);
+      const double2 vhm = ld2(p.hm), vtg = ld2(p.target);
+      const uint2 vw = *reinterpret_cast<const uint2*>(p.hvac + i0);
+      const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
+      T[0] = vT.x; T[HPT - 1] = vT.y; Tm[0] = vTm.x; Tm[HPT - 1] = vTm.y;
+      ua[0] = vua.x; ua[HPT - 1] = vua.y; ca[0] = vca.x; ca[HPT - 1] = vca.y;
+      hm[0] = vhm.x; hm[HPT - 1] = vhm.y;
+      tg[0] = vtg.x; tg[HPT - 1] = vtg.y; w0[0] = vw.x; w0[HPT - 1] = vw.y;
+      cls[0] = vc & 0xFF; cls[HPT - 1] = vc >> 8;
+      if (CACHED) {
+        const double2 r1 = ld2(p.coef), r2 = ld2(p.coef + cs), A3 = ld2(p.coef + 2 * cs);
+        const double2 A4 = ld2(p.coef + 3 * cs), e1 = ld2(p.coef + 4 * cs), e2 = ld2(p.coef + 5 * cs);
+        kc[0] = RcCoef{r1.x, r2.x, A3.x, A4.x, e1.x, e2.x};
+        kc[HPT - 1] = RcCoef{r1.y, r2.y, A3.y, A4.y, e1.y, e2.y};
+      } else {
+        const double2 vcm = ld2(p.cm);
+        cm[0] = vcm.x; cm[HPT - 1] = vcm.y;
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < HPT; ++h) {
+        const int64_t i = valid[h] ? i0 + h : 0;
+        T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i];
+        hm[h] = p.hm[i]; tg[h] = p.target[i]; w0[h] = p.hvac[i]; cls[h] = p.cap_idx[i];
+        if (CACHED) {
+          const double* c = p.coef + i;
+          kc[h] = RcCoef{c[0], c[cs], c[2 * cs], c[3 * cs], c[4 * cs], c[5 * cs]};
+        } else {
+          cm[h] = p.cm[i];
+        }
+      }
+    }
+
+    // random controller bits of this tick (and the next, for the lookahead) for the tile
+    bool rnd[HPT], rnd1[HPT];
+    if (want_rnd) {
+      const WaveRandom wr(p.seed, p.goff + tile * 64 * HPT, tk.tick);
+#pragma unroll
+      for (int h = 0; h < HPT; ++h) {
+        rnd[h] = wr.get(p.goff + i0 + h, false);
+        rnd1[h] = wr.get(p.goff + i0 + h, true);
+      }
+    } else {
+#pragma unroll
+      for (int h = 0; h < HPT; ++h) rnd[h] = rnd1[h] = false;
+    }
+
+    bool house_ok = true;
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) house_ok = house_ok && fabs(T[h]) < 1048576.0 && fabs(Tm[h]) < 1048576.0;
+    const bool tile_fast = FAST && fast_ok && __all(house_ok);
+
+    double Tn[HPT], Tmn[HPT], rw[HPT], pen[HPT];
+    uint32_t w[HPT];
+    bool on[HPT], on1[HPT];
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
-      rnd[h] = wr.get(p.goff + i0 + h, false);
-      rnd1[h] = wr.get(p.goff + i0 + h, true);
-    }
-  } else {
-#pragma unroll
-    for (int h = 0; h < HPT; ++h) rnd[h] = rnd1[h] = false;
-  }
-
-  double Tn[HPT], Tmn[HPT], rw[HPT], pen[HPT];
-  uint32_t w[HPT];
-  bool on[HPT], on1[HPT];
-#pragma unroll
-  for (int h = 0; h < HPT; ++h) {
-    const int64_t i = i0 + h;
-    const bool a = valid[h] && pick_action(action_mode, action, i, rnd[h], T[h], tg[h], p.deadband, w0[h]);
-    w[h] = hvac_fsm(w0[h], a, p.dt, p.L);
-    on[h] = hv_on(w[h]);
-    const double q = on[h] ? p.q_on[cls[h]] : 0.0;
-    if (!CACHED) kc[h] = rc_coeffs_t<FAST>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
-    rc_apply_t<FAST>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
-    pen[h] = deadband_l2(tg[h], p.deadband, Tn[h]);
-    // x / 1.0 == x exactly: the default normaliser (integer target) costs no division
-    const double tpen = p.alpha_temp * pen[h];
-    rw[h] = p.penalty_mode == MDR_PEN_INDIVIDUAL_L2
-                ? -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig_term)
-                : pen[h];  // finalised by k_reward_finalize
-    on1[h] = false;
-    if (valid[h] && lookahead) {
-      bool an;
-      if (lookahead == MDR_ACT_RANDOM) an = rnd1[h];
-      else if (lookahead == MDR_ACT_ALWAYS_ON) an = true;
-      else if (lookahead == kActBangBang) an = ctrl_bangbang(Tn[h], tg[h]);
-      else an = ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
-      on1[h] = hv_on(hvac_fsm(w[h], an, p.dt, p.L));
-    }
-  }
-
-  // ---- stores
-  if (HPT == 2 && valid[HPT - 1]) {
-    *reinterpret_cast<double2*>(p.t_air + i0) = make_double2(Tn[0], Tn[HPT - 1]);
-    *reinterpret_cast<double2*>(p.t_mass + i0) = make_double2(Tmn[0], Tmn[HPT - 1]);
-    *reinterpret_cast<uint2*>(p.hvac + i0) = make_uint2(w[0], w[HPT - 1]);
-    *reinterpret_cast<double2*>(reward + i0) = make_double2(rw[0], rw[HPT - 1]);
-  } else {
-#pragma unroll
-    for (int h = 0; h < HPT; ++h)
-      if (valid[h]) {
-        p.t_air[i0 + h] = Tn[h]; p.t_mass[i0 + h] = Tmn[h]; p.hvac[i0 + h] = w[h]; reward[i0 + h] = rw[h];
+      const int64_t i = i0 + h;
+      const bool a = valid[h] && pick_action(action_mode, action, i, rnd[h], T[h], tg[h], p.deadband, w0[h]);
+      w[h] = hvac_fsm(w0[h], a, p.dt, p.L);
+      on[h] = hv_on(w[h]);
+      const double q = on[h] ? p.q_on[cls[h]] : 0.0;
+      if (tile_fast) {
+        if (!CACHED) kc[h] = rc_coeffs_t<FAST>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+        rc_apply_t<FAST>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
+      } else {
+        if (!CACHED) kc[h] = rc_coeffs_t<false>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+        rc_apply_t<false>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
       }
-  }
-  if (ctrl != MDR_CTRL_NONE && ctrl_out) {
-#pragma unroll
-    for (int h = 0; h < HPT; ++h)
-      if (valid[h]) {
-        const bool a1 = ctrl == MDR_CTRL_BANGBANG ? ctrl_bangbang(Tn[h], tg[h])
-                                                   : ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
-        ctrl_out[i0 + h] = a1 ? 1 : 0;
+      pen[h] = deadband_l2(tg[h], p.deadband, Tn[h]);
+      // x / 1.0 == x exactly: the default normaliser (integer target) costs no division
+      const double tpen = p.alpha_temp * pen[h];
+      rw[h] = p.penalty_mode == MDR_PEN_INDIVIDUAL_L2
+                  ? -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig_term)
+                  : pen[h];  // finalised by k_reward_finalize
+      on1[h] = false;
+      if (valid[h] && lookahead) {
+        bool an;
+        if (lookahead == MDR_ACT_RANDOM) an = rnd1[h];
+        else if (lookahead == MDR_ACT_ALWAYS_ON) an = true;
+        else if (lookahead == kActBangBang) an = ctrl_bangbang(Tn[h], tg[h]);
+        else an = ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
+        on1[h] = hv_on(hvac_fsm(w[h], an, p.dt, p.L));
       }
+      if (valid[h]) { pen_sum += pen[h] / (double)p.n_global; pen_max = fmax(pen_max, pen[h]); }
+    }
+
+    // ---- stores
+    if (HPT == 2 && valid[HPT - 1]) {
+      *reinterpret_cast<double2*>(p.t_air + i0) = make_double2(Tn[0], Tn[HPT - 1]);
+      *reinterpret_cast<double2*>(p.t_mass + i0) = make_double2(Tmn[0], Tmn[HPT - 1]);
+      *reinterpret_cast<uint2*>(p.hvac + i0) = make_uint2(w[0], w[HPT - 1]);
+      *reinterpret_cast<double2*>(reward + i0) = make_double2(rw[0], rw[HPT - 1]);
+    } else {
+#pragma unroll
+      for (int h = 0; h < HPT; ++h)
+        if (valid[h]) {
+          p.t_air[i0 + h] = Tn[h]; p.t_mass[i0 + h] = Tmn[h]; p.hvac[i0 + h] = w[h]; reward[i0 + h] = rw[h];
+        }
+    }
+    if (ctrl != MDR_CTRL_NONE && ctrl_out) {
+#pragma unroll
+      for (int h = 0; h < HPT; ++h)
+        if (valid[h]) {
+          const bool a1 = ctrl == MDR_CTRL_BANGBANG ? ctrl_bangbang(Tn[h], tg[h])
+                                                     : ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
+          ctrl_out[i0 + h] = a1 ? 1 : 0;
+        }
+    }
+    if (lookahead) {
+      for (int k = 0; k < p.n_cap; ++k) {
+        unsigned c = 0;
+#pragma unroll
+        for (int h = 0; h < HPT; ++h) c += (unsigned)__popcll(__ballot(on1[h] && cls[h] == k));
+        if (lane == 0 && c) atomicAdd(&hist[k], c);
+      }
+    }
   }
 
   // ---- cluster reductions for the next launch / the common penalty modes
   if (lookahead) {
-    __syncthreads();  // hist zeroed
-    const int lane = tid & 63;
-    for (int k = 0; k < p.n_cap; ++k) {
-      unsigned c = 0;
-#pragma unroll
-      for (int h = 0; h < HPT; ++h) c += (unsigned)__popcll(__ballot(on1[h] && cls[h] == k));
-      if (lane == 0 && c) atomicAdd(&hist[k], c);
-    }
     __syncthreads();
     if (tid < p.n_cap && hist[tid])
       atomicAdd(&next_slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)hist[tid]);
   }
   if (p.penalty_mode != MDR_PEN_INDIVIDUAL_L2) {
-    double sacc = 0.0, macc = 0.0;
-#pragma unroll
-    for (int h = 0; h < HPT; ++h)
-      if (valid[h]) { sacc += pen[h] / (double)p.n_global; macc = fmax(macc, pen[h]); }
+    double sacc = pen_sum, macc = pen_max;
     for (int off = 32; off > 0; off >>= 1) {
       sacc += __shfl_xor(sacc, off);
       macc = fmax(macc, __shfl_xor(macc, off));
     }
-    if ((tid & 63) == 0) { s_red[0][tid >> 6] = sacc; s_red[1][tid >> 6] = macc; }
+    if (lane == 0) { s_red[0][tid >> 6] = sacc; s_red[1][tid >> 6] = macc; }
     __syncthreads();
     if (tid == 0) {
       double bs = 0.0, bm = 0.0;
@@ -289,14 +310,28 @@ __global__ void k_div_check(const double* __restrict__ a, const double* __restri
   if (__double_as_longlong(f) != __double_as_longlong(q)) atomicAdd(mismatches, 1ull);
 }
 
-// Param-only thermal coefficients (rc_coeffs) of every house, for the CACHED step variant.
-__global__ void __launch_bounds__(256) k_coeffs(KParams p, double* __restrict__ coef) {
+// After a parameter change: (a) flag any house whose parameters leave the range in which the
+// shared-reciprocal division is provably identical to `/` (Ua in [2^-20, 2^20], Ca/Cm/Hm in
+// [2^-10, 2^50]; the step then uses the plain operator), (b) for the CACHED variant, the
+// param-only thermal coefficients (rc_coeffs) of every house.
+__device__ __forceinline__ bool in_pow2_range(double x, int lo, int hi) {
+  const int e = (int)((__double_as_longlong(x) >> 52) & 0x7FF) - 1023;
+  return x > 0.0 && e >= lo && e < hi;
+}
+
+__global__ void __launch_bounds__(256) k_refresh(KParams p, double* __restrict__ coef, int* params_bad) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n) return;
-  const RcCoef k = rc_coeffs(p.ua[i], p.ca[i], p.cm[i], p.hm[i], (double)p.dt);
-  const int64_t cs = p.coef_stride;
-  coef[i] = k.r1; coef[i + cs] = k.r2; coef[i + 2 * cs] = k.A3;
-  coef[i + 3 * cs] = k.A4; coef[i + 4 * cs] = k.e1; coef[i + 5 * cs] = k.e2;
+  const double ua = p.ua[i], ca = p.ca[i], cm = p.cm[i], hm = p.hm[i];
+  const bool ok = in_pow2_range(ua, -20, 20) && in_pow2_range(ca, -10, 50) &&
+                  in_pow2_range(cm, -10, 50) && in_pow2_range(hm, -10, 50);
+  if (!ok) atomicOr(params_bad, 1);
+  if (coef) {
+    const RcCoef k = rc_coeffs(ua, ca, cm, hm, (double)p.dt);
+    const int64_t cs = p.coef_stride;
+    coef[i] = k.r1; coef[i + cs] = k.r2; coef[i + 2 * cs] = k.A3;
+    coef[i + 3 * cs] = k.A4; coef[i + 4 * cs] = k.e1; coef[i + 5 * cs] = k.e2;
+  }
 }
 
 // Memory-floor probe for k_step's access pattern: the same loads and stores, trivial arithmetic

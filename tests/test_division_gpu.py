@@ -55,3 +55,30 @@ def test_step_variants_bit_identical(variant):
     s0, s1 = envs[0].shard.host_state(), envs[1].shard.host_state()
     for k in s0:
         np.testing.assert_array_equal(s0[k], s1[k])
+
+
+def test_fast_division_guard_fallback():
+    """Out-of-range parameters (Ua = 1e-9 < 2^-20) or temperatures route the tile to the plain
+    `/` operator: results stay bit-identical to the reference-order kernel."""
+    import torch
+
+    import golden_util as gu
+    from mdr_amd.environment import Environment
+
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": 5000,
+                                     "power_grid_prop.signal_properties.mode": "flat"})
+    envs = []
+    for fast in ("0", "1"):
+        os.environ["MDR_FASTDIV"] = fast
+        e = Environment(props, rng=random.Random(2), population="synthetic", seed=3)
+        e.shard.ua[17] = 1e-9
+        e.shard.t_air[4000] = 3.0e6
+        e.shard.params_changed()
+        envs.append(e)
+    os.environ.pop("MDR_FASTDIV")
+    for t in range(10):
+        rs = [e.step_tensor(None, action_mode="random", lookahead="random").clone() for e in envs]
+        assert torch.equal(rs[0], rs[1])
+    s0, s1 = envs[0].shard.host_state(), envs[1].shard.host_state()
+    np.testing.assert_array_equal(s0["T"], s1["T"])
+    np.testing.assert_array_equal(s0["Tm"], s1["Tm"])

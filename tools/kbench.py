@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--houses", default="1048576,4194304,16777216")
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="hpt2,fast2,coef2,fcoef2,probe")
+    ap.add_argument("--variants", default="hpt2,fast2,fast2g2,fast2g4,fast1,fcoef2,probe")
     a = ap.parse_args()
     import torch
 
@@ -33,6 +33,7 @@ def main():
             os.environ["MDR_HPT"] = "1" if v.endswith("1") else "2"
             os.environ["MDR_VARIANT"] = "coef" if "coef" in v else "raw"
             os.environ["MDR_FASTDIV"] = "1" if v.startswith("f") else "0"
+            os.environ["MDR_GRID_OVERSUB"] = v.split("g")[-1] if "g" in v[4:] else "1"
             envs[v] = Environment(env_props(n), device="cuda:0", rng=random.Random(1),
                                   population="synthetic", seed=5)
             rews = torch.empty(n, dtype=torch.float64, device="cuda:0")
