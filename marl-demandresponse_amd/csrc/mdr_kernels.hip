@@ -114,13 +114,12 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   if (zero_slab && blockIdx.x == 0)
     for (int j = tid; j < kCountShards * p.n_cap; j += blockDim.x) zero_slab[j] = 0ull;
 
+  __syncthreads();  // hist zeroed before any wave adds to it (no load is in flight yet)
   const TickArgs tk = tkp ? *tkp : tk0;
-  // per-tick signal penalty (rewards_calculator.py:183-203), uniform; once per wave
-  const double P = wave_power(counts, p.p_on, p.n_cap);
-  const double x = (P - tk.s_prev) / (double)p.n_global;
-  const double sig_term = p.alpha_sig * (x * x) / p.norm_sig;
-  if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
-  __syncthreads();  // hist zeroed before any wave adds to it
+  // per-tick signal penalty (rewards_calculator.py:183-203): uniform, computed once per wave in
+  // its first tile, after that tile's loads are issued (the count loads overlap them)
+  double sig_term = 0.0;
+  bool have_sig = false;
 
   const bool want_rnd = action_mode == MDR_ACT_RANDOM || lookahead == MDR_ACT_RANDOM;
   // shared-reciprocal division only where it is provably the IEEE quotient (mdr_device.h)
@@ -176,6 +175,14 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
           cm[h] = p.cm[i];
         }
       }
+    }
+
+    if (!have_sig) {
+      const double P = wave_power(counts, p.p_on, p.n_cap);
+      const double x = (P - tk.s_prev) / (double)p.n_global;
+      sig_term = p.alpha_sig * (x * x) / p.norm_sig;
+      have_sig = true;
+      if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
     }
 
     // random controller bits of this tick (and the next, for the lookahead) for the tile
@@ -350,9 +357,11 @@ __global__ void __launch_bounds__(256) k_probe_stream(KParams p, double* __restr
   const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
   const double s0 = vua.x + vca.x + vcm.x + vhm.x + vtg.x + (double)(vc & 0xFF);
   const double s1 = vua.y + vca.y + vcm.y + vhm.y + vtg.y + (double)(vc >> 8);
-  *reinterpret_cast<double2*>(p.t_air + i0) = make_double2(vT.x * 1.0, vT.y * 1.0);
-  *reinterpret_cast<double2*>(p.t_mass + i0) = make_double2(vTm.x * 1.0, vTm.y * 1.0);
-  *reinterpret_cast<uint2*>(p.hvac + i0) = vw;
+  // values depend on every load (0 * s is not foldable: s may be inf/nan), so neither the loads
+  // nor the write-backs can be elided
+  *reinterpret_cast<double2*>(p.t_air + i0) = make_double2(vT.x + 0.0 * s0, vT.y + 0.0 * s1);
+  *reinterpret_cast<double2*>(p.t_mass + i0) = make_double2(vTm.x + 0.0 * s0, vTm.y + 0.0 * s1);
+  *reinterpret_cast<uint2*>(p.hvac + i0) = make_uint2(vw.x ^ (vc & 0x100000u), vw.y);
   *reinterpret_cast<double2*>(reward + i0) = make_double2(s0, s1);
 }
 
