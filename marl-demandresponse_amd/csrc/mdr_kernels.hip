@@ -97,55 +97,6 @@ __device__ __forceinline__ bool pick_action(int mode, const uint8_t* action, int
   return ctrl_deadband(T, tgt, deadband, hv_on(w0));
 }
 
-// Per-tile registers of the step kernel: the inputs of HPT houses of one lane.
-template <int HPT>
-struct TileIn {
-  uint32_t w0[HPT];
-  double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
-  RcCoef kc[HPT];
-  int cls[HPT];
-};
-
-// Issue every load of a tile (16-B-per-lane vector loads when the lane's HPT houses exist).
-template <int HPT, bool CACHED>
-__device__ __forceinline__ void load_tile(const KParams& p, int64_t i0, TileIn<HPT>& r) {
-  const int64_t cs = p.coef_stride;
-  if (HPT == 2 && i0 + HPT - 1 < p.n) {
-    auto ld2 = [&](const double* a) { return *reinterpret_cast<const double2*>(a + i0); };
-    const double2 vT = ld2(p.t_air), vTm = ld2(p.t_mass), vua = ld2(p.ua), vca = ld2(p.ca);
-    const double2 vhm = ld2(p.hm), vtg = ld2(p.target);
-    const uint2 vw = *reinterpret_cast<const uint2*>(p.hvac + i0);
-    const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
-    r.T[0] = vT.x; r.T[HPT - 1] = vT.y; r.Tm[0] = vTm.x; r.Tm[HPT - 1] = vTm.y;
-    r.ua[0] = vua.x; r.ua[HPT - 1] = vua.y; r.ca[0] = vca.x; r.ca[HPT - 1] = vca.y;
-    r.hm[0] = vhm.x; r.hm[HPT - 1] = vhm.y;
-    r.tg[0] = vtg.x; r.tg[HPT - 1] = vtg.y; r.w0[0] = vw.x; r.w0[HPT - 1] = vw.y;
-    r.cls[0] = vc & 0xFF; r.cls[HPT - 1] = vc >> 8;
-    if (CACHED) {
-      const double2 r1 = ld2(p.coef), r2 = ld2(p.coef + cs), A3 = ld2(p.coef + 2 * cs);
-      const double2 A4 = ld2(p.coef + 3 * cs), e1 = ld2(p.coef + 4 * cs), e2 = ld2(p.coef + 5 * cs);
-      r.kc[0] = RcCoef{r1.x, r2.x, A3.x, A4.x, e1.x, e2.x};
-      r.kc[HPT - 1] = RcCoef{r1.y, r2.y, A3.y, A4.y, e1.y, e2.y};
-    } else {
-      const double2 vcm = ld2(p.cm);
-      r.cm[0] = vcm.x; r.cm[HPT - 1] = vcm.y;
-    }
-  } else {
-#pragma unroll
-    for (int h = 0; h < HPT; ++h) {
-      const int64_t i = i0 + h < p.n ? i0 + h : 0;
-      r.T[h] = p.t_air[i]; r.Tm[h] = p.t_mass[i]; r.ua[h] = p.ua[i]; r.ca[h] = p.ca[i];
-      r.hm[h] = p.hm[i]; r.tg[h] = p.target[i]; r.w0[h] = p.hvac[i]; r.cls[h] = p.cap_idx[i];
-      if (CACHED) {
-        const double* c = p.coef + i;
-        r.kc[h] = RcCoef{c[0], c[cs], c[2 * cs], c[3 * cs], c[4 * cs], c[5 * cs]};
-      } else {
-        r.cm[h] = p.cm[i];
-      }
-    }
-  }
-}
-
 template <int HPT, bool CACHED, bool FAST>
 __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __restrict__ action,
                                                 int action_mode, TickArgs tk0, const TickArgs* tkp,
@@ -174,30 +125,57 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   // shared-reciprocal division only where it is provably the IEEE quotient (mdr_device.h)
   const bool fast_ok = FAST && !*p.params_bad && p.fast_tick_ok && fabs(tk.t_od_prev) < 1048576.0 &&
                        fabs(tk.solar) < 1099511627776.0;
+  const int64_t cs = p.coef_stride;
   double pen_sum = 0.0, pen_max = 0.0;
   // grid-stride over wave tiles of 64*HPT houses (the grid is sized to the resident capacity;
   // the trip count is wave-uniform, so the cross-lane random-bit exchange stays convergent)
   const int64_t tiles = (p.n + 64 * HPT - 1) / (64 * HPT);
-  const int64_t first = (int64_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6);
-  TileIn<HPT> cur;
-  if (first < tiles) load_tile<HPT, CACHED>(p, first * 64 * HPT + (int64_t)lane * HPT, cur);
-  for (int64_t tile = first; tile < tiles; tile += (int64_t)gridDim.x * (blockDim.x >> 6)) {
+  for (int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6); tile < tiles;
+       tile += (int64_t)gridDim.x * (blockDim.x >> 6)) {
     const int64_t i0 = tile * 64 * HPT + (int64_t)lane * HPT;
     bool valid[HPT];
 #pragma unroll
     for (int h = 0; h < HPT; ++h) valid[h] = i0 + h < p.n;
 
-    // the tile's inputs were loaded one iteration ahead (software pipelining): issue the NEXT
-    // tile's loads now so they are in flight while this tile computes
-    const TileIn<HPT> in = cur;
-    const int64_t ntile = tile + (int64_t)gridDim.x * (blockDim.x >> 6);
-    if (ntile < tiles) load_tile<HPT, CACHED>(p, ntile * 64 * HPT + (int64_t)lane * HPT, cur);
-    const uint32_t* w0 = in.w0;
-    const double *T = in.T, *Tm = in.Tm, *ua = in.ua, *ca = in.ca, *cm = in.cm, *hm = in.hm, *tg = in.tg;
-    const int* cls = in.cls;
+    // ---- all per-house loads first (one round trip)
+    uint32_t w0[HPT];
+    double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
     RcCoef kc[HPT];
+    int cls[HPT];
+    if (HPT == 2 && valid[HPT - 1]) {
+      auto ld2 = [&](const double* a) { return *reinterpret_cast<const double2*>(a + i0); };
+      const double2 vT = ld2(p.t_air), vTm = ld2(p.t_mass), vua = ld2(p.ua), vca = ld2(p.ca);
+      const double2 vhm = ld2(p.hm), vtg = ld2(p.target);
+      const uint2 vw = *reinterpret_cast<const uint2*>(p.hvac + i0);
+      const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
+      T[0] = vT.x; T[HPT - 1] = vT.y; Tm[0] = vTm.x; Tm[HPT - 1] = vTm.y;
+      ua[0] = vua.x; ua[HPT - 1] = vua.y; ca[0] = vca.x; ca[HPT - 1] = vca.y;
+      hm[0] = vhm.x; hm[HPT - 1] = vhm.y;
+      tg[0] = vtg.x; tg[HPT - 1] = vtg.y; w0[0] = vw.x; w0[HPT - 1] = vw.y;
+      cls[0] = vc & 0xFF; cls[HPT - 1] = vc >> 8;
+      if (CACHED) {
+        const double2 r1 = ld2(p.coef), r2 = ld2(p.coef + cs), A3 = ld2(p.coef + 2 * cs);
+        const double2 A4 = ld2(p.coef + 3 * cs), e1 = ld2(p.coef + 4 * cs), e2 = ld2(p.coef + 5 * cs);
+        kc[0] = RcCoef{r1.x, r2.x, A3.x, A4.x, e1.x, e2.x};
+        kc[HPT - 1] = RcCoef{r1.y, r2.y, A3.y, A4.y, e1.y, e2.y};
+      } else {
+        const double2 vcm = ld2(p.cm);
+        cm[0] = vcm.x; cm[HPT - 1] = vcm.y;
+      }
+    } else {
 #pragma unroll
-    for (int h = 0; h < HPT; ++h) kc[h] = in.kc[h];
+      for (int h = 0; h < HPT; ++h) {
+        const int64_t i = valid[h] ? i0 + h : 0;
+        T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i];
+        hm[h] = p.hm[i]; tg[h] = p.target[i]; w0[h] = p.hvac[i]; cls[h] = p.cap_idx[i];
+        if (CACHED) {
+          const double* c = p.coef + i;
+          kc[h] = RcCoef{c[0], c[cs], c[2 * cs], c[3 * cs], c[4 * cs], c[5 * cs]};
+        } else {
+          cm[h] = p.cm[i];
+        }
+      }
+    }
 
     if (!have_sig) {
       const double P = wave_power(counts, p.p_on, p.n_cap);
