@@ -77,7 +77,6 @@ struct mdr_ctx {
   double* d_pen_partial = nullptr;       // 2 per block of k_step
   double* d_partial2 = nullptr;
   int pen_blocks = 0;
-  unsigned step_grid = 0;                // k_step grid: min(tiles, resident blocks x oversub)
   int hpt = 2;                           // houses per thread of k_step (MDR_HPT env overrides)
   bool cached = false;                   // cached param-only thermal coefficients (MDR_VARIANT=coef)
   bool fastdiv = true;                   // shared-reciprocal exact division (MDR_FASTDIV=0 disables)
@@ -151,18 +150,25 @@ int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const 
   if (int rc = refresh_if_dirty(c, st)) return rc;
   KParams kp = c->kp;
   kp.coef = c->cached ? c->d_coef : nullptr;
-#define MDR_LAUNCH_STEP(H, C, F)                                                                      \
-  hipLaunchKernelGGL((k_step_t<H, C, F>), dim3(c->step_grid), dim3(256), 0, st, kp, action,               \
-                     mode, tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer,              \
+#define MDR_LAUNCH_STEP(H, C, F, A, LA)                                                               \
+  hipLaunchKernelGGL((k_step_t<H, C, F, A, LA>), dim3(blocks(kp.n, 256 * H)), dim3(256), 0, st, kp,       \
+                     action, mode, tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer,      \
                      c->d_pen_partial)
-  if (c->hpt == 2) {
-    if (c->fastdiv) {
-      if (c->cached) MDR_LAUNCH_STEP(2, true, true); else MDR_LAUNCH_STEP(2, false, true);
+  const bool hot_random = mode == MDR_ACT_RANDOM && lookahead == MDR_ACT_RANDOM;
+  const bool hot_buffer = mode == MDR_ACT_BUFFER && lookahead == 0;
+  if (c->hpt == 2 && c->fastdiv) {
+    if (c->cached) {
+      if (hot_random) MDR_LAUNCH_STEP(2, true, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
+      else MDR_LAUNCH_STEP(2, true, true, -1, -1);
     } else {
-      if (c->cached) MDR_LAUNCH_STEP(2, true, false); else MDR_LAUNCH_STEP(2, false, false);
+      if (hot_random) MDR_LAUNCH_STEP(2, false, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
+      else if (hot_buffer) MDR_LAUNCH_STEP(2, false, true, MDR_ACT_BUFFER, 0);
+      else MDR_LAUNCH_STEP(2, false, true, -1, -1);
     }
+  } else if (c->hpt == 2) {
+    if (c->cached) MDR_LAUNCH_STEP(2, true, false, -1, -1); else MDR_LAUNCH_STEP(2, false, false, -1, -1);
   } else {
-    if (c->cached) MDR_LAUNCH_STEP(1, true, false); else MDR_LAUNCH_STEP(1, false, false);
+    MDR_LAUNCH_STEP(1, false, false, -1, -1);
   }
 #undef MDR_LAUNCH_STEP
   LAUNCH_CHECK("k_step");
@@ -194,7 +200,8 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   if (cfg->n_local < 1 || cfg->n_global < cfg->n_local || cfg->global_offset < 0 ||
       cfg->global_offset + cfg->n_local > cfg->n_global)
     return fail(MDR_EARG, "mdr_create: bad shard geometry");
-  if (cfg->n_local > (int64_t)INT32_MAX) return fail(MDR_EARG, "mdr_create: n_local exceeds int32 (greedy indices)");
+  if (cfg->n_local >= ((int64_t)1 << 29))
+    return fail(MDR_EARG, "mdr_create: n_local must be < 2^29 (32-bit byte offsets); shard across GPUs");
   if (cfg->n_cap < 1 || cfg->n_cap > MDR_MAX_CAP) return fail(MDR_EARG, "mdr_create: n_cap out of range");
   if (cfg->dt < 0) return fail(MDR_EARG, "mdr_create: negative dt");
   if (cfg->penalty_mode < 0 || cfg->penalty_mode > 3) return fail(MDR_EARG, "mdr_create: bad penalty mode");
@@ -252,24 +259,7 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
     if (hipMalloc(&c->d_coef, 6 * sizeof(double) * cfg->n_local) != hipSuccess)
       return cleanup(fail(MDR_ENOMEM, "coefficients"));
   }
-  {
-    // resident-grid sizing for the grid-stride step kernel
-    const void* fn = c->hpt == 2 ? (c->cached ? (c->fastdiv ? (const void*)k_step_t<2, true, true> : (const void*)k_step_t<2, true, false>)
-                                              : (c->fastdiv ? (const void*)k_step_t<2, false, true> : (const void*)k_step_t<2, false, false>))
-                                 : (c->cached ? (const void*)k_step_t<1, true, false> : (const void*)k_step_t<1, false, false>);
-    int per_cu = 0, cus = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, 256, 0) != hipSuccess || per_cu < 1) per_cu = 1;
-    hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, cfg->device) == hipSuccess) cus = prop.multiProcessorCount;
-    if (cus < 1) cus = 256;
-    int oversub = 1;
-    if (const char* e = getenv("MDR_GRID_OVERSUB")) oversub = atoi(e) > 0 ? atoi(e) : 1;
-    const int64_t tiles_blocks = blocks(cfg->n_local, 256 * c->hpt);
-    const int64_t resident = (int64_t)per_cu * cus * oversub;
-    c->step_grid = (unsigned)(tiles_blocks < resident ? tiles_blocks : resident);
-    if (const char* e = getenv("MDR_GRID")) if (atoi(e) > 0) c->step_grid = (unsigned)atoi(e);
-  }
-  c->pen_blocks = (int)c->step_grid;  // one penalty partial per k_step block
+  c->pen_blocks = (int)blocks(cfg->n_local, 256 * c->hpt);  // = k_step grid
   if (hipMalloc(&c->d_pen_partial, 2 * sizeof(double) * c->pen_blocks) != hipSuccess ||
       hipMalloc(&c->d_partial2, 2 * sizeof(double)) != hipSuccess)
     return cleanup(fail(MDR_ENOMEM, "penalty partials"));

@@ -56,7 +56,7 @@ struct ObsArgs {
 
 __global__ void k_power_counts(KParams p, const uint8_t* action, int action_mode, uint64_t tick,
                                const TickArgs* tkp, unsigned long long* slab);
-template <int HPT, bool CACHED, bool FAST>
+template <int HPT, bool CACHED, bool FAST, int ACT, int LA>
 __global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, TickArgs tk,
                          const TickArgs* tkp, const unsigned long long* counts, double* reward,
                          int ctrl, uint8_t* ctrl_out, double* p_out, int lookahead,

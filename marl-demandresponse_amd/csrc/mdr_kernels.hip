@@ -88,7 +88,7 @@ __device__ __forceinline__ double wave_power(const unsigned long long* __restric
   return P;
 }
 
-__device__ __forceinline__ bool pick_action(int mode, const uint8_t* action, int64_t i, bool rnd,
+__device__ __forceinline__ bool pick_action(int mode, const uint8_t* action, uint32_t i, bool rnd,
                                             double T, double tgt, double deadband, uint32_t w0) {
   if (mode == MDR_ACT_BUFFER) return action[i] != 0;
   if (mode == MDR_ACT_RANDOM) return rnd;
@@ -97,15 +97,19 @@ __device__ __forceinline__ bool pick_action(int mode, const uint8_t* action, int
   return ctrl_deadband(T, tgt, deadband, hv_on(w0));
 }
 
-template <int HPT, bool CACHED, bool FAST>
+template <int HPT, bool CACHED, bool FAST, int ACT, int LA>
 __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __restrict__ action,
-                                                int action_mode, TickArgs tk0, const TickArgs* tkp,
+                                                int action_mode_rt, TickArgs tk0, const TickArgs* tkp,
                                                 const unsigned long long* __restrict__ counts,
                                                 double* __restrict__ reward, int ctrl,
                                                 uint8_t* __restrict__ ctrl_out, double* p_out,
-                                                int lookahead, unsigned long long* next_slab,
+                                                int lookahead_rt, unsigned long long* next_slab,
                                                 unsigned long long* zero_slab,
                                                 double* __restrict__ pen_partial) {
+  // ACT / LA >= 0: action source / lookahead fixed at compile time (the hot configurations);
+  // -1: taken from the runtime arguments
+  const int action_mode = ACT >= 0 ? ACT : action_mode_rt;
+  const int lookahead = LA >= 0 ? LA : lookahead_rt;
   __shared__ unsigned hist[MDR_MAX_CAP];
   __shared__ double s_red[2][4];
   const int tid = threadIdx.x;
@@ -114,171 +118,160 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   if (zero_slab && blockIdx.x == 0)
     for (int j = tid; j < kCountShards * p.n_cap; j += blockDim.x) zero_slab[j] = 0ull;
 
-  __syncthreads();  // hist zeroed before any wave adds to it (no load is in flight yet)
-  const TickArgs tk = tkp ? *tkp : tk0;
-  // per-tick signal penalty (rewards_calculator.py:183-203): uniform, computed once per wave in
-  // its first tile, after that tile's loads are issued (the count loads overlap them)
-  double sig_term = 0.0;
-  bool have_sig = false;
-
-  const bool want_rnd = action_mode == MDR_ACT_RANDOM || lookahead == MDR_ACT_RANDOM;
-  // shared-reciprocal division only where it is provably the IEEE quotient (mdr_device.h)
-  const bool fast_ok = FAST && !*p.params_bad && p.fast_tick_ok && fabs(tk.t_od_prev) < 1048576.0 &&
-                       fabs(tk.solar) < 1099511627776.0;
-  const int64_t cs = p.coef_stride;
-  double pen_sum = 0.0, pen_max = 0.0;
-  // grid-stride over wave tiles of 64*HPT houses (the grid is sized to the resident capacity;
-  // the trip count is wave-uniform, so the cross-lane random-bit exchange stays convergent)
-  const int64_t tiles = (p.n + 64 * HPT - 1) / (64 * HPT);
-  for (int64_t tile = (int64_t)blockIdx.x * (blockDim.x >> 6) + (tid >> 6); tile < tiles;
-       tile += (int64_t)gridDim.x * (blockDim.x >> 6)) {
-    const int64_t i0 = tile * 64 * HPT + (int64_t)lane * HPT;
-    bool valid[HPT];
+  // one wave tile of 64*HPT consecutive houses per wave (no grid-stride loop: straight-line code
+  // keeps the kernel-argument SGPRs short-lived); 32-bit element indices (n_local < 2^29) so
+  // every access is an SGPR base + 32-bit VGPR offset
+  const uint32_t tile = blockIdx.x * (blockDim.x >> 6) + (tid >> 6);
+  const uint32_t n = (uint32_t)p.n;
+  const uint32_t i0 = tile * (64u * HPT) + (uint32_t)lane * HPT;
+  bool valid[HPT];
 #pragma unroll
-    for (int h = 0; h < HPT; ++h) valid[h] = i0 + h < p.n;
+  for (int h = 0; h < HPT; ++h) valid[h] = i0 + h < n;
 
-    // ---- all per-house loads first (one round trip)
-    uint32_t w0[HPT];
-    double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
-    RcCoef kc[HPT];
-    int cls[HPT];
-    if (HPT == 2 && valid[HPT - 1]) {
-      auto ld2 = [&](const double* a) { return *reinterpret_cast<const double2*>(a + i0); };
-      const double2 vT = ld2(p.t_air), vTm = ld2(p.t_mass), vua = ld2(p.ua), vca = ld2(p.ca);
-      const double2 vhm = ld2(p.hm), vtg = ld2(p.target);
-      const uint2 vw = *reinterpret_cast<const uint2*>(p.hvac + i0);
-      const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
-      T[0] = vT.x; T[HPT - 1] = vT.y; Tm[0] = vTm.x; Tm[HPT - 1] = vTm.y;
-      ua[0] = vua.x; ua[HPT - 1] = vua.y; ca[0] = vca.x; ca[HPT - 1] = vca.y;
-      hm[0] = vhm.x; hm[HPT - 1] = vhm.y;
-      tg[0] = vtg.x; tg[HPT - 1] = vtg.y; w0[0] = vw.x; w0[HPT - 1] = vw.y;
-      cls[0] = vc & 0xFF; cls[HPT - 1] = vc >> 8;
-      if (CACHED) {
-        const double2 r1 = ld2(p.coef), r2 = ld2(p.coef + cs), A3 = ld2(p.coef + 2 * cs);
-        const double2 A4 = ld2(p.coef + 3 * cs), e1 = ld2(p.coef + 4 * cs), e2 = ld2(p.coef + 5 * cs);
-        kc[0] = RcCoef{r1.x, r2.x, A3.x, A4.x, e1.x, e2.x};
-        kc[HPT - 1] = RcCoef{r1.y, r2.y, A3.y, A4.y, e1.y, e2.y};
-      } else {
-        const double2 vcm = ld2(p.cm);
-        cm[0] = vcm.x; cm[HPT - 1] = vcm.y;
-      }
+  // ---- all per-house loads first (one round trip)
+  uint32_t w0[HPT];
+  double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
+  RcCoef kc[HPT];
+  int cls[HPT];
+  const uint32_t cs = (uint32_t)p.coef_stride;
+  if (HPT == 2 && valid[HPT - 1]) {
+    auto ld2 = [&](const double* a) { return *reinterpret_cast<const double2*>(a + i0); };
+    const double2 vT = ld2(p.t_air), vTm = ld2(p.t_mass), vua = ld2(p.ua), vca = ld2(p.ca);
+    const double2 vhm = ld2(p.hm), vtg = ld2(p.target);
+    const uint2 vw = *reinterpret_cast<const uint2*>(p.hvac + i0);
+    const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
+    T[0] = vT.x; T[HPT - 1] = vT.y; Tm[0] = vTm.x; Tm[HPT - 1] = vTm.y;
+    ua[0] = vua.x; ua[HPT - 1] = vua.y; ca[0] = vca.x; ca[HPT - 1] = vca.y;
+    hm[0] = vhm.x; hm[HPT - 1] = vhm.y;
+    tg[0] = vtg.x; tg[HPT - 1] = vtg.y; w0[0] = vw.x; w0[HPT - 1] = vw.y;
+    cls[0] = vc & 0xFF; cls[HPT - 1] = vc >> 8;
+    if (CACHED) {
+      const double2 r1 = ld2(p.coef), r2 = ld2(p.coef + cs), A3 = ld2(p.coef + 2 * cs);
+      const double2 A4 = ld2(p.coef + 3 * cs), e1 = ld2(p.coef + 4 * cs), e2 = ld2(p.coef + 5 * cs);
+      kc[0] = RcCoef{r1.x, r2.x, A3.x, A4.x, e1.x, e2.x};
+      kc[HPT - 1] = RcCoef{r1.y, r2.y, A3.y, A4.y, e1.y, e2.y};
     } else {
-#pragma unroll
-      for (int h = 0; h < HPT; ++h) {
-        const int64_t i = valid[h] ? i0 + h : 0;
-        T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i];
-        hm[h] = p.hm[i]; tg[h] = p.target[i]; w0[h] = p.hvac[i]; cls[h] = p.cap_idx[i];
-        if (CACHED) {
-          const double* c = p.coef + i;
-          kc[h] = RcCoef{c[0], c[cs], c[2 * cs], c[3 * cs], c[4 * cs], c[5 * cs]};
-        } else {
-          cm[h] = p.cm[i];
-        }
-      }
+      const double2 vcm = ld2(p.cm);
+      cm[0] = vcm.x; cm[HPT - 1] = vcm.y;
     }
-
-    if (!have_sig) {
-      const double P = wave_power(counts, p.p_on, p.n_cap);
-      const double x = (P - tk.s_prev) / (double)p.n_global;
-      sig_term = p.alpha_sig * (x * x) / p.norm_sig;
-      have_sig = true;
-      if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
-    }
-
-    // random controller bits of this tick (and the next, for the lookahead) for the tile
-    bool rnd[HPT], rnd1[HPT];
-    if (want_rnd) {
-      const WaveRandom wr(p.seed, p.goff + tile * 64 * HPT, tk.tick);
-#pragma unroll
-      for (int h = 0; h < HPT; ++h) {
-        rnd[h] = wr.get(p.goff + i0 + h, false);
-        rnd1[h] = wr.get(p.goff + i0 + h, true);
-      }
-    } else {
-#pragma unroll
-      for (int h = 0; h < HPT; ++h) rnd[h] = rnd1[h] = false;
-    }
-
-    bool house_ok = true;
-#pragma unroll
-    for (int h = 0; h < HPT; ++h) house_ok = house_ok && fabs(T[h]) < 1048576.0 && fabs(Tm[h]) < 1048576.0;
-    const bool tile_fast = FAST && fast_ok && __all(house_ok);
-
-    double Tn[HPT], Tmn[HPT], rw[HPT], pen[HPT];
-    uint32_t w[HPT];
-    bool on[HPT], on1[HPT];
+  } else {
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
-      const int64_t i = i0 + h;
-      const bool a = valid[h] && pick_action(action_mode, action, i, rnd[h], T[h], tg[h], p.deadband, w0[h]);
-      w[h] = hvac_fsm(w0[h], a, p.dt, p.L);
-      on[h] = hv_on(w[h]);
-      const double q = on[h] ? p.q_on[cls[h]] : 0.0;
-      if (tile_fast) {
-        if (!CACHED) kc[h] = rc_coeffs_t<FAST>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
-        rc_apply_t<FAST>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
+      const uint32_t i = valid[h] ? i0 + h : 0u;
+      T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i];
+      hm[h] = p.hm[i]; tg[h] = p.target[i]; w0[h] = p.hvac[i]; cls[h] = p.cap_idx[i];
+      if (CACHED) {
+        const double* c = p.coef + i;
+        kc[h] = RcCoef{c[0], c[cs], c[2 * cs], c[3 * cs], c[4 * cs], c[5 * cs]};
       } else {
-        if (!CACHED) kc[h] = rc_coeffs_t<false>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
-        rc_apply_t<false>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
+        cm[h] = p.cm[i];
       }
-      pen[h] = deadband_l2(tg[h], p.deadband, Tn[h]);
-      // x / 1.0 == x exactly: the default normaliser (integer target) costs no division
-      const double tpen = p.alpha_temp * pen[h];
-      rw[h] = p.penalty_mode == MDR_PEN_INDIVIDUAL_L2
-                  ? -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig_term)
-                  : pen[h];  // finalised by k_reward_finalize
-      on1[h] = false;
-      if (valid[h] && lookahead) {
-        bool an;
-        if (lookahead == MDR_ACT_RANDOM) an = rnd1[h];
-        else if (lookahead == MDR_ACT_ALWAYS_ON) an = true;
-        else if (lookahead == kActBangBang) an = ctrl_bangbang(Tn[h], tg[h]);
-        else an = ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
-        on1[h] = hv_on(hvac_fsm(w[h], an, p.dt, p.L));
-      }
-      if (valid[h]) { pen_sum += pen[h] / (double)p.n_global; pen_max = fmax(pen_max, pen[h]); }
     }
+  }
+  __syncthreads();  // hist zeroed (the loads above stay in flight across the barrier)
 
-    // ---- stores
-    if (HPT == 2 && valid[HPT - 1]) {
-      *reinterpret_cast<double2*>(p.t_air + i0) = make_double2(Tn[0], Tn[HPT - 1]);
-      *reinterpret_cast<double2*>(p.t_mass + i0) = make_double2(Tmn[0], Tmn[HPT - 1]);
-      *reinterpret_cast<uint2*>(p.hvac + i0) = make_uint2(w[0], w[HPT - 1]);
-      *reinterpret_cast<double2*>(reward + i0) = make_double2(rw[0], rw[HPT - 1]);
+  const TickArgs tk = tkp ? *tkp : tk0;
+  // per-tick signal penalty (rewards_calculator.py:183-203), uniform in the wave
+  const double P = wave_power(counts, p.p_on, p.n_cap);
+  const double x = (P - tk.s_prev) / (double)p.n_global;
+  const double sig_term = p.alpha_sig * (x * x) / p.norm_sig;
+  if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
+
+  // random controller bits of this tick (and the next, for the lookahead) for the whole wave
+  bool rnd[HPT], rnd1[HPT];
+  if (action_mode == MDR_ACT_RANDOM || lookahead == MDR_ACT_RANDOM) {
+    const WaveRandom wr(p.seed, p.goff + (uint64_t)tile * (64u * HPT), tk.tick);
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) {
+      rnd[h] = wr.get(p.goff + i0 + h, false);
+      rnd1[h] = wr.get(p.goff + i0 + h, true);
+    }
+  } else {
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) rnd[h] = rnd1[h] = false;
+  }
+
+  // shared-reciprocal division only where it is provably the IEEE quotient (mdr_device.h)
+  bool house_ok = true;
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) house_ok = house_ok && fabs(T[h]) < 1048576.0 && fabs(Tm[h]) < 1048576.0;
+  const bool tile_fast = FAST && !*p.params_bad && p.fast_tick_ok && fabs(tk.t_od_prev) < 1048576.0 &&
+                         fabs(tk.solar) < 1099511627776.0 && __all(house_ok);
+
+  double Tn[HPT], Tmn[HPT], rw[HPT], pen[HPT];
+  uint32_t w[HPT];
+  bool on[HPT], on1[HPT];
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) {
+    const uint32_t i = i0 + h;
+    const bool a = valid[h] && pick_action(action_mode, action, i, rnd[h], T[h], tg[h], p.deadband, w0[h]);
+    w[h] = hvac_fsm(w0[h], a, p.dt, p.L);
+    on[h] = hv_on(w[h]);
+    const double q = on[h] ? p.q_on[cls[h]] : 0.0;
+    if (tile_fast) {
+      if (!CACHED) kc[h] = rc_coeffs_t<FAST>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+      rc_apply_t<FAST>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
     } else {
-#pragma unroll
-      for (int h = 0; h < HPT; ++h)
-        if (valid[h]) {
-          p.t_air[i0 + h] = Tn[h]; p.t_mass[i0 + h] = Tmn[h]; p.hvac[i0 + h] = w[h]; reward[i0 + h] = rw[h];
-        }
+      if (!CACHED) kc[h] = rc_coeffs_t<false>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+      rc_apply_t<false>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
     }
-    if (ctrl != MDR_CTRL_NONE && ctrl_out) {
-#pragma unroll
-      for (int h = 0; h < HPT; ++h)
-        if (valid[h]) {
-          const bool a1 = ctrl == MDR_CTRL_BANGBANG ? ctrl_bangbang(Tn[h], tg[h])
-                                                     : ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
-          ctrl_out[i0 + h] = a1 ? 1 : 0;
-        }
-    }
+    pen[h] = deadband_l2(tg[h], p.deadband, Tn[h]);
+    // x / 1.0 == x exactly: the default normaliser (integer target) costs no division
+    const double tpen = p.alpha_temp * pen[h];
+    rw[h] = p.penalty_mode == MDR_PEN_INDIVIDUAL_L2
+                ? -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig_term)
+                : pen[h];  // finalised by k_reward_finalize
+    on1[h] = false;
     if (lookahead) {
-      for (int k = 0; k < p.n_cap; ++k) {
-        unsigned c = 0;
-#pragma unroll
-        for (int h = 0; h < HPT; ++h) c += (unsigned)__popcll(__ballot(on1[h] && cls[h] == k));
-        if (lane == 0 && c) atomicAdd(&hist[k], c);
-      }
+      bool an;
+      if (lookahead == MDR_ACT_RANDOM) an = rnd1[h];
+      else if (lookahead == MDR_ACT_ALWAYS_ON) an = true;
+      else if (lookahead == kActBangBang) an = ctrl_bangbang(Tn[h], tg[h]);
+      else an = ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
+      on1[h] = valid[h] && hv_on(hvac_fsm(w[h], an, p.dt, p.L));
     }
+  }
+
+  // ---- stores
+  if (HPT == 2 && valid[HPT - 1]) {
+    *reinterpret_cast<double2*>(p.t_air + i0) = make_double2(Tn[0], Tn[HPT - 1]);
+    *reinterpret_cast<double2*>(p.t_mass + i0) = make_double2(Tmn[0], Tmn[HPT - 1]);
+    *reinterpret_cast<uint2*>(p.hvac + i0) = make_uint2(w[0], w[HPT - 1]);
+    *reinterpret_cast<double2*>(reward + i0) = make_double2(rw[0], rw[HPT - 1]);
+  } else {
+#pragma unroll
+    for (int h = 0; h < HPT; ++h)
+      if (valid[h]) {
+        p.t_air[i0 + h] = Tn[h]; p.t_mass[i0 + h] = Tmn[h]; p.hvac[i0 + h] = w[h]; reward[i0 + h] = rw[h];
+      }
+  }
+  if (ctrl != MDR_CTRL_NONE && ctrl_out) {
+#pragma unroll
+    for (int h = 0; h < HPT; ++h)
+      if (valid[h]) {
+        const bool a1 = ctrl == MDR_CTRL_BANGBANG ? ctrl_bangbang(Tn[h], tg[h])
+                                                   : ctrl_deadband(Tn[h], tg[h], p.deadband, on[h]);
+        ctrl_out[i0 + h] = a1 ? 1 : 0;
+      }
   }
 
   // ---- cluster reductions for the next launch / the common penalty modes
   if (lookahead) {
+    for (int k = 0; k < p.n_cap; ++k) {
+      unsigned c = 0;
+#pragma unroll
+      for (int h = 0; h < HPT; ++h) c += (unsigned)__popcll(__ballot(on1[h] && cls[h] == k));
+      if (lane == 0 && c) atomicAdd(&hist[k], c);
+    }
     __syncthreads();
     if (tid < p.n_cap && hist[tid])
       atomicAdd(&next_slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)hist[tid]);
   }
   if (p.penalty_mode != MDR_PEN_INDIVIDUAL_L2) {
-    double sacc = pen_sum, macc = pen_max;
+    double sacc = 0.0, macc = 0.0;
+#pragma unroll
+    for (int h = 0; h < HPT; ++h)
+      if (valid[h]) { sacc += pen[h] / (double)p.n_global; macc = fmax(macc, pen[h]); }
     for (int off = 32; off > 0; off >>= 1) {
       sacc += __shfl_xor(sacc, off);
       macc = fmax(macc, __shfl_xor(macc, off));
@@ -294,17 +287,18 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   }
 }
 
-#define MDR_INST_STEP(H, C, F)                                                                    \
-  template __global__ void k_step_t<H, C, F>(KParams, const uint8_t*, int, TickArgs, const TickArgs*, \
-                                             const unsigned long long*, double*, int, uint8_t*,   \
-                                             double*, int, unsigned long long*, unsigned long long*, \
-                                             double*);
-MDR_INST_STEP(1, false, false)
-MDR_INST_STEP(2, false, false)
-MDR_INST_STEP(1, true, false)
-MDR_INST_STEP(2, true, false)
-MDR_INST_STEP(2, false, true)
-MDR_INST_STEP(2, true, true)
+#define MDR_INST_STEP(H, C, F, A, LA)                                                            \
+  template __global__ void k_step_t<H, C, F, A, LA>(                                             \
+      KParams, const uint8_t*, int, TickArgs, const TickArgs*, const unsigned long long*,        \
+      double*, int, uint8_t*, double*, int, unsigned long long*, unsigned long long*, double*);
+MDR_INST_STEP(1, false, false, -1, -1)
+MDR_INST_STEP(2, false, false, -1, -1)
+MDR_INST_STEP(2, true, false, -1, -1)
+MDR_INST_STEP(2, false, true, -1, -1)
+MDR_INST_STEP(2, true, true, -1, -1)
+MDR_INST_STEP(2, false, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
+MDR_INST_STEP(2, false, true, MDR_ACT_BUFFER, 0)
+MDR_INST_STEP(2, true, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
 
 // Division self-check: q_fast = shared-reciprocal sequence, q_ieee = the / operator.
 __global__ void k_div_check(const double* __restrict__ a, const double* __restrict__ b, int64_t n,

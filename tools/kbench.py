@@ -18,7 +18,7 @@ def main():
     ap.add_argument("--houses", default="1048576,4194304,16777216")
     ap.add_argument("--launches", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="hpt2,fast2,fast2g2,fast1,fcoef2,probe")
+    ap.add_argument("--variants", default="hpt2,fast2,fcoef2,probe")
     a = ap.parse_args()
     import torch
 
