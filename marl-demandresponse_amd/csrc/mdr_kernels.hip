@@ -97,6 +97,17 @@ __device__ __forceinline__ bool pick_action(int mode, const uint8_t* action, uin
   return ctrl_deadband(T, tgt, deadband, hv_on(w0));
 }
 
+// Loads/stores at an SGPR base + 32-bit VGPR byte offset (computed in 32 bits, so the compiler
+// emits the saddr form instead of a 64-bit address add per array).
+template <typename V>
+__device__ __forceinline__ V ldo(const void* base, uint32_t off) {
+  return *reinterpret_cast<const V*>(reinterpret_cast<const char*>(base) + off);
+}
+template <typename V>
+__device__ __forceinline__ void sto(void* base, uint32_t off, V v) {
+  *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + off) = v;
+}
+
 template <int HPT, bool CACHED, bool FAST, int ACT, int LA>
 __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __restrict__ action,
                                                 int action_mode_rt, TickArgs tk0, const TickArgs* tkp,
@@ -135,11 +146,12 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   int cls[HPT];
   const uint32_t cs = (uint32_t)p.coef_stride;
   if (HPT == 2 && valid[HPT - 1]) {
-    auto ld2 = [&](const double* a) { return *reinterpret_cast<const double2*>(a + i0); };
+    const uint32_t o8 = i0 * 8u;
+    auto ld2 = [&](const double* a) { return ldo<double2>(a, o8); };
     const double2 vT = ld2(p.t_air), vTm = ld2(p.t_mass), vua = ld2(p.ua), vca = ld2(p.ca);
     const double2 vhm = ld2(p.hm), vtg = ld2(p.target);
-    const uint2 vw = *reinterpret_cast<const uint2*>(p.hvac + i0);
-    const unsigned short vc = *reinterpret_cast<const unsigned short*>(p.cap_idx + i0);
+    const uint2 vw = ldo<uint2>(p.hvac, i0 * 4u);
+    const unsigned short vc = ldo<unsigned short>(p.cap_idx, i0);
     T[0] = vT.x; T[HPT - 1] = vT.y; Tm[0] = vTm.x; Tm[HPT - 1] = vTm.y;
     ua[0] = vua.x; ua[HPT - 1] = vua.y; ca[0] = vca.x; ca[HPT - 1] = vca.y;
     hm[0] = vhm.x; hm[HPT - 1] = vhm.y;
@@ -234,10 +246,11 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
 
   // ---- stores
   if (HPT == 2 && valid[HPT - 1]) {
-    *reinterpret_cast<double2*>(p.t_air + i0) = make_double2(Tn[0], Tn[HPT - 1]);
-    *reinterpret_cast<double2*>(p.t_mass + i0) = make_double2(Tmn[0], Tmn[HPT - 1]);
-    *reinterpret_cast<uint2*>(p.hvac + i0) = make_uint2(w[0], w[HPT - 1]);
-    *reinterpret_cast<double2*>(reward + i0) = make_double2(rw[0], rw[HPT - 1]);
+    const uint32_t o8 = i0 * 8u;
+    sto(p.t_air, o8, make_double2(Tn[0], Tn[HPT - 1]));
+    sto(p.t_mass, o8, make_double2(Tmn[0], Tmn[HPT - 1]));
+    sto(p.hvac, i0 * 4u, make_uint2(w[0], w[HPT - 1]));
+    sto(reward, o8, make_double2(rw[0], rw[HPT - 1]));
   } else {
 #pragma unroll
     for (int h = 0; h < HPT; ++h)
