@@ -40,7 +40,6 @@ def parse():
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--houses", type=int, default=1 << 20, help="houses per GPU")
     ap.add_argument("--chunk", type=int, default=100, help="ticks per graph-captured rollout call")
-    ap.add_argument("--kernel-samples", type=int, default=200)
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="random", choices=["random", "buffer"])
@@ -152,12 +151,14 @@ def main():
 
     barrier()
     torch.cuda.synchronize()
+    # HIP events on the stream the k_step launches are issued on (the graph side stream)
+    launch_stream = env.rollout_stream()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
-    ev0.record()
+    ev0.record(launch_stream)
     for c in chunks:
         run(c)
-    ev1.record()
+    ev1.record(launch_stream)
     torch.cuda.synchronize()
     t1 = time.perf_counter()
     barrier()
@@ -171,20 +172,28 @@ def main():
         elapsed = float(t.item())
     value = n_total * args.steps / elapsed
 
-    # dominant kernel k_step: per-launch duration with HIP events on its stream (one launch per
-    # tick under the fused random controller with lookahead; same state, not in the timed loop)
-    kms = []
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world == 1:
-        env.step_tensor(None, action_mode="random", lookahead="random")
-        for _ in range(args.kernel_samples):
-            e0.record()
-            env.step_tensor(None, action_mode="random", lookahead="random")
-            e1.record()
-            e1.synchronize()
-            kms.append(e0.elapsed_time(e1))
+    # dominant kernel k_step: one launch per tick (fused random controller + lookahead), so its
+    # average launch duration over the timed region = launch-stream event time / steps (this
+    # includes the ~1 us graph inter-kernel gap; rocprofv3's per-kernel average is in profiles/)
     per_tick_ms = gpu_ms / args.steps
-    kern_ms = sorted(kms)[len(kms) // 2] if kms else per_tick_ms
+    kern_ms, kern_launches = per_tick_ms, args.steps
+    if world > 1:
+        # the sharded timed region also holds the per-tick RCCL allreduce: time k_step alone in
+        # a local graph rollout of the same shard (after the timed region, rewards discarded)
+        from mdr_amd._lib import ACT_RANDOM
+
+        sh = env.shard
+        ls = sh.launch_stream(True)
+        kern_launches = min(args.steps, 500)
+        ticks = env.driver_window(kern_launches)
+        rbuf = rew[0]
+        sh.rollout(ticks, None, 0, ACT_RANDOM, rbuf, 0, True)  # capture
+        torch.cuda.synchronize()
+        ev0.record(ls)
+        sh.rollout(ticks, None, 0, ACT_RANDOM, rbuf, 0, True)
+        ev1.record(ls)
+        torch.cuda.synchronize()
+        kern_ms = ev0.elapsed_time(ev1) / kern_launches
     bytes_launch = BYTES_PER_HOUSE_STEP * n_loc
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(n_loc)
@@ -210,7 +219,7 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "kernel": "mdr::k_step",
-                     "kernel_avg_us": kern_ms * 1e3, "gpu_us_per_tick_timed": per_tick_ms * 1e3,
+                     "kernel_avg_us": kern_ms * 1e3, "launches_timed": kern_launches,
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "bytes_per_house_step": BYTES_PER_HOUSE_STEP},
     }

@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define MDR_ABI_VERSION 1
+#define MDR_ABI_VERSION 2
 #define MDR_MAX_CAP 64
 
 enum {
@@ -189,10 +189,11 @@ int mdr_reward_finalize(mdr_ctx* ctx, const mdr_tick* tick, double* reward, void
  * rew_stride elements per tick (0 = reuse one buffer).  With an in-kernel action source
  * (MDR_ACT_RANDOM / _ALWAYS_ON / _BANGBANG / _DEADBAND_BANGBANG) every tick is ONE launch (the
  * counts of tick t+1 come from tick t's lookahead); with MDR_ACT_BUFFER two.  use_graph != 0
- * captures the sequence in a hipGraph (cached per shape) and replays it. */
+ * captures the sequence in a hipGraph (cached per shape) and replays it.  p_out (device scalar,
+ * may be NULL) receives the cluster power of the LAST tick, as mdr_step's p_out. */
 int mdr_rollout(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t* action,
                 int64_t act_stride, int action_mode, double* reward, int64_t rew_stride,
-                int use_graph, void* stream);
+                double* p_out, int use_graph, void* stream);
 
 /* ---- observation vector (norm_state_dict, norm.py:178-218) ----------------------------- */
 typedef struct mdr_obs_spec {
@@ -245,7 +246,7 @@ int mdr_rccl_allreduce(mdr_ctx* ctx, void* buf, int64_t count, int dtype, void* 
  * per tick  [phase 1 if BUFFER] -> allreduce(counts) -> phase 2 (with lookahead when possible) */
 int mdr_rollout_sharded(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t* action,
                         int64_t act_stride, int action_mode, double* reward, int64_t rew_stride,
-                        void* stream);
+                        double* p_out, void* stream);
 
 /* ---- diagnostics ------------------------------------------------------------------------ */
 /* Memory-floor probe: the loads/stores of one mdr_step over the bound arrays with no arithmetic

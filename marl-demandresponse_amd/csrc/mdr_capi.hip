@@ -56,10 +56,11 @@ struct GraphKey {
   int64_t act_stride;
   void* rew;
   int64_t rew_stride;
+  void* p_out;
   void* stream;
   bool operator<(const GraphKey& o) const {
-    return std::tie(n_ticks, mode, act, act_stride, rew, rew_stride, stream) <
-           std::tie(o.n_ticks, o.mode, o.act, o.act_stride, o.rew, o.rew_stride, o.stream);
+    return std::tie(n_ticks, mode, act, act_stride, rew, rew_stride, p_out, stream) <
+           std::tie(o.n_ticks, o.mode, o.act, o.act_stride, o.rew, o.rew_stride, o.p_out, o.stream);
   }
 };
 
@@ -411,7 +412,7 @@ static int stage_ticks(mdr_ctx* c, int n, const mdr_tick* ticks, hipStream_t st)
 
 // The launch sequence of a rollout; tick args come from d_ticks so a captured graph is reusable.
 static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t act_stride, int mode,
-                            double* reward, int64_t rew_stride, hipStream_t st) {
+                            double* reward, int64_t rew_stride, double* p_out, hipStream_t st) {
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, 3 * c->slab_len * sizeof(unsigned long long), st));
   c->ring = 0;
   const bool la = lookahead_ok(mode);
@@ -431,14 +432,14 @@ static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t ac
       LAUNCH_CHECK("k_power_counts");
     }
     int rc = launch_step(c, a, mode, TickArgs{}, c->d_ticks + t, r, la ? mode : 0, MDR_CTRL_NONE,
-                         nullptr, nullptr, st);
+                         nullptr, t == n - 1 ? p_out : nullptr, st);
     if (rc) return rc;
   }
   return MDR_OK;
 }
 
 int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action, int64_t act_stride,
-                int mode, double* reward, int64_t rew_stride, int use_graph, void* stream) {
+                int mode, double* reward, int64_t rew_stride, double* p_out, int use_graph, void* stream) {
   if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout: bad argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout: context not bound");
   if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout: bad action source");
@@ -450,17 +451,17 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   rc = stage_ticks(c, n, ticks, st);
   if (rc) return rc;
   if (!use_graph) {
-    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, st);
+    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st);
     c->counts_ready = false;
     return rc;
   }
-  GraphKey key{n, mode, action, act_stride, reward, rew_stride, stream};
+  GraphKey key{n, mode, action, act_stride, reward, rew_stride, p_out, stream};
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     if (st == nullptr) return fail(MDR_EARG, "mdr_rollout: graph capture needs a non-default stream");
     hipGraph_t g;
     HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, st);
+    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st);
     hipError_t e = hipStreamEndCapture(st, &g);
     if (rc) return rc;
     if (e != hipSuccess) return fail(MDR_EHIP, std::string("capture: ") + hipGetErrorString(e));
@@ -627,7 +628,8 @@ int mdr_rccl_allreduce(mdr_ctx* c, void* buf, int64_t count, int dtype, void* st
 }
 
 int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
-                        int64_t act_stride, int mode, double* reward, int64_t rew_stride, void* stream) {
+                        int64_t act_stride, int mode, double* reward, int64_t rew_stride, double* p_out,
+                        void* stream) {
   if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout_sharded: bad argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout_sharded: context not bound");
   if (!c->comm) return fail(MDR_ESTATE, "mdr_rollout_sharded: RCCL not initialised");
@@ -654,7 +656,7 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
     RCCL_TRY(ncclAllReduce(slab_at(c, c->ring), slab_at(c, c->ring), c->slab_len, ncclUint64, ncclSum,
                            c->comm, st));
     rc = launch_step(c, a, mode, TickArgs{}, c->d_ticks + t, reward + (int64_t)t * rew_stride,
-                     la ? mode : 0, MDR_CTRL_NONE, nullptr, nullptr, st);
+                     la ? mode : 0, MDR_CTRL_NONE, nullptr, t == n - 1 ? p_out : nullptr, st);
     if (rc) return rc;
   }
   c->counts_ready = false;

@@ -12,7 +12,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MDR_LIB", os.path.join(HERE, "libmdr_hip.so"))
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 MAX_CAP = 64
 
 # enums (mdr.h)
@@ -95,7 +95,7 @@ SIGNATURES = {
     "mdr_penalty_partials": (I, [VP, VP]),
     "mdr_penalty_buffer": (I, [VP, P(VP)]),
     "mdr_reward_finalize": (I, [VP, P(mdr_tick), VP, VP]),
-    "mdr_rollout": (I, [VP, I, P(mdr_tick), VP, I64, I, VP, I64, I, VP]),
+    "mdr_rollout": (I, [VP, I, P(mdr_tick), VP, I64, I, VP, I64, VP, I, VP]),
     "mdr_msg_width": (I, [P(mdr_obs_spec)]),
     "mdr_obs": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, VP, VP]),
     "mdr_halo_pack": (I, [VP, P(mdr_obs_spec), VP, VP]),
@@ -103,7 +103,7 @@ SIGNATURES = {
     "mdr_rccl_unique_id": (I, [VP]),
     "mdr_rccl_init": (I, [VP, VP, I, I]),
     "mdr_rccl_allreduce": (I, [VP, VP, I64, I, VP]),
-    "mdr_rollout_sharded": (I, [VP, I, P(mdr_tick), VP, I64, I, VP, I64, VP]),
+    "mdr_rollout_sharded": (I, [VP, I, P(mdr_tick), VP, I64, I, VP, I64, VP, VP]),
     "mdr_probe_stream": (I, [VP, VP, VP]),
     "mdr_div_check": (I, [VP, VP, I64, VP, VP]),
     "mdr_event_record": (I, [VP, I, VP]),

@@ -68,7 +68,8 @@ class RcclComm:
         n = shard.n
         L.check(shard.lib.mdr_rollout_sharded(shard.ctx, len(ticks), arr, L.ptr(actions),
                                               n if actions is not None else 0, mode, L.ptr(rewards),
-                                              rew_stride, shard.stream()), "mdr_rollout_sharded")
+                                              rew_stride, L.ptr(shard.p_dev), shard.stream()),
+                "mdr_rollout_sharded")
 
     def ring_halo(self, shard, spec):
         """Message features of the houses just before / after this shard on the global ring."""
@@ -105,3 +106,69 @@ class RcclComm:
                 full = torch.cat(parts).cpu().numpy()
                 dst[key] = full.astype(a.dtype) if a.dtype != np.float64 else full
         return out_st, out_prm
+
+
+def device_view(ptr: int, n: int, typestr: str, device):
+    """Zero-copy torch view of n elements of library-owned device memory."""
+    import torch
+
+    class _Arr:
+        __slots__ = ("__cuda_array_interface__",)
+
+    a = _Arr()
+    a.__cuda_array_interface__ = {"shape": (int(n),), "typestr": typestr, "data": (int(ptr), False),
+                                  "version": 2, "strides": None}
+    return torch.as_tensor(a, device=device)
+
+
+class TorchComm(RcclComm):
+    """The same exchanges issued through ``torch.distributed`` collectives on zero-copy views of
+    the library's count / penalty buffers instead of the library's own RCCL communicator.
+
+    With the 'nccl' backend this is still RCCL (torch's communicator); with 'gloo' it lets
+    several ranks share one GPU, which is how the sharded device path is tested on a 1-GPU box.
+    Rollouts issue one step per tick from Python (no C loop)."""
+
+    def attach(self, shard) -> None:
+        pass
+
+    def allreduce_counts(self, shard) -> None:
+        ptr, n = shard.counts_buffer()
+        self.dist.all_reduce(device_view(ptr, n, "<i8", shard.device))  # counts < 2^63: same bits
+
+    def allreduce_penalty(self, shard) -> None:
+        p = C.c_void_p()
+        L.check(shard.lib.mdr_penalty_buffer(shard.ctx, C.byref(p)), "mdr_penalty_buffer")
+        self.dist.all_reduce(device_view(p.value, 1, "<f8", shard.device))
+        self.dist.all_reduce(device_view(p.value + 8, 1, "<f8", shard.device), op=self.dist.ReduceOp.MAX)
+
+    def rollout(self, shard, ticks, actions, mode, rewards, rew_stride) -> None:
+        for t, tk in enumerate(ticks):
+            a = actions[t] if actions is not None else None
+            shard.power_counts(a, mode, tk.tick)
+            self.allreduce_counts(shard)
+            shard.step(a, mode, tk, reward=rewards[t] if rew_stride else rewards)
+
+
+def make_comm(kind: str = "auto"):
+    """Communicator for a sharded Environment: 'rccl' (libmdr_hip's own RCCL communicator, per-tick
+    allreduces issued from C), 'torch' (torch.distributed collectives), or 'auto' (rccl, falling
+    back to torch with a warning if the library communicator cannot be created)."""
+    if kind == "torch":
+        return TorchComm()
+    if kind == "rccl":
+        return RcclComm()
+    if kind != "auto":
+        raise ValueError(f"unknown comm kind {kind!r}")
+    return _AutoComm()
+
+
+class _AutoComm(RcclComm):
+    def attach(self, shard) -> None:
+        try:
+            super().attach(shard)
+        except Exception as e:  # noqa: BLE001
+            import warnings
+
+            warnings.warn(f"libmdr RCCL communicator unavailable ({e}); using torch.distributed collectives")
+            self.__class__ = TorchComm

@@ -319,6 +319,14 @@ class Environment:
         self._P_dev_valid = True
         return rewards
 
+    def rollout_stream(self, use_graph: bool = True):
+        """Stream the k_step launches of ``rollout`` are issued on (for HIP-event timing)."""
+        import torch
+
+        if self._comm is not None:
+            return torch.cuda.current_stream(self._shard.device)
+        return self._shard.launch_stream(use_graph)
+
     # ------------------------------------------------------------------ observations
     def _cluster_power(self) -> float:
         if self._P_dev_valid:

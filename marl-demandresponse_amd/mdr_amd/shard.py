@@ -162,18 +162,26 @@ class HipShard:
         torch = self.torch
         cur = torch.cuda.current_stream(self.device)
         if use_graph:
-            if getattr(self, "_side", None) is None:
-                self._side = torch.cuda.Stream(self.device)
-            s = self._side
+            s = self.launch_stream(True)
             s.wait_stream(cur)
             handle = s.cuda_stream
         else:
             handle = cur.cuda_stream
         L.check(self.lib.mdr_rollout(self.ctx, len(ticks), arr, L.ptr(action), act_stride, mode,
-                                     L.ptr(reward), rew_stride, int(use_graph), handle),
+                                     L.ptr(reward), rew_stride, L.ptr(self.p_dev), int(use_graph), handle),
                 "mdr_rollout")
         if use_graph:
             cur.wait_stream(self._side)
+
+    def launch_stream(self, use_graph=True):
+        """The torch stream rollout kernels run on (the shard's side stream for graph rollouts,
+        else the caller's current stream) — where timing events must be recorded."""
+        torch = self.torch
+        if not use_graph:
+            return torch.cuda.current_stream(self.device)
+        if getattr(self, "_side", None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        return self._side
 
     def greedy(self, budget: float, action):
         L.check(self.lib.mdr_ctrl_greedy(self.ctx, float(budget), L.ptr(action), self.stream()),

@@ -1,0 +1,115 @@
+"""Sharded device path on the GPU: the house-sharded Environment (one process per rank) must
+reproduce the single-process run on the same seeds.
+
+* world 1 over the library's own RCCL communicator (backend 'nccl'): exercises mdr_rccl_init,
+  mdr_rccl_allreduce and the C rollout loop mdr_rollout_sharded on a real device;
+* world 2 over torch.distributed/gloo (TorchComm) with both ranks on cuda:0: exercises the
+  sharding, the per-tick count / penalty allreduces and the ring-halo observation exchange with
+  the HIP kernels (RCCL cannot put two ranks on one GPU; the 8-GPU RCCL run is the driver's).
+
+Integers (on/lock/sso, counts, hence P) and everything derived per house in fp64 are bit-exact;
+the common penalty modes reduce the cluster penalty in a different order per shard, so rewards
+there are compared to 1e-12.
+"""
+import os
+import random
+import sys
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+T_STEP, T_BUF, T_ROLL = 5, 3, 6
+
+
+def _overrides(n, mode):
+    return {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals",
+            "reward_prop.penalty_props.mode": mode, "reward_prop.penalty_props.alpha_common_max": 0.5}
+
+
+def _run(env, n_total, torch, dev):
+    """Fixed tick script: fused random steps, buffer steps, a rollout (individual_L2 only)."""
+    lo, nl = env._offset, env.n_local
+    rewards = []
+    for _ in range(T_STEP):
+        rewards.append(env.step_tensor(None, action_mode="random", lookahead="random").cpu().numpy().copy())
+    for t in range(T_BUF):
+        a = np.random.RandomState(100 + t).randint(0, 2, n_total).astype(np.uint8)[lo:lo + nl]
+        rewards.append(env.step_tensor(torch.from_numpy(a).to(dev)).cpu().numpy().copy())
+    if env.shard.penalty_mode == 0:
+        r = env.rollout(T_ROLL, action_mode="random")
+        rewards.extend(r.cpu().numpy().copy())
+    st = env.shard.host_state()
+    obs = env.obs_tensor().cpu().numpy().copy()
+    return {"rewards": np.array(rewards), "T": st["T"], "Tm": st["Tm"], "on": st["on"], "lock": st["lock"],
+            "sso": st["sso"], "P": env._cluster_power(), "obs": obs}
+
+
+def _worker(rank, world, port, backend, kind, n, mode, out_dir):
+    sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "marl-demandresponse_amd"), os.path.dirname(HERE)]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    kw = {"device_id": dev} if backend == "nccl" else {}
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    import golden_util as g
+
+    from mdr_amd.distributed import make_comm
+    from mdr_amd.environment import Environment
+
+    env = Environment(g.props_from_overrides(_overrides(n, mode)), device=dev, rng=random.Random(4),
+                      population="synthetic", seed=77, rank=rank, world=world, comm=make_comm(kind))
+    res = _run(env, n, torch, dev)
+    res["lo"] = env._offset
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
+    torch.cuda.synchronize()
+    dist.destroy_process_group()
+
+
+def _free_port():
+    import socket
+
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+@pytest.mark.parametrize("backend,kind,world,n,mode", [
+    ("nccl", "rccl", 1, 3001, "individual_L2"),
+    ("gloo", "torch", 2, 3001, "individual_L2"),
+    ("gloo", "torch", 2, 2048, "common_L2"),
+])
+def test_sharded_equals_single(tmp_path, backend, kind, world, n, mode):
+    import torch
+
+    from mdr_amd.environment import Environment
+
+    mp.start_processes(_worker, args=(world, _free_port(), backend, kind, n, mode, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    parts = sorted((np.load(tmp_path / f"rank{r}.npz") for r in range(world)), key=lambda p: int(p["lo"]))
+    dev = torch.device("cuda", 0)
+    env = Environment(gu.props_from_overrides(_overrides(n, mode)), device=dev, rng=random.Random(4),
+                      population="synthetic", seed=77)
+    ref = _run(env, n, torch, dev)
+    for key in ("on", "lock", "sso", "T", "Tm"):
+        np.testing.assert_array_equal(np.concatenate([p[key] for p in parts]), ref[key], err_msg=key)
+    got_r = np.concatenate([p["rewards"] for p in parts], axis=1)
+    if mode == "individual_L2":
+        np.testing.assert_array_equal(got_r, ref["rewards"])
+    else:
+        np.testing.assert_allclose(got_r, ref["rewards"], rtol=1e-12, atol=1e-15)
+    for p in parts:
+        assert float(p["P"]) == ref["P"]
+    obs = np.concatenate([p["obs"] for p in parts])
+    np.testing.assert_array_equal(obs, ref["obs"])

@@ -193,6 +193,8 @@ def test_rollout_equals_steps(torch_gpu):
     s1, s2 = e1.shard.host_state(), e2.shard.host_state()
     for k in s1:
         np.testing.assert_array_equal(s1[k], s2[k])
+    assert e1._cluster_power() == e2._cluster_power()  # rollout's p_out = last tick's P
+    np.testing.assert_array_equal(e1.obs_tensor().cpu().numpy(), e2.obs_tensor().cpu().numpy())
 
 
 def test_rollout_buffer_actions_vs_oracle(torch_gpu):

@@ -22,6 +22,6 @@ STEPS=${STEPS:-smoke,pytest,bench,prof}
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
   step rocprof 600 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- \
-    python bench.py --steps 500 --warmup 100 --no-cpu-baseline --kernel-samples 50 || true
+    python bench.py --steps 500 --warmup 100 --no-cpu-baseline || true
 fi
 echo "== done"
