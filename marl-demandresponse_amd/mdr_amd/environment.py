@@ -319,6 +319,20 @@ class Environment:
         self._P_dev_valid = True
         return rewards
 
+    def greedy_actions(self, out=None):
+        """GreedyMyopic.get_action (greedy_myopic_controller.py:67-104) on device: the next tick's
+        actions from the current state, budget = the current regulation signal (obs reg_signal).
+        Returns a uint8 [n_local] device tensor (``out`` if given)."""
+        import torch
+
+        if self.world > 1:
+            raise NotImplementedError("greedy over a sharded cluster (needs a global sort)")
+        sh = self._shard
+        if out is None:
+            out = torch.empty(self._n_local, dtype=torch.uint8, device=sh.device)
+        sh.greedy(float(self.power_grid.current_signal), out)
+        return out
+
     def rollout_stream(self, use_graph: bool = True):
         """Stream the k_step launches of ``rollout`` are issued on (for HIP-event timing)."""
         import torch
