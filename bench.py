@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="random", choices=["random", "buffer"])
+    ap.add_argument("--comm", default="default", choices=["default", "none", "rccl", "torch"],
+                    help="exchange for the sharded path (default: rccl when WORLD_SIZE > 1); "
+                         "'rccl' at world 1 exercises the sharded C loop on one GPU")
     return ap.parse_args()
 
 
@@ -108,13 +111,18 @@ def main():
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     comm = None
-    if world > 1:
+    kind = args.comm if args.comm != "default" else ("rccl" if world > 1 else "none")
+    if world > 1 and kind == "none":
+        raise SystemExit("--comm none needs WORLD_SIZE 1")
+    if kind != "none":
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=dev)
-        from mdr_amd.distributed import RcclComm
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        os.environ.setdefault("MASTER_PORT", "29511")
+        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        from mdr_amd.distributed import make_comm
 
-        comm = RcclComm()
+        comm = make_comm(kind)
     from mdr_amd.environment import Environment
 
     n_total = args.houses * world
@@ -144,7 +152,7 @@ def main():
     torch.cuda.synchronize()
 
     def barrier():
-        if world > 1:
+        if comm is not None:
             import torch.distributed as dist
 
             dist.barrier()
@@ -164,7 +172,7 @@ def main():
     barrier()
     elapsed = t1 - t0
     gpu_ms = ev0.elapsed_time(ev1)
-    if world > 1:
+    if comm is not None:
         import torch.distributed as dist
 
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
@@ -177,7 +185,7 @@ def main():
     # includes the ~1 us graph inter-kernel gap; rocprofv3's per-kernel average is in profiles/)
     per_tick_ms = gpu_ms / args.steps
     kern_ms, kern_launches = per_tick_ms, args.steps
-    if world > 1:
+    if comm is not None:
         # the sharded timed region also holds the per-tick RCCL allreduce: time k_step alone in
         # a local graph rollout of the same shard (after the timed region, rewards discarded)
         from mdr_amd._lib import ACT_RANDOM
@@ -214,8 +222,10 @@ def main():
                                "(BASELINE metric at 1M houses; configs[1]'s controller)",
                    "houses_per_gpu": n_loc, "houses_total": n_total, "dt_s": props.time_step.seconds,
                    "signal": "sinusoidals", "penalty": "individual_L2", "action_mode": args.mode,
-                   "chunk_ticks": chunk, "parallelism": f"house-sharded x{world} (RCCL allreduce of "
-                                                        "per-tick power counts)" if world > 1 else "1 GPU"},
+                   "chunk_ticks": chunk,
+                   "sharded_pipeline": comm.pipeline(env.shard) if comm is not None else None,
+                   "parallelism": f"house-sharded x{world} ({kind} allreduce of "
+                                                        "per-tick power counts)" if comm is not None else "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": traffic, "kernel": "mdr::k_step",
@@ -227,7 +237,7 @@ def main():
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)
-    if world > 1:
+    if comm is not None:
         import torch.distributed as dist
 
         dist.destroy_process_group()

@@ -247,6 +247,14 @@ int mdr_rccl_allreduce(mdr_ctx* ctx, void* buf, int64_t count, int dtype, void* 
 int mdr_rollout_sharded(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t* action,
                         int64_t act_stride, int action_mode, double* reward, int64_t rew_stride,
                         double* p_out, void* stream);
+/* Pipeline of mdr_rollout_sharded for in-kernel action sources with one reward row per tick:
+ *   0 serial      allreduce(counts of t) -> step(t) on the caller's stream
+ *   1 overlapped  step(t) on the caller's stream concurrent with allreduce(counts of t) on a
+ *                 context stream; step(t+1) writes tick t's reward (bit-identical)
+ *  -1 undecided   the next rollout of >= 16 ticks times both on its own ticks (max over ranks)
+ *                 and keeps the faster; MDR_SHARDED_OVERLAP=0/1 forces one at mdr_create.
+ * us_serial / us_overlap (may be NULL) receive the calibration's per-tick times. */
+int mdr_rollout_sharded_mode(mdr_ctx* ctx, int* mode, double* us_serial, double* us_overlap);
 
 /* ---- diagnostics ------------------------------------------------------------------------ */
 /* Memory-floor probe: the loads/stores of one mdr_step over the bound arrays with no arithmetic

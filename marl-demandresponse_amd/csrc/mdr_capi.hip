@@ -71,7 +71,8 @@ struct mdr_ctx {
   KParams kp{};
   bool bound = false;
   double* d_tables = nullptr;           // q_on[MDR_MAX_CAP] | p_on[MDR_MAX_CAP]
-  unsigned long long* d_slab = nullptr;  // 3 x kCountShards x n_cap ring of count slabs
+  unsigned long long* d_slab = nullptr;  // kSlabs x kCountShards x n_cap count slabs (ring of 3 on
+                                         // the step path, 4 in the overlapped sharded pipeline)
   int slab_len = 0;
   int ring = 0;                          // slab of the current tick
   bool counts_ready = false;             // current slab filled (phase 1 or previous lookahead)
@@ -102,6 +103,10 @@ struct mdr_ctx {
   // multi-GPU
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
+  int overlap_mode = -1;                 // sharded pipeline: -1 calibrate, 0 serial, 1 overlapped
+  double calib_us[2] = {0.0, 0.0};       // calibration: us/tick serial, overlapped (max over ranks)
+  hipStream_t comm_stream = nullptr;     // per-tick allreduce of the overlapped pipeline
+  hipEvent_t ev_k1[kSlabs] = {}, ev_ar[kSlabs] = {}, ev_pc = nullptr;
   hipEvent_t ev[16] = {};
 };
 
@@ -142,19 +147,19 @@ int refresh_if_dirty(mdr_ctx* c, hipStream_t st) {
   return MDR_OK;
 }
 
-int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const TickArgs* tkp,
-                double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
-                hipStream_t st) {
-  unsigned long long* cur = slab_at(c, c->ring);
-  unsigned long long* nxt = slab_at(c, c->ring + 1);
-  unsigned long long* zer = slab_at(c, c->ring + 2);
+// k_step launch with explicit count slabs; reward_lag: the launch writes the previous tick's
+// reward from `cur` (nullptr: none), see k_step_t
+int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const TickArgs* tkp,
+                   double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
+                   const unsigned long long* cur, unsigned long long* nxt, unsigned long long* zer,
+                   int reward_lag, hipStream_t st) {
   if (int rc = refresh_if_dirty(c, st)) return rc;
   KParams kp = c->kp;
   kp.coef = c->cached ? c->d_coef : nullptr;
 #define MDR_LAUNCH_STEP(H, C, F, A, LA)                                                               \
   hipLaunchKernelGGL((k_step_t<H, C, F, A, LA>), dim3(blocks(kp.n, 256 * H)), dim3(256), 0, st, kp,       \
                      action, mode, tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer,      \
-                     c->d_pen_partial)
+                     c->d_pen_partial, reward_lag)
   const bool hot_random = mode == MDR_ACT_RANDOM && lookahead == MDR_ACT_RANDOM;
   const bool hot_buffer = mode == MDR_ACT_BUFFER && lookahead == 0;
   if (c->hpt == 2 && c->fastdiv) {
@@ -173,6 +178,15 @@ int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const 
   }
 #undef MDR_LAUNCH_STEP
   LAUNCH_CHECK("k_step");
+  return MDR_OK;
+}
+
+int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const TickArgs* tkp,
+                double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
+                hipStream_t st) {
+  int rc = launch_step_on(c, action, mode, tk, tkp, reward, lookahead, ctrl, ctrl_out, p_out,
+                          slab_at(c, c->ring), slab_at(c, c->ring + 1), slab_at(c, c->ring + 2), 0, st);
+  if (rc) return rc;
   c->ring = (c->ring + 1) % 3;
   c->counts_ready = lookahead != 0;
   return MDR_OK;
@@ -248,9 +262,9 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
     k.fast_tick_ok = ok ? 1 : 0;
   }
   c->slab_len = kCountShards * cfg->n_cap;
-  if (hipMalloc(&c->d_slab, 3 * c->slab_len * sizeof(unsigned long long)) != hipSuccess)
+  if (hipMalloc(&c->d_slab, kSlabs * c->slab_len * sizeof(unsigned long long)) != hipSuccess)
     return cleanup(fail(MDR_ENOMEM, "count slabs"));
-  if (hipMemset(c->d_slab, 0, 3 * c->slab_len * sizeof(unsigned long long)) != hipSuccess)
+  if (hipMemset(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long)) != hipSuccess)
     return cleanup(fail(MDR_EHIP, "count slabs memset"));
   if (const char* e = getenv("MDR_HPT")) c->hpt = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("MDR_VARIANT")) c->cached = strcmp(e, "coef") == 0;
@@ -268,6 +282,13 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
     return cleanup(fail(MDR_EHIP, "event"));
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(MDR_EHIP, "event"));
+  for (int i = 0; i < kSlabs; ++i)
+    if (hipEventCreateWithFlags(&c->ev_k1[i], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_ar[i], hipEventDisableTiming) != hipSuccess)
+      return cleanup(fail(MDR_EHIP, "event"));
+  if (hipEventCreateWithFlags(&c->ev_pc, hipEventDisableTiming) != hipSuccess)
+    return cleanup(fail(MDR_EHIP, "event"));
+  if (const char* e = getenv("MDR_SHARDED_OVERLAP")) c->overlap_mode = atoi(e) < 0 ? -1 : atoi(e) != 0;
   *out = c;
   return MDR_OK;
 }
@@ -288,6 +309,12 @@ int mdr_destroy(mdr_ctx* c) {
   if (c->ticks_free) hipEventDestroy(c->ticks_free);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
+  for (int i = 0; i < kSlabs; ++i) {
+    if (c->ev_k1[i]) hipEventDestroy(c->ev_k1[i]);
+    if (c->ev_ar[i]) hipEventDestroy(c->ev_ar[i]);
+  }
+  if (c->ev_pc) hipEventDestroy(c->ev_pc);
+  if (c->comm_stream) hipStreamDestroy(c->comm_stream);
   hipFree(c->g_key); hipFree(c->g_key2); hipFree(c->g_ps); hipFree(c->g_incl);
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
@@ -413,7 +440,7 @@ static int stage_ticks(mdr_ctx* c, int n, const mdr_tick* ticks, hipStream_t st)
 // The launch sequence of a rollout; tick args come from d_ticks so a captured graph is reusable.
 static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t act_stride, int mode,
                             double* reward, int64_t rew_stride, double* p_out, hipStream_t st) {
-  HIP_TRY(hipMemsetAsync(c->d_slab, 0, 3 * c->slab_len * sizeof(unsigned long long), st));
+  HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
   c->ring = 0;
   const bool la = lookahead_ok(mode);
   for (int t = 0; t < n; ++t) {
@@ -613,6 +640,7 @@ int mdr_rccl_init(mdr_ctx* c, const uint8_t* id128, int world, int rank) {
   ncclUniqueId id;
   memcpy(&id, id128, 128);
   RCCL_TRY(ncclCommInitRank(&c->comm, world, id, rank));
+  if (!c->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
   c->world = world;
   c->rank = rank;
   return MDR_OK;
@@ -626,6 +654,107 @@ int mdr_rccl_allreduce(mdr_ctx* c, void* buf, int64_t count, int dtype, void* st
   RCCL_TRY(ncclAllReduce(buf, buf, (size_t)count, t, op, c->comm, S(stream)));
   return MDR_OK;
 }
+
+}  // extern "C"
+
+namespace {
+// Overlapped sharded pipeline (in-kernel action source with lookahead, one reward row per tick).
+// The per-tick exchange only feeds the reward's signal term, so the reward of tick t is written
+// one launch later (k_step reward_lag; bit-identical, no extra bytes):
+//   compute stream  K(t): state of tick t, reward of tick t-1 from the loaded state + allreduced
+//                   slab (t-1)%4, lookahead counts of t+1 into slab (t+1)%4, zero slab (t+2)%4
+//   comm stream     allreduce(slab t%4) once K(t-1) has filled it — concurrent with K(t)
+// K(t+1) waits for allreduce(t); after the loop k_reward_state writes the last tick's reward.
+int rollout_sharded_overlap(mdr_ctx* c, const TickArgs* ticks, int n, int mode, double* reward,
+                            int64_t rew_stride, double* p_out, hipStream_t st) {
+  hipStream_t cs = c->comm_stream;
+  auto slab = [&](int t) { return c->d_slab + (size_t)(t % kSlabs) * c->slab_len; };
+  HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
+  hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, nullptr,
+                     mode, (uint64_t)0, ticks, slab(0));
+  LAUNCH_CHECK("k_power_counts");
+  HIP_TRY(hipEventRecord(c->ev_pc, st));
+  for (int t = 0; t < n; ++t) {
+    // comm stream: counts of tick t are complete once K(t-1) (or phase 1) has finished
+    HIP_TRY(hipStreamWaitEvent(cs, t == 0 ? c->ev_pc : c->ev_k1[(t - 1) % kSlabs], 0));
+    RCCL_TRY(ncclAllReduce(slab(t), slab(t), c->slab_len, ncclUint64, ncclSum, c->comm, cs));
+    HIP_TRY(hipEventRecord(c->ev_ar[t % kSlabs], cs));
+    // compute stream: K(t) needs the allreduced counts of tick t-1 for that tick's reward
+    if (t >= 1) HIP_TRY(hipStreamWaitEvent(st, c->ev_ar[(t - 1) % kSlabs], 0));
+    int rc = launch_step_on(c, nullptr, mode, TickArgs{}, ticks + t,
+                            t >= 1 ? reward + (int64_t)(t - 1) * rew_stride : reward, mode, MDR_CTRL_NONE,
+                            nullptr, nullptr, t >= 1 ? slab(t - 1) : nullptr, slab(t + 1), slab(t + 2),
+                            1, st);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c->ev_k1[t % kSlabs], st));
+  }
+  HIP_TRY(hipStreamWaitEvent(st, c->ev_ar[(n - 1) % kSlabs], 0));
+  hipLaunchKernelGGL(k_reward_state, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp,
+                     ticks + (n - 1), slab(n - 1), reward + (int64_t)(n - 1) * rew_stride, p_out);
+  LAUNCH_CHECK("k_reward_state");
+  // leave the step path's invariant (slab ring+1 zero) behind
+  HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
+  c->ring = 0;
+  c->counts_ready = false;
+  return MDR_OK;
+}
+
+// Serial sharded ticks on one stream: [phase 1 if needed] -> allreduce(counts) -> k_step.
+int rollout_sharded_serial(mdr_ctx* c, const TickArgs* ticks, int n, const uint8_t* action,
+                           int64_t act_stride, int mode, double* reward, int64_t rew_stride,
+                           double* p_out, hipStream_t st) {
+  HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
+  c->ring = 0;
+  const bool la = lookahead_ok(mode);
+  for (int t = 0; t < n; ++t) {
+    const uint8_t* a = action ? action + (int64_t)t * act_stride : nullptr;
+    if (!la || t == 0) {
+      hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, a, mode,
+                         (uint64_t)0, ticks + t, slab_at(c, c->ring));
+      LAUNCH_CHECK("k_power_counts");
+    }
+    RCCL_TRY(ncclAllReduce(slab_at(c, c->ring), slab_at(c, c->ring), c->slab_len, ncclUint64, ncclSum,
+                           c->comm, st));
+    int rc = launch_step(c, a, mode, TickArgs{}, ticks + t, reward + (int64_t)t * rew_stride,
+                         la ? mode : 0, MDR_CTRL_NONE, nullptr, t == n - 1 ? p_out : nullptr, st);
+    if (rc) return rc;
+  }
+  c->counts_ready = false;
+  return MDR_OK;
+}
+
+// MDR_SHARDED_AUTO: the first eligible rollout (>= 16 ticks) runs half its ticks serial and half
+// overlapped, times both on the stream, takes the max over ranks (RCCL) so every rank decides
+// the same, and keeps the faster pipeline.  Both produce bit-identical results.
+int rollout_sharded_calibrate(mdr_ctx* c, int n, int mode, double* reward, int64_t rew_stride,
+                              double* p_out, hipStream_t st) {
+  const int n1 = n / 2;
+  HIP_TRY(hipEventRecord(c->ev[13], st));
+  int rc = rollout_sharded_serial(c, c->d_ticks, n1, nullptr, 0, mode, reward, rew_stride, nullptr, st);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c->ev[14], st));
+  rc = rollout_sharded_overlap(c, c->d_ticks + n1, n - n1, mode, reward + (int64_t)n1 * rew_stride,
+                               rew_stride, p_out, st);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c->ev[15], st));
+  HIP_TRY(hipEventSynchronize(c->ev[15]));
+  float ms_serial = 0.f, ms_overlap = 0.f;
+  HIP_TRY(hipEventElapsedTime(&ms_serial, c->ev[13], c->ev[14]));
+  HIP_TRY(hipEventElapsedTime(&ms_overlap, c->ev[14], c->ev[15]));
+  double h[2] = {ms_serial / n1, ms_overlap / (n - n1)};
+  double* d = c->d_partial2;  // 2 doubles of scratch, free outside the common-penalty steps
+  HIP_TRY(hipMemcpyAsync(d, h, sizeof(h), hipMemcpyHostToDevice, st));
+  RCCL_TRY(ncclAllReduce(d, d, 2, ncclFloat64, ncclMax, c->comm, st));
+  HIP_TRY(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  c->calib_us[0] = h[0] * 1e3;
+  c->calib_us[1] = h[1] * 1e3;
+  c->overlap_mode = h[1] < h[0] ? 1 : 0;
+  return MDR_OK;
+}
+}  // namespace
+
+extern "C" {
 
 int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
                         int64_t act_stride, int mode, double* reward, int64_t rew_stride, double* p_out,
@@ -643,23 +772,19 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
   if (rc) return rc;
   rc = stage_ticks(c, n, ticks, st);
   if (rc) return rc;
-  HIP_TRY(hipMemsetAsync(c->d_slab, 0, 3 * c->slab_len * sizeof(unsigned long long), st));
-  c->ring = 0;
-  const bool la = lookahead_ok(mode);
-  for (int t = 0; t < n; ++t) {
-    const uint8_t* a = action ? action + (int64_t)t * act_stride : nullptr;
-    if (!la || t == 0) {
-      hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, a, mode,
-                         (uint64_t)0, c->d_ticks + t, slab_at(c, c->ring));
-      LAUNCH_CHECK("k_power_counts");
-    }
-    RCCL_TRY(ncclAllReduce(slab_at(c, c->ring), slab_at(c, c->ring), c->slab_len, ncclUint64, ncclSum,
-                           c->comm, st));
-    rc = launch_step(c, a, mode, TickArgs{}, c->d_ticks + t, reward + (int64_t)t * rew_stride,
-                     la ? mode : 0, MDR_CTRL_NONE, nullptr, t == n - 1 ? p_out : nullptr, st);
-    if (rc) return rc;
-  }
-  c->counts_ready = false;
+  const bool can_overlap = lookahead_ok(mode) && rew_stride != 0 && c->comm_stream;
+  if (can_overlap && c->overlap_mode < 0 && n >= 16)
+    return rollout_sharded_calibrate(c, n, mode, reward, rew_stride, p_out, st);
+  if (can_overlap && c->overlap_mode == 1)
+    return rollout_sharded_overlap(c, c->d_ticks, n, mode, reward, rew_stride, p_out, st);
+  return rollout_sharded_serial(c, c->d_ticks, n, action, act_stride, mode, reward, rew_stride, p_out, st);
+}
+
+int mdr_rollout_sharded_mode(mdr_ctx* c, int* mode, double* us_serial, double* us_overlap) {
+  if (!c || !mode) return fail(MDR_EARG, "mdr_rollout_sharded_mode: null argument");
+  *mode = c->overlap_mode;
+  if (us_serial) *us_serial = c->calib_us[0];
+  if (us_overlap) *us_overlap = c->calib_us[1];
   return MDR_OK;
 }
 

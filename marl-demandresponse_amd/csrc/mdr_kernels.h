@@ -8,6 +8,7 @@
 namespace mdr {
 
 constexpr int kCountShards = 64;  // atomic shards for the per-class ON counts
+constexpr int kSlabs = 4;         // count slabs: ring of 3 (step path) / 4 (overlapped pipeline)
 constexpr int kObsBlock = 128;    // houses per obs tile
 constexpr int kActBangBang = 16;  // internal action modes: controller evaluated on the loaded state
 constexpr int kActDeadband = 17;
@@ -61,13 +62,15 @@ __global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, Tick
                          const TickArgs* tkp, const unsigned long long* counts, double* reward,
                          int ctrl, uint8_t* ctrl_out, double* p_out, int lookahead,
                          unsigned long long* next_slab, unsigned long long* zero_slab,
-                         double* pen_partial);
+                         double* pen_partial, int reward_lag);
 __global__ void k_probe_stream(KParams p, double* reward);
 __global__ void k_refresh(KParams p, double* coef, int* params_bad);
 __global__ void k_div_check(const double* a, const double* b, int64_t n, unsigned long long* mismatches);
 __global__ void k_pen_reduce(const double* pen_partial, int nblk, double* partial2);
 __global__ void k_reward_finalize(KParams p, TickArgs tk, const unsigned long long* counts,
                                   const double* partial2, double* reward);
+__global__ void k_reward_state(KParams p, const TickArgs* tkp, const unsigned long long* counts,
+                               double* reward, double* p_out);
 __global__ void k_populate(KParams p, PopArgs a);
 __global__ void k_obs(KParams p, ObsArgs o, const double* p_dev, float* obs);
 __global__ void k_halo_pack(KParams p, ObsArgs o, int lo, int hi, float* out);

@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
                                                 uint8_t* __restrict__ ctrl_out, double* p_out,
                                                 int lookahead_rt, unsigned long long* next_slab,
                                                 unsigned long long* zero_slab,
-                                                double* __restrict__ pen_partial) {
+                                                double* __restrict__ pen_partial, int reward_lag) {
   // ACT / LA >= 0: action source / lookahead fixed at compile time (the hot configurations);
   // -1: taken from the runtime arguments
   const int action_mode = ACT >= 0 ? ACT : action_mode_rt;
@@ -183,11 +183,19 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   __syncthreads();  // hist zeroed (the loads above stay in flight across the barrier)
 
   const TickArgs tk = tkp ? *tkp : tk0;
-  // per-tick signal penalty (rewards_calculator.py:183-203), uniform in the wave
-  const double P = wave_power(counts, p.p_on, p.n_cap);
-  const double x = (P - tk.s_prev) / (double)p.n_global;
-  const double sig_term = p.alpha_sig * (x * x) / p.norm_sig;
-  if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
+  // per-tick signal penalty (rewards_calculator.py:183-203), uniform in the wave.
+  // reward_lag (overlapped multi-GPU pipeline, tkp required): this launch writes the reward of the
+  // PREVIOUS tick — its temperature penalty from the loaded state (= that tick's result) and its
+  // signal term from `counts` = that tick's allreduced slab — so the allreduce of tick t runs
+  // concurrently with the launch of tick t.  counts == nullptr there (first tick): no reward.
+  double sig_term = 0.0;
+  const bool write_rew = counts != nullptr;
+  if (counts) {
+    const double P = wave_power(counts, p.p_on, p.n_cap);
+    const double x = (P - (reward_lag ? tkp[-1].s_prev : tk.s_prev)) / (double)p.n_global;
+    sig_term = p.alpha_sig * (x * x) / p.norm_sig;
+    if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
+  }
 
   // random controller bits of this tick (and the next, for the lookahead) for the whole wave
   bool rnd[HPT], rnd1[HPT];
@@ -227,7 +235,7 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
       if (!CACHED) kc[h] = rc_coeffs_t<false>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
       rc_apply_t<false>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
     }
-    pen[h] = deadband_l2(tg[h], p.deadband, Tn[h]);
+    pen[h] = deadband_l2(tg[h], p.deadband, reward_lag ? T[h] : Tn[h]);
     // x / 1.0 == x exactly: the default normaliser (integer target) costs no division
     const double tpen = p.alpha_temp * pen[h];
     rw[h] = p.penalty_mode == MDR_PEN_INDIVIDUAL_L2
@@ -250,12 +258,13 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
     sto(p.t_air, o8, make_double2(Tn[0], Tn[HPT - 1]));
     sto(p.t_mass, o8, make_double2(Tmn[0], Tmn[HPT - 1]));
     sto(p.hvac, i0 * 4u, make_uint2(w[0], w[HPT - 1]));
-    sto(reward, o8, make_double2(rw[0], rw[HPT - 1]));
+    if (write_rew) sto(reward, o8, make_double2(rw[0], rw[HPT - 1]));
   } else {
 #pragma unroll
     for (int h = 0; h < HPT; ++h)
       if (valid[h]) {
-        p.t_air[i0 + h] = Tn[h]; p.t_mass[i0 + h] = Tmn[h]; p.hvac[i0 + h] = w[h]; reward[i0 + h] = rw[h];
+        p.t_air[i0 + h] = Tn[h]; p.t_mass[i0 + h] = Tmn[h]; p.hvac[i0 + h] = w[h];
+        if (write_rew) reward[i0 + h] = rw[h];
       }
   }
   if (ctrl != MDR_CTRL_NONE && ctrl_out) {
@@ -303,7 +312,7 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
 #define MDR_INST_STEP(H, C, F, A, LA)                                                            \
   template __global__ void k_step_t<H, C, F, A, LA>(                                             \
       KParams, const uint8_t*, int, TickArgs, const TickArgs*, const unsigned long long*,        \
-      double*, int, uint8_t*, double*, int, unsigned long long*, unsigned long long*, double*);
+      double*, int, uint8_t*, double*, int, unsigned long long*, unsigned long long*, double*, int);
 MDR_INST_STEP(1, false, false, -1, -1)
 MDR_INST_STEP(2, false, false, -1, -1)
 MDR_INST_STEP(2, true, false, -1, -1)
@@ -409,6 +418,22 @@ __global__ void __launch_bounds__(256) k_reward_finalize(KParams p, TickArgs tk,
   else tp = (p.alpha_ind_l2 * pen + p.alpha_common_l2 * common_l2 + p.alpha_common_max * common_max) /
             (p.alpha_ind_l2 + p.alpha_common_l2 + p.alpha_common_max);
   reward[i] = -(p.alpha_temp * tp / p.norm_temp + sig_term);
+}
+
+// Reward of the last tick of an overlapped multi-GPU rollout (the k_step launches there write
+// the previous tick's reward): temperature penalty from the current state, signal term from the
+// tick's allreduced counts (rewards_calculator.py:135-203, individual_L2).
+__global__ void __launch_bounds__(256) k_reward_state(KParams p, const TickArgs* __restrict__ tkp,
+                                                      const unsigned long long* __restrict__ counts,
+                                                      double* __restrict__ reward, double* p_out) {
+  const double P = wave_power(counts, p.p_on, p.n_cap);
+  const double x = (P - tkp->s_prev) / (double)p.n_global;
+  const double sig_term = p.alpha_sig * (x * x) / p.norm_sig;
+  if (p_out && blockIdx.x == 0 && threadIdx.x == 0) *p_out = P;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const double tpen = p.alpha_temp * deadband_l2(p.target[i], p.deadband, p.t_air[i]);
+  reward[i] = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig_term);
 }
 
 // --------------------------------------------------------------------------------------- population

@@ -104,6 +104,7 @@ SIGNATURES = {
     "mdr_rccl_init": (I, [VP, VP, I, I]),
     "mdr_rccl_allreduce": (I, [VP, VP, I64, I, VP]),
     "mdr_rollout_sharded": (I, [VP, I, P(mdr_tick), VP, I64, I, VP, I64, VP, VP]),
+    "mdr_rollout_sharded_mode": (I, [VP, P(I), P(D), P(D)]),
     "mdr_probe_stream": (I, [VP, VP, VP]),
     "mdr_div_check": (I, [VP, VP, I64, VP, VP]),
     "mdr_event_record": (I, [VP, I, VP]),

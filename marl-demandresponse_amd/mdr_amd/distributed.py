@@ -71,6 +71,14 @@ class RcclComm:
                                               rew_stride, L.ptr(shard.p_dev), shard.stream()),
                 "mdr_rollout_sharded")
 
+    def pipeline(self, shard) -> dict:
+        """Which sharded rollout pipeline the library picked (mdr_rollout_sharded_mode)."""
+        m, s, o = C.c_int(), C.c_double(), C.c_double()
+        L.check(shard.lib.mdr_rollout_sharded_mode(shard.ctx, C.byref(m), C.byref(s), C.byref(o)),
+                "mdr_rollout_sharded_mode")
+        return {"mode": {-1: "undecided", 0: "serial", 1: "overlapped"}[m.value],
+                "calib_us_per_tick_serial": s.value, "calib_us_per_tick_overlapped": o.value}
+
     def ring_halo(self, shard, spec):
         """Message features of the houses just before / after this shard on the global ring."""
         import torch
@@ -141,6 +149,9 @@ class TorchComm(RcclComm):
         L.check(shard.lib.mdr_penalty_buffer(shard.ctx, C.byref(p)), "mdr_penalty_buffer")
         self.dist.all_reduce(device_view(p.value, 1, "<f8", shard.device))
         self.dist.all_reduce(device_view(p.value + 8, 1, "<f8", shard.device), op=self.dist.ReduceOp.MAX)
+
+    def pipeline(self, shard) -> dict:
+        return {"mode": "torch.distributed per-step"}
 
     def rollout(self, shard, ticks, actions, mode, rewards, rew_stride) -> None:
         for t, tk in enumerate(ticks):

@@ -2,7 +2,9 @@
 reproduce the single-process run on the same seeds.
 
 * world 1 over the library's own RCCL communicator (backend 'nccl'): exercises mdr_rccl_init,
-  mdr_rccl_allreduce and the C rollout loop mdr_rollout_sharded on a real device;
+  mdr_rccl_allreduce and the C rollout loop mdr_rollout_sharded on a real device: the serial
+  loop, the overlapped two-stream pipeline (reward written one launch later) and the default
+  calibration that runs half the rollout each way;
 * world 2 over torch.distributed/gloo (TorchComm) with both ranks on cuda:0: exercises the
   sharding, the per-tick count / penalty allreduces and the ring-halo observation exchange with
   the HIP kernels (RCCL cannot put two ranks on one GPU; the 8-GPU RCCL run is the driver's).
@@ -24,7 +26,7 @@ import golden_util as gu
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-T_STEP, T_BUF, T_ROLL = 5, 3, 6
+T_STEP, T_BUF, T_ROLL = 5, 3, 20  # a 20-tick rollout triggers the pipeline calibration
 
 
 def _overrides(n, mode):
@@ -57,6 +59,9 @@ def _worker(rank, world, port, backend, kind, n, mode, out_dir):
     import torch
     import torch.distributed as dist
 
+    if kind.startswith("rccl-"):  # force the serial / overlapped C loop (default: calibrate)
+        os.environ["MDR_SHARDED_OVERLAP"] = "0" if kind == "rccl-serial" else "1"
+        kind = "rccl"
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     kw = {"device_id": dev} if backend == "nccl" else {}
@@ -87,6 +92,8 @@ def _free_port():
 
 @pytest.mark.parametrize("backend,kind,world,n,mode", [
     ("nccl", "rccl", 1, 3001, "individual_L2"),
+    ("nccl", "rccl-serial", 1, 3001, "individual_L2"),
+    ("nccl", "rccl-overlap", 1, 3001, "individual_L2"),
     ("gloo", "torch", 2, 3001, "individual_L2"),
     ("gloo", "torch", 2, 2048, "common_L2"),
 ])
