@@ -120,8 +120,8 @@ typedef struct mdr_ctx mdr_ctx;
 
 /* ---- lifecycle ------------------------------------------------------------------------- */
 int mdr_abi_version(void);
-/* sizeof of the ABI structs, for binding checks: out[0..5] = mdr_config, mdr_soa, mdr_tick,
- * mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars; returns the number written */
+/* sizeof of the ABI structs, for binding checks: out[0..6] = mdr_config, mdr_soa, mdr_tick,
+ * mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars, mdr_actor_spec; returns the number written */
 int mdr_abi_sizes(int64_t* out, int n);
 const char* mdr_last_error(void);
 int mdr_create(mdr_ctx** out, const mdr_config* cfg);
@@ -235,6 +235,45 @@ int mdr_halo_pack(mdr_ctx* ctx, const mdr_obs_spec* spec, float* out, void* stre
 /* Next actions for the whole shard (single GPU: shard = cluster) from the current state: order
  * by -(T - target) ascending, then the reference's sequential take rule with budget S. */
 int mdr_ctrl_greedy(mdr_ctx* ctx, double budget, uint8_t* action, void* stream);
+
+/* ---- MA-PPO actor fused with the observation ----------------- */
+/* Replaces MAPPO.select_actions (server/app/core/agents/trainables/mappo.py:83-97) over
+ * norm_state_dict vectors (server/app/utils/norm.py:178-218) with Actor.forward
+ * (server/app/core/agents/trainables/network.py:29-33; actor_layers = [h1, h2], default [100, 100],
+ * server/app/core/agents/trainables/ppo.py:23-26): one persistent launch builds every house's obs
+ * row on chip, runs both hidden layers on MFMA, softmax + Categorical sampling in fp32. */
+enum { MDR_PREC_BF16 = 1,   /* bf16 products, fp32 accumulate (~4e-3 relative) */
+       MDR_PREC_BF16X3 = 3  /* split-bf16 (hi*hi + hi*lo + lo*hi), fp32 accumulate (~1e-5) */ };
+
+typedef struct mdr_actor_spec {
+  int32_t n_in;      /* obs features (= mdr_obs_spec.n_feat), <= 128 */
+  int32_t h1, h2;    /* hidden widths (actor_layers), each <= 128 */
+  int32_t n_act;     /* actions (num_action, 2), <= 4 */
+  int32_t precision; /* MDR_PREC_* */
+} mdr_actor_spec;
+
+/* Load (or replace, after a PPO update) the actor weights.  Device fp32 tensors in nn.Linear
+ * layout: w1 [h1][n_in], b1 [h1], w2 [h2][h1], b2 [h2], w3 [n_act][h2], b3 [n_act] (the
+ * reference Actor's fc.0 / fc.1 / fc.2).  They are packed into MFMA fragment order on `stream`. */
+int mdr_actor_load(mdr_ctx* ctx, const mdr_actor_spec* spec, const float* w1, const float* b1,
+                   const float* w2, const float* b2, const float* w3, const float* b3, void* stream);
+/* One select_actions over the shard.  Outputs (device, any may be NULL): action u8 [n_local],
+ * prob f32 [n_local] (probability of the sampled action, MAPPO.last_probs), probs f32
+ * [n_local][n_act], obs_out f32 [n_local][n_in].  Sampling: Philox4x32-10(seed, global house id,
+ * tick).  count_next != 0 also fills the cluster-power counts the sampled actions produce, so the
+ * next mdr_step(MDR_ACT_BUFFER) needs no mdr_power_counts. */
+int mdr_actor_act(mdr_ctx* ctx, const mdr_obs_spec* obs, const mdr_obs_scalars* sc, const double* p_dev,
+                  uint64_t tick, uint8_t* action, float* prob, float* probs, float* obs_out,
+                  int count_next, void* stream);
+/* n_ticks of (select_actions -> env.step) on device, hipGraph-captured when use_graph:
+ *   tick t: actor on the state after tick t-1 (obs scalars obs_sc[t]: p ignored — the cluster
+ *   power comes from p_dev, which each step rewrites), then the step with those actions.
+ * action [n_ticks][n_local] u8 / prob [n_ticks][n_local] f32 (stride 0 = overwrite one row) and
+ * reward [n_ticks][n_local] f64 (rew_stride 0 = one row).  p_dev: device double, in/out. */
+int mdr_actor_rollout(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const mdr_obs_scalars* obs_sc,
+                      const mdr_obs_spec* obs, uint8_t* action, int64_t act_stride, float* prob,
+                      int64_t prob_stride, double* reward, int64_t rew_stride, double* p_dev,
+                      int use_graph, void* stream);
 
 /* ---- multi-GPU (RCCL over xGMI) --------------------------------------------------------- */
 /* ncclUniqueId is 128 bytes; rank 0 creates it, the caller broadcasts it (torch.distributed). */

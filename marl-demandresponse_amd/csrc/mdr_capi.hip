@@ -15,6 +15,7 @@
 #include <tuple>
 #include <vector>
 
+#include "mdr_actor.h"
 #include "mdr_kernels.h"
 
 using namespace mdr;
@@ -108,6 +109,17 @@ struct mdr_ctx {
   hipStream_t comm_stream = nullptr;     // per-tick allreduce of the overlapped pipeline
   hipEvent_t ev_k1[kSlabs] = {}, ev_ar[kSlabs] = {}, ev_pc = nullptr;
   hipEvent_t ev[16] = {};
+  // MA-PPO actor (row P): packed weight image, per-tick obs scalars of actor rollouts
+  unsigned char* d_actor = nullptr;
+  size_t actor_cap = 0;
+  mdr_actor_spec actor{};
+  bool actor_ready = false;
+  int n_cu = 0;
+  double* d_obs_sc = nullptr;  // [ticks_cap][4]
+  double* h_obs_sc = nullptr;  // pinned staging
+  int obs_sc_cap = 0;
+  uint8_t* d_act = nullptr;    // [n_local] actor actions when the caller keeps none
+  std::map<std::vector<int64_t>, hipGraphExec_t> actor_graphs;
 };
 
 namespace {
@@ -199,11 +211,11 @@ extern "C" {
 int mdr_abi_version(void) { return MDR_ABI_VERSION; }
 
 int mdr_abi_sizes(int64_t* out, int n) {
-  const int64_t v[6] = {(int64_t)sizeof(mdr_config), (int64_t)sizeof(mdr_soa), (int64_t)sizeof(mdr_tick),
+  const int64_t v[7] = {(int64_t)sizeof(mdr_config), (int64_t)sizeof(mdr_soa), (int64_t)sizeof(mdr_tick),
                         (int64_t)sizeof(mdr_pop_spec), (int64_t)sizeof(mdr_obs_spec),
-                        (int64_t)sizeof(mdr_obs_scalars)};
+                        (int64_t)sizeof(mdr_obs_scalars), (int64_t)sizeof(mdr_actor_spec)};
   int k = 0;
-  for (; out && k < n && k < 6; ++k) out[k] = v[k];
+  for (; out && k < n && k < 7; ++k) out[k] = v[k];
   return k;
 }
 
@@ -288,6 +300,9 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
       return cleanup(fail(MDR_EHIP, "event"));
   if (hipEventCreateWithFlags(&c->ev_pc, hipEventDisableTiming) != hipSuccess)
     return cleanup(fail(MDR_EHIP, "event"));
+  if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess ||
+      c->n_cu < 1)
+    c->n_cu = 256;
   if (const char* e = getenv("MDR_SHARDED_OVERLAP")) c->overlap_mode = atoi(e) < 0 ? -1 : atoi(e) != 0;
   *out = c;
   return MDR_OK;
@@ -298,6 +313,11 @@ int mdr_destroy(mdr_ctx* c) {
   hipSetDevice(c->cfg.device);
   hipDeviceSynchronize();
   for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
+  for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
+  hipFree(c->d_actor);
+  hipFree(c->d_act);
+  hipFree(c->d_obs_sc);
+  if (c->h_obs_sc) hipHostFree(c->h_obs_sc);
   hipFree(c->d_tables);
   hipFree(c->d_coef);
   hipFree(c->d_flags);
@@ -540,15 +560,20 @@ static int expected_feat(const mdr_obs_spec* sp) {
   return base + sp->n_comm * mdr_msg_width(sp);
 }
 
+static int check_obs_spec(const mdr_obs_spec* sp, const char* who) {
+  if (sp->n_feat != expected_feat(sp)) return fail(MDR_EARG, std::string(who) + ": n_feat does not match the flags");
+  if (sp->n_comm < 0 || sp->n_comm > 64) return fail(MDR_EARG, std::string(who) + ": n_comm out of range");
+  if (sp->comm_mode == MDR_COMM_TABLE && sp->n_comm > 0 && !sp->comm_table)
+    return fail(MDR_EARG, std::string(who) + ": TABLE mode without a table");
+  if (sp->comm_mode == MDR_COMM_TABLE && mdr_msg_width(sp) > 16) return fail(MDR_EARG, std::string(who) + ": msg width");
+  return MDR_OK;
+}
+
 int mdr_obs(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc, const double* p_dev,
             float* obs, void* stream) {
   if (!c || !sp || !sc || !obs) return fail(MDR_EARG, "mdr_obs: null argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_obs: context not bound");
-  if (sp->n_feat != expected_feat(sp)) return fail(MDR_EARG, "mdr_obs: n_feat does not match the flags");
-  if (sp->n_comm < 0 || sp->n_comm > 64) return fail(MDR_EARG, "mdr_obs: n_comm out of range");
-  if (sp->comm_mode == MDR_COMM_TABLE && sp->n_comm > 0 && !sp->comm_table)
-    return fail(MDR_EARG, "mdr_obs: TABLE mode without a table");
-  if (sp->comm_mode == MDR_COMM_TABLE && mdr_msg_width(sp) > 16) return fail(MDR_EARG, "mdr_obs: msg width");
+  if (int rc = check_obs_spec(sp, "mdr_obs")) return rc;
   ObsArgs o = obs_args(c, sp, sc);
   const int lo = sp->n_comm / 2, hi = (sp->n_comm + 1) / 2;
   size_t tile = ((size_t)kObsBlock * sp->n_feat + 3) & ~(size_t)3;
@@ -823,6 +848,208 @@ int mdr_event_elapsed_ms(mdr_ctx* c, int s0, int s1, float* ms) {
   if (!c || !ms || s0 < 0 || s1 < 0 || s0 >= 16 || s1 >= 16) return fail(MDR_EARG, "mdr_event_elapsed_ms: bad slot");
   HIP_TRY(hipEventSynchronize(c->ev[s1]));
   HIP_TRY(hipEventElapsedTime(ms, c->ev[s0], c->ev[s1]));
+  return MDR_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------------------ actor
+namespace {
+
+int align16(int x) { return (x + 15) & ~15; }
+
+// Packed-image offsets + the LDS plan of k_actor for `nw` waves per block.
+ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw) {
+  ActorDims d{};
+  d.n_in = a.n_in; d.h1 = a.h1; d.h2 = a.h2; d.n_act = a.n_act;
+  d.ks1 = (a.n_in + 15) / 16;
+  d.ks2 = (a.h1 + 15) / 16;
+  int fs = (a.n_in + 3) & ~3;
+  if (((fs / 4) & 1) == 0) fs += 4;  // odd multiple of 16 B: conflict-free ds_read_b128 rows
+  d.fs = fs;
+  d.off_w1 = 0;
+  d.off_w2 = kActorMB * d.ks1 * 2048;
+  d.off_tail = d.off_w2 + kActorMB * d.ks2 * 2048;
+  d.off_end = align16(d.off_tail + ((2 + a.n_act) * kActorRows + a.n_act) * 4);
+  const int HB = 32 * nw;
+  const int K = sp ? sp->n_comm : 0, M = sp ? mdr_msg_width(sp) : 0;
+  d.lds_obs = d.off_end;
+  d.lds_msg = d.lds_obs + align16((HB * fs + 16 * d.ks1) * 4);
+  const int nmsg = (sp && sp->comm_mode == MDR_COMM_RING) ? (K / 2 + HB + (K + 1) / 2) * M : 0;
+  d.lds_hw = d.lds_msg + align16(nmsg * 4);
+  d.lds_hist = d.lds_hw + HB * 4;
+  d.lds_total = d.lds_hist + MDR_MAX_CAP * 4;
+  return d;
+}
+
+int actor_plan(const mdr_ctx* c, const mdr_obs_spec* sp, ActorDims* d, int* nw) {
+  for (int w = 8; w >= 2; w >>= 1) {
+    *d = actor_layout(c->actor, sp, w);
+    if (d->lds_total <= 160 * 1024) { *nw = w; return MDR_OK; }
+  }
+  return fail(MDR_EARG, "mdr_actor: weights + obs rows exceed the 160 KiB LDS of a CU");
+}
+
+int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const double* p_dev, uint64_t tick,
+                 const TickArgs* tkp, const ActorOut& out, hipStream_t st) {
+  ActorDims d;
+  int nw = 0;
+  if (int rc = actor_plan(c, sp, &d, &nw)) return rc;
+  const int64_t ntile = (c->kp.n + 32 * nw - 1) / (32 * nw);
+  const unsigned grid = (unsigned)std::min<int64_t>(ntile, (int64_t)c->n_cu);
+  static bool lds_attr = false;  // > 64 KiB of dynamic LDS must be opted into per kernel
+  if (!lds_attr) {
+    HIP_TRY(hipFuncSetAttribute((const void*)k_actor<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_TRY(hipFuncSetAttribute((const void*)k_actor<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    lds_attr = true;
+  }
+  if (c->actor.precision == MDR_PREC_BF16)
+    hipLaunchKernelGGL(k_actor<1>, dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, c->d_actor, out, tick, tkp);
+  else
+    hipLaunchKernelGGL(k_actor<3>, dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, c->d_actor, out, tick, tkp);
+  LAUNCH_CHECK("k_actor");
+  return MDR_OK;
+}
+
+int check_actor_obs(const mdr_ctx* c, const mdr_obs_spec* sp, const char* who) {
+  if (!c->actor_ready) return fail(MDR_ESTATE, std::string(who) + ": no actor loaded (mdr_actor_load)");
+  if (int rc = check_obs_spec(sp, who)) return rc;
+  if (sp->n_feat != c->actor.n_in) return fail(MDR_EARG, std::string(who) + ": obs n_feat != actor n_in");
+  return MDR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mdr_actor_load(mdr_ctx* c, const mdr_actor_spec* a, const float* w1, const float* b1, const float* w2,
+                   const float* b2, const float* w3, const float* b3, void* stream) {
+  if (!c || !a || !w1 || !b1 || !w2 || !b2 || !w3 || !b3) return fail(MDR_EARG, "mdr_actor_load: null argument");
+  if (a->n_in < 1 || a->n_in > kActorMaxIn || a->h1 < 1 || a->h1 > kActorRows || a->h2 < 1 ||
+      a->h2 > kActorRows || a->n_act < 2 || a->n_act > kActorMaxAct)
+    return fail(MDR_EARG, "mdr_actor_load: shape outside n_in <= 128, hidden <= 128, 2 <= n_act <= 4");
+  if (a->precision != MDR_PREC_BF16 && a->precision != MDR_PREC_BF16X3)
+    return fail(MDR_EARG, "mdr_actor_load: bad precision");
+  const ActorDims d = actor_layout(*a, nullptr, 2);
+  if ((size_t)d.off_end > c->actor_cap) {
+    HIP_TRY(hipStreamSynchronize(S(stream)));
+    hipFree(c->d_actor);
+    c->d_actor = nullptr;
+    HIP_TRY(hipMalloc(&c->d_actor, d.off_end));
+    c->actor_cap = d.off_end;
+    for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
+    c->actor_graphs.clear();
+  }
+  const int nthreads = (kActorMB * (d.ks1 + d.ks2) + 1) * 64;
+  hipLaunchKernelGGL(k_actor_pack, dim3(blocks(nthreads, 256)), dim3(256), 0, S(stream), d, w1, b1, w2, b2, w3,
+                     b3, c->d_actor);
+  LAUNCH_CHECK("k_actor_pack");
+  c->actor = *a;
+  c->actor_ready = true;
+  return MDR_OK;
+}
+
+int mdr_actor_act(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc, const double* p_dev,
+                  uint64_t tick, uint8_t* action, float* prob, float* probs, float* obs_out, int count_next,
+                  void* stream) {
+  if (!c || !sp || !sc) return fail(MDR_EARG, "mdr_actor_act: null argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_act: context not bound");
+  if (int rc = check_actor_obs(c, sp, "mdr_actor_act")) return rc;
+  hipStream_t st = S(stream);
+  ActorOut out{action, prob, probs, obs_out, nullptr};
+  if (count_next) {
+    // the counts of the tick these actions drive go into the current slab (from zero)
+    out.count_next = slab_at(c, c->ring);
+    HIP_TRY(hipMemsetAsync(out.count_next, 0, c->slab_len * sizeof(unsigned long long), st));
+  }
+  if (int rc = launch_actor(c, sp, obs_args(c, sp, sc), p_dev, tick, nullptr, out, st)) return rc;
+  if (count_next) c->counts_ready = true;
+  return MDR_OK;
+}
+
+int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_scalars* osc,
+                      const mdr_obs_spec* sp, uint8_t* action, int64_t act_stride, float* prob,
+                      int64_t prob_stride, double* reward, int64_t rew_stride, double* p_dev, int use_graph,
+                      void* stream) {
+  if (!c || !ticks || !osc || !sp || !reward || !p_dev || n < 1) return fail(MDR_EARG, "mdr_actor_rollout: bad argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_rollout: context not bound");
+  if (int rc = check_actor_obs(c, sp, "mdr_actor_rollout")) return rc;
+  if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
+    return fail(MDR_EARG, "mdr_actor_rollout: common penalty modes need the per-step API");
+  hipStream_t st = S(stream);
+  if (int rc = refresh_if_dirty(c, st)) return rc;
+  if (int rc = stage_ticks(c, n, ticks, st)) return rc;
+  // per-tick obs scalars [s, solar, t_od, -] next to the tick drivers
+  if (n > c->obs_sc_cap) {
+    HIP_TRY(hipStreamSynchronize(st));
+    hipFree(c->d_obs_sc);
+    if (c->h_obs_sc) hipHostFree(c->h_obs_sc);
+    c->d_obs_sc = nullptr;
+    c->h_obs_sc = nullptr;
+    const int cap = n < 64 ? 64 : n;
+    HIP_TRY(hipMalloc(&c->d_obs_sc, (size_t)cap * 4 * sizeof(double)));
+    HIP_TRY(hipHostMalloc(&c->h_obs_sc, (size_t)cap * 4 * sizeof(double), hipHostMallocDefault));
+    c->obs_sc_cap = cap;
+    for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
+    c->actor_graphs.clear();
+  }
+  HIP_TRY(hipEventSynchronize(c->ticks_free));  // (stage_ticks' event also covers this buffer)
+  for (int t = 0; t < n; ++t) {
+    c->h_obs_sc[4 * t] = osc[t].s;
+    c->h_obs_sc[4 * t + 1] = osc[t].solar;
+    c->h_obs_sc[4 * t + 2] = osc[t].t_od;
+    c->h_obs_sc[4 * t + 3] = 0.0;
+  }
+  HIP_TRY(hipMemcpyAsync(c->d_obs_sc, c->h_obs_sc, (size_t)n * 4 * sizeof(double), hipMemcpyHostToDevice, st));
+  HIP_TRY(hipEventRecord(c->ticks_free, st));
+
+  ObsArgs o = obs_args(c, sp, &osc[0]);
+  auto launches = [&]() -> int {
+    HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
+    c->ring = 0;
+    for (int t = 0; t < n; ++t) {
+      // the current slab is zero here: the memset above (t = 0), then the previous two steps
+      // (each zeroes the slab two ahead and a BUFFER step writes no lookahead)
+      ObsArgs ot = o;
+      ot.sc_dev = c->d_obs_sc + 4 * t;
+      ActorOut out{action ? action + (int64_t)t * act_stride : c->d_act, prob ? prob + (int64_t)t * prob_stride : nullptr,
+                   nullptr, nullptr, slab_at(c, c->ring)};
+      if (int rc = launch_actor(c, sp, ot, p_dev, 0, c->d_ticks + t, out, st)) return rc;
+      if (int rc = launch_step(c, out.action, MDR_ACT_BUFFER, TickArgs{}, c->d_ticks + t,
+                               reward + (int64_t)t * rew_stride, 0, MDR_CTRL_NONE, nullptr, p_dev, st))
+        return rc;
+    }
+    return MDR_OK;
+  };
+  if (!action && !c->d_act) HIP_TRY(hipMalloc(&c->d_act, c->kp.n));  // context-owned action row
+  if (!use_graph) {
+    const int rc = launches();
+    c->counts_ready = false;
+    return rc;
+  }
+  if (st == nullptr) return fail(MDR_EARG, "mdr_actor_rollout: graph capture needs a non-default stream");
+  std::vector<int64_t> key{n, (int64_t)(uintptr_t)action, act_stride, (int64_t)(uintptr_t)prob, prob_stride,
+                           (int64_t)(uintptr_t)reward, rew_stride, (int64_t)(uintptr_t)p_dev,
+                           (int64_t)(uintptr_t)stream, (int64_t)(uintptr_t)sp->comm_table,
+                           (int64_t)(uintptr_t)sp->halo_msg, sp->n_feat, (int64_t)(uintptr_t)c->d_actor};
+  auto it = c->actor_graphs.find(key);
+  if (it == c->actor_graphs.end()) {
+    hipGraph_t g;
+    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
+    const int rc = launches();
+    hipError_t e = hipStreamEndCapture(st, &g);
+    if (rc) return rc;
+    if (e != hipSuccess) return fail(MDR_EHIP, std::string("capture: ") + hipGetErrorString(e));
+    hipGraphExec_t ex;
+    e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+    hipGraphDestroy(g);
+    if (e != hipSuccess) return fail(MDR_EHIP, std::string("instantiate: ") + hipGetErrorString(e));
+    it = c->actor_graphs.emplace(key, ex).first;
+  } else {
+    c->ring = n % 3;
+  }
+  HIP_TRY(hipGraphLaunch(it->second, st));
+  c->counts_ready = false;
   return MDR_OK;
 }
 

@@ -53,6 +53,7 @@ struct ObsArgs {
   const float* halo_msg;  // [lo + hi][msg_w] or null
   double norm_reg_sig, cfg_ua, cfg_ca, cfg_cm, cfg_hm, cfg_cop, cfg_lcf, cfg_cap;
   double p, s, solar, t_od;
+  const double* sc_dev;  // per-tick device scalars [s, solar, t_od] overriding the values above, or null
 };
 
 __global__ void k_power_counts(KParams p, const uint8_t* action, int action_mode, uint64_t tick,

@@ -8,6 +8,7 @@
 #include "mdr_kernels.h"
 
 #include "mdr_device.h"
+#include "mdr_obs_dev.h"
 
 namespace mdr {
 
@@ -469,103 +470,21 @@ __global__ void __launch_bounds__(256) k_populate(KParams p, PopArgs a) {
 
 // --------------------------------------------------------------------------------------- obs
 // norm_state_dict (norm.py:178-218) as float32 rows, staged through LDS and flushed with
-// 16-B coalesced stores.  Message sources for a block [b0, b0+B) of the ring topology are the
-// houses [b0 - lo, b0 + B + hi); their message features are computed once into LDS.
-__device__ __forceinline__ void msg_features(const KParams& p, const ObsArgs& o, int64_t j,
-                                             float* dst) {
-  const uint32_t w = p.hvac[j];
-  const int cls = p.cap_idx[j];
-  const double pmax = p.p_on[cls];
-  const double R = o.norm_reg_sig;
-  dst[0] = (float)((p.t_air[j] - p.target[j]) / 5.0);
-  dst[1] = (float)trunc((double)hv_sso(w) / (double)p.L);
-  dst[2] = (float)((hv_on(w) ? pmax : 0.0) / R);
-  dst[3] = (float)(pmax / R);
-  int f = 4;
-  if (o.msg_thermal) {
-    dst[f++] = (float)(p.ua[j] / o.cfg_ua);
-    dst[f++] = (float)(p.ca[j] / o.cfg_ca);
-    dst[f++] = (float)(p.cm[j] / o.cfg_cm);
-    dst[f++] = (float)(p.hm[j] / o.cfg_hm);
-  }
-  if (o.msg_hvac) {
-    dst[f++] = (float)o.cfg_cop;
-    dst[f++] = (float)o.cfg_lcf;
-    dst[f++] = (float)o.cfg_cap;
-  }
-}
-
+// 16-B coalesced stores.  Row assembly: mdr_obs_dev.h (shared with the fused actor kernel).
 __global__ void __launch_bounds__(kObsBlock) k_obs(KParams p, ObsArgs o, const double* p_dev,
                                                    float* __restrict__ obs) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int F = o.n_feat, M = o.msg_w, K = o.n_comm;
-  const int lo = K / 2, hi = (K + 1) / 2;
+  const int F = o.n_feat;
   const int64_t b0 = (int64_t)blockIdx.x * kObsBlock;
   const int nb = (int)min((int64_t)kObsBlock, p.n - b0);
   float* tile = smem;                                  // [kObsBlock][F]
   float* msg = smem + ((kObsBlock * F + 3) & ~3);      // [lo + kObsBlock + hi][M]
   const double P = p_dev ? *p_dev : o.p;
-  const double R = o.norm_reg_sig;
 
-  if (o.comm_mode == MDR_COMM_RING && K > 0) {
-    const int nsrc = lo + nb + hi;
-    for (int s = threadIdx.x; s < nsrc; s += kObsBlock) {
-      int64_t j = b0 - lo + s;              // local index, may fall outside the shard
-      if (o.halo_msg && (j < 0 || j >= p.n)) {
-        // multi-GPU ring: [0, lo) = houses before the shard, [lo, lo+hi) = houses after it
-        const int h = j < 0 ? (int)(j + lo) : (int)(lo + (j - p.n));
-        for (int m = 0; m < M; ++m) msg[s * M + m] = o.halo_msg[h * M + m];
-      } else {
-        j %= p.n;
-        if (j < 0) j += p.n;
-        msg_features(p, o, j, msg + s * M);
-      }
-    }
-  }
+  obs_stage_ring(p, o, b0, nb, msg, threadIdx.x, kObsBlock);
   __syncthreads();
   const int t = threadIdx.x;
-  if (t < nb) {
-    const int64_t i = b0 + t;
-    float* row = tile + t * F;
-    const uint32_t w = p.hvac[i];
-    int f = 0;
-    row[f++] = hv_on(w) ? 1.f : 0.f;
-    row[f++] = hv_lock(w) ? 1.f : 0.f;
-    row[f++] = (float)trunc((double)hv_sso(w) / (double)p.L);
-    row[f++] = 1.f;  // int(lockout_duration / lockout_duration)
-    if (o.hvac_state) { row[f++] = (float)(o.cfg_cop / o.cfg_cop); row[f++] = (float)(o.cfg_lcf / o.cfg_lcf); }
-    row[f++] = (float)(P / R);
-    row[f++] = (float)(o.s / (R * (double)p.n_global));
-    row[f++] = (float)p.deadband;
-    const double tgt = p.target[i];
-    row[f++] = (float)((p.t_air[i] - 20.0) / 5.0);
-    row[f++] = (float)((p.t_mass[i] - 20.0) / 5.0);
-    row[f++] = (float)((tgt - 20.0) / 5.0);
-    if (o.solar_state) row[f++] = (float)(o.solar / 1000.0);
-    if (o.thermal_state) {
-      row[f++] = (float)(p.ua[i] / o.cfg_ua);
-      row[f++] = (float)(p.ca[i] / o.cfg_ca);
-      row[f++] = (float)(p.cm[i] / o.cfg_cm);
-      row[f++] = (float)(p.hm[i] / o.cfg_hm);
-      row[f++] = (float)((o.t_od - 20.0) / 5.0);
-    }
-    if (K > 0) {
-      if (o.comm_mode == MDR_COMM_RING) {
-        // neighbours [i-lo .. i-1, i+1 .. i+hi] (agent_communication_builder.py:65-83)
-        for (int k = 0; k < K; ++k) {
-          const int s = k < lo ? (t + k) : (t + lo + 1 + (k - lo));
-          for (int m = 0; m < M; ++m) row[f++] = msg[s * M + m];
-        }
-      } else {
-        float tmp[16];
-        for (int k = 0; k < K; ++k) {
-          const int64_t j = o.comm_table[i * K + k];
-          msg_features(p, o, j, tmp);
-          for (int m = 0; m < M; ++m) row[f++] = tmp[m];
-        }
-      }
-    }
-  }
+  if (t < nb) obs_build_row(p, o, P, b0 + t, t, msg, tile + t * F);
   __syncthreads();
   // coalesced flush of the contiguous tile obs[b0 .. b0+nb) rows
   const int64_t nflt = (int64_t)nb * F;

@@ -77,6 +77,14 @@ class mdr_obs_scalars(C.Structure):
     _fields_ = [("p", C.c_double), ("s", C.c_double), ("solar", C.c_double), ("t_od", C.c_double)]
 
 
+class mdr_actor_spec(C.Structure):
+    _fields_ = [("n_in", C.c_int32), ("h1", C.c_int32), ("h2", C.c_int32), ("n_act", C.c_int32),
+                ("precision", C.c_int32)]
+
+
+PREC_BF16, PREC_BF16X3 = 1, 3
+PRECISIONS = {"bf16": PREC_BF16, "bf16x3": PREC_BF16X3}
+
 P, VP, I, I64, U64, D = C.POINTER, C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_double
 
 # name -> (restype, argtypes); every symbol declared in include/mdr.h
@@ -100,6 +108,10 @@ SIGNATURES = {
     "mdr_obs": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, VP, VP]),
     "mdr_halo_pack": (I, [VP, P(mdr_obs_spec), VP, VP]),
     "mdr_ctrl_greedy": (I, [VP, D, VP, VP]),
+    "mdr_actor_load": (I, [VP, P(mdr_actor_spec), VP, VP, VP, VP, VP, VP, VP]),
+    "mdr_actor_act": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, U64, VP, VP, VP, VP, I, VP]),
+    "mdr_actor_rollout": (I, [VP, I, P(mdr_tick), P(mdr_obs_scalars), P(mdr_obs_spec), VP, I64, VP, I64,
+                              VP, I64, VP, I, VP]),
     "mdr_rccl_unique_id": (I, [VP]),
     "mdr_rccl_init": (I, [VP, VP, I, I]),
     "mdr_rccl_allreduce": (I, [VP, VP, I64, I, VP]),
@@ -137,10 +149,10 @@ def load(path: str = LIB_PATH):
             fn.argtypes = args
         if lib.mdr_abi_version() != ABI_VERSION:
             raise MdrLibraryError("libmdr_hip.so ABI version mismatch; rebuild it")
-        sizes = (C.c_int64 * 6)()
-        lib.mdr_abi_sizes(sizes, 6)
+        sizes = (C.c_int64 * 7)()
+        lib.mdr_abi_sizes(sizes, 7)
         want = [C.sizeof(t) for t in (mdr_config, mdr_soa, mdr_tick, mdr_pop_spec, mdr_obs_spec,
-                                      mdr_obs_scalars)]
+                                      mdr_obs_scalars, mdr_actor_spec)]
         if list(sizes) != want:
             raise MdrLibraryError(f"ABI struct sizes differ: library {list(sizes)} vs binding {want}")
         _lib = lib

@@ -1,0 +1,156 @@
+"""MA-PPO actor on the device, fused with the observation.
+
+Reference:
+  * ``Actor`` — server/app/core/agents/trainables/network.py:14-33: Linear(num_state, l0), ReLU, ...,
+    Linear(l_last, num_action), softmax; ``actor_layers`` default [100, 100]
+    (server/app/core/agents/trainables/ppo.py:23-26).
+  * ``MAPPO.select_actions`` — server/app/core/agents/trainables/mappo.py:83-97: one batch-1 forward
+    per agent over ``norm_state_dict`` (server/app/utils/norm.py:178-218), ``Categorical(p).sample()``,
+    ``last_probs[i] = p[action]``.
+
+``Actor`` here is the same torch module (same parameter names ``fc.0 / fc.1 / fc.2``, so a reference
+``state_dict`` loads unchanged); it is the training-side network.  ``DeviceActor`` binds its
+weights to an ``Environment`` shard and runs ``select_actions`` for every house as ONE HIP launch
+(``mdr_actor_act``): obs rows built on chip, both hidden layers on MFMA (split-bf16 by default,
+~1e-5 of fp32), softmax + sampling in fp32.  ``rollout`` chains actor -> env.step for n ticks in one
+hipGraph (``mdr_actor_rollout``).  There is no CPU path: the library raises when it is missing.
+"""
+from __future__ import annotations
+
+import json
+from typing import Optional
+
+import numpy as np
+
+from . import _lib as L
+
+
+def _torch():
+    import torch
+
+    return torch
+
+
+def make_actor(num_state: int, num_action: int = 2, layers=(100, 100), seed: Optional[int] = 1):
+    """The reference Actor (network.py:14-33) as a torch module; ``seed`` reproduces
+    ``torch.manual_seed(seed)`` before construction like MAPPO.__init__ (mappo.py:41-42)."""
+    torch = _torch()
+    nn = torch.nn
+
+    class Actor(nn.Module):
+        def __init__(self):
+            super().__init__()
+            ls = json.loads(layers) if isinstance(layers, str) else list(layers)
+            self.layers = [int(x) for x in ls]
+            self.fc = nn.ModuleList([nn.Linear(num_state, self.layers[0])])
+            self.fc.extend([nn.Linear(self.layers[i], self.layers[i + 1]) for i in range(len(self.layers) - 1)])
+            self.fc.append(nn.Linear(self.layers[-1], num_action))
+
+        def forward(self, x):
+            for i in range(len(self.layers)):
+                x = torch.nn.functional.relu(self.fc[i](x))
+            return torch.nn.functional.softmax(self.fc[len(self.layers)](x), dim=1)
+
+    if seed is not None:
+        torch.manual_seed(seed)
+    return Actor()
+
+
+class DeviceActor:
+    """``MAPPO.select_actions`` for every house of an Environment shard in one launch."""
+
+    def __init__(self, env, actor, precision: str = "bf16x3"):
+        if precision not in L.PRECISIONS:
+            raise ValueError(f"precision must be one of {sorted(L.PRECISIONS)}")
+        if len(actor.layers) != 2:
+            raise NotImplementedError("the fused actor kernel takes two hidden layers (actor_layers = [h1, h2])")
+        self.env = env
+        self.actor = actor
+        self.precision = precision
+        self.n_in = actor.fc[0].in_features
+        self.n_act = actor.fc[-1].out_features
+        self.load_weights()
+
+    def load_weights(self):
+        """(Re)pack the actor's current fp32 weights (call after every optimiser step)."""
+        torch = _torch()
+        sh = self.env.shard
+        dev = sh.device
+        ws = []
+        for lin in self.actor.fc:
+            ws.append(lin.weight.detach().to(device=dev, dtype=torch.float32).contiguous())
+            ws.append(lin.bias.detach().to(device=dev, dtype=torch.float32).contiguous())
+        spec = L.mdr_actor_spec(self.n_in, self.actor.fc[0].out_features, self.actor.fc[1].out_features,
+                                self.n_act, L.PRECISIONS[self.precision])
+        sh.actor_load(spec, *ws)
+        torch.cuda.current_stream(dev).synchronize()  # the packed image is read by later launches only
+
+    def _check_obs(self, spec):
+        if spec.n_feat != self.n_in:
+            raise ValueError(f"actor expects {self.n_in} obs features, the environment produces {spec.n_feat}")
+
+    def select_actions(self, action=None, prob=None, probs=None, obs_out=None, count_next: bool = True):
+        """Actions for the NEXT env.step of every local house (mappo.py:83-97), on device.
+        Returns (action u8 [n_local], prob f32 [n_local]).  With ``count_next`` the launch also
+        counts the cluster power these actions produce, so ``env.step_tensor(action)`` is one
+        launch."""
+        torch = _torch()
+        env = self.env
+        sh = env.shard
+        spec, sc, keep = env.bound_obs_spec()
+        self._check_obs(spec)
+        n = env.n_local
+        if action is None:
+            action = torch.empty(n, dtype=torch.uint8, device=sh.device)
+        if prob is None:
+            prob = torch.empty(n, dtype=torch.float32, device=sh.device)
+        sh.actor_act(spec, sc, env._tick, action, prob, probs, obs_out, count_next, use_p_dev=env._P_dev_valid)
+        if keep:
+            torch.cuda.current_stream(sh.device).synchronize()
+        env._counts_ready = ("actor", action.data_ptr()) if count_next else 0
+        return action, prob
+
+    def rollout(self, n_ticks: int, rewards=None, actions=None, probs=None, use_graph: bool = True):
+        """n_ticks of (select_actions -> env.step) in one graph-captured C call (single shard,
+        individual_L2).  ``rewards`` float64 [n_ticks, N] (or [N], overwritten each tick);
+        ``actions`` u8 / ``probs`` f32 [n_ticks, N] (or [N]) optional outputs."""
+        torch = _torch()
+        env = self.env
+        sh = env.shard
+        if env.world > 1:
+            raise NotImplementedError("sharded actor rollouts: loop select_actions / step_tensor")
+        if sh.penalty_mode != 0:
+            raise NotImplementedError("actor rollouts support individual_L2; use step_tensor")
+        spec, _sc, keep = env.bound_obs_spec()
+        self._check_obs(spec)
+        n = env.n_local
+        if rewards is None:
+            rewards = torch.empty((n_ticks, n), dtype=torch.float64, device=sh.device)
+        rs = 0 if rewards.dim() == 1 else n
+        as_ = 0 if actions is None or actions.dim() == 1 else n
+        ps = 0 if probs is None or probs.dim() == 1 else n
+        if not env._P_dev_valid:
+            sh.p_dev.fill_(float(env._P_host))
+        solar0 = float(env._solar)
+        ticks = env.driver_window(n_ticks)
+        # obs before tick t: signal / OD temperature after tick t-1 (= tick t's s_prev, t_od_prev),
+        # solar gain of tick t-1's datetime
+        osc = [L.mdr_obs_scalars(0.0, t.s_prev, solar0 if i == 0 else ticks[i - 1].solar, t.t_od_prev)
+               for i, t in enumerate(ticks)]
+        sh.actor_rollout(ticks, osc, spec, actions, as_, probs, ps, rewards, rs, use_graph)
+        if keep:
+            torch.cuda.current_stream(sh.device).synchronize()
+        env._counts_ready = 0
+        env._P_dev_valid = True
+        return rewards
+
+
+def reference_probs(actor, obs):
+    """Actor.forward in torch fp32 (the reference network on the same obs) — test helper."""
+    torch = _torch()
+    with torch.no_grad():
+        return actor(obs.float())
+
+
+def to_numpy(x) -> np.ndarray:
+    return x.detach().cpu().numpy()

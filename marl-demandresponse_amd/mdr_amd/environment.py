@@ -207,7 +207,9 @@ class Environment:
         self._tod_prev = self.current_od_temp
         self._s_prev = self.power_grid.current_signal
         tick = self._tick_args()
-        if mode == L.ACT_BUFFER or self._counts_ready != mode:
+        if mode == L.ACT_BUFFER and self._counts_ready == ("actor", actions.data_ptr()):
+            pass  # the actor launch that wrote these actions also counted their cluster power
+        elif mode == L.ACT_BUFFER or self._counts_ready != mode:
             # phase 1 (unless the previous launch already counted this tick under the same source)
             if mode in (L.ACT_BUFFER, L.ACT_RANDOM, L.ACT_ALWAYS_ON):
                 sh.power_counts(actions, mode, self._tick)
@@ -371,14 +373,14 @@ class Environment:
         spec.cfg_cap = float(hp.hvac_prop.cooling_capacity)
         return spec
 
-    def obs_tensor(self, out=None):
-        """``norm_state_dict`` for every local house as float32 [n_local, F] on device."""
+    def bound_obs_spec(self):
+        """(spec, scalars, keep): the obs spec with its device tables bound (comm table, ring halo
+        of the neighbouring shards), the tick's obs scalars, and the tensors that must stay alive
+        until the launch that reads them has run."""
         import torch
 
         sh = self._shard
         spec = self.obs_spec()
-        if out is None:
-            out = torch.empty((self._n_local, spec.n_feat), dtype=torch.float32, device=sh.device)
         keep = []
         if spec.comm_mode == L.COMM_TABLE and spec.n_comm > 0:
             if self.world > 1:
@@ -392,6 +394,16 @@ class Environment:
             spec.halo_msg = L.ptr(halo)
         sc = L.mdr_obs_scalars(float(self._P_host), float(self.power_grid.current_signal),
                                float(self._solar), float(self.current_od_temp))
+        return spec, sc, keep
+
+    def obs_tensor(self, out=None):
+        """``norm_state_dict`` for every local house as float32 [n_local, F] on device."""
+        import torch
+
+        sh = self._shard
+        spec, sc, keep = self.bound_obs_spec()
+        if out is None:
+            out = torch.empty((self._n_local, spec.n_feat), dtype=torch.float32, device=sh.device)
         sh.obs(spec, sc, out, use_p_dev=self._P_dev_valid)
         if keep:
             torch.cuda.current_stream(sh.device).synchronize()

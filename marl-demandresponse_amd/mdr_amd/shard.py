@@ -192,6 +192,37 @@ class HipShard:
                                  L.ptr(self.p_dev) if use_p_dev else 0, L.ptr(out), self.stream()),
                 "mdr_obs")
 
+    # ------------------------------------------------------------------ MA-PPO actor (row P)
+    def actor_load(self, spec, w1, b1, w2, b2, w3, b3):
+        L.check(self.lib.mdr_actor_load(self.ctx, C.byref(spec), *(L.ptr(t) for t in (w1, b1, w2, b2, w3, b3)),
+                                        self.stream()), "mdr_actor_load")
+
+    def actor_act(self, spec, scalars, tick, action, prob, probs, obs_out, count_next, use_p_dev=True):
+        L.check(self.lib.mdr_actor_act(self.ctx, C.byref(spec), C.byref(scalars),
+                                       L.ptr(self.p_dev) if use_p_dev else 0, int(tick), L.ptr(action),
+                                       L.ptr(prob), L.ptr(probs), L.ptr(obs_out), int(count_next),
+                                       self.stream()), "mdr_actor_act")
+
+    def actor_rollout(self, ticks, obs_sc, spec, action, act_stride, prob, prob_stride, reward, rew_stride,
+                      use_graph=True):
+        """n ticks of actor -> step in one C call (graph-captured on the shard's side stream)."""
+        n = len(ticks)
+        arr = (L.mdr_tick * n)(*ticks)
+        sca = (L.mdr_obs_scalars * n)(*obs_sc)
+        torch = self.torch
+        cur = torch.cuda.current_stream(self.device)
+        if use_graph:
+            s = self.launch_stream(True)
+            s.wait_stream(cur)
+            handle = s.cuda_stream
+        else:
+            handle = cur.cuda_stream
+        L.check(self.lib.mdr_actor_rollout(self.ctx, n, arr, sca, C.byref(spec), L.ptr(action), act_stride,
+                                           L.ptr(prob), prob_stride, L.ptr(reward), rew_stride, L.ptr(self.p_dev),
+                                           int(use_graph), handle), "mdr_actor_rollout")
+        if use_graph:
+            cur.wait_stream(self._side)
+
     def halo_pack(self, spec, out):
         L.check(self.lib.mdr_halo_pack(self.ctx, C.byref(spec), L.ptr(out), self.stream()), "mdr_halo_pack")
 

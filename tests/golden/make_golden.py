@@ -22,6 +22,8 @@ Fixtures (names follow SURVEY §8(c) F1..F9):
   F7 greedy.npz        GreedyMyopic decisions along a trajectory
   F8 comm.json         neighbour tables for the deterministic comm modes (+ random_fixed seeded)
   F9 rng_order.npz     population after 1 and 3 resets for seeds {0, 4, 123}
+  P  policy.npz        MAPPO actor (seed 1, the reference init) on reference norm_state_dict
+                       vectors: weights, obs, Actor.forward probabilities (row P)
 
 Usage:  python tests/golden/make_golden.py   (writes next to this file)
 """
@@ -418,6 +420,34 @@ def gen_rng_order() -> None:
     np.savez_compressed(os.path.join(OUT, "rng_order.npz"), **out)
 
 
+# ---------------------------------------------------------------------------------------- P
+def gen_policy() -> None:
+    """MAPPO(MAPPOProperties(), num_state=F, seed=1) (mappo.py:37-60) on the norm_state_dict vectors
+    the trajectory fixtures hold; probabilities from its actor_net (network.py:29-33) in fp32."""
+    import torch
+
+    from app.core.agents.trainables.mappo import MAPPO, MAPPOProperties
+
+    out = {}
+    for case, (traj, keys) in {"c1": ("c1_sin_dbbc", ("norm_t0", "norm_t1", "norm_t50")),
+                               "wide": ("n30_maxerr_groups_hvacmsg", ("norm_t0", "norm_t50"))}.items():
+        d = np.load(os.path.join(OUT, f"traj_{traj}.npz"))
+        obs = np.concatenate([d[k] for k in keys]).astype(np.float32)
+        agent = MAPPO(MAPPOProperties(), num_state=obs.shape[1])
+        with torch.no_grad():
+            probs = agent.actor_net(torch.from_numpy(obs)).numpy()
+        for k, v in agent.actor_net.state_dict().items():
+            out[f"{case}_{k}"] = v.numpy()
+        out[f"{case}_obs"] = obs
+        out[f"{case}_probs"] = probs
+        # select_actions on the same vectors: last_probs[i] = probs[i, action[i]]
+        torch.manual_seed(7)
+        acts = agent.select_actions(list(obs.astype(np.float64)))
+        out[f"{case}_sel_action"] = np.array([acts[i] for i in range(len(obs))], np.int64)
+        out[f"{case}_sel_prob"] = np.array([agent.last_probs[i] for i in range(len(obs))], np.float32)
+    np.savez_compressed(os.path.join(OUT, "policy.npz"), **out)
+
+
 def main() -> None:
     with open(os.path.join(OUT, "marl_env_prop.json"), "w") as f:
         json.dump(env_prop_json(), f, indent=1, sort_keys=True)
@@ -454,6 +484,7 @@ def main() -> None:
     gen_greedy()
     gen_comm()
     gen_rng_order()
+    gen_policy()
     print("golden fixtures written to", OUT)
 
 

@@ -1,0 +1,202 @@
+"""Fused obs + MA-PPO actor kernel (row P) vs the reference actor and torch fp32.
+
+Reference: Actor.forward (server/app/core/agents/trainables/network.py:29-33) with the MAPPO seed-1
+initialisation (mappo.py:41-50), on norm_state_dict vectors (norm.py:178-218); golden
+``tests/golden/policy.npz`` (reference probabilities on reference obs vectors).
+
+Tolerances on action probabilities (the kernel's documented precision, mdr.h MDR_PREC_*):
+  bf16x3 (split-bf16 MFMA, fp32 accumulate)  atol 1e-4 against torch fp32 on the same obs
+  bf16   (one bf16 product per term)         atol 3e-2
+Obs rows: within 2 float32 ulps of the reference (as tests/test_env_parity_gpu.py); bit-identical
+to the standalone obs kernel.  Sampling RNG is not part of parity; the sampled
+action is checked for consistency (prob == probs[action]) and statistically.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+
+pytestmark = pytest.mark.gpu
+
+PROB_ATOL = {"bf16x3": 1e-4, "bf16": 3e-2}
+POLICY_CASES = {"c1": ("c1_sin_dbbc", (0, 1, 50)), "wide": ("n30_maxerr_groups_hvacmsg", (0, 50))}
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def ref_actor(torch, case):
+    from mdr_amd.actor import make_actor
+
+    d = gu.load("policy.npz")
+    n_in = d[f"{case}_fc.0.weight"].shape[1]
+    a = make_actor(n_in, 2, [100, 100], seed=None)
+    a.load_state_dict({k[len(case) + 1:]: torch.from_numpy(d[k]) for k in d.files
+                       if k.startswith(case + "_fc.")})
+    return a.to("cuda"), d
+
+
+def make_env(props, rng_seed, resets=1, **kw):
+    from mdr_amd.environment import Environment
+
+    env = Environment(props, rng=random.Random(rng_seed), **kw)
+    for _ in range(resets - 1):
+        env.reset(return_obs=False)
+    return env
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
+@pytest.mark.parametrize("case", sorted(POLICY_CASES))
+def test_actor_golden(torch_gpu, case, precision):
+    """Reference actor weights + reference trajectory state: obs rows and probabilities."""
+    from mdr_amd.actor import DeviceActor
+
+    torch = torch_gpu
+    actor, pol = ref_actor(torch, case)
+    name, ticks = POLICY_CASES[case]
+    d, meta = gu.traj(name)
+    props = gu.props_from_overrides(meta["overrides"])
+    env = make_env(props, meta["seed"], meta["resets"])
+    da = DeviceActor(env, actor, precision=precision)
+    N, F = meta["N"], pol[f"{case}_obs"].shape[1]
+    ref_obs = pol[f"{case}_obs"].reshape(len(ticks), N, F)
+    ref_probs = pol[f"{case}_probs"].reshape(len(ticks), N, 2)
+    worst = 0.0
+    for t in range(max(ticks) + 1):
+        if t in ticks:
+            k = ticks.index(t)
+            probs = torch.empty((N, 2), dtype=torch.float32, device="cuda")
+            obs = torch.empty((N, F), dtype=torch.float32, device="cuda")
+            act, prob = da.select_actions(probs=probs, obs_out=obs, count_next=False)
+            o = obs.cpu().numpy()
+            np.testing.assert_array_max_ulp(o, ref_obs[k], maxulp=2)
+            np.testing.assert_array_equal(o, env.obs_tensor().cpu().numpy())  # == standalone obs kernel
+            with torch.no_grad():
+                tp = actor(obs).cpu().numpy()  # torch fp32 on the identical rows
+            p = probs.cpu().numpy()
+            err = float(np.abs(p - tp).max())
+            worst = max(worst, err)
+            assert err < PROB_ATOL[precision], (t, err)
+            assert np.abs(p - ref_probs[k]).max() < PROB_ATOL[precision] + 1e-5
+            a = act.cpu().numpy()
+            np.testing.assert_array_equal(prob.cpu().numpy(), p[np.arange(N), a])
+        if t < max(ticks):
+            env.step_tensor(torch.from_numpy(d["actions"][t]).to("cuda"))
+    print(f"{case} {precision}: max |p - p_torch| = {worst:.3g}")
+
+
+def scaled_actor(torch, n_in, scale, seed=3):
+    from mdr_amd.actor import make_actor
+
+    a = make_actor(n_in, 2, [100, 100], seed=seed)
+    with torch.no_grad():
+        for p in a.parameters():
+            p.mul_(scale)
+    return a.to("cuda")
+
+
+@pytest.mark.parametrize("precision", ["bf16x3", "bf16"])
+@pytest.mark.parametrize("n", [1, 37, 300, 4099])
+def test_actor_vs_torch_sizes(torch_gpu, n, precision):
+    """Ragged sizes, spread-out logits (weights x3): probabilities vs torch fp32 on the same obs."""
+    from mdr_amd.actor import DeviceActor
+
+    torch = torch_gpu
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env = make_env(props, 11)
+    rs = np.random.RandomState(n)
+    for _ in range(7):
+        env.step_tensor(torch.from_numpy(rs.randint(0, 2, n).astype(np.uint8)).to("cuda"))
+    F = env.obs_spec().n_feat
+    actor = scaled_actor(torch, F, 3.0)
+    da = DeviceActor(env, actor, precision=precision)
+    probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
+    obs = torch.empty((n, F), dtype=torch.float32, device="cuda")
+    act, prob = da.select_actions(probs=probs, obs_out=obs, count_next=False)
+    with torch.no_grad():
+        tp = actor(obs).cpu().numpy()
+    p = probs.cpu().numpy()
+    err = float(np.abs(p - tp).max())
+    print(f"n={n} {precision}: max |p - p_torch| = {err:.3g}, p1 spread {tp[:, 1].min():.3f}..{tp[:, 1].max():.3f}")
+    assert err < PROB_ATOL[precision]
+    a = act.cpu().numpy()
+    assert set(np.unique(a)) <= {0, 1}
+    np.testing.assert_array_equal(prob.cpu().numpy(), p[np.arange(n), a])
+
+
+def test_actor_sampling_statistics(torch_gpu):
+    """Categorical sampling: the fraction of houses turning on matches the mean probability."""
+    from mdr_amd.actor import DeviceActor
+
+    torch = torch_gpu
+    n = 200_000
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env = make_env(props, 5, population="synthetic", seed=77)
+    actor = scaled_actor(torch, env.obs_spec().n_feat, 1.0)
+    da = DeviceActor(env, actor)
+    probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
+    act, _ = da.select_actions(probs=probs, count_next=False)
+    p1 = probs[:, 1].double()
+    mean, var = float(p1.mean()), float((p1 * (1 - p1)).sum())
+    ones = float(act.double().sum())
+    assert abs(ones - mean * n) < 6 * var ** 0.5 + 1, (ones, mean * n, var ** 0.5)
+
+
+def test_actor_count_next_equals_power_counts(torch_gpu):
+    """select_actions(count_next) + step_tensor == the same actions through mdr_power_counts."""
+    from mdr_amd.actor import DeviceActor
+
+    torch = torch_gpu
+    n = 5000
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env_a, env_b = make_env(props, 21), make_env(props, 21)
+    actor = scaled_actor(torch, env_a.obs_spec().n_feat, 2.0)
+    da = DeviceActor(env_a, actor)
+    for t in range(6):
+        act, _ = da.select_actions(count_next=True)
+        ra = env_a.step_tensor(act).clone()
+        rb = env_b.step_tensor(act.clone()).clone()
+        torch.testing.assert_close(ra, rb, rtol=0, atol=0)
+        for k in ("t_air", "t_mass", "hvac"):
+            assert torch.equal(getattr(env_a.shard, k), getattr(env_b.shard, k)), (t, k)
+
+
+def test_actor_rollout_equals_loop(torch_gpu):
+    """DeviceActor.rollout (one hipGraph: actor -> step per tick) == select_actions/step_tensor loop."""
+    from mdr_amd.actor import DeviceActor
+
+    torch = torch_gpu
+    n, T = 3001, 12
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env_a, env_b = make_env(props, 8), make_env(props, 8)
+    actor = scaled_actor(torch, env_a.obs_spec().n_feat, 2.0)
+    da, db = DeviceActor(env_a, actor), DeviceActor(env_b, actor)
+    rew = torch.empty((T, n), dtype=torch.float64, device="cuda")
+    acts = torch.empty((T, n), dtype=torch.uint8, device="cuda")
+    probs = torch.empty((T, n), dtype=torch.float32, device="cuda")
+    da.rollout(T, rewards=rew, actions=acts, probs=probs)
+    for t in range(T):
+        a, p = db.select_actions(count_next=True)
+        r = env_b.step_tensor(a)
+        assert torch.equal(a, acts[t]), t
+        assert torch.equal(p, probs[t]), t
+        assert torch.equal(r, rew[t]), t
+    for k in ("t_air", "t_mass", "hvac"):
+        assert torch.equal(getattr(env_a.shard, k), getattr(env_b.shard, k)), k
+    # a second rollout replays the cached graph with the next ticks' drivers
+    da.rollout(T, rewards=rew, actions=acts, probs=probs)
+    for t in range(T):
+        a, p = db.select_actions(count_next=True)
+        r = env_b.step_tensor(a)
+        assert torch.equal(a, acts[t]) and torch.equal(r, rew[t]), t

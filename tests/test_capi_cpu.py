@@ -34,10 +34,11 @@ def test_abi_struct_sizes_and_version():
 
     lib = _lib.load()
     assert lib.mdr_abi_version() == _lib.ABI_VERSION
-    sizes = (C.c_int64 * 6)()
-    assert lib.mdr_abi_sizes(sizes, 6) == 6
+    sizes = (C.c_int64 * 7)()
+    assert lib.mdr_abi_sizes(sizes, 7) == 7
     assert list(sizes) == [C.sizeof(t) for t in (_lib.mdr_config, _lib.mdr_soa, _lib.mdr_tick,
-                                                 _lib.mdr_pop_spec, _lib.mdr_obs_spec, _lib.mdr_obs_scalars)]
+                                                 _lib.mdr_pop_spec, _lib.mdr_obs_spec, _lib.mdr_obs_scalars,
+                                                 _lib.mdr_actor_spec)]
 
 
 def test_argument_errors_without_gpu():

@@ -135,3 +135,35 @@ def test_perlin_restatement_statistics():
     sig = D.Signal(C.SignalProperties(mode="perlin"), 10, rng=random.Random(1))
     s = [float(sig(42000.0, dt.datetime(2021, 5, 5, 12, 0, k))) for k in range(0, 60, 4)]
     assert min(s) >= 0.0
+
+
+def test_actor_init_matches_reference_mappo():
+    """make_actor(seed=1) reproduces MAPPO's actor initialisation (mappo.py:41-50) and forward:
+    the reference's own weights and probabilities in tests/golden/policy.npz."""
+    import torch
+
+    from mdr_amd.actor import make_actor
+
+    d = gu.load("policy.npz")
+    for case in ("c1", "wide"):
+        a = make_actor(d[f"{case}_fc.0.weight"].shape[1], 2, [100, 100], seed=1)
+        for k, v in a.state_dict().items():
+            np.testing.assert_array_equal(v.numpy(), d[f"{case}_{k}"], err_msg=k)
+        with torch.no_grad():
+            p = a(torch.from_numpy(d[f"{case}_obs"])).numpy()
+        np.testing.assert_allclose(p, d[f"{case}_probs"], rtol=0, atol=1e-6)
+        # select_actions bookkeeping: last_probs[i] = probs[i, action[i]]
+        np.testing.assert_allclose(d[f"{case}_sel_prob"],
+                                   d[f"{case}_probs"][np.arange(len(p)), d[f"{case}_sel_action"]], atol=1e-6)
+
+
+def test_device_actor_has_no_cpu_path():
+    """DeviceActor needs the HIP library and a GPU: on a CPU box the Environment itself refuses."""
+    import pytest as _pt
+
+    from mdr_amd import _lib
+    from mdr_amd.environment import Environment
+
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": 4})
+    with _pt.raises(_lib.MdrLibraryError):
+        Environment(props)

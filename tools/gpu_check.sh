@@ -17,7 +17,7 @@ step() {  # step NAME SECONDS CMD...
 }
 STEPS=${STEPS:-smoke,pytest,bench,prof}
 [[ $STEPS == *smoke* ]] && { step smoke 420 python __graft_entry__.py smoke || true; }
-[[ $STEPS == *pytest* ]] && { step pytest_gpu 900 python -m pytest tests -m gpu -q --maxfail=20 -p no:cacheprovider || true; }
+[[ $STEPS == *pytest* ]] && { step pytest_gpu 900 python -u -m pytest tests -m gpu -v --maxfail=20 -p no:cacheprovider --timeout 120 --timeout-method thread || true; }
 [[ $STEPS == *bench* ]] && { step bench 600 python bench.py ${BENCH_ARGS:-} || true; }
 if [[ $STEPS == *prof* ]]; then
   export TMPDIR=/tmp
