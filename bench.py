@@ -31,6 +31,7 @@ for _p in (ROOT, os.path.join(ROOT, "marl-demandresponse_amd")):
 METRIC = "house-steps/s (env.step throughput) at 1M houses; % HBM roofline"
 BYTES_PER_HOUSE_STEP = 99  # SURVEY §8(d) B_core: state r/w 42 + action 1 + params 48 + reward 8
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s
+BF16_PEAK_TFS = 2516.6     # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (no sparsity)
 
 
 def parse():
@@ -43,6 +44,11 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="random", choices=["random", "buffer"])
+    ap.add_argument("--workload", default="step", choices=["step", "actor"],
+                    help="step: env.step with fused random actions (the BASELINE metric); actor: "
+                         "config C5, MA-PPO actor select_actions fused with the obs, then env.step")
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16"],
+                    help="actor MFMA precision (--workload actor)")
     ap.add_argument("--comm", default="default", choices=["default", "none", "rccl", "torch"],
                     help="exchange for the sharded path (default: rccl when WORLD_SIZE > 1); "
                          "'rccl' at world 1 exercises the sharded C loop on one GPU")
@@ -136,10 +142,21 @@ def main():
     if args.mode == "buffer":
         acts = (torch.rand((chunk, n_loc), device=dev) < 0.5).to(torch.uint8)
     rew = torch.empty((chunk, n_loc), dtype=torch.float64, device=dev)
+    dactor = None
+    if args.workload == "actor":
+        if world > 1:
+            raise SystemExit("--workload actor runs on one GPU (sharded actor rollouts: see DESIGN.md)")
+        from mdr_amd.actor import DeviceActor, make_actor
+
+        dactor = DeviceActor(env, make_actor(env.obs_spec().n_feat, 2, [100, 100], seed=1),
+                             precision=args.precision)
 
     def run(n):
-        env.rollout(n, actions=None if acts is None else acts[:n], action_mode=args.mode,
-                    rewards=rew[:n])
+        if dactor is not None:
+            dactor.rollout(n, rewards=rew[:n])
+        else:
+            env.rollout(n, actions=None if acts is None else acts[:n], action_mode=args.mode,
+                        rewards=rew[:n])
 
     # warmup: captures the graphs of every chunk size used below
     done = 0
@@ -202,6 +219,22 @@ def main():
         ev1.record(ls)
         torch.cuda.synchronize()
         kern_ms = ev0.elapsed_time(ev1) / kern_launches
+    if dactor is not None:
+        # the rollout graph interleaves k_actor and k_step: time each kernel alone, back to back
+        # on the current stream (HIP events on that stream), over the same state
+        cur = torch.cuda.current_stream(dev)
+        K = 50
+        act_buf = torch.empty(n_loc, dtype=torch.uint8, device=dev)
+        prob_buf = torch.empty(n_loc, dtype=torch.float32, device=dev)
+        dactor.select_actions(action=act_buf, prob=prob_buf, count_next=False)
+        torch.cuda.synchronize()
+        ev0.record(cur)
+        for _ in range(K):
+            dactor.select_actions(action=act_buf, prob=prob_buf, count_next=False)
+        ev1.record(cur)
+        torch.cuda.synchronize()
+        actor_ms = ev0.elapsed_time(ev1) / K
+        kern_ms = max(per_tick_ms - actor_ms, 1e-6)  # the step kernel's share of a tick
     bytes_launch = BYTES_PER_HOUSE_STEP * n_loc
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
     traffic = pmc_traffic(n_loc)
@@ -233,6 +266,25 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "bytes_per_house_step": BYTES_PER_HOUSE_STEP},
     }
+    if dactor is not None:
+        a = dactor.actor
+        flops_house = 2 * sum(l.in_features * l.out_features for l in a.fc)  # 30,400 at F = 50
+        flops_launch = flops_house * n_loc
+        tfs = flops_launch / (actor_ms * 1e-3) / 1e12
+        out["dtype"] = f"f64 env step + {args.precision} MFMA actor (fp32 accumulate)"
+        out["data"] = ("synthetic (device Philox population, reference noise model); actor = the "
+                       "reference MAPPO init (torch seed 1), actions sampled on device")
+        out["config"]["workload"] = ("C5: 1M houses, MA-PPO actor select_actions fused with the obs "
+                                     "(one launch) -> env.step (one launch) per tick, hipGraph chunks")
+        out["config"]["action_mode"] = "mappo_actor"
+        out["config"]["actor"] = {"layers": [a.fc[0].in_features, 100, 100, 2], "precision": args.precision}
+        out["roofline"] = {"bound": "mfma", "achieved": tfs, "peak": BF16_PEAK_TFS, "unit": "TFLOP/s",
+                           "frac": tfs / BF16_PEAK_TFS, "traffic": None, "kernel": "mdr::k_actor",
+                           "kernel_avg_us": actor_ms * 1e3, "launches_timed": K,
+                           "algorithmic_flops_per_launch": flops_launch, "flops_per_house": flops_house,
+                           "mfma_products_per_mac": 3 if args.precision == "bf16x3" else 1,
+                           "step_kernel": {"kernel": "mdr::k_step (BUFFER)", "avg_us": kern_ms * 1e3,
+                                           "hbm_GBps": achieved, "frac": achieved / HBM_PEAK_GBS}}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
     if rank == 0:

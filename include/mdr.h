@@ -248,7 +248,7 @@ enum { MDR_PREC_BF16 = 1,   /* bf16 products, fp32 accumulate (~4e-3 relative) *
 typedef struct mdr_actor_spec {
   int32_t n_in;      /* obs features (= mdr_obs_spec.n_feat), <= 128 */
   int32_t h1, h2;    /* hidden widths (actor_layers), each <= 128 */
-  int32_t n_act;     /* actions (num_action, 2), <= 4 */
+  int32_t n_act;     /* actions (num_action): 2, the on/off decision */
   int32_t precision; /* MDR_PREC_* */
 } mdr_actor_spec;
 
@@ -302,6 +302,13 @@ int mdr_probe_stream(mdr_ctx* ctx, double* reward, void* stream);
 /* Exact-division self-check: counts (into *mismatches, device int64) the i where the
  * shared-reciprocal division sequence of the step kernels differs bitwise from a[i] / b[i]. */
 int mdr_div_check(const double* a, const double* b, int64_t n, int64_t* mismatches, void* stream);
+
+/* Phase profile of one mdr_actor_act launch (no outputs written): shader cycles per phase
+ * averaged over the launch's blocks, cycles_out[8] (host): loop-top barrier wait, obs build,
+ * prefetch + obs_out, layer 1, layer 2, -, output layer + softmax + stores (+ weight fill), tiles
+ * per block.  Synchronises the stream. */
+int mdr_actor_profile(mdr_ctx* ctx, const mdr_obs_spec* obs, const mdr_obs_scalars* sc, const double* p_dev,
+                      double* cycles_out, void* stream);
 
 /* ---- timing helpers for bench.py (HIP events on the given stream) ---------------------- */
 int mdr_event_record(mdr_ctx* ctx, int slot, void* stream);

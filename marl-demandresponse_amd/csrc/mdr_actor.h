@@ -6,7 +6,7 @@ namespace mdr {
 
 constexpr int kActorMB = 4;       // 32-row MFMA blocks per hidden layer (hidden width <= 128)
 constexpr int kActorRows = 32 * kActorMB;
-constexpr int kActorMaxAct = 4;   // actions (the reference uses 2)
+constexpr int kActorNA = 2;       // actions: on / off (MAPPO num_action = 2, mappo.py:38)
 constexpr int kActorMaxIn = 128;  // obs features (8 k-steps of 16)
 
 // Shapes + byte offsets of the packed weight image (identical in global memory and in LDS) and
@@ -16,7 +16,9 @@ struct ActorDims {
   int ks1, ks2;  // k-steps of layer 1 (ceil(n_in/16)) and layer 2 (ceil(h1/16))
   int fs;        // LDS obs row stride (floats): >= n_in, multiple of 4, odd multiple of 4 words
   int off_w1, off_w2, off_tail, off_end;  // packed image: W1 / W2 fragments (hi, lo), fp32 tail
-  int lds_obs, lds_msg, lds_hw, lds_hist, lds_total;
+  int lds_cf, lds_hist, lds_wave, wave_stride;  // block LDS: obs consts, count histogram, wave slices
+  int w_msg, w_hw, w_cls;                        // offsets inside a wave slice (rows at 0)
+  int lds_total;
 };
 
 struct ActorOut {
@@ -25,11 +27,12 @@ struct ActorOut {
   float* probs;                  // [n][n_act] all action probabilities, or null
   float* obs;                    // [n][n_in] the observation rows, or null
   unsigned long long* count_next;  // count slab of the tick these actions drive, or null
+  unsigned long long* prof;        // diagnostics: [grid][8] per-phase shader cycles, or null
 };
 
 __global__ void k_actor_pack(ActorDims d, const float* w1, const float* b1, const float* w2,
                              const float* b2, const float* w3, const float* b3, unsigned char* out);
-template <int PREC>
+template <int PREC, bool PROF>
 __global__ void k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
                         const unsigned char* wpack, ActorOut out, uint64_t tick, const TickArgs* tkp);
 

@@ -50,8 +50,10 @@ __global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const fl
   const int r = lane & 31, h = lane >> 5;
   float v[8];
   bf16x8 hi, lo;
+  // fragments are stored k-step-major (f = k-step * kActorMB + mb), so the kernel's unrolled
+  // (k-step, mb) loops address them with compile-time LDS offsets whatever ks1 / ks2 are
   if (f < nf1) {  // W1 [H1][n_in], fragment (mb, ks)
-    const int mb = f / d.ks1, ks = f % d.ks1;
+    const int ks = f / kActorMB, mb = f % kActorMB;
     const int row = 32 * mb + r;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -63,7 +65,7 @@ __global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const fl
     reinterpret_cast<bf16x8*>(out + d.off_w1)[(2 * f + 1) * 64 + lane] = lo;
   } else if (f < nf1 + nf2) {  // W2 [H2][H1], fragment (mb, q) in the accumulator k order
     const int f2 = f - nf1;
-    const int mb = f2 / d.ks2, q = f2 % d.ks2;
+    const int q = f2 / kActorMB, mb = f2 % kActorMB;
     const int row = 32 * mb + r;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -73,14 +75,14 @@ __global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const fl
     split8(v, hi, lo);
     reinterpret_cast<bf16x8*>(out + d.off_w2)[(2 * f2) * 64 + lane] = hi;
     reinterpret_cast<bf16x8*>(out + d.off_w2)[(2 * f2 + 1) * 64 + lane] = lo;
-  } else if (f == nf1 + nf2) {  // fp32 tail: b1, b2 [128], W3 [n_act][128], b3 [n_act]
+  } else if (f == nf1 + nf2) {  // fp32 tail: b1, b2 [128], W3^T [128][2] (row-interleaved), b3 [2]
     float* t = reinterpret_cast<float*>(out + d.off_tail);
     for (int i = lane; i < kActorRows; i += 64) {
       t[i] = i < d.h1 ? b1[i] : 0.f;
       t[kActorRows + i] = i < d.h2 ? b2[i] : 0.f;
-      for (int a = 0; a < d.n_act; ++a) t[2 * kActorRows + a * kActorRows + i] = i < d.h2 ? w3[a * d.h2 + i] : 0.f;
+      for (int a = 0; a < kActorNA; ++a) t[2 * kActorRows + i * kActorNA + a] = i < d.h2 ? w3[a * d.h2 + i] : 0.f;
     }
-    if (lane < d.n_act) t[(2 + d.n_act) * kActorRows + lane] = b3[lane];
+    if (lane < kActorNA) t[(2 + kActorNA) * kActorRows + lane] = b3[lane];
   }
 }
 
@@ -96,80 +98,165 @@ __device__ __forceinline__ float philox_u01f(uint64_t seed, uint64_t gid, uint64
   return (float)(c.x >> 8) * (1.0f / 16777216.0f);  // [0, 1), 24 bits
 }
 
-template <int PREC>
+// LDS written by some lanes of a wave and read by others: the wave's LDS operations execute in
+// issue order, so a wavefront-scope fence (orders the compiler, waits lgkmcnt) is enough.
+__device__ __forceinline__ void wave_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
+// Persistent, wave-independent: every wave of the block shares the LDS weight image but owns its
+// own 32-house tiles (rows, ring messages, FSM words in a private LDS slice), so waves never wait
+// for each other inside the loop and one wave's obs build / memory phase overlaps another's MFMAs
+// on the same SIMD.  Each lane prefetches one obs source of the wave's NEXT tile into registers
+// before the current tile's MFMAs.
+template <int PREC, bool PROF>
 __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
                                                const unsigned char* __restrict__ wpack, ActorOut out,
                                                uint64_t tick0, const TickArgs* tkp) {
   const uint64_t tick = tkp ? tkp->tick : tick0;
+  // diagnostics (out.prof): shader cycles per phase, accumulated by lane 0 of every wave:
+  // [0] weight fill + block barrier, [1] obs build + message copy, [2] prefetch issue + obs_out,
+  // [3] layer 1, [4] split + layer 2, [5] output layer + softmax + stores, [6] -, [7] tiles
+  unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  unsigned long long plast = PROF ? clock64() : 0ull;
+#define PSTAMP(k)                                \
+  do {                                           \
+    if (PROF) {                                  \
+      const unsigned long long now_ = clock64(); \
+      pacc[k] += now_ - plast;                   \
+      plast = now_;                              \
+    }                                            \
+  } while (0)
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nthr = blockDim.x, nw = nthr >> 6;
-  const int HB = 32 * nw;  // houses per block iteration
   const int r = lane & 31, h = lane >> 5;
   const int F = o.n_feat, FS = d.fs;
+  const int K = o.n_comm, M = o.msg_w;
+  const bool ring = o.comm_mode == MDR_COMM_RING && K > 0;
+  const int lo = ring ? K / 2 : 0, hi = ring ? (K + 1) / 2 : 0;
+  const bool thermal = obs_needs_thermal(o);
 
-  // LDS carve-up (byte offsets computed on the host, mdr_actor_lds)
-  unsigned char* s_w1 = smem;
-  unsigned char* s_w2 = smem + d.off_w2;
+  // LDS: [weights image | obs consts | count histogram | per-wave slices]
+  const unsigned char* s_w1 = smem;
+  const unsigned char* s_w2 = smem + d.off_w2;
   const float* s_tail = reinterpret_cast<const float*>(smem + d.off_tail);
-  float* s_obs = reinterpret_cast<float*>(smem + d.lds_obs);     // [HB][FS] + 16 ks1
-  float* s_msg = reinterpret_cast<float*>(smem + d.lds_msg);     // [lo + HB + hi][M]
-  uint32_t* s_hw = reinterpret_cast<uint32_t*>(smem + d.lds_hw); // [HB] hvac words
+  float* s_cf = reinterpret_cast<float*>(smem + d.lds_cf);
   unsigned* s_hist = reinterpret_cast<unsigned*>(smem + d.lds_hist);
+  unsigned char* wbase = smem + d.lds_wave + wv * d.wave_stride;
+  float* w_obs = reinterpret_cast<float*>(wbase);                  // [32][FS] + 16 ks1 overrun
+  float* w_msg = reinterpret_cast<float*>(wbase + d.w_msg);        // [lo + 32 + hi][M]
+  uint32_t* w_hw = reinterpret_cast<uint32_t*>(wbase + d.w_hw);    // [32] hvac words
+  uint8_t* w_cls = wbase + d.w_cls;                                // [32] capacity classes
 
-  // weights -> LDS once per block (PREC 1 skips the lo fragments)
   {
     const uint4* src = reinterpret_cast<const uint4*>(wpack);
     uint4* dst = reinterpret_cast<uint4*>(smem);
     const int n16 = d.off_end / 16;
     for (int q = tid; q < n16; q += nthr) {
-      if (PREC == 1 && q < d.off_tail / 16) {
-        const int frag = q / 64;  // 1-KB fragments: even = hi, odd = lo
-        if (frag & 1) continue;
-      }
+      if (PREC == 1 && q < d.off_tail / 16 && ((q >> 6) & 1)) continue;  // bf16: no lo fragments
       dst[q] = src[q];
     }
-    for (int q = tid; q < HB * FS + 16 * d.ks1; q += nthr) s_obs[q] = 0.f;  // + the k-padding overrun
+    for (int q = lane; q < 32 * FS + 16 * d.ks1; q += 64) w_obs[q] = 0.f;
     if (tid < MDR_MAX_CAP) s_hist[tid] = 0u;
+    if (o.sc_dev) { o.s = o.sc_dev[0]; o.solar = o.sc_dev[1]; o.t_od = o.sc_dev[2]; }
+    obs_consts(p, o, p_dev ? *p_dev : o.p, s_cf, tid, nthr);
   }
-  const double P = p_dev ? *p_dev : o.p;
-  if (o.sc_dev) { o.s = o.sc_dev[0]; o.solar = o.sc_dev[1]; o.t_od = o.sc_dev[2]; }
+  __syncthreads();
+  PSTAMP(0);
   const float* b1 = s_tail;
   const float* b2 = s_tail + kActorRows;
   const float* w3 = s_tail + 2 * kActorRows;
-  const float* b3 = s_tail + (2 + d.n_act) * kActorRows;
+  const float* b3 = s_tail + (2 + kActorNA) * kActorRows;
 
-  const int64_t n = p.n;
-  const int64_t ntile = (n + HB - 1) / HB;
-  for (int64_t tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
-    const int64_t b0 = tile * HB;
-    const int nb = (int)min((int64_t)HB, n - b0);
-    __syncthreads();  // previous iteration done with s_obs / s_msg (and the initial fill visible)
-    obs_stage_ring(p, o, b0, nb, s_msg, tid, nthr);
-    __syncthreads();
-    if (tid < nb) {
-      float* row = s_obs + tid * FS;
-      s_hw[tid] = obs_build_row(p, o, P, b0 + tid, tid, s_msg, row);
-      for (int f = F; f < FS; ++f) row[f] = 0.f;
-    }
-    __syncthreads();
-    if (out.obs) {  // optional obs[b0 .. b0 + nb) rows to HBM (training buffers)
-      const int64_t nflt = (int64_t)nb * F;
-      float* dst = out.obs + b0 * F;
-      for (int64_t q = tid; q < nflt; q += nthr) {
-        const int rr = (int)(q / F);
-        dst[q] = s_obs[rr * FS + (int)(q - (int64_t)rr * F)];
+  const uint32_t n = (uint32_t)p.n;
+  const uint32_t ntile = (n + 31u) / 32u;
+  const uint32_t stride = gridDim.x * (uint32_t)nw;
+  const int nsrc_max = lo + 32 + hi;
+  HouseRegs src{};
+  int src_kind = 0;  // 0 none, 1 house, 2 halo
+  auto source_of = [&](uint32_t tl, int s, HouseRegs& rg) -> int {
+    const uint32_t b0 = tl * 32u;
+    const int nb = (int)min(32u, n - b0);
+    if (s >= lo + nb + hi) return 0;
+    int64_t j = (int64_t)b0 - lo + s;
+    if (o.halo_msg && (j < 0 || j >= (int64_t)n)) return 2;
+    j %= (int64_t)n;
+    if (j < 0) j += n;
+    house_load(p, j, thermal, rg);
+    return 1;
+  };
+  auto build = [&](uint32_t b0, int nb, int s, int kind, const HouseRegs& rg) {
+    if (kind == 2) {
+      const int64_t j = (int64_t)b0 - lo + s;
+      const int hh = j < 0 ? (int)(j + lo) : (int)(lo + (j - (int64_t)n));
+      for (int m = 0; m < M; ++m) w_msg[s * M + m] = o.halo_msg[hh * M + m];
+    } else if (kind == 1) {
+      if (ring) msg_from_regs(p, o, rg, s_cf, w_msg + s * M);
+      const int t = s - lo;
+      if (t >= 0 && t < nb) {
+        float* row = w_obs + t * FS;
+        const int f = row_scalars(p, o, rg, s_cf, row);
+        if (!ring) row_messages(p, o, (int64_t)b0 + t, t, s_cf, w_msg, row, f);  // TABLE gathers / none
+        for (int q = F; q < FS; ++q) row[q] = 0.f;
+        w_hw[t] = rg.w;
+        w_cls[t] = (uint8_t)rg.cls;
       }
     }
+  };
+  uint32_t tile = blockIdx.x * (uint32_t)nw + (uint32_t)wv;
+  if (tile < ntile) src_kind = source_of(tile, lane, src);
+
+  for (; tile < ntile; tile += stride) {
+    const uint32_t b0 = tile * 32u;
+    const int nb = (int)min(32u, n - b0);
+    if (PROF && lane == 0) pacc[7] += 1;
+    wave_sync();  // this wave's previous MFMA reads of w_obs are done (compiler ordering)
+    build(b0, nb, lane, src_kind, src);
+    if (nsrc_max > 64 && lane + 64 < lo + nb + hi) {  // rings wider than 32 neighbours
+      HouseRegs r2;
+      const int k2 = source_of(tile, lane + 64, r2);
+      build(b0, nb, lane + 64, k2, r2);
+    }
+    wave_sync();
+    if (ring) {  // messages into the rows: lanes r and r + 32 each copy half of row r's K messages
+      const int base = F - K * M;
+      const int kh = (K + 1) / 2;
+      if (r < nb) {
+        for (int k = h * kh; k < min(K, (h + 1) * kh); ++k) {
+          const int sidx = k < lo ? (r + k) : (r + k + 1);
+          float* dst = w_obs + r * FS + base + k * M;
+          const float* sp = w_msg + sidx * M;
+          for (int m = 0; m < M; ++m) dst[m] = sp[m];
+        }
+      }
+      wave_sync();
+    }
+    PSTAMP(1);
+    if (tile + stride < ntile) src_kind = source_of(tile + stride, lane, src);  // in flight during the MFMAs
+    else src_kind = 0;
+    if (out.obs) {  // optional obs rows to HBM (training buffers)
+      float* dst = out.obs + (size_t)b0 * F;
+      for (int q = lane; q < nb * F; q += 64) {
+        const int rr = q / F;
+        dst[q] = w_obs[rr * FS + (q - rr * F)];
+      }
+    }
+    PSTAMP(2);
 
     // ---- layer 1: acc1[mb] = b1 + W1 · X  (X^T columns = this wave's 32 houses)
-    const float* xrow = s_obs + (32 * wv + r) * FS + 8 * h;
+    const float* xrow = w_obs + r * FS + 8 * h;
     f32x16 acc1[kActorMB];
 #pragma unroll
     for (int mb = 0; mb < kActorMB; ++mb)
 #pragma unroll
       for (int g = 0; g < 16; ++g) acc1[mb][g] = b1[32 * mb + (g & 3) + 8 * (g >> 2) + 4 * h];
-    for (int ks = 0; ks < d.ks1; ++ks) {
+    // k-steps unrolled with uniform guards (a loop here makes the compiler drain the prefetch
+    // loads, vmcnt(0), at its header)
+#pragma unroll
+    for (int ks = 0; ks < kActorMaxIn / 16; ++ks) {
+      if (ks >= d.ks1) break;
       const float4 x0 = *reinterpret_cast<const float4*>(xrow + 16 * ks);
       const float4 x1 = *reinterpret_cast<const float4*>(xrow + 16 * ks + 4);
       const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
@@ -178,7 +265,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
       bf16x8 ah[kActorMB], al[kActorMB];
 #pragma unroll
       for (int mb = 0; mb < kActorMB; ++mb) {
-        const int f = mb * d.ks1 + ks;
+        const int f = ks * kActorMB + mb;
         ah[mb] = lds_frag(s_w1, 2 * f, lane);
         if (PREC == 3) al[mb] = lds_frag(s_w1, 2 * f + 1, lane);
       }
@@ -191,6 +278,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
 #pragma unroll
       for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], xh, acc1[mb], 0, 0, 0);
     }
+    PSTAMP(3);
 
     // ---- ReLU + split: layer 1's accumulators become layer 2's B fragments in place
     bf16x8 hh[2 * kActorMB], hl[2 * kActorMB];
@@ -214,7 +302,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
       bf16x8 ah[kActorMB], al[kActorMB];
 #pragma unroll
       for (int mb = 0; mb < kActorMB; ++mb) {
-        const int f = mb * d.ks2 + q;
+        const int f = q * kActorMB + mb;
         ah[mb] = lds_frag(s_w2, 2 * f, lane);
         if (PREC == 3) al[mb] = lds_frag(s_w2, 2 * f + 1, lane);
       }
@@ -227,81 +315,70 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
 #pragma unroll
       for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], hh[q], acc2[mb], 0, 0, 0);
     }
+    PSTAMP(4);
 
     // ---- output layer (fp32 VALU): this lane's 64 hidden rows, then the partner half's
-    float z[kActorMaxAct];
+    float z0 = 0.f, z1 = 0.f;
+    {
+#pragma clang fp contract(fast)
 #pragma unroll
-    for (int a = 0; a < kActorMaxAct; ++a) z[a] = 0.f;
+      for (int mb = 0; mb < kActorMB; ++mb)
 #pragma unroll
-    for (int mb = 0; mb < kActorMB; ++mb)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) {
-        const int row = 32 * mb + (g & 3) + 8 * (g >> 2) + 4 * h;
-        const float x = fmaxf(acc2[mb][g], 0.f);
-#pragma unroll
-        for (int a = 0; a < kActorMaxAct; ++a)
-          if (a < d.n_act) z[a] += w3[a * kActorRows + row] * x;
-      }
-#pragma unroll
-    for (int a = 0; a < kActorMaxAct; ++a)
-      if (a < d.n_act) z[a] = z[a] + __shfl_xor(z[a], 32) + b3[a];
-
-    // ---- softmax (fp32, max-subtracted like torch) + Categorical sample
-    float zmax = z[0];
-#pragma unroll
-    for (int a = 1; a < kActorMaxAct; ++a)
-      if (a < d.n_act) zmax = fmaxf(zmax, z[a]);
-    float e[kActorMaxAct], se = 0.f;
-#pragma unroll
-    for (int a = 0; a < kActorMaxAct; ++a)
-      if (a < d.n_act) { e[a] = expf(z[a] - zmax); se += e[a]; }
-    const int hl_ = 32 * wv + r;  // house within the block tile
-    const bool valid = hl_ < nb;
-    const int64_t i = b0 + hl_;
-    const float u = philox_u01f(p.seed, (uint64_t)(p.goff + i), tick);
-    // Categorical(probs).sample(): first action whose cumulative probability exceeds u
-    float pr[kActorMaxAct];
-    int act = d.n_act - 1;
-    float cum = 0.f;
-    bool found = false;
-#pragma unroll
-    for (int a = 0; a < kActorMaxAct; ++a)
-      if (a < d.n_act) {
-        pr[a] = e[a] / se;
-        if (out.probs && valid && h == 0) out.probs[i * d.n_act + a] = pr[a];
-        if (a < d.n_act - 1 && !found) {
-          cum += pr[a];
-          if (u < cum) { act = a; found = true; }
+        for (int g = 0; g < 16; ++g) {
+          const int row = 32 * mb + (g & 3) + 8 * (g >> 2) + 4 * h;
+          const float x = fmaxf(acc2[mb][g], 0.f);
+          const float2 w = *reinterpret_cast<const float2*>(w3 + row * kActorNA);
+          z0 += w.x * x;
+          z1 += w.y * x;
         }
-      }
-    float pa = 0.f;
-#pragma unroll
-    for (int a = 0; a < kActorMaxAct; ++a)
-      if (a == act) pa = pr[a];
+    }
+    z0 = z0 + __shfl_xor(z0, 32) + b3[0];
+    z1 = z1 + __shfl_xor(z1, 32) + b3[1];
+
+    // ---- softmax over the 2 actions (fp32, max-subtracted like torch) + Categorical sample
+    const float zmax = fmaxf(z0, z1);
+    const float e0 = expf(z0 - zmax), e1 = expf(z1 - zmax);
+    const float se = e0 + e1;
+    const float p0 = e0 / se, p1 = e1 / se;
+    const bool valid = r < nb;
+    const uint32_t i = b0 + (uint32_t)r;
+    // Categorical(probs).sample(): action 0 iff u < p0
+    const float u = philox_u01f(p.seed, (uint64_t)p.goff + i, tick);
+    const int act = u < p0 ? 0 : 1;
+    const float pa = act ? p1 : p0;
     if (valid && h == 0) {
+      if (out.probs) *reinterpret_cast<float2*>(out.probs + 2 * (size_t)i) = make_float2(p0, p1);
       if (out.action) out.action[i] = (uint8_t)act;
       if (out.prob) out.prob[i] = pa;
     }
     if (out.count_next) {
       // the ON houses the new actions produce (hvac.py:43-64 on action != 0), per capacity class
-      const bool on1 = valid && h == 0 && hv_on(hvac_fsm(s_hw[hl_], act != 0, p.dt, p.L));
-      const int cls = valid ? p.cap_idx[i] : 0;
+      const bool on1 = valid && h == 0 && hv_on(hvac_fsm(w_hw[r], act != 0, p.dt, p.L));
+      const int cls = valid ? w_cls[r] : 0;
       for (int k = 0; k < p.n_cap; ++k) {
         const unsigned long long m = __ballot(on1 && cls == k);
         if (lane == 0 && m) atomicAdd(&s_hist[k], (unsigned)__popcll(m));
       }
     }
+    PSTAMP(5);
+  }
+  if (PROF && lane == 0) {
+    for (int k = 0; k < 8; ++k) out.prof[(blockIdx.x * nw + wv) * 8 + k] = pacc[k];
   }
   if (out.count_next) {
     __syncthreads();
     if (tid < p.n_cap && s_hist[tid])
       atomicAdd(&out.count_next[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)s_hist[tid]);
   }
+#undef PSTAMP
 }
 
-template __global__ void k_actor<1>(KParams, ObsArgs, ActorDims, const double*, const unsigned char*,
-                                    ActorOut, uint64_t, const TickArgs*);
-template __global__ void k_actor<3>(KParams, ObsArgs, ActorDims, const double*, const unsigned char*,
-                                    ActorOut, uint64_t, const TickArgs*);
+#define MDR_INST_ACTOR(P, F)                                                                   \
+  template __global__ void k_actor<P, F>(KParams, ObsArgs, ActorDims, const double*, const unsigned char*, \
+                                         ActorOut, uint64_t, const TickArgs*);
+MDR_INST_ACTOR(1, false)
+MDR_INST_ACTOR(3, false)
+MDR_INST_ACTOR(1, true)
+MDR_INST_ACTOR(3, true)
 
 }  // namespace mdr

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "mdr_actor.h"
+#include "mdr_obs_dev.h"
 #include "mdr_kernels.h"
 
 using namespace mdr;
@@ -870,20 +871,22 @@ ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw) 
   d.off_w1 = 0;
   d.off_w2 = kActorMB * d.ks1 * 2048;
   d.off_tail = d.off_w2 + kActorMB * d.ks2 * 2048;
-  d.off_end = align16(d.off_tail + ((2 + a.n_act) * kActorRows + a.n_act) * 4);
-  const int HB = 32 * nw;
+  d.off_end = align16(d.off_tail + ((2 + kActorNA) * kActorRows + kActorNA) * 4);
   const int K = sp ? sp->n_comm : 0, M = sp ? mdr_msg_width(sp) : 0;
-  d.lds_obs = d.off_end;
-  d.lds_msg = d.lds_obs + align16((HB * fs + 16 * d.ks1) * 4);
-  const int nmsg = (sp && sp->comm_mode == MDR_COMM_RING) ? (K / 2 + HB + (K + 1) / 2) * M : 0;
-  d.lds_hw = d.lds_msg + align16(nmsg * 4);
-  d.lds_hist = d.lds_hw + HB * 4;
-  d.lds_total = d.lds_hist + MDR_MAX_CAP * 4;
+  const bool ring = sp && sp->comm_mode == MDR_COMM_RING && K > 0;
+  d.lds_cf = d.off_end;
+  d.lds_hist = d.lds_cf + align16(kObsConst * 4);
+  d.lds_wave = d.lds_hist + MDR_MAX_CAP * 4;
+  d.w_msg = align16((32 * fs + 16 * d.ks1) * 4);
+  d.w_hw = d.w_msg + align16((ring ? (K / 2 + 32 + (K + 1) / 2) * M : 0) * 4);
+  d.w_cls = d.w_hw + 32 * 4;
+  d.wave_stride = align16(d.w_cls + 32);
+  d.lds_total = d.lds_wave + nw * d.wave_stride;
   return d;
 }
 
 int actor_plan(const mdr_ctx* c, const mdr_obs_spec* sp, ActorDims* d, int* nw) {
-  for (int w = 8; w >= 2; w >>= 1) {
+  for (int w = 8; w >= 1; --w) {
     *d = actor_layout(c->actor, sp, w);
     if (d->lds_total <= 160 * 1024) { *nw = w; return MDR_OK; }
   }
@@ -895,18 +898,25 @@ int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const dou
   ActorDims d;
   int nw = 0;
   if (int rc = actor_plan(c, sp, &d, &nw)) return rc;
-  const int64_t ntile = (c->kp.n + 32 * nw - 1) / (32 * nw);
+  const int64_t ntile = (c->kp.n + 32 * nw - 1) / (32 * nw);  // blocks with at least one tile per wave
   const unsigned grid = (unsigned)std::min<int64_t>(ntile, (int64_t)c->n_cu);
   static bool lds_attr = false;  // > 64 KiB of dynamic LDS must be opted into per kernel
   if (!lds_attr) {
-    HIP_TRY(hipFuncSetAttribute((const void*)k_actor<1>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_TRY(hipFuncSetAttribute((const void*)k_actor<3>, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    for (const void* k : {(const void*)k_actor<1, false>, (const void*)k_actor<3, false>,
+                          (const void*)k_actor<1, true>, (const void*)k_actor<3, true>})
+      HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     lds_attr = true;
   }
-  if (c->actor.precision == MDR_PREC_BF16)
-    hipLaunchKernelGGL(k_actor<1>, dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, c->d_actor, out, tick, tkp);
-  else
-    hipLaunchKernelGGL(k_actor<3>, dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, c->d_actor, out, tick, tkp);
+#define MDR_LAUNCH_ACTOR(P, F)                                                                      \
+  hipLaunchKernelGGL((k_actor<P, F>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
+                     c->d_actor, out, tick, tkp)
+  const bool bf16 = c->actor.precision == MDR_PREC_BF16;
+  if (out.prof) {
+    if (bf16) MDR_LAUNCH_ACTOR(1, true); else MDR_LAUNCH_ACTOR(3, true);
+  } else {
+    if (bf16) MDR_LAUNCH_ACTOR(1, false); else MDR_LAUNCH_ACTOR(3, false);
+  }
+#undef MDR_LAUNCH_ACTOR
   LAUNCH_CHECK("k_actor");
   return MDR_OK;
 }
@@ -926,8 +936,8 @@ int mdr_actor_load(mdr_ctx* c, const mdr_actor_spec* a, const float* w1, const f
                    const float* b2, const float* w3, const float* b3, void* stream) {
   if (!c || !a || !w1 || !b1 || !w2 || !b2 || !w3 || !b3) return fail(MDR_EARG, "mdr_actor_load: null argument");
   if (a->n_in < 1 || a->n_in > kActorMaxIn || a->h1 < 1 || a->h1 > kActorRows || a->h2 < 1 ||
-      a->h2 > kActorRows || a->n_act < 2 || a->n_act > kActorMaxAct)
-    return fail(MDR_EARG, "mdr_actor_load: shape outside n_in <= 128, hidden <= 128, 2 <= n_act <= 4");
+      a->h2 > kActorRows || a->n_act != kActorNA)
+    return fail(MDR_EARG, "mdr_actor_load: shape outside n_in <= 128, hidden <= 128, n_act == 2");
   if (a->precision != MDR_PREC_BF16 && a->precision != MDR_PREC_BF16X3)
     return fail(MDR_EARG, "mdr_actor_load: bad precision");
   const ActorDims d = actor_layout(*a, nullptr, 2);
@@ -956,7 +966,7 @@ int mdr_actor_act(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc,
   if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_act: context not bound");
   if (int rc = check_actor_obs(c, sp, "mdr_actor_act")) return rc;
   hipStream_t st = S(stream);
-  ActorOut out{action, prob, probs, obs_out, nullptr};
+  ActorOut out{action, prob, probs, obs_out, nullptr, nullptr};
   if (count_next) {
     // the counts of the tick these actions drive go into the current slab (from zero)
     out.count_next = slab_at(c, c->ring);
@@ -965,6 +975,36 @@ int mdr_actor_act(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc,
   if (int rc = launch_actor(c, sp, obs_args(c, sp, sc), p_dev, tick, nullptr, out, st)) return rc;
   if (count_next) c->counts_ready = true;
   return MDR_OK;
+}
+
+int mdr_actor_profile(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc, const double* p_dev,
+                      double* cycles_out, void* stream) {
+  if (!c || !sp || !sc || !cycles_out) return fail(MDR_EARG, "mdr_actor_profile: null argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_profile: context not bound");
+  if (int rc = check_actor_obs(c, sp, "mdr_actor_profile")) return rc;
+  hipStream_t st = S(stream);
+  const int nb = c->n_cu * 8;  // waves (at most 8 per block, one block per CU)
+  unsigned long long* d = nullptr;
+  HIP_TRY(hipMalloc(&d, (size_t)nb * 8 * sizeof(unsigned long long)));
+  HIP_TRY(hipMemsetAsync(d, 0, (size_t)nb * 8 * sizeof(unsigned long long), st));
+  ActorOut out{nullptr, nullptr, nullptr, nullptr, nullptr, d};
+  int rc = launch_actor(c, sp, obs_args(c, sp, sc), p_dev, 0, nullptr, out, st);
+  std::vector<unsigned long long> h((size_t)nb * 8);
+  if (!rc && hipStreamSynchronize(st) == hipSuccess &&
+      hipMemcpy(h.data(), d, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost) == hipSuccess) {
+    int used = 0;
+    for (int k = 0; k < 8; ++k) cycles_out[k] = 0.0;
+    for (int b = 0; b < nb; ++b) {
+      if (h[b * 8 + 7] == 0) continue;
+      ++used;
+      for (int k = 0; k < 8; ++k) cycles_out[k] += (double)h[b * 8 + k];
+    }
+    for (int k = 0; k < 8; ++k) cycles_out[k] /= used ? used : 1;
+  } else if (!rc) {
+    rc = fail(MDR_EHIP, "mdr_actor_profile: readback");
+  }
+  hipFree(d);
+  return rc;
 }
 
 int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_scalars* osc,
@@ -1013,7 +1053,7 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
       ObsArgs ot = o;
       ot.sc_dev = c->d_obs_sc + 4 * t;
       ActorOut out{action ? action + (int64_t)t * act_stride : c->d_act, prob ? prob + (int64_t)t * prob_stride : nullptr,
-                   nullptr, nullptr, slab_at(c, c->ring)};
+                   nullptr, nullptr, slab_at(c, c->ring), nullptr};
       if (int rc = launch_actor(c, sp, ot, p_dev, 0, c->d_ticks + t, out, st)) return rc;
       if (int rc = launch_step(c, out.action, MDR_ACT_BUFFER, TickArgs{}, c->d_ticks + t,
                                reward + (int64_t)t * rew_stride, 0, MDR_CTRL_NONE, nullptr, p_dev, st))

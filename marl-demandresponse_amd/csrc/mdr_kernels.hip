@@ -479,12 +479,13 @@ __global__ void __launch_bounds__(kObsBlock) k_obs(KParams p, ObsArgs o, const d
   const int nb = (int)min((int64_t)kObsBlock, p.n - b0);
   float* tile = smem;                                  // [kObsBlock][F]
   float* msg = smem + ((kObsBlock * F + 3) & ~3);      // [lo + kObsBlock + hi][M]
-  const double P = p_dev ? *p_dev : o.p;
-
-  obs_stage_ring(p, o, b0, nb, msg, threadIdx.x, kObsBlock);
+  __shared__ float cf[kObsConst];
+  obs_consts(p, o, p_dev ? *p_dev : o.p, cf, threadIdx.x, kObsBlock);
+  __syncthreads();
+  obs_stage_ring(p, o, b0, nb, cf, msg, threadIdx.x, kObsBlock);
   __syncthreads();
   const int t = threadIdx.x;
-  if (t < nb) obs_build_row(p, o, P, b0 + t, t, msg, tile + t * F);
+  if (t < nb) obs_build_row(p, o, b0 + t, t, cf, msg, tile + t * F);
   __syncthreads();
   // coalesced flush of the contiguous tile obs[b0 .. b0+nb) rows
   const int64_t nflt = (int64_t)nb * F;
@@ -504,11 +505,14 @@ __global__ void __launch_bounds__(kObsBlock) k_obs(KParams p, ObsArgs o, const d
 __global__ void k_halo_pack(KParams p, ObsArgs o, int lo, int hi, float* out) {
   const int t = threadIdx.x;
   const int M = o.msg_w;
-  if (t < hi) msg_features(p, o, t % p.n, out + t * M);
+  __shared__ float cf[kObsConst];
+  obs_consts(p, o, o.p, cf, t, blockDim.x);  // (the message features use only cf[8..] and P_max/R)
+  __syncthreads();
+  if (t < hi) msg_features(p, o, t % p.n, cf, out + t * M);
   else if (t < hi + lo) {
     int64_t j = p.n - lo + (t - hi);
     if (j < 0) j = ((j % p.n) + p.n) % p.n;
-    msg_features(p, o, j, out + t * M);
+    msg_features(p, o, j, cf, out + t * M);
   }
 }
 

@@ -1,46 +1,131 @@
 // mdr_obs_dev.h — the norm_state_dict observation row (server/app/utils/norm.py:178-218) as
 // device functions, shared by k_obs (obs tensor) and k_actor (obs fused with the MA-PPO actor).
 //
-// A block stages the message features of its ring neighbourhood once in LDS (obs_stage_ring),
-// then every house's row is assembled from its own state + the staged messages (obs_build_row).
-// Feature order and arithmetic follow norm.py exactly (float64 math, one cast to float32 per
-// feature), so both kernels produce bit-identical rows.
+// A house's state is loaded once into registers (HouseRegs); its message features
+// (msg_from_regs) and its own row features (row_scalars) are computed from them.  Feature order
+// and arithmetic follow norm.py exactly (float64 math, one cast to float32 per feature), so every
+// kernel that uses these functions produces bit-identical rows.
 #pragma once
 #include "mdr_device.h"
 #include "mdr_kernels.h"
 
 namespace mdr {
 
-// Message a house j sends (Building.message, building.py:101-139, normalised by
-// norm.py:60-110): (T - target)/5, int(sso/L), P/R, P_max/R [, Ua, Ca, Cm, Hm ratios][, cop, lcf, cap]
-__device__ __forceinline__ void msg_features(const KParams& p, const ObsArgs& o, int64_t j,
-                                             float* dst) {
-  const uint32_t w = p.hvac[j];
-  const int cls = p.cap_idx[j];
-  const double pmax = p.p_on[cls];
+struct HouseRegs {
+  double T, Tm, tg, ua, ca, cm, hm;
+  uint32_t w;
+  int cls;
+};
+
+// thermal: also load Ua, Ca, Cm, Hm (state_prop.thermal / message_prop.thermal)
+__device__ __forceinline__ void house_load(const KParams& p, int64_t j, bool thermal, HouseRegs& r) {
+  r.T = p.t_air[j];
+  r.Tm = p.t_mass[j];
+  r.tg = p.target[j];
+  r.w = p.hvac[j];
+  r.cls = p.cap_idx[j];
+  if (thermal) {
+    r.ua = p.ua[j];
+    r.ca = p.ca[j];
+    r.cm = p.cm[j];
+    r.hm = p.hm[j];
+  } else {
+    r.ua = r.ca = r.cm = r.hm = 0.0;
+  }
+}
+
+__device__ __forceinline__ bool obs_needs_thermal(const ObsArgs& o) { return o.thermal_state || o.msg_thermal; }
+
+// House-independent features of a tick, computed once per block into LDS (float32, each from the
+// same float64 expression norm.py evaluates):
+//   cf[0] int(L / L) = 1, cf[1] cop/cop, cf[2] lcf/lcf, cf[3] P/R, cf[4] S/(R N), cf[5] deadband,
+//   cf[6] solar/1000, cf[7] (T_od - 20)/5, cf[8..10] message hvac constants (cop, lcf, cap),
+//   cf[kObsPmr + k] P_max(class k)/R  (a message's curr/max consumption features).
+constexpr int kObsPmr = 16;
+constexpr int kObsConst = kObsPmr + MDR_MAX_CAP;
+__device__ __forceinline__ void obs_consts(const KParams& p, const ObsArgs& o, double P, float* cf, int tid,
+                                           int nthr) {
   const double R = o.norm_reg_sig;
-  dst[0] = (float)((p.t_air[j] - p.target[j]) / 5.0);
-  dst[1] = (float)trunc((double)hv_sso(w) / (double)p.L);
-  dst[2] = (float)((hv_on(w) ? pmax : 0.0) / R);
-  dst[3] = (float)(pmax / R);
+  if (tid == 0) {
+    cf[0] = 1.f;
+    cf[1] = (float)(o.cfg_cop / o.cfg_cop);
+    cf[2] = (float)(o.cfg_lcf / o.cfg_lcf);
+    cf[3] = (float)(P / R);
+    cf[4] = (float)(o.s / (R * (double)p.n_global));
+    cf[5] = (float)p.deadband;
+    cf[6] = (float)(o.solar / 1000.0);
+    cf[7] = (float)((o.t_od - 20.0) / 5.0);
+    cf[8] = (float)o.cfg_cop;
+    cf[9] = (float)o.cfg_lcf;
+    cf[10] = (float)o.cfg_cap;
+  }
+  for (int k = tid; k < p.n_cap; k += nthr) cf[kObsPmr + k] = (float)(p.p_on[k] / R);
+}
+
+// int(sso / L) of norm.py: for 0 <= sso < 2^30 and L >= 1 the float64 quotient never rounds up to
+// the next integer, so truncating it equals the integer quotient
+__device__ __forceinline__ float sso_ratio(uint32_t w, int L) { return (float)(hv_sso(w) / (uint32_t)L); }
+
+// Message a house sends (Building.message, building.py:101-139, normalised by norm.py:60-110):
+// (T - target)/5, int(sso/L), P/R, P_max/R [, Ua, Ca, Cm, Hm ratios][, cop, lcf, cap]
+__device__ __forceinline__ void msg_from_regs(const KParams& p, const ObsArgs& o, const HouseRegs& r,
+                                              const float* cf, float* dst) {
+  const float pmr = cf[kObsPmr + r.cls];
+  dst[0] = (float)((r.T - r.tg) / 5.0);
+  dst[1] = sso_ratio(r.w, p.L);
+  dst[2] = hv_on(r.w) ? pmr : 0.f;  // (0.0 / R) == +0
+  dst[3] = pmr;
   int f = 4;
   if (o.msg_thermal) {
-    dst[f++] = (float)(p.ua[j] / o.cfg_ua);
-    dst[f++] = (float)(p.ca[j] / o.cfg_ca);
-    dst[f++] = (float)(p.cm[j] / o.cfg_cm);
-    dst[f++] = (float)(p.hm[j] / o.cfg_hm);
+    dst[f++] = (float)(r.ua / o.cfg_ua);
+    dst[f++] = (float)(r.ca / o.cfg_ca);
+    dst[f++] = (float)(r.cm / o.cfg_cm);
+    dst[f++] = (float)(r.hm / o.cfg_hm);
   }
   if (o.msg_hvac) {
-    dst[f++] = (float)o.cfg_cop;
-    dst[f++] = (float)o.cfg_lcf;
-    dst[f++] = (float)o.cfg_cap;
+    dst[f++] = cf[8];
+    dst[f++] = cf[9];
+    dst[f++] = cf[10];
   }
+}
+
+__device__ __forceinline__ void msg_features(const KParams& p, const ObsArgs& o, int64_t j, const float* cf,
+                                             float* dst) {
+  HouseRegs r;
+  house_load(p, j, o.msg_thermal != 0, r);
+  msg_from_regs(p, o, r, cf, dst);
+}
+
+// The house's own features (everything before the messages); returns how many were written.
+__device__ __forceinline__ int row_scalars(const KParams& p, const ObsArgs& o, const HouseRegs& r,
+                                           const float* cf, float* row) {
+  int f = 0;
+  row[f++] = hv_on(r.w) ? 1.f : 0.f;
+  row[f++] = hv_lock(r.w) ? 1.f : 0.f;
+  row[f++] = sso_ratio(r.w, p.L);
+  row[f++] = cf[0];
+  if (o.hvac_state) { row[f++] = cf[1]; row[f++] = cf[2]; }
+  row[f++] = cf[3];
+  row[f++] = cf[4];
+  row[f++] = cf[5];
+  row[f++] = (float)((r.T - 20.0) / 5.0);
+  row[f++] = (float)((r.Tm - 20.0) / 5.0);
+  row[f++] = (float)((r.tg - 20.0) / 5.0);
+  if (o.solar_state) row[f++] = cf[6];
+  if (o.thermal_state) {
+    row[f++] = (float)(r.ua / o.cfg_ua);
+    row[f++] = (float)(r.ca / o.cfg_ca);
+    row[f++] = (float)(r.cm / o.cfg_cm);
+    row[f++] = (float)(r.hm / o.cfg_hm);
+    row[f++] = cf[7];
+  }
+  return f;
 }
 
 // RING topology: message sources of the houses [b0, b0 + nb) are [b0 - lo, b0 + nb + hi);
 // their features go to msg[(s) * M] for s = 0 .. lo + nb + hi.  Threads tid, tid + nthr, ...
 __device__ __forceinline__ void obs_stage_ring(const KParams& p, const ObsArgs& o, int64_t b0, int nb,
-                                               float* msg, int tid, int nthr) {
+                                               const float* cf, float* msg, int tid, int nthr) {
   const int K = o.n_comm, M = o.msg_w;
   if (o.comm_mode != MDR_COMM_RING || K <= 0) return;
   const int lo = K / 2, hi = (K + 1) / 2;
@@ -54,57 +139,42 @@ __device__ __forceinline__ void obs_stage_ring(const KParams& p, const ObsArgs& 
     } else {
       j %= p.n;
       if (j < 0) j += p.n;
-      msg_features(p, o, j, msg + s * M);
+      msg_features(p, o, j, cf, msg + s * M);
     }
   }
 }
 
-// The F-wide row of local house i (= b0 + t) into row[0 .. F).  P: cluster power of the tick.
-// The hvac word is returned (callers that need the FSM state reuse the load).
-__device__ __forceinline__ uint32_t obs_build_row(const KParams& p, const ObsArgs& o, double P,
-                                                  int64_t i, int t, const float* msg, float* row) {
+// Messages of local house i (row index t in the block tile) appended at row[f ..).
+__device__ __forceinline__ void row_messages(const KParams& p, const ObsArgs& o, int64_t i, int t,
+                                             const float* cf, const float* msg, float* row, int f) {
   const int M = o.msg_w, K = o.n_comm;
   const int lo = K / 2;
-  const double R = o.norm_reg_sig;
-  const uint32_t w = p.hvac[i];
-  int f = 0;
-  row[f++] = hv_on(w) ? 1.f : 0.f;
-  row[f++] = hv_lock(w) ? 1.f : 0.f;
-  row[f++] = (float)trunc((double)hv_sso(w) / (double)p.L);
-  row[f++] = 1.f;  // int(lockout_duration / lockout_duration)
-  if (o.hvac_state) { row[f++] = (float)(o.cfg_cop / o.cfg_cop); row[f++] = (float)(o.cfg_lcf / o.cfg_lcf); }
-  row[f++] = (float)(P / R);
-  row[f++] = (float)(o.s / (R * (double)p.n_global));
-  row[f++] = (float)p.deadband;
-  const double tgt = p.target[i];
-  row[f++] = (float)((p.t_air[i] - 20.0) / 5.0);
-  row[f++] = (float)((p.t_mass[i] - 20.0) / 5.0);
-  row[f++] = (float)((tgt - 20.0) / 5.0);
-  if (o.solar_state) row[f++] = (float)(o.solar / 1000.0);
-  if (o.thermal_state) {
-    row[f++] = (float)(p.ua[i] / o.cfg_ua);
-    row[f++] = (float)(p.ca[i] / o.cfg_ca);
-    row[f++] = (float)(p.cm[i] / o.cfg_cm);
-    row[f++] = (float)(p.hm[i] / o.cfg_hm);
-    row[f++] = (float)((o.t_od - 20.0) / 5.0);
-  }
-  if (K > 0) {
-    if (o.comm_mode == MDR_COMM_RING) {
-      // neighbours [i-lo .. i-1, i+1 .. i+hi] (agent_communication_builder.py:65-83)
-      for (int k = 0; k < K; ++k) {
-        const int s = k < lo ? (t + k) : (t + lo + 1 + (k - lo));
-        for (int m = 0; m < M; ++m) row[f++] = msg[s * M + m];
-      }
-    } else {
-      float tmp[16];
-      for (int k = 0; k < K; ++k) {
-        const int64_t j = o.comm_table[i * K + k];
-        msg_features(p, o, j, tmp);
-        for (int m = 0; m < M; ++m) row[f++] = tmp[m];
-      }
+  if (K <= 0) return;
+  if (o.comm_mode == MDR_COMM_RING) {
+    // neighbours [i-lo .. i-1, i+1 .. i+hi] (agent_communication_builder.py:65-83)
+    for (int k = 0; k < K; ++k) {
+      const int s = k < lo ? (t + k) : (t + lo + 1 + (k - lo));
+      for (int m = 0; m < M; ++m) row[f++] = msg[s * M + m];
+    }
+  } else {
+    float tmp[16];
+    for (int k = 0; k < K; ++k) {
+      const int64_t j = o.comm_table[i * K + k];
+      msg_features(p, o, j, cf, tmp);
+      for (int m = 0; m < M; ++m) row[f++] = tmp[m];
     }
   }
-  return w;
+}
+
+// The F-wide row of local house i (= b0 + t) into row[0 .. F); cf: obs_consts of the tick.
+// The hvac word is returned (callers that need the FSM state reuse the load).
+__device__ __forceinline__ uint32_t obs_build_row(const KParams& p, const ObsArgs& o, int64_t i, int t,
+                                                  const float* cf, const float* msg, float* row) {
+  HouseRegs r;
+  house_load(p, i, o.thermal_state != 0, r);
+  const int f = row_scalars(p, o, r, cf, row);
+  row_messages(p, o, i, t, cf, msg, row, f);
+  return r.w;
 }
 
 }  // namespace mdr

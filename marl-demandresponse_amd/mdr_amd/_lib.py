@@ -112,6 +112,7 @@ SIGNATURES = {
     "mdr_actor_act": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, U64, VP, VP, VP, VP, I, VP]),
     "mdr_actor_rollout": (I, [VP, I, P(mdr_tick), P(mdr_obs_scalars), P(mdr_obs_spec), VP, I64, VP, I64,
                               VP, I64, VP, I, VP]),
+    "mdr_actor_profile": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, P(D), VP]),
     "mdr_rccl_unique_id": (I, [VP]),
     "mdr_rccl_init": (I, [VP, VP, I, I]),
     "mdr_rccl_allreduce": (I, [VP, VP, I64, I, VP]),
