@@ -84,6 +84,7 @@ struct mdr_ctx {
   int hpt = 2;                           // houses per thread of k_step (MDR_HPT env overrides)
   bool cached = false;                   // cached param-only thermal coefficients (MDR_VARIANT=coef)
   bool fastdiv = true;                   // shared-reciprocal exact division (MDR_FASTDIV=0 disables)
+  int tpw = 0;                           // k_step_pipe tiles per wave (MDR_TPW; 0: k_step_t)
   bool coef_dirty = true;
   double* d_coef = nullptr;              // [6][n] r1, r2, A3, A4, e1, e2
   int* d_flags = nullptr;                // [0] params_bad
@@ -175,6 +176,31 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
                      c->d_pen_partial, reward_lag)
   const bool hot_random = mode == MDR_ACT_RANDOM && lookahead == MDR_ACT_RANDOM;
   const bool hot_buffer = mode == MDR_ACT_BUFFER && lookahead == 0;
+  // software-pipelined form of the two hot configurations (k_step_pipe): individual_L2, <= 4
+  // capacity classes, no controller output, no reward lag, 2-byte aligned action rows
+  const bool pipe_ok = c->tpw >= 1 && c->hpt == 2 && c->fastdiv && !c->cached && (hot_random || hot_buffer) &&
+                       kp.penalty_mode == MDR_PEN_INDIVIDUAL_L2 && kp.n_cap <= kPipeMaxCap &&
+                       ctrl == MDR_CTRL_NONE && !reward_lag && (!action || ((uintptr_t)action & 1u) == 0);
+  if (pipe_ok) {
+    int tpw = c->tpw >= 8 ? 8 : c->tpw >= 4 ? 4 : c->tpw >= 2 ? 2 : 1;
+    if (hot_buffer) tpw = tpw >= 4 ? 4 : 2;  // the instantiated buffer variants
+    const dim3 grid(blocks(blocks(kp.n, 128), 4 * tpw));  // every tile covered: ceil(tiles / (4 waves x tpw))
+#define MDR_LAUNCH_PIPE(T, A, LA)                                                                     \
+  hipLaunchKernelGGL((k_step_pipe<T, A, LA>), grid, dim3(256), 0, st, kp, action, tk, tkp, cur, reward, \
+                     p_out, nxt, zer)
+    if (hot_random) {
+      if (tpw == 8) MDR_LAUNCH_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
+      else if (tpw == 4) MDR_LAUNCH_PIPE(4, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
+      else if (tpw == 2) MDR_LAUNCH_PIPE(2, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
+      else MDR_LAUNCH_PIPE(1, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
+    } else {
+      if (tpw >= 4) MDR_LAUNCH_PIPE(4, MDR_ACT_BUFFER, 0);
+      else MDR_LAUNCH_PIPE(2, MDR_ACT_BUFFER, 0);
+    }
+#undef MDR_LAUNCH_PIPE
+    LAUNCH_CHECK("k_step_pipe");
+    return MDR_OK;
+  }
   if (c->hpt == 2 && c->fastdiv) {
     if (c->cached) {
       if (hot_random) MDR_LAUNCH_STEP(2, true, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
@@ -282,6 +308,10 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   if (const char* e = getenv("MDR_HPT")) c->hpt = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("MDR_VARIANT")) c->cached = strcmp(e, "coef") == 0;
   if (const char* e = getenv("MDR_FASTDIV")) c->fastdiv = atoi(e) != 0;
+  // k_step_pipe depth measured on MI355X (tools/kbench.py, profiles/r01b_kbench_pipe.log): 2 tiles per
+  // wave up to ~1.5M houses per shard, 4 above; MDR_TPW=0 selects the one-tile kernel k_step_t
+  c->tpw = cfg->n_local <= 1572864 ? 2 : 4;
+  if (const char* e = getenv("MDR_TPW")) c->tpw = atoi(e);
   if (c->cached) {
     k.coef_stride = cfg->n_local;
     if (hipMalloc(&c->d_coef, 6 * sizeof(double) * cfg->n_local) != hipSuccess)

@@ -64,6 +64,11 @@ __global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, Tick
                          int ctrl, uint8_t* ctrl_out, double* p_out, int lookahead,
                          unsigned long long* next_slab, unsigned long long* zero_slab,
                          double* pen_partial, int reward_lag);
+template <int TPW, int ACT, int LA>
+__global__ void k_step_pipe(KParams p, const uint8_t* action, TickArgs tk, const TickArgs* tkp,
+                            const unsigned long long* counts, double* reward, double* p_out,
+                            unsigned long long* next_slab, unsigned long long* zero_slab);
+constexpr int kPipeMaxCap = 4;
 __global__ void k_probe_stream(KParams p, double* reward);
 __global__ void k_refresh(KParams p, double* coef, int* params_bad);
 __global__ void k_div_check(const double* a, const double* b, int64_t n, unsigned long long* mismatches);

@@ -310,6 +310,199 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
   }
 }
 
+// --------------------------------------------------------------------------------------- K1'
+// Software-pipelined form of the hot step configurations (HPT = 2, shared-reciprocal division,
+// individual_L2, <= kPipeCap capacity classes): a wave steps TPW tiles (strided over the grid),
+// issuing tile k+1's loads before computing tile k, so the memory stream of one tile overlaps the
+// fp64 arithmetic of the previous one.  Straight-line code (TPW and the class loops are unrolled
+// at compile time): a loop in the body would make the compiler drain the in-flight loads at its
+// header.  Results are bit-identical to k_step_t (same per-house expressions).
+constexpr int kPipeCap = 4;
+
+struct Tile2 {
+  double2 T, Tm, ua, ca, cm, hm, tg;
+  uint2 w;
+  unsigned cls;  // two u8 capacity classes
+  unsigned act;  // two u8 actions (MDR_ACT_BUFFER)
+};
+
+// full: the whole wave tile is inside the shard (wave-uniform), so every lane takes the 16-B path;
+// otherwise (the last, ragged tile) each house is loaded on its own from a clamped index (a house
+// past the end is computed on a copy of house n-1 and never stored or counted)
+template <bool ACT_BUF>
+__device__ __forceinline__ void load_tile2(const KParams& p, const uint8_t* action, uint32_t i0, uint32_t n,
+                                           bool full, Tile2& t) {
+  if (full) {
+    const uint32_t o8 = i0 * 8u;
+    t.T = ldo<double2>(p.t_air, o8); t.Tm = ldo<double2>(p.t_mass, o8);
+    t.ua = ldo<double2>(p.ua, o8); t.ca = ldo<double2>(p.ca, o8); t.cm = ldo<double2>(p.cm, o8);
+    t.hm = ldo<double2>(p.hm, o8); t.tg = ldo<double2>(p.target, o8);
+    t.w = ldo<uint2>(p.hvac, i0 * 4u);
+    t.cls = ldo<unsigned short>(p.cap_idx, i0);
+    t.act = ACT_BUF ? (unsigned)ldo<unsigned short>(action, i0) : 0u;
+  } else {
+    const uint32_t a = i0 < n ? i0 : n - 1u, b = i0 + 1u < n ? i0 + 1u : n - 1u;
+    t.T = make_double2(p.t_air[a], p.t_air[b]); t.Tm = make_double2(p.t_mass[a], p.t_mass[b]);
+    t.ua = make_double2(p.ua[a], p.ua[b]); t.ca = make_double2(p.ca[a], p.ca[b]);
+    t.cm = make_double2(p.cm[a], p.cm[b]); t.hm = make_double2(p.hm[a], p.hm[b]);
+    t.tg = make_double2(p.target[a], p.target[b]);
+    t.w = make_uint2(p.hvac[a], p.hvac[b]);
+    t.cls = (unsigned)p.cap_idx[a] | ((unsigned)p.cap_idx[b] << 8);
+    t.act = ACT_BUF ? ((unsigned)action[a] | ((unsigned)action[b] << 8)) : 0u;
+  }
+}
+
+template <int TPW, int ACT, int LA>
+__global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __restrict__ action, TickArgs tk0,
+                                                   const TickArgs* tkp, const unsigned long long* __restrict__ counts,
+                                                   double* __restrict__ reward, double* p_out,
+                                                   unsigned long long* next_slab, unsigned long long* zero_slab) {
+  constexpr int HPT = 2;
+  constexpr bool AB = ACT == MDR_ACT_BUFFER;
+  __shared__ unsigned hist[MDR_MAX_CAP];
+  const int tid = threadIdx.x;
+  const int lane = tid & 63;
+  if (tid < p.n_cap) hist[tid] = 0;
+  if (zero_slab && blockIdx.x == 0)
+    for (int j = tid; j < kCountShards * p.n_cap; j += blockDim.x) zero_slab[j] = 0ull;
+  const uint32_t n = (uint32_t)p.n;
+  const uint32_t ntiles = (n + 64u * HPT - 1u) / (64u * HPT);
+  const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
+  const uint32_t gw = blockIdx.x * (blockDim.x >> 6) + (uint32_t)(tid >> 6);
+
+  // the tick's cluster power: this lane's count-slab shard (issued before the first tile's loads,
+  // so waiting for it leaves them in flight)
+  unsigned long long cnt[kPipeCap];
+#pragma unroll
+  for (int k = 0; k < kPipeCap; ++k) cnt[k] = counts ? counts[lane * p.n_cap + (k < p.n_cap ? k : 0)] : 0ull;
+  // the cooling-capacity tables as uniform scalars (scalar loads: no vmcnt, so a lookup never
+  // drains the in-flight tile loads)
+  double q_on[kPipeCap];
+#pragma unroll
+  for (int k = 0; k < kPipeCap; ++k) q_on[k] = p.q_on[k < p.n_cap ? k : 0];
+  auto full_tile = [&](uint32_t t) { return (t + 1u) * (64u * HPT) <= n; };
+  Tile2 buf[2];
+  if (gw < ntiles) load_tile2<AB>(p, action, gw * (64u * HPT) + (uint32_t)lane * HPT, n, full_tile(gw), buf[0]);
+  if (LA) __syncthreads();  // hist zeroed (a bare s_barrier: the tile loads stay in flight)
+  const TickArgs tk = tkp ? *tkp : tk0;
+  double sig_term = 0.0;
+  if (counts) {
+    double P = 0.0;
+#pragma unroll
+    for (int k = 0; k < kPipeCap; ++k)
+      if (k < p.n_cap) P += (double)wave_sum_counts(cnt[k]) * p.p_on[k];
+    const double x = (P - tk.s_prev) / (double)p.n_global;
+    sig_term = p.alpha_sig * (x * x) / p.norm_sig;
+    if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P;
+  }
+  const bool tick_fast = !*p.params_bad && p.fast_tick_ok && fabs(tk.t_od_prev) < 1048576.0 &&
+                         fabs(tk.solar) < 1099511627776.0;
+  unsigned la_cnt[kPipeCap] = {0u, 0u, 0u, 0u};
+
+#pragma unroll
+  for (int k = 0; k < TPW; ++k) {
+    const uint32_t tile = gw + (uint32_t)k * nwaves;
+    if (tile >= ntiles) break;  // wave-uniform
+    if (k + 1 < TPW && tile + nwaves < ntiles)
+      load_tile2<AB>(p, action, (tile + nwaves) * (64u * HPT) + (uint32_t)lane * HPT, n,
+                     full_tile(tile + nwaves), buf[(k + 1) & 1]);
+    const Tile2& in = buf[k & 1];
+    const uint32_t i0 = tile * (64u * HPT) + (uint32_t)lane * HPT;
+    const double T[2] = {in.T.x, in.T.y}, Tm[2] = {in.Tm.x, in.Tm.y}, ua[2] = {in.ua.x, in.ua.y};
+    const double ca[2] = {in.ca.x, in.ca.y}, cm[2] = {in.cm.x, in.cm.y}, hm[2] = {in.hm.x, in.hm.y};
+    const double tg[2] = {in.tg.x, in.tg.y};
+    const uint32_t w0[2] = {in.w.x, in.w.y};
+    const int cls[2] = {(int)(in.cls & 0xFF), (int)((in.cls >> 8) & 0xFF)};
+    bool valid[2] = {i0 < n, i0 + 1 < n};
+
+    bool rnd[2] = {false, false}, rnd1[2] = {false, false};
+    if (ACT == MDR_ACT_RANDOM || LA == MDR_ACT_RANDOM) {
+      const WaveRandom wr(p.seed, p.goff + (uint64_t)tile * (64u * HPT), tk.tick);
+#pragma unroll
+      for (int h = 0; h < HPT; ++h) {
+        rnd[h] = wr.get(p.goff + i0 + h, false);
+        rnd1[h] = wr.get(p.goff + i0 + h, true);
+      }
+    }
+    bool house_ok = true;
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) house_ok = house_ok && fabs(T[h]) < 1048576.0 && fabs(Tm[h]) < 1048576.0;
+    const bool tile_fast = tick_fast && __all(house_ok);
+
+    double Tn[2], Tmn[2], rw[2];
+    uint32_t w[2];
+    bool on1[2];
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) {
+      const bool a = valid[h] && (AB ? ((in.act >> (8 * h)) & 0xFFu) != 0u
+                                     : pick_action(ACT, action, i0 + h, rnd[h], T[h], tg[h], p.deadband, w0[h]));
+      w[h] = hvac_fsm(w0[h], a, p.dt, p.L);
+      const bool on = hv_on(w[h]);
+      double qc = q_on[0];
+#pragma unroll
+      for (int c = 1; c < kPipeCap; ++c) qc = cls[h] == c ? q_on[c] : qc;
+      const double q = on ? qc : 0.0;
+      RcCoef kc;
+      if (tile_fast) {
+        kc = rc_coeffs_t<true>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+        rc_apply_t<true>(T[h], Tm[h], ua[h], ca[h], hm[h], kc, q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
+      } else {
+        kc = rc_coeffs_t<false>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+        rc_apply_t<false>(T[h], Tm[h], ua[h], ca[h], hm[h], kc, q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
+      }
+      const double tpen = p.alpha_temp * deadband_l2(tg[h], p.deadband, Tn[h]);
+      rw[h] = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig_term);
+      on1[h] = false;
+      if (LA) {
+        bool an;
+        if (LA == MDR_ACT_RANDOM) an = rnd1[h];
+        else if (LA == MDR_ACT_ALWAYS_ON) an = true;
+        else if (LA == kActBangBang) an = ctrl_bangbang(Tn[h], tg[h]);
+        else an = ctrl_deadband(Tn[h], tg[h], p.deadband, on);
+        on1[h] = valid[h] && hv_on(hvac_fsm(w[h], an, p.dt, p.L));
+      }
+    }
+    if (valid[1]) {
+      const uint32_t o8 = i0 * 8u;
+      sto(p.t_air, o8, make_double2(Tn[0], Tn[1]));
+      sto(p.t_mass, o8, make_double2(Tmn[0], Tmn[1]));
+      sto(p.hvac, i0 * 4u, make_uint2(w[0], w[1]));
+      if (counts) sto(reward, o8, make_double2(rw[0], rw[1]));
+    } else if (valid[0]) {
+      p.t_air[i0] = Tn[0]; p.t_mass[i0] = Tmn[0]; p.hvac[i0] = w[0];
+      if (counts) reward[i0] = rw[0];
+    }
+    if (LA) {
+#pragma unroll
+      for (int c = 0; c < kPipeCap; ++c)
+        if (c < p.n_cap)
+          la_cnt[c] += (unsigned)__popcll(__ballot(on1[0] && cls[0] == c)) +
+                       (unsigned)__popcll(__ballot(on1[1] && cls[1] == c));
+    }
+  }
+  if (LA) {
+    if (lane == 0) {
+#pragma unroll
+      for (int c = 0; c < kPipeCap; ++c)
+        if (c < p.n_cap && la_cnt[c]) atomicAdd(&hist[c], la_cnt[c]);
+    }
+    __syncthreads();
+    if (tid < p.n_cap && hist[tid])
+      atomicAdd(&next_slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)hist[tid]);
+  }
+}
+
+#define MDR_INST_PIPE(T, A, LA)                                                                    \
+  template __global__ void k_step_pipe<T, A, LA>(KParams, const uint8_t*, TickArgs, const TickArgs*, \
+                                                 const unsigned long long*, double*, double*,         \
+                                                 unsigned long long*, unsigned long long*);
+MDR_INST_PIPE(1, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
+MDR_INST_PIPE(2, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
+MDR_INST_PIPE(4, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
+MDR_INST_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
+MDR_INST_PIPE(2, MDR_ACT_BUFFER, 0)
+MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0)
+
 #define MDR_INST_STEP(H, C, F, A, LA)                                                            \
   template __global__ void k_step_t<H, C, F, A, LA>(                                             \
       KParams, const uint8_t*, int, TickArgs, const TickArgs*, const unsigned long long*,        \

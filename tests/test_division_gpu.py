@@ -57,9 +57,47 @@ def test_step_variants_bit_identical(variant):
         np.testing.assert_array_equal(s0[k], s1[k])
 
 
-def test_fast_division_guard_fallback():
+@pytest.mark.parametrize("tpw", ["1", "2", "4", "8"])
+@pytest.mark.parametrize("mode", ["random", "buffer"])
+def test_pipelined_step_bit_identical(tpw, mode):
+    """k_step_pipe (MDR_TPW tiles per wave, next tile's loads issued before this tile's math) ==
+    k_step_t bit for bit: ragged shard (odd size, partial last tile), fused random actions with
+    lookahead and buffer actions, per-step API and graph rollouts."""
+    import torch
+
+    import golden_util as gu
+    from mdr_amd.environment import Environment
+
+    n = 100_003
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    envs = []
+    for t in ("0", tpw):
+        os.environ["MDR_TPW"] = t
+        envs.append(Environment(props, rng=random.Random(2), population="synthetic", seed=3))
+    os.environ.pop("MDR_TPW")
+    g = torch.Generator(device="cuda").manual_seed(11)
+    for t in range(25):
+        if mode == "random":
+            rs = [e.step_tensor(None, action_mode="random", lookahead="random").clone() for e in envs]
+        else:
+            a = (torch.rand(n, device="cuda", generator=g) < 0.5).to(torch.uint8)
+            rs = [e.step_tensor(a, action_mode="buffer").clone() for e in envs]
+        assert torch.equal(rs[0], rs[1]), f"tick {t}"
+        assert float(envs[0].shard.p_dev.item()) == float(envs[1].shard.p_dev.item())
+    acts = (torch.rand((30, n), device="cuda", generator=g) < 0.5).to(torch.uint8) if mode == "buffer" else None
+    rr = [e.rollout(30, actions=acts, action_mode=mode) for e in envs]
+    assert torch.equal(rr[0], rr[1])
+    s0, s1 = envs[0].shard.host_state(), envs[1].shard.host_state()
+    for k in s0:
+        np.testing.assert_array_equal(s0[k], s1[k])
+
+
+@pytest.mark.parametrize("tpw", ["0", "4"])
+def test_fast_division_guard_fallback(tpw):
     """Out-of-range parameters (Ua = 1e-9 < 2^-20) or temperatures route the tile to the plain
-    `/` operator: results stay bit-identical to the reference-order kernel."""
+    `/` operator: results stay bit-identical to the reference-order kernel (k_step_t and
+    k_step_pipe)."""
     import torch
 
     import golden_util as gu
@@ -70,12 +108,13 @@ def test_fast_division_guard_fallback():
     envs = []
     for fast in ("0", "1"):
         os.environ["MDR_FASTDIV"] = fast
+        os.environ["MDR_TPW"] = tpw if fast == "1" else "0"
         e = Environment(props, rng=random.Random(2), population="synthetic", seed=3)
         e.shard.ua[17] = 1e-9
         e.shard.t_air[4000] = 3.0e6
         e.shard.params_changed()
         envs.append(e)
-    os.environ.pop("MDR_FASTDIV")
+    os.environ.pop("MDR_FASTDIV"), os.environ.pop("MDR_TPW")
     for t in range(10):
         rs = [e.step_tensor(None, action_mode="random", lookahead="random").clone() for e in envs]
         assert torch.equal(rs[0], rs[1])

@@ -34,10 +34,14 @@ def main():
             os.environ["MDR_VARIANT"] = "coef" if "coef" in v else "raw"
             os.environ["MDR_FASTDIV"] = "1" if v.startswith("f") else "0"
             os.environ["MDR_GRID_OVERSUB"] = v.split("g")[-1] if "g" in v[4:] else "1"
+            os.environ["MDR_TPW"] = v.split("t")[-1] if "t" in v[4:] else "0"  # fast2t4: k_step_pipe, 4 tiles/wave
             envs[v] = Environment(env_props(n), device="cuda:0", rng=random.Random(1),
                                   population="synthetic", seed=5)
             rews = torch.empty(n, dtype=torch.float64, device="cuda:0")
-            envs[v].rollout(a.launches, action_mode="random", rewards=rews)  # captures the graph
+            # one driver window replayed every round: the events time the graph alone (no host drivers)
+            envs[v]._kb_ticks = envs[v].driver_window(a.launches)
+            sh = envs[v].shard
+            sh.rollout(envs[v]._kb_ticks, None, 0, L.ACT_RANDOM, rews, 0, True)  # captures the graph
             envs[v]._kb_rew = rews
         torch.cuda.synchronize()
         for r in range(a.rounds):
@@ -51,9 +55,11 @@ def main():
                     e1.record()
                 else:
                     torch.cuda.synchronize()
-                    e0.record()
-                    env.rollout(a.launches, action_mode="random", rewards=env._kb_rew)
-                    e1.record()
+                    ls = sh.launch_stream(True)
+                    sh.rollout(env._kb_ticks, None, 0, L.ACT_RANDOM, env._kb_rew, 0, True)  # stage ticks
+                    e0.record(ls)
+                    sh.rollout(env._kb_ticks, None, 0, L.ACT_RANDOM, env._kb_rew, 0, True)
+                    e1.record(ls)
                 e1.synchronize()
                 us = e0.elapsed_time(e1) * 1e3 / a.launches
                 res.setdefault((n, v), []).append(us)
