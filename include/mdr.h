@@ -15,6 +15,7 @@
  *   controllers                    server/app/core/agents/controllers/bangbang_controllers.py:25-89,
  *                                  server/app/core/agents/controllers/greedy_myopic_controller.py:67-104
  *   Environment.reset / noise      server/app/core/environment/environment.py:49-70,161-194
+ *   PowerInterpolator (base power) server/app/core/environment/power_grid/interpolation.py:186-264
  *
  * The reference has no FFI: its boundary is a Python object (Environment.reset/step).  The
  * Python layer mdr_amd.Environment keeps that object surface and binds these symbols with ctypes
@@ -120,8 +121,9 @@ typedef struct mdr_ctx mdr_ctx;
 
 /* ---- lifecycle ------------------------------------------------------------------------- */
 int mdr_abi_version(void);
-/* sizeof of the ABI structs, for binding checks: out[0..6] = mdr_config, mdr_soa, mdr_tick,
- * mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars, mdr_actor_spec; returns the number written */
+/* sizeof of the ABI structs, for binding checks: out[0..7] = mdr_config, mdr_soa, mdr_tick,
+ * mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars, mdr_actor_spec, mdr_interp_spec; returns the number
+ * written */
 int mdr_abi_sizes(int64_t* out, int n);
 const char* mdr_last_error(void);
 int mdr_create(mdr_ctx** out, const mdr_config* cfg);
@@ -274,6 +276,31 @@ int mdr_actor_rollout(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const md
                       const mdr_obs_spec* obs, uint8_t* action, int64_t act_stride, float* prob,
                       int64_t prob_stride, double* reward, int64_t rew_stride, double* p_dev,
                       int use_graph, void* stream);
+
+/* ---- interpolated base power ---------------------------------------- */
+/* Replaces PowerInterpolator (server/app/core/environment/power_grid/interpolation.py:24-264) as
+ * PowerGrid.power_step calls it every interp_update_period seconds (power_grid.py:149-161): the
+ * host draws the sampled house ids (random.choices, interpolation.py:218-224 — the reference's RNG
+ * stream) and the per-tick scalars; the per-house clip / nearest / multilinear lookup over the
+ * Monte-Carlo table (interpolate_grid_fast, :137-178) reads the device state directly.
+ * Axes in interp_dict_keys.csv order: Ua_ratio, Cm_ratio, Ca_ratio, Hm_ratio (nearest), air_temp,
+ * mass_temp, OD_temp (linear), HVAC_power (nearest), hour, date (linear). */
+#define MDR_INTERP_AXES 10
+typedef struct mdr_interp_spec {
+  int32_t len[MDR_INTERP_AXES]; /* grid points per axis (linear axes: >= 2, strictly ascending) */
+  const double* grid;           /* host: the axis values, concatenated in axis order */
+  const double* values;         /* host: the table, prod(len) doubles, C order over the axes */
+  double cfg_ua, cfg_cm, cfg_ca, cfg_hm; /* house_prop Ua, Cm, Ca, Hm (the ratio denominators) */
+} mdr_interp_spec;
+/* Copy the grid + table to the device (synchronous); replaces a previous table. */
+int mdr_interp_load(mdr_ctx* ctx, const mdr_interp_spec* spec);
+/* vals[s] (device double[n]) = the interpolated power of house ids[s] (device int64 global ids)
+ * at outdoor temperature od_temp and the point's hour / date (interpolation.py:204-216); houses
+ * outside this shard give +0.0, so a sum-allreduce of vals assembles the cluster's values. */
+int mdr_interp_values(mdr_ctx* ctx, const int64_t* ids, int n, double od_temp, double hour, double date,
+                      double* vals, void* stream);
+/* out[0] (device) = (sum of vals[0..n) in order) * multi_factor — the base power. */
+int mdr_interp_sum(const double* vals, int n, double multi_factor, double* out, void* stream);
 
 /* ---- multi-GPU (RCCL over xGMI) --------------------------------------------------------- */
 /* ncclUniqueId is 128 bytes; rank 0 creates it, the caller broadcasts it (torch.distributed). */

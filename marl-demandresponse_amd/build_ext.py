@@ -12,8 +12,8 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
-SRC = [os.path.join(HERE, "csrc", f) for f in ("mdr_kernels.hip", "mdr_actor.hip", "mdr_capi.hip")]
-HDR = [os.path.join(HERE, "csrc", f) for f in ("mdr_kernels.h", "mdr_device.h", "mdr_obs_dev.h", "mdr_actor.h")] + [
+SRC = [os.path.join(HERE, "csrc", f) for f in ("mdr_kernels.hip", "mdr_actor.hip", "mdr_interp.hip", "mdr_capi.hip")]
+HDR = [os.path.join(HERE, "csrc", f) for f in ("mdr_kernels.h", "mdr_device.h", "mdr_obs_dev.h", "mdr_actor.h", "mdr_interp.h")] + [
     os.path.join(ROOT, "include", "mdr.h")]
 OUT = os.path.join(HERE, "mdr_amd", "libmdr_hip.so")
 ARCH = os.environ.get("MDR_OFFLOAD_ARCH", "gfx950")

@@ -16,6 +16,7 @@
 #include <vector>
 
 #include "mdr_actor.h"
+#include "mdr_interp.h"
 #include "mdr_obs_dev.h"
 #include "mdr_kernels.h"
 
@@ -122,6 +123,11 @@ struct mdr_ctx {
   int obs_sc_cap = 0;
   uint8_t* d_act = nullptr;    // [n_local] actor actions when the caller keeps none
   std::map<std::vector<int64_t>, hipGraphExec_t> actor_graphs;
+  // interpolated base power (row a10): grid | table | capacities
+  double* d_interp = nullptr;
+  size_t interp_bytes = 0;
+  InterpArgs interp{};
+  bool interp_ready = false;
 };
 
 namespace {
@@ -238,11 +244,12 @@ extern "C" {
 int mdr_abi_version(void) { return MDR_ABI_VERSION; }
 
 int mdr_abi_sizes(int64_t* out, int n) {
-  const int64_t v[7] = {(int64_t)sizeof(mdr_config), (int64_t)sizeof(mdr_soa), (int64_t)sizeof(mdr_tick),
+  const int64_t v[8] = {(int64_t)sizeof(mdr_config), (int64_t)sizeof(mdr_soa), (int64_t)sizeof(mdr_tick),
                         (int64_t)sizeof(mdr_pop_spec), (int64_t)sizeof(mdr_obs_spec),
-                        (int64_t)sizeof(mdr_obs_scalars), (int64_t)sizeof(mdr_actor_spec)};
+                        (int64_t)sizeof(mdr_obs_scalars), (int64_t)sizeof(mdr_actor_spec),
+                        (int64_t)sizeof(mdr_interp_spec)};
   int k = 0;
-  for (; out && k < n && k < 7; ++k) out[k] = v[k];
+  for (; out && k < n && k < 8; ++k) out[k] = v[k];
   return k;
 }
 
@@ -346,6 +353,7 @@ int mdr_destroy(mdr_ctx* c) {
   for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
   for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
   hipFree(c->d_actor);
+  hipFree(c->d_interp);
   hipFree(c->d_act);
   hipFree(c->d_obs_sc);
   if (c->h_obs_sc) hipHostFree(c->h_obs_sc);
@@ -1120,6 +1128,83 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
   }
   HIP_TRY(hipGraphLaunch(it->second, st));
   c->counts_ready = false;
+  return MDR_OK;
+}
+
+}  // extern "C"
+
+// ------------------------------------------------------------------------ interpolation (a10)
+extern "C" {
+
+int mdr_interp_load(mdr_ctx* c, const mdr_interp_spec* sp) {
+  if (!c || !sp || !sp->grid || !sp->values) return fail(MDR_EARG, "mdr_interp_load: null argument");
+  InterpArgs a{};
+  int64_t ng = 0, total = 1;
+  for (int k = 0; k < kInterpAxes; ++k) {
+    const bool linear = !(k < 4 || k == 7);
+    if (sp->len[k] < (linear ? 2 : 1) || sp->len[k] > (1 << 16))
+      return fail(MDR_EARG, "mdr_interp_load: axis length out of range");
+    a.len[k] = sp->len[k];
+    a.off[k] = (int)ng;
+    double lo = sp->grid[ng], hi = sp->grid[ng];
+    for (int i = 0; i < sp->len[k]; ++i) {
+      const double g = sp->grid[ng + i];
+      if (linear && i > 0 && !(g > sp->grid[ng + i - 1]))
+        return fail(MDR_EARG, "mdr_interp_load: a linear axis is not strictly ascending");
+      lo = g < lo ? g : lo;
+      hi = g > hi ? g : hi;
+    }
+    a.lo[k] = lo;
+    a.hi[k] = hi;
+    ng += sp->len[k];
+  }
+  for (int k = kInterpAxes - 1; k >= 0; --k) {
+    a.stride[k] = total;
+    total *= sp->len[k];
+  }
+  const int lin[kInterpLinear] = {4, 5, 6, 8, 9};
+  for (int q = 0; q < kInterpLinear; ++q) a.lstride[q] = a.stride[lin[q]];
+  a.cfg[0] = sp->cfg_ua; a.cfg[1] = sp->cfg_cm; a.cfg[2] = sp->cfg_ca; a.cfg[3] = sp->cfg_hm;
+  const size_t bytes = (size_t)(ng + total + MDR_MAX_CAP) * sizeof(double);
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  if (bytes > c->interp_bytes) {
+    HIP_TRY(hipDeviceSynchronize());  // a previous table may still be read by queued launches
+    hipFree(c->d_interp);
+    c->d_interp = nullptr;
+    c->interp_bytes = 0;
+    if (hipMalloc(&c->d_interp, bytes) != hipSuccess) return fail(MDR_ENOMEM, "mdr_interp_load: table");
+    c->interp_bytes = bytes;
+  } else {
+    HIP_TRY(hipDeviceSynchronize());
+  }
+  HIP_TRY(hipMemcpy(c->d_interp, sp->grid, ng * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->d_interp + ng, sp->values, total * sizeof(double), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->d_interp + ng + total, c->cfg.cap_table, MDR_MAX_CAP * sizeof(double),
+                    hipMemcpyHostToDevice));
+  a.grid = c->d_interp;
+  a.table = c->d_interp + ng;
+  a.cap = c->d_interp + ng + total;
+  c->interp = a;
+  c->interp_ready = true;
+  return MDR_OK;
+}
+
+int mdr_interp_values(mdr_ctx* c, const int64_t* ids, int n, double od, double hour, double date, double* vals,
+                      void* stream) {
+  if (!c || n < 0 || (n > 0 && (!ids || !vals))) return fail(MDR_EARG, "mdr_interp_values: bad argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_interp_values: context not bound");
+  if (!c->interp_ready) return fail(MDR_ESTATE, "mdr_interp_values: no table (mdr_interp_load)");
+  if (n == 0) return MDR_OK;
+  hipLaunchKernelGGL(k_interp_values, dim3(blocks(n, 64)), dim3(64), 0, S(stream), c->kp, c->interp, ids, n,
+                     od, hour, date, vals);
+  LAUNCH_CHECK("k_interp_values");
+  return MDR_OK;
+}
+
+int mdr_interp_sum(const double* vals, int n, double factor, double* out, void* stream) {
+  if (n < 0 || !out || (n > 0 && !vals)) return fail(MDR_EARG, "mdr_interp_sum: bad argument");
+  hipLaunchKernelGGL(k_interp_sum, dim3(1), dim3(64), 0, S(stream), vals, n, factor, out);
+  LAUNCH_CHECK("k_interp_sum");
   return MDR_OK;
 }
 

@@ -82,8 +82,20 @@ class mdr_actor_spec(C.Structure):
                 ("precision", C.c_int32)]
 
 
+INTERP_AXES = 10
+
+
+class mdr_interp_spec(C.Structure):
+    _fields_ = [("len", C.c_int32 * INTERP_AXES), ("grid", C.c_void_p), ("values", C.c_void_p),
+                ("cfg_ua", C.c_double), ("cfg_cm", C.c_double), ("cfg_ca", C.c_double), ("cfg_hm", C.c_double)]
+
+
 PREC_BF16, PREC_BF16X3 = 1, 3
 PRECISIONS = {"bf16": PREC_BF16, "bf16x3": PREC_BF16X3}
+
+# the structs mdr_abi_sizes reports, in its order
+ABI_STRUCTS = (mdr_config, mdr_soa, mdr_tick, mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars, mdr_actor_spec,
+               mdr_interp_spec)
 
 P, VP, I, I64, U64, D = C.POINTER, C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_double
 
@@ -113,6 +125,9 @@ SIGNATURES = {
     "mdr_actor_rollout": (I, [VP, I, P(mdr_tick), P(mdr_obs_scalars), P(mdr_obs_spec), VP, I64, VP, I64,
                               VP, I64, VP, I, VP]),
     "mdr_actor_profile": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, P(D), VP]),
+    "mdr_interp_load": (I, [VP, P(mdr_interp_spec)]),
+    "mdr_interp_values": (I, [VP, VP, I, D, D, D, VP, VP]),
+    "mdr_interp_sum": (I, [VP, I, D, VP, VP]),
     "mdr_rccl_unique_id": (I, [VP]),
     "mdr_rccl_init": (I, [VP, VP, I, I]),
     "mdr_rccl_allreduce": (I, [VP, VP, I64, I, VP]),
@@ -150,10 +165,9 @@ def load(path: str = LIB_PATH):
             fn.argtypes = args
         if lib.mdr_abi_version() != ABI_VERSION:
             raise MdrLibraryError("libmdr_hip.so ABI version mismatch; rebuild it")
-        sizes = (C.c_int64 * 7)()
-        lib.mdr_abi_sizes(sizes, 7)
-        want = [C.sizeof(t) for t in (mdr_config, mdr_soa, mdr_tick, mdr_pop_spec, mdr_obs_spec,
-                                      mdr_obs_scalars, mdr_actor_spec)]
+        sizes = (C.c_int64 * len(ABI_STRUCTS))()
+        lib.mdr_abi_sizes(sizes, len(ABI_STRUCTS))
+        want = [C.sizeof(t) for t in ABI_STRUCTS]
         if list(sizes) != want:
             raise MdrLibraryError(f"ABI struct sizes differ: library {list(sizes)} vs binding {want}")
         _lib = lib

@@ -131,13 +131,21 @@ class DeviceActor:
         ps = 0 if probs is None or probs.dim() == 1 else n
         if not env._P_dev_valid:
             sh.p_dev.fill_(float(env._P_host))
-        solar0 = float(env._solar)
-        ticks = env.driver_window(n_ticks)
-        # obs before tick t: signal / OD temperature after tick t-1 (= tick t's s_prev, t_od_prev),
-        # solar gain of tick t-1's datetime
-        osc = [L.mdr_obs_scalars(0.0, t.s_prev, solar0 if i == 0 else ticks[i - 1].solar, t.t_od_prev)
-               for i, t in enumerate(ticks)]
-        sh.actor_rollout(ticks, osc, spec, actions, as_, probs, ps, rewards, rs, use_graph)
+        done = 0
+        while done < n_ticks:  # one window unless interpolation ends it early (driver_window)
+            solar0 = float(env._solar)
+            ticks = env.driver_window(n_ticks - done)
+            k = len(ticks)
+            # obs before tick t: signal / OD temperature after tick t-1 (= tick t's s_prev,
+            # t_od_prev), solar gain of tick t-1's datetime
+            osc = [L.mdr_obs_scalars(0.0, t.s_prev, solar0 if i == 0 else ticks[i - 1].solar, t.t_od_prev)
+                   for i, t in enumerate(ticks)]
+            sl = (lambda x, st: None if x is None else (x[done:done + k] if st else x))
+            g = use_graph and (k == n_ticks or not (rs or as_ or ps))
+            sh.actor_rollout(ticks, osc, spec, sl(actions, as_), as_, sl(probs, ps), ps, sl(rewards, rs), rs, g)
+            env._P_dev_valid = True
+            env.finish_grid_step()
+            done += k
         if keep:
             torch.cuda.current_stream(sh.device).synchronize()
         env._counts_ready = 0

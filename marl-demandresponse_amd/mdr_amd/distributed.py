@@ -63,6 +63,10 @@ class RcclComm:
         L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, p.value, 1, 1, shard.stream()), "allreduce pen sum")
         L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, p.value + 8, 1, 2, shard.stream()), "allreduce pen max")
 
+    def allreduce_sum(self, shard, t) -> None:
+        """In-place double sum over ranks of a device tensor (interpolation sample values)."""
+        L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, L.ptr(t), t.numel(), 1, shard.stream()), "allreduce sum")
+
     def rollout(self, shard, ticks, actions, mode, rewards, rew_stride) -> None:
         arr = (L.mdr_tick * len(ticks))(*ticks)
         n = shard.n
@@ -149,6 +153,9 @@ class TorchComm(RcclComm):
         L.check(shard.lib.mdr_penalty_buffer(shard.ctx, C.byref(p)), "mdr_penalty_buffer")
         self.dist.all_reduce(device_view(p.value, 1, "<f8", shard.device))
         self.dist.all_reduce(device_view(p.value + 8, 1, "<f8", shard.device), op=self.dist.ReduceOp.MAX)
+
+    def allreduce_sum(self, shard, t) -> None:
+        self.dist.all_reduce(t)
 
     def pipeline(self, shard) -> dict:
         return {"mode": "torch.distributed per-step"}

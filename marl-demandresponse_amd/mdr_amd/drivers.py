@@ -2,12 +2,13 @@
 
 These are O(1) per tick (the same value for every house), so they stay on the host and reach the
 kernels as ``mdr_tick`` arguments.  Each function keeps the reference's expression order so the
-values are bit-identical (pinned by tests/test_drivers_golden.py):
+values are bit-identical (pinned by tests/test_oracle_golden.py and tests/test_host_logic.py):
 
   solar_gain      server/app/utils/utils.py:42-117
   od_temp         server/app/core/environment/environment.py:132-159
   Signal          server/app/core/environment/power_grid/signal_calculator.py:11-129
-  GridSignal      server/app/core/environment/power_grid/power_grid.py:21-161
+  GridSignal      server/app/core/environment/power_grid/power_grid.py:21-161 (interpolation
+                  base power: mdr_amd/interpolation.py, lookup on device)
   deadband_l2     server/app/utils/utils.py:4-23 (scalar, for the reward normalisers)
 """
 from __future__ import annotations
@@ -129,7 +130,8 @@ class GridSignal:
     power_grid.py:44-49) because the reference does not copy it.
     """
 
-    def __init__(self, grid_props, nb_agents: int, max_power: float, rng=_random, signal_fn=None):
+    def __init__(self, grid_props, nb_agents: int, max_power: float, rng=_random, signal_fn=None,
+                 house_prop=None):
         self.gp = grid_props
         self.nb_agents = nb_agents
         self.max_power = max_power
@@ -139,18 +141,31 @@ class GridSignal:
         self.signal = Signal(grid_props.signal_properties, nb_agents, rng)
         self.signal_fn = signal_fn
         bp = grid_props.base_power_props
+        self.interp = None
+        # evaluate(interp, ids, od, hour, date, factor) -> base power: the device lookup, set by the
+        # Environment that owns the state (interpolation mode only)
+        self.evaluate = None
         if bp.mode == "interpolation":
-            raise NotImplementedError(
-                "base_power_props.mode='interpolation' needs the Monte-Carlo table "
-                "(mergedGridSearchResultFinal.npy), which the reference does not ship (SURVEY §8(f))")
-        if bp.mode != "constant":
+            from .interpolation import Interpolator
+
+            if house_prop is None:
+                raise ValueError("interpolation base power needs the house properties (ratio denominators)")
+            self.interp = Interpolator(bp, house_prop, nb_agents, rng)  # power_grid.py:60-66
+        elif bp.mode != "constant":
             raise ValueError(f"unknown base power mode {bp.mode!r}")
 
-    def base_power(self):
+    def needs_state(self, dt_seconds: int) -> bool:
+        """True if the next step interpolates, i.e. reads the post-step house state."""
+        return self.interp is not None and self.interp.due(dt_seconds)
+
+    def base_power(self, t=None, od=None, dt_seconds: int = 0):
+        """PowerGrid.power_step (power_grid.py:130-161)."""
+        if self.interp is not None:
+            return self.interp.power_step(t, od, dt_seconds, self.evaluate)
         return self.gp.base_power_props.avg_power_per_hvac * self.nb_agents
 
-    def step(self, t: _dt.datetime):
-        base = self.base_power()
+    def step(self, t: _dt.datetime, od=None, dt_seconds: int = 0):
+        base = self.base_power(t, od, dt_seconds)
         s = self.signal_fn(base, t) if self.signal_fn is not None else self.signal(base, t)
         s = s * self.gp.artificial_ratio
         self.current_signal = np.minimum(s, self.max_power)

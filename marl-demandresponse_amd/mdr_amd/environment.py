@@ -138,12 +138,13 @@ class Environment:
             table, idx = popmod.cap_table(hv, ())
             local = None
         self._cap_values = table
-        # outdoor temperature, grid, rewards calculator, first signal (environment.py:59-69)
+        # outdoor temperature, grid, rewards calculator (environment.py:59-66)
         self.current_od_temp = od_temp(self.date_time, p.temp_prop, rng)
-        self.power_grid = GridSignal(p.power_grid_prop, n, self._max_power, rng, self._signal_fn)
+        self.power_grid = GridSignal(p.power_grid_prop, n, self._max_power, rng, self._signal_fn, hp)
+        self.power_grid.evaluate = self._interp_evaluate
         self._norm_temp, self._norm_sig = reward_normalisers(p.reward_prop, hp)
-        self.power_grid.step(self.date_time)
-        # device state (Building.reset / HVAC.reset: init temps, on, no lockout, sso = 0)
+        # device state (Building.reset / HVAC.reset: init temps, on, no lockout, sso = 0); before the
+        # first grid step, which reads it in interpolation mode
         self._ensure_shard(table)
         sh = self._shard
         if local is not None:
@@ -155,6 +156,8 @@ class Environment:
         self._solar = 0.0
         self._tick = 0
         self._counts_ready = 0
+        self._grid_pending = False
+        self.power_grid.step(self.date_time, self.current_od_temp, p.time_step.seconds)  # first signal (:67-69)
         self._obs_links = self._links if self._links is not None else popmod.random_links(cp, rng)
         return self.get_obs() if return_obs else None
 
@@ -231,7 +234,7 @@ class Environment:
         if self._links is None:
             popmod.random_links(cp, self.rng)  # the discarded Cluster.get_obs() (cluster.py:89)
         self.current_od_temp = od_temp(self.date_time, p.temp_prop, self.rng)
-        self.power_grid.step(self.date_time)
+        self.power_grid.step(self.date_time, self.current_od_temp, p.time_step.seconds)
         self._obs_links = self._links if self._links is not None else popmod.random_links(cp, self.rng)
         self._tick += 1
         return reward
@@ -276,13 +279,19 @@ class Environment:
 
     # ------------------------------------------------------------------ many ticks per call
     def driver_window(self, n_ticks: int):
-        """Advance the host drivers n_ticks ahead (same RNG order as n calls of step) and return
-        the per-tick ``mdr_tick`` list for a rollout.  Valid when nothing else draws from the RNG
-        between ticks (random_sample comm mode draws, so it is excluded)."""
+        """Advance the host drivers up to n_ticks ahead (same RNG order as n calls of step) and
+        return the per-tick ``mdr_tick`` list for a rollout.  Valid when nothing else draws from
+        the RNG between ticks (random_sample comm mode draws, so it is excluded).
+
+        In interpolation base-power mode the window stops after a tick whose grid step reads the
+        post-step house state: run the returned ticks on the device, then ``finish_grid_step()``."""
         if self._links is None:
             raise NotImplementedError("random_sample comm mode draws per tick; use step()")
+        if self._grid_pending:
+            raise RuntimeError("a deferred grid step is pending: run the previous window, then finish_grid_step()")
         p = self.init_props
         hp = p.cluster_prop.house_prop
+        dts = p.time_step.seconds
         ticks = []
         for _ in range(n_ticks):
             self.date_time = self.date_time + p.time_step
@@ -291,9 +300,36 @@ class Environment:
             self._s_prev = self.power_grid.current_signal
             ticks.append(self._tick_args())
             self.current_od_temp = od_temp(self.date_time, p.temp_prop, self.rng)
-            self.power_grid.step(self.date_time)
             self._tick += 1
+            if self.power_grid.needs_state(dts):
+                self._grid_pending = True
+                break
+            self.power_grid.step(self.date_time, self.current_od_temp, dts)
         return ticks
+
+    def finish_grid_step(self):
+        """The grid step driver_window deferred (interpolation mode), once its ticks have run."""
+        if self._grid_pending:
+            self._grid_pending = False
+            self.power_grid.step(self.date_time, self.current_od_temp, self.init_props.time_step.seconds)
+
+    def _interp_evaluate(self, interp, ids, od, hour, date, factor) -> float:
+        """Interpolated power of the sampled houses on device (k_interp_values; sharded: summed
+        over ranks, one non-zero per slot, so exact), ordered sum x N/k (k_interp_sum)."""
+        import torch
+
+        sh = self._shard
+        if getattr(sh, "_interp_src", None) is not interp.values:
+            sh.interp_load(interp.grids, interp.values, interp.cfg)
+            sh._interp_src = interp.values
+        ids_t = torch.as_tensor(np.asarray(ids, np.int64)).to(sh.device)
+        vals = torch.empty(len(ids), dtype=torch.float64, device=sh.device)
+        sh.interp_values(ids_t, od, hour, date, vals)
+        if self._comm is not None:
+            self._comm.allreduce_sum(sh, vals)
+        out = torch.empty(1, dtype=torch.float64, device=sh.device)
+        sh.interp_sum(vals, factor, out)
+        return float(out.item())
 
     def rollout(self, n_ticks: int, actions=None, action_mode: str = "random", rewards=None,
                 use_graph: bool = True):
@@ -311,14 +347,22 @@ class Environment:
         if rewards is None:
             rewards = torch.empty((n_ticks, self._n_local), dtype=torch.float64, device=sh.device)
         rew_stride = 0 if rewards.dim() == 1 else self._n_local  # 1-D: every tick overwrites it
-        ticks = self.driver_window(n_ticks)
-        if self._comm is not None:
-            self._comm.rollout(sh, ticks, actions, mode, rewards, rew_stride)
-        else:
-            sh.rollout(ticks, actions, self._n_local if actions is not None else 0, mode, rewards,
-                       rew_stride, use_graph)
+        done = 0
+        while done < n_ticks:  # one window unless interpolation ends it early (driver_window)
+            ticks = self.driver_window(n_ticks - done)
+            k = len(ticks)
+            a = None if actions is None else actions[done:done + k]
+            r = rewards[done:done + k] if rew_stride else rewards
+            if self._comm is not None:
+                self._comm.rollout(sh, ticks, a, mode, r, rew_stride)
+            else:
+                # graphs are cached per (length, buffers): shorter windows only reuse them on 1-D rewards
+                g = use_graph and (k == n_ticks or (a is None and not rew_stride))
+                sh.rollout(ticks, a, self._n_local if a is not None else 0, mode, r, rew_stride, g)
+            self._P_dev_valid = True
+            self.finish_grid_step()
+            done += k
         self._counts_ready = 0
-        self._P_dev_valid = True
         return rewards
 
     def greedy_actions(self, out=None):
@@ -489,6 +533,8 @@ class Environment:
                 ("t_air", "t_mass", "hvac", "ua", "ca", "cm", "hm", "target", "cap_idx")}
         host.update(date_time=self.date_time, current_od_temp=self.current_od_temp,
                     current_signal=self.power_grid.current_signal, solar=self._solar, tick=self._tick,
+                    interp=None if self.power_grid.interp is None else
+                    (self.power_grid.interp.since, self.power_grid.interp.base),
                     P=self._cluster_power(), cap_values=list(self._cap_values),
                     links=copy.deepcopy(self._links), obs_links=copy.deepcopy(self._obs_links))
         return host
@@ -505,6 +551,8 @@ class Environment:
         self.date_time = sd["date_time"]
         self.current_od_temp = sd["current_od_temp"]
         self.power_grid.current_signal = sd["current_signal"]
+        if sd.get("interp") is not None and self.power_grid.interp is not None:
+            self.power_grid.interp.since, self.power_grid.interp.base = sd["interp"]
         self._solar, self._tick = sd["solar"], sd["tick"]
         self._P_host, self._P_dev_valid = sd["P"], False
         self._links = sd["links"]

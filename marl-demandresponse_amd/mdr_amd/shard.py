@@ -223,6 +223,24 @@ class HipShard:
         if use_graph:
             cur.wait_stream(self._side)
 
+    def interp_load(self, grids, values, cfg):
+        """Monte-Carlo table + axes to the device (mdr_interp_load, synchronous)."""
+        grid = np.ascontiguousarray(np.concatenate([np.asarray(g, np.float64) for g in grids]))
+        vals = np.ascontiguousarray(values, np.float64).reshape(-1)
+        spec = L.mdr_interp_spec()
+        spec.len[:] = [len(g) for g in grids]
+        spec.grid, spec.values = grid.ctypes.data, vals.ctypes.data
+        spec.cfg_ua, spec.cfg_cm, spec.cfg_ca, spec.cfg_hm = (float(x) for x in cfg)
+        L.check(self.lib.mdr_interp_load(self.ctx, C.byref(spec)), "mdr_interp_load")
+
+    def interp_values(self, ids, od, hour, date, vals):
+        L.check(self.lib.mdr_interp_values(self.ctx, L.ptr(ids), int(ids.numel()), float(od), float(hour),
+                                           float(date), L.ptr(vals), self.stream()), "mdr_interp_values")
+
+    def interp_sum(self, vals, factor, out):
+        L.check(self.lib.mdr_interp_sum(L.ptr(vals), int(vals.numel()), float(factor), L.ptr(out),
+                                        self.stream()), "mdr_interp_sum")
+
     def halo_pack(self, spec, out):
         L.check(self.lib.mdr_halo_pack(self.ctx, C.byref(spec), L.ptr(out), self.stream()), "mdr_halo_pack")
 

@@ -327,6 +327,7 @@ class OracleEnv:
         if gp.signal_properties.mode == "perlin":
             raise NotImplementedError("perlin signal parity is unpinned")
         self.S = 0.0
+        self._interp_since = gp.base_power_props.interp_update_period + 1  # power_grid.py:64-66
         self._grid_step()
         self.cur_links = self._links_for_obs()
         return self.obs()
@@ -339,10 +340,27 @@ class OracleEnv:
         return self.links if self.links is not None else self._random_links()
 
     def _grid_step(self):
+        """PowerGrid.step (power_grid.py:80-161); interpolation mode via oracle/interp_np.py."""
         gp = self.p.power_grid_prop
-        if gp.base_power_props.mode != "constant":
-            raise NotImplementedError("interpolation base power is out of the oracle's scope")
-        base = gp.base_power_props.avg_power_per_hvac * self.n
+        bp = gp.base_power_props
+        if bp.mode == "interpolation":
+            from . import interp_np as IN
+
+            if getattr(self, "_interp", None) is None:
+                keys, grids, values = IN.load_files(bp)
+                hp = self.p.cluster_prop.house_prop
+                self._interp = IN.OracleInterp(grids, values, hp.Ua, hp.Cm, hp.Ca, hp.Hm)
+            self._interp_since += self.p.time_step.seconds
+            if self._interp_since >= bp.interp_update_period:
+                self._base = IN.interpolate_power(self._interp, self.pop, self.T, self.Tm, self.Tod, self.date,
+                                                  self.p.cluster_prop.house_prop.solar_gain,
+                                                  bp.interp_nb_agents, self.rng)
+                self._interp_since = 0
+            base = self._base
+        elif bp.mode != "constant":
+            raise ValueError(f"unknown base power mode {bp.mode!r}")
+        else:
+            base = bp.avg_power_per_hvac * self.n
         s = signal(gp.signal_properties.mode, gp.signal_properties, base, self.date, self.n)
         s = s * gp.artificial_ratio
         self.S = np.minimum(s, self.max_power)

@@ -24,6 +24,9 @@ Fixtures (names follow SURVEY §8(c) F1..F9):
   F9 rng_order.npz     population after 1 and 3 resets for seeds {0, 4, 123}
   P  policy.npz        MAPPO actor (seed 1, the reference init) on reference norm_state_dict
                        vectors: weights, obs, Actor.forward probabilities (row P)
+  a10 interp.npz       PowerInterpolator.interpolate_grid_fast on 400 swept points over a synthetic
+                       table of the reference grid (interp_parameters_dict.json / interp_dict_keys.csv,
+                       copied next to it), + traj_interp_*.npz trajectories in interpolation mode
 
 Usage:  python tests/golden/make_golden.py   (writes next to this file)
 """
@@ -448,7 +451,83 @@ def gen_policy() -> None:
     np.savez_compressed(os.path.join(OUT, "policy.npz"), **out)
 
 
+# ---------------------------------------------------------------------------------------- a10
+INTERP_SRC = os.path.join(REF, "v0/monteCarlo")
+INTERP_SEED = 2024
+BPP = "power_grid_prop.base_power_props."
+
+
+def interp_table_path() -> str:
+    """The synthetic Monte-Carlo table (oracle/interp_np.synthetic_table, seed 2024) as a .npy
+    (the reference does not ship mergedGridSearchResultFinal.npy); tests rebuild the same file."""
+    sys.path.insert(0, os.path.dirname(os.path.dirname(OUT)))
+    from oracle.interp_np import synthetic_table
+
+    with open(os.path.join(OUT, "interp_parameters_dict.json")) as f:
+        params = json.load(f)
+    path = os.path.join(tempfile.gettempdir(), f"mdr_interp_table_{INTERP_SEED}.npy")
+    np.save(path, synthetic_table([len(v) for v in params.values()], INTERP_SEED))
+    return path
+
+
+def interp_overrides(extra: dict) -> dict:
+    d = {BPP + "mode": "interpolation", BPP + "path_datafile": interp_table_path(),
+         BPP + "path_parameter_dict": os.path.join(OUT, "interp_parameters_dict.json"),
+         BPP + "path_dict_keys": os.path.join(OUT, "interp_dict_keys.csv")}
+    d.update(extra)
+    return d
+
+
+def gen_interp() -> None:
+    """a10: PowerInterpolator.interpolate_grid_fast on swept points (inside, outside and exactly
+    on the grid) of the reference grid over the synthetic table."""
+    import shutil
+
+    from app.core.environment.power_grid.interpolation import PowerInterpolator
+    from app.core.environment.power_grid.power_grid_properties import BasePowerProperties
+
+    for name in ("interp_parameters_dict.json", "interp_dict_keys.csv"):
+        shutil.copy(os.path.join(INTERP_SRC, name), os.path.join(OUT, name))
+    bpp = BasePowerProperties(mode="interpolation", path_datafile=interp_table_path(),
+                              path_parameter_dict=os.path.join(OUT, "interp_parameters_dict.json"),
+                              path_dict_keys=os.path.join(OUT, "interp_dict_keys.csv"))
+    pi = PowerInterpolator(bpp, BuildingProperties())
+    keys = list(pi.dict_keys)
+    rs = np.random.RandomState(21)
+    M = 400
+    raw, clipped, val = np.zeros((M, len(keys))), np.zeros((M, len(keys))), np.zeros(M)
+    for m in range(M):
+        pt = {}
+        for k in keys:
+            g = np.array(pi.parameters_dict[k], np.float64)
+            lo, hi = g.min(), g.max()
+            if m % 4 == 0 or rs.random_sample() < 0.15:
+                pt[k] = float(rs.choice(g))  # exactly on a grid point (the ends included)
+            else:
+                pt[k] = float(rs.uniform(lo - 0.15 * (hi - lo), hi + 0.15 * (hi - lo)))
+        raw[m] = [pt[k] for k in keys]
+        pt = pi.clip_interpolation_point(pt)
+        clipped[m] = [pt[k] for k in keys]
+        val[m] = float(pi.interpolate_grid_fast(pt))
+    np.savez_compressed(os.path.join(OUT, "interp.npz"), keys=np.array(keys), raw=raw, clipped=clipped,
+                        value=val, table_seed=np.int64(INTERP_SEED))
+
+
+def gen_interp_traj() -> None:
+    sig = "power_grid_prop.signal_properties.mode"
+    gen_traj("interp_sin_random", interp_overrides({sig: "sinusoidals", BPP + "interp_update_period": 40,
+                                                    BPP + "interp_nb_agents": 20}),
+             N=50, T=80, seed=8, controller="random", norm_ticks=(0, 80))
+    gen_traj("interp_flat_dbbc_nosolar", interp_overrides({sig: "flat",
+                                                           "cluster_prop.house_prop.solar_gain": False}),
+             N=12, T=160, seed=3, controller="deadband_bbc", norm_ticks=(0,))
+
+
 def main() -> None:
+    if len(sys.argv) > 1:  # only the named generators, e.g. `make_golden.py gen_interp gen_interp_traj`
+        for name in sys.argv[1:]:
+            globals()[name]()
+        return
     with open(os.path.join(OUT, "marl_env_prop.json"), "w") as f:
         json.dump(env_prop_json(), f, indent=1, sort_keys=True)
     gen_lockout()
@@ -485,6 +564,8 @@ def main() -> None:
     gen_comm()
     gen_rng_order()
     gen_policy()
+    gen_interp()
+    gen_interp_traj()
     print("golden fixtures written to", OUT)
 
 

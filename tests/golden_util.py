@@ -4,6 +4,7 @@ from __future__ import annotations
 import datetime as dt
 import json
 import os
+import tempfile
 
 import numpy as np
 
@@ -24,10 +25,43 @@ def base_env_prop() -> dict:
         return json.load(f)
 
 
+BPP = "power_grid_prop.base_power_props."
+
+
+def interp_table_path() -> str:
+    """The synthetic Monte-Carlo table the interpolation goldens were made with (the reference does
+    not ship mergedGridSearchResultFinal.npy): oracle/interp_np.synthetic_table(seed in interp.npz)
+    over the reference grid, written once per machine."""
+    import numpy as _np
+
+    from oracle.interp_np import synthetic_table
+
+    seed = int(load("interp.npz")["table_seed"])
+    out = os.path.join(tempfile.gettempdir(), f"mdr_interp_table_{seed}_{os.getuid()}.npy")
+    if not os.path.exists(out):
+        with open(path("interp_parameters_dict.json")) as f:
+            lens = [len(v) for v in json.load(f).values()]
+        tmp = f"{out}.{os.getpid()}.tmp.npy"
+        _np.save(tmp, synthetic_table(lens, seed))
+        os.replace(tmp, out)
+    return out
+
+
+def localize(overrides: dict) -> dict:
+    """Point an interpolation-mode config at this checkout's fixture files."""
+    if overrides.get(BPP + "mode") != "interpolation":
+        return overrides
+    o = dict(overrides)
+    o[BPP + "path_datafile"] = interp_table_path()
+    o[BPP + "path_parameter_dict"] = path("interp_parameters_dict.json")
+    o[BPP + "path_dict_keys"] = path("interp_dict_keys.csv")
+    return o
+
+
 def props_from_overrides(overrides: dict):
     from mdr_amd.config import EnvironmentProperties, override
 
-    return EnvironmentProperties.from_dict(override(base_env_prop(), overrides))
+    return EnvironmentProperties.from_dict(override(base_env_prop(), localize(overrides)))
 
 
 def traj(name: str):
@@ -41,4 +75,4 @@ def from_epoch(x: float) -> dt.datetime:
 
 
 TRAJ_NAMES = ("c1_sin_dbbc", "c1_flat_random", "fixed_steps_bbc", "n400_random_common",
-              "n64_mixture_2d", "n30_maxerr_groups_hvacmsg")
+              "n64_mixture_2d", "n30_maxerr_groups_hvacmsg", "interp_sin_random", "interp_flat_dbbc_nosolar")

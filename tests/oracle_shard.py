@@ -117,6 +117,29 @@ class OracleShard:
         r = -(self.props.reward_prop.alpha_temp * tp / self._norm_t + self._sig)
         (self.reward if reward is None else reward).copy_(torch.from_numpy(r))
 
+    def interp_load(self, grids, values, cfg):
+        from oracle import interp_np as IN
+
+        self._interp = IN.OracleInterp(grids, values, *cfg)
+
+    def interp_values(self, ids, od, hour, date, vals):
+        o, caps = self._interp, self._caps()
+        out = np.zeros(ids.numel())
+        for s, g in enumerate(ids.tolist()):
+            j = g - self.offset
+            if 0 <= j < self.n:
+                x = o.house_point(float(self.ua[j]), float(self.cm[j]), float(self.ca[j]), float(self.hm[j]),
+                                  float(self.t_air[j]), float(self.t_mass[j]), float(self.target[j]), od,
+                                  float(caps[j]), hour, date)
+                out[s] = o.point(x)
+        vals.copy_(torch.from_numpy(out))
+
+    def interp_sum(self, vals, factor, out):
+        b = 0.0
+        for v in vals.tolist():
+            b += v
+        out[0] = b * factor
+
     def host_state(self):
         on, lock, sso = decode_hvac(self.hvac.numpy().copy())
         return {"T": self.t_air.numpy().copy(), "Tm": self.t_mass.numpy().copy(), "on": on,
@@ -145,6 +168,9 @@ class GlooComm:
         self.dist.all_reduce(s)
         self.dist.all_reduce(m, op=self.dist.ReduceOp.MAX)
         shard.partial2[0], shard.partial2[1] = s[0], m[0]
+
+    def allreduce_sum(self, shard, t):
+        self.dist.all_reduce(t)
 
     def allgather_state(self, shard, st, prm, n):
         out_st, out_prm = {}, {}

@@ -34,11 +34,12 @@ def test_abi_struct_sizes_and_version():
 
     lib = _lib.load()
     assert lib.mdr_abi_version() == _lib.ABI_VERSION
-    sizes = (C.c_int64 * 7)()
-    assert lib.mdr_abi_sizes(sizes, 7) == 7
+    sizes = (C.c_int64 * 8)()
+    assert lib.mdr_abi_sizes(sizes, 8) == 8
     assert list(sizes) == [C.sizeof(t) for t in (_lib.mdr_config, _lib.mdr_soa, _lib.mdr_tick,
                                                  _lib.mdr_pop_spec, _lib.mdr_obs_spec, _lib.mdr_obs_scalars,
-                                                 _lib.mdr_actor_spec)]
+                                                 _lib.mdr_actor_spec, _lib.mdr_interp_spec)]
+    assert _lib.ABI_STRUCTS[-1] is _lib.mdr_interp_spec
 
 
 def test_argument_errors_without_gpu():
@@ -62,6 +63,9 @@ def test_argument_errors_without_gpu():
     spec = _lib.mdr_obs_spec()
     spec.msg_thermal, spec.msg_hvac = 1, 1
     assert lib.mdr_msg_width(C.byref(spec)) == 11
+    assert lib.mdr_interp_load(None, None) == -1
+    assert lib.mdr_interp_values(None, None, 1, 0.0, 0.0, 0.0, None, None) == -1
+    assert lib.mdr_interp_sum(None, -1, 1.0, None, None) == -1
 
 
 def test_environment_fails_loudly_without_gpu():

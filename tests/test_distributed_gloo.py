@@ -62,12 +62,18 @@ def _free_port():
     return p
 
 
-@pytest.mark.parametrize("mode,n", [("individual_L2", 101), ("common_L2", 64), ("mixture", 37)])
-def test_sharded_env_equals_oracle(tmp_path, mode, n):
+INTERP = {gu.BPP + "mode": "interpolation", gu.BPP + "interp_update_period": 8, gu.BPP + "interp_nb_agents": 30}
+
+
+@pytest.mark.parametrize("mode,n,extra", [("individual_L2", 101, {}), ("common_L2", 64, {}), ("mixture", 37, {}),
+                                          ("individual_L2", 101, INTERP)])
+def test_sharded_env_equals_oracle(tmp_path, mode, n, extra):
+    """Sharded orchestration (2 ranks, gloo) == the oracle; the interpolation case draws its
+    sampled houses on every rank and sums the per-rank sample values (base power every 2 ticks)."""
     world, T, seed = 2, 12, 21
     overrides = {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals",
                  "reward_prop.penalty_props.mode": mode, "reward_prop.penalty_props.alpha_common_max": 0.5,
-                 "cluster_prop.house_prop.deadband": 0.3}
+                 "cluster_prop.house_prop.deadband": 0.3, **extra}
     actions = np.random.RandomState(n).randint(0, 2, (T, n)).astype(np.uint8)
     mp.start_processes(_worker, args=(world, _free_port(), overrides, seed, actions, str(tmp_path)),
                        nprocs=world, join=True, start_method="spawn")

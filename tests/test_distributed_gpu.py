@@ -29,9 +29,17 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 T_STEP, T_BUF, T_ROLL = 5, 3, 20  # a 20-tick rollout triggers the pipeline calibration
 
 
+INTERP = "interp"  # mode suffix: interpolation base power (row a10), re-estimated every 3 ticks
+
+
 def _overrides(n, mode):
-    return {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals",
-            "reward_prop.penalty_props.mode": mode, "reward_prop.penalty_props.alpha_common_max": 0.5}
+    pen, _, extra = mode.partition("+")
+    o = {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals",
+         "reward_prop.penalty_props.mode": pen, "reward_prop.penalty_props.alpha_common_max": 0.5}
+    if extra == INTERP:
+        o.update({gu.BPP + "mode": "interpolation", gu.BPP + "interp_update_period": 12,
+                  gu.BPP + "interp_nb_agents": 200})
+    return o
 
 
 def _run(env, n_total, torch, dev):
@@ -96,6 +104,8 @@ def _free_port():
     ("nccl", "rccl-overlap", 1, 3001, "individual_L2"),
     ("gloo", "torch", 2, 3001, "individual_L2"),
     ("gloo", "torch", 2, 2048, "common_L2"),
+    ("nccl", "rccl", 1, 3001, "individual_L2+interp"),
+    ("gloo", "torch", 2, 3001, "individual_L2+interp"),
 ])
 def test_sharded_equals_single(tmp_path, backend, kind, world, n, mode):
     import torch
@@ -112,7 +122,7 @@ def test_sharded_equals_single(tmp_path, backend, kind, world, n, mode):
     for key in ("on", "lock", "sso", "T", "Tm"):
         np.testing.assert_array_equal(np.concatenate([p[key] for p in parts]), ref[key], err_msg=key)
     got_r = np.concatenate([p["rewards"] for p in parts], axis=1)
-    if mode == "individual_L2":
+    if mode.startswith("individual_L2"):
         np.testing.assert_array_equal(got_r, ref["rewards"])
     else:
         np.testing.assert_allclose(got_r, ref["rewards"], rtol=1e-12, atol=1e-15)

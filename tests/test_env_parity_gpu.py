@@ -46,6 +46,7 @@ def test_golden_trajectory_dict_api(torch_gpu, name):
     if obs is None:
         obs = env.get_obs()
     N, T = meta["N"], meta["T"]
+    interp = meta["overrides"].get(gu.BPP + "mode") == "interpolation"
     assert obs[0]["cluster_hvac_power"] == float(d["init_P"])
     assert obs[0]["reg_signal"] == float(d["init_S"])
     np.testing.assert_array_equal([obs[i]["Ua"] for i in range(N)], d["pop_Ua"])
@@ -75,7 +76,10 @@ def test_golden_trajectory_dict_api(torch_gpu, name):
         np.testing.assert_allclose(Tmn, d["traj_Tm"][t], rtol=TEMP_RTOL, atol=0, err_msg=f"Tm t={t}")
         np.testing.assert_allclose([rew[i] for i in range(N)], d["traj_reward"][t], rtol=1e-9, atol=1e-12)
         assert obs[0]["cluster_hvac_power"] == float(d["traj_P"][t])
-        assert obs[0]["reg_signal"] == float(d["traj_S"][t])
+        if interp:  # base power from interpolated post-step temperatures (exp: ulp-level vs numpy)
+            np.testing.assert_allclose(obs[0]["reg_signal"], float(d["traj_S"][t]), rtol=TEMP_RTOL, atol=0)
+        else:
+            assert obs[0]["reg_signal"] == float(d["traj_S"][t])
         assert obs[0]["OD_temp"] == float(d["traj_Tod"][t])
         assert obs[0]["solar_gain"] == float(d["traj_G"][t])
         m0 = np.array([obs[i]["message"][0]["current_temp_diff_to_target"] for i in range(N)])

@@ -186,3 +186,24 @@ def test_greedy_golden():
         a = O.greedy(d["T"][t], d["target"][t], d["cap"][t], float(d["cop"]), d["lock"][t].astype(bool),
                      float(d["S"][t]))
         np.testing.assert_array_equal(a, d["action"][t].astype(bool), err_msg=f"t={t}")
+
+
+def test_interp_points_golden():
+    """a10: the oracle's clip + nearest + multilinear lookup equals the reference PowerInterpolator
+    (interpolate_grid_fast over scipy interpn) bit for bit on 400 swept points of the reference grid
+    over the synthetic table."""
+    import json
+
+    from oracle import interp_np as IN
+
+    d = gu.load("interp.npz")
+    with open(gu.path("interp_parameters_dict.json")) as f:
+        params = json.load(f)
+    keys = [str(k) for k in d["keys"]]
+    assert tuple(keys) == IN.KEYS
+    grids = [params[k] for k in keys]
+    o = IN.OracleInterp(grids, np.load(gu.interp_table_path()), 1.0, 1.0, 1.0, 1.0)
+    for m in range(len(d["value"])):
+        c = o.clip(list(d["raw"][m]))
+        np.testing.assert_array_equal(c, d["clipped"][m])
+        assert o.point(c) == float(d["value"][m]), m
