@@ -109,8 +109,15 @@ __device__ __forceinline__ void sto(void* base, uint32_t off, V v) {
   *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + off) = v;
 }
 
+// MDR_STEP_WAVES (build-time A/B knob): cap k_step_t at that many waves/SIMD (VGPR budget 512/W).
+#ifdef MDR_STEP_WAVES
+#define MDR_STEP_OCC __attribute__((amdgpu_waves_per_eu(MDR_STEP_WAVES)))
+#else
+#define MDR_STEP_OCC
+#endif
+
 template <int HPT, bool CACHED, bool FAST, int ACT, int LA>
-__global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __restrict__ action,
+__global__ void __launch_bounds__(256) MDR_STEP_OCC k_step_t(KParams p, const uint8_t* __restrict__ action,
                                                 int action_mode_rt, TickArgs tk0, const TickArgs* tkp,
                                                 const unsigned long long* __restrict__ counts,
                                                 double* __restrict__ reward, int ctrl,
