@@ -216,6 +216,10 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
       else if (hot_buffer) MDR_LAUNCH_STEP(2, false, true, MDR_ACT_BUFFER, 0);
       else MDR_LAUNCH_STEP(2, false, true, -1, -1);
     }
+  } else if (c->hpt == 1 && c->fastdiv && !c->cached) {
+    // one house per lane: 16384 waves at 1M (A/B against HPT = 2, MDR_HPT=1)
+    if (hot_random) MDR_LAUNCH_STEP(1, false, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
+    else MDR_LAUNCH_STEP(1, false, true, -1, -1);
   } else if (c->hpt == 2) {
     if (c->cached) MDR_LAUNCH_STEP(2, true, false, -1, -1); else MDR_LAUNCH_STEP(2, false, false, -1, -1);
   } else {

@@ -515,6 +515,8 @@ MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0)
       KParams, const uint8_t*, int, TickArgs, const TickArgs*, const unsigned long long*,        \
       double*, int, uint8_t*, double*, int, unsigned long long*, unsigned long long*, double*, int);
 MDR_INST_STEP(1, false, false, -1, -1)
+MDR_INST_STEP(1, false, true, -1, -1)
+MDR_INST_STEP(1, false, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
 MDR_INST_STEP(2, false, false, -1, -1)
 MDR_INST_STEP(2, true, false, -1, -1)
 MDR_INST_STEP(2, false, true, -1, -1)
