@@ -34,6 +34,20 @@ HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s
 BF16_PEAK_TFS = 2516.6     # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (no sparsity)
 
 
+
+def step_kernel_name(n_loc: int, mode: str) -> str:
+    """The k_step instantiation the library launches for this bench (launch_step_on in mdr_capi.hip)."""
+    if any(k in os.environ for k in ("MDR_HPT", "MDR_VARIANT", "MDR_FASTDIV")):
+        return "mdr::k_step (variant chosen by MDR_* env)"
+    tpw = int(os.environ.get("MDR_TPW", 2 if n_loc <= 1572864 else 4))
+    act = "RANDOM,RANDOM" if mode == "random" else "BUFFER,0"
+    if tpw <= 0:
+        return f"mdr::k_step_t<2,false,true,{act}>"
+    tpw = 8 if tpw >= 8 else 4 if tpw >= 4 else 2 if tpw >= 2 else 1
+    if mode != "random":
+        tpw = 4 if tpw >= 4 else 2
+    return f"mdr::k_step_pipe<{tpw},{act}>"
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -261,7 +275,7 @@ def main():
                                                         "per-tick power counts)" if comm is not None else "1 GPU"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "kernel": "mdr::k_step",
+                     "traffic": traffic, "kernel": step_kernel_name(n_loc, args.mode),
                      "kernel_avg_us": kern_ms * 1e3, "launches_timed": kern_launches,
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "bytes_per_house_step": BYTES_PER_HOUSE_STEP},
