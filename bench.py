@@ -5,13 +5,18 @@ Workload (BASELINE.json metric "house-steps/s (env.step throughput) at 1M houses
 houses per GPU (weak scaling: N_total = 1,048,576 x n_gpus), MARLconfig env_prop (dt = 4 s,
 L = 40 s, individual_L2 rewards), sinusoidal regulation signal (perlin is parity-unpinned),
 synthetic population drawn on device (Philox, the reference noise model), random actions from
-the fused Philox controller (configs[1]'s controller; a tick is ONE fused HIP launch).  A step =
-one env.step of every house: lockout FSM + RC thermal + cluster power + rewards, with the host
-scalar drivers (outdoor temperature RNG, solar, signal) computed per tick inside the timed
-region.  Ticks are issued as hipGraph-captured chunks (mdr_rollout); multi-GPU runs allreduce
-the per-tick cluster-power counts with RCCL inside the loop (mdr_rollout_sharded).
+the fused Philox controller (configs[1]'s controller).  A step = one env.step of every house:
+lockout FSM + RC thermal + cluster power + rewards (every tick's reward row is written), with the
+host scalar drivers (outdoor temperature RNG, solar, signal) computed per tick inside the timed
+region.  Ticks are issued as hipGraph-captured chunks (mdr_rollout), each chunk temporally
+blocked into windows of up to 32 ticks per launch (k_step_window; --window 0 = one launch per
+tick); multi-GPU runs allreduce each window's cluster-power counts with RCCL inside the loop
+(mdr_rollout_sharded).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--houses H] [--chunk C]
+Other workloads: --workload actor (config C5: MA-PPO actor fused with the obs, then env.step),
+--workload greedy (config C3: device greedy-myopic controller, then env.step).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--houses H] [--chunk C] [--window W]
     torchrun --nproc-per-node N bench.py --gpus N ...
 """
 from __future__ import annotations
@@ -30,13 +35,19 @@ for _p in (ROOT, os.path.join(ROOT, "marl-demandresponse_amd")):
 
 METRIC = "house-steps/s (env.step throughput) at 1M houses; % HBM roofline"
 BYTES_PER_HOUSE_STEP = 99  # SURVEY §8(d) B_core: state r/w 42 + action 1 + params 48 + reward 8
+STATE_RW, PARAMS, REWARD, ACTION = 42, 48, 8, 1  # the §8(d) field sizes (bytes per house)
+GREEDY_EXTRA = 26          # §8(d): + greedy key r/w 16, perm r/w 8, (P, lockout) gather 2
 HBM_PEAK_GBS = 8000.0      # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s
 BF16_PEAK_TFS = 2516.6     # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 2.4 GHz (no sparsity)
 
 
 
-def step_kernel_name(n_loc: int, mode: str) -> str:
-    """The k_step instantiation the library launches for this bench (launch_step_on in mdr_capi.hip)."""
+def step_kernel_name(n_loc: int, mode: str, window: int) -> str:
+    """The step kernel the library launches for this bench (mdr_capi.hip: window_launches /
+    launch_step_on)."""
+    act = {"random": "MDR_ACT_RANDOM", "buffer": "MDR_ACT_BUFFER"}[mode]
+    if window > 0:
+        return f"mdr::k_step_window<{act}>"
     if any(k in os.environ for k in ("MDR_HPT", "MDR_VARIANT", "MDR_FASTDIV")):
         return "mdr::k_step (variant chosen by MDR_* env)"
     tpw = int(os.environ.get("MDR_TPW", 2 if n_loc <= 1572864 else 4))
@@ -48,19 +59,32 @@ def step_kernel_name(n_loc: int, mode: str) -> str:
         tpw = 4 if tpw >= 4 else 2
     return f"mdr::k_step_pipe<{tpw},{act}>"
 
+
+def window_bytes(n: int, k: int, mode: str) -> int:
+    """Algorithmic HBM bytes of one k_step_window launch of k ticks over n houses, in SURVEY
+    §8(d)'s field sizes: state read+written once (42), parameters read once (48), one reward row
+    per tick (8 k), plus the action rows for buffer mode (k)."""
+    return n * (STATE_RW + PARAMS + REWARD * k + (ACTION * k if mode == "buffer" else 0))
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
     ap.add_argument("--houses", type=int, default=1 << 20, help="houses per GPU")
-    ap.add_argument("--chunk", type=int, default=100, help="ticks per graph-captured rollout call")
+    ap.add_argument("--chunk", type=int, default=128, help="ticks per graph-captured rollout call")
+    ap.add_argument("--window", type=int, default=32,
+                    help="ticks per temporally blocked launch (k_step_window, <= 32); 0 = one launch per tick")
+    ap.add_argument("--kernel-ticks", type=int, default=512,
+                    help="ticks of the kernel-only timing after the timed region (roofline.kernel_avg_us)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline time budget")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="random", choices=["random", "buffer"])
-    ap.add_argument("--workload", default="step", choices=["step", "actor"],
+    ap.add_argument("--workload", default="step", choices=["step", "actor", "greedy"],
                     help="step: env.step with fused random actions (the BASELINE metric); actor: "
-                         "config C5, MA-PPO actor select_actions fused with the obs, then env.step")
+                         "config C5, MA-PPO actor select_actions fused with the obs, then env.step; "
+                         "greedy: config C3, device greedy-myopic controller then env.step")
     ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16"],
                     help="actor MFMA precision (--workload actor)")
     ap.add_argument("--comm", default="default", choices=["default", "none", "rccl", "torch"],
@@ -78,44 +102,107 @@ def env_props(n_total: int):
     return p
 
 
-def cpu_baseline(budget_s: float):
-    """Oracle (oracle/env_np.py, NumPy fp64) on a bounded sample of the same workload."""
+def _synthetic_pop(props, n, seed):
+    import numpy as np
+
+    rs = np.random.RandomState(seed)
+    hp = props.cluster_prop.house_prop
+    tri = lambda k: rs.triangular(0.9, 1.0, 1.1, k)  # noqa: E731  (Tri(lo, hi, mode=1))
+    return {"Ua": tri(n), "Ca": hp.Ca * tri(n), "Cm": hp.Cm * tri(n), "Hm": hp.Hm * tri(n),
+            "target": hp.target_temp + np.abs(rs.normal(0, 1, n)),
+            "cap": rs.choice([12500.0, 15000.0, 17500.0], n)}
+
+
+def _cpu_run(job):
+    """One CPU-baseline measurement in this process: (config, houses, seconds) ->
+    (house-steps, elapsed s).  oracle/env_np.py (NumPy fp64, one thread)."""
     import numpy as np
 
     from oracle import env_np as O
 
-    n = 65536
-    props = env_props(n)
-    rs = np.random.RandomState(0)
-    hp = props.cluster_prop.house_prop
-    tri = lambda k: rs.triangular(0.9, 1.0, 1.1, k)  # noqa: E731  (Tri(lo, hi, mode=1))
-    pop = {"Ua": tri(n), "Ca": hp.Ca * tri(n), "Cm": hp.Cm * tri(n), "Hm": hp.Hm * tri(n),
-           "target": hp.target_temp + np.abs(rs.normal(0, 1, n)),
-           "cap": rs.choice([12500.0, 15000.0, 17500.0], n)}
-    ora = O.OracleEnv(props, random.Random(1), population=pop)
-    acts = rs.randint(0, 2, (16, n)).astype(bool)
-    t0 = time.perf_counter()
+    cfg, n, seconds = job
+    os.environ.setdefault("OMP_NUM_THREADS", "1")
+    if cfg == "C1":  # 50 houses, deadband bang-bang, reference population + RNG stream
+        props = env_props(n)
+        ora = O.OracleEnv(props, random.Random(4))
+        hp = props.cluster_prop.house_prop
+        act = lambda: O.deadband_bangbang(ora.T, ora.pop["target"], hp.deadband, ora.on)  # noqa: E731
+    else:
+        props = env_props(n)
+        ora = O.OracleEnv(props, random.Random(1), population=_synthetic_pop(props, n, 0))
+        if cfg == "C2":  # random actions
+            rs = np.random.RandomState(1)
+            acts = rs.randint(0, 2, (16, n)).astype(bool)
+            act = lambda: acts[ticks % 16]  # noqa: E731
+        else:  # C3: greedy-myopic on the post-step state, budget = the current signal
+            cap = ora.pop["cap"]
+            cop = props.cluster_prop.house_prop.hvac_prop.cop
+            act = lambda: O.greedy(ora.T, ora.pop["target"], cap, cop, ora.lock, float(ora.S))  # noqa: E731
     ticks = 0
+    t0 = time.perf_counter()
     while True:
-        ora.step(acts[ticks % 16])
+        ora.step(act())
         ticks += 1
         el = time.perf_counter() - t0
-        if el > budget_s:
-            break
-    return {"value": n * ticks / el, "unit": "house-steps/s", "cores": 1, "kind": "port",
-            "sample": f"{n} houses x {ticks} ticks, random actions, oracle/env_np.py NumPy fp64 "
-                      f"restatement (single thread) on the GPU box host, {el:.1f} s"}
+        if el > seconds:
+            return n * ticks, el
 
 
-def pmc_traffic(houses: int):
-    """HBM bytes per k_step launch from the committed rocprofv3 PMC pass (profiles/), if any."""
+def _cpu_model() -> str:
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    import platform
+
+    return platform.processor() or "unknown"
+
+
+def cpu_baseline(budget_s: float):
+    """The oracle (oracle/env_np.py: NumPy fp64 restatement of the reference env step) timed on
+    this host on bounded samples of BASELINE's configs: C1 (50 houses, deadband bang-bang), C2
+    (65,536 houses, random actions: the bench workload's per-house work) and C3 (1,048,576 houses,
+    greedy-myopic, one core: the algorithm is sequential), 1 core and all cores (independent
+    processes, one per core, each stepping its own C2 sample).  The headline entry is C2 on all
+    cores."""
+    import multiprocessing as mp
+
+    ncpu = os.cpu_count() or 1
+    procs = max(1, min(ncpu, 16))  # the GPU box grants 16 cores to a job
+    b = budget_s
+    out = {"cpu_model": _cpu_model(), "os_cpu_count": ncpu, "configs": {}}
+    hs, el = _cpu_run(("C1", 50, 0.15 * b))
+    out["configs"]["C1_50_deadband_bbc_1core"] = {"value": hs / el, "ticks": hs // 50}
+    hs, el = _cpu_run(("C2", 65536, 0.3 * b))
+    c2_1 = hs / el
+    out["configs"]["C2_65536_random_1core"] = {"value": c2_1, "ticks": hs // 65536}
+    ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_run, [("C2", 65536, 0.3 * b)] * procs)
+    c2_all = sum(h for h, _ in res) / max(e for _, e in res)
+    out["configs"][f"C2_65536_random_{procs}cores"] = {"value": c2_all, "procs": procs}
+    hs, el = _cpu_run(("C3", 1 << 20, 0.2 * b))
+    out["configs"]["C3_1048576_greedy_1core"] = {"value": hs / el, "ticks": hs // (1 << 20)}
+    out.update({"value": c2_all, "unit": "house-steps/s", "cores": procs, "kind": "port",
+                "sample": f"oracle/env_np.py (NumPy fp64 restatement, 1 thread per process) on {procs} "
+                          f"processes x 65,536 houses, random actions, {0.3 * b:.1f} s each "
+                          f"(1 core: {c2_1:.3e}); host {out['cpu_model']}, os.cpu_count() = {ncpu}"})
+    return out
+
+
+def pmc_traffic(kernel: str, houses: int):
+    """HBM bytes per launch of `kernel` at `houses` from the committed rocprofv3 PMC passes
+    (profiles/pmc_traffic.json, written by tools/collect_profiles.py), if collected."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
-        rec = d.get(str(houses))
+        rec = d.get(kernel, {}).get(str(houses))
         return None if rec is None else float(rec["hbm_bytes_per_launch"])
-    except (OSError, ValueError, KeyError):
+    except (OSError, ValueError, KeyError, AttributeError):
         return None
 
 
@@ -128,6 +215,9 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.cpu_seconds)  # before this process touches the GPU
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     comm = None
@@ -143,6 +233,7 @@ def main():
         from mdr_amd.distributed import make_comm
 
         comm = make_comm(kind)
+    from mdr_amd import _lib as L
     from mdr_amd.environment import Environment
 
     n_total = args.houses * world
@@ -150,6 +241,9 @@ def main():
     env = Environment(props, device=dev, rng=random.Random(4), population="synthetic", seed=1234,
                       rank=rank, world=world, comm=comm)
     n_loc = env.n_local
+    sh = env.shard
+    window = min(max(args.window, 0), 32)
+    sh.set_rollout_window(window)
     chunk = min(args.chunk, args.steps)
     chunks = [chunk] * (args.steps // chunk) + ([args.steps % chunk] if args.steps % chunk else [])
     acts = None
@@ -158,16 +252,23 @@ def main():
     rew = torch.empty((chunk, n_loc), dtype=torch.float64, device=dev)
     dactor = None
     if args.workload == "actor":
-        if world > 1:
-            raise SystemExit("--workload actor runs on one GPU (sharded actor rollouts: see DESIGN.md)")
         from mdr_amd.actor import DeviceActor, make_actor
 
         dactor = DeviceActor(env, make_actor(env.obs_spec().n_feat, 2, [100, 100], seed=1),
                              precision=args.precision)
+    g_act = None
+    if args.workload == "greedy":
+        if world > 1:
+            raise SystemExit("--workload greedy runs on one GPU (config C3)")
+        g_act = torch.empty(n_loc, dtype=torch.uint8, device=dev)
 
     def run(n):
         if dactor is not None:
             dactor.rollout(n, rewards=rew[:n])
+        elif g_act is not None:  # C3: controller on the post-step state -> step, every tick
+            for t in range(n):
+                env.greedy_actions(out=g_act)
+                env.step_tensor(g_act, rewards=rew[t])
         else:
             env.rollout(n, actions=None if acts is None else acts[:n], action_mode=args.mode,
                         rewards=rew[:n])
@@ -190,8 +291,8 @@ def main():
 
     barrier()
     torch.cuda.synchronize()
-    # HIP events on the stream the k_step launches are issued on (the graph side stream)
-    launch_stream = env.rollout_stream()
+    # HIP events on the stream the step launches are issued on (the graph side stream)
+    launch_stream = env.rollout_stream(use_graph=g_act is None)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0 = time.perf_counter()
     ev0.record(launch_stream)
@@ -211,32 +312,46 @@ def main():
         elapsed = float(t.item())
     value = n_total * args.steps / elapsed
 
-    # dominant kernel k_step: one launch per tick (fused random controller + lookahead), so its
-    # average launch duration over the timed region = launch-stream event time / steps (this
-    # includes the ~1 us graph inter-kernel gap; rocprofv3's per-kernel average is in profiles/)
-    per_tick_ms = gpu_ms / args.steps
-    kern_ms, kern_launches = per_tick_ms, args.steps
-    if comm is not None:
-        # the sharded timed region also holds the per-tick RCCL allreduce: time k_step alone in
-        # a local graph rollout of the same shard (after the timed region, rewards discarded)
-        from mdr_amd._lib import ACT_RANDOM
-
-        sh = env.shard
+    # ---- roofline of the dominant kernel: timed ALONE after the timed region, >= 500 ticks in one
+    # graph-captured local rollout (rewards kept: [ticks, n] rows), HIP events on its launch stream
+    cur = torch.cuda.current_stream(dev)
+    kt = max(args.kernel_ticks, 1)
+    mode_id = L.ACT_RANDOM if args.mode == "random" else L.ACT_BUFFER
+    kern = step_kernel_name(n_loc, args.mode, window)
+    actor_ms = None
+    if dactor is None and g_act is None:
+        kbuf = torch.empty((kt, n_loc), dtype=torch.float64, device=dev)
+        kacts = None if acts is None else (torch.rand((kt, n_loc), device=dev) < 0.5).to(torch.uint8)
+        kticks = env.driver_window(kt)
         ls = sh.launch_stream(True)
-        kern_launches = min(args.steps, 500)
-        ticks = env.driver_window(kern_launches)
-        rbuf = rew[0]
-        sh.rollout(ticks, None, 0, ACT_RANDOM, rbuf, 0, True)  # capture
-        torch.cuda.synchronize()
-        ev0.record(ls)
-        sh.rollout(ticks, None, 0, ACT_RANDOM, rbuf, 0, True)
+        for rep in range(2):  # capture, then the timed replay
+            if rep:
+                torch.cuda.synchronize()
+                ev0.record(ls)
+            sh.rollout(kticks, kacts, n_loc if kacts is not None else 0, mode_id, kbuf, n_loc, True)
         ev1.record(ls)
         torch.cuda.synchronize()
-        kern_ms = ev0.elapsed_time(ev1) / kern_launches
-    if dactor is not None:
-        # the rollout graph interleaves k_actor and k_step: time each kernel alone, back to back
-        # on the current stream (HIP events on that stream), over the same state
-        cur = torch.cuda.current_stream(dev)
+        del kbuf
+        launches = -(-kt // window) if window > 0 else kt
+        kern_ms = ev0.elapsed_time(ev1) / launches
+        k_win = kt // launches if window > 0 else 1
+        bytes_launch = window_bytes(n_loc, k_win, args.mode) if window > 0 else BYTES_PER_HOUSE_STEP * n_loc
+        steps_launch = k_win
+    elif g_act is not None:
+        K = 20
+        torch.cuda.synchronize()
+        ev0.record(cur)
+        for t in range(K):
+            env.greedy_actions(out=g_act)
+            env.step_tensor(g_act, rewards=rew[t % rew.shape[0]])
+        ev1.record(cur)
+        torch.cuda.synchronize()
+        launches, kern_ms = K, ev0.elapsed_time(ev1) / K
+        bytes_launch = (BYTES_PER_HOUSE_STEP + GREEDY_EXTRA) * n_loc
+        steps_launch = 1
+        kern = "greedy tick: k_greedy_keys + hipCUB radix sort + scan + k_greedy_walk + k_step"
+    else:
+        # the actor rollout graph interleaves k_actor and k_step: time the actor alone
         K = 50
         act_buf = torch.empty(n_loc, dtype=torch.uint8, device=dev)
         prob_buf = torch.empty(n_loc, dtype=torch.float32, device=dev)
@@ -248,10 +363,12 @@ def main():
         ev1.record(cur)
         torch.cuda.synchronize()
         actor_ms = ev0.elapsed_time(ev1) / K
-        kern_ms = max(per_tick_ms - actor_ms, 1e-6)  # the step kernel's share of a tick
-    bytes_launch = BYTES_PER_HOUSE_STEP * n_loc
+        launches = K
+        kern_ms = max(gpu_ms / args.steps - actor_ms, 1e-6)  # the step kernel's share of a tick
+        bytes_launch = BYTES_PER_HOUSE_STEP * n_loc
+        steps_launch = 1
     achieved = bytes_launch / (kern_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(n_loc)
+    traffic = pmc_traffic(kern, n_loc)
     out = {
         "metric": METRIC,
         "value": value,
@@ -265,21 +382,31 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (device Philox population, reference noise model; fused Philox random actions)",
-        "config": {"workload": "1M houses per GPU, random actions, fused FSM+thermal+reward step "
-                               "(BASELINE metric at 1M houses; configs[1]'s controller)",
+        "config": {"workload": "1M houses per GPU, random actions, fused FSM+thermal+reward step, every "
+                               "tick's reward row written (BASELINE metric at 1M houses; configs[1]'s controller)",
                    "houses_per_gpu": n_loc, "houses_total": n_total, "dt_s": props.time_step.seconds,
                    "signal": "sinusoidals", "penalty": "individual_L2", "action_mode": args.mode,
-                   "chunk_ticks": chunk,
-                   "sharded_pipeline": comm.pipeline(env.shard) if comm is not None else None,
+                   "chunk_ticks": chunk, "window_ticks": window,
+                   "sharded_pipeline": comm.pipeline(sh) if comm is not None else None,
                    "parallelism": f"house-sharded x{world} ({kind} allreduce of "
-                                                        "per-tick power counts)" if comm is not None else "1 GPU"},
+                                  "per-window power counts)" if comm is not None else "1 GPU"},
+        "timed_region": {"wall_s": elapsed, "launch_stream_event_ms": gpu_ms,
+                         "includes": "host drivers (OD-temperature RNG, solar, signal) + tick staging + "
+                                     "graph launches + device work"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS,
-                     "traffic": traffic, "kernel": step_kernel_name(n_loc, args.mode),
-                     "kernel_avg_us": kern_ms * 1e3, "launches_timed": kern_launches,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kern,
+                     "kernel_avg_us": kern_ms * 1e3, "launches_timed": launches,
+                     "house_steps_per_launch": steps_launch * n_loc,
                      "algorithmic_bytes_per_launch": bytes_launch,
-                     "bytes_per_house_step": BYTES_PER_HOUSE_STEP},
+                     "bytes_per_house_step": bytes_launch / (steps_launch * n_loc),
+                     "timing": "HIP events around a graph replay of >= 500 ticks after the timed region"},
     }
+    if g_act is not None:
+        out["data"] = "synthetic (device Philox population, reference noise model)"
+        out["config"]["workload"] = ("C3: 1M houses, device GreedyMyopic (sort by -(T - target), budget = "
+                                     "signal) on the post-step state, then env.step, every tick")
+        out["config"]["action_mode"] = "greedy_myopic"
+        out["roofline"]["timing"] = "HIP events around 20 greedy+step ticks after the timed region"
     if dactor is not None:
         a = dactor.actor
         flops_house = 2 * sum(l.in_features * l.out_features for l in a.fc)  # 30,400 at F = 50
@@ -294,13 +421,13 @@ def main():
         out["config"]["actor"] = {"layers": [a.fc[0].in_features, 100, 100, 2], "precision": args.precision}
         out["roofline"] = {"bound": "mfma", "achieved": tfs, "peak": BF16_PEAK_TFS, "unit": "TFLOP/s",
                            "frac": tfs / BF16_PEAK_TFS, "traffic": None, "kernel": "mdr::k_actor",
-                           "kernel_avg_us": actor_ms * 1e3, "launches_timed": K,
+                           "kernel_avg_us": actor_ms * 1e3, "launches_timed": launches,
                            "algorithmic_flops_per_launch": flops_launch, "flops_per_house": flops_house,
                            "mfma_products_per_mac": 3 if args.precision == "bf16x3" else 1,
                            "step_kernel": {"kernel": "mdr::k_step (BUFFER)", "avg_us": kern_ms * 1e3,
                                            "hbm_GBps": achieved, "frac": achieved / HBM_PEAK_GBS}}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_seconds)
+    if cpu is not None:
+        out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
     if comm is not None:

@@ -197,6 +197,15 @@ int mdr_rollout(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t*
                 int64_t act_stride, int action_mode, double* reward, int64_t rew_stride,
                 double* p_out, int use_graph, void* stream);
 
+/* Open-loop sources (MDR_ACT_RANDOM / _ALWAYS_ON / _BUFFER) with individual_L2 and <= 4 capacity
+ * classes run TEMPORALLY BLOCKED: windows of up to `ticks` steps per launch (k_step_window), the
+ * state and parameters read and written once per window, rewards written every tick, each tick's
+ * cluster power from counts the previous launch ran ahead (the FSM of an open-loop source does
+ * not depend on the thermal state).  Bit-identical to the one-tick path.  ticks in 1..32
+ * (default 32; MDR_WINDOW env at mdr_create), 0 = one launch per tick.  Applies to mdr_rollout and
+ * mdr_rollout_sharded; drops cached rollout graphs. */
+int mdr_set_rollout_window(mdr_ctx* ctx, int ticks);
+
 /* ---- observation vector (norm_state_dict, norm.py:178-218) ----------------------------- */
 typedef struct mdr_obs_spec {
   int32_t n_feat;        /* features per house written (row length of obs) */

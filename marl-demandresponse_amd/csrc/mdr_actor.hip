@@ -160,7 +160,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     }
     for (int q = lane; q < 32 * FS + 16 * d.ks1; q += 64) w_obs[q] = 0.f;
     if (tid < MDR_MAX_CAP) s_hist[tid] = 0u;
-    if (o.sc_dev) { o.s = o.sc_dev[0]; o.solar = o.sc_dev[1]; o.t_od = o.sc_dev[2]; }
+    if (o.sc_dev) { o.s = o.sc_dev[1]; o.solar = o.sc_dev[2]; o.t_od = o.sc_dev[3]; }  // mdr_obs_scalars row
     obs_consts(p, o, p_dev ? *p_dev : o.p, s_cf, tid, nthr);
   }
   __syncthreads();

@@ -86,14 +86,15 @@ struct mdr_ctx {
   bool cached = false;                   // cached param-only thermal coefficients (MDR_VARIANT=coef)
   bool fastdiv = true;                   // shared-reciprocal exact division (MDR_FASTDIV=0 disables)
   int tpw = 0;                           // k_step_pipe tiles per wave (MDR_TPW; 0: k_step_t)
+  int win = kWindowMax;                  // ticks per k_step_window launch (MDR_WINDOW; 0: one-tick path)
+  unsigned long long* d_wslab = nullptr; // 3 window count slabs [kWindowMax][kCountShards][n_cap]
+  int wslab_len = 0;
   bool coef_dirty = true;
   double* d_coef = nullptr;              // [6][n] r1, r2, A3, A4, e1, e2
   int* d_flags = nullptr;                // [0] params_bad
   // rollout tick drivers
   TickArgs* d_ticks = nullptr;
-  TickArgs* h_ticks = nullptr;  // pinned staging
   int ticks_cap = 0;
-  hipEvent_t ticks_free = nullptr;
   std::map<GraphKey, std::pair<hipGraphExec_t, int>> graphs;  // exec, ring phase at end
   // greedy scratch
   int64_t g_cap = 0;
@@ -119,8 +120,6 @@ struct mdr_ctx {
   bool actor_ready = false;
   int n_cu = 0;
   double* d_obs_sc = nullptr;  // [ticks_cap][4]
-  double* h_obs_sc = nullptr;  // pinned staging
-  int obs_sc_cap = 0;
   uint8_t* d_act = nullptr;    // [n_local] actor actions when the caller keeps none
   std::map<std::vector<int64_t>, hipGraphExec_t> actor_graphs;
   // interpolated base power (row a10): grid | table | capacities
@@ -323,6 +322,14 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   // wave up to ~1.5M houses per shard, 4 above; MDR_TPW=0 selects the one-tile kernel k_step_t
   c->tpw = cfg->n_local <= 1572864 ? 2 : 4;
   if (const char* e = getenv("MDR_TPW")) c->tpw = atoi(e);
+  if (const char* e = getenv("MDR_WINDOW")) c->win = atoi(e) < 0 ? 0 : atoi(e) > kWindowMax ? kWindowMax : atoi(e);
+  if (cfg->n_cap <= kWindowCap) {
+    c->wslab_len = kWindowMax * kCountShards * cfg->n_cap;
+    if (hipMalloc(&c->d_wslab, 3 * sizeof(unsigned long long) * c->wslab_len) != hipSuccess)
+      return cleanup(fail(MDR_ENOMEM, "window count slabs"));
+  } else {
+    c->win = 0;
+  }
   if (c->cached) {
     k.coef_stride = cfg->n_local;
     if (hipMalloc(&c->d_coef, 6 * sizeof(double) * cfg->n_local) != hipSuccess)
@@ -332,8 +339,6 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   if (hipMalloc(&c->d_pen_partial, 2 * sizeof(double) * c->pen_blocks) != hipSuccess ||
       hipMalloc(&c->d_partial2, 2 * sizeof(double)) != hipSuccess)
     return cleanup(fail(MDR_ENOMEM, "penalty partials"));
-  if (hipEventCreateWithFlags(&c->ticks_free, hipEventDisableTiming) != hipSuccess)
-    return cleanup(fail(MDR_EHIP, "event"));
   for (auto& e : c->ev)
     if (hipEventCreate(&e) != hipSuccess) return cleanup(fail(MDR_EHIP, "event"));
   for (int i = 0; i < kSlabs; ++i)
@@ -360,16 +365,14 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->d_interp);
   hipFree(c->d_act);
   hipFree(c->d_obs_sc);
-  if (c->h_obs_sc) hipHostFree(c->h_obs_sc);
   hipFree(c->d_tables);
   hipFree(c->d_coef);
   hipFree(c->d_flags);
   hipFree(c->d_slab);
+  hipFree(c->d_wslab);
   hipFree(c->d_pen_partial);
   hipFree(c->d_partial2);
   hipFree(c->d_ticks);
-  if (c->h_ticks) hipHostFree(c->h_ticks);
-  if (c->ticks_free) hipEventDestroy(c->ticks_free);
   for (auto& e : c->ev)
     if (e) hipEventDestroy(e);
   for (int i = 0; i < kSlabs; ++i) {
@@ -479,30 +482,87 @@ int mdr_reward_finalize(mdr_ctx* c, const mdr_tick* tick, double* reward, void* 
 }
 
 // ------------------------------------------------------------------------------------ rollout
+// n 32-byte records from host memory into device memory on `st`, through kernel arguments:
+// nothing on the host waits for the device, and the host array may be reused on return
+static int stage_recs(const void* src, int n, void* dst, hipStream_t st) {
+  const Rec32* s = static_cast<const Rec32*>(src);
+  Rec32* d = static_cast<Rec32*>(dst);
+  for (int off = 0; off < n; off += kStageRecs) {
+    const int m = n - off < kStageRecs ? n - off : kStageRecs;
+    StagePack pk;
+    memcpy(pk.r, s + off, (size_t)m * sizeof(Rec32));
+    hipLaunchKernelGGL(k_stage32, dim3(1), dim3(kStageRecs), 0, st, pk, m, d + off);
+    LAUNCH_CHECK("k_stage32");
+  }
+  return MDR_OK;
+}
+
 static int stage_ticks(mdr_ctx* c, int n, const mdr_tick* ticks, hipStream_t st) {
   if (n > c->ticks_cap) {
-    HIP_TRY(hipEventSynchronize(c->ticks_free));
+    HIP_TRY(hipDeviceSynchronize());  // queued graphs may still read the old buffers
     hipFree(c->d_ticks);
-    if (c->h_ticks) hipHostFree(c->h_ticks);
+    hipFree(c->d_obs_sc);
     c->d_ticks = nullptr;
-    c->h_ticks = nullptr;
-    int cap = n < 64 ? 64 : n;
+    c->d_obs_sc = nullptr;
+    int cap = n < 128 ? 128 : n;
     HIP_TRY(hipMalloc(&c->d_ticks, cap * sizeof(TickArgs)));
-    HIP_TRY(hipHostMalloc(&c->h_ticks, cap * sizeof(TickArgs), hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&c->d_obs_sc, (size_t)cap * 4 * sizeof(double)));
     c->ticks_cap = cap;
     for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
     c->graphs.clear();
+    for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
+    c->actor_graphs.clear();
   }
-  HIP_TRY(hipEventSynchronize(c->ticks_free));  // previous H2D of the staging buffer done
-  for (int i = 0; i < n; ++i) c->h_ticks[i] = to_tick(&ticks[i]);
-  HIP_TRY(hipMemcpyAsync(c->d_ticks, c->h_ticks, n * sizeof(TickArgs), hipMemcpyHostToDevice, st));
-  HIP_TRY(hipEventRecord(c->ticks_free, st));
+  // stream order: every earlier launch reading d_ticks (a replayed graph) precedes this write
+  return stage_recs(ticks, n, c->d_ticks, st);
+}
+
+// ---- windowed rollout (k_step_window): open-loop action sources, individual_L2
+static bool window_ok(const mdr_ctx* c, int mode) {
+  return c->win > 0 && c->d_wslab && c->kp.n_cap <= kWindowCap && c->kp.penalty_mode == MDR_PEN_INDIVIDUAL_L2 &&
+         (mode == MDR_ACT_RANDOM || mode == MDR_ACT_ALWAYS_ON || mode == MDR_ACT_BUFFER);
+}
+
+// n ticks as ceil(n / win) windows of near-equal size: one k_count_window for the first window,
+// then one k_step_window per window (each counting the next window's ticks).  comm != nullptr:
+// sum-allreduce each window's count slab before its launch (sharded serial pipeline).
+static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t* action, int64_t act_stride,
+                           int mode, double* reward, int64_t rew_stride, double* p_out, ncclComm_t comm,
+                           hipStream_t st) {
+  const int nw = (n + c->win - 1) / c->win;
+  const int base = n / nw, rem = n % nw;
+  auto wsz = [&](int w) { return base + (w < rem ? 1 : 0); };
+  auto slab = [&](int w) { return c->d_wslab + (size_t)(w % 3) * c->wslab_len; };
+  HIP_TRY(hipMemsetAsync(c->d_wslab, 0, 3 * sizeof(unsigned long long) * c->wslab_len, st));
+  const unsigned grid = blocks(blocks(c->kp.n, 128), 4);  // one 128-house tile per wave, 4 waves per block
+  KParams kp = c->kp;
+#define MDR_WIN_DISPATCH(KERNEL, ...)                                                                      \
+  do {                                                                                                     \
+    if (mode == MDR_ACT_RANDOM) hipLaunchKernelGGL(KERNEL<MDR_ACT_RANDOM>, dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
+    else if (mode == MDR_ACT_ALWAYS_ON) hipLaunchKernelGGL(KERNEL<MDR_ACT_ALWAYS_ON>, dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL(KERNEL<MDR_ACT_BUFFER>, dim3(grid), dim3(256), 0, st, __VA_ARGS__);           \
+  } while (0)
+  MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, wsz(0), slab(0));
+  LAUNCH_CHECK("k_count_window");
+  int t0 = 0;
+  for (int w = 0; w < nw; ++w) {
+    const int K = wsz(w), la = w + 1 < nw ? wsz(w + 1) : 0;
+    if (comm) RCCL_TRY(ncclAllReduce(slab(w), slab(w), (size_t)K * c->slab_len, ncclUint64, ncclSum, comm, st));
+    const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
+    MDR_WIN_DISPATCH(k_step_window, kp, a, act_stride, tk + t0, K, la, slab(w), reward + (int64_t)t0 * rew_stride,
+                     rew_stride, w == nw - 1 ? p_out : nullptr, slab(w + 1), slab(w + 2), c->wslab_len);
+    LAUNCH_CHECK("k_step_window");
+    t0 += K;
+  }
+#undef MDR_WIN_DISPATCH
   return MDR_OK;
 }
 
 // The launch sequence of a rollout; tick args come from d_ticks so a captured graph is reusable.
 static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t act_stride, int mode,
                             double* reward, int64_t rew_stride, double* p_out, hipStream_t st) {
+  if (window_ok(c, mode)) return window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride,
+                                                 p_out, nullptr, st);
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
   c->ring = 0;
   const bool la = lookahead_ok(mode);
@@ -840,6 +900,11 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
   if (rc) return rc;
   rc = stage_ticks(c, n, ticks, st);
   if (rc) return rc;
+  if (window_ok(c, mode)) {
+    rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, c->comm, st);
+    c->counts_ready = false;
+    return rc;
+  }
   const bool can_overlap = lookahead_ok(mode) && rew_stride != 0 && c->comm_stream;
   if (can_overlap && c->overlap_mode < 0 && n >= 16)
     return rollout_sharded_calibrate(c, n, mode, reward, rew_stride, p_out, st);
@@ -853,6 +918,18 @@ int mdr_rollout_sharded_mode(mdr_ctx* c, int* mode, double* us_serial, double* u
   *mode = c->overlap_mode;
   if (us_serial) *us_serial = c->calib_us[0];
   if (us_overlap) *us_overlap = c->calib_us[1];
+  return MDR_OK;
+}
+
+int mdr_set_rollout_window(mdr_ctx* c, int ticks) {
+  if (!c || ticks < 0 || ticks > kWindowMax) return fail(MDR_EARG, "mdr_set_rollout_window: ticks outside 0..32");
+  if (ticks > 0 && !c->d_wslab) return fail(MDR_EARG, "mdr_set_rollout_window: more than 4 capacity classes");
+  if (ticks != c->win) {
+    HIP_TRY(hipDeviceSynchronize());  // cached graphs may be in flight
+    for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
+    c->graphs.clear();
+    c->win = ticks;
+  }
   return MDR_OK;
 }
 
@@ -1061,29 +1138,8 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
   hipStream_t st = S(stream);
   if (int rc = refresh_if_dirty(c, st)) return rc;
   if (int rc = stage_ticks(c, n, ticks, st)) return rc;
-  // per-tick obs scalars [s, solar, t_od, -] next to the tick drivers
-  if (n > c->obs_sc_cap) {
-    HIP_TRY(hipStreamSynchronize(st));
-    hipFree(c->d_obs_sc);
-    if (c->h_obs_sc) hipHostFree(c->h_obs_sc);
-    c->d_obs_sc = nullptr;
-    c->h_obs_sc = nullptr;
-    const int cap = n < 64 ? 64 : n;
-    HIP_TRY(hipMalloc(&c->d_obs_sc, (size_t)cap * 4 * sizeof(double)));
-    HIP_TRY(hipHostMalloc(&c->h_obs_sc, (size_t)cap * 4 * sizeof(double), hipHostMallocDefault));
-    c->obs_sc_cap = cap;
-    for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
-    c->actor_graphs.clear();
-  }
-  HIP_TRY(hipEventSynchronize(c->ticks_free));  // (stage_ticks' event also covers this buffer)
-  for (int t = 0; t < n; ++t) {
-    c->h_obs_sc[4 * t] = osc[t].s;
-    c->h_obs_sc[4 * t + 1] = osc[t].solar;
-    c->h_obs_sc[4 * t + 2] = osc[t].t_od;
-    c->h_obs_sc[4 * t + 3] = 0.0;
-  }
-  HIP_TRY(hipMemcpyAsync(c->d_obs_sc, c->h_obs_sc, (size_t)n * 4 * sizeof(double), hipMemcpyHostToDevice, st));
-  HIP_TRY(hipEventRecord(c->ticks_free, st));
+  // per-tick obs scalars [s, solar, t_od, -] next to the tick drivers (same capacity)
+  if (int rc = stage_recs(osc, n, c->d_obs_sc, st)) return rc;
 
   ObsArgs o = obs_args(c, sp, &osc[0]);
   auto launches = [&]() -> int {

@@ -42,6 +42,18 @@ struct TickArgs {
   uint64_t tick;
 };
 
+// Rollout tick drivers / per-tick obs scalars are staged into device memory by a kernel that
+// takes them BY VALUE (kernel arguments are copied at launch), so the host never waits for a
+// previous copy to finish before rewriting a staging buffer.
+struct Rec32 {
+  double v[4];
+};
+constexpr int kStageRecs = 64;  // 2 KiB of records per staging launch
+struct StagePack {
+  Rec32 r[kStageRecs];
+};
+static_assert(sizeof(TickArgs) == sizeof(Rec32), "TickArgs is staged as a 32-byte record");
+
 struct PopArgs {
   double target_temp, std_target, lo, hi, ca0, cm0, hm0, init_air, init_mass;
 };
@@ -53,9 +65,10 @@ struct ObsArgs {
   const float* halo_msg;  // [lo + hi][msg_w] or null
   double norm_reg_sig, cfg_ua, cfg_ca, cfg_cm, cfg_hm, cfg_cop, cfg_lcf, cfg_cap;
   double p, s, solar, t_od;
-  const double* sc_dev;  // per-tick device scalars [s, solar, t_od] overriding the values above, or null
+  const double* sc_dev;  // per-tick device mdr_obs_scalars row {-, s, solar, t_od} overriding the values above, or null
 };
 
+__global__ void k_stage32(StagePack pk, int n, Rec32* dst);
 __global__ void k_power_counts(KParams p, const uint8_t* action, int action_mode, uint64_t tick,
                                const TickArgs* tkp, unsigned long long* slab);
 template <int HPT, bool CACHED, bool FAST, int ACT, int LA>
@@ -69,6 +82,16 @@ __global__ void k_step_pipe(KParams p, const uint8_t* action, TickArgs tk, const
                             const unsigned long long* counts, double* reward, double* p_out,
                             unsigned long long* next_slab, unsigned long long* zero_slab);
 constexpr int kPipeMaxCap = 4;
+constexpr int kWindowMax = 32;  // = kWinMax: ticks per k_step_window launch
+constexpr int kWindowCap = 4;   // = kWinCap: capacity classes the window kernel supports
+template <int ACT>
+__global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int K,
+                              int la_K, const unsigned long long* counts, double* reward, int64_t rew_stride,
+                              double* p_out, unsigned long long* next_slab, unsigned long long* zero_slab,
+                              int zero_len);
+template <int ACT>
+__global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int nt,
+                               unsigned long long* slab);
 __global__ void k_probe_stream(KParams p, double* reward);
 __global__ void k_refresh(KParams p, double* coef, int* params_bad);
 __global__ void k_div_check(const double* a, const double* b, int64_t n, unsigned long long* mismatches);

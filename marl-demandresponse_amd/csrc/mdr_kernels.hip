@@ -31,6 +31,11 @@ __device__ __forceinline__ void count_on(bool on, int cls, int n_cap, unsigned* 
   }
 }
 
+__global__ void k_stage32(StagePack pk, int n, Rec32* __restrict__ dst) {
+  const int i = threadIdx.x;
+  if (i < n) dst[i] = pk.r[i];
+}
+
 // --------------------------------------------------------------------------------------- K0
 // Phase 1: FSM only -> ON count per capacity class (cluster.py:82-88).  Reads 6 B per house.
 __global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* __restrict__ action,
@@ -498,6 +503,309 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
       atomicAdd(&next_slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)hist[tid]);
   }
 }
+
+// --------------------------------------------------------------------------------------- K1W
+// Temporally blocked step for OPEN-LOOP action sources (random / always-on / action buffer), the
+// rollout path: one launch steps a window of K ticks.  Each wave loads its tile's state and
+// parameters ONCE, keeps them in registers for the K ticks, and writes the state back once; per
+// tick it writes only the reward row.  Per house-step that is 8 B + 89 B / K of HBM traffic
+// instead of 89-99 B.  What makes it exact:
+//   * an open-loop source's actions do not depend on the thermal state, so the lockout FSM — and
+//     with it every tick's ON set and cluster power P(t) — can be run ahead of the thermal
+//     update.  The launch of window w runs the FSM through window w+1 (the "lookahead") and
+//     accumulates window w+1's per-tick ON counts per capacity class into its count slabs, so
+//     each tick's reward has its GLOBAL P(t) when the next launch starts (same integer counts as
+//     the one-tick kernels: bit-identical P);
+//   * the parameter-only part of the RC update (roots r1/r2, A3/A4, exp(r dt) and the shared
+//     reciprocals of Ca, Ua and r2-r1) is computed once per window, not once per tick — the same
+//     expressions in the same order (rc_coeffs_t / recip), so results are bit-identical to the
+//     one-tick kernels, which recompute them every tick;
+//   * the per-tick drivers (t_od_prev, solar, s_prev) of the window are wave-uniform scalar loads
+//     of the staged mdr_tick array; the K signal penalties are reduced lane-parallel (lane j:
+//     tick j) from the count slabs at launch start and broadcast with readlane.
+// Counts layout: slab[j][kCountShards][n_cap] (u64) per window tick j.
+constexpr int kWinMax = 32;    // ticks per window launch (and per lookahead)
+constexpr int kWinCap = 4;     // capacity classes held in registers
+
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)b, l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
+}
+
+// Per-window thermal constants of one house (FAST path: shared reciprocals).
+struct RcWin {
+  RcCoef k;
+  Recip rCa, rc, rd;  // 1/Ca, 1/Ua (= 1/c), 1/(r2 - r1)
+  double UaHm;
+};
+
+__device__ __forceinline__ RcWin rc_window(double ua, double ca, double cm, double hm, double dt) {
+  RcWin w;
+  w.k = rc_coeffs_t<true>(ua, ca, cm, hm, dt);
+  w.rCa = recip(ca);
+  w.rc = recip(ua);
+  w.rd = recip(w.k.r2 - w.k.r1);
+  w.UaHm = ua + hm;
+  return w;
+}
+
+// rc_apply_t<FAST> with the window's reciprocals (identical operations and order)
+template <bool FAST>
+__device__ __forceinline__ void rc_apply_win(double T, double Tm, double Ua, double Hm, const RcWin& w,
+                                             double q_hvac, double solar, double t_od, double& T_out,
+                                             double& Tm_out) {
+  const RcCoef& k = w.k;
+  const double od_k = t_od + 273.0;
+  const double t_k = T + 273.0;
+  const double tm_k = Tm + 273.0;
+  const double Qa = q_hvac + solar;
+  const double d = Qa + Ua * od_k;
+  double dTA0dt, d_c, r2d_c, A1;
+  if (FAST) {
+    dTA0dt = div_by(Hm * tm_k, w.rCa) - div_by(w.UaHm * t_k, w.rCa) + div_by(Ua * od_k, w.rCa) +
+             div_by(Qa, w.rCa);
+    d_c = div_by(d, w.rc);
+    r2d_c = div_by(k.r2 * d, w.rc);
+    A1 = div_by(k.r2 * t_k - dTA0dt - r2d_c, w.rd);
+  } else {
+    const double Ca = -w.rCa.nb, c = -w.rc.nb;  // (exact negations of the stored -b)
+    dTA0dt = Hm * tm_k / Ca - w.UaHm * t_k / Ca + Ua * od_k / Ca + Qa / Ca;
+    d_c = d / c;
+    r2d_c = k.r2 * d / c;
+    A1 = (k.r2 * t_k - dTA0dt - r2d_c) / -w.rd.nb;
+  }
+  const double A2 = t_k - d_c - A1;
+  const double t_new = A1 * k.e1 + A2 * k.e2 + d_c;
+  const double tm_new = A1 * k.A3 * k.e1 + A2 * k.A4 * k.e2 + 0.0 + d_c;
+  T_out = t_new - 273.0;
+  Tm_out = tm_new - 273.0;
+}
+
+// Philox words of the (64-house group, tick) slots a wave tile needs, in LDS:
+// slot s = j * G + g for tick offset j and group g0 + g (G = groups the tile spans, 2 or 3).
+__device__ __forceinline__ void win_random_stage(uint64_t seed, uint64_t g0, int G, const TickArgs* tkp, int nt,
+                                                 uint2* rw) {
+  const int lane = threadIdx.x & 63;
+  const int ns = G * nt;
+  for (int s = lane; s < ns; s += 64) {
+    const int j = s / G;
+    const int g = s - j * G;
+    uint32_t lo, hi;
+    philox_words(seed, g0 + (uint64_t)g, tkp[j].tick, lo, hi);
+    rw[s] = make_uint2(lo, hi);
+  }
+}
+
+template <int ACT>
+__device__ __forceinline__ bool win_action(const uint2* rw, int G, uint64_t g0, int j, uint64_t gid,
+                                           const uint8_t* arow, uint32_t i) {
+  if (ACT == MDR_ACT_ALWAYS_ON) return true;
+  if (ACT == MDR_ACT_BUFFER) return arow[i] != 0;
+  const uint2 wd = rw[j * G + (int)((gid >> 6) - g0)];
+  return bit_of(wd.x, wd.y, gid);
+}
+
+// FSM-only run of nt ticks (tick offsets j0 .. j0+nt-1 of the staged random slots / action rows)
+// from words w[0..1], ON counts per tick and class into the block histogram hist[j][kWinCap].
+template <int ACT>
+__device__ __forceinline__ void win_count(const KParams& p, uint32_t wa, uint32_t wb, int cls0, int cls1, bool v0,
+                                          bool v1, uint32_t i0, uint64_t gid0, const uint2* rw, int G, uint64_t g0,
+                                          int j0, int nt, const uint8_t* action, int64_t act_stride,
+                                          unsigned* hist) {
+  const int lane = threadIdx.x & 63;
+  for (int j = 0; j < nt; ++j) {
+    const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)(j0 + j) * act_stride : nullptr;
+    const bool a0 = v0 && win_action<ACT>(rw, G, g0, j0 + j, gid0, arow, i0);
+    const bool a1 = v1 && win_action<ACT>(rw, G, g0, j0 + j, gid0 + 1, arow, i0 + 1);
+    wa = hvac_fsm(wa, a0, p.dt, p.L);
+    wb = hvac_fsm(wb, a1, p.dt, p.L);
+    const bool o0 = v0 && hv_on(wa), o1 = v1 && hv_on(wb);
+#pragma unroll
+    for (int c = 0; c < kWinCap; ++c) {
+      if (c < p.n_cap) {
+        const unsigned cnt = (unsigned)__popcll(__ballot(o0 && cls0 == c)) +
+                             (unsigned)__popcll(__ballot(o1 && cls1 == c));
+        if (lane == 0 && cnt) atomicAdd(&hist[j * kWinCap + c], cnt);
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsigned* hist,
+                                          unsigned long long* slab) {
+  for (int e = threadIdx.x; e < nt * p.n_cap; e += blockDim.x) {
+    const int j = e / p.n_cap, c = e - j * p.n_cap;
+    const unsigned v = hist[j * kWinCap + c];
+    if (v) atomicAdd(&slab[((size_t)j * kCountShards + blockIdx.x % kCountShards) * p.n_cap + c],
+                     (unsigned long long)v);
+  }
+}
+
+// First window of a rollout: ON counts of ticks 0 .. nt-1 (no state change).
+template <int ACT>
+__global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* __restrict__ action,
+                                                      int64_t act_stride, const TickArgs* __restrict__ tkp, int nt,
+                                                      unsigned long long* __restrict__ slab) {
+  __shared__ uint2 s_rw[4][3 * kWinMax];
+  __shared__ unsigned s_hist[kWinMax * kWinCap];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int j = tid; j < kWinMax * kWinCap; j += blockDim.x) s_hist[j] = 0;
+  const uint32_t n = (uint32_t)p.n;
+  const uint32_t tile = blockIdx.x * 4u + (uint32_t)wv;
+  const uint32_t i0 = tile * 128u + (uint32_t)lane * 2u;
+  const bool v0 = i0 < n, v1 = i0 + 1u < n;
+  const uint32_t ia = v0 ? i0 : n - 1u, ib = v1 ? i0 + 1u : n - 1u;
+  const uint32_t wa = p.hvac[ia], wb = p.hvac[ib];
+  const int cls0 = p.cap_idx[ia], cls1 = p.cap_idx[ib];
+  const uint64_t gbase = (uint64_t)p.goff + (uint64_t)tile * 128u;
+  const uint64_t g0 = gbase >> 6;
+  const int G = (int)(((gbase + 127u) >> 6) - g0) + 1;
+  if (ACT == MDR_ACT_RANDOM) win_random_stage(p.seed, g0, G, tkp, nt, s_rw[wv]);
+  __syncthreads();
+  win_count<ACT>(p, wa, wb, cls0, cls1, v0, v1, i0, (uint64_t)p.goff + i0, s_rw[wv], G, g0, 0, nt, action,
+                 act_stride, s_hist);
+  __syncthreads();
+  win_flush(p, nt, s_hist, slab);
+}
+
+// One window of K ticks.  counts: slabs of ticks 0..K-1 (complete, global); la_K > 0: run the
+// FSM on through the next la_K ticks (tkp[K..K+la_K), action rows K..) and accumulate their ON
+// counts into next_slab; block 0 zeroes zero_slab (zero_len u64) for the launch after next.
+template <int ACT>
+__global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* __restrict__ action,
+                                                     int64_t act_stride, const TickArgs* __restrict__ tkp, int K,
+                                                     int la_K, const unsigned long long* __restrict__ counts,
+                                                     double* __restrict__ reward, int64_t rew_stride,
+                                                     double* p_out, unsigned long long* next_slab,
+                                                     unsigned long long* zero_slab, int zero_len) {
+  __shared__ uint2 s_rw[4][3 * 2 * kWinMax];
+  __shared__ unsigned s_hist[kWinMax * kWinCap];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  for (int j = tid; j < kWinMax * kWinCap; j += blockDim.x) s_hist[j] = 0;
+  if (zero_slab && blockIdx.x == 0)
+    for (int j = tid; j < zero_len; j += blockDim.x) zero_slab[j] = 0ull;
+  const uint32_t n = (uint32_t)p.n;
+  const uint32_t tile = blockIdx.x * 4u + (uint32_t)wv;
+  const uint32_t i0 = tile * 128u + (uint32_t)lane * 2u;
+  const bool v0 = i0 < n, v1 = i0 + 1u < n;
+  const bool full = (tile + 1u) * 128u <= n;  // wave-uniform
+
+  // ---- state + parameters, once per window
+  Tile2 t;
+  load_tile2<false>(p, nullptr, i0, n, full, t);
+  const int cls0 = (int)(t.cls & 0xFF), cls1 = (int)((t.cls >> 8) & 0xFF);
+  double q_on[kWinCap];
+#pragma unroll
+  for (int k = 0; k < kWinCap; ++k) q_on[k] = p.q_on[k < p.n_cap ? k : 0];
+
+  // ---- per-tick signal penalty of the window, lane j <- tick j (rewards_calculator.py:183-203)
+  double sig_l = 0.0, P_l = 0.0;
+  if (lane < K) {
+    const unsigned long long* cj = counts + (size_t)lane * kCountShards * p.n_cap;
+    for (int k = 0; k < p.n_cap; ++k) {
+      unsigned long long c = 0;
+      for (int q = 0; q < kCountShards; ++q) c += cj[q * p.n_cap + k];
+      P_l += (double)c * p.p_on[k];
+    }
+    const double x = (P_l - tkp[lane].s_prev) / (double)p.n_global;
+    sig_l = p.alpha_sig * (x * x) / p.norm_sig;
+  }
+  const double P_last = readlane_f64(P_l, K - 1);
+  if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P_last;
+
+  // ---- random controller bits for the window + lookahead
+  const uint64_t gid0 = (uint64_t)p.goff + i0;
+  const uint64_t gbase = (uint64_t)p.goff + (uint64_t)tile * 128u;
+  const uint64_t g0 = gbase >> 6;
+  const int G = (int)(((gbase + 127u) >> 6) - g0) + 1;
+  if (ACT == MDR_ACT_RANDOM) win_random_stage(p.seed, g0, G, tkp, K + la_K, s_rw[wv]);
+  __syncthreads();  // LDS histogram zeroed, random words staged
+
+  const bool params_ok = !*p.params_bad && p.fast_tick_ok;
+  double T[2] = {t.T.x, t.T.y}, Tm[2] = {t.Tm.x, t.Tm.y};
+  const double ua[2] = {t.ua.x, t.ua.y}, hm[2] = {t.hm.x, t.hm.y}, tg[2] = {t.tg.x, t.tg.y};
+  const int cls[2] = {cls0, cls1};
+  uint32_t w[2] = {t.w.x, t.w.y};
+  double qc[2];
+  RcWin rw[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    qc[h] = q_on[0];
+#pragma unroll
+    for (int c = 1; c < kWinCap; ++c) qc[h] = cls[h] == c ? q_on[c] : qc[h];
+    if (params_ok) {
+      rw[h] = rc_window(ua[h], h ? t.ca.y : t.ca.x, h ? t.cm.y : t.cm.x, hm[h], (double)p.dt);
+    } else {  // IEEE division (identical bits; parameters outside the fast-division range)
+      rw[h].k = rc_coeffs_t<false>(ua[h], h ? t.ca.y : t.ca.x, h ? t.cm.y : t.cm.x, hm[h], (double)p.dt);
+      rw[h].rCa.nb = -(h ? t.ca.y : t.ca.x);
+      rw[h].rc.nb = -ua[h];
+      rw[h].rd.nb = -(rw[h].k.r2 - rw[h].k.r1);
+      rw[h].UaHm = ua[h] + hm[h];
+    }
+  }
+  const uint32_t o8 = i0 * 8u;
+  const bool vec_rew = full && (rew_stride & 1) == 0 && (((uintptr_t)reward) & 15u) == 0;
+
+  for (int j = 0; j < K; ++j) {
+    const TickArgs tk = tkp[j];
+    const double sig = readlane_f64(sig_l, j);
+    const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)j * act_stride : nullptr;
+    bool house_ok = fabs(T[0]) < 1048576.0 && fabs(Tm[0]) < 1048576.0 && fabs(T[1]) < 1048576.0 &&
+                    fabs(Tm[1]) < 1048576.0;
+    const bool fast = params_ok && fabs(tk.t_od_prev) < 1048576.0 && fabs(tk.solar) < 1099511627776.0 &&
+                      __all(house_ok);
+    double rwd[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const bool valid = h ? v1 : v0;
+      const bool a = valid && win_action<ACT>(s_rw[wv], G, g0, j, gid0 + h, arow, i0 + h);
+      w[h] = hvac_fsm(w[h], a, p.dt, p.L);
+      const double q = hv_on(w[h]) ? qc[h] : 0.0;
+      double Tn, Tmn;
+      if (fast) rc_apply_win<true>(T[h], Tm[h], ua[h], hm[h], rw[h], q, tk.solar, tk.t_od_prev, Tn, Tmn);
+      else rc_apply_win<false>(T[h], Tm[h], ua[h], hm[h], rw[h], q, tk.solar, tk.t_od_prev, Tn, Tmn);
+      T[h] = Tn;
+      Tm[h] = Tmn;
+      const double tpen = p.alpha_temp * deadband_l2(tg[h], p.deadband, Tn);
+      rwd[h] = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig);
+    }
+    double* rrow = reward + (int64_t)j * rew_stride;
+    if (vec_rew) sto(rrow, o8, make_double2(rwd[0], rwd[1]));
+    else {
+      if (v0) rrow[i0] = rwd[0];
+      if (v1) rrow[i0 + 1] = rwd[1];
+    }
+  }
+
+  // ---- state back, once per window
+  if (v1) {
+    sto(p.t_air, o8, make_double2(T[0], T[1]));
+    sto(p.t_mass, o8, make_double2(Tm[0], Tm[1]));
+    sto(p.hvac, i0 * 4u, make_uint2(w[0], w[1]));
+  } else if (v0) {
+    p.t_air[i0] = T[0]; p.t_mass[i0] = Tm[0]; p.hvac[i0] = w[0];
+  }
+
+  // ---- lookahead: ON counts of the next window's ticks
+  if (la_K > 0) {
+    win_count<ACT>(p, w[0], w[1], cls0, cls1, v0, v1, i0, gid0, s_rw[wv], G, g0, K, la_K,
+                   ACT == MDR_ACT_BUFFER ? action : nullptr, act_stride, s_hist);
+    __syncthreads();
+    win_flush(p, la_K, s_hist, next_slab);
+  }
+}
+
+#define MDR_INST_WIN(A)                                                                             \
+  template __global__ void k_step_window<A>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
+                                            const unsigned long long*, double*, int64_t, double*,      \
+                                            unsigned long long*, unsigned long long*, int);             \
+  template __global__ void k_count_window<A>(KParams, const uint8_t*, int64_t, const TickArgs*, int,    \
+                                             unsigned long long*);
+MDR_INST_WIN(MDR_ACT_RANDOM)
+MDR_INST_WIN(MDR_ACT_ALWAYS_ON)
+MDR_INST_WIN(MDR_ACT_BUFFER)
 
 #define MDR_INST_PIPE(T, A, LA)                                                                    \
   template __global__ void k_step_pipe<T, A, LA>(KParams, const uint8_t*, TickArgs, const TickArgs*, \

@@ -108,6 +108,7 @@ SIGNATURES = {
     "mdr_destroy": (I, [VP]),
     "mdr_bind": (I, [VP, P(mdr_soa)]),
     "mdr_params_changed": (I, [VP]),
+    "mdr_set_rollout_window": (I, [VP, I]),
     "mdr_populate": (I, [VP, P(mdr_pop_spec), VP]),
     "mdr_power_counts": (I, [VP, VP, I, U64, VP]),
     "mdr_counts_buffer": (I, [VP, P(VP), P(I)]),
@@ -115,14 +116,14 @@ SIGNATURES = {
     "mdr_penalty_partials": (I, [VP, VP]),
     "mdr_penalty_buffer": (I, [VP, P(VP)]),
     "mdr_reward_finalize": (I, [VP, P(mdr_tick), VP, VP]),
-    "mdr_rollout": (I, [VP, I, P(mdr_tick), VP, I64, I, VP, I64, VP, I, VP]),
+    "mdr_rollout": (I, [VP, I, VP, VP, I64, I, VP, I64, VP, I, VP]),  # ticks: const mdr_tick*
     "mdr_msg_width": (I, [P(mdr_obs_spec)]),
     "mdr_obs": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, VP, VP]),
     "mdr_halo_pack": (I, [VP, P(mdr_obs_spec), VP, VP]),
     "mdr_ctrl_greedy": (I, [VP, D, VP, VP]),
     "mdr_actor_load": (I, [VP, P(mdr_actor_spec), VP, VP, VP, VP, VP, VP, VP]),
     "mdr_actor_act": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, U64, VP, VP, VP, VP, I, VP]),
-    "mdr_actor_rollout": (I, [VP, I, P(mdr_tick), P(mdr_obs_scalars), P(mdr_obs_spec), VP, I64, VP, I64,
+    "mdr_actor_rollout": (I, [VP, I, VP, VP, P(mdr_obs_spec), VP, I64, VP, I64,
                               VP, I64, VP, I, VP]),
     "mdr_actor_profile": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, P(D), VP]),
     "mdr_interp_load": (I, [VP, P(mdr_interp_spec)]),
@@ -131,7 +132,7 @@ SIGNATURES = {
     "mdr_rccl_unique_id": (I, [VP]),
     "mdr_rccl_init": (I, [VP, VP, I, I]),
     "mdr_rccl_allreduce": (I, [VP, VP, I64, I, VP]),
-    "mdr_rollout_sharded": (I, [VP, I, P(mdr_tick), VP, I64, I, VP, I64, VP, VP]),
+    "mdr_rollout_sharded": (I, [VP, I, VP, VP, I64, I, VP, I64, VP, VP]),
     "mdr_rollout_sharded_mode": (I, [VP, P(I), P(D), P(D)]),
     "mdr_probe_stream": (I, [VP, VP, VP]),
     "mdr_div_check": (I, [VP, VP, I64, VP, VP]),

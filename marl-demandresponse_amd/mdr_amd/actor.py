@@ -138,8 +138,11 @@ class DeviceActor:
             k = len(ticks)
             # obs before tick t: signal / OD temperature after tick t-1 (= tick t's s_prev,
             # t_od_prev), solar gain of tick t-1's datetime
-            osc = [L.mdr_obs_scalars(0.0, t.s_prev, solar0 if i == 0 else ticks[i - 1].solar, t.t_od_prev)
-                   for i, t in enumerate(ticks)]
+            osc = np.zeros((k, 4), np.float64)  # mdr_obs_scalars rows (p unused: p_dev)
+            osc[:, 1] = ticks.s_prev
+            osc[0, 2] = solar0
+            osc[1:, 2] = ticks.solar[:-1]
+            osc[:, 3] = ticks.t_od_prev
             sl = (lambda x, st: None if x is None else (x[done:done + k] if st else x))
             g = use_graph and (k == n_ticks or not (rs or as_ or ps))
             sh.actor_rollout(ticks, osc, spec, sl(actions, as_), as_, sl(probs, ps), ps, sl(rewards, rs), rs, g)

@@ -68,9 +68,8 @@ class RcclComm:
         L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, L.ptr(t), t.numel(), 1, shard.stream()), "allreduce sum")
 
     def rollout(self, shard, ticks, actions, mode, rewards, rew_stride) -> None:
-        arr = (L.mdr_tick * len(ticks))(*ticks)
         n = shard.n
-        L.check(shard.lib.mdr_rollout_sharded(shard.ctx, len(ticks), arr, L.ptr(actions),
+        L.check(shard.lib.mdr_rollout_sharded(shard.ctx, len(ticks), ticks.ptr(), L.ptr(actions),
                                               n if actions is not None else 0, mode, L.ptr(rewards),
                                               rew_stride, L.ptr(shard.p_dev), shard.stream()),
                 "mdr_rollout_sharded")
@@ -161,7 +160,8 @@ class TorchComm(RcclComm):
         return {"mode": "torch.distributed per-step"}
 
     def rollout(self, shard, ticks, actions, mode, rewards, rew_stride) -> None:
-        for t, tk in enumerate(ticks):
+        for t in range(len(ticks)):
+            tk = ticks.struct(t)
             a = actions[t] if actions is not None else None
             shard.power_counts(a, mode, tk.tick)
             self.allreduce_counts(shard)

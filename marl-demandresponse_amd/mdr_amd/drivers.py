@@ -14,7 +14,7 @@ values are bit-identical (pinned by tests/test_oracle_golden.py and tests/test_h
 from __future__ import annotations
 
 import datetime as _dt
-import math
+import functools
 import random as _random
 
 import numpy as np
@@ -34,12 +34,20 @@ def _powf(v: float, k: int) -> float:
 
 
 def solar_gain(t: _dt.datetime, window_area: float, shading_coeff: float) -> float:
-    """Solar heat gain through the windows (W) at time t; identical for every house."""
-    x = t.hour + t.minute / 60 - 7.5
+    """Solar heat gain through the windows (W) at time t; identical for every house.
+
+    It depends on (month, day, hour, minute) only, so a tick reuses the value of the previous
+    ticks in the same minute (memoised: the same expression evaluated once, bit-identical)."""
+    return _solar_memo(t.month, t.day, t.hour, t.minute, window_area, shading_coeff)
+
+
+@functools.lru_cache(maxsize=1 << 16)
+def _solar_memo(month: int, day: int, hour: int, minute: int, window_area: float, shading_coeff: float):
+    x = hour + minute / 60 - 7.5
     if x < 0 or x > 10:
         load = 0
     else:
-        y = t.month + t.day / 30 - 1
+        y = month + day / 30 - 1
         load = SOLAR_TERMS[0][0]
         for c, i, j in SOLAR_TERMS[1:]:
             if i and j:
@@ -52,14 +60,20 @@ def solar_gain(t: _dt.datetime, window_area: float, shading_coeff: float) -> flo
 
 
 def od_temp(t: _dt.datetime, temp_prop, rng=_random):
-    """Sinusoidal daily outdoor temperature + one gauss(0, temp_std) draw (consumes the RNG)."""
-    amplitude = (temp_prop.day_temp - temp_prop.night_temp) / 2.0
-    bias = (temp_prop.day_temp + temp_prop.night_temp) / 2.0
-    delay = -6.0 + temp_prop.phase
-    time_day = t.hour + t.minute / 60.0
-    temperature = amplitude * np.sin(2 * np.pi * (time_day + delay) / 24.0) + bias
+    """Sinusoidal daily outdoor temperature + one gauss(0, temp_std) draw (consumes the RNG).
+    The deterministic part depends on (hour, minute) only and is memoised."""
+    temperature = _od_det(t.hour, t.minute, temp_prop.day_temp, temp_prop.night_temp, temp_prop.phase)
     temperature += rng.gauss(0, temp_prop.temp_std)
     return temperature
+
+
+@functools.lru_cache(maxsize=1 << 12)
+def _od_det(hour: int, minute: int, day_temp, night_temp, phase):
+    amplitude = (day_temp - night_temp) / 2.0
+    bias = (day_temp + night_temp) / 2.0
+    delay = -6.0 + phase
+    time_day = hour + minute / 60.0
+    return amplitude * np.sin(2 * np.pi * (time_day + delay) / 24.0) + bias
 
 
 def deadband_l2(target, deadband, value):
@@ -138,6 +152,7 @@ class GridSignal:
         grid_props.artificial_ratio = grid_props.artificial_ratio * \
             grid_props.artificial_signal_ratio_range ** (rng.random() * 2 - 1)
         self.current_signal = 0.0
+        self._memo = {}
         self.signal = Signal(grid_props.signal_properties, nb_agents, rng)
         self.signal_fn = signal_fn
         bp = grid_props.base_power_props
@@ -166,9 +181,22 @@ class GridSignal:
 
     def step(self, t: _dt.datetime, od=None, dt_seconds: int = 0):
         base = self.base_power(t, od, dt_seconds)
+        key = None
+        if self.signal_fn is None and self.signal.mode != "perlin":
+            # flat / sinusoidals / regular_steps depend on (base, seconds of day) only: memoised
+            key = (base, _seconds_of_day(t) if self.signal.mode != "flat" else 0,
+                   self.gp.artificial_ratio, self.max_power)
+            hit = self._memo.get(key)
+            if hit is not None:
+                self.current_signal = hit
+                return hit
         s = self.signal_fn(base, t) if self.signal_fn is not None else self.signal(base, t)
         s = s * self.gp.artificial_ratio
         self.current_signal = np.minimum(s, self.max_power)
+        if key is not None:
+            if len(self._memo) > (1 << 17):
+                self._memo.clear()
+            self._memo[key] = self.current_signal
         return self.current_signal
 
     def get_obs(self):

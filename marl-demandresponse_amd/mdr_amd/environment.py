@@ -32,6 +32,50 @@ ACTION_MODES = {"buffer": L.ACT_BUFFER, "random": L.ACT_RANDOM, "always_on": L.A
                 "bangbang": L.ACT_BANGBANG, "deadband_bangbang": L.ACT_DEADBAND_BANGBANG}
 
 
+class TickWindow:
+    """The per-tick drivers of a rollout window: one C-contiguous float64 [n, 4] array in the
+    mdr_tick layout (t_od_prev, solar, s_prev as f64; tick as u64 bits), so the C ABI reads it in
+    place — no per-tick Python objects."""
+
+    __slots__ = ("a",)
+
+    def __init__(self, a: np.ndarray):
+        assert a.dtype == np.float64 and a.ndim == 2 and a.shape[1] == 4 and a.flags.c_contiguous
+        self.a = a
+
+    def __len__(self) -> int:
+        return self.a.shape[0]
+
+    @property
+    def t_od_prev(self) -> np.ndarray:
+        return self.a[:, 0]
+
+    @property
+    def solar(self) -> np.ndarray:
+        return self.a[:, 1]
+
+    @property
+    def s_prev(self) -> np.ndarray:
+        return self.a[:, 2]
+
+    @property
+    def tick(self) -> np.ndarray:
+        return self.a[:, 3].view(np.uint64)
+
+    def ptr(self) -> int:
+        """Host address of the mdr_tick[n] array (valid while this object lives)."""
+        return self.a.ctypes.data
+
+    def struct(self, i: int) -> L.mdr_tick:
+        r = self.a[i]
+        return L.mdr_tick(float(r[0]), float(r[1]), float(r[2]), int(self.tick[i]))
+
+    def __getitem__(self, sl: slice) -> "TickWindow":
+        if not isinstance(sl, slice):
+            raise TypeError("TickWindow slices only (use .struct(i) for one tick)")
+        return TickWindow(np.ascontiguousarray(self.a[sl]))
+
+
 def shard_range(n: int, rank: int, world: int):
     """Contiguous house range of a rank (SURVEY §8(e)): [r*n//w, (r+1)*n//w)."""
     lo = rank * n // world
@@ -184,10 +228,12 @@ class Environment:
         return L.mdr_tick(float(self._tod_prev), float(self._solar), float(self._s_prev), self._tick)
 
     def step_tensor(self, actions=None, action_mode: str = "buffer", lookahead: Optional[str] = None,
-                    ctrl: Optional[str] = None, ctrl_out=None):
+                    ctrl: Optional[str] = None, ctrl_out=None, rewards=None):
         """One tick on device.  ``actions``: uint8/bool tensor [n_local] on the shard's device
         (``action_mode='buffer'``) or None with an in-kernel source ('random', 'always_on',
-        'bangbang', 'deadband_bangbang').  Returns the device reward tensor (float64 [n_local]).
+        'bangbang', 'deadband_bangbang').  Returns the device reward tensor (float64 [n_local]):
+        ``rewards`` if given (a contiguous float64 [n_local] device tensor), else the shard's
+        reward buffer (overwritten by the next tick).
 
         ``lookahead`` names the NEXT tick's in-kernel action source: its cluster-power counts
         are computed by this launch, so the next tick is a single kernel.
@@ -222,12 +268,15 @@ class Environment:
             self._comm.allreduce_counts(sh)
         la = ACTION_MODES[lookahead] if lookahead else 0
         cm = {None: 0, "bangbang": L.CTRL_BANGBANG, "deadband_bangbang": L.CTRL_DEADBAND_BANGBANG}[ctrl]
-        reward = sh.step(actions, mode, tick, lookahead=la, ctrl=cm, ctrl_out=ctrl_out)
+        if rewards is not None and (rewards.dtype != sh.reward.dtype or rewards.numel() != self._n_local
+                                    or not rewards.is_contiguous()):
+            raise ValueError(f"rewards must be a contiguous float64 tensor of {self._n_local} elements")
+        reward = sh.step(actions, mode, tick, lookahead=la, ctrl=cm, ctrl_out=ctrl_out, reward=rewards)
         if sh.penalty_mode != 0:
             sh.penalty_partials()
             if self._comm is not None:
                 self._comm.allreduce_penalty(sh)
-            sh.reward_finalize(tick)
+            sh.reward_finalize(tick, reward=reward)
         self._counts_ready = la
         self._P_dev_valid = True
         cp = p.cluster_prop
@@ -278,10 +327,11 @@ class Environment:
         return self.get_obs(), rewards
 
     # ------------------------------------------------------------------ many ticks per call
-    def driver_window(self, n_ticks: int):
+    def driver_window(self, n_ticks: int) -> "TickWindow":
         """Advance the host drivers up to n_ticks ahead (same RNG order as n calls of step) and
-        return the per-tick ``mdr_tick`` list for a rollout.  Valid when nothing else draws from
-        the RNG between ticks (random_sample comm mode draws, so it is excluded).
+        return the per-tick drivers of a rollout as a ``TickWindow`` (the mdr_tick array the C
+        ABI reads).  Valid when nothing else draws from the RNG between ticks (random_sample comm
+        mode draws, so it is excluded).
 
         In interpolation base-power mode the window stops after a tick whose grid step reads the
         post-step house state: run the returned ticks on the device, then ``finish_grid_step()``."""
@@ -292,20 +342,37 @@ class Environment:
         p = self.init_props
         hp = p.cluster_prop.house_prop
         dts = p.time_step.seconds
-        ticks = []
+        step = p.time_step
+        solar_on, wa, shc = hp.solar_gain, hp.window_area, hp.shading_coeff
+        tp, rng, grid = p.temp_prop, self.rng, self.power_grid
+        date, tod, tick0 = self.date_time, self.current_od_temp, self._tick
+        sol, s_prev = self._solar, self.power_grid.current_signal
+        tods, sols, sprevs = [], [], []
         for _ in range(n_ticks):
-            self.date_time = self.date_time + p.time_step
-            self._solar = solar_gain(self.date_time, hp.window_area, hp.shading_coeff) if hp.solar_gain else 0.0
-            self._tod_prev = self.current_od_temp
-            self._s_prev = self.power_grid.current_signal
-            ticks.append(self._tick_args())
-            self.current_od_temp = od_temp(self.date_time, p.temp_prop, self.rng)
-            self._tick += 1
-            if self.power_grid.needs_state(dts):
+            # environment.py:86-106: time advances, the cluster steps with the previous OD
+            # temperature and the new datetime's solar gain, then a new OD temperature (1 gauss)
+            # and the new signal; the reward of the tick uses the previous signal
+            date = date + step
+            sol = solar_gain(date, wa, shc) if solar_on else 0.0
+            s_prev = grid.current_signal
+            tods.append(tod)
+            sols.append(sol)
+            sprevs.append(s_prev)
+            tod = od_temp(date, tp, rng)
+            if grid.needs_state(dts):
                 self._grid_pending = True
                 break
-            self.power_grid.step(self.date_time, self.current_od_temp, dts)
-        return ticks
+            grid.step(date, tod, dts)
+        k = len(tods)
+        buf = np.empty((k, 4), np.float64)
+        buf[:, 0] = tods
+        buf[:, 1] = sols
+        buf[:, 2] = sprevs
+        buf[:, 3].view(np.uint64)[:] = np.arange(tick0, tick0 + k, dtype=np.uint64)
+        self.date_time, self._solar, self._tick, self.current_od_temp = date, sol, tick0 + k, tod
+        if k:
+            self._tod_prev, self._s_prev = tods[-1], s_prev
+        return TickWindow(buf)
 
     def finish_grid_step(self):
         """The grid step driver_window deferred (interpolation mode), once its ticks have run."""

@@ -115,6 +115,10 @@ class HipShard:
         self.hvac.copy_(t.from_numpy(np.ascontiguousarray(hvac_words, np.int32)).to(dev))
         self.params_changed()
 
+    def set_rollout_window(self, ticks: int):
+        """Ticks per temporally blocked rollout launch (0: one launch per tick), mdr_set_rollout_window."""
+        L.check(self.lib.mdr_set_rollout_window(self.ctx, int(ticks)), "mdr_set_rollout_window")
+
     def params_changed(self):
         L.check(self.lib.mdr_params_changed(self.ctx), "mdr_params_changed")
 
@@ -156,9 +160,9 @@ class HipShard:
                 "mdr_reward_finalize")
 
     def rollout(self, ticks, action, act_stride, mode, reward, rew_stride, use_graph=True):
-        """Many ticks in one C call.  Graph capture needs a non-default stream: the rollout runs
-        on the shard's own stream, ordered after / before the caller's current stream."""
-        arr = (L.mdr_tick * len(ticks))(*ticks)
+        """Many ticks in one C call (``ticks``: a TickWindow).  Graph capture needs a non-default
+        stream: the rollout runs on the shard's own stream, ordered after / before the caller's
+        current stream."""
         torch = self.torch
         cur = torch.cuda.current_stream(self.device)
         if use_graph:
@@ -167,7 +171,7 @@ class HipShard:
             handle = s.cuda_stream
         else:
             handle = cur.cuda_stream
-        L.check(self.lib.mdr_rollout(self.ctx, len(ticks), arr, L.ptr(action), act_stride, mode,
+        L.check(self.lib.mdr_rollout(self.ctx, len(ticks), ticks.ptr(), L.ptr(action), act_stride, mode,
                                      L.ptr(reward), rew_stride, L.ptr(self.p_dev), int(use_graph), handle),
                 "mdr_rollout")
         if use_graph:
@@ -205,10 +209,11 @@ class HipShard:
 
     def actor_rollout(self, ticks, obs_sc, spec, action, act_stride, prob, prob_stride, reward, rew_stride,
                       use_graph=True):
-        """n ticks of actor -> step in one C call (graph-captured on the shard's side stream)."""
+        """n ticks of actor -> step in one C call (graph-captured on the shard's side stream).
+        ``ticks``: TickWindow; ``obs_sc``: float64 [n, 4] array in the mdr_obs_scalars layout."""
         n = len(ticks)
-        arr = (L.mdr_tick * n)(*ticks)
-        sca = (L.mdr_obs_scalars * n)(*obs_sc)
+        obs_sc = np.ascontiguousarray(obs_sc, np.float64)
+        assert obs_sc.shape == (n, 4)
         torch = self.torch
         cur = torch.cuda.current_stream(self.device)
         if use_graph:
@@ -217,7 +222,7 @@ class HipShard:
             handle = s.cuda_stream
         else:
             handle = cur.cuda_stream
-        L.check(self.lib.mdr_actor_rollout(self.ctx, n, arr, sca, C.byref(spec), L.ptr(action), act_stride,
+        L.check(self.lib.mdr_actor_rollout(self.ctx, n, ticks.ptr(), obs_sc.ctypes.data, C.byref(spec), L.ptr(action), act_stride,
                                            L.ptr(prob), prob_stride, L.ptr(reward), rew_stride, L.ptr(self.p_dev),
                                            int(use_graph), handle), "mdr_actor_rollout")
         if use_graph:

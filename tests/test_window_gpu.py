@@ -1,0 +1,118 @@
+"""Temporally blocked rollouts (k_step_window: K ticks per launch, the FSM run ahead for each
+tick's cluster power) against the one-tick path and against the oracle.
+
+The one-tick kernels are themselves pinned to the reference goldens (test_env_parity_gpu.py), so
+bit-identity to them carries the reference parity over; the oracle check below replays the exact
+in-kernel random actions (tests/philox_np.py) so the benched action source is oracle-checked.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+import philox_np as PX
+from oracle import env_np as O
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def torch_gpu():
+    import torch
+
+    assert torch.cuda.is_available(), "GPU tests need an MI355X"
+    return torch
+
+
+def _pair(n, seed=3, pop="synthetic", extra=None):
+    from mdr_amd.environment import Environment
+
+    ov = {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals"}
+    ov.update(extra or {})
+    props = gu.props_from_overrides(ov)
+    e1 = Environment(props, rng=random.Random(seed), population=pop, seed=77)
+    e2 = Environment(props, rng=random.Random(seed), population=pop, seed=77)
+    return e1, e2
+
+
+def _same_state(torch, e1, e2):
+    torch.cuda.synchronize()
+    s1, s2 = e1.shard.host_state(), e2.shard.host_state()
+    for k in s1:
+        np.testing.assert_array_equal(s1[k], s2[k], err_msg=k)
+    assert e1._cluster_power() == e2._cluster_power()
+
+
+@pytest.mark.parametrize("n,ticks,win", [(1, 5, 32), (2, 33, 32), (257, 40, 7), (4099, 65, 32),
+                                         (20011, 64, 16), (131072, 50, 32)])
+@pytest.mark.parametrize("mode", ["random", "always_on", "buffer"])
+def test_window_equals_one_tick(torch_gpu, n, ticks, win, mode):
+    """Windowed rollout == the one-launch-per-tick rollout, bit for bit (rewards, state, P)."""
+    torch = torch_gpu
+    e1, e2 = _pair(n)
+    e1.shard.set_rollout_window(win)
+    e2.shard.set_rollout_window(0)
+    acts = None
+    if mode == "buffer":
+        g = torch.Generator(device="cuda").manual_seed(n)
+        acts = (torch.rand((ticks, n), device="cuda", generator=g) < 0.5).to(torch.uint8)
+    for rep in range(2):  # second call replays the cached graphs
+        r1 = e1.rollout(ticks, actions=acts, action_mode=mode)
+        r2 = e2.rollout(ticks, actions=acts, action_mode=mode)
+        np.testing.assert_array_equal(r1.cpu().numpy(), r2.cpu().numpy())
+        _same_state(torch, e1, e2)
+
+
+def test_window_one_row_rewards(torch_gpu):
+    """rewards given as ONE row (every tick overwrites it): the last tick's rewards remain."""
+    torch = torch_gpu
+    e1, e2 = _pair(5001)
+    row = torch.empty(5001, dtype=torch.float64, device="cuda")
+    e1.rollout(45, action_mode="random", rewards=row)
+    full = e2.rollout(45, action_mode="random")
+    np.testing.assert_array_equal(row.cpu().numpy(), full[-1].cpu().numpy())
+    _same_state(torch, e1, e2)
+
+
+def test_window_then_steps(torch_gpu):
+    """A windowed rollout leaves the env where step_tensor continues from (counts, ticks, P)."""
+    torch = torch_gpu
+    e1, e2 = _pair(3000)
+    e1.rollout(37, action_mode="random")
+    for _ in range(37):
+        e2.step_tensor(None, action_mode="random")
+    r1 = [e1.step_tensor(None, action_mode="random").clone() for _ in range(5)]
+    r2 = [e2.step_tensor(None, action_mode="random").clone() for _ in range(5)]
+    np.testing.assert_array_equal(torch.stack(r1).cpu().numpy(), torch.stack(r2).cpu().numpy())
+    _same_state(torch, e1, e2)
+
+
+def test_random_rollout_vs_oracle_replayed_actions(torch_gpu):
+    """rollout(action_mode='random') at 65,536 houses x 50 ticks == the oracle stepping the SAME
+    Philox actions (restated in NumPy): on/lock/sso exact, temperatures rtol 1e-10, rewards, P."""
+    from mdr_amd.environment import Environment
+
+    n, T, seed = 65536, 50, 4
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env = Environment(props, rng=random.Random(seed), seed=1234)
+    ora = O.OracleEnv(props, random.Random(seed))
+    tick0 = env._tick
+    R = env.rollout(T, action_mode="random").cpu().numpy()
+    gids = np.arange(n, dtype=np.uint64)
+    ones = 0
+    for t in range(T):
+        a = PX.random_actions(1234, gids, tick0 + t)
+        ones += int(a.sum())
+        o, rr = ora.step(a)
+        np.testing.assert_allclose(R[t], rr, rtol=1e-9, atol=1e-12, err_msg=f"reward t={t}")
+    st = env.shard.host_state()
+    np.testing.assert_array_equal(st["on"], o["on"])
+    np.testing.assert_array_equal(st["lock"], o["lock"])
+    np.testing.assert_array_equal(st["sso"], o["sso"])
+    np.testing.assert_allclose(st["T"], o["T"], rtol=1e-10, atol=0)
+    np.testing.assert_allclose(st["Tm"], o["Tm"], rtol=1e-10, atol=0)
+    assert env.cluster.current_power_consumption == o["P"]
+    # Bernoulli(0.5): 3.3M draws within 4 sigma
+    assert abs(ones / (n * T) - 0.5) < 4 * 0.5 / np.sqrt(n * T)

@@ -1,8 +1,13 @@
-"""Kernel A/B microbenchmark for k_step (one process, interleaved rounds; cdna guide §5.4 r24).
+"""Kernel A/B microbenchmark for the step kernels (one process, interleaved rounds; cdna guide §5.4).
 
-    python tools/kbench.py [--houses 1048576,4194304] [--launches 200] [--rounds 5]
-Prints per-launch microseconds and algorithmic GB/s (99 B/house-step) per variant, plus the
-memory-floor probe (same loads/stores, no arithmetic).
+    python tools/kbench.py [--houses 1048576,4194304] [--ticks 128] [--rounds 5] [--variants w32,w0,probe]
+
+Variants: wK = temporally blocked rollout, K ticks per k_step_window launch; w0 = one launch per
+tick (k_step_pipe / k_step_t, MDR_TPW / MDR_HPT / MDR_FASTDIV still select among those); probe =
+the memory-floor probe of the one-tick kernel (same loads/stores, no arithmetic).  Every tick's
+reward row is kept ([ticks, n] float64), so reward writes really go to HBM.  Prints per-tick
+microseconds, house-steps/s and algorithmic GB/s (window: SURVEY §8(d) field sizes, state and
+parameters once per window + 8 B reward per tick; one-tick: 99 B/house-step).
 """
 import argparse
 import os
@@ -16,13 +21,13 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "marl-demandresponse_amd")]
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--houses", default="1048576,4194304,16777216")
-    ap.add_argument("--launches", type=int, default=200)
+    ap.add_argument("--ticks", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="hpt2,fast2,fcoef2,probe")
+    ap.add_argument("--variants", default="w32,w16,w0,probe")
     a = ap.parse_args()
     import torch
 
-    from bench import env_props
+    from bench import BYTES_PER_HOUSE_STEP, env_props, window_bytes
     from mdr_amd import _lib as L
     from mdr_amd.environment import Environment
 
@@ -30,19 +35,16 @@ def main():
     for n in [int(x) for x in a.houses.split(",")]:
         envs = {}
         for v in a.variants.split(","):
-            os.environ["MDR_HPT"] = "1" if v.endswith("1") else "2"
-            os.environ["MDR_VARIANT"] = "coef" if "coef" in v else "raw"
-            os.environ["MDR_FASTDIV"] = "1" if v.startswith("f") else "0"
-            os.environ["MDR_GRID_OVERSUB"] = v.split("g")[-1] if "g" in v[4:] else "1"
-            os.environ["MDR_TPW"] = v.split("t")[-1] if "t" in v[4:] else "0"  # fast2t4: k_step_pipe, 4 tiles/wave
-            envs[v] = Environment(env_props(n), device="cuda:0", rng=random.Random(1),
-                                  population="synthetic", seed=5)
-            rews = torch.empty(n, dtype=torch.float64, device="cuda:0")
+            env = Environment(env_props(n), device="cuda:0", rng=random.Random(1), population="synthetic", seed=5)
+            sh = env.shard
+            if v.startswith("w"):
+                sh.set_rollout_window(int(v[1:]))
+            env._kb_rew = torch.empty((a.ticks, n), dtype=torch.float64, device="cuda:0")
             # one driver window replayed every round: the events time the graph alone (no host drivers)
-            envs[v]._kb_ticks = envs[v].driver_window(a.launches)
-            sh = envs[v].shard
-            sh.rollout(envs[v]._kb_ticks, None, 0, L.ACT_RANDOM, rews, 0, True)  # captures the graph
-            envs[v]._kb_rew = rews
+            env._kb_ticks = env.driver_window(a.ticks)
+            if v != "probe":
+                sh.rollout(env._kb_ticks, None, 0, L.ACT_RANDOM, env._kb_rew, n, True)  # captures the graph
+            envs[v] = env
         torch.cuda.synchronize()
         for r in range(a.rounds):
             for v, env in envs.items():
@@ -50,24 +52,30 @@ def main():
                 sh = env.shard
                 if v == "probe":
                     e0.record()
-                    for _ in range(a.launches):
-                        L.check(sh.lib.mdr_probe_stream(sh.ctx, L.ptr(sh.reward), sh.stream()))
+                    for t in range(a.ticks):
+                        L.check(sh.lib.mdr_probe_stream(sh.ctx, L.ptr(env._kb_rew[t]), sh.stream()))
                     e1.record()
                 else:
                     torch.cuda.synchronize()
                     ls = sh.launch_stream(True)
-                    sh.rollout(env._kb_ticks, None, 0, L.ACT_RANDOM, env._kb_rew, 0, True)  # stage ticks
                     e0.record(ls)
-                    sh.rollout(env._kb_ticks, None, 0, L.ACT_RANDOM, env._kb_rew, 0, True)
+                    sh.rollout(env._kb_ticks, None, 0, L.ACT_RANDOM, env._kb_rew, n, True)
                     e1.record(ls)
                 e1.synchronize()
-                us = e0.elapsed_time(e1) * 1e3 / a.launches
+                us = e0.elapsed_time(e1) * 1e3 / a.ticks
                 res.setdefault((n, v), []).append(us)
         for v in envs:
             ts = sorted(res[(n, v)])
             med = ts[len(ts) // 2]
-            print(f"n={n:>9} {v:>6}: {med:8.2f} us/launch (min {ts[0]:.2f})  "
-                  f"{99 * n / med / 1e3:8.1f} GB/s algorithmic  {n / med * 1e6:.3e} house-steps/s", flush=True)
+            if v.startswith("w") and int(v[1:]) > 0:
+                k = int(v[1:])
+                launches = -(-a.ticks // k)
+                kk = a.ticks // launches
+                gbs = window_bytes(n, kk, "random") / (med * kk) / 1e3
+            else:
+                gbs = BYTES_PER_HOUSE_STEP * n / med / 1e3
+            print(f"n={n:>9} {v:>6}: {med:8.2f} us/tick (min {ts[0]:.2f})  {gbs:8.1f} GB/s algorithmic  "
+                  f"{n / med * 1e6:.3e} house-steps/s", flush=True)
         del envs
         torch.cuda.empty_cache()
 
