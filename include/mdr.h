@@ -141,7 +141,7 @@ int mdr_params_changed(mdr_ctx* ctx);
 /* Synthetic population drawn on device from Philox4x32-10(seed, global house id): the reference
  * noise model (building.py:224-267, hvac.py:66-70: target = target_temp + |N(0, std_target)|,
  * Ua = Tri(lo, hi, 1) (the reference ASSIGNS the factor), Cm/Ca/Hm = cfg * Tri(lo, hi, 1), cap =
- * uniform over cap_table) with a counter-based RNG instead of MT19937, so a population is
+ * a uniform entry of cooling_capacity_list) with a counter-based RNG instead of MT19937, so a population is
  * identical for any sharding.  Initial state as Building.reset/HVAC.reset: T = init temps, on,
  * no lockout, sso = 0.  Writes every bound array. */
 typedef struct mdr_pop_spec {
@@ -149,6 +149,10 @@ typedef struct mdr_pop_spec {
   double thermo_lo, thermo_hi;      /* noise_prop.factor_thermo_low / _high */
   double ca, cm, hm;                /* house_prop.Ca, Cm, Hm */
   double init_air, init_mass;       /* house_prop.init_air_temp, init_mass_temp */
+  int32_t n_draw;                   /* cap drawn uniformly over n_draw list entries (random.choices
+                                       of noise_prop.cooling_capacity_list, hvac.py:68-70);
+                                       0 = uniform over the whole cap_table */
+  uint8_t draw_idx[MDR_MAX_CAP];    /* cap_table index of each list entry */
 } mdr_pop_spec;
 int mdr_populate(mdr_ctx* ctx, const mdr_pop_spec* spec, void* stream);
 

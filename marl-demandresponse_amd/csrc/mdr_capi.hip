@@ -415,8 +415,12 @@ int mdr_bind(mdr_ctx* c, const mdr_soa* s) {
 int mdr_populate(mdr_ctx* c, const mdr_pop_spec* sp, void* stream) {
   if (!c || !sp) return fail(MDR_EARG, "mdr_populate: null argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_populate: context not bound");
+  if (sp->n_draw < 0 || sp->n_draw > MDR_MAX_CAP) return fail(MDR_EARG, "mdr_populate: n_draw out of range");
+  for (int k = 0; k < sp->n_draw; ++k)
+    if (sp->draw_idx[k] >= c->cfg.n_cap) return fail(MDR_EARG, "mdr_populate: draw_idx outside the cap table");
   PopArgs a{sp->target_temp, sp->std_target, sp->thermo_lo, sp->thermo_hi, sp->ca, sp->cm, sp->hm,
-            sp->init_air, sp->init_mass};
+            sp->init_air, sp->init_mass, sp->n_draw, {}};
+  memcpy(a.draw_idx, sp->draw_idx, sizeof(a.draw_idx));
   hipLaunchKernelGGL(k_populate, dim3(blocks(c->kp.n, 256)), dim3(256), 0, S(stream), c->kp, a);
   LAUNCH_CHECK("k_populate");
   c->counts_ready = false;

@@ -56,6 +56,8 @@ static_assert(sizeof(TickArgs) == sizeof(Rec32), "TickArgs is staged as a 32-byt
 
 struct PopArgs {
   double target_temp, std_target, lo, hi, ca0, cm0, hm0, init_air, init_mass;
+  int n_draw;                     // capacity drawn over n_draw list entries (0: all n_cap)
+  uint8_t draw_idx[MDR_MAX_CAP];  // table index of each list entry
 };
 
 struct ObsArgs {

@@ -972,7 +972,10 @@ __global__ void __launch_bounds__(256) k_populate(KParams p, PopArgs a) {
   const_cast<double*>(p.cm)[i] = a.cm0 * triangular(u01(r0.w), a.lo, a.hi, 1.0);
   const_cast<double*>(p.ca)[i] = a.ca0 * triangular(u01(r1.x), a.lo, a.hi, 1.0);
   const_cast<double*>(p.hm)[i] = a.hm0 * triangular(u01(r1.y), a.lo, a.hi, 1.0);
-  const_cast<uint8_t*>(p.cap_idx)[i] = (uint8_t)(((uint64_t)r1.z * (uint64_t)p.n_cap) >> 32);
+  if (a.n_draw > 0)  // random.choices(cooling_capacity_list): a uniform list entry
+    const_cast<uint8_t*>(p.cap_idx)[i] = a.draw_idx[((uint64_t)r1.z * (uint64_t)a.n_draw) >> 32];
+  else
+    const_cast<uint8_t*>(p.cap_idx)[i] = (uint8_t)(((uint64_t)r1.z * (uint64_t)p.n_cap) >> 32);
   p.t_air[i] = a.init_air;
   p.t_mass[i] = a.init_mass;
   p.hvac[i] = kOnBit;

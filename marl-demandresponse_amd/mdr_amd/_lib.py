@@ -59,7 +59,7 @@ class mdr_tick(C.Structure):
 class mdr_pop_spec(C.Structure):
     _fields_ = [(k, C.c_double) for k in
                 ("target_temp", "std_target", "thermo_lo", "thermo_hi", "ca", "cm", "hm",
-                 "init_air", "init_mass")]
+                 "init_air", "init_mass")] + [("n_draw", C.c_int32), ("draw_idx", C.c_uint8 * MAX_CAP)]
 
 
 class mdr_obs_spec(C.Structure):

@@ -33,12 +33,10 @@ class RcclComm:
         self.dist = dist
         self.rank = dist.get_rank()
         self.world = dist.get_world_size()
-        self._attached = set()
-
     def attach(self, shard) -> None:
         import torch
 
-        if id(shard) in self._attached:
+        if getattr(shard, "_rccl_ready", False):  # (on the shard: a new shard may reuse a freed id)
             return
         lib = shard.lib
         uid = torch.zeros(128, dtype=torch.uint8)
@@ -51,7 +49,7 @@ class RcclComm:
         host = bytes(dev_uid.cpu().tolist())
         arr = (C.c_uint8 * 128).from_buffer_copy(host)
         L.check(lib.mdr_rccl_init(shard.ctx, arr, self.world, self.rank), "mdr_rccl_init")
-        self._attached.add(id(shard))
+        shard._rccl_ready = True
 
     def allreduce_counts(self, shard) -> None:
         ptr, n = shard.counts_buffer()

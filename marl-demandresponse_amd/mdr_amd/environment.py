@@ -195,7 +195,7 @@ class Environment:
             sh.upload(local, idx, np.full(nl, float(hp.init_air_temp)), np.full(nl, float(hp.init_mass_temp)),
                       encode_hvac(np.ones(nl, bool), np.zeros(nl, bool), np.zeros(nl, np.int64)))
         else:
-            sh.populate(hp)
+            sh.populate(hp, table)
         self._host_params = None
         self._solar = 0.0
         self._tick = 0
@@ -632,6 +632,10 @@ class Environment:
         state into a fresh context; the RNG is shared like the reference's global random."""
         new = object.__new__(Environment)
         memo[id(self)] = new
+        # every nested reference to the RNG (the grid's Interpolator keeps one; by default it is
+        # the `random` module, which deepcopy cannot copy) stays shared, like the reference's
+        # global random
+        memo[id(self.rng)] = self.rng
         for k, v in self.__dict__.items():
             if k in ("_shard", "cluster", "rng", "_comm", "_shard_factory"):
                 continue

@@ -122,11 +122,17 @@ class HipShard:
     def params_changed(self):
         L.check(self.lib.mdr_params_changed(self.ctx), "mdr_params_changed")
 
-    def populate(self, hp):
+    def populate(self, hp, cap_values):
+        """Synthetic population on device; the capacity of a house is a uniform entry of
+        cooling_capacity_list (random.choices, hvac.py:68-70), mapped into ``cap_values``."""
         nz = hp.noise_prop
         spec = L.mdr_pop_spec(hp.target_temp, nz.std_target_temp, nz.factor_thermo_low,
                               nz.factor_thermo_high, hp.Ca, hp.Cm, hp.Hm, hp.init_air_temp,
                               hp.init_mass_temp)
+        lst = list(hp.hvac_prop.noise_prop.cooling_capacity_list)
+        spec.n_draw = len(lst)
+        for k, v in enumerate(lst):
+            spec.draw_idx[k] = list(cap_values).index(v)
         L.check(self.lib.mdr_populate(self.ctx, C.byref(spec), self.stream()), "mdr_populate")
 
     # ------------------------------------------------------------------ tick
