@@ -251,7 +251,7 @@ def main():
         acts = (torch.rand((chunk, n_loc), device=dev) < 0.5).to(torch.uint8)
     rew = torch.empty((chunk, n_loc), dtype=torch.float64, device=dev)
     dactor = None
-    if args.workload == "actor":
+    if args.workload == "actor":  # (sharded: the RCCL C loop with the ring-halo exchange per tick)
         from mdr_amd.actor import DeviceActor, make_actor
 
         dactor = DeviceActor(env, make_actor(env.obs_spec().n_feat, 2, [100, 100], seed=1),

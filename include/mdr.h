@@ -290,6 +290,17 @@ int mdr_actor_rollout(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const md
                       int64_t prob_stride, double* reward, int64_t rew_stride, double* p_dev,
                       int use_graph, void* stream);
 
+/* mdr_actor_rollout over a house-sharded cluster (config C5 on N GPUs, RCCL communicator of
+ * mdr_rccl_init), no graph: per tick the 'neighbours' ring obs gets the edge houses' message
+ * features of ranks r-1 / r+1 (mdr_halo_pack + grouped ncclSend/ncclRecv), then the actor, a
+ * sum-allreduce of the ON counts its actions produce, then the step.  obs->halo_msg is ignored
+ * (the context owns the halo buffer); TABLE comm modes are single-shard only.  Bit-identical to
+ * the single-shard rollout. */
+int mdr_actor_rollout_sharded(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const mdr_obs_scalars* obs_sc,
+                              const mdr_obs_spec* obs, uint8_t* action, int64_t act_stride, float* prob,
+                              int64_t prob_stride, double* reward, int64_t rew_stride, double* p_dev,
+                              void* stream);
+
 /* ---- interpolated base power ---------------------------------------- */
 /* Replaces PowerInterpolator (server/app/core/environment/power_grid/interpolation.py:24-264) as
  * PowerGrid.power_step calls it every interp_update_period seconds (power_grid.py:149-161): the

@@ -121,6 +121,8 @@ struct mdr_ctx {
   int n_cu = 0;
   double* d_obs_sc = nullptr;  // [ticks_cap][4]
   uint8_t* d_act = nullptr;    // [n_local] actor actions when the caller keeps none
+  float* d_halo = nullptr;     // sharded actor rollout: packed edge rows | received ring halo
+  size_t halo_bytes = 0;
   std::map<std::vector<int64_t>, hipGraphExec_t> actor_graphs;
   // interpolated base power (row a10): grid | table | capacities
   double* d_interp = nullptr;
@@ -364,6 +366,7 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->d_actor);
   hipFree(c->d_interp);
   hipFree(c->d_act);
+  hipFree(c->d_halo);
   hipFree(c->d_obs_sc);
   hipFree(c->d_tables);
   hipFree(c->d_coef);
@@ -1191,6 +1194,84 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
     c->ring = n % 3;
   }
   HIP_TRY(hipGraphLaunch(it->second, st));
+  c->counts_ready = false;
+  return MDR_OK;
+}
+
+// Sharded MA-PPO rollout (config C5): per tick
+//   [ring obs across shards] k_halo_pack -> grouped RCCL send/recv of the edge houses' message
+//   features with ranks r-1 / r+1 -> k_actor (obs on chip, actions, ON counts of those actions)
+//   -> RCCL sum-allreduce of the count slab -> k_step (BUFFER actions, global P)
+// Actions are sampled from Philox keyed by (seed, GLOBAL house id, tick) and the counts are exact
+// integers, so the sharded run is bit-identical to the single-shard one.
+int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_scalars* osc,
+                              const mdr_obs_spec* sp, uint8_t* action, int64_t act_stride, float* prob,
+                              int64_t prob_stride, double* reward, int64_t rew_stride, double* p_dev,
+                              void* stream) {
+  if (!c || !ticks || !osc || !sp || !reward || !p_dev || n < 1)
+    return fail(MDR_EARG, "mdr_actor_rollout_sharded: bad argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_rollout_sharded: context not bound");
+  if (!c->comm) return fail(MDR_ESTATE, "mdr_actor_rollout_sharded: RCCL not initialised");
+  if (int rc = check_actor_obs(c, sp, "mdr_actor_rollout_sharded")) return rc;
+  if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
+    return fail(MDR_EARG, "mdr_actor_rollout_sharded: common penalty modes need the per-step API");
+  const int K = sp->n_comm, M = mdr_msg_width(sp);
+  const int lo = K / 2, hi = (K + 1) / 2;
+  // MDR_FORCE_HALO=1 (test hook): exchange the halo even at world 1 (send/recv to self), which
+  // must reproduce the local ring wrap-around — the 1-GPU check of the multi-GPU exchange
+  static const bool force_halo = getenv("MDR_FORCE_HALO") && atoi(getenv("MDR_FORCE_HALO")) != 0;
+  const bool halo = (c->world > 1 || force_halo) && K > 0;
+  if (halo && sp->comm_mode != MDR_COMM_RING)
+    return fail(MDR_EARG, "mdr_actor_rollout_sharded: across shards only the 'neighbours' ring obs is supported");
+  if (halo && c->kp.n < (lo > hi ? lo : hi))
+    return fail(MDR_EARG, "mdr_actor_rollout_sharded: shard smaller than the ring half-width");
+  hipStream_t st = S(stream);
+  if (int rc = refresh_if_dirty(c, st)) return rc;
+  if (int rc = stage_ticks(c, n, ticks, st)) return rc;
+  if (int rc = stage_recs(osc, n, c->d_obs_sc, st)) return rc;
+  if (!action && !c->d_act) HIP_TRY(hipMalloc(&c->d_act, c->kp.n));
+  const size_t hbytes = (size_t)2 * (lo + hi) * M * sizeof(float);
+  if (halo && hbytes > c->halo_bytes) {
+    HIP_TRY(hipStreamSynchronize(st));
+    hipFree(c->d_halo);
+    c->d_halo = nullptr;
+    HIP_TRY(hipMalloc(&c->d_halo, hbytes));
+    c->halo_bytes = hbytes;
+  }
+  float* mine = c->d_halo;                                    // [hi first | lo last] of this shard
+  float* recv = c->d_halo ? c->d_halo + (size_t)(lo + hi) * M : nullptr;  // [lo before | hi after]
+  mdr_obs_spec spec = *sp;
+  spec.halo_msg = halo ? recv : nullptr;
+  const ObsArgs o = obs_args(c, &spec, &osc[0]);
+  const int prev = (c->rank + c->world - 1) % c->world, next = (c->rank + 1) % c->world;
+  HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
+  c->ring = 0;
+  for (int t = 0; t < n; ++t) {
+    if (halo) {
+      hipLaunchKernelGGL(k_halo_pack, dim3(1), dim3(64), 0, st, c->kp, o, lo, hi, mine);
+      LAUNCH_CHECK("k_halo_pack");
+      RCCL_TRY(ncclGroupStart());
+      // the previous rank's last lo houses come first in the halo, the next rank's first hi after
+      if (lo) {
+        RCCL_TRY(ncclSend(mine + (size_t)hi * M, (size_t)lo * M, ncclFloat32, next, c->comm, st));
+        RCCL_TRY(ncclRecv(recv, (size_t)lo * M, ncclFloat32, prev, c->comm, st));
+      }
+      if (hi) {
+        RCCL_TRY(ncclSend(mine, (size_t)hi * M, ncclFloat32, prev, c->comm, st));
+        RCCL_TRY(ncclRecv(recv + (size_t)lo * M, (size_t)hi * M, ncclFloat32, next, c->comm, st));
+      }
+      RCCL_TRY(ncclGroupEnd());
+    }
+    ObsArgs ot = o;
+    ot.sc_dev = c->d_obs_sc + 4 * t;
+    ActorOut out{action ? action + (int64_t)t * act_stride : c->d_act,
+                 prob ? prob + (int64_t)t * prob_stride : nullptr, nullptr, nullptr, slab_at(c, c->ring), nullptr};
+    if (int rc = launch_actor(c, &spec, ot, p_dev, 0, c->d_ticks + t, out, st)) return rc;
+    RCCL_TRY(ncclAllReduce(slab_at(c, c->ring), slab_at(c, c->ring), c->slab_len, ncclUint64, ncclSum, c->comm, st));
+    if (int rc = launch_step(c, out.action, MDR_ACT_BUFFER, TickArgs{}, c->d_ticks + t,
+                             reward + (int64_t)t * rew_stride, 0, MDR_CTRL_NONE, nullptr, p_dev, st))
+      return rc;
+  }
   c->counts_ready = false;
   return MDR_OK;
 }

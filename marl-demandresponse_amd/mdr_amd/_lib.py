@@ -125,6 +125,7 @@ SIGNATURES = {
     "mdr_actor_act": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, U64, VP, VP, VP, VP, I, VP]),
     "mdr_actor_rollout": (I, [VP, I, VP, VP, P(mdr_obs_spec), VP, I64, VP, I64,
                               VP, I64, VP, I, VP]),
+    "mdr_actor_rollout_sharded": (I, [VP, I, VP, VP, P(mdr_obs_spec), VP, I64, VP, I64, VP, I64, VP, VP]),
     "mdr_actor_profile": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, P(D), VP]),
     "mdr_interp_load": (I, [VP, P(mdr_interp_spec)]),
     "mdr_interp_values": (I, [VP, VP, I, D, D, D, VP, VP]),

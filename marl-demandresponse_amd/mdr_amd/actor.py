@@ -117,11 +117,12 @@ class DeviceActor:
         torch = _torch()
         env = self.env
         sh = env.shard
-        if env.world > 1:
-            raise NotImplementedError("sharded actor rollouts: loop select_actions / step_tensor")
         if sh.penalty_mode != 0:
             raise NotImplementedError("actor rollouts support individual_L2; use step_tensor")
-        spec, _sc, keep = env.bound_obs_spec()
+        if env.world > 1 and not getattr(env._comm, "native", False):
+            return self._rollout_stepwise(n_ticks, rewards, actions, probs)
+        sharded = env.world > 1
+        spec, _sc, keep = env.bound_obs_spec() if not sharded else (env.obs_spec(), None, [])
         self._check_obs(spec)
         n = env.n_local
         if rewards is None:
@@ -144,8 +145,12 @@ class DeviceActor:
             osc[1:, 2] = ticks.solar[:-1]
             osc[:, 3] = ticks.t_od_prev
             sl = (lambda x, st: None if x is None else (x[done:done + k] if st else x))
-            g = use_graph and (k == n_ticks or not (rs or as_ or ps))
-            sh.actor_rollout(ticks, osc, spec, sl(actions, as_), as_, sl(probs, ps), ps, sl(rewards, rs), rs, g)
+            if sharded:  # C loop: ring halo + actor + count allreduce + step per tick (RCCL)
+                sh.actor_rollout_sharded(ticks, osc, spec, sl(actions, as_), as_, sl(probs, ps), ps,
+                                         sl(rewards, rs), rs)
+            else:
+                g = use_graph and (k == n_ticks or not (rs or as_ or ps))
+                sh.actor_rollout(ticks, osc, spec, sl(actions, as_), as_, sl(probs, ps), ps, sl(rewards, rs), rs, g)
             env._P_dev_valid = True
             env.finish_grid_step()
             done += k
@@ -153,6 +158,26 @@ class DeviceActor:
             torch.cuda.current_stream(sh.device).synchronize()
         env._counts_ready = 0
         env._P_dev_valid = True
+        return rewards
+
+
+    def _rollout_stepwise(self, n_ticks, rewards, actions, probs):
+        """Sharded rollout over a torch.distributed communicator (e.g. gloo): per tick
+        select_actions (ring halo all-gather, ON counts of the actions) then step_tensor (count
+        allreduce, step) from Python — the same launches and exchanges as the C loop."""
+        torch = _torch()
+        env = self.env
+        sh = env.shard
+        n = env.n_local
+        if rewards is None:
+            rewards = torch.empty((n_ticks, n), dtype=torch.float64, device=sh.device)
+        a_tmp = torch.empty(n, dtype=torch.uint8, device=sh.device)
+        p_tmp = torch.empty(n, dtype=torch.float32, device=sh.device)
+        for t in range(n_ticks):
+            a = a_tmp if actions is None else (actions[t] if actions.dim() == 2 else actions)
+            p = p_tmp if probs is None else (probs[t] if probs.dim() == 2 else probs)
+            self.select_actions(action=a, prob=p, count_next=True)
+            env.step_tensor(a, rewards=rewards[t] if rewards.dim() == 2 else rewards)
         return rewards
 
 

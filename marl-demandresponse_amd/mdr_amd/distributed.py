@@ -25,6 +25,8 @@ from . import _lib as L
 class RcclComm:
     """Collectives of a sharded Environment, over the libmdr_hip RCCL communicator."""
 
+    native = True  # the library's own communicator: C rollout loops may issue the collectives
+
     def __init__(self):
         import torch.distributed as dist
 
@@ -137,6 +139,8 @@ class TorchComm(RcclComm):
     With the 'nccl' backend this is still RCCL (torch's communicator); with 'gloo' it lets
     several ranks share one GPU, which is how the sharded device path is tested on a 1-GPU box.
     Rollouts issue one step per tick from Python (no C loop)."""
+
+    native = False
 
     def attach(self, shard) -> None:
         pass

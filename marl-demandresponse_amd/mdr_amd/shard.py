@@ -234,6 +234,18 @@ class HipShard:
         if use_graph:
             cur.wait_stream(self._side)
 
+    def actor_rollout_sharded(self, ticks, obs_sc, spec, action, act_stride, prob, prob_stride, reward,
+                              rew_stride):
+        """n ticks of ring halo -> actor -> count allreduce -> step over the RCCL communicator
+        (mdr_actor_rollout_sharded), on the caller's current stream."""
+        n = len(ticks)
+        obs_sc = np.ascontiguousarray(obs_sc, np.float64)
+        assert obs_sc.shape == (n, 4)
+        L.check(self.lib.mdr_actor_rollout_sharded(self.ctx, n, ticks.ptr(), obs_sc.ctypes.data, C.byref(spec),
+                                                   L.ptr(action), act_stride, L.ptr(prob), prob_stride,
+                                                   L.ptr(reward), rew_stride, L.ptr(self.p_dev), self.stream()),
+                "mdr_actor_rollout_sharded")
+
     def interp_load(self, grids, values, cfg):
         """Monte-Carlo table + axes to the device (mdr_interp_load, synchronous)."""
         grid = np.ascontiguousarray(np.concatenate([np.asarray(g, np.float64) for g in grids]))

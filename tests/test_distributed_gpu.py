@@ -67,8 +67,9 @@ def _worker(rank, world, port, backend, kind, n, mode, out_dir):
     import torch
     import torch.distributed as dist
 
-    if kind.startswith("rccl-"):  # force the serial / overlapped C loop (default: calibrate)
+    if kind.startswith("rccl-"):  # per-tick C loop (window 0), forced serial / overlapped pipeline
         os.environ["MDR_SHARDED_OVERLAP"] = "0" if kind == "rccl-serial" else "1"
+        os.environ["MDR_WINDOW"] = "0"
         kind = "rccl"
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
@@ -130,3 +131,74 @@ def test_sharded_equals_single(tmp_path, backend, kind, world, n, mode):
         assert float(p["P"]) == ref["P"]
     obs = np.concatenate([p["obs"] for p in parts])
     np.testing.assert_array_equal(obs, ref["obs"])
+
+
+# ---------------------------------------------------------------- sharded MA-PPO rollout (C5)
+T_ACT = 12
+
+
+def _actor_run(env, torch):
+    from mdr_amd.actor import DeviceActor, make_actor
+
+    da = DeviceActor(env, make_actor(env.obs_spec().n_feat, 2, [100, 100], seed=1))
+    nl = env.n_local
+    A = torch.zeros((T_ACT, nl), dtype=torch.uint8, device=env.shard.device)
+    Pr = torch.zeros((T_ACT, nl), dtype=torch.float32, device=env.shard.device)
+    R = da.rollout(T_ACT, actions=A, probs=Pr)
+    torch.cuda.synchronize()
+    st = env.shard.host_state()
+    return {"rewards": R.cpu().numpy(), "actions": A.cpu().numpy(), "probs": Pr.cpu().numpy(),
+            "T": st["T"], "on": st["on"], "sso": st["sso"], "P": env._cluster_power()}
+
+
+def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo):
+    sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "marl-demandresponse_amd"), os.path.dirname(HERE)]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    if force_halo:
+        os.environ["MDR_FORCE_HALO"] = "1"
+    import torch
+    import torch.distributed as dist
+
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    kw = {"device_id": dev} if backend == "nccl" else {}
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    import golden_util as g
+
+    from mdr_amd.distributed import make_comm
+    from mdr_amd.environment import Environment
+
+    env = Environment(g.props_from_overrides(_overrides(n, "individual_L2")), device=dev, rng=random.Random(4),
+                      population="synthetic", seed=77, rank=rank, world=world, comm=make_comm(kind))
+    res = _actor_run(env, torch)
+    res["lo"] = env._offset
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("backend,kind,world,force_halo", [
+    ("nccl", "rccl", 1, False),   # C loop: actor -> RCCL count allreduce -> step
+    ("nccl", "rccl", 1, True),    # + the ring-halo pack / ncclSend / ncclRecv (to self)
+    ("gloo", "torch", 2, False),  # two shards on cuda:0, per-tick Python loop, all-gather halo
+])
+def test_sharded_actor_rollout_equals_single(tmp_path, backend, kind, world, force_halo):
+    """Sharded MA-PPO rollout (config C5) == the single-process graph rollout: actions, sampled
+    probabilities, rewards, state and P bit for bit."""
+    import torch
+
+    from mdr_amd.environment import Environment
+
+    n = 3001
+    mp.start_processes(_actor_worker, args=(world, _free_port(), backend, kind, n, str(tmp_path), force_halo),
+                       nprocs=world, join=True, start_method="spawn")
+    parts = sorted((np.load(tmp_path / f"rank{r}.npz") for r in range(world)), key=lambda p: int(p["lo"]))
+    env = Environment(gu.props_from_overrides(_overrides(n, "individual_L2")), device=torch.device("cuda", 0),
+                      rng=random.Random(4), population="synthetic", seed=77)
+    ref = _actor_run(env, torch)
+    for key in ("actions", "probs", "rewards"):
+        np.testing.assert_array_equal(np.concatenate([p[key] for p in parts], axis=1), ref[key], err_msg=key)
+    for key in ("T", "on", "sso"):
+        np.testing.assert_array_equal(np.concatenate([p[key] for p in parts]), ref[key], err_msg=key)
+    for p in parts:
+        assert float(p["P"]) == ref["P"]
