@@ -37,21 +37,29 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(s) <= t for s in SRC + HDR + [__file__])
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
-        return OUT
-    tmp = OUT + ".tmp"
-    cmd = [hipcc()] + FLAGS + SRC + ["-o", tmp, "-L/opt/rocm/lib", "-lrccl",
-                                     "-Wl,-rpath,/opt/rocm/lib"]
+def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
+    """Build the library (``defines``: extra -D flags for A/B variants built next to it, e.g.
+    ``out=mdr_amd/libmdr_w4.so, defines=["MDR_WIN_WAVES=4"]``, loaded with MDR_LIB=...)."""
+    if not force and out == OUT and up_to_date():
+        return out
+    tmp = out + ".tmp"
+    cmd = [hipcc()] + FLAGS + ["-D" + d for d in defines] + SRC + ["-o", tmp, "-L/opt/rocm/lib", "-lrccl",
+                                                                    "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         sys.stderr.write(r.stdout + r.stderr)
         raise RuntimeError(f"hipcc failed ({r.returncode})")
-    os.replace(tmp, OUT)
-    return OUT
+    os.replace(tmp, out)
+    return out
 
 
 if __name__ == "__main__":
-    print(build(force="--force" in sys.argv, verbose=True))
+    # python build_ext.py [--force] [--variant NAME DEFINE ...]  (variant -> mdr_amd/libmdr_NAME.so)
+    if "--variant" in sys.argv:
+        i = sys.argv.index("--variant")
+        name, defs = sys.argv[i + 1], sys.argv[i + 2:]
+        print(build(force=True, verbose=True, out=os.path.join(HERE, "mdr_amd", f"libmdr_{name}.so"), defines=defs))
+    else:
+        print(build(force="--force" in sys.argv, verbose=True))

@@ -87,6 +87,7 @@ struct mdr_ctx {
   bool fastdiv = true;                   // shared-reciprocal exact division (MDR_FASTDIV=0 disables)
   int tpw = 0;                           // k_step_pipe tiles per wave (MDR_TPW; 0: k_step_t)
   int win = kWindowMax;                  // ticks per k_step_window launch (MDR_WINDOW; 0: one-tick path)
+  int win_hpt = 2;                       // houses per lane of k_step_window (MDR_WIN_HPT)
   unsigned long long* d_wslab = nullptr; // 3 window count slabs [kWindowMax][kCountShards][n_cap]
   int wslab_len = 0;
   bool coef_dirty = true;
@@ -324,6 +325,7 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   // wave up to ~1.5M houses per shard, 4 above; MDR_TPW=0 selects the one-tile kernel k_step_t
   c->tpw = cfg->n_local <= 1572864 ? 2 : 4;
   if (const char* e = getenv("MDR_TPW")) c->tpw = atoi(e);
+  if (const char* e = getenv("MDR_WIN_HPT")) c->win_hpt = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("MDR_WINDOW")) c->win = atoi(e) < 0 ? 0 : atoi(e) > kWindowMax ? kWindowMax : atoi(e);
   if (cfg->n_cap <= kWindowCap) {
     c->wslab_len = kWindowMax * kCountShards * cfg->n_cap;
@@ -541,13 +543,19 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
   auto wsz = [&](int w) { return base + (w < rem ? 1 : 0); };
   auto slab = [&](int w) { return c->d_wslab + (size_t)(w % 3) * c->wslab_len; };
   HIP_TRY(hipMemsetAsync(c->d_wslab, 0, 3 * sizeof(unsigned long long) * c->wslab_len, st));
-  const unsigned grid = blocks(blocks(c->kp.n, 128), 4);  // one 128-house tile per wave, 4 waves per block
+  const int hpt = c->win_hpt;
+  const unsigned grid = blocks(blocks(c->kp.n, 64 * hpt), 4);  // one 64*hpt-house tile per wave, 4 waves per block
   KParams kp = c->kp;
-#define MDR_WIN_DISPATCH(KERNEL, ...)                                                                      \
-  do {                                                                                                     \
-    if (mode == MDR_ACT_RANDOM) hipLaunchKernelGGL(KERNEL<MDR_ACT_RANDOM>, dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
-    else if (mode == MDR_ACT_ALWAYS_ON) hipLaunchKernelGGL(KERNEL<MDR_ACT_ALWAYS_ON>, dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
-    else hipLaunchKernelGGL(KERNEL<MDR_ACT_BUFFER>, dim3(grid), dim3(256), 0, st, __VA_ARGS__);           \
+#define MDR_WIN_DISPATCH_H(KERNEL, H, ...)                                                                     \
+  do {                                                                                                         \
+    if (mode == MDR_ACT_RANDOM) hipLaunchKernelGGL((KERNEL<MDR_ACT_RANDOM, H>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
+    else if (mode == MDR_ACT_ALWAYS_ON) hipLaunchKernelGGL((KERNEL<MDR_ACT_ALWAYS_ON, H>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL((KERNEL<MDR_ACT_BUFFER, H>), dim3(grid), dim3(256), 0, st, __VA_ARGS__);           \
+  } while (0)
+#define MDR_WIN_DISPATCH(KERNEL, ...)                                     \
+  do {                                                                   \
+    if (hpt == 1) MDR_WIN_DISPATCH_H(KERNEL, 1, __VA_ARGS__);            \
+    else MDR_WIN_DISPATCH_H(KERNEL, 2, __VA_ARGS__);                     \
   } while (0)
   MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, wsz(0), slab(0));
   LAUNCH_CHECK("k_count_window");
@@ -562,6 +570,7 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     t0 += K;
   }
 #undef MDR_WIN_DISPATCH
+#undef MDR_WIN_DISPATCH_H
   return MDR_OK;
 }
 

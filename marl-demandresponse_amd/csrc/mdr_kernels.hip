@@ -598,6 +598,18 @@ __device__ __forceinline__ void win_random_stage(uint64_t seed, uint64_t g0, int
   }
 }
 
+// the random actions of house gid for window ticks 0 .. nt-1 as bits of one 64-bit mask (LDS
+// reads once per window, none in the tick loop)
+__device__ __forceinline__ uint64_t win_random_mask(const uint2* rw, int G, uint64_t g0, int nt, uint64_t gid) {
+  uint64_t m = 0;
+  const int g = (int)((gid >> 6) - g0);
+  for (int j = 0; j < nt; ++j) {
+    const uint2 wd = rw[j * G + g];
+    m |= (uint64_t)bit_of(wd.x, wd.y, gid) << j;
+  }
+  return m;
+}
+
 template <int ACT>
 __device__ __forceinline__ bool win_action(const uint2* rw, int G, uint64_t g0, int j, uint64_t gid,
                                            const uint8_t* arow, uint32_t i) {
@@ -608,25 +620,31 @@ __device__ __forceinline__ bool win_action(const uint2* rw, int G, uint64_t g0, 
 }
 
 // FSM-only run of nt ticks (tick offsets j0 .. j0+nt-1 of the staged random slots / action rows)
-// from words w[0..1], ON counts per tick and class into the block histogram hist[j][kWinCap].
-template <int ACT>
-__device__ __forceinline__ void win_count(const KParams& p, uint32_t wa, uint32_t wb, int cls0, int cls1, bool v0,
-                                          bool v1, uint32_t i0, uint64_t gid0, const uint2* rw, int G, uint64_t g0,
+// from words w[0..HPT), ON counts per tick and class into the block histogram hist[j][kWinCap].
+template <int ACT, int HPT>
+__device__ __forceinline__ void win_count(const KParams& p, const uint32_t* w_in, const int* cls, const bool* v,
+                                          uint32_t i0, uint64_t gid0, const uint2* rw, int G, uint64_t g0,
                                           int j0, int nt, const uint8_t* action, int64_t act_stride,
                                           unsigned* hist) {
   const int lane = threadIdx.x & 63;
+  uint32_t w[HPT];
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) w[h] = w_in[h];
   for (int j = 0; j < nt; ++j) {
     const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)(j0 + j) * act_stride : nullptr;
-    const bool a0 = v0 && win_action<ACT>(rw, G, g0, j0 + j, gid0, arow, i0);
-    const bool a1 = v1 && win_action<ACT>(rw, G, g0, j0 + j, gid0 + 1, arow, i0 + 1);
-    wa = hvac_fsm(wa, a0, p.dt, p.L);
-    wb = hvac_fsm(wb, a1, p.dt, p.L);
-    const bool o0 = v0 && hv_on(wa), o1 = v1 && hv_on(wb);
+    bool on[HPT];
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) {
+      const bool a = v[h] && win_action<ACT>(rw, G, g0, j0 + j, gid0 + h, arow, i0 + h);
+      w[h] = hvac_fsm(w[h], a, p.dt, p.L);
+      on[h] = v[h] && hv_on(w[h]);
+    }
 #pragma unroll
     for (int c = 0; c < kWinCap; ++c) {
       if (c < p.n_cap) {
-        const unsigned cnt = (unsigned)__popcll(__ballot(o0 && cls0 == c)) +
-                             (unsigned)__popcll(__ballot(o1 && cls1 == c));
+        unsigned cnt = 0;
+#pragma unroll
+        for (int h = 0; h < HPT; ++h) cnt += (unsigned)__popcll(__ballot(on[h] && cls[h] == c));
         if (lane == 0 && cnt) atomicAdd(&hist[j * kWinCap + c], cnt);
       }
     }
@@ -643,38 +661,66 @@ __device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsign
   }
 }
 
+// the wave tile: 64 * HPT consecutive houses, HPT per lane; groups of 64 global ids it spans
+template <int HPT>
+struct WinTile {
+  uint32_t tile, i0;
+  bool v[HPT];
+  bool full;
+  uint64_t gid0, g0;
+  int G;
+  __device__ __forceinline__ WinTile(const KParams& p) {
+    const uint32_t n = (uint32_t)p.n;
+    tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    i0 = tile * (64u * HPT) + (uint32_t)(threadIdx.x & 63) * HPT;
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) v[h] = i0 + h < n;
+    full = (tile + 1u) * (64u * HPT) <= n;
+    gid0 = (uint64_t)p.goff + i0;
+    const uint64_t gbase = (uint64_t)p.goff + (uint64_t)tile * (64u * HPT);
+    g0 = gbase >> 6;
+    G = (int)(((gbase + 64u * HPT - 1u) >> 6) - g0) + 1;
+  }
+};
+
 // First window of a rollout: ON counts of ticks 0 .. nt-1 (no state change).
-template <int ACT>
+template <int ACT, int HPT>
 __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* __restrict__ action,
                                                       int64_t act_stride, const TickArgs* __restrict__ tkp, int nt,
                                                       unsigned long long* __restrict__ slab) {
   __shared__ uint2 s_rw[4][3 * kWinMax];
   __shared__ unsigned s_hist[kWinMax * kWinCap];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int tid = threadIdx.x, wv = tid >> 6;
   for (int j = tid; j < kWinMax * kWinCap; j += blockDim.x) s_hist[j] = 0;
+  const WinTile<HPT> t(p);
   const uint32_t n = (uint32_t)p.n;
-  const uint32_t tile = blockIdx.x * 4u + (uint32_t)wv;
-  const uint32_t i0 = tile * 128u + (uint32_t)lane * 2u;
-  const bool v0 = i0 < n, v1 = i0 + 1u < n;
-  const uint32_t ia = v0 ? i0 : n - 1u, ib = v1 ? i0 + 1u : n - 1u;
-  const uint32_t wa = p.hvac[ia], wb = p.hvac[ib];
-  const int cls0 = p.cap_idx[ia], cls1 = p.cap_idx[ib];
-  const uint64_t gbase = (uint64_t)p.goff + (uint64_t)tile * 128u;
-  const uint64_t g0 = gbase >> 6;
-  const int G = (int)(((gbase + 127u) >> 6) - g0) + 1;
-  if (ACT == MDR_ACT_RANDOM) win_random_stage(p.seed, g0, G, tkp, nt, s_rw[wv]);
+  uint32_t w[HPT];
+  int cls[HPT];
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) {
+    const uint32_t i = t.v[h] ? t.i0 + h : n - 1u;
+    w[h] = p.hvac[i];
+    cls[h] = p.cap_idx[i];
+  }
+  if (ACT == MDR_ACT_RANDOM) win_random_stage(p.seed, t.g0, t.G, tkp, nt, s_rw[wv]);
   __syncthreads();
-  win_count<ACT>(p, wa, wb, cls0, cls1, v0, v1, i0, (uint64_t)p.goff + i0, s_rw[wv], G, g0, 0, nt, action,
-                 act_stride, s_hist);
+  win_count<ACT, HPT>(p, w, cls, t.v, t.i0, t.gid0, s_rw[wv], t.G, t.g0, 0, nt, action, act_stride, s_hist);
   __syncthreads();
   win_flush(p, nt, s_hist, slab);
 }
 
+// MDR_WIN_WAVES (build-time A/B knob): cap k_step_window at that many waves per SIMD
+#ifdef MDR_WIN_WAVES
+#define MDR_WIN_OCC __attribute__((amdgpu_waves_per_eu(MDR_WIN_WAVES)))
+#else
+#define MDR_WIN_OCC
+#endif
+
 // One window of K ticks.  counts: slabs of ticks 0..K-1 (complete, global); la_K > 0: run the
 // FSM on through the next la_K ticks (tkp[K..K+la_K), action rows K..) and accumulate their ON
 // counts into next_slab; block 0 zeroes zero_slab (zero_len u64) for the launch after next.
-template <int ACT>
-__global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* __restrict__ action,
+template <int ACT, int HPT>
+__global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, const uint8_t* __restrict__ action,
                                                      int64_t act_stride, const TickArgs* __restrict__ tkp, int K,
                                                      int la_K, const unsigned long long* __restrict__ counts,
                                                      double* __restrict__ reward, int64_t rew_stride,
@@ -687,22 +733,38 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
   if (zero_slab && blockIdx.x == 0)
     for (int j = tid; j < zero_len; j += blockDim.x) zero_slab[j] = 0ull;
   const uint32_t n = (uint32_t)p.n;
-  const uint32_t tile = blockIdx.x * 4u + (uint32_t)wv;
-  const uint32_t i0 = tile * 128u + (uint32_t)lane * 2u;
-  const bool v0 = i0 < n, v1 = i0 + 1u < n;
-  const bool full = (tile + 1u) * 128u <= n;  // wave-uniform
+  const WinTile<HPT> t(p);
+  const uint32_t i0 = t.i0;
 
   // ---- state + parameters, once per window
-  Tile2 t;
-  load_tile2<false>(p, nullptr, i0, n, full, t);
-  const int cls0 = (int)(t.cls & 0xFF), cls1 = (int)((t.cls >> 8) & 0xFF);
+  double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
+  uint32_t w[HPT];
+  int cls[HPT];
+  if (HPT == 2) {
+    Tile2 tl;
+    load_tile2<false>(p, nullptr, i0, n, t.full, tl);
+    T[0] = tl.T.x; T[HPT - 1] = tl.T.y; Tm[0] = tl.Tm.x; Tm[HPT - 1] = tl.Tm.y;
+    ua[0] = tl.ua.x; ua[HPT - 1] = tl.ua.y; ca[0] = tl.ca.x; ca[HPT - 1] = tl.ca.y;
+    cm[0] = tl.cm.x; cm[HPT - 1] = tl.cm.y; hm[0] = tl.hm.x; hm[HPT - 1] = tl.hm.y;
+    tg[0] = tl.tg.x; tg[HPT - 1] = tl.tg.y; w[0] = tl.w.x; w[HPT - 1] = tl.w.y;
+    cls[0] = (int)(tl.cls & 0xFF); cls[HPT - 1] = (int)((tl.cls >> 8) & 0xFF);
+  } else {
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) {
+      const uint32_t i = t.v[h] ? i0 + h : n - 1u;
+      T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i]; cm[h] = p.cm[i];
+      hm[h] = p.hm[i]; tg[h] = p.target[i]; w[h] = p.hvac[i]; cls[h] = p.cap_idx[i];
+    }
+  }
   double q_on[kWinCap];
 #pragma unroll
   for (int k = 0; k < kWinCap; ++k) q_on[k] = p.q_on[k < p.n_cap ? k : 0];
 
   // ---- per-tick signal penalty of the window, lane j <- tick j (rewards_calculator.py:183-203)
-  double sig_l = 0.0, P_l = 0.0;
+  double sig_l = 0.0, P_l = 0.0, tod_l = 0.0, sol_l = 0.0;
   if (lane < K) {
+    tod_l = tkp[lane].t_od_prev;  // the window's drivers, lane j <- tick j (readlane per tick)
+    sol_l = tkp[lane].solar;
     const unsigned long long* cj = counts + (size_t)lane * kCountShards * p.n_cap;
     for (int k = 0; k < p.n_cap; ++k) {
       unsigned long long c = 0;
@@ -716,51 +778,48 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
   if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P_last;
 
   // ---- random controller bits for the window + lookahead
-  const uint64_t gid0 = (uint64_t)p.goff + i0;
-  const uint64_t gbase = (uint64_t)p.goff + (uint64_t)tile * 128u;
-  const uint64_t g0 = gbase >> 6;
-  const int G = (int)(((gbase + 127u) >> 6) - g0) + 1;
-  if (ACT == MDR_ACT_RANDOM) win_random_stage(p.seed, g0, G, tkp, K + la_K, s_rw[wv]);
+  if (ACT == MDR_ACT_RANDOM) win_random_stage(p.seed, t.g0, t.G, tkp, K + la_K, s_rw[wv]);
   __syncthreads();  // LDS histogram zeroed, random words staged
 
   const bool params_ok = !*p.params_bad && p.fast_tick_ok;
-  double T[2] = {t.T.x, t.T.y}, Tm[2] = {t.Tm.x, t.Tm.y};
-  const double ua[2] = {t.ua.x, t.ua.y}, hm[2] = {t.hm.x, t.hm.y}, tg[2] = {t.tg.x, t.tg.y};
-  const int cls[2] = {cls0, cls1};
-  uint32_t w[2] = {t.w.x, t.w.y};
-  double qc[2];
-  RcWin rw[2];
+  double qc[HPT];
+  RcWin rw[HPT];
+  uint64_t rmask[HPT];
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < HPT; ++h) {
     qc[h] = q_on[0];
 #pragma unroll
     for (int c = 1; c < kWinCap; ++c) qc[h] = cls[h] == c ? q_on[c] : qc[h];
     if (params_ok) {
-      rw[h] = rc_window(ua[h], h ? t.ca.y : t.ca.x, h ? t.cm.y : t.cm.x, hm[h], (double)p.dt);
+      rw[h] = rc_window(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
     } else {  // IEEE division (identical bits; parameters outside the fast-division range)
-      rw[h].k = rc_coeffs_t<false>(ua[h], h ? t.ca.y : t.ca.x, h ? t.cm.y : t.cm.x, hm[h], (double)p.dt);
-      rw[h].rCa.nb = -(h ? t.ca.y : t.ca.x);
+      rw[h].k = rc_coeffs_t<false>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+      rw[h].rCa.nb = -ca[h];
       rw[h].rc.nb = -ua[h];
       rw[h].rd.nb = -(rw[h].k.r2 - rw[h].k.r1);
       rw[h].UaHm = ua[h] + hm[h];
     }
+    rmask[h] = ACT == MDR_ACT_RANDOM ? win_random_mask(s_rw[wv], t.G, t.g0, K, t.gid0 + h) : 0ull;
   }
   const uint32_t o8 = i0 * 8u;
-  const bool vec_rew = full && (rew_stride & 1) == 0 && (((uintptr_t)reward) & 15u) == 0;
+  const bool vec_rew = HPT == 2 && t.full && (rew_stride & 1) == 0 && (((uintptr_t)reward) & 15u) == 0;
 
   for (int j = 0; j < K; ++j) {
-    const TickArgs tk = tkp[j];
+    TickArgs tk;
+    tk.t_od_prev = readlane_f64(tod_l, j);
+    tk.solar = readlane_f64(sol_l, j);
     const double sig = readlane_f64(sig_l, j);
     const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)j * act_stride : nullptr;
-    bool house_ok = fabs(T[0]) < 1048576.0 && fabs(Tm[0]) < 1048576.0 && fabs(T[1]) < 1048576.0 &&
-                    fabs(Tm[1]) < 1048576.0;
+    bool house_ok = true;
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) house_ok = house_ok && fabs(T[h]) < 1048576.0 && fabs(Tm[h]) < 1048576.0;
     const bool fast = params_ok && fabs(tk.t_od_prev) < 1048576.0 && fabs(tk.solar) < 1099511627776.0 &&
                       __all(house_ok);
-    double rwd[2];
+    double rwd[HPT];
 #pragma unroll
-    for (int h = 0; h < 2; ++h) {
-      const bool valid = h ? v1 : v0;
-      const bool a = valid && win_action<ACT>(s_rw[wv], G, g0, j, gid0 + h, arow, i0 + h);
+    for (int h = 0; h < HPT; ++h) {
+      const bool a = t.v[h] && (ACT == MDR_ACT_RANDOM ? ((rmask[h] >> j) & 1ull) != 0
+                                                      : win_action<ACT>(s_rw[wv], t.G, t.g0, j, t.gid0 + h, arow, i0 + h));
       w[h] = hvac_fsm(w[h], a, p.dt, p.L);
       const double q = hv_on(w[h]) ? qc[h] : 0.0;
       double Tn, Tmn;
@@ -772,40 +831,46 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
       rwd[h] = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig);
     }
     double* rrow = reward + (int64_t)j * rew_stride;
-    if (vec_rew) sto(rrow, o8, make_double2(rwd[0], rwd[1]));
+    if (vec_rew) sto(rrow, o8, make_double2(rwd[0], rwd[HPT - 1]));
     else {
-      if (v0) rrow[i0] = rwd[0];
-      if (v1) rrow[i0 + 1] = rwd[1];
+#pragma unroll
+      for (int h = 0; h < HPT; ++h)
+        if (t.v[h]) rrow[i0 + h] = rwd[h];
     }
   }
 
   // ---- state back, once per window
-  if (v1) {
-    sto(p.t_air, o8, make_double2(T[0], T[1]));
-    sto(p.t_mass, o8, make_double2(Tm[0], Tm[1]));
-    sto(p.hvac, i0 * 4u, make_uint2(w[0], w[1]));
-  } else if (v0) {
-    p.t_air[i0] = T[0]; p.t_mass[i0] = Tm[0]; p.hvac[i0] = w[0];
+  if (HPT == 2 && t.v[HPT - 1]) {
+    sto(p.t_air, o8, make_double2(T[0], T[HPT - 1]));
+    sto(p.t_mass, o8, make_double2(Tm[0], Tm[HPT - 1]));
+    sto(p.hvac, i0 * 4u, make_uint2(w[0], w[HPT - 1]));
+  } else {
+#pragma unroll
+    for (int h = 0; h < HPT; ++h)
+      if (t.v[h]) { p.t_air[i0 + h] = T[h]; p.t_mass[i0 + h] = Tm[h]; p.hvac[i0 + h] = w[h]; }
   }
 
   // ---- lookahead: ON counts of the next window's ticks
   if (la_K > 0) {
-    win_count<ACT>(p, w[0], w[1], cls0, cls1, v0, v1, i0, gid0, s_rw[wv], G, g0, K, la_K,
-                   ACT == MDR_ACT_BUFFER ? action : nullptr, act_stride, s_hist);
+    win_count<ACT, HPT>(p, w, cls, t.v, i0, t.gid0, s_rw[wv], t.G, t.g0, K, la_K,
+                        ACT == MDR_ACT_BUFFER ? action : nullptr, act_stride, s_hist);
     __syncthreads();
     win_flush(p, la_K, s_hist, next_slab);
   }
 }
 
-#define MDR_INST_WIN(A)                                                                             \
-  template __global__ void k_step_window<A>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
-                                            const unsigned long long*, double*, int64_t, double*,      \
-                                            unsigned long long*, unsigned long long*, int);             \
-  template __global__ void k_count_window<A>(KParams, const uint8_t*, int64_t, const TickArgs*, int,    \
-                                             unsigned long long*);
-MDR_INST_WIN(MDR_ACT_RANDOM)
-MDR_INST_WIN(MDR_ACT_ALWAYS_ON)
-MDR_INST_WIN(MDR_ACT_BUFFER)
+#define MDR_INST_WIN(A, H)                                                                             \
+  template __global__ void k_step_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
+                                               const unsigned long long*, double*, int64_t, double*,      \
+                                               unsigned long long*, unsigned long long*, int);             \
+  template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, int,    \
+                                                unsigned long long*);
+MDR_INST_WIN(MDR_ACT_RANDOM, 1)
+MDR_INST_WIN(MDR_ACT_ALWAYS_ON, 1)
+MDR_INST_WIN(MDR_ACT_BUFFER, 1)
+MDR_INST_WIN(MDR_ACT_RANDOM, 2)
+MDR_INST_WIN(MDR_ACT_ALWAYS_ON, 2)
+MDR_INST_WIN(MDR_ACT_BUFFER, 2)
 
 #define MDR_INST_PIPE(T, A, LA)                                                                    \
   template __global__ void k_step_pipe<T, A, LA>(KParams, const uint8_t*, TickArgs, const TickArgs*, \

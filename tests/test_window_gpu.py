@@ -47,9 +47,12 @@ def _same_state(torch, e1, e2):
 @pytest.mark.parametrize("n,ticks,win", [(1, 5, 32), (2, 33, 32), (257, 40, 7), (4099, 65, 32),
                                          (20011, 64, 16), (131072, 50, 32)])
 @pytest.mark.parametrize("mode", ["random", "always_on", "buffer"])
-def test_window_equals_one_tick(torch_gpu, n, ticks, win, mode):
-    """Windowed rollout == the one-launch-per-tick rollout, bit for bit (rewards, state, P)."""
+@pytest.mark.parametrize("hpt", ["1", "2"])
+def test_window_equals_one_tick(torch_gpu, monkeypatch, n, ticks, win, mode, hpt):
+    """Windowed rollout (1 or 2 houses per lane) == the one-launch-per-tick rollout, bit for bit
+    (rewards, state, P)."""
     torch = torch_gpu
+    monkeypatch.setenv("MDR_WIN_HPT", hpt)  # read by mdr_create
     e1, e2 = _pair(n)
     e1.shard.set_rollout_window(win)
     e2.shard.set_rollout_window(0)

@@ -2,7 +2,8 @@
 
     python tools/kbench.py [--houses 1048576,4194304] [--ticks 128] [--rounds 5] [--variants w32,w0,probe]
 
-Variants: wK = temporally blocked rollout, K ticks per k_step_window launch; w0 = one launch per
+Variants: wK[hH] = temporally blocked rollout, K ticks per k_step_window launch (H houses per
+lane, default 2); w0 = one launch per
 tick (k_step_pipe / k_step_t, MDR_TPW / MDR_HPT / MDR_FASTDIV still select among those); probe =
 the memory-floor probe of the one-tick kernel (same loads/stores, no arithmetic).  Every tick's
 reward row is kept ([ticks, n] float64), so reward writes really go to HBM.  Prints per-tick
@@ -35,10 +36,12 @@ def main():
     for n in [int(x) for x in a.houses.split(",")]:
         envs = {}
         for v in a.variants.split(","):
+            hpt = v.partition("h")[2]  # wKhH: houses per lane of k_step_window (MDR_WIN_HPT at mdr_create)
+            os.environ["MDR_WIN_HPT"] = hpt or "2"
             env = Environment(env_props(n), device="cuda:0", rng=random.Random(1), population="synthetic", seed=5)
             sh = env.shard
             if v.startswith("w"):
-                sh.set_rollout_window(int(v[1:]))
+                sh.set_rollout_window(int(v[1:].partition("h")[0]))
             env._kb_rew = torch.empty((a.ticks, n), dtype=torch.float64, device="cuda:0")
             # one driver window replayed every round: the events time the graph alone (no host drivers)
             env._kb_ticks = env.driver_window(a.ticks)
@@ -67,8 +70,8 @@ def main():
         for v in envs:
             ts = sorted(res[(n, v)])
             med = ts[len(ts) // 2]
-            if v.startswith("w") and int(v[1:]) > 0:
-                k = int(v[1:])
+            if v.startswith("w") and int(v[1:].partition("h")[0]) > 0:
+                k = int(v[1:].partition("h")[0])
                 launches = -(-a.ticks // k)
                 kk = a.ticks // launches
                 gbs = window_bytes(n, kk, "random") / (med * kk) / 1e3
