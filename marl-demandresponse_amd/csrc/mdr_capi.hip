@@ -112,6 +112,7 @@ struct mdr_ctx {
   int overlap_mode = -1;                 // sharded pipeline: -1 calibrate, 0 serial, 1 overlapped
   double calib_us[2] = {0.0, 0.0};       // calibration: us/tick serial, overlapped (max over ranks)
   hipStream_t comm_stream = nullptr;     // per-tick allreduce of the overlapped pipeline
+  hipStream_t cap_stream = nullptr;      // graph capture (graphs are replayed on the caller's stream)
   hipEvent_t ev_k1[kSlabs] = {}, ev_ar[kSlabs] = {}, ev_pc = nullptr;
   hipEvent_t ev[16] = {};
   // MA-PPO actor (row P): packed weight image, per-tick obs scalars of actor rollouts
@@ -386,6 +387,7 @@ int mdr_destroy(mdr_ctx* c) {
   }
   if (c->ev_pc) hipEventDestroy(c->ev_pc);
   if (c->comm_stream) hipStreamDestroy(c->comm_stream);
+  if (c->cap_stream) hipStreamDestroy(c->cap_stream);
   hipFree(c->g_key); hipFree(c->g_key2); hipFree(c->g_ps); hipFree(c->g_incl);
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
@@ -526,6 +528,24 @@ static int stage_ticks(mdr_ctx* c, int n, const mdr_tick* ticks, hipStream_t st)
   return stage_recs(ticks, n, c->d_ticks, st);
 }
 
+// Capture a launch sequence into an executable graph on the context's own capture stream (the
+// capture executes nothing), so the graph can then be launched on ANY caller stream — the null
+// stream included — with no cross-stream synchronisation around each replay.
+template <typename F>
+static int capture_graph(mdr_ctx* c, F&& launches, hipGraphExec_t* out) {
+  if (!c->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
+  hipGraph_t g;
+  HIP_TRY(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
+  const int rc = launches(c->cap_stream);
+  hipError_t e = hipStreamEndCapture(c->cap_stream, &g);
+  if (rc) return rc;
+  if (e != hipSuccess) return fail(MDR_EHIP, std::string("capture: ") + hipGetErrorString(e));
+  e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (e != hipSuccess) return fail(MDR_EHIP, std::string("instantiate: ") + hipGetErrorString(e));
+  return MDR_OK;
+}
+
 // ---- windowed rollout (k_step_window): open-loop action sources, individual_L2
 static bool window_ok(const mdr_ctx* c, int mode) {
   return c->win > 0 && c->d_wslab && c->kp.n_cap <= kWindowCap && c->kp.penalty_mode == MDR_PEN_INDIVIDUAL_L2 &&
@@ -621,20 +641,14 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
     c->counts_ready = false;
     return rc;
   }
-  GraphKey key{n, mode, action, act_stride, reward, rew_stride, p_out, stream};
+  GraphKey key{n, mode, action, act_stride, reward, rew_stride, p_out, nullptr};
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
-    if (st == nullptr) return fail(MDR_EARG, "mdr_rollout: graph capture needs a non-default stream");
-    hipGraph_t g;
-    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st);
-    hipError_t e = hipStreamEndCapture(st, &g);
-    if (rc) return rc;
-    if (e != hipSuccess) return fail(MDR_EHIP, std::string("capture: ") + hipGetErrorString(e));
     hipGraphExec_t ex;
-    e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
-    hipGraphDestroy(g);
-    if (e != hipSuccess) return fail(MDR_EHIP, std::string("instantiate: ") + hipGetErrorString(e));
+    rc = capture_graph(c, [&](hipStream_t cs) {
+      return rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, cs);
+    }, &ex);
+    if (rc) return rc;
     it = c->graphs.emplace(key, std::make_pair(ex, c->ring)).first;
   }
   HIP_TRY(hipGraphLaunch(it->second.first, st));
@@ -1158,8 +1172,8 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
   if (int rc = stage_recs(osc, n, c->d_obs_sc, st)) return rc;
 
   ObsArgs o = obs_args(c, sp, &osc[0]);
-  auto launches = [&]() -> int {
-    HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
+  auto launches = [&](hipStream_t ls) -> int {
+    HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), ls));
     c->ring = 0;
     for (int t = 0; t < n; ++t) {
       // the current slab is zero here: the memset above (t = 0), then the previous two steps
@@ -1168,36 +1182,27 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
       ot.sc_dev = c->d_obs_sc + 4 * t;
       ActorOut out{action ? action + (int64_t)t * act_stride : c->d_act, prob ? prob + (int64_t)t * prob_stride : nullptr,
                    nullptr, nullptr, slab_at(c, c->ring), nullptr};
-      if (int rc = launch_actor(c, sp, ot, p_dev, 0, c->d_ticks + t, out, st)) return rc;
+      if (int rc = launch_actor(c, sp, ot, p_dev, 0, c->d_ticks + t, out, ls)) return rc;
       if (int rc = launch_step(c, out.action, MDR_ACT_BUFFER, TickArgs{}, c->d_ticks + t,
-                               reward + (int64_t)t * rew_stride, 0, MDR_CTRL_NONE, nullptr, p_dev, st))
+                               reward + (int64_t)t * rew_stride, 0, MDR_CTRL_NONE, nullptr, p_dev, ls))
         return rc;
     }
     return MDR_OK;
   };
   if (!action && !c->d_act) HIP_TRY(hipMalloc(&c->d_act, c->kp.n));  // context-owned action row
   if (!use_graph) {
-    const int rc = launches();
+    const int rc = launches(st);
     c->counts_ready = false;
     return rc;
   }
-  if (st == nullptr) return fail(MDR_EARG, "mdr_actor_rollout: graph capture needs a non-default stream");
   std::vector<int64_t> key{n, (int64_t)(uintptr_t)action, act_stride, (int64_t)(uintptr_t)prob, prob_stride,
                            (int64_t)(uintptr_t)reward, rew_stride, (int64_t)(uintptr_t)p_dev,
-                           (int64_t)(uintptr_t)stream, (int64_t)(uintptr_t)sp->comm_table,
+                           (int64_t)(uintptr_t)sp->comm_table,
                            (int64_t)(uintptr_t)sp->halo_msg, sp->n_feat, (int64_t)(uintptr_t)c->d_actor};
   auto it = c->actor_graphs.find(key);
   if (it == c->actor_graphs.end()) {
-    hipGraph_t g;
-    HIP_TRY(hipStreamBeginCapture(st, hipStreamCaptureModeThreadLocal));
-    const int rc = launches();
-    hipError_t e = hipStreamEndCapture(st, &g);
-    if (rc) return rc;
-    if (e != hipSuccess) return fail(MDR_EHIP, std::string("capture: ") + hipGetErrorString(e));
     hipGraphExec_t ex;
-    e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
-    hipGraphDestroy(g);
-    if (e != hipSuccess) return fail(MDR_EHIP, std::string("instantiate: ") + hipGetErrorString(e));
+    if (int rc = capture_graph(c, launches, &ex)) return rc;
     it = c->actor_graphs.emplace(key, ex).first;
   } else {
     c->ring = n % 3;

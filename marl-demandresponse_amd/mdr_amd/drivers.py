@@ -67,6 +67,11 @@ def od_temp(t: _dt.datetime, temp_prop, rng=_random):
     return temperature
 
 
+def od_daily(hour: int, minute: int, temp_prop):
+    """The deterministic (daily sinusoid) part of od_temp, as np.float64."""
+    return _od_det(hour, minute, temp_prop.day_temp, temp_prop.night_temp, temp_prop.phase)
+
+
 @functools.lru_cache(maxsize=1 << 12)
 def _od_det(hour: int, minute: int, day_temp, night_temp, phase):
     amplitude = (day_temp - night_temp) / 2.0
@@ -198,6 +203,32 @@ class GridSignal:
                 self._memo.clear()
             self._memo[key] = self.current_signal
         return self.current_signal
+
+    def signal_series(self, sod) -> np.ndarray:
+        """``step`` at a series of ticks (seconds of day ``sod``, int64 array) for a constant base
+        power: the same IEEE operations as the per-tick path, elementwise (float64 array)."""
+        base = self.base_power()
+        sp = self.signal.sp
+        mode = self.signal.mode
+        n = len(sod)
+        if mode == "flat":
+            s = np.full(n, base, np.float64)
+        elif mode == "sinusoidals":
+            amplitudes = [base * r for r in sp.amplitude_ratios]
+            if len(sp.periods) != len(amplitudes):
+                raise ValueError("Power grid signal parameters: periods and amplitude_ratios lists "
+                                 "should have the same length.")
+            s = np.full(n, base, np.float64)
+            for k, period in enumerate(sp.periods):
+                s = s + amplitudes[k] * np.sin(2 * np.pi * sod / period)
+        elif mode == "regular_steps":
+            amplitude = sp.amplitude_per_hvac * self.nb_agents
+            ratio = base / amplitude
+            s = amplitude * np.heaviside((sod % sp.period) - (1 - ratio) * sp.period, 1)
+        else:
+            raise ValueError(f"no series form for signal mode {mode!r}")
+        s = s * self.gp.artificial_ratio
+        return np.minimum(s, self.max_power)
 
     def get_obs(self):
         return {"reg_signal": self.current_signal}

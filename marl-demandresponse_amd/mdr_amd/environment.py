@@ -24,12 +24,21 @@ import numpy as np
 
 from . import _lib as L
 from . import config as cfgmod
+from . import drivers
 from . import population as popmod
 from .drivers import GridSignal, od_temp, reward_normalisers, solar_gain
 from .shard import HipShard, encode_hvac
 
 ACTION_MODES = {"buffer": L.ACT_BUFFER, "random": L.ACT_RANDOM, "always_on": L.ACT_ALWAYS_ON,
                 "bangbang": L.ACT_BANGBANG, "deadband_bangbang": L.ACT_DEADBAND_BANGBANG}
+
+
+def _runs(key: np.ndarray):
+    """(values of the runs of equal consecutive keys as ints, run index of every element)."""
+    chg = np.empty(key.shape[0], bool)
+    chg[0] = True
+    np.not_equal(key[1:], key[:-1], out=chg[1:])
+    return key[chg].tolist(), np.cumsum(chg) - 1
 
 
 class TickWindow:
@@ -339,6 +348,69 @@ class Environment:
             raise NotImplementedError("random_sample comm mode draws per tick; use step()")
         if self._grid_pending:
             raise RuntimeError("a deferred grid step is pending: run the previous window, then finish_grid_step()")
+        if n_ticks >= 2 and self._vector_drivers_ok():
+            return self._driver_window_vec(n_ticks)
+        return self._driver_window_loop(n_ticks)
+
+    def _vector_drivers_ok(self) -> bool:
+        g = self.power_grid
+        st = self.init_props.time_step
+        return (g.interp is None and g.signal_fn is None and g.signal.mode in ("flat", "sinusoidals", "regular_steps")
+                and st.microseconds == 0 and st.days == 0 and st.seconds > 0)
+
+    def _driver_window_vec(self, n: int) -> "TickWindow":
+        """driver_window for a constant base power and a flat / sinusoidal / regular-steps signal,
+        evaluated over the whole window at once — the same values as the per-tick loop, bit for
+        bit (tests/test_host_logic.py): solar gain and the daily outdoor-temperature curve are
+        computed once per distinct (day, minute) with the scalar code; the n gauss draws come in
+        the reference order (nothing else draws in between); the signal and the gauss additions
+        are the same IEEE operations elementwise (NumPy's vectorised sin equals its scalar sin)."""
+        p = self.init_props
+        hp = p.cluster_prop.house_prop
+        tp, rng, grid = p.temp_prop, self.rng, self.power_grid
+        dts = p.time_step.seconds
+        d0 = self.date_time
+        s0 = d0.hour * 3600 + d0.minute * 60 + d0.second
+        abs_s = s0 + dts * np.arange(1, n + 1, dtype=np.int64)  # seconds since d0's midnight
+        day_off, sod = np.divmod(abs_s, 86400)
+        mod = sod // 60  # minute of the day
+        # solar gain of every tick's NEW datetime (environment.py:86-88, building.py:176-179)
+        if hp.solar_gain:
+            uk, inv = _runs(day_off * 1440 + mod)
+            day0 = d0.replace(hour=0, minute=0, second=0, microsecond=0)
+            vals = []
+            for k in uk:
+                dd = day0 + _dt.timedelta(days=k // 1440)
+                vals.append(solar_gain(dd.replace(hour=(k % 1440) // 60, minute=k % 60), hp.window_area,
+                                       hp.shading_coeff))
+            sol = np.asarray(vals, np.float64)[inv]
+            sol_last = vals[-1]
+        else:
+            sol = np.zeros(n)
+            sol_last = 0.0
+        # outdoor temperature: the daily curve of each tick + one gauss per tick, in tick order
+        um, minv = _runs(mod)
+        det = np.asarray([drivers.od_daily(m // 60, m % 60, tp) for m in um], np.float64)[minv]
+        gs = np.fromiter((rng.gauss(0, tp.temp_std) for _ in range(n)), np.float64, n)
+        tod = det + gs
+        # regulation signal after each tick (power_grid.py:80-102, signal_calculator.py:33-98)
+        sig = grid.signal_series(sod)
+        buf = np.empty((n, 4), np.float64)
+        buf[0, 0] = self.current_od_temp
+        buf[1:, 0] = tod[:-1]
+        buf[:, 1] = sol
+        buf[0, 2] = grid.current_signal
+        buf[1:, 2] = sig[:-1]
+        tick0 = self._tick
+        buf[:, 3].view(np.uint64)[:] = np.arange(tick0, tick0 + n, dtype=np.uint64)
+        self.date_time = d0 + p.time_step * n
+        self._solar, self._tick = sol_last, tick0 + n
+        self._tod_prev, self._s_prev = tod[-2], sig[-2]
+        self.current_od_temp = tod[-1]
+        grid.current_signal = sig[-1]
+        return TickWindow(buf)
+
+    def _driver_window_loop(self, n_ticks: int) -> "TickWindow":
         p = self.init_props
         hp = p.cluster_prop.house_prop
         dts = p.time_step.seconds

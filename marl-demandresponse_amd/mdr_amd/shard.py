@@ -166,32 +166,17 @@ class HipShard:
                 "mdr_reward_finalize")
 
     def rollout(self, ticks, action, act_stride, mode, reward, rew_stride, use_graph=True):
-        """Many ticks in one C call (``ticks``: a TickWindow).  Graph capture needs a non-default
-        stream: the rollout runs on the shard's own stream, ordered after / before the caller's
-        current stream."""
-        torch = self.torch
-        cur = torch.cuda.current_stream(self.device)
-        if use_graph:
-            s = self.launch_stream(True)
-            s.wait_stream(cur)
-            handle = s.cuda_stream
-        else:
-            handle = cur.cuda_stream
+        """Many ticks in one C call (``ticks``: a TickWindow), on the caller's current stream; with
+        ``use_graph`` the launch sequence is captured once (on the library's capture stream) and
+        replayed as a hipGraph."""
         L.check(self.lib.mdr_rollout(self.ctx, len(ticks), ticks.ptr(), L.ptr(action), act_stride, mode,
-                                     L.ptr(reward), rew_stride, L.ptr(self.p_dev), int(use_graph), handle),
+                                     L.ptr(reward), rew_stride, L.ptr(self.p_dev), int(use_graph), self.stream()),
                 "mdr_rollout")
-        if use_graph:
-            cur.wait_stream(self._side)
 
     def launch_stream(self, use_graph=True):
-        """The torch stream rollout kernels run on (the shard's side stream for graph rollouts,
-        else the caller's current stream) — where timing events must be recorded."""
-        torch = self.torch
-        if not use_graph:
-            return torch.cuda.current_stream(self.device)
-        if getattr(self, "_side", None) is None:
-            self._side = torch.cuda.Stream(self.device)
-        return self._side
+        """The torch stream rollout kernels run on (the caller's current stream) — where timing
+        events must be recorded."""
+        return self.torch.cuda.current_stream(self.device)
 
     def greedy(self, budget: float, action):
         L.check(self.lib.mdr_ctrl_greedy(self.ctx, float(budget), L.ptr(action), self.stream()),
@@ -215,24 +200,15 @@ class HipShard:
 
     def actor_rollout(self, ticks, obs_sc, spec, action, act_stride, prob, prob_stride, reward, rew_stride,
                       use_graph=True):
-        """n ticks of actor -> step in one C call (graph-captured on the shard's side stream).
+        """n ticks of actor -> step in one C call (graph-captured, replayed on the current stream).
         ``ticks``: TickWindow; ``obs_sc``: float64 [n, 4] array in the mdr_obs_scalars layout."""
         n = len(ticks)
         obs_sc = np.ascontiguousarray(obs_sc, np.float64)
         assert obs_sc.shape == (n, 4)
-        torch = self.torch
-        cur = torch.cuda.current_stream(self.device)
-        if use_graph:
-            s = self.launch_stream(True)
-            s.wait_stream(cur)
-            handle = s.cuda_stream
-        else:
-            handle = cur.cuda_stream
-        L.check(self.lib.mdr_actor_rollout(self.ctx, n, ticks.ptr(), obs_sc.ctypes.data, C.byref(spec), L.ptr(action), act_stride,
-                                           L.ptr(prob), prob_stride, L.ptr(reward), rew_stride, L.ptr(self.p_dev),
-                                           int(use_graph), handle), "mdr_actor_rollout")
-        if use_graph:
-            cur.wait_stream(self._side)
+        L.check(self.lib.mdr_actor_rollout(self.ctx, n, ticks.ptr(), obs_sc.ctypes.data, C.byref(spec),
+                                           L.ptr(action), act_stride, L.ptr(prob), prob_stride, L.ptr(reward),
+                                           rew_stride, L.ptr(self.p_dev), int(use_graph), self.stream()),
+                "mdr_actor_rollout")
 
     def actor_rollout_sharded(self, ticks, obs_sc, spec, action, act_stride, prob, prob_stride, reward,
                               rew_stride):
