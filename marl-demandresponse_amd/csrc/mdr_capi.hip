@@ -531,7 +531,7 @@ static int stage_ticks(mdr_ctx* c, int n, const mdr_tick* ticks, hipStream_t st)
 // Capture a launch sequence into an executable graph on the context's own capture stream (the
 // capture executes nothing), so the graph can then be launched on ANY caller stream — the null
 // stream included — with no cross-stream synchronisation around each replay.
-template <typename F>
+extern "C++" template <typename F>
 static int capture_graph(mdr_ctx* c, F&& launches, hipGraphExec_t* out) {
   if (!c->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
   hipGraph_t g;
