@@ -79,6 +79,8 @@ def parse():
     ap.add_argument("--kernel-ticks", type=int, default=512,
                     help="ticks of the kernel-only timing after the timed region (roofline.kernel_avg_us)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline time budget")
+    ap.add_argument("--clock-warmup", type=float, default=0.2,
+                    help="seconds of non-environment device work before the timed region (GPU clock ramp)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--mode", default="random", choices=["random", "buffer"])
     ap.add_argument("--workload", default="step", choices=["step", "actor", "greedy"],
@@ -289,6 +291,15 @@ def main():
 
             dist.barrier()
 
+    # the cpu_baseline (or a short warmup) leaves the GPU on idle clocks: ~0.2 s of unrelated device
+    # work (a buffer increment; no environment state is touched) before the timed region
+    spin = torch.zeros(1 << 26, dtype=torch.float32, device=dev)
+    t_spin = time.perf_counter()
+    while time.perf_counter() - t_spin < args.clock_warmup:
+        for _ in range(8):
+            spin.add_(1.0)
+        torch.cuda.synchronize()
+    del spin
     barrier()
     torch.cuda.synchronize()
     # HIP events on the stream the step launches are issued on (the graph side stream)
@@ -392,7 +403,9 @@ def main():
                                   "per-window power counts)" if comm is not None else "1 GPU"},
         "timed_region": {"wall_s": elapsed, "launch_stream_event_ms": gpu_ms,
                          "includes": "host drivers (OD-temperature RNG, solar, signal) + tick staging + "
-                                     "graph launches + device work"},
+                                     "graph launches + device work",
+                         "before": f"{args.warmup} warmup steps (graph capture of every chunk size) and "
+                                   f"{args.clock_warmup:.2f} s of non-environment device work (GPU clock ramp)"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kern,
                      "kernel_avg_us": kern_ms * 1e3, "launches_timed": launches,

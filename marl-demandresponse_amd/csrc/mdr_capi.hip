@@ -329,7 +329,8 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   if (const char* e = getenv("MDR_WIN_HPT")) c->win_hpt = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("MDR_WINDOW")) c->win = atoi(e) < 0 ? 0 : atoi(e) > kWindowMax ? kWindowMax : atoi(e);
   if (cfg->n_cap <= kWindowCap) {
-    c->wslab_len = kWindowMax * kCountShards * cfg->n_cap;
+    // a window count slot: sharded slab | reduced counts | blocks-done counter (mdr_kernels.hip)
+    c->wslab_len = kWindowMax * kCountShards * cfg->n_cap + kWindowMax * cfg->n_cap + 1;
     if (hipMalloc(&c->d_wslab, 3 * sizeof(unsigned long long) * c->wslab_len) != hipSuccess)
       return cleanup(fail(MDR_ENOMEM, "window count slabs"));
   } else {
@@ -577,15 +578,19 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     if (hpt == 1) MDR_WIN_DISPATCH_H(KERNEL, 1, __VA_ARGS__);            \
     else MDR_WIN_DISPATCH_H(KERNEL, 2, __VA_ARGS__);                     \
   } while (0)
+  const int ncap = c->kp.n_cap;
+  auto red = [&](int w) { return slab(w) + (size_t)kWindowMax * kCountShards * ncap; };
   MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, wsz(0), slab(0));
   LAUNCH_CHECK("k_count_window");
   int t0 = 0;
   for (int w = 0; w < nw; ++w) {
     const int K = wsz(w), la = w + 1 < nw ? wsz(w + 1) : 0;
-    if (comm) RCCL_TRY(ncclAllReduce(slab(w), slab(w), (size_t)K * c->slab_len, ncclUint64, ncclSum, comm, st));
+    // sharded: every rank's per-tick class counts are summed (exact integers) before the launch
+    if (comm) RCCL_TRY(ncclAllReduce(red(w), red(w), (size_t)K * ncap, ncclUint64, ncclSum, comm, st));
     const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
-    MDR_WIN_DISPATCH(k_step_window, kp, a, act_stride, tk + t0, K, la, slab(w), reward + (int64_t)t0 * rew_stride,
-                     rew_stride, w == nw - 1 ? p_out : nullptr, slab(w + 1), slab(w + 2), c->wslab_len);
+    MDR_WIN_DISPATCH(k_step_window, kp, a, act_stride, tk + t0, K, la, red(w), reward + (int64_t)t0 * rew_stride,
+                     rew_stride, w == nw - 1 ? p_out : nullptr, slab(w + 1), slab(w + 2),
+                     kWindowMax * kCountShards * ncap);
     LAUNCH_CHECK("k_step_window");
     t0 += K;
   }

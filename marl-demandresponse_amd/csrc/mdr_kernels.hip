@@ -651,14 +651,40 @@ __device__ __forceinline__ void win_count(const KParams& p, const uint32_t* w_in
   }
 }
 
-__device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsigned* hist,
-                                          unsigned long long* slab) {
-  for (int e = threadIdx.x; e < nt * p.n_cap; e += blockDim.x) {
-    const int j = e / p.n_cap, c = e - j * p.n_cap;
+// Window count slot layout (u64): [slab: kWinMax][kCountShards][n_cap] | [red: kWinMax][n_cap] |
+// [blocks-done counter].  Producers accumulate the block histograms into the sharded slab; the
+// LAST block to finish reduces the shards into red (exact integer counts per tick and class) and
+// re-arms the counter, so a consumer reads n_cap counts per tick instead of 64 * n_cap.
+__device__ __forceinline__ unsigned long long* win_red(unsigned long long* slot, int n_cap) {
+  return slot + (size_t)kWinMax * kCountShards * n_cap;
+}
+
+__device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsigned* hist, unsigned long long* slot) {
+  __shared__ bool s_last;
+  const int ncap = p.n_cap;
+  for (int e = threadIdx.x; e < nt * ncap; e += blockDim.x) {
+    const int j = e / ncap, c = e - j * ncap;
     const unsigned v = hist[j * kWinCap + c];
-    if (v) atomicAdd(&slab[((size_t)j * kCountShards + blockIdx.x % kCountShards) * p.n_cap + c],
+    if (v) atomicAdd(&slot[((size_t)j * kCountShards + blockIdx.x % kCountShards) * ncap + c],
                      (unsigned long long)v);
   }
+  __threadfence();  // this block's slab atomics are visible device-wide before it signals
+  __syncthreads();
+  unsigned long long* red = win_red(slot, ncap);
+  unsigned long long* done = red + (size_t)kWinMax * ncap;
+  if (threadIdx.x == 0) s_last = atomicAdd(done, 1ull) == (unsigned long long)gridDim.x - 1ull;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();
+  for (int e = threadIdx.x; e < nt * ncap; e += blockDim.x) {
+    const int j = e / ncap, c = e - j * ncap;
+    unsigned long long sum = 0;
+    for (int q = 0; q < kCountShards; ++q)
+      sum += __hip_atomic_load(&slot[((size_t)j * kCountShards + q) * ncap + c], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    red[j * ncap + c] = sum;
+  }
+  if (threadIdx.x == 0) *done = 0ull;  // re-armed for the slot's next use
 }
 
 // the wave tile: 64 * HPT consecutive houses, HPT per lane; groups of 64 global ids it spans
@@ -687,7 +713,7 @@ struct WinTile {
 template <int ACT, int HPT>
 __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* __restrict__ action,
                                                       int64_t act_stride, const TickArgs* __restrict__ tkp, int nt,
-                                                      unsigned long long* __restrict__ slab) {
+                                                      unsigned long long* __restrict__ slot) {
   __shared__ uint2 s_rw[4][3 * kWinMax];
   __shared__ unsigned s_hist[kWinMax * kWinCap];
   const int tid = threadIdx.x, wv = tid >> 6;
@@ -706,7 +732,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
   __syncthreads();
   win_count<ACT, HPT>(p, w, cls, t.v, t.i0, t.gid0, s_rw[wv], t.G, t.g0, 0, nt, action, act_stride, s_hist);
   __syncthreads();
-  win_flush(p, nt, s_hist, slab);
+  win_flush(p, nt, s_hist, slot);
 }
 
 // MDR_WIN_WAVES (build-time A/B knob): cap k_step_window at that many waves per SIMD
@@ -716,15 +742,16 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
 #define MDR_WIN_OCC
 #endif
 
-// One window of K ticks.  counts: slabs of ticks 0..K-1 (complete, global); la_K > 0: run the
-// FSM on through the next la_K ticks (tkp[K..K+la_K), action rows K..) and accumulate their ON
-// counts into next_slab; block 0 zeroes zero_slab (zero_len u64) for the launch after next.
+// One window of K ticks.  red: the ticks' global ON counts per class [K][n_cap] (reduced by the
+// previous launch, allreduced across ranks when sharded); la_K > 0: run the FSM on through the
+// next la_K ticks (tkp[K..K+la_K), action rows K..) and count them into next_slot; block 0 zeroes
+// the slab part (zero_len u64) of zero_slot for the launch after next.
 template <int ACT, int HPT>
 __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, const uint8_t* __restrict__ action,
                                                      int64_t act_stride, const TickArgs* __restrict__ tkp, int K,
-                                                     int la_K, const unsigned long long* __restrict__ counts,
+                                                     int la_K, const unsigned long long* __restrict__ red,
                                                      double* __restrict__ reward, int64_t rew_stride,
-                                                     double* p_out, unsigned long long* next_slab,
+                                                     double* p_out, unsigned long long* next_slot,
                                                      unsigned long long* zero_slab, int zero_len) {
   __shared__ uint2 s_rw[4][3 * 2 * kWinMax];
   __shared__ unsigned s_hist[kWinMax * kWinCap];
@@ -765,12 +792,7 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   if (lane < K) {
     tod_l = tkp[lane].t_od_prev;  // the window's drivers, lane j <- tick j (readlane per tick)
     sol_l = tkp[lane].solar;
-    const unsigned long long* cj = counts + (size_t)lane * kCountShards * p.n_cap;
-    for (int k = 0; k < p.n_cap; ++k) {
-      unsigned long long c = 0;
-      for (int q = 0; q < kCountShards; ++q) c += cj[q * p.n_cap + k];
-      P_l += (double)c * p.p_on[k];
-    }
+    for (int k = 0; k < p.n_cap; ++k) P_l += (double)red[lane * p.n_cap + k] * p.p_on[k];
     const double x = (P_l - tkp[lane].s_prev) / (double)p.n_global;
     sig_l = p.alpha_sig * (x * x) / p.norm_sig;
   }
@@ -855,7 +877,7 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
     win_count<ACT, HPT>(p, w, cls, t.v, i0, t.gid0, s_rw[wv], t.G, t.g0, K, la_K,
                         ACT == MDR_ACT_BUFFER ? action : nullptr, act_stride, s_hist);
     __syncthreads();
-    win_flush(p, la_K, s_hist, next_slab);
+    win_flush(p, la_K, s_hist, next_slot);
   }
 }
 
