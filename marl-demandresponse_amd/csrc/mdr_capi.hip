@@ -329,8 +329,8 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   if (const char* e = getenv("MDR_WIN_HPT")) c->win_hpt = atoi(e) == 1 ? 1 : 2;
   if (const char* e = getenv("MDR_WINDOW")) c->win = atoi(e) < 0 ? 0 : atoi(e) > kWindowMax ? kWindowMax : atoi(e);
   if (cfg->n_cap <= kWindowCap) {
-    // a window count slot: sharded slab | reduced counts | blocks-done counter (mdr_kernels.hip)
-    c->wslab_len = kWindowMax * kCountShards * cfg->n_cap + kWindowMax * cfg->n_cap + 1;
+    // a window count slot: sharded slab | reduced counts (mdr_kernels.hip)
+    c->wslab_len = kWindowMax * kCountShards * cfg->n_cap + kWindowMax * cfg->n_cap;
     if (hipMalloc(&c->d_wslab, 3 * sizeof(unsigned long long) * c->wslab_len) != hipSuccess)
       return cleanup(fail(MDR_ENOMEM, "window count slabs"));
   } else {
@@ -585,6 +585,8 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
   int t0 = 0;
   for (int w = 0; w < nw; ++w) {
     const int K = wsz(w), la = w + 1 < nw ? wsz(w + 1) : 0;
+    hipLaunchKernelGGL(k_win_reduce, dim3(1), dim3(256), 0, st, slab(w), K, ncap);
+    LAUNCH_CHECK("k_win_reduce");
     // sharded: every rank's per-tick class counts are summed (exact integers) before the launch
     if (comm) RCCL_TRY(ncclAllReduce(red(w), red(w), (size_t)K * ncap, ncclUint64, ncclSum, comm, st));
     const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;

@@ -91,6 +91,7 @@ __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stri
                               int la_K, const unsigned long long* counts, double* reward, int64_t rew_stride,
                               double* p_out, unsigned long long* next_slab, unsigned long long* zero_slab,
                               int zero_len);
+__global__ void k_win_reduce(unsigned long long* slot, int nt, int n_cap);
 template <int ACT, int HPT>
 __global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int nt,
                                unsigned long long* slab);

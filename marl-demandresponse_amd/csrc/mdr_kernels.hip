@@ -651,16 +651,17 @@ __device__ __forceinline__ void win_count(const KParams& p, const uint32_t* w_in
   }
 }
 
-// Window count slot layout (u64): [slab: kWinMax][kCountShards][n_cap] | [red: kWinMax][n_cap] |
-// [blocks-done counter].  Producers accumulate the block histograms into the sharded slab; the
-// LAST block to finish reduces the shards into red (exact integer counts per tick and class) and
-// re-arms the counter, so a consumer reads n_cap counts per tick instead of 64 * n_cap.
+// Window count slot layout (u64): [slab: kWinMax][kCountShards][n_cap] | [red: kWinMax][n_cap].
+// Producers accumulate their block histograms into the sharded slab; k_win_reduce (one block,
+// the next graph node: the kernel boundary makes every producer atomic visible — an in-kernel
+// last-block reduction would need an agent-scope release fence per block, i.e. an L2 write-back
+// on this multi-XCD chip) sums the shards into red, the exact per-tick class counts a consumer
+// reads (n_cap values per tick instead of kCountShards * n_cap).
 __device__ __forceinline__ unsigned long long* win_red(unsigned long long* slot, int n_cap) {
   return slot + (size_t)kWinMax * kCountShards * n_cap;
 }
 
 __device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsigned* hist, unsigned long long* slot) {
-  __shared__ bool s_last;
   const int ncap = p.n_cap;
   for (int e = threadIdx.x; e < nt * ncap; e += blockDim.x) {
     const int j = e / ncap, c = e - j * ncap;
@@ -668,23 +669,16 @@ __device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsign
     if (v) atomicAdd(&slot[((size_t)j * kCountShards + blockIdx.x % kCountShards) * ncap + c],
                      (unsigned long long)v);
   }
-  __threadfence();  // this block's slab atomics are visible device-wide before it signals
-  __syncthreads();
-  unsigned long long* red = win_red(slot, ncap);
-  unsigned long long* done = red + (size_t)kWinMax * ncap;
-  if (threadIdx.x == 0) s_last = atomicAdd(done, 1ull) == (unsigned long long)gridDim.x - 1ull;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();
-  for (int e = threadIdx.x; e < nt * ncap; e += blockDim.x) {
-    const int j = e / ncap, c = e - j * ncap;
+}
+
+__global__ void __launch_bounds__(256) k_win_reduce(unsigned long long* __restrict__ slot, int nt, int n_cap) {
+  unsigned long long* red = win_red(slot, n_cap);
+  for (int e = threadIdx.x; e < nt * n_cap; e += blockDim.x) {
+    const int j = e / n_cap, c = e - j * n_cap;
     unsigned long long sum = 0;
-    for (int q = 0; q < kCountShards; ++q)
-      sum += __hip_atomic_load(&slot[((size_t)j * kCountShards + q) * ncap + c], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    red[j * ncap + c] = sum;
+    for (int q = 0; q < kCountShards; ++q) sum += slot[((size_t)j * kCountShards + q) * n_cap + c];
+    red[j * n_cap + c] = sum;
   }
-  if (threadIdx.x == 0) *done = 0ull;  // re-armed for the slot's next use
 }
 
 // the wave tile: 64 * HPT consecutive houses, HPT per lane; groups of 64 global ids it spans
