@@ -45,9 +45,8 @@ BF16_PEAK_TFS = 2516.6     # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 
 def step_kernel_name(n_loc: int, mode: str, window: int) -> str:
     """The step kernel the library launches for this bench (mdr_capi.hip: window_launches /
     launch_step_on)."""
-    act = {"random": "MDR_ACT_RANDOM", "buffer": "MDR_ACT_BUFFER"}[mode]
-    if window > 0:
-        return f"mdr::k_step_window<{act}>"
+    if window > 0:  # the rocprofv3 spelling: k_step_window<ACT, HPT=2> (MDR_ACT_RANDOM = 1, _BUFFER = 0)
+        return f"void mdr::k_step_window<{1 if mode == 'random' else 0}, 2>"
     if any(k in os.environ for k in ("MDR_HPT", "MDR_VARIANT", "MDR_FASTDIV")):
         return "mdr::k_step (variant chosen by MDR_* env)"
     tpw = int(os.environ.get("MDR_TPW", 2 if n_loc <= 1572864 else 4))
@@ -305,6 +304,9 @@ def main():
     # HIP events on the stream the step launches are issued on (the graph side stream)
     launch_stream = env.rollout_stream(use_graph=g_act is None)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for ev in (ev0, ev1):  # torch creates the HIP event on its first record(): not inside the timed region
+        ev.record(launch_stream)
+    torch.cuda.synchronize()
     t0 = time.perf_counter()
     ev0.record(launch_stream)
     for c in chunks:

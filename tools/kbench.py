@@ -49,9 +49,11 @@ def main():
                 sh.rollout(env._kb_ticks, None, 0, L.ACT_RANDOM, env._kb_rew, n, True)  # captures the graph
             envs[v] = env
         torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()  # torch creates the HIP events lazily on the first record(): not inside a timing
+        e1.record()
         for r in range(a.rounds):
             for v, env in envs.items():
-                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 sh = env.shard
                 if v == "probe":
                     e0.record()

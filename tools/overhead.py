@@ -53,6 +53,18 @@ def main():
             print(f"idle {idle:5.0f} ms rep {r}: drivers {1e6 * (t1 - t0):7.1f} us  C rollout call "
                   f"{1e6 * (t2 - t1):7.1f} us  sync wait {1e6 * (t3 - t2):7.1f} us  wall {1e6 * (t3 - t0):7.1f} us  "
                   f"event window {1e3 * e0.elapsed_time(e1):7.1f} us", flush=True)
+    # the bench's own call: Environment.rollout (drivers + C call), one timed region per rep
+    for r in range(a.reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(ls)
+        env.rollout(T, rewards=rew)
+        t1 = time.perf_counter()
+        e1.record(ls)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        print(f"env.rollout rep {r}: call {1e6 * (t1 - t0):7.1f} us  wall {1e6 * (t2 - t0):7.1f} us  "
+              f"event window {1e3 * e0.elapsed_time(e1):7.1f} us", flush=True)
     # device-only replay of the same graph (no host drivers): the floor of the timed region
     for r in range(3):
         torch.cuda.synchronize()
