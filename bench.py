@@ -81,6 +81,8 @@ def parse():
     ap.add_argument("--clock-warmup", type=float, default=0.2,
                     help="seconds of non-environment device work before the timed region (GPU clock ramp)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--trace", action="store_true",
+                    help="print host phase timestamps of the timed region to stderr (diagnostics)")
     ap.add_argument("--mode", default="random", choices=["random", "buffer"])
     ap.add_argument("--workload", default="step", choices=["step", "actor", "greedy"],
                     help="step: env.step with fused random actions (the BASELINE metric); actor: "
@@ -307,13 +309,35 @@ def main():
     for ev in (ev0, ev1):  # torch creates the HIP event on its first record(): not inside the timed region
         ev.record(launch_stream)
     torch.cuda.synchronize()
+    trace = []
+    if args.trace:  # wrap the two host phases of a rollout call with timestamps
+        dw, ro = env.driver_window, sh.rollout
+
+        def _dw(*a, **k):
+            trace.append(("drivers>", time.perf_counter()))
+            r = dw(*a, **k)
+            trace.append(("drivers<", time.perf_counter()))
+            return r
+
+        def _ro(*a, **k):
+            trace.append(("C call>", time.perf_counter()))
+            r = ro(*a, **k)
+            trace.append(("C call<", time.perf_counter()))
+            return r
+
+        env.driver_window, sh.rollout = _dw, _ro
     t0 = time.perf_counter()
     ev0.record(launch_stream)
     for c in chunks:
         run(c)
     ev1.record(launch_stream)
+    t_sub = time.perf_counter()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if args.trace:
+        env.driver_window, sh.rollout = dw, ro
+        print("trace (us from t0): " + ", ".join(f"{k} {1e6 * (t - t0):.1f}" for k, t in trace) +
+              f", submitted {1e6 * (t_sub - t0):.1f}, synchronized {1e6 * (t1 - t0):.1f}", file=sys.stderr)
     barrier()
     elapsed = t1 - t0
     gpu_ms = ev0.elapsed_time(ev1)

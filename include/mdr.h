@@ -246,6 +246,15 @@ int mdr_obs(mdr_ctx* ctx, const mdr_obs_spec* spec, const mdr_obs_scalars* sc,
  * rows [0, hi) = first hi houses, rows [hi, hi + lo) = last lo houses. */
 int mdr_halo_pack(mdr_ctx* ctx, const mdr_obs_spec* spec, float* out, void* stream);
 
+/* ---- cluster statistics for the server's Metrics / UI summary ----------- */
+/* One deterministic reduction over the shard's state (+ reward, may be NULL) into out[12] (device
+ * doubles): sum(T - target/N), sum|T - target/N|, max(0, max(T - target/N)), sum (T - target/N)^2,
+ * sum reward/N (Metrics.update, metrics_service.py:108-157, its operator precedence kept),
+ * sum T, sum (T - target), sum |T - target|, sum T_mass, sum target, #lockout, #on
+ * (ClientManagerService, client_manager_service.py:62-111,177-196).  Sharded: sum-allreduce all but
+ * out[2] (max-allreduce). */
+int mdr_cluster_stats(mdr_ctx* ctx, const double* reward, double* out, void* stream);
+
 /* ---- greedy-myopic controller (greedy_myopic_controller.py:67-104) --------------------- */
 /* Next actions for the whole shard (single GPU: shard = cluster) from the current state: order
  * by -(T - target) ascending, then the reference's sequential take rule with budget S. */

@@ -124,6 +124,7 @@ struct mdr_ctx {
   double* d_obs_sc = nullptr;  // [ticks_cap][4]
   uint8_t* d_act = nullptr;    // [n_local] actor actions when the caller keeps none
   float* d_halo = nullptr;     // sharded actor rollout: packed edge rows | received ring halo
+  double* d_stats = nullptr;   // k_cluster_stats block partials
   size_t halo_bytes = 0;
   std::map<std::vector<int64_t>, hipGraphExec_t> actor_graphs;
   // interpolated base power (row a10): grid | table | capacities
@@ -371,6 +372,7 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->d_interp);
   hipFree(c->d_act);
   hipFree(c->d_halo);
+  hipFree(c->d_stats);
   hipFree(c->d_obs_sc);
   hipFree(c->d_tables);
   hipFree(c->d_coef);
@@ -970,6 +972,18 @@ int mdr_set_rollout_window(mdr_ctx* c, int ticks) {
   return MDR_OK;
 }
 
+int mdr_cluster_stats(mdr_ctx* c, const double* reward, double* out, void* stream) {
+  if (!c || !out) return fail(MDR_EARG, "mdr_cluster_stats: null argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_cluster_stats: context not bound");
+  if (!c->d_stats) HIP_TRY(hipMalloc(&c->d_stats, sizeof(double) * kStats * kStatsBlocks));
+  const unsigned nb = (unsigned)std::min<int64_t>(kStatsBlocks, (c->kp.n + 255) / 256);
+  hipLaunchKernelGGL(k_cluster_stats, dim3(nb), dim3(256), 0, S(stream), c->kp, reward, c->d_stats);
+  LAUNCH_CHECK("k_cluster_stats");
+  hipLaunchKernelGGL(k_cluster_stats_final, dim3(1), dim3(64), 0, S(stream), c->d_stats, (int)nb, out);
+  LAUNCH_CHECK("k_cluster_stats_final");
+  return MDR_OK;
+}
+
 int mdr_params_changed(mdr_ctx* c) {
   if (!c) return fail(MDR_EARG, "mdr_params_changed: null ctx");
   c->coef_dirty = true;
@@ -1255,6 +1269,7 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
   if (halo && hbytes > c->halo_bytes) {
     HIP_TRY(hipStreamSynchronize(st));
     hipFree(c->d_halo);
+  hipFree(c->d_stats);
     c->d_halo = nullptr;
     HIP_TRY(hipMalloc(&c->d_halo, hbytes));
     c->halo_bytes = hbytes;

@@ -104,6 +104,10 @@ __global__ void k_reward_finalize(KParams p, TickArgs tk, const unsigned long lo
 __global__ void k_reward_state(KParams p, const TickArgs* tkp, const unsigned long long* counts,
                                double* reward, double* p_out);
 __global__ void k_populate(KParams p, PopArgs a);
+constexpr int kStats = 12;       // k_cluster_stats outputs (mdr.h mdr_cluster_stats)
+constexpr int kStatsBlocks = 512;
+__global__ void k_cluster_stats(KParams p, const double* reward, double* partial);
+__global__ void k_cluster_stats_final(const double* partial, int nblk, double* out);
 __global__ void k_obs(KParams p, ObsArgs o, const double* p_dev, float* obs);
 __global__ void k_halo_pack(KParams p, ObsArgs o, int lo, int hi, float* out);
 __global__ void k_greedy_keys(KParams p, double* key, int* idx);

@@ -619,33 +619,43 @@ __device__ __forceinline__ bool win_action(const uint2* rw, int G, uint64_t g0, 
   return bit_of(wd.x, wd.y, gid);
 }
 
-// FSM-only run of nt ticks (tick offsets j0 .. j0+nt-1 of the staged random slots / action rows)
-// from words w[0..HPT), ON counts per tick and class into the block histogram hist[j][kWinCap].
+// FSM-only run of nt ticks (tick offsets j0 .. j0+nt-1 of the window) from words w[0..HPT), the
+// wave's ON count per tick and capacity class into its own LDS row cnt[j][kWinCap] (plain stores,
+// summed over the block's waves by win_flush).  Random actions come from the per-house bit masks
+// (bit j0 + j), the class membership from wave ballots taken once, so a tick costs the FSM, one
+// ballot per house slot and scalar bit counts.
 template <int ACT, int HPT>
 __device__ __forceinline__ void win_count(const KParams& p, const uint32_t* w_in, const int* cls, const bool* v,
-                                          uint32_t i0, uint64_t gid0, const uint2* rw, int G, uint64_t g0,
-                                          int j0, int nt, const uint8_t* action, int64_t act_stride,
-                                          unsigned* hist) {
+                                          const uint64_t* rmask, uint32_t i0, int j0, int nt,
+                                          const uint8_t* action, int64_t act_stride, unsigned* cnt) {
   const int lane = threadIdx.x & 63;
   uint32_t w[HPT];
+  uint64_t cm[HPT][kWinCap];
 #pragma unroll
-  for (int h = 0; h < HPT; ++h) w[h] = w_in[h];
+  for (int h = 0; h < HPT; ++h) {
+    w[h] = w_in[h];
+#pragma unroll
+    for (int c = 0; c < kWinCap; ++c) cm[h][c] = __ballot(v[h] && cls[h] == c);
+  }
   for (int j = 0; j < nt; ++j) {
     const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)(j0 + j) * act_stride : nullptr;
-    bool on[HPT];
+    uint64_t on[HPT];
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
-      const bool a = v[h] && win_action<ACT>(rw, G, g0, j0 + j, gid0 + h, arow, i0 + h);
+      bool a;
+      if (ACT == MDR_ACT_RANDOM) a = ((rmask[h] >> (j0 + j)) & 1ull) != 0;
+      else if (ACT == MDR_ACT_ALWAYS_ON) a = true;
+      else a = v[h] && arow[i0 + h] != 0;
       w[h] = hvac_fsm(w[h], a, p.dt, p.L);
-      on[h] = v[h] && hv_on(w[h]);
+      on[h] = __ballot(hv_on(w[h]));
     }
+    if (lane == 0) {
 #pragma unroll
-    for (int c = 0; c < kWinCap; ++c) {
-      if (c < p.n_cap) {
-        unsigned cnt = 0;
+      for (int c = 0; c < kWinCap; ++c) {
+        unsigned k = 0;
 #pragma unroll
-        for (int h = 0; h < HPT; ++h) cnt += (unsigned)__popcll(__ballot(on[h] && cls[h] == c));
-        if (lane == 0 && cnt) atomicAdd(&hist[j * kWinCap + c], cnt);
+        for (int h = 0; h < HPT; ++h) k += (unsigned)__popcll(on[h] & cm[h][c]);
+        cnt[j * kWinCap + c] = k;
       }
     }
   }
@@ -661,11 +671,14 @@ __device__ __forceinline__ unsigned long long* win_red(unsigned long long* slot,
   return slot + (size_t)kWinMax * kCountShards * n_cap;
 }
 
-__device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsigned* hist, unsigned long long* slot) {
+// sum the block's per-wave rows cnt[4][kWinMax][kWinCap] and add them to this block's slab shard
+__device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsigned (*cnt)[kWinMax * kWinCap],
+                                          unsigned long long* slot) {
   const int ncap = p.n_cap;
   for (int e = threadIdx.x; e < nt * ncap; e += blockDim.x) {
     const int j = e / ncap, c = e - j * ncap;
-    const unsigned v = hist[j * kWinCap + c];
+    const unsigned v = cnt[0][j * kWinCap + c] + cnt[1][j * kWinCap + c] + cnt[2][j * kWinCap + c] +
+                       cnt[3][j * kWinCap + c];
     if (v) atomicAdd(&slot[((size_t)j * kCountShards + blockIdx.x % kCountShards) * ncap + c],
                      (unsigned long long)v);
   }
@@ -709,9 +722,8 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
                                                       int64_t act_stride, const TickArgs* __restrict__ tkp, int nt,
                                                       unsigned long long* __restrict__ slot) {
   __shared__ uint2 s_rw[4][3 * kWinMax];
-  __shared__ unsigned s_hist[kWinMax * kWinCap];
+  __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
   const int tid = threadIdx.x, wv = tid >> 6;
-  for (int j = tid; j < kWinMax * kWinCap; j += blockDim.x) s_hist[j] = 0;
   const WinTile<HPT> t(p);
   const uint32_t n = (uint32_t)p.n;
   uint32_t w[HPT];
@@ -722,11 +734,16 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
     w[h] = p.hvac[i];
     cls[h] = p.cap_idx[i];
   }
-  if (ACT == MDR_ACT_RANDOM) win_random_stage(p.seed, t.g0, t.G, tkp, nt, s_rw[wv]);
+  uint64_t rmask[HPT] = {};
+  if (ACT == MDR_ACT_RANDOM) {
+    win_random_stage(p.seed, t.g0, t.G, tkp, nt, s_rw[wv]);
+    __syncthreads();
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) rmask[h] = win_random_mask(s_rw[wv], t.G, t.g0, nt, t.gid0 + h);
+  }
+  win_count<ACT, HPT>(p, w, cls, t.v, rmask, t.i0, 0, nt, action, act_stride, s_cnt[wv]);
   __syncthreads();
-  win_count<ACT, HPT>(p, w, cls, t.v, t.i0, t.gid0, s_rw[wv], t.G, t.g0, 0, nt, action, act_stride, s_hist);
-  __syncthreads();
-  win_flush(p, nt, s_hist, slot);
+  win_flush(p, nt, s_cnt, slot);
 }
 
 // MDR_WIN_WAVES (build-time A/B knob): cap k_step_window at that many waves per SIMD
@@ -748,9 +765,8 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
                                                      double* p_out, unsigned long long* next_slot,
                                                      unsigned long long* zero_slab, int zero_len) {
   __shared__ uint2 s_rw[4][3 * 2 * kWinMax];
-  __shared__ unsigned s_hist[kWinMax * kWinCap];
+  __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  for (int j = tid; j < kWinMax * kWinCap; j += blockDim.x) s_hist[j] = 0;
   if (zero_slab && blockIdx.x == 0)
     for (int j = tid; j < zero_len; j += blockDim.x) zero_slab[j] = 0ull;
   const uint32_t n = (uint32_t)p.n;
@@ -794,8 +810,10 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P_last;
 
   // ---- random controller bits for the window + lookahead
-  if (ACT == MDR_ACT_RANDOM) win_random_stage(p.seed, t.g0, t.G, tkp, K + la_K, s_rw[wv]);
-  __syncthreads();  // LDS histogram zeroed, random words staged
+  if (ACT == MDR_ACT_RANDOM) {
+    win_random_stage(p.seed, t.g0, t.G, tkp, K + la_K, s_rw[wv]);
+    __syncthreads();  // random words staged
+  }
 
   const bool params_ok = !*p.params_bad && p.fast_tick_ok;
   double qc[HPT];
@@ -815,7 +833,7 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
       rw[h].rd.nb = -(rw[h].k.r2 - rw[h].k.r1);
       rw[h].UaHm = ua[h] + hm[h];
     }
-    rmask[h] = ACT == MDR_ACT_RANDOM ? win_random_mask(s_rw[wv], t.G, t.g0, K, t.gid0 + h) : 0ull;
+    rmask[h] = ACT == MDR_ACT_RANDOM ? win_random_mask(s_rw[wv], t.G, t.g0, K + la_K, t.gid0 + h) : 0ull;
   }
   const uint32_t o8 = i0 * 8u;
   const bool vec_rew = HPT == 2 && t.full && (rew_stride & 1) == 0 && (((uintptr_t)reward) & 15u) == 0;
@@ -868,10 +886,10 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
 
   // ---- lookahead: ON counts of the next window's ticks
   if (la_K > 0) {
-    win_count<ACT, HPT>(p, w, cls, t.v, i0, t.gid0, s_rw[wv], t.G, t.g0, K, la_K,
-                        ACT == MDR_ACT_BUFFER ? action : nullptr, act_stride, s_hist);
+    win_count<ACT, HPT>(p, w, cls, t.v, rmask, i0, K, la_K, ACT == MDR_ACT_BUFFER ? action : nullptr, act_stride,
+                        s_cnt[wv]);
     __syncthreads();
-    win_flush(p, la_K, s_hist, next_slot);
+    win_flush(p, la_K, s_cnt, next_slot);
   }
 }
 
@@ -1026,6 +1044,69 @@ __global__ void __launch_bounds__(256) k_reward_state(KParams p, const TickArgs*
   if (i >= p.n) return;
   const double tpen = p.alpha_temp * deadband_l2(p.target[i], p.deadband, p.t_air[i]);
   reward[i] = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig_term);
+}
+
+// --------------------------------------------------------------------------------------- stats
+// Cluster statistics the server reads after every tick, one pass over the state:
+// Metrics.update (metrics_service.py:108-157) and the UI summary / graph data
+// (client_manager_service.py:62-111,177-196).  Deterministic two-level reduction (fixed block
+// partials, then one block in index order), so a run is reproducible; the reference sums
+// sequentially in house order, so floating-point sums agree to rounding (~1e-15 relative).
+//   s[0] sum (T - target / N)    (metrics' temp_error, operator precedence as the reference)
+//   s[1] sum |T - target / N|    s[2] max(0, max (T - target / N))    s[3] sum (T - target / N)^2
+//   s[4] sum reward / N          s[5] sum T     s[6] sum (T - target)   s[7] sum |T - target|
+//   s[8] sum T_mass              s[9] sum target   s[10] # lockout     s[11] # on
+__global__ void __launch_bounds__(256) k_cluster_stats(KParams p, const double* __restrict__ reward,
+                                                       double* __restrict__ partial) {
+  __shared__ double sh[kStats][4];
+  double a[kStats];
+#pragma unroll
+  for (int k = 0; k < kStats; ++k) a[k] = 0.0;
+  const double N = (double)p.n_global;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double T = p.t_air[i], tg = p.target[i];
+    const double e = T - tg / N;
+    const double d = T - tg;
+    a[0] += e;
+    a[1] += fabs(e);
+    a[2] = fmax(a[2], e);
+    a[3] += e * e;
+    if (reward) a[4] += reward[i] / N;
+    a[5] += T;
+    a[6] += d;
+    a[7] += fabs(d);
+    a[8] += p.t_mass[i];
+    a[9] += tg;
+    const uint32_t w = p.hvac[i];
+    a[10] += hv_lock(w) ? 1.0 : 0.0;
+    a[11] += hv_on(w) ? 1.0 : 0.0;
+  }
+#pragma unroll
+  for (int k = 0; k < kStats; ++k)
+    for (int off = 32; off > 0; off >>= 1) {
+      const double o = __shfl_xor(a[k], off);
+      a[k] = k == 2 ? fmax(a[k], o) : a[k] + o;
+    }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0)
+#pragma unroll
+    for (int k = 0; k < kStats; ++k) sh[k][wv] = a[k];
+  __syncthreads();
+  if (threadIdx.x < kStats) {
+    const int k = threadIdx.x;
+    double v = sh[k][0];
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) v = k == 2 ? fmax(v, sh[k][w]) : v + sh[k][w];
+    partial[(size_t)blockIdx.x * kStats + k] = v;
+  }
+}
+
+__global__ void __launch_bounds__(64) k_cluster_stats_final(const double* __restrict__ partial, int nblk,
+                                                            double* __restrict__ out) {
+  const int k = threadIdx.x;
+  if (k >= kStats) return;
+  double v = k == 2 ? 0.0 : partial[k];  // max starts at 0 like the reference's max_temp_error
+  for (int b = k == 2 ? 0 : 1; b < nblk; ++b) v = k == 2 ? fmax(v, partial[(size_t)b * kStats + k]) : v + partial[(size_t)b * kStats + k];
+  out[k] = v;
 }
 
 // --------------------------------------------------------------------------------------- population

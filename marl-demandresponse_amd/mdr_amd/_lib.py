@@ -121,6 +121,7 @@ SIGNATURES = {
     "mdr_obs": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, VP, VP]),
     "mdr_halo_pack": (I, [VP, P(mdr_obs_spec), VP, VP]),
     "mdr_ctrl_greedy": (I, [VP, D, VP, VP]),
+    "mdr_cluster_stats": (I, [VP, VP, VP, VP]),
     "mdr_actor_load": (I, [VP, P(mdr_actor_spec), VP, VP, VP, VP, VP, VP, VP]),
     "mdr_actor_act": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, U64, VP, VP, VP, VP, I, VP]),
     "mdr_actor_rollout": (I, [VP, I, VP, VP, P(mdr_obs_spec), VP, I64, VP, I64,

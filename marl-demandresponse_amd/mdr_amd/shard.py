@@ -178,6 +178,10 @@ class HipShard:
         events must be recorded."""
         return self.torch.cuda.current_stream(self.device)
 
+    def cluster_stats(self, reward, out):
+        """out (device float64 [12]) <- mdr_cluster_stats of the current state (+ reward or None)."""
+        L.check(self.lib.mdr_cluster_stats(self.ctx, L.ptr(reward), L.ptr(out), self.stream()), "mdr_cluster_stats")
+
     def greedy(self, budget: float, action):
         L.check(self.lib.mdr_ctrl_greedy(self.ctx, float(budget), L.ptr(action), self.stream()),
                 "mdr_ctrl_greedy")

@@ -298,3 +298,34 @@ def test_one_million_houses_properties(torch_gpu):
                    props.reward_prop, props.cluster_prop.house_prop.target_temp)
     np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12)
     assert np.all(np.isfinite(r))
+
+
+def test_greedy_one_million_vs_oracle(torch_gpu):
+    """Config C3 at its stated size: 1,048,576 houses, device GreedyMyopic on the post-step state
+    -> env.step, 4 ticks, against the oracle's greedy (stable order) and step on the same population:
+    actions and on/lock/sso exact, temperatures rtol 1e-10, rewards, P."""
+    from mdr_amd.environment import Environment
+
+    n = 1 << 20
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env = Environment(props, rng=random.Random(21), population="synthetic", seed=21)
+    prm = env.shard.host_params()
+    caps = np.array(env._cap_values, np.float64)[prm["cap_idx"]]
+    pop = {"Ua": prm["ua"], "Ca": prm["ca"], "Cm": prm["cm"], "Hm": prm["hm"], "target": prm["target"], "cap": caps}
+    ora = O.OracleEnv(props, random.Random(21), population=pop)
+    hv = props.cluster_prop.house_prop.hvac_prop
+    for t in range(4):
+        assert float(env.power_grid.current_signal) == float(ora.S)
+        a = env.greedy_actions().cpu().numpy().astype(bool)
+        ref = O.greedy(ora.T, ora.pop["target"], caps, hv.cop, ora.lock, float(ora.S))
+        np.testing.assert_array_equal(a, ref, err_msg=f"greedy t={t}")
+        r = env.step_tensor(torch_gpu.from_numpy(a.astype(np.uint8)).to("cuda")).cpu().numpy()
+        o, rr = ora.step(a)
+        st = env.shard.host_state()
+        np.testing.assert_array_equal(st["on"], o["on"])
+        np.testing.assert_array_equal(st["lock"], o["lock"])
+        np.testing.assert_array_equal(st["sso"], o["sso"])
+        np.testing.assert_allclose(st["T"], o["T"], rtol=TEMP_RTOL, atol=0)
+        np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12)
+        assert env.cluster.current_power_consumption == o["P"]

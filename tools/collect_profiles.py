@@ -54,7 +54,7 @@ def main():
     if os.path.exists(path):
         with open(path) as f:
             db = json.load(f)
-    for d in sorted(glob.glob(os.path.join(src, "pmc_*"))):
+    for d in sorted(p for p in glob.glob(os.path.join(src, "pmc_*")) if os.path.isdir(p)):
         houses = int(d.rsplit("_", 1)[1])
         csvs = sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True))
         for i, p in enumerate(csvs):
