@@ -6,6 +6,7 @@
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -641,10 +642,13 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
     return fail(MDR_EARG, "mdr_rollout: common penalty modes need the per-step API");
   hipStream_t st = S(stream);
+  static const bool trace = getenv("MDR_TRACE") != nullptr;  // host-side phase timing (diagnostics)
+  const auto t0 = std::chrono::steady_clock::now();
   int rc = refresh_if_dirty(c, st);
   if (rc) return rc;
   rc = stage_ticks(c, n, ticks, st);
   if (rc) return rc;
+  const auto t1 = std::chrono::steady_clock::now();
   if (!use_graph) {
     rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st);
     c->counts_ready = false;
@@ -660,9 +664,16 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
     if (rc) return rc;
     it = c->graphs.emplace(key, std::make_pair(ex, c->ring)).first;
   }
+  const auto t2 = std::chrono::steady_clock::now();
   HIP_TRY(hipGraphLaunch(it->second.first, st));
   c->ring = it->second.second;
   c->counts_ready = false;
+  if (trace) {
+    const auto t3 = std::chrono::steady_clock::now();
+    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
+    fprintf(stderr, "mdr_rollout n=%d: stage %.1f us, graph lookup/capture %.1f us, hipGraphLaunch %.1f us\n", n,
+            us(t0, t1), us(t1, t2), us(t2, t3));
+  }
   return MDR_OK;
 }
 

@@ -67,6 +67,22 @@ def od_temp(t: _dt.datetime, temp_prop, rng=_random):
     return temperature
 
 
+def solar_minute(month: int, day: int, hour: int, minute: int, window_area: float, shading_coeff: float):
+    """solar_gain at a (month, day, hour, minute) (memoised)."""
+    return _solar_memo(month, day, hour, minute, window_area, shading_coeff)
+
+
+def od_day_list(temp_prop) -> list:
+    """The daily outdoor-temperature curve (od_temp without the gauss draw) for every minute of the
+    day, as a list of np.float64 (the scalar expression, evaluated once per process and config)."""
+    return _od_day(temp_prop.day_temp, temp_prop.night_temp, temp_prop.phase)
+
+
+@functools.lru_cache(maxsize=16)
+def _od_day(day_temp, night_temp, phase):
+    return [_od_det(m // 60, m % 60, day_temp, night_temp, phase) for m in range(1440)]
+
+
 def od_daily(hour: int, minute: int, temp_prop):
     """The deterministic (daily sinusoid) part of od_temp, as np.float64."""
     return _od_det(hour, minute, temp_prop.day_temp, temp_prop.night_temp, temp_prop.phase)
@@ -203,6 +219,15 @@ class GridSignal:
                 self._memo.clear()
             self._memo[key] = self.current_signal
         return self.current_signal
+
+    def day_table(self) -> np.ndarray:
+        """current_signal after a step at every second of the day (constant base power and a
+        flat / sinusoidal / regular-steps signal), cached per (base, artificial ratio, cap)."""
+        key = (self.base_power(), self.gp.artificial_ratio, self.max_power)
+        if getattr(self, "_day_key", None) != key:
+            self._day_tab = self.signal_series(np.arange(86400, dtype=np.int64))
+            self._day_key = key
+        return self._day_tab
 
     def signal_series(self, sod) -> np.ndarray:
         """``step`` at a series of ticks (seconds of day ``sod``, int64 array) for a constant base

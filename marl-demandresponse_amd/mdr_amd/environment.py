@@ -211,6 +211,9 @@ class Environment:
         self._counts_ready = 0
         self._grid_pending = False
         self.power_grid.step(self.date_time, self.current_od_temp, p.time_step.seconds)  # first signal (:67-69)
+        if self._vector_drivers_ok():  # rollout driver tables, built here rather than inside a rollout
+            self.power_grid.day_table()
+            drivers.od_day_list(p.temp_prop)
         self._obs_links = self._links if self._links is not None else popmod.random_links(cp, rng)
         return self.get_obs() if return_obs else None
 
@@ -356,58 +359,56 @@ class Environment:
         g = self.power_grid
         st = self.init_props.time_step
         return (g.interp is None and g.signal_fn is None and g.signal.mode in ("flat", "sinusoidals", "regular_steps")
-                and st.microseconds == 0 and st.days == 0 and st.seconds > 0)
+                and st.microseconds == 0 and st.days == 0 and 0 < st.seconds < 86400)
 
     def _driver_window_vec(self, n: int) -> "TickWindow":
-        """driver_window for a constant base power and a flat / sinusoidal / regular-steps signal,
-        evaluated over the whole window at once — the same values as the per-tick loop, bit for
-        bit (tests/test_host_logic.py): solar gain and the daily outdoor-temperature curve are
-        computed once per distinct (day, minute) with the scalar code; the n gauss draws come in
-        the reference order (nothing else draws in between); the signal and the gauss additions
-        are the same IEEE operations elementwise (NumPy's vectorised sin equals its scalar sin)."""
+        """driver_window for a constant base power and a flat / sinusoidal / regular-steps signal:
+        the same values as the per-tick loop, bit for bit (tests/test_driver_window.py), from
+        per-day lookup tables built at reset — the regulation signal by second of the day
+        (GridSignal.day_table) and the outdoor-temperature daily curve by minute
+        (drivers.od_day_list) — plus the solar gain once per minute (memoised scalar code) and the
+        n gauss draws in the reference order (nothing else draws in between).  A short Python
+        loop: no per-tick objects beyond the draws, and no NumPy call per tick."""
         p = self.init_props
         hp = p.cluster_prop.house_prop
-        tp, rng, grid = p.temp_prop, self.rng, self.power_grid
+        tp, grid = p.temp_prop, self.power_grid
+        sig_tab = grid.day_table()
+        od_tab = drivers.od_day_list(tp)
+        gauss, std = self.rng.gauss, tp.temp_std
         dts = p.time_step.seconds
         d0 = self.date_time
-        s0 = d0.hour * 3600 + d0.minute * 60 + d0.second
-        abs_s = s0 + dts * np.arange(1, n + 1, dtype=np.int64)  # seconds since d0's midnight
-        day_off, sod = np.divmod(abs_s, 86400)
-        mod = sod // 60  # minute of the day
-        # solar gain of every tick's NEW datetime (environment.py:86-88, building.py:176-179)
-        if hp.solar_gain:
-            uk, inv = _runs(day_off * 1440 + mod)
-            day0 = d0.replace(hour=0, minute=0, second=0, microsecond=0)
-            vals = []
-            for k in uk:
-                dd = day0 + _dt.timedelta(days=k // 1440)
-                vals.append(solar_gain(dd.replace(hour=(k % 1440) // 60, minute=k % 60), hp.window_area,
-                                       hp.shading_coeff))
-            sol = np.asarray(vals, np.float64)[inv]
-            sol_last = vals[-1]
-        else:
-            sol = np.zeros(n)
-            sol_last = 0.0
-        # outdoor temperature: the daily curve of each tick + one gauss per tick, in tick order
-        um, minv = _runs(mod)
-        det = np.asarray([drivers.od_daily(m // 60, m % 60, tp) for m in um], np.float64)[minv]
-        gs = np.fromiter((rng.gauss(0, tp.temp_std) for _ in range(n)), np.float64, n)
-        tod = det + gs
-        # regulation signal after each tick (power_grid.py:80-102, signal_calculator.py:33-98)
-        sig = grid.signal_series(sod)
+        s = d0.hour * 3600 + d0.minute * 60 + d0.second
+        solar_on, wa, shc = hp.solar_gain, hp.window_area, hp.shading_coeff
+        month, mday, day_off = d0.month, d0.day, 0
+        sol, last_m = 0.0, -1
+        tods, sols, sigs = [self.current_od_temp], [], [grid.current_signal]
+        for _ in range(n):
+            # environment.py:86-106: the new datetime's solar gain, the previous OD temperature
+            # for the step, then one gauss for the new OD temperature and the new signal
+            s += dts
+            if s >= 86400:
+                s -= 86400
+                day_off += 1
+                dd = d0 + _dt.timedelta(days=day_off)
+                month, mday, last_m = dd.month, dd.day, -1
+            m = s // 60
+            if solar_on and m != last_m:
+                sol = drivers.solar_minute(month, mday, m // 60, m % 60, wa, shc)
+                last_m = m
+            sols.append(sol)
+            tods.append(od_tab[m] + gauss(0, std))
+            sigs.append(sig_tab[s])
         buf = np.empty((n, 4), np.float64)
-        buf[0, 0] = self.current_od_temp
-        buf[1:, 0] = tod[:-1]
-        buf[:, 1] = sol
-        buf[0, 2] = grid.current_signal
-        buf[1:, 2] = sig[:-1]
+        buf[:, 0] = tods[:n]
+        buf[:, 1] = sols
+        buf[:, 2] = sigs[:n]
         tick0 = self._tick
         buf[:, 3].view(np.uint64)[:] = np.arange(tick0, tick0 + n, dtype=np.uint64)
         self.date_time = d0 + p.time_step * n
-        self._solar, self._tick = sol_last, tick0 + n
-        self._tod_prev, self._s_prev = tod[-2], sig[-2]
-        self.current_od_temp = tod[-1]
-        grid.current_signal = sig[-1]
+        self._solar, self._tick = sol, tick0 + n
+        self._tod_prev, self._s_prev = tods[n - 1], sigs[n - 1]
+        self.current_od_temp = tods[n]
+        grid.current_signal = sigs[n]
         return TickWindow(buf)
 
     def _driver_window_loop(self, n_ticks: int) -> "TickWindow":
