@@ -64,8 +64,12 @@ class RcclComm:
         L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, p.value + 8, 1, 2, shard.stream()), "allreduce pen max")
 
     def allreduce_sum(self, shard, t) -> None:
-        """In-place double sum over ranks of a device tensor (interpolation sample values)."""
+        """In-place double sum over ranks of a device tensor (interpolation sample values, stats)."""
         L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, L.ptr(t), t.numel(), 1, shard.stream()), "allreduce sum")
+
+    def allreduce_max(self, shard, t) -> None:
+        """In-place double max over ranks of a device tensor."""
+        L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, L.ptr(t), t.numel(), 2, shard.stream()), "allreduce max")
 
     def rollout(self, shard, ticks, actions, mode, rewards, rew_stride) -> None:
         n = shard.n
@@ -157,6 +161,9 @@ class TorchComm(RcclComm):
 
     def allreduce_sum(self, shard, t) -> None:
         self.dist.all_reduce(t)
+
+    def allreduce_max(self, shard, t) -> None:
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
 
     def pipeline(self, shard) -> dict:
         return {"mode": "torch.distributed per-step"}

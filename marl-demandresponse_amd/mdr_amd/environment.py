@@ -17,6 +17,7 @@ from __future__ import annotations
 import copy
 import datetime as _dt
 import random as _random
+from collections.abc import Sequence
 from types import SimpleNamespace
 from typing import Dict, Optional
 
@@ -27,6 +28,7 @@ from . import config as cfgmod
 from . import drivers
 from . import population as popmod
 from .drivers import GridSignal, od_temp, reward_normalisers, solar_gain
+from .lazydict import LazyDict
 from .shard import HipShard, encode_hvac
 
 ACTION_MODES = {"buffer": L.ACT_BUFFER, "random": L.ACT_RANDOM, "always_on": L.ACT_ALWAYS_ON,
@@ -39,6 +41,40 @@ def _runs(key: np.ndarray):
     chg[0] = True
     np.not_equal(key[1:], key[:-1], out=chg[1:])
     return key[chg].tolist(), np.cumsum(chg) - 1
+
+
+class _BuildingList(Sequence):
+    """The parts of ``Building`` / ``HVAC`` the server reads (cluster.py:48-62), per house on access,
+    from one host copy of the state taken when the list is created."""
+
+    def __init__(self, env):
+        self._env = env
+        self._st = env._shard.host_state()
+        self._prm = env._params_host()
+
+    def __len__(self) -> int:
+        return self._env._n_local
+
+    def __getitem__(self, i):
+        if isinstance(i, slice):
+            return [self[j] for j in range(*i.indices(len(self)))]
+        i = int(i)
+        if i < 0:
+            i += len(self)
+        if not 0 <= i < len(self):
+            raise IndexError(i)
+        st, prm, env = self._st, self._prm, self._env
+        hp = env.init_props.cluster_prop.house_prop
+        cap = env._cap_values[int(prm["cap_idx"][i])]
+        hv = SimpleNamespace(turned_on=bool(st["on"][i]), lockout=bool(st["lock"][i]),
+                             seconds_since_off=int(st["sso"][i]),
+                             init_props=SimpleNamespace(cooling_capacity=cap, cop=hp.hvac_prop.cop,
+                                                        max_consumption=cap / hp.hvac_prop.cop,
+                                                        lockout_duration=hp.hvac_prop.lockout_duration))
+        ip = SimpleNamespace(Ua=float(prm["ua"][i]), Ca=float(prm["ca"][i]), Cm=float(prm["cm"][i]),
+                             Hm=float(prm["hm"][i]), target_temp=float(prm["target"][i]), deadband=hp.deadband)
+        return SimpleNamespace(indoor_temp=float(st["T"][i]), current_mass_temp=float(st["Tm"][i]),
+                               current_solar_gain=env._solar, init_props=ip, hvac=hv)
 
 
 class TickWindow:
@@ -335,7 +371,7 @@ class Environment:
         sh.action.copy_(torch.from_numpy(a).to(sh.device))
         reward = self.step_tensor(sh.action)
         r = reward.cpu().numpy()
-        rewards = {lo + i: float(r[i]) for i in range(nl)}
+        rewards = LazyDict(lambda g: float(r[g - lo]), range(lo, lo + nl))
         return self.get_obs(), rewards
 
     # ------------------------------------------------------------------ many ticks per call
@@ -599,72 +635,74 @@ class Environment:
         return self._host_params
 
     def get_obs(self) -> Dict[int, dict]:
-        """environment.py:110-130 — one 21-key dict per (local) house, with its messages."""
+        """environment.py:110-130 — one 21-key dict per (local) house, with its messages.  Single
+        shard: a LazyDict over a device snapshot of this tick's state, each house's dict built the
+        first time it is read (one device->host copy on the first read).  Sharded: messages name
+        houses on other shards, so the cluster state is gathered (a collective) and built now."""
+        if self.world > 1:
+            st, prm = self._comm.allgather_state(self._shard, self._shard.host_state(), self._params_host(), self.n)
+            build = self._obs_builder(lambda: (st, prm), 0)
+            return {g: build(g) for g in range(self._offset, self._offset + self._n_local)}
+        sh = self._shard
+        snap = (sh.t_air.clone(), sh.t_mass.clone(), sh.hvac.clone())
+        cache = []
+
+        def host():
+            if not cache:
+                from .shard import decode_hvac
+
+                on, lock, sso = decode_hvac(snap[2].cpu().numpy())
+                cache.append(({"T": snap[0].cpu().numpy(), "Tm": snap[1].cpu().numpy(), "on": on, "lock": lock,
+                               "sso": sso}, self._params_host()))
+            return cache[0]
+
+        return LazyDict(self._obs_builder(host, 0), range(self._n_local))
+
+    def _obs_builder(self, host, lo: int):
+        """house id -> its obs dict, from the host arrays ``host()`` returns (state, params)
+        indexed by global id, and this tick's scalars (captured now)."""
         p = self.init_props
         cp, hp = p.cluster_prop, p.cluster_prop.house_prop
         hv = hp.hvac_prop
-        st = self._shard.host_state()
-        prm = self._params_host()
-        lo, nl = self._offset, self._n_local
-        if self.world > 1:  # messages need neighbours on other shards: gather the cluster state
-            st, prm = self._comm.allgather_state(self._shard, st, prm, self.n)
-        else:
-            lo = 0
-        caps = [self._cap_values[j] for j in prm["cap_idx"].tolist()]
-        maxc = [c / hv.cop for c in caps]
-        T, Tm = st["T"].tolist(), st["Tm"].tolist()
-        on, lock, sso = st["on"].tolist(), st["lock"].tolist(), st["sso"].tolist()
-        tgt = prm["target"].tolist()
-        ua, ca, cm, hm = (prm[k].tolist() for k in ("ua", "ca", "cm", "hm"))
-        P = self._cluster_power()
-        G = self._solar
+        cap_values = list(self._cap_values)
+        P, G = self._cluster_power(), self._solar
         od, dt_, S = self.current_od_temp, self.date_time, self.power_grid.current_signal
         L_, cop, lcf, db = hv.lockout_duration, hv.cop, hv.latent_cooling_fraction, hp.deadband
         mp = cp.message_prop
         links = self._obs_links
 
-        def message(j):
-            m = {"seconds_since_off": sso[j], "curr_consumption": maxc[j] if on[j] else 0.0,
-                 "max_consumption": maxc[j], "lockout_duration": L_,
-                 "current_temp_diff_to_target": T[j] - tgt[j]}
+        def message(st, prm, j):
+            cap = cap_values[int(prm["cap_idx"][j])]
+            on_j = bool(st["on"][j])
+            m = {"seconds_since_off": int(st["sso"][j]), "curr_consumption": cap / cop if on_j else 0.0,
+                 "max_consumption": cap / cop, "lockout_duration": L_,
+                 "current_temp_diff_to_target": float(st["T"][j]) - float(prm["target"][j])}
             if mp.hvac:
-                m.update({"cop": cop, "latent_cooling_fraction": lcf, "cooling_capacity": caps[j]})
+                m.update({"cop": cop, "latent_cooling_fraction": lcf, "cooling_capacity": cap})
             if mp.thermal:
-                m.update({"Ca": ca[j], "Ua": ua[j], "Cm": cm[j], "Hm": hm[j]})
+                m.update({"Ca": float(prm["ca"][j]), "Ua": float(prm["ua"][j]), "Cm": float(prm["cm"][j]),
+                          "Hm": float(prm["hm"][j])})
             return m
 
-        obs = {}
-        for g in range(lo, lo + nl):  # arrays are indexed by global house id from here on
+        def build(g):
+            st, prm = host()
             row = links[g] if links is not None else ()
-            obs[g] = {
-                "turned_on": on[g], "seconds_since_off": sso[g], "lockout": lock[g], "cop": cop,
-                "cooling_capacity": caps[g], "latent_cooling_fraction": lcf, "lockout_duration": L_,
-                "target_temp": tgt[g], "deadband": db, "Ua": ua[g], "Ca": ca[g], "Cm": cm[g],
-                "Hm": hm[g], "indoor_temp": T[g], "mass_temp": Tm[g], "solar_gain": G,
-                "cluster_hvac_power": P, "message": [message(int(j)) for j in row],
+            return {
+                "turned_on": bool(st["on"][g]), "seconds_since_off": int(st["sso"][g]), "lockout": bool(st["lock"][g]),
+                "cop": cop, "cooling_capacity": cap_values[int(prm["cap_idx"][g])], "latent_cooling_fraction": lcf,
+                "lockout_duration": L_, "target_temp": float(prm["target"][g]), "deadband": db,
+                "Ua": float(prm["ua"][g]), "Ca": float(prm["ca"][g]), "Cm": float(prm["cm"][g]),
+                "Hm": float(prm["hm"][g]), "indoor_temp": float(st["T"][g]), "mass_temp": float(st["Tm"][g]),
+                "solar_gain": G, "cluster_hvac_power": P, "message": [message(st, prm, int(j)) for j in row],
                 "OD_temp": od, "datetime": dt_, "reg_signal": S,
             }
-        return obs
+
+        return build
 
     # ------------------------------------------------------------------ server-facing views
     def _building_views(self):
-        st = self._shard.host_state()
-        prm = self._params_host()
-        hp = self.init_props.cluster_prop.house_prop
-        out = []
-        for i in range(self._n_local):
-            cap = self._cap_values[int(prm["cap_idx"][i])]
-            hv = SimpleNamespace(turned_on=bool(st["on"][i]), lockout=bool(st["lock"][i]),
-                                 seconds_since_off=int(st["sso"][i]),
-                                 init_props=SimpleNamespace(cooling_capacity=cap, cop=hp.hvac_prop.cop,
-                                                            max_consumption=cap / hp.hvac_prop.cop,
-                                                            lockout_duration=hp.hvac_prop.lockout_duration))
-            ip = SimpleNamespace(Ua=float(prm["ua"][i]), Ca=float(prm["ca"][i]), Cm=float(prm["cm"][i]),
-                                 Hm=float(prm["hm"][i]), target_temp=float(prm["target"][i]),
-                                 deadband=hp.deadband)
-            out.append(SimpleNamespace(indoor_temp=float(st["T"][i]), current_mass_temp=float(st["Tm"][i]),
-                                       current_solar_gain=self._solar, init_props=ip, hvac=hv))
-        return out
+        """cluster.buildings: a lazy sequence of per-house views (built when indexed)."""
+        return _BuildingList(self)
 
     # ------------------------------------------------------------------ checkpoint / deepcopy
     def state_dict(self) -> dict:

@@ -72,6 +72,24 @@ def _install_stubs() -> None:
     ctl = types.ModuleType("app.core.agents.controllers")
     ctl.__path__ = [os.path.join(REF, "app/core/agents/controllers")]
     sys.modules["app.core.agents.controllers"] = ctl
+    # services (Metrics, ClientManagerService) without wandb / socket.io: no-op stand-ins
+    wb = types.ModuleType("app.services.wandb_service")
+
+    class WandbManager:
+        def initialize(self, *a, **k):
+            pass
+
+        def log(self, *a, **k):
+            pass
+
+        def save(self, *a, **k):
+            pass
+
+    wb.WandbManager = WandbManager
+    sys.modules["app.services.wandb_service"] = wb
+    sm = types.ModuleType("app.services.socket_manager_service")
+    sm.SocketManager = object
+    sys.modules["app.services.socket_manager_service"] = sm
 
 
 _install_stubs()
@@ -523,6 +541,59 @@ def gen_interp_traj() -> None:
              N=12, T=160, seed=3, controller="deadband_bbc", norm_ticks=(0,))
 
 
+# ------------------------------------------------------------------------ services
+def gen_services(N: int = 50, T: int = 120, seed: int = 4, start_stats_from: int = 30) -> None:
+    """The reference's per-tick consumers along a ControllerManager-style loop
+    (controller_manager.py:104-187: random.seed, three resets, then per tick update_data(obs) ->
+    deadband bang-bang actions -> env.step -> Metrics.update(obs, next_obs, rewards, step)):
+    Metrics' accumulators after every update (metrics_service.py:108-157) and the UI summary
+    strings + graph data + house-list status counts (client_manager_service.py:62-245)."""
+    import asyncio
+
+    from app.services.client_manager_service import ClientManagerService, DESCRIPTION_KEYS
+    from app.services.metrics_service import Metrics
+
+    props = make_props({"cluster_prop.nb_agents": N, "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    random.seed(seed)
+    env = Environment(props)
+    obs = env.reset()
+    obs = env.reset()
+    met = Metrics(sys.modules["app.services.wandb_service"].WandbManager())
+    met.initialize(N, start_stats_from, T)
+    ui = ClientManagerService(None)
+    ui.initialize_data(False)
+    ctl = [DeadbandBangBangController({"id": i}, None) for i in range(N)]
+    fields = ["cumul_avg_reward", "cumul_temp_offset", "cumul_temp_error", "cumul_signal_offset",
+              "cumul_signal_error", "cumul_squared_error_temp", "max_temp_error", "cumul_OD_temp", "cumul_signal",
+              "cumul_cons", "cumul_squared_error_sig", "cumul_squared_max_error_temp"]
+    rec = {f: [] for f in fields}
+    desc, graph, status = [], [], []
+    for step in range(T):
+        asyncio.run(ui.update_data(obs_dict=obs, time_step=step))
+        desc.append([ui.description[step][k] for k in DESCRIPTION_KEYS])
+        graph.append([ui.temp_diff[-1], ui.temp_err[-1], ui.air_temp[-1], ui.mass_temp[-1], ui.target_temp[-1],
+                      ui.outdoor_temp[-1], ui.signal[-1], ui.consumption[-1]])
+        hd = ui.houses_data[step]
+        status.append([sum(h["hvacStatus"] == s for h in hd) for s in ("ON", "Lockout", "OFF")] +
+                      [sum(h.get("secondsSinceOff", 0) for h in hd)])
+        acts = {i: ctl[i].act(obs) for i in range(N)}
+        nxt, rew = env.step(acts)
+        met.update(obs, nxt, rew, step)
+        for f in fields:
+            rec[f].append(float(getattr(met, f)))
+        obs = nxt
+    met.update_rms(T)
+    out = {f"metrics_{f}": np.array(v, np.float64) for f, v in rec.items()}
+    out["rms"] = np.array([met.rmse_sig_per_ag, met.rmse_temp, met.rms_max_error_temp], np.float64)
+    out["ui_graph"] = np.array(graph, np.float64)
+    out["ui_status"] = np.array(status, np.int64)
+    out["ui_desc_json"] = np.frombuffer(json.dumps(desc).encode(), np.uint8)
+    meta = {"N": N, "T": T, "seed": seed, "start_stats_from": start_stats_from, "resets": 3,
+            "controller": "deadband_bbc", "signal": "sinusoidals", "keys": list(DESCRIPTION_KEYS)}
+    out["meta_json"] = np.frombuffer(json.dumps(meta).encode(), np.uint8)
+    np.savez_compressed(os.path.join(OUT, "services.npz"), **out)
+
+
 def main() -> None:
     if len(sys.argv) > 1:  # only the named generators, e.g. `make_golden.py gen_interp gen_interp_traj`
         for name in sys.argv[1:]:
@@ -566,6 +637,7 @@ def main() -> None:
     gen_policy()
     gen_interp()
     gen_interp_traj()
+    gen_services()
     print("golden fixtures written to", OUT)
 
 

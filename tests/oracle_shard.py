@@ -172,6 +172,9 @@ class GlooComm:
     def allreduce_sum(self, shard, t):
         self.dist.all_reduce(t)
 
+    def allreduce_max(self, shard, t):
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+
     def allgather_state(self, shard, st, prm, n):
         out_st, out_prm = {}, {}
         for src, dst, keys in ((st, out_st, ("T", "Tm", "on", "lock", "sso")),
