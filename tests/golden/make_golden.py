@@ -24,6 +24,8 @@ Fixtures (names follow SURVEY §8(c) F1..F9):
   F9 rng_order.npz     population after 1 and 3 resets for seeds {0, 4, 123}
   P  policy.npz        MAPPO actor (seed 1, the reference init) on reference norm_state_dict
                        vectors: weights, obs, Actor.forward probabilities (row P)
+  f1 services.npz     reference Metrics + ClientManagerService along a ControllerManager loop
+  f2 mappo.npz        one reference MAPPO.update at N = 2 (init, transitions, returns, final weights)
   a10 interp.npz       PowerInterpolator.interpolate_grid_fast on 400 swept points over a synthetic
                        table of the reference grid (interp_parameters_dict.json / interp_dict_keys.csv,
                        copied next to it), + traj_interp_*.npz trajectories in interpolation mode
@@ -594,6 +596,51 @@ def gen_services(N: int = 50, T: int = 120, seed: int = 4, start_stats_from: int
     np.savez_compressed(os.path.join(OUT, "services.npz"), **out)
 
 
+# ------------------------------------------------------------------------ MAPPO update (§8(f) 2)
+def gen_mappo(num_state: int = 14, T: int = 40, batch_size: int = 16, epochs: int = 3) -> None:
+    """One reference MAPPO.update (mappo.py:128-217) at N = 2 houses, where the reference's critic
+    width (num_state + 1) matches its input (state ++ the other house's action).  num_state = 14 is
+    the obs width of a 2-house cluster.  Inputs are synthetic transitions (float32-exact states),
+    stored through MAPPO.store_transition; the minibatch order comes from torch.manual_seed(123)."""
+    import torch
+    from app.core.agents.trainables.mappo import MAPPO, MAPPOProperties
+
+    cfg = MAPPOProperties(batch_size=batch_size, ppo_update_time=epochs)
+    agent = MAPPO(cfg, num_state=num_state, num_action=2, seed=1)
+    init = {f"init_actor_{k}": v.detach().numpy().copy() for k, v in agent.actor_net.state_dict().items()}
+    init.update({f"init_critic_{k}": v.detach().numpy().copy() for k, v in agent.critic_net.state_dict().items()})
+    rs = np.random.RandomState(5)
+    states = rs.normal(0, 1, (T + 1, 2, num_state)).astype(np.float32)
+    actions = rs.randint(0, 2, (T, 2)).astype(np.int64)
+    probs = rs.uniform(0.3, 0.9, (T, 2)).astype(np.float32)
+    rewards = -rs.uniform(0, 2, (T, 2))
+    done = np.array([(t % 20) == 19 for t in range(T)])
+    for t in range(T):
+        agent.last_actions = {0: int(actions[t, 0]), 1: int(actions[t, 1])}
+        agent.last_probs = {0: float(probs[t, 0]), 1: float(probs[t, 1])}
+        agent.store_transition([states[t, 0].astype(np.float64), states[t, 1].astype(np.float64)],
+                               [states[t + 1, 0].astype(np.float64), states[t + 1, 1].astype(np.float64)],
+                               {0: float(rewards[t, 0]), 1: float(rewards[t, 1])}, bool(done[t]))
+    reward = [tr.reward for tr in agent.buffer]
+    dn = [tr.done for tr in agent.buffer]
+    R, Gt = 0, []
+    for i in reversed(range(len(reward))):  # the update's own return loop (mappo.py:135-140)
+        if dn[i]:
+            R = 0
+        R = reward[i] + agent.gamma * R
+        Gt.insert(0, R)
+    torch.manual_seed(123)
+    agent.update(T)
+    out = dict(init)
+    out.update({f"final_actor_{k}": v.detach().numpy().copy() for k, v in agent.actor_net.state_dict().items()})
+    out.update({f"final_critic_{k}": v.detach().numpy().copy() for k, v in agent.critic_net.state_dict().items()})
+    out.update(states=states, actions=actions, probs=probs, rewards=rewards, done=done, Gt=np.array(Gt))
+    meta = {"num_state": num_state, "T": T, "batch_size": batch_size, "ppo_update_time": epochs, "seed": 1,
+            "update_seed": 123, "training_steps": agent.training_step}
+    out["meta_json"] = np.frombuffer(json.dumps(meta).encode(), np.uint8)
+    np.savez_compressed(os.path.join(OUT, "mappo.npz"), **out)
+
+
 def main() -> None:
     if len(sys.argv) > 1:  # only the named generators, e.g. `make_golden.py gen_interp gen_interp_traj`
         for name in sys.argv[1:]:
@@ -638,6 +685,7 @@ def main() -> None:
     gen_interp()
     gen_interp_traj()
     gen_services()
+    gen_mappo()
     print("golden fixtures written to", OUT)
 
 
