@@ -581,6 +581,19 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     if (hpt == 1) MDR_WIN_DISPATCH_H(KERNEL, 1, __VA_ARGS__);            \
     else MDR_WIN_DISPATCH_H(KERNEL, 2, __VA_ARGS__);                     \
   } while (0)
+  // k_step_window: + the deadband = 0 specialisation (branch-free penalty)
+#define MDR_WIN_DISPATCH_S(H, DB, ...)                                                                        \
+  do {                                                                                                        \
+    if (mode == MDR_ACT_RANDOM) hipLaunchKernelGGL((k_step_window<MDR_ACT_RANDOM, H, DB>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
+    else if (mode == MDR_ACT_ALWAYS_ON) hipLaunchKernelGGL((k_step_window<MDR_ACT_ALWAYS_ON, H, DB>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
+    else hipLaunchKernelGGL((k_step_window<MDR_ACT_BUFFER, H, DB>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
+  } while (0)
+  const bool db0 = c->kp.deadband == 0.0;
+#define MDR_STEP_WIN_DISPATCH(...)                                         \
+  do {                                                                    \
+    if (hpt == 1) { if (db0) MDR_WIN_DISPATCH_S(1, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(1, false, __VA_ARGS__); } \
+    else { if (db0) MDR_WIN_DISPATCH_S(2, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(2, false, __VA_ARGS__); }        \
+  } while (0)
   const int ncap = c->kp.n_cap;
   auto red = [&](int w) { return slab(w) + (size_t)kWindowMax * kCountShards * ncap; };
   MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, wsz(0), slab(0));
@@ -593,7 +606,7 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     // sharded: every rank's per-tick class counts are summed (exact integers) before the launch
     if (comm) RCCL_TRY(ncclAllReduce(red(w), red(w), (size_t)K * ncap, ncclUint64, ncclSum, comm, st));
     const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
-    MDR_WIN_DISPATCH(k_step_window, kp, a, act_stride, tk + t0, K, la, red(w), reward + (int64_t)t0 * rew_stride,
+    MDR_STEP_WIN_DISPATCH(kp, a, act_stride, tk + t0, K, la, red(w), reward + (int64_t)t0 * rew_stride,
                      rew_stride, w == nw - 1 ? p_out : nullptr, slab(w + 1), slab(w + 2),
                      kWindowMax * kCountShards * ncap);
     LAUNCH_CHECK("k_step_window");
@@ -601,6 +614,8 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
   }
 #undef MDR_WIN_DISPATCH
 #undef MDR_WIN_DISPATCH_H
+#undef MDR_WIN_DISPATCH_S
+#undef MDR_STEP_WIN_DISPATCH
   return MDR_OK;
 }
 

@@ -22,20 +22,22 @@ constexpr uint32_t kSsoMask = (1u << 30) - 1u;  // seconds_since_off saturates a
 //   lockout = not (on or sso >= L)
 //   if lockout: on = False
 //   else: on = action; if on: sso = 0 elif sso + dt < L: lockout = True
+// 32-bit arithmetic: sso <= 2^30 - 1 and 0 <= dt < 2^31 (mdr_create rejects dt < 0), so
+// sso + dt < 2^32 never wraps; a negative L behaves as 0 (sso >= L always, sso + dt < L never).
 __device__ __forceinline__ uint32_t hvac_fsm(uint32_t w, bool action, int dt, int L) {
   const bool on = (w & kOnBit) != 0;
-  int64_t sso = (int64_t)(w & kSsoMask);
-  if (!on) sso += dt;
-  const bool locked = !(on || sso >= (int64_t)L);
+  const uint32_t Lu = L < 0 ? 0u : (uint32_t)L;
+  uint32_t sso = w & kSsoMask;
+  if (!on) sso += (uint32_t)dt;
+  const bool locked = !(on || sso >= Lu);
   bool non = false, nlock = locked;
   if (!locked) {
     non = action;
     if (non) sso = 0;
-    else if (sso + dt < (int64_t)L) nlock = true;
+    else if (sso + (uint32_t)dt < Lu) nlock = true;
   }
-  if (sso > (int64_t)kSsoMask) sso = kSsoMask;
-  if (sso < 0) sso = 0;
-  return (uint32_t)sso | (nlock ? kLockBit : 0u) | (non ? kOnBit : 0u);
+  sso = sso < kSsoMask ? sso : kSsoMask;
+  return sso | (nlock ? kLockBit : 0u) | (non ? kOnBit : 0u);
 }
 
 __device__ __forceinline__ bool hv_on(uint32_t w) { return (w & kOnBit) != 0; }
@@ -156,7 +158,10 @@ __device__ __forceinline__ void rc_apply_t(double T, double Tm, double Ua, doubl
   }
   const double A2 = t_k - d_c - A1;
   const double t_new = A1 * k.e1 + A2 * k.e2 + d_c;
-  const double tm_new = A1 * k.A3 * k.e1 + A2 * k.A4 * k.e2 + 0.0 + d_c;  // + g (= Qm/Hm = 0)
+  // the reference adds g (= Qm/Hm = 0.0) before d/c; x + 0.0 differs from x only for x = -0.0, and
+  // then only in the sign of a zero tm_new, which the "- 273" below maps to the same -273.0: the
+  // addition cannot change T_mass, so it is not evaluated
+  const double tm_new = A1 * k.A3 * k.e1 + A2 * k.A4 * k.e2 + d_c;
   T_out = t_new - 273.0;
   Tm_out = tm_new - 273.0;
 }
@@ -172,6 +177,13 @@ __device__ __forceinline__ void rc_update(double T, double Tm, double Ua, double
                                           double dt, double& T_out, double& Tm_out) {
   const RcCoef k = rc_coeffs(Ua, Ca, Cm, Hm, dt);
   rc_apply(T, Tm, Ua, Ca, Hm, k, q_hvac, solar, t_od, T_out, Tm_out);
+}
+
+// deadbandL2 with deadband = 0 (the default): hi = lo = target + 0.0, and both branches of the
+// reference give (value - target)^2; value == target or NaN gives 0.0 — branch-free
+__device__ __forceinline__ double deadband_l2_0(double hi, double value) {
+  const double x = value - hi;
+  return (value < hi || value > hi) ? x * x : 0.0;
 }
 
 // deadbandL2, server/app/utils/utils.py:4-23  (x**2 evaluated as x*x)

@@ -86,7 +86,7 @@ __global__ void k_step_pipe(KParams p, const uint8_t* action, TickArgs tk, const
 constexpr int kPipeMaxCap = 4;
 constexpr int kWindowMax = 32;  // = kWinMax: ticks per k_step_window launch
 constexpr int kWindowCap = 4;   // = kWinCap: capacity classes the window kernel supports
-template <int ACT, int HPT>
+template <int ACT, int HPT, bool DB0>
 __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int K,
                               int la_K, const unsigned long long* counts, double* reward, int64_t rew_stride,
                               double* p_out, unsigned long long* next_slab, unsigned long long* zero_slab,

@@ -551,13 +551,13 @@ __device__ __forceinline__ RcWin rc_window(double ua, double ca, double cm, doub
   return w;
 }
 
-// rc_apply_t<FAST> with the window's reciprocals (identical operations and order)
+// rc_apply_t<FAST> with the window's reciprocals (identical operations and order); od_k =
+// t_od_prev + 273.0 is a per-tick scalar the caller computes once per window lane
 template <bool FAST>
 __device__ __forceinline__ void rc_apply_win(double T, double Tm, double Ua, double Hm, const RcWin& w,
-                                             double q_hvac, double solar, double t_od, double& T_out,
+                                             double q_hvac, double solar, double od_k, double& T_out,
                                              double& Tm_out) {
   const RcCoef& k = w.k;
-  const double od_k = t_od + 273.0;
   const double t_k = T + 273.0;
   const double tm_k = Tm + 273.0;
   const double Qa = q_hvac + solar;
@@ -578,7 +578,7 @@ __device__ __forceinline__ void rc_apply_win(double T, double Tm, double Ua, dou
   }
   const double A2 = t_k - d_c - A1;
   const double t_new = A1 * k.e1 + A2 * k.e2 + d_c;
-  const double tm_new = A1 * k.A3 * k.e1 + A2 * k.A4 * k.e2 + 0.0 + d_c;
+  const double tm_new = A1 * k.A3 * k.e1 + A2 * k.A4 * k.e2 + d_c;  // (+ g = 0.0 elided: mdr_device.h)
   T_out = t_new - 273.0;
   Tm_out = tm_new - 273.0;
 }
@@ -757,7 +757,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
 // previous launch, allreduced across ranks when sharded); la_K > 0: run the FSM on through the
 // next la_K ticks (tkp[K..K+la_K), action rows K..) and count them into next_slot; block 0 zeroes
 // the slab part (zero_len u64) of zero_slot for the launch after next.
-template <int ACT, int HPT>
+template <int ACT, int HPT, bool DB0>
 __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, const uint8_t* __restrict__ action,
                                                      int64_t act_stride, const TickArgs* __restrict__ tkp, int K,
                                                      int la_K, const unsigned long long* __restrict__ red,
@@ -798,14 +798,18 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   for (int k = 0; k < kWinCap; ++k) q_on[k] = p.q_on[k < p.n_cap ? k : 0];
 
   // ---- per-tick signal penalty of the window, lane j <- tick j (rewards_calculator.py:183-203)
-  double sig_l = 0.0, P_l = 0.0, tod_l = 0.0, sol_l = 0.0;
+  double sig_l = 0.0, P_l = 0.0, odk_l = 0.0, sol_l = 0.0;
+  bool tick_ok = true;
   if (lane < K) {
-    tod_l = tkp[lane].t_od_prev;  // the window's drivers, lane j <- tick j (readlane per tick)
+    const double tod = tkp[lane].t_od_prev;  // the window's drivers, lane j <- tick j (readlane per tick)
     sol_l = tkp[lane].solar;
+    odk_l = tod + 273.0;  // rc_apply's od_k, once per tick
+    tick_ok = fabs(tod) < 1048576.0 && fabs(sol_l) < 1099511627776.0;  // fast-division operand ranges
     for (int k = 0; k < p.n_cap; ++k) P_l += (double)red[lane * p.n_cap + k] * p.p_on[k];
     const double x = (P_l - tkp[lane].s_prev) / (double)p.n_global;
     sig_l = p.alpha_sig * (x * x) / p.norm_sig;
   }
+  const uint64_t tick_ok_bits = __ballot(tick_ok);
   const double P_last = readlane_f64(P_l, K - 1);
   if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P_last;
 
@@ -838,17 +842,22 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   const uint32_t o8 = i0 * 8u;
   const bool vec_rew = HPT == 2 && t.full && (rew_stride & 1) == 0 && (((uintptr_t)reward) & 15u) == 0;
 
+  double lo_tg[HPT], hi_tg[HPT];  // deadbandL2 thresholds (utils.py:4-23), once per window
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) {
+    hi_tg[h] = tg[h] + p.deadband / 2.0;
+    lo_tg[h] = tg[h] - p.deadband / 2.0;
+  }
+
   for (int j = 0; j < K; ++j) {
-    TickArgs tk;
-    tk.t_od_prev = readlane_f64(tod_l, j);
-    tk.solar = readlane_f64(sol_l, j);
+    const double od_k = readlane_f64(odk_l, j);
+    const double solar = readlane_f64(sol_l, j);
     const double sig = readlane_f64(sig_l, j);
     const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)j * act_stride : nullptr;
     bool house_ok = true;
 #pragma unroll
     for (int h = 0; h < HPT; ++h) house_ok = house_ok && fabs(T[h]) < 1048576.0 && fabs(Tm[h]) < 1048576.0;
-    const bool fast = params_ok && fabs(tk.t_od_prev) < 1048576.0 && fabs(tk.solar) < 1099511627776.0 &&
-                      __all(house_ok);
+    const bool fast = params_ok && ((tick_ok_bits >> j) & 1ull) && __all(house_ok);
     double rwd[HPT];
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
@@ -857,11 +866,19 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
       w[h] = hvac_fsm(w[h], a, p.dt, p.L);
       const double q = hv_on(w[h]) ? qc[h] : 0.0;
       double Tn, Tmn;
-      if (fast) rc_apply_win<true>(T[h], Tm[h], ua[h], hm[h], rw[h], q, tk.solar, tk.t_od_prev, Tn, Tmn);
-      else rc_apply_win<false>(T[h], Tm[h], ua[h], hm[h], rw[h], q, tk.solar, tk.t_od_prev, Tn, Tmn);
+      if (fast) rc_apply_win<true>(T[h], Tm[h], ua[h], hm[h], rw[h], q, solar, od_k, Tn, Tmn);
+      else rc_apply_win<false>(T[h], Tm[h], ua[h], hm[h], rw[h], q, solar, od_k, Tn, Tmn);
       T[h] = Tn;
       Tm[h] = Tmn;
-      const double tpen = p.alpha_temp * deadband_l2(tg[h], p.deadband, Tn);
+      double pen;
+      if (DB0) {
+        pen = deadband_l2_0(hi_tg[h], Tn);
+      } else {
+        pen = 0.0;
+        if (hi_tg[h] < Tn) { const double x = Tn - hi_tg[h]; pen = x * x; }
+        else if (lo_tg[h] > Tn) { const double x = lo_tg[h] - Tn; pen = x * x; }
+      }
+      const double tpen = p.alpha_temp * pen;
       rwd[h] = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig);
     }
     double* rrow = reward + (int64_t)j * rew_stride;
@@ -893,11 +910,14 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   }
 }
 
-#define MDR_INST_WIN(A, H)                                                                             \
-  template __global__ void k_step_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
-                                               const unsigned long long*, double*, int64_t, double*,      \
-                                               unsigned long long*, unsigned long long*, int);             \
-  template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, int,    \
+#define MDR_INST_WIN(A, H)                                                                               \
+  template __global__ void k_step_window<A, H, true>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
+                                                     const unsigned long long*, double*, int64_t, double*,      \
+                                                     unsigned long long*, unsigned long long*, int);             \
+  template __global__ void k_step_window<A, H, false>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
+                                                      const unsigned long long*, double*, int64_t, double*,      \
+                                                      unsigned long long*, unsigned long long*, int);             \
+  template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, int,             \
                                                 unsigned long long*);
 MDR_INST_WIN(MDR_ACT_RANDOM, 1)
 MDR_INST_WIN(MDR_ACT_ALWAYS_ON, 1)

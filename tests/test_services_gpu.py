@@ -40,7 +40,10 @@ def test_server_loop_matches_reference_services():
         desc = [loop.ui.description[step][k] for k in DESCRIPTION_KEYS]
         for k, got, ref in zip(DESCRIPTION_KEYS, desc, want_desc[step]):
             if k in ("Average temperature error",):
-                np.testing.assert_allclose(float(got), float(ref), rtol=1e-12, err_msg=f"{k} step {step}")
+                # a difference of two house sums (blocked device order vs the reference's house order):
+                # cancellation, so the bound is absolute
+                np.testing.assert_allclose(float(got), float(ref), rtol=1e-12, atol=1e-11,
+                                           err_msg=f"{k} step {step}")
             else:
                 assert got == ref, (k, step, got, ref)
         ui = loop.ui
