@@ -89,8 +89,11 @@ struct mdr_ctx {
   int tpw = 0;                           // k_step_pipe tiles per wave (MDR_TPW; 0: k_step_t)
   int win = kWindowMax;                  // ticks per k_step_window launch (MDR_WINDOW; 0: one-tick path)
   int win_hpt = 2;                       // houses per lane of k_step_window (MDR_WIN_HPT)
-  unsigned long long* d_wslab = nullptr; // 3 window count slabs [kWindowMax][kCountShards][n_cap]
+  unsigned long long* d_wslab = nullptr; // 3 window count slots (mdr_kernels.hip K1W: slab | red | rec)
   int wslab_len = 0;
+  bool wslab_dirty = true;               // the slots' shard part must be zero when a rollout starts
+  uint64_t* d_onb = nullptr;             // per-tick ON lane masks of the next window [tiles][HPT][kWindowMax]
+  uint32_t* d_wah = nullptr;             // FSM word at the end of the next window, per house
   bool coef_dirty = true;
   double* d_coef = nullptr;              // [6][n] r1, r2, A3, A4, e1, e2
   int* d_flags = nullptr;                // [0] params_bad
@@ -332,8 +335,11 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   if (const char* e = getenv("MDR_WINDOW")) c->win = atoi(e) < 0 ? 0 : atoi(e) > kWindowMax ? kWindowMax : atoi(e);
   if (cfg->n_cap <= kWindowCap) {
     // a window count slot: sharded slab | reduced counts (mdr_kernels.hip)
-    c->wslab_len = kWindowMax * kCountShards * cfg->n_cap + kWindowMax * cfg->n_cap;
-    if (hipMalloc(&c->d_wslab, 3 * sizeof(unsigned long long) * c->wslab_len) != hipSuccess)
+    c->wslab_len = kWindowMax * kCountShards * cfg->n_cap + kWindowMax * cfg->n_cap + kWindowMax * kWindowRec;
+    const size_t tiles64 = ((size_t)cfg->n_local + 63) / 64 + 1;  // 64-house lane groups (either HPT)
+    if (hipMalloc(&c->d_wslab, 3 * sizeof(unsigned long long) * c->wslab_len) != hipSuccess ||
+        hipMalloc(&c->d_onb, tiles64 * kWindowMax * sizeof(uint64_t)) != hipSuccess ||
+        hipMalloc(&c->d_wah, ((size_t)cfg->n_local + 1) * sizeof(uint32_t)) != hipSuccess)
       return cleanup(fail(MDR_ENOMEM, "window count slabs"));
   } else {
     c->win = 0;
@@ -380,6 +386,8 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->d_flags);
   hipFree(c->d_slab);
   hipFree(c->d_wslab);
+  hipFree(c->d_onb);
+  hipFree(c->d_wah);
   hipFree(c->d_pen_partial);
   hipFree(c->d_partial2);
   hipFree(c->d_ticks);
@@ -551,25 +559,39 @@ static int capture_graph(mdr_ctx* c, F&& launches, hipGraphExec_t* out) {
 }
 
 // ---- windowed rollout (k_step_window): open-loop action sources, individual_L2
+// (the lookahead's FSM runs on unsaturated seconds-since-off: L <= 2^30 - 1 and 33 ticks of dt
+// from a saturated value stay below 2^32 — mdr_kernels.hip win_run)
 static bool window_ok(const mdr_ctx* c, int mode) {
   return c->win > 0 && c->d_wslab && c->kp.n_cap <= kWindowCap && c->kp.penalty_mode == MDR_PEN_INDIVIDUAL_L2 &&
+         c->kp.L < (1 << 30) && c->kp.dt <= (1 << 26) &&
          (mode == MDR_ACT_RANDOM || mode == MDR_ACT_ALWAYS_ON || mode == MDR_ACT_BUFFER);
 }
 
+// the window slots' shard part is zero between rollouts (k_win_reduce zeroes what it reads);
+// after allocation or a failed launch sequence it is cleared once, outside any graph
+static int wslab_clean(mdr_ctx* c, hipStream_t st) {
+  if (!c->wslab_dirty || !c->d_wslab) return MDR_OK;
+  HIP_TRY(hipMemsetAsync(c->d_wslab, 0, 3 * sizeof(unsigned long long) * c->wslab_len, st));
+  c->wslab_dirty = false;
+  return MDR_OK;
+}
+
 // n ticks as ceil(n / win) windows of near-equal size: one k_count_window for the first window,
-// then one k_step_window per window (each counting the next window's ticks).  comm != nullptr:
-// sum-allreduce each window's count slab before its launch (sharded serial pipeline).
+// then per window k_win_reduce (shard sums -> counts + tick records; sharded: counts allreduced
+// first, records by k_win_final) and one k_step_window (counting the next window's ticks).
 static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t* action, int64_t act_stride,
                            int mode, double* reward, int64_t rew_stride, double* p_out, ncclComm_t comm,
                            hipStream_t st) {
   const int nw = (n + c->win - 1) / c->win;
   const int base = n / nw, rem = n % nw;
   auto wsz = [&](int w) { return base + (w < rem ? 1 : 0); };
-  auto slab = [&](int w) { return c->d_wslab + (size_t)(w % 3) * c->wslab_len; };
-  HIP_TRY(hipMemsetAsync(c->d_wslab, 0, 3 * sizeof(unsigned long long) * c->wslab_len, st));
+  auto slot = [&](int w) { return c->d_wslab + (size_t)(w % 3) * c->wslab_len; };
   const int hpt = c->win_hpt;
   const unsigned grid = blocks(blocks(c->kp.n, 64 * hpt), 4);  // one 64*hpt-house tile per wave, 4 waves per block
   KParams kp = c->kp;
+  const int ncap = kp.n_cap;
+  auto red = [&](int w) { return slot(w) + (size_t)kWindowMax * kCountShards * ncap; };
+  auto rec = [&](int w) { return reinterpret_cast<const double*>(red(w) + (size_t)kWindowMax * ncap); };
 #define MDR_WIN_DISPATCH_H(KERNEL, H, ...)                                                                     \
   do {                                                                                                         \
     if (mode == MDR_ACT_RANDOM) hipLaunchKernelGGL((KERNEL<MDR_ACT_RANDOM, H>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
@@ -581,37 +603,40 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     if (hpt == 1) MDR_WIN_DISPATCH_H(KERNEL, 1, __VA_ARGS__);            \
     else MDR_WIN_DISPATCH_H(KERNEL, 2, __VA_ARGS__);                     \
   } while (0)
-  // k_step_window: + the deadband = 0 specialisation (branch-free penalty)
+  // k_step_window: + the deadband 0 / norm_temp 1 specialisation (branch-free penalty, no division)
 #define MDR_WIN_DISPATCH_S(H, DB, ...)                                                                        \
   do {                                                                                                        \
     if (mode == MDR_ACT_RANDOM) hipLaunchKernelGGL((k_step_window<MDR_ACT_RANDOM, H, DB>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
     else if (mode == MDR_ACT_ALWAYS_ON) hipLaunchKernelGGL((k_step_window<MDR_ACT_ALWAYS_ON, H, DB>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
     else hipLaunchKernelGGL((k_step_window<MDR_ACT_BUFFER, H, DB>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
   } while (0)
-  const bool db0 = c->kp.deadband == 0.0;
+  const bool db0 = c->kp.deadband == 0.0 && c->kp.norm_temp == 1.0;
 #define MDR_STEP_WIN_DISPATCH(...)                                         \
   do {                                                                    \
     if (hpt == 1) { if (db0) MDR_WIN_DISPATCH_S(1, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(1, false, __VA_ARGS__); } \
     else { if (db0) MDR_WIN_DISPATCH_S(2, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(2, false, __VA_ARGS__); }        \
   } while (0)
-  const int ncap = c->kp.n_cap;
-  auto red = [&](int w) { return slab(w) + (size_t)kWindowMax * kCountShards * ncap; };
-  MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, wsz(0), slab(0));
+  c->wslab_dirty = true;  // until the sequence is fully issued
+  MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, wsz(0), slot(0), c->d_onb, c->d_wah);
   LAUNCH_CHECK("k_count_window");
   int t0 = 0;
   for (int w = 0; w < nw; ++w) {
     const int K = wsz(w), la = w + 1 < nw ? wsz(w + 1) : 0;
-    hipLaunchKernelGGL(k_win_reduce, dim3(1), dim3(256), 0, st, slab(w), K, ncap);
+    double* po = w == nw - 1 ? p_out : nullptr;
+    hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0, comm ? 0 : 1, po);
     LAUNCH_CHECK("k_win_reduce");
-    // sharded: every rank's per-tick class counts are summed (exact integers) before the launch
-    if (comm) RCCL_TRY(ncclAllReduce(red(w), red(w), (size_t)K * ncap, ncclUint64, ncclSum, comm, st));
+    if (comm) {  // sharded: every rank's per-tick class counts are summed (exact integers) first
+      RCCL_TRY(ncclAllReduce(red(w), red(w), (size_t)K * ncap, ncclUint64, ncclSum, comm, st));
+      hipLaunchKernelGGL(k_win_final, dim3(1), dim3(64), 0, st, kp, slot(w), K, tk + t0, po);
+      LAUNCH_CHECK("k_win_final");
+    }
     const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
-    MDR_STEP_WIN_DISPATCH(kp, a, act_stride, tk + t0, K, la, red(w), reward + (int64_t)t0 * rew_stride,
-                     rew_stride, w == nw - 1 ? p_out : nullptr, slab(w + 1), slab(w + 2),
-                     kWindowMax * kCountShards * ncap);
+    MDR_STEP_WIN_DISPATCH(kp, a, act_stride, tk + t0, K, la, rec(w), reward + (int64_t)t0 * rew_stride, rew_stride,
+                          c->d_onb, c->d_wah, slot(w + 1));
     LAUNCH_CHECK("k_step_window");
     t0 += K;
   }
+  c->wslab_dirty = false;
 #undef MDR_WIN_DISPATCH
 #undef MDR_WIN_DISPATCH_H
 #undef MDR_WIN_DISPATCH_S
@@ -663,6 +688,8 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   if (rc) return rc;
   rc = stage_ticks(c, n, ticks, st);
   if (rc) return rc;
+  rc = wslab_clean(c, st);
+  if (rc) return rc;
   const auto t1 = std::chrono::steady_clock::now();
   if (!use_graph) {
     rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st);
@@ -680,7 +707,10 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
     it = c->graphs.emplace(key, std::make_pair(ex, c->ring)).first;
   }
   const auto t2 = std::chrono::steady_clock::now();
-  HIP_TRY(hipGraphLaunch(it->second.first, st));
+  if (hipGraphLaunch(it->second.first, st) != hipSuccess) {
+    c->wslab_dirty = true;
+    return fail(MDR_EHIP, "mdr_rollout: hipGraphLaunch");
+  }
   c->ring = it->second.second;
   c->counts_ready = false;
   if (trace) {
@@ -966,6 +996,8 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
   rc = stage_ticks(c, n, ticks, st);
   if (rc) return rc;
   if (window_ok(c, mode)) {
+    rc = wslab_clean(c, st);
+    if (rc) return rc;
     rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, c->comm, st);
     c->counts_ready = false;
     return rc;

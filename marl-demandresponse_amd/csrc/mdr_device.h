@@ -166,19 +166,6 @@ __device__ __forceinline__ void rc_apply_t(double T, double Tm, double Ua, doubl
   Tm_out = tm_new - 273.0;
 }
 
-__device__ __forceinline__ void rc_apply(double T, double Tm, double Ua, double Ca, double Hm,
-                                         const RcCoef& k, double q_hvac, double solar, double t_od,
-                                         double& T_out, double& Tm_out) {
-  rc_apply_t<false>(T, Tm, Ua, Ca, Hm, k, q_hvac, solar, t_od, T_out, Tm_out);
-}
-
-__device__ __forceinline__ void rc_update(double T, double Tm, double Ua, double Ca, double Cm,
-                                          double Hm, double q_hvac, double solar, double t_od,
-                                          double dt, double& T_out, double& Tm_out) {
-  const RcCoef k = rc_coeffs(Ua, Ca, Cm, Hm, dt);
-  rc_apply(T, Tm, Ua, Ca, Hm, k, q_hvac, solar, t_od, T_out, Tm_out);
-}
-
 // deadbandL2 with deadband = 0 (the default): hi = lo = target + 0.0, and both branches of the
 // reference give (value - target)^2; value == target or NaN gives 0.0 — branch-free
 __device__ __forceinline__ double deadband_l2_0(double hi, double value) {
@@ -256,13 +243,6 @@ struct WaveRandom {
     return bit_of((uint32_t)__shfl((int)lo, src), (uint32_t)__shfl((int)hi, src), gid);
   }
 };
-
-// the same bit evaluated for one house alone (host-side checks / slow paths)
-__device__ __forceinline__ bool random_action(uint64_t seed, uint64_t gid, uint64_t tick) {
-  uint32_t lo, hi;
-  philox_words(seed, gid >> 6, tick, lo, hi);
-  return bit_of(lo, hi, gid);
-}
 
 __device__ __forceinline__ double u01(uint32_t x) { return ((double)x + 0.5) * 2.3283064365386963e-10; }
 

@@ -86,15 +86,17 @@ __global__ void k_step_pipe(KParams p, const uint8_t* action, TickArgs tk, const
 constexpr int kPipeMaxCap = 4;
 constexpr int kWindowMax = 32;  // = kWinMax: ticks per k_step_window launch
 constexpr int kWindowCap = 4;   // = kWinCap: capacity classes the window kernel supports
-template <int ACT, int HPT, bool DB0>
+constexpr int kWindowRec = 4;   // = kWinRec: doubles per tick record of a window count slot
+template <int ACT, int HPT, bool SIMPLE>  // SIMPLE: deadband 0 and norm_temp 1 (reward without branches / division)
 __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int K,
-                              int la_K, const unsigned long long* counts, double* reward, int64_t rew_stride,
-                              double* p_out, unsigned long long* next_slab, unsigned long long* zero_slab,
-                              int zero_len);
-__global__ void k_win_reduce(unsigned long long* slot, int nt, int n_cap);
+                              int la_K, const double* rec, double* reward, int64_t rew_stride, uint64_t* onb,
+                              uint32_t* wah, unsigned long long* next_slot);
+__global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, int fin,
+                             double* p_out);
+__global__ void k_win_final(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
 template <int ACT, int HPT>
 __global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int nt,
-                               unsigned long long* slab);
+                               unsigned long long* slot, uint64_t* onb, uint32_t* wah);
 __global__ void k_probe_stream(KParams p, double* reward);
 __global__ void k_refresh(KParams p, double* coef, int* params_bad);
 __global__ void k_div_check(const double* a, const double* b, int64_t n, unsigned long long* mismatches);

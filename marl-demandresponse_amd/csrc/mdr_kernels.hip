@@ -506,33 +506,31 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
 
 // --------------------------------------------------------------------------------------- K1W
 // Temporally blocked step for OPEN-LOOP action sources (random / always-on / action buffer), the
-// rollout path: one launch steps a window of K ticks.  Each wave loads its tile's state and
+// rollout path: one launch steps a window of K <= 32 ticks.  Each wave loads its tile's state and
 // parameters ONCE, keeps them in registers for the K ticks, and writes the state back once; per
-// tick it writes only the reward row.  Per house-step that is 8 B + 89 B / K of HBM traffic
-// instead of 89-99 B.  What makes it exact:
+// tick it writes only the reward row.  What makes it exact:
 //   * an open-loop source's actions do not depend on the thermal state, so the lockout FSM — and
 //     with it every tick's ON set and cluster power P(t) — can be run ahead of the thermal
-//     update.  The launch of window w runs the FSM through window w+1 (the "lookahead") and
-//     accumulates window w+1's per-tick ON counts per capacity class into its count slabs, so
-//     each tick's reward has its GLOBAL P(t) when the next launch starts (same integer counts as
-//     the one-tick kernels: bit-identical P);
+//     update.  The launch of window w runs the FSM through window w+1 (the "lookahead"): it
+//     counts window w+1's per-tick ON houses per capacity class (so each tick's reward has its
+//     GLOBAL P(t) when the next launch starts: the same integer counts as the one-tick kernels,
+//     bit-identical P), stores the per-tick ON lane masks and the FSM word at the end of window
+//     w+1.  The next launch's thermal loop then needs no FSM at all: a tick's heat source is
+//     selected by its stored ON mask;
+//   * the lookahead keeps the FSM's booleans as wave lane masks (SALU logic) and the random
+//     actions as lane masks built from the Philox words of the wave's 64-house groups, so a
+//     house-tick of lookahead costs four vector ops;
 //   * the parameter-only part of the RC update (roots r1/r2, A3/A4, exp(r dt) and the shared
 //     reciprocals of Ca, Ua and r2-r1) is computed once per window, not once per tick — the same
 //     expressions in the same order (rc_coeffs_t / recip), so results are bit-identical to the
 //     one-tick kernels, which recompute them every tick;
-//   * the per-tick drivers (t_od_prev, solar, s_prev) of the window are wave-uniform scalar loads
-//     of the staged mdr_tick array; the K signal penalties are reduced lane-parallel (lane j:
-//     tick j) from the count slabs at launch start and broadcast with readlane.
-// Counts layout: slab[j][kCountShards][n_cap] (u64) per window tick j.
+//   * per tick, the record {t_od_prev + 273, solar, signal penalty, range flag} is computed once
+//     by k_win_reduce (from the reduced counts) and read by the thermal loop with scalar loads.
+// Houses of a wave tile: 64 * HPT consecutive ids, house h of lane l = tile * 64 * HPT + 64 h + l
+// (coalesced 8-B accesses; lane l of house slot h is bit l of that slot's lane masks).
 constexpr int kWinMax = 32;    // ticks per window launch (and per lookahead)
 constexpr int kWinCap = 4;     // capacity classes held in registers
-
-__device__ __forceinline__ double readlane_f64(double v, int l) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readlane((int)b, l);
-  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
-  return __longlong_as_double(((long long)hi << 32) | (long long)(unsigned)lo);
-}
+constexpr int kWinRec = 4;     // doubles per tick record
 
 // Per-window thermal constants of one house (FAST path: shared reciprocals).
 struct RcWin {
@@ -583,92 +581,182 @@ __device__ __forceinline__ void rc_apply_win(double T, double Tm, double Ua, dou
   Tm_out = tm_new - 273.0;
 }
 
-// Philox words of the (64-house group, tick) slots a wave tile needs, in LDS:
-// slot s = j * G + g for tick offset j and group g0 + g (G = groups the tile spans, 2 or 3).
-__device__ __forceinline__ void win_random_stage(uint64_t seed, uint64_t g0, int G, const TickArgs* tkp, int nt,
-                                                 uint2* rw) {
-  const int lane = threadIdx.x & 63;
-  const int ns = G * nt;
-  for (int s = lane; s < ns; s += 64) {
-    const int j = s / G;
-    const int g = s - j * G;
-    uint32_t lo, hi;
-    philox_words(seed, g0 + (uint64_t)g, tkp[j].tick, lo, hi);
-    rw[s] = make_uint2(lo, hi);
+static_assert(kCountShards == 64, "k_win_reduce reduces the shards with one wave");
+
+// Window count slot (u64 units): [slab: kWinMax][kCountShards][n_cap] | [red: kWinMax][n_cap] |
+// [rec: kWinMax][kWinRec] (double).  Producers accumulate block histograms into the sharded slab;
+// k_win_reduce (the next graph node: the kernel boundary makes every producer atomic visible — an
+// in-kernel last-block reduction would need an agent-scope release fence per block, i.e. an L2
+// write-back on this multi-XCD chip) sums the shards into red, zeroes the shards for the slot's
+// next use, and writes the tick records.
+__device__ __forceinline__ unsigned long long* win_red(unsigned long long* slot, int n_cap) {
+  return slot + (size_t)kWinMax * kCountShards * n_cap;
+}
+__device__ __forceinline__ double* win_rec(unsigned long long* slot, int n_cap) {
+  return reinterpret_cast<double*>(win_red(slot, n_cap) + (size_t)kWinMax * n_cap);
+}
+
+// tick record j from the tick's global class counts (rewards_calculator.py:183-203 signal part;
+// the operations and order of the one-tick kernels)
+__device__ __forceinline__ void win_tick_record(const KParams& p, const unsigned long long* cnt, const TickArgs& tk,
+                                                double* rec, double* p_out) {
+  double P = 0.0;
+  for (int k = 0; k < p.n_cap; ++k) P += (double)cnt[k] * p.p_on[k];
+  const double x = (P - tk.s_prev) / (double)p.n_global;
+  rec[0] = tk.t_od_prev + 273.0;  // rc_apply's od_k
+  rec[1] = tk.solar;
+  rec[2] = p.alpha_sig * (x * x) / p.norm_sig;
+  rec[3] = fabs(tk.t_od_prev) < 1048576.0 && fabs(tk.solar) < 1099511627776.0 ? 1.0 : 0.0;  // fast-division ranges
+  if (p_out) *p_out = P;
+}
+
+// one block per tick j, one wave per class: sum the 64 shards, zero them; fin: + the tick record
+// (sharded rollouts: fin = 0, the records follow the cross-rank allreduce in k_win_final)
+__global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long long* __restrict__ slot, int nt,
+                                                    const TickArgs* __restrict__ tkp, int fin, double* p_out) {
+  __shared__ unsigned long long s_red[kWinCap];
+  const int j = blockIdx.x, c = threadIdx.x >> 6, q = threadIdx.x & 63, ncap = p.n_cap;
+  unsigned long long v = 0;
+  if (c < ncap) {
+    unsigned long long* e = &slot[((size_t)j * kCountShards + q) * ncap + c];
+    v = *e;
+    *e = 0ull;
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+  if (q == 0 && c < ncap) {
+    win_red(slot, ncap)[j * ncap + c] = v;
+    s_red[c] = v;
+  }
+  if (fin) {
+    __syncthreads();
+    if (threadIdx.x == 0)
+      win_tick_record(p, s_red, tkp[j], win_rec(slot, ncap) + j * kWinRec, j == nt - 1 ? p_out : nullptr);
   }
 }
 
-// the random actions of house gid for window ticks 0 .. nt-1 as bits of one 64-bit mask (LDS
-// reads once per window, none in the tick loop)
-__device__ __forceinline__ uint64_t win_random_mask(const uint2* rw, int G, uint64_t g0, int nt, uint64_t gid) {
-  uint64_t m = 0;
-  const int g = (int)((gid >> 6) - g0);
-  for (int j = 0; j < nt; ++j) {
-    const uint2 wd = rw[j * G + g];
-    m |= (uint64_t)bit_of(wd.x, wd.y, gid) << j;
+// tick records from the (allreduced) counts of a sharded rollout window
+__global__ void __launch_bounds__(64) k_win_final(KParams p, unsigned long long* __restrict__ slot, int nt,
+                                                  const TickArgs* __restrict__ tkp, double* p_out) {
+  const int j = threadIdx.x;
+  if (j < nt)
+    win_tick_record(p, win_red(slot, p.n_cap) + j * p.n_cap, tkp[j], win_rec(slot, p.n_cap) + j * kWinRec,
+                    j == nt - 1 ? p_out : nullptr);
+}
+
+// the wave tile: 64 * HPT consecutive houses, house slot h of lane l = i0 + 64 h
+template <int HPT>
+struct WinTile {
+  uint32_t tile, i0;
+  uint32_t idx[HPT];  // the lane's house per slot, clamped to n - 1 for loads
+  bool v[HPT];
+  uint64_t g0;        // first 64-house group of global ids the tile touches
+  int sh;             // global id of the tile's first house mod 64 (0 when the shard offset is aligned)
+  __device__ __forceinline__ WinTile(const KParams& p) {
+    const uint32_t n = (uint32_t)p.n;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    tile = blockIdx.x * (blockDim.x >> 6) + wv;
+    i0 = tile * (64u * HPT) + (uint32_t)(threadIdx.x & 63);
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) {
+      const uint32_t i = i0 + 64u * h;
+      v[h] = i < n;
+      idx[h] = v[h] ? i : n - 1u;
+    }
+    const uint64_t gbase = (uint64_t)p.goff + (uint64_t)tile * (64u * HPT);
+    g0 = gbase >> 6;
+    sh = (int)(gbase & 63u);
   }
-  return m;
+};
+
+__device__ __forceinline__ uint64_t readlane_u64(uint32_t lo, uint32_t hi, int l) {
+  return ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, l) << 32) |
+         (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, l);
 }
 
-template <int ACT>
-__device__ __forceinline__ bool win_action(const uint2* rw, int G, uint64_t g0, int j, uint64_t gid,
-                                           const uint8_t* arow, uint32_t i) {
-  if (ACT == MDR_ACT_ALWAYS_ON) return true;
-  if (ACT == MDR_ACT_BUFFER) return arow[i] != 0;
-  const uint2 wd = rw[j * G + (int)((gid >> 6) - g0)];
-  return bit_of(wd.x, wd.y, gid);
-}
-
-// FSM-only run of nt ticks (tick offsets j0 .. j0+nt-1 of the window) from words w[0..HPT), the
-// wave's ON count per tick and capacity class into its own LDS row cnt[j][kWinCap] (plain stores,
-// summed over the block's waves by win_flush).  Random actions come from the per-house bit masks
-// (bit j0 + j), the class membership from wave ballots taken once, so a tick costs the FSM, one
-// ballot per house slot and scalar bit counts.
+// FSM-only run of nt <= kWinMax ticks (HVAC.step, hvac.py:43-64; the transitions of hvac_fsm) from
+// the words w[h]; tkp / action: the run's first tick.  Per tick it counts the wave's ON houses per
+// capacity class into its LDS row cnt[t][kWinCap] and keeps the ON lane mask; at the end the lane
+// masks are stored to onb[h][t] (this wave's rows) and w[h] becomes the FSM word after the run.
+// The booleans (on, can, action) stay wave lane masks, so the per-house work of a tick is the
+// seconds-since-off arithmetic: one add, one select, one compare, one select.  Transitions use the
+// unsaturated sso (window_ok guarantees L < 2^30 and sso + kWinMax dt < 2^32), so saturating once
+// at the end gives the per-tick-saturated value; the lock bit is recomputed from the last tick.
 template <int ACT, int HPT>
-__device__ __forceinline__ void win_count(const KParams& p, const uint32_t* w_in, const int* cls, const bool* v,
-                                          const uint64_t* rmask, uint32_t i0, int j0, int nt,
-                                          const uint8_t* action, int64_t act_stride, unsigned* cnt) {
+__device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uint64_t (*cm)[kWinCap],
+                                        const WinTile<HPT>& t, const TickArgs* tkp, int nt, const uint8_t* action,
+                                        int64_t act_stride, unsigned* cnt, uint64_t* onb) {
   const int lane = threadIdx.x & 63;
-  uint32_t w[HPT];
-  uint64_t cm[HPT][kWinCap];
+  const uint32_t Lu = p.L < 0 ? 0u : (uint32_t)p.L, dt = (uint32_t)p.dt;
+  bool on[HPT];
+  uint32_t sso[HPT];
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
-    w[h] = w_in[h];
-#pragma unroll
-    for (int c = 0; c < kWinCap; ++c) cm[h][c] = __ballot(v[h] && cls[h] == c);
+    on[h] = (w[h] & kOnBit) != 0;
+    sso[h] = w[h] & kSsoMask;
   }
+  // Philox words of the run's ticks (random controller, mdr_device.h philox_words): lane l holds
+  // tick (l & 31) of group g0 + (l >> 5); lanes 0..31 of the second pair: group g0 + 2 (a tile of
+  // 128 houses off a 64-house boundary spans three groups)
+  uint32_t wa_lo = 0, wa_hi = 0, wb_lo = 0, wb_hi = 0;
+  const int G = HPT + (t.sh ? 1 : 0);
+  if (ACT == MDR_ACT_RANDOM) {
+    const int jj = lane & 31;
+    const uint64_t tick = tkp[jj < nt ? jj : 0].tick;
+    philox_words(p.seed, t.g0 + (uint64_t)(lane >> 5), tick, wa_lo, wa_hi);
+    if (G > 2) philox_words(p.seed, t.g0 + 2u, tick, wb_lo, wb_hi);
+  }
+  uint32_t ob_lo[HPT], ob_hi[HPT];  // lane j <- the ON lane mask of tick j
+  bool can[HPT] = {}, non[HPT] = {};
+  uint32_t s1[HPT] = {};
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) ob_lo[h] = ob_hi[h] = 0u;
   for (int j = 0; j < nt; ++j) {
-    const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)(j0 + j) * act_stride : nullptr;
-    uint64_t on[HPT];
+    uint64_t W[HPT + 1];
+    if (ACT == MDR_ACT_RANDOM) {
+      W[0] = readlane_u64(wa_lo, wa_hi, j);
+      if (HPT + 1 > 1) W[1] = G > 1 ? readlane_u64(wa_lo, wa_hi, j + 32) : 0ull;
+      if (HPT + 1 > 2) W[HPT] = G > 2 ? readlane_u64(wb_lo, wb_hi, j) : 0ull;
+    }
+    const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)j * act_stride : nullptr;
+    unsigned k[kWinCap] = {};
+    const bool me = lane == j;  // the lane that keeps tick j's masks
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
       bool a;
-      if (ACT == MDR_ACT_RANDOM) a = ((rmask[h] >> (j0 + j)) & 1ull) != 0;
-      else if (ACT == MDR_ACT_ALWAYS_ON) a = true;
-      else a = v[h] && arow[i0 + h] != 0;
-      w[h] = hvac_fsm(w[h], a, p.dt, p.L);
-      on[h] = __ballot(hv_on(w[h]));
+      if (ACT == MDR_ACT_RANDOM) {
+        const uint64_t m = t.sh ? (W[h] >> t.sh) | (W[h + 1] << (64 - t.sh)) : W[h];
+        a = __builtin_amdgcn_inverse_ballot_w64(m);
+      } else if (ACT == MDR_ACT_ALWAYS_ON) {
+        a = true;
+      } else {
+        a = arow[t.idx[h]] != 0;
+      }
+      s1[h] = on[h] ? sso[h] : sso[h] + dt;
+      can[h] = on[h] || s1[h] >= Lu;
+      non[h] = can[h] && a;
+      sso[h] = non[h] ? 0u : s1[h];
+      on[h] = non[h];
+      const uint64_t ob = __ballot(on[h]);
+      ob_lo[h] = me ? (uint32_t)ob : ob_lo[h];
+      ob_hi[h] = me ? (uint32_t)(ob >> 32) : ob_hi[h];
+#pragma unroll
+      for (int c = 0; c < kWinCap; ++c) k[c] += (unsigned)__popcll(ob & cm[h][c]);
     }
     if (lane == 0) {
 #pragma unroll
-      for (int c = 0; c < kWinCap; ++c) {
-        unsigned k = 0;
-#pragma unroll
-        for (int h = 0; h < HPT; ++h) k += (unsigned)__popcll(on[h] & cm[h][c]);
-        cnt[j * kWinCap + c] = k;
-      }
+      for (int c = 0; c < kWinCap; ++c) cnt[j * kWinCap + c] = k[c];
     }
   }
-}
-
-// Window count slot layout (u64): [slab: kWinMax][kCountShards][n_cap] | [red: kWinMax][n_cap].
-// Producers accumulate their block histograms into the sharded slab; k_win_reduce (one block,
-// the next graph node: the kernel boundary makes every producer atomic visible — an in-kernel
-// last-block reduction would need an agent-scope release fence per block, i.e. an L2 write-back
-// on this multi-XCD chip) sums the shards into red, the exact per-tick class counts a consumer
-// reads (n_cap values per tick instead of kCountShards * n_cap).
-__device__ __forceinline__ unsigned long long* win_red(unsigned long long* slot, int n_cap) {
-  return slot + (size_t)kWinMax * kCountShards * n_cap;
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) {
+    // the last tick's lockout (hvac.py:58-63): locked before the decision, or turned off with
+    // too little time to finish the lockout
+    const bool lock = nt > 0 && (!can[h] || (!non[h] && s1[h] + dt < Lu));
+    const uint32_t s = sso[h] < kSsoMask ? sso[h] : kSsoMask;
+    w[h] = s | (lock ? kLockBit : 0u) | (on[h] ? kOnBit : 0u);
+    if (lane < nt) onb[h * kWinMax + lane] = ((uint64_t)ob_hi[h] << 32) | ob_lo[h];
+  }
 }
 
 // sum the block's per-wave rows cnt[4][kWinMax][kWinCap] and add them to this block's slab shard
@@ -684,64 +772,38 @@ __device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsign
   }
 }
 
-__global__ void __launch_bounds__(256) k_win_reduce(unsigned long long* __restrict__ slot, int nt, int n_cap) {
-  unsigned long long* red = win_red(slot, n_cap);
-  for (int e = threadIdx.x; e < nt * n_cap; e += blockDim.x) {
-    const int j = e / n_cap, c = e - j * n_cap;
-    unsigned long long sum = 0;
-    for (int q = 0; q < kCountShards; ++q) sum += slot[((size_t)j * kCountShards + q) * n_cap + c];
-    red[j * n_cap + c] = sum;
-  }
+// class membership lane masks of the tile (valid houses only)
+template <int HPT>
+__device__ __forceinline__ void win_classes(const WinTile<HPT>& t, const int* cls, uint64_t (*cm)[kWinCap]) {
+#pragma unroll
+  for (int h = 0; h < HPT; ++h)
+#pragma unroll
+    for (int c = 0; c < kWinCap; ++c) cm[h][c] = __ballot(t.v[h] && cls[h] == c);
 }
 
-// the wave tile: 64 * HPT consecutive houses, HPT per lane; groups of 64 global ids it spans
-template <int HPT>
-struct WinTile {
-  uint32_t tile, i0;
-  bool v[HPT];
-  bool full;
-  uint64_t gid0, g0;
-  int G;
-  __device__ __forceinline__ WinTile(const KParams& p) {
-    const uint32_t n = (uint32_t)p.n;
-    tile = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    i0 = tile * (64u * HPT) + (uint32_t)(threadIdx.x & 63) * HPT;
-#pragma unroll
-    for (int h = 0; h < HPT; ++h) v[h] = i0 + h < n;
-    full = (tile + 1u) * (64u * HPT) <= n;
-    gid0 = (uint64_t)p.goff + i0;
-    const uint64_t gbase = (uint64_t)p.goff + (uint64_t)tile * (64u * HPT);
-    g0 = gbase >> 6;
-    G = (int)(((gbase + 64u * HPT - 1u) >> 6) - g0) + 1;
-  }
-};
-
-// First window of a rollout: ON counts of ticks 0 .. nt-1 (no state change).
+// First window of a rollout: ON counts, ON lane masks and end-of-window FSM words of ticks
+// 0 .. nt-1 from the current state (hvac itself is not changed).
 template <int ACT, int HPT>
 __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* __restrict__ action,
                                                       int64_t act_stride, const TickArgs* __restrict__ tkp, int nt,
-                                                      unsigned long long* __restrict__ slot) {
-  __shared__ uint2 s_rw[4][3 * kWinMax];
+                                                      unsigned long long* __restrict__ slot, uint64_t* __restrict__ onb,
+                                                      uint32_t* __restrict__ wah) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
-  const int tid = threadIdx.x, wv = tid >> 6;
+  const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
-  const uint32_t n = (uint32_t)p.n;
   uint32_t w[HPT];
   int cls[HPT];
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
-    const uint32_t i = t.v[h] ? t.i0 + h : n - 1u;
-    w[h] = p.hvac[i];
-    cls[h] = p.cap_idx[i];
+    w[h] = p.hvac[t.idx[h]];
+    cls[h] = p.cap_idx[t.idx[h]];
   }
-  uint64_t rmask[HPT] = {};
-  if (ACT == MDR_ACT_RANDOM) {
-    win_random_stage(p.seed, t.g0, t.G, tkp, nt, s_rw[wv]);
-    __syncthreads();
+  uint64_t cm[HPT][kWinCap];
+  win_classes<HPT>(t, cls, cm);
+  win_run<ACT, HPT>(p, w, cm, t, tkp, nt, action, act_stride, s_cnt[wv], onb + (size_t)t.tile * HPT * kWinMax);
 #pragma unroll
-    for (int h = 0; h < HPT; ++h) rmask[h] = win_random_mask(s_rw[wv], t.G, t.g0, nt, t.gid0 + h);
-  }
-  win_count<ACT, HPT>(p, w, cls, t.v, rmask, t.i0, 0, nt, action, act_stride, s_cnt[wv]);
+  for (int h = 0; h < HPT; ++h)
+    if (t.v[h]) wah[t.i0 + 64u * h] = w[h];
   __syncthreads();
   win_flush(p, nt, s_cnt, slot);
 }
@@ -753,172 +815,123 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
 #define MDR_WIN_OCC
 #endif
 
-// One window of K ticks.  red: the ticks' global ON counts per class [K][n_cap] (reduced by the
-// previous launch, allreduced across ranks when sharded); la_K > 0: run the FSM on through the
-// next la_K ticks (tkp[K..K+la_K), action rows K..) and count them into next_slot; block 0 zeroes
-// the slab part (zero_len u64) of zero_slot for the launch after next.
-template <int ACT, int HPT, bool DB0>
+// One window of K ticks.  slot: this window's slot (red counts are folded into its tick records);
+// onb / wah: the window's ON lane masks and end-of-window FSM words (from k_count_window or the
+// previous launch's lookahead), replaced by the next window's when la_K > 0: then the FSM runs on
+// through the next la_K ticks (tkp[K..K+la_K), action rows K..) and counts them into next_slot.
+template <int ACT, int HPT, bool SIMPLE>
 __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, const uint8_t* __restrict__ action,
                                                      int64_t act_stride, const TickArgs* __restrict__ tkp, int K,
-                                                     int la_K, const unsigned long long* __restrict__ red,
+                                                     int la_K, const double* __restrict__ rec,
                                                      double* __restrict__ reward, int64_t rew_stride,
-                                                     double* p_out, unsigned long long* next_slot,
-                                                     unsigned long long* zero_slab, int zero_len) {
-  __shared__ uint2 s_rw[4][3 * 2 * kWinMax];
+                                                     uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
+                                                     unsigned long long* __restrict__ next_slot) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (zero_slab && blockIdx.x == 0)
-    for (int j = tid; j < zero_len; j += blockDim.x) zero_slab[j] = 0ull;
-  const uint32_t n = (uint32_t)p.n;
+  const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
-  const uint32_t i0 = t.i0;
+  uint64_t* onb_w = onb + (size_t)t.tile * HPT * kWinMax;  // this wave's rows [HPT][kWinMax]
 
   // ---- state + parameters, once per window
-  double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
-  uint32_t w[HPT];
+  double T[HPT], Tm[HPT], ua[HPT], hm[HPT], tg[HPT];
+  uint32_t w_end[HPT];
   int cls[HPT];
-  if (HPT == 2) {
-    Tile2 tl;
-    load_tile2<false>(p, nullptr, i0, n, t.full, tl);
-    T[0] = tl.T.x; T[HPT - 1] = tl.T.y; Tm[0] = tl.Tm.x; Tm[HPT - 1] = tl.Tm.y;
-    ua[0] = tl.ua.x; ua[HPT - 1] = tl.ua.y; ca[0] = tl.ca.x; ca[HPT - 1] = tl.ca.y;
-    cm[0] = tl.cm.x; cm[HPT - 1] = tl.cm.y; hm[0] = tl.hm.x; hm[HPT - 1] = tl.hm.y;
-    tg[0] = tl.tg.x; tg[HPT - 1] = tl.tg.y; w[0] = tl.w.x; w[HPT - 1] = tl.w.y;
-    cls[0] = (int)(tl.cls & 0xFF); cls[HPT - 1] = (int)((tl.cls >> 8) & 0xFF);
-  } else {
+  RcWin rw[HPT];
+  const bool params_ok = !*p.params_bad && p.fast_tick_ok;
 #pragma unroll
-    for (int h = 0; h < HPT; ++h) {
-      const uint32_t i = t.v[h] ? i0 + h : n - 1u;
-      T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i]; cm[h] = p.cm[i];
-      hm[h] = p.hm[i]; tg[h] = p.target[i]; w[h] = p.hvac[i]; cls[h] = p.cap_idx[i];
+  for (int h = 0; h < HPT; ++h) {
+    const uint32_t i = t.idx[h];
+    T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; hm[h] = p.hm[i]; tg[h] = p.target[i];
+    w_end[h] = wah[i];
+    cls[h] = p.cap_idx[i];
+    const double ca = p.ca[i], cm = p.cm[i];
+    if (params_ok) {
+      rw[h] = rc_window(ua[h], ca, cm, hm[h], (double)p.dt);
+    } else {  // IEEE division (identical bits; parameters outside the fast-division range)
+      rw[h].k = rc_coeffs_t<false>(ua[h], ca, cm, hm[h], (double)p.dt);
+      rw[h].rCa.nb = -ca;
+      rw[h].rc.nb = -ua[h];
+      rw[h].rd.nb = -(rw[h].k.r2 - rw[h].k.r1);
+      rw[h].UaHm = ua[h] + hm[h];
     }
   }
   double q_on[kWinCap];
 #pragma unroll
-  for (int k = 0; k < kWinCap; ++k) q_on[k] = p.q_on[k < p.n_cap ? k : 0];
-
-  // ---- per-tick signal penalty of the window, lane j <- tick j (rewards_calculator.py:183-203)
-  double sig_l = 0.0, P_l = 0.0, odk_l = 0.0, sol_l = 0.0;
-  bool tick_ok = true;
-  if (lane < K) {
-    const double tod = tkp[lane].t_od_prev;  // the window's drivers, lane j <- tick j (readlane per tick)
-    sol_l = tkp[lane].solar;
-    odk_l = tod + 273.0;  // rc_apply's od_k, once per tick
-    tick_ok = fabs(tod) < 1048576.0 && fabs(sol_l) < 1099511627776.0;  // fast-division operand ranges
-    for (int k = 0; k < p.n_cap; ++k) P_l += (double)red[lane * p.n_cap + k] * p.p_on[k];
-    const double x = (P_l - tkp[lane].s_prev) / (double)p.n_global;
-    sig_l = p.alpha_sig * (x * x) / p.norm_sig;
-  }
-  const uint64_t tick_ok_bits = __ballot(tick_ok);
-  const double P_last = readlane_f64(P_l, K - 1);
-  if (p_out && blockIdx.x == 0 && tid == 0) *p_out = P_last;
-
-  // ---- random controller bits for the window + lookahead
-  if (ACT == MDR_ACT_RANDOM) {
-    win_random_stage(p.seed, t.g0, t.G, tkp, K + la_K, s_rw[wv]);
-    __syncthreads();  // random words staged
-  }
-
-  const bool params_ok = !*p.params_bad && p.fast_tick_ok;
-  double qc[HPT];
-  RcWin rw[HPT];
-  uint64_t rmask[HPT];
+  for (int c = 0; c < kWinCap; ++c) q_on[c] = p.q_on[c < p.n_cap ? c : 0];
+  double qc[HPT], lo_tg[HPT], hi_tg[HPT];  // heat when ON; deadbandL2 thresholds (utils.py:4-23)
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
     qc[h] = q_on[0];
 #pragma unroll
     for (int c = 1; c < kWinCap; ++c) qc[h] = cls[h] == c ? q_on[c] : qc[h];
-    if (params_ok) {
-      rw[h] = rc_window(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
-    } else {  // IEEE division (identical bits; parameters outside the fast-division range)
-      rw[h].k = rc_coeffs_t<false>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
-      rw[h].rCa.nb = -ca[h];
-      rw[h].rc.nb = -ua[h];
-      rw[h].rd.nb = -(rw[h].k.r2 - rw[h].k.r1);
-      rw[h].UaHm = ua[h] + hm[h];
-    }
-    rmask[h] = ACT == MDR_ACT_RANDOM ? win_random_mask(s_rw[wv], t.G, t.g0, K + la_K, t.gid0 + h) : 0ull;
-  }
-  const uint32_t o8 = i0 * 8u;
-  const bool vec_rew = HPT == 2 && t.full && (rew_stride & 1) == 0 && (((uintptr_t)reward) & 15u) == 0;
-
-  double lo_tg[HPT], hi_tg[HPT];  // deadbandL2 thresholds (utils.py:4-23), once per window
-#pragma unroll
-  for (int h = 0; h < HPT; ++h) {
     hi_tg[h] = tg[h] + p.deadband / 2.0;
     lo_tg[h] = tg[h] - p.deadband / 2.0;
   }
 
+  // ---- the K ticks: heat source from the stored ON masks, RC thermal, reward
   for (int j = 0; j < K; ++j) {
-    const double od_k = readlane_f64(odk_l, j);
-    const double solar = readlane_f64(sol_l, j);
-    const double sig = readlane_f64(sig_l, j);
-    const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)j * act_stride : nullptr;
+    const double od_k = rec[j * kWinRec + 0];
+    const double solar = rec[j * kWinRec + 1];
+    const double sig = rec[j * kWinRec + 2];
+    const bool tick_ok = rec[j * kWinRec + 3] != 0.0;
     bool house_ok = true;
 #pragma unroll
     for (int h = 0; h < HPT; ++h) house_ok = house_ok && fabs(T[h]) < 1048576.0 && fabs(Tm[h]) < 1048576.0;
-    const bool fast = params_ok && ((tick_ok_bits >> j) & 1ull) && __all(house_ok);
-    double rwd[HPT];
+    const bool fast = params_ok && tick_ok && __all(house_ok);
+    double* rrow = reward + (int64_t)j * rew_stride;
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
-      const bool a = t.v[h] && (ACT == MDR_ACT_RANDOM ? ((rmask[h] >> j) & 1ull) != 0
-                                                      : win_action<ACT>(s_rw[wv], t.G, t.g0, j, t.gid0 + h, arow, i0 + h));
-      w[h] = hvac_fsm(w[h], a, p.dt, p.L);
-      const double q = hv_on(w[h]) ? qc[h] : 0.0;
+      const bool on = __builtin_amdgcn_inverse_ballot_w64(onb_w[h * kWinMax + j]);
+      const double q = on ? qc[h] : 0.0;
       double Tn, Tmn;
       if (fast) rc_apply_win<true>(T[h], Tm[h], ua[h], hm[h], rw[h], q, solar, od_k, Tn, Tmn);
       else rc_apply_win<false>(T[h], Tm[h], ua[h], hm[h], rw[h], q, solar, od_k, Tn, Tmn);
       T[h] = Tn;
       Tm[h] = Tmn;
-      double pen;
-      if (DB0) {
-        pen = deadband_l2_0(hi_tg[h], Tn);
+      double r;
+      if (SIMPLE) {  // deadband 0, norm_temp 1 (the defaults): branch-free, no division
+        r = -(p.alpha_temp * deadband_l2_0(hi_tg[h], Tn) + sig);
       } else {
-        pen = 0.0;
+        double pen = 0.0;
         if (hi_tg[h] < Tn) { const double x = Tn - hi_tg[h]; pen = x * x; }
         else if (lo_tg[h] > Tn) { const double x = lo_tg[h] - Tn; pen = x * x; }
+        const double tpen = p.alpha_temp * pen;
+        r = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig);
       }
-      const double tpen = p.alpha_temp * pen;
-      rwd[h] = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig);
-    }
-    double* rrow = reward + (int64_t)j * rew_stride;
-    if (vec_rew) sto(rrow, o8, make_double2(rwd[0], rwd[HPT - 1]));
-    else {
-#pragma unroll
-      for (int h = 0; h < HPT; ++h)
-        if (t.v[h]) rrow[i0 + h] = rwd[h];
+      if (t.v[h]) rrow[t.i0 + 64u * h] = r;
     }
   }
 
-  // ---- state back, once per window
-  if (HPT == 2 && t.v[HPT - 1]) {
-    sto(p.t_air, o8, make_double2(T[0], T[HPT - 1]));
-    sto(p.t_mass, o8, make_double2(Tm[0], Tm[HPT - 1]));
-    sto(p.hvac, i0 * 4u, make_uint2(w[0], w[HPT - 1]));
-  } else {
+  // ---- state back, once per window (the FSM word at the window's end came with the ON masks)
+#pragma unroll
+  for (int h = 0; h < HPT; ++h)
+    if (t.v[h]) {
+      const uint32_t i = t.i0 + 64u * h;
+      p.t_air[i] = T[h]; p.t_mass[i] = Tm[h]; p.hvac[i] = w_end[h];
+    }
+
+  // ---- lookahead: the next window's ON masks, FSM words and class counts
+  if (la_K > 0) {
+    uint64_t cm[HPT][kWinCap];
+    win_classes<HPT>(t, cls, cm);
+    win_run<ACT, HPT>(p, w_end, cm, t, tkp + K, la_K,
+                      ACT == MDR_ACT_BUFFER ? action + (int64_t)K * act_stride : nullptr, act_stride, s_cnt[wv], onb_w);
 #pragma unroll
     for (int h = 0; h < HPT; ++h)
-      if (t.v[h]) { p.t_air[i0 + h] = T[h]; p.t_mass[i0 + h] = Tm[h]; p.hvac[i0 + h] = w[h]; }
-  }
-
-  // ---- lookahead: ON counts of the next window's ticks
-  if (la_K > 0) {
-    win_count<ACT, HPT>(p, w, cls, t.v, rmask, i0, K, la_K, ACT == MDR_ACT_BUFFER ? action : nullptr, act_stride,
-                        s_cnt[wv]);
+      if (t.v[h]) wah[t.i0 + 64u * h] = w_end[h];
     __syncthreads();
     win_flush(p, la_K, s_cnt, next_slot);
   }
 }
 
-#define MDR_INST_WIN(A, H)                                                                               \
+#define MDR_INST_WIN(A, H)                                                                                      \
   template __global__ void k_step_window<A, H, true>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
-                                                     const unsigned long long*, double*, int64_t, double*,      \
-                                                     unsigned long long*, unsigned long long*, int);             \
+                                                     const double*, double*, int64_t, uint64_t*, uint32_t*,      \
+                                                     unsigned long long*);                                      \
   template __global__ void k_step_window<A, H, false>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
-                                                      const unsigned long long*, double*, int64_t, double*,      \
-                                                      unsigned long long*, unsigned long long*, int);             \
-  template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, int,             \
-                                                unsigned long long*);
+                                                      const double*, double*, int64_t, uint64_t*, uint32_t*,      \
+                                                      unsigned long long*);                                      \
+  template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, int,            \
+                                                unsigned long long*, uint64_t*, uint32_t*);
 MDR_INST_WIN(MDR_ACT_RANDOM, 1)
 MDR_INST_WIN(MDR_ACT_ALWAYS_ON, 1)
 MDR_INST_WIN(MDR_ACT_BUFFER, 1)

@@ -189,6 +189,10 @@ def ptr(t) -> int:
 
 
 def stream_handle(device) -> int:
+    """The caller's current HIP stream on `device` (raw handle; no torch Stream object is built)."""
     import torch
 
-    return torch.cuda.current_stream(device).cuda_stream
+    idx = getattr(device, "index", None)
+    if idx is None:
+        return torch.cuda.current_stream(device).cuda_stream
+    return torch._C._cuda_getCurrentRawStream(idx)

@@ -15,6 +15,7 @@ from __future__ import annotations
 
 import datetime as _dt
 import functools
+import math as _math
 import random as _random
 
 import numpy as np
@@ -81,6 +82,63 @@ def od_day_list(temp_prop) -> list:
 @functools.lru_cache(maxsize=16)
 def _od_day(day_temp, night_temp, phase):
     return [_od_det(m // 60, m % 60, day_temp, night_temp, phase) for m in range(1440)]
+
+
+def od_day_floats(temp_prop) -> list:
+    """od_day_list as Python floats (the same values: np.float64 -> float is exact; float
+    arithmetic rounds like np.float64's and skips NumPy's scalar overhead)."""
+    return _od_day_f(temp_prop.day_temp, temp_prop.night_temp, temp_prop.phase)
+
+
+@functools.lru_cache(maxsize=16)
+def _od_day_f(day_temp, night_temp, phase):
+    return [float(x) for x in _od_day(day_temp, night_temp, phase)]
+
+
+def _gauss_n_inline(rng, n: int, sigma: float) -> list:
+    # random.Random.gauss (Lib/random.py, CPython 3.10) unrolled over n draws: the same pairs of
+    # random() calls, the same cached second value (gauss_next), the same `mu + z * sigma` with
+    # mu = 0 as the reference passes it (environment.py:132-159 via od_temp)
+    random, log, sqrt, cos, sin = rng.random, _math.log, _math.sqrt, _math.cos, _math.sin
+    out = []
+    z = rng.gauss_next
+    for _ in range(n):
+        if z is None:
+            x2pi = random() * _TWOPI
+            g2rad = sqrt(-2.0 * log(1.0 - random()))
+            out.append(0 + cos(x2pi) * g2rad * sigma)
+            z = sin(x2pi) * g2rad
+        else:
+            out.append(0 + z * sigma)
+            z = None
+    rng.gauss_next = z
+    return out
+
+
+def _gauss_n_calls(rng, n: int, sigma: float) -> list:
+    g = rng.gauss
+    return [g(0, sigma) for _ in range(n)]
+
+
+def _inline_matches() -> bool:
+    """The unrolled draw is used only if it reproduces this interpreter's random.gauss exactly
+    (values and the generator state after every draw)."""
+    a, b = _random.Random(20240611), _random.Random(20240611)
+    for n in (1, 2, 3, 7):
+        if _gauss_n_inline(a, n, 1.7) != [b.gauss(0, 1.7) for _ in range(n)] or a.getstate() != b.getstate():
+            return False
+    return True
+
+
+_TWOPI = 2.0 * _math.pi
+_GAUSS_N = _gauss_n_inline if _inline_matches() else _gauss_n_calls
+
+
+def gauss_n(rng, n: int, sigma: float) -> list:
+    """[rng.gauss(0, sigma) for _ in range(n)], bit for bit and in the same RNG order (rng: a
+    random.Random or the random module, whose bound functions share its hidden instance)."""
+    inst = getattr(rng, "_inst", rng)  # the `random` module draws from random._inst
+    return _GAUSS_N(inst, n, sigma)
 
 
 def od_daily(hour: int, minute: int, temp_prop):

@@ -409,16 +409,19 @@ class Environment:
         hp = p.cluster_prop.house_prop
         tp, grid = p.temp_prop, self.power_grid
         sig_tab = grid.day_table()
-        od_tab = drivers.od_day_list(tp)
-        gauss, std = self.rng.gauss, tp.temp_std
+        od_tab = drivers.od_day_floats(tp)
+        gs = drivers.gauss_n(self.rng, n, tp.temp_std)  # the n draws, in order (nothing else draws)
         dts = p.time_step.seconds
         d0 = self.date_time
         s = d0.hour * 3600 + d0.minute * 60 + d0.second
         solar_on, wa, shc = hp.solar_gain, hp.window_area, hp.shading_coeff
         month, mday, day_off = d0.month, d0.day, 0
         sol, last_m = 0.0, -1
-        tods, sols, sigs = [self.current_od_temp], [], [grid.current_signal]
-        for _ in range(n):
+        # flat [t_od_prev, solar, s_prev, 0.0] * n, then one array; the tick column is set below
+        tod, sig = float(self.current_od_temp), grid.current_signal
+        flat = []
+        push = flat.extend
+        for g in gs:
             # environment.py:86-106: the new datetime's solar gain, the previous OD temperature
             # for the step, then one gauss for the new OD temperature and the new signal
             s += dts
@@ -431,20 +434,17 @@ class Environment:
             if solar_on and m != last_m:
                 sol = drivers.solar_minute(month, mday, m // 60, m % 60, wa, shc)
                 last_m = m
-            sols.append(sol)
-            tods.append(od_tab[m] + gauss(0, std))
-            sigs.append(sig_tab[s])
-        buf = np.empty((n, 4), np.float64)
-        buf[:, 0] = tods[:n]
-        buf[:, 1] = sols
-        buf[:, 2] = sigs[:n]
+            push((tod, sol, sig, 0.0))
+            tod = od_tab[m] + g
+            sig = sig_tab[s]
+        buf = np.array(flat, np.float64).reshape(n, 4)
         tick0 = self._tick
         buf[:, 3].view(np.uint64)[:] = np.arange(tick0, tick0 + n, dtype=np.uint64)
         self.date_time = d0 + p.time_step * n
         self._solar, self._tick = sol, tick0 + n
-        self._tod_prev, self._s_prev = tods[n - 1], sigs[n - 1]
-        self.current_od_temp = tods[n]
-        grid.current_signal = sigs[n]
+        self._tod_prev, self._s_prev = flat[-4], flat[-2]
+        self.current_od_temp = np.float64(tod)
+        grid.current_signal = sig
         return TickWindow(buf)
 
     def _driver_window_loop(self, n_ticks: int) -> "TickWindow":

@@ -49,6 +49,14 @@ def main():
         line = [ln for ln in f if ln.startswith("{")][-1]
     with open(os.path.join(dst, f"{tag}_bench.json"), "w") as f:
         f.write(line)
+    for d in sorted(p for p in glob.glob(os.path.join(src, "stats_*")) if os.path.isdir(p)):  # WORKLOADS
+        w = os.path.basename(d)[len("stats_"):]
+        shutil.copy(os.path.join(d, "run_kernel_stats.csv"), os.path.join(dst, f"{tag}_{w}_kernel_stats.csv"))
+        with open(os.path.join(src, f"bench_{w}.log")) as f:
+            lines = [ln for ln in f if ln.startswith("{")]
+        if lines:
+            with open(os.path.join(dst, f"{tag}_{w}_bench.json"), "w") as f:
+                f.write(lines[-1])
     path = os.path.join(dst, "pmc_traffic.json")
     db = {}
     if os.path.exists(path):
