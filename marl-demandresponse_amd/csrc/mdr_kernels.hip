@@ -7,6 +7,8 @@
 // no contraction on this path.
 #include "mdr_kernels.h"
 
+#include <type_traits>
+
 #include "mdr_device.h"
 #include "mdr_obs_dev.h"
 
@@ -675,25 +677,28 @@ __device__ __forceinline__ uint64_t readlane_u64(uint32_t lo, uint32_t hi, int l
 }
 
 // FSM-only run of nt <= kWinMax ticks (HVAC.step, hvac.py:43-64; the transitions of hvac_fsm) from
-// the words w[h]; tkp / action: the run's first tick.  Per tick it counts the wave's ON houses per
-// capacity class into its LDS row cnt[t][kWinCap] and keeps the ON lane mask; at the end the lane
-// masks are stored to onb[h][t] (this wave's rows) and w[h] becomes the FSM word after the run.
-// The booleans (on, can, action) stay wave lane masks, so the per-house work of a tick is the
-// seconds-since-off arithmetic: one add, one select, one compare, one select.  Transitions use the
-// unsaturated sso (window_ok guarantees L < 2^30 and sso + kWinMax dt < 2^32), so saturating once
-// at the end gives the per-tick-saturated value; the lock bit is recomputed from the last tick.
+// the words w[h]; tkp / action: the run's first tick.  The booleans (on, can, action) are wave lane
+// masks carried in scalar registers, so the per-house work of a tick is the seconds-since-off
+// arithmetic: one select, one add, one compare, one select.  Each tick's ON masks go to the wave's
+// LDS rows msk[t][HPT]; at the end lane t counts tick t's ON houses per capacity class into
+// cnt[t][kWinCap], stores the masks to onb[t][HPT] (this wave's rows, read by the next window's
+// thermal loop) and w[h] becomes the FSM word after the run.  Transitions use the unsaturated
+// seconds-since-off (window_ok guarantees L < 2^30 and sso + (kWinMax + 1) dt < 2^32), so saturating
+// once at the end gives the per-tick-saturated value; the lock bit comes from the last tick.
 template <int ACT, int HPT>
 __device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uint64_t (*cm)[kWinCap],
                                         const WinTile<HPT>& t, const TickArgs* tkp, int nt, const uint8_t* action,
-                                        int64_t act_stride, unsigned* cnt, uint64_t* onb) {
+                                        int64_t act_stride, uint64_t* msk, unsigned* cnt, uint64_t* onb) {
   const int lane = threadIdx.x & 63;
   const uint32_t Lu = p.L < 0 ? 0u : (uint32_t)p.L, dt = (uint32_t)p.dt;
-  bool on[HPT];
-  uint32_t sso[HPT];
+  uint64_t on_m[HPT], can_m[HPT], non_m[HPT];
+  uint32_t sso[HPT], s1[HPT];
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
-    on[h] = (w[h] & kOnBit) != 0;
+    on_m[h] = __ballot((w[h] & kOnBit) != 0);
     sso[h] = w[h] & kSsoMask;
+    s1[h] = sso[h];
+    can_m[h] = non_m[h] = 0ull;
   }
   // Philox words of the run's ticks (random controller, mdr_device.h philox_words): lane l holds
   // tick (l & 31) of group g0 + (l >> 5); lanes 0..31 of the second pair: group g0 + 2 (a tile of
@@ -706,11 +711,6 @@ __device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uin
     philox_words(p.seed, t.g0 + (uint64_t)(lane >> 5), tick, wa_lo, wa_hi);
     if (G > 2) philox_words(p.seed, t.g0 + 2u, tick, wb_lo, wb_hi);
   }
-  uint32_t ob_lo[HPT], ob_hi[HPT];  // lane j <- the ON lane mask of tick j
-  bool can[HPT] = {}, non[HPT] = {};
-  uint32_t s1[HPT] = {};
-#pragma unroll
-  for (int h = 0; h < HPT; ++h) ob_lo[h] = ob_hi[h] = 0u;
   for (int j = 0; j < nt; ++j) {
     uint64_t W[HPT + 1];
     if (ACT == MDR_ACT_RANDOM) {
@@ -719,43 +719,45 @@ __device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uin
       if (HPT + 1 > 2) W[HPT] = G > 2 ? readlane_u64(wb_lo, wb_hi, j) : 0ull;
     }
     const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)j * act_stride : nullptr;
-    unsigned k[kWinCap] = {};
-    const bool me = lane == j;  // the lane that keeps tick j's masks
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
-      bool a;
-      if (ACT == MDR_ACT_RANDOM) {
-        const uint64_t m = t.sh ? (W[h] >> t.sh) | (W[h + 1] << (64 - t.sh)) : W[h];
-        a = __builtin_amdgcn_inverse_ballot_w64(m);
-      } else if (ACT == MDR_ACT_ALWAYS_ON) {
-        a = true;
-      } else {
-        a = arow[t.idx[h]] != 0;
-      }
-      s1[h] = on[h] ? sso[h] : sso[h] + dt;
-      can[h] = on[h] || s1[h] >= Lu;
-      non[h] = can[h] && a;
-      sso[h] = non[h] ? 0u : s1[h];
-      on[h] = non[h];
-      const uint64_t ob = __ballot(on[h]);
-      ob_lo[h] = me ? (uint32_t)ob : ob_lo[h];
-      ob_hi[h] = me ? (uint32_t)(ob >> 32) : ob_hi[h];
-#pragma unroll
-      for (int c = 0; c < kWinCap; ++c) k[c] += (unsigned)__popcll(ob & cm[h][c]);
+      uint64_t a;  // the actions as a lane mask
+      if (ACT == MDR_ACT_RANDOM) a = t.sh ? (W[h] >> t.sh) | (W[h + 1] << (64 - t.sh)) : W[h];
+      else if (ACT == MDR_ACT_ALWAYS_ON) a = ~0ull;
+      else a = __ballot(arow[t.idx[h]] != 0);
+      s1[h] = __builtin_amdgcn_inverse_ballot_w64(on_m[h]) ? sso[h] : sso[h] + dt;  // if not on: sso += dt
+      can_m[h] = on_m[h] | __ballot(s1[h] >= Lu);                                  // not locked
+      non_m[h] = can_m[h] & a;
+      sso[h] = __builtin_amdgcn_inverse_ballot_w64(non_m[h]) ? 0u : s1[h];
+      on_m[h] = non_m[h];
     }
     if (lane == 0) {
 #pragma unroll
-      for (int c = 0; c < kWinCap; ++c) cnt[j * kWinCap + c] = k[c];
+      for (int h = 0; h < HPT; ++h) msk[j * HPT + h] = on_m[h];
     }
   }
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
     // the last tick's lockout (hvac.py:58-63): locked before the decision, or turned off with
     // too little time to finish the lockout
-    const bool lock = nt > 0 && (!can[h] || (!non[h] && s1[h] + dt < Lu));
+    const uint64_t lock_m = nt > 0 ? ~can_m[h] | (~non_m[h] & __ballot(s1[h] + dt < Lu)) : 0ull;
     const uint32_t s = sso[h] < kSsoMask ? sso[h] : kSsoMask;
-    w[h] = s | (lock ? kLockBit : 0u) | (on[h] ? kOnBit : 0u);
-    if (lane < nt) onb[h * kWinMax + lane] = ((uint64_t)ob_hi[h] << 32) | ob_lo[h];
+    w[h] = s | (__builtin_amdgcn_inverse_ballot_w64(lock_m) ? kLockBit : 0u) |
+           (__builtin_amdgcn_inverse_ballot_w64(on_m[h]) ? kOnBit : 0u);
+  }
+  __builtin_amdgcn_wave_barrier();  // lane 0's LDS rows before the lanes read them (one wave)
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  if (lane < nt) {
+    unsigned k[kWinCap] = {};
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) {
+      const uint64_t m = msk[lane * HPT + h];
+      onb[lane * HPT + h] = m;
+#pragma unroll
+      for (int c = 0; c < kWinCap; ++c) k[c] += (unsigned)__popcll(m & cm[h][c]);
+    }
+#pragma unroll
+    for (int c = 0; c < kWinCap; ++c) cnt[lane * kWinCap + c] = k[c];
   }
 }
 
@@ -789,6 +791,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
                                                       unsigned long long* __restrict__ slot, uint64_t* __restrict__ onb,
                                                       uint32_t* __restrict__ wah) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
+  __shared__ uint64_t s_msk[4][kWinMax * HPT];
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
   uint32_t w[HPT];
@@ -800,7 +803,8 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
   }
   uint64_t cm[HPT][kWinCap];
   win_classes<HPT>(t, cls, cm);
-  win_run<ACT, HPT>(p, w, cm, t, tkp, nt, action, act_stride, s_cnt[wv], onb + (size_t)t.tile * HPT * kWinMax);
+  win_run<ACT, HPT>(p, w, cm, t, tkp, nt, action, act_stride, s_msk[wv], s_cnt[wv],
+                    onb + (size_t)t.tile * HPT * kWinMax);
 #pragma unroll
   for (int h = 0; h < HPT; ++h)
     if (t.v[h]) wah[t.i0 + 64u * h] = w[h];
@@ -827,9 +831,10 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
                                                      uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
                                                      unsigned long long* __restrict__ next_slot) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
+  __shared__ uint64_t s_msk[4][kWinMax * HPT];
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
-  uint64_t* onb_w = onb + (size_t)t.tile * HPT * kWinMax;  // this wave's rows [HPT][kWinMax]
+  uint64_t* onb_w = onb + (size_t)t.tile * HPT * kWinMax;  // this wave's rows [kWinMax][HPT]
 
   // ---- state + parameters, once per window
   double T[HPT], Tm[HPT], ua[HPT], hm[HPT], tg[HPT];
@@ -868,37 +873,61 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   }
 
   // ---- the K ticks: heat source from the stored ON masks, RC thermal, reward
+  // the tick's scalars (record, ON masks) are loaded one tick ahead (scalar loads, no vector work)
+  double r_od = rec[0], r_sol = rec[1], r_sig = rec[2];
+  uint64_t r_ok = __double_as_longlong(rec[3]);  // 1.0 or 0.0: compared as bits (scalar unit)
+  uint64_t r_on[HPT];
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) r_on[h] = onb_w[h];
+  const uint32_t rb = t.i0 * 8u;  // byte offset of the lane's house in a reward row (n < 2^29)
   for (int j = 0; j < K; ++j) {
-    const double od_k = rec[j * kWinRec + 0];
-    const double solar = rec[j * kWinRec + 1];
-    const double sig = rec[j * kWinRec + 2];
-    const bool tick_ok = rec[j * kWinRec + 3] != 0.0;
+    const double od_k = r_od, solar = r_sol, sig = r_sig;
+    const bool tick_ok = r_ok != 0;
+    uint64_t on_m[HPT];
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) on_m[h] = r_on[h];
+    const int jn = j + 1 < K ? j + 1 : j;
+    r_od = rec[jn * kWinRec + 0];
+    r_sol = rec[jn * kWinRec + 1];
+    r_sig = rec[jn * kWinRec + 2];
+    r_ok = __double_as_longlong(rec[jn * kWinRec + 3]);
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) r_on[h] = onb_w[jn * HPT + h];
     bool house_ok = true;
 #pragma unroll
     for (int h = 0; h < HPT; ++h) house_ok = house_ok && fabs(T[h]) < 1048576.0 && fabs(Tm[h]) < 1048576.0;
-    const bool fast = params_ok && tick_ok && __all(house_ok);
-    double* rrow = reward + (int64_t)j * rew_stride;
+    // all lanes in range: the comparison mask itself against exec (no vector round trip)
+    const bool fast = params_ok && tick_ok && __builtin_amdgcn_ballot_w64(house_ok) == __builtin_amdgcn_read_exec();
+    char* rrow = reinterpret_cast<char*>(reward + (int64_t)j * rew_stride);
+    auto houses = [&](auto fast_c) {
+      constexpr bool F = decltype(fast_c)::value;
 #pragma unroll
-    for (int h = 0; h < HPT; ++h) {
-      const bool on = __builtin_amdgcn_inverse_ballot_w64(onb_w[h * kWinMax + j]);
-      const double q = on ? qc[h] : 0.0;
-      double Tn, Tmn;
-      if (fast) rc_apply_win<true>(T[h], Tm[h], ua[h], hm[h], rw[h], q, solar, od_k, Tn, Tmn);
-      else rc_apply_win<false>(T[h], Tm[h], ua[h], hm[h], rw[h], q, solar, od_k, Tn, Tmn);
-      T[h] = Tn;
-      Tm[h] = Tmn;
-      double r;
-      if (SIMPLE) {  // deadband 0, norm_temp 1 (the defaults): branch-free, no division
-        r = -(p.alpha_temp * deadband_l2_0(hi_tg[h], Tn) + sig);
-      } else {
-        double pen = 0.0;
-        if (hi_tg[h] < Tn) { const double x = Tn - hi_tg[h]; pen = x * x; }
-        else if (lo_tg[h] > Tn) { const double x = lo_tg[h] - Tn; pen = x * x; }
-        const double tpen = p.alpha_temp * pen;
-        r = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig);
+      for (int h = 0; h < HPT; ++h) {
+        const bool on = __builtin_amdgcn_inverse_ballot_w64(on_m[h]);
+        const double q = on ? qc[h] : 0.0;
+        double Tn, Tmn;
+        rc_apply_win<F>(T[h], Tm[h], ua[h], hm[h], rw[h], q, solar, od_k, Tn, Tmn);
+        T[h] = Tn;
+        Tm[h] = Tmn;
+        double r;
+        if (SIMPLE) {  // deadband 0, norm_temp 1 (the defaults): no branches, no division
+          // on the fast path Tn is finite (the operand ranges checked above), so the reference's
+          // two comparisons reduce to x * x (x = 0 gives +0 either way); off it a NaN gives 0
+          const double x = Tn - hi_tg[h];
+          const double pen = F ? x * x : deadband_l2_0(hi_tg[h], Tn);
+          r = -(p.alpha_temp * pen + sig);
+        } else {
+          double pen = 0.0;
+          if (hi_tg[h] < Tn) { const double x = Tn - hi_tg[h]; pen = x * x; }
+          else if (lo_tg[h] > Tn) { const double x = lo_tg[h] - Tn; pen = x * x; }
+          const double tpen = p.alpha_temp * pen;
+          r = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig);
+        }
+        if (t.v[h]) *reinterpret_cast<double*>(rrow + (rb + 512u * h)) = r;
       }
-      if (t.v[h]) rrow[t.i0 + 64u * h] = r;
-    }
+    };
+    if (fast) houses(std::true_type());
+    else houses(std::false_type());
   }
 
   // ---- state back, once per window (the FSM word at the window's end came with the ON masks)
@@ -914,7 +943,8 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
     uint64_t cm[HPT][kWinCap];
     win_classes<HPT>(t, cls, cm);
     win_run<ACT, HPT>(p, w_end, cm, t, tkp + K, la_K,
-                      ACT == MDR_ACT_BUFFER ? action + (int64_t)K * act_stride : nullptr, act_stride, s_cnt[wv], onb_w);
+                      ACT == MDR_ACT_BUFFER ? action + (int64_t)K * act_stride : nullptr, act_stride, s_msk[wv],
+                      s_cnt[wv], onb_w);
 #pragma unroll
     for (int h = 0; h < HPT; ++h)
       if (t.v[h]) wah[t.i0 + 64u * h] = w_end[h];
