@@ -82,6 +82,14 @@ def parse():
                     help="seconds of non-environment device work before the timed region (GPU clock ramp; "
                          "off by default: measured to slow the host side of a short timed region ~3x, "
                          "profiles/r02c_bench20_trace.log)")
+    ap.add_argument("--host-spin-ms", type=float, default=3.0,
+                    help="milliseconds of an idle host busy-loop right before the clock starts (no environment "
+                         "or device work: keeps the core out of a low-power state after the GPU sync)")
+    ap.add_argument("--gc-off", action="store_true", help="diagnostics: disable Python's cyclic GC in the timed region")
+    ap.add_argument("--min-warmup-calls", type=int, default=3,
+                    help="warmup runs at least W steps AND at least this many rollout calls of the timed chunk "
+                         "size (graph capture + 2 replays: the first replay of a graph and of the host path is "
+                         "2-3x slower than the steady state, profiles/r02e_bench20_warmup.log)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--trace", action="store_true",
                     help="print host phase timestamps of the timed region to stderr (diagnostics)")
@@ -274,18 +282,21 @@ def main():
             for t in range(n):
                 env.greedy_actions(out=g_act)
                 env.step_tensor(g_act, rewards=rew[t])
-        else:
-            env.rollout(n, actions=None if acts is None else acts[:n], action_mode=args.mode,
-                        rewards=rew[:n])
+        else:  # (whole buffers when the chunk fills them: no tensor views built per call)
+            env.rollout(n, actions=None if acts is None else (acts if n == chunk else acts[:n]),
+                        action_mode=args.mode, rewards=rew if n == chunk else rew[:n])
 
     # warmup: captures the graphs of every chunk size used below
     done = 0
     for c in sorted(set(chunks)):
         run(c)
         done += c
-    while done < args.warmup:
+    calls = len(set(chunks))
+    while done < args.warmup or calls < args.min_warmup_calls:
         run(chunk)
         done += chunk
+        calls += 1
+    warm_steps = done
     torch.cuda.synchronize()
 
     def barrier():
@@ -328,6 +339,13 @@ def main():
 
         env.driver_window, sh.rollout = _dw, _ro
     ev0.record(launch_stream)  # on the idle stream, before the clock starts (not part of a step)
+    t_spin = time.perf_counter()
+    while time.perf_counter() - t_spin < args.host_spin_ms * 1e-3:
+        pass
+    if args.gc_off:
+        import gc
+
+        gc.disable()
     t0 = time.perf_counter()
     for c in chunks:
         run(c)
@@ -335,6 +353,8 @@ def main():
     t_sub = time.perf_counter()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
+    if args.gc_off:
+        gc.enable()
     if args.trace:
         env.driver_window, sh.rollout = dw, ro
         print("trace (us from t0): " + ", ".join(f"{k} {1e6 * (t - t0):.1f}" for k, t in trace) +
@@ -415,6 +435,7 @@ def main():
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "warmup_steps_run": warm_steps,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
         "scaling": "weak",
@@ -432,9 +453,12 @@ def main():
         "timed_region": {"wall_s": elapsed, "launch_stream_event_ms": gpu_ms,
                          "includes": "host drivers (OD-temperature RNG, solar, signal) + tick staging + "
                                      "graph launches + device work",
-                         "before": f"{args.warmup} warmup steps (graph capture of every chunk size)" +
+                         "before": f"{warm_steps} warmup steps (>= the {args.warmup} requested and >= "
+                                   f"{args.min_warmup_calls} rollout calls: graph capture of every chunk size, "
+                                   "then replays until the host path is in steady state)" +
                                    (f" and {args.clock_warmup:.2f} s of non-environment device work"
-                                    if args.clock_warmup > 0 else "")},
+                                    if args.clock_warmup > 0 else "") +
+                                   (f"; a {args.host_spin_ms:g} ms idle host busy-loop" if args.host_spin_ms > 0 else "")},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kern,
                      "kernel_avg_us": kern_ms * 1e3, "launches_timed": launches,

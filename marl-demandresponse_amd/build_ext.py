@@ -1,4 +1,5 @@
-"""Build libmdr_hip.so in-tree for gfx950 (hipcc, no JIT cache): ``python build_ext.py``.
+"""Build libmdr_hip.so in-tree for gfx950 (hipcc, no JIT cache) and the host-driver extension
+mdr_amd/_mdr_host (gcc, CPython C API): ``python build_ext.py``.
 
 Flags that matter for parity: ``-ffp-contract=off`` (no a*b+c fusion: the reference evaluates every
 operation with its own rounding) and no fast-math (correctly rounded fp64 division / sqrt).
@@ -37,6 +38,36 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(s) <= t for s in SRC + HDR + [__file__])
 
 
+HOST_SRC = os.path.join(HERE, "csrc", "mdr_host.c")
+
+
+def host_out() -> str:
+    import sysconfig
+
+    return os.path.join(HERE, "mdr_amd", "_mdr_host" + sysconfig.get_config_var("EXT_SUFFIX"))
+
+
+def build_host(force: bool = False, verbose: bool = False) -> str:
+    """The rollout host drivers (csrc/mdr_host.c) as a CPython extension next to the package."""
+    import sysconfig
+
+    out = host_out()
+    if not force and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(HOST_SRC),
+                                                                          os.path.getmtime(__file__)):
+        return out
+    cc = os.environ.get("CC", "gcc")
+    cmd = [cc, "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-Wall",
+           "-I" + sysconfig.get_paths()["include"], HOST_SRC, "-o", out + ".tmp", "-lm"]
+    if verbose:
+        print(" ".join(cmd), flush=True)
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        sys.stderr.write(r.stdout + r.stderr)
+        raise RuntimeError(f"{cc} failed ({r.returncode})")
+    os.replace(out + ".tmp", out)
+    return out
+
+
 def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()) -> str:
     """Build the library (``defines``: extra -D flags for A/B variants built next to it, e.g.
     ``out=mdr_amd/libmdr_w4.so, defines=["MDR_WIN_WAVES=4"]``, loaded with MDR_LIB=...)."""
@@ -63,3 +94,4 @@ if __name__ == "__main__":
         print(build(force=True, verbose=True, out=os.path.join(HERE, "mdr_amd", f"libmdr_{name}.so"), defines=defs))
     else:
         print(build(force="--force" in sys.argv, verbose=True))
+        print(build_host(force="--force" in sys.argv, verbose=True))

@@ -555,6 +555,9 @@ static int capture_graph(mdr_ctx* c, F&& launches, hipGraphExec_t* out) {
   e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
   hipGraphDestroy(g);
   if (e != hipSuccess) return fail(MDR_EHIP, std::string("instantiate: ") + hipGetErrorString(e));
+  // upload the executable graph now (capture time), not on its first replay
+  e = hipGraphUpload(*out, c->cap_stream);
+  if (e != hipSuccess) return fail(MDR_EHIP, std::string("graph upload: ") + hipGetErrorString(e));
   return MDR_OK;
 }
 

@@ -30,6 +30,10 @@ SOLAR_TERMS = (
 )
 
 
+SOLAR_TERMS_ARRAY = np.array(SOLAR_TERMS, np.float64).reshape(-1)  # for the host-driver extension
+SOLAR_TERMS_ARRAY.setflags(write=False)
+
+
 def _powf(v: float, k: int) -> float:
     return v if k == 1 else v ** k
 
@@ -82,6 +86,25 @@ def od_day_list(temp_prop) -> list:
 @functools.lru_cache(maxsize=16)
 def _od_day(day_temp, night_temp, phase):
     return [_od_det(m // 60, m % 60, day_temp, night_temp, phase) for m in range(1440)]
+
+
+def od_day_array(temp_prop) -> np.ndarray:
+    """od_day_list as a float64[1440] array (cached per config; the host-driver extension's table)."""
+    return _od_day_a(temp_prop.day_temp, temp_prop.night_temp, temp_prop.phase)
+
+
+@functools.lru_cache(maxsize=16)
+def _od_day_a(day_temp, night_temp, phase):
+    a = np.array(_od_day(day_temp, night_temp, phase), np.float64)
+    a.setflags(write=False)
+    return a
+
+
+@functools.lru_cache(maxsize=64)
+def solar_day_table(month: int, day: int, window_area: float, shading_coeff: float) -> np.ndarray:
+    """Per-minute solar gain of one (month, day), filled on demand by the host-driver extension
+    (NaN = not computed yet; each value is solar_minute's)."""
+    return np.full(1440, np.nan, np.float64)
 
 
 def od_day_floats(temp_prop) -> list:

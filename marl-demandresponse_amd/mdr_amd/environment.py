@@ -31,6 +31,11 @@ from .drivers import GridSignal, od_temp, reward_normalisers, solar_gain
 from .lazydict import LazyDict
 from .shard import HipShard, encode_hvac
 
+try:  # the rollout host drivers in C (csrc/mdr_host.c, built by build_ext.py); host code only
+    from . import _mdr_host as _host
+except ImportError:  # pragma: no cover - the Python loop computes the same values
+    _host = None
+
 ACTION_MODES = {"buffer": L.ACT_BUFFER, "random": L.ACT_RANDOM, "always_on": L.ACT_ALWAYS_ON,
                 "bangbang": L.ACT_BANGBANG, "deadband_bangbang": L.ACT_DEADBAND_BANGBANG}
 
@@ -399,6 +404,43 @@ class Environment:
 
     def _driver_window_vec(self, n: int) -> "TickWindow":
         """driver_window for a constant base power and a flat / sinusoidal / regular-steps signal:
+        the host-driver extension (csrc/mdr_host.c) when it is built, else the Python loop below
+        (the same values bit for bit: tests/test_driver_window.py)."""
+        if _host is None:
+            return self._driver_window_vec_py(n)
+        p = self.init_props
+        hp = p.cluster_prop.house_prop
+        tp, grid = p.temp_prop, self.power_grid
+        sig_tab = grid.day_table()
+        od_tab = drivers.od_day_array(tp)
+        dts = p.time_step.seconds
+        d0 = self.date_time
+        s = d0.hour * 3600 + d0.minute * 60 + d0.second
+        rng = getattr(self.rng, "_inst", self.rng)  # the `random` module draws from random._inst
+        solar_on, wa, shc = hp.solar_gain, hp.window_area, hp.shading_coeff
+        buf = np.empty((n, 4), np.float64)
+        tod, sig, sol = float(self.current_od_temp), float(grid.current_signal), 0.0
+        tick0, done, day_off = self._tick, 0, 0
+        while True:
+            dd = d0 + _dt.timedelta(days=day_off) if day_off else d0
+            sol_tab = drivers.solar_day_table(dd.month, dd.day, wa, shc) if solar_on else None
+            k, s, tod, sig, sol = _host.drivers(rng, rng.random, tp.temp_std, n - done, s, dts, od_tab, sig_tab,
+                                                sol_tab, dd.month, dd.day, wa, shc, drivers.SOLAR_TERMS_ARRAY,
+                                                tod, sig, sol, tick0 + done, buf[done:])
+            done += k
+            if done == n:
+                break
+            s -= 86400  # the next tick is on the next day
+            day_off += 1
+        self.date_time = d0 + p.time_step * n
+        self._solar, self._tick = sol, tick0 + n
+        self._tod_prev, self._s_prev = buf[n - 1, 0], buf[n - 1, 2]
+        self.current_od_temp = np.float64(tod)
+        grid.current_signal = np.float64(sig)
+        return TickWindow(buf)
+
+    def _driver_window_vec_py(self, n: int) -> "TickWindow":
+        """driver_window for a constant base power and a flat / sinusoidal / regular-steps signal:
         the same values as the per-tick loop, bit for bit (tests/test_driver_window.py), from
         per-day lookup tables built at reset — the regulation signal by second of the day
         (GridSignal.day_table) and the outdoor-temperature daily curve by minute
@@ -527,8 +569,9 @@ class Environment:
         while done < n_ticks:  # one window unless interpolation ends it early (driver_window)
             ticks = self.driver_window(n_ticks - done)
             k = len(ticks)
-            a = None if actions is None else actions[done:done + k]
-            r = rewards[done:done + k] if rew_stride else rewards
+            whole = done == 0 and k == n_ticks  # one window: the caller's buffers as they are
+            a = None if actions is None else (actions if whole and actions.shape[0] == k else actions[done:done + k])
+            r = rewards[done:done + k] if rew_stride and not (whole and rewards.shape[0] == k) else rewards
             if self._comm is not None:
                 self._comm.rollout(sh, ticks, a, mode, r, rew_stride)
             else:

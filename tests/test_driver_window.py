@@ -15,7 +15,8 @@ from oracle_shard import OracleShard
 CASES = [("sinusoidals", True, dt.datetime(2021, 1, 31, 23, 50), 600),
          ("sinusoidals", False, dt.datetime(2021, 6, 1, 7, 28, 30), 37),
          ("flat", True, dt.datetime(2021, 3, 14, 17, 59, 58), 200),
-         ("regular_steps", True, dt.datetime(2021, 12, 31, 23, 59, 2), 333)]
+         ("regular_steps", True, dt.datetime(2021, 12, 31, 23, 59, 2), 333),
+         ("flat", True, dt.datetime(2021, 5, 9, 6, 0), 30000)]  # 33 h: every daylight minute's solar gain
 
 
 def _env(mode, solar, start, seed):
@@ -28,11 +29,11 @@ def _env(mode, solar, start, seed):
     return Environment(props, rng=random.Random(seed), _shard_factory=OracleShard)
 
 
-def _check(mode, solar, start, n):
+def _check(mode, solar, start, n, vec="_driver_window_vec"):
     a, b = _env(mode, solar, start, 11), _env(mode, solar, start, 11)
     assert a._vector_drivers_ok()
     for rep in range(2):
-        wa = a._driver_window_vec(n)
+        wa = getattr(a, vec)(n)
         wb = b._driver_window_loop(n)
         np.testing.assert_array_equal(wa.a.view(np.uint64), wb.a.view(np.uint64))  # bitwise, incl. tick
         assert a.date_time == b.date_time
@@ -46,6 +47,44 @@ def _check(mode, solar, start, n):
 @pytest.mark.parametrize("mode,solar,start,n", CASES)
 def test_vector_drivers_equal_loop(mode, solar, start, n):
     _check(mode, solar, start, n)
+
+
+@pytest.mark.parametrize("mode,solar,start,n", CASES)
+def test_python_vector_drivers_equal_loop(mode, solar, start, n):
+    _check(mode, solar, start, n, vec="_driver_window_vec_py")
+
+
+def test_native_drivers_built():
+    """The C host drivers (csrc/mdr_host.c) are the ones driver_window runs."""
+    from mdr_amd import environment
+
+    assert environment._host is not None
+
+
+def test_native_drivers_module_rng_and_short_windows():
+    """The `random` module as the generator (its hidden instance), a cached gauss_next carried
+    across calls, windows of 1 and 2 ticks."""
+    import random as R
+
+    from mdr_amd.environment import Environment
+
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": 10, "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    props.start_datetime = dt.datetime(2021, 7, 4, 23, 59, 50)
+    props.start_datetime_mode = "fixed"
+    R.seed(5)
+    a = Environment(props, rng=R, _shard_factory=OracleShard)
+    R.seed(5)
+    b = Environment(props, rng=R, _shard_factory=OracleShard)
+    R.seed(7)
+    R.gauss(0, 1)  # leaves a cached deviate
+    st = R.getstate()
+    outs = []
+    for env, f in ((a, "_driver_window_vec"), (b, "_driver_window_loop")):
+        R.setstate(st)
+        rows = [getattr(env, f)(k).a.copy() for k in (2, 1, 3, 7)]
+        outs.append((np.concatenate(rows).view(np.uint64), R.getstate()))
+    np.testing.assert_array_equal(outs[0][0], outs[1][0])
+    assert outs[0][1] == outs[1][1]
 
 
 @pytest.mark.gpu
