@@ -75,8 +75,10 @@ def parse():
     ap.add_argument("--chunk", type=int, default=128, help="ticks per graph-captured rollout call")
     ap.add_argument("--window", type=int, default=32,
                     help="ticks per temporally blocked launch (k_step_window, <= 32); 0 = one launch per tick")
-    ap.add_argument("--kernel-ticks", type=int, default=512,
+    ap.add_argument("--kernel-ticks", type=int, default=1024,
                     help="ticks of the kernel-only timing after the timed region (roofline.kernel_avg_us)")
+    ap.add_argument("--kernel-warm-ticks", type=int, default=2048,
+                    help="untimed kernel-only ticks before that timing (the GPU at its steady-state clock)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline time budget")
     ap.add_argument("--clock-warmup", type=float, default=0.0,
                     help="seconds of non-environment device work before the timed region (GPU clock ramp; "
@@ -377,22 +379,29 @@ def main():
     mode_id = L.ACT_RANDOM if args.mode == "random" else L.ACT_BUFFER
     simple = env.init_props.cluster_prop.house_prop.deadband == 0.0 and env._norm_temp == 1.0
     kern = step_kernel_name(n_loc, args.mode, window, simple)
-    actor_ms = None
+    actor_ms = graph_ms = None
     if dactor is None and g_act is None:
         kbuf = torch.empty((kt, n_loc), dtype=torch.float64, device=dev)
         kacts = None if acts is None else (torch.rand((kt, n_loc), device=dev) < 0.5).to(torch.uint8)
         kticks = env.driver_window(kt)
         ls = sh.launch_stream(True)
-        for rep in range(2):  # capture, then the timed replay
+        for rep in range(2):  # the whole graph (count, reduce and step kernels): capture, then a timed replay
             if rep:
                 torch.cuda.synchronize()
                 ev0.record(ls)
             sh.rollout(kticks, kacts, n_loc if kacts is not None else 0, mode_id, kbuf, n_loc, True)
         ev1.record(ls)
         torch.cuda.synchronize()
+        graph_ms = ev0.elapsed_time(ev1)
+        # the step kernel ALONE, in steady state: --kernel-warm-ticks untimed, then the same rollout
+        # issued directly with hipExtLaunchKernel start/stop events around every step-kernel launch
+        # (mdr_time_step_kernels), averaged over its launches
+        for _ in range(max(args.kernel_warm_ticks, 0) // kt):
+            sh.rollout(env.driver_window(kt), kacts, n_loc if kacts is not None else 0, mode_id, kbuf, n_loc, True)
+        step_ms, launches = sh.time_step_kernels(env.driver_window(kt), kacts, n_loc if kacts is not None else 0,
+                                                 mode_id, kbuf, n_loc)
         del kbuf
-        launches = -(-kt // window) if window > 0 else kt
-        kern_ms = ev0.elapsed_time(ev1) / launches
+        kern_ms = step_ms / launches
         k_win = kt // launches if window > 0 else 1
         bytes_launch = window_bytes(n_loc, k_win, args.mode) if window > 0 else BYTES_PER_HOUSE_STEP * n_loc
         steps_launch = k_win
@@ -462,10 +471,12 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "kernel": kern,
                      "kernel_avg_us": kern_ms * 1e3, "launches_timed": launches,
+                     "graph_us_per_launch": None if graph_ms is None else graph_ms * 1e3 / launches,
                      "house_steps_per_launch": steps_launch * n_loc,
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "bytes_per_house_step": bytes_launch / (steps_launch * n_loc),
-                     "timing": "HIP events around a graph replay of >= 500 ticks after the timed region"},
+                     "timing": "hipExtLaunchKernel start/stop events around each step-kernel launch of a 1024-tick rollout "
+                  "after the timed region and 2048 untimed kernel-only ticks (steady-state clock)"},
     }
     if g_act is not None:
         out["data"] = "synthetic (device Philox population, reference noise model)"

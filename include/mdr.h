@@ -210,6 +210,14 @@ int mdr_rollout(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t*
  * mdr_rollout_sharded; drops cached rollout graphs. */
 int mdr_set_rollout_window(mdr_ctx* ctx, int ticks);
 
+/* Measurement (no reference counterpart): mdr_rollout's launch sequence issued directly (no graph)
+ * with an event pair around every step-kernel launch; *ms = the summed step-kernel time,
+ * *launches = step launches (windows, or ticks on the one-tick path).  Advances the state like
+ * mdr_rollout; synchronises the stream. */
+int mdr_time_step_kernels(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t* action,
+                          int64_t act_stride, int action_mode, double* reward, int64_t rew_stride,
+                          void* stream, float* ms, int* launches);
+
 /* ---- observation vector (norm_state_dict, norm.py:178-218) ----------------------------- */
 typedef struct mdr_obs_spec {
   int32_t n_feat;        /* features per house written (row length of obs) */

@@ -2,6 +2,7 @@
 //
 // The C ABI (include/mdr.h) is what the Python layer (mdr_amd, via ctypes) and any other host
 // binds.  It owns only small scratch; every launch goes to the caller's stream.
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
@@ -119,6 +120,7 @@ struct mdr_ctx {
   hipStream_t cap_stream = nullptr;      // graph capture (graphs are replayed on the caller's stream)
   hipEvent_t ev_k1[kSlabs] = {}, ev_ar[kSlabs] = {}, ev_pc = nullptr;
   hipEvent_t ev[16] = {};
+  std::vector<hipEvent_t>* step_events = nullptr;  // mdr_time_step_kernels: events around each step launch
   // MA-PPO actor (row P): packed weight image, per-tick obs scalars of actor rollouts
   unsigned char* d_actor = nullptr;
   size_t actor_cap = 0;
@@ -562,6 +564,16 @@ static int capture_graph(mdr_ctx* c, F&& launches, hipGraphExec_t* out) {
 }
 
 // ---- windowed rollout (k_step_window): open-loop action sources, individual_L2
+// mdr_time_step_kernels: an event pair around each step-kernel launch (direct launches only)
+static int step_mark(mdr_ctx* c, hipStream_t st) {
+  if (!c->step_events) return MDR_OK;
+  hipEvent_t e;
+  HIP_TRY(hipEventCreate(&e));
+  c->step_events->push_back(e);
+  HIP_TRY(hipEventRecord(e, st));
+  return MDR_OK;
+}
+
 // (the lookahead's FSM runs on unsaturated seconds-since-off: L <= 2^30 - 1 and 33 ticks of dt
 // from a saturated value stay below 2^32 — mdr_kernels.hip win_run)
 static bool window_ok(const mdr_ctx* c, int mode) {
@@ -607,11 +619,18 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     else MDR_WIN_DISPATCH_H(KERNEL, 2, __VA_ARGS__);                     \
   } while (0)
   // k_step_window: + the deadband 0 / norm_temp 1 specialisation (branch-free penalty, no division)
+  // (mdr_time_step_kernels: hipExtLaunchKernel's start / stop events time the step kernel itself)
+  hipEvent_t t_start = nullptr, t_stop = nullptr;
+#define MDR_STEP_LAUNCH(KERNEL, ...)                                                                       \
+  do {                                                                                                     \
+    if (t_start) hipExtLaunchKernelGGL((KERNEL), dim3(grid), dim3(256), 0, st, t_start, t_stop, 0, __VA_ARGS__); \
+    else hipLaunchKernelGGL((KERNEL), dim3(grid), dim3(256), 0, st, __VA_ARGS__);                          \
+  } while (0)
 #define MDR_WIN_DISPATCH_S(H, DB, ...)                                                                        \
   do {                                                                                                        \
-    if (mode == MDR_ACT_RANDOM) hipLaunchKernelGGL((k_step_window<MDR_ACT_RANDOM, H, DB>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
-    else if (mode == MDR_ACT_ALWAYS_ON) hipLaunchKernelGGL((k_step_window<MDR_ACT_ALWAYS_ON, H, DB>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
-    else hipLaunchKernelGGL((k_step_window<MDR_ACT_BUFFER, H, DB>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
+    if (mode == MDR_ACT_RANDOM) MDR_STEP_LAUNCH((k_step_window<MDR_ACT_RANDOM, H, DB>), __VA_ARGS__);        \
+    else if (mode == MDR_ACT_ALWAYS_ON) MDR_STEP_LAUNCH((k_step_window<MDR_ACT_ALWAYS_ON, H, DB>), __VA_ARGS__); \
+    else MDR_STEP_LAUNCH((k_step_window<MDR_ACT_BUFFER, H, DB>), __VA_ARGS__);                              \
   } while (0)
   const bool db0 = c->kp.deadband == 0.0 && c->kp.norm_temp == 1.0;
 #define MDR_STEP_WIN_DISPATCH(...)                                         \
@@ -634,6 +653,12 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
       LAUNCH_CHECK("k_win_final");
     }
     const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
+    if (c->step_events) {
+      HIP_TRY(hipEventCreate(&t_start));
+      c->step_events->push_back(t_start);
+      HIP_TRY(hipEventCreate(&t_stop));
+      c->step_events->push_back(t_stop);
+    }
     MDR_STEP_WIN_DISPATCH(kp, a, act_stride, tk + t0, K, la, rec(w), reward + (int64_t)t0 * rew_stride, rew_stride,
                           c->d_onb, c->d_wah, slot(w + 1));
     LAUNCH_CHECK("k_step_window");
@@ -644,6 +669,7 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
 #undef MDR_WIN_DISPATCH_H
 #undef MDR_WIN_DISPATCH_S
 #undef MDR_STEP_WIN_DISPATCH
+#undef MDR_STEP_LAUNCH
   return MDR_OK;
 }
 
@@ -670,9 +696,11 @@ static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t ac
                          (uint64_t)0, c->d_ticks + t, slab_at(c, c->ring));
       LAUNCH_CHECK("k_power_counts");
     }
+    if (int rc = step_mark(c, st)) return rc;
     int rc = launch_step(c, a, mode, TickArgs{}, c->d_ticks + t, r, la ? mode : 0, MDR_CTRL_NONE,
                          nullptr, t == n - 1 ? p_out : nullptr, st);
     if (rc) return rc;
+    if (int rc2 = step_mark(c, st)) return rc2;
   }
   return MDR_OK;
 }
@@ -722,6 +750,41 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
     fprintf(stderr, "mdr_rollout n=%d: stage %.1f us, graph lookup/capture %.1f us, hipGraphLaunch %.1f us\n", n,
             us(t0, t1), us(t1, t2), us(t2, t3));
   }
+  return MDR_OK;
+}
+
+// Measurement: one rollout as direct launches (no graph) with an event pair around every step-kernel
+// launch (k_step_window on the window path, k_step_* per tick otherwise); *ms = the summed kernel
+// time, *launches = the number of step launches.  Synchronises on the last event.
+int mdr_time_step_kernels(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action, int64_t act_stride,
+                          int mode, double* reward, int64_t rew_stride, void* stream, float* ms, int* launches) {
+  if (!c || !ticks || !reward || !ms || !launches || n < 1) return fail(MDR_EARG, "mdr_time_step_kernels: bad argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_time_step_kernels: context not bound");
+  if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action))
+    return fail(MDR_EARG, "mdr_time_step_kernels: bad action source");
+  if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
+    return fail(MDR_EARG, "mdr_time_step_kernels: common penalty modes need the per-step API");
+  hipStream_t st = S(stream);
+  int rc = refresh_if_dirty(c, st);
+  if (!rc) rc = stage_ticks(c, n, ticks, st);
+  if (!rc) rc = wslab_clean(c, st);
+  if (rc) return rc;
+  std::vector<hipEvent_t> evs;
+  c->step_events = &evs;
+  rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, nullptr, st);
+  c->step_events = nullptr;
+  c->counts_ready = false;
+  float total = 0.0f;
+  if (!rc && !evs.empty() && hipEventSynchronize(evs.back()) != hipSuccess) rc = fail(MDR_EHIP, "event sync");
+  for (size_t i = 0; !rc && i + 1 < evs.size(); i += 2) {
+    float e = 0.0f;
+    if (hipEventElapsedTime(&e, evs[i], evs[i + 1]) != hipSuccess) rc = fail(MDR_EHIP, "event elapsed");
+    total += e;
+  }
+  for (hipEvent_t e : evs) hipEventDestroy(e);
+  if (rc) return rc;
+  *ms = total;
+  *launches = (int)(evs.size() / 2);
   return MDR_OK;
 }
 

@@ -173,6 +173,14 @@ class HipShard:
                                      L.ptr(reward), rew_stride, L.ptr(self.p_dev), int(use_graph), self.stream()),
                 "mdr_rollout")
 
+    def time_step_kernels(self, ticks, action, act_stride, mode, reward, rew_stride):
+        """mdr_time_step_kernels: (summed step-kernel ms, step launches) of one directly launched rollout."""
+        ms, nl = C.c_float(), C.c_int()
+        L.check(self.lib.mdr_time_step_kernels(self.ctx, len(ticks), ticks.ptr(), L.ptr(action), act_stride, mode,
+                                               L.ptr(reward), rew_stride, self.stream(), C.byref(ms), C.byref(nl)),
+                "mdr_time_step_kernels")
+        return float(ms.value), int(nl.value)
+
     def launch_stream(self, use_graph=True):
         """The torch stream rollout kernels run on (the caller's current stream) — where timing
         events must be recorded."""

@@ -119,3 +119,24 @@ def test_random_rollout_vs_oracle_replayed_actions(torch_gpu):
     assert env.cluster.current_power_consumption == o["P"]
     # Bernoulli(0.5): 3.3M draws within 4 sigma
     assert abs(ones / (n * T) - 0.5) < 4 * 0.5 / np.sqrt(n * T)
+
+
+def test_time_step_kernels_advances_like_rollout(torch_gpu):
+    """mdr_time_step_kernels (the bench's per-launch kernel timing) issues the rollout's launch
+    sequence directly: one step launch per window, positive time, and the same state and rewards
+    as a graph-replayed rollout."""
+    torch = torch_gpu
+    from mdr_amd import _lib as L
+
+    n, T = 70001, 75
+    e1, e2 = _pair(n)
+    r1 = torch.empty((T, n), dtype=torch.float64, device="cuda")
+    r2 = torch.empty_like(r1)
+    ms, launches = e1.shard.time_step_kernels(e1.driver_window(T), None, 0, L.ACT_RANDOM, r1, n)
+    e2.rollout(T, action_mode="random", rewards=r2)
+    assert launches == -(-T // 32) and ms > 0.0
+    torch.cuda.synchronize()
+    s1, s2 = e1.shard.host_state(), e2.shard.host_state()
+    for k in s1:
+        np.testing.assert_array_equal(s1[k], s2[k], err_msg=k)
+    assert torch.equal(r1, r2)
