@@ -592,8 +592,8 @@ static int wslab_clean(mdr_ctx* c, hipStream_t st) {
 }
 
 // n ticks as ceil(n / win) windows of near-equal size: one k_count_window for the first window,
-// then per window k_win_reduce (shard sums -> counts + tick records; sharded: counts allreduced
-// first, records by k_win_final) and one k_step_window (counting the next window's ticks).
+// then per window k_win_reduce (shard sums -> counts + tick records; sharded: the shards are
+// allreduced first) and one k_step_window (counting the next window's ticks).
 static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t* action, int64_t act_stride,
                            int mode, double* reward, int64_t rew_stride, double* p_out, ncclComm_t comm,
                            hipStream_t st) {
@@ -605,8 +605,9 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
   const unsigned grid = blocks(blocks(c->kp.n, 64 * hpt), 4);  // one 64*hpt-house tile per wave, 4 waves per block
   KParams kp = c->kp;
   const int ncap = kp.n_cap;
-  auto red = [&](int w) { return slot(w) + (size_t)kWindowMax * kCountShards * ncap; };
-  auto rec = [&](int w) { return reinterpret_cast<const double*>(red(w) + (size_t)kWindowMax * ncap); };
+  auto rec = [&](int w) {  // the slot's tick records, after its shards and reduced counts
+    return reinterpret_cast<const double*>(slot(w) + (size_t)kWindowMax * kCountShards * ncap + (size_t)kWindowMax * ncap);
+  };
 #define MDR_WIN_DISPATCH_H(KERNEL, H, ...)                                                                     \
   do {                                                                                                         \
     if (mode == MDR_ACT_RANDOM) hipLaunchKernelGGL((KERNEL<MDR_ACT_RANDOM, H>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
@@ -645,13 +646,12 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
   for (int w = 0; w < nw; ++w) {
     const int K = wsz(w), la = w + 1 < nw ? wsz(w + 1) : 0;
     double* po = w == nw - 1 ? p_out : nullptr;
-    hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0, comm ? 0 : 1, po);
+    // sharded: every rank's sharded per-tick class counts are summed first (exact integers; the
+    // slot's shard part, K x 64 x n_cap values), so one reduce kernel yields the global counts
+    if (comm)
+      RCCL_TRY(ncclAllReduce(slot(w), slot(w), (size_t)K * kCountShards * ncap, ncclUint64, ncclSum, comm, st));
+    hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0, po);
     LAUNCH_CHECK("k_win_reduce");
-    if (comm) {  // sharded: every rank's per-tick class counts are summed (exact integers) first
-      RCCL_TRY(ncclAllReduce(red(w), red(w), (size_t)K * ncap, ncclUint64, ncclSum, comm, st));
-      hipLaunchKernelGGL(k_win_final, dim3(1), dim3(64), 0, st, kp, slot(w), K, tk + t0, po);
-      LAUNCH_CHECK("k_win_final");
-    }
     const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
     if (c->step_events) {
       HIP_TRY(hipEventCreate(&t_start));

@@ -91,9 +91,7 @@ template <int ACT, int HPT, bool SIMPLE>  // SIMPLE: deadband 0 and norm_temp 1 
 __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int K,
                               int la_K, const double* rec, double* reward, int64_t rew_stride, uint64_t* onb,
                               uint32_t* wah, unsigned long long* next_slot);
-__global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, int fin,
-                             double* p_out);
-__global__ void k_win_final(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
+__global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
 template <int ACT, int HPT>
 __global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int nt,
                                unsigned long long* slot, uint64_t* onb, uint32_t* wah);

@@ -612,10 +612,10 @@ __device__ __forceinline__ void win_tick_record(const KParams& p, const unsigned
   if (p_out) *p_out = P;
 }
 
-// one block per tick j, one wave per class: sum the 64 shards, zero them; fin: + the tick record
-// (sharded rollouts: fin = 0, the records follow the cross-rank allreduce in k_win_final)
+// one block per tick j, one wave per class: sum the 64 shards (sharded rollouts: already summed
+// over ranks by the allreduce), zero them, and write the tick record
 __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long long* __restrict__ slot, int nt,
-                                                    const TickArgs* __restrict__ tkp, int fin, double* p_out) {
+                                                    const TickArgs* __restrict__ tkp, double* p_out) {
   __shared__ unsigned long long s_red[kWinCap];
   const int j = blockIdx.x, c = threadIdx.x >> 6, q = threadIdx.x & 63, ncap = p.n_cap;
   unsigned long long v = 0;
@@ -630,20 +630,9 @@ __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long lon
     win_red(slot, ncap)[j * ncap + c] = v;
     s_red[c] = v;
   }
-  if (fin) {
-    __syncthreads();
-    if (threadIdx.x == 0)
-      win_tick_record(p, s_red, tkp[j], win_rec(slot, ncap) + j * kWinRec, j == nt - 1 ? p_out : nullptr);
-  }
-}
-
-// tick records from the (allreduced) counts of a sharded rollout window
-__global__ void __launch_bounds__(64) k_win_final(KParams p, unsigned long long* __restrict__ slot, int nt,
-                                                  const TickArgs* __restrict__ tkp, double* p_out) {
-  const int j = threadIdx.x;
-  if (j < nt)
-    win_tick_record(p, win_red(slot, p.n_cap) + j * p.n_cap, tkp[j], win_rec(slot, p.n_cap) + j * kWinRec,
-                    j == nt - 1 ? p_out : nullptr);
+  __syncthreads();
+  if (threadIdx.x == 0)
+    win_tick_record(p, s_red, tkp[j], win_rec(slot, ncap) + j * kWinRec, j == nt - 1 ? p_out : nullptr);
 }
 
 // the wave tile: 64 * HPT consecutive houses, house slot h of lane l = i0 + 64 h
