@@ -210,6 +210,14 @@ int mdr_rollout(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t*
  * mdr_rollout_sharded; drops cached rollout graphs. */
 int mdr_set_rollout_window(mdr_ctx* ctx, int ticks);
 
+/* Optional, before mdr_rollout (no reference counterpart): launch the first window's lockout-FSM
+ * count of an n_ticks rollout whose first tick id is tick0 — it needs the tick ids only, so it runs
+ * while the host computes the ticks' drivers.  The next mdr_rollout with the same n_ticks, action
+ * source, action buffer and first tick id uses it; any other entry point called in between
+ * discards it.  A no-op for rollouts that do not take the temporally blocked path. */
+int mdr_rollout_begin(mdr_ctx* ctx, int n_ticks, uint64_t tick0, const uint8_t* action, int64_t act_stride,
+                      int action_mode, void* stream);
+
 /* Measurement (no reference counterpart): mdr_rollout's launch sequence issued directly (no graph)
  * with an event pair around every step-kernel launch; *ms = the summed step-kernel time,
  * *launches = step launches (windows, or ticks on the one-tick path).  Advances the state like

@@ -121,6 +121,13 @@ struct mdr_ctx {
   hipEvent_t ev_k1[kSlabs] = {}, ev_ar[kSlabs] = {}, ev_pc = nullptr;
   hipEvent_t ev[16] = {};
   std::vector<hipEvent_t>* step_events = nullptr;  // mdr_time_step_kernels: events around each step launch
+  struct {                               // mdr_rollout_begin: the first window already counted
+    bool on = false;
+    int n = 0, mode = 0;
+    uint64_t tick0 = 0;
+    const uint8_t* action = nullptr;
+    int64_t act_stride = 0;
+  } begun;
   // MA-PPO actor (row P): packed weight image, per-tick obs scalars of actor rollouts
   unsigned char* d_actor = nullptr;
   size_t actor_cap = 0;
@@ -254,6 +261,15 @@ int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const 
 }  // namespace
 
 extern "C" {
+
+// an early first-window count (mdr_rollout_begin) is only valid for the mdr_rollout that follows
+// it directly: every other entry point that changes the state or uses the slots discards it
+static void drop_begun(mdr_ctx* c) {
+  if (c && c->begun.on) {
+    c->begun.on = false;
+    c->wslab_dirty = true;
+  }
+}
 
 int mdr_abi_version(void) { return MDR_ABI_VERSION; }
 
@@ -411,6 +427,7 @@ int mdr_destroy(mdr_ctx* c) {
 }
 
 int mdr_bind(mdr_ctx* c, const mdr_soa* s) {
+  drop_begun(c);
   if (!c || !s) return fail(MDR_EARG, "mdr_bind: null argument");
   if (!s->t_air || !s->t_mass || !s->hvac || !s->ua || !s->ca || !s->cm || !s->hm || !s->target ||
       !s->cap_idx)
@@ -434,6 +451,7 @@ int mdr_bind(mdr_ctx* c, const mdr_soa* s) {
 }
 
 int mdr_populate(mdr_ctx* c, const mdr_pop_spec* sp, void* stream) {
+  drop_begun(c);
   if (!c || !sp) return fail(MDR_EARG, "mdr_populate: null argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_populate: context not bound");
   if (sp->n_draw < 0 || sp->n_draw > MDR_MAX_CAP) return fail(MDR_EARG, "mdr_populate: n_draw out of range");
@@ -450,6 +468,7 @@ int mdr_populate(mdr_ctx* c, const mdr_pop_spec* sp, void* stream) {
 }
 
 int mdr_power_counts(mdr_ctx* c, const uint8_t* action, int mode, uint64_t tick, void* stream) {
+  drop_begun(c);
   if (!c) return fail(MDR_EARG, "mdr_power_counts: null ctx");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_power_counts: context not bound");
   if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action))
@@ -471,6 +490,7 @@ int mdr_counts_buffer(mdr_ctx* c, int64_t** ptr, int* len) {
 
 int mdr_step(mdr_ctx* c, const uint8_t* action, int mode, const mdr_tick* tick, double* reward,
              int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out, void* stream) {
+  drop_begun(c);
   if (!c || !tick || !reward) return fail(MDR_EARG, "mdr_step: null argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_step: context not bound");
   if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action))
@@ -596,7 +616,7 @@ static int wslab_clean(mdr_ctx* c, hipStream_t st) {
 // allreduced first) and one k_step_window (counting the next window's ticks).
 static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t* action, int64_t act_stride,
                            int mode, double* reward, int64_t rew_stride, double* p_out, ncclComm_t comm,
-                           hipStream_t st) {
+                           hipStream_t st, bool counted = false) {
   const int nw = (n + c->win - 1) / c->win;
   const int base = n / nw, rem = n % nw;
   auto wsz = [&](int w) { return base + (w < rem ? 1 : 0); };
@@ -640,8 +660,10 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     else { if (db0) MDR_WIN_DISPATCH_S(2, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(2, false, __VA_ARGS__); }        \
   } while (0)
   c->wslab_dirty = true;  // until the sequence is fully issued
-  MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, wsz(0), slot(0), c->d_onb, c->d_wah);
-  LAUNCH_CHECK("k_count_window");
+  if (!counted) {  // (counted: mdr_rollout_begin launched it already)
+    MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, (uint64_t)0, wsz(0), slot(0), c->d_onb, c->d_wah);
+    LAUNCH_CHECK("k_count_window");
+  }
   int t0 = 0;
   for (int w = 0; w < nw; ++w) {
     const int K = wsz(w), la = w + 1 < nw ? wsz(w + 1) : 0;
@@ -675,9 +697,9 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
 
 // The launch sequence of a rollout; tick args come from d_ticks so a captured graph is reusable.
 static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t act_stride, int mode,
-                            double* reward, int64_t rew_stride, double* p_out, hipStream_t st) {
+                            double* reward, int64_t rew_stride, double* p_out, hipStream_t st, bool counted = false) {
   if (window_ok(c, mode)) return window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride,
-                                                 p_out, nullptr, st);
+                                                 p_out, nullptr, st, counted);
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
   c->ring = 0;
   const bool la = lookahead_ok(mode);
@@ -715,6 +737,11 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   hipStream_t st = S(stream);
   static const bool trace = getenv("MDR_TRACE") != nullptr;  // host-side phase timing (diagnostics)
   const auto t0 = std::chrono::steady_clock::now();
+  // the first window counted ahead by mdr_rollout_begin for exactly this call?
+  const bool counted = c->begun.on && c->begun.n == n && c->begun.mode == mode && c->begun.tick0 == ticks[0].tick &&
+                       c->begun.action == action && c->begun.act_stride == act_stride && window_ok(c, mode);
+  if (c->begun.on && !counted) c->wslab_dirty = true;  // an unmatched early count: clear its shards
+  c->begun.on = false;
   int rc = refresh_if_dirty(c, st);
   if (rc) return rc;
   rc = stage_ticks(c, n, ticks, st);
@@ -723,16 +750,16 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   if (rc) return rc;
   const auto t1 = std::chrono::steady_clock::now();
   if (!use_graph) {
-    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st);
+    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st, counted);
     c->counts_ready = false;
     return rc;
   }
-  GraphKey key{n, mode, action, act_stride, reward, rew_stride, p_out, nullptr};
+  GraphKey key{n, mode + (counted ? 1000 : 0), action, act_stride, reward, rew_stride, p_out, nullptr};
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraphExec_t ex;
     rc = capture_graph(c, [&](hipStream_t cs) {
-      return rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, cs);
+      return rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, cs, counted);
     }, &ex);
     if (rc) return rc;
     it = c->graphs.emplace(key, std::make_pair(ex, c->ring)).first;
@@ -753,11 +780,53 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   return MDR_OK;
 }
 
+// The first window's FSM counts of an mdr_rollout of n ticks from tick id tick0, launched before the
+// host has the ticks' drivers (they only need the tick ids), so the count overlaps the host work.
+// The next mdr_rollout with the same (n, mode, action, tick0) skips its count; any other call
+// discards it.  A no-op (returns 0) when the rollout will not take the temporally blocked path.
+int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, int64_t act_stride, int mode,
+                      void* stream) {
+  if (!c || n < 1) return fail(MDR_EARG, "mdr_rollout_begin: bad argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout_begin: context not bound");
+  if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout_begin: bad action source");
+  if (c->begun.on) c->wslab_dirty = true;  // a previous early count that no rollout consumed
+  c->begun.on = false;
+  if (!window_ok(c, mode)) return MDR_OK;
+  hipStream_t st = S(stream);
+  int rc = refresh_if_dirty(c, st);
+  if (!rc) rc = wslab_clean(c, st);
+  if (rc) return rc;
+  const int nw = (n + c->win - 1) / c->win;
+  const int k0 = n / nw + (n % nw ? 1 : 0);  // window_launches' first window
+  const unsigned grid = blocks(blocks(c->kp.n, 64 * c->win_hpt), 4);
+  c->wslab_dirty = true;
+#define MDR_BEGIN_COUNT(A, H)                                                                                   \
+  hipLaunchKernelGGL((k_count_window<A, H>), dim3(grid), dim3(256), 0, st, c->kp, action, act_stride,          \
+                     (const TickArgs*)nullptr, tick0, k0, c->d_wslab, c->d_onb, c->d_wah)
+  if (c->win_hpt == 1) {
+    if (mode == MDR_ACT_RANDOM) MDR_BEGIN_COUNT(MDR_ACT_RANDOM, 1);
+    else if (mode == MDR_ACT_ALWAYS_ON) MDR_BEGIN_COUNT(MDR_ACT_ALWAYS_ON, 1);
+    else MDR_BEGIN_COUNT(MDR_ACT_BUFFER, 1);
+  } else {
+    if (mode == MDR_ACT_RANDOM) MDR_BEGIN_COUNT(MDR_ACT_RANDOM, 2);
+    else if (mode == MDR_ACT_ALWAYS_ON) MDR_BEGIN_COUNT(MDR_ACT_ALWAYS_ON, 2);
+    else MDR_BEGIN_COUNT(MDR_ACT_BUFFER, 2);
+  }
+#undef MDR_BEGIN_COUNT
+  LAUNCH_CHECK("k_count_window");
+  c->wslab_dirty = false;
+  c->begun.on = true;
+  c->begun.n = n; c->begun.mode = mode; c->begun.tick0 = tick0;
+  c->begun.action = action; c->begun.act_stride = act_stride;
+  return MDR_OK;
+}
+
 // Measurement: one rollout as direct launches (no graph) with an event pair around every step-kernel
 // launch (k_step_window on the window path, k_step_* per tick otherwise); *ms = the summed kernel
 // time, *launches = the number of step launches.  Synchronises on the last event.
 int mdr_time_step_kernels(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action, int64_t act_stride,
                           int mode, double* reward, int64_t rew_stride, void* stream, float* ms, int* launches) {
+  drop_begun(c);
   if (!c || !ticks || !reward || !ms || !launches || n < 1) return fail(MDR_EARG, "mdr_time_step_kernels: bad argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_time_step_kernels: context not bound");
   if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action))
@@ -1048,6 +1117,7 @@ extern "C" {
 int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
                         int64_t act_stride, int mode, double* reward, int64_t rew_stride, double* p_out,
                         void* stream) {
+  drop_begun(c);
   if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout_sharded: bad argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout_sharded: context not bound");
   if (!c->comm) return fail(MDR_ESTATE, "mdr_rollout_sharded: RCCL not initialised");
@@ -1085,6 +1155,7 @@ int mdr_rollout_sharded_mode(mdr_ctx* c, int* mode, double* us_serial, double* u
 }
 
 int mdr_set_rollout_window(mdr_ctx* c, int ticks) {
+  drop_begun(c);
   if (!c || ticks < 0 || ticks > kWindowMax) return fail(MDR_EARG, "mdr_set_rollout_window: ticks outside 0..32");
   if (ticks > 0 && !c->d_wslab) return fail(MDR_EARG, "mdr_set_rollout_window: more than 4 capacity classes");
   if (ticks != c->win) {
@@ -1109,6 +1180,7 @@ int mdr_cluster_stats(mdr_ctx* c, const double* reward, double* out, void* strea
 }
 
 int mdr_params_changed(mdr_ctx* c) {
+  drop_begun(c);
   if (!c) return fail(MDR_EARG, "mdr_params_changed: null ctx");
   c->coef_dirty = true;
   return MDR_OK;
@@ -1116,6 +1188,7 @@ int mdr_params_changed(mdr_ctx* c) {
 
 // ------------------------------------------------------------------------------------ diagnostics
 int mdr_probe_stream(mdr_ctx* c, double* reward, void* stream) {
+  drop_begun(c);
   if (!c || !reward) return fail(MDR_EARG, "mdr_probe_stream: null argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_probe_stream: context not bound");
   hipLaunchKernelGGL(k_probe_stream, dim3(blocks(c->kp.n, 512)), dim3(256), 0, S(stream), c->kp, reward);
@@ -1256,6 +1329,7 @@ int mdr_actor_load(mdr_ctx* c, const mdr_actor_spec* a, const float* w1, const f
 int mdr_actor_act(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc, const double* p_dev,
                   uint64_t tick, uint8_t* action, float* prob, float* probs, float* obs_out, int count_next,
                   void* stream) {
+  drop_begun(c);
   if (!c || !sp || !sc) return fail(MDR_EARG, "mdr_actor_act: null argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_act: context not bound");
   if (int rc = check_actor_obs(c, sp, "mdr_actor_act")) return rc;
@@ -1305,6 +1379,7 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
                       const mdr_obs_spec* sp, uint8_t* action, int64_t act_stride, float* prob,
                       int64_t prob_stride, double* reward, int64_t rew_stride, double* p_dev, int use_graph,
                       void* stream) {
+  drop_begun(c);
   if (!c || !ticks || !osc || !sp || !reward || !p_dev || n < 1) return fail(MDR_EARG, "mdr_actor_rollout: bad argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_rollout: context not bound");
   if (int rc = check_actor_obs(c, sp, "mdr_actor_rollout")) return rc;
@@ -1367,6 +1442,7 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
                               const mdr_obs_spec* sp, uint8_t* action, int64_t act_stride, float* prob,
                               int64_t prob_stride, double* reward, int64_t rew_stride, double* p_dev,
                               void* stream) {
+  drop_begun(c);
   if (!c || !ticks || !osc || !sp || !reward || !p_dev || n < 1)
     return fail(MDR_EARG, "mdr_actor_rollout_sharded: bad argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_rollout_sharded: context not bound");

@@ -93,8 +93,8 @@ __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stri
                               uint32_t* wah, unsigned long long* next_slot);
 __global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
 template <int ACT, int HPT>
-__global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int nt,
-                               unsigned long long* slot, uint64_t* onb, uint32_t* wah);
+__global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp,
+                               uint64_t tick0, int nt, unsigned long long* slot, uint64_t* onb, uint32_t* wah);
 __global__ void k_probe_stream(KParams p, double* reward);
 __global__ void k_refresh(KParams p, double* coef, int* params_bad);
 __global__ void k_div_check(const double* a, const double* b, int64_t n, unsigned long long* mismatches);

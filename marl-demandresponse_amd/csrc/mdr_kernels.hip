@@ -676,8 +676,9 @@ __device__ __forceinline__ uint64_t readlane_u64(uint32_t lo, uint32_t hi, int l
 // once at the end gives the per-tick-saturated value; the lock bit comes from the last tick.
 template <int ACT, int HPT>
 __device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uint64_t (*cm)[kWinCap],
-                                        const WinTile<HPT>& t, const TickArgs* tkp, int nt, const uint8_t* action,
-                                        int64_t act_stride, uint64_t* msk, unsigned* cnt, uint64_t* onb) {
+                                        const WinTile<HPT>& t, const TickArgs* tkp, uint64_t tick0, int nt,
+                                        const uint8_t* action, int64_t act_stride, uint64_t* msk, unsigned* cnt,
+                                        uint64_t* onb) {
   const int lane = threadIdx.x & 63;
   const uint32_t Lu = p.L < 0 ? 0u : (uint32_t)p.L, dt = (uint32_t)p.dt;
   uint64_t on_m[HPT], can_m[HPT], non_m[HPT];
@@ -695,8 +696,8 @@ __device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uin
   uint32_t wa_lo = 0, wa_hi = 0, wb_lo = 0, wb_hi = 0;
   const int G = HPT + (t.sh ? 1 : 0);
   if (ACT == MDR_ACT_RANDOM) {
-    const int jj = lane & 31;
-    const uint64_t tick = tkp[jj < nt ? jj : 0].tick;
+    const int jj = lane & 31;  // (tick ids: the staged drivers', or consecutive from tick0 before staging)
+    const uint64_t tick = tkp ? tkp[jj < nt ? jj : 0].tick : tick0 + (uint64_t)(jj < nt ? jj : 0);
     philox_words(p.seed, t.g0 + (uint64_t)(lane >> 5), tick, wa_lo, wa_hi);
     if (G > 2) philox_words(p.seed, t.g0 + 2u, tick, wb_lo, wb_hi);
   }
@@ -773,12 +774,13 @@ __device__ __forceinline__ void win_classes(const WinTile<HPT>& t, const int* cl
 }
 
 // First window of a rollout: ON counts, ON lane masks and end-of-window FSM words of ticks
-// 0 .. nt-1 from the current state (hvac itself is not changed).
+// 0 .. nt-1 from the current state (hvac itself is not changed).  Tick ids from the staged drivers,
+// or tick0 + t when tkp is null (mdr_rollout_begin: launched before the host computes the drivers).
 template <int ACT, int HPT>
 __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* __restrict__ action,
-                                                      int64_t act_stride, const TickArgs* __restrict__ tkp, int nt,
-                                                      unsigned long long* __restrict__ slot, uint64_t* __restrict__ onb,
-                                                      uint32_t* __restrict__ wah) {
+                                                      int64_t act_stride, const TickArgs* __restrict__ tkp,
+                                                      uint64_t tick0, int nt, unsigned long long* __restrict__ slot,
+                                                      uint64_t* __restrict__ onb, uint32_t* __restrict__ wah) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
   __shared__ uint64_t s_msk[4][kWinMax * HPT];
   const int wv = threadIdx.x >> 6;
@@ -792,7 +794,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
   }
   uint64_t cm[HPT][kWinCap];
   win_classes<HPT>(t, cls, cm);
-  win_run<ACT, HPT>(p, w, cm, t, tkp, nt, action, act_stride, s_msk[wv], s_cnt[wv],
+  win_run<ACT, HPT>(p, w, cm, t, tkp, tick0, nt, action, act_stride, s_msk[wv], s_cnt[wv],
                     onb + (size_t)t.tile * HPT * kWinMax);
 #pragma unroll
   for (int h = 0; h < HPT; ++h)
@@ -931,7 +933,7 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   if (la_K > 0) {
     uint64_t cm[HPT][kWinCap];
     win_classes<HPT>(t, cls, cm);
-    win_run<ACT, HPT>(p, w_end, cm, t, tkp + K, la_K,
+    win_run<ACT, HPT>(p, w_end, cm, t, tkp + K, 0, la_K,
                       ACT == MDR_ACT_BUFFER ? action + (int64_t)K * act_stride : nullptr, act_stride, s_msk[wv],
                       s_cnt[wv], onb_w);
 #pragma unroll
@@ -949,7 +951,7 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   template __global__ void k_step_window<A, H, false>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
                                                       const double*, double*, int64_t, uint64_t*, uint32_t*,      \
                                                       unsigned long long*);                                      \
-  template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, int,            \
+  template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, uint64_t, int,  \
                                                 unsigned long long*, uint64_t*, uint32_t*);
 MDR_INST_WIN(MDR_ACT_RANDOM, 1)
 MDR_INST_WIN(MDR_ACT_ALWAYS_ON, 1)

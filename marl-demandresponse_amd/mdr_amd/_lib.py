@@ -110,6 +110,7 @@ SIGNATURES = {
     "mdr_params_changed": (I, [VP]),
     "mdr_set_rollout_window": (I, [VP, I]),
     "mdr_time_step_kernels": (I, [VP, I, VP, VP, I64, I, VP, I64, VP, P(C.c_float), P(I)]),
+    "mdr_rollout_begin": (I, [VP, I, U64, VP, I64, I, VP]),
     "mdr_populate": (I, [VP, P(mdr_pop_spec), VP]),
     "mdr_power_counts": (I, [VP, VP, I, U64, VP]),
     "mdr_counts_buffer": (I, [VP, P(VP), P(I)]),

@@ -565,6 +565,10 @@ class Environment:
         if rewards is None:
             rewards = torch.empty((n_ticks, self._n_local), dtype=torch.float64, device=sh.device)
         rew_stride = 0 if rewards.dim() == 1 else self._n_local  # 1-D: every tick overwrites it
+        if self._comm is None and self.power_grid.interp is None and self._links is not None:
+            # the first window's FSM count needs only the tick ids: on the device while the host
+            # computes the drivers (mdr_rollout_begin; the rollout below consumes it)
+            sh.rollout_begin(n_ticks, self._tick, actions, self._n_local if actions is not None else 0, mode)
         done = 0
         while done < n_ticks:  # one window unless interpolation ends it early (driver_window)
             ticks = self.driver_window(n_ticks - done)

@@ -173,6 +173,11 @@ class HipShard:
                                      L.ptr(reward), rew_stride, L.ptr(self.p_dev), int(use_graph), self.stream()),
                 "mdr_rollout")
 
+    def rollout_begin(self, n, tick0, action, act_stride, mode):
+        """mdr_rollout_begin: the first window's count, launched before the host computes the drivers."""
+        L.check(self.lib.mdr_rollout_begin(self.ctx, n, tick0, L.ptr(action), act_stride, mode, self.stream()),
+                "mdr_rollout_begin")
+
     def time_step_kernels(self, ticks, action, act_stride, mode, reward, rew_stride):
         """mdr_time_step_kernels: (summed step-kernel ms, step launches) of one directly launched rollout."""
         ms, nl = C.c_float(), C.c_int()

@@ -140,3 +140,54 @@ def test_time_step_kernels_advances_like_rollout(torch_gpu):
     for k in s1:
         np.testing.assert_array_equal(s1[k], s2[k], err_msg=k)
     assert torch.equal(r1, r2)
+
+
+@pytest.mark.parametrize("mode", ["random", "buffer"])
+def test_rollout_begin_early_count(torch_gpu, mode):
+    """mdr_rollout_begin (the first window's count launched before the drivers): Environment.rollout
+    uses it, and an early count that the next call does not match (another length, a step in
+    between, another first tick) is discarded — every variant equals a twin run without it."""
+    torch = torch_gpu
+    from mdr_amd import _lib as L
+
+    n = 9001
+    e1, e2 = _pair(n)
+    m = L.ACT_RANDOM if mode == "random" else L.ACT_BUFFER
+    acts = (torch.rand((40, n), device="cuda") < 0.5).to(torch.uint8) if mode == "buffer" else None
+    r1 = torch.empty((40, n), dtype=torch.float64, device="cuda")
+    r2 = torch.empty_like(r1)
+
+    def roll(env, k, r, begin=True):
+        a = None if acts is None else acts[:k]
+        if not begin:  # the twin: the same C calls without the early count
+            ticks = env.driver_window(k)
+            env.shard.rollout(ticks, a, n if a is not None else 0, m, r[:k], n, True)
+            env._P_dev_valid = True
+        else:
+            env.rollout(k, actions=a, action_mode=mode, rewards=r[:k])
+
+    for k in (20, 40, 7):  # consumed early counts (Environment.rollout calls mdr_rollout_begin)
+        roll(e1, k, r1)
+        roll(e2, k, r2, begin=False)
+        _same_state(torch, e1, e2)
+        assert torch.equal(r1[:k], r2[:k])
+    # unmatched early counts: another length, an intervening step, a stale first tick
+    sa = None if acts is None else acts
+    e1.shard.rollout_begin(33, e1._tick, sa, n if sa is not None else 0, m)
+    roll(e1, 20, r1, begin=False)
+    roll(e2, 20, r2, begin=False)
+    _same_state(torch, e1, e2)
+    assert torch.equal(r1[:20], r2[:20])
+    e1.shard.rollout_begin(20, e1._tick, sa, n if sa is not None else 0, m)
+    step_a = (torch.rand(n, device="cuda") < 0.5).to(torch.uint8)
+    e1.step_tensor(step_a)
+    e2.step_tensor(step_a)
+    roll(e1, 20, r1, begin=False)
+    roll(e2, 20, r2, begin=False)
+    _same_state(torch, e1, e2)
+    assert torch.equal(r1[:20], r2[:20])
+    e1.shard.rollout_begin(20, e1._tick + 5, sa, n if sa is not None else 0, m)
+    roll(e1, 20, r1, begin=False)
+    roll(e2, 20, r2, begin=False)
+    _same_state(torch, e1, e2)
+    assert torch.equal(r1[:20], r2[:20])
