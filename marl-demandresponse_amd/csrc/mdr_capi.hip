@@ -653,7 +653,11 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     else if (mode == MDR_ACT_ALWAYS_ON) MDR_STEP_LAUNCH((k_step_window<MDR_ACT_ALWAYS_ON, H, DB>), __VA_ARGS__); \
     else MDR_STEP_LAUNCH((k_step_window<MDR_ACT_BUFFER, H, DB>), __VA_ARGS__);                              \
   } while (0)
-  const bool db0 = c->kp.deadband == 0.0 && c->kp.norm_temp == 1.0;
+  // SIMPLE = deadband 0, norm_temp 1, and reward weights whose signal / temperature penalties are
+  // >= +0 (k_step_window forms -(a + s) as (-a) + (-s), exact for such operands)
+  const bool db0 = c->kp.deadband == 0.0 && c->kp.norm_temp == 1.0 && c->kp.alpha_temp >= 0.0 &&
+                   !std::signbit(c->kp.alpha_temp) && c->kp.alpha_sig >= 0.0 && !std::signbit(c->kp.alpha_sig) &&
+                   c->kp.norm_sig > 0.0;
 #define MDR_STEP_WIN_DISPATCH(...)                                         \
   do {                                                                    \
     if (hpt == 1) { if (db0) MDR_WIN_DISPATCH_S(1, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(1, false, __VA_ARGS__); } \

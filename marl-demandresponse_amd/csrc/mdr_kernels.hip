@@ -599,15 +599,18 @@ __device__ __forceinline__ double* win_rec(unsigned long long* slot, int n_cap) 
 }
 
 // tick record j from the tick's global class counts (rewards_calculator.py:183-203 signal part;
-// the operations and order of the one-tick kernels)
+// the operations and order of the one-tick kernels); rec[2] is the NEGATED signal penalty (an exact
+// negation: the reward is then formed without a sign flip, k_step_window)
 __device__ __forceinline__ void win_tick_record(const KParams& p, const unsigned long long* cnt, const TickArgs& tk,
-                                                double* rec, double* p_out) {
+                                                const double* p_on, double* rec, double* p_out) {
   double P = 0.0;
-  for (int k = 0; k < p.n_cap; ++k) P += (double)cnt[k] * p.p_on[k];
+#pragma unroll
+  for (int k = 0; k < kWinCap; ++k)
+    if (k < p.n_cap) P += (double)cnt[k] * p_on[k];
   const double x = (P - tk.s_prev) / (double)p.n_global;
   rec[0] = tk.t_od_prev + 273.0;  // rc_apply's od_k
   rec[1] = tk.solar;
-  rec[2] = p.alpha_sig * (x * x) / p.norm_sig;
+  rec[2] = -(p.alpha_sig * (x * x) / p.norm_sig);
   rec[3] = fabs(tk.t_od_prev) < 1048576.0 && fabs(tk.solar) < 1099511627776.0 ? 1.0 : 0.0;  // fast-division ranges
   if (p_out) *p_out = P;
 }
@@ -618,6 +621,15 @@ __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long lon
                                                     const TickArgs* __restrict__ tkp, double* p_out) {
   __shared__ unsigned long long s_red[kWinCap];
   const int j = blockIdx.x, c = threadIdx.x >> 6, q = threadIdx.x & 63, ncap = p.n_cap;
+  // the record's other inputs are loaded by thread 0 while the shards are read (one memory
+  // round trip instead of three dependent ones)
+  TickArgs tk{};
+  double p_on[kWinCap];
+  if (threadIdx.x == 0) {
+    tk = tkp[j];
+#pragma unroll
+    for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < ncap ? k : 0];
+  }
   unsigned long long v = 0;
   if (c < ncap) {
     unsigned long long* e = &slot[((size_t)j * kCountShards + q) * ncap + c];
@@ -632,7 +644,7 @@ __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long lon
   }
   __syncthreads();
   if (threadIdx.x == 0)
-    win_tick_record(p, s_red, tkp[j], win_rec(slot, ncap) + j * kWinRec, j == nt - 1 ? p_out : nullptr);
+    win_tick_record(p, s_red, tk, p_on, win_rec(slot, ncap) + j * kWinRec, j == nt - 1 ? p_out : nullptr);
 }
 
 // the wave tile: 64 * HPT consecutive houses, house slot h of lane l = i0 + 64 h
@@ -665,83 +677,90 @@ __device__ __forceinline__ uint64_t readlane_u64(uint32_t lo, uint32_t hi, int l
          (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, l);
 }
 
+// lane `lane` of a VGPR set to the wave-uniform val (v_writelane_b32: val in an SGPR, the lane
+// select in M0, which does not count against the one-SGPR constant-bus limit of gfx950)
+__device__ __forceinline__ uint32_t writelane_u32(uint32_t old, uint32_t val, int lane) {
+  uint32_t r;
+  asm("v_writelane_b32 %0, %1, m0" : "=v"(r) : "s"(val), "{m0}"(lane), "0"(old));
+  return r;
+}
+
 // FSM-only run of nt <= kWinMax ticks (HVAC.step, hvac.py:43-64; the transitions of hvac_fsm) from
 // the words w[h]; tkp / action: the run's first tick.  The booleans (on, can, action) are wave lane
-// masks carried in scalar registers, so the per-house work of a tick is the seconds-since-off
-// arithmetic: one select, one add, one compare, one select.  Each tick's ON masks go to the wave's
-// LDS rows msk[t][HPT]; at the end lane t counts tick t's ON houses per capacity class into
-// cnt[t][kWinCap], stores the masks to onb[t][HPT] (this wave's rows, read by the next window's
-// thermal loop) and w[h] becomes the FSM word after the run.  Transitions use the unsaturated
-// seconds-since-off (window_ok guarantees L < 2^30 and sso + (kWinMax + 1) dt < 2^32), so saturating
-// once at the end gives the per-tick-saturated value; the lock bit comes from the last tick.
-template <int ACT, int HPT>
-__device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uint64_t (*cm)[kWinCap],
-                                        const WinTile<HPT>& t, const TickArgs* tkp, uint64_t tick0, int nt,
-                                        const uint8_t* action, int64_t act_stride, uint64_t* msk, unsigned* cnt,
-                                        uint64_t* onb) {
+// masks carried in scalar registers, and the loop carries s1 = the seconds-since-off after the
+// tick's "if not on: sso += dt" instead of sso itself: tick j+1's s1 is 0 for a house turned on at
+// tick j and s1 + dt otherwise, so the per-house work of a tick is one compare, one add and one
+// select.  Tick j's ON masks are written into lane j of per-wave VGPRs (v_writelane); at the end
+// lane t counts tick t's ON houses per capacity class into cnt[t][kWinCap], stores the masks to
+// onb[t][HPT] (this wave's rows, read by the next window's thermal loop) and w[h] becomes the FSM
+// word after the run.  Transitions use the unsaturated seconds-since-off (window_ok guarantees
+// L < 2^30 and sso + (kWinMax + 1) dt < 2^32), so saturating once at the end gives the
+// per-tick-saturated value; the lock bit comes from the last tick.  SH: the tile starts off a
+// 64-house group boundary (sharded runs), so a random action mask is spliced from two words.
+template <int ACT, int HPT, bool SH>
+__device__ __forceinline__ void win_run_t(const KParams& p, uint32_t* w, const uint64_t (*cm)[kWinCap],
+                                          const WinTile<HPT>& t, const TickArgs* tkp, uint64_t tick0, int nt,
+                                          const uint8_t* action, int64_t act_stride, unsigned* cnt, uint64_t* onb) {
   const int lane = threadIdx.x & 63;
   const uint32_t Lu = p.L < 0 ? 0u : (uint32_t)p.L, dt = (uint32_t)p.dt;
-  uint64_t on_m[HPT], can_m[HPT], non_m[HPT];
-  uint32_t sso[HPT], s1[HPT];
+  uint64_t on_m[HPT], can_m[HPT];
+  uint32_t s1[HPT], mlo[HPT], mhi[HPT];
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
     on_m[h] = __ballot((w[h] & kOnBit) != 0);
-    sso[h] = w[h] & kSsoMask;
-    s1[h] = sso[h];
-    can_m[h] = non_m[h] = 0ull;
+    const uint32_t sso = w[h] & kSsoMask;
+    s1[h] = __builtin_amdgcn_inverse_ballot_w64(on_m[h]) ? sso : sso + dt;  // if not on: sso += dt
+    can_m[h] = 0ull;
+    mlo[h] = mhi[h] = 0u;
   }
   // Philox words of the run's ticks (random controller, mdr_device.h philox_words): lane l holds
   // tick (l & 31) of group g0 + (l >> 5); lanes 0..31 of the second pair: group g0 + 2 (a tile of
   // 128 houses off a 64-house boundary spans three groups)
   uint32_t wa_lo = 0, wa_hi = 0, wb_lo = 0, wb_hi = 0;
-  const int G = HPT + (t.sh ? 1 : 0);
+  constexpr int G = HPT + (SH ? 1 : 0);
   if (ACT == MDR_ACT_RANDOM) {
     const int jj = lane & 31;  // (tick ids: the staged drivers', or consecutive from tick0 before staging)
     const uint64_t tick = tkp ? tkp[jj < nt ? jj : 0].tick : tick0 + (uint64_t)(jj < nt ? jj : 0);
     philox_words(p.seed, t.g0 + (uint64_t)(lane >> 5), tick, wa_lo, wa_hi);
-    if (G > 2) philox_words(p.seed, t.g0 + 2u, tick, wb_lo, wb_hi);
+    if constexpr (G > 2) philox_words(p.seed, t.g0 + 2u, tick, wb_lo, wb_hi);
   }
   for (int j = 0; j < nt; ++j) {
-    uint64_t W[HPT + 1];
+    uint64_t W[G];
     if (ACT == MDR_ACT_RANDOM) {
       W[0] = readlane_u64(wa_lo, wa_hi, j);
-      if (HPT + 1 > 1) W[1] = G > 1 ? readlane_u64(wa_lo, wa_hi, j + 32) : 0ull;
-      if (HPT + 1 > 2) W[HPT] = G > 2 ? readlane_u64(wb_lo, wb_hi, j) : 0ull;
+      if constexpr (G > 1) W[1] = readlane_u64(wa_lo, wa_hi, j + 32);
+      if constexpr (G > 2) W[2] = readlane_u64(wb_lo, wb_hi, j);
     }
     const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)j * act_stride : nullptr;
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
       uint64_t a;  // the actions as a lane mask
-      if (ACT == MDR_ACT_RANDOM) a = t.sh ? (W[h] >> t.sh) | (W[h + 1] << (64 - t.sh)) : W[h];
+      if (ACT == MDR_ACT_RANDOM) a = SH ? (W[h] >> t.sh) | (W[h + 1] << (64 - t.sh)) : W[h];
       else if (ACT == MDR_ACT_ALWAYS_ON) a = ~0ull;
       else a = __ballot(arow[t.idx[h]] != 0);
-      s1[h] = __builtin_amdgcn_inverse_ballot_w64(on_m[h]) ? sso[h] : sso[h] + dt;  // if not on: sso += dt
-      can_m[h] = on_m[h] | __ballot(s1[h] >= Lu);                                  // not locked
-      non_m[h] = can_m[h] & a;
-      sso[h] = __builtin_amdgcn_inverse_ballot_w64(non_m[h]) ? 0u : s1[h];
-      on_m[h] = non_m[h];
-    }
-    if (lane == 0) {
-#pragma unroll
-      for (int h = 0; h < HPT; ++h) msk[j * HPT + h] = on_m[h];
+      can_m[h] = on_m[h] | __ballot(s1[h] >= Lu);  // not locked
+      on_m[h] = can_m[h] & a;
+      s1[h] = __builtin_amdgcn_inverse_ballot_w64(on_m[h]) ? 0u : s1[h] + dt;  // the next tick's s1
+      mlo[h] = writelane_u32(mlo[h], (uint32_t)on_m[h], j);
+      mhi[h] = writelane_u32(mhi[h], (uint32_t)(on_m[h] >> 32), j);
     }
   }
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
-    // the last tick's lockout (hvac.py:58-63): locked before the decision, or turned off with
-    // too little time to finish the lockout
-    const uint64_t lock_m = nt > 0 ? ~can_m[h] | (~non_m[h] & __ballot(s1[h] + dt < Lu)) : 0ull;
-    const uint32_t s = sso[h] < kSsoMask ? sso[h] : kSsoMask;
-    w[h] = s | (__builtin_amdgcn_inverse_ballot_w64(lock_m) ? kLockBit : 0u) |
-           (__builtin_amdgcn_inverse_ballot_w64(on_m[h]) ? kOnBit : 0u);
+    // the last tick's lockout (hvac.py:58-63): locked before the decision, or turned off with too
+    // little time to finish the lockout (for a house left off, s1 now holds that tick's s1 + dt);
+    // its seconds-since-off: 0 if turned on, else the last tick's s1 (= s1 - dt)
+    const bool on = __builtin_amdgcn_inverse_ballot_w64(on_m[h]);
+    const uint64_t lock_m = nt > 0 ? ~can_m[h] | (~on_m[h] & __ballot(s1[h] < Lu)) : 0ull;
+    const uint32_t sso = nt > 0 ? (on ? 0u : s1[h] - dt) : w[h] & kSsoMask;
+    const uint32_t s = sso < kSsoMask ? sso : kSsoMask;
+    w[h] = s | (__builtin_amdgcn_inverse_ballot_w64(lock_m) ? kLockBit : 0u) | (on ? kOnBit : 0u);
   }
-  __builtin_amdgcn_wave_barrier();  // lane 0's LDS rows before the lanes read them (one wave)
-  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
   if (lane < nt) {
     unsigned k[kWinCap] = {};
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
-      const uint64_t m = msk[lane * HPT + h];
+      const uint64_t m = ((uint64_t)mhi[h] << 32) | mlo[h];
       onb[lane * HPT + h] = m;
 #pragma unroll
       for (int c = 0; c < kWinCap; ++c) k[c] += (unsigned)__popcll(m & cm[h][c]);
@@ -749,6 +768,16 @@ __device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uin
 #pragma unroll
     for (int c = 0; c < kWinCap; ++c) cnt[lane * kWinCap + c] = k[c];
   }
+}
+
+template <int ACT, int HPT>
+__device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uint64_t (*cm)[kWinCap],
+                                        const WinTile<HPT>& t, const TickArgs* tkp, uint64_t tick0, int nt,
+                                        const uint8_t* action, int64_t act_stride, unsigned* cnt, uint64_t* onb) {
+  if (ACT == MDR_ACT_RANDOM && t.sh != 0)
+    win_run_t<ACT, HPT, true>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb);
+  else
+    win_run_t<ACT, HPT, false>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb);
 }
 
 // sum the block's per-wave rows cnt[4][kWinMax][kWinCap] and add them to this block's slab shard
@@ -782,7 +811,6 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
                                                       uint64_t tick0, int nt, unsigned long long* __restrict__ slot,
                                                       uint64_t* __restrict__ onb, uint32_t* __restrict__ wah) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
-  __shared__ uint64_t s_msk[4][kWinMax * HPT];
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
   uint32_t w[HPT];
@@ -794,8 +822,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
   }
   uint64_t cm[HPT][kWinCap];
   win_classes<HPT>(t, cls, cm);
-  win_run<ACT, HPT>(p, w, cm, t, tkp, tick0, nt, action, act_stride, s_msk[wv], s_cnt[wv],
-                    onb + (size_t)t.tile * HPT * kWinMax);
+  win_run<ACT, HPT>(p, w, cm, t, tkp, tick0, nt, action, act_stride, s_cnt[wv], onb + (size_t)t.tile * HPT * kWinMax);
 #pragma unroll
   for (int h = 0; h < HPT; ++h)
     if (t.v[h]) wah[t.i0 + 64u * h] = w[h];
@@ -822,7 +849,6 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
                                                      uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
                                                      unsigned long long* __restrict__ next_slot) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
-  __shared__ uint64_t s_msk[4][kWinMax * HPT];
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
   uint64_t* onb_w = onb + (size_t)t.tile * HPT * kWinMax;  // this wave's rows [kWinMax][HPT]
@@ -871,8 +897,9 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
 #pragma unroll
   for (int h = 0; h < HPT; ++h) r_on[h] = onb_w[h];
   const uint32_t rb = t.i0 * 8u;  // byte offset of the lane's house in a reward row (n < 2^29)
+  const double nalpha = -p.alpha_temp;
   for (int j = 0; j < K; ++j) {
-    const double od_k = r_od, solar = r_sol, sig = r_sig;
+    const double od_k = r_od, solar = r_sol, nsig = r_sig;
     const bool tick_ok = r_ok != 0;
     uint64_t on_m[HPT];
 #pragma unroll
@@ -903,16 +930,19 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
         double r;
         if (SIMPLE) {  // deadband 0, norm_temp 1 (the defaults): no branches, no division
           // on the fast path Tn is finite (the operand ranges checked above), so the reference's
-          // two comparisons reduce to x * x (x = 0 gives +0 either way); off it a NaN gives 0
+          // two comparisons reduce to x * x (x = 0 gives +0 either way); off it a NaN gives 0.
+          // -(a * pen + s) == (-a) * pen + (-s) bit for bit: negation is exact and rounding is
+          // symmetric, and with a, s >= +0 (mdr_capi checks the signs for SIMPLE) the only zero
+          // sum is +0 + +0, whose negation is -0 either way
           const double x = Tn - hi_tg[h];
           const double pen = F ? x * x : deadband_l2_0(hi_tg[h], Tn);
-          r = -(p.alpha_temp * pen + sig);
+          r = nalpha * pen + nsig;
         } else {
           double pen = 0.0;
           if (hi_tg[h] < Tn) { const double x = Tn - hi_tg[h]; pen = x * x; }
           else if (lo_tg[h] > Tn) { const double x = lo_tg[h] - Tn; pen = x * x; }
           const double tpen = p.alpha_temp * pen;
-          r = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + sig);
+          r = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + -nsig);
         }
         if (t.v[h]) *reinterpret_cast<double*>(rrow + (rb + 512u * h)) = r;
       }
@@ -934,8 +964,8 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
     uint64_t cm[HPT][kWinCap];
     win_classes<HPT>(t, cls, cm);
     win_run<ACT, HPT>(p, w_end, cm, t, tkp + K, 0, la_K,
-                      ACT == MDR_ACT_BUFFER ? action + (int64_t)K * act_stride : nullptr, act_stride, s_msk[wv],
-                      s_cnt[wv], onb_w);
+                      ACT == MDR_ACT_BUFFER ? action + (int64_t)K * act_stride : nullptr, act_stride, s_cnt[wv],
+                      onb_w);
 #pragma unroll
     for (int h = 0; h < HPT; ++h)
       if (t.v[h]) wah[t.i0 + 64u * h] = w_end[h];
