@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MDR_ABI_VERSION 2
+#define MDR_ABI_VERSION 3
 #define MDR_MAX_CAP 64
 
 enum {
@@ -217,6 +217,27 @@ int mdr_set_rollout_window(mdr_ctx* ctx, int ticks);
  * discards it.  A no-op for rollouts that do not take the temporally blocked path. */
 int mdr_rollout_begin(mdr_ctx* ctx, int n_ticks, uint64_t tick0, const uint8_t* action, int64_t act_stride,
                       int action_mode, void* stream);
+
+/* Optional, before mdr_rollout (no reference counterpart; replaces the host-side ordering of
+ * environment.py:72-108 — drivers first, then the cluster step — by launch first): launch the
+ * whole rollout graph NOW, before the host computes the ticks' drivers.  It counts the first
+ * window's FSM and then waits on the device until the matching mdr_rollout (same n_ticks, tick0 =
+ * ticks[0].tick, action source and buffers, reward, rew_stride, p_out) posts the drivers through
+ * pinned host memory; the graph launch and the count overlap the host work.  Any other entry point
+ * called in between cancels it (every kernel of the graph then returns at once, the state is
+ * unchanged); a graph left without drivers for 10 s cancels itself and the next rollout call
+ * reports it.  The host must not synchronise the device between the two calls.  Falls back to
+ * mdr_rollout_begin when it does not apply (no pinned memory, > 1024 ticks, not the temporally
+ * blocked path, or a random source whose tick0 is not where the previous rollout ended). */
+int mdr_rollout_launch(mdr_ctx* ctx, int n_ticks, uint64_t tick0, const uint8_t* action, int64_t act_stride,
+                       int action_mode, double* reward, int64_t rew_stride, double* p_out, void* stream);
+
+/* Cancel a pending mdr_rollout_launch whose drivers will not be posted (e.g. the host failed to
+ * compute them).  A no-op when none is pending. */
+int mdr_rollout_cancel(mdr_ctx* ctx);
+
+/* Diagnostics: *count = launch-first graphs launched so far on this context. */
+int mdr_rollout_launched(mdr_ctx* ctx, uint64_t* count);
 
 /* Measurement (no reference counterpart): mdr_rollout's launch sequence issued directly (no graph)
  * with an event pair around every step-kernel launch; *ms = the summed step-kernel time,

@@ -7,6 +7,7 @@
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -128,6 +129,24 @@ struct mdr_ctx {
     const uint8_t* action = nullptr;
     int64_t act_stride = 0;
   } begun;
+  // launch-first rollouts (mdr_rollout_launch): the graph runs ahead of the host's tick drivers
+  uint64_t* d_lf = nullptr;              // device: [0] seq of the last k_lf_wait, [1] next rollout's tick id, [2] abort (int)
+  TickArgs* h_lf_ring = nullptr;         // pinned: 2 slots x kLfCap tick records
+  uint64_t* h_lf_ctl = nullptr;          // pinned: [0] posted seq, [1] acked seq | abort << 62, [2] cancelled seq
+  uint64_t lf_seq = 0;                   // launch-first graphs launched (= the device's [0] once they ran)
+  uint64_t lf_timeout = 0;               // k_lf_wait's bound, wall-clock ticks
+  uint64_t lf_timeouts_seen = 0;
+  bool next_tick_known = false;          // d_lf[1] as written by the last rollout graph
+  uint64_t next_tick = 0;
+  struct {
+    bool on = false;
+    uint64_t seq = 0, tick0 = 0;
+    int n = 0, mode = 0, ring_end = 0;
+    const uint8_t* action = nullptr;
+    int64_t act_stride = 0, rew_stride = 0;
+    double* reward = nullptr;
+    double* p_out = nullptr;
+  } lf;
   // MA-PPO actor (row P): packed weight image, per-tick obs scalars of actor rollouts
   unsigned char* d_actor = nullptr;
   size_t actor_cap = 0;
@@ -264,11 +283,19 @@ extern "C" {
 
 // an early first-window count (mdr_rollout_begin) is only valid for the mdr_rollout that follows
 // it directly: every other entry point that changes the state or uses the slots discards it
+static void lf_cancel(mdr_ctx* c) {
+  if (!c || !c->lf.on) return;
+  __atomic_store_n(&c->h_lf_ctl[2], c->lf.seq, __ATOMIC_RELEASE);  // k_lf_wait aborts the graph
+  c->lf.on = false;
+  c->wslab_dirty = true;  // its count wrote the first slot's shards; no reduce cleared them
+}
+
 static void drop_begun(mdr_ctx* c) {
   if (c && c->begun.on) {
     c->begun.on = false;
     c->wslab_dirty = true;
   }
+  lf_cancel(c);
 }
 
 int mdr_abi_version(void) { return MDR_ABI_VERSION; }
@@ -330,6 +357,25 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   k.q_on = c->d_tables;
   k.p_on = c->d_tables + MDR_MAX_CAP;
   if (hipMalloc(&c->d_flags, 16) != hipSuccess) return cleanup(fail(MDR_ENOMEM, "flags"));
+  if (hipMalloc(&c->d_lf, 64) != hipSuccess || hipMemset(c->d_lf, 0, 64) != hipSuccess)
+    return cleanup(fail(MDR_ENOMEM, "launch-first words"));
+  {
+    // launch-first ring + control words in fine-grained (coherent) pinned memory; optional: without
+    // it mdr_rollout_launch falls back to mdr_rollout_begin
+    if (hipHostMalloc(&c->h_lf_ring, 2 * sizeof(TickArgs) * kLfCap, hipHostMallocCoherent) != hipSuccess ||
+        hipHostMalloc(&c->h_lf_ctl, 64, hipHostMallocCoherent) != hipSuccess) {
+      (void)hipGetLastError();
+      if (c->h_lf_ring) hipHostFree(c->h_lf_ring);
+      c->h_lf_ring = nullptr;
+      c->h_lf_ctl = nullptr;
+    } else {
+      memset(c->h_lf_ctl, 0, 64);
+    }
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg->device) != hipSuccess || khz <= 0)
+      khz = 100000;  // gfx9: 100 MHz
+    c->lf_timeout = (uint64_t)khz * 1000ull * 10ull;  // 10 s
+  }
   k.params_bad = c->d_flags;
   {
     // the fast division is provably exact for dt < 2^20 s and |q_on| < 2^40 W (mdr_device.h)
@@ -390,7 +436,11 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
 int mdr_destroy(mdr_ctx* c) {
   if (!c) return MDR_OK;
   hipSetDevice(c->cfg.device);
+  lf_cancel(c);  // a launched graph still waiting for its drivers must not hold the synchronize
   hipDeviceSynchronize();
+  hipFree(c->d_lf);
+  if (c->h_lf_ring) hipHostFree(c->h_lf_ring);
+  if (c->h_lf_ctl) hipHostFree(c->h_lf_ctl);
   for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
   for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
   hipFree(c->d_actor);
@@ -542,7 +592,7 @@ static int stage_recs(const void* src, int n, void* dst, hipStream_t st) {
   return MDR_OK;
 }
 
-static int stage_ticks(mdr_ctx* c, int n, const mdr_tick* ticks, hipStream_t st) {
+static int ensure_ticks(mdr_ctx* c, int n) {
   if (n > c->ticks_cap) {
     HIP_TRY(hipDeviceSynchronize());  // queued graphs may still read the old buffers
     hipFree(c->d_ticks);
@@ -558,6 +608,11 @@ static int stage_ticks(mdr_ctx* c, int n, const mdr_tick* ticks, hipStream_t st)
     for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
     c->actor_graphs.clear();
   }
+  return MDR_OK;
+}
+
+static int stage_ticks(mdr_ctx* c, int n, const mdr_tick* ticks, hipStream_t st) {
+  if (int rc = ensure_ticks(c, n)) return rc;
   // stream order: every earlier launch reading d_ticks (a replayed graph) precedes this write
   return stage_recs(ticks, n, c->d_ticks, st);
 }
@@ -614,9 +669,13 @@ static int wslab_clean(mdr_ctx* c, hipStream_t st) {
 // n ticks as ceil(n / win) windows of near-equal size: one k_count_window for the first window,
 // then per window k_win_reduce (shard sums -> counts + tick records; sharded: the shards are
 // allreduced first) and one k_step_window (counting the next window's ticks).
+// lf (launch-first, mdr_rollout_launch): the count reads the first tick id from d_lf[1] (written by
+// the previous rollout's last reduce), then k_lf_wait stages the drivers once the host posts them;
+// every later kernel returns at once if it was cancelled.  Every sequence's last reduce writes the
+// tick id the next rollout starts at into d_lf[1].
 static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t* action, int64_t act_stride,
                            int mode, double* reward, int64_t rew_stride, double* p_out, ncclComm_t comm,
-                           hipStream_t st, bool counted = false) {
+                           hipStream_t st, bool counted = false, bool lf = false) {
   const int nw = (n + c->win - 1) / c->win;
   const int base = n / nw, rem = n % nw;
   auto wsz = [&](int w) { return base + (w < rem ? 1 : 0); };
@@ -664,8 +723,17 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     else { if (db0) MDR_WIN_DISPATCH_S(2, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(2, false, __VA_ARGS__); }        \
   } while (0)
   c->wslab_dirty = true;  // until the sequence is fully issued
-  if (!counted) {  // (counted: mdr_rollout_begin launched it already)
-    MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, (uint64_t)0, wsz(0), slot(0), c->d_onb, c->d_wah);
+  const int* abort = lf ? reinterpret_cast<const int*>(c->d_lf + 2) : nullptr;
+  if (lf) {
+    MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, (const TickArgs*)nullptr, (uint64_t)0,
+                     (const uint64_t*)(c->d_lf + 1), wsz(0), slot(0), c->d_onb, c->d_wah);
+    LAUNCH_CHECK("k_count_window");
+    hipLaunchKernelGGL(k_lf_wait, dim3(1), dim3(256), 0, st, c->h_lf_ring, kLfCap, c->h_lf_ctl, c->d_lf,
+                       reinterpret_cast<int*>(c->d_lf + 2), n, const_cast<TickArgs*>(tk), c->lf_timeout);
+    LAUNCH_CHECK("k_lf_wait");
+  } else if (!counted) {  // (counted: mdr_rollout_begin launched it already)
+    MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, (uint64_t)0, (const uint64_t*)nullptr, wsz(0),
+                     slot(0), c->d_onb, c->d_wah);
     LAUNCH_CHECK("k_count_window");
   }
   int t0 = 0;
@@ -676,7 +744,8 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     // slot's shard part, K x 64 x n_cap values), so one reduce kernel yields the global counts
     if (comm)
       RCCL_TRY(ncclAllReduce(slot(w), slot(w), (size_t)K * kCountShards * ncap, ncclUint64, ncclSum, comm, st));
-    hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0, po);
+    hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0, po, abort,
+                       w == nw - 1 ? c->d_lf + 1 : nullptr);
     LAUNCH_CHECK("k_win_reduce");
     const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
     if (c->step_events) {
@@ -686,7 +755,7 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
       c->step_events->push_back(t_stop);
     }
     MDR_STEP_WIN_DISPATCH(kp, a, act_stride, tk + t0, K, la, rec(w), reward + (int64_t)t0 * rew_stride, rew_stride,
-                          c->d_onb, c->d_wah, slot(w + 1));
+                          c->d_onb, c->d_wah, slot(w + 1), abort);
     LAUNCH_CHECK("k_step_window");
     t0 += K;
   }
@@ -701,9 +770,10 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
 
 // The launch sequence of a rollout; tick args come from d_ticks so a captured graph is reusable.
 static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t act_stride, int mode,
-                            double* reward, int64_t rew_stride, double* p_out, hipStream_t st, bool counted = false) {
+                            double* reward, int64_t rew_stride, double* p_out, hipStream_t st, bool counted = false,
+                            bool lf = false) {
   if (window_ok(c, mode)) return window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride,
-                                                 p_out, nullptr, st, counted);
+                                                 p_out, nullptr, st, counted, lf);
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
   c->ring = 0;
   const bool la = lookahead_ok(mode);
@@ -731,6 +801,45 @@ static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t ac
   return MDR_OK;
 }
 
+// a launch-first graph that timed out waiting for its drivers (k_lf_wait abort code 2) did not
+// advance the state although its mdr_rollout returned: report it once, at the next rollout call
+static int lf_check(mdr_ctx* c) {
+  if (!c->h_lf_ctl) return MDR_OK;
+  const uint64_t a = __atomic_load_n(&c->h_lf_ctl[1], __ATOMIC_ACQUIRE);
+  const uint64_t seq = a & ((1ull << 62) - 1);
+  if ((a >> 62) == 2 && seq > c->lf_timeouts_seen) {
+    c->lf_timeouts_seen = seq;
+    c->wslab_dirty = true;
+    c->next_tick_known = false;
+    return fail(MDR_ESTATE, "a launch-first rollout timed out waiting for its tick drivers (10 s): its ticks were "
+                            "not applied to the device state");
+  }
+  return MDR_OK;
+}
+
+// post the drivers of the launched graph: ring slot seq & 1 (free once graph seq - 2 acknowledged
+// it; graphs run in order and every earlier one was posted or cancelled, so this wait always ends)
+static int lf_post(mdr_ctx* c, const mdr_tick* ticks, int n) {
+  const uint64_t seq = c->lf.seq, need = seq >= 2 ? seq - 2 : 0;
+  const auto t0 = std::chrono::steady_clock::now();
+  while ((__atomic_load_n(&c->h_lf_ctl[1], __ATOMIC_ACQUIRE) & ((1ull << 62) - 1)) < need) {
+    __builtin_ia32_pause();
+    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
+      lf_cancel(c);
+      return fail(MDR_EHIP, "mdr_rollout: the device did not consume a launch-first ring slot within 30 s");
+    }
+  }
+  static_assert(sizeof(mdr_tick) == sizeof(TickArgs), "mdr_tick is a 32-byte record");
+  memcpy(c->h_lf_ring + (size_t)(seq & 1u) * kLfCap, ticks, (size_t)n * sizeof(TickArgs));
+  __atomic_store_n(&c->h_lf_ctl[0], seq, __ATOMIC_RELEASE);  // (x86: the records are visible first)
+  c->lf.on = false;
+  c->ring = c->lf.ring_end;
+  c->counts_ready = false;
+  c->next_tick_known = true;
+  c->next_tick = ticks[n - 1].tick + 1;
+  return MDR_OK;
+}
+
 int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action, int64_t act_stride,
                 int mode, double* reward, int64_t rew_stride, double* p_out, int use_graph, void* stream) {
   if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout: bad argument");
@@ -741,6 +850,14 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   hipStream_t st = S(stream);
   static const bool trace = getenv("MDR_TRACE") != nullptr;  // host-side phase timing (diagnostics)
   const auto t0 = std::chrono::steady_clock::now();
+  if (int rc = lf_check(c)) return rc;
+  if (c->lf.on) {  // launched by mdr_rollout_launch for exactly this call: post the drivers
+    if (use_graph && c->lf.n == n && c->lf.mode == mode && c->lf.tick0 == ticks[0].tick && c->lf.action == action &&
+        c->lf.act_stride == act_stride && c->lf.reward == reward && c->lf.rew_stride == rew_stride &&
+        c->lf.p_out == p_out)
+      return lf_post(c, ticks, n);
+    lf_cancel(c);
+  }
   // the first window counted ahead by mdr_rollout_begin for exactly this call?
   const bool counted = c->begun.on && c->begun.n == n && c->begun.mode == mode && c->begun.tick0 == ticks[0].tick &&
                        c->begun.action == action && c->begun.act_stride == act_stride && window_ok(c, mode);
@@ -756,6 +873,8 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   if (!use_graph) {
     rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st, counted);
     c->counts_ready = false;
+    c->next_tick_known = !rc && window_ok(c, mode);
+    c->next_tick = ticks[n - 1].tick + 1;
     return rc;
   }
   GraphKey key{n, mode + (counted ? 1000 : 0), action, act_stride, reward, rew_stride, p_out, nullptr};
@@ -775,6 +894,8 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   }
   c->ring = it->second.second;
   c->counts_ready = false;
+  c->next_tick_known = window_ok(c, mode);  // (the window sequence's last reduce wrote it)
+  c->next_tick = ticks[n - 1].tick + 1;
   if (trace) {
     const auto t3 = std::chrono::steady_clock::now();
     auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
@@ -806,7 +927,7 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   c->wslab_dirty = true;
 #define MDR_BEGIN_COUNT(A, H)                                                                                   \
   hipLaunchKernelGGL((k_count_window<A, H>), dim3(grid), dim3(256), 0, st, c->kp, action, act_stride,          \
-                     (const TickArgs*)nullptr, tick0, k0, c->d_wslab, c->d_onb, c->d_wah)
+                     (const TickArgs*)nullptr, tick0, (const uint64_t*)nullptr, k0, c->d_wslab, c->d_onb, c->d_wah)
   if (c->win_hpt == 1) {
     if (mode == MDR_ACT_RANDOM) MDR_BEGIN_COUNT(MDR_ACT_RANDOM, 1);
     else if (mode == MDR_ACT_ALWAYS_ON) MDR_BEGIN_COUNT(MDR_ACT_ALWAYS_ON, 1);
@@ -822,6 +943,73 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   c->begun.on = true;
   c->begun.n = n; c->begun.mode = mode; c->begun.tick0 = tick0;
   c->begun.action = action; c->begun.act_stride = act_stride;
+  return MDR_OK;
+}
+
+// Launch-first rollout: the graph of an mdr_rollout of n ticks from tick id tick0 is launched NOW,
+// before the host has computed the ticks' drivers.  It counts the first window's FSM and then waits
+// on the device (k_lf_wait) until the matching mdr_rollout posts the drivers through pinned memory,
+// so the graph launch and the count overlap the host work.  The next mdr_rollout with the same
+// arguments posts; any other entry point cancels it (the graph then skips every kernel).  Falls
+// back to mdr_rollout_begin when the launch-first path does not apply: a random source needs the
+// device to know tick0 (the previous rollout ended at tick0 - 1), n <= 1024, the windowed path.
+int mdr_rollout_launch(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, int64_t act_stride, int mode,
+                       double* reward, int64_t rew_stride, double* p_out, void* stream) {
+  drop_begun(c);
+  if (!c || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout_launch: bad argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout_launch: context not bound");
+  if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout_launch: bad action source");
+  if (int rc = lf_check(c)) return rc;
+  const bool ok = c->h_lf_ring && window_ok(c, mode) && n <= kLfCap && c->kp.penalty_mode == MDR_PEN_INDIVIDUAL_L2 &&
+                  (mode != MDR_ACT_RANDOM || (c->next_tick_known && c->next_tick == tick0)) &&
+                  !getenv("MDR_NO_LAUNCH_FIRST");
+  if (!ok) return mdr_rollout_begin(c, n, tick0, action, act_stride, mode, stream);
+  hipStream_t st = S(stream);
+  int rc = refresh_if_dirty(c, st);
+  if (!rc) rc = wslab_clean(c, st);
+  if (!rc) rc = ensure_ticks(c, n);
+  if (rc) return rc;
+  GraphKey key{n, mode + 2000, action, act_stride, reward, rew_stride, p_out, nullptr};
+  auto it = c->graphs.find(key);
+  if (it == c->graphs.end()) {
+    hipGraphExec_t ex;
+    rc = capture_graph(c, [&](hipStream_t cs) {
+      return rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, cs, false, true);
+    }, &ex);
+    if (rc) return rc;
+    it = c->graphs.emplace(key, std::make_pair(ex, c->ring)).first;
+  }
+  if (hipGraphLaunch(it->second.first, st) != hipSuccess) {
+    c->wslab_dirty = true;
+    return fail(MDR_EHIP, "mdr_rollout_launch: hipGraphLaunch");
+  }
+  c->lf_seq += 1;
+  c->lf.on = true;
+  c->lf.seq = c->lf_seq;
+  c->lf.tick0 = tick0;
+  c->lf.n = n;
+  c->lf.mode = mode;
+  c->lf.ring_end = it->second.second;
+  c->lf.action = action;
+  c->lf.act_stride = act_stride;
+  c->lf.reward = reward;
+  c->lf.rew_stride = rew_stride;
+  c->lf.p_out = p_out;
+  return MDR_OK;
+}
+
+// Diagnostics: launch-first graphs launched so far on this context.
+int mdr_rollout_launched(mdr_ctx* c, uint64_t* count) {
+  if (!c || !count) return fail(MDR_EARG, "mdr_rollout_launched: null argument");
+  *count = c->lf_seq;
+  return MDR_OK;
+}
+
+// Cancel a launched rollout whose drivers will not come (the launched graph skips its kernels; the
+// device state is unchanged).  A no-op when none is pending.
+int mdr_rollout_cancel(mdr_ctx* c) {
+  if (!c) return fail(MDR_EARG, "mdr_rollout_cancel: null context");
+  drop_begun(c);
   return MDR_OK;
 }
 
@@ -847,6 +1035,8 @@ int mdr_time_step_kernels(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_
   rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, nullptr, st);
   c->step_events = nullptr;
   c->counts_ready = false;
+  c->next_tick_known = !rc && window_ok(c, mode);
+  c->next_tick = ticks[n - 1].tick + 1;
   float total = 0.0f;
   if (!rc && !evs.empty() && hipEventSynchronize(evs.back()) != hipSuccess) rc = fail(MDR_EHIP, "event sync");
   for (size_t i = 0; !rc && i + 1 < evs.size(); i += 2) {
@@ -1140,6 +1330,8 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
     if (rc) return rc;
     rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, c->comm, st);
     c->counts_ready = false;
+    c->next_tick_known = !rc;
+    c->next_tick = ticks[n - 1].tick + 1;
     return rc;
   }
   const bool can_overlap = lookahead_ok(mode) && rew_stride != 0 && c->comm_stream;

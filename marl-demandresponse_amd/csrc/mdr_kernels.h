@@ -90,11 +90,16 @@ constexpr int kWindowRec = 4;   // = kWinRec: doubles per tick record of a windo
 template <int ACT, int HPT, bool SIMPLE>  // SIMPLE: deadband 0 and norm_temp 1 (reward without branches / division)
 __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int K,
                               int la_K, const double* rec, double* reward, int64_t rew_stride, uint64_t* onb,
-                              uint32_t* wah, unsigned long long* next_slot);
-__global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
+                              uint32_t* wah, unsigned long long* next_slot, const int* abort);
+__global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out,
+                             const int* abort, uint64_t* next_tick);
 template <int ACT, int HPT>
 __global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp,
-                               uint64_t tick0, int nt, unsigned long long* slot, uint64_t* onb, uint32_t* wah);
+                               uint64_t tick0, const uint64_t* tick0p, int nt, unsigned long long* slot,
+                               uint64_t* onb, uint32_t* wah);
+__global__ void k_lf_wait(const TickArgs* ring, int cap, uint64_t* ctl, uint64_t* dseq, int* dabort, int n,
+                          TickArgs* dst, uint64_t timeout_ticks);
+constexpr int kLfCap = 1024;  // ticks per launch-first ring slot
 __global__ void k_probe_stream(KParams p, double* reward);
 __global__ void k_refresh(KParams p, double* coef, int* params_bad);
 __global__ void k_div_check(const double* a, const double* b, int64_t n, unsigned long long* mismatches);

@@ -618,8 +618,10 @@ __device__ __forceinline__ void win_tick_record(const KParams& p, const unsigned
 // one block per tick j, one wave per class: sum the 64 shards (sharded rollouts: already summed
 // over ranks by the allreduce), zero them, and write the tick record
 __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long long* __restrict__ slot, int nt,
-                                                    const TickArgs* __restrict__ tkp, double* p_out) {
+                                                    const TickArgs* __restrict__ tkp, double* p_out,
+                                                    const int* __restrict__ abort, uint64_t* __restrict__ next_tick) {
   __shared__ unsigned long long s_red[kWinCap];
+  if (abort && *abort) return;  // a cancelled launch-first rollout (k_lf_wait)
   const int j = blockIdx.x, c = threadIdx.x >> 6, q = threadIdx.x & 63, ncap = p.n_cap;
   // the record's other inputs are loaded by thread 0 while the shards are read (one memory
   // round trip instead of three dependent ones)
@@ -643,8 +645,10 @@ __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long lon
     s_red[c] = v;
   }
   __syncthreads();
-  if (threadIdx.x == 0)
+  if (threadIdx.x == 0) {
     win_tick_record(p, s_red, tk, p_on, win_rec(slot, ncap) + j * kWinRec, j == nt - 1 ? p_out : nullptr);
+    if (next_tick && j == nt - 1) *next_tick = tk.tick + 1;  // the tick id the next rollout starts at
+  }
 }
 
 // the wave tile: 64 * HPT consecutive houses, house slot h of lane l = i0 + 64 h
@@ -808,7 +812,8 @@ __device__ __forceinline__ void win_classes(const WinTile<HPT>& t, const int* cl
 template <int ACT, int HPT>
 __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* __restrict__ action,
                                                       int64_t act_stride, const TickArgs* __restrict__ tkp,
-                                                      uint64_t tick0, int nt, unsigned long long* __restrict__ slot,
+                                                      uint64_t tick0, const uint64_t* __restrict__ tick0p, int nt,
+                                                      unsigned long long* __restrict__ slot,
                                                       uint64_t* __restrict__ onb, uint32_t* __restrict__ wah) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
   const int wv = threadIdx.x >> 6;
@@ -822,7 +827,8 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
   }
   uint64_t cm[HPT][kWinCap];
   win_classes<HPT>(t, cls, cm);
-  win_run<ACT, HPT>(p, w, cm, t, tkp, tick0, nt, action, act_stride, s_cnt[wv], onb + (size_t)t.tile * HPT * kWinMax);
+  win_run<ACT, HPT>(p, w, cm, t, tkp, tick0p ? *tick0p : tick0, nt, action, act_stride, s_cnt[wv],
+                    onb + (size_t)t.tile * HPT * kWinMax);
 #pragma unroll
   for (int h = 0; h < HPT; ++h)
     if (t.v[h]) wah[t.i0 + 64u * h] = w[h];
@@ -847,8 +853,10 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
                                                      int la_K, const double* __restrict__ rec,
                                                      double* __restrict__ reward, int64_t rew_stride,
                                                      uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
-                                                     unsigned long long* __restrict__ next_slot) {
+                                                     unsigned long long* __restrict__ next_slot,
+                                                     const int* __restrict__ abort) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
+  if (abort && *abort) return;  // a cancelled launch-first rollout (k_lf_wait)
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
   uint64_t* onb_w = onb + (size_t)t.tile * HPT * kWinMax;  // this wave's rows [kWinMax][HPT]
@@ -974,15 +982,59 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   }
 }
 
+// Launch-first rollouts (mdr_rollout_launch): the graph is launched BEFORE the host has the ticks'
+// drivers, and this one-block kernel (after the first window's FSM count, which needs only tick
+// ids) waits for them.  The host writes the n records into ring slot (seq & 1) of pinned memory
+// and then posts seq (ctl[0]); a cancel posts ctl[2] instead.  Thread 0 polls with system-scope
+// loads (no cached copy) and a bounded wait: after timeout wall-clock ticks the rollout is aborted
+// like a cancel, so every wave always exits.  The records are copied to dst (the device staging
+// the reduce / step kernels read), then *dseq = seq, *dabort = 0 (run) / 1 (cancelled) / 2 (timed
+// out) for the kernels that follow, and ctl[1] = seq | abort << 62 acknowledges the slot to the
+// host (which reuses it two launches later).  Only vector memory operations touch host memory.
+__global__ void __launch_bounds__(256) k_lf_wait(const TickArgs* ring, int cap, uint64_t* ctl, uint64_t* dseq,
+                                                 int* dabort, int n, TickArgs* __restrict__ dst,
+                                                 uint64_t timeout_ticks) {
+  __shared__ uint64_t s_seq;
+  __shared__ int s_ab;
+  if (threadIdx.x == 0) {
+    const uint64_t want = *dseq + 1;
+    const uint64_t t0 = wall_clock64();
+    int ab = 0;
+    for (;;) {
+      if (__hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= want) break;
+      if (__hip_atomic_load(&ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= want) { ab = 1; break; }
+      if (wall_clock64() - t0 > timeout_ticks) { ab = 2; break; }
+      __builtin_amdgcn_s_sleep(2);
+    }
+    s_seq = want;
+    s_ab = ab;
+  }
+  __syncthreads();
+  const uint64_t want = s_seq;
+  const int ab = s_ab;
+  if (!ab) {
+    const uint64_t* src = reinterpret_cast<const uint64_t*>(ring + (size_t)(want & 1u) * cap);
+    uint64_t* d = reinterpret_cast<uint64_t*>(dst);
+    for (int i = threadIdx.x; i < 4 * n; i += blockDim.x)
+      d[i] = __hip_atomic_load(&src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    *dseq = want;
+    *dabort = ab;
+    __hip_atomic_store(&ctl[1], want | ((uint64_t)ab << 62), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 #define MDR_INST_WIN(A, H)                                                                                      \
   template __global__ void k_step_window<A, H, true>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
                                                      const double*, double*, int64_t, uint64_t*, uint32_t*,      \
-                                                     unsigned long long*);                                      \
+                                                     unsigned long long*, const int*);                          \
   template __global__ void k_step_window<A, H, false>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
                                                       const double*, double*, int64_t, uint64_t*, uint32_t*,      \
-                                                      unsigned long long*);                                      \
-  template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, uint64_t, int,  \
-                                                unsigned long long*, uint64_t*, uint32_t*);
+                                                      unsigned long long*, const int*);                          \
+  template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, uint64_t,       \
+                                                const uint64_t*, int, unsigned long long*, uint64_t*, uint32_t*);
 MDR_INST_WIN(MDR_ACT_RANDOM, 1)
 MDR_INST_WIN(MDR_ACT_ALWAYS_ON, 1)
 MDR_INST_WIN(MDR_ACT_BUFFER, 1)

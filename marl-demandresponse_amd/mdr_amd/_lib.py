@@ -12,7 +12,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MDR_LIB", os.path.join(HERE, "libmdr_hip.so"))
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MAX_CAP = 64
 
 # enums (mdr.h)
@@ -111,6 +111,9 @@ SIGNATURES = {
     "mdr_set_rollout_window": (I, [VP, I]),
     "mdr_time_step_kernels": (I, [VP, I, VP, VP, I64, I, VP, I64, VP, P(C.c_float), P(I)]),
     "mdr_rollout_begin": (I, [VP, I, U64, VP, I64, I, VP]),
+    "mdr_rollout_launch": (I, [VP, I, U64, VP, I64, I, VP, I64, VP, VP]),
+    "mdr_rollout_cancel": (I, [VP]),
+    "mdr_rollout_launched": (I, [VP, VP]),
     "mdr_populate": (I, [VP, P(mdr_pop_spec), VP]),
     "mdr_power_counts": (I, [VP, VP, I, U64, VP]),
     "mdr_counts_buffer": (I, [VP, P(VP), P(I)]),

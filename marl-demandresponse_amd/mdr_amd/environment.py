@@ -565,26 +565,40 @@ class Environment:
         if rewards is None:
             rewards = torch.empty((n_ticks, self._n_local), dtype=torch.float64, device=sh.device)
         rew_stride = 0 if rewards.dim() == 1 else self._n_local  # 1-D: every tick overwrites it
+        launched = False
         if self._comm is None and self.power_grid.interp is None and self._links is not None:
-            # the first window's FSM count needs only the tick ids: on the device while the host
-            # computes the drivers (mdr_rollout_begin; the rollout below consumes it)
-            sh.rollout_begin(n_ticks, self._tick, actions, self._n_local if actions is not None else 0, mode)
-        done = 0
-        while done < n_ticks:  # one window unless interpolation ends it early (driver_window)
-            ticks = self.driver_window(n_ticks - done)
-            k = len(ticks)
-            whole = done == 0 and k == n_ticks  # one window: the caller's buffers as they are
-            a = None if actions is None else (actions if whole and actions.shape[0] == k else actions[done:done + k])
-            r = rewards[done:done + k] if rew_stride and not (whole and rewards.shape[0] == k) else rewards
-            if self._comm is not None:
-                self._comm.rollout(sh, ticks, a, mode, r, rew_stride)
+            act_stride = self._n_local if actions is not None else 0
+            if use_graph:
+                # the whole graph is launched before the host computes the drivers: its first
+                # window's FSM count needs only the tick ids, then it waits on the device for the
+                # drivers that sh.rollout below posts (mdr_rollout_launch; falls back to counting
+                # the first window early, mdr_rollout_begin)
+                sh.rollout_launch(n_ticks, self._tick, actions, act_stride, mode, rewards, rew_stride)
+                launched = True
             else:
-                # graphs are cached per (length, buffers): shorter windows only reuse them on 1-D rewards
-                g = use_graph and (k == n_ticks or (a is None and not rew_stride))
-                sh.rollout(ticks, a, self._n_local if a is not None else 0, mode, r, rew_stride, g)
-            self._P_dev_valid = True
-            self.finish_grid_step()
-            done += k
+                sh.rollout_begin(n_ticks, self._tick, actions, act_stride, mode)
+        done = 0
+        try:
+            while done < n_ticks:  # one window unless interpolation ends it early (driver_window)
+                ticks = self.driver_window(n_ticks - done)
+                k = len(ticks)
+                whole = done == 0 and k == n_ticks  # one window: the caller's buffers as they are
+                a = None if actions is None else (actions if whole and actions.shape[0] == k else actions[done:done + k])
+                r = rewards[done:done + k] if rew_stride and not (whole and rewards.shape[0] == k) else rewards
+                if self._comm is not None:
+                    self._comm.rollout(sh, ticks, a, mode, r, rew_stride)
+                else:
+                    # graphs are cached per (length, buffers): shorter windows only reuse them on 1-D rewards
+                    g = use_graph and (k == n_ticks or (a is None and not rew_stride))
+                    sh.rollout(ticks, a, self._n_local if a is not None else 0, mode, r, rew_stride, g)
+                launched = False
+                self._P_dev_valid = True
+                self.finish_grid_step()
+                done += k
+        except BaseException:
+            if launched:  # the launched graph must not wait for drivers that will not come
+                sh.rollout_cancel()
+            raise
         self._counts_ready = 0
         return rewards
 

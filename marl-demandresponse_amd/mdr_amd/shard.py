@@ -178,6 +178,21 @@ class HipShard:
         L.check(self.lib.mdr_rollout_begin(self.ctx, n, tick0, L.ptr(action), act_stride, mode, self.stream()),
                 "mdr_rollout_begin")
 
+    def rollout_launch(self, n, tick0, action, act_stride, mode, reward, rew_stride):
+        """mdr_rollout_launch: the whole rollout graph, launched before the host computes the drivers
+        (the matching ``rollout`` posts them; ``rollout_cancel`` if they will not come)."""
+        L.check(self.lib.mdr_rollout_launch(self.ctx, n, tick0, L.ptr(action), act_stride, mode, L.ptr(reward),
+                                            rew_stride, L.ptr(self.p_dev), self.stream()), "mdr_rollout_launch")
+
+    def rollout_cancel(self):
+        L.check(self.lib.mdr_rollout_cancel(self.ctx), "mdr_rollout_cancel")
+
+    def rollout_launched(self) -> int:
+        """Launch-first rollout graphs launched so far (mdr_rollout_launched)."""
+        v = C.c_uint64()
+        L.check(self.lib.mdr_rollout_launched(self.ctx, C.byref(v)), "mdr_rollout_launched")
+        return int(v.value)
+
     def time_step_kernels(self, ticks, action, act_stride, mode, reward, rew_stride):
         """mdr_time_step_kernels: (summed step-kernel ms, step launches) of one directly launched rollout."""
         ms, nl = C.c_float(), C.c_int()

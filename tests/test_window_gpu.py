@@ -191,3 +191,68 @@ def test_rollout_begin_early_count(torch_gpu, mode):
     roll(e2, 20, r2, begin=False)
     _same_state(torch, e1, e2)
     assert torch.equal(r1[:20], r2[:20])
+
+
+@pytest.mark.parametrize("mode", ["random", "always_on", "buffer"])
+def test_rollout_launch_first(torch_gpu, mode):
+    """mdr_rollout_launch (Environment.rollout's default): the rollout graph is launched before the
+    host computes the drivers and waits on the device for them.  Back-to-back calls without a host
+    synchronisation, calls of other lengths, a step in between, a cancelled launch (the drivers
+    raise) and a call longer than the ring all equal a twin that stages the drivers first (plain
+    mdr_rollout); the launch-first path really ran (mdr_rollout_launched)."""
+    torch = torch_gpu
+    from mdr_amd import _lib as L
+
+    n = 20011
+    e1, e2 = _pair(n)
+    m = {"random": L.ACT_RANDOM, "always_on": L.ACT_ALWAYS_ON, "buffer": L.ACT_BUFFER}[mode]
+    T = 1100
+    acts = (torch.rand((T, n), device="cuda") < 0.5).to(torch.uint8) if mode == "buffer" else None
+    r1 = torch.empty((T, n), dtype=torch.float64, device="cuda")
+    r2 = torch.empty_like(r1)
+
+    def twin(k):
+        a = None if acts is None else acts[:k]
+        ticks = e2.driver_window(k)
+        e2.shard.rollout(ticks, a, n if a is not None else 0, m, r2[:k], n, True)
+        e2._P_dev_valid = True
+        e2.finish_grid_step()
+
+    def roll(k):
+        e1.rollout(k, actions=None if acts is None else acts[:k], action_mode=mode, rewards=r1[:k])
+
+    def check(k):
+        _same_state(torch, e1, e2)
+        assert torch.equal(r1[:k], r2[:k])
+
+    l0 = e1.shard.rollout_launched()
+    for k in (20, 20, 20, 32, 7, 20):  # back to back, no host synchronisation in between
+        roll(k)
+        twin(k)
+    check(20)
+    assert e1.shard.rollout_launched() - l0 >= 4, "launch-first path not taken"
+    # a step in between (the device's next tick id is stale for a random source: falls back)
+    step_a = (torch.rand(n, device="cuda") < 0.5).to(torch.uint8)
+    e1.step_tensor(step_a)
+    e2.step_tensor(step_a)
+    for k in (20, 20):
+        roll(k)
+        twin(k)
+    check(20)
+    # a cancelled launch: the drivers raise after the graph was launched; nothing changes
+    orig = e1.driver_window
+    e1.driver_window = lambda k: (_ for _ in ()).throw(RuntimeError("driver failure"))
+    with pytest.raises(RuntimeError):
+        roll(20)
+    e1.driver_window = orig
+    for k in (20, 20):
+        roll(k)
+        twin(k)
+    check(20)
+    # longer than the launch-first ring (1024 ticks): the early-count path
+    roll(T)
+    twin(T)
+    check(T)
+    roll(20)
+    twin(20)
+    check(20)

@@ -65,6 +65,28 @@ def main():
         t2 = time.perf_counter()
         print(f"env.rollout rep {r}: call {1e6 * (t1 - t0):7.1f} us  wall {1e6 * (t2 - t0):7.1f} us  "
               f"event window {1e3 * e0.elapsed_time(e1):7.1f} us", flush=True)
+    # the launch-first sequence of Environment.rollout, phase by phase
+    from mdr_amd import _lib as L
+    for r in range(a.reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        e0.record(ls)
+        sh.rollout_launch(T, env._tick, None, 0, L.ACT_RANDOM, rew, n)
+        t1 = time.perf_counter()
+        ticks = env.driver_window(T)
+        t2 = time.perf_counter()
+        sh.rollout(ticks, None, 0, L.ACT_RANDOM, rew, n, True)
+        t3 = time.perf_counter()
+        env._P_dev_valid = True
+        env.finish_grid_step()
+        t4 = time.perf_counter()
+        e1.record(ls)
+        torch.cuda.synchronize()
+        t5 = time.perf_counter()
+        print(f"launch-first rep {r}: launch {1e6 * (t1 - t0):6.1f} us  drivers {1e6 * (t2 - t1):6.1f} us  "
+              f"post {1e6 * (t3 - t2):6.1f} us  grid {1e6 * (t4 - t3):6.1f} us  sync {1e6 * (t5 - t4):6.1f} us  "
+              f"wall {1e6 * (t5 - t0):6.1f} us  event {1e3 * e0.elapsed_time(e1):6.1f} us  "
+              f"launched {sh.rollout_launched()}", flush=True)
     # device-only replay of the same graph (no host drivers): the floor of the timed region
     for r in range(3):
         torch.cuda.synchronize()
