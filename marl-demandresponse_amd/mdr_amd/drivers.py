@@ -208,9 +208,13 @@ class Signal:
         if self.mode == "perlin":
             from .perlin import Perlin
 
-            # SignalCalculator draws the perlin seed from the global RNG (signal_calculator.py:24-31)
+            # SignalCalculator draws the perlin seed from the global RNG (signal_calculator.py:24-31);
+            # MDR_PERLIN_RESEED_GLOBAL=1: the pre-1.12 perlin_noise side effect on that generator
+            import os
+
+            side = os.environ.get("MDR_PERLIN_RESEED_GLOBAL", "0") == "1"
             self.perlin = Perlin(1, signal_props.nb_octaves, signal_props.octaves_step,
-                                 signal_props.period, rng.random())
+                                 signal_props.period, rng.random(), global_rng=rng if side else None)
         elif self.mode not in ("flat", "sinusoidals", "regular_steps"):
             raise ValueError(f"unknown signal mode {self.mode!r}")
 

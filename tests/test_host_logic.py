@@ -4,6 +4,7 @@ bit-identical to the reference (same expressions, same RNG call order)."""
 import copy
 import datetime as dt
 import json
+import math
 import random
 
 import numpy as np
@@ -135,6 +136,34 @@ def test_perlin_restatement_statistics():
     sig = D.Signal(C.SignalProperties(mode="perlin"), 10, rng=random.Random(1))
     s = [float(sig(42000.0, dt.datetime(2021, 5, 5, 12, 0, k))) for k in range(0, 60, 4)]
     assert min(s) >= 0.0
+
+
+def test_perlin_published_algorithm():
+    """The 1-D lattice noise as perlin_noise publishes it: gradient of lattice point k =
+    uniform(-1, 1) of a Mersenne Twister seeded with (k + 1) * seed, contribution fade(1 - |d|) *
+    g * d; the pre-1.12 global-RNG side effect reseeds the given generator (parity unpinned)."""
+    from mdr_amd.perlin import Perlin, _GradientNoise1D, _fade
+
+    seed = 0.4172
+    g = _GradientNoise1D(10, seed)
+    for x in (0.0137, 0.5, 2.25, 7.91):
+        xs = x * 10
+        want = 0
+        for k in (math.floor(xs), math.floor(xs + 1)):
+            gk = random.Random((k + 1) * seed).uniform(-1, 1)
+            want += _fade(1 - abs(xs - k)) * (gk * (xs - k))
+        assert g.noise(x) == want
+    rng = random.Random(5)
+    side = _GradientNoise1D(10, seed, global_rng=rng)
+    assert side.noise(0.5) == g.noise(0.5)
+    ref = random.Random(7 * seed)  # the last lattice point of xs = 5.0 is k = 6: seed (6 + 1) * seed
+    ref.uniform(-1, 1)
+    assert rng.random() == ref.random()
+    # the octave sum (perlin.py:51-56): last octave divided by 2**n - 1
+    pn = Perlin(1, 3, 5, 300, seed)
+    x = 1234.5
+    n = [pn.noise_list[j].noise(x / 300) for j in range(3)]
+    assert pn.calculate_noise(x) == 1 * (0 + n[0] / 1 + n[1] / 2 + n[2] / 7)
 
 
 def test_actor_init_matches_reference_mappo():
