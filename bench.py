@@ -208,17 +208,45 @@ def cpu_baseline(budget_s: float):
     return out
 
 
-def pmc_traffic(kernel: str, houses: int):
-    """HBM bytes per launch of `kernel` at `houses` from the committed rocprofv3 PMC passes
-    (profiles/pmc_traffic.json, written by tools/collect_profiles.py), if collected."""
+def pmc_record(kernel: str, houses: int):
+    """The committed rocprofv3 PMC record of `kernel` at `houses` (profiles/pmc_traffic.json,
+    written by tools/collect_profiles.py: per-launch counter sums), or None."""
     path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
     try:
         with open(path) as f:
             d = json.load(f)
         rec = d.get(kernel, {}).get(str(houses))
-        return None if rec is None else float(rec["hbm_bytes_per_launch"])
-    except (OSError, ValueError, KeyError, AttributeError):
+        return rec if isinstance(rec, dict) else None
+    except (OSError, ValueError, AttributeError):
         return None
+
+
+def pmc_traffic(kernel: str, houses: int):
+    """HBM bytes per launch of `kernel` at `houses` from the committed PMC passes, if collected."""
+    rec = pmc_record(kernel, houses)
+    try:
+        return None if rec is None else float(rec["hbm_bytes_per_launch"])
+    except (KeyError, TypeError, ValueError):
+        return None
+
+
+# wave64 VALU issue peak of MI355X: 256 CUs x 4 SIMDs, one wave64 instruction per 4 cycles per SIMD
+# (16 lanes; fp64 FMA at full rate), 2.4 GHz peak engine clock (MI355X_MICROARCH.md)
+VALU_PEAK_GINST = 1024 * 2.4 / 4.0  # G wave-instructions / s
+
+
+def valu_roofline(kernel: str, houses: int, kern_ms: float):
+    """The issue-rate roofline that actually bounds the temporally blocked step kernel (fp64 VALU):
+    SQ_INSTS_VALU per launch from the committed PMC record over the live per-launch time."""
+    rec = pmc_record(kernel, houses)
+    if rec is None or "SQ_INSTS_VALU" not in rec or kern_ms <= 0:
+        return None
+    inst = float(rec["SQ_INSTS_VALU"])
+    ach = inst / (kern_ms * 1e-3) / 1e9
+    return {"achieved": ach, "peak": VALU_PEAK_GINST, "unit": "G wave64 VALU instr/s", "frac": ach / VALU_PEAK_GINST,
+            "valu_instr_per_launch": inst,
+            "source": "SQ_INSTS_VALU per launch (profiles/pmc_traffic.json) / kernel_avg_us; peak = 1024 SIMDs x "
+                      "2.4 GHz / 4 cycles (the clock under this fp64 load is ~1.75 GHz, GRBM_GUI_ACTIVE)"}
 
 
 def main():
@@ -476,7 +504,8 @@ def main():
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "bytes_per_house_step": bytes_launch / (steps_launch * n_loc),
                      "timing": "hipExtLaunchKernel start/stop events around each step-kernel launch of a 1024-tick rollout "
-                  "after the timed region and 2048 untimed kernel-only ticks (steady-state clock)"},
+                  "after the timed region and 2048 untimed kernel-only ticks (steady-state clock)",
+                     "valu": valu_roofline(kern, n_loc, kern_ms)},
     }
     if g_act is not None:
         out["data"] = "synthetic (device Philox population, reference noise model)"
