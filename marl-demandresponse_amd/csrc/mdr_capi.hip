@@ -96,6 +96,10 @@ struct mdr_ctx {
   bool wslab_dirty = true;               // the slots' shard part must be zero when a rollout starts
   uint64_t* d_onb = nullptr;             // per-tick ON lane masks of the next window [tiles][HPT][kWindowMax]
   uint32_t* d_wah = nullptr;             // FSM word at the end of the next window, per house
+  uint64_t* d_onb2 = nullptr;            // second set for the count-ahead pipeline (window_launches pipe)
+  uint32_t* d_wah2 = nullptr;
+  size_t onb_bytes = 0, wah_bytes = 0;
+  bool win_pipe = true;                  // sharded windows: counts + allreduce on the comm stream (MDR_WINDOW_PIPELINE=0: serial)
   bool coef_dirty = true;
   double* d_coef = nullptr;              // [6][n] r1, r2, A3, A4, e1, e2
   int* d_flags = nullptr;                // [0] params_bad
@@ -401,9 +405,10 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
     // a window count slot: sharded slab | reduced counts (mdr_kernels.hip)
     c->wslab_len = kWindowMax * kCountShards * cfg->n_cap + kWindowMax * cfg->n_cap + kWindowMax * kWindowRec;
     const size_t tiles64 = ((size_t)cfg->n_local + 63) / 64 + 1;  // 64-house lane groups (either HPT)
+    c->onb_bytes = tiles64 * kWindowMax * sizeof(uint64_t);
+    c->wah_bytes = ((size_t)cfg->n_local + 1) * sizeof(uint32_t);
     if (hipMalloc(&c->d_wslab, 3 * sizeof(unsigned long long) * c->wslab_len) != hipSuccess ||
-        hipMalloc(&c->d_onb, tiles64 * kWindowMax * sizeof(uint64_t)) != hipSuccess ||
-        hipMalloc(&c->d_wah, ((size_t)cfg->n_local + 1) * sizeof(uint32_t)) != hipSuccess)
+        hipMalloc(&c->d_onb, c->onb_bytes) != hipSuccess || hipMalloc(&c->d_wah, c->wah_bytes) != hipSuccess)
       return cleanup(fail(MDR_ENOMEM, "window count slabs"));
   } else {
     c->win = 0;
@@ -429,6 +434,7 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
       c->n_cu < 1)
     c->n_cu = 256;
   if (const char* e = getenv("MDR_SHARDED_OVERLAP")) c->overlap_mode = atoi(e) < 0 ? -1 : atoi(e) != 0;
+  if (const char* e = getenv("MDR_WINDOW_PIPELINE")) c->win_pipe = atoi(e) != 0;
   *out = c;
   return MDR_OK;
 }
@@ -456,6 +462,8 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->d_wslab);
   hipFree(c->d_onb);
   hipFree(c->d_wah);
+  hipFree(c->d_onb2);
+  hipFree(c->d_wah2);
   hipFree(c->d_pen_partial);
   hipFree(c->d_partial2);
   hipFree(c->d_ticks);
@@ -673,9 +681,15 @@ static int wslab_clean(mdr_ctx* c, hipStream_t st) {
 // the previous rollout's last reduce), then k_lf_wait stages the drivers once the host posts them;
 // every later kernel returns at once if it was cancelled.  Every sequence's last reduce writes the
 // tick id the next rollout starts at into d_lf[1].
+//
+// pipe (sharded, comm stream present): the count-ahead pipeline.  The FSM of an open-loop source
+// needs no thermal state, so window w's count (from the FSM words at the end of window w-1) and
+// the allreduce of its counts run on the comm stream, up to two windows ahead of the compute
+// stream's reduce + step (which then has no lookahead): the allreduce latency hides behind the
+// step kernels.  Two sets of ON-mask / end-word buffers alternate; events order the reuse.
 static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t* action, int64_t act_stride,
                            int mode, double* reward, int64_t rew_stride, double* p_out, ncclComm_t comm,
-                           hipStream_t st, bool counted = false, bool lf = false) {
+                           hipStream_t st, bool counted = false, bool lf = false, bool pipe = false) {
   const int nw = (n + c->win - 1) / c->win;
   const int base = n / nw, rem = n % nw;
   auto wsz = [&](int w) { return base + (w < rem ? 1 : 0); };
@@ -723,17 +737,63 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     else { if (db0) MDR_WIN_DISPATCH_S(2, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(2, false, __VA_ARGS__); }        \
   } while (0)
   c->wslab_dirty = true;  // until the sequence is fully issued
+  if (pipe) {
+    hipStream_t cs = c->comm_stream;
+    uint64_t* onbs[2] = {c->d_onb, c->d_onb2};
+    uint32_t* wahs[2] = {c->d_wah, c->d_wah2};
+    HIP_TRY(hipEventRecord(c->ev_pc, st));  // the state and staged ticks, before the first count
+    HIP_TRY(hipStreamWaitEvent(cs, c->ev_pc, 0));
+    int t0 = 0;
+    for (int w = 0; w < nw; ++w) {
+      const int K = wsz(w);
+      // comm stream: count(w) + allreduce; count(w) reuses the buffers step(w - 2) read
+      if (w >= 2) HIP_TRY(hipStreamWaitEvent(cs, c->ev_k1[(w - 2) % kSlabs], 0));
+      const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
+      const uint32_t* w_in = w == 0 ? nullptr : wahs[(w - 1) % 2];
+#define MDR_CNT_ON(H)                                                                                             \
+  do {                                                                                                            \
+    if (mode == MDR_ACT_RANDOM)                                                                                   \
+      hipLaunchKernelGGL((k_count_window<MDR_ACT_RANDOM, H>), dim3(grid), dim3(256), 0, cs, kp, a, act_stride,     \
+                         tk + t0, (uint64_t)0, (const uint64_t*)nullptr, K, slot(w), onbs[w % 2], wahs[w % 2], w_in); \
+    else if (mode == MDR_ACT_ALWAYS_ON)                                                                           \
+      hipLaunchKernelGGL((k_count_window<MDR_ACT_ALWAYS_ON, H>), dim3(grid), dim3(256), 0, cs, kp, a, act_stride,  \
+                         tk + t0, (uint64_t)0, (const uint64_t*)nullptr, K, slot(w), onbs[w % 2], wahs[w % 2], w_in); \
+    else                                                                                                          \
+      hipLaunchKernelGGL((k_count_window<MDR_ACT_BUFFER, H>), dim3(grid), dim3(256), 0, cs, kp, a, act_stride,     \
+                         tk + t0, (uint64_t)0, (const uint64_t*)nullptr, K, slot(w), onbs[w % 2], wahs[w % 2], w_in); \
+  } while (0)
+      if (hpt == 1) MDR_CNT_ON(1); else MDR_CNT_ON(2);
+#undef MDR_CNT_ON
+      LAUNCH_CHECK("k_count_window");
+      if (comm)
+        RCCL_TRY(ncclAllReduce(slot(w), slot(w), (size_t)K * kCountShards * ncap, ncclUint64, ncclSum, comm, cs));
+      HIP_TRY(hipEventRecord(c->ev_ar[w % kSlabs], cs));
+      // compute stream: reduce + step (no lookahead)
+      HIP_TRY(hipStreamWaitEvent(st, c->ev_ar[w % kSlabs], 0));
+      hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0,
+                         w == nw - 1 ? p_out : nullptr, (const int*)nullptr, w == nw - 1 ? c->d_lf + 1 : nullptr);
+      LAUNCH_CHECK("k_win_reduce");
+      const int* no_abort = nullptr;
+      MDR_STEP_WIN_DISPATCH(kp, a, act_stride, tk + t0, K, 0, rec(w), reward + (int64_t)t0 * rew_stride, rew_stride,
+                            onbs[w % 2], wahs[w % 2], slot(w), no_abort);
+      LAUNCH_CHECK("k_step_window");
+      HIP_TRY(hipEventRecord(c->ev_k1[w % kSlabs], st));
+      t0 += K;
+    }
+    c->wslab_dirty = false;
+    return MDR_OK;
+  }
   const int* abort = lf ? reinterpret_cast<const int*>(c->d_lf + 2) : nullptr;
   if (lf) {
     MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, (const TickArgs*)nullptr, (uint64_t)0,
-                     (const uint64_t*)(c->d_lf + 1), wsz(0), slot(0), c->d_onb, c->d_wah);
+                     (const uint64_t*)(c->d_lf + 1), wsz(0), slot(0), c->d_onb, c->d_wah, (const uint32_t*)nullptr);
     LAUNCH_CHECK("k_count_window");
     hipLaunchKernelGGL(k_lf_wait, dim3(1), dim3(256), 0, st, c->h_lf_ring, kLfCap, c->h_lf_ctl, c->d_lf,
                        reinterpret_cast<int*>(c->d_lf + 2), n, const_cast<TickArgs*>(tk), c->lf_timeout);
     LAUNCH_CHECK("k_lf_wait");
   } else if (!counted) {  // (counted: mdr_rollout_begin launched it already)
     MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, (uint64_t)0, (const uint64_t*)nullptr, wsz(0),
-                     slot(0), c->d_onb, c->d_wah);
+                     slot(0), c->d_onb, c->d_wah, (const uint32_t*)nullptr);
     LAUNCH_CHECK("k_count_window");
   }
   int t0 = 0;
@@ -766,6 +826,20 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
 #undef MDR_STEP_WIN_DISPATCH
 #undef MDR_STEP_LAUNCH
   return MDR_OK;
+}
+
+// the second ON-mask / end-word set of the count-ahead pipeline (allocated on first use)
+static bool pipe_buffers(mdr_ctx* c) {
+  if (c->d_onb2 && c->d_wah2) return true;
+  if (hipMalloc(&c->d_onb2, c->onb_bytes) != hipSuccess || hipMalloc(&c->d_wah2, c->wah_bytes) != hipSuccess) {
+    (void)hipGetLastError();
+    hipFree(c->d_onb2);
+    hipFree(c->d_wah2);
+    c->d_onb2 = nullptr;
+    c->d_wah2 = nullptr;
+    return false;
+  }
+  return true;
 }
 
 // The launch sequence of a rollout; tick args come from d_ticks so a captured graph is reusable.
@@ -870,6 +944,18 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   rc = wslab_clean(c, st);
   if (rc) return rc;
   const auto t1 = std::chrono::steady_clock::now();
+  static const bool pipe_single = getenv("MDR_PIPE_SINGLE") != nullptr;  // A/B: count-ahead pipeline, 1 GPU
+  if (pipe_single && window_ok(c, mode) && !counted) {
+    if (!c->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+    if (pipe_buffers(c)) {
+      rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st, false,
+                           false, true);
+      c->counts_ready = false;
+      c->next_tick_known = !rc;
+      c->next_tick = ticks[n - 1].tick + 1;
+      return rc;
+    }
+  }
   if (!use_graph) {
     rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st, counted);
     c->counts_ready = false;
@@ -927,7 +1013,8 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   c->wslab_dirty = true;
 #define MDR_BEGIN_COUNT(A, H)                                                                                   \
   hipLaunchKernelGGL((k_count_window<A, H>), dim3(grid), dim3(256), 0, st, c->kp, action, act_stride,          \
-                     (const TickArgs*)nullptr, tick0, (const uint64_t*)nullptr, k0, c->d_wslab, c->d_onb, c->d_wah)
+                     (const TickArgs*)nullptr, tick0, (const uint64_t*)nullptr, k0, c->d_wslab, c->d_onb, c->d_wah,  \
+                     (const uint32_t*)nullptr)
   if (c->win_hpt == 1) {
     if (mode == MDR_ACT_RANDOM) MDR_BEGIN_COUNT(MDR_ACT_RANDOM, 1);
     else if (mode == MDR_ACT_ALWAYS_ON) MDR_BEGIN_COUNT(MDR_ACT_ALWAYS_ON, 1);
@@ -1124,6 +1211,14 @@ int mdr_halo_pack(mdr_ctx* c, const mdr_obs_spec* sp, float* out, void* stream) 
 }
 
 // ------------------------------------------------------------------------------------ greedy
+// The greedy order: a stable sort of (key, house) pairs (hipCUB / rocprim radix sort; at 2^20
+// houses rocprim runs its block merge sort, which measured faster here than forcing Onesweep:
+// 212 us vs ~250 us incl. its per-pass lookback resets, profiles/r02g_greedy_kernel_stats.csv)
+static hipError_t greedy_sort(void* tmp, size_t& bytes, const double* kin, double* kout, const int* vin, int* vout,
+                              int64_t n, hipStream_t st) {
+  return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, (int)n, 0, 64, st);
+}
+
 static int greedy_scratch(mdr_ctx* c) {
   const int64_t n = c->kp.n;
   if (c->g_cap >= n) return MDR_OK;
@@ -1140,7 +1235,7 @@ static int greedy_scratch(mdr_ctx* c) {
   HIP_TRY(hipMalloc(&c->g_kpos, 2 * sizeof(int64_t)));
   HIP_TRY(hipMalloc(&c->g_extra, 64 * sizeof(int64_t)));
   size_t b1 = 0, b2 = 0;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(nullptr, b1, c->g_key, c->g_key2, c->g_idx, c->g_idx2, (int)n));
+  HIP_TRY(greedy_sort(nullptr, b1, c->g_key, c->g_key2, c->g_idx, c->g_idx2, n, nullptr));
   HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b2, c->g_ps, c->g_incl, (int)n));
   c->g_tmp_bytes = b1 > b2 ? b1 : b2;
   HIP_TRY(hipMalloc(&c->g_tmp, c->g_tmp_bytes));
@@ -1158,8 +1253,7 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   hipLaunchKernelGGL(k_greedy_keys, dim3(blocks(n, 256)), dim3(256), 0, st, c->kp, c->g_key, c->g_idx);
   LAUNCH_CHECK("k_greedy_keys");
   size_t b = c->g_tmp_bytes;
-  HIP_TRY(hipcub::DeviceRadixSort::SortPairs(c->g_tmp, b, c->g_key, c->g_key2, c->g_idx, c->g_idx2, n,
-                                             0, 64, st));
+  HIP_TRY(greedy_sort(c->g_tmp, b, c->g_key, c->g_key2, c->g_idx, c->g_idx2, n, st));
   hipLaunchKernelGGL(k_greedy_gather, dim3(blocks(n, 256)), dim3(256), 0, st, c->kp, c->g_idx2, c->g_ps,
                      c->g_ls);
   LAUNCH_CHECK("k_greedy_gather");
@@ -1328,7 +1422,9 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
   if (window_ok(c, mode)) {
     rc = wslab_clean(c, st);
     if (rc) return rc;
-    rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, c->comm, st);
+    const bool pipe = c->win_pipe && c->comm_stream && pipe_buffers(c);
+    rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, c->comm, st, false,
+                         false, pipe);
     c->counts_ready = false;
     c->next_tick_known = !rc;
     c->next_tick = ticks[n - 1].tick + 1;

@@ -96,7 +96,7 @@ __global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const 
 template <int ACT, int HPT>
 __global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp,
                                uint64_t tick0, const uint64_t* tick0p, int nt, unsigned long long* slot,
-                               uint64_t* onb, uint32_t* wah);
+                               uint64_t* onb, uint32_t* wah, const uint32_t* w_in);
 __global__ void k_lf_wait(const TickArgs* ring, int cap, uint64_t* ctl, uint64_t* dseq, int* dabort, int n,
                           TickArgs* dst, uint64_t timeout_ticks);
 constexpr int kLfCap = 1024;  // ticks per launch-first ring slot

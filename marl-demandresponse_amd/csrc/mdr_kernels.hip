@@ -814,7 +814,8 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
                                                       int64_t act_stride, const TickArgs* __restrict__ tkp,
                                                       uint64_t tick0, const uint64_t* __restrict__ tick0p, int nt,
                                                       unsigned long long* __restrict__ slot,
-                                                      uint64_t* __restrict__ onb, uint32_t* __restrict__ wah) {
+                                                      uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
+                                                      const uint32_t* __restrict__ w_in) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
@@ -822,7 +823,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
   int cls[HPT];
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
-    w[h] = p.hvac[t.idx[h]];
+    w[h] = w_in ? w_in[t.idx[h]] : p.hvac[t.idx[h]];
     cls[h] = p.cap_idx[t.idx[h]];
   }
   uint64_t cm[HPT][kWinCap];
@@ -1034,7 +1035,8 @@ __global__ void __launch_bounds__(256) k_lf_wait(const TickArgs* ring, int cap, 
                                                       const double*, double*, int64_t, uint64_t*, uint32_t*,      \
                                                       unsigned long long*, const int*);                          \
   template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, uint64_t,       \
-                                                const uint64_t*, int, unsigned long long*, uint64_t*, uint32_t*);
+                                                const uint64_t*, int, unsigned long long*, uint64_t*, uint32_t*,  \
+                                                const uint32_t*);
 MDR_INST_WIN(MDR_ACT_RANDOM, 1)
 MDR_INST_WIN(MDR_ACT_ALWAYS_ON, 1)
 MDR_INST_WIN(MDR_ACT_BUFFER, 1)

@@ -26,7 +26,7 @@ import golden_util as gu
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-T_STEP, T_BUF, T_ROLL = 5, 3, 20  # a 20-tick rollout triggers the pipeline calibration
+T_STEP, T_BUF, T_ROLL = 5, 3, 70  # >= 16 ticks trigger the per-tick pipeline calibration; 3 windows
 
 
 INTERP = "interp"  # mode suffix: interpolation base power (row a10), re-estimated every 3 ticks
@@ -67,7 +67,10 @@ def _worker(rank, world, port, backend, kind, n, mode, out_dir):
     import torch
     import torch.distributed as dist
 
-    if kind.startswith("rccl-"):  # per-tick C loop (window 0), forced serial / overlapped pipeline
+    if kind == "rccl-winserial":  # windows without the count-ahead pipeline (one stream)
+        os.environ["MDR_WINDOW_PIPELINE"] = "0"
+        kind = "rccl"
+    elif kind.startswith("rccl-"):  # per-tick C loop (window 0), forced serial / overlapped pipeline
         os.environ["MDR_SHARDED_OVERLAP"] = "0" if kind == "rccl-serial" else "1"
         os.environ["MDR_WINDOW"] = "0"
         kind = "rccl"
@@ -101,6 +104,7 @@ def _free_port():
 
 @pytest.mark.parametrize("backend,kind,world,n,mode", [
     ("nccl", "rccl", 1, 3001, "individual_L2"),
+    ("nccl", "rccl-winserial", 1, 3001, "individual_L2"),
     ("nccl", "rccl-serial", 1, 3001, "individual_L2"),
     ("nccl", "rccl-overlap", 1, 3001, "individual_L2"),
     ("gloo", "torch", 2, 3001, "individual_L2"),
