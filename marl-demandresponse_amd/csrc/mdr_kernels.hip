@@ -920,11 +920,12 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
     r_ok = __double_as_longlong(rec[jn * kWinRec + 3]);
 #pragma unroll
     for (int h = 0; h < HPT; ++h) r_on[h] = onb_w[jn * HPT + h];
-    bool house_ok = true;
+    // all lanes in range: the comparison masks themselves (v_cmp writes a lane mask) against exec
+    uint64_t ok_m = ~0ull;
 #pragma unroll
-    for (int h = 0; h < HPT; ++h) house_ok = house_ok && fabs(T[h]) < 1048576.0 && fabs(Tm[h]) < 1048576.0;
-    // all lanes in range: the comparison mask itself against exec (no vector round trip)
-    const bool fast = params_ok && tick_ok && __builtin_amdgcn_ballot_w64(house_ok) == __builtin_amdgcn_read_exec();
+    for (int h = 0; h < HPT; ++h)
+      ok_m &= __builtin_amdgcn_ballot_w64(fabs(T[h]) < 1048576.0) & __builtin_amdgcn_ballot_w64(fabs(Tm[h]) < 1048576.0);
+    const bool fast = params_ok && tick_ok && ok_m == __builtin_amdgcn_read_exec();
     char* rrow = reinterpret_cast<char*>(reward + (int64_t)j * rew_stride);
     auto houses = [&](auto fast_c) {
       constexpr bool F = decltype(fast_c)::value;
