@@ -264,6 +264,9 @@ typedef struct mdr_obs_spec {
   double norm_reg_sig;   /* R */
   double cfg_ua, cfg_ca, cfg_cm, cfg_hm; /* house_prop (un-noised) for the thermal ratios */
   double cfg_cap;        /* hvac_prop.cooling_capacity (message hvac feature) */
+  const float* msg_all;  /* TABLE mode, multi-GPU: [n_global][msg_w] message features of every house
+                            (mdr_msg_pack of each shard, all-gathered); comm_table then holds GLOBAL
+                            house ids; NULL = single shard (table ids are local) */
 } mdr_obs_spec;
 
 typedef struct mdr_obs_scalars {
@@ -281,6 +284,10 @@ int mdr_obs(mdr_ctx* ctx, const mdr_obs_spec* spec, const mdr_obs_scalars* sc,
             const double* p_dev, float* obs, void* stream);
 /* message features of this shard's first hi and last lo houses -> out[(hi + lo) * msg_w] floats:
  * rows [0, hi) = first hi houses, rows [hi, hi + lo) = last lo houses. */
+/* Message features (Building.message, building.py:79-139) of every local house: out [n_local][msg_w]
+ * (sharded table comm modes all-gather these into mdr_obs_spec.msg_all). */
+int mdr_msg_pack(mdr_ctx* ctx, const mdr_obs_spec* spec, float* out, void* stream);
+
 int mdr_halo_pack(mdr_ctx* ctx, const mdr_obs_spec* spec, float* out, void* stream);
 
 /* ---- cluster statistics for the server's Metrics / UI summary ----------- */
@@ -296,6 +303,15 @@ int mdr_cluster_stats(mdr_ctx* ctx, const double* reward, double* out, void* str
 /* Next actions for the whole shard (single GPU: shard = cluster) from the current state: order
  * by -(T - target) ascending, then the reference's sequential take rule with budget S. */
 int mdr_ctrl_greedy(mdr_ctx* ctx, double budget, uint8_t* action, void* stream);
+
+/* Sharded greedy (the all-gather form): mdr_greedy_inputs writes this shard's
+ * rows key = -(T - target), P = cooling capacity / cop, lockout (u8); the caller all-gathers them
+ * in global house order, and every rank runs mdr_greedy_select over the n gathered rows — the same
+ * sort / sequential take rule as mdr_ctrl_greedy — writing the cluster's actions (u8 [n]), of
+ * which it keeps its own slice. */
+int mdr_greedy_inputs(mdr_ctx* ctx, double* key, double* power, uint8_t* lock, void* stream);
+int mdr_greedy_select(mdr_ctx* ctx, int64_t n, const double* key, const double* power, const uint8_t* lock,
+                      double budget, uint8_t* action, void* stream);
 
 /* ---- MA-PPO actor fused with the observation ----------------- */
 /* Replaces MAPPO.select_actions (server/app/core/agents/trainables/mappo.py:83-97) over

@@ -1152,6 +1152,7 @@ static ObsArgs obs_args(const mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_
   o.msg_hvac = sp->msg_hvac;
   o.comm_table = sp->comm_table;
   o.halo_msg = sp->halo_msg;
+  o.msg_all = sp->msg_all;
   o.norm_reg_sig = sp->norm_reg_sig;
   o.cfg_ua = sp->cfg_ua;
   o.cfg_ca = sp->cfg_ca;
@@ -1200,6 +1201,16 @@ int mdr_obs(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc, const
   return MDR_OK;
 }
 
+int mdr_msg_pack(mdr_ctx* c, const mdr_obs_spec* sp, float* out, void* stream) {
+  if (!c || !sp || !out) return fail(MDR_EARG, "mdr_msg_pack: null argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_msg_pack: context not bound");
+  ObsArgs o = obs_args(c, sp, nullptr);
+  if (o.msg_w > 16) return fail(MDR_EARG, "mdr_msg_pack: message wider than 16");
+  hipLaunchKernelGGL(k_msg_pack, dim3(blocks(c->kp.n, 256)), dim3(256), 0, S(stream), c->kp, o, out);
+  LAUNCH_CHECK("k_msg_pack");
+  return MDR_OK;
+}
+
 int mdr_halo_pack(mdr_ctx* c, const mdr_obs_spec* sp, float* out, void* stream) {
   if (!c || !sp || !out) return fail(MDR_EARG, "mdr_halo_pack: null argument");
   ObsArgs o = obs_args(c, sp, nullptr);
@@ -1219,8 +1230,7 @@ static hipError_t greedy_sort(void* tmp, size_t& bytes, const double* kin, doubl
   return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, (int)n, 0, 64, st);
 }
 
-static int greedy_scratch(mdr_ctx* c) {
-  const int64_t n = c->kp.n;
+static int greedy_scratch(mdr_ctx* c, int64_t n) {
   if (c->g_cap >= n) return MDR_OK;
   hipFree(c->g_key); hipFree(c->g_key2); hipFree(c->g_ps); hipFree(c->g_incl);
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
@@ -1246,7 +1256,7 @@ static int greedy_scratch(mdr_ctx* c) {
 int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   if (!c || !action) return fail(MDR_EARG, "mdr_ctrl_greedy: null argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_ctrl_greedy: context not bound");
-  int rc = greedy_scratch(c);
+  int rc = greedy_scratch(c, c->kp.n);
   if (rc) return rc;
   hipStream_t st = S(stream);
   const int n = (int)c->kp.n;
@@ -1266,6 +1276,41 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   LAUNCH_CHECK("k_greedy_walk");
   hipLaunchKernelGGL(k_greedy_apply, dim3(blocks(n, 256)), dim3(256), 0, st, (int64_t)n, c->g_idx2,
                      c->g_kpos, c->g_extra, action);
+  LAUNCH_CHECK("k_greedy_apply");
+  return MDR_OK;
+}
+
+int mdr_greedy_inputs(mdr_ctx* c, double* key, double* power, uint8_t* lock, void* stream) {
+  if (!c || !key || !power || !lock) return fail(MDR_EARG, "mdr_greedy_inputs: null argument");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_greedy_inputs: context not bound");
+  hipLaunchKernelGGL(k_greedy_inputs, dim3(blocks(c->kp.n, 256)), dim3(256), 0, S(stream), c->kp, key, power, lock);
+  LAUNCH_CHECK("k_greedy_inputs");
+  return MDR_OK;
+}
+
+int mdr_greedy_select(mdr_ctx* c, int64_t n, const double* key, const double* power, const uint8_t* lock,
+                      double budget, uint8_t* action, void* stream) {
+  if (!c || !key || !power || !lock || !action || n < 1) return fail(MDR_EARG, "mdr_greedy_select: bad argument");
+  if (n >= ((int64_t)1 << 31)) return fail(MDR_EARG, "mdr_greedy_select: n must be < 2^31");
+  int rc = greedy_scratch(c, n);
+  if (rc) return rc;
+  hipStream_t st = S(stream);
+  hipLaunchKernelGGL(k_greedy_iota, dim3(blocks(n, 256)), dim3(256), 0, st, n, c->g_idx);
+  LAUNCH_CHECK("k_greedy_iota");
+  size_t b = c->g_tmp_bytes;
+  HIP_TRY(greedy_sort(c->g_tmp, b, key, c->g_key2, c->g_idx, c->g_idx2, n, st));
+  hipLaunchKernelGGL(k_greedy_gather_rows, dim3(blocks(n, 256)), dim3(256), 0, st, n, c->g_idx2, power, lock,
+                     c->g_ps, c->g_ls);
+  LAUNCH_CHECK("k_greedy_gather_rows");
+  b = c->g_tmp_bytes;
+  HIP_TRY(hipcub::DeviceScan::InclusiveSum(c->g_tmp, b, c->g_ps, c->g_incl, (int)n, st));
+  double pmin = INFINITY;
+  for (int k = 0; k < c->cfg.n_cap; ++k) pmin = fmin(pmin, c->cfg.cap_table[k] / c->cfg.cop);
+  hipLaunchKernelGGL(k_greedy_walk, dim3(1), dim3(256), 0, st, n, c->g_incl, c->g_ps, c->g_ls, budget, pmin,
+                     c->g_kpos, c->g_extra, 64);
+  LAUNCH_CHECK("k_greedy_walk");
+  hipLaunchKernelGGL(k_greedy_apply, dim3(blocks(n, 256)), dim3(256), 0, st, n, c->g_idx2, c->g_kpos, c->g_extra,
+                     action);
   LAUNCH_CHECK("k_greedy_apply");
   return MDR_OK;
 }

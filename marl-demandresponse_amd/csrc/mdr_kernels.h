@@ -65,6 +65,7 @@ struct ObsArgs {
   int hvac_state, solar_state, thermal_state, msg_thermal, msg_hvac;
   const int32_t* comm_table;
   const float* halo_msg;  // [lo + hi][msg_w] or null
+  const float* msg_all;   // TABLE, sharded: [n_global][msg_w] (comm_table ids are global) or null
   double norm_reg_sig, cfg_ua, cfg_ca, cfg_cm, cfg_hm, cfg_cop, cfg_lcf, cfg_cap;
   double p, s, solar, t_od;
   const double* sc_dev;  // per-tick device mdr_obs_scalars row {-, s, solar, t_od} overriding the values above, or null
@@ -115,6 +116,7 @@ __global__ void k_cluster_stats(KParams p, const double* reward, double* partial
 __global__ void k_cluster_stats_final(const double* partial, int nblk, double* out);
 __global__ void k_obs(KParams p, ObsArgs o, const double* p_dev, float* obs);
 __global__ void k_halo_pack(KParams p, ObsArgs o, int lo, int hi, float* out);
+__global__ void k_msg_pack(KParams p, ObsArgs o, float* out);
 __global__ void k_greedy_keys(KParams p, double* key, int* idx);
 __global__ void k_greedy_gather(KParams p, const int* perm, double* psorted, uint8_t* lsorted);
 __global__ void k_greedy_walk(int64_t n, const double* incl, const double* psorted,
@@ -122,5 +124,9 @@ __global__ void k_greedy_walk(int64_t n, const double* incl, const double* psort
                               int64_t* extra, int max_extra);
 __global__ void k_greedy_apply(int64_t n, const int* perm, const int64_t* kpos, const int64_t* extra,
                                uint8_t* action);
+__global__ void k_greedy_inputs(KParams p, double* key, double* power, uint8_t* lock);
+__global__ void k_greedy_iota(int64_t n, int* idx);
+__global__ void k_greedy_gather_rows(int64_t n, const int* perm, const double* power, const uint8_t* lock,
+                                     double* psorted, uint8_t* lsorted);
 
 }  // namespace mdr

@@ -1330,6 +1330,15 @@ __global__ void k_halo_pack(KParams p, ObsArgs o, int lo, int hi, float* out) {
   }
 }
 
+// message features of every local house (sharded table comm modes: all-gathered into msg_all)
+__global__ void k_msg_pack(KParams p, ObsArgs o, float* out) {
+  __shared__ float cf[kObsConst];
+  obs_consts(p, o, o.p, cf, threadIdx.x, blockDim.x);  // (messages use only cf[8..] and P_max/R)
+  __syncthreads();
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < p.n) msg_features(p, o, i, cf, out + i * o.msg_w);
+}
+
 // --------------------------------------------------------------------------------------- greedy
 // GreedyMyopic.get_action (greedy_myopic_controller.py:67-104), device form:
 //   key_i = -(T_i - target_i), sorted ascending (stable radix sort; pandas' quicksort tie order
@@ -1408,6 +1417,32 @@ __global__ void __launch_bounds__(256) k_greedy_walk(int64_t n, const double* __
     pos += first + 1;
   }
   if (threadIdx.x == 0) { kpos[0] = s_k; kpos[1] = s_ne < max_extra ? s_ne : max_extra; }
+}
+
+// sharded greedy (mdr_greedy_inputs / mdr_greedy_select): this shard's (key, P, lockout) rows, and
+// the generic gather / iota for the cluster-wide selection over the gathered rows
+__global__ void k_greedy_inputs(KParams p, double* __restrict__ key, double* __restrict__ power,
+                                uint8_t* __restrict__ lock) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  key[i] = -(p.t_air[i] - p.target[i]);
+  power[i] = p.p_on[p.cap_idx[i]];
+  lock[i] = hv_lock(p.hvac[i]) ? 1 : 0;
+}
+
+__global__ void k_greedy_iota(int64_t n, int* __restrict__ idx) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) idx[i] = (int)i;
+}
+
+__global__ void k_greedy_gather_rows(int64_t n, const int* __restrict__ perm, const double* __restrict__ power,
+                                     const uint8_t* __restrict__ lock, double* __restrict__ psorted,
+                                     uint8_t* __restrict__ lsorted) {
+  const int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= n) return;
+  const int i = perm[j];
+  psorted[j] = power[i];
+  lsorted[j] = lock[i];
 }
 
 __global__ void k_greedy_apply(int64_t n, const int* __restrict__ perm, const int64_t* kpos,

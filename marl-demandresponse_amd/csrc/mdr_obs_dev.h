@@ -160,6 +160,10 @@ __device__ __forceinline__ void row_messages(const KParams& p, const ObsArgs& o,
     float tmp[16];
     for (int k = 0; k < K; ++k) {
       const int64_t j = o.comm_table[i * K + k];
+      if (o.msg_all) {  // sharded: the all-gathered rows, global ids
+        for (int m = 0; m < M; ++m) row[f++] = o.msg_all[j * M + m];
+        continue;
+      }
       msg_features(p, o, j, cf, tmp);
       for (int m = 0; m < M; ++m) row[f++] = tmp[m];
     }

@@ -69,7 +69,7 @@ class mdr_obs_spec(C.Structure):
         ("n_comm", C.c_int32), ("comm_mode", C.c_int32),
         ("comm_table", C.c_void_p), ("halo_msg", C.c_void_p),
         ("norm_reg_sig", C.c_double), ("cfg_ua", C.c_double), ("cfg_ca", C.c_double),
-        ("cfg_cm", C.c_double), ("cfg_hm", C.c_double), ("cfg_cap", C.c_double),
+        ("cfg_cm", C.c_double), ("cfg_hm", C.c_double), ("cfg_cap", C.c_double), ("msg_all", C.c_void_p),
     ]
 
 
@@ -125,7 +125,10 @@ SIGNATURES = {
     "mdr_msg_width": (I, [P(mdr_obs_spec)]),
     "mdr_obs": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, VP, VP]),
     "mdr_halo_pack": (I, [VP, P(mdr_obs_spec), VP, VP]),
+    "mdr_msg_pack": (I, [VP, P(mdr_obs_spec), VP, VP]),
     "mdr_ctrl_greedy": (I, [VP, D, VP, VP]),
+    "mdr_greedy_inputs": (I, [VP, VP, VP, VP, VP]),
+    "mdr_greedy_select": (I, [VP, I64, VP, VP, VP, D, VP, VP]),
     "mdr_cluster_stats": (I, [VP, VP, VP, VP]),
     "mdr_actor_load": (I, [VP, P(mdr_actor_spec), VP, VP, VP, VP, VP, VP, VP]),
     "mdr_actor_act": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, U64, VP, VP, VP, VP, I, VP]),

@@ -103,6 +103,17 @@ class RcclComm:
         # rows [hi, hi+lo) of a pack = that shard's last lo houses; rows [0, hi) = its first hi
         return torch.cat([prev[hi:hi + lo], nxt[:hi]]).contiguous()
 
+    def allgather_cat(self, shard, t, sizes):
+        """The ranks' 1-D device tensors (rank r holds sizes[r] elements) concatenated in rank
+        order = global house order (all_gather over rows padded to the largest shard)."""
+        import torch
+
+        m = max(sizes)
+        buf = t if t.numel() == m else torch.cat([t, t.new_zeros(m - t.numel())])
+        parts = [torch.empty_like(buf) for _ in range(self.world)]
+        self.dist.all_gather(parts, buf.contiguous())
+        return torch.cat([p[:s] for p, s in zip(parts, sizes)])
+
     def allgather_state(self, shard, st: dict, prm: dict, n: int):
         """Full-cluster host copies of the state/params (dict obs of a sharded env: messages
         reference houses on other shards)."""

@@ -608,11 +608,24 @@ class Environment:
         Returns a uint8 [n_local] device tensor (``out`` if given)."""
         import torch
 
-        if self.world > 1:
-            raise NotImplementedError("greedy over a sharded cluster (needs a global sort)")
         sh = self._shard
         if out is None:
             out = torch.empty(self._n_local, dtype=torch.uint8, device=sh.device)
+        if self.world > 1:
+            # the cluster-wide order needs every house: all-gather this shard's (key, P, lockout)
+            # rows in global order, the same selection on every rank, keep this shard's slice
+            # (SURVEY §8(e) item 4)
+            nl = self._n_local
+            key = torch.empty(nl, dtype=torch.float64, device=sh.device)
+            pw = torch.empty(nl, dtype=torch.float64, device=sh.device)
+            lk = torch.empty(nl, dtype=torch.uint8, device=sh.device)
+            sh.greedy_inputs(key, pw, lk)
+            sizes = [shard_range(self.n, r, self.world)[1] for r in range(self.world)]
+            rows = [self._comm.allgather_cat(sh, t, sizes) for t in (key, pw, lk)]
+            full = torch.empty(self.n, dtype=torch.uint8, device=sh.device)
+            sh.greedy_select(self.n, *rows, float(self.power_grid.current_signal), full)
+            out.copy_(full[self._offset:self._offset + nl])
+            return out
         sh.greedy(float(self.power_grid.current_signal), out)
         return out
 
@@ -664,9 +677,19 @@ class Environment:
         spec = self.obs_spec()
         keep = []
         if spec.comm_mode == L.COMM_TABLE and spec.n_comm > 0:
+            links = np.asarray(self._obs_links, np.int32)
             if self.world > 1:
-                raise NotImplementedError("non-ring comm modes are single-shard for the device obs")
-            tab = torch.from_numpy(np.ascontiguousarray(self._obs_links, np.int32)).to(sh.device)
+                # neighbours anywhere in the cluster: every shard's message rows, all-gathered in
+                # global order (mdr_msg_pack), indexed by the global ids of this shard's table rows
+                links = links[self._offset:self._offset + self._n_local]
+                m = sh.lib.mdr_msg_width(L.C.byref(spec))
+                mine = torch.empty((self._n_local, m), dtype=torch.float32, device=sh.device)
+                sh.msg_pack(spec, mine)
+                sizes = [shard_range(self.n, r, self.world)[1] * m for r in range(self.world)]
+                allm = self._comm.allgather_cat(sh, mine.reshape(-1), sizes)
+                keep.append(allm)
+                spec.msg_all = L.ptr(allm)
+            tab = torch.from_numpy(np.ascontiguousarray(links)).to(sh.device)
             keep.append(tab)
             spec.comm_table = L.ptr(tab)
         if spec.comm_mode == L.COMM_RING and self.world > 1 and spec.n_comm > 0:

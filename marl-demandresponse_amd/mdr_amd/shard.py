@@ -210,6 +210,20 @@ class HipShard:
         """out (device float64 [12]) <- mdr_cluster_stats of the current state (+ reward or None)."""
         L.check(self.lib.mdr_cluster_stats(self.ctx, L.ptr(reward), L.ptr(out), self.stream()), "mdr_cluster_stats")
 
+    def msg_pack(self, spec, out):
+        """Message features of every local house into out [n_local, msg_w] (mdr_msg_pack)."""
+        L.check(self.lib.mdr_msg_pack(self.ctx, C.byref(spec), L.ptr(out), self.stream()), "mdr_msg_pack")
+
+    def greedy_inputs(self, key, power, lock):
+        """This shard's greedy rows: key = -(T - target), P, lockout (mdr_greedy_inputs)."""
+        L.check(self.lib.mdr_greedy_inputs(self.ctx, L.ptr(key), L.ptr(power), L.ptr(lock), self.stream()),
+                "mdr_greedy_inputs")
+
+    def greedy_select(self, n: int, key, power, lock, budget: float, action):
+        """Greedy decisions over n gathered rows (mdr_greedy_select)."""
+        L.check(self.lib.mdr_greedy_select(self.ctx, int(n), L.ptr(key), L.ptr(power), L.ptr(lock), float(budget),
+                                           L.ptr(action), self.stream()), "mdr_greedy_select")
+
     def greedy(self, budget: float, action):
         L.check(self.lib.mdr_ctrl_greedy(self.ctx, float(budget), L.ptr(action), self.stream()),
                 "mdr_ctrl_greedy")

@@ -140,6 +140,23 @@ class OracleShard:
             b += v
         out[0] = b * factor
 
+    def greedy_inputs(self, key, power, lock):
+        _, lk, _ = decode_hvac(self.hvac.numpy().copy())
+        key.copy_(-(self.t_air - self.target))
+        power.copy_(torch.from_numpy(self._caps() / self.props.cluster_prop.house_prop.hvac_prop.cop))
+        lock.copy_(torch.from_numpy(np.asarray(lk, np.uint8)))
+
+    def greedy_select(self, n, key, power, lock, budget, action):
+        """O.greedy's rule over the gathered rows (stable order)."""
+        k, p, lk = key.numpy(), power.numpy(), lock.numpy().astype(bool)
+        act = np.zeros(int(n), np.uint8)
+        tot = 0
+        for i in np.argsort(k, kind="stable"):
+            if p[i] + tot < budget or abs(p[i] + tot - budget) < abs(tot - budget) and not lk[i]:
+                tot += p[i]
+                act[i] = 1
+        action.copy_(torch.from_numpy(act))
+
     def host_state(self):
         on, lock, sso = decode_hvac(self.hvac.numpy().copy())
         return {"T": self.t_air.numpy().copy(), "Tm": self.t_mass.numpy().copy(), "on": on,
@@ -174,6 +191,13 @@ class GlooComm:
 
     def allreduce_max(self, shard, t):
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+
+    def allgather_cat(self, shard, t, sizes):
+        m = max(sizes)
+        buf = t if t.numel() == m else torch.cat([t, t.new_zeros(m - t.numel())])
+        parts = [torch.empty_like(buf) for _ in range(self.world)]
+        self.dist.all_gather(parts, buf.contiguous())
+        return torch.cat([p[:s] for p, s in zip(parts, sizes)])
 
     def allgather_state(self, shard, st, prm, n):
         out_st, out_prm = {}, {}

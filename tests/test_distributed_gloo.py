@@ -95,3 +95,48 @@ def test_sharded_env_equals_oracle(tmp_path, mode, n, extra):
     links = O.comm_links(props.cluster_prop, random)
     ref = np.array([[ora.T[j] - ora.pop["target"][j] for j in row] for row in links])
     np.testing.assert_array_equal(msgs, ref)
+
+
+def _greedy_worker(rank, world, port, overrides, seed, T, out_dir):
+    import torch.distributed as dist
+
+    sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "marl-demandresponse_amd"), os.path.dirname(HERE)]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import golden_util as g
+    from oracle_shard import GlooComm, OracleShard
+
+    from mdr_amd.environment import Environment
+
+    env = Environment(g.props_from_overrides(overrides), rng=random.Random(seed), rank=rank, world=world,
+                      comm=GlooComm(), _shard_factory=OracleShard)
+    acts, Ts = [], []
+    for _ in range(T):
+        a = env.greedy_actions()
+        acts.append(a.numpy().copy())
+        env.step_tensor(a)
+        Ts.append(env.shard.host_state()["T"])
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), lo=env._offset, acts=np.array(acts), T=np.array(Ts))
+    dist.destroy_process_group()
+
+
+def test_sharded_greedy_equals_oracle(tmp_path):
+    """Sharded GreedyMyopic (all-gather of the shards' key / P / lockout rows, the same selection
+    on every rank, each keeps its slice) == the single-process oracle's greedy + step."""
+    world, T, seed, n = 2, 6, 9, 75
+    overrides = {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals"}
+    mp.start_processes(_greedy_worker, args=(world, _free_port(), overrides, seed, T, str(tmp_path)),
+                       nprocs=world, join=True, start_method="spawn")
+    parts = sorted((np.load(tmp_path / f"rank{r}.npz") for r in range(world)), key=lambda p: int(p["lo"]))
+    props = gu.props_from_overrides(overrides)
+    ora = O.OracleEnv(props, random.Random(seed))
+    hv = props.cluster_prop.house_prop.hvac_prop
+    caps = np.asarray(ora.pop["cap"], np.float64)
+    for t in range(T):
+        ref = O.greedy(ora.T, ora.pop["target"], caps, hv.cop, ora.lock, float(ora.S))
+        got = np.concatenate([p["acts"][t] for p in parts]).astype(bool)
+        np.testing.assert_array_equal(got, ref, err_msg=f"t={t}")
+        assert 0 < got.sum() < n or t > 0
+        o, _ = ora.step(ref)
+        np.testing.assert_array_equal(np.concatenate([p["T"][t] for p in parts]), o["T"])

@@ -26,7 +26,7 @@ import golden_util as gu
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-T_STEP, T_BUF, T_ROLL = 5, 3, 70  # >= 16 ticks trigger the per-tick pipeline calibration; 3 windows
+T_STEP, T_BUF, T_GREEDY, T_ROLL = 5, 3, 2, 70  # >= 16 ticks trigger the per-tick pipeline calibration; 3 windows
 
 
 INTERP = "interp"  # mode suffix: interpolation base power (row a10), re-estimated every 3 ticks
@@ -39,11 +39,13 @@ def _overrides(n, mode):
     if extra == INTERP:
         o.update({gu.BPP + "mode": "interpolation", gu.BPP + "interp_update_period": 12,
                   gu.BPP + "interp_nb_agents": 200})
+    elif extra in ("closed_groups", "random_fixed"):  # table comm modes (sharded: all-gathered messages)
+        o["cluster_prop.agents_comm_prop.mode"] = extra
     return o
 
 
 def _run(env, n_total, torch, dev):
-    """Fixed tick script: fused random steps, buffer steps, a rollout (individual_L2 only)."""
+    """Fixed tick script: fused random steps, buffer steps, greedy steps, a rollout (individual_L2 only)."""
     lo, nl = env._offset, env.n_local
     rewards = []
     for _ in range(T_STEP):
@@ -51,6 +53,8 @@ def _run(env, n_total, torch, dev):
     for t in range(T_BUF):
         a = np.random.RandomState(100 + t).randint(0, 2, n_total).astype(np.uint8)[lo:lo + nl]
         rewards.append(env.step_tensor(torch.from_numpy(a).to(dev)).cpu().numpy().copy())
+    for t in range(T_GREEDY):  # GreedyMyopic over the whole cluster (sharded: all-gathered rows)
+        rewards.append(env.step_tensor(env.greedy_actions()).cpu().numpy().copy())
     if env.shard.penalty_mode == 0:
         r = env.rollout(T_ROLL, action_mode="random")
         rewards.extend(r.cpu().numpy().copy())
@@ -111,6 +115,8 @@ def _free_port():
     ("gloo", "torch", 2, 2048, "common_L2"),
     ("nccl", "rccl", 1, 3001, "individual_L2+interp"),
     ("gloo", "torch", 2, 3001, "individual_L2+interp"),
+    ("gloo", "torch", 2, 2992, "individual_L2+closed_groups"),
+    ("gloo", "torch", 2, 3001, "common_L2+random_fixed"),
 ])
 def test_sharded_equals_single(tmp_path, backend, kind, world, n, mode):
     import torch
