@@ -95,6 +95,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--trace", action="store_true",
                     help="print host phase timestamps of the timed region to stderr (diagnostics)")
+    ap.add_argument("--graph", default="on", choices=["on", "off"],
+                    help="off: rollout calls as direct kernel launches (no hipGraph)")
     ap.add_argument("--mode", default="random", choices=["random", "buffer"])
     ap.add_argument("--workload", default="step", choices=["step", "actor", "greedy"],
                     help="step: env.step with fused random actions (the BASELINE metric); actor: "
@@ -305,6 +307,8 @@ def main():
             raise SystemExit("--workload greedy runs on one GPU (config C3)")
         g_act = torch.empty(n_loc, dtype=torch.uint8, device=dev)
 
+    use_graph = args.graph == "on"
+
     def run(n):
         if dactor is not None:
             dactor.rollout(n, rewards=rew[:n])
@@ -314,7 +318,7 @@ def main():
                 env.step_tensor(g_act, rewards=rew[t])
         else:  # (whole buffers when the chunk fills them: no tensor views built per call)
             env.rollout(n, actions=None if acts is None else (acts if n == chunk else acts[:n]),
-                        action_mode=args.mode, rewards=rew if n == chunk else rew[:n])
+                        action_mode=args.mode, rewards=rew if n == chunk else rew[:n], use_graph=use_graph)
 
     # warmup: captures the graphs of every chunk size used below
     done = 0
@@ -346,7 +350,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     # HIP events on the stream the step launches are issued on (the graph side stream)
-    launch_stream = env.rollout_stream(use_graph=g_act is None)
+    launch_stream = env.rollout_stream(use_graph=g_act is None and use_graph)
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for ev in (ev0, ev1):  # torch creates the HIP event on its first record(): not inside the timed region
         ev.record(launch_stream)

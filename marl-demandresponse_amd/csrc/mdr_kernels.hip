@@ -954,7 +954,16 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
           const double tpen = p.alpha_temp * pen;
           r = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + -nsig);
         }
-        if (t.v[h]) *reinterpret_cast<double*>(rrow + (rb + 512u * h)) = r;
+        if (t.v[h]) {
+#ifdef MDR_REWARD_WT
+          // write-through (sc1) store: the row leaves the XCD's L2 at once, so the launch ends with
+          // no dirty reward lines to write back at the kernel boundary
+          __hip_atomic_store(reinterpret_cast<unsigned long long*>(rrow + (rb + 512u * h)),
+                             (unsigned long long)__double_as_longlong(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#else
+          *reinterpret_cast<double*>(rrow + (rb + 512u * h)) = r;
+#endif
+        }
       }
     };
     if (fast) houses(std::true_type());
