@@ -45,8 +45,10 @@ BF16_PEAK_TFS = 2516.6     # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 
 def step_kernel_name(n_loc: int, mode: str, window: int, simple: bool = True) -> str:
     """The step kernel the library launches for this bench (mdr_capi.hip: window_launches /
     launch_step_on)."""
-    if window > 0:  # the rocprofv3 spelling: k_step_window<ACT, HPT=2, SIMPLE> (MDR_ACT_RANDOM = 1, _BUFFER = 0)
-        return f"void mdr::k_step_window<{1 if mode == 'random' else 0}, 2, {'true' if simple else 'false'}>"
+    if window > 0:  # the rocprofv3 spelling: k_step_window<ACT, HPT=2, SIMPLE, KA> (MDR_ACT_RANDOM = 1, _BUFFER
+        # = 0; KA: the first window of a direct rollout call, drivers as kernel arguments — the
+        # kernel-only timing below launches the KA = false instantiation, the same thermal loop)
+        return f"void mdr::k_step_window<{1 if mode == 'random' else 0}, 2, {'true' if simple else 'false'}, false>"
     if any(k in os.environ for k in ("MDR_HPT", "MDR_VARIANT", "MDR_FASTDIV")):
         return "mdr::k_step (variant chosen by MDR_* env)"
     tpw = int(os.environ.get("MDR_TPW", 2 if n_loc <= 1572864 else 4))
@@ -95,8 +97,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--trace", action="store_true",
                     help="print host phase timestamps of the timed region to stderr (diagnostics)")
-    ap.add_argument("--graph", default="on", choices=["on", "off"],
-                    help="off: rollout calls as direct kernel launches (no hipGraph)")
+    ap.add_argument("--graph", default="default", choices=["default", "on", "off"],
+                    help="rollout launch policy: default = Environment.rollout's (direct launches), on = "
+                         "hipGraph launch-first sequences, off = direct launches")
     ap.add_argument("--mode", default="random", choices=["random", "buffer"])
     ap.add_argument("--workload", default="step", choices=["step", "actor", "greedy"],
                     help="step: env.step with fused random actions (the BASELINE metric); actor: "
@@ -307,7 +310,7 @@ def main():
             raise SystemExit("--workload greedy runs on one GPU (config C3)")
         g_act = torch.empty(n_loc, dtype=torch.uint8, device=dev)
 
-    use_graph = args.graph == "on"
+    use_graph = {"default": None, "on": True, "off": False}[args.graph]
 
     def run(n):
         if dactor is not None:
@@ -350,7 +353,7 @@ def main():
     barrier()
     torch.cuda.synchronize()
     # HIP events on the stream the step launches are issued on (the graph side stream)
-    launch_stream = env.rollout_stream(use_graph=g_act is None and use_graph)
+    launch_stream = env.rollout_stream()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for ev in (ev0, ev1):  # torch creates the HIP event on its first record(): not inside the timed region
         ev.record(launch_stream)

@@ -132,12 +132,14 @@ struct mdr_ctx {
     uint64_t tick0 = 0;
     const uint8_t* action = nullptr;
     int64_t act_stride = 0;
+    bool ka = false;                     // its P-only reduce ran too: the step takes the drivers as arguments
   } begun;
   // launch-first rollouts (mdr_rollout_launch): the graph runs ahead of the host's tick drivers
   uint64_t* d_lf = nullptr;              // device: [0] seq of the last k_lf_wait, [1] next rollout's tick id, [2] abort (int)
   TickArgs* h_lf_ring = nullptr;         // pinned: 2 slots x kLfCap tick records
   uint64_t* h_lf_ctl = nullptr;          // pinned: [0] posted seq, [1] acked seq | abort << 62, [2] cancelled seq
   uint64_t lf_seq = 0;                   // launch-first graphs launched (= the device's [0] once they ran)
+  bool lf_disabled = false;              // a direct launch-first sequence failed part-way: begin path only
   uint64_t lf_timeout = 0;               // k_lf_wait's bound, wall-clock ticks
   uint64_t lf_timeouts_seen = 0;
   bool next_tick_known = false;          // d_lf[1] as written by the last rollout graph
@@ -657,6 +659,13 @@ static int step_mark(mdr_ctx* c, hipStream_t st) {
   return MDR_OK;
 }
 
+// SIMPLE = deadband 0, norm_temp 1, and reward weights whose signal / temperature penalties are
+// >= +0 (k_step_window forms -(a + s) as (-a) + (-s), exact for such operands)
+static bool win_simple(const mdr_ctx* c) {
+  return c->kp.deadband == 0.0 && c->kp.norm_temp == 1.0 && c->kp.alpha_temp >= 0.0 && !std::signbit(c->kp.alpha_temp) &&
+         c->kp.alpha_sig >= 0.0 && !std::signbit(c->kp.alpha_sig) && c->kp.norm_sig > 0.0;
+}
+
 // (the lookahead's FSM runs on unsaturated seconds-since-off: L <= 2^30 - 1 and 33 ticks of dt
 // from a saturated value stay below 2^32 — mdr_kernels.hip win_run)
 static bool window_ok(const mdr_ctx* c, int mode) {
@@ -687,9 +696,17 @@ static int wslab_clean(mdr_ctx* c, hipStream_t st) {
 // the allreduce of its counts run on the comm stream, up to two windows ahead of the compute
 // stream's reduce + step (which then has no lookahead): the allreduce latency hides behind the
 // step kernels.  Two sets of ON-mask / end-word buffers alternate; events order the reuse.
+//
+// host_ticks (direct launches, mdr_rollout with use_graph = 0): the drivers are still in host
+// memory; the first reduce carries the first kStageRecs of them as kernel arguments and stages
+// them into tk (k_win_reduce_staged), the rest are staged behind the first step kernel (their
+// first reader is the second step kernel's lookahead), so no staging launch sits in front of the
+// first window.  Tick ids are consecutive (the caller checked), so the first count needs only
+// host_ticks[0].tick.
 static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t* action, int64_t act_stride,
                            int mode, double* reward, int64_t rew_stride, double* p_out, ncclComm_t comm,
-                           hipStream_t st, bool counted = false, bool lf = false, bool pipe = false) {
+                           hipStream_t st, bool counted = false, bool lf = false, bool pipe = false,
+                           const mdr_tick* host_ticks = nullptr, bool ka = false) {
   const int nw = (n + c->win - 1) / c->win;
   const int base = n / nw, rem = n % nw;
   auto wsz = [&](int w) { return base + (w < rem ? 1 : 0); };
@@ -726,11 +743,7 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     else if (mode == MDR_ACT_ALWAYS_ON) MDR_STEP_LAUNCH((k_step_window<MDR_ACT_ALWAYS_ON, H, DB>), __VA_ARGS__); \
     else MDR_STEP_LAUNCH((k_step_window<MDR_ACT_BUFFER, H, DB>), __VA_ARGS__);                              \
   } while (0)
-  // SIMPLE = deadband 0, norm_temp 1, and reward weights whose signal / temperature penalties are
-  // >= +0 (k_step_window forms -(a + s) as (-a) + (-s), exact for such operands)
-  const bool db0 = c->kp.deadband == 0.0 && c->kp.norm_temp == 1.0 && c->kp.alpha_temp >= 0.0 &&
-                   !std::signbit(c->kp.alpha_temp) && c->kp.alpha_sig >= 0.0 && !std::signbit(c->kp.alpha_sig) &&
-                   c->kp.norm_sig > 0.0;
+  const bool db0 = win_simple(c);
 #define MDR_STEP_WIN_DISPATCH(...)                                         \
   do {                                                                    \
     if (hpt == 1) { if (db0) MDR_WIN_DISPATCH_S(1, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(1, false, __VA_ARGS__); } \
@@ -775,7 +788,7 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
       LAUNCH_CHECK("k_win_reduce");
       const int* no_abort = nullptr;
       MDR_STEP_WIN_DISPATCH(kp, a, act_stride, tk + t0, K, 0, rec(w), reward + (int64_t)t0 * rew_stride, rew_stride,
-                            onbs[w % 2], wahs[w % 2], slot(w), no_abort);
+                            onbs[w % 2], wahs[w % 2], slot(w), no_abort, WinDrv{});
       LAUNCH_CHECK("k_step_window");
       HIP_TRY(hipEventRecord(c->ev_k1[w % kSlabs], st));
       t0 += K;
@@ -792,7 +805,8 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
                        reinterpret_cast<int*>(c->d_lf + 2), n, const_cast<TickArgs*>(tk), c->lf_timeout);
     LAUNCH_CHECK("k_lf_wait");
   } else if (!counted) {  // (counted: mdr_rollout_begin launched it already)
-    MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, tk, (uint64_t)0, (const uint64_t*)nullptr, wsz(0),
+    MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, host_ticks ? (const TickArgs*)nullptr : tk,
+                     host_ticks ? host_ticks[0].tick : (uint64_t)0, (const uint64_t*)nullptr, wsz(0),
                      slot(0), c->d_onb, c->d_wah, (const uint32_t*)nullptr);
     LAUNCH_CHECK("k_count_window");
   }
@@ -804,9 +818,49 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     // slot's shard part, K x 64 x n_cap values), so one reduce kernel yields the global counts
     if (comm)
       RCCL_TRY(ncclAllReduce(slot(w), slot(w), (size_t)K * kCountShards * ncap, ncclUint64, ncclSum, comm, st));
-    hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0, po, abort,
-                       w == nw - 1 ? c->d_lf + 1 : nullptr);
-    LAUNCH_CHECK("k_win_reduce");
+    if (ka && w == 0) {
+      // the P-only reduce of this window ran in mdr_rollout_begin; the drivers ride on the step
+      // launch (k_step_window<..., KA>); the later windows' drivers are staged behind it
+      WinDrv dv{};
+      for (int j = 0; j < K; ++j) {
+        const mdr_tick& h = host_ticks[j];
+        dv.od_k[j] = h.t_od_prev + 273.0;  // (k_win_reduce's rec[0]: the same IEEE addition)
+        dv.solar[j] = h.solar;
+        dv.s_prev[j] = h.s_prev;
+        if (fabs(h.t_od_prev) < 1048576.0 && fabs(h.solar) < 1099511627776.0) dv.ok |= 1u << j;  // (win_tick_record)
+      }
+      dv.tick0 = host_ticks[0].tick;
+      if (nw == 1) {
+        dv.p_out = p_out;
+        dv.next_tick = c->d_lf + 1;
+      }
+      const uint8_t* a = action;
+#define MDR_KA_LAUNCH(A)                                                                                        \
+  hipLaunchKernelGGL((k_step_window<A, 2, true, true>), dim3(grid), dim3(256), 0, st, kp, a, act_stride, tk, K, la, \
+                     rec(0), reward, rew_stride, c->d_onb, c->d_wah, slot(1), (const int*)nullptr, dv)
+      if (mode == MDR_ACT_RANDOM) MDR_KA_LAUNCH(MDR_ACT_RANDOM);
+      else if (mode == MDR_ACT_ALWAYS_ON) MDR_KA_LAUNCH(MDR_ACT_ALWAYS_ON);
+      else MDR_KA_LAUNCH(MDR_ACT_BUFFER);
+#undef MDR_KA_LAUNCH
+      LAUNCH_CHECK("k_step_window<KA>");
+      if (n > K) {
+        if (int rc = stage_recs(host_ticks + K, n - K, const_cast<TickArgs*>(tk) + K, st)) return rc;
+      }
+      t0 += K;
+      continue;
+    }
+    if (host_ticks && w == 0) {
+      StagePack pk;
+      const int m = n < kStageRecs ? n : kStageRecs;
+      memcpy(pk.r, host_ticks, (size_t)m * sizeof(Rec32));
+      hipLaunchKernelGGL(k_win_reduce_staged, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, pk, m,
+                         const_cast<TickArgs*>(tk), po, w == nw - 1 ? c->d_lf + 1 : nullptr);
+      LAUNCH_CHECK("k_win_reduce_staged");
+    } else {
+      hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0, po, abort,
+                         w == nw - 1 ? c->d_lf + 1 : nullptr);
+      LAUNCH_CHECK("k_win_reduce");
+    }
     const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
     if (c->step_events) {
       HIP_TRY(hipEventCreate(&t_start));
@@ -815,8 +869,12 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
       c->step_events->push_back(t_stop);
     }
     MDR_STEP_WIN_DISPATCH(kp, a, act_stride, tk + t0, K, la, rec(w), reward + (int64_t)t0 * rew_stride, rew_stride,
-                          c->d_onb, c->d_wah, slot(w + 1), abort);
+                          c->d_onb, c->d_wah, slot(w + 1), abort, WinDrv{});
     LAUNCH_CHECK("k_step_window");
+    if (host_ticks && w == 0 && n > kStageRecs) {  // (K + la <= 2 * kWindowMax = kStageRecs were staged)
+      if (int rc = stage_recs(host_ticks + kStageRecs, n - kStageRecs, const_cast<TickArgs*>(tk) + kStageRecs, st))
+        return rc;
+    }
     t0 += K;
   }
   c->wslab_dirty = false;
@@ -936,15 +994,35 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   const bool counted = c->begun.on && c->begun.n == n && c->begun.mode == mode && c->begun.tick0 == ticks[0].tick &&
                        c->begun.action == action && c->begun.act_stride == act_stride && window_ok(c, mode);
   if (c->begun.on && !counted) c->wslab_dirty = true;  // an unmatched early count: clear its shards
+  const bool ka = counted && c->begun.ka;
   c->begun.on = false;
   int rc = refresh_if_dirty(c, st);
   if (rc) return rc;
+  static const bool pipe_single = getenv("MDR_PIPE_SINGLE") != nullptr;  // A/B: count-ahead pipeline, 1 GPU
+  // (ka: the P-only reduce already consumed the first window's shards, so only the direct KA
+  // sequence can follow it, whatever use_graph asks)
+  if (ka || (!use_graph && !pipe_single && window_ok(c, mode))) {
+    // direct launches of the windowed path: the drivers travel as kernel arguments of the first
+    // reduce (window_launches host_ticks); needs consecutive tick ids (as driver_window makes them)
+    bool consec = true;
+    for (int i = 1; i < n && consec; ++i) consec = ticks[i].tick == ticks[0].tick + (uint64_t)i;
+    if (consec || ka) {  // (ka: mdr_rollout_begin checked the window's ids against tick0: consecutive by construction)
+      rc = ensure_ticks(c, n);
+      if (!rc) rc = wslab_clean(c, st);
+      if (!rc)
+        rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st,
+                             counted, false, false, ticks, ka);
+      c->counts_ready = false;
+      c->next_tick_known = !rc;
+      c->next_tick = ticks[n - 1].tick + 1;
+      return rc;
+    }
+  }
   rc = stage_ticks(c, n, ticks, st);
   if (rc) return rc;
   rc = wslab_clean(c, st);
   if (rc) return rc;
   const auto t1 = std::chrono::steady_clock::now();
-  static const bool pipe_single = getenv("MDR_PIPE_SINGLE") != nullptr;  // A/B: count-ahead pipeline, 1 GPU
   if (pipe_single && window_ok(c, mode) && !counted) {
     if (!c->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
     if (pipe_buffers(c)) {
@@ -1026,7 +1104,16 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   }
 #undef MDR_BEGIN_COUNT
   LAUNCH_CHECK("k_count_window");
+  // the window's P (the counts need no drivers): the matching direct mdr_rollout then launches the
+  // step kernel with the drivers as arguments (k_step_window<..., KA>), nothing in between
+  const bool ka = c->win_hpt == 2 && win_simple(c) && !getenv("MDR_NO_KA");
+  if (ka) {
+    hipLaunchKernelGGL(k_win_reduce, dim3(k0), dim3(64 * c->kp.n_cap), 0, st, c->kp, c->d_wslab, k0,
+                       (const TickArgs*)nullptr, (double*)nullptr, (const int*)nullptr, (uint64_t*)nullptr);
+    LAUNCH_CHECK("k_win_reduce (P only)");
+  }
   c->wslab_dirty = false;
+  c->begun.ka = ka;
   c->begun.on = true;
   c->begun.n = n; c->begun.mode = mode; c->begun.tick0 = tick0;
   c->begun.action = action; c->begun.act_stride = act_stride;
@@ -1049,26 +1136,47 @@ int mdr_rollout_launch(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action,
   if (int rc = lf_check(c)) return rc;
   const bool ok = c->h_lf_ring && window_ok(c, mode) && n <= kLfCap && c->kp.penalty_mode == MDR_PEN_INDIVIDUAL_L2 &&
                   (mode != MDR_ACT_RANDOM || (c->next_tick_known && c->next_tick == tick0)) &&
-                  !getenv("MDR_NO_LAUNCH_FIRST");
+                  !c->lf_disabled && !getenv("MDR_NO_LAUNCH_FIRST");
   if (!ok) return mdr_rollout_begin(c, n, tick0, action, act_stride, mode, stream);
   hipStream_t st = S(stream);
   int rc = refresh_if_dirty(c, st);
   if (!rc) rc = wslab_clean(c, st);
   if (!rc) rc = ensure_ticks(c, n);
   if (rc) return rc;
-  GraphKey key{n, mode + 2000, action, act_stride, reward, rew_stride, p_out, nullptr};
-  auto it = c->graphs.find(key);
-  if (it == c->graphs.end()) {
-    hipGraphExec_t ex;
-    rc = capture_graph(c, [&](hipStream_t cs) {
-      return rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, cs, false, true);
-    }, &ex);
-    if (rc) return rc;
-    it = c->graphs.emplace(key, std::make_pair(ex, c->ring)).first;
-  }
-  if (hipGraphLaunch(it->second.first, st) != hipSuccess) {
-    c->wslab_dirty = true;
-    return fail(MDR_EHIP, "mdr_rollout_launch: hipGraphLaunch");
+  int ring_end = c->ring;
+  if (!getenv("MDR_LF_GRAPH")) {
+    // direct launches (the default: measured faster than a graph replay, whose host call costs
+    // 10-15 us before the device starts): count, wait, then the windows, issued one by one
+    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st, false, true);
+    if (rc) {
+      // a sequence that failed part-way may or may not have queued its k_lf_wait: cancel it (it
+      // aborts if it runs) and stop using launch-first on this context, whose device-side sequence
+      // number can no longer be trusted to match the host's
+      c->lf_seq += 1;
+      c->lf.on = true;
+      c->lf.seq = c->lf_seq;
+      lf_cancel(c);
+      c->lf_disabled = true;
+      c->next_tick_known = false;
+      return rc;
+    }
+    ring_end = c->ring;
+  } else {
+    GraphKey key{n, mode + 2000, action, act_stride, reward, rew_stride, p_out, nullptr};
+    auto it = c->graphs.find(key);
+    if (it == c->graphs.end()) {
+      hipGraphExec_t ex;
+      rc = capture_graph(c, [&](hipStream_t cs) {
+        return rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, cs, false, true);
+      }, &ex);
+      if (rc) return rc;
+      it = c->graphs.emplace(key, std::make_pair(ex, c->ring)).first;
+    }
+    if (hipGraphLaunch(it->second.first, st) != hipSuccess) {
+      c->wslab_dirty = true;
+      return fail(MDR_EHIP, "mdr_rollout_launch: hipGraphLaunch");
+    }
+    ring_end = it->second.second;
   }
   c->lf_seq += 1;
   c->lf.on = true;
@@ -1076,7 +1184,7 @@ int mdr_rollout_launch(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action,
   c->lf.tick0 = tick0;
   c->lf.n = n;
   c->lf.mode = mode;
-  c->lf.ring_end = it->second.second;
+  c->lf.ring_end = ring_end;
   c->lf.action = action;
   c->lf.act_stride = act_stride;
   c->lf.reward = reward;

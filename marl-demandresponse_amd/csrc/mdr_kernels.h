@@ -88,12 +88,26 @@ constexpr int kPipeMaxCap = 4;
 constexpr int kWindowMax = 32;  // = kWinMax: ticks per k_step_window launch
 constexpr int kWindowCap = 4;   // = kWinCap: capacity classes the window kernel supports
 constexpr int kWindowRec = 4;   // = kWinRec: doubles per tick record of a window count slot
-template <int ACT, int HPT, bool SIMPLE>  // SIMPLE: deadband 0 and norm_temp 1 (reward without branches / division)
+// The first window's drivers as kernel arguments (k_step_window<..., KA = true>): the host computes
+// them while the window's count and P-only reduce already run, and launches the step kernel with
+// them, so no reduce or staging launch sits between the host's drivers and the thermal loop.
+struct WinDrv {
+  double od_k[kWindowMax];    // t_od_prev + 273.0 (rc_apply's od_k: the same IEEE addition on the host)
+  double solar[kWindowMax];
+  double s_prev[kWindowMax];  // the signal the tick's reward compares P with
+  uint64_t tick0;             // the window's first tick id (ids are consecutive)
+  double* p_out;              // last window: <- P of its last tick
+  uint64_t* next_tick;        // last window: <- the tick id the next rollout starts at
+  uint32_t ok;                // bit j: tick j's drivers are in the fast-division ranges
+};
+template <int ACT, int HPT, bool SIMPLE, bool KA = false>  // SIMPLE: deadband 0 and norm_temp 1 (reward without branches / division)
 __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int K,
                               int la_K, const double* rec, double* reward, int64_t rew_stride, uint64_t* onb,
-                              uint32_t* wah, unsigned long long* next_slot, const int* abort);
+                              uint32_t* wah, unsigned long long* next_slot, const int* abort, WinDrv dv);
 __global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out,
                              const int* abort, uint64_t* next_tick);
+__global__ void k_win_reduce_staged(KParams p, unsigned long long* slot, int nt, StagePack pk, int n_pk,
+                                    TickArgs* dst, double* p_out, uint64_t* next_tick);
 template <int ACT, int HPT>
 __global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp,
                                uint64_t tick0, const uint64_t* tick0p, int nt, unsigned long long* slot,

@@ -601,34 +601,44 @@ __device__ __forceinline__ double* win_rec(unsigned long long* slot, int n_cap) 
 // tick record j from the tick's global class counts (rewards_calculator.py:183-203 signal part;
 // the operations and order of the one-tick kernels); rec[2] is the NEGATED signal penalty (an exact
 // negation: the reward is then formed without a sign flip, k_step_window)
-__device__ __forceinline__ void win_tick_record(const KParams& p, const unsigned long long* cnt, const TickArgs& tk,
-                                                const double* p_on, double* rec, double* p_out) {
+// P = sum over classes of count * p_on, in the one-tick kernels' order (cluster.py:73-89)
+__device__ __forceinline__ double win_power(const KParams& p, const unsigned long long* cnt, const double* p_on) {
   double P = 0.0;
 #pragma unroll
   for (int k = 0; k < kWinCap; ++k)
     if (k < p.n_cap) P += (double)cnt[k] * p_on[k];
-  const double x = (P - tk.s_prev) / (double)p.n_global;
+  return P;
+}
+
+// the negated signal penalty of a tick with cluster power P (rewards_calculator.py:183-203)
+__device__ __forceinline__ double win_nsig(const KParams& p, double P, double s_prev) {
+  const double x = (P - s_prev) / (double)p.n_global;
+  return -(p.alpha_sig * (x * x) / p.norm_sig);
+}
+
+__device__ __forceinline__ void win_tick_record(const KParams& p, const unsigned long long* cnt, const TickArgs& tk,
+                                                const double* p_on, double* rec, double* p_out) {
+  const double P = win_power(p, cnt, p_on);
   rec[0] = tk.t_od_prev + 273.0;  // rc_apply's od_k
   rec[1] = tk.solar;
-  rec[2] = -(p.alpha_sig * (x * x) / p.norm_sig);
+  rec[2] = win_nsig(p, P, tk.s_prev);
   rec[3] = fabs(tk.t_od_prev) < 1048576.0 && fabs(tk.solar) < 1099511627776.0 ? 1.0 : 0.0;  // fast-division ranges
   if (p_out) *p_out = P;
 }
 
 // one block per tick j, one wave per class: sum the 64 shards (sharded rollouts: already summed
-// over ranks by the allreduce), zero them, and write the tick record
-__global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long long* __restrict__ slot, int nt,
-                                                    const TickArgs* __restrict__ tkp, double* p_out,
-                                                    const int* __restrict__ abort, uint64_t* __restrict__ next_tick) {
+// over ranks by the allreduce), zero them, and write the tick record.  tk_j: the tick's drivers,
+// read by thread 0 only (win_reduce_body is shared by the two reduce kernels below)
+__device__ __forceinline__ void win_reduce_body(const KParams& p, unsigned long long* __restrict__ slot, int nt,
+                                                const TickArgs* tk_j, double* p_out, uint64_t* next_tick) {
   __shared__ unsigned long long s_red[kWinCap];
-  if (abort && *abort) return;  // a cancelled launch-first rollout (k_lf_wait)
   const int j = blockIdx.x, c = threadIdx.x >> 6, q = threadIdx.x & 63, ncap = p.n_cap;
   // the record's other inputs are loaded by thread 0 while the shards are read (one memory
   // round trip instead of three dependent ones)
   TickArgs tk{};
   double p_on[kWinCap];
   if (threadIdx.x == 0) {
-    tk = tkp[j];
+    if (tk_j) tk = *tk_j;
 #pragma unroll
     for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < ncap ? k : 0];
   }
@@ -646,9 +656,32 @@ __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long lon
   }
   __syncthreads();
   if (threadIdx.x == 0) {
-    win_tick_record(p, s_red, tk, p_on, win_rec(slot, ncap) + j * kWinRec, j == nt - 1 ? p_out : nullptr);
-    if (next_tick && j == nt - 1) *next_tick = tk.tick + 1;  // the tick id the next rollout starts at
+    if (tk_j) {
+      win_tick_record(p, s_red, tk, p_on, win_rec(slot, ncap) + j * kWinRec, j == nt - 1 ? p_out : nullptr);
+      if (next_tick && j == nt - 1) *next_tick = tk.tick + 1;  // the tick id the next rollout starts at
+    } else {  // P only (the drivers come later, as kernel arguments of k_step_window<..., KA>)
+      win_rec(slot, ncap)[j * kWinRec] = win_power(p, s_red, p_on);
+    }
   }
+}
+
+__global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long long* __restrict__ slot, int nt,
+                                                    const TickArgs* __restrict__ tkp, double* p_out,
+                                                    const int* __restrict__ abort, uint64_t* __restrict__ next_tick) {
+  if (abort && *abort) return;  // a cancelled launch-first rollout (k_lf_wait)
+  win_reduce_body(p, slot, nt, tkp ? tkp + blockIdx.x : nullptr, p_out, next_tick);
+}
+
+// The first window's reduce of a directly launched rollout, with the drivers of its first n_pk
+// ticks (this window's and the next one's) as kernel arguments: no separate staging launch in
+// front of it.  Block 0 also stages those records into dst (the device tick array that the step
+// kernel's lookahead and the next window's reduce read).
+__global__ void __launch_bounds__(256) k_win_reduce_staged(KParams p, unsigned long long* __restrict__ slot, int nt,
+                                                           StagePack pk, int n_pk, TickArgs* __restrict__ dst,
+                                                           double* p_out, uint64_t* __restrict__ next_tick) {
+  if (blockIdx.x == 0 && (int)threadIdx.x < n_pk)
+    reinterpret_cast<Rec32*>(dst)[threadIdx.x] = pk.r[threadIdx.x];
+  win_reduce_body(p, slot, nt, reinterpret_cast<const TickArgs*>(&pk.r[blockIdx.x]), p_out, next_tick);
 }
 
 // the wave tile: 64 * HPT consecutive houses, house slot h of lane l = i0 + 64 h
@@ -848,19 +881,34 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
 // onb / wah: the window's ON lane masks and end-of-window FSM words (from k_count_window or the
 // previous launch's lookahead), replaced by the next window's when la_K > 0: then the FSM runs on
 // through the next la_K ticks (tkp[K..K+la_K), action rows K..) and counts them into next_slot.
-template <int ACT, int HPT, bool SIMPLE>
+// KA (the first window of a directly launched rollout): the tick drivers come as kernel arguments
+// (dv) and rec holds only each tick's P (the P-only k_win_reduce); lane j derives tick j's signal
+// penalty once (win_nsig, the reduce's expression) and the thermal loop reads it with v_readlane.
+template <int ACT, int HPT, bool SIMPLE, bool KA>
 __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, const uint8_t* __restrict__ action,
                                                      int64_t act_stride, const TickArgs* __restrict__ tkp, int K,
                                                      int la_K, const double* __restrict__ rec,
                                                      double* __restrict__ reward, int64_t rew_stride,
                                                      uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
                                                      unsigned long long* __restrict__ next_slot,
-                                                     const int* __restrict__ abort) {
+                                                     const int* __restrict__ abort, WinDrv dv) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
   if (abort && *abort) return;  // a cancelled launch-first rollout (k_lf_wait)
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
   uint64_t* onb_w = onb + (size_t)t.tile * HPT * kWinMax;  // this wave's rows [kWinMax][HPT]
+  // KA: lane j = tick j's negated signal penalty (its two loads go out first, beside the state's)
+  uint32_t ns_lo = 0, ns_hi = 0;
+  if (KA) {
+    const int l = (int)(threadIdx.x & 63) < K ? (int)(threadIdx.x & 63) : 0;
+    const double ns = win_nsig(p, rec[l * kWinRec], dv.s_prev[l]);
+    ns_lo = (uint32_t)__double_as_longlong(ns);
+    ns_hi = (uint32_t)((uint64_t)__double_as_longlong(ns) >> 32);
+    if (dv.p_out && blockIdx.x == 0 && threadIdx.x == 0) {  // (last window)
+      *dv.p_out = rec[(K - 1) * kWinRec];
+      *dv.next_tick = dv.tick0 + (uint64_t)K;
+    }
+  }
 
   // ---- state + parameters, once per window
   double T[HPT], Tm[HPT], ua[HPT], hm[HPT], tg[HPT];
@@ -900,8 +948,9 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
 
   // ---- the K ticks: heat source from the stored ON masks, RC thermal, reward
   // the tick's scalars (record, ON masks) are loaded one tick ahead (scalar loads, no vector work)
-  double r_od = rec[0], r_sol = rec[1], r_sig = rec[2];
-  uint64_t r_ok = __double_as_longlong(rec[3]);  // 1.0 or 0.0: compared as bits (scalar unit)
+  auto lane_nsig = [&](int j) { return __longlong_as_double((long long)readlane_u64(ns_lo, ns_hi, j)); };
+  double r_od = KA ? dv.od_k[0] : rec[0], r_sol = KA ? dv.solar[0] : rec[1], r_sig = KA ? lane_nsig(0) : rec[2];
+  uint64_t r_ok = KA ? (uint64_t)(dv.ok & 1u) : __double_as_longlong(rec[3]);  // 1.0 or 0.0: compared as bits (scalar unit)
   uint64_t r_on[HPT];
 #pragma unroll
   for (int h = 0; h < HPT; ++h) r_on[h] = onb_w[h];
@@ -914,10 +963,17 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
 #pragma unroll
     for (int h = 0; h < HPT; ++h) on_m[h] = r_on[h];
     const int jn = j + 1 < K ? j + 1 : j;
-    r_od = rec[jn * kWinRec + 0];
-    r_sol = rec[jn * kWinRec + 1];
-    r_sig = rec[jn * kWinRec + 2];
-    r_ok = __double_as_longlong(rec[jn * kWinRec + 3]);
+    if (KA) {
+      r_od = dv.od_k[jn];
+      r_sol = dv.solar[jn];
+      r_sig = lane_nsig(jn);
+      r_ok = (dv.ok >> jn) & 1u;
+    } else {
+      r_od = rec[jn * kWinRec + 0];
+      r_sol = rec[jn * kWinRec + 1];
+      r_sig = rec[jn * kWinRec + 2];
+      r_ok = __double_as_longlong(rec[jn * kWinRec + 3]);
+    }
 #pragma unroll
     for (int h = 0; h < HPT; ++h) r_on[h] = onb_w[jn * HPT + h];
     // all lanes in range: the comparison masks themselves (v_cmp writes a lane mask) against exec
@@ -982,7 +1038,7 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   if (la_K > 0) {
     uint64_t cm[HPT][kWinCap];
     win_classes<HPT>(t, cls, cm);
-    win_run<ACT, HPT>(p, w_end, cm, t, tkp + K, 0, la_K,
+    win_run<ACT, HPT>(p, w_end, cm, t, KA ? nullptr : tkp + K, KA ? dv.tick0 + (uint64_t)K : 0, la_K,
                       ACT == MDR_ACT_BUFFER ? action + (int64_t)K * act_stride : nullptr, act_stride, s_cnt[wv],
                       onb_w);
 #pragma unroll
@@ -1038,12 +1094,12 @@ __global__ void __launch_bounds__(256) k_lf_wait(const TickArgs* ring, int cap, 
 }
 
 #define MDR_INST_WIN(A, H)                                                                                      \
-  template __global__ void k_step_window<A, H, true>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
-                                                     const double*, double*, int64_t, uint64_t*, uint32_t*,      \
-                                                     unsigned long long*, const int*);                          \
-  template __global__ void k_step_window<A, H, false>(KParams, const uint8_t*, int64_t, const TickArgs*, int, int, \
-                                                      const double*, double*, int64_t, uint64_t*, uint32_t*,      \
-                                                      unsigned long long*, const int*);                          \
+  template __global__ void k_step_window<A, H, true, false>(KParams, const uint8_t*, int64_t, const TickArgs*, int,  \
+                                                            int, const double*, double*, int64_t, uint64_t*,       \
+                                                            uint32_t*, unsigned long long*, const int*, WinDrv);    \
+  template __global__ void k_step_window<A, H, false, false>(KParams, const uint8_t*, int64_t, const TickArgs*, int, \
+                                                             int, const double*, double*, int64_t, uint64_t*,      \
+                                                             uint32_t*, unsigned long long*, const int*, WinDrv);   \
   template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, uint64_t,       \
                                                 const uint64_t*, int, unsigned long long*, uint64_t*, uint32_t*,  \
                                                 const uint32_t*);
@@ -1053,6 +1109,13 @@ MDR_INST_WIN(MDR_ACT_BUFFER, 1)
 MDR_INST_WIN(MDR_ACT_RANDOM, 2)
 MDR_INST_WIN(MDR_ACT_ALWAYS_ON, 2)
 MDR_INST_WIN(MDR_ACT_BUFFER, 2)
+#define MDR_INST_WIN_KA(A)                                                                                   \
+  template __global__ void k_step_window<A, 2, true, true>(KParams, const uint8_t*, int64_t, const TickArgs*, int, \
+                                                           int, const double*, double*, int64_t, uint64_t*,       \
+                                                           uint32_t*, unsigned long long*, const int*, WinDrv);
+MDR_INST_WIN_KA(MDR_ACT_RANDOM)
+MDR_INST_WIN_KA(MDR_ACT_ALWAYS_ON)
+MDR_INST_WIN_KA(MDR_ACT_BUFFER)
 
 #define MDR_INST_PIPE(T, A, LA)                                                                    \
   template __global__ void k_step_pipe<T, A, LA>(KParams, const uint8_t*, TickArgs, const TickArgs*, \

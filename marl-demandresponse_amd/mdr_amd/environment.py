@@ -48,6 +48,7 @@ def _runs(key: np.ndarray):
     return key[chg].tolist(), np.cumsum(chg) - 1
 
 
+
 class _BuildingList(Sequence):
     """The parts of ``Building`` / ``HVAC`` the server reads (cluster.py:48-62), per house on access,
     from one host copy of the state taken when the list is created."""
@@ -550,12 +551,20 @@ class Environment:
         return float(out.item())
 
     def rollout(self, n_ticks: int, actions=None, action_mode: str = "random", rewards=None,
-                use_graph: bool = True):
-        """n_ticks steps in one C call (hipGraph-captured).  ``actions``: uint8 [n_ticks, N]
-        (buffer mode) or None; ``rewards``: float64 [n_ticks, N] output (allocated if None), or a
-        1-D [N] buffer that every tick overwrites."""
+                use_graph=None):
+        """n_ticks steps in one C call.  ``actions``: uint8 [n_ticks, N] (buffer mode) or None;
+        ``rewards``: float64 [n_ticks, N] output (allocated if None), or a 1-D [N] buffer that every
+        tick overwrites.  ``use_graph``: None / False (the default: direct launches) = the first
+        window's count and its P-only reduce are launched before the host computes the drivers
+        (mdr_rollout_begin), which then ride as kernel arguments of the first step kernel
+        (k_step_window<..., KA>; the later windows' drivers are staged behind it); True =
+        launch-first (mdr_rollout_launch: count, a device-side wait and the windows are issued
+        before the drivers, which the matching mdr_rollout posts; direct launches, or one hipGraph
+        replay with MDR_LF_GRAPH=1).  Measured on MI355X: profiles/r02h_ab.log."""
         import torch
 
+        if use_graph is None:
+            use_graph = False
         sh = self._shard
         if sh.penalty_mode != 0:
             raise NotImplementedError("rollout supports individual_L2; use step_tensor for common penalties")

@@ -193,9 +193,10 @@ def test_rollout_begin_early_count(torch_gpu, mode):
     assert torch.equal(r1[:20], r2[:20])
 
 
+@pytest.mark.parametrize("lf_graph", [False, True])
 @pytest.mark.parametrize("mode", ["random", "always_on", "buffer"])
-def test_rollout_launch_first(torch_gpu, mode):
-    """mdr_rollout_launch (Environment.rollout's default): the rollout graph is launched before the
+def test_rollout_launch_first(torch_gpu, monkeypatch, mode, lf_graph):
+    """mdr_rollout_launch (Environment.rollout with use_graph=True): the rollout graph is launched before the
     host computes the drivers and waits on the device for them.  Back-to-back calls without a host
     synchronisation, calls of other lengths, a step in between, a cancelled launch (the drivers
     raise) and a call longer than the ring all equal a twin that stages the drivers first (plain
@@ -203,6 +204,8 @@ def test_rollout_launch_first(torch_gpu, mode):
     torch = torch_gpu
     from mdr_amd import _lib as L
 
+    if lf_graph:  # one hipGraph replay per call instead of direct launches
+        monkeypatch.setenv("MDR_LF_GRAPH", "1")
     n = 20011
     e1, e2 = _pair(n)
     m = {"random": L.ACT_RANDOM, "always_on": L.ACT_ALWAYS_ON, "buffer": L.ACT_BUFFER}[mode]
@@ -219,7 +222,7 @@ def test_rollout_launch_first(torch_gpu, mode):
         e2.finish_grid_step()
 
     def roll(k):
-        e1.rollout(k, actions=None if acts is None else acts[:k], action_mode=mode, rewards=r1[:k])
+        e1.rollout(k, actions=None if acts is None else acts[:k], action_mode=mode, rewards=r1[:k], use_graph=True)
 
     def check(k):
         _same_state(torch, e1, e2)
@@ -256,3 +259,37 @@ def test_rollout_launch_first(torch_gpu, mode):
     roll(20)
     twin(20)
     check(20)
+
+
+@pytest.mark.parametrize("ka", [True, False])
+@pytest.mark.parametrize("mode", ["random", "always_on", "buffer"])
+def test_rollout_direct_kernarg_drivers(torch_gpu, monkeypatch, mode, ka):
+    """Environment.rollout's default (direct launches): the first window's count and P-only reduce
+    are launched before the drivers exist; the drivers then ride as kernel arguments of the first
+    step kernel (k_step_window<..., KA>; ka=False, MDR_NO_KA: of the first reduce,
+    k_win_reduce_staged) and the rest are staged behind the first step kernel.  Calls of 1, 20,
+    45, 64, 65, 100 and 131 ticks back to back equal a graph-replayed twin that stages every driver
+    first (rewards, state, P and the next rollout's tick id compared with ==)."""
+    torch = torch_gpu
+    from mdr_amd import _lib as L
+
+    if not ka:
+        monkeypatch.setenv("MDR_NO_KA", "1")
+
+    n = 9000
+    e1, e2 = _pair(n)
+    m = {"random": L.ACT_RANDOM, "always_on": L.ACT_ALWAYS_ON, "buffer": L.ACT_BUFFER}[mode]
+    T = 131
+    acts = (torch.rand((T, n), device="cuda") < 0.5).to(torch.uint8) if mode == "buffer" else None
+    r1 = torch.empty((T, n), dtype=torch.float64, device="cuda")
+    r2 = torch.empty_like(r1)
+    for k in (1, 20, 45, 64, 65, 100, 131):
+        a = None if acts is None else acts[:k]
+        e1.rollout(k, actions=a, action_mode=mode, rewards=r1[:k])
+        ticks = e2.driver_window(k)
+        e2.shard.rollout(ticks, a, n if a is not None else 0, m, r2[:k], n, True)
+        e2._P_dev_valid = True
+        e2.finish_grid_step()
+        _same_state(torch, e1, e2)
+        assert torch.equal(r1[:k], r2[:k]), k
+        assert float(e1.shard.p_dev.item()) == float(e2.shard.p_dev.item())
