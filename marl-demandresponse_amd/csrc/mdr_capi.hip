@@ -133,6 +133,7 @@ struct mdr_ctx {
     const uint8_t* action = nullptr;
     int64_t act_stride = 0;
     bool ka = false;                     // its P-only reduce ran too: the step takes the drivers as arguments
+    bool sharded = false;                // counts allreduced over the ranks (for mdr_rollout_sharded)
   } begun;
   // launch-first rollouts (mdr_rollout_launch): the graph runs ahead of the host's tick drivers
   uint64_t* d_lf = nullptr;              // device: [0] seq of the last k_lf_wait, [1] next rollout's tick id, [2] abort (int)
@@ -991,8 +992,9 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
     lf_cancel(c);
   }
   // the first window counted ahead by mdr_rollout_begin for exactly this call?
-  const bool counted = c->begun.on && c->begun.n == n && c->begun.mode == mode && c->begun.tick0 == ticks[0].tick &&
-                       c->begun.action == action && c->begun.act_stride == act_stride && window_ok(c, mode);
+  const bool counted = c->begun.on && !c->begun.sharded && c->begun.n == n && c->begun.mode == mode &&
+                       c->begun.tick0 == ticks[0].tick && c->begun.action == action &&
+                       c->begun.act_stride == act_stride && window_ok(c, mode);
   if (c->begun.on && !counted) c->wslab_dirty = true;  // an unmatched early count: clear its shards
   const bool ka = counted && c->begun.ka;
   c->begun.on = false;
@@ -1081,6 +1083,11 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   if (c->begun.on) c->wslab_dirty = true;  // a previous early count that no rollout consumed
   c->begun.on = false;
   if (!window_ok(c, mode)) return MDR_OK;
+  // a sharded context (RCCL attached): single-window rollouts only, counts allreduced here, so
+  // the matching mdr_rollout_sharded launches just the KA step kernel
+  const bool sharded = c->comm != nullptr;
+  const bool ka = c->win_hpt == 2 && win_simple(c) && !getenv("MDR_NO_KA");
+  if (sharded && (n > c->win || !ka)) return MDR_OK;
   hipStream_t st = S(stream);
   int rc = refresh_if_dirty(c, st);
   if (!rc) rc = wslab_clean(c, st);
@@ -1104,9 +1111,11 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   }
 #undef MDR_BEGIN_COUNT
   LAUNCH_CHECK("k_count_window");
+  if (sharded)  // every rank's sharded per-tick class counts, summed (exact integers)
+    RCCL_TRY(ncclAllReduce(c->d_wslab, c->d_wslab, (size_t)k0 * kCountShards * c->kp.n_cap, ncclUint64, ncclSum,
+                           c->comm, st));
   // the window's P (the counts need no drivers): the matching direct mdr_rollout then launches the
   // step kernel with the drivers as arguments (k_step_window<..., KA>), nothing in between
-  const bool ka = c->win_hpt == 2 && win_simple(c) && !getenv("MDR_NO_KA");
   if (ka) {
     hipLaunchKernelGGL(k_win_reduce, dim3(k0), dim3(64 * c->kp.n_cap), 0, st, c->kp, c->d_wslab, k0,
                        (const TickArgs*)nullptr, (double*)nullptr, (const int*)nullptr, (uint64_t*)nullptr);
@@ -1114,6 +1123,7 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   }
   c->wslab_dirty = false;
   c->begun.ka = ka;
+  c->begun.sharded = sharded;
   c->begun.on = true;
   c->begun.n = n; c->begun.mode = mode; c->begun.tick0 = tick0;
   c->begun.action = action; c->begun.act_stride = act_stride;
@@ -1558,8 +1568,24 @@ extern "C" {
 int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
                         int64_t act_stride, int mode, double* reward, int64_t rew_stride, double* p_out,
                         void* stream) {
-  drop_begun(c);
   if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout_sharded: bad argument");
+  // a single window begun by mdr_rollout_begin on this sharded context (count, allreduce, P-only
+  // reduce already issued): only the KA step kernel is left, with these drivers as its arguments
+  if (c->begun.on && c->begun.sharded && c->begun.ka && c->comm && c->begun.n == n && c->begun.mode == mode &&
+      c->begun.tick0 == ticks[0].tick && c->begun.action == action && c->begun.act_stride == act_stride &&
+      window_ok(c, mode) && n <= c->win) {
+    c->begun.on = false;
+    hipStream_t st = S(stream);
+    int rc = ensure_ticks(c, n);
+    if (!rc)
+      rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st, true,
+                           false, false, ticks, true);
+    c->counts_ready = false;
+    c->next_tick_known = !rc;
+    c->next_tick = ticks[n - 1].tick + 1;
+    return rc;
+  }
+  drop_begun(c);
   if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout_sharded: context not bound");
   if (!c->comm) return fail(MDR_ESTATE, "mdr_rollout_sharded: RCCL not initialised");
   if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout_sharded: bad action source");

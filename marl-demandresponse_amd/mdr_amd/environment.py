@@ -586,6 +586,11 @@ class Environment:
                 launched = True
             else:
                 sh.rollout_begin(n_ticks, self._tick, actions, act_stride, mode)
+        elif (getattr(self._comm, "native", False) and self.power_grid.interp is None
+              and self._links is not None):
+            # sharded (library RCCL communicator): a single-window rollout's count, its allreduce
+            # and its P-only reduce go out before the drivers (mdr_rollout_begin; a no-op otherwise)
+            sh.rollout_begin(n_ticks, self._tick, actions, self._n_local if actions is not None else 0, mode)
         done = 0
         try:
             while done < n_ticks:  # one window unless interpolation ends it early (driver_window)

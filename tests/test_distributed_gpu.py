@@ -58,6 +58,8 @@ def _run(env, n_total, torch, dev):
     if env.shard.penalty_mode == 0:
         r = env.rollout(T_ROLL, action_mode="random")
         rewards.extend(r.cpu().numpy().copy())
+        for k in (20, 32):  # single windows: library RCCL -> begin (count + allreduce + P-only reduce) + KA step
+            rewards.extend(env.rollout(k, action_mode="random").cpu().numpy().copy())
     st = env.shard.host_state()
     obs = env.obs_tensor().cpu().numpy().copy()
     return {"rewards": np.array(rewards), "T": st["T"], "Tm": st["Tm"], "on": st["on"], "lock": st["lock"],
