@@ -262,6 +262,49 @@ def test_greedy_vs_oracle_large(torch_gpu):
         np.testing.assert_array_equal(out.cpu().numpy().astype(bool), ref)
 
 
+def test_greedy_key_runs_vs_oracle(torch_gpu):
+    """mdr_ctrl_greedy on adversarial key layouts: 300 identical temperatures, 700 keys 1e-9 apart
+    in DESCENDING house order, 100 houses at exactly their target (key -0.0), random lockouts,
+    budgets that put the pivot inside each group; the oracle's stable numpy order decides."""
+    torch = torch_gpu
+    from mdr_amd.environment import Environment
+    from mdr_amd.shard import encode_hvac
+
+    n = 50_000
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "flat"})
+    env = Environment(props, rng=random.Random(3), population="synthetic", seed=8)
+    sh = env.shard
+    prm = sh.host_params()
+    rs = np.random.RandomState(5)
+    tg = prm["target"].copy()
+    T = tg + rs.normal(0.0, 1.5, n)
+    T[1000:1300] = 23.25                                  # identical keys (per house target differs: set it)
+    tg[1000:1300] = 22.0
+    T[2000:2700] = 22.5 + 1e-9 * np.arange(700)           # keys -(0.5 + i 1e-9): descending in house order
+    tg[2000:2700] = 22.0
+    T[3000:3100] = tg[3000:3100]                          # key -0.0
+    lock = rs.rand(n) < 0.3
+    sh.t_air.copy_(torch.from_numpy(T).cuda())
+    sh.target.copy_(torch.from_numpy(tg).cuda())
+    sh.hvac.copy_(torch.from_numpy(encode_hvac(np.zeros(n, bool), lock, np.full(n, 5))).cuda())
+    caps = np.array(env._cap_values, np.float64)[prm["cap_idx"]]
+    cop = props.cluster_prop.house_prop.hvac_prop.cop
+    key = -(T - tg)
+    order = np.argsort(key, kind="stable")
+    pw = caps[order] / cop
+    cum = np.cumsum(pw)
+    budgets = [0.0, 1e12, float(cum[n // 2])]
+    for grp in (slice(1000, 1300), slice(2000, 2700), slice(3000, 3100)):  # pivot inside each group
+        pos = np.nonzero(np.isin(order, np.arange(n)[grp]))[0]
+        budgets += [float(cum[pos[len(pos) // 2]] - 1.0), float(cum[pos[len(pos) // 2]] + 0.5)]
+    for S in budgets:
+        out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        sh.greedy(S, out)
+        ref = O.greedy(T, tg, caps, cop, lock, S)
+        np.testing.assert_array_equal(out.cpu().numpy().astype(bool), ref, err_msg=f"S={S}")
+
+
 def test_one_million_houses_properties(torch_gpu):
     """Full-size (1,048,576 houses) size-independent checks: FSM bit-exact vs the oracle on the
     same input state, temperatures within tolerance, P == sum of ON power (exact integers)."""
