@@ -301,8 +301,12 @@ int mdr_cluster_stats(mdr_ctx* ctx, const double* reward, double* out, void* str
 
 /* ---- greedy-myopic controller (greedy_myopic_controller.py:67-104) --------------------- */
 /* Next actions for the whole shard (single GPU: shard = cluster) from the current state: order
- * by -(T - target) ascending, then the reference's sequential take rule with budget S. */
+ * by -(T - target) ascending, then the reference's sequential take rule with budget S.  Histogram
+ * select: only the houses around the budget crossing are ordered; synchronises `stream` once to
+ * read back whether that window decided the tick, else the full-sort form runs (same result). */
 int mdr_ctrl_greedy(mdr_ctx* ctx, double budget, uint8_t* action, void* stream);
+/* Diagnostics: mdr_ctrl_greedy calls the histogram select handed to the full-sort form. */
+int mdr_greedy_fallbacks(mdr_ctx* ctx, uint64_t* count);
 
 /* Sharded greedy (the all-gather form): mdr_greedy_inputs writes this shard's
  * rows key = -(T - target), P = cooling capacity / cop, lockout (u8); the caller all-gathers them

@@ -116,6 +116,16 @@ struct mdr_ctx {
   size_t g_tmp_bytes = 0;
   int64_t* g_kpos = nullptr;
   int64_t* g_extra = nullptr;
+  // histogram-select greedy (k_gq_*): partial min/max, bin histogram, selection, staged window
+  double* g_part = nullptr;
+  unsigned* g_hist = nullptr;
+  GqSel* g_sel = nullptr;
+  uint4* g_stage = nullptr;
+  uint4* g_sorted = nullptr;             // the window in (key, house) order (k_gq_rank)
+  unsigned* g_bcnt = nullptr;
+  int* g_flag = nullptr;
+  int* h_gq_flag = nullptr;              // pinned: the overflow flag read back after the window
+  uint64_t gq_fallbacks = 0;             // calls the histogram select handed to the sort form
   // multi-GPU
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
@@ -482,6 +492,8 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->g_key); hipFree(c->g_key2); hipFree(c->g_ps); hipFree(c->g_incl);
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
+  hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_stage); hipFree(c->g_bcnt);
+  hipFree(c->g_flag); hipHostFree(c->h_gq_flag); hipFree(c->g_sorted);
   if (c->comm) ncclCommDestroy(c->comm);
   delete c;
   return MDR_OK;
@@ -1353,6 +1365,10 @@ static int greedy_scratch(mdr_ctx* c, int64_t n) {
   hipFree(c->g_key); hipFree(c->g_key2); hipFree(c->g_ps); hipFree(c->g_incl);
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
+  hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_stage); hipFree(c->g_bcnt);
+  hipFree(c->g_flag); hipHostFree(c->h_gq_flag); hipFree(c->g_sorted);
+  c->g_part = nullptr; c->g_hist = nullptr; c->g_sel = nullptr; c->g_stage = nullptr; c->g_bcnt = nullptr;
+  c->g_flag = nullptr; c->h_gq_flag = nullptr; c->g_sorted = nullptr;
   HIP_TRY(hipMalloc(&c->g_key, n * sizeof(double)));
   HIP_TRY(hipMalloc(&c->g_key2, n * sizeof(double)));
   HIP_TRY(hipMalloc(&c->g_ps, n * sizeof(double)));
@@ -1362,6 +1378,16 @@ static int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_ls, n));
   HIP_TRY(hipMalloc(&c->g_kpos, 2 * sizeof(int64_t)));
   HIP_TRY(hipMalloc(&c->g_extra, 64 * sizeof(int64_t)));
+  const int64_t nstage = (n + kGqStage - 1) / kGqStage;
+  HIP_TRY(hipMalloc(&c->g_part, 2 * kGqParts * sizeof(double)));
+  HIP_TRY(hipMalloc(&c->g_hist, (kGqBins + kGqSuper) * 4 * sizeof(unsigned)));
+  HIP_TRY(hipMemset(c->g_hist, 0, (kGqBins + kGqSuper) * 4 * sizeof(unsigned)));  // (k_gq_select re-zeroes it)
+  HIP_TRY(hipMalloc(&c->g_sel, 128));
+  HIP_TRY(hipMalloc(&c->g_stage, nstage * kGqStage * sizeof(uint4)));
+  HIP_TRY(hipMalloc(&c->g_bcnt, nstage * sizeof(unsigned)));
+  HIP_TRY(hipMalloc(&c->g_sorted, 2 * kGqCap * sizeof(uint4)));  // [sorted | gathered window]
+  HIP_TRY(hipMalloc(&c->g_flag, sizeof(int)));
+  HIP_TRY(hipHostMalloc(&c->h_gq_flag, sizeof(int), hipHostMallocDefault));
   size_t b1 = 0, b2 = 0;
   HIP_TRY(greedy_sort(nullptr, b1, c->g_key, c->g_key2, c->g_idx, c->g_idx2, n, nullptr));
   HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b2, c->g_ps, c->g_incl, (int)n));
@@ -1378,6 +1404,41 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   if (rc) return rc;
   hipStream_t st = S(stream);
   const int n = (int)c->kp.n;
+  double pmin = INFINITY;
+  for (int k = 0; k < c->cfg.n_cap; ++k) pmin = fmin(pmin, c->cfg.cap_table[k] / c->cfg.cop);
+  if (c->kp.n_cap <= 4 && n < (1 << 30) && !getenv("MDR_GREEDY_SORT")) {
+    // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster; the sort form below
+    // runs only when the candidate window cannot decide (the flag read back here)
+    HIP_TRY(hipMemsetAsync(c->g_sel, 0, 128, st));
+    hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_part, c->g_sel);
+    LAUNCH_CHECK("k_gq_keys");
+    hipLaunchKernelGGL(k_gq_super, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_part, kGqParts,
+                       c->g_hist, c->g_sel);
+    LAUNCH_CHECK("k_gq_super");
+    hipLaunchKernelGGL(k_gq_select_super, dim3(1), dim3(256), 0, st, c->kp, c->g_hist, budget, c->g_sel);
+    LAUNCH_CHECK("k_gq_select_super");
+    hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_hist, c->g_sel);
+    LAUNCH_CHECK("k_gq_bins");
+    hipLaunchKernelGGL(k_gq_select_bin, dim3(1), dim3(128), 0, st, c->kp, c->g_hist, budget, c->g_sel);
+    LAUNCH_CHECK("k_gq_select_bin");
+    hipLaunchKernelGGL(k_gq_apply, dim3(blocks(n, 256)), dim3(256), 0, st, c->kp, c->g_key, c->g_sel, action);
+    LAUNCH_CHECK("k_gq_apply");
+    const int nstage = (n + kGqStage - 1) / kGqStage;
+    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(256), 0, st, c->kp, c->g_key, c->g_sel, c->g_stage, c->g_bcnt);
+    LAUNCH_CHECK("k_gq_compact");
+    hipLaunchKernelGGL(k_gq_gather, dim3(nstage), dim3(256), 0, st, c->g_stage, c->g_bcnt, c->g_sel, c->g_sorted + kGqCap);
+    LAUNCH_CHECK("k_gq_gather");
+    hipLaunchKernelGGL(k_gq_rank, dim3(kGqRankBlocks), dim3(256), 0, st, c->g_sorted + kGqCap, c->g_sel, c->g_sorted);
+    LAUNCH_CHECK("k_gq_rank");
+    hipLaunchKernelGGL(k_gq_finish, dim3(1), dim3(1024), 0, st, c->kp, c->g_sorted, budget, pmin, c->g_sel, action,
+                       c->g_flag);
+    LAUNCH_CHECK("k_gq_finish");
+    HIP_TRY(hipMemcpyAsync(c->h_gq_flag, c->g_flag, sizeof(int), hipMemcpyDeviceToHost, st));
+    HIP_TRY(hipStreamSynchronize(st));
+
+    if (!*c->h_gq_flag) return MDR_OK;
+    c->gq_fallbacks += 1;
+  }
   hipLaunchKernelGGL(k_greedy_keys, dim3(blocks(n, 256)), dim3(256), 0, st, c->kp, c->g_key, c->g_idx);
   LAUNCH_CHECK("k_greedy_keys");
   size_t b = c->g_tmp_bytes;
@@ -1387,14 +1448,18 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   LAUNCH_CHECK("k_greedy_gather");
   b = c->g_tmp_bytes;
   HIP_TRY(hipcub::DeviceScan::InclusiveSum(c->g_tmp, b, c->g_ps, c->g_incl, n, st));
-  double pmin = INFINITY;
-  for (int k = 0; k < c->cfg.n_cap; ++k) pmin = fmin(pmin, c->cfg.cap_table[k] / c->cfg.cop);
   hipLaunchKernelGGL(k_greedy_walk, dim3(1), dim3(256), 0, st, (int64_t)n, c->g_incl, c->g_ps, c->g_ls,
                      budget, pmin, c->g_kpos, c->g_extra, 64);
   LAUNCH_CHECK("k_greedy_walk");
   hipLaunchKernelGGL(k_greedy_apply, dim3(blocks(n, 256)), dim3(256), 0, st, (int64_t)n, c->g_idx2,
                      c->g_kpos, c->g_extra, action);
   LAUNCH_CHECK("k_greedy_apply");
+  return MDR_OK;
+}
+
+int mdr_greedy_fallbacks(mdr_ctx* c, uint64_t* count) {
+  if (!c || !count) return fail(MDR_EARG, "mdr_greedy_fallbacks: null argument");
+  *count = c->gq_fallbacks;
   return MDR_OK;
 }
 

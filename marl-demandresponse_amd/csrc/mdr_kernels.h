@@ -138,6 +138,25 @@ __global__ void k_greedy_walk(int64_t n, const double* incl, const double* psort
                               int64_t* extra, int max_extra);
 __global__ void k_greedy_apply(int64_t n, const int* perm, const int64_t* kpos, const int64_t* extra,
                                uint8_t* action);
+constexpr int kGqBins = 16384;  // histogram-select greedy: key bins
+constexpr int kGqCap = 4096;    // candidate window capacity (LDS, 16 B per house)
+constexpr int kGqAfter = 256;   // window houses past the crossing bin (the gap walk's room)
+constexpr int kGqStage = 4096;  // houses per k_gq_compact block
+constexpr int kGqParts = 256;   // k_gq_keys / k_gq_hist grid
+constexpr int kGqSuper = 256;   // superbins (64 bins each) of the select's first pass
+struct GqSel;
+__global__ void k_gq_keys(KParams p, double* key, double* part, GqSel* sel);
+__global__ void k_gq_super(KParams p, const double* key, const double* part, int nparts, unsigned* hist, GqSel* sel);
+__global__ void k_gq_select_super(KParams p, unsigned* hist, double S, GqSel* sel);
+__global__ void k_gq_bins(KParams p, const double* key, unsigned* hist, const GqSel* sel);
+__global__ void k_gq_select_bin(KParams p, unsigned* hist, double S, GqSel* sel);
+__global__ void k_gq_apply(KParams p, const double* key, const GqSel* sel, uint8_t* action);
+__global__ void k_gq_compact(KParams p, const double* key, const GqSel* sel, uint4* stage, unsigned* bcnt);
+constexpr int kGqRankBlocks = 256;  // k_gq_rank grid
+__global__ void k_gq_gather(const uint4* stage, const unsigned* bcnt, const GqSel* sel, uint4* win);
+__global__ void k_gq_rank(const uint4* win, const GqSel* sel, uint4* sorted);
+__global__ void k_gq_finish(KParams p, const uint4* sorted, double S, double pmin, const GqSel* sel, uint8_t* action,
+                            int* flag);
 __global__ void k_greedy_inputs(KParams p, double* key, double* power, uint8_t* lock);
 __global__ void k_greedy_iota(int64_t n, int* idx);
 __global__ void k_greedy_gather_rows(int64_t n, const int* perm, const double* power, const uint8_t* lock,

@@ -1491,6 +1491,383 @@ __global__ void __launch_bounds__(256) k_greedy_walk(int64_t n, const double* __
   if (threadIdx.x == 0) { kpos[0] = s_k; kpos[1] = s_ne < max_extra ? s_ne : max_extra; }
 }
 
+// ---- histogram-select form (mdr_ctrl_greedy's default; the sort form above is its fallback).
+// Only the houses around the budget crossing need an order: houses are binned by a monotone
+// linear quantisation of the key over [kmin, kmax] (kGqBins bins, class counts per bin), the bin
+// b* where the cumulative P crosses S is found from the bin sums, every house in a lower bin is
+// taken, and only the houses of bins [b*, b_end] (at most kGqCap, with >= kGqAfter houses past
+// b*) are ordered — by (key value, house), as the stable sort orders them — in one workgroup's
+// LDS, where the exact crossing position and the gap walk are evaluated.  Sums of P are exact
+// for integer P (every sum of P here is).  Inputs the candidate window cannot decide (NaN keys,
+// a crossing bin over kGqCap houses, a walk that leaves the window) raise sel.overflow and the
+// host reruns the sort form.
+struct GqSel {
+  double kmin, scale, base_tot;
+  unsigned long long base_cnt, total;
+  int bstar, bend, all, overflow, more_after, ncand, sb;
+};
+static_assert(sizeof(GqSel) <= 128, "GqSel fits the 128-B sel buffer");
+
+// okey: -0.0 folded onto +0.0 (value order, numpy's stable argsort), sign-magnitude -> unsigned
+__device__ __forceinline__ uint64_t gq_okey(double k) {
+  const uint64_t b = (uint64_t)__double_as_longlong(k + 0.0);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+__device__ __forceinline__ int gq_bin(double k, double kmin, double scale) {
+  const double d = (k - kmin) * scale;  // k >= kmin: monotone non-decreasing in k
+  return d >= (double)(kGqBins - 1) ? kGqBins - 1 : (int)d;
+}
+
+// K1: keys + per-block (min, max) of the finite keys; a NaN key raises the overflow flag
+__global__ void __launch_bounds__(256) k_gq_keys(KParams p, double* __restrict__ key, double* __restrict__ part,
+                                                 GqSel* __restrict__ sel) {
+  __shared__ double s_lo[4], s_hi[4];
+  double lo = INFINITY, hi = -INFINITY;
+  bool nan = false;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double k = -(p.t_air[i] - p.target[i]);
+    key[i] = k;
+    if (k != k) nan = true;
+    else { lo = fmin(lo, k); hi = fmax(hi, k); }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, off));
+    hi = fmax(hi, __shfl_xor(hi, off));
+  }
+  if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
+  if (__any(nan) && (threadIdx.x & 63) == 0) sel->overflow = 1;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    part[2 * blockIdx.x] = fmin(fmin(s_lo[0], s_lo[1]), fmin(s_lo[2], s_lo[3]));
+    part[2 * blockIdx.x + 1] = fmax(fmax(s_hi[0], s_hi[1]), fmax(s_hi[2], s_hi[3]));
+  }
+}
+
+// K2a: every block reduces the partials (the same bits in every block) and counts its houses per
+// superbin (kGqBins / kGqSuper consecutive bins) and class; block 0 publishes kmin / scale
+__global__ void __launch_bounds__(256) k_gq_super(KParams p, const double* __restrict__ key,
+                                                  const double* __restrict__ part, int nparts,
+                                                  unsigned* __restrict__ hist, GqSel* __restrict__ sel) {
+  __shared__ unsigned s_sh[4][kGqSuper * 4];  // one copy per wave (less atomic contention on hot superbins)
+  __shared__ double s_lo[4], s_hi[4];
+  double lo = INFINITY, hi = -INFINITY;
+  for (int b = threadIdx.x; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, off));
+    hi = fmax(hi, __shfl_xor(hi, off));
+  }
+  if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
+  for (int e = threadIdx.x; e < 4 * kGqSuper * 4; e += blockDim.x) (&s_sh[0][0])[e] = 0u;
+  __syncthreads();
+  const double kmin = fmin(fmin(s_lo[0], s_lo[1]), fmin(s_lo[2], s_lo[3]));
+  const double kmax = fmax(fmax(s_hi[0], s_hi[1]), fmax(s_hi[2], s_hi[3]));
+  const double range = kmax - kmin;
+  const double scale = range > 0.0 && range < INFINITY ? (double)kGqBins / range : 0.0;
+  if (blockIdx.x == 0 && threadIdx.x == 0) { sel->kmin = kmin; sel->scale = scale; }
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double k = key[i];
+    if (k != k) continue;
+    atomicAdd(&s_sh[threadIdx.x >> 6][(gq_bin(k, kmin, scale) / (kGqBins / kGqSuper)) * 4 + (p.cap_idx[i] & 3u)], 1u);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < kGqSuper * 4; e += blockDim.x) {
+    const unsigned v = s_sh[0][e] + s_sh[1][e] + s_sh[2][e] + s_sh[3][e];
+    if (v) atomicAdd(&hist[kGqBins * 4 + e], v);
+  }
+}
+
+// K3a (one workgroup, thread t = superbin t): the superbin where the cumulative P crosses S, the P
+// and house count before it (sums of P: exact for integer P); zeroes the superbin histogram
+__global__ void __launch_bounds__(256) k_gq_select_super(KParams p, unsigned* __restrict__ hist, double S,
+                                                         GqSel* __restrict__ sel) {
+  static_assert(kGqSuper == 256, "one superbin per thread");
+  __shared__ double s_w[4];
+  __shared__ unsigned long long s_wc[4];
+  __shared__ int s_first;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  double p_on[kWinCap];
+#pragma unroll
+  for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
+  const uint4 v = *reinterpret_cast<const uint4*>(hist + kGqBins * 4 + tid * 4);
+  unsigned long long c[kWinCap] = {v.x, v.y, v.z, v.w};
+  const double ps = win_power(p, c, p_on);
+  const unsigned long long cs = c[0] + c[1] + c[2] + c[3];
+  double x = ps;
+  unsigned long long xc = cs;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const double y = __shfl_up(x, off);
+    const unsigned long long yc = __shfl_up(xc, off);
+    if (lane >= off) { x += y; xc += yc; }
+  }
+  if (lane == 63) { s_w[wv] = x; s_wc[wv] = xc; }
+  if (tid == 0) s_first = kGqSuper;
+  __syncthreads();
+  double before = x - ps;
+  unsigned long long beforec = xc - cs;
+  for (int w = 0; w < wv; ++w) { before += s_w[w]; beforec += s_wc[w]; }
+  if (!(before + ps < S)) atomicMin(&s_first, tid);
+  __syncthreads();
+  if (tid == s_first) { sel->base_tot = before; sel->base_cnt = beforec; }
+  if (tid == 0) {
+    sel->sb = s_first;
+    sel->all = s_first >= kGqSuper;
+    sel->total = s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
+  }
+  *reinterpret_cast<uint4*>(hist + kGqBins * 4 + tid * 4) = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// K2b: class counts of the bins of superbins sb and sb + 1 (the crossing superbin and the room
+// after it), from the houses in them only
+__global__ void __launch_bounds__(256) k_gq_bins(KParams p, const double* __restrict__ key,
+                                                 unsigned* __restrict__ hist, const GqSel* __restrict__ sel) {
+  constexpr int NB = 2 * (kGqBins / kGqSuper);
+  __shared__ unsigned s_h[4][NB * 4];
+  if (sel->all || sel->overflow) return;
+  for (int e = threadIdx.x; e < 4 * NB * 4; e += blockDim.x) (&s_h[0][0])[e] = 0u;
+  __syncthreads();
+  const int bb = sel->sb * (kGqBins / kGqSuper);
+  const double kmin = sel->kmin, scale = sel->scale;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (int64_t)gridDim.x * blockDim.x) {
+    const double k = key[i];
+    if (k != k) continue;
+    const int b = gq_bin(k, kmin, scale) - bb;
+    if (b >= 0 && b < NB) atomicAdd(&s_h[threadIdx.x >> 6][b * 4 + (p.cap_idx[i] & 3u)], 1u);
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < NB * 4; e += blockDim.x) {
+    const unsigned v = s_h[0][e] + s_h[1][e] + s_h[2][e] + s_h[3][e];
+    if (v) atomicAdd(&hist[e], v);
+  }
+}
+
+// K3b (one wave per 64 bins: 128 threads): the crossing bin inside superbin sb (lane l = its bin l),
+// the candidate window [b*, b_end] over the next 64 bins; zeroes the bin histogram
+__global__ void __launch_bounds__(128) k_gq_select_bin(KParams p, unsigned* __restrict__ hist, double S,
+                                                       GqSel* __restrict__ sel) {
+  static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
+  __shared__ unsigned s_c[128];
+  __shared__ int s_l0;
+  __shared__ double s_base;
+  __shared__ unsigned long long s_basec;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const bool on = !sel->all && !sel->overflow;
+  const int bb = sel->sb * 64;
+  double p_on[kWinCap];
+#pragma unroll
+  for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
+  const uint4 v = *reinterpret_cast<const uint4*>(hist + tid * 4);
+  unsigned long long c[kWinCap] = {v.x, v.y, v.z, v.w};
+  s_c[tid] = v.x + v.y + v.z + v.w;
+  if (tid < 64 && on) {  // wave 0: the crossing bin of superbin sb (it crosses: K3a)
+    const double pb = win_power(p, c, p_on);
+    const unsigned long long cb = c[0] + c[1] + c[2] + c[3];
+    double xb = pb;
+    unsigned long long xcb = cb;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double y = __shfl_up(xb, off);
+      const unsigned long long yc = __shfl_up(xcb, off);
+      if (lane >= off) { xb += y; xcb += yc; }
+    }
+    const double bef = sel->base_tot + (xb - pb);
+    const unsigned long long befc = sel->base_cnt + (xcb - cb);
+    const unsigned long long m = __ballot(!(bef + pb < S));
+    const int l0 = m ? __ffsll((long long)m) - 1 : 63;
+    if (lane == l0) { s_l0 = l0; s_base = bef; s_basec = befc; }
+  }
+  __syncthreads();
+  if (tid < 64 && on) {  // the window: bins l0 .. l0 + 63 of the 128 loaded
+    const int l0 = s_l0;
+    const int li = l0 + lane;
+    const unsigned long long c2 = li < 128 && bb + li < kGqBins ? s_c[li] : 0ull;
+    const bool valid = li < 128 && bb + li < kGqBins;
+    unsigned long long pre = c2;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const unsigned long long y = __shfl_up(pre, off);
+      if (lane >= off) pre += y;
+    }
+    const unsigned long long c0 = __shfl(c2, 0);
+    const unsigned long long fit = __ballot(valid && pre <= (unsigned long long)kGqCap);
+    const unsigned long long enough = __ballot(valid && pre >= c0 + kGqAfter) & fit;
+    int le;
+    if (!(fit & 1ull)) le = 0;  // the crossing bin alone overflows the window
+    else if (enough) le = __ffsll((long long)enough) - 1;
+    else le = 63 - __clzll((long long)fit);
+    const int cnt = (int)__shfl(pre, le);
+    if (lane == 0) {
+      if (!(fit & 1ull)) sel->overflow = 1;
+      sel->bstar = bb + l0;
+      sel->bend = bb + l0 + le;
+      sel->base_tot = s_base;
+      sel->more_after = s_basec + (unsigned long long)cnt < sel->total;
+      sel->ncand = cnt;
+    }
+  }
+  *reinterpret_cast<uint4*>(hist + tid * 4) = make_uint4(0u, 0u, 0u, 0u);
+}
+
+// K6: every house of a bin below b* is taken; the rest start as not taken (K5 sets the window's)
+__global__ void k_gq_apply(KParams p, const double* __restrict__ key, const GqSel* __restrict__ sel,
+                           uint8_t* __restrict__ action) {
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= p.n) return;
+  const double k = key[i];
+  action[i] = sel->all ? 1 : (k == k && gq_bin(k, sel->kmin, sel->scale) < sel->bstar ? 1 : 0);
+}
+
+// K4: the window's houses, staged per block of kGqStage houses (okey, house << 2 | class, lock)
+__global__ void __launch_bounds__(256) k_gq_compact(KParams p, const double* __restrict__ key,
+                                                    const GqSel* __restrict__ sel, uint4* __restrict__ stage,
+                                                    unsigned* __restrict__ bcnt) {
+  __shared__ unsigned s_n;
+  if (threadIdx.x == 0) s_n = 0u;
+  __syncthreads();
+  const bool on = !sel->all && !sel->overflow;
+  const int bs = sel->bstar, be = sel->bend;
+  const double kmin = sel->kmin, scale = sel->scale;
+  const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
+  if (on) {
+    for (int t = threadIdx.x; t < kGqStage; t += blockDim.x) {
+      const int64_t i = b0 + t;
+      if (i >= p.n) break;
+      const double k = key[i];
+      const int b = gq_bin(k, kmin, scale);
+      if (b < bs || b > be) continue;
+      const unsigned slot = atomicAdd(&s_n, 1u);
+      const uint64_t ok = gq_okey(k);
+      stage[b0 + slot] = make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), ((uint32_t)i << 2) | (p.cap_idx[i] & 3u),
+                                    hv_lock(p.hvac[i]) ? 1u : 0u);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) bcnt[blockIdx.x] = on ? s_n : 0u;
+}
+
+__device__ __forceinline__ bool gq_less(const uint4& a, const uint4& b) {
+  const uint64_t ka = ((uint64_t)a.y << 32) | a.x, kb = ((uint64_t)b.y << 32) | b.x;
+  return ka < kb || (ka == kb && a.z < b.z);  // (z = house << 2 | class: house order on equal keys)
+}
+
+// K5a: stage block b copies its window houses to win[offset_b ..) (offset_b: the counts of the
+// stage blocks before it), so the window becomes one contiguous array
+__global__ void __launch_bounds__(256) k_gq_gather(const uint4* __restrict__ stage, const unsigned* __restrict__ bcnt,
+                                                   const GqSel* __restrict__ sel, uint4* __restrict__ win) {
+  __shared__ unsigned s_w[4];
+  if (sel->all || sel->overflow) return;
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const unsigned c = bcnt[b];
+  if (c == 0u) return;  // (block-uniform)
+  unsigned o = 0;
+  for (int q = tid; q < b; q += blockDim.x) o += bcnt[q];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) o += __shfl_xor(o, off);
+  if (lane == 0) s_w[wv] = o;
+  __syncthreads();
+  o = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+  for (unsigned e = tid; e < c; e += blockDim.x) win[o + e] = stage[(int64_t)b * kGqStage + e];
+}
+
+// K5b (kGqRankBlocks workgroups): the window into LDS; one wave per house computes its rank (how
+// many window houses precede it in (key, house) order, the lanes splitting the comparisons) and
+// writes it to sorted[rank]
+__global__ void __launch_bounds__(256) k_gq_rank(const uint4* __restrict__ win, const GqSel* __restrict__ sel,
+                                                 uint4* __restrict__ sorted) {
+  __shared__ uint4 s_e[kGqCap];
+  if (sel->all || sel->overflow) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nth = blockDim.x;
+  const int ncand = sel->ncand;
+  for (int e = tid; e < ncand; e += nth) s_e[e] = win[e];
+  __syncthreads();
+  const int nwv = (int)gridDim.x * (nth >> 6);
+  for (int e = (int)blockIdx.x * (nth >> 6) + wv; e < ncand; e += nwv) {
+    const uint4 me = s_e[e];
+    unsigned r = 0;
+#pragma unroll 4
+    for (int f = lane; f < ncand; f += 64) r += gq_less(s_e[f], me) ? 1u : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) r += __shfl_xor(r, off);
+    if (lane == 0) sorted[r] = me;
+  }
+}
+
+// K5c (one workgroup of 1024): the sorted window into LDS, the exact crossing position from
+// base_tot, the window's prefix taken, then the gap walk (k_greedy_walk's rule)
+__global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __restrict__ sorted, double S,
+                                                    double pmin, const GqSel* __restrict__ sel,
+                                                    uint8_t* __restrict__ action, int* __restrict__ flag) {
+  __shared__ uint4 s_e[kGqCap];
+  __shared__ double s_w[16];
+  __shared__ double s_tot;
+  __shared__ int s_k, s_first;
+  __shared__ unsigned long long s_bal[16];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nth = blockDim.x;
+  double pon[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) pon[k] = p.p_on[k < p.n_cap ? k : 0];
+  auto P_of = [&](uint32_t z) {
+    const uint32_t cl = z & 3u;
+    return cl == 0u ? pon[0] : cl == 1u ? pon[1] : cl == 2u ? pon[2] : pon[3];
+  };
+  if (sel->all || sel->overflow) {
+    if (tid == 0) *flag = sel->overflow;
+    return;
+  }
+  const int ncand = sel->ncand;
+  for (int e = tid; e < ncand; e += nth) s_e[e] = sorted[e];
+  if (tid == 0) { s_tot = sel->base_tot; s_k = -1; }
+  __syncthreads();
+  for (int c0 = 0; c0 < ncand; c0 += nth) {
+    const int j = c0 + tid;
+    const double pj = j < ncand ? P_of(s_e[j].z) : 0.0;
+    double x = pj;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const double y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) s_w[wv] = x;
+    __syncthreads();
+    for (int w = 0; w < wv; ++w) x += s_w[w];
+    const double tot = s_tot;
+    const unsigned long long bl = __ballot(j < ncand && !(tot + x < S));
+    if (lane == 0) s_bal[wv] = bl;
+    if (tid == 0) s_first = -1;
+    __syncthreads();
+    if (tid == 0)
+      for (int w = 0; w < 16; ++w)
+        if (s_bal[w]) { s_first = w * 64 + __ffsll((long long)s_bal[w]) - 1; break; }
+    __syncthreads();
+    const int f = s_first;
+    if (f >= 0 && tid == f) { s_k = c0 + f; s_tot = tot + (x - pj); }  // (exclusive: exact for integer P)
+    if (f < 0 && tid == nth - 1) s_tot = tot + x;                     // the round's total
+    __syncthreads();
+    if (f >= 0) break;
+  }
+  const int k = s_k;  // >= 0: the crossing lies in bin b*, inside the window
+  for (int j = tid; j < (k < 0 ? ncand : k); j += nth) action[s_e[j].z >> 2] = 1;
+  if (tid == 0) {
+    int ovf = k < 0;
+    if (!ovf) {
+      double tot = s_tot;
+      int j = k;
+      for (; j < ncand; ++j) {
+        if (!(tot < S) || 2.0 * (S - tot) < pmin * (1.0 - 1e-9)) break;
+        const double pj = P_of(s_e[j].z);
+        if ((pj + tot < S) || (fabs(pj + tot - S) < fabs(tot - S) && !s_e[j].w)) {
+          action[s_e[j].z >> 2] = 1;
+          tot += pj;
+        }
+      }
+      if (j >= ncand && sel->more_after && tot < S && !(2.0 * (S - tot) < pmin * (1.0 - 1e-9))) ovf = 1;
+    }
+    *flag = ovf;
+  }
+}
+
 // sharded greedy (mdr_greedy_inputs / mdr_greedy_select): this shard's (key, P, lockout) rows, and
 // the generic gather / iota for the cluster-wide selection over the gathered rows
 __global__ void k_greedy_inputs(KParams p, double* __restrict__ key, double* __restrict__ power,

@@ -127,6 +127,7 @@ SIGNATURES = {
     "mdr_halo_pack": (I, [VP, P(mdr_obs_spec), VP, VP]),
     "mdr_msg_pack": (I, [VP, P(mdr_obs_spec), VP, VP]),
     "mdr_ctrl_greedy": (I, [VP, D, VP, VP]),
+    "mdr_greedy_fallbacks": (I, [VP, VP]),
     "mdr_greedy_inputs": (I, [VP, VP, VP, VP, VP]),
     "mdr_greedy_select": (I, [VP, I64, VP, VP, VP, D, VP, VP]),
     "mdr_cluster_stats": (I, [VP, VP, VP, VP]),

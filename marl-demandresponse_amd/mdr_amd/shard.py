@@ -228,6 +228,12 @@ class HipShard:
         L.check(self.lib.mdr_ctrl_greedy(self.ctx, float(budget), L.ptr(action), self.stream()),
                 "mdr_ctrl_greedy")
 
+    def greedy_fallbacks(self) -> int:
+        """mdr_ctrl_greedy calls whose histogram select fell back to the full sort (mdr_greedy_fallbacks)."""
+        v = C.c_uint64()
+        L.check(self.lib.mdr_greedy_fallbacks(self.ctx, C.byref(v)), "mdr_greedy_fallbacks")
+        return int(v.value)
+
     def obs(self, spec, scalars, out, use_p_dev=True):
         L.check(self.lib.mdr_obs(self.ctx, C.byref(spec), C.byref(scalars),
                                  L.ptr(self.p_dev) if use_p_dev else 0, L.ptr(out), self.stream()),

@@ -262,14 +262,20 @@ def test_greedy_vs_oracle_large(torch_gpu):
         np.testing.assert_array_equal(out.cpu().numpy().astype(bool), ref)
 
 
-def test_greedy_key_runs_vs_oracle(torch_gpu):
-    """mdr_ctrl_greedy on adversarial key layouts: 300 identical temperatures, 700 keys 1e-9 apart
-    in DESCENDING house order, 100 houses at exactly their target (key -0.0), random lockouts,
-    budgets that put the pivot inside each group; the oracle's stable numpy order decides."""
+@pytest.mark.parametrize("form", ["select", "sort"])
+def test_greedy_key_runs_vs_oracle(torch_gpu, monkeypatch, form):
+    """mdr_ctrl_greedy on adversarial key layouts, in both forms (select: the default histogram
+    select; sort: MDR_GREEDY_SORT, the full 64-bit key sort): 300 identical temperatures, 700 keys
+    1e-9 apart in DESCENDING house order, 100 houses at exactly their target (key -0.0), random
+    lockouts, budgets that put the pivot inside each group; the oracle's stable numpy order
+    decides.  The select form decides all of these itself (no fallback); a cluster of identical
+    keys (one bin) is handed to the sort form and still matches."""
     torch = torch_gpu
     from mdr_amd.environment import Environment
     from mdr_amd.shard import encode_hvac
 
+    if form == "sort":
+        monkeypatch.setenv("MDR_GREEDY_SORT", "1")
     n = 50_000
     props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
                                      "power_grid_prop.signal_properties.mode": "flat"})
@@ -298,11 +304,23 @@ def test_greedy_key_runs_vs_oracle(torch_gpu):
     for grp in (slice(1000, 1300), slice(2000, 2700), slice(3000, 3100)):  # pivot inside each group
         pos = np.nonzero(np.isin(order, np.arange(n)[grp]))[0]
         budgets += [float(cum[pos[len(pos) // 2]] - 1.0), float(cum[pos[len(pos) // 2]] + 0.5)]
+    f0 = sh.greedy_fallbacks()
     for S in budgets:
         out = torch.zeros(n, dtype=torch.uint8, device="cuda")
         sh.greedy(S, out)
         ref = O.greedy(T, tg, caps, cop, lock, S)
         np.testing.assert_array_equal(out.cpu().numpy().astype(bool), ref, err_msg=f"S={S}")
+    assert sh.greedy_fallbacks() == f0  # (the sort form never counts)
+    # every key identical: one bin of n houses > the window -> the sort form decides
+    sh.t_air.copy_(torch.full((n,), 23.0, dtype=torch.float64, device="cuda"))
+    sh.target.copy_(torch.full((n,), 22.0, dtype=torch.float64, device="cuda"))
+    for S in (float(cum[n // 3]), 1e12):
+        out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+        sh.greedy(S, out)
+        ref = O.greedy(np.full(n, 23.0), np.full(n, 22.0), caps, cop, lock, S)
+        np.testing.assert_array_equal(out.cpu().numpy().astype(bool), ref, err_msg=f"equal keys S={S}")
+    if form == "select":
+        assert sh.greedy_fallbacks() == f0 + 1  # (S = 1e12 takes everything: decided by the bins)
 
 
 def test_one_million_houses_properties(torch_gpu):
