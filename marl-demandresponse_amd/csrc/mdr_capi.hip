@@ -1383,6 +1383,7 @@ static int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_hist, (kGqBins + kGqSuper) * 4 * sizeof(unsigned)));
   HIP_TRY(hipMemset(c->g_hist, 0, (kGqBins + kGqSuper) * 4 * sizeof(unsigned)));  // (k_gq_select re-zeroes it)
   HIP_TRY(hipMalloc(&c->g_sel, 128));
+  HIP_TRY(hipMemset(c->g_sel, 0, 128));
   HIP_TRY(hipMalloc(&c->g_stage, nstage * kGqStage * sizeof(uint4)));
   HIP_TRY(hipMalloc(&c->g_bcnt, nstage * sizeof(unsigned)));
   HIP_TRY(hipMalloc(&c->g_sorted, 2 * kGqCap * sizeof(uint4)));  // [sorted | gathered window]
@@ -1409,7 +1410,7 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   if (c->kp.n_cap <= 4 && n < (1 << 30) && !getenv("MDR_GREEDY_SORT")) {
     // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster; the sort form below
     // runs only when the candidate window cannot decide (the flag read back here)
-    HIP_TRY(hipMemsetAsync(c->g_sel, 0, 128, st));
+    // (g_sel's only accumulated field, overflow, is cleared by k_gq_finish for the next call)
     hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_part, c->g_sel);
     LAUNCH_CHECK("k_gq_keys");
     hipLaunchKernelGGL(k_gq_super, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_part, kGqParts,
@@ -1421,10 +1422,9 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
     LAUNCH_CHECK("k_gq_bins");
     hipLaunchKernelGGL(k_gq_select_bin, dim3(1), dim3(128), 0, st, c->kp, c->g_hist, budget, c->g_sel);
     LAUNCH_CHECK("k_gq_select_bin");
-    hipLaunchKernelGGL(k_gq_apply, dim3(blocks(n, 256)), dim3(256), 0, st, c->kp, c->g_key, c->g_sel, action);
-    LAUNCH_CHECK("k_gq_apply");
     const int nstage = (n + kGqStage - 1) / kGqStage;
-    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(256), 0, st, c->kp, c->g_key, c->g_sel, c->g_stage, c->g_bcnt);
+    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(256), 0, st, c->kp, c->g_key, c->g_sel, c->g_stage, c->g_bcnt,
+                       action);
     LAUNCH_CHECK("k_gq_compact");
     hipLaunchKernelGGL(k_gq_gather, dim3(nstage), dim3(256), 0, st, c->g_stage, c->g_bcnt, c->g_sel, c->g_sorted + kGqCap);
     LAUNCH_CHECK("k_gq_gather");

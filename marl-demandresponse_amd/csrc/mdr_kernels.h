@@ -150,12 +150,12 @@ __global__ void k_gq_super(KParams p, const double* key, const double* part, int
 __global__ void k_gq_select_super(KParams p, unsigned* hist, double S, GqSel* sel);
 __global__ void k_gq_bins(KParams p, const double* key, unsigned* hist, const GqSel* sel);
 __global__ void k_gq_select_bin(KParams p, unsigned* hist, double S, GqSel* sel);
-__global__ void k_gq_apply(KParams p, const double* key, const GqSel* sel, uint8_t* action);
-__global__ void k_gq_compact(KParams p, const double* key, const GqSel* sel, uint4* stage, unsigned* bcnt);
+__global__ void k_gq_compact(KParams p, const double* key, const GqSel* sel, uint4* stage, unsigned* bcnt,
+                             uint8_t* action);
 constexpr int kGqRankBlocks = 256;  // k_gq_rank grid
 __global__ void k_gq_gather(const uint4* stage, const unsigned* bcnt, const GqSel* sel, uint4* win);
 __global__ void k_gq_rank(const uint4* win, const GqSel* sel, uint4* sorted);
-__global__ void k_gq_finish(KParams p, const uint4* sorted, double S, double pmin, const GqSel* sel, uint8_t* action,
+__global__ void k_gq_finish(KParams p, const uint4* sorted, double S, double pmin, GqSel* sel, uint8_t* action,
                             int* flag);
 __global__ void k_greedy_inputs(KParams p, double* key, double* power, uint8_t* lock);
 __global__ void k_greedy_iota(int64_t n, int* idx);

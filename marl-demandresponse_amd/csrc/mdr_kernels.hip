@@ -1710,33 +1710,26 @@ __global__ void __launch_bounds__(128) k_gq_select_bin(KParams p, unsigned* __re
   *reinterpret_cast<uint4*>(hist + tid * 4) = make_uint4(0u, 0u, 0u, 0u);
 }
 
-// K6: every house of a bin below b* is taken; the rest start as not taken (K5 sets the window's)
-__global__ void k_gq_apply(KParams p, const double* __restrict__ key, const GqSel* __restrict__ sel,
-                           uint8_t* __restrict__ action) {
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= p.n) return;
-  const double k = key[i];
-  action[i] = sel->all ? 1 : (k == k && gq_bin(k, sel->kmin, sel->scale) < sel->bstar ? 1 : 0);
-}
-
-// K4: the window's houses, staged per block of kGqStage houses (okey, house << 2 | class, lock)
+// K4: every house of a bin below b* is taken, the rest start as not taken (K5c sets the window's);
+// the window's houses are staged per block of kGqStage houses (okey, house << 2 | class, lock)
 __global__ void __launch_bounds__(256) k_gq_compact(KParams p, const double* __restrict__ key,
                                                     const GqSel* __restrict__ sel, uint4* __restrict__ stage,
-                                                    unsigned* __restrict__ bcnt) {
+                                                    unsigned* __restrict__ bcnt, uint8_t* __restrict__ action) {
   __shared__ unsigned s_n;
   if (threadIdx.x == 0) s_n = 0u;
   __syncthreads();
-  const bool on = !sel->all && !sel->overflow;
+  const bool all = sel->all, on = !all && !sel->overflow;
   const int bs = sel->bstar, be = sel->bend;
   const double kmin = sel->kmin, scale = sel->scale;
   const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
-  if (on) {
+  {
     for (int t = threadIdx.x; t < kGqStage; t += blockDim.x) {
       const int64_t i = b0 + t;
       if (i >= p.n) break;
       const double k = key[i];
-      const int b = gq_bin(k, kmin, scale);
-      if (b < bs || b > be) continue;
+      const int b = k == k ? gq_bin(k, kmin, scale) : kGqBins;
+      action[i] = all || b < bs ? 1 : 0;
+      if (!on || b < bs || b > be) continue;
       const unsigned slot = atomicAdd(&s_n, 1u);
       const uint64_t ok = gq_okey(k);
       stage[b0 + slot] = make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), ((uint32_t)i << 2) | (p.cap_idx[i] & 3u),
@@ -1797,7 +1790,7 @@ __global__ void __launch_bounds__(256) k_gq_rank(const uint4* __restrict__ win, 
 // K5c (one workgroup of 1024): the sorted window into LDS, the exact crossing position from
 // base_tot, the window's prefix taken, then the gap walk (k_greedy_walk's rule)
 __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __restrict__ sorted, double S,
-                                                    double pmin, const GqSel* __restrict__ sel,
+                                                    double pmin, GqSel* __restrict__ sel,
                                                     uint8_t* __restrict__ action, int* __restrict__ flag) {
   __shared__ uint4 s_e[kGqCap];
   __shared__ double s_w[16];
@@ -1813,7 +1806,7 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __re
     return cl == 0u ? pon[0] : cl == 1u ? pon[1] : cl == 2u ? pon[2] : pon[3];
   };
   if (sel->all || sel->overflow) {
-    if (tid == 0) *flag = sel->overflow;
+    if (tid == 0) { *flag = sel->overflow; sel->overflow = 0; }  // (the next call starts clear)
     return;
   }
   const int ncand = sel->ncand;
