@@ -134,3 +134,42 @@ def test_interp_rollout_equals_steps(mode):
     sa, sb = a.shard.host_state(), b.shard.host_state()
     for k in sa:
         np.testing.assert_array_equal(sa[k], sb[k])
+
+
+def test_deepcopy_interpolation_env_shares_rng():
+    """TrainingManager.test deep-copies the env (training_manager.py:269).  In interpolation mode
+    the grid's Interpolator holds the generator — here the `random` module itself, the reference's
+    global random, which copy.deepcopy cannot copy: the copy must share it (not fork it), start from
+    the same device state, and step exactly like the original from the same RNG state."""
+    import copy
+
+    import torch
+
+    from mdr_amd.environment import Environment
+
+    n = 3001
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals",
+                                     gu.BPP + "mode": "interpolation", gu.BPP + "interp_update_period": 8,
+                                     gu.BPP + "interp_nb_agents": 32})
+    random.seed(11)
+    env = Environment(props, rng=random, population="synthetic", seed=3)
+    for _ in range(5):
+        env.step_tensor(None, action_mode="random", lookahead="random")
+    twin = copy.deepcopy(env)
+    assert twin.rng is env.rng is random
+    assert twin.power_grid.interp.rng is env.power_grid.interp.rng
+    s0, s1 = env.shard.host_state(), twin.shard.host_state()
+    for k in s0:
+        np.testing.assert_array_equal(s0[k], s1[k])
+    acts = torch.from_numpy(np.random.RandomState(2).randint(0, 2, (12, n)).astype(np.uint8)).to("cuda")
+    out = []
+    for e in (env, twin):  # the same RNG state for each: identical trajectories
+        random.seed(77)
+        out.append(torch.stack([e.step_tensor(acts[t]).clone() for t in range(12)]))
+        out.append(float(e.power_grid.current_signal))
+    assert torch.equal(out[0], out[2])
+    assert out[1] == out[3]
+    s0, s1 = env.shard.host_state(), twin.shard.host_state()
+    for k in s0:
+        np.testing.assert_array_equal(s0[k], s1[k])
