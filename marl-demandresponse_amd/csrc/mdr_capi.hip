@@ -1383,7 +1383,11 @@ static int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_hist, (kGqBins + kGqSuper) * 4 * sizeof(unsigned)));
   HIP_TRY(hipMemset(c->g_hist, 0, (kGqBins + kGqSuper) * 4 * sizeof(unsigned)));  // (k_gq_select re-zeroes it)
   HIP_TRY(hipMalloc(&c->g_sel, 128));
-  HIP_TRY(hipMemset(c->g_sel, 0, 128));
+  {
+    unsigned char init[128] = {};
+    gq_sel_init(init);
+    HIP_TRY(hipMemcpy(c->g_sel, init, 128, hipMemcpyHostToDevice));
+  }
   HIP_TRY(hipMalloc(&c->g_stage, nstage * kGqStage * sizeof(uint4)));
   HIP_TRY(hipMalloc(&c->g_bcnt, nstage * sizeof(unsigned)));
   HIP_TRY(hipMalloc(&c->g_sorted, 2 * kGqCap * sizeof(uint4)));  // [sorted | gathered window]
@@ -1411,12 +1415,10 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
     // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster; the sort form below
     // runs only when the candidate window cannot decide (the flag read back here)
     // (g_sel's only accumulated field, overflow, is cleared by k_gq_finish for the next call)
-    hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_part, c->g_sel);
+    hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_part, c->g_hist, c->g_sel);
     LAUNCH_CHECK("k_gq_keys");
-    hipLaunchKernelGGL(k_gq_super, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_part, kGqParts,
-                       c->g_hist, c->g_sel);
-    LAUNCH_CHECK("k_gq_super");
-    hipLaunchKernelGGL(k_gq_select_super, dim3(1), dim3(256), 0, st, c->kp, c->g_hist, budget, c->g_sel);
+    hipLaunchKernelGGL(k_gq_select_super, dim3(1), dim3(256), 0, st, c->kp, c->g_hist, budget, c->g_part, kGqParts,
+                       c->g_sel);
     LAUNCH_CHECK("k_gq_select_super");
     hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_hist, c->g_sel);
     LAUNCH_CHECK("k_gq_bins");

@@ -145,9 +145,9 @@ constexpr int kGqStage = 4096;  // houses per k_gq_compact block
 constexpr int kGqParts = 256;   // k_gq_keys / k_gq_hist grid
 constexpr int kGqSuper = 256;   // superbins (64 bins each) of the select's first pass
 struct GqSel;
-__global__ void k_gq_keys(KParams p, double* key, double* part, GqSel* sel);
-__global__ void k_gq_super(KParams p, const double* key, const double* part, int nparts, unsigned* hist, GqSel* sel);
-__global__ void k_gq_select_super(KParams p, unsigned* hist, double S, GqSel* sel);
+__global__ void k_gq_keys(KParams p, double* key, double* part, unsigned* hist, GqSel* sel);
+__global__ void k_gq_select_super(KParams p, unsigned* hist, double S, const double* part, int nparts, GqSel* sel);
+void gq_sel_init(void* sel128);  // host: the first call's quantisation (keys in [-32, 32])
 __global__ void k_gq_bins(KParams p, const double* key, unsigned* hist, const GqSel* sel);
 __global__ void k_gq_select_bin(KParams p, unsigned* hist, double S, GqSel* sel);
 __global__ void k_gq_compact(KParams p, const double* key, const GqSel* sel, uint4* stage, unsigned* bcnt,

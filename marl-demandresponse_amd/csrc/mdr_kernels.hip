@@ -1502,33 +1502,49 @@ __global__ void __launch_bounds__(256) k_greedy_walk(int64_t n, const double* __
 // a crossing bin over kGqCap houses, a walk that leaves the window) raise sel.overflow and the
 // host reruns the sort form.
 struct GqSel {
-  double kmin, scale, base_tot;
+  double kmin, scale, base_tot;  // (kmin, scale): this call's quantisation (the previous call's key range)
   unsigned long long base_cnt, total;
   int bstar, bend, all, overflow, more_after, ncand, sb;
+  double nkmin, nscale;          // the range of this call's keys, for the next call
 };
 static_assert(sizeof(GqSel) <= 128, "GqSel fits the 128-B sel buffer");
+void gq_sel_init(void* sel128) {
+  GqSel* g = static_cast<GqSel*>(sel128);  // (a zeroed 128-B host buffer)
+  g->kmin = -32.0;
+  g->scale = (double)kGqBins / 64.0;
+}
 
 // okey: -0.0 folded onto +0.0 (value order, numpy's stable argsort), sign-magnitude -> unsigned
 __device__ __forceinline__ uint64_t gq_okey(double k) {
   const uint64_t b = (uint64_t)__double_as_longlong(k + 0.0);
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
+// monotone non-decreasing in k for ANY (kmin, scale >= 0) — keys outside the range clamp to the end
+// bins — so a stale range (the previous call's) only costs window size, never exactness
 __device__ __forceinline__ int gq_bin(double k, double kmin, double scale) {
-  const double d = (k - kmin) * scale;  // k >= kmin: monotone non-decreasing in k
-  return d >= (double)(kGqBins - 1) ? kGqBins - 1 : (int)d;
+  const double d = (k - kmin) * scale;
+  return d >= (double)(kGqBins - 1) ? kGqBins - 1 : (d > 0.0 ? (int)d : 0);
 }
 
-// K1: keys + per-block (min, max) of the finite keys; a NaN key raises the overflow flag
+// K1: keys, per-block (min, max) of the finite keys (the next call's range), and the class counts
+// per superbin (kGqBins / kGqSuper consecutive bins) under this call's quantisation; a NaN key
+// raises the overflow flag
 __global__ void __launch_bounds__(256) k_gq_keys(KParams p, double* __restrict__ key, double* __restrict__ part,
-                                                 GqSel* __restrict__ sel) {
+                                                 unsigned* __restrict__ hist, GqSel* __restrict__ sel) {
+  __shared__ unsigned s_sh[4][kGqSuper * 4];  // one copy per wave (less atomic contention on hot superbins)
   __shared__ double s_lo[4], s_hi[4];
+  for (int e = threadIdx.x; e < 4 * kGqSuper * 4; e += blockDim.x) (&s_sh[0][0])[e] = 0u;
+  __syncthreads();
+  const double kmin = sel->kmin, scale = sel->scale;
   double lo = INFINITY, hi = -INFINITY;
   bool nan = false;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (int64_t)gridDim.x * blockDim.x) {
     const double k = -(p.t_air[i] - p.target[i]);
     key[i] = k;
-    if (k != k) nan = true;
-    else { lo = fmin(lo, k); hi = fmax(hi, k); }
+    if (k != k) { nan = true; continue; }
+    lo = fmin(lo, k);
+    hi = fmax(hi, k);
+    atomicAdd(&s_sh[threadIdx.x >> 6][(gq_bin(k, kmin, scale) / (kGqBins / kGqSuper)) * 4 + (p.cap_idx[i] & 3u)], 1u);
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -1542,36 +1558,6 @@ __global__ void __launch_bounds__(256) k_gq_keys(KParams p, double* __restrict__
     part[2 * blockIdx.x] = fmin(fmin(s_lo[0], s_lo[1]), fmin(s_lo[2], s_lo[3]));
     part[2 * blockIdx.x + 1] = fmax(fmax(s_hi[0], s_hi[1]), fmax(s_hi[2], s_hi[3]));
   }
-}
-
-// K2a: every block reduces the partials (the same bits in every block) and counts its houses per
-// superbin (kGqBins / kGqSuper consecutive bins) and class; block 0 publishes kmin / scale
-__global__ void __launch_bounds__(256) k_gq_super(KParams p, const double* __restrict__ key,
-                                                  const double* __restrict__ part, int nparts,
-                                                  unsigned* __restrict__ hist, GqSel* __restrict__ sel) {
-  __shared__ unsigned s_sh[4][kGqSuper * 4];  // one copy per wave (less atomic contention on hot superbins)
-  __shared__ double s_lo[4], s_hi[4];
-  double lo = INFINITY, hi = -INFINITY;
-  for (int b = threadIdx.x; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    lo = fmin(lo, __shfl_xor(lo, off));
-    hi = fmax(hi, __shfl_xor(hi, off));
-  }
-  if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
-  for (int e = threadIdx.x; e < 4 * kGqSuper * 4; e += blockDim.x) (&s_sh[0][0])[e] = 0u;
-  __syncthreads();
-  const double kmin = fmin(fmin(s_lo[0], s_lo[1]), fmin(s_lo[2], s_lo[3]));
-  const double kmax = fmax(fmax(s_hi[0], s_hi[1]), fmax(s_hi[2], s_hi[3]));
-  const double range = kmax - kmin;
-  const double scale = range > 0.0 && range < INFINITY ? (double)kGqBins / range : 0.0;
-  if (blockIdx.x == 0 && threadIdx.x == 0) { sel->kmin = kmin; sel->scale = scale; }
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (int64_t)gridDim.x * blockDim.x) {
-    const double k = key[i];
-    if (k != k) continue;
-    atomicAdd(&s_sh[threadIdx.x >> 6][(gq_bin(k, kmin, scale) / (kGqBins / kGqSuper)) * 4 + (p.cap_idx[i] & 3u)], 1u);
-  }
-  __syncthreads();
   for (int e = threadIdx.x; e < kGqSuper * 4; e += blockDim.x) {
     const unsigned v = s_sh[0][e] + s_sh[1][e] + s_sh[2][e] + s_sh[3][e];
     if (v) atomicAdd(&hist[kGqBins * 4 + e], v);
@@ -1581,9 +1567,28 @@ __global__ void __launch_bounds__(256) k_gq_super(KParams p, const double* __res
 // K3a (one workgroup, thread t = superbin t): the superbin where the cumulative P crosses S, the P
 // and house count before it (sums of P: exact for integer P); zeroes the superbin histogram
 __global__ void __launch_bounds__(256) k_gq_select_super(KParams p, unsigned* __restrict__ hist, double S,
+                                                         const double* __restrict__ part, int nparts,
                                                          GqSel* __restrict__ sel) {
   static_assert(kGqSuper == 256, "one superbin per thread");
-  __shared__ double s_w[4];
+  __shared__ double s_w[4], s_lo[4], s_hi[4];
+  {  // the next call's range: (min, max) of this call's keys
+    double lo = INFINITY, hi = -INFINITY;
+    for (int b = threadIdx.x; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      lo = fmin(lo, __shfl_xor(lo, off));
+      hi = fmax(hi, __shfl_xor(hi, off));
+    }
+    if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const double kmin = fmin(fmin(s_lo[0], s_lo[1]), fmin(s_lo[2], s_lo[3]));
+      const double kmax = fmax(fmax(s_hi[0], s_hi[1]), fmax(s_hi[2], s_hi[3]));
+      const double range = kmax - kmin;
+      sel->nkmin = kmin == kmin && kmin < INFINITY ? kmin : 0.0;
+      sel->nscale = range > 0.0 && range < INFINITY ? (double)kGqBins / range : 0.0;
+    }
+  }
   __shared__ unsigned long long s_wc[4];
   __shared__ int s_first;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -1608,7 +1613,7 @@ __global__ void __launch_bounds__(256) k_gq_select_super(KParams p, unsigned* __
   double before = x - ps;
   unsigned long long beforec = xc - cs;
   for (int w = 0; w < wv; ++w) { before += s_w[w]; beforec += s_wc[w]; }
-  if (!(before + ps < S)) atomicMin(&s_first, tid);
+  if (cs > 0 && !(before + ps < S)) atomicMin(&s_first, tid);  // (the first position: a non-empty superbin)
   __syncthreads();
   if (tid == s_first) { sel->base_tot = before; sel->base_cnt = beforec; }
   if (tid == 0) {
@@ -1674,7 +1679,7 @@ __global__ void __launch_bounds__(128) k_gq_select_bin(KParams p, unsigned* __re
     }
     const double bef = sel->base_tot + (xb - pb);
     const unsigned long long befc = sel->base_cnt + (xcb - cb);
-    const unsigned long long m = __ballot(!(bef + pb < S));
+    const unsigned long long m = __ballot(cb > 0 && !(bef + pb < S));
     const int l0 = m ? __ffsll((long long)m) - 1 : 63;
     if (lane == l0) { s_l0 = l0; s_base = bef; s_basec = befc; }
   }
@@ -1806,7 +1811,12 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __re
     return cl == 0u ? pon[0] : cl == 1u ? pon[1] : cl == 2u ? pon[2] : pon[3];
   };
   if (sel->all || sel->overflow) {
-    if (tid == 0) { *flag = sel->overflow; sel->overflow = 0; }  // (the next call starts clear)
+    if (tid == 0) {
+      *flag = sel->overflow;
+      sel->overflow = 0;  // (the next call starts clear, with this call's key range)
+      sel->kmin = sel->nkmin;
+      sel->scale = sel->nscale;
+    }
     return;
   }
   const int ncand = sel->ncand;
@@ -1858,6 +1868,8 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __re
       if (j >= ncand && sel->more_after && tot < S && !(2.0 * (S - tot) < pmin * (1.0 - 1e-9))) ovf = 1;
     }
     *flag = ovf;
+    sel->kmin = sel->nkmin;  // (every kernel of this call has read the quantisation)
+    sel->scale = sel->nscale;
   }
 }
 

@@ -1,5 +1,6 @@
 #!/bin/bash
 # A/B of the rollout path: 20-step (driver) and 2000-step bench lines under variants.
+# (wt20/wt2000 need the write-through variant built first: python marl-demandresponse_amd/build_ext.py --variant wt MDR_REWARD_WT)
 #   default lib, launch-first graph | MDR_NO_LAUNCH_FIRST | --graph off | write-through reward lib
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
