@@ -78,7 +78,9 @@ def parse():
     ap.add_argument("--window", type=int, default=32,
                     help="ticks per temporally blocked launch (k_step_window, <= 32); 0 = one launch per tick")
     ap.add_argument("--kernel-ticks", type=int, default=1024,
-                    help="ticks of the kernel-only timing after the timed region (roofline.kernel_avg_us)")
+                    help="ticks per kernel-only timing call after the timed region (roofline.kernel_avg_us)")
+    ap.add_argument("--kernel-reps", type=int, default=16,
+                    help="kernel-only timing calls (16 x 1024 ticks = 512 timed launches of the 32-tick window kernel)")
     ap.add_argument("--kernel-warm-ticks", type=int, default=2048,
                     help="untimed kernel-only ticks before that timing (the GPU at its steady-state clock)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0, help="cpu_baseline time budget")
@@ -433,11 +435,15 @@ def main():
         # (mdr_time_step_kernels), averaged over its launches
         for _ in range(max(args.kernel_warm_ticks, 0) // kt):
             sh.rollout(env.driver_window(kt), kacts, n_loc if kacts is not None else 0, mode_id, kbuf, n_loc, True)
-        step_ms, launches = sh.time_step_kernels(env.driver_window(kt), kacts, n_loc if kacts is not None else 0,
-                                                 mode_id, kbuf, n_loc)
+        step_ms, launches = 0.0, 0
+        for _ in range(max(args.kernel_reps, 1)):
+            ms_r, l_r = sh.time_step_kernels(env.driver_window(kt), kacts, n_loc if kacts is not None else 0,
+                                             mode_id, kbuf, n_loc)
+            step_ms += ms_r
+            launches += l_r
         del kbuf
         kern_ms = step_ms / launches
-        k_win = kt // launches if window > 0 else 1
+        k_win = kt * max(args.kernel_reps, 1) // launches if window > 0 else 1
         bytes_launch = window_bytes(n_loc, k_win, args.mode) if window > 0 else BYTES_PER_HOUSE_STEP * n_loc
         steps_launch = k_win
     elif g_act is not None:
@@ -510,8 +516,9 @@ def main():
                      "house_steps_per_launch": steps_launch * n_loc,
                      "algorithmic_bytes_per_launch": bytes_launch,
                      "bytes_per_house_step": bytes_launch / (steps_launch * n_loc),
-                     "timing": "hipExtLaunchKernel start/stop events around each step-kernel launch of a 1024-tick rollout "
-                  "after the timed region and 2048 untimed kernel-only ticks (steady-state clock)",
+                     "timing": f"hipExtLaunchKernel start/stop events around each step-kernel launch of {max(args.kernel_reps, 1)} "
+                               f"{kt}-tick rollouts after the timed region and {args.kernel_warm_ticks} untimed kernel-only "
+                               "ticks (steady-state clock)",
                      "valu": valu_roofline(kern, n_loc, kern_ms)},
     }
     if g_act is not None:
