@@ -246,6 +246,9 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     PSTAMP(2);
 
     // ---- layer 1: acc1[mb] = b1 + W1 · X  (X^T columns = this wave's 32 houses)
+    // (the wave in its MFMA phases gets issue priority over the SIMD's other wave, which is then
+    // building observations or running the output layer on the VALU: C5 actor 151 -> 141 us at 1M)
+    __builtin_amdgcn_s_setprio(3);
     const float* xrow = w_obs + r * FS + 8 * h;
     f32x16 acc1[kActorMB];
 #pragma unroll
@@ -315,6 +318,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
 #pragma unroll
       for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], hh[q], acc2[mb], 0, 0, 0);
     }
+    __builtin_amdgcn_s_setprio(0);
     PSTAMP(4);
 
     // ---- output layer (fp32 VALU): this lane's 64 hidden rows, then the partner half's
