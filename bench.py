@@ -458,7 +458,8 @@ def main():
         launches, kern_ms = K, ev0.elapsed_time(ev1) / K
         bytes_launch = (BYTES_PER_HOUSE_STEP + GREEDY_EXTRA) * n_loc
         steps_launch = 1
-        kern = "greedy tick: k_greedy_keys + hipCUB radix sort + scan + k_greedy_walk + k_step"
+        kern = ("greedy tick: histogram select (k_gq_keys, k_gq_select_super, k_gq_bins, k_gq_select_bin, "
+                "k_gq_compact, k_gq_gather, k_gq_rank, k_gq_finish) + k_power_counts + k_step_pipe")
     else:
         # the actor rollout graph interleaves k_actor and k_step: time the actor alone
         K = 50
