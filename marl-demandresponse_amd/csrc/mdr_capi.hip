@@ -1380,8 +1380,8 @@ static int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_extra, 64 * sizeof(int64_t)));
   const int64_t nstage = (n + kGqStage - 1) / kGqStage;
   HIP_TRY(hipMalloc(&c->g_part, 2 * kGqParts * sizeof(double)));
-  HIP_TRY(hipMalloc(&c->g_hist, (kGqBins + kGqSuper) * 4 * sizeof(unsigned)));
-  HIP_TRY(hipMemset(c->g_hist, 0, (kGqBins + kGqSuper) * 4 * sizeof(unsigned)));  // (k_gq_select re-zeroes it)
+  HIP_TRY(hipMalloc(&c->g_hist, (kGqBins + kGqSuper * kGqCopies) * 4 * sizeof(unsigned)));
+  HIP_TRY(hipMemset(c->g_hist, 0, (kGqBins + kGqSuper * kGqCopies) * 4 * sizeof(unsigned)));  // (k_gq_select re-zeroes it)
   HIP_TRY(hipMalloc(&c->g_sel, 128));
   {
     unsigned char init[128] = {};
@@ -1415,17 +1415,17 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
     // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster; the sort form below
     // runs only when the candidate window cannot decide (the flag read back here)
     // (g_sel's only accumulated field, overflow, is cleared by k_gq_finish for the next call)
-    hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_part, c->g_hist, c->g_sel);
+    hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_part, c->g_hist, c->g_sel);
     LAUNCH_CHECK("k_gq_keys");
     hipLaunchKernelGGL(k_gq_select_super, dim3(1), dim3(256), 0, st, c->kp, c->g_hist, budget, c->g_part, kGqParts,
                        c->g_sel);
     LAUNCH_CHECK("k_gq_select_super");
-    hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(256), 0, st, c->kp, c->g_key, c->g_hist, c->g_sel);
+    hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_hist, c->g_sel);
     LAUNCH_CHECK("k_gq_bins");
     hipLaunchKernelGGL(k_gq_select_bin, dim3(1), dim3(128), 0, st, c->kp, c->g_hist, budget, c->g_sel);
     LAUNCH_CHECK("k_gq_select_bin");
     const int nstage = (n + kGqStage - 1) / kGqStage;
-    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(256), 0, st, c->kp, c->g_key, c->g_sel, c->g_stage, c->g_bcnt,
+    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_sel, c->g_stage, c->g_bcnt,
                        action);
     LAUNCH_CHECK("k_gq_compact");
     hipLaunchKernelGGL(k_gq_gather, dim3(nstage), dim3(256), 0, st, c->g_stage, c->g_bcnt, c->g_sel, c->g_sorted + kGqCap);

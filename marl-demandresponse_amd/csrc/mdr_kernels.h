@@ -142,7 +142,10 @@ constexpr int kGqBins = 16384;  // histogram-select greedy: key bins
 constexpr int kGqCap = 4096;    // candidate window capacity (LDS, 16 B per house)
 constexpr int kGqAfter = 256;   // window houses past the crossing bin (the gap walk's room)
 constexpr int kGqStage = 4096;  // houses per k_gq_compact block
-constexpr int kGqParts = 256;   // k_gq_keys / k_gq_hist grid
+constexpr int kGqParts = 256;   // k_gq_keys / k_gq_bins grid (one block per CU)
+constexpr int kGqThreads = 1024; // k_gq_keys / k_gq_bins / k_gq_compact block size
+constexpr int kGqCopies = 8;    // copies of the global superbin / bin histograms (blockIdx % kGqCopies)
+constexpr int kGqUnroll = 4;    // houses per thread per pass of k_gq_keys / k_gq_bins
 constexpr int kGqSuper = 256;   // superbins (64 bins each) of the select's first pass
 struct GqSel;
 __global__ void k_gq_keys(KParams p, double* key, double* part, unsigned* hist, GqSel* sel);

@@ -1529,22 +1529,40 @@ __device__ __forceinline__ int gq_bin(double k, double kmin, double scale) {
 // K1: keys, per-block (min, max) of the finite keys (the next call's range), and the class counts
 // per superbin (kGqBins / kGqSuper consecutive bins) under this call's quantisation; a NaN key
 // raises the overflow flag
-__global__ void __launch_bounds__(256) k_gq_keys(KParams p, double* __restrict__ key, double* __restrict__ part,
-                                                 unsigned* __restrict__ hist, GqSel* __restrict__ sel) {
-  __shared__ unsigned s_sh[4][kGqSuper * 4];  // one copy per wave (less atomic contention on hot superbins)
-  __shared__ double s_lo[4], s_hi[4];
-  for (int e = threadIdx.x; e < 4 * kGqSuper * 4; e += blockDim.x) (&s_sh[0][0])[e] = 0u;
+__global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, double* __restrict__ key, double* __restrict__ part,
+                                                        unsigned* __restrict__ hist, GqSel* __restrict__ sel) {
+  constexpr int NW = kGqThreads / 64;
+  __shared__ unsigned s_sh[NW][kGqSuper * 4];  // one copy per wave (less atomic contention on hot superbins)
+  __shared__ double s_lo[NW], s_hi[NW];
+  for (int e = threadIdx.x; e < NW * kGqSuper * 4; e += blockDim.x) (&s_sh[0][0])[e] = 0u;
   __syncthreads();
   const double kmin = sel->kmin, scale = sel->scale;
   double lo = INFINITY, hi = -INFINITY;
   bool nan = false;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (int64_t)gridDim.x * blockDim.x) {
-    const double k = -(p.t_air[i] - p.target[i]);
-    key[i] = k;
-    if (k != k) { nan = true; continue; }
-    lo = fmin(lo, k);
-    hi = fmax(hi, k);
-    atomicAdd(&s_sh[threadIdx.x >> 6][(gq_bin(k, kmin, scale) / (kGqBins / kGqSuper)) * 4 + (p.cap_idx[i] & 3u)], 1u);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  // kGqUnroll houses per thread per pass, every load issued before the first use (the grid is one
+  // block per CU: without the batch each pass waits out a full HBM latency)
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < p.n; i0 += kGqUnroll * stride) {
+    double ta[kGqUnroll], tg[kGqUnroll];
+    unsigned cl[kGqUnroll];
+#pragma unroll
+    for (int u = 0; u < kGqUnroll; ++u) {
+      const int64_t i = i0 + u * stride;
+      ta[u] = i < p.n ? p.t_air[i] : 0.0;
+      tg[u] = i < p.n ? p.target[i] : 0.0;
+      cl[u] = i < p.n ? p.cap_idx[i] : 0u;
+    }
+#pragma unroll
+    for (int u = 0; u < kGqUnroll; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= p.n) break;
+      const double k = -(ta[u] - tg[u]);
+      key[i] = k;
+      if (k != k) { nan = true; continue; }
+      lo = fmin(lo, k);
+      hi = fmax(hi, k);
+      atomicAdd(&s_sh[threadIdx.x >> 6][(gq_bin(k, kmin, scale) / (kGqBins / kGqSuper)) * 4 + (cl[u] & 3u)], 1u);
+    }
   }
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -1555,12 +1573,16 @@ __global__ void __launch_bounds__(256) k_gq_keys(KParams p, double* __restrict__
   if (__any(nan) && (threadIdx.x & 63) == 0) sel->overflow = 1;
   __syncthreads();
   if (threadIdx.x == 0) {
-    part[2 * blockIdx.x] = fmin(fmin(s_lo[0], s_lo[1]), fmin(s_lo[2], s_lo[3]));
-    part[2 * blockIdx.x + 1] = fmax(fmax(s_hi[0], s_hi[1]), fmax(s_hi[2], s_hi[3]));
+    double l = s_lo[0], h = s_hi[0];
+    for (int w = 1; w < NW; ++w) { l = fmin(l, s_lo[w]); h = fmax(h, s_hi[w]); }
+    part[2 * blockIdx.x] = l;
+    part[2 * blockIdx.x + 1] = h;
   }
   for (int e = threadIdx.x; e < kGqSuper * 4; e += blockDim.x) {
-    const unsigned v = s_sh[0][e] + s_sh[1][e] + s_sh[2][e] + s_sh[3][e];
-    if (v) atomicAdd(&hist[kGqBins * 4 + e], v);
+    unsigned v = 0u;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += s_sh[w][e];
+    if (v) atomicAdd(&hist[kGqBins * 4 + (blockIdx.x % kGqCopies) * (kGqSuper * 4) + e], v);  // (kGqCopies copies: fewer atomics per address)
   }
 }
 
@@ -1595,8 +1617,12 @@ __global__ void __launch_bounds__(256) k_gq_select_super(KParams p, unsigned* __
   double p_on[kWinCap];
 #pragma unroll
   for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
-  const uint4 v = *reinterpret_cast<const uint4*>(hist + kGqBins * 4 + tid * 4);
-  unsigned long long c[kWinCap] = {v.x, v.y, v.z, v.w};
+  unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
+#pragma unroll
+  for (int q = 0; q < kGqCopies; ++q) {  // (the copies k_gq_keys spread its atomics over; zeroed below)
+    const uint4 v = *reinterpret_cast<const uint4*>(hist + kGqBins * 4 + q * (kGqSuper * 4) + tid * 4);
+    c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] += v.w;
+  }
   const double ps = win_power(p, c, p_on);
   const unsigned long long cs = c[0] + c[1] + c[2] + c[3];
   double x = ps;
@@ -1621,30 +1647,44 @@ __global__ void __launch_bounds__(256) k_gq_select_super(KParams p, unsigned* __
     sel->all = s_first >= kGqSuper;
     sel->total = s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
   }
-  *reinterpret_cast<uint4*>(hist + kGqBins * 4 + tid * 4) = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int q = 0; q < kGqCopies; ++q)
+    *reinterpret_cast<uint4*>(hist + kGqBins * 4 + q * (kGqSuper * 4) + tid * 4) = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // K2b: class counts of the bins of superbins sb and sb + 1 (the crossing superbin and the room
 // after it), from the houses in them only
-__global__ void __launch_bounds__(256) k_gq_bins(KParams p, const double* __restrict__ key,
-                                                 unsigned* __restrict__ hist, const GqSel* __restrict__ sel) {
-  constexpr int NB = 2 * (kGqBins / kGqSuper);
-  __shared__ unsigned s_h[4][NB * 4];
+__global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const double* __restrict__ key,
+                                                        unsigned* __restrict__ hist, const GqSel* __restrict__ sel) {
+  constexpr int NB = 2 * (kGqBins / kGqSuper), NW = kGqThreads / 64;
+  __shared__ unsigned s_h[NW][NB * 4];
   if (sel->all || sel->overflow) return;
-  for (int e = threadIdx.x; e < 4 * NB * 4; e += blockDim.x) (&s_h[0][0])[e] = 0u;
+  for (int e = threadIdx.x; e < NW * NB * 4; e += blockDim.x) (&s_h[0][0])[e] = 0u;
   __syncthreads();
   const int bb = sel->sb * (kGqBins / kGqSuper);
   const double kmin = sel->kmin, scale = sel->scale;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < p.n; i += (int64_t)gridDim.x * blockDim.x) {
-    const double k = key[i];
-    if (k != k) continue;
-    const int b = gq_bin(k, kmin, scale) - bb;
-    if (b >= 0 && b < NB) atomicAdd(&s_h[threadIdx.x >> 6][b * 4 + (p.cap_idx[i] & 3u)], 1u);
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < p.n; i0 += kGqUnroll * stride) {
+    double kk[kGqUnroll];
+#pragma unroll
+    for (int u = 0; u < kGqUnroll; ++u) {
+      const int64_t i = i0 + u * stride;
+      kk[u] = i < p.n ? key[i] : NAN;
+    }
+#pragma unroll
+    for (int u = 0; u < kGqUnroll; ++u) {
+      const double k = kk[u];
+      if (k != k) continue;
+      const int b = gq_bin(k, kmin, scale) - bb;
+      if (b >= 0 && b < NB) atomicAdd(&s_h[threadIdx.x >> 6][b * 4 + (p.cap_idx[i0 + u * stride] & 3u)], 1u);
+    }
   }
   __syncthreads();
   for (int e = threadIdx.x; e < NB * 4; e += blockDim.x) {
-    const unsigned v = s_h[0][e] + s_h[1][e] + s_h[2][e] + s_h[3][e];
-    if (v) atomicAdd(&hist[e], v);
+    unsigned v = 0u;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += s_h[w][e];
+    if (v) atomicAdd(&hist[(blockIdx.x % kGqCopies) * (NB * 4) + e], v);
   }
 }
 
@@ -1653,6 +1693,7 @@ __global__ void __launch_bounds__(256) k_gq_bins(KParams p, const double* __rest
 __global__ void __launch_bounds__(128) k_gq_select_bin(KParams p, unsigned* __restrict__ hist, double S,
                                                        GqSel* __restrict__ sel) {
   static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
+  static_assert(kGqCopies * 512 <= kGqBins * 4, "the bin copies fit below the superbin copies");
   __shared__ unsigned s_c[128];
   __shared__ int s_l0;
   __shared__ double s_base;
@@ -1663,9 +1704,13 @@ __global__ void __launch_bounds__(128) k_gq_select_bin(KParams p, unsigned* __re
   double p_on[kWinCap];
 #pragma unroll
   for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
-  const uint4 v = *reinterpret_cast<const uint4*>(hist + tid * 4);
-  unsigned long long c[kWinCap] = {v.x, v.y, v.z, v.w};
-  s_c[tid] = v.x + v.y + v.z + v.w;
+  unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
+#pragma unroll
+  for (int q = 0; q < kGqCopies; ++q) {  // (k_gq_bins' copies, 128 bins x 4 classes each; zeroed below)
+    const uint4 v = *reinterpret_cast<const uint4*>(hist + q * 512 + tid * 4);
+    c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] += v.w;
+  }
+  s_c[tid] = (unsigned)(c[0] + c[1] + c[2] + c[3]);
   if (tid < 64 && on) {  // wave 0: the crossing bin of superbin sb (it crosses: K3a)
     const double pb = win_power(p, c, p_on);
     const unsigned long long cb = c[0] + c[1] + c[2] + c[3];
@@ -1712,12 +1757,13 @@ __global__ void __launch_bounds__(128) k_gq_select_bin(KParams p, unsigned* __re
       sel->ncand = cnt;
     }
   }
-  *reinterpret_cast<uint4*>(hist + tid * 4) = make_uint4(0u, 0u, 0u, 0u);
+#pragma unroll
+  for (int q = 0; q < kGqCopies; ++q) *reinterpret_cast<uint4*>(hist + q * 512 + tid * 4) = make_uint4(0u, 0u, 0u, 0u);
 }
 
 // K4: every house of a bin below b* is taken, the rest start as not taken (K5c sets the window's);
 // the window's houses are staged per block of kGqStage houses (okey, house << 2 | class, lock)
-__global__ void __launch_bounds__(256) k_gq_compact(KParams p, const double* __restrict__ key,
+__global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const double* __restrict__ key,
                                                     const GqSel* __restrict__ sel, uint4* __restrict__ stage,
                                                     unsigned* __restrict__ bcnt, uint8_t* __restrict__ action) {
   __shared__ unsigned s_n;
@@ -1727,11 +1773,19 @@ __global__ void __launch_bounds__(256) k_gq_compact(KParams p, const double* __r
   const int bs = sel->bstar, be = sel->bend;
   const double kmin = sel->kmin, scale = sel->scale;
   const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
+  constexpr int U = kGqStage / kGqThreads;
+  double kk[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {  // (every load before the first use)
+    const int64_t i = b0 + u * kGqThreads + threadIdx.x;
+    kk[u] = i < p.n ? key[i] : 0.0;
+  }
   {
-    for (int t = threadIdx.x; t < kGqStage; t += blockDim.x) {
-      const int64_t i = b0 + t;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = b0 + u * kGqThreads + threadIdx.x;
       if (i >= p.n) break;
-      const double k = key[i];
+      const double k = kk[u];
       const int b = k == k ? gq_bin(k, kmin, scale) : kGqBins;
       action[i] = all || b < bs ? 1 : 0;
       if (!on || b < bs || b > be) continue;
@@ -1778,17 +1832,46 @@ __global__ void __launch_bounds__(256) k_gq_rank(const uint4* __restrict__ win, 
   if (sel->all || sel->overflow) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nth = blockDim.x;
   const int ncand = sel->ncand;
-  for (int e = tid; e < ncand; e += nth) s_e[e] = win[e];
-  __syncthreads();
-  const int nwv = (int)gridDim.x * (nth >> 6);
-  for (int e = (int)blockIdx.x * (nth >> 6) + wv; e < ncand; e += nwv) {
-    const uint4 me = s_e[e];
-    unsigned r = 0;
-#pragma unroll 4
-    for (int f = lane; f < ncand; f += 64) r += gq_less(s_e[f], me) ? 1u : 0u;
+  {
+    constexpr int U = kGqCap / 256;  // (blockDim 256: every load issued before the LDS stores)
+    uint4 v[U];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) r += __shfl_xor(r, off);
-    if (lane == 0) sorted[r] = me;
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + u * 256;
+      if (e < ncand) v[u] = win[e];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + u * 256;
+      if (e < ncand) s_e[e] = v[u];
+    }
+  }
+  __syncthreads();
+  // each wave ranks EPW houses at once: one LDS read of a window house serves all EPW comparisons
+  constexpr int EPW = kGqCap / (kGqRankBlocks * 4);
+  static_assert(EPW * kGqRankBlocks * 4 == kGqCap, "launch: kGqRankBlocks x 256 threads cover the window");
+  const int nwv = (int)gridDim.x * (nth >> 6);
+  const int e0 = (int)blockIdx.x * (nth >> 6) + wv;
+  if (e0 >= ncand) return;  // (wave-uniform; no barrier follows)
+  uint4 me[EPW];
+  unsigned r[EPW];
+#pragma unroll
+  for (int j = 0; j < EPW; ++j) {
+    const int e = e0 + j * nwv;
+    me[j] = e < ncand ? s_e[e] : make_uint4(0u, 0u, 0u, 0u);
+    r[j] = 0u;
+  }
+#pragma unroll 2
+  for (int f = lane; f < ncand; f += 64) {
+    const uint4 o = s_e[f];
+#pragma unroll
+    for (int j = 0; j < EPW; ++j) r[j] += gq_less(o, me[j]) ? 1u : 0u;
+  }
+#pragma unroll
+  for (int j = 0; j < EPW; ++j) {
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) r[j] += __shfl_xor(r[j], off);
+    if (lane == 0 && e0 + j * nwv < ncand) sorted[r[j]] = me[j];
   }
 }
 
@@ -1820,7 +1903,20 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __re
     return;
   }
   const int ncand = sel->ncand;
-  for (int e = tid; e < ncand; e += nth) s_e[e] = sorted[e];
+  {
+    constexpr int U = kGqCap / 1024;  // (blockDim 1024: every load issued before the LDS stores)
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + u * 1024;
+      if (e < ncand) v[u] = sorted[e];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + u * 1024;
+      if (e < ncand) s_e[e] = v[u];
+    }
+  }
   if (tid == 0) { s_tot = sel->base_tot; s_k = -1; }
   __syncthreads();
   for (int c0 = 0; c0 < ncand; c0 += nth) {
