@@ -1430,7 +1430,7 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
     LAUNCH_CHECK("k_gq_compact");
     hipLaunchKernelGGL(k_gq_gather, dim3(nstage), dim3(256), 0, st, c->g_stage, c->g_bcnt, c->g_sel, c->g_sorted + kGqCap);
     LAUNCH_CHECK("k_gq_gather");
-    hipLaunchKernelGGL(k_gq_rank, dim3(kGqRankBlocks), dim3(256), 0, st, c->g_sorted + kGqCap, c->g_sel, c->g_sorted);
+    hipLaunchKernelGGL(k_gq_rank, dim3(kGqRankBlocks), dim3(kGqRankThreads), 0, st, c->g_sorted + kGqCap, c->g_sel, c->g_sorted);
     LAUNCH_CHECK("k_gq_rank");
     hipLaunchKernelGGL(k_gq_finish, dim3(1), dim3(1024), 0, st, c->kp, c->g_sorted, budget, pmin, c->g_sel, action,
                        c->g_flag);

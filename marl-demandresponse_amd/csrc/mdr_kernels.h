@@ -156,6 +156,7 @@ __global__ void k_gq_select_bin(KParams p, unsigned* hist, double S, GqSel* sel)
 __global__ void k_gq_compact(KParams p, const double* key, const GqSel* sel, uint4* stage, unsigned* bcnt,
                              uint8_t* action);
 constexpr int kGqRankBlocks = 256;  // k_gq_rank grid
+constexpr int kGqRankThreads = 1024;  // k_gq_rank block size
 __global__ void k_gq_gather(const uint4* stage, const unsigned* bcnt, const GqSel* sel, uint4* win);
 __global__ void k_gq_rank(const uint4* win, const GqSel* sel, uint4* sorted);
 __global__ void k_gq_finish(KParams p, const uint4* sorted, double S, double pmin, GqSel* sel, uint8_t* action,

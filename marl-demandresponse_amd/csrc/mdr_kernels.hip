@@ -1826,30 +1826,31 @@ __global__ void __launch_bounds__(256) k_gq_gather(const uint4* __restrict__ sta
 // K5b (kGqRankBlocks workgroups): the window into LDS; one wave per house computes its rank (how
 // many window houses precede it in (key, house) order, the lanes splitting the comparisons) and
 // writes it to sorted[rank]
-__global__ void __launch_bounds__(256) k_gq_rank(const uint4* __restrict__ win, const GqSel* __restrict__ sel,
+__global__ void __launch_bounds__(kGqRankThreads) k_gq_rank(const uint4* __restrict__ win, const GqSel* __restrict__ sel,
                                                  uint4* __restrict__ sorted) {
   __shared__ uint4 s_e[kGqCap];
   if (sel->all || sel->overflow) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nth = blockDim.x;
   const int ncand = sel->ncand;
   {
-    constexpr int U = kGqCap / 256;  // (blockDim 256: every load issued before the LDS stores)
+    constexpr int U = kGqCap / kGqRankThreads;  // (every load issued before the LDS stores)
     uint4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int e = tid + u * 256;
+      const int e = tid + u * kGqRankThreads;
       if (e < ncand) v[u] = win[e];
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
-      const int e = tid + u * 256;
+      const int e = tid + u * kGqRankThreads;
       if (e < ncand) s_e[e] = v[u];
     }
   }
   __syncthreads();
-  // each wave ranks EPW houses at once: one LDS read of a window house serves all EPW comparisons
-  constexpr int EPW = kGqCap / (kGqRankBlocks * 4);
-  static_assert(EPW * kGqRankBlocks * 4 == kGqCap, "launch: kGqRankBlocks x 256 threads cover the window");
+  // each wave ranks EPW houses at once (one LDS read of a window house serves all EPW comparisons);
+  // 16 waves per CU hide the LDS latency of the comparison loop
+  constexpr int EPW = kGqCap / (kGqRankBlocks * (kGqRankThreads / 64));
+  static_assert(EPW >= 1 && EPW * kGqRankBlocks * (kGqRankThreads / 64) == kGqCap, "the launch covers the window");
   const int nwv = (int)gridDim.x * (nth >> 6);
   const int e0 = (int)blockIdx.x * (nth >> 6) + wv;
   if (e0 >= ncand) return;  // (wave-uniform; no barrier follows)
