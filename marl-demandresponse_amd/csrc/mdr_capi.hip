@@ -202,7 +202,7 @@ int launch_counts(mdr_ctx* c, const uint8_t* action, int mode, uint64_t tick, co
   int m = mode;
   if (m == MDR_ACT_BANGBANG || m == MDR_ACT_DEADBAND_BANGBANG)
     return fail(MDR_EARG, "phase 1 with a bang-bang action source: use mdr_step lookahead or a BUFFER");
-  hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, action, m,
+  hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256 * kPcHouses)), dim3(256), 0, st, c->kp, action, m,
                      tick, tkp, slab_at(c, c->ring));
   LAUNCH_CHECK("k_power_counts");
   return MDR_OK;
@@ -933,7 +933,7 @@ static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t ac
         // caller must provide the first actions: handled by the caller (mode remapped to BUFFER)
         return fail(MDR_EARG, "rollout: bang-bang sources need a BUFFER first tick (use mdr_step)");
       }
-      hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, a, m,
+      hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256 * kPcHouses)), dim3(256), 0, st, c->kp, a, m,
                          (uint64_t)0, c->d_ticks + t, slab_at(c, c->ring));
       LAUNCH_CHECK("k_power_counts");
     }
@@ -1546,7 +1546,7 @@ int rollout_sharded_overlap(mdr_ctx* c, const TickArgs* ticks, int n, int mode, 
   hipStream_t cs = c->comm_stream;
   auto slab = [&](int t) { return c->d_slab + (size_t)(t % kSlabs) * c->slab_len; };
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
-  hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, nullptr,
+  hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256 * kPcHouses)), dim3(256), 0, st, c->kp, nullptr,
                      mode, (uint64_t)0, ticks, slab(0));
   LAUNCH_CHECK("k_power_counts");
   HIP_TRY(hipEventRecord(c->ev_pc, st));
@@ -1585,7 +1585,7 @@ int rollout_sharded_serial(mdr_ctx* c, const TickArgs* ticks, int n, const uint8
   for (int t = 0; t < n; ++t) {
     const uint8_t* a = action ? action + (int64_t)t * act_stride : nullptr;
     if (!la || t == 0) {
-      hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, a, mode,
+      hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256 * kPcHouses)), dim3(256), 0, st, c->kp, a, mode,
                          (uint64_t)0, ticks + t, slab_at(c, c->ring));
       LAUNCH_CHECK("k_power_counts");
     }

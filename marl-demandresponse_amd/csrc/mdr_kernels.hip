@@ -47,22 +47,42 @@ __global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* 
   const uint64_t tick = tkp ? tkp->tick : tick0;
   __shared__ unsigned hist[MDR_MAX_CAP];
   if ((int)threadIdx.x < p.n_cap) hist[threadIdx.x] = 0;
+  // kPcHouses chunks of 256 houses per block, every load issued before the first use
+  uint32_t hw[kPcHouses];
+  int cls[kPcHouses];
+  bool a[kPcHouses];
+#pragma unroll
+  for (int u = 0; u < kPcHouses; ++u) {
+    const int64_t c0 = ((int64_t)blockIdx.x * kPcHouses + u) * blockDim.x;
+    const int64_t i = c0 + threadIdx.x;
+    a[u] = action_mode == MDR_ACT_ALWAYS_ON;
+    if (action_mode == MDR_ACT_RANDOM) {
+      const WaveRandom wr(p.seed, p.goff + c0 + (threadIdx.x & ~63), tick);  // whole wave, before any divergence
+      a[u] = wr.get(p.goff + i, false);
+    }
+    hw[u] = 0u;
+    cls[u] = -1;
+    if (i < p.n) {
+      if (action_mode == MDR_ACT_BUFFER) a[u] = action[i] != 0;
+      hw[u] = p.hvac[i];
+      cls[u] = p.cap_idx[i];
+    }
+  }
   __syncthreads();
-  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  const int64_t wave0 = (int64_t)blockIdx.x * blockDim.x + (threadIdx.x & ~63);
-  bool a = action_mode == MDR_ACT_ALWAYS_ON;
-  if (action_mode == MDR_ACT_RANDOM) {
-    const WaveRandom wr(p.seed, p.goff + wave0, tick);  // whole wave, before any divergence
-    a = wr.get(p.goff + i, false);
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int u = 0; u < kPcHouses; ++u) {
+    const bool on = cls[u] >= 0 && hv_on(hvac_fsm(hw[u], a[u], p.dt, p.L));
+    for (int k = 0; k < p.n_cap; ++k) {
+      const unsigned long long m = __ballot(on && cls[u] == k);
+      if (lane == 0 && m) atomicAdd(&hist[k], (unsigned)__popcll(m));
+    }
   }
-  bool on = false;
-  int cls = 0;
-  if (i < p.n) {
-    if (action_mode == MDR_ACT_BUFFER) a = action[i] != 0;
-    on = hv_on(hvac_fsm(p.hvac[i], a, p.dt, p.L));
-    cls = p.cap_idx[i];
+  __syncthreads();
+  if ((int)threadIdx.x < p.n_cap) {
+    const unsigned v = hist[threadIdx.x];
+    if (v) atomicAdd(&slab[(blockIdx.x % kCountShards) * p.n_cap + threadIdx.x], (unsigned long long)v);
   }
-  count_on(on, cls, p.n_cap, hist, slab);
 }
 
 // --------------------------------------------------------------------------------------- K1
