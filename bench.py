@@ -2,16 +2,18 @@
 """bench.py — vectorised env.step throughput (house-steps/s) on MI355X, with HBM roofline.
 
 Workload (BASELINE.json metric "house-steps/s (env.step throughput) at 1M houses"): 1,048,576
-houses per GPU (weak scaling: N_total = 1,048,576 x n_gpus), MARLconfig env_prop (dt = 4 s,
-L = 40 s, individual_L2 rewards), sinusoidal regulation signal (perlin is parity-unpinned),
-synthetic population drawn on device (Philox, the reference noise model), random actions from
-the fused Philox controller (configs[1]'s controller).  A step = one env.step of every house:
-lockout FSM + RC thermal + cluster power + rewards (every tick's reward row is written), with the
-host scalar drivers (outdoor temperature RNG, solar, signal) computed per tick inside the timed
-region.  Ticks are issued as hipGraph-captured chunks (mdr_rollout), each chunk temporally
-blocked into windows of up to 32 ticks per launch (k_step_window; --window 0 = one launch per
-tick); multi-GPU runs allreduce each window's cluster-power counts with RCCL inside the loop
-(mdr_rollout_sharded).
+houses — on one GPU configs[1]'s workload at the metric's size; under torchrun (WORLD_SIZE > 1)
+config C4, the same 1,048,576-house cluster sharded over the GPUs (131,072 per GPU at 8: strong
+scaling; --scaling weak keeps 1,048,576 per GPU) — with MARLconfig env_prop (dt = 4 s, L = 40 s,
+individual_L2 rewards), sinusoidal regulation signal (perlin is parity-unpinned), synthetic
+population drawn on device (Philox, the reference noise model), random actions from the fused
+Philox controller (configs[1]'s controller).  A step = one env.step of every house: lockout FSM +
+thermal update + cluster power + rewards (every tick's reward row is written), with the host
+scalar drivers (outdoor temperature RNG, solar, signal) computed per tick inside the timed region.
+Ticks are issued as rollout calls of up to --chunk ticks (mdr_rollout, direct launches), each
+temporally blocked into windows of up to 32 ticks per launch (k_step_window; --window 0 = one
+launch per tick); multi-GPU runs allreduce each window's cluster-power counts with RCCL inside the
+loop (mdr_rollout_sharded, count-ahead pipeline).
 
 Other workloads: --workload actor (config C5: MA-PPO actor fused with the obs, then env.step),
 --workload greedy (config C3: device greedy-myopic controller, then env.step).
@@ -42,22 +44,17 @@ BF16_PEAK_TFS = 2516.6     # dense bf16 MFMA: 256 CU x 4 SIMD x 1024 FLOP/clk x 
 
 
 
-def step_kernel_name(n_loc: int, mode: str, window: int, simple: bool = True) -> str:
+def step_kernel_name(n_loc: int, mode: str, window: int, simple: bool = True, thermal: str = "affine") -> str:
     """The step kernel the library launches for this bench (mdr_capi.hip: window_launches /
     launch_step_on)."""
-    if window > 0:  # the rocprofv3 spelling: k_step_window<ACT, HPT=2, SIMPLE, KA> (MDR_ACT_RANDOM = 1, _BUFFER
-        # = 0; KA: the first window of a direct rollout call, drivers as kernel arguments — the
-        # kernel-only timing below launches the KA = false instantiation, the same thermal loop)
-        return f"void mdr::k_step_window<{1 if mode == 'random' else 0}, 2, {'true' if simple else 'false'}, false>"
-    if any(k in os.environ for k in ("MDR_HPT", "MDR_VARIANT", "MDR_FASTDIV")):
-        return "mdr::k_step (variant chosen by MDR_* env)"
-    tpw = int(os.environ.get("MDR_TPW", 2 if n_loc <= 1572864 else 4))
+    if window > 0:  # the rocprofv3 spelling: k_step_window<ACT, HPT=2, SIMPLE, KA, FORM> (MDR_ACT_RANDOM = 1,
+        # _BUFFER = 0; KA: the first window of a direct rollout call, drivers as kernel arguments — the
+        # kernel-only timing below launches the KA = false instantiation, the same thermal loop; FORM:
+        # MDR_THERMAL_AFFINE = 1, _EXACT = 0)
+        return (f"void mdr::k_step_window<{1 if mode == 'random' else 0}, 2, {'true' if simple else 'false'}, "
+                f"false, {1 if thermal == 'affine' else 0}>")
+    tpw = 2 if n_loc <= 1572864 else 4  # mdr_capi.hip default_tpw
     act = "RANDOM,RANDOM" if mode == "random" else "BUFFER,0"
-    if tpw <= 0:
-        return f"mdr::k_step_t<2,false,true,{act}>"
-    tpw = 8 if tpw >= 8 else 4 if tpw >= 4 else 2 if tpw >= 2 else 1
-    if mode != "random":
-        tpw = 4 if tpw >= 4 else 2
     return f"mdr::k_step_pipe<{tpw},{act}>"
 
 
@@ -73,7 +70,13 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=200)
-    ap.add_argument("--houses", type=int, default=1 << 20, help="houses per GPU")
+    ap.add_argument("--houses", type=int, default=1 << 20,
+                    help="houses in the cluster (strong scaling, the default) or per GPU (--scaling weak)")
+    ap.add_argument("--scaling", default="strong", choices=["strong", "weak"],
+                    help="multi-GPU: strong = the --houses cluster sharded over the GPUs (config C4), weak = "
+                         "--houses per GPU")
+    ap.add_argument("--thermal", default="affine", choices=["affine", "exact"],
+                    help="k_step_window's per-tick thermal update (mdr.h MDR_OPT_WINDOW_THERMAL)")
     ap.add_argument("--chunk", type=int, default=128, help="ticks per graph-captured rollout call")
     ap.add_argument("--window", type=int, default=32,
                     help="ticks per temporally blocked launch (k_step_window, <= 32); 0 = one launch per tick")
@@ -99,9 +102,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--trace", action="store_true",
                     help="print host phase timestamps of the timed region to stderr (diagnostics)")
-    ap.add_argument("--graph", default="default", choices=["default", "on", "off"],
-                    help="rollout launch policy: default = Environment.rollout's (direct launches), on = "
-                         "hipGraph launch-first sequences, off = direct launches")
+    ap.add_argument("--graph", default="off", choices=["on", "off"],
+                    help="rollout launch policy: off = Environment.rollout's default (direct launches, the first "
+                         "window's drivers as kernel arguments), on = staged drivers + hipGraph replay")
     ap.add_argument("--mode", default="random", choices=["random", "buffer"])
     ap.add_argument("--workload", default="step", choices=["step", "actor", "greedy"],
                     help="step: env.step with fused random actions (the BASELINE metric); actor: "
@@ -202,8 +205,12 @@ def cpu_baseline(budget_s: float):
     c2_1 = hs / el
     out["configs"]["C2_65536_random_1core"] = {"value": c2_1, "ticks": hs // 65536}
     ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
-    with ctx.Pool(procs) as pool:
+    pool = ctx.Pool(procs)
+    try:
         res = pool.map(_cpu_run, [("C2", 65536, 0.3 * b)] * procs)
+    finally:  # the workers exit on their own (no terminate(): no SIGTERM'd interpreters)
+        pool.close()
+        pool.join()
     c2_all = sum(h for h, _ in res) / max(e for _, e in res)
     out["configs"][f"C2_65536_random_{procs}cores"] = {"value": c2_all, "procs": procs}
     hs, el = _cpu_run(("C3", 1 << 20, 0.2 * b))
@@ -286,7 +293,7 @@ def main():
     from mdr_amd import _lib as L
     from mdr_amd.environment import Environment
 
-    n_total = args.houses * world
+    n_total = args.houses * world if args.scaling == "weak" else args.houses
     props = env_props(n_total)
     env = Environment(props, device=dev, rng=random.Random(4), population="synthetic", seed=1234,
                       rank=rank, world=world, comm=comm)
@@ -294,6 +301,7 @@ def main():
     sh = env.shard
     window = min(max(args.window, 0), 32)
     sh.set_rollout_window(window)
+    sh.set_option("window_thermal", L.THERMAL_AFFINE if args.thermal == "affine" else L.THERMAL_EXACT)
     chunk = min(args.chunk, args.steps)
     chunks = [chunk] * (args.steps // chunk) + ([args.steps % chunk] if args.steps % chunk else [])
     acts = None
@@ -312,7 +320,7 @@ def main():
             raise SystemExit("--workload greedy runs on one GPU (config C3)")
         g_act = torch.empty(n_loc, dtype=torch.uint8, device=dev)
 
-    use_graph = {"default": None, "on": True, "off": False}[args.graph]
+    use_graph = args.graph == "on"
 
     def run(n):
         if dactor is not None:
@@ -354,7 +362,7 @@ def main():
         del spin
     barrier()
     torch.cuda.synchronize()
-    # HIP events on the stream the step launches are issued on (the graph side stream)
+    # HIP events on the stream the step launches are issued on
     launch_stream = env.rollout_stream()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     for ev in (ev0, ev1):  # torch creates the HIP event on its first record(): not inside the timed region
@@ -415,13 +423,13 @@ def main():
     kt = max(args.kernel_ticks, 1)
     mode_id = L.ACT_RANDOM if args.mode == "random" else L.ACT_BUFFER
     simple = env.init_props.cluster_prop.house_prop.deadband == 0.0 and env._norm_temp == 1.0
-    kern = step_kernel_name(n_loc, args.mode, window, simple)
+    kern = step_kernel_name(n_loc, args.mode, window, simple, args.thermal)
     actor_ms = graph_ms = None
     if dactor is None and g_act is None:
         kbuf = torch.empty((kt, n_loc), dtype=torch.float64, device=dev)
         kacts = None if acts is None else (torch.rand((kt, n_loc), device=dev) < 0.5).to(torch.uint8)
         kticks = env.driver_window(kt)
-        ls = sh.launch_stream(True)
+        ls = sh.launch_stream()
         for rep in range(2):  # the whole graph (count, reduce and step kernels): capture, then a timed replay
             if rep:
                 torch.cuda.synchronize()
@@ -489,7 +497,7 @@ def main():
         "warmup_steps_run": warm_steps,
         "ms_per_step": elapsed * 1e3 / args.steps,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if world > 1 and args.scaling == "strong" else "weak",
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (device Philox population, reference noise model; fused Philox random actions)",
@@ -545,8 +553,9 @@ def main():
                            "kernel_avg_us": actor_ms * 1e3, "launches_timed": launches,
                            "algorithmic_flops_per_launch": flops_launch, "flops_per_house": flops_house,
                            "mfma_products_per_mac": 3 if args.precision == "bf16x3" else 1,
-                           "step_kernel": {"kernel": "mdr::k_step (BUFFER)", "avg_us": kern_ms * 1e3,
-                                           "hbm_GBps": achieved, "frac": achieved / HBM_PEAK_GBS}}
+                           "step_share": {"what": "launch-stream time per tick minus k_actor's time: the step "
+                                                  "kernel's share of a tick (not a kernel duration)",
+                                          "us_per_tick": kern_ms * 1e3}}
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MDR_ABI_VERSION 3
+#define MDR_ABI_VERSION 4
 #define MDR_MAX_CAP 64
 
 enum {
@@ -131,11 +131,34 @@ int mdr_destroy(mdr_ctx* ctx);
 /* Bind the caller-owned SoA arrays (Environment.reset, environment.py:49-70). */
 int mdr_bind(mdr_ctx* ctx, const mdr_soa* soa);
 
-/* The caller rewrote ua/ca/cm/hm (or dt changed): derived per-house coefficients the context may
- * cache (the CACHED step variant keeps r1, r2, A3, A4, exp(r1 dt), exp(r2 dt) of every house,
- * bit-identical to recomputing them per tick) are refreshed before the next step.  mdr_bind and
- * mdr_populate imply it. */
+/* The caller rewrote ua/ca/cm/hm (or dt changed): the per-house flag that routes a house outside
+ * the exact shared-reciprocal division range to the IEEE operator is recomputed before the next
+ * step.  mdr_bind and mdr_populate imply it. */
 int mdr_params_changed(mdr_ctx* ctx);
+
+/* ---- options (no reference counterpart) ------------------------------------------------ */
+/* Alternative launch forms of the same computation, for verification and measurement; every
+ * option has a test that pins it against the default.  Drops cached rollout graphs.
+ *   MDR_OPT_STEP_TPW        per-tick step kernel: 1/2/4/8 = k_step_pipe tiles per wave, 0 = the
+ *                           one-tile k_step_t, -1 = the measured default (2 up to 1.5M houses, 4)
+ *   MDR_OPT_FASTDIV         1 = shared-reciprocal exact division (default), 0 = the IEEE operator
+ *                           everywhere (bit-identical results)
+ *   MDR_OPT_WINDOW_PIPELINE sharded window rollouts: 1 = count + allreduce on a side stream up to
+ *                           two windows ahead (default), 0 = one stream
+ *   MDR_OPT_SHARDED_OVERLAP sharded one-tick rollouts: 1 = allreduce of tick t beside the step of
+ *                           tick t, rewards written one launch later (default), 0 = serial
+ *   MDR_OPT_GREEDY_SORT     1 = mdr_ctrl_greedy always runs the full-sort form
+ *   MDR_OPT_FORCE_HALO      1 = mdr_actor_rollout_sharded exchanges the ring halo even at world 1
+ *                           (send/recv to self: the one-GPU check of the multi-GPU exchange)
+ *   MDR_OPT_WINDOW_THERMAL  k_step_window's per-tick thermal update: MDR_THERMAL_AFFINE (default)
+ *                           = the reference's update as a per-house affine transition formed once
+ *                           per window (4 FMAs per temperature per tick; ~1e-13 K per tick from the
+ *                           reference order), MDR_THERMAL_EXACT = the reference's expression in its
+ *                           operation order every tick (bit-identical to the one-tick kernels) */
+enum { MDR_OPT_STEP_TPW = 1, MDR_OPT_FASTDIV = 2, MDR_OPT_WINDOW_PIPELINE = 3, MDR_OPT_SHARDED_OVERLAP = 4,
+       MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7 };
+enum { MDR_THERMAL_EXACT = 0, MDR_THERMAL_AFFINE = 1 };
+int mdr_set_option(mdr_ctx* ctx, int option, int64_t value);
 
 /* ---- population ------------------------------------------------------------------------ */
 /* Synthetic population drawn on device from Philox4x32-10(seed, global house id): the reference
@@ -206,38 +229,20 @@ int mdr_rollout(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t*
  * state and parameters read and written once per window, rewards written every tick, each tick's
  * cluster power from counts the previous launch ran ahead (the FSM of an open-loop source does
  * not depend on the thermal state).  Bit-identical to the one-tick path.  ticks in 1..32
- * (default 32; MDR_WINDOW env at mdr_create), 0 = one launch per tick.  Applies to mdr_rollout and
+ * (default 32), 0 = one launch per tick.  Applies to mdr_rollout and
  * mdr_rollout_sharded; drops cached rollout graphs. */
 int mdr_set_rollout_window(mdr_ctx* ctx, int ticks);
 
 /* Optional, before mdr_rollout (no reference counterpart): launch the first window's lockout-FSM
- * count of an n_ticks rollout whose first tick id is tick0 — it needs the tick ids only, so it runs
- * while the host computes the ticks' drivers.  The next mdr_rollout with the same n_ticks, action
- * source, action buffer and first tick id uses it; any other entry point called in between
- * discards it.  A no-op for rollouts that do not take the temporally blocked path. */
+ * count of an n_ticks rollout whose first tick id is tick0, and that window's cluster power — they
+ * need the tick ids only, so they run while the host computes the ticks' drivers.  The next
+ * mdr_rollout with the same n_ticks, action source, action buffer and first tick id (and
+ * consecutive tick ids) uses them and launches the first window's step kernel with the drivers as
+ * kernel arguments; any other entry point called in between discards them.  A no-op for rollouts
+ * that do not take the temporally blocked path.  On a context with an RCCL communicator it also
+ * allreduces the counts (single-window rollouts; the match is mdr_rollout_sharded). */
 int mdr_rollout_begin(mdr_ctx* ctx, int n_ticks, uint64_t tick0, const uint8_t* action, int64_t act_stride,
                       int action_mode, void* stream);
-
-/* Optional, before mdr_rollout (no reference counterpart; replaces the host-side ordering of
- * environment.py:72-108 — drivers first, then the cluster step — by launch first): launch the
- * whole rollout graph NOW, before the host computes the ticks' drivers.  It counts the first
- * window's FSM and then waits on the device until the matching mdr_rollout (same n_ticks, tick0 =
- * ticks[0].tick, action source and buffers, reward, rew_stride, p_out) posts the drivers through
- * pinned host memory; the graph launch and the count overlap the host work.  Any other entry point
- * called in between cancels it (every kernel of the graph then returns at once, the state is
- * unchanged); a graph left without drivers for 10 s cancels itself and the next rollout call
- * reports it.  The host must not synchronise the device between the two calls.  Falls back to
- * mdr_rollout_begin when it does not apply (no pinned memory, > 1024 ticks, not the temporally
- * blocked path, or a random source whose tick0 is not where the previous rollout ended). */
-int mdr_rollout_launch(mdr_ctx* ctx, int n_ticks, uint64_t tick0, const uint8_t* action, int64_t act_stride,
-                       int action_mode, double* reward, int64_t rew_stride, double* p_out, void* stream);
-
-/* Cancel a pending mdr_rollout_launch whose drivers will not be posted (e.g. the host failed to
- * compute them).  A no-op when none is pending. */
-int mdr_rollout_cancel(mdr_ctx* ctx);
-
-/* Diagnostics: *count = launch-first graphs launched so far on this context. */
-int mdr_rollout_launched(mdr_ctx* ctx, uint64_t* count);
 
 /* Measurement (no reference counterpart): mdr_rollout's launch sequence issued directly (no graph)
  * with an event pair around every step-kernel launch; *ms = the summed step-kernel time,
@@ -303,7 +308,8 @@ int mdr_cluster_stats(mdr_ctx* ctx, const double* reward, double* out, void* str
 /* Next actions for the whole shard (single GPU: shard = cluster) from the current state: order
  * by -(T - target) ascending, then the reference's sequential take rule with budget S.  Histogram
  * select: only the houses around the budget crossing are ordered; synchronises `stream` once to
- * read back whether that window decided the tick, else the full-sort form runs (same result). */
+ * read back whether that window decided the tick, else the full-sort form runs (same result;
+ * MDR_OPT_GREEDY_SORT forces it). */
 int mdr_ctrl_greedy(mdr_ctx* ctx, double budget, uint8_t* action, void* stream);
 /* Diagnostics: mdr_ctrl_greedy calls the histogram select handed to the full-sort form. */
 int mdr_greedy_fallbacks(mdr_ctx* ctx, uint64_t* count);
@@ -403,14 +409,11 @@ int mdr_rccl_allreduce(mdr_ctx* ctx, void* buf, int64_t count, int dtype, void* 
 int mdr_rollout_sharded(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t* action,
                         int64_t act_stride, int action_mode, double* reward, int64_t rew_stride,
                         double* p_out, void* stream);
-/* Pipeline of mdr_rollout_sharded for in-kernel action sources with one reward row per tick:
- *   0 serial      allreduce(counts of t) -> step(t) on the caller's stream
- *   1 overlapped  step(t) on the caller's stream concurrent with allreduce(counts of t) on a
- *                 context stream; step(t+1) writes tick t's reward (bit-identical)
- *  -1 undecided   the next rollout of >= 16 ticks times both on its own ticks (max over ranks)
- *                 and keeps the faster; MDR_SHARDED_OVERLAP=0/1 forces one at mdr_create.
- * us_serial / us_overlap (may be NULL) receive the calibration's per-tick times. */
-int mdr_rollout_sharded_mode(mdr_ctx* ctx, int* mode, double* us_serial, double* us_overlap);
+/* Pipelines mdr_rollout_sharded uses (MDR_OPT_WINDOW_PIPELINE / MDR_OPT_SHARDED_OVERLAP with the
+ * communicator's side stream present): *window_pipeline = windows counted + allreduced on the side
+ * stream ahead of the steps; *tick_overlap = one-tick rollouts with the allreduce of tick t beside
+ * the step of tick t (that tick's reward written by the next launch, bit-identical). */
+int mdr_rollout_sharded_mode(mdr_ctx* ctx, int* window_pipeline, int* tick_overlap);
 
 /* ---- diagnostics ------------------------------------------------------------------------ */
 /* Memory-floor probe: the loads/stores of one mdr_step over the bound arrays with no arithmetic

@@ -7,8 +7,6 @@
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
-#include <atomic>
-#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -63,10 +61,9 @@ struct GraphKey {
   void* rew;
   int64_t rew_stride;
   void* p_out;
-  void* stream;
   bool operator<(const GraphKey& o) const {
-    return std::tie(n_ticks, mode, act, act_stride, rew, rew_stride, p_out, stream) <
-           std::tie(o.n_ticks, o.mode, o.act, o.act_stride, o.rew, o.rew_stride, o.p_out, o.stream);
+    return std::tie(n_ticks, mode, act, act_stride, rew, rew_stride, p_out) <
+           std::tie(o.n_ticks, o.mode, o.act, o.act_stride, o.rew, o.rew_stride, o.p_out);
   }
 };
 
@@ -82,15 +79,18 @@ struct mdr_ctx {
   int slab_len = 0;
   int ring = 0;                          // slab of the current tick
   bool counts_ready = false;             // current slab filled (phase 1 or previous lookahead)
-  double* d_pen_partial = nullptr;       // 2 per block of k_step
+  double* d_pen_partial = nullptr;       // 2 per block of k_step_t
   double* d_partial2 = nullptr;
   int pen_blocks = 0;
-  int hpt = 2;                           // houses per thread of k_step (MDR_HPT env overrides)
-  bool cached = false;                   // cached param-only thermal coefficients (MDR_VARIANT=coef)
-  bool fastdiv = true;                   // shared-reciprocal exact division (MDR_FASTDIV=0 disables)
-  int tpw = 0;                           // k_step_pipe tiles per wave (MDR_TPW; 0: k_step_t)
-  int win = kWindowMax;                  // ticks per k_step_window launch (MDR_WINDOW; 0: one-tick path)
-  int win_hpt = 2;                       // houses per lane of k_step_window (MDR_WIN_HPT)
+  // ---- options (mdr_set_option; defaults are the measured-fastest exact configuration)
+  int tpw = 0;                           // MDR_OPT_STEP_TPW: k_step_pipe tiles per wave (0: k_step_t)
+  bool fastdiv = true;                   // MDR_OPT_FASTDIV: shared-reciprocal exact division
+  bool win_pipe = true;                  // MDR_OPT_WINDOW_PIPELINE: sharded count-ahead window pipeline
+  bool tick_overlap = true;              // MDR_OPT_SHARDED_OVERLAP: per-tick sharded two-stream pipeline
+  bool greedy_sort = false;              // MDR_OPT_GREEDY_SORT: the full-sort greedy form only
+  bool force_halo = false;               // MDR_OPT_FORCE_HALO: sharded actor halo exchange at world 1
+  int thermal = MDR_THERMAL_AFFINE;      // MDR_OPT_WINDOW_THERMAL: k_step_window's per-tick update
+  int win = kWindowMax;                  // ticks per k_step_window launch (0: one-tick path)
   unsigned long long* d_wslab = nullptr; // 3 window count slots (mdr_kernels.hip K1W: slab | red | rec)
   int wslab_len = 0;
   bool wslab_dirty = true;               // the slots' shard part must be zero when a rollout starts
@@ -99,9 +99,7 @@ struct mdr_ctx {
   uint64_t* d_onb2 = nullptr;            // second set for the count-ahead pipeline (window_launches pipe)
   uint32_t* d_wah2 = nullptr;
   size_t onb_bytes = 0, wah_bytes = 0;
-  bool win_pipe = true;                  // sharded windows: counts + allreduce on the comm stream (MDR_WINDOW_PIPELINE=0: serial)
   bool coef_dirty = true;
-  double* d_coef = nullptr;              // [6][n] r1, r2, A3, A4, e1, e2
   int* d_flags = nullptr;                // [0] params_bad
   // rollout tick drivers
   TickArgs* d_ticks = nullptr;
@@ -129,9 +127,7 @@ struct mdr_ctx {
   // multi-GPU
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
-  int overlap_mode = -1;                 // sharded pipeline: -1 calibrate, 0 serial, 1 overlapped
-  double calib_us[2] = {0.0, 0.0};       // calibration: us/tick serial, overlapped (max over ranks)
-  hipStream_t comm_stream = nullptr;     // per-tick allreduce of the overlapped pipeline
+  hipStream_t comm_stream = nullptr;     // per-tick / per-window allreduces of the overlapped pipelines
   hipStream_t cap_stream = nullptr;      // graph capture (graphs are replayed on the caller's stream)
   hipEvent_t ev_k1[kSlabs] = {}, ev_ar[kSlabs] = {}, ev_pc = nullptr;
   hipEvent_t ev[16] = {};
@@ -142,28 +138,8 @@ struct mdr_ctx {
     uint64_t tick0 = 0;
     const uint8_t* action = nullptr;
     int64_t act_stride = 0;
-    bool ka = false;                     // its P-only reduce ran too: the step takes the drivers as arguments
     bool sharded = false;                // counts allreduced over the ranks (for mdr_rollout_sharded)
   } begun;
-  // launch-first rollouts (mdr_rollout_launch): the graph runs ahead of the host's tick drivers
-  uint64_t* d_lf = nullptr;              // device: [0] seq of the last k_lf_wait, [1] next rollout's tick id, [2] abort (int)
-  TickArgs* h_lf_ring = nullptr;         // pinned: 2 slots x kLfCap tick records
-  uint64_t* h_lf_ctl = nullptr;          // pinned: [0] posted seq, [1] acked seq | abort << 62, [2] cancelled seq
-  uint64_t lf_seq = 0;                   // launch-first graphs launched (= the device's [0] once they ran)
-  bool lf_disabled = false;              // a direct launch-first sequence failed part-way: begin path only
-  uint64_t lf_timeout = 0;               // k_lf_wait's bound, wall-clock ticks
-  uint64_t lf_timeouts_seen = 0;
-  bool next_tick_known = false;          // d_lf[1] as written by the last rollout graph
-  uint64_t next_tick = 0;
-  struct {
-    bool on = false;
-    uint64_t seq = 0, tick0 = 0;
-    int n = 0, mode = 0, ring_end = 0;
-    const uint8_t* action = nullptr;
-    int64_t act_stride = 0, rew_stride = 0;
-    double* reward = nullptr;
-    double* p_out = nullptr;
-  } lf;
   // MA-PPO actor (row P): packed weight image, per-tick obs scalars of actor rollouts
   unsigned char* d_actor = nullptr;
   size_t actor_cap = 0;
@@ -196,6 +172,10 @@ bool lookahead_ok(int m) { return m != MDR_ACT_BUFFER; }
 
 TickArgs to_tick(const mdr_tick* t) { return TickArgs{t->t_od_prev, t->solar, t->s_prev, t->tick}; }
 
+// k_step_pipe depth measured on MI355X (profiles/r01b_kbench_pipe.log): 2 tiles per wave up to
+// ~1.5M houses per shard, 4 above
+int default_tpw(int64_t n) { return n <= 1572864 ? 2 : 4; }
+
 // phase 1 into the current slab
 int launch_counts(mdr_ctx* c, const uint8_t* action, int mode, uint64_t tick, const TickArgs* tkp,
                   hipStream_t st) {
@@ -208,13 +188,12 @@ int launch_counts(mdr_ctx* c, const uint8_t* action, int mode, uint64_t tick, co
   return MDR_OK;
 }
 
-// parameter-derived state (fast-division range flag, cached coefficients) after a change;
-// called before any launch sequence is captured, so graphs never contain it
+// parameter-derived state (the fast-division range flag) after a change; called before any
+// launch sequence is captured, so graphs never contain it
 int refresh_if_dirty(mdr_ctx* c, hipStream_t st) {
   if (!c->coef_dirty) return MDR_OK;
   HIP_TRY(hipMemsetAsync(c->d_flags, 0, sizeof(int), st));
-  hipLaunchKernelGGL(k_refresh, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp,
-                     c->cached ? c->d_coef : nullptr, c->d_flags);
+  hipLaunchKernelGGL(k_refresh, dim3(blocks(c->kp.n, 256)), dim3(256), 0, st, c->kp, c->d_flags);
   LAUNCH_CHECK("k_refresh");
   c->coef_dirty = false;
   return MDR_OK;
@@ -227,17 +206,16 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
                    const unsigned long long* cur, unsigned long long* nxt, unsigned long long* zer,
                    int reward_lag, hipStream_t st) {
   if (int rc = refresh_if_dirty(c, st)) return rc;
-  KParams kp = c->kp;
-  kp.coef = c->cached ? c->d_coef : nullptr;
-#define MDR_LAUNCH_STEP(H, C, F, A, LA)                                                               \
-  hipLaunchKernelGGL((k_step_t<H, C, F, A, LA>), dim3(blocks(kp.n, 256 * H)), dim3(256), 0, st, kp,       \
-                     action, mode, tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer,      \
-                     c->d_pen_partial, reward_lag)
+  const KParams kp = c->kp;
+#define MDR_LAUNCH_STEP(F, A, LA)                                                                     \
+  hipLaunchKernelGGL((k_step_t<2, F, A, LA>), dim3(blocks(kp.n, 512)), dim3(256), 0, st, kp, action, mode, \
+                     tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer, c->d_pen_partial,    \
+                     reward_lag)
   const bool hot_random = mode == MDR_ACT_RANDOM && lookahead == MDR_ACT_RANDOM;
   const bool hot_buffer = mode == MDR_ACT_BUFFER && lookahead == 0;
   // software-pipelined form of the two hot configurations (k_step_pipe): individual_L2, <= 4
   // capacity classes, no controller output, no reward lag, 2-byte aligned action rows
-  const bool pipe_ok = c->tpw >= 1 && c->hpt == 2 && c->fastdiv && !c->cached && (hot_random || hot_buffer) &&
+  const bool pipe_ok = c->tpw >= 1 && c->fastdiv && (hot_random || hot_buffer) &&
                        kp.penalty_mode == MDR_PEN_INDIVIDUAL_L2 && kp.n_cap <= kPipeMaxCap &&
                        ctrl == MDR_CTRL_NONE && !reward_lag && (!action || ((uintptr_t)action & 1u) == 0);
   if (pipe_ok) {
@@ -260,23 +238,12 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
     LAUNCH_CHECK("k_step_pipe");
     return MDR_OK;
   }
-  if (c->hpt == 2 && c->fastdiv) {
-    if (c->cached) {
-      if (hot_random) MDR_LAUNCH_STEP(2, true, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
-      else MDR_LAUNCH_STEP(2, true, true, -1, -1);
-    } else {
-      if (hot_random) MDR_LAUNCH_STEP(2, false, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
-      else if (hot_buffer) MDR_LAUNCH_STEP(2, false, true, MDR_ACT_BUFFER, 0);
-      else MDR_LAUNCH_STEP(2, false, true, -1, -1);
-    }
-  } else if (c->hpt == 1 && c->fastdiv && !c->cached) {
-    // one house per lane: 16384 waves at 1M (A/B against HPT = 2, MDR_HPT=1)
-    if (hot_random) MDR_LAUNCH_STEP(1, false, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
-    else MDR_LAUNCH_STEP(1, false, true, -1, -1);
-  } else if (c->hpt == 2) {
-    if (c->cached) MDR_LAUNCH_STEP(2, true, false, -1, -1); else MDR_LAUNCH_STEP(2, false, false, -1, -1);
+  if (c->fastdiv) {
+    if (hot_random) MDR_LAUNCH_STEP(true, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
+    else if (hot_buffer) MDR_LAUNCH_STEP(true, MDR_ACT_BUFFER, 0);
+    else MDR_LAUNCH_STEP(true, -1, -1);
   } else {
-    MDR_LAUNCH_STEP(1, false, false, -1, -1);
+    MDR_LAUNCH_STEP(false, -1, -1);
   }
 #undef MDR_LAUNCH_STEP
   LAUNCH_CHECK("k_step");
@@ -300,19 +267,11 @@ extern "C" {
 
 // an early first-window count (mdr_rollout_begin) is only valid for the mdr_rollout that follows
 // it directly: every other entry point that changes the state or uses the slots discards it
-static void lf_cancel(mdr_ctx* c) {
-  if (!c || !c->lf.on) return;
-  __atomic_store_n(&c->h_lf_ctl[2], c->lf.seq, __ATOMIC_RELEASE);  // k_lf_wait aborts the graph
-  c->lf.on = false;
-  c->wslab_dirty = true;  // its count wrote the first slot's shards; no reduce cleared them
-}
-
 static void drop_begun(mdr_ctx* c) {
   if (c && c->begun.on) {
     c->begun.on = false;
     c->wslab_dirty = true;
   }
-  lf_cancel(c);
 }
 
 int mdr_abi_version(void) { return MDR_ABI_VERSION; }
@@ -374,25 +333,6 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   k.q_on = c->d_tables;
   k.p_on = c->d_tables + MDR_MAX_CAP;
   if (hipMalloc(&c->d_flags, 16) != hipSuccess) return cleanup(fail(MDR_ENOMEM, "flags"));
-  if (hipMalloc(&c->d_lf, 64) != hipSuccess || hipMemset(c->d_lf, 0, 64) != hipSuccess)
-    return cleanup(fail(MDR_ENOMEM, "launch-first words"));
-  {
-    // launch-first ring + control words in fine-grained (coherent) pinned memory; optional: without
-    // it mdr_rollout_launch falls back to mdr_rollout_begin
-    if (hipHostMalloc(&c->h_lf_ring, 2 * sizeof(TickArgs) * kLfCap, hipHostMallocCoherent) != hipSuccess ||
-        hipHostMalloc(&c->h_lf_ctl, 64, hipHostMallocCoherent) != hipSuccess) {
-      (void)hipGetLastError();
-      if (c->h_lf_ring) hipHostFree(c->h_lf_ring);
-      c->h_lf_ring = nullptr;
-      c->h_lf_ctl = nullptr;
-    } else {
-      memset(c->h_lf_ctl, 0, 64);
-    }
-    int khz = 0;
-    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, cfg->device) != hipSuccess || khz <= 0)
-      khz = 100000;  // gfx9: 100 MHz
-    c->lf_timeout = (uint64_t)khz * 1000ull * 10ull;  // 10 s
-  }
   k.params_bad = c->d_flags;
   {
     // the fast division is provably exact for dt < 2^20 s and |q_on| < 2^40 W (mdr_device.h)
@@ -405,19 +345,11 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
     return cleanup(fail(MDR_ENOMEM, "count slabs"));
   if (hipMemset(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long)) != hipSuccess)
     return cleanup(fail(MDR_EHIP, "count slabs memset"));
-  if (const char* e = getenv("MDR_HPT")) c->hpt = atoi(e) == 1 ? 1 : 2;
-  if (const char* e = getenv("MDR_VARIANT")) c->cached = strcmp(e, "coef") == 0;
-  if (const char* e = getenv("MDR_FASTDIV")) c->fastdiv = atoi(e) != 0;
-  // k_step_pipe depth measured on MI355X (tools/kbench.py, profiles/r01b_kbench_pipe.log): 2 tiles per
-  // wave up to ~1.5M houses per shard, 4 above; MDR_TPW=0 selects the one-tile kernel k_step_t
-  c->tpw = cfg->n_local <= 1572864 ? 2 : 4;
-  if (const char* e = getenv("MDR_TPW")) c->tpw = atoi(e);
-  if (const char* e = getenv("MDR_WIN_HPT")) c->win_hpt = atoi(e) == 1 ? 1 : 2;
-  if (const char* e = getenv("MDR_WINDOW")) c->win = atoi(e) < 0 ? 0 : atoi(e) > kWindowMax ? kWindowMax : atoi(e);
+  c->tpw = default_tpw(cfg->n_local);
   if (cfg->n_cap <= kWindowCap) {
     // a window count slot: sharded slab | reduced counts (mdr_kernels.hip)
     c->wslab_len = kWindowMax * kCountShards * cfg->n_cap + kWindowMax * cfg->n_cap + kWindowMax * kWindowRec;
-    const size_t tiles64 = ((size_t)cfg->n_local + 63) / 64 + 1;  // 64-house lane groups (either HPT)
+    const size_t tiles64 = ((size_t)cfg->n_local + 63) / 64 + 1;  // 64-house lane groups
     c->onb_bytes = tiles64 * kWindowMax * sizeof(uint64_t);
     c->wah_bytes = ((size_t)cfg->n_local + 1) * sizeof(uint32_t);
     if (hipMalloc(&c->d_wslab, 3 * sizeof(unsigned long long) * c->wslab_len) != hipSuccess ||
@@ -426,12 +358,7 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   } else {
     c->win = 0;
   }
-  if (c->cached) {
-    k.coef_stride = cfg->n_local;
-    if (hipMalloc(&c->d_coef, 6 * sizeof(double) * cfg->n_local) != hipSuccess)
-      return cleanup(fail(MDR_ENOMEM, "coefficients"));
-  }
-  c->pen_blocks = (int)blocks(cfg->n_local, 256 * c->hpt);  // = k_step grid
+  c->pen_blocks = (int)blocks(cfg->n_local, 512);  // = k_step_t grid
   if (hipMalloc(&c->d_pen_partial, 2 * sizeof(double) * c->pen_blocks) != hipSuccess ||
       hipMalloc(&c->d_partial2, 2 * sizeof(double)) != hipSuccess)
     return cleanup(fail(MDR_ENOMEM, "penalty partials"));
@@ -446,22 +373,22 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   if (hipDeviceGetAttribute(&c->n_cu, hipDeviceAttributeMultiprocessorCount, cfg->device) != hipSuccess ||
       c->n_cu < 1)
     c->n_cu = 256;
-  if (const char* e = getenv("MDR_SHARDED_OVERLAP")) c->overlap_mode = atoi(e) < 0 ? -1 : atoi(e) != 0;
-  if (const char* e = getenv("MDR_WINDOW_PIPELINE")) c->win_pipe = atoi(e) != 0;
   *out = c;
   return MDR_OK;
+}
+
+static void destroy_graphs(mdr_ctx* c) {
+  for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
+  c->graphs.clear();
+  for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
+  c->actor_graphs.clear();
 }
 
 int mdr_destroy(mdr_ctx* c) {
   if (!c) return MDR_OK;
   hipSetDevice(c->cfg.device);
-  lf_cancel(c);  // a launched graph still waiting for its drivers must not hold the synchronize
   hipDeviceSynchronize();
-  hipFree(c->d_lf);
-  if (c->h_lf_ring) hipHostFree(c->h_lf_ring);
-  if (c->h_lf_ctl) hipHostFree(c->h_lf_ctl);
-  for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
-  for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
+  destroy_graphs(c);
   hipFree(c->d_actor);
   hipFree(c->d_interp);
   hipFree(c->d_act);
@@ -469,7 +396,6 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->d_stats);
   hipFree(c->d_obs_sc);
   hipFree(c->d_tables);
-  hipFree(c->d_coef);
   hipFree(c->d_flags);
   hipFree(c->d_slab);
   hipFree(c->d_wslab);
@@ -496,6 +422,31 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->g_flag); hipHostFree(c->h_gq_flag); hipFree(c->g_sorted);
   if (c->comm) ncclCommDestroy(c->comm);
   delete c;
+  return MDR_OK;
+}
+
+int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
+  drop_begun(c);
+  if (!c) return fail(MDR_EARG, "mdr_set_option: null ctx");
+  switch (option) {
+    case MDR_OPT_STEP_TPW:
+      if (value < -1 || value > 8) return fail(MDR_EARG, "mdr_set_option: STEP_TPW outside -1..8");
+      c->tpw = value < 0 ? default_tpw(c->kp.n) : (int)value;
+      break;
+    case MDR_OPT_FASTDIV: c->fastdiv = value != 0; break;
+    case MDR_OPT_WINDOW_PIPELINE: c->win_pipe = value != 0; break;
+    case MDR_OPT_SHARDED_OVERLAP: c->tick_overlap = value != 0; break;
+    case MDR_OPT_GREEDY_SORT: c->greedy_sort = value != 0; break;
+    case MDR_OPT_FORCE_HALO: c->force_halo = value != 0; break;
+    case MDR_OPT_WINDOW_THERMAL:
+      if (value != MDR_THERMAL_EXACT && value != MDR_THERMAL_AFFINE)
+        return fail(MDR_EARG, "mdr_set_option: WINDOW_THERMAL must be MDR_THERMAL_EXACT or _AFFINE");
+      c->thermal = (int)value;
+      break;
+    default: return fail(MDR_EARG, "mdr_set_option: unknown option");
+  }
+  HIP_TRY(hipDeviceSynchronize());  // cached graphs may be in flight
+  destroy_graphs(c);
   return MDR_OK;
 }
 
@@ -626,10 +577,7 @@ static int ensure_ticks(mdr_ctx* c, int n) {
     HIP_TRY(hipMalloc(&c->d_ticks, cap * sizeof(TickArgs)));
     HIP_TRY(hipMalloc(&c->d_obs_sc, (size_t)cap * 4 * sizeof(double)));
     c->ticks_cap = cap;
-    for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
-    c->graphs.clear();
-    for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
-    c->actor_graphs.clear();
+    destroy_graphs(c);
   }
   return MDR_OK;
 }
@@ -662,16 +610,6 @@ static int capture_graph(mdr_ctx* c, F&& launches, hipGraphExec_t* out) {
 }
 
 // ---- windowed rollout (k_step_window): open-loop action sources, individual_L2
-// mdr_time_step_kernels: an event pair around each step-kernel launch (direct launches only)
-static int step_mark(mdr_ctx* c, hipStream_t st) {
-  if (!c->step_events) return MDR_OK;
-  hipEvent_t e;
-  HIP_TRY(hipEventCreate(&e));
-  c->step_events->push_back(e);
-  HIP_TRY(hipEventRecord(e, st));
-  return MDR_OK;
-}
-
 // SIMPLE = deadband 0, norm_temp 1, and reward weights whose signal / temperature penalties are
 // >= +0 (k_step_window forms -(a + s) as (-a) + (-s), exact for such operands)
 static bool win_simple(const mdr_ctx* c) {
@@ -696,72 +634,104 @@ static int wslab_clean(mdr_ctx* c, hipStream_t st) {
   return MDR_OK;
 }
 
-// n ticks as ceil(n / win) windows of near-equal size: one k_count_window for the first window,
-// then per window k_win_reduce (shard sums -> counts + tick records; sharded: the shards are
-// allreduced first) and one k_step_window (counting the next window's ticks).
-// lf (launch-first, mdr_rollout_launch): the count reads the first tick id from d_lf[1] (written by
-// the previous rollout's last reduce), then k_lf_wait stages the drivers once the host posts them;
-// every later kernel returns at once if it was cancelled.  Every sequence's last reduce writes the
-// tick id the next rollout starts at into d_lf[1].
+static unsigned win_grid(const mdr_ctx* c) { return blocks(blocks(c->kp.n, 64 * kWinHpt), 4); }  // a tile per wave
+
+// the first window's FSM count: ticks from tk (staged) or tick0 + j (tk == nullptr), from the
+// state's FSM words (w_in == nullptr) or from the end words of the previous window
+static int launch_count(mdr_ctx* c, int mode, const uint8_t* action, int64_t act_stride, const TickArgs* tk,
+                        uint64_t tick0, int K, unsigned long long* slot, uint64_t* onb, uint32_t* wah,
+                        const uint32_t* w_in, hipStream_t st) {
+  const unsigned grid = win_grid(c);
+#define MDR_COUNT(A)                                                                                  \
+  hipLaunchKernelGGL((k_count_window<A, kWinHpt>), dim3(grid), dim3(256), 0, st, c->kp, action, act_stride, tk, \
+                     tick0, K, slot, onb, wah, w_in)
+  if (mode == MDR_ACT_RANDOM) MDR_COUNT(MDR_ACT_RANDOM);
+  else if (mode == MDR_ACT_ALWAYS_ON) MDR_COUNT(MDR_ACT_ALWAYS_ON);
+  else MDR_COUNT(MDR_ACT_BUFFER);
+#undef MDR_COUNT
+  LAUNCH_CHECK("k_count_window");
+  return MDR_OK;
+}
+
+// one k_step_window launch: the (ACT, SIMPLE, KA, FORM) instantiation for this context; with
+// step_events (mdr_time_step_kernels) hipExtLaunchKernel's start / stop events time it
+static int launch_step_window(mdr_ctx* c, int mode, bool ka, const uint8_t* action, int64_t act_stride,
+                              const TickArgs* tk, int K, int la_K, const double* rec, double* reward,
+                              int64_t rew_stride, uint64_t* onb, uint32_t* wah, unsigned long long* next_slot,
+                              const WinDrv& dv, hipStream_t st) {
+  const unsigned grid = win_grid(c);
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  if (c->step_events) {
+    HIP_TRY(hipEventCreate(&t0));
+    c->step_events->push_back(t0);
+    HIP_TRY(hipEventCreate(&t1));
+    c->step_events->push_back(t1);
+  }
+  const KParams kp = c->kp;
+#define MDR_SW_L(A, SI, KA_, FO)                                                                          \
+  do {                                                                                                    \
+    if (t0)                                                                                               \
+      hipExtLaunchKernelGGL((k_step_window<A, kWinHpt, SI, KA_, FO>), dim3(grid), dim3(256), 0, st, t0, t1, 0, kp, \
+                            action, act_stride, tk, K, la_K, rec, reward, rew_stride, onb, wah, next_slot, dv); \
+    else                                                                                                  \
+      hipLaunchKernelGGL((k_step_window<A, kWinHpt, SI, KA_, FO>), dim3(grid), dim3(256), 0, st, kp, action,  \
+                         act_stride, tk, K, la_K, rec, reward, rew_stride, onb, wah, next_slot, dv);       \
+  } while (0)
+#define MDR_SW_F(A, SI, KA_)                                                            \
+  do {                                                                                  \
+    if (c->thermal == MDR_THERMAL_AFFINE) MDR_SW_L(A, SI, KA_, MDR_THERMAL_AFFINE);     \
+    else MDR_SW_L(A, SI, KA_, MDR_THERMAL_EXACT);                                       \
+  } while (0)
+#define MDR_SW_K(A, SI)                         \
+  do {                                          \
+    if (ka) MDR_SW_F(A, SI, true);              \
+    else MDR_SW_F(A, SI, false);                \
+  } while (0)
+#define MDR_SW_S(A)                             \
+  do {                                          \
+    if (win_simple(c)) MDR_SW_K(A, true);       \
+    else MDR_SW_K(A, false);                    \
+  } while (0)
+  if (mode == MDR_ACT_RANDOM) MDR_SW_S(MDR_ACT_RANDOM);
+  else if (mode == MDR_ACT_ALWAYS_ON) MDR_SW_S(MDR_ACT_ALWAYS_ON);
+  else MDR_SW_S(MDR_ACT_BUFFER);
+#undef MDR_SW_S
+#undef MDR_SW_K
+#undef MDR_SW_F
+#undef MDR_SW_L
+  LAUNCH_CHECK("k_step_window");
+  return MDR_OK;
+}
+
+// n ticks as ceil(n / win) windows of near-equal size: a k_count_window for the first window, then
+// per window k_win_reduce (shard sums -> counts + tick records; sharded: the shards are allreduced
+// first) and one k_step_window (counting the next window's ticks).  Tick drivers come from tk
+// (device, staged) for every window.
+//
+// host_ticks (direct launches, mdr_rollout without a graph; ids consecutive, checked by the caller):
+// the first window's count and a P-only reduce (already issued by mdr_rollout_begin when counted)
+// need only the tick ids; its step kernel then takes the drivers as kernel arguments
+// (k_step_window<..., KA>), and the later windows' drivers are staged into tk behind it (their
+// first reader is the first step kernel's lookahead... which reads tick ids only: tick0 + K + j).
 //
 // pipe (sharded, comm stream present): the count-ahead pipeline.  The FSM of an open-loop source
 // needs no thermal state, so window w's count (from the FSM words at the end of window w-1) and
 // the allreduce of its counts run on the comm stream, up to two windows ahead of the compute
 // stream's reduce + step (which then has no lookahead): the allreduce latency hides behind the
 // step kernels.  Two sets of ON-mask / end-word buffers alternate; events order the reuse.
-//
-// host_ticks (direct launches, mdr_rollout with use_graph = 0): the drivers are still in host
-// memory; the first reduce carries the first kStageRecs of them as kernel arguments and stages
-// them into tk (k_win_reduce_staged), the rest are staged behind the first step kernel (their
-// first reader is the second step kernel's lookahead), so no staging launch sits in front of the
-// first window.  Tick ids are consecutive (the caller checked), so the first count needs only
-// host_ticks[0].tick.
 static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t* action, int64_t act_stride,
                            int mode, double* reward, int64_t rew_stride, double* p_out, ncclComm_t comm,
-                           hipStream_t st, bool counted = false, bool lf = false, bool pipe = false,
-                           const mdr_tick* host_ticks = nullptr, bool ka = false) {
+                           hipStream_t st, bool counted = false, bool pipe = false,
+                           const mdr_tick* host_ticks = nullptr) {
   const int nw = (n + c->win - 1) / c->win;
   const int base = n / nw, rem = n % nw;
   auto wsz = [&](int w) { return base + (w < rem ? 1 : 0); };
   auto slot = [&](int w) { return c->d_wslab + (size_t)(w % 3) * c->wslab_len; };
-  const int hpt = c->win_hpt;
-  const unsigned grid = blocks(blocks(c->kp.n, 64 * hpt), 4);  // one 64*hpt-house tile per wave, 4 waves per block
-  KParams kp = c->kp;
+  const KParams kp = c->kp;
   const int ncap = kp.n_cap;
   auto rec = [&](int w) {  // the slot's tick records, after its shards and reduced counts
     return reinterpret_cast<const double*>(slot(w) + (size_t)kWindowMax * kCountShards * ncap + (size_t)kWindowMax * ncap);
   };
-#define MDR_WIN_DISPATCH_H(KERNEL, H, ...)                                                                     \
-  do {                                                                                                         \
-    if (mode == MDR_ACT_RANDOM) hipLaunchKernelGGL((KERNEL<MDR_ACT_RANDOM, H>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
-    else if (mode == MDR_ACT_ALWAYS_ON) hipLaunchKernelGGL((KERNEL<MDR_ACT_ALWAYS_ON, H>), dim3(grid), dim3(256), 0, st, __VA_ARGS__); \
-    else hipLaunchKernelGGL((KERNEL<MDR_ACT_BUFFER, H>), dim3(grid), dim3(256), 0, st, __VA_ARGS__);           \
-  } while (0)
-#define MDR_WIN_DISPATCH(KERNEL, ...)                                     \
-  do {                                                                   \
-    if (hpt == 1) MDR_WIN_DISPATCH_H(KERNEL, 1, __VA_ARGS__);            \
-    else MDR_WIN_DISPATCH_H(KERNEL, 2, __VA_ARGS__);                     \
-  } while (0)
-  // k_step_window: + the deadband 0 / norm_temp 1 specialisation (branch-free penalty, no division)
-  // (mdr_time_step_kernels: hipExtLaunchKernel's start / stop events time the step kernel itself)
-  hipEvent_t t_start = nullptr, t_stop = nullptr;
-#define MDR_STEP_LAUNCH(KERNEL, ...)                                                                       \
-  do {                                                                                                     \
-    if (t_start) hipExtLaunchKernelGGL((KERNEL), dim3(grid), dim3(256), 0, st, t_start, t_stop, 0, __VA_ARGS__); \
-    else hipLaunchKernelGGL((KERNEL), dim3(grid), dim3(256), 0, st, __VA_ARGS__);                          \
-  } while (0)
-#define MDR_WIN_DISPATCH_S(H, DB, ...)                                                                        \
-  do {                                                                                                        \
-    if (mode == MDR_ACT_RANDOM) MDR_STEP_LAUNCH((k_step_window<MDR_ACT_RANDOM, H, DB>), __VA_ARGS__);        \
-    else if (mode == MDR_ACT_ALWAYS_ON) MDR_STEP_LAUNCH((k_step_window<MDR_ACT_ALWAYS_ON, H, DB>), __VA_ARGS__); \
-    else MDR_STEP_LAUNCH((k_step_window<MDR_ACT_BUFFER, H, DB>), __VA_ARGS__);                              \
-  } while (0)
-  const bool db0 = win_simple(c);
-#define MDR_STEP_WIN_DISPATCH(...)                                         \
-  do {                                                                    \
-    if (hpt == 1) { if (db0) MDR_WIN_DISPATCH_S(1, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(1, false, __VA_ARGS__); } \
-    else { if (db0) MDR_WIN_DISPATCH_S(2, true, __VA_ARGS__); else MDR_WIN_DISPATCH_S(2, false, __VA_ARGS__); }        \
-  } while (0)
   c->wslab_dirty = true;  // until the sequence is fully issued
   if (pipe) {
     hipStream_t cs = c->comm_stream;
@@ -775,65 +745,45 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
       // comm stream: count(w) + allreduce; count(w) reuses the buffers step(w - 2) read
       if (w >= 2) HIP_TRY(hipStreamWaitEvent(cs, c->ev_k1[(w - 2) % kSlabs], 0));
       const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
-      const uint32_t* w_in = w == 0 ? nullptr : wahs[(w - 1) % 2];
-#define MDR_CNT_ON(H)                                                                                             \
-  do {                                                                                                            \
-    if (mode == MDR_ACT_RANDOM)                                                                                   \
-      hipLaunchKernelGGL((k_count_window<MDR_ACT_RANDOM, H>), dim3(grid), dim3(256), 0, cs, kp, a, act_stride,     \
-                         tk + t0, (uint64_t)0, (const uint64_t*)nullptr, K, slot(w), onbs[w % 2], wahs[w % 2], w_in); \
-    else if (mode == MDR_ACT_ALWAYS_ON)                                                                           \
-      hipLaunchKernelGGL((k_count_window<MDR_ACT_ALWAYS_ON, H>), dim3(grid), dim3(256), 0, cs, kp, a, act_stride,  \
-                         tk + t0, (uint64_t)0, (const uint64_t*)nullptr, K, slot(w), onbs[w % 2], wahs[w % 2], w_in); \
-    else                                                                                                          \
-      hipLaunchKernelGGL((k_count_window<MDR_ACT_BUFFER, H>), dim3(grid), dim3(256), 0, cs, kp, a, act_stride,     \
-                         tk + t0, (uint64_t)0, (const uint64_t*)nullptr, K, slot(w), onbs[w % 2], wahs[w % 2], w_in); \
-  } while (0)
-      if (hpt == 1) MDR_CNT_ON(1); else MDR_CNT_ON(2);
-#undef MDR_CNT_ON
-      LAUNCH_CHECK("k_count_window");
+      if (int rc = launch_count(c, mode, a, act_stride, tk + t0, 0, K, slot(w), onbs[w % 2], wahs[w % 2],
+                                w == 0 ? nullptr : wahs[(w - 1) % 2], cs))
+        return rc;
       if (comm)
         RCCL_TRY(ncclAllReduce(slot(w), slot(w), (size_t)K * kCountShards * ncap, ncclUint64, ncclSum, comm, cs));
       HIP_TRY(hipEventRecord(c->ev_ar[w % kSlabs], cs));
       // compute stream: reduce + step (no lookahead)
       HIP_TRY(hipStreamWaitEvent(st, c->ev_ar[w % kSlabs], 0));
       hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0,
-                         w == nw - 1 ? p_out : nullptr, (const int*)nullptr, w == nw - 1 ? c->d_lf + 1 : nullptr);
+                         w == nw - 1 ? p_out : nullptr);
       LAUNCH_CHECK("k_win_reduce");
-      const int* no_abort = nullptr;
-      MDR_STEP_WIN_DISPATCH(kp, a, act_stride, tk + t0, K, 0, rec(w), reward + (int64_t)t0 * rew_stride, rew_stride,
-                            onbs[w % 2], wahs[w % 2], slot(w), no_abort, WinDrv{});
-      LAUNCH_CHECK("k_step_window");
+      if (int rc = launch_step_window(c, mode, false, a, act_stride, tk + t0, K, 0, rec(w),
+                                      reward + (int64_t)t0 * rew_stride, rew_stride, onbs[w % 2], wahs[w % 2],
+                                      slot(w), WinDrv{}, st))
+        return rc;
       HIP_TRY(hipEventRecord(c->ev_k1[w % kSlabs], st));
       t0 += K;
     }
     c->wslab_dirty = false;
     return MDR_OK;
   }
-  const int* abort = lf ? reinterpret_cast<const int*>(c->d_lf + 2) : nullptr;
-  if (lf) {
-    MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, (const TickArgs*)nullptr, (uint64_t)0,
-                     (const uint64_t*)(c->d_lf + 1), wsz(0), slot(0), c->d_onb, c->d_wah, (const uint32_t*)nullptr);
-    LAUNCH_CHECK("k_count_window");
-    hipLaunchKernelGGL(k_lf_wait, dim3(1), dim3(256), 0, st, c->h_lf_ring, kLfCap, c->h_lf_ctl, c->d_lf,
-                       reinterpret_cast<int*>(c->d_lf + 2), n, const_cast<TickArgs*>(tk), c->lf_timeout);
-    LAUNCH_CHECK("k_lf_wait");
-  } else if (!counted) {  // (counted: mdr_rollout_begin launched it already)
-    MDR_WIN_DISPATCH(k_count_window, kp, action, act_stride, host_ticks ? (const TickArgs*)nullptr : tk,
-                     host_ticks ? host_ticks[0].tick : (uint64_t)0, (const uint64_t*)nullptr, wsz(0),
-                     slot(0), c->d_onb, c->d_wah, (const uint32_t*)nullptr);
-    LAUNCH_CHECK("k_count_window");
+  if (!counted) {  // (counted: mdr_rollout_begin launched the count and its P-only reduce already)
+    if (int rc = launch_count(c, mode, action, act_stride, host_ticks ? nullptr : tk,
+                              host_ticks ? host_ticks[0].tick : 0, wsz(0), slot(0), c->d_onb, c->d_wah, nullptr, st))
+      return rc;
+    if (host_ticks && comm)
+      RCCL_TRY(ncclAllReduce(slot(0), slot(0), (size_t)wsz(0) * kCountShards * ncap, ncclUint64, ncclSum, comm, st));
+    if (host_ticks) {  // the P-only reduce of the first window (the drivers come with the step)
+      hipLaunchKernelGGL(k_win_reduce, dim3(wsz(0)), dim3(64 * ncap), 0, st, kp, slot(0), wsz(0),
+                         (const TickArgs*)nullptr, (double*)nullptr);
+      LAUNCH_CHECK("k_win_reduce (P only)");
+    }
   }
   int t0 = 0;
   for (int w = 0; w < nw; ++w) {
     const int K = wsz(w), la = w + 1 < nw ? wsz(w + 1) : 0;
-    double* po = w == nw - 1 ? p_out : nullptr;
-    // sharded: every rank's sharded per-tick class counts are summed first (exact integers; the
-    // slot's shard part, K x 64 x n_cap values), so one reduce kernel yields the global counts
-    if (comm)
-      RCCL_TRY(ncclAllReduce(slot(w), slot(w), (size_t)K * kCountShards * ncap, ncclUint64, ncclSum, comm, st));
-    if (ka && w == 0) {
-      // the P-only reduce of this window ran in mdr_rollout_begin; the drivers ride on the step
-      // launch (k_step_window<..., KA>); the later windows' drivers are staged behind it
+    const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
+    if (host_ticks && w == 0) {
+      // KA: the drivers ride on the step launch; the later windows' drivers are staged behind it
       WinDrv dv{};
       for (int j = 0; j < K; ++j) {
         const mdr_tick& h = host_ticks[j];
@@ -843,59 +793,29 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
         if (fabs(h.t_od_prev) < 1048576.0 && fabs(h.solar) < 1099511627776.0) dv.ok |= 1u << j;  // (win_tick_record)
       }
       dv.tick0 = host_ticks[0].tick;
-      if (nw == 1) {
-        dv.p_out = p_out;
-        dv.next_tick = c->d_lf + 1;
-      }
-      const uint8_t* a = action;
-#define MDR_KA_LAUNCH(A)                                                                                        \
-  hipLaunchKernelGGL((k_step_window<A, 2, true, true>), dim3(grid), dim3(256), 0, st, kp, a, act_stride, tk, K, la, \
-                     rec(0), reward, rew_stride, c->d_onb, c->d_wah, slot(1), (const int*)nullptr, dv)
-      if (mode == MDR_ACT_RANDOM) MDR_KA_LAUNCH(MDR_ACT_RANDOM);
-      else if (mode == MDR_ACT_ALWAYS_ON) MDR_KA_LAUNCH(MDR_ACT_ALWAYS_ON);
-      else MDR_KA_LAUNCH(MDR_ACT_BUFFER);
-#undef MDR_KA_LAUNCH
-      LAUNCH_CHECK("k_step_window<KA>");
-      if (n > K) {
+      if (nw == 1) dv.p_out = p_out;
+      if (int rc = launch_step_window(c, mode, true, a, act_stride, tk, K, la, rec(0), reward, rew_stride, c->d_onb,
+                                      c->d_wah, slot(1), dv, st))
+        return rc;
+      if (n > K)
         if (int rc = stage_recs(host_ticks + K, n - K, const_cast<TickArgs*>(tk) + K, st)) return rc;
-      }
       t0 += K;
       continue;
     }
-    if (host_ticks && w == 0) {
-      StagePack pk;
-      const int m = n < kStageRecs ? n : kStageRecs;
-      memcpy(pk.r, host_ticks, (size_t)m * sizeof(Rec32));
-      hipLaunchKernelGGL(k_win_reduce_staged, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, pk, m,
-                         const_cast<TickArgs*>(tk), po, w == nw - 1 ? c->d_lf + 1 : nullptr);
-      LAUNCH_CHECK("k_win_reduce_staged");
-    } else {
-      hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0, po, abort,
-                         w == nw - 1 ? c->d_lf + 1 : nullptr);
-      LAUNCH_CHECK("k_win_reduce");
-    }
-    const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
-    if (c->step_events) {
-      HIP_TRY(hipEventCreate(&t_start));
-      c->step_events->push_back(t_start);
-      HIP_TRY(hipEventCreate(&t_stop));
-      c->step_events->push_back(t_stop);
-    }
-    MDR_STEP_WIN_DISPATCH(kp, a, act_stride, tk + t0, K, la, rec(w), reward + (int64_t)t0 * rew_stride, rew_stride,
-                          c->d_onb, c->d_wah, slot(w + 1), abort, WinDrv{});
-    LAUNCH_CHECK("k_step_window");
-    if (host_ticks && w == 0 && n > kStageRecs) {  // (K + la <= 2 * kWindowMax = kStageRecs were staged)
-      if (int rc = stage_recs(host_ticks + kStageRecs, n - kStageRecs, const_cast<TickArgs*>(tk) + kStageRecs, st))
-        return rc;
-    }
+    // sharded: every rank's sharded per-tick class counts are summed first (exact integers; the
+    // slot's shard part, K x 64 x n_cap values), so one reduce kernel yields the global counts
+    if (comm)
+      RCCL_TRY(ncclAllReduce(slot(w), slot(w), (size_t)K * kCountShards * ncap, ncclUint64, ncclSum, comm, st));
+    hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0,
+                       w == nw - 1 ? p_out : nullptr);
+    LAUNCH_CHECK("k_win_reduce");
+    if (int rc = launch_step_window(c, mode, false, a, act_stride, tk + t0, K, la, rec(w),
+                                    reward + (int64_t)t0 * rew_stride, rew_stride, c->d_onb, c->d_wah, slot(w + 1),
+                                    WinDrv{}, st))
+      return rc;
     t0 += K;
   }
   c->wslab_dirty = false;
-#undef MDR_WIN_DISPATCH
-#undef MDR_WIN_DISPATCH_H
-#undef MDR_WIN_DISPATCH_S
-#undef MDR_STEP_WIN_DISPATCH
-#undef MDR_STEP_LAUNCH
   return MDR_OK;
 }
 
@@ -913,12 +833,14 @@ static bool pipe_buffers(mdr_ctx* c) {
   return true;
 }
 
-// The launch sequence of a rollout; tick args come from d_ticks so a captured graph is reusable.
+// The launch sequence of a rollout with staged drivers (d_ticks), so a captured graph is reusable:
+// the window sequence, or one step launch per tick (+ phase 1 where no lookahead counts ahead).
 static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t act_stride, int mode,
-                            double* reward, int64_t rew_stride, double* p_out, hipStream_t st, bool counted = false,
-                            bool lf = false) {
-  if (window_ok(c, mode)) return window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride,
-                                                 p_out, nullptr, st, counted, lf);
+                            double* reward, int64_t rew_stride, double* p_out, hipStream_t st) {
+  if (window_ok(c, mode))
+    return window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st);
+  if (mode == MDR_ACT_BANGBANG || mode == MDR_ACT_DEADBAND_BANGBANG)
+    return fail(MDR_EARG, "rollout: bang-bang sources need the per-step API (mdr_step with a lookahead)");
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
   c->ring = 0;
   const bool la = lookahead_ok(mode);
@@ -926,63 +848,32 @@ static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t ac
     const uint8_t* a = action ? action + (int64_t)t * act_stride : nullptr;
     double* r = reward + (int64_t)t * rew_stride;
     if (!la || t == 0) {
-      int m = mode;
-      if (t == 0 && (mode == MDR_ACT_BANGBANG || mode == MDR_ACT_DEADBAND_BANGBANG)) {
-        // first tick under a bang-bang source: phase 1 needs the decision on the current state;
-        // write it into the context's scratch via a zero-reward dry step is not possible, so the
-        // caller must provide the first actions: handled by the caller (mode remapped to BUFFER)
-        return fail(MDR_EARG, "rollout: bang-bang sources need a BUFFER first tick (use mdr_step)");
-      }
-      hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256 * kPcHouses)), dim3(256), 0, st, c->kp, a, m,
+      hipLaunchKernelGGL(k_power_counts, dim3(blocks(c->kp.n, 256 * kPcHouses)), dim3(256), 0, st, c->kp, a, mode,
                          (uint64_t)0, c->d_ticks + t, slab_at(c, c->ring));
       LAUNCH_CHECK("k_power_counts");
     }
-    if (int rc = step_mark(c, st)) return rc;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (c->step_events) {
+      HIP_TRY(hipEventCreate(&e0));
+      c->step_events->push_back(e0);
+      HIP_TRY(hipEventRecord(e0, st));
+    }
     int rc = launch_step(c, a, mode, TickArgs{}, c->d_ticks + t, r, la ? mode : 0, MDR_CTRL_NONE,
                          nullptr, t == n - 1 ? p_out : nullptr, st);
     if (rc) return rc;
-    if (int rc2 = step_mark(c, st)) return rc2;
-  }
-  return MDR_OK;
-}
-
-// a launch-first graph that timed out waiting for its drivers (k_lf_wait abort code 2) did not
-// advance the state although its mdr_rollout returned: report it once, at the next rollout call
-static int lf_check(mdr_ctx* c) {
-  if (!c->h_lf_ctl) return MDR_OK;
-  const uint64_t a = __atomic_load_n(&c->h_lf_ctl[1], __ATOMIC_ACQUIRE);
-  const uint64_t seq = a & ((1ull << 62) - 1);
-  if ((a >> 62) == 2 && seq > c->lf_timeouts_seen) {
-    c->lf_timeouts_seen = seq;
-    c->wslab_dirty = true;
-    c->next_tick_known = false;
-    return fail(MDR_ESTATE, "a launch-first rollout timed out waiting for its tick drivers (10 s): its ticks were "
-                            "not applied to the device state");
-  }
-  return MDR_OK;
-}
-
-// post the drivers of the launched graph: ring slot seq & 1 (free once graph seq - 2 acknowledged
-// it; graphs run in order and every earlier one was posted or cancelled, so this wait always ends)
-static int lf_post(mdr_ctx* c, const mdr_tick* ticks, int n) {
-  const uint64_t seq = c->lf.seq, need = seq >= 2 ? seq - 2 : 0;
-  const auto t0 = std::chrono::steady_clock::now();
-  while ((__atomic_load_n(&c->h_lf_ctl[1], __ATOMIC_ACQUIRE) & ((1ull << 62) - 1)) < need) {
-    __builtin_ia32_pause();
-    if (std::chrono::steady_clock::now() - t0 > std::chrono::seconds(30)) {
-      lf_cancel(c);
-      return fail(MDR_EHIP, "mdr_rollout: the device did not consume a launch-first ring slot within 30 s");
+    if (c->step_events) {
+      HIP_TRY(hipEventCreate(&e1));
+      c->step_events->push_back(e1);
+      HIP_TRY(hipEventRecord(e1, st));
     }
   }
-  static_assert(sizeof(mdr_tick) == sizeof(TickArgs), "mdr_tick is a 32-byte record");
-  memcpy(c->h_lf_ring + (size_t)(seq & 1u) * kLfCap, ticks, (size_t)n * sizeof(TickArgs));
-  __atomic_store_n(&c->h_lf_ctl[0], seq, __ATOMIC_RELEASE);  // (x86: the records are visible first)
-  c->lf.on = false;
-  c->ring = c->lf.ring_end;
-  c->counts_ready = false;
-  c->next_tick_known = true;
-  c->next_tick = ticks[n - 1].tick + 1;
   return MDR_OK;
+}
+
+static bool consecutive(const mdr_tick* ticks, int n) {
+  for (int i = 1; i < n; ++i)
+    if (ticks[i].tick != ticks[0].tick + (uint64_t)i) return false;
+  return true;
 }
 
 int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action, int64_t act_stride,
@@ -993,100 +884,64 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
     return fail(MDR_EARG, "mdr_rollout: common penalty modes need the per-step API");
   hipStream_t st = S(stream);
-  static const bool trace = getenv("MDR_TRACE") != nullptr;  // host-side phase timing (diagnostics)
-  const auto t0 = std::chrono::steady_clock::now();
-  if (int rc = lf_check(c)) return rc;
-  if (c->lf.on) {  // launched by mdr_rollout_launch for exactly this call: post the drivers
-    if (use_graph && c->lf.n == n && c->lf.mode == mode && c->lf.tick0 == ticks[0].tick && c->lf.action == action &&
-        c->lf.act_stride == act_stride && c->lf.reward == reward && c->lf.rew_stride == rew_stride &&
-        c->lf.p_out == p_out)
-      return lf_post(c, ticks, n);
-    lf_cancel(c);
-  }
-  // the first window counted ahead by mdr_rollout_begin for exactly this call?
+  const bool win = window_ok(c, mode);
+  const bool consec = consecutive(ticks, n);
+  // the first window counted ahead by mdr_rollout_begin for exactly this call?  (Its count took
+  // the ids tick0 + j and its P-only reduce consumed the slot's shards: only the direct sequence
+  // with the drivers as kernel arguments can follow it, whatever use_graph asks.)
   const bool counted = c->begun.on && !c->begun.sharded && c->begun.n == n && c->begun.mode == mode &&
                        c->begun.tick0 == ticks[0].tick && c->begun.action == action &&
-                       c->begun.act_stride == act_stride && window_ok(c, mode);
+                       c->begun.act_stride == act_stride && win && consec;
   if (c->begun.on && !counted) c->wslab_dirty = true;  // an unmatched early count: clear its shards
-  const bool ka = counted && c->begun.ka;
   c->begun.on = false;
   int rc = refresh_if_dirty(c, st);
   if (rc) return rc;
-  static const bool pipe_single = getenv("MDR_PIPE_SINGLE") != nullptr;  // A/B: count-ahead pipeline, 1 GPU
-  // (ka: the P-only reduce already consumed the first window's shards, so only the direct KA
-  // sequence can follow it, whatever use_graph asks)
-  if (ka || (!use_graph && !pipe_single && window_ok(c, mode))) {
-    // direct launches of the windowed path: the drivers travel as kernel arguments of the first
-    // reduce (window_launches host_ticks); needs consecutive tick ids (as driver_window makes them)
-    bool consec = true;
-    for (int i = 1; i < n && consec; ++i) consec = ticks[i].tick == ticks[0].tick + (uint64_t)i;
-    if (consec || ka) {  // (ka: mdr_rollout_begin checked the window's ids against tick0: consecutive by construction)
-      rc = ensure_ticks(c, n);
-      if (!rc) rc = wslab_clean(c, st);
-      if (!rc)
-        rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st,
-                             counted, false, false, ticks, ka);
-      c->counts_ready = false;
-      c->next_tick_known = !rc;
-      c->next_tick = ticks[n - 1].tick + 1;
-      return rc;
-    }
-  }
-  rc = stage_ticks(c, n, ticks, st);
-  if (rc) return rc;
-  rc = wslab_clean(c, st);
-  if (rc) return rc;
-  const auto t1 = std::chrono::steady_clock::now();
-  if (pipe_single && window_ok(c, mode) && !counted) {
-    if (!c->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
-    if (pipe_buffers(c)) {
-      rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st, false,
-                           false, true);
-      c->counts_ready = false;
-      c->next_tick_known = !rc;
-      c->next_tick = ticks[n - 1].tick + 1;
-      return rc;
-    }
-  }
-  if (!use_graph) {
-    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st, counted);
+  if (counted || (win && !use_graph && consec)) {
+    // direct launches of the windowed path: the first window's drivers travel as kernel arguments
+    // of its step kernel (window_launches host_ticks)
+    rc = ensure_ticks(c, n);
+    if (!rc) rc = wslab_clean(c, st);
+    if (!rc)
+      rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st, counted,
+                           false, ticks);
     c->counts_ready = false;
-    c->next_tick_known = !rc && window_ok(c, mode);
-    c->next_tick = ticks[n - 1].tick + 1;
     return rc;
   }
-  GraphKey key{n, mode + (counted ? 1000 : 0), action, act_stride, reward, rew_stride, p_out, nullptr};
+  rc = stage_ticks(c, n, ticks, st);
+  if (!rc) rc = wslab_clean(c, st);
+  if (rc) return rc;
+  if (!use_graph) {
+    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st);
+    c->counts_ready = false;
+    return rc;
+  }
+  GraphKey key{n, mode, action, act_stride, reward, rew_stride, p_out};
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraphExec_t ex;
     rc = capture_graph(c, [&](hipStream_t cs) {
-      return rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, cs, counted);
+      return rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, cs);
     }, &ex);
-    if (rc) return rc;
+    if (rc) {
+      c->wslab_dirty = true;
+      return rc;
+    }
     it = c->graphs.emplace(key, std::make_pair(ex, c->ring)).first;
   }
-  const auto t2 = std::chrono::steady_clock::now();
   if (hipGraphLaunch(it->second.first, st) != hipSuccess) {
     c->wslab_dirty = true;
     return fail(MDR_EHIP, "mdr_rollout: hipGraphLaunch");
   }
   c->ring = it->second.second;
   c->counts_ready = false;
-  c->next_tick_known = window_ok(c, mode);  // (the window sequence's last reduce wrote it)
-  c->next_tick = ticks[n - 1].tick + 1;
-  if (trace) {
-    const auto t3 = std::chrono::steady_clock::now();
-    auto us = [](auto a, auto b) { return std::chrono::duration<double, std::micro>(b - a).count(); };
-    fprintf(stderr, "mdr_rollout n=%d: stage %.1f us, graph lookup/capture %.1f us, hipGraphLaunch %.1f us\n", n,
-            us(t0, t1), us(t1, t2), us(t2, t3));
-  }
   return MDR_OK;
 }
 
-// The first window's FSM counts of an mdr_rollout of n ticks from tick id tick0, launched before the
-// host has the ticks' drivers (they only need the tick ids), so the count overlaps the host work.
-// The next mdr_rollout with the same (n, mode, action, tick0) skips its count; any other call
-// discards it.  A no-op (returns 0) when the rollout will not take the temporally blocked path.
+// The first window's FSM counts (and its cluster power P) of an mdr_rollout of n ticks from tick
+// id tick0, launched before the host has the ticks' drivers (they only need the tick ids), so the
+// count overlaps the host work.  The next mdr_rollout with the same (n, mode, action, tick0) skips
+// them; any other call discards them.  A no-op (returns 0) when the rollout will not take the
+// temporally blocked path.
 int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, int64_t act_stride, int mode,
                       void* stream) {
   if (!c || n < 1) return fail(MDR_EARG, "mdr_rollout_begin: bad argument");
@@ -1098,43 +953,25 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   // a sharded context (RCCL attached): single-window rollouts only, counts allreduced here, so
   // the matching mdr_rollout_sharded launches just the KA step kernel
   const bool sharded = c->comm != nullptr;
-  const bool ka = c->win_hpt == 2 && win_simple(c) && !getenv("MDR_NO_KA");
-  if (sharded && (n > c->win || !ka)) return MDR_OK;
+  if (sharded && n > c->win) return MDR_OK;
   hipStream_t st = S(stream);
   int rc = refresh_if_dirty(c, st);
   if (!rc) rc = wslab_clean(c, st);
   if (rc) return rc;
   const int nw = (n + c->win - 1) / c->win;
   const int k0 = n / nw + (n % nw ? 1 : 0);  // window_launches' first window
-  const unsigned grid = blocks(blocks(c->kp.n, 64 * c->win_hpt), 4);
   c->wslab_dirty = true;
-#define MDR_BEGIN_COUNT(A, H)                                                                                   \
-  hipLaunchKernelGGL((k_count_window<A, H>), dim3(grid), dim3(256), 0, st, c->kp, action, act_stride,          \
-                     (const TickArgs*)nullptr, tick0, (const uint64_t*)nullptr, k0, c->d_wslab, c->d_onb, c->d_wah,  \
-                     (const uint32_t*)nullptr)
-  if (c->win_hpt == 1) {
-    if (mode == MDR_ACT_RANDOM) MDR_BEGIN_COUNT(MDR_ACT_RANDOM, 1);
-    else if (mode == MDR_ACT_ALWAYS_ON) MDR_BEGIN_COUNT(MDR_ACT_ALWAYS_ON, 1);
-    else MDR_BEGIN_COUNT(MDR_ACT_BUFFER, 1);
-  } else {
-    if (mode == MDR_ACT_RANDOM) MDR_BEGIN_COUNT(MDR_ACT_RANDOM, 2);
-    else if (mode == MDR_ACT_ALWAYS_ON) MDR_BEGIN_COUNT(MDR_ACT_ALWAYS_ON, 2);
-    else MDR_BEGIN_COUNT(MDR_ACT_BUFFER, 2);
-  }
-#undef MDR_BEGIN_COUNT
-  LAUNCH_CHECK("k_count_window");
+  rc = launch_count(c, mode, action, act_stride, nullptr, tick0, k0, c->d_wslab, c->d_onb, c->d_wah, nullptr, st);
+  if (rc) return rc;
   if (sharded)  // every rank's sharded per-tick class counts, summed (exact integers)
     RCCL_TRY(ncclAllReduce(c->d_wslab, c->d_wslab, (size_t)k0 * kCountShards * c->kp.n_cap, ncclUint64, ncclSum,
                            c->comm, st));
   // the window's P (the counts need no drivers): the matching direct mdr_rollout then launches the
   // step kernel with the drivers as arguments (k_step_window<..., KA>), nothing in between
-  if (ka) {
-    hipLaunchKernelGGL(k_win_reduce, dim3(k0), dim3(64 * c->kp.n_cap), 0, st, c->kp, c->d_wslab, k0,
-                       (const TickArgs*)nullptr, (double*)nullptr, (const int*)nullptr, (uint64_t*)nullptr);
-    LAUNCH_CHECK("k_win_reduce (P only)");
-  }
+  hipLaunchKernelGGL(k_win_reduce, dim3(k0), dim3(64 * c->kp.n_cap), 0, st, c->kp, c->d_wslab, k0,
+                     (const TickArgs*)nullptr, (double*)nullptr);
+  LAUNCH_CHECK("k_win_reduce (P only)");
   c->wslab_dirty = false;
-  c->begun.ka = ka;
   c->begun.sharded = sharded;
   c->begun.on = true;
   c->begun.n = n; c->begun.mode = mode; c->begun.tick0 = tick0;
@@ -1142,97 +979,10 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   return MDR_OK;
 }
 
-// Launch-first rollout: the graph of an mdr_rollout of n ticks from tick id tick0 is launched NOW,
-// before the host has computed the ticks' drivers.  It counts the first window's FSM and then waits
-// on the device (k_lf_wait) until the matching mdr_rollout posts the drivers through pinned memory,
-// so the graph launch and the count overlap the host work.  The next mdr_rollout with the same
-// arguments posts; any other entry point cancels it (the graph then skips every kernel).  Falls
-// back to mdr_rollout_begin when the launch-first path does not apply: a random source needs the
-// device to know tick0 (the previous rollout ended at tick0 - 1), n <= 1024, the windowed path.
-int mdr_rollout_launch(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, int64_t act_stride, int mode,
-                       double* reward, int64_t rew_stride, double* p_out, void* stream) {
-  drop_begun(c);
-  if (!c || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout_launch: bad argument");
-  if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout_launch: context not bound");
-  if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout_launch: bad action source");
-  if (int rc = lf_check(c)) return rc;
-  const bool ok = c->h_lf_ring && window_ok(c, mode) && n <= kLfCap && c->kp.penalty_mode == MDR_PEN_INDIVIDUAL_L2 &&
-                  (mode != MDR_ACT_RANDOM || (c->next_tick_known && c->next_tick == tick0)) &&
-                  !c->lf_disabled && !getenv("MDR_NO_LAUNCH_FIRST");
-  if (!ok) return mdr_rollout_begin(c, n, tick0, action, act_stride, mode, stream);
-  hipStream_t st = S(stream);
-  int rc = refresh_if_dirty(c, st);
-  if (!rc) rc = wslab_clean(c, st);
-  if (!rc) rc = ensure_ticks(c, n);
-  if (rc) return rc;
-  int ring_end = c->ring;
-  if (!getenv("MDR_LF_GRAPH")) {
-    // direct launches (the default: measured faster than a graph replay, whose host call costs
-    // 10-15 us before the device starts): count, wait, then the windows, issued one by one
-    rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, st, false, true);
-    if (rc) {
-      // a sequence that failed part-way may or may not have queued its k_lf_wait: cancel it (it
-      // aborts if it runs) and stop using launch-first on this context, whose device-side sequence
-      // number can no longer be trusted to match the host's
-      c->lf_seq += 1;
-      c->lf.on = true;
-      c->lf.seq = c->lf_seq;
-      lf_cancel(c);
-      c->lf_disabled = true;
-      c->next_tick_known = false;
-      return rc;
-    }
-    ring_end = c->ring;
-  } else {
-    GraphKey key{n, mode + 2000, action, act_stride, reward, rew_stride, p_out, nullptr};
-    auto it = c->graphs.find(key);
-    if (it == c->graphs.end()) {
-      hipGraphExec_t ex;
-      rc = capture_graph(c, [&](hipStream_t cs) {
-        return rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, p_out, cs, false, true);
-      }, &ex);
-      if (rc) return rc;
-      it = c->graphs.emplace(key, std::make_pair(ex, c->ring)).first;
-    }
-    if (hipGraphLaunch(it->second.first, st) != hipSuccess) {
-      c->wslab_dirty = true;
-      return fail(MDR_EHIP, "mdr_rollout_launch: hipGraphLaunch");
-    }
-    ring_end = it->second.second;
-  }
-  c->lf_seq += 1;
-  c->lf.on = true;
-  c->lf.seq = c->lf_seq;
-  c->lf.tick0 = tick0;
-  c->lf.n = n;
-  c->lf.mode = mode;
-  c->lf.ring_end = ring_end;
-  c->lf.action = action;
-  c->lf.act_stride = act_stride;
-  c->lf.reward = reward;
-  c->lf.rew_stride = rew_stride;
-  c->lf.p_out = p_out;
-  return MDR_OK;
-}
-
-// Diagnostics: launch-first graphs launched so far on this context.
-int mdr_rollout_launched(mdr_ctx* c, uint64_t* count) {
-  if (!c || !count) return fail(MDR_EARG, "mdr_rollout_launched: null argument");
-  *count = c->lf_seq;
-  return MDR_OK;
-}
-
-// Cancel a launched rollout whose drivers will not come (the launched graph skips its kernels; the
-// device state is unchanged).  A no-op when none is pending.
-int mdr_rollout_cancel(mdr_ctx* c) {
-  if (!c) return fail(MDR_EARG, "mdr_rollout_cancel: null context");
-  drop_begun(c);
-  return MDR_OK;
-}
-
-// Measurement: one rollout as direct launches (no graph) with an event pair around every step-kernel
-// launch (k_step_window on the window path, k_step_* per tick otherwise); *ms = the summed kernel
-// time, *launches = the number of step launches.  Synchronises on the last event.
+// Measurement: one rollout as direct launches (no graph, drivers staged first) with an event pair
+// around every step-kernel launch (k_step_window on the window path, k_step_* per tick otherwise);
+// *ms = the summed kernel time, *launches = the number of step launches.  Synchronises on the last
+// event.
 int mdr_time_step_kernels(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action, int64_t act_stride,
                           int mode, double* reward, int64_t rew_stride, void* stream, float* ms, int* launches) {
   drop_begun(c);
@@ -1252,8 +1002,6 @@ int mdr_time_step_kernels(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_
   rc = rollout_launches(c, n, action, act_stride, mode, reward, rew_stride, nullptr, st);
   c->step_events = nullptr;
   c->counts_ready = false;
-  c->next_tick_known = !rc && window_ok(c, mode);
-  c->next_tick = ticks[n - 1].tick + 1;
   float total = 0.0f;
   if (!rc && !evs.empty() && hipEventSynchronize(evs.back()) != hipSuccess) rc = fail(MDR_EHIP, "event sync");
   for (size_t i = 0; !rc && i + 1 < evs.size(); i += 2) {
@@ -1411,7 +1159,7 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   const int n = (int)c->kp.n;
   double pmin = INFINITY;
   for (int k = 0; k < c->cfg.n_cap; ++k) pmin = fmin(pmin, c->cfg.cap_table[k] / c->cfg.cop);
-  if (c->kp.n_cap <= 4 && n < (1 << 30) && !getenv("MDR_GREEDY_SORT")) {
+  if (c->kp.n_cap <= 4 && n < (1 << 30) && !c->greedy_sort) {
     // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster; the sort form below
     // runs only when the candidate window cannot decide (the flag read back here)
     // (g_sel's only accumulated field, overflow, is cleared by k_gq_finish for the next call)
@@ -1599,35 +1347,6 @@ int rollout_sharded_serial(mdr_ctx* c, const TickArgs* ticks, int n, const uint8
   return MDR_OK;
 }
 
-// MDR_SHARDED_AUTO: the first eligible rollout (>= 16 ticks) runs half its ticks serial and half
-// overlapped, times both on the stream, takes the max over ranks (RCCL) so every rank decides
-// the same, and keeps the faster pipeline.  Both produce bit-identical results.
-int rollout_sharded_calibrate(mdr_ctx* c, int n, int mode, double* reward, int64_t rew_stride,
-                              double* p_out, hipStream_t st) {
-  const int n1 = n / 2;
-  HIP_TRY(hipEventRecord(c->ev[13], st));
-  int rc = rollout_sharded_serial(c, c->d_ticks, n1, nullptr, 0, mode, reward, rew_stride, nullptr, st);
-  if (rc) return rc;
-  HIP_TRY(hipEventRecord(c->ev[14], st));
-  rc = rollout_sharded_overlap(c, c->d_ticks + n1, n - n1, mode, reward + (int64_t)n1 * rew_stride,
-                               rew_stride, p_out, st);
-  if (rc) return rc;
-  HIP_TRY(hipEventRecord(c->ev[15], st));
-  HIP_TRY(hipEventSynchronize(c->ev[15]));
-  float ms_serial = 0.f, ms_overlap = 0.f;
-  HIP_TRY(hipEventElapsedTime(&ms_serial, c->ev[13], c->ev[14]));
-  HIP_TRY(hipEventElapsedTime(&ms_overlap, c->ev[14], c->ev[15]));
-  double h[2] = {ms_serial / n1, ms_overlap / (n - n1)};
-  double* d = c->d_partial2;  // 2 doubles of scratch, free outside the common-penalty steps
-  HIP_TRY(hipMemcpyAsync(d, h, sizeof(h), hipMemcpyHostToDevice, st));
-  RCCL_TRY(ncclAllReduce(d, d, 2, ncclFloat64, ncclMax, c->comm, st));
-  HIP_TRY(hipMemcpyAsync(h, d, sizeof(h), hipMemcpyDeviceToHost, st));
-  HIP_TRY(hipStreamSynchronize(st));
-  c->calib_us[0] = h[0] * 1e3;
-  c->calib_us[1] = h[1] * 1e3;
-  c->overlap_mode = h[1] < h[0] ? 1 : 0;
-  return MDR_OK;
-}
 }  // namespace
 
 extern "C" {
@@ -1638,18 +1357,16 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
   if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout_sharded: bad argument");
   // a single window begun by mdr_rollout_begin on this sharded context (count, allreduce, P-only
   // reduce already issued): only the KA step kernel is left, with these drivers as its arguments
-  if (c->begun.on && c->begun.sharded && c->begun.ka && c->comm && c->begun.n == n && c->begun.mode == mode &&
+  if (c->begun.on && c->begun.sharded && c->comm && c->begun.n == n && c->begun.mode == mode &&
       c->begun.tick0 == ticks[0].tick && c->begun.action == action && c->begun.act_stride == act_stride &&
-      window_ok(c, mode) && n <= c->win) {
+      window_ok(c, mode) && n <= c->win && consecutive(ticks, n)) {
     c->begun.on = false;
     hipStream_t st = S(stream);
     int rc = ensure_ticks(c, n);
     if (!rc)
       rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st, true,
-                           false, false, ticks, true);
+                           false, ticks);
     c->counts_ready = false;
-    c->next_tick_known = !rc;
-    c->next_tick = ticks[n - 1].tick + 1;
     return rc;
   }
   drop_begun(c);
@@ -1670,25 +1387,20 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
     if (rc) return rc;
     const bool pipe = c->win_pipe && c->comm_stream && pipe_buffers(c);
     rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, c->comm, st, false,
-                         false, pipe);
+                         pipe);
     c->counts_ready = false;
-    c->next_tick_known = !rc;
-    c->next_tick = ticks[n - 1].tick + 1;
     return rc;
   }
   const bool can_overlap = lookahead_ok(mode) && rew_stride != 0 && c->comm_stream;
-  if (can_overlap && c->overlap_mode < 0 && n >= 16)
-    return rollout_sharded_calibrate(c, n, mode, reward, rew_stride, p_out, st);
-  if (can_overlap && c->overlap_mode == 1)
+  if (can_overlap && c->tick_overlap)
     return rollout_sharded_overlap(c, c->d_ticks, n, mode, reward, rew_stride, p_out, st);
   return rollout_sharded_serial(c, c->d_ticks, n, action, act_stride, mode, reward, rew_stride, p_out, st);
 }
 
-int mdr_rollout_sharded_mode(mdr_ctx* c, int* mode, double* us_serial, double* us_overlap) {
-  if (!c || !mode) return fail(MDR_EARG, "mdr_rollout_sharded_mode: null argument");
-  *mode = c->overlap_mode;
-  if (us_serial) *us_serial = c->calib_us[0];
-  if (us_overlap) *us_overlap = c->calib_us[1];
+int mdr_rollout_sharded_mode(mdr_ctx* c, int* window_pipeline, int* tick_overlap) {
+  if (!c || !window_pipeline || !tick_overlap) return fail(MDR_EARG, "mdr_rollout_sharded_mode: null argument");
+  *window_pipeline = c->win > 0 && c->win_pipe && c->comm_stream != nullptr;
+  *tick_overlap = c->tick_overlap && c->comm_stream != nullptr;
   return MDR_OK;
 }
 
@@ -1698,8 +1410,7 @@ int mdr_set_rollout_window(mdr_ctx* c, int ticks) {
   if (ticks > 0 && !c->d_wslab) return fail(MDR_EARG, "mdr_set_rollout_window: more than 4 capacity classes");
   if (ticks != c->win) {
     HIP_TRY(hipDeviceSynchronize());  // cached graphs may be in flight
-    for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
-    c->graphs.clear();
+    destroy_graphs(c);
     c->win = ticks;
   }
   return MDR_OK;
@@ -1992,8 +1703,7 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
   const int lo = K / 2, hi = (K + 1) / 2;
   // MDR_FORCE_HALO=1 (test hook): exchange the halo even at world 1 (send/recv to self), which
   // must reproduce the local ring wrap-around — the 1-GPU check of the multi-GPU exchange
-  static const bool force_halo = getenv("MDR_FORCE_HALO") && atoi(getenv("MDR_FORCE_HALO")) != 0;
-  const bool halo = (c->world > 1 || force_halo) && K > 0;
+  const bool halo = (c->world > 1 || c->force_halo) && K > 0;
   if (halo && sp->comm_mode != MDR_COMM_RING)
     return fail(MDR_EARG, "mdr_actor_rollout_sharded: across shards only the 'neighbours' ring obs is supported");
   if (halo && c->kp.n < (lo > hi ? lo : hi))
@@ -2007,7 +1717,6 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
   if (halo && hbytes > c->halo_bytes) {
     HIP_TRY(hipStreamSynchronize(st));
     hipFree(c->d_halo);
-  hipFree(c->d_stats);
     c->d_halo = nullptr;
     HIP_TRY(hipMalloc(&c->d_halo, hbytes));
     c->halo_bytes = hbytes;

@@ -31,8 +31,6 @@ struct KParams {
   const uint8_t* cap_idx;
   const double* q_on;  // [n_cap] -cap/(1+lcf)      (device, context-owned)
   const double* p_on;  // [n_cap] cap/cop
-  const double* coef;  // [6][coef_stride] cached rc_coeffs (r1, r2, A3, A4, e1, e2) or null
-  int64_t coef_stride;
   const int* params_bad;  // device flag: some house's parameters are outside the fast-division range
   int fast_tick_ok;       // host-checked: dt and the capacity table are inside that range
 };
@@ -75,7 +73,7 @@ __global__ void k_stage32(StagePack pk, int n, Rec32* dst);
 constexpr int kPcHouses = 4;  // chunks of 256 houses per k_power_counts block (grid: blocks(n, 256 * kPcHouses))
 __global__ void k_power_counts(KParams p, const uint8_t* action, int action_mode, uint64_t tick,
                                const TickArgs* tkp, unsigned long long* slab);
-template <int HPT, bool CACHED, bool FAST, int ACT, int LA>
+template <int HPT, bool FAST, int ACT, int LA>
 __global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, TickArgs tk,
                          const TickArgs* tkp, const unsigned long long* counts, double* reward,
                          int ctrl, uint8_t* ctrl_out, double* p_out, int lookahead,
@@ -89,6 +87,7 @@ constexpr int kPipeMaxCap = 4;
 constexpr int kWindowMax = 32;  // = kWinMax: ticks per k_step_window launch
 constexpr int kWindowCap = 4;   // = kWinCap: capacity classes the window kernel supports
 constexpr int kWindowRec = 4;   // = kWinRec: doubles per tick record of a window count slot
+constexpr int kWinHpt = 2;      // houses per lane of the window kernels (a 128-house tile per wave)
 // The first window's drivers as kernel arguments (k_step_window<..., KA = true>): the host computes
 // them while the window's count and P-only reduce already run, and launches the step kernel with
 // them, so no reduce or staging launch sits between the host's drivers and the thermal loop.
@@ -98,26 +97,22 @@ struct WinDrv {
   double s_prev[kWindowMax];  // the signal the tick's reward compares P with
   uint64_t tick0;             // the window's first tick id (ids are consecutive)
   double* p_out;              // last window: <- P of its last tick
-  uint64_t* next_tick;        // last window: <- the tick id the next rollout starts at
   uint32_t ok;                // bit j: tick j's drivers are in the fast-division ranges
 };
-template <int ACT, int HPT, bool SIMPLE, bool KA = false>  // SIMPLE: deadband 0 and norm_temp 1 (reward without branches / division)
+// SIMPLE: deadband 0 and norm_temp 1 (reward without branches / division); FORM: the per-tick
+// thermal update, MDR_THERMAL_EXACT (the reference's expression) or MDR_THERMAL_AFFINE (its
+// per-window transition coefficients, mdr_kernels.hip K1W)
+template <int ACT, int HPT, bool SIMPLE, bool KA, int FORM>
 __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int K,
                               int la_K, const double* rec, double* reward, int64_t rew_stride, uint64_t* onb,
-                              uint32_t* wah, unsigned long long* next_slot, const int* abort, WinDrv dv);
-__global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out,
-                             const int* abort, uint64_t* next_tick);
-__global__ void k_win_reduce_staged(KParams p, unsigned long long* slot, int nt, StagePack pk, int n_pk,
-                                    TickArgs* dst, double* p_out, uint64_t* next_tick);
+                              uint32_t* wah, unsigned long long* next_slot, WinDrv dv);
+__global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
 template <int ACT, int HPT>
 __global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp,
-                               uint64_t tick0, const uint64_t* tick0p, int nt, unsigned long long* slot,
-                               uint64_t* onb, uint32_t* wah, const uint32_t* w_in);
-__global__ void k_lf_wait(const TickArgs* ring, int cap, uint64_t* ctl, uint64_t* dseq, int* dabort, int n,
-                          TickArgs* dst, uint64_t timeout_ticks);
-constexpr int kLfCap = 1024;  // ticks per launch-first ring slot
+                               uint64_t tick0, int nt, unsigned long long* slot, uint64_t* onb, uint32_t* wah,
+                               const uint32_t* w_in);
 __global__ void k_probe_stream(KParams p, double* reward);
-__global__ void k_refresh(KParams p, double* coef, int* params_bad);
+__global__ void k_refresh(KParams p, int* params_bad);
 __global__ void k_div_check(const double* a, const double* b, int64_t n, unsigned long long* mismatches);
 __global__ void k_pen_reduce(const double* pen_partial, int nblk, double* partial2);
 __global__ void k_reward_finalize(KParams p, TickArgs tk, const unsigned long long* counts,

@@ -136,15 +136,8 @@ __device__ __forceinline__ void sto(void* base, uint32_t off, V v) {
   *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + off) = v;
 }
 
-// MDR_STEP_WAVES (build-time A/B knob): cap k_step_t at that many waves/SIMD (VGPR budget 512/W).
-#ifdef MDR_STEP_WAVES
-#define MDR_STEP_OCC __attribute__((amdgpu_waves_per_eu(MDR_STEP_WAVES)))
-#else
-#define MDR_STEP_OCC
-#endif
-
-template <int HPT, bool CACHED, bool FAST, int ACT, int LA>
-__global__ void __launch_bounds__(256) MDR_STEP_OCC k_step_t(KParams p, const uint8_t* __restrict__ action,
+template <int HPT, bool FAST, int ACT, int LA>
+__global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __restrict__ action,
                                                 int action_mode_rt, TickArgs tk0, const TickArgs* tkp,
                                                 const unsigned long long* __restrict__ counts,
                                                 double* __restrict__ reward, int ctrl,
@@ -176,10 +169,9 @@ __global__ void __launch_bounds__(256) MDR_STEP_OCC k_step_t(KParams p, const ui
 
   // ---- all per-house loads first (one round trip)
   uint32_t w0[HPT];
-  double T[HPT], Tm[HPT], ua[HPT], ca[HPT], cm[HPT], hm[HPT], tg[HPT];
-  RcCoef kc[HPT];
+  double T[HPT], Tm[HPT], ua[HPT], ca[HPT], hm[HPT], tg[HPT];
+  double cm[HPT];
   int cls[HPT];
-  const uint32_t cs = (uint32_t)p.coef_stride;
   if (HPT == 2 && valid[HPT - 1]) {
     const uint32_t o8 = i0 * 8u;
     auto ld2 = [&](const double* a) { return ldo<double2>(a, o8); };
@@ -192,27 +184,15 @@ __global__ void __launch_bounds__(256) MDR_STEP_OCC k_step_t(KParams p, const ui
     hm[0] = vhm.x; hm[HPT - 1] = vhm.y;
     tg[0] = vtg.x; tg[HPT - 1] = vtg.y; w0[0] = vw.x; w0[HPT - 1] = vw.y;
     cls[0] = vc & 0xFF; cls[HPT - 1] = vc >> 8;
-    if (CACHED) {
-      const double2 r1 = ld2(p.coef), r2 = ld2(p.coef + cs), A3 = ld2(p.coef + 2 * cs);
-      const double2 A4 = ld2(p.coef + 3 * cs), e1 = ld2(p.coef + 4 * cs), e2 = ld2(p.coef + 5 * cs);
-      kc[0] = RcCoef{r1.x, r2.x, A3.x, A4.x, e1.x, e2.x};
-      kc[HPT - 1] = RcCoef{r1.y, r2.y, A3.y, A4.y, e1.y, e2.y};
-    } else {
-      const double2 vcm = ld2(p.cm);
-      cm[0] = vcm.x; cm[HPT - 1] = vcm.y;
-    }
+    const double2 vcm = ld2(p.cm);
+    cm[0] = vcm.x; cm[HPT - 1] = vcm.y;
   } else {
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
       const uint32_t i = valid[h] ? i0 + h : 0u;
       T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; ca[h] = p.ca[i];
       hm[h] = p.hm[i]; tg[h] = p.target[i]; w0[h] = p.hvac[i]; cls[h] = p.cap_idx[i];
-      if (CACHED) {
-        const double* c = p.coef + i;
-        kc[h] = RcCoef{c[0], c[cs], c[2 * cs], c[3 * cs], c[4 * cs], c[5 * cs]};
-      } else {
-        cm[h] = p.cm[i];
-      }
+      cm[h] = p.cm[i];
     }
   }
   __syncthreads();  // hist zeroed (the loads above stay in flight across the barrier)
@@ -264,11 +244,11 @@ __global__ void __launch_bounds__(256) MDR_STEP_OCC k_step_t(KParams p, const ui
     on[h] = hv_on(w[h]);
     const double q = on[h] ? p.q_on[cls[h]] : 0.0;
     if (tile_fast) {
-      if (!CACHED) kc[h] = rc_coeffs_t<FAST>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
-      rc_apply_t<FAST>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
+      const RcCoef kc = rc_coeffs_t<FAST>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+      rc_apply_t<FAST>(T[h], Tm[h], ua[h], ca[h], hm[h], kc, q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
     } else {
-      if (!CACHED) kc[h] = rc_coeffs_t<false>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
-      rc_apply_t<false>(T[h], Tm[h], ua[h], ca[h], hm[h], kc[h], q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
+      const RcCoef kc = rc_coeffs_t<false>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+      rc_apply_t<false>(T[h], Tm[h], ua[h], ca[h], hm[h], kc, q, tk.solar, tk.t_od_prev, Tn[h], Tmn[h]);
     }
     pen[h] = deadband_l2(tg[h], p.deadband, reward_lag ? T[h] : Tn[h]);
     // x / 1.0 == x exactly: the default normaliser (integer target) costs no division
@@ -650,7 +630,7 @@ __device__ __forceinline__ void win_tick_record(const KParams& p, const unsigned
 // over ranks by the allreduce), zero them, and write the tick record.  tk_j: the tick's drivers,
 // read by thread 0 only (win_reduce_body is shared by the two reduce kernels below)
 __device__ __forceinline__ void win_reduce_body(const KParams& p, unsigned long long* __restrict__ slot, int nt,
-                                                const TickArgs* tk_j, double* p_out, uint64_t* next_tick) {
+                                                const TickArgs* tk_j, double* p_out) {
   __shared__ unsigned long long s_red[kWinCap];
   const int j = blockIdx.x, c = threadIdx.x >> 6, q = threadIdx.x & 63, ncap = p.n_cap;
   // the record's other inputs are loaded by thread 0 while the shards are read (one memory
@@ -678,7 +658,6 @@ __device__ __forceinline__ void win_reduce_body(const KParams& p, unsigned long 
   if (threadIdx.x == 0) {
     if (tk_j) {
       win_tick_record(p, s_red, tk, p_on, win_rec(slot, ncap) + j * kWinRec, j == nt - 1 ? p_out : nullptr);
-      if (next_tick && j == nt - 1) *next_tick = tk.tick + 1;  // the tick id the next rollout starts at
     } else {  // P only (the drivers come later, as kernel arguments of k_step_window<..., KA>)
       win_rec(slot, ncap)[j * kWinRec] = win_power(p, s_red, p_on);
     }
@@ -686,22 +665,8 @@ __device__ __forceinline__ void win_reduce_body(const KParams& p, unsigned long 
 }
 
 __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long long* __restrict__ slot, int nt,
-                                                    const TickArgs* __restrict__ tkp, double* p_out,
-                                                    const int* __restrict__ abort, uint64_t* __restrict__ next_tick) {
-  if (abort && *abort) return;  // a cancelled launch-first rollout (k_lf_wait)
-  win_reduce_body(p, slot, nt, tkp ? tkp + blockIdx.x : nullptr, p_out, next_tick);
-}
-
-// The first window's reduce of a directly launched rollout, with the drivers of its first n_pk
-// ticks (this window's and the next one's) as kernel arguments: no separate staging launch in
-// front of it.  Block 0 also stages those records into dst (the device tick array that the step
-// kernel's lookahead and the next window's reduce read).
-__global__ void __launch_bounds__(256) k_win_reduce_staged(KParams p, unsigned long long* __restrict__ slot, int nt,
-                                                           StagePack pk, int n_pk, TickArgs* __restrict__ dst,
-                                                           double* p_out, uint64_t* __restrict__ next_tick) {
-  if (blockIdx.x == 0 && (int)threadIdx.x < n_pk)
-    reinterpret_cast<Rec32*>(dst)[threadIdx.x] = pk.r[threadIdx.x];
-  win_reduce_body(p, slot, nt, reinterpret_cast<const TickArgs*>(&pk.r[blockIdx.x]), p_out, next_tick);
+                                                    const TickArgs* __restrict__ tkp, double* p_out) {
+  win_reduce_body(p, slot, nt, tkp ? tkp + blockIdx.x : nullptr, p_out);
 }
 
 // the wave tile: 64 * HPT consecutive houses, house slot h of lane l = i0 + 64 h
@@ -865,8 +830,7 @@ __device__ __forceinline__ void win_classes(const WinTile<HPT>& t, const int* cl
 template <int ACT, int HPT>
 __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* __restrict__ action,
                                                       int64_t act_stride, const TickArgs* __restrict__ tkp,
-                                                      uint64_t tick0, const uint64_t* __restrict__ tick0p, int nt,
-                                                      unsigned long long* __restrict__ slot,
+                                                      uint64_t tick0, int nt, unsigned long long* __restrict__ slot,
                                                       uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
                                                       const uint32_t* __restrict__ w_in) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
@@ -881,7 +845,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
   }
   uint64_t cm[HPT][kWinCap];
   win_classes<HPT>(t, cls, cm);
-  win_run<ACT, HPT>(p, w, cm, t, tkp, tick0p ? *tick0p : tick0, nt, action, act_stride, s_cnt[wv],
+  win_run<ACT, HPT>(p, w, cm, t, tkp, tick0, nt, action, act_stride, s_cnt[wv],
                     onb + (size_t)t.tile * HPT * kWinMax);
 #pragma unroll
   for (int h = 0; h < HPT; ++h)
@@ -890,12 +854,48 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
   win_flush(p, nt, s_cnt, slot);
 }
 
-// MDR_WIN_WAVES (build-time A/B knob): cap k_step_window at that many waves per SIMD
-#ifdef MDR_WIN_WAVES
-#define MDR_WIN_OCC __attribute__((amdgpu_waves_per_eu(MDR_WIN_WAVES)))
-#else
-#define MDR_WIN_OCC
-#endif
+// Per-window affine transition of one house (FORM = MDR_THERMAL_AFFINE).  The reference's update
+// (building.py:141-222) is LINEAR in (t_k, tm_k, Qa, od_k) for fixed parameters: with
+// D = r2 - r1, dTA0dt = (Hm tm_k - (Ua+Hm) t_k + Ua od_k + Qa) / Ca and d/c = Qa / Ua + od_k,
+//   A1     = a_t t_k + a_m tm_k + a_q Qa + a_o od_k
+//            a_t = (r2 + (Ua+Hm)/Ca) / D, a_m = -(Hm/Ca) / D, a_q = -(1/Ca + r2/Ua) / D,
+//            a_o = -(Ua/Ca + r2) / D
+//   t_new  = A1 (e1 - e2) + e2 t_k + (d/c)(1 - e2)
+//   tm_new = A1 (A3 e1 - A4 e2) + A4 e2 t_k + (d/c)(1 - A4 e2)
+// so one tick is t_new = tt t_k + tm tm_k + tq Qa + to od_k (and the same for tm_new), four FMAs
+// per temperature, with the coefficients formed ONCE per window from the reference's own roots,
+// ratios and decay factors (rc_coeffs_t, bit-identical to the exact path's).  Same mathematics,
+// another rounding sequence: ~1e-13 K per tick against the reference order, far inside the
+// north star's 1e-5 (tests/test_window_gpu.py bounds it over 2,000 ticks).  Heat when ON is folded
+// in: qt = tq * q_on(class), so Qa = on ? q_on + solar : solar costs one select.
+struct AffWin {
+  double tt, tm, tq, to, qt;  // air:  t_new  = tt t_k + tm tm_k + tq solar + to od_k + (on ? qt : 0)
+  double mt, mm, mq, mo, qm;  // mass: tm_new = mt t_k + mm tm_k + mq solar + mo od_k + (on ? qm : 0)
+};
+
+__device__ __forceinline__ AffWin aff_window(double ua, double ca, double cm, double hm, double dt, double qc,
+                                             bool fast) {
+  const RcCoef k = fast ? rc_coeffs_t<true>(ua, ca, cm, hm, dt) : rc_coeffs_t<false>(ua, ca, cm, hm, dt);
+  const double iD = 1.0 / (k.r2 - k.r1), iCa = 1.0 / ca, iUa = 1.0 / ua;
+  const double a_t = (k.r2 + (ua + hm) * iCa) * iD;
+  const double a_m = -(hm * iCa) * iD;
+  const double a_q = -(iCa + k.r2 * iUa) * iD;
+  const double a_o = -(ua * iCa + k.r2) * iD;
+  const double E = k.e1 - k.e2, F = k.A3 * k.e1 - k.A4 * k.e2, G = k.A4 * k.e2;
+  const double one_e2 = 1.0 - k.e2, one_G = 1.0 - G;
+  AffWin w;
+  w.tt = a_t * E + k.e2;
+  w.tm = a_m * E;
+  w.tq = a_q * E + one_e2 * iUa;
+  w.to = a_o * E + one_e2;
+  w.mt = a_t * F + G;
+  w.mm = a_m * F;
+  w.mq = a_q * F + one_G * iUa;
+  w.mo = a_o * F + one_G;
+  w.qt = w.tq * qc;
+  w.qm = w.mq * qc;
+  return w;
+}
 
 // One window of K ticks.  slot: this window's slot (red counts are folded into its tick records);
 // onb / wah: the window's ON lane masks and end-of-window FSM words (from k_count_window or the
@@ -904,16 +904,18 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
 // KA (the first window of a directly launched rollout): the tick drivers come as kernel arguments
 // (dv) and rec holds only each tick's P (the P-only k_win_reduce); lane j derives tick j's signal
 // penalty once (win_nsig, the reduce's expression) and the thermal loop reads it with v_readlane.
-template <int ACT, int HPT, bool SIMPLE, bool KA>
-__global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, const uint8_t* __restrict__ action,
+// FORM: MDR_THERMAL_EXACT runs the reference's expression per tick (rc_apply_win: bit-identical to
+// the one-tick kernels); MDR_THERMAL_AFFINE the per-window transition above (Kelvin state kept in
+// registers for the window).
+template <int ACT, int HPT, bool SIMPLE, bool KA, int FORM>
+__global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* __restrict__ action,
                                                      int64_t act_stride, const TickArgs* __restrict__ tkp, int K,
                                                      int la_K, const double* __restrict__ rec,
                                                      double* __restrict__ reward, int64_t rew_stride,
                                                      uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
-                                                     unsigned long long* __restrict__ next_slot,
-                                                     const int* __restrict__ abort, WinDrv dv) {
+                                                     unsigned long long* __restrict__ next_slot, WinDrv dv) {
+  constexpr bool AFF = FORM == MDR_THERMAL_AFFINE;
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
-  if (abort && *abort) return;  // a cancelled launch-first rollout (k_lf_wait)
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
   uint64_t* onb_w = onb + (size_t)t.tile * HPT * kWinMax;  // this wave's rows [kWinMax][HPT]
@@ -924,34 +926,21 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
     const double ns = win_nsig(p, rec[l * kWinRec], dv.s_prev[l]);
     ns_lo = (uint32_t)__double_as_longlong(ns);
     ns_hi = (uint32_t)((uint64_t)__double_as_longlong(ns) >> 32);
-    if (dv.p_out && blockIdx.x == 0 && threadIdx.x == 0) {  // (last window)
-      *dv.p_out = rec[(K - 1) * kWinRec];
-      *dv.next_tick = dv.tick0 + (uint64_t)K;
-    }
+    if (dv.p_out && blockIdx.x == 0 && threadIdx.x == 0) *dv.p_out = rec[(K - 1) * kWinRec];  // (last window)
   }
 
   // ---- state + parameters, once per window
-  double T[HPT], Tm[HPT], ua[HPT], hm[HPT], tg[HPT];
+  double T[HPT], Tm[HPT], ua[HPT], hm[HPT], tg[HPT], ca[HPT], cm[HPT];
   uint32_t w_end[HPT];
   int cls[HPT];
-  RcWin rw[HPT];
   const bool params_ok = !*p.params_bad && p.fast_tick_ok;
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
     const uint32_t i = t.idx[h];
     T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; hm[h] = p.hm[i]; tg[h] = p.target[i];
+    ca[h] = p.ca[i]; cm[h] = p.cm[i];
     w_end[h] = wah[i];
     cls[h] = p.cap_idx[i];
-    const double ca = p.ca[i], cm = p.cm[i];
-    if (params_ok) {
-      rw[h] = rc_window(ua[h], ca, cm, hm[h], (double)p.dt);
-    } else {  // IEEE division (identical bits; parameters outside the fast-division range)
-      rw[h].k = rc_coeffs_t<false>(ua[h], ca, cm, hm[h], (double)p.dt);
-      rw[h].rCa.nb = -ca;
-      rw[h].rc.nb = -ua[h];
-      rw[h].rd.nb = -(rw[h].k.r2 - rw[h].k.r1);
-      rw[h].UaHm = ua[h] + hm[h];
-    }
   }
   double q_on[kWinCap];
 #pragma unroll
@@ -965,8 +954,34 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
     hi_tg[h] = tg[h] + p.deadband / 2.0;
     lo_tg[h] = tg[h] - p.deadband / 2.0;
   }
+  // per-house constants of the form
+  RcWin rw[AFF ? 1 : HPT];
+  AffWin aw[AFF ? HPT : 1];
+  double tk[HPT], tmk[HPT], hk[HPT];  // AFFINE: Kelvin state, Kelvin penalty threshold
+  bool win_finite = true;             // AFFINE: every coefficient and temperature finite
+#pragma unroll
+  for (int h = 0; h < HPT; ++h) {
+    if constexpr (AFF) {
+      aw[h] = aff_window(ua[h], ca[h], cm[h], hm[h], (double)p.dt, qc[h], params_ok);
+      tk[h] = T[h] + 273.0;
+      tmk[h] = Tm[h] + 273.0;
+      hk[h] = hi_tg[h] + 273.0;
+      const AffWin& a = aw[h];
+      const double s = a.tt + a.tm + a.tq + a.to + a.qt + a.mt + a.mm + a.mq + a.mo + a.qm + tk[h] + tmk[h] + hk[h];
+      win_finite = win_finite && (s - s == 0.0);
+    } else if (params_ok) {
+      rw[h] = rc_window(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+    } else {  // IEEE division (identical bits; parameters outside the fast-division range)
+      rw[h].k = rc_coeffs_t<false>(ua[h], ca[h], cm[h], hm[h], (double)p.dt);
+      rw[h].rCa.nb = -ca[h];
+      rw[h].rc.nb = -ua[h];
+      rw[h].rd.nb = -(rw[h].k.r2 - rw[h].k.r1);
+      rw[h].UaHm = ua[h] + hm[h];
+    }
+  }
+  if constexpr (AFF) win_finite = __all(win_finite);
 
-  // ---- the K ticks: heat source from the stored ON masks, RC thermal, reward
+  // ---- the K ticks: heat source from the stored ON masks, thermal update, reward
   // the tick's scalars (record, ON masks) are loaded one tick ahead (scalar loads, no vector work)
   auto lane_nsig = [&](int j) { return __longlong_as_double((long long)readlane_u64(ns_lo, ns_hi, j)); };
   double r_od = KA ? dv.od_k[0] : rec[0], r_sol = KA ? dv.solar[0] : rec[1], r_sig = KA ? lane_nsig(0) : rec[2];
@@ -996,54 +1011,79 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
     }
 #pragma unroll
     for (int h = 0; h < HPT; ++h) r_on[h] = onb_w[jn * HPT + h];
-    // all lanes in range: the comparison masks themselves (v_cmp writes a lane mask) against exec
-    uint64_t ok_m = ~0ull;
-#pragma unroll
-    for (int h = 0; h < HPT; ++h)
-      ok_m &= __builtin_amdgcn_ballot_w64(fabs(T[h]) < 1048576.0) & __builtin_amdgcn_ballot_w64(fabs(Tm[h]) < 1048576.0);
-    const bool fast = params_ok && tick_ok && ok_m == __builtin_amdgcn_read_exec();
     char* rrow = reinterpret_cast<char*>(reward + (int64_t)j * rew_stride);
-    auto houses = [&](auto fast_c) {
+    // the reward from the new Celsius temperature Tn (Kelvin tkn on the affine path)
+    auto reward_of = [&](int h, double Tn, double tkn, auto fast_c) {
       constexpr bool F = decltype(fast_c)::value;
-#pragma unroll
-      for (int h = 0; h < HPT; ++h) {
-        const bool on = __builtin_amdgcn_inverse_ballot_w64(on_m[h]);
-        const double q = on ? qc[h] : 0.0;
-        double Tn, Tmn;
-        rc_apply_win<F>(T[h], Tm[h], ua[h], hm[h], rw[h], q, solar, od_k, Tn, Tmn);
-        T[h] = Tn;
-        Tm[h] = Tmn;
-        double r;
-        if (SIMPLE) {  // deadband 0, norm_temp 1 (the defaults): no branches, no division
-          // on the fast path Tn is finite (the operand ranges checked above), so the reference's
-          // two comparisons reduce to x * x (x = 0 gives +0 either way); off it a NaN gives 0.
-          // -(a * pen + s) == (-a) * pen + (-s) bit for bit: negation is exact and rounding is
-          // symmetric, and with a, s >= +0 (mdr_capi checks the signs for SIMPLE) the only zero
-          // sum is +0 + +0, whose negation is -0 either way
-          const double x = Tn - hi_tg[h];
-          const double pen = F ? x * x : deadband_l2_0(hi_tg[h], Tn);
-          r = nalpha * pen + nsig;
-        } else {
-          double pen = 0.0;
-          if (hi_tg[h] < Tn) { const double x = Tn - hi_tg[h]; pen = x * x; }
-          else if (lo_tg[h] > Tn) { const double x = lo_tg[h] - Tn; pen = x * x; }
-          const double tpen = p.alpha_temp * pen;
-          r = -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + -nsig);
+      if (SIMPLE) {  // deadband 0, norm_temp 1 (the defaults): no branches, no division
+        // on the fast path Tn is finite, so the reference's two comparisons reduce to x * x (x = 0
+        // gives +0 either way); off it a NaN gives 0.  -(a * pen + s) == (-a) * pen + (-s) bit for
+        // bit: negation is exact and rounding is symmetric, and with a, s >= +0 (mdr_capi checks
+        // the signs for SIMPLE) the only zero sum is +0 + +0, whose negation is -0 either way
+        if (AFF && F) {
+          const double x = tkn - hk[h];
+          return __builtin_fma(nalpha, x * x, nsig);
         }
-        if (t.v[h]) {
-#ifdef MDR_REWARD_WT
-          // write-through (sc1) store: the row leaves the XCD's L2 at once, so the launch ends with
-          // no dirty reward lines to write back at the kernel boundary
-          __hip_atomic_store(reinterpret_cast<unsigned long long*>(rrow + (rb + 512u * h)),
-                             (unsigned long long)__double_as_longlong(r), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
-          *reinterpret_cast<double*>(rrow + (rb + 512u * h)) = r;
-#endif
-        }
+        const double x = Tn - hi_tg[h];
+        const double pen = F ? x * x : deadband_l2_0(hi_tg[h], Tn);
+        return nalpha * pen + nsig;
       }
+      double pen = 0.0;
+      if (hi_tg[h] < Tn) { const double x = Tn - hi_tg[h]; pen = x * x; }
+      else if (lo_tg[h] > Tn) { const double x = lo_tg[h] - Tn; pen = x * x; }
+      const double tpen = p.alpha_temp * pen;
+      return -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + -nsig);
     };
-    if (fast) houses(std::true_type());
-    else houses(std::false_type());
+    if constexpr (AFF) {
+      auto houses = [&](auto fast_c) {
+        constexpr bool F = decltype(fast_c)::value;
+#pragma unroll
+        for (int h = 0; h < HPT; ++h) {
+          const AffWin& a = aw[h];
+          const bool on = __builtin_amdgcn_inverse_ballot_w64(on_m[h]);
+          const double ut = __builtin_fma(a.to, od_k, __builtin_fma(a.tq, solar, on ? a.qt : 0.0));
+          const double um = __builtin_fma(a.mo, od_k, __builtin_fma(a.mq, solar, on ? a.qm : 0.0));
+          const double tkn = __builtin_fma(a.tt, tk[h], __builtin_fma(a.tm, tmk[h], ut));
+          const double tmkn = __builtin_fma(a.mt, tk[h], __builtin_fma(a.mm, tmk[h], um));
+          tk[h] = tkn;
+          tmk[h] = tmkn;
+          const double r = reward_of(h, tkn - 273.0, tkn, fast_c);  // (Celsius unused on the SIMPLE fast path)
+          if (t.v[h]) *reinterpret_cast<double*>(rrow + (rb + 512u * h)) = r;
+        }
+      };
+      if (win_finite && tick_ok) houses(std::true_type());
+      else houses(std::false_type());
+    } else {
+      // all lanes in range: the comparison masks themselves (v_cmp writes a lane mask) against exec
+      uint64_t ok_m = ~0ull;
+#pragma unroll
+      for (int h = 0; h < HPT; ++h)
+        ok_m &= __builtin_amdgcn_ballot_w64(fabs(T[h]) < 1048576.0) & __builtin_amdgcn_ballot_w64(fabs(Tm[h]) < 1048576.0);
+      const bool fast = params_ok && tick_ok && ok_m == __builtin_amdgcn_read_exec();
+      auto houses = [&](auto fast_c) {
+        constexpr bool F = decltype(fast_c)::value;
+#pragma unroll
+        for (int h = 0; h < HPT; ++h) {
+          const bool on = __builtin_amdgcn_inverse_ballot_w64(on_m[h]);
+          const double q = on ? qc[h] : 0.0;
+          double Tn, Tmn;
+          rc_apply_win<F>(T[h], Tm[h], ua[h], hm[h], rw[h], q, solar, od_k, Tn, Tmn);
+          T[h] = Tn;
+          Tm[h] = Tmn;
+          const double r = reward_of(h, Tn, 0.0, fast_c);
+          if (t.v[h]) *reinterpret_cast<double*>(rrow + (rb + 512u * h)) = r;
+        }
+      };
+      if (fast) houses(std::true_type());
+      else houses(std::false_type());
+    }
+  }
+  if constexpr (AFF) {
+#pragma unroll
+    for (int h = 0; h < HPT; ++h) {
+      T[h] = tk[h] - 273.0;
+      Tm[h] = tmk[h] - 273.0;
+    }
   }
 
   // ---- state back, once per window (the FSM word at the window's end came with the ON masks)
@@ -1056,9 +1096,9 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
 
   // ---- lookahead: the next window's ON masks, FSM words and class counts
   if (la_K > 0) {
-    uint64_t cm[HPT][kWinCap];
-    win_classes<HPT>(t, cls, cm);
-    win_run<ACT, HPT>(p, w_end, cm, t, KA ? nullptr : tkp + K, KA ? dv.tick0 + (uint64_t)K : 0, la_K,
+    uint64_t cmk[HPT][kWinCap];
+    win_classes<HPT>(t, cls, cmk);
+    win_run<ACT, HPT>(p, w_end, cmk, t, KA ? nullptr : tkp + K, KA ? dv.tick0 + (uint64_t)K : 0, la_K,
                       ACT == MDR_ACT_BUFFER ? action + (int64_t)K * act_stride : nullptr, act_stride, s_cnt[wv],
                       onb_w);
 #pragma unroll
@@ -1069,73 +1109,20 @@ __global__ void __launch_bounds__(256) MDR_WIN_OCC k_step_window(KParams p, cons
   }
 }
 
-// Launch-first rollouts (mdr_rollout_launch): the graph is launched BEFORE the host has the ticks'
-// drivers, and this one-block kernel (after the first window's FSM count, which needs only tick
-// ids) waits for them.  The host writes the n records into ring slot (seq & 1) of pinned memory
-// and then posts seq (ctl[0]); a cancel posts ctl[2] instead.  Thread 0 polls with system-scope
-// loads (no cached copy) and a bounded wait: after timeout wall-clock ticks the rollout is aborted
-// like a cancel, so every wave always exits.  The records are copied to dst (the device staging
-// the reduce / step kernels read), then *dseq = seq, *dabort = 0 (run) / 1 (cancelled) / 2 (timed
-// out) for the kernels that follow, and ctl[1] = seq | abort << 62 acknowledges the slot to the
-// host (which reuses it two launches later).  Only vector memory operations touch host memory.
-__global__ void __launch_bounds__(256) k_lf_wait(const TickArgs* ring, int cap, uint64_t* ctl, uint64_t* dseq,
-                                                 int* dabort, int n, TickArgs* __restrict__ dst,
-                                                 uint64_t timeout_ticks) {
-  __shared__ uint64_t s_seq;
-  __shared__ int s_ab;
-  if (threadIdx.x == 0) {
-    const uint64_t want = *dseq + 1;
-    const uint64_t t0 = wall_clock64();
-    int ab = 0;
-    for (;;) {
-      if (__hip_atomic_load(&ctl[0], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= want) break;
-      if (__hip_atomic_load(&ctl[2], __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) >= want) { ab = 1; break; }
-      if (wall_clock64() - t0 > timeout_ticks) { ab = 2; break; }
-      __builtin_amdgcn_s_sleep(2);
-    }
-    s_seq = want;
-    s_ab = ab;
-  }
-  __syncthreads();
-  const uint64_t want = s_seq;
-  const int ab = s_ab;
-  if (!ab) {
-    const uint64_t* src = reinterpret_cast<const uint64_t*>(ring + (size_t)(want & 1u) * cap);
-    uint64_t* d = reinterpret_cast<uint64_t*>(dst);
-    for (int i = threadIdx.x; i < 4 * n; i += blockDim.x)
-      d[i] = __hip_atomic_load(&src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    *dseq = want;
-    *dabort = ab;
-    __hip_atomic_store(&ctl[1], want | ((uint64_t)ab << 62), __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
-  }
-}
-
-#define MDR_INST_WIN(A, H)                                                                                      \
-  template __global__ void k_step_window<A, H, true, false>(KParams, const uint8_t*, int64_t, const TickArgs*, int,  \
-                                                            int, const double*, double*, int64_t, uint64_t*,       \
-                                                            uint32_t*, unsigned long long*, const int*, WinDrv);    \
-  template __global__ void k_step_window<A, H, false, false>(KParams, const uint8_t*, int64_t, const TickArgs*, int, \
-                                                             int, const double*, double*, int64_t, uint64_t*,      \
-                                                             uint32_t*, unsigned long long*, const int*, WinDrv);   \
-  template __global__ void k_count_window<A, H>(KParams, const uint8_t*, int64_t, const TickArgs*, uint64_t,       \
-                                                const uint64_t*, int, unsigned long long*, uint64_t*, uint32_t*,  \
-                                                const uint32_t*);
-MDR_INST_WIN(MDR_ACT_RANDOM, 1)
-MDR_INST_WIN(MDR_ACT_ALWAYS_ON, 1)
-MDR_INST_WIN(MDR_ACT_BUFFER, 1)
-MDR_INST_WIN(MDR_ACT_RANDOM, 2)
-MDR_INST_WIN(MDR_ACT_ALWAYS_ON, 2)
-MDR_INST_WIN(MDR_ACT_BUFFER, 2)
-#define MDR_INST_WIN_KA(A)                                                                                   \
-  template __global__ void k_step_window<A, 2, true, true>(KParams, const uint8_t*, int64_t, const TickArgs*, int, \
-                                                           int, const double*, double*, int64_t, uint64_t*,       \
-                                                           uint32_t*, unsigned long long*, const int*, WinDrv);
-MDR_INST_WIN_KA(MDR_ACT_RANDOM)
-MDR_INST_WIN_KA(MDR_ACT_ALWAYS_ON)
-MDR_INST_WIN_KA(MDR_ACT_BUFFER)
+#define MDR_INST_WIN_F(A, SI, KA_, FO)                                                                         \
+  template __global__ void k_step_window<A, kWinHpt, SI, KA_, FO>(KParams, const uint8_t*, int64_t, const TickArgs*, \
+                                                                  int, int, const double*, double*, int64_t,   \
+                                                                  uint64_t*, uint32_t*, unsigned long long*, WinDrv);
+#define MDR_INST_WIN(A)                                                                                         \
+  MDR_INST_WIN_F(A, true, false, MDR_THERMAL_EXACT) MDR_INST_WIN_F(A, false, false, MDR_THERMAL_EXACT)          \
+  MDR_INST_WIN_F(A, true, true, MDR_THERMAL_EXACT) MDR_INST_WIN_F(A, false, true, MDR_THERMAL_EXACT)            \
+  MDR_INST_WIN_F(A, true, false, MDR_THERMAL_AFFINE) MDR_INST_WIN_F(A, false, false, MDR_THERMAL_AFFINE)        \
+  MDR_INST_WIN_F(A, true, true, MDR_THERMAL_AFFINE) MDR_INST_WIN_F(A, false, true, MDR_THERMAL_AFFINE)          \
+  template __global__ void k_count_window<A, kWinHpt>(KParams, const uint8_t*, int64_t, const TickArgs*, uint64_t, \
+                                                      int, unsigned long long*, uint64_t*, uint32_t*, const uint32_t*);
+MDR_INST_WIN(MDR_ACT_RANDOM)
+MDR_INST_WIN(MDR_ACT_ALWAYS_ON)
+MDR_INST_WIN(MDR_ACT_BUFFER)
 
 #define MDR_INST_PIPE(T, A, LA)                                                                    \
   template __global__ void k_step_pipe<T, A, LA>(KParams, const uint8_t*, TickArgs, const TickArgs*, \
@@ -1148,20 +1135,14 @@ MDR_INST_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
 MDR_INST_PIPE(2, MDR_ACT_BUFFER, 0)
 MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0)
 
-#define MDR_INST_STEP(H, C, F, A, LA)                                                            \
-  template __global__ void k_step_t<H, C, F, A, LA>(                                             \
+#define MDR_INST_STEP(F, A, LA)                                                                  \
+  template __global__ void k_step_t<2, F, A, LA>(                                                \
       KParams, const uint8_t*, int, TickArgs, const TickArgs*, const unsigned long long*,        \
       double*, int, uint8_t*, double*, int, unsigned long long*, unsigned long long*, double*, int);
-MDR_INST_STEP(1, false, false, -1, -1)
-MDR_INST_STEP(1, false, true, -1, -1)
-MDR_INST_STEP(1, false, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
-MDR_INST_STEP(2, false, false, -1, -1)
-MDR_INST_STEP(2, true, false, -1, -1)
-MDR_INST_STEP(2, false, true, -1, -1)
-MDR_INST_STEP(2, true, true, -1, -1)
-MDR_INST_STEP(2, false, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
-MDR_INST_STEP(2, false, true, MDR_ACT_BUFFER, 0)
-MDR_INST_STEP(2, true, true, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
+MDR_INST_STEP(false, -1, -1)
+MDR_INST_STEP(true, -1, -1)
+MDR_INST_STEP(true, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
+MDR_INST_STEP(true, MDR_ACT_BUFFER, 0)
 
 // Division self-check: q_fast = shared-reciprocal sequence, q_ieee = the / operator.
 __global__ void k_div_check(const double* __restrict__ a, const double* __restrict__ b, int64_t n,
@@ -1174,28 +1155,21 @@ __global__ void k_div_check(const double* __restrict__ a, const double* __restri
   if (__double_as_longlong(f) != __double_as_longlong(q)) atomicAdd(mismatches, 1ull);
 }
 
-// After a parameter change: (a) flag any house whose parameters leave the range in which the
+// After a parameter change: flag any house whose parameters leave the range in which the
 // shared-reciprocal division is provably identical to `/` (Ua in [2^-20, 2^20], Ca/Cm/Hm in
-// [2^-10, 2^50]; the step then uses the plain operator), (b) for the CACHED variant, the
-// param-only thermal coefficients (rc_coeffs) of every house.
+// [2^-10, 2^50]; the step then uses the plain operator).
 __device__ __forceinline__ bool in_pow2_range(double x, int lo, int hi) {
   const int e = (int)((__double_as_longlong(x) >> 52) & 0x7FF) - 1023;
   return x > 0.0 && e >= lo && e < hi;
 }
 
-__global__ void __launch_bounds__(256) k_refresh(KParams p, double* __restrict__ coef, int* params_bad) {
+__global__ void __launch_bounds__(256) k_refresh(KParams p, int* params_bad) {
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= p.n) return;
   const double ua = p.ua[i], ca = p.ca[i], cm = p.cm[i], hm = p.hm[i];
   const bool ok = in_pow2_range(ua, -20, 20) && in_pow2_range(ca, -10, 50) &&
                   in_pow2_range(cm, -10, 50) && in_pow2_range(hm, -10, 50);
   if (!ok) atomicOr(params_bad, 1);
-  if (coef) {
-    const RcCoef k = rc_coeffs(ua, ca, cm, hm, (double)p.dt);
-    const int64_t cs = p.coef_stride;
-    coef[i] = k.r1; coef[i + cs] = k.r2; coef[i + 2 * cs] = k.A3;
-    coef[i + 3 * cs] = k.A4; coef[i + 4 * cs] = k.e1; coef[i + 5 * cs] = k.e2;
-  }
 }
 
 // Memory-floor probe for k_step's access pattern: the same loads and stores, trivial arithmetic

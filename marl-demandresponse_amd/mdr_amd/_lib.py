@@ -12,7 +12,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MDR_LIB", os.path.join(HERE, "libmdr_hip.so"))
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MAX_CAP = 64
 
 # enums (mdr.h)
@@ -21,6 +21,10 @@ CTRL_NONE, CTRL_BANGBANG, CTRL_DEADBAND_BANGBANG = 0, 1, 2
 COMM_RING, COMM_TABLE = 0, 1
 PEN_MODES = {"individual_L2": 0, "common_L2": 1, "common_max_error": 2, "mixture": 3}
 ERRORS = {-1: "MDR_EARG", -2: "MDR_EHIP", -3: "MDR_ERCCL", -4: "MDR_ENOMEM", -5: "MDR_ESTATE"}
+# mdr_set_option (mdr.h): alternative launch forms of the same computation
+OPTIONS = {"step_tpw": 1, "fastdiv": 2, "window_pipeline": 3, "sharded_overlap": 4, "greedy_sort": 5,
+           "force_halo": 6, "window_thermal": 7}
+THERMAL_EXACT, THERMAL_AFFINE = 0, 1
 
 
 class MdrLibraryError(RuntimeError):
@@ -109,11 +113,9 @@ SIGNATURES = {
     "mdr_bind": (I, [VP, P(mdr_soa)]),
     "mdr_params_changed": (I, [VP]),
     "mdr_set_rollout_window": (I, [VP, I]),
+    "mdr_set_option": (I, [VP, I, I64]),
     "mdr_time_step_kernels": (I, [VP, I, VP, VP, I64, I, VP, I64, VP, P(C.c_float), P(I)]),
     "mdr_rollout_begin": (I, [VP, I, U64, VP, I64, I, VP]),
-    "mdr_rollout_launch": (I, [VP, I, U64, VP, I64, I, VP, I64, VP, VP]),
-    "mdr_rollout_cancel": (I, [VP]),
-    "mdr_rollout_launched": (I, [VP, VP]),
     "mdr_populate": (I, [VP, P(mdr_pop_spec), VP]),
     "mdr_power_counts": (I, [VP, VP, I, U64, VP]),
     "mdr_counts_buffer": (I, [VP, P(VP), P(I)]),
@@ -144,7 +146,7 @@ SIGNATURES = {
     "mdr_rccl_init": (I, [VP, VP, I, I]),
     "mdr_rccl_allreduce": (I, [VP, VP, I64, I, VP]),
     "mdr_rollout_sharded": (I, [VP, I, VP, VP, I64, I, VP, I64, VP, VP]),
-    "mdr_rollout_sharded_mode": (I, [VP, P(I), P(D), P(D)]),
+    "mdr_rollout_sharded_mode": (I, [VP, P(I), P(I)]),
     "mdr_probe_stream": (I, [VP, VP, VP]),
     "mdr_div_check": (I, [VP, VP, I64, VP, VP]),
     "mdr_event_record": (I, [VP, I, VP]),

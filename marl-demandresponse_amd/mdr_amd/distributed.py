@@ -79,12 +79,11 @@ class RcclComm:
                 "mdr_rollout_sharded")
 
     def pipeline(self, shard) -> dict:
-        """Which sharded rollout pipeline the library picked (mdr_rollout_sharded_mode)."""
-        m, s, o = C.c_int(), C.c_double(), C.c_double()
-        L.check(shard.lib.mdr_rollout_sharded_mode(shard.ctx, C.byref(m), C.byref(s), C.byref(o)),
-                "mdr_rollout_sharded_mode")
-        return {"mode": {-1: "undecided", 0: "serial", 1: "overlapped"}[m.value],
-                "calib_us_per_tick_serial": s.value, "calib_us_per_tick_overlapped": o.value}
+        """The sharded rollout pipelines the library uses (mdr_rollout_sharded_mode)."""
+        w, t = C.c_int(), C.c_int()
+        L.check(shard.lib.mdr_rollout_sharded_mode(shard.ctx, C.byref(w), C.byref(t)), "mdr_rollout_sharded_mode")
+        return {"window": "count-ahead (side-stream count + allreduce)" if w.value else "one stream",
+                "one_tick": "overlapped (reward one launch later)" if t.value else "serial"}
 
     def ring_halo(self, shard, spec):
         """Message features of the houses just before / after this shard on the global ring."""

@@ -161,6 +161,8 @@ def gauss_n(rng, n: int, sigma: float) -> list:
     """[rng.gauss(0, sigma) for _ in range(n)], bit for bit and in the same RNG order (rng: a
     random.Random or the random module, whose bound functions share its hidden instance)."""
     inst = getattr(rng, "_inst", rng)  # the `random` module draws from random._inst
+    if type(inst).gauss is not _random.Random.gauss:  # a subclass's own gauss: call it
+        return _gauss_n_calls(inst, n, sigma)
     return _GAUSS_N(inst, n, sigma)
 
 

@@ -127,6 +127,15 @@ class TickWindow:
         return TickWindow(np.ascontiguousarray(self.a[sl]))
 
 
+def _host_gauss_ok(rng) -> bool:
+    """The C host drivers restate CPython's random.gauss (its gauss_next cache, the generator's own
+    random()); use them only when that is what the generator draws with: the ``random`` module or a
+    random.Random whose gauss is not overridden, while the unrolled restatement is in use
+    (drivers._GAUSS_N: chosen at import only if it reproduces this interpreter's gauss)."""
+    inst = getattr(rng, "_inst", rng)
+    return type(inst).gauss is _random.Random.gauss and drivers._GAUSS_N is drivers._gauss_n_inline
+
+
 def shard_range(n: int, rank: int, world: int):
     """Contiguous house range of a rank (SURVEY §8(e)): [r*n//w, (r+1)*n//w)."""
     lo = rank * n // world
@@ -407,7 +416,7 @@ class Environment:
         """driver_window for a constant base power and a flat / sinusoidal / regular-steps signal:
         the host-driver extension (csrc/mdr_host.c) when it is built, else the Python loop below
         (the same values bit for bit: tests/test_driver_window.py)."""
-        if _host is None:
+        if _host is None or not _host_gauss_ok(self.rng):
             return self._driver_window_vec_py(n)
         p = self.init_props
         hp = p.cluster_prop.house_prop
@@ -551,20 +560,17 @@ class Environment:
         return float(out.item())
 
     def rollout(self, n_ticks: int, actions=None, action_mode: str = "random", rewards=None,
-                use_graph=None):
+                use_graph: bool = False):
         """n_ticks steps in one C call.  ``actions``: uint8 [n_ticks, N] (buffer mode) or None;
         ``rewards``: float64 [n_ticks, N] output (allocated if None), or a 1-D [N] buffer that every
-        tick overwrites.  ``use_graph``: None / False (the default: direct launches) = the first
-        window's count and its P-only reduce are launched before the host computes the drivers
-        (mdr_rollout_begin), which then ride as kernel arguments of the first step kernel
-        (k_step_window<..., KA>; the later windows' drivers are staged behind it); True =
-        launch-first (mdr_rollout_launch: count, a device-side wait and the windows are issued
-        before the drivers, which the matching mdr_rollout posts; direct launches, or one hipGraph
-        replay with MDR_LF_GRAPH=1).  Measured on MI355X: profiles/r02h_ab.log."""
+        tick overwrites.  Default (direct launches): the first window's count and its cluster power
+        are launched before the host computes the drivers (mdr_rollout_begin), which then ride as
+        kernel arguments of the first step kernel (k_step_window<..., KA>); the later windows'
+        drivers are staged behind it.  ``use_graph=True``: the drivers are staged first and the
+        launch sequence is replayed as a cached hipGraph (measured slower for both short and long
+        calls, profiles/r02h_ab.log)."""
         import torch
 
-        if use_graph is None:
-            use_graph = False
         sh = self._shard
         if sh.penalty_mode != 0:
             raise NotImplementedError("rollout supports individual_L2; use step_tensor for common penalties")
@@ -574,45 +580,26 @@ class Environment:
         if rewards is None:
             rewards = torch.empty((n_ticks, self._n_local), dtype=torch.float64, device=sh.device)
         rew_stride = 0 if rewards.dim() == 1 else self._n_local  # 1-D: every tick overwrites it
-        launched = False
-        if self._comm is None and self.power_grid.interp is None and self._links is not None:
-            act_stride = self._n_local if actions is not None else 0
-            if use_graph:
-                # the whole graph is launched before the host computes the drivers: its first
-                # window's FSM count needs only the tick ids, then it waits on the device for the
-                # drivers that sh.rollout below posts (mdr_rollout_launch; falls back to counting
-                # the first window early, mdr_rollout_begin)
-                sh.rollout_launch(n_ticks, self._tick, actions, act_stride, mode, rewards, rew_stride)
-                launched = True
-            else:
-                sh.rollout_begin(n_ticks, self._tick, actions, act_stride, mode)
-        elif (getattr(self._comm, "native", False) and self.power_grid.interp is None
-              and self._links is not None):
-            # sharded (library RCCL communicator): a single-window rollout's count, its allreduce
-            # and its P-only reduce go out before the drivers (mdr_rollout_begin; a no-op otherwise)
+        drivers_whole = self.power_grid.interp is None and self._links is not None  # one driver window
+        if drivers_whole and not use_graph and (self._comm is None or getattr(self._comm, "native", False)):
+            # the first window's count (sharded: + its allreduce) and P, before the drivers exist
             sh.rollout_begin(n_ticks, self._tick, actions, self._n_local if actions is not None else 0, mode)
         done = 0
-        try:
-            while done < n_ticks:  # one window unless interpolation ends it early (driver_window)
-                ticks = self.driver_window(n_ticks - done)
-                k = len(ticks)
-                whole = done == 0 and k == n_ticks  # one window: the caller's buffers as they are
-                a = None if actions is None else (actions if whole and actions.shape[0] == k else actions[done:done + k])
-                r = rewards[done:done + k] if rew_stride and not (whole and rewards.shape[0] == k) else rewards
-                if self._comm is not None:
-                    self._comm.rollout(sh, ticks, a, mode, r, rew_stride)
-                else:
-                    # graphs are cached per (length, buffers): shorter windows only reuse them on 1-D rewards
-                    g = use_graph and (k == n_ticks or (a is None and not rew_stride))
-                    sh.rollout(ticks, a, self._n_local if a is not None else 0, mode, r, rew_stride, g)
-                launched = False
-                self._P_dev_valid = True
-                self.finish_grid_step()
-                done += k
-        except BaseException:
-            if launched:  # the launched graph must not wait for drivers that will not come
-                sh.rollout_cancel()
-            raise
+        while done < n_ticks:  # one window unless interpolation ends it early (driver_window)
+            ticks = self.driver_window(n_ticks - done)
+            k = len(ticks)
+            whole = done == 0 and k == n_ticks  # one window: the caller's buffers as they are
+            a = None if actions is None else (actions if whole and actions.shape[0] == k else actions[done:done + k])
+            r = rewards[done:done + k] if rew_stride and not (whole and rewards.shape[0] == k) else rewards
+            if self._comm is not None:
+                self._comm.rollout(sh, ticks, a, mode, r, rew_stride)
+            else:
+                # graphs are cached per (length, buffers): shorter windows only reuse them on 1-D rewards
+                g = use_graph and (k == n_ticks or (a is None and not rew_stride))
+                sh.rollout(ticks, a, self._n_local if a is not None else 0, mode, r, rew_stride, g)
+            self._P_dev_valid = True
+            self.finish_grid_step()
+            done += k
         self._counts_ready = 0
         return rewards
 
@@ -643,13 +630,11 @@ class Environment:
         sh.greedy(float(self.power_grid.current_signal), out)
         return out
 
-    def rollout_stream(self, use_graph: bool = True):
-        """Stream the k_step launches of ``rollout`` are issued on (for HIP-event timing)."""
+    def rollout_stream(self):
+        """Stream the step launches of ``rollout`` are issued on (for HIP-event timing)."""
         import torch
 
-        if self._comm is not None:
-            return torch.cuda.current_stream(self._shard.device)
-        return self._shard.launch_stream(use_graph)
+        return torch.cuda.current_stream(self._shard.device)
 
     # ------------------------------------------------------------------ observations
     def _cluster_power(self) -> float:

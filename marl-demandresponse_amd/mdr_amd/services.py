@@ -153,10 +153,13 @@ def observe(env) -> dict:
 
 class HouseList(Sequence):
     """ClientManagerService.update_houses_data's N-entry house list (client_manager_service.py:
-    198-230) over a device snapshot of the state: an entry is built when it is read."""
+    198-230) over a snapshot of the state: an entry is built when it is read.  The snapshot is a
+    device copy until ``offload()`` moves it to host memory (UISummary keeps only the latest tick's
+    list on the device, so a long server run grows host memory like the reference's list, not HBM)."""
 
     def __init__(self, env):
         sh = env.shard
+        self._n = sh.n
         self._t, self._tg, self._hv = sh.t_air.clone(), sh.target.clone(), sh.hvac.clone()
         self._host = None
         self._lo = env._offset
@@ -167,10 +170,15 @@ class HouseList(Sequence):
 
             on, lock, sso = decode_hvac(self._hv.cpu().numpy())
             self._host = (self._t.cpu().numpy(), self._tg.cpu().numpy(), on, lock, sso)
+            self._t = self._tg = self._hv = None  # (the device copies are no longer needed)
         return self._host
 
+    def offload(self) -> None:
+        """Move the snapshot to host memory now (one device->host copy) and free its device copy."""
+        self._arrays()
+
     def __len__(self) -> int:
-        return int(self._t.numel())
+        return self._n
 
     def __getitem__(self, i):
         if isinstance(i, slice):
@@ -246,6 +254,8 @@ class UISummary:
             str(np.mean(self.temp_err)),
         ]
         self.description[time_step] = dict(zip(DESCRIPTION_KEYS, values))
+        if self.houses_data:  # the previous tick's snapshot leaves HBM
+            self.houses_data[next(reversed(self.houses_data))].offload()
         self.houses_data[time_step] = HouseList(env)
 
     @staticmethod

@@ -119,6 +119,12 @@ class HipShard:
         """Ticks per temporally blocked rollout launch (0: one launch per tick), mdr_set_rollout_window."""
         L.check(self.lib.mdr_set_rollout_window(self.ctx, int(ticks)), "mdr_set_rollout_window")
 
+    def set_option(self, name: str, value: int):
+        """mdr_set_option: an alternative launch form of the same computation (mdr.h MDR_OPT_*:
+        step_tpw, fastdiv, window_pipeline, sharded_overlap, greedy_sort, force_halo,
+        window_thermal)."""
+        L.check(self.lib.mdr_set_option(self.ctx, L.OPTIONS[name], int(value)), f"mdr_set_option({name})")
+
     def params_changed(self):
         L.check(self.lib.mdr_params_changed(self.ctx), "mdr_params_changed")
 
@@ -167,8 +173,9 @@ class HipShard:
 
     def rollout(self, ticks, action, act_stride, mode, reward, rew_stride, use_graph=True):
         """Many ticks in one C call (``ticks``: a TickWindow), on the caller's current stream; with
-        ``use_graph`` the launch sequence is captured once (on the library's capture stream) and
-        replayed as a hipGraph."""
+        ``use_graph`` the drivers are staged and the launch sequence is captured once (on the
+        library's capture stream) and replayed as a hipGraph; without, the windows are launched
+        directly with the first window's drivers as kernel arguments."""
         L.check(self.lib.mdr_rollout(self.ctx, len(ticks), ticks.ptr(), L.ptr(action), act_stride, mode,
                                      L.ptr(reward), rew_stride, L.ptr(self.p_dev), int(use_graph), self.stream()),
                 "mdr_rollout")
@@ -178,21 +185,6 @@ class HipShard:
         L.check(self.lib.mdr_rollout_begin(self.ctx, n, tick0, L.ptr(action), act_stride, mode, self.stream()),
                 "mdr_rollout_begin")
 
-    def rollout_launch(self, n, tick0, action, act_stride, mode, reward, rew_stride):
-        """mdr_rollout_launch: the whole rollout graph, launched before the host computes the drivers
-        (the matching ``rollout`` posts them; ``rollout_cancel`` if they will not come)."""
-        L.check(self.lib.mdr_rollout_launch(self.ctx, n, tick0, L.ptr(action), act_stride, mode, L.ptr(reward),
-                                            rew_stride, L.ptr(self.p_dev), self.stream()), "mdr_rollout_launch")
-
-    def rollout_cancel(self):
-        L.check(self.lib.mdr_rollout_cancel(self.ctx), "mdr_rollout_cancel")
-
-    def rollout_launched(self) -> int:
-        """Launch-first rollout graphs launched so far (mdr_rollout_launched)."""
-        v = C.c_uint64()
-        L.check(self.lib.mdr_rollout_launched(self.ctx, C.byref(v)), "mdr_rollout_launched")
-        return int(v.value)
-
     def time_step_kernels(self, ticks, action, act_stride, mode, reward, rew_stride):
         """mdr_time_step_kernels: (summed step-kernel ms, step launches) of one directly launched rollout."""
         ms, nl = C.c_float(), C.c_int()
@@ -201,7 +193,7 @@ class HipShard:
                 "mdr_time_step_kernels")
         return float(ms.value), int(nl.value)
 
-    def launch_stream(self, use_graph=True):
+    def launch_stream(self):
         """The torch stream rollout kernels run on (the caller's current stream) — where timing
         events must be recorded."""
         return self.torch.cuda.current_stream(self.device)

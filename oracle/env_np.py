@@ -405,27 +405,38 @@ class OracleEnv:
 
 def norm_vector(p, pop, o, links) -> np.ndarray:
     """``norm_state_dict`` (norm.py:178-218) for all houses, float64 [N, F]."""
+    n = p.cluster_prop.nb_agents
+    has = links is not None and len(links) > 0 and len(links[0]) > 0
+    return norm_vector_rows(p, pop, o, np.arange(n), links if has else None)
+
+
+def norm_vector_rows(p, pop, o, rows, links_rows) -> np.ndarray:
+    """``norm_state_dict`` (norm.py:178-218) of the houses ``rows`` only, float64 [len(rows), F];
+    ``links_rows``: their neighbour ids [len(rows), k] (None: no messages).  State and population
+    arrays cover the whole cluster (normalisers use the cluster size nb_agents)."""
     cp, hp = p.cluster_prop, p.cluster_prop.house_prop
     hv = hp.hvac_prop
     sp, mp = p.state_prop, cp.message_prop
     R = p.reward_prop.norm_reg_sig
     L = hv.lockout_duration
     n = cp.nb_agents
-    cols = [o["on"].astype(np.float64), o["lock"].astype(np.float64),
-            np.trunc(o["sso"] / L), np.full(n, float(int(L / L)))]
+    rows = np.asarray(rows, np.int64)
+    m = rows.shape[0]
+    cols = [o["on"][rows].astype(np.float64), o["lock"][rows].astype(np.float64),
+            np.trunc(o["sso"][rows] / L), np.full(m, float(int(L / L)))]
     if sp.hvac:
-        cols += [np.full(n, hv.cop / hv.cop), np.full(n, hv.latent_cooling_fraction / hv.latent_cooling_fraction)]
-    cols += [np.full(n, o["P"] / R), np.full(n, o["S"] / (R * n)), np.full(n, float(hp.deadband)),
-             (o["T"] - 20) / 5, (o["Tm"] - 20) / 5, (pop["target"] - 20) / 5]
+        cols += [np.full(m, hv.cop / hv.cop), np.full(m, hv.latent_cooling_fraction / hv.latent_cooling_fraction)]
+    cols += [np.full(m, o["P"] / R), np.full(m, o["S"] / (R * n)), np.full(m, float(hp.deadband)),
+             (o["T"][rows] - 20) / 5, (o["Tm"][rows] - 20) / 5, (pop["target"][rows] - 20) / 5]
     if sp.solar_gain:
-        cols.append(np.full(n, o["G"] / 1000))
+        cols.append(np.full(m, o["G"] / 1000))
     if sp.thermal:
-        cols += [pop["Ua"] / hp.Ua, pop["Ca"] / hp.Ca, pop["Cm"] / hp.Cm, pop["Hm"] / hp.Hm]
-        cols.append(np.full(n, (o["Tod"] - 20) / 5))
+        cols += [pop["Ua"][rows] / hp.Ua, pop["Ca"][rows] / hp.Ca, pop["Cm"][rows] / hp.Cm, pop["Hm"][rows] / hp.Hm]
+        cols.append(np.full(m, (o["Tod"] - 20) / 5))
     base = np.stack(cols, 1)
-    if not links or not links[0]:
+    if links_rows is None:
         return base
-    idx = np.asarray(links, np.int64)  # [N, k]
+    idx = np.asarray(links_rows, np.int64)  # [m, k]
     curr = np.where(o["on"], pop["cap"] / hv.cop, 0.0)
     mx = pop["cap"] / hv.cop
     per = [(o["T"][idx] - pop["target"][idx]) / 5, np.trunc(o["sso"][idx] / L), curr[idx] / R, mx[idx] / R]
@@ -433,9 +444,9 @@ def norm_vector(p, pop, o, links) -> np.ndarray:
         per += [pop["Ua"][idx] / hp.Ua, pop["Ca"][idx] / hp.Ca, pop["Cm"][idx] / hp.Cm, pop["Hm"][idx] / hp.Hm]
     if mp.hvac:
         k = idx.shape[1]
-        per += [np.full((n, k), hv.cop), np.full((n, k), hv.latent_cooling_fraction),
-                np.full((n, k), float(hv.cooling_capacity))]
-    msg = np.stack(per, 2).reshape(n, -1)
+        per += [np.full((m, k), hv.cop), np.full((m, k), hv.latent_cooling_fraction),
+                np.full((m, k), float(hv.cooling_capacity))]
+    msg = np.stack(per, 2).reshape(m, -1)
     return np.concatenate([base, msg], 1)
 
 

@@ -2,9 +2,9 @@
 reproduce the single-process run on the same seeds.
 
 * world 1 over the library's own RCCL communicator (backend 'nccl'): exercises mdr_rccl_init,
-  mdr_rccl_allreduce and the C rollout loop mdr_rollout_sharded on a real device: the serial
-  loop, the overlapped two-stream pipeline (reward written one launch later) and the default
-  calibration that runs half the rollout each way;
+  mdr_rccl_allreduce and the C rollout loop mdr_rollout_sharded on a real device: the count-ahead
+  window pipeline (default) and its one-stream form, the per-tick loop serial and overlapped
+  (reward written one launch later);
 * world 2 over torch.distributed/gloo (TorchComm) with both ranks on cuda:0: exercises the
   sharding, the per-tick count / penalty allreduces and the ring-halo observation exchange with
   the HIP kernels (RCCL cannot put two ranks on one GPU; the 8-GPU RCCL run is the driver's).
@@ -26,7 +26,7 @@ import golden_util as gu
 pytestmark = pytest.mark.gpu
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-T_STEP, T_BUF, T_GREEDY, T_ROLL = 5, 3, 2, 70  # >= 16 ticks trigger the per-tick pipeline calibration; 3 windows
+T_STEP, T_BUF, T_GREEDY, T_ROLL = 5, 3, 2, 70  # 3 windows
 
 
 INTERP = "interp"  # mode suffix: interpolation base power (row a10), re-estimated every 3 ticks
@@ -66,6 +66,17 @@ def _run(env, n_total, torch, dev):
             "sso": st["sso"], "P": env._cluster_power(), "obs": obs}
 
 
+def _variant(env, kind):
+    """The launch form a test kind selects (mdr_set_option), on the sharded env and its reference:
+    rccl-winserial = windows without the count-ahead pipeline (one stream); rccl-serial /
+    rccl-overlap = the per-tick C loop (window 0), serial or two-stream."""
+    if kind == "rccl-winserial":
+        env.shard.set_option("window_pipeline", 0)
+    elif kind in ("rccl-serial", "rccl-overlap"):
+        env.shard.set_rollout_window(0)
+        env.shard.set_option("sharded_overlap", kind == "rccl-overlap")
+
+
 def _worker(rank, world, port, backend, kind, n, mode, out_dir):
     sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "marl-demandresponse_amd"), os.path.dirname(HERE)]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -73,13 +84,6 @@ def _worker(rank, world, port, backend, kind, n, mode, out_dir):
     import torch
     import torch.distributed as dist
 
-    if kind == "rccl-winserial":  # windows without the count-ahead pipeline (one stream)
-        os.environ["MDR_WINDOW_PIPELINE"] = "0"
-        kind = "rccl"
-    elif kind.startswith("rccl-"):  # per-tick C loop (window 0), forced serial / overlapped pipeline
-        os.environ["MDR_SHARDED_OVERLAP"] = "0" if kind == "rccl-serial" else "1"
-        os.environ["MDR_WINDOW"] = "0"
-        kind = "rccl"
     torch.cuda.set_device(0)
     dev = torch.device("cuda", 0)
     kw = {"device_id": dev} if backend == "nccl" else {}
@@ -90,7 +94,9 @@ def _worker(rank, world, port, backend, kind, n, mode, out_dir):
     from mdr_amd.environment import Environment
 
     env = Environment(g.props_from_overrides(_overrides(n, mode)), device=dev, rng=random.Random(4),
-                      population="synthetic", seed=77, rank=rank, world=world, comm=make_comm(kind))
+                      population="synthetic", seed=77, rank=rank, world=world,
+                      comm=make_comm("rccl" if kind.startswith("rccl") else kind))
+    _variant(env, kind)
     res = _run(env, n, torch, dev)
     res["lo"] = env._offset
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
@@ -119,6 +125,8 @@ def _free_port():
     ("gloo", "torch", 2, 3001, "individual_L2+interp"),
     ("gloo", "torch", 2, 2992, "individual_L2+closed_groups"),
     ("gloo", "torch", 2, 3001, "common_L2+random_fixed"),
+    ("nccl", "rccl", 1, 131072, "individual_L2"),    # C4's per-GPU shard size
+    ("gloo", "torch", 2, 262144, "individual_L2"),   # two C4-sized shards on cuda:0
 ])
 def test_sharded_equals_single(tmp_path, backend, kind, world, n, mode):
     import torch
@@ -131,6 +139,7 @@ def test_sharded_equals_single(tmp_path, backend, kind, world, n, mode):
     dev = torch.device("cuda", 0)
     env = Environment(gu.props_from_overrides(_overrides(n, mode)), device=dev, rng=random.Random(4),
                       population="synthetic", seed=77)
+    _variant(env, kind)
     ref = _run(env, n, torch, dev)
     for key in ("on", "lock", "sso", "T", "Tm"):
         np.testing.assert_array_equal(np.concatenate([p[key] for p in parts]), ref[key], err_msg=key)
@@ -167,8 +176,6 @@ def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo):
     sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "marl-demandresponse_amd"), os.path.dirname(HERE)]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
-    if force_halo:
-        os.environ["MDR_FORCE_HALO"] = "1"
     import torch
     import torch.distributed as dist
 
@@ -183,6 +190,8 @@ def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo):
 
     env = Environment(g.props_from_overrides(_overrides(n, "individual_L2")), device=dev, rng=random.Random(4),
                       population="synthetic", seed=77, rank=rank, world=world, comm=make_comm(kind))
+    if force_halo:
+        env.shard.set_option("force_halo", 1)
     res = _actor_run(env, torch)
     res["lo"] = env._offset
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)

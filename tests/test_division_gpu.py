@@ -1,6 +1,5 @@
 """The step kernels' shared-reciprocal division (mdr_device.h `recip`/`div_by`) must be
 bit-identical to the IEEE `/` operator inside its guarded operand range ([2^-300, 2^300])."""
-import os
 import random
 
 import numpy as np
@@ -34,9 +33,11 @@ def test_shared_reciprocal_division_is_exact():
     assert total == 0
 
 
-@pytest.mark.parametrize("variant", [("raw", "1"), ("coef", "0"), ("coef", "1")])
-def test_step_variants_bit_identical(variant):
-    """raw/fast-division/cached-coefficient kernels produce bit-identical trajectories."""
+@pytest.mark.parametrize("tpw", [0, -1])
+def test_step_fastdiv_bit_identical(tpw):
+    """The shared-reciprocal division (default) and the IEEE operator everywhere
+    (MDR_OPT_FASTDIV = 0) produce bit-identical trajectories, in k_step_t (tpw 0) and in the
+    default per-tick kernel."""
     import torch
 
     import golden_util as gu
@@ -45,10 +46,11 @@ def test_step_variants_bit_identical(variant):
     props = gu.props_from_overrides({"cluster_prop.nb_agents": 100_003,
                                      "power_grid_prop.signal_properties.mode": "sinusoidals"})
     envs = []
-    for var, fast in (("raw", "0"), variant):
-        os.environ["MDR_VARIANT"], os.environ["MDR_FASTDIV"] = var, fast
-        envs.append(Environment(props, rng=random.Random(2), population="synthetic", seed=3))
-    os.environ.pop("MDR_VARIANT"), os.environ.pop("MDR_FASTDIV")
+    for fast in (0, 1):
+        e = Environment(props, rng=random.Random(2), population="synthetic", seed=3)
+        e.shard.set_option("fastdiv", fast)
+        e.shard.set_option("step_tpw", tpw)
+        envs.append(e)
     for t in range(40):
         rs = [e.step_tensor(None, action_mode="random", lookahead="random").clone() for e in envs]
         assert torch.equal(rs[0], rs[1])
@@ -57,10 +59,10 @@ def test_step_variants_bit_identical(variant):
         np.testing.assert_array_equal(s0[k], s1[k])
 
 
-@pytest.mark.parametrize("tpw", ["1", "2", "4", "8"])
+@pytest.mark.parametrize("tpw", [1, 2, 4, 8])
 @pytest.mark.parametrize("mode", ["random", "buffer"])
 def test_pipelined_step_bit_identical(tpw, mode):
-    """k_step_pipe (MDR_TPW tiles per wave, next tile's loads issued before this tile's math) ==
+    """k_step_pipe (MDR_OPT_STEP_TPW tiles per wave, next tile's loads issued before this tile's math) ==
     k_step_t bit for bit: ragged shard (odd size, partial last tile), fused random actions with
     lookahead and buffer actions, per-step API and graph rollouts."""
     import torch
@@ -72,10 +74,10 @@ def test_pipelined_step_bit_identical(tpw, mode):
     props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
                                      "power_grid_prop.signal_properties.mode": "sinusoidals"})
     envs = []
-    for t in ("0", tpw):
-        os.environ["MDR_TPW"] = t
-        envs.append(Environment(props, rng=random.Random(2), population="synthetic", seed=3))
-    os.environ.pop("MDR_TPW")
+    for t in (0, tpw):
+        e = Environment(props, rng=random.Random(2), population="synthetic", seed=3)
+        e.shard.set_option("step_tpw", t)
+        envs.append(e)
     g = torch.Generator(device="cuda").manual_seed(11)
     for t in range(25):
         if mode == "random":
@@ -93,7 +95,7 @@ def test_pipelined_step_bit_identical(tpw, mode):
         np.testing.assert_array_equal(s0[k], s1[k])
 
 
-@pytest.mark.parametrize("tpw", ["0", "4"])
+@pytest.mark.parametrize("tpw", [0, 4])
 def test_fast_division_guard_fallback(tpw):
     """Out-of-range parameters (Ua = 1e-9 < 2^-20) or temperatures route the tile to the plain
     `/` operator: results stay bit-identical to the reference-order kernel (k_step_t and
@@ -106,15 +108,14 @@ def test_fast_division_guard_fallback(tpw):
     props = gu.props_from_overrides({"cluster_prop.nb_agents": 5000,
                                      "power_grid_prop.signal_properties.mode": "flat"})
     envs = []
-    for fast in ("0", "1"):
-        os.environ["MDR_FASTDIV"] = fast
-        os.environ["MDR_TPW"] = tpw if fast == "1" else "0"
+    for fast in (0, 1):
         e = Environment(props, rng=random.Random(2), population="synthetic", seed=3)
+        e.shard.set_option("fastdiv", fast)
+        e.shard.set_option("step_tpw", tpw if fast else 0)
         e.shard.ua[17] = 1e-9
         e.shard.t_air[4000] = 3.0e6
         e.shard.params_changed()
         envs.append(e)
-    os.environ.pop("MDR_FASTDIV"), os.environ.pop("MDR_TPW")
     for t in range(10):
         rs = [e.step_tensor(None, action_mode="random", lookahead="random").clone() for e in envs]
         assert torch.equal(rs[0], rs[1])

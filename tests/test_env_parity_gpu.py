@@ -179,7 +179,7 @@ def test_fused_bangbang_matches_dict_controller(torch_gpu, ctrl):
 
 
 def test_rollout_equals_steps(torch_gpu):
-    """mdr_rollout (graph-captured, lookahead counts) == the same ticks via step_tensor."""
+    """mdr_rollout (temporally blocked windows, exact thermal form) == the same ticks via step_tensor."""
     torch = torch_gpu
     props = gu.props_from_overrides({"cluster_prop.nb_agents": 20000,
                                      "power_grid_prop.signal_properties.mode": "sinusoidals"})
@@ -187,6 +187,7 @@ def test_rollout_equals_steps(torch_gpu):
 
     e1 = Environment(props, rng=random.Random(3), population="synthetic", seed=77)
     e2 = Environment(props, rng=random.Random(3), population="synthetic", seed=77)
+    e1.shard.set_option("window_thermal", 0)  # MDR_THERMAL_EXACT: bit-identical to the one-tick kernels
     R = e1.rollout(50, action_mode="random")
     R2 = e1.rollout(50, action_mode="random")  # graph replay
     rews = []
@@ -263,9 +264,9 @@ def test_greedy_vs_oracle_large(torch_gpu):
 
 
 @pytest.mark.parametrize("form", ["select", "sort"])
-def test_greedy_key_runs_vs_oracle(torch_gpu, monkeypatch, form):
+def test_greedy_key_runs_vs_oracle(torch_gpu, form):
     """mdr_ctrl_greedy on adversarial key layouts, in both forms (select: the default histogram
-    select; sort: MDR_GREEDY_SORT, the full 64-bit key sort): 300 identical temperatures, 700 keys
+    select; sort: MDR_OPT_GREEDY_SORT, the full 64-bit key sort): 300 identical temperatures, 700 keys
     1e-9 apart in DESCENDING house order, 100 houses at exactly their target (key -0.0), random
     lockouts, budgets that put the pivot inside each group; the oracle's stable numpy order
     decides.  The select form decides all of these itself (no fallback); a cluster of identical
@@ -274,13 +275,12 @@ def test_greedy_key_runs_vs_oracle(torch_gpu, monkeypatch, form):
     from mdr_amd.environment import Environment
     from mdr_amd.shard import encode_hvac
 
-    if form == "sort":
-        monkeypatch.setenv("MDR_GREEDY_SORT", "1")
     n = 50_000
     props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
                                      "power_grid_prop.signal_properties.mode": "flat"})
     env = Environment(props, rng=random.Random(3), population="synthetic", seed=8)
     sh = env.shard
+    sh.set_option("greedy_sort", form == "sort")
     prm = sh.host_params()
     rs = np.random.RandomState(5)
     tg = prm["target"].copy()

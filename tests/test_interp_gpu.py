@@ -118,6 +118,7 @@ def test_interp_rollout_equals_steps(mode):
                                      gu.BPP + "interp_nb_agents": 64})
     a = Environment(props, rng=random.Random(9), population="synthetic", seed=4)
     b = Environment(props, rng=random.Random(9), population="synthetic", seed=4)
+    b.shard.set_option("window_thermal", 0)  # MDR_THERMAL_EXACT: the interpolated signal reads T bit for bit
     acts = torch.from_numpy(np.random.RandomState(5).randint(0, 2, (T, n)).astype(np.uint8)).to("cuda")
     rew_a, sig = [], []
     for t in range(T):

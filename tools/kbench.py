@@ -2,9 +2,9 @@
 
     python tools/kbench.py [--houses 1048576,4194304] [--ticks 128] [--rounds 5] [--variants w32,w0,probe]
 
-Variants: wK[hH] = temporally blocked rollout, K ticks per k_step_window launch (H houses per
-lane, default 2); w0 = one launch per
-tick (k_step_pipe / k_step_t, MDR_TPW / MDR_HPT / MDR_FASTDIV still select among those); probe =
+Variants: wK[e] = temporally blocked rollout, K ticks per k_step_window launch (affine per-window
+thermal transition; e = the exact per-tick expression, MDR_OPT_WINDOW_THERMAL); w0 = one launch per
+tick (k_step_pipe); probe =
 the memory-floor probe of the one-tick kernel (same loads/stores, no arithmetic).  Every tick's
 reward row is kept ([ticks, n] float64), so reward writes really go to HBM.  Prints per-tick
 microseconds, house-steps/s and algorithmic GB/s (window: SURVEY §8(d) field sizes, state and
@@ -24,7 +24,7 @@ def main():
     ap.add_argument("--houses", default="1048576,4194304,16777216")
     ap.add_argument("--ticks", type=int, default=128)
     ap.add_argument("--rounds", type=int, default=5)
-    ap.add_argument("--variants", default="w32,w16,w0,probe")
+    ap.add_argument("--variants", default="w32,w32e,w16,w0,probe")
     a = ap.parse_args()
     import torch
 
@@ -36,12 +36,11 @@ def main():
     for n in [int(x) for x in a.houses.split(",")]:
         envs = {}
         for v in a.variants.split(","):
-            hpt = v.partition("h")[2]  # wKhH: houses per lane of k_step_window (MDR_WIN_HPT at mdr_create)
-            os.environ["MDR_WIN_HPT"] = hpt or "2"
             env = Environment(env_props(n), device="cuda:0", rng=random.Random(1), population="synthetic", seed=5)
             sh = env.shard
             if v.startswith("w"):
-                sh.set_rollout_window(int(v[1:].partition("h")[0]))
+                sh.set_rollout_window(int(v[1:].rstrip("e")))
+                sh.set_option("window_thermal", L.THERMAL_EXACT if v.endswith("e") else L.THERMAL_AFFINE)
             env._kb_rew = torch.empty((a.ticks, n), dtype=torch.float64, device="cuda:0")
             # one driver window replayed every round: the events time the graph alone (no host drivers)
             env._kb_ticks = env.driver_window(a.ticks)
@@ -62,7 +61,7 @@ def main():
                     e1.record()
                 else:
                     torch.cuda.synchronize()
-                    ls = sh.launch_stream(True)
+                    ls = sh.launch_stream()
                     e0.record(ls)
                     sh.rollout(env._kb_ticks, None, 0, L.ACT_RANDOM, env._kb_rew, n, True)
                     e1.record(ls)
@@ -72,8 +71,8 @@ def main():
         for v in envs:
             ts = sorted(res[(n, v)])
             med = ts[len(ts) // 2]
-            if v.startswith("w") and int(v[1:].partition("h")[0]) > 0:
-                k = int(v[1:].partition("h")[0])
+            if v.startswith("w") and int(v[1:].rstrip("e")) > 0:
+                k = int(v[1:].rstrip("e"))
                 launches = -(-a.ticks // k)
                 kk = a.ticks // launches
                 gbs = window_bytes(n, kk, "random") / (med * kk) / 1e3
