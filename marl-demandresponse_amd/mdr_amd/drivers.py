@@ -200,6 +200,22 @@ def _seconds_of_day(t: _dt.datetime) -> int:
     return t.hour * 3600 + t.minute * 60 + t.second
 
 
+@functools.lru_cache(maxsize=8)
+def _day_stamps(year: int, month: int, day: int) -> np.ndarray:
+    """time.mktime(t.timetuple()) % 86400 (signal_calculator.py:113) for every second t of the
+    day, as the per-tick perlin path computes it: from midnight's stamp when the day has 86,400
+    local seconds, else (a DST day) one mktime per second."""
+    import time
+
+    d0 = _dt.datetime(year, month, day)
+    m0 = time.mktime(d0.timetuple())
+    m1 = time.mktime((d0 + _dt.timedelta(days=1)).timetuple())
+    sod = np.arange(86400, dtype=np.float64)
+    if m1 - m0 == 86400.0:
+        return (m0 + sod) % 86400
+    return np.array([time.mktime((d0 + _dt.timedelta(seconds=k)).timetuple()) % 86400 for k in range(86400)])
+
+
 class Signal:
     """Regulation-signal shape (signal_calculator.py), without the base-power part."""
 
@@ -307,18 +323,33 @@ class GridSignal:
             self._memo[key] = self.current_signal
         return self.current_signal
 
-    def day_table(self) -> np.ndarray:
-        """current_signal after a step at every second of the day (constant base power and a
-        flat / sinusoidal / regular-steps signal), cached per (base, artificial ratio, cap)."""
-        key = (self.base_power(), self.gp.artificial_ratio, self.max_power)
+    def series_ok(self) -> bool:
+        """The signal has a per-second-of-day table: constant base power, no caller signal_fn, and
+        perlin only without the pre-1.12 global-RNG side effect (its draws interleave with the
+        per-tick gauss draws)."""
+        sig = self.signal
+        return (self.interp is None and self.signal_fn is None and
+                (sig.mode != "perlin" or sig.perlin.noise_list[0].global_rng is None))
+
+    def day_table(self, date=None) -> np.ndarray:
+        """current_signal after a step at every second of the day ``date`` (constant base power),
+        cached per (base, artificial ratio, cap) — and per date in perlin mode, whose noise follows
+        time.mktime (local time: a DST day has other stamps)."""
+        dkey = (date.year, date.month, date.day) if self.signal.mode == "perlin" else None
+        if dkey is None and date is None and self.signal.mode == "perlin":
+            raise ValueError("a perlin day table needs its date")
+        key = (self.base_power(), self.gp.artificial_ratio, self.max_power, dkey)
         if getattr(self, "_day_key", None) != key:
-            self._day_tab = self.signal_series(np.arange(86400, dtype=np.int64))
+            sod = np.arange(86400, dtype=np.int64)
+            stamps = _day_stamps(*dkey) if dkey is not None else None
+            self._day_tab = self.signal_series(sod, stamps)
             self._day_key = key
         return self._day_tab
 
-    def signal_series(self, sod) -> np.ndarray:
-        """``step`` at a series of ticks (seconds of day ``sod``, int64 array) for a constant base
-        power: the same IEEE operations as the per-tick path, elementwise (float64 array)."""
+    def signal_series(self, sod, stamps=None) -> np.ndarray:
+        """``step`` at a series of ticks (seconds of day ``sod``, int64 array; perlin: the ticks'
+        time.mktime(t) % 86400 ``stamps``) for a constant base power: the same IEEE operations as
+        the per-tick path, elementwise (float64 array)."""
         base = self.base_power()
         sp = self.signal.sp
         mode = self.signal.mode
@@ -337,6 +368,9 @@ class GridSignal:
             amplitude = sp.amplitude_per_hvac * self.nb_agents
             ratio = base / amplitude
             s = amplitude * np.heaviside((sod % sp.period) - (1 - ratio) * sp.period, 1)
+        elif mode == "perlin":
+            noise = self.signal.perlin.calculate_noise_array(stamps)
+            s = np.maximum(0, base + (base * sp.amplitude_ratios[0] * noise))
         else:
             raise ValueError(f"no series form for signal mode {mode!r}")
         s = s * self.gp.artificial_ratio

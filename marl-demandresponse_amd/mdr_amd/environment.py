@@ -263,7 +263,7 @@ class Environment:
         self._grid_pending = False
         self.power_grid.step(self.date_time, self.current_od_temp, p.time_step.seconds)  # first signal (:67-69)
         if self._vector_drivers_ok():  # rollout driver tables, built here rather than inside a rollout
-            self.power_grid.day_table()
+            self.power_grid.day_table(self.date_time)
             drivers.od_day_list(p.temp_prop)
         self._obs_links = self._links if self._links is not None else popmod.random_links(cp, rng)
         return self.get_obs() if return_obs else None
@@ -407,10 +407,8 @@ class Environment:
         return self._driver_window_loop(n_ticks)
 
     def _vector_drivers_ok(self) -> bool:
-        g = self.power_grid
         st = self.init_props.time_step
-        return (g.interp is None and g.signal_fn is None and g.signal.mode in ("flat", "sinusoidals", "regular_steps")
-                and st.microseconds == 0 and st.days == 0 and 0 < st.seconds < 86400)
+        return self.power_grid.series_ok() and st.microseconds == 0 and st.days == 0 and 0 < st.seconds < 86400
 
     def _driver_window_vec(self, n: int) -> "TickWindow":
         """driver_window for a constant base power and a flat / sinusoidal / regular-steps signal:
@@ -421,7 +419,6 @@ class Environment:
         p = self.init_props
         hp = p.cluster_prop.house_prop
         tp, grid = p.temp_prop, self.power_grid
-        sig_tab = grid.day_table()
         od_tab = drivers.od_day_array(tp)
         dts = p.time_step.seconds
         d0 = self.date_time
@@ -433,6 +430,7 @@ class Environment:
         tick0, done, day_off = self._tick, 0, 0
         while True:
             dd = d0 + _dt.timedelta(days=day_off) if day_off else d0
+            sig_tab = grid.day_table(dd)  # (the tick's new datetime: its signal)
             sol_tab = drivers.solar_day_table(dd.month, dd.day, wa, shc) if solar_on else None
             k, s, tod, sig, sol = _host.drivers(rng, rng.random, tp.temp_std, n - done, s, dts, od_tab, sig_tab,
                                                 sol_tab, dd.month, dd.day, wa, shc, drivers.SOLAR_TERMS_ARRAY,
@@ -460,7 +458,7 @@ class Environment:
         p = self.init_props
         hp = p.cluster_prop.house_prop
         tp, grid = p.temp_prop, self.power_grid
-        sig_tab = grid.day_table()
+        sig_tab = grid.day_table(self.date_time)
         od_tab = drivers.od_day_floats(tp)
         gs = drivers.gauss_n(self.rng, n, tp.temp_std)  # the n draws, in order (nothing else draws)
         dts = p.time_step.seconds
@@ -482,6 +480,7 @@ class Environment:
                 day_off += 1
                 dd = d0 + _dt.timedelta(days=day_off)
                 month, mday, last_m = dd.month, dd.day, -1
+                sig_tab = grid.day_table(dd)
             m = s // 60
             if solar_on and m != last_m:
                 sol = drivers.solar_minute(month, mday, m // 60, m % 60, wa, shc)

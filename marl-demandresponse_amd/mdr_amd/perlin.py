@@ -12,8 +12,10 @@ rand_vec.RandVec, tools.sample_vector / hasher / fade) as we know it:
   max(1, int(|k| + 1)) and ``seed`` is the float ``random.random()`` SignalCalculator passes
   (signal_calculator.py:24-31), so ``random.seed`` hashes the float;
 * a lattice point contributes ``fade(1 - |xs - k|) * g * (xs - k)`` with fade(t) = 6 t**5 -
-  15 t**4 + 10 t**3, and the contributions are summed with Python's ``sum`` (from int 0), in the
-  order of ``itertools.product``.
+  15 t**4 + 10 t**3 (evaluated here with products, t**3 = t*t*t, t**4 = t**3*t, t**5 = t**4*t, so
+  the scalar and the vectorised forms below agree bit for bit; the package's ``**`` may differ by an
+  ulp), and the contributions are summed with Python's ``sum`` (from int 0), in the order of
+  ``itertools.product``.
 
 The package draws the gradient by reseeding the GLOBAL ``random`` module; releases from 1.12 save
 and restore the global state around it, earlier ones leave it reseeded (the reference's later
@@ -28,10 +30,15 @@ from __future__ import annotations
 import math
 import random
 
+import numpy as np
 
-def _fade(t: float) -> float:
-    # tools.fade: the package rejects t outside [-0.1, 1.1]; 1 - |d| with |d| <= 1 never is
-    return 6 * t ** 5 - 15 * t ** 4 + 10 * t ** 3
+
+def _fade(t):
+    # tools.fade: the package rejects t outside [-0.1, 1.1]; 1 - |d| with |d| <= 1 never is.
+    # Products (not **): the same IEEE operations for a float and for a float64 array
+    t3 = t * t * t
+    t4 = t3 * t
+    return 6 * (t4 * t) - 15 * t4 + 10 * t3
 
 
 def _hasher(k: int) -> int:
@@ -71,6 +78,20 @@ class _GradientNoise1D:
             total += _fade(1 - abs(d)) * (self._grad(k) * d)  # weight_to * dot(vec, dists)
         return total
 
+    def noise_array(self, x: np.ndarray) -> np.ndarray:
+        """``noise`` of every element of a float64 array, bit for bit (the gradients of the lattice
+        points it touches are drawn once each, in increasing k; no global-RNG side effect)."""
+        if self.global_rng is not None:
+            raise ValueError("the pre-1.12 global-RNG side effect has no array form")
+        xs = x * self.octaves
+        total = np.zeros_like(xs)
+        for k in (np.floor(xs), np.floor(xs + 1)):
+            ks = np.unique(k)
+            g = np.array([self._grad(int(v)) for v in ks], np.float64)[np.searchsorted(ks, k)]
+            d = xs - k
+            total = total + _fade(1 - np.abs(d)) * (g * d)
+        return total
+
 
 class Perlin:
     """Octave sum of the reference's Perlin helper (perlin.py:5-56)."""
@@ -88,4 +109,13 @@ class Perlin:
         for j in range(self.nb_octaves - 1):
             noise += self.noise_list[j].noise(x / self.period) / (2 ** j)
         noise += self.noise_list[-1].noise(x / self.period) / (2 ** self.nb_octaves - 1)
+        return self.amplitude * noise
+
+    def calculate_noise_array(self, x: np.ndarray) -> np.ndarray:
+        """``calculate_noise`` of every element of a float64 array, bit for bit."""
+        xp = np.asarray(x, np.float64) / self.period
+        noise = np.zeros_like(xp)
+        for j in range(self.nb_octaves - 1):
+            noise = noise + self.noise_list[j].noise_array(xp) / (2 ** j)
+        noise = noise + self.noise_list[-1].noise_array(xp) / (2 ** self.nb_octaves - 1)
         return self.amplitude * noise

@@ -18,6 +18,7 @@ Reference map (file:line relative to /root/reference):
   solar_gain           server/app/utils/utils.py:42-117
   od_temp              server/app/core/environment/environment.py:132-159
   signal_*             server/app/core/environment/power_grid/signal_calculator.py:33-129
+                       (perlin: oracle/perlin_np.py, the package's published algorithm — parity unpinned)
   grid_step            server/app/core/environment/power_grid/power_grid.py:80-161
   deadband_l2          server/app/utils/utils.py:4-23
   rewards              server/app/core/environment/rewards_calculator.py:29-203
@@ -141,7 +142,7 @@ def _tsec(t: _dt.datetime) -> int:
     return t.hour * 3600 + t.minute * 60 + t.second
 
 
-def signal(mode: str, sp, base: float, t: _dt.datetime, nb_agents: int) -> float:
+def signal(mode: str, sp, base: float, t: _dt.datetime, nb_agents: int, perlin=None) -> float:
     if mode == "flat":
         return base
     if mode == "sinusoidals":
@@ -158,7 +159,12 @@ def signal(mode: str, sp, base: float, t: _dt.datetime, nb_agents: int) -> float
         ratio = base / amp
         per = sp.period
         return amp * np.heaviside((_tsec(t) % per) - (1 - ratio) * per, 1)
-    raise NotImplementedError(f"signal mode {mode!r} is not restated (perlin parity is unpinned)")
+    if mode == "perlin" and perlin is not None:  # signal_calculator.py:100-115 (parity unpinned)
+        import time
+
+        stamp = time.mktime(t.timetuple()) % 86400
+        return np.maximum(0, base + (base * sp.amplitude_ratios[0] * perlin.calculate_noise(stamp)))
+    raise NotImplementedError(f"signal mode {mode!r} is not restated")
 
 
 # ------------------------------------------------------------------------------- rewards
@@ -324,8 +330,12 @@ class OracleEnv:
         gp = p.power_grid_prop
         gp.artificial_ratio = gp.artificial_ratio * gp.artificial_signal_ratio_range ** (
             self.rng.random() * 2 - 1)
-        if gp.signal_properties.mode == "perlin":
-            raise NotImplementedError("perlin signal parity is unpinned")
+        self._perlin = None
+        sp = gp.signal_properties
+        if sp.mode == "perlin":  # SignalCalculator draws its seed next (signal_calculator.py:24-31)
+            from .perlin_np import PerlinSignal
+
+            self._perlin = PerlinSignal(sp.nb_octaves, sp.octaves_step, sp.period, self.rng.random())
         self.S = 0.0
         self._interp_since = gp.base_power_props.interp_update_period + 1  # power_grid.py:64-66
         self._grid_step()
@@ -361,7 +371,7 @@ class OracleEnv:
             raise ValueError(f"unknown base power mode {bp.mode!r}")
         else:
             base = bp.avg_power_per_hvac * self.n
-        s = signal(gp.signal_properties.mode, gp.signal_properties, base, self.date, self.n)
+        s = signal(gp.signal_properties.mode, gp.signal_properties, base, self.date, self.n, self._perlin)
         s = s * gp.artificial_ratio
         self.S = np.minimum(s, self.max_power)
 

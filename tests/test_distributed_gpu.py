@@ -70,7 +70,9 @@ def _variant(env, kind):
     """The launch form a test kind selects (mdr_set_option), on the sharded env and its reference:
     rccl-winserial = windows without the count-ahead pipeline (one stream); rccl-serial /
     rccl-overlap = the per-tick C loop (window 0), serial or two-stream."""
-    if kind == "rccl-winserial":
+    if kind == "torch":  # TorchComm steps every tick from Python (one-tick kernels): the exact form
+        env.shard.set_option("window_thermal", 0)
+    elif kind == "rccl-winserial":
         env.shard.set_option("window_pipeline", 0)
     elif kind in ("rccl-serial", "rccl-overlap"):
         env.shard.set_rollout_window(0)

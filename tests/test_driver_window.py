@@ -1,8 +1,9 @@
 """driver_window's vectorised series (Environment._driver_window_vec) == the per-tick driver loop,
 bit for bit: tick drivers (t_od_prev, solar, s_prev, tick), and the env's datetime, OD temperature,
 signal and RNG state afterwards.  Windows cross midnight and month ends; all three vectorisable
-signal modes; solar gain on and off.  The GPU-marked copy runs the same check on the GPU box's
-host CPU (NumPy's vectorised sin must equal its scalar sin there too)."""
+signal modes and perlin (its restated noise tabulated per date, mdr_amd/perlin.py); solar gain on and
+off.  The GPU-marked copy runs the same check on the GPU box's host CPU (NumPy's vectorised sin
+must equal its scalar sin there too)."""
 import datetime as dt
 import random
 
@@ -16,7 +17,9 @@ CASES = [("sinusoidals", True, dt.datetime(2021, 1, 31, 23, 50), 600),
          ("sinusoidals", False, dt.datetime(2021, 6, 1, 7, 28, 30), 37),
          ("flat", True, dt.datetime(2021, 3, 14, 17, 59, 58), 200),
          ("regular_steps", True, dt.datetime(2021, 12, 31, 23, 59, 2), 333),
-         ("flat", True, dt.datetime(2021, 5, 9, 6, 0), 30000)]  # 33 h: every daylight minute's solar gain
+         ("flat", True, dt.datetime(2021, 5, 9, 6, 0), 30000),  # 33 h: every daylight minute's solar gain
+         ("perlin", True, dt.datetime(2021, 1, 31, 23, 50), 600),  # perlin day tables of two dates
+         ("perlin", False, dt.datetime(2021, 8, 2, 11, 3, 30), 45)]
 
 
 def _env(mode, solar, start, seed):
@@ -91,3 +94,22 @@ def test_native_drivers_module_rng_and_short_windows():
 def test_vector_drivers_equal_loop_on_gpu_host():
     for case in CASES:
         _check(*case)
+
+
+def test_overridden_gauss_uses_it():
+    """A random.Random subclass with its own gauss: driver_window draws through that gauss (the C
+    drivers and the unrolled draw restate CPython's gauss, so they are not used), equal to the
+    per-tick loop."""
+    from mdr_amd import environment
+
+    class MyRandom(random.Random):
+        def gauss(self, mu=0.0, sigma=1.0):
+            return mu + sigma * (self.random() - 0.5)
+
+    assert not environment._host_gauss_ok(MyRandom(3)) and environment._host_gauss_ok(random.Random(3))
+    a, b = _env("sinusoidals", True, dt.datetime(2021, 4, 1, 12, 0), 11), _env("sinusoidals", True,
+                                                                                dt.datetime(2021, 4, 1, 12, 0), 11)
+    a.rng, b.rng = MyRandom(9), MyRandom(9)
+    wa, wb = a.driver_window(50), b._driver_window_loop(50)
+    np.testing.assert_array_equal(wa.a.view(np.uint64), wb.a.view(np.uint64))
+    assert a.rng.random() == b.rng.random()

@@ -390,3 +390,52 @@ def test_greedy_one_million_vs_oracle(torch_gpu):
         np.testing.assert_allclose(st["T"], o["T"], rtol=TEMP_RTOL, atol=0)
         np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12)
         assert env.cluster.current_power_consumption == o["P"]
+
+
+@pytest.mark.parametrize("path", ["step", "rollout"])
+def test_perlin_trajectory_vs_oracle(torch_gpu, path):
+    """Perlin signal mode (the MARLconfig default) on the GPU path, against the
+    oracle fed an independent scalar restatement of the same published algorithm
+    (oracle/perlin_np.py; parity with the absent third-party package is UNPINNED).  The seed is
+    drawn in the reference's order (signal_calculator.py:24-31).  'step': dict-free step_tensor
+    ticks with buffer actions; 'rollout': the default rollout (direct launches, perlin tabulated per
+    date into the C host drivers, affine windows) with the replayed Philox actions, crossing
+    midnight.  Signal within 1e-12 relative (the two restatements round the fade's powers
+    differently), masks exact, temperatures rtol 1e-10, rewards rtol 1e-9."""
+    import datetime as dt
+
+    import philox_np as PX
+
+    torch = torch_gpu
+    from mdr_amd.environment import Environment
+
+    n, T = 4099, 240
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "perlin"})
+    props.start_datetime = dt.datetime(2021, 6, 30, 23, 50)
+    props.start_datetime_mode = "fixed"
+    env = Environment(props, rng=random.Random(17), seed=99)
+    ora = O.OracleEnv(props, random.Random(17))
+    np.testing.assert_allclose(float(env.power_grid.current_signal), ora.S, rtol=1e-12)
+    assert env._vector_drivers_ok()
+    gids = np.arange(n, dtype=np.uint64)
+    if path == "rollout":
+        tick0 = env._tick
+        R = env.rollout(T, action_mode="random").cpu().numpy()
+        for t in range(T):
+            o, rr = ora.step(PX.random_actions(99, gids, tick0 + t))
+            np.testing.assert_allclose(R[t], rr, rtol=1e-9, atol=1e-12, err_msg=f"reward t={t}")
+    else:
+        rs = np.random.RandomState(3)
+        for t in range(T):
+            a = rs.randint(0, 2, n).astype(np.uint8)
+            r = env.step_tensor(torch.from_numpy(a).to("cuda")).cpu().numpy()
+            o, rr = ora.step(a.astype(bool))
+            np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12, err_msg=f"reward t={t}")
+            np.testing.assert_allclose(float(env.power_grid.current_signal), o["S"], rtol=1e-12)
+    st = env.shard.host_state()
+    for k in ("on", "lock", "sso"):
+        np.testing.assert_array_equal(st[k], o[k], err_msg=k)
+    np.testing.assert_allclose(st["T"], o["T"], rtol=TEMP_RTOL, atol=0)
+    np.testing.assert_allclose(float(env.power_grid.current_signal), o["S"], rtol=1e-12)
+    assert env.cluster.current_power_consumption == o["P"]
+    assert env.date_time == o["date"] and env.date_time.day == 1  # crossed midnight into July

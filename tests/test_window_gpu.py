@@ -30,8 +30,12 @@ def torch_gpu():
     return torch
 
 
-AFFINE_T_RTOL = 1e-11     # affine vs exact thermal form, within a rollout of <= 131 ticks
-AFFINE_LONG_RTOL = 1e-9   # over 2,000 ticks
+# affine vs exact thermal form: the reference's own expression cancels terms of ~5,000 K to a
+# ~293 K result, so the two rounding sequences part by ~1e-12 K per tick (measured: 9e-11 K, 5e-12
+# relative, after 100 ticks); north star: 1e-5
+AFFINE_T_RTOL = 1e-10     # temperatures, within a rollout of <= 131 ticks
+AFFINE_R_RTOL, AFFINE_R_ATOL = 1e-9, 1e-10  # rewards -(x^2 + s): relative error grows as x -> 0
+AFFINE_LONG_RTOL = 1e-8   # temperatures over 2,000 ticks
 
 
 def _pair(n, seed=3, pop="synthetic", extra=None, thermal=None):
@@ -76,7 +80,7 @@ def _same_state(torch, e1, e2):
 def test_window_equals_one_tick(torch_gpu, n, ticks, win, mode, thermal, use_graph):
     """Windowed rollout (direct launches with kernel-argument drivers, or a replayed graph) vs the
     one-launch-per-tick rollout: EXACT bit for bit (rewards, state, P); AFFINE with the masks,
-    counters and P bit for bit and temperatures / rewards within AFFINE_T_RTOL."""
+    counters and P bit for bit, temperatures within AFFINE_T_RTOL, rewards within AFFINE_R_*."""
     torch = torch_gpu
     e1, e2 = _pair(n, thermal=thermal)
     e1.shard.set_rollout_window(win)
@@ -92,7 +96,7 @@ def test_window_equals_one_tick(torch_gpu, n, ticks, win, mode, thermal, use_gra
             np.testing.assert_array_equal(r1.cpu().numpy(), r2.cpu().numpy())
             _same_state(torch, e1, e2)
         else:
-            np.testing.assert_allclose(r1.cpu().numpy(), r2.cpu().numpy(), rtol=AFFINE_T_RTOL, atol=1e-12)
+            np.testing.assert_allclose(r1.cpu().numpy(), r2.cpu().numpy(), rtol=AFFINE_R_RTOL, atol=AFFINE_R_ATOL)
             _close_state(torch, e1, e2, AFFINE_T_RTOL)
 
 
@@ -113,7 +117,7 @@ def test_affine_form_long_run(torch_gpu, n):
         _close_state(torch, e1, e2, AFFINE_LONG_RTOL)
         d = (r1 - r2).abs().max().item()
         worst = max(worst, d)
-        assert d <= 1e-9, (c, d)
+        assert d <= 1e-8, (c, d)
     s1, s2 = e1.shard.host_state(), e2.shard.host_state()
     rel = float(np.max(np.abs(s1["T"] - s2["T"]) / np.abs(s2["T"])))
     print(f"n={n}: after 2000 ticks max rel |T_affine - T_exact| = {rel:.3g}, max |dr| = {worst:.3g}")
