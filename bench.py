@@ -326,9 +326,9 @@ def main():
         if dactor is not None:
             dactor.rollout(n, rewards=rew[:n])
         elif g_act is not None:  # C3: controller on the post-step state -> step, every tick
-            for t in range(n):
+            for t in range(n):  # (the step's epilogue writes the next greedy call's keys)
                 env.greedy_actions(out=g_act)
-                env.step_tensor(g_act, rewards=rew[t])
+                env.step_tensor(g_act, rewards=rew[t], ctrl="greedy_keys")
         else:  # (whole buffers when the chunk fills them: no tensor views built per call)
             env.rollout(n, actions=None if acts is None else (acts if n == chunk else acts[:n]),
                         action_mode=args.mode, rewards=rew if n == chunk else rew[:n], use_graph=use_graph)
@@ -460,14 +460,14 @@ def main():
         ev0.record(cur)
         for t in range(K):
             env.greedy_actions(out=g_act)
-            env.step_tensor(g_act, rewards=rew[t % rew.shape[0]])
+            env.step_tensor(g_act, rewards=rew[t % rew.shape[0]], ctrl="greedy_keys")
         ev1.record(cur)
         torch.cuda.synchronize()
         launches, kern_ms = K, ev0.elapsed_time(ev1) / K
         bytes_launch = (BYTES_PER_HOUSE_STEP + GREEDY_EXTRA) * n_loc
         steps_launch = 1
-        kern = ("greedy tick: histogram select (k_gq_keys, k_gq_select_super, k_gq_bins, k_gq_select_bin, "
-                "k_gq_compact, k_gq_gather, k_gq_rank, k_gq_finish) + k_power_counts + k_step_pipe")
+        kern = ("greedy tick: histogram select (k_gq_bins, k_gq_compact, k_gq_gather, k_gq_rank, k_gq_finish; "
+                "keys from the previous k_step_pipe's epilogue) + k_step_pipe")
     else:
         # the actor rollout graph interleaves k_actor and k_step: time the actor alone
         K = 50

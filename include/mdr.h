@@ -71,8 +71,10 @@ enum {
   MDR_ACT_DEADBAND_BANGBANG = 17 /* DeadbandBangBangController, bangbang_controllers.py:25-42 */
 };
 
-/* controller evaluated on the post-step state, written as the NEXT tick's action buffer */
-enum { MDR_CTRL_NONE = 0, MDR_CTRL_BANGBANG = 1, MDR_CTRL_DEADBAND_BANGBANG = 2 };
+/* controller evaluated on the post-step state, written as the NEXT tick's action buffer
+ * (MDR_CTRL_GREEDY_KEYS: no action buffer — the greedy controller's keys and key histogram of the
+ * post-step state are prepared for the next mdr_ctrl_greedy, which then skips its key pass) */
+enum { MDR_CTRL_NONE = 0, MDR_CTRL_BANGBANG = 1, MDR_CTRL_DEADBAND_BANGBANG = 2, MDR_CTRL_GREEDY_KEYS = 3 };
 
 /* communication (message) topology, agent_communication_builder.py:36-203 */
 enum { MDR_COMM_RING = 0, MDR_COMM_TABLE = 1 };
@@ -201,6 +203,7 @@ int mdr_counts_buffer(mdr_ctx* ctx, int64_t** dev_ptr, int* len);
  *                 state, so the next tick needs no phase-1 launch
  *   ctrl_out    : if non-NULL, the bang-bang (ctrl = MDR_CTRL_*) decision on the new state
  *   p_out       : if non-NULL, device double receiving the tick's cluster power
+ *   ctrl = MDR_CTRL_GREEDY_KEYS: the next mdr_ctrl_greedy's keys (see MDR_CTRL_*)
  * For common penalty modes reward holds the raw penalty until mdr_reward_finalize. */
 int mdr_step(mdr_ctx* ctx, const uint8_t* action, int action_mode, const mdr_tick* tick,
              double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
@@ -306,12 +309,15 @@ int mdr_cluster_stats(mdr_ctx* ctx, const double* reward, double* out, void* str
 
 /* ---- greedy-myopic controller (greedy_myopic_controller.py:67-104) --------------------- */
 /* Next actions for the whole shard (single GPU: shard = cluster) from the current state: order
- * by -(T - target) ascending, then the reference's sequential take rule with budget S.  Histogram
- * select: only the houses around the budget crossing are ordered; synchronises `stream` once to
- * read back whether that window decided the tick, else the full-sort form runs (same result;
- * MDR_OPT_GREEDY_SORT forces it). */
+ * by -(T - target) ascending, then the reference's sequential take rule with budget S.  Also fills
+ * the current tick's cluster-power counts with the ON houses those actions produce, so the next
+ * mdr_step(action, MDR_ACT_BUFFER) needs no mdr_power_counts.  Asynchronous (no host
+ * synchronisation): histogram select on device — only the houses around the budget crossing are
+ * ordered; what that window cannot decide (a crossing among NaN keys or inside a bin of > 4,096
+ * houses, e.g. identical keys; a walk past the window) the last kernel decides exactly itself.
+ * With more than 4 capacity classes (or MDR_OPT_GREEDY_SORT) the full-sort form runs. */
 int mdr_ctrl_greedy(mdr_ctx* ctx, double budget, uint8_t* action, void* stream);
-/* Diagnostics: mdr_ctrl_greedy calls the histogram select handed to the full-sort form. */
+/* Diagnostics (synchronises): mdr_ctrl_greedy calls decided by the exact in-kernel fallback. */
 int mdr_greedy_fallbacks(mdr_ctx* ctx, uint64_t* count);
 
 /* Sharded greedy (the all-gather form): mdr_greedy_inputs writes this shard's

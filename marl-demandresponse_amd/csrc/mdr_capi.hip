@@ -121,9 +121,9 @@ struct mdr_ctx {
   uint4* g_stage = nullptr;
   uint4* g_sorted = nullptr;             // the window in (key, house) order (k_gq_rank)
   unsigned* g_bcnt = nullptr;
-  int* g_flag = nullptr;
-  int* h_gq_flag = nullptr;              // pinned: the overflow flag read back after the window
-  uint64_t gq_fallbacks = 0;             // calls the histogram select handed to the sort form
+  int gq_parts_cap = 0;                  // g_part capacity in (min, max) pairs
+  bool gq_keys_ready = false;            // keys + superbin histogram of the current state are in place
+  int gq_nparts = 0;                     //   (from the last step's epilogue: its grid's partials)
   // multi-GPU
   ncclComm_t comm = nullptr;
   int world = 1, rank = 0;
@@ -201,12 +201,20 @@ int refresh_if_dirty(mdr_ctx* c, hipStream_t st) {
 
 // k_step launch with explicit count slabs; reward_lag: the launch writes the previous tick's
 // reward from `cur` (nullptr: none), see k_step_t
+int greedy_scratch(mdr_ctx* c, int64_t n);
+int launch_gq_keys(mdr_ctx* c, hipStream_t st);
+
 int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const TickArgs* tkp,
                    double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
                    const unsigned long long* cur, unsigned long long* nxt, unsigned long long* zer,
                    int reward_lag, hipStream_t st) {
   if (int rc = refresh_if_dirty(c, st)) return rc;
   const KParams kp = c->kp;
+  const bool gq = ctrl == MDR_CTRL_GREEDY_KEYS;
+  if (gq) {
+    if (int rc = greedy_scratch(c, kp.n)) return rc;
+    ctrl = MDR_CTRL_NONE;
+  }
 #define MDR_LAUNCH_STEP(F, A, LA)                                                                     \
   hipLaunchKernelGGL((k_step_t<2, F, A, LA>), dim3(blocks(kp.n, 512)), dim3(256), 0, st, kp, action, mode, \
                      tk, tkp, cur, reward, ctrl, ctrl_out, p_out, lookahead, nxt, zer, c->d_pen_partial,    \
@@ -221,21 +229,32 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
   if (pipe_ok) {
     int tpw = c->tpw >= 8 ? 8 : c->tpw >= 4 ? 4 : c->tpw >= 2 ? 2 : 1;
     if (hot_buffer) tpw = tpw >= 4 ? 4 : 2;  // the instantiated buffer variants
-    const dim3 grid(blocks(blocks(kp.n, 128), 4 * tpw));  // every tile covered: ceil(tiles / (4 waves x tpw))
-#define MDR_LAUNCH_PIPE(T, A, LA)                                                                     \
-  hipLaunchKernelGGL((k_step_pipe<T, A, LA>), grid, dim3(256), 0, st, kp, action, tk, tkp, cur, reward, \
-                     p_out, nxt, zer)
+    const unsigned nb = blocks(blocks(kp.n, 128), 4 * tpw);  // every tile covered: ceil(tiles / (4 waves x tpw))
+    const dim3 grid(nb);
+    // the greedy controller's keys in the epilogue (buffer actions: the C3 loop), when its
+    // partials buffer holds this grid
+    const bool epi = gq && hot_buffer && (int)nb <= c->gq_parts_cap;
+    GqOut go{};
+    if (epi) go = GqOut{c->g_key, c->g_part, c->g_hist, c->g_sel};
+#define MDR_LAUNCH_PIPE(T, A, LA, G)                                                                     \
+  hipLaunchKernelGGL((k_step_pipe<T, A, LA, G>), grid, dim3(256), 0, st, kp, action, tk, tkp, cur, reward, \
+                     p_out, nxt, zer, go)
     if (hot_random) {
-      if (tpw == 8) MDR_LAUNCH_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
-      else if (tpw == 4) MDR_LAUNCH_PIPE(4, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
-      else if (tpw == 2) MDR_LAUNCH_PIPE(2, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
-      else MDR_LAUNCH_PIPE(1, MDR_ACT_RANDOM, MDR_ACT_RANDOM);
+      if (tpw == 8) MDR_LAUNCH_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false);
+      else if (tpw == 4) MDR_LAUNCH_PIPE(4, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false);
+      else if (tpw == 2) MDR_LAUNCH_PIPE(2, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false);
+      else MDR_LAUNCH_PIPE(1, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false);
+    } else if (epi) {
+      if (tpw >= 4) MDR_LAUNCH_PIPE(4, MDR_ACT_BUFFER, 0, true);
+      else MDR_LAUNCH_PIPE(2, MDR_ACT_BUFFER, 0, true);
     } else {
-      if (tpw >= 4) MDR_LAUNCH_PIPE(4, MDR_ACT_BUFFER, 0);
-      else MDR_LAUNCH_PIPE(2, MDR_ACT_BUFFER, 0);
+      if (tpw >= 4) MDR_LAUNCH_PIPE(4, MDR_ACT_BUFFER, 0, false);
+      else MDR_LAUNCH_PIPE(2, MDR_ACT_BUFFER, 0, false);
     }
 #undef MDR_LAUNCH_PIPE
     LAUNCH_CHECK("k_step_pipe");
+    if (gq && !epi) return launch_gq_keys(c, st);
+    if (epi) c->gq_nparts = (int)nb;
     return MDR_OK;
   }
   if (c->fastdiv) {
@@ -247,17 +266,20 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
   }
 #undef MDR_LAUNCH_STEP
   LAUNCH_CHECK("k_step");
+  if (gq) return launch_gq_keys(c, st);
   return MDR_OK;
 }
 
 int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const TickArgs* tkp,
                 double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
                 hipStream_t st) {
+  c->gq_keys_ready = false;
   int rc = launch_step_on(c, action, mode, tk, tkp, reward, lookahead, ctrl, ctrl_out, p_out,
                           slab_at(c, c->ring), slab_at(c, c->ring + 1), slab_at(c, c->ring + 2), 0, st);
   if (rc) return rc;
   c->ring = (c->ring + 1) % 3;
   c->counts_ready = lookahead != 0;
+  c->gq_keys_ready = ctrl == MDR_CTRL_GREEDY_KEYS;
   return MDR_OK;
 }
 
@@ -272,6 +294,7 @@ static void drop_begun(mdr_ctx* c) {
     c->begun.on = false;
     c->wslab_dirty = true;
   }
+  if (c) c->gq_keys_ready = false;  // (every such entry point may change the state)
 }
 
 int mdr_abi_version(void) { return MDR_ABI_VERSION; }
@@ -419,7 +442,7 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
   hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_stage); hipFree(c->g_bcnt);
-  hipFree(c->g_flag); hipHostFree(c->h_gq_flag); hipFree(c->g_sorted);
+  hipFree(c->g_sorted);
   if (c->comm) ncclCommDestroy(c->comm);
   delete c;
   return MDR_OK;
@@ -521,7 +544,7 @@ int mdr_step(mdr_ctx* c, const uint8_t* action, int mode, const mdr_tick* tick, 
     return fail(MDR_EARG, "mdr_step: bad action source");
   if (lookahead && (!check_mode(lookahead) || !lookahead_ok(lookahead)))
     return fail(MDR_EARG, "mdr_step: bad lookahead source");
-  if (ctrl < MDR_CTRL_NONE || ctrl > MDR_CTRL_DEADBAND_BANGBANG) return fail(MDR_EARG, "mdr_step: bad ctrl");
+  if (ctrl < MDR_CTRL_NONE || ctrl > MDR_CTRL_GREEDY_KEYS) return fail(MDR_EARG, "mdr_step: bad ctrl");
   if (!c->counts_ready) return fail(MDR_ESTATE, "mdr_step: no cluster-power counts for this tick (call mdr_power_counts)");
   return launch_step(c, action, mode, to_tick(tick), nullptr, reward, lookahead, ctrl, ctrl_out, p_out,
                      S(stream));
@@ -879,6 +902,7 @@ static bool consecutive(const mdr_tick* ticks, int n) {
 int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action, int64_t act_stride,
                 int mode, double* reward, int64_t rew_stride, double* p_out, int use_graph, void* stream) {
   if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout: bad argument");
+  c->gq_keys_ready = false;
   if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout: context not bound");
   if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout: bad action source");
   if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
@@ -945,6 +969,7 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
 int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, int64_t act_stride, int mode,
                       void* stream) {
   if (!c || n < 1) return fail(MDR_EARG, "mdr_rollout_begin: bad argument");
+  c->gq_keys_ready = false;
   if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout_begin: context not bound");
   if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout_begin: bad action source");
   if (c->begun.on) c->wslab_dirty = true;  // a previous early count that no rollout consumed
@@ -1100,23 +1125,28 @@ int mdr_halo_pack(mdr_ctx* c, const mdr_obs_spec* sp, float* out, void* stream) 
 }
 
 // ------------------------------------------------------------------------------------ greedy
+}  // extern "C"
+
+namespace {
+
 // The greedy order: a stable sort of (key, house) pairs (hipCUB / rocprim radix sort; at 2^20
 // houses rocprim runs its block merge sort, which measured faster here than forcing Onesweep:
 // 212 us vs ~250 us incl. its per-pass lookback resets, profiles/r02g_greedy_kernel_stats.csv)
-static hipError_t greedy_sort(void* tmp, size_t& bytes, const double* kin, double* kout, const int* vin, int* vout,
-                              int64_t n, hipStream_t st) {
+hipError_t greedy_sort(void* tmp, size_t& bytes, const double* kin, double* kout, const int* vin, int* vout,
+                       int64_t n, hipStream_t st) {
   return hipcub::DeviceRadixSort::SortPairs(tmp, bytes, kin, kout, vin, vout, (int)n, 0, 64, st);
 }
 
-static int greedy_scratch(mdr_ctx* c, int64_t n) {
+int greedy_scratch(mdr_ctx* c, int64_t n) {
   if (c->g_cap >= n) return MDR_OK;
   hipFree(c->g_key); hipFree(c->g_key2); hipFree(c->g_ps); hipFree(c->g_incl);
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
   hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_stage); hipFree(c->g_bcnt);
-  hipFree(c->g_flag); hipHostFree(c->h_gq_flag); hipFree(c->g_sorted);
+  hipFree(c->g_sorted);
   c->g_part = nullptr; c->g_hist = nullptr; c->g_sel = nullptr; c->g_stage = nullptr; c->g_bcnt = nullptr;
-  c->g_flag = nullptr; c->h_gq_flag = nullptr; c->g_sorted = nullptr;
+  c->g_sorted = nullptr;
+  c->gq_keys_ready = false;
   HIP_TRY(hipMalloc(&c->g_key, n * sizeof(double)));
   HIP_TRY(hipMalloc(&c->g_key2, n * sizeof(double)));
   HIP_TRY(hipMalloc(&c->g_ps, n * sizeof(double)));
@@ -1127,9 +1157,12 @@ static int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_kpos, 2 * sizeof(int64_t)));
   HIP_TRY(hipMalloc(&c->g_extra, 64 * sizeof(int64_t)));
   const int64_t nstage = (n + kGqStage - 1) / kGqStage;
-  HIP_TRY(hipMalloc(&c->g_part, 2 * kGqParts * sizeof(double)));
-  HIP_TRY(hipMalloc(&c->g_hist, (kGqBins + kGqSuper * kGqCopies) * 4 * sizeof(unsigned)));
-  HIP_TRY(hipMemset(c->g_hist, 0, (kGqBins + kGqSuper * kGqCopies) * 4 * sizeof(unsigned)));  // (k_gq_select re-zeroes it)
+  // (min, max) partials: k_gq_keys' grid, or the grid of the step kernel whose epilogue writes the
+  // keys (k_step_pipe: a block per 4 x tpw x 128 houses, tpw >= 2)
+  c->gq_parts_cap = (int)std::max<int64_t>(kGqParts, (n + 1023) / 1024);
+  HIP_TRY(hipMalloc(&c->g_part, 2 * (size_t)c->gq_parts_cap * sizeof(double)));
+  HIP_TRY(hipMalloc(&c->g_hist, kGqHistWords * sizeof(unsigned)));
+  HIP_TRY(hipMemset(c->g_hist, 0, kGqHistWords * sizeof(unsigned)));  // (the kernels re-zero what they read)
   HIP_TRY(hipMalloc(&c->g_sel, 128));
   {
     unsigned char init[128] = {};
@@ -1139,8 +1172,6 @@ static int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_stage, nstage * kGqStage * sizeof(uint4)));
   HIP_TRY(hipMalloc(&c->g_bcnt, nstage * sizeof(unsigned)));
   HIP_TRY(hipMalloc(&c->g_sorted, 2 * kGqCap * sizeof(uint4)));  // [sorted | gathered window]
-  HIP_TRY(hipMalloc(&c->g_flag, sizeof(int)));
-  HIP_TRY(hipHostMalloc(&c->h_gq_flag, sizeof(int), hipHostMallocDefault));
   size_t b1 = 0, b2 = 0;
   HIP_TRY(greedy_sort(nullptr, b1, c->g_key, c->g_key2, c->g_idx, c->g_idx2, n, nullptr));
   HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b2, c->g_ps, c->g_incl, (int)n));
@@ -1150,44 +1181,55 @@ static int greedy_scratch(mdr_ctx* c, int64_t n) {
   return MDR_OK;
 }
 
+// the keys and superbin histogram of the current state (when no step epilogue prepared them)
+int launch_gq_keys(mdr_ctx* c, hipStream_t st) {
+  hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_part, c->g_hist,
+                     c->g_sel);
+  LAUNCH_CHECK("k_gq_keys");
+  c->gq_nparts = kGqParts;
+  return MDR_OK;
+}
+
+}  // namespace
+
+extern "C" {
+
 int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   if (!c || !action) return fail(MDR_EARG, "mdr_ctrl_greedy: null argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_ctrl_greedy: context not bound");
+  const bool keys_ready = c->gq_keys_ready && c->g_cap >= c->kp.n;  // (the last step's epilogue wrote them)
+  drop_begun(c);
+  c->gq_keys_ready = false;  // (the histogram is consumed below)
   int rc = greedy_scratch(c, c->kp.n);
   if (rc) return rc;
   hipStream_t st = S(stream);
   const int n = (int)c->kp.n;
   double pmin = INFINITY;
   for (int k = 0; k < c->cfg.n_cap; ++k) pmin = fmin(pmin, c->cfg.cap_table[k] / c->cfg.cop);
-  if (c->kp.n_cap <= 4 && n < (1 << 30) && !c->greedy_sort) {
-    // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster; the sort form below
-    // runs only when the candidate window cannot decide (the flag read back here)
-    // (g_sel's only accumulated field, overflow, is cleared by k_gq_finish for the next call)
-    hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_part, c->g_hist, c->g_sel);
-    LAUNCH_CHECK("k_gq_keys");
-    hipLaunchKernelGGL(k_gq_select_super, dim3(1), dim3(256), 0, st, c->kp, c->g_hist, budget, c->g_part, kGqParts,
-                       c->g_sel);
-    LAUNCH_CHECK("k_gq_select_super");
-    hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_hist, c->g_sel);
+  unsigned long long* slab = slab_at(c, c->ring);  // the counts of the actions decided here
+  if (c->kp.n_cap <= 4 && !c->greedy_sort) {
+    // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster, no host
+    // synchronisation; k_gq_finish decides exactly what the candidate window cannot
+    if (!keys_ready)
+      if (int rc2 = launch_gq_keys(c, st)) return rc2;
+    hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_hist, c->g_part,
+                       c->gq_nparts, budget, c->g_sel, slab);
     LAUNCH_CHECK("k_gq_bins");
-    hipLaunchKernelGGL(k_gq_select_bin, dim3(1), dim3(128), 0, st, c->kp, c->g_hist, budget, c->g_sel);
-    LAUNCH_CHECK("k_gq_select_bin");
     const int nstage = (n + kGqStage - 1) / kGqStage;
-    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_sel, c->g_stage, c->g_bcnt,
-                       action);
+    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_hist, budget, c->g_sel,
+                       c->g_stage, c->g_bcnt, action, slab);
     LAUNCH_CHECK("k_gq_compact");
-    hipLaunchKernelGGL(k_gq_gather, dim3(nstage), dim3(256), 0, st, c->g_stage, c->g_bcnt, c->g_sel, c->g_sorted + kGqCap);
+    hipLaunchKernelGGL(k_gq_gather, dim3(nstage), dim3(256), 0, st, c->g_stage, c->g_bcnt, c->g_sel, c->g_sorted + kGqCap,
+                       c->g_hist);
     LAUNCH_CHECK("k_gq_gather");
-    hipLaunchKernelGGL(k_gq_rank, dim3(kGqRankBlocks), dim3(kGqRankThreads), 0, st, c->g_sorted + kGqCap, c->g_sel, c->g_sorted);
+    hipLaunchKernelGGL(k_gq_rank, dim3(kGqRankBlocks), dim3(kGqRankThreads), 0, st, c->g_sorted + kGqCap, c->g_sel,
+                       c->g_sorted);
     LAUNCH_CHECK("k_gq_rank");
-    hipLaunchKernelGGL(k_gq_finish, dim3(1), dim3(1024), 0, st, c->kp, c->g_sorted, budget, pmin, c->g_sel, action,
-                       c->g_flag);
+    hipLaunchKernelGGL(k_gq_finish, dim3(1), dim3(1024), 0, st, c->kp, c->g_sorted, c->g_key, budget, pmin, c->g_sel,
+                       action, slab);
     LAUNCH_CHECK("k_gq_finish");
-    HIP_TRY(hipMemcpyAsync(c->h_gq_flag, c->g_flag, sizeof(int), hipMemcpyDeviceToHost, st));
-    HIP_TRY(hipStreamSynchronize(st));
-
-    if (!*c->h_gq_flag) return MDR_OK;
-    c->gq_fallbacks += 1;
+    c->counts_ready = true;
+    return MDR_OK;
   }
   hipLaunchKernelGGL(k_greedy_keys, dim3(blocks(n, 256)), dim3(256), 0, st, c->kp, c->g_key, c->g_idx);
   LAUNCH_CHECK("k_greedy_keys");
@@ -1204,12 +1246,20 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   hipLaunchKernelGGL(k_greedy_apply, dim3(blocks(n, 256)), dim3(256), 0, st, (int64_t)n, c->g_idx2,
                      c->g_kpos, c->g_extra, action);
   LAUNCH_CHECK("k_greedy_apply");
+  // the counts of these actions, as the histogram form leaves them
+  HIP_TRY(hipMemsetAsync(slab, 0, c->slab_len * sizeof(unsigned long long), st));
+  if (int rc2 = launch_counts(c, action, MDR_ACT_BUFFER, 0, nullptr, st)) return rc2;
+  c->counts_ready = true;
   return MDR_OK;
 }
 
 int mdr_greedy_fallbacks(mdr_ctx* c, uint64_t* count) {
   if (!c || !count) return fail(MDR_EARG, "mdr_greedy_fallbacks: null argument");
-  *count = c->gq_fallbacks;
+  *count = 0;
+  if (!c->g_sel) return MDR_OK;
+  unsigned char h[128];
+  HIP_TRY(hipMemcpy(h, c->g_sel, 128, hipMemcpyDeviceToHost));
+  *count = gq_fallbacks_of(h);
   return MDR_OK;
 }
 

@@ -85,6 +85,70 @@ __global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* 
   }
 }
 
+// ---- greedy selection state and key-histogram helpers (the k_gq_* kernels below; k_step_pipe
+// writes the keys in its GQ epilogue)
+struct GqSel {
+  double kmin, scale;            // this call's quantisation (the previous call's key range)
+  double nkmin, nscale;          // the range of this call's keys, for the next call
+  double base_tot;               // P of the houses before the window (exact for integer P)
+  unsigned long long base_cnt, total;
+  int sb, bstar, bend, all, overflow, more_after, ncand;
+  unsigned fallbacks;            // calls decided by k_gq_finish's exact fallback (diagnostics)
+};
+static_assert(sizeof(GqSel) <= 128, "GqSel fits the 128-B sel buffer");
+void gq_sel_init(void* sel128) {
+  GqSel* g = static_cast<GqSel*>(sel128);  // (a zeroed 128-B host buffer)
+  g->kmin = -32.0;
+  g->scale = (double)kGqBins / 64.0;
+}
+unsigned gq_fallbacks_of(const void* sel128) { return static_cast<const GqSel*>(sel128)->fallbacks; }
+
+constexpr int kGqSupN = kGqSuper + 1;  // superbins + one for NaN keys (sorted last, pandas' na_position)
+constexpr int kGqSupStride = kGqSupN * 4;
+
+// okey: -0.0 folded onto +0.0 (value order, numpy's stable argsort), sign-magnitude -> unsigned;
+// NaN after every number
+__device__ __forceinline__ uint64_t gq_okey(double k) {
+  if (k != k) return ~0ull;
+  const uint64_t b = (uint64_t)__double_as_longlong(k + 0.0);
+  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+}
+// monotone non-decreasing in k for ANY (kmin, scale >= 0) — keys outside the range clamp to the end
+// bins — so a stale range (the previous call's) only costs window size, never exactness
+__device__ __forceinline__ int gq_bin(double k, double kmin, double scale) {
+  const double d = (k - kmin) * scale;
+  return d >= (double)(kGqBins - 1) ? kGqBins - 1 : (d > 0.0 ? (int)d : 0);
+}
+__device__ __forceinline__ int gq_super(double k, double kmin, double scale) {
+  return k != k ? kGqSuper : gq_bin(k, kmin, scale) / (kGqBins / kGqSuper);
+}
+
+// the keys' producer side, shared by k_gq_keys and the step kernel's epilogue: a block's houses go
+// into per-wave LDS superbin histograms, then one flush per block (spread over kGqCopies copies)
+// and the block's (min, max) of the finite keys into part[]
+__device__ __forceinline__ void gq_flush(const unsigned* s_sh, int nw, unsigned* hist, double lo, double hi,
+                                         double* part) {
+  __shared__ double s_lo[16], s_hi[16];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, off));
+    hi = fmax(hi, __shfl_xor(hi, off));
+  }
+  if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double l = s_lo[0], h = s_hi[0];
+    for (int w = 1; w < nw; ++w) { l = fmin(l, s_lo[w]); h = fmax(h, s_hi[w]); }
+    part[2 * blockIdx.x] = l;
+    part[2 * blockIdx.x + 1] = h;
+  }
+  for (int e = threadIdx.x; e < kGqSupStride; e += blockDim.x) {
+    unsigned v = 0u;
+    for (int w = 0; w < nw; ++w) v += s_sh[w * kGqSupStride + e];
+    if (v) atomicAdd(&hist[kGqBins * 4 + (blockIdx.x % kGqCopies) * kGqSupStride + e], v);
+  }
+}
+
 // --------------------------------------------------------------------------------------- K1
 // Phase 2: fused FSM + RC thermal + reward (environment.py:86-101) for one tick, HPT houses per
 // thread (HPT = 2: 16-B-per-lane loads/stores of the fp64 SoA arrays, two independent fp64
@@ -366,17 +430,26 @@ __device__ __forceinline__ void load_tile2(const KParams& p, const uint8_t* acti
   }
 }
 
-template <int TPW, int ACT, int LA>
+// GQ: the greedy controller's keys of the post-step state, their superbin histogram and the
+// block's key range (k_gq_keys' outputs, gq_flush) as an epilogue, so the next mdr_ctrl_greedy
+// skips its key pass
+template <int TPW, int ACT, int LA, bool GQ>
 __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __restrict__ action, TickArgs tk0,
                                                    const TickArgs* tkp, const unsigned long long* __restrict__ counts,
                                                    double* __restrict__ reward, double* p_out,
-                                                   unsigned long long* next_slab, unsigned long long* zero_slab) {
+                                                   unsigned long long* next_slab, unsigned long long* zero_slab,
+                                                   GqOut gq) {
   constexpr int HPT = 2;
   constexpr bool AB = ACT == MDR_ACT_BUFFER;
   __shared__ unsigned hist[MDR_MAX_CAP];
+  __shared__ unsigned s_gq[GQ ? 4 * kGqSupStride : 1];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   if (tid < p.n_cap) hist[tid] = 0;
+  if (GQ)
+    for (int e = tid; e < 4 * kGqSupStride; e += blockDim.x) s_gq[e] = 0u;
+  double gq_lo = INFINITY, gq_hi = -INFINITY;
+  const double gq_kmin = GQ ? gq.sel->kmin : 0.0, gq_scale = GQ ? gq.sel->scale : 0.0;
   if (zero_slab && blockIdx.x == 0)
     for (int j = tid; j < kCountShards * p.n_cap; j += blockDim.x) zero_slab[j] = 0ull;
   const uint32_t n = (uint32_t)p.n;
@@ -397,7 +470,7 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
   auto full_tile = [&](uint32_t t) { return (t + 1u) * (64u * HPT) <= n; };
   Tile2 buf[2];
   if (gw < ntiles) load_tile2<AB>(p, action, gw * (64u * HPT) + (uint32_t)lane * HPT, n, full_tile(gw), buf[0]);
-  if (LA) __syncthreads();  // hist zeroed (a bare s_barrier: the tile loads stay in flight)
+  if (LA || GQ) __syncthreads();  // hist zeroed (a bare s_barrier: the tile loads stay in flight)
   const TickArgs tk = tkp ? *tkp : tk0;
   double sig_term = 0.0;
   if (counts) {
@@ -486,6 +559,21 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
       p.t_air[i0] = Tn[0]; p.t_mass[i0] = Tmn[0]; p.hvac[i0] = w[0];
       if (counts) reward[i0] = rw[0];
     }
+    if (GQ) {  // greedy_myopic_controller.py:79 on the post-step state
+      const double k0 = -(Tn[0] - tg[0]), k1 = -(Tn[1] - tg[1]);
+      if (valid[1]) sto(gq.key, i0 * 8u, make_double2(k0, k1));
+      else if (valid[0]) gq.key[i0] = k0;
+#pragma unroll
+      for (int h = 0; h < HPT; ++h) {
+        const double k = h ? k1 : k0;
+        if (!valid[h]) continue;
+        if (k == k) {
+          gq_lo = fmin(gq_lo, k);
+          gq_hi = fmax(gq_hi, k);
+        }
+        atomicAdd(&s_gq[(tid >> 6) * kGqSupStride + gq_super(k, gq_kmin, gq_scale) * 4 + (cls[h] & 3)], 1u);
+      }
+    }
     if (LA) {
 #pragma unroll
       for (int c = 0; c < kPipeCap; ++c)
@@ -503,6 +591,10 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
     __syncthreads();
     if (tid < p.n_cap && hist[tid])
       atomicAdd(&next_slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)hist[tid]);
+  }
+  if (GQ) {
+    __syncthreads();
+    gq_flush(s_gq, 4, gq.hist, gq_lo, gq_hi, gq.part);
   }
 }
 
@@ -1124,16 +1216,18 @@ MDR_INST_WIN(MDR_ACT_RANDOM)
 MDR_INST_WIN(MDR_ACT_ALWAYS_ON)
 MDR_INST_WIN(MDR_ACT_BUFFER)
 
-#define MDR_INST_PIPE(T, A, LA)                                                                    \
-  template __global__ void k_step_pipe<T, A, LA>(KParams, const uint8_t*, TickArgs, const TickArgs*, \
-                                                 const unsigned long long*, double*, double*,         \
-                                                 unsigned long long*, unsigned long long*);
-MDR_INST_PIPE(1, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
-MDR_INST_PIPE(2, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
-MDR_INST_PIPE(4, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
-MDR_INST_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM)
-MDR_INST_PIPE(2, MDR_ACT_BUFFER, 0)
-MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0)
+#define MDR_INST_PIPE(T, A, LA, G)                                                                    \
+  template __global__ void k_step_pipe<T, A, LA, G>(KParams, const uint8_t*, TickArgs, const TickArgs*, \
+                                                    const unsigned long long*, double*, double*,         \
+                                                    unsigned long long*, unsigned long long*, GqOut);
+MDR_INST_PIPE(1, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false)
+MDR_INST_PIPE(2, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false)
+MDR_INST_PIPE(4, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false)
+MDR_INST_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false)
+MDR_INST_PIPE(2, MDR_ACT_BUFFER, 0, false)
+MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0, false)
+MDR_INST_PIPE(2, MDR_ACT_BUFFER, 0, true)
+MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0, true)
 
 #define MDR_INST_STEP(F, A, LA)                                                                  \
   template __global__ void k_step_t<2, F, A, LA>(                                                \
@@ -1485,54 +1579,32 @@ __global__ void __launch_bounds__(256) k_greedy_walk(int64_t n, const double* __
   if (threadIdx.x == 0) { kpos[0] = s_k; kpos[1] = s_ne < max_extra ? s_ne : max_extra; }
 }
 
-// ---- histogram-select form (mdr_ctrl_greedy's default; the sort form above is its fallback).
+// ---- histogram-select form (mdr_ctrl_greedy for <= 4 capacity classes; the sort form above
+// serves wider capacity tables and the all-gathered sharded rows).
 // Only the houses around the budget crossing need an order: houses are binned by a monotone
 // linear quantisation of the key over [kmin, kmax] (kGqBins bins, class counts per bin), the bin
 // b* where the cumulative P crosses S is found from the bin sums, every house in a lower bin is
 // taken, and only the houses of bins [b*, b_end] (at most kGqCap, with >= kGqAfter houses past
-// b*) are ordered — by (key value, house), as the stable sort orders them — in one workgroup's
-// LDS, where the exact crossing position and the gap walk are evaluated.  Sums of P are exact
-// for integer P (every sum of P here is).  Inputs the candidate window cannot decide (NaN keys,
-// a crossing bin over kGqCap houses, a walk that leaves the window) raise sel.overflow and the
-// host reruns the sort form.
-struct GqSel {
-  double kmin, scale, base_tot;  // (kmin, scale): this call's quantisation (the previous call's key range)
-  unsigned long long base_cnt, total;
-  int bstar, bend, all, overflow, more_after, ncand, sb;
-  double nkmin, nscale;          // the range of this call's keys, for the next call
-};
-static_assert(sizeof(GqSel) <= 128, "GqSel fits the 128-B sel buffer");
-void gq_sel_init(void* sel128) {
-  GqSel* g = static_cast<GqSel*>(sel128);  // (a zeroed 128-B host buffer)
-  g->kmin = -32.0;
-  g->scale = (double)kGqBins / 64.0;
-}
-
-// okey: -0.0 folded onto +0.0 (value order, numpy's stable argsort), sign-magnitude -> unsigned
-__device__ __forceinline__ uint64_t gq_okey(double k) {
-  const uint64_t b = (uint64_t)__double_as_longlong(k + 0.0);
-  return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
-}
-// monotone non-decreasing in k for ANY (kmin, scale >= 0) — keys outside the range clamp to the end
-// bins — so a stale range (the previous call's) only costs window size, never exactness
-__device__ __forceinline__ int gq_bin(double k, double kmin, double scale) {
-  const double d = (k - kmin) * scale;
-  return d >= (double)(kGqBins - 1) ? kGqBins - 1 : (d > 0.0 ? (int)d : 0);
-}
-
+// b*) are ordered — by (key value, house), as the stable sort orders them — in LDS, where the exact
+// crossing position and the gap walk are evaluated.  Sums of P are exact for integer P (every sum
+// of P here is).  What the candidate window cannot decide (a crossing among NaN keys, a crossing
+// bin over kGqCap houses — e.g. thousands of identical keys —, a walk that leaves the window) the
+// last kernel decides itself, in the same launch, with an exact radix select over the 96-bit
+// (key, house) order (k_gq_finish's fallback): no host synchronisation, no sort, every tick.
+// The launches of one decision: [keys: k_gq_keys, or the previous step kernel's epilogue] ->
+// k_gq_bins -> k_gq_compact -> k_gq_gather -> k_gq_rank -> k_gq_finish; compact and finish also
+// count the ON houses the decided actions produce (the next step's cluster power).
 // K1: keys, per-block (min, max) of the finite keys (the next call's range), and the class counts
-// per superbin (kGqBins / kGqSuper consecutive bins) under this call's quantisation; a NaN key
-// raises the overflow flag
+// per superbin (kGqBins / kGqSuper consecutive bins; NaN keys in their own) under this call's
+// quantisation
 __global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, double* __restrict__ key, double* __restrict__ part,
-                                                        unsigned* __restrict__ hist, GqSel* __restrict__ sel) {
+                                                        unsigned* __restrict__ hist, const GqSel* __restrict__ sel) {
   constexpr int NW = kGqThreads / 64;
-  __shared__ unsigned s_sh[NW][kGqSuper * 4];  // one copy per wave (less atomic contention on hot superbins)
-  __shared__ double s_lo[NW], s_hi[NW];
-  for (int e = threadIdx.x; e < NW * kGqSuper * 4; e += blockDim.x) (&s_sh[0][0])[e] = 0u;
+  __shared__ unsigned s_sh[NW * kGqSupStride];  // one copy per wave (less atomic contention on hot superbins)
+  for (int e = threadIdx.x; e < NW * kGqSupStride; e += blockDim.x) s_sh[e] = 0u;
   __syncthreads();
   const double kmin = sel->kmin, scale = sel->scale;
   double lo = INFINITY, hi = -INFINITY;
-  bool nan = false;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   // kGqUnroll houses per thread per pass, every load issued before the first use (the grid is one
   // block per CU: without the batch each pass waits out a full HBM latency)
@@ -1550,77 +1622,23 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, double* __res
     for (int u = 0; u < kGqUnroll; ++u) {
       const int64_t i = i0 + u * stride;
       if (i >= p.n) break;
-      const double k = -(ta[u] - tg[u]);
+      const double k = -(ta[u] - tg[u]);  // greedy_myopic_controller.py:79
       key[i] = k;
-      if (k != k) { nan = true; continue; }
-      lo = fmin(lo, k);
-      hi = fmax(hi, k);
-      atomicAdd(&s_sh[threadIdx.x >> 6][(gq_bin(k, kmin, scale) / (kGqBins / kGqSuper)) * 4 + (cl[u] & 3u)], 1u);
+      if (k == k) {
+        lo = fmin(lo, k);
+        hi = fmax(hi, k);
+      }
+      atomicAdd(&s_sh[(threadIdx.x >> 6) * kGqSupStride + gq_super(k, kmin, scale) * 4 + (cl[u] & 3u)], 1u);
     }
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    lo = fmin(lo, __shfl_xor(lo, off));
-    hi = fmax(hi, __shfl_xor(hi, off));
-  }
-  if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
-  if (__any(nan) && (threadIdx.x & 63) == 0) sel->overflow = 1;
   __syncthreads();
-  if (threadIdx.x == 0) {
-    double l = s_lo[0], h = s_hi[0];
-    for (int w = 1; w < NW; ++w) { l = fmin(l, s_lo[w]); h = fmax(h, s_hi[w]); }
-    part[2 * blockIdx.x] = l;
-    part[2 * blockIdx.x + 1] = h;
-  }
-  for (int e = threadIdx.x; e < kGqSuper * 4; e += blockDim.x) {
-    unsigned v = 0u;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) v += s_sh[w][e];
-    if (v) atomicAdd(&hist[kGqBins * 4 + (blockIdx.x % kGqCopies) * (kGqSuper * 4) + e], v);  // (kGqCopies copies: fewer atomics per address)
-  }
+  gq_flush(s_sh, NW, hist, lo, hi, part);
 }
 
-// K3a (one workgroup, thread t = superbin t): the superbin where the cumulative P crosses S, the P
-// and house count before it (sums of P: exact for integer P); zeroes the superbin histogram
-__global__ void __launch_bounds__(256) k_gq_select_super(KParams p, unsigned* __restrict__ hist, double S,
-                                                         const double* __restrict__ part, int nparts,
-                                                         GqSel* __restrict__ sel) {
-  static_assert(kGqSuper == 256, "one superbin per thread");
-  __shared__ double s_w[4], s_lo[4], s_hi[4];
-  {  // the next call's range: (min, max) of this call's keys
-    double lo = INFINITY, hi = -INFINITY;
-    for (int b = threadIdx.x; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      lo = fmin(lo, __shfl_xor(lo, off));
-      hi = fmax(hi, __shfl_xor(hi, off));
-    }
-    if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      const double kmin = fmin(fmin(s_lo[0], s_lo[1]), fmin(s_lo[2], s_lo[3]));
-      const double kmax = fmax(fmax(s_hi[0], s_hi[1]), fmax(s_hi[2], s_hi[3]));
-      const double range = kmax - kmin;
-      sel->nkmin = kmin == kmin && kmin < INFINITY ? kmin : 0.0;
-      sel->nscale = range > 0.0 && range < INFINITY ? (double)kGqBins / range : 0.0;
-    }
-  }
-  __shared__ unsigned long long s_wc[4];
-  __shared__ int s_first;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  double p_on[kWinCap];
-#pragma unroll
-  for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
-  unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
-#pragma unroll
-  for (int q = 0; q < kGqCopies; ++q) {  // (the copies k_gq_keys spread its atomics over; zeroed below)
-    const uint4 v = *reinterpret_cast<const uint4*>(hist + kGqBins * 4 + q * (kGqSuper * 4) + tid * 4);
-    c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] += v.w;
-  }
-  const double ps = win_power(p, c, p_on);
-  const unsigned long long cs = c[0] + c[1] + c[2] + c[3];
-  double x = ps;
-  unsigned long long xc = cs;
+// a block-wide inclusive scan of (double P, u64 count) over the first n <= blockDim.x threads
+// (wave shuffles, then the wave totals through LDS); returns the inclusive values
+__device__ __forceinline__ void gq_block_scan(double& x, unsigned long long& xc, double* s_w, unsigned long long* s_wc) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
     const double y = __shfl_up(x, off);
@@ -1628,53 +1646,98 @@ __global__ void __launch_bounds__(256) k_gq_select_super(KParams p, unsigned* __
     if (lane >= off) { x += y; xc += yc; }
   }
   if (lane == 63) { s_w[wv] = x; s_wc[wv] = xc; }
-  if (tid == 0) s_first = kGqSuper;
   __syncthreads();
-  double before = x - ps;
-  unsigned long long beforec = xc - cs;
-  for (int w = 0; w < wv; ++w) { before += s_w[w]; beforec += s_wc[w]; }
-  if (cs > 0 && !(before + ps < S)) atomicMin(&s_first, tid);  // (the first position: a non-empty superbin)
-  __syncthreads();
-  if (tid == s_first) { sel->base_tot = before; sel->base_cnt = beforec; }
-  if (tid == 0) {
-    sel->sb = s_first;
-    sel->all = s_first >= kGqSuper;
-    sel->total = s_wc[0] + s_wc[1] + s_wc[2] + s_wc[3];
-  }
-#pragma unroll
-  for (int q = 0; q < kGqCopies; ++q)
-    *reinterpret_cast<uint4*>(hist + kGqBins * 4 + q * (kGqSuper * 4) + tid * 4) = make_uint4(0u, 0u, 0u, 0u);
+  for (int w = 0; w < wv; ++w) { x += s_w[w]; xc += s_wc[w]; }  // (fixed order: the same sums in every block)
 }
 
-// K2b: class counts of the bins of superbins sb and sb + 1 (the crossing superbin and the room
-// after it), from the houses in them only
+// K2: every block first finds the crossing superbin itself (the cumulative P where it reaches S;
+// the same arithmetic in every block, so every block agrees), block 0 records it and the next
+// call's key range and zeroes the current count slab (compact and finish fill it); then the class
+// counts of the bins of superbins sb and sb + 1 (the crossing superbin and the room after it)
 __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const double* __restrict__ key,
-                                                        unsigned* __restrict__ hist, const GqSel* __restrict__ sel) {
+                                                        unsigned* __restrict__ hist, const double* __restrict__ part,
+                                                        int nparts, double S, GqSel* __restrict__ sel,
+                                                        unsigned long long* __restrict__ slab) {
   constexpr int NB = 2 * (kGqBins / kGqSuper), NW = kGqThreads / 64;
+  static_assert(kGqSupN <= kGqThreads, "one superbin per thread");
   __shared__ unsigned s_h[NW][NB * 4];
-  if (sel->all || sel->overflow) return;
-  for (int e = threadIdx.x; e < NW * NB * 4; e += blockDim.x) (&s_h[0][0])[e] = 0u;
+  __shared__ double s_w[NW];
+  __shared__ unsigned long long s_wc[NW];
+  __shared__ int s_first;
+  const int tid = threadIdx.x;
+  double p_on[kWinCap];
+#pragma unroll
+  for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
+  unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
+  if (tid < kGqSupN)
+#pragma unroll
+    for (int q = 0; q < kGqCopies; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4*>(hist + kGqBins * 4 + q * kGqSupStride + tid * 4);
+      c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] += v.w;
+    }
+  const double ps = win_power(p, c, p_on);
+  const unsigned long long cs = c[0] + c[1] + c[2] + c[3];
+  double x = ps;
+  unsigned long long xc = cs;
+  if (tid == 0) s_first = kGqSupN;
+  gq_block_scan(x, xc, s_w, s_wc);
+  const double before = x - ps;
+  if (tid < kGqSupN && cs > 0 && !(before + ps < S)) atomicMin(&s_first, tid);  // (the first: a non-empty superbin)
   __syncthreads();
-  const int bb = sel->sb * (kGqBins / kGqSuper);
+  const int sb = s_first;
+  if (blockIdx.x == 0) {
+    if (tid == sb) { sel->base_tot = before; sel->base_cnt = xc - cs; }
+    if (tid == kGqSupN - 1) sel->total = xc;
+    if (tid == 0) {
+      sel->sb = sb;
+      sel->all = sb >= kGqSupN;
+      sel->overflow = sb == kGqSuper;  // the crossing among NaN keys: the fallback orders them by house
+    }
+    // the next call's range: (min, max) of this call's finite keys
+    double lo = INFINITY, hi = -INFINITY;
+    for (int b = tid; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) {
+      lo = fmin(lo, __shfl_xor(lo, off));
+      hi = fmax(hi, __shfl_xor(hi, off));
+    }
+    __shared__ double s_lo[NW], s_hi[NW];
+    if ((tid & 63) == 0) { s_lo[tid >> 6] = lo; s_hi[tid >> 6] = hi; }
+    __syncthreads();
+    if (tid == 0) {
+      double kmin = s_lo[0], kmax = s_hi[0];
+      for (int w = 1; w < NW; ++w) { kmin = fmin(kmin, s_lo[w]); kmax = fmax(kmax, s_hi[w]); }
+      const double range = kmax - kmin;
+      sel->nkmin = kmin == kmin && kmin < INFINITY ? kmin : 0.0;
+      sel->nscale = range > 0.0 && range < INFINITY ? (double)kGqBins / range : 0.0;
+    }
+    for (int e = tid; e < kCountShards * p.n_cap; e += blockDim.x) slab[e] = 0ull;
+  }
+  if (sb >= kGqSuper) return;  // everything taken, or a NaN crossing (block-uniform)
+  for (int e = tid; e < NW * NB * 4; e += blockDim.x) (&s_h[0][0])[e] = 0u;
+  __syncthreads();
+  const int bb = sb * (kGqBins / kGqSuper);
   const double kmin = sel->kmin, scale = sel->scale;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < p.n; i0 += kGqUnroll * stride) {
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + tid; i0 < p.n; i0 += kGqUnroll * stride) {
     double kk[kGqUnroll];
+    unsigned cl[kGqUnroll];
 #pragma unroll
     for (int u = 0; u < kGqUnroll; ++u) {
       const int64_t i = i0 + u * stride;
       kk[u] = i < p.n ? key[i] : NAN;
+      cl[u] = i < p.n ? p.cap_idx[i] : 0u;
     }
 #pragma unroll
     for (int u = 0; u < kGqUnroll; ++u) {
       const double k = kk[u];
       if (k != k) continue;
       const int b = gq_bin(k, kmin, scale) - bb;
-      if (b >= 0 && b < NB) atomicAdd(&s_h[threadIdx.x >> 6][b * 4 + (p.cap_idx[i0 + u * stride] & 3u)], 1u);
+      if (b >= 0 && b < NB) atomicAdd(&s_h[tid >> 6][b * 4 + (cl[u] & 3u)], 1u);
     }
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < NB * 4; e += blockDim.x) {
+  for (int e = tid; e < NB * 4; e += blockDim.x) {
     unsigned v = 0u;
 #pragma unroll
     for (int w = 0; w < NW; ++w) v += s_h[w][e];
@@ -1682,52 +1745,68 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const double*
   }
 }
 
-// K3b (one wave per 64 bins: 128 threads): the crossing bin inside superbin sb (lane l = its bin l),
-// the candidate window [b*, b_end] over the next 64 bins; zeroes the bin histogram
-__global__ void __launch_bounds__(128) k_gq_select_bin(KParams p, unsigned* __restrict__ hist, double S,
-                                                       GqSel* __restrict__ sel) {
+// K3: every block finds the crossing bin inside superbin sb (lane l = its bin l) and the candidate
+// window [b*, b_end] over the next 64 bins (the same arithmetic in every block; block 0 records it
+// and zeroes the superbin histograms); then every house of a bin below b* is taken, the rest start
+// as not taken (k_gq_finish sets the window's), the window's houses are staged per block of
+// kGqStage houses (okey, house << 2 | class, FSM word), and the ON houses of the decided (non-
+// window) houses are counted into the slab
+__global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const double* __restrict__ key,
+                                                           unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
+                                                           uint4* __restrict__ stage, unsigned* __restrict__ bcnt,
+                                                           uint8_t* __restrict__ action,
+                                                           unsigned long long* __restrict__ slab) {
   static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
   static_assert(kGqCopies * 512 <= kGqBins * 4, "the bin copies fit below the superbin copies");
   __shared__ unsigned s_c[128];
-  __shared__ int s_l0;
+  __shared__ int s_l0, s_le, s_n;
   __shared__ double s_base;
   __shared__ unsigned long long s_basec;
+  __shared__ unsigned s_cnt[kWinCap];
   const int tid = threadIdx.x, lane = tid & 63;
-  const bool on = !sel->all && !sel->overflow;
+  const bool all = sel->all, ovf = sel->overflow;
+  const bool on = !all && !ovf;
   const int bb = sel->sb * 64;
-  double p_on[kWinCap];
+  if (tid < kWinCap) s_cnt[tid] = 0u;
+  if (tid == 0) { s_n = 0; s_l0 = 0; s_le = 0; }
+  if (blockIdx.x == 0)  // (k_gq_bins read them; the next producer fills them again)
+    for (int e = tid; e < kGqCopies * kGqSupStride; e += blockDim.x) hist[kGqBins * 4 + e] = 0u;
+  if (on && tid < 128) {
+    double p_on[kWinCap];
 #pragma unroll
-  for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
-  unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
+    for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
+    unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
 #pragma unroll
-  for (int q = 0; q < kGqCopies; ++q) {  // (k_gq_bins' copies, 128 bins x 4 classes each; zeroed below)
-    const uint4 v = *reinterpret_cast<const uint4*>(hist + q * 512 + tid * 4);
-    c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] += v.w;
-  }
-  s_c[tid] = (unsigned)(c[0] + c[1] + c[2] + c[3]);
-  if (tid < 64 && on) {  // wave 0: the crossing bin of superbin sb (it crosses: K3a)
-    const double pb = win_power(p, c, p_on);
-    const unsigned long long cb = c[0] + c[1] + c[2] + c[3];
-    double xb = pb;
-    unsigned long long xcb = cb;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double y = __shfl_up(xb, off);
-      const unsigned long long yc = __shfl_up(xcb, off);
-      if (lane >= off) { xb += y; xcb += yc; }
+    for (int q = 0; q < kGqCopies; ++q) {  // (k_gq_bins' copies, 128 bins x 4 classes each)
+      const uint4 v = *reinterpret_cast<const uint4*>(hist + q * 512 + tid * 4);
+      c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] += v.w;
     }
-    const double bef = sel->base_tot + (xb - pb);
-    const unsigned long long befc = sel->base_cnt + (xcb - cb);
-    const unsigned long long m = __ballot(cb > 0 && !(bef + pb < S));
-    const int l0 = m ? __ffsll((long long)m) - 1 : 63;
-    if (lane == l0) { s_l0 = l0; s_base = bef; s_basec = befc; }
+    s_c[tid] = (unsigned)(c[0] + c[1] + c[2] + c[3]);
+    if (tid < 64) {  // wave 0: the crossing bin of superbin sb (it crosses: k_gq_bins)
+      const double pb = win_power(p, c, p_on);
+      const unsigned long long cb = c[0] + c[1] + c[2] + c[3];
+      double xb = pb;
+      unsigned long long xcb = cb;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const double y = __shfl_up(xb, off);
+        const unsigned long long yc = __shfl_up(xcb, off);
+        if (lane >= off) { xb += y; xcb += yc; }
+      }
+      const double bef = sel->base_tot + (xb - pb);
+      const unsigned long long befc = sel->base_cnt + (xcb - cb);
+      const unsigned long long m = __ballot(cb > 0 && !(bef + pb < S));
+      const int l0 = m ? __ffsll((long long)m) - 1 : 63;
+      if (lane == l0) { s_l0 = l0; s_base = bef; s_basec = befc; }
+    }
   }
   __syncthreads();
-  if (tid < 64 && on) {  // the window: bins l0 .. l0 + 63 of the 128 loaded
+  bool wovf = false;
+  if (on && tid < 64) {  // the window: bins l0 .. l0 + 63 of the 128 loaded
     const int l0 = s_l0;
     const int li = l0 + lane;
-    const unsigned long long c2 = li < 128 && bb + li < kGqBins ? s_c[li] : 0ull;
     const bool valid = li < 128 && bb + li < kGqBins;
+    const unsigned long long c2 = valid ? s_c[li] : 0ull;
     unsigned long long pre = c2;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
@@ -1742,8 +1821,10 @@ __global__ void __launch_bounds__(128) k_gq_select_bin(KParams p, unsigned* __re
     else if (enough) le = __ffsll((long long)enough) - 1;
     else le = 63 - __clzll((long long)fit);
     const int cnt = (int)__shfl(pre, le);
-    if (lane == 0) {
-      if (!(fit & 1ull)) sel->overflow = 1;
+    wovf = !(fit & 1ull);
+    if (lane == 0) s_le = wovf ? -1 : le;
+    if (lane == 0 && blockIdx.x == 0) {
+      if (wovf) sel->overflow = 1;
       sel->bstar = bb + l0;
       sel->bend = bb + l0 + le;
       sel->base_tot = s_base;
@@ -1751,46 +1832,54 @@ __global__ void __launch_bounds__(128) k_gq_select_bin(KParams p, unsigned* __re
       sel->ncand = cnt;
     }
   }
-#pragma unroll
-  for (int q = 0; q < kGqCopies; ++q) *reinterpret_cast<uint4*>(hist + q * 512 + tid * 4) = make_uint4(0u, 0u, 0u, 0u);
-}
-
-// K4: every house of a bin below b* is taken, the rest start as not taken (K5c sets the window's);
-// the window's houses are staged per block of kGqStage houses (okey, house << 2 | class, lock)
-__global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const double* __restrict__ key,
-                                                    const GqSel* __restrict__ sel, uint4* __restrict__ stage,
-                                                    unsigned* __restrict__ bcnt, uint8_t* __restrict__ action) {
-  __shared__ unsigned s_n;
-  if (threadIdx.x == 0) s_n = 0u;
   __syncthreads();
-  const bool all = sel->all, on = !all && !sel->overflow;
-  const int bs = sel->bstar, be = sel->bend;
+  if (ovf || s_le < 0) {  // the fallback in k_gq_finish decides every house (block-uniform)
+    if (tid == 0) bcnt[blockIdx.x] = 0u;
+    return;
+  }
+  const int bs = bb + s_l0, be = bb + s_l0 + s_le;
   const double kmin = sel->kmin, scale = sel->scale;
   const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
   constexpr int U = kGqStage / kGqThreads;
   double kk[U];
+  uint32_t hw[U];
+  unsigned cl[U];
 #pragma unroll
   for (int u = 0; u < U; ++u) {  // (every load before the first use)
-    const int64_t i = b0 + u * kGqThreads + threadIdx.x;
+    const int64_t i = b0 + u * kGqThreads + tid;
     kk[u] = i < p.n ? key[i] : 0.0;
+    hw[u] = i < p.n ? p.hvac[i] : 0u;
+    cl[u] = i < p.n ? p.cap_idx[i] : 0u;
   }
-  {
+  unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int64_t i = b0 + u * kGqThreads + threadIdx.x;
-      if (i >= p.n) break;
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = b0 + u * kGqThreads + tid;
+    bool dec = false, take = false;  // dec: decided here (outside the window)
+    if (i < p.n) {
       const double k = kk[u];
       const int b = k == k ? gq_bin(k, kmin, scale) : kGqBins;
-      action[i] = all || b < bs ? 1 : 0;
-      if (!on || b < bs || b > be) continue;
-      const unsigned slot = atomicAdd(&s_n, 1u);
-      const uint64_t ok = gq_okey(k);
-      stage[b0 + slot] = make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), ((uint32_t)i << 2) | (p.cap_idx[i] & 3u),
-                                    hv_lock(p.hvac[i]) ? 1u : 0u);
+      take = all || b < bs;
+      action[i] = take ? 1 : 0;
+      dec = all || b < bs || b > be;
+      if (!dec) {
+        const unsigned slot = atomicAdd(&s_n, 1u);
+        const uint64_t ok = gq_okey(k);
+        stage[b0 + slot] = make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), ((uint32_t)i << 2) | (cl[u] & 3u), hw[u]);
+      }
     }
+    const bool on1 = dec && hv_on(hvac_fsm(hw[u], take, p.dt, p.L));
+#pragma unroll
+    for (int c = 0; c < kWinCap; ++c) oncnt[c] += (unsigned)__popcll(__ballot(on1 && (cl[u] & 3u) == (unsigned)c));
   }
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < kWinCap; ++c)
+      if (oncnt[c]) atomicAdd(&s_cnt[c], oncnt[c]);
   __syncthreads();
-  if (threadIdx.x == 0) bcnt[blockIdx.x] = on ? s_n : 0u;
+  if (tid == 0) bcnt[blockIdx.x] = s_n;
+  if (tid < p.n_cap && s_cnt[tid])
+    atomicAdd(&slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)s_cnt[tid]);
 }
 
 __device__ __forceinline__ bool gq_less(const uint4& a, const uint4& b) {
@@ -1798,13 +1887,17 @@ __device__ __forceinline__ bool gq_less(const uint4& a, const uint4& b) {
   return ka < kb || (ka == kb && a.z < b.z);  // (z = house << 2 | class: house order on equal keys)
 }
 
-// K5a: stage block b copies its window houses to win[offset_b ..) (offset_b: the counts of the
-// stage blocks before it), so the window becomes one contiguous array
+// K4: stage block b copies its window houses to win[offset_b ..) (offset_b: the counts of the
+// stage blocks before it), so the window becomes one contiguous array; block 0 zeroes the bin
+// histograms (k_gq_compact read them)
 __global__ void __launch_bounds__(256) k_gq_gather(const uint4* __restrict__ stage, const unsigned* __restrict__ bcnt,
-                                                   const GqSel* __restrict__ sel, uint4* __restrict__ win) {
+                                                   const GqSel* __restrict__ sel, uint4* __restrict__ win,
+                                                   unsigned* __restrict__ hist) {
   __shared__ unsigned s_w[4];
-  if (sel->all || sel->overflow) return;
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (b == 0)
+    for (int e = tid; e < kGqCopies * 512; e += blockDim.x) hist[e] = 0u;
+  if (sel->all || sel->overflow) return;
   const unsigned c = bcnt[b];
   if (c == 0u) return;  // (block-uniform)
   unsigned o = 0;
@@ -1817,7 +1910,7 @@ __global__ void __launch_bounds__(256) k_gq_gather(const uint4* __restrict__ sta
   for (unsigned e = tid; e < c; e += blockDim.x) win[o + e] = stage[(int64_t)b * kGqStage + e];
 }
 
-// K5b (kGqRankBlocks workgroups): the window into LDS; one wave per house computes its rank (how
+// K5 (kGqRankBlocks workgroups): the window into LDS; one wave per house computes its rank (how
 // many window houses precede it in (key, house) order, the lanes splitting the comparisons) and
 // writes it to sorted[rank]
 __global__ void __launch_bounds__(kGqRankThreads) k_gq_rank(const uint4* __restrict__ win, const GqSel* __restrict__ sel,
@@ -1870,16 +1963,189 @@ __global__ void __launch_bounds__(kGqRankThreads) k_gq_rank(const uint4* __restr
   }
 }
 
-// K5c (one workgroup of 1024): the sorted window into LDS, the exact crossing position from
-// base_tot, the window's prefix taken, then the gap walk (k_greedy_walk's rule)
-__global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __restrict__ sorted, double S,
-                                                    double pmin, GqSel* __restrict__ sel,
-                                                    uint8_t* __restrict__ action, int* __restrict__ flag) {
+// the greedy take rule at one house (greedy_myopic_controller.py:93-101)
+__device__ __forceinline__ bool gq_take(double pj, double tot, double S, bool lock) {
+  return (pj + tot < S) || (fabs(pj + tot - S) < fabs(tot - S) && !lock);
+}
+// the walk is over once no class can be taken (P > 0: nothing once tot >= S; with gap g = S - tot a
+// house needs P < 2g — a conservative margin, the exact rule decides)
+__device__ __forceinline__ bool gq_walk_over(double tot, double S, double pmin) {
+  return !(tot < S) || 2.0 * (S - tot) < pmin * (1.0 - 1e-9);
+}
+
+// 96-bit (okey, house) order for the exact fallback
+struct GqKey {
+  uint64_t k;
+  uint32_t h;
+};
+__device__ __forceinline__ bool gq_key_less(const GqKey& a, const GqKey& b) {
+  return a.k < b.k || (a.k == b.k && a.h < b.h);
+}
+// digit L (0 = most significant) of the 96-bit key, 8 bits each
+__device__ __forceinline__ unsigned gq_digit(const GqKey& c, int L) {
+  return L < 8 ? (unsigned)(c.k >> (56 - 8 * L)) & 0xFFu : (c.h >> (24 - 8 * (L - 8))) & 0xFFu;
+}
+// the top 8L bits of the key equal those of the prefix
+__device__ __forceinline__ bool gq_prefix_eq(const GqKey& c, const GqKey& pre, int L) {
+  if (L == 0) return true;
+  if (L <= 8) {
+    const int sh = 64 - 8 * L;
+    return sh == 0 ? c.k == pre.k : (c.k >> sh) == (pre.k >> sh);
+  }
+  const int sh = 32 - 8 * (L - 8);
+  return c.k == pre.k && (c.h >> sh) == (pre.h >> sh);
+}
+
+// The exact decision of the whole cluster by one workgroup, for what the window cannot decide:
+// (1) the crossing house k (the first position where the cumulative P of the (key, house) order
+// reaches S) by a radix select over the 96-bit key, 12 passes of 8 bits over all houses with class
+// counts (exact P); (2) the gap walk from k: each pass takes the first house after the current one
+// that the take rule admits (the houses in between fail it, and a failing house changes nothing),
+// until the gap admits no class; (3) every house's action and the ON counts of the decided actions.
+// ~15 passes over the keys by one CU: milliseconds, for inputs the window form cannot take (a NaN
+// crossing, a crossing bin of more than kGqCap houses, a walk past the window).
+__device__ void gq_exact(const KParams& p, const double* __restrict__ key, double S, double pmin,
+                         uint8_t* __restrict__ action, unsigned long long* __restrict__ slab) {
+  __shared__ unsigned s_h[256 * 4];
+  __shared__ double s_w[16];
+  __shared__ unsigned long long s_wc[16];
+  __shared__ int s_d;
+  __shared__ double s_base;
+  __shared__ GqKey s_best[16];
+  __shared__ int s_ntake, s_all;
+  __shared__ uint32_t s_take[64];
+  __shared__ unsigned s_cnt[kWinCap];
+  const int tid = threadIdx.x, nth = blockDim.x, lane = tid & 63, wv = tid >> 6;
+  const int64_t n = p.n;
+  double p_on[kWinCap];
+#pragma unroll
+  for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
+  auto key_of = [&](int64_t i) { return GqKey{gq_okey(key[i]), (uint32_t)i}; };
+  GqKey pre{0ull, 0u};
+  double base = 0.0;
+  if (tid == 0) { s_all = 0; s_ntake = 0; }
+  for (int L = 0; L < 12; ++L) {
+    for (int e = tid; e < 256 * 4; e += nth) s_h[e] = 0u;
+    __syncthreads();
+    for (int64_t i = tid; i < n; i += nth) {
+      const GqKey c = key_of(i);
+      if (gq_prefix_eq(c, pre, L)) atomicAdd(&s_h[gq_digit(c, L) * 4 + (p.cap_idx[i] & 3u)], 1u);
+    }
+    __syncthreads();
+    unsigned long long c4[kWinCap] = {0ull, 0ull, 0ull, 0ull};
+    if (tid < 256)
+#pragma unroll
+      for (int k = 0; k < kWinCap; ++k) c4[k] = s_h[tid * 4 + k];
+    const double pd = win_power(p, c4, p_on);
+    const unsigned long long cd = c4[0] + c4[1] + c4[2] + c4[3];
+    double x = pd;
+    unsigned long long xc = cd;
+    if (tid == 0) s_d = 256;
+    gq_block_scan(x, xc, s_w, s_wc);
+    if (tid < 256 && cd > 0 && !(base + (x - pd) + pd < S)) atomicMin(&s_d, tid);
+    __syncthreads();
+    const int d = s_d;
+    if (d >= 256) {  // (L = 0 only: the whole cluster's P stays below S) everything is taken
+      if (tid == 0) s_all = 1;
+      break;
+    }
+    if (tid == d) s_base = base + (x - pd);
+    __syncthreads();
+    base = s_base;
+    if (L < 8) pre.k |= (uint64_t)d << (56 - 8 * L);
+    else pre.h |= (uint32_t)d << (24 - 8 * (L - 8));
+    __syncthreads();  // (s_d / s_base reused by the next level)
+  }
+  const bool all = s_all != 0;
+  // (2) the walk from the crossing house pre (its own take first)
+  if (!all) {
+    double tot = base;
+    GqKey cur = pre;
+    bool first = true;
+    for (int guard = 0; guard < 64; ++guard) {
+      if (gq_walk_over(tot, S, pmin)) break;
+      GqKey best{~0ull, ~0u};
+      bool found = false;
+      if (first) {
+        const int64_t i = pre.h;
+        found = gq_take(p_on[p.cap_idx[i] & 3u], tot, S, hv_lock(p.hvac[i]));
+        best = pre;
+      } else {
+        for (int64_t i = tid; i < n; i += nth) {
+          const GqKey c = key_of(i);
+          if (!gq_key_less(cur, c)) continue;
+          if (!gq_take(p_on[p.cap_idx[i] & 3u], tot, S, hv_lock(p.hvac[i]))) continue;
+          if (gq_key_less(c, best)) best = c;
+        }
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+          const GqKey o{(uint64_t)__shfl_xor((long long)best.k, off), (uint32_t)__shfl_xor((int)best.h, off)};
+          if (gq_key_less(o, best)) best = o;
+        }
+        if (lane == 0) s_best[wv] = best;
+        __syncthreads();
+        best = s_best[0];
+        for (int w = 1; w < (nth >> 6); ++w)
+          if (gq_key_less(s_best[w], best)) best = s_best[w];
+        __syncthreads();
+        found = best.k != ~0ull || best.h != ~0u;
+      }
+      if (found) {
+        if (tid == 0) s_take[s_ntake] = best.h;
+        tot += p_on[p.cap_idx[best.h] & 3u];
+        __syncthreads();
+        if (tid == 0) s_ntake += 1;
+        cur = best;
+      } else if (!first) {
+        break;  // no house after cur is admitted
+      }
+      first = false;
+      __syncthreads();
+    }
+  }
+  // (3) every house's action and the ON counts of the decided actions
+  if (tid < kWinCap) s_cnt[tid] = 0u;
+  for (int e = tid; e < kCountShards * p.n_cap; e += nth) slab[e] = 0ull;
+  __syncthreads();
+  const int ntake = s_ntake;
+  unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
+  for (int64_t i0 = 0; i0 < n; i0 += nth) {
+    const int64_t i = i0 + tid;
+    bool on1 = false;
+    unsigned cl = 0u;
+    if (i < n) {
+      bool take = all || gq_key_less(key_of(i), pre);
+      for (int t = 0; t < ntake; ++t) take = take || s_take[t] == (uint32_t)i;
+      action[i] = take ? 1 : 0;
+      cl = p.cap_idx[i] & 3u;
+      on1 = hv_on(hvac_fsm(p.hvac[i], take, p.dt, p.L));
+    }
+#pragma unroll
+    for (int c = 0; c < kWinCap; ++c) oncnt[c] += (unsigned)__popcll(__ballot(on1 && cl == (unsigned)c));
+  }
+  if (lane == 0)
+#pragma unroll
+    for (int c = 0; c < kWinCap; ++c)
+      if (oncnt[c]) atomicAdd(&s_cnt[c], oncnt[c]);
+  __syncthreads();
+  if (tid < p.n_cap) slab[tid] = s_cnt[tid];  // (shard 0; the others stay zero)
+}
+
+// K6 (one workgroup of 1024): the sorted window into LDS, the exact crossing position from
+// base_tot, the window's prefix taken, then the gap walk (k_greedy_walk's rule); the ON counts of
+// the window's decided actions; what the window cannot decide goes to gq_exact; finally this
+// call's key range becomes the next call's quantisation
+__global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __restrict__ sorted,
+                                                    const double* __restrict__ key, double S, double pmin,
+                                                    GqSel* __restrict__ sel, uint8_t* __restrict__ action,
+                                                    unsigned long long* __restrict__ slab) {
   __shared__ uint4 s_e[kGqCap];
+  __shared__ uint8_t s_tk[kGqCap];
   __shared__ double s_w[16];
   __shared__ double s_tot;
-  __shared__ int s_k, s_first;
+  __shared__ int s_k, s_first, s_ovf;
   __shared__ unsigned long long s_bal[16];
+  __shared__ unsigned s_cnt[kWinCap];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nth = blockDim.x;
   double pon[4];
 #pragma unroll
@@ -1888,77 +2154,103 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __re
     const uint32_t cl = z & 3u;
     return cl == 0u ? pon[0] : cl == 1u ? pon[1] : cl == 2u ? pon[2] : pon[3];
   };
-  if (sel->all || sel->overflow) {
-    if (tid == 0) {
-      *flag = sel->overflow;
-      sel->overflow = 0;  // (the next call starts clear, with this call's key range)
-      sel->kmin = sel->nkmin;
-      sel->scale = sel->nscale;
-    }
-    return;
-  }
-  const int ncand = sel->ncand;
-  {
-    constexpr int U = kGqCap / 1024;  // (blockDim 1024: every load issued before the LDS stores)
-    uint4 v[U];
+  const bool all = sel->all;
+  bool ovf = sel->overflow;
+  if (!all && !ovf) {
+    const int ncand = sel->ncand;
+    {
+      constexpr int U = kGqCap / 1024;  // (blockDim 1024: every load issued before the LDS stores)
+      uint4 v[U];
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = tid + u * 1024;
-      if (e < ncand) v[u] = sorted[e];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = tid + u * 1024;
-      if (e < ncand) s_e[e] = v[u];
-    }
-  }
-  if (tid == 0) { s_tot = sel->base_tot; s_k = -1; }
-  __syncthreads();
-  for (int c0 = 0; c0 < ncand; c0 += nth) {
-    const int j = c0 + tid;
-    const double pj = j < ncand ? P_of(s_e[j].z) : 0.0;
-    double x = pj;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double y = __shfl_up(x, off);
-      if (lane >= off) x += y;
-    }
-    if (lane == 63) s_w[wv] = x;
-    __syncthreads();
-    for (int w = 0; w < wv; ++w) x += s_w[w];
-    const double tot = s_tot;
-    const unsigned long long bl = __ballot(j < ncand && !(tot + x < S));
-    if (lane == 0) s_bal[wv] = bl;
-    if (tid == 0) s_first = -1;
-    __syncthreads();
-    if (tid == 0)
-      for (int w = 0; w < 16; ++w)
-        if (s_bal[w]) { s_first = w * 64 + __ffsll((long long)s_bal[w]) - 1; break; }
-    __syncthreads();
-    const int f = s_first;
-    if (f >= 0 && tid == f) { s_k = c0 + f; s_tot = tot + (x - pj); }  // (exclusive: exact for integer P)
-    if (f < 0 && tid == nth - 1) s_tot = tot + x;                     // the round's total
-    __syncthreads();
-    if (f >= 0) break;
-  }
-  const int k = s_k;  // >= 0: the crossing lies in bin b*, inside the window
-  for (int j = tid; j < (k < 0 ? ncand : k); j += nth) action[s_e[j].z >> 2] = 1;
-  if (tid == 0) {
-    int ovf = k < 0;
-    if (!ovf) {
-      double tot = s_tot;
-      int j = k;
-      for (; j < ncand; ++j) {
-        if (!(tot < S) || 2.0 * (S - tot) < pmin * (1.0 - 1e-9)) break;
-        const double pj = P_of(s_e[j].z);
-        if ((pj + tot < S) || (fabs(pj + tot - S) < fabs(tot - S) && !s_e[j].w)) {
-          action[s_e[j].z >> 2] = 1;
-          tot += pj;
-        }
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * 1024;
+        if (e < ncand) v[u] = sorted[e];
       }
-      if (j >= ncand && sel->more_after && tot < S && !(2.0 * (S - tot) < pmin * (1.0 - 1e-9))) ovf = 1;
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * 1024;
+        if (e < ncand) { s_e[e] = v[u]; s_tk[e] = 0; }
+      }
     }
-    *flag = ovf;
+    if (tid == 0) { s_tot = sel->base_tot; s_k = -1; }
+    if (tid < kWinCap) s_cnt[tid] = 0u;
+    __syncthreads();
+    for (int c0 = 0; c0 < ncand; c0 += nth) {
+      const int j = c0 + tid;
+      const double pj = j < ncand ? P_of(s_e[j].z) : 0.0;
+      double x = pj;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const double y = __shfl_up(x, off);
+        if (lane >= off) x += y;
+      }
+      if (lane == 63) s_w[wv] = x;
+      __syncthreads();
+      for (int w = 0; w < wv; ++w) x += s_w[w];
+      const double tot = s_tot;
+      const unsigned long long bl = __ballot(j < ncand && !(tot + x < S));
+      if (lane == 0) s_bal[wv] = bl;
+      if (tid == 0) s_first = -1;
+      __syncthreads();
+      if (tid == 0)
+        for (int w = 0; w < 16; ++w)
+          if (s_bal[w]) { s_first = w * 64 + __ffsll((long long)s_bal[w]) - 1; break; }
+      __syncthreads();
+      const int f = s_first;
+      if (f >= 0 && tid == f) { s_k = c0 + f; s_tot = tot + (x - pj); }  // (exclusive: exact for integer P)
+      if (f < 0 && tid == nth - 1) s_tot = tot + x;                     // the round's total
+      __syncthreads();
+      if (f >= 0) break;
+    }
+    const int k = s_k;  // >= 0: the crossing lies in bin b*, inside the window
+    for (int j = tid; j < (k < 0 ? ncand : k); j += nth) s_tk[j] = 1;
+    if (tid == 0) {
+      int o = k < 0;
+      if (!o) {
+        double tot = s_tot;
+        int j = k;
+        for (; j < ncand; ++j) {
+          if (gq_walk_over(tot, S, pmin)) break;
+          const double pj = P_of(s_e[j].z);
+          if (gq_take(pj, tot, S, hv_lock(s_e[j].w))) {
+            s_tk[j] = 1;
+            tot += pj;
+          }
+        }
+        if (j >= ncand && sel->more_after && !gq_walk_over(tot, S, pmin)) o = 1;
+      }
+      s_ovf = o;
+    }
+    __syncthreads();
+    ovf = s_ovf != 0;
+    if (!ovf) {  // the window's actions and the ON counts they produce
+      unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
+      for (int j0 = 0; j0 < ncand; j0 += nth) {
+        const int j = j0 + tid;
+        bool on1 = false;
+        unsigned cl = 0u;
+        if (j < ncand) {
+          const uint4 e = s_e[j];
+          const bool take = s_tk[j] != 0;
+          if (take) action[e.z >> 2] = 1;
+          cl = e.z & 3u;
+          on1 = hv_on(hvac_fsm(e.w, take, p.dt, p.L));
+        }
+#pragma unroll
+        for (int c = 0; c < kWinCap; ++c) oncnt[c] += (unsigned)__popcll(__ballot(on1 && cl == (unsigned)c));
+      }
+      if (lane == 0)
+#pragma unroll
+        for (int c = 0; c < kWinCap; ++c)
+          if (oncnt[c]) atomicAdd(&s_cnt[c], oncnt[c]);
+      __syncthreads();
+      if (tid < p.n_cap && s_cnt[tid]) atomicAdd(&slab[tid], (unsigned long long)s_cnt[tid]);
+    }
+  }
+  if (ovf) gq_exact(p, key, S, pmin, action, slab);
+  if (tid == 0) {
+    if (ovf) sel->fallbacks += 1;
+    sel->overflow = 0;       // (the next call starts clear, with this call's key range)
     sel->kmin = sel->nkmin;  // (every kernel of this call has read the quantisation)
     sel->scale = sel->nscale;
   }

@@ -17,7 +17,7 @@ MAX_CAP = 64
 
 # enums (mdr.h)
 ACT_BUFFER, ACT_RANDOM, ACT_ALWAYS_ON, ACT_BANGBANG, ACT_DEADBAND_BANGBANG = 0, 1, 2, 16, 17
-CTRL_NONE, CTRL_BANGBANG, CTRL_DEADBAND_BANGBANG = 0, 1, 2
+CTRL_NONE, CTRL_BANGBANG, CTRL_DEADBAND_BANGBANG, CTRL_GREEDY_KEYS = 0, 1, 2, 3
 COMM_RING, COMM_TABLE = 0, 1
 PEN_MODES = {"individual_L2": 0, "common_L2": 1, "common_max_error": 2, "mixture": 3}
 ERRORS = {-1: "MDR_EARG", -2: "MDR_EHIP", -3: "MDR_ERCCL", -4: "MDR_ENOMEM", -5: "MDR_ESTATE"}

@@ -299,7 +299,9 @@ class Environment:
         reward buffer (overwritten by the next tick).
 
         ``lookahead`` names the NEXT tick's in-kernel action source: its cluster-power counts
-        are computed by this launch, so the next tick is a single kernel.
+        are computed by this launch, so the next tick is a single kernel.  ``ctrl``: a controller
+        evaluated on the post-step state ('bangbang' / 'deadband_bangbang' into ``ctrl_out``), or
+        'greedy_keys': the next ``greedy_actions`` call's keys, prepared by this launch.
         """
         p = self.init_props
         hp = p.cluster_prop.house_prop
@@ -319,8 +321,8 @@ class Environment:
         self._tod_prev = self.current_od_temp
         self._s_prev = self.power_grid.current_signal
         tick = self._tick_args()
-        if mode == L.ACT_BUFFER and self._counts_ready == ("actor", actions.data_ptr()):
-            pass  # the actor launch that wrote these actions also counted their cluster power
+        if mode == L.ACT_BUFFER and self._counts_ready in (("actor", actions.data_ptr()), ("greedy", actions.data_ptr())):
+            pass  # the actor / greedy launches that wrote these actions also counted their cluster power
         elif mode == L.ACT_BUFFER or self._counts_ready != mode:
             # phase 1 (unless the previous launch already counted this tick under the same source)
             if mode in (L.ACT_BUFFER, L.ACT_RANDOM, L.ACT_ALWAYS_ON):
@@ -330,7 +332,10 @@ class Environment:
         if self._comm is not None:
             self._comm.allreduce_counts(sh)
         la = ACTION_MODES[lookahead] if lookahead else 0
-        cm = {None: 0, "bangbang": L.CTRL_BANGBANG, "deadband_bangbang": L.CTRL_DEADBAND_BANGBANG}[ctrl]
+        cm = {None: 0, "bangbang": L.CTRL_BANGBANG, "deadband_bangbang": L.CTRL_DEADBAND_BANGBANG,
+              "greedy_keys": L.CTRL_GREEDY_KEYS}[ctrl]
+        if cm == L.CTRL_GREEDY_KEYS and self.world > 1:
+            cm = 0  # (the sharded greedy gathers its rows itself)
         if rewards is not None and (rewards.dtype != sh.reward.dtype or rewards.numel() != self._n_local
                                     or not rewards.is_contiguous()):
             raise ValueError(f"rewards must be a contiguous float64 tensor of {self._n_local} elements")
@@ -605,7 +610,9 @@ class Environment:
     def greedy_actions(self, out=None):
         """GreedyMyopic.get_action (greedy_myopic_controller.py:67-104) on device: the next tick's
         actions from the current state, budget = the current regulation signal (obs reg_signal).
-        Returns a uint8 [n_local] device tensor (``out`` if given)."""
+        Returns a uint8 [n_local] device tensor (``out`` if given).  Single shard: the launches also
+        count the cluster power of these actions, so ``step_tensor(out)`` is one launch, and a
+        preceding ``step_tensor(..., ctrl='greedy_keys')`` has already written their keys."""
         import torch
 
         sh = self._shard
@@ -627,6 +634,7 @@ class Environment:
             out.copy_(full[self._offset:self._offset + nl])
             return out
         sh.greedy(float(self.power_grid.current_signal), out)
+        self._counts_ready = ("greedy", out.data_ptr())
         return out
 
     def rollout_stream(self):

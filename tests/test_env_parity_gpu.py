@@ -269,8 +269,8 @@ def test_greedy_key_runs_vs_oracle(torch_gpu, form):
     select; sort: MDR_OPT_GREEDY_SORT, the full 64-bit key sort): 300 identical temperatures, 700 keys
     1e-9 apart in DESCENDING house order, 100 houses at exactly their target (key -0.0), random
     lockouts, budgets that put the pivot inside each group; the oracle's stable numpy order
-    decides.  The select form decides all of these itself (no fallback); a cluster of identical
-    keys (one bin) is handed to the sort form and still matches."""
+    decides.  The select form's window decides all of these; a cluster of identical keys (one bin
+    of every house) goes to its exact in-kernel fallback and still matches."""
     torch = torch_gpu
     from mdr_amd.environment import Environment
     from mdr_amd.shard import encode_hvac
@@ -310,7 +310,7 @@ def test_greedy_key_runs_vs_oracle(torch_gpu, form):
         sh.greedy(S, out)
         ref = O.greedy(T, tg, caps, cop, lock, S)
         np.testing.assert_array_equal(out.cpu().numpy().astype(bool), ref, err_msg=f"S={S}")
-    assert sh.greedy_fallbacks() == f0  # (the sort form never counts)
+    assert sh.greedy_fallbacks() == f0  # (the window decided every one of these)
     # every key identical: one bin of n houses > the window -> the sort form decides
     sh.t_air.copy_(torch.full((n,), 23.0, dtype=torch.float64, device="cuda"))
     sh.target.copy_(torch.full((n,), 22.0, dtype=torch.float64, device="cuda"))
@@ -320,7 +320,9 @@ def test_greedy_key_runs_vs_oracle(torch_gpu, form):
         ref = O.greedy(np.full(n, 23.0), np.full(n, 22.0), caps, cop, lock, S)
         np.testing.assert_array_equal(out.cpu().numpy().astype(bool), ref, err_msg=f"equal keys S={S}")
     if form == "select":
-        assert sh.greedy_fallbacks() == f0 + 1  # (S = 1e12 takes everything: decided by the bins)
+        # the n identical keys make one bin of n houses > the window: decided by k_gq_finish's exact
+        # in-kernel fallback (S = 1e12 takes everything: decided by the superbins)
+        assert sh.greedy_fallbacks() == f0 + 1
 
 
 def test_one_million_houses_properties(torch_gpu):
@@ -439,3 +441,100 @@ def test_perlin_trajectory_vs_oracle(torch_gpu, path):
     np.testing.assert_allclose(float(env.power_grid.current_signal), o["S"], rtol=1e-12)
     assert env.cluster.current_power_consumption == o["P"]
     assert env.date_time == o["date"] and env.date_time.day == 1  # crossed midnight into July
+
+
+
+def _greedy_env(n, seed):
+    from mdr_amd.environment import Environment
+
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    return props, Environment(props, rng=random.Random(seed), population="synthetic", seed=seed)
+
+
+def test_greedy_loop_keys_epilogue_and_counts(torch_gpu):
+    """Config C3's loop as the bench runs it: greedy_actions (its launches also count the ON houses
+    of the decided actions) -> step_tensor(ctrl='greedy_keys') (one launch: those counts, and the
+    next greedy call's keys written by the step kernel's epilogue) == the same decisions through a
+    twin that recomputes keys (k_gq_keys) and counts (mdr_power_counts) every tick, and == the
+    oracle's greedy + step; 12 ticks at 200,003 houses (ragged tiles)."""
+    torch = torch_gpu
+    n = 200_003
+    props, a = _greedy_env(n, 23)
+    _, b = _greedy_env(n, 23)
+    prm = a.shard.host_params()
+    caps = np.array(a._cap_values, np.float64)[prm["cap_idx"]]
+    pop = {"Ua": prm["ua"], "Ca": prm["ca"], "Cm": prm["cm"], "Hm": prm["hm"], "target": prm["target"], "cap": caps}
+    ora = O.OracleEnv(props, random.Random(23), population=pop)
+    cop = props.cluster_prop.house_prop.hvac_prop.cop
+    ga = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for t in range(12):
+        aa = a.greedy_actions(out=ga)
+        ab = b.greedy_actions().clone()  # another buffer: its step recounts with mdr_power_counts
+        assert torch.equal(aa, ab), t
+        ref = O.greedy(ora.T, ora.pop["target"], caps, cop, ora.lock, float(ora.S))
+        np.testing.assert_array_equal(aa.cpu().numpy().astype(bool), ref, err_msg=f"greedy t={t}")
+        ra = a.step_tensor(aa, ctrl="greedy_keys").clone()
+        rb = b.step_tensor(ab).clone()
+        assert torch.equal(ra, rb), t
+        o, rr = ora.step(ref)
+        np.testing.assert_allclose(ra.cpu().numpy(), rr, rtol=1e-9, atol=1e-12)
+        assert a.cluster.current_power_consumption == o["P"]
+    st = a.shard.host_state()
+    np.testing.assert_array_equal(st["on"], o["on"])
+    np.testing.assert_allclose(st["T"], o["T"], rtol=TEMP_RTOL, atol=0)
+
+
+@pytest.mark.parametrize("case", ["nan_crossing", "nan_after", "identical_crossing"])
+def test_greedy_exact_fallback(torch_gpu, case):
+    """Inputs the candidate window cannot decide go to k_gq_finish's exact in-kernel radix select
+    (no host synchronisation): a crossing among NaN keys (NaN temperatures sort last, in house order,
+    as numpy's stable argsort and pandas' na_position='last' put them), NaN keys after the crossing,
+    10,000 identical keys around the crossing; actions and the counted cluster power == the oracle."""
+    torch = torch_gpu
+    n = 60_000
+    props, env = _greedy_env(n, 31)
+    sh = env.shard
+    prm = sh.host_params()
+    caps = np.array(env._cap_values, np.float64)[prm["cap_idx"]]
+    cop = props.cluster_prop.house_prop.hvac_prop.cop
+    rs = np.random.RandomState(7)
+    tg = prm["target"].copy()
+    T = tg + rs.normal(0.0, 1.0, n)
+    lock = rs.rand(n) < 0.3
+    if case.startswith("nan"):
+        T[rs.choice(n, 5000, replace=False)] = np.nan
+    else:
+        T[20000:30000] = 24.0
+        tg[20000:30000] = 22.5
+    sh.t_air.copy_(torch.from_numpy(T).cuda())
+    sh.target.copy_(torch.from_numpy(tg).cuda())
+    from mdr_amd.shard import encode_hvac
+
+    sh.hvac.copy_(torch.from_numpy(encode_hvac(~lock & (rs.rand(n) < 0.5), lock, rs.randint(0, 60, n))).cuda())
+    sh.params_changed()
+    key = -(T - tg)
+    order = np.argsort(key, kind="stable")
+    cum = np.cumsum((caps / cop)[order])
+    finite = int(np.isfinite(key).sum())
+    if case == "nan_crossing":
+        S = float(cum[finite + 1234]) - 0.5
+    elif case == "nan_after":
+        S = float(cum[finite // 2]) + 0.5
+    else:
+        pos = np.nonzero((order >= 20000) & (order < 30000))[0]
+        S = float(cum[pos[len(pos) // 2]]) - 1.0
+    f0 = sh.greedy_fallbacks()
+    out = torch.zeros(n, dtype=torch.uint8, device="cuda")
+    sh.greedy(S, out)
+    ref = O.greedy(T, tg, caps, cop, lock, S)
+    np.testing.assert_array_equal(out.cpu().numpy().astype(bool), ref)
+    if case != "nan_after":
+        assert sh.greedy_fallbacks() >= f0 + 1
+    # the counts the greedy launches left == the ON houses those actions produce
+    st0 = sh.host_state()
+    hv = props.cluster_prop.house_prop.hvac_prop
+    on, _, _ = O.hvac_step(st0["on"], st0["lock"], st0["sso"], ref, hv.lockout_duration, props.time_step.seconds)
+    env._counts_ready = ("greedy", out.data_ptr())
+    env.step_tensor(out)
+    assert env.cluster.current_power_consumption == float(np.sum(np.where(on, caps / cop, 0.0)))
