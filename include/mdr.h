@@ -336,7 +336,9 @@ int mdr_greedy_select(mdr_ctx* ctx, int64_t n, const double* key, const double* 
  * server/app/core/agents/trainables/ppo.py:23-26): one persistent launch builds every house's obs
  * row on chip, runs both hidden layers on MFMA, softmax + Categorical sampling in fp32. */
 enum { MDR_PREC_BF16 = 1,   /* bf16 products, fp32 accumulate (~4e-3 relative) */
-       MDR_PREC_BF16X3 = 3  /* split-bf16 (hi*hi + hi*lo + lo*hi), fp32 accumulate (~1e-5) */ };
+       MDR_PREC_BF16X3 = 3, /* split-bf16 (hi*hi + hi*lo + lo*hi), fp32 accumulate (~1e-5) */
+       MDR_PREC_FP32 = 6    /* three-way split-bf16 (24 significant bits, 6 products), fp32 accumulate:
+                               fp32-faithful (~1e-7), the reference Actor's precision */ };
 
 typedef struct mdr_actor_spec {
   int32_t n_in;      /* obs features (= mdr_obs_spec.n_feat), <= 128 */

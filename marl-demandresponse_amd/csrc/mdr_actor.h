@@ -15,7 +15,8 @@ struct ActorDims {
   int n_in, h1, h2, n_act;
   int ks1, ks2;  // k-steps of layer 1 (ceil(n_in/16)) and layer 2 (ceil(h1/16))
   int fs;        // LDS obs row stride (floats): >= n_in, multiple of 4, odd multiple of 4 words
-  int off_w1, off_w2, off_tail, off_end;  // packed image: W1 / W2 fragments (hi, lo), fp32 tail
+  int nf;        // bf16 fragments per (row block, k-step): 2 = (hi, lo), 3 = (hi, mid, lo) for MDR_PREC_FP32
+  int off_w1, off_w2, off_tail, off_end;  // packed image: W1 / W2 fragments, fp32 tail
   int lds_cf, lds_hist, lds_wave, wave_stride;  // block LDS: obs consts, count histogram, wave slices
   int w_msg, w_hw, w_cls;                        // offsets inside a wave slice (rows at 0)
   int lds_total;

@@ -14,6 +14,9 @@
 //   MDR_PREC_BF16X3 — every fp32 operand x is split x = hi + lo (hi = bf16(x), lo = bf16(x - hi))
 //                     and a·b ≈ ah·bh + ah·bl + al·bh, accumulated in fp32: ~1e-5 relative to the
 //                     fp32 reference (bf16 alone: ~4e-3).
+//   MDR_PREC_FP32   — three-way split x = hi + mid + lo (24 significant bits: the whole fp32
+//                     significand) and a·b ≈ ah·bh + ah·bm + am·bh + ah·bl + al·bh + am·bm (the dropped
+//                     terms are <= 2^-24 relative): fp32-faithful, 6 MFMAs per term.
 //   MDR_PREC_BF16   — one bf16 product per term.
 // Bias adds, ReLU, the output layer, softmax and sampling are fp32.
 //
@@ -40,6 +43,31 @@ __device__ __forceinline__ void split8(const float* v, bf16x8& hi, bf16x8& lo) {
   }
 }
 
+__device__ __forceinline__ void split8x3(const float* v, bf16x8& hi, bf16x8& mid, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    hi[j] = (__bf16)v[j];
+    const float r = v[j] - (float)hi[j];  // exact (Sterbenz / the leading bits cancel)
+    mid[j] = (__bf16)r;
+    lo[j] = (__bf16)(r - (float)mid[j]);
+  }
+}
+
+// the packed fragments of one (row block, k-step): nf = 2 (hi, lo) or 3 (hi, mid, lo)
+__device__ __forceinline__ void pack_frags(const ActorDims& d, const float* v, unsigned char* base, int f, int lane) {
+  bf16x8 hi, mid, lo;
+  if (d.nf == 3) split8x3(v, hi, mid, lo);
+  else split8(v, hi, lo);
+  bf16x8* o = reinterpret_cast<bf16x8*>(base);
+  o[(d.nf * f) * 64 + lane] = hi;
+  if (d.nf == 3) {
+    o[(3 * f + 1) * 64 + lane] = mid;
+    o[(3 * f + 2) * 64 + lane] = lo;
+  } else {
+    o[(2 * f + 1) * 64 + lane] = lo;
+  }
+}
+
 __global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const float* __restrict__ b1,
                              const float* __restrict__ w2, const float* __restrict__ b2,
                              const float* __restrict__ w3, const float* __restrict__ b3,
@@ -49,7 +77,6 @@ __global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const fl
   const int lane = g & 63, f = g >> 6;
   const int r = lane & 31, h = lane >> 5;
   float v[8];
-  bf16x8 hi, lo;
   // fragments are stored k-step-major (f = k-step * kActorMB + mb), so the kernel's unrolled
   // (k-step, mb) loops address them with compile-time LDS offsets whatever ks1 / ks2 are
   if (f < nf1) {  // W1 [H1][n_in], fragment (mb, ks)
@@ -60,9 +87,7 @@ __global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const fl
       const int k = 16 * ks + 8 * h + j;
       v[j] = (row < d.h1 && k < d.n_in) ? w1[row * d.n_in + k] : 0.f;
     }
-    split8(v, hi, lo);
-    reinterpret_cast<bf16x8*>(out + d.off_w1)[(2 * f) * 64 + lane] = hi;
-    reinterpret_cast<bf16x8*>(out + d.off_w1)[(2 * f + 1) * 64 + lane] = lo;
+    pack_frags(d, v, out + d.off_w1, f, lane);
   } else if (f < nf1 + nf2) {  // W2 [H2][H1], fragment (mb, q) in the accumulator k order
     const int f2 = f - nf1;
     const int q = f2 / kActorMB, mb = f2 % kActorMB;
@@ -72,9 +97,7 @@ __global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const fl
       const int k = 16 * q + 8 * (j >> 2) + 4 * h + (j & 3);
       v[j] = (row < d.h2 && k < d.h1) ? w2[row * d.h1 + k] : 0.f;
     }
-    split8(v, hi, lo);
-    reinterpret_cast<bf16x8*>(out + d.off_w2)[(2 * f2) * 64 + lane] = hi;
-    reinterpret_cast<bf16x8*>(out + d.off_w2)[(2 * f2 + 1) * 64 + lane] = lo;
+    pack_frags(d, v, out + d.off_w2, f2, lane);
   } else if (f == nf1 + nf2) {  // fp32 tail: b1, b2 [128], W3^T [128][2] (row-interleaved), b3 [2]
     float* t = reinterpret_cast<float*>(out + d.off_tail);
     for (int i = lane; i < kActorRows; i += 64) {
@@ -133,6 +156,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
   const int nthr = blockDim.x, nw = nthr >> 6;
   const int r = lane & 31, h = lane >> 5;
   const int F = o.n_feat, FS = d.fs;
+  constexpr int NF = PREC == 6 ? 3 : 2;  // packed fragments per (row block, k-step)
   const int K = o.n_comm, M = o.msg_w;
   const bool ring = o.comm_mode == MDR_COMM_RING && K > 0;
   const int lo = ring ? K / 2 : 0, hi = ring ? (K + 1) / 2 : 0;
@@ -155,7 +179,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     uint4* dst = reinterpret_cast<uint4*>(smem);
     const int n16 = d.off_end / 16;
     for (int q = tid; q < n16; q += nthr) {
-      if (PREC == 1 && q < d.off_tail / 16 && ((q >> 6) & 1)) continue;  // bf16: no lo fragments
+      if (PREC == 1 && q < d.off_tail / 16 && ((q >> 6) & 1)) continue;  // bf16: no lo fragments (nf = 2)
       dst[q] = src[q];
     }
     for (int q = lane; q < 32 * FS + 16 * d.ks1; q += 64) w_obs[q] = 0.f;
@@ -263,14 +287,28 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
       const float4 x0 = *reinterpret_cast<const float4*>(xrow + 16 * ks);
       const float4 x1 = *reinterpret_cast<const float4*>(xrow + 16 * ks + 4);
       const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      bf16x8 xh, xl;
-      split8(xv, xh, xl);
-      bf16x8 ah[kActorMB], al[kActorMB];
+      bf16x8 xh, xl, xm;
+      if (PREC == 6) split8x3(xv, xh, xm, xl);
+      else split8(xv, xh, xl);
+      bf16x8 ah[kActorMB], al[kActorMB], am[kActorMB];
 #pragma unroll
       for (int mb = 0; mb < kActorMB; ++mb) {
         const int f = ks * kActorMB + mb;
-        ah[mb] = lds_frag(s_w1, 2 * f, lane);
-        if (PREC == 3) al[mb] = lds_frag(s_w1, 2 * f + 1, lane);
+        ah[mb] = lds_frag(s_w1, NF * f, lane);
+        if (PREC == 3) al[mb] = lds_frag(s_w1, NF * f + 1, lane);
+        if (PREC == 6) { am[mb] = lds_frag(s_w1, NF * f + 1, lane); al[mb] = lds_frag(s_w1, NF * f + 2, lane); }
+      }
+      if (PREC == 6) {  // smallest terms first
+#pragma unroll
+        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mb], xm, acc1[mb], 0, 0, 0);
+#pragma unroll
+        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mb], xh, acc1[mb], 0, 0, 0);
+#pragma unroll
+        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], xl, acc1[mb], 0, 0, 0);
+#pragma unroll
+        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mb], xh, acc1[mb], 0, 0, 0);
+#pragma unroll
+        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], xm, acc1[mb], 0, 0, 0);
       }
       if (PREC == 3) {
 #pragma unroll
@@ -284,13 +322,14 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     PSTAMP(3);
 
     // ---- ReLU + split: layer 1's accumulators become layer 2's B fragments in place
-    bf16x8 hh[2 * kActorMB], hl[2 * kActorMB];
+    bf16x8 hh[2 * kActorMB], hl[2 * kActorMB], hm[PREC == 6 ? 2 * kActorMB : 1];
 #pragma unroll
     for (int q = 0; q < 2 * kActorMB; ++q) {
       float v[8];
 #pragma unroll
       for (int j = 0; j < 8; ++j) v[j] = fmaxf(acc1[q >> 1][8 * (q & 1) + j], 0.f);
-      split8(v, hh[q], hl[q]);
+      if constexpr (PREC == 6) split8x3(v, hh[q], hm[q], hl[q]);
+      else split8(v, hh[q], hl[q]);
     }
 
     // ---- layer 2: acc2[mb] = b2 + W2 · relu(H1)
@@ -302,12 +341,25 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
 #pragma unroll
     for (int q = 0; q < 2 * kActorMB; ++q) {
       if (q >= d.ks2) break;
-      bf16x8 ah[kActorMB], al[kActorMB];
+      bf16x8 ah[kActorMB], al[kActorMB], am[kActorMB];
 #pragma unroll
       for (int mb = 0; mb < kActorMB; ++mb) {
         const int f = q * kActorMB + mb;
-        ah[mb] = lds_frag(s_w2, 2 * f, lane);
-        if (PREC == 3) al[mb] = lds_frag(s_w2, 2 * f + 1, lane);
+        ah[mb] = lds_frag(s_w2, NF * f, lane);
+        if (PREC == 3) al[mb] = lds_frag(s_w2, NF * f + 1, lane);
+        if (PREC == 6) { am[mb] = lds_frag(s_w2, NF * f + 1, lane); al[mb] = lds_frag(s_w2, NF * f + 2, lane); }
+      }
+      if constexpr (PREC == 6) {  // smallest terms first
+#pragma unroll
+        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mb], hm[q], acc2[mb], 0, 0, 0);
+#pragma unroll
+        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mb], hh[q], acc2[mb], 0, 0, 0);
+#pragma unroll
+        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], hl[q], acc2[mb], 0, 0, 0);
+#pragma unroll
+        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mb], hh[q], acc2[mb], 0, 0, 0);
+#pragma unroll
+        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], hm[q], acc2[mb], 0, 0, 0);
       }
       if (PREC == 3) {
 #pragma unroll
@@ -382,7 +434,9 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
                                          ActorOut, uint64_t, const TickArgs*);
 MDR_INST_ACTOR(1, false)
 MDR_INST_ACTOR(3, false)
+MDR_INST_ACTOR(6, false)
 MDR_INST_ACTOR(1, true)
 MDR_INST_ACTOR(3, true)
+MDR_INST_ACTOR(6, true)
 
 }  // namespace mdr

@@ -1534,9 +1534,10 @@ ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw) 
   int fs = (a.n_in + 3) & ~3;
   if (((fs / 4) & 1) == 0) fs += 4;  // odd multiple of 16 B: conflict-free ds_read_b128 rows
   d.fs = fs;
+  d.nf = a.precision == MDR_PREC_FP32 ? 3 : 2;
   d.off_w1 = 0;
-  d.off_w2 = kActorMB * d.ks1 * 2048;
-  d.off_tail = d.off_w2 + kActorMB * d.ks2 * 2048;
+  d.off_w2 = kActorMB * d.ks1 * d.nf * 1024;
+  d.off_tail = d.off_w2 + kActorMB * d.ks2 * d.nf * 1024;
   d.off_end = align16(d.off_tail + ((2 + kActorNA) * kActorRows + kActorNA) * 4);
   const int K = sp ? sp->n_comm : 0, M = sp ? mdr_msg_width(sp) : 0;
   const bool ring = sp && sp->comm_mode == MDR_COMM_RING && K > 0;
@@ -1568,19 +1569,23 @@ int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const dou
   const unsigned grid = (unsigned)std::min<int64_t>(ntile, (int64_t)c->n_cu);
   static bool lds_attr = false;  // > 64 KiB of dynamic LDS must be opted into per kernel
   if (!lds_attr) {
-    for (const void* k : {(const void*)k_actor<1, false>, (const void*)k_actor<3, false>,
-                          (const void*)k_actor<1, true>, (const void*)k_actor<3, true>})
+    for (const void* k : {(const void*)k_actor<1, false>, (const void*)k_actor<3, false>, (const void*)k_actor<6, false>,
+                          (const void*)k_actor<1, true>, (const void*)k_actor<3, true>, (const void*)k_actor<6, true>})
       HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     lds_attr = true;
   }
 #define MDR_LAUNCH_ACTOR(P, F)                                                                      \
   hipLaunchKernelGGL((k_actor<P, F>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
                      c->d_actor, out, tick, tkp)
-  const bool bf16 = c->actor.precision == MDR_PREC_BF16;
+  const int prec = c->actor.precision;
   if (out.prof) {
-    if (bf16) MDR_LAUNCH_ACTOR(1, true); else MDR_LAUNCH_ACTOR(3, true);
+    if (prec == MDR_PREC_BF16) MDR_LAUNCH_ACTOR(1, true);
+    else if (prec == MDR_PREC_FP32) MDR_LAUNCH_ACTOR(6, true);
+    else MDR_LAUNCH_ACTOR(3, true);
   } else {
-    if (bf16) MDR_LAUNCH_ACTOR(1, false); else MDR_LAUNCH_ACTOR(3, false);
+    if (prec == MDR_PREC_BF16) MDR_LAUNCH_ACTOR(1, false);
+    else if (prec == MDR_PREC_FP32) MDR_LAUNCH_ACTOR(6, false);
+    else MDR_LAUNCH_ACTOR(3, false);
   }
 #undef MDR_LAUNCH_ACTOR
   LAUNCH_CHECK("k_actor");
@@ -1604,7 +1609,7 @@ int mdr_actor_load(mdr_ctx* c, const mdr_actor_spec* a, const float* w1, const f
   if (a->n_in < 1 || a->n_in > kActorMaxIn || a->h1 < 1 || a->h1 > kActorRows || a->h2 < 1 ||
       a->h2 > kActorRows || a->n_act != kActorNA)
     return fail(MDR_EARG, "mdr_actor_load: shape outside n_in <= 128, hidden <= 128, n_act == 2");
-  if (a->precision != MDR_PREC_BF16 && a->precision != MDR_PREC_BF16X3)
+  if (a->precision != MDR_PREC_BF16 && a->precision != MDR_PREC_BF16X3 && a->precision != MDR_PREC_FP32)
     return fail(MDR_EARG, "mdr_actor_load: bad precision");
   const ActorDims d = actor_layout(*a, nullptr, 2);
   if ((size_t)d.off_end > c->actor_cap) {

@@ -94,8 +94,8 @@ class mdr_interp_spec(C.Structure):
                 ("cfg_ua", C.c_double), ("cfg_cm", C.c_double), ("cfg_ca", C.c_double), ("cfg_hm", C.c_double)]
 
 
-PREC_BF16, PREC_BF16X3 = 1, 3
-PRECISIONS = {"bf16": PREC_BF16, "bf16x3": PREC_BF16X3}
+PREC_BF16, PREC_BF16X3, PREC_FP32 = 1, 3, 6
+PRECISIONS = {"bf16": PREC_BF16, "bf16x3": PREC_BF16X3, "fp32": PREC_FP32}
 
 # the structs mdr_abi_sizes reports, in its order
 ABI_STRUCTS = (mdr_config, mdr_soa, mdr_tick, mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars, mdr_actor_spec,
