@@ -118,9 +118,8 @@ struct mdr_ctx {
   double* g_part = nullptr;
   unsigned* g_hist = nullptr;
   GqSel* g_sel = nullptr;
-  uint4* g_stage = nullptr;
-  uint4* g_sorted = nullptr;             // the window in (key, house) order (k_gq_rank)
-  unsigned* g_bcnt = nullptr;
+  uint4* g_win = nullptr;                // the candidate window, unordered (k_gq_compact)
+  uint4* g_sorted = nullptr;             // the window in (key, house) order (k_gq_select)
   int gq_parts_cap = 0;                  // g_part capacity in (min, max) pairs
   bool gq_keys_ready = false;            // keys + superbin histogram of the current state are in place
   int gq_nparts = 0;                     //   (from the last step's epilogue: its grid's partials)
@@ -199,10 +198,13 @@ int refresh_if_dirty(mdr_ctx* c, hipStream_t st) {
   return MDR_OK;
 }
 
-// k_step launch with explicit count slabs; reward_lag: the launch writes the previous tick's
-// reward from `cur` (nullptr: none), see k_step_t
 int greedy_scratch(mdr_ctx* c, int64_t n);
 int launch_gq_keys(mdr_ctx* c, hipStream_t st);
+// the histogram select's per-house codes (gq_code, 4 B) live in the sort form's key buffer
+uint32_t* gq_codes(mdr_ctx* c) { return reinterpret_cast<uint32_t*>(c->g_key); }
+
+// k_step launch with explicit count slabs; reward_lag: the launch writes the previous tick's
+// reward from `cur` (nullptr: none), see k_step_t
 
 int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const TickArgs* tkp,
                    double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
@@ -235,7 +237,7 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
     // partials buffer holds this grid
     const bool epi = gq && hot_buffer && (int)nb <= c->gq_parts_cap;
     GqOut go{};
-    if (epi) go = GqOut{c->g_key, c->g_part, c->g_hist, c->g_sel};
+    if (epi) go = GqOut{gq_codes(c), c->g_part, c->g_hist, c->g_sel};
 #define MDR_LAUNCH_PIPE(T, A, LA, G)                                                                     \
   hipLaunchKernelGGL((k_step_pipe<T, A, LA, G>), grid, dim3(256), 0, st, kp, action, tk, tkp, cur, reward, \
                      p_out, nxt, zer, go)
@@ -441,7 +443,7 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->g_key); hipFree(c->g_key2); hipFree(c->g_ps); hipFree(c->g_incl);
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
-  hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_stage); hipFree(c->g_bcnt);
+  hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_win);
   hipFree(c->g_sorted);
   if (c->comm) ncclCommDestroy(c->comm);
   delete c;
@@ -1142,9 +1144,9 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   hipFree(c->g_key); hipFree(c->g_key2); hipFree(c->g_ps); hipFree(c->g_incl);
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
-  hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_stage); hipFree(c->g_bcnt);
+  hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_win);
   hipFree(c->g_sorted);
-  c->g_part = nullptr; c->g_hist = nullptr; c->g_sel = nullptr; c->g_stage = nullptr; c->g_bcnt = nullptr;
+  c->g_part = nullptr; c->g_hist = nullptr; c->g_sel = nullptr; c->g_win = nullptr;
   c->g_sorted = nullptr;
   c->gq_keys_ready = false;
   HIP_TRY(hipMalloc(&c->g_key, n * sizeof(double)));
@@ -1156,7 +1158,6 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_ls, n));
   HIP_TRY(hipMalloc(&c->g_kpos, 2 * sizeof(int64_t)));
   HIP_TRY(hipMalloc(&c->g_extra, 64 * sizeof(int64_t)));
-  const int64_t nstage = (n + kGqStage - 1) / kGqStage;
   // (min, max) partials: k_gq_keys' grid, or the grid of the step kernel whose epilogue writes the
   // keys (k_step_pipe: a block per 4 x tpw x 128 houses, tpw >= 2)
   c->gq_parts_cap = (int)std::max<int64_t>(kGqParts, (n + 1023) / 1024);
@@ -1169,9 +1170,8 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
     gq_sel_init(init);
     HIP_TRY(hipMemcpy(c->g_sel, init, 128, hipMemcpyHostToDevice));
   }
-  HIP_TRY(hipMalloc(&c->g_stage, nstage * kGqStage * sizeof(uint4)));
-  HIP_TRY(hipMalloc(&c->g_bcnt, nstage * sizeof(unsigned)));
-  HIP_TRY(hipMalloc(&c->g_sorted, 2 * kGqCap * sizeof(uint4)));  // [sorted | gathered window]
+  HIP_TRY(hipMalloc(&c->g_win, kGqCap * sizeof(uint4)));
+  HIP_TRY(hipMalloc(&c->g_sorted, kGqCap * sizeof(uint4)));
   size_t b1 = 0, b2 = 0;
   HIP_TRY(greedy_sort(nullptr, b1, c->g_key, c->g_key2, c->g_idx, c->g_idx2, n, nullptr));
   HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b2, c->g_ps, c->g_incl, (int)n));
@@ -1183,7 +1183,7 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
 
 // the keys and superbin histogram of the current state (when no step epilogue prepared them)
 int launch_gq_keys(mdr_ctx* c, hipStream_t st) {
-  hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_part, c->g_hist,
+  hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_part, c->g_hist,
                      c->g_sel);
   LAUNCH_CHECK("k_gq_keys");
   c->gq_nparts = kGqParts;
@@ -1209,25 +1209,19 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   unsigned long long* slab = slab_at(c, c->ring);  // the counts of the actions decided here
   if (c->kp.n_cap <= 4 && !c->greedy_sort) {
     // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster, no host
-    // synchronisation; k_gq_finish decides exactly what the candidate window cannot
+    // synchronisation; k_gq_select decides exactly what the candidate window cannot
     if (!keys_ready)
       if (int rc2 = launch_gq_keys(c, st)) return rc2;
-    hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_hist, c->g_part,
+    hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, c->g_part,
                        c->gq_nparts, budget, c->g_sel, slab);
     LAUNCH_CHECK("k_gq_bins");
     const int nstage = (n + kGqStage - 1) / kGqStage;
-    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, c->g_key, c->g_hist, budget, c->g_sel,
-                       c->g_stage, c->g_bcnt, action, slab);
+    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
+                       c->g_sel, c->g_win, action, slab);
     LAUNCH_CHECK("k_gq_compact");
-    hipLaunchKernelGGL(k_gq_gather, dim3(nstage), dim3(256), 0, st, c->g_stage, c->g_bcnt, c->g_sel, c->g_sorted + kGqCap,
-                       c->g_hist);
-    LAUNCH_CHECK("k_gq_gather");
-    hipLaunchKernelGGL(k_gq_rank, dim3(kGqRankBlocks), dim3(kGqRankThreads), 0, st, c->g_sorted + kGqCap, c->g_sel,
-                       c->g_sorted);
-    LAUNCH_CHECK("k_gq_rank");
-    hipLaunchKernelGGL(k_gq_finish, dim3(1), dim3(1024), 0, st, c->kp, c->g_sorted, c->g_key, budget, pmin, c->g_sel,
-                       action, slab);
-    LAUNCH_CHECK("k_gq_finish");
+    hipLaunchKernelGGL(k_gq_select, dim3(kGqSelBlocks), dim3(1024), 0, st, c->kp, c->g_win, c->g_sorted, budget, pmin,
+                       c->g_sel, action, slab, c->g_hist);
+    LAUNCH_CHECK("k_gq_select");
     c->counts_ready = true;
     return MDR_OK;
   }

@@ -82,7 +82,7 @@ __global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, Tick
 struct GqSel;
 // the greedy controller's key outputs of a step kernel's epilogue (k_step_pipe GQ; k_gq_keys' outputs)
 struct GqOut {
-  double* key;
+  uint32_t* code;    // [n] the house's key bin << 2 | capacity class (gq_code)
   double* part;      // [grid][2] per-block (min, max) of the finite keys
   unsigned* hist;    // g_hist (the superbin copies follow its kGqBins * 4 bin words)
   const GqSel* sel;  // this call's quantisation
@@ -152,20 +152,17 @@ constexpr int kGqCopies = 8;    // copies of the global superbin / bin histogram
 constexpr int kGqUnroll = 4;    // houses per thread per pass of k_gq_keys / k_gq_bins
 constexpr int kGqSuper = 256;   // superbins (64 bins each) of the select's first pass (+ 1 for NaN keys)
 constexpr int kGqHistWords = kGqBins * 4 + kGqCopies * (kGqSuper + 1) * 4;  // g_hist: bin copies | superbin copies
+constexpr int kGqSelBlocks = 64;  // k_gq_select grid (1024 threads each)
 struct GqSel;
 void gq_sel_init(void* sel128);            // host: the first call's quantisation (keys in [-32, 32])
 unsigned gq_fallbacks_of(const void* sel128);  // host: GqSel.fallbacks of a copied-back selection
-__global__ void k_gq_keys(KParams p, double* key, double* part, unsigned* hist, const GqSel* sel);
-__global__ void k_gq_bins(KParams p, const double* key, unsigned* hist, const double* part, int nparts, double S,
+__global__ void k_gq_keys(KParams p, uint32_t* code, double* part, unsigned* hist, const GqSel* sel);
+__global__ void k_gq_bins(KParams p, const uint32_t* code, unsigned* hist, const double* part, int nparts, double S,
                           GqSel* sel, unsigned long long* slab);
-__global__ void k_gq_compact(KParams p, const double* key, unsigned* hist, double S, GqSel* sel, uint4* stage,
-                             unsigned* bcnt, uint8_t* action, unsigned long long* slab);
-constexpr int kGqRankBlocks = 256;  // k_gq_rank grid
-constexpr int kGqRankThreads = 1024;  // k_gq_rank block size
-__global__ void k_gq_gather(const uint4* stage, const unsigned* bcnt, const GqSel* sel, uint4* win, unsigned* hist);
-__global__ void k_gq_rank(const uint4* win, const GqSel* sel, uint4* sorted);
-__global__ void k_gq_finish(KParams p, const uint4* sorted, const double* key, double S, double pmin, GqSel* sel,
-                            uint8_t* action, unsigned long long* slab);
+__global__ void k_gq_compact(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel, uint4* win,
+                             uint8_t* action, unsigned long long* slab);
+__global__ void k_gq_select(KParams p, const uint4* win, uint4* sorted, double S, double pmin, GqSel* sel,
+                            uint8_t* action, unsigned long long* slab, unsigned* hist);
 __global__ void k_greedy_inputs(KParams p, double* key, double* power, uint8_t* lock);
 __global__ void k_greedy_iota(int64_t n, int* idx);
 __global__ void k_greedy_gather_rows(int64_t n, const int* perm, const double* power, const uint8_t* lock,

@@ -93,7 +93,9 @@ struct GqSel {
   double base_tot;               // P of the houses before the window (exact for integer P)
   unsigned long long base_cnt, total;
   int sb, bstar, bend, all, overflow, more_after, ncand;
-  unsigned fallbacks;            // calls decided by k_gq_finish's exact fallback (diagnostics)
+  unsigned fallbacks;            // calls decided by the exact fallback (gq_exact; diagnostics)
+  unsigned wcount;               // k_gq_compact's window allocator (zeroed by k_gq_bins)
+  unsigned ticket;               // k_gq_select's block ticket (the last block resets it)
 };
 static_assert(sizeof(GqSel) <= 128, "GqSel fits the 128-B sel buffer");
 void gq_sel_init(void* sel128) {
@@ -119,8 +121,13 @@ __device__ __forceinline__ int gq_bin(double k, double kmin, double scale) {
   const double d = (k - kmin) * scale;
   return d >= (double)(kGqBins - 1) ? kGqBins - 1 : (d > 0.0 ? (int)d : 0);
 }
-__device__ __forceinline__ int gq_super(double k, double kmin, double scale) {
-  return k != k ? kGqSuper : gq_bin(k, kmin, scale) / (kGqBins / kGqSuper);
+// a house's code: its key bin (kGqBins for a NaN key) << 2 | its capacity class; the superbin is
+// code >> 8 (kGqBins / kGqSuper = 64 bins each; NaN keys land in superbin kGqSuper)
+__device__ __forceinline__ uint32_t gq_code(double k, double kmin, double scale, unsigned cls) {
+  return ((uint32_t)(k != k ? kGqBins : gq_bin(k, kmin, scale)) << 2) | (cls & 3u);
+}
+__device__ __forceinline__ double gq_key_of(const KParams& p, int64_t i) {
+  return -(p.t_air[i] - p.target[i]);  // greedy_myopic_controller.py:79
 }
 
 // the keys' producer side, shared by k_gq_keys and the step kernel's epilogue: a block's houses go
@@ -559,10 +566,12 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
       p.t_air[i0] = Tn[0]; p.t_mass[i0] = Tmn[0]; p.hvac[i0] = w[0];
       if (counts) reward[i0] = rw[0];
     }
-    if (GQ) {  // greedy_myopic_controller.py:79 on the post-step state
+    if (GQ) {  // greedy_myopic_controller.py:79 on the post-step state (gq_key_of)
       const double k0 = -(Tn[0] - tg[0]), k1 = -(Tn[1] - tg[1]);
-      if (valid[1]) sto(gq.key, i0 * 8u, make_double2(k0, k1));
-      else if (valid[0]) gq.key[i0] = k0;
+      const uint32_t c0 = gq_code(k0, gq_kmin, gq_scale, (unsigned)cls[0]);
+      const uint32_t c1 = gq_code(k1, gq_kmin, gq_scale, (unsigned)cls[1]);
+      if (valid[1]) sto(gq.code, i0 * 4u, make_uint2(c0, c1));
+      else if (valid[0]) gq.code[i0] = c0;
 #pragma unroll
       for (int h = 0; h < HPT; ++h) {
         const double k = h ? k1 : k0;
@@ -571,7 +580,8 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
           gq_lo = fmin(gq_lo, k);
           gq_hi = fmax(gq_hi, k);
         }
-        atomicAdd(&s_gq[(tid >> 6) * kGqSupStride + gq_super(k, gq_kmin, gq_scale) * 4 + (cls[h] & 3)], 1u);
+        const uint32_t c = h ? c1 : c0;
+        atomicAdd(&s_gq[(tid >> 6) * kGqSupStride + (c >> 8) * 4 + (c & 3u)], 1u);
       }
     }
     if (LA) {
@@ -1590,14 +1600,16 @@ __global__ void __launch_bounds__(256) k_greedy_walk(int64_t n, const double* __
 // of P here is).  What the candidate window cannot decide (a crossing among NaN keys, a crossing
 // bin over kGqCap houses — e.g. thousands of identical keys —, a walk that leaves the window) the
 // last kernel decides itself, in the same launch, with an exact radix select over the 96-bit
-// (key, house) order (k_gq_finish's fallback): no host synchronisation, no sort, every tick.
-// The launches of one decision: [keys: k_gq_keys, or the previous step kernel's epilogue] ->
-// k_gq_bins -> k_gq_compact -> k_gq_gather -> k_gq_rank -> k_gq_finish; compact and finish also
-// count the ON houses the decided actions produce (the next step's cluster power).
-// K1: keys, per-block (min, max) of the finite keys (the next call's range), and the class counts
+// (key, house) order (gq_exact): no host synchronisation, no sort, every tick.
+// The houses travel as 4-B codes (gq_code: key bin << 2 | class) written by the key producer; the
+// exact key is re-read from the state (gq_key_of) only for the window's houses.
+// The launches of one decision: [codes: k_gq_keys, or the previous step kernel's epilogue] ->
+// k_gq_bins -> k_gq_compact -> k_gq_select; compact and select also count the ON houses the
+// decided actions produce (the next step's cluster power).
+// K1: codes, per-block (min, max) of the finite keys (the next call's range), and the class counts
 // per superbin (kGqBins / kGqSuper consecutive bins; NaN keys in their own) under this call's
 // quantisation
-__global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, double* __restrict__ key, double* __restrict__ part,
+__global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, uint32_t* __restrict__ code, double* __restrict__ part,
                                                         unsigned* __restrict__ hist, const GqSel* __restrict__ sel) {
   constexpr int NW = kGqThreads / 64;
   __shared__ unsigned s_sh[NW * kGqSupStride];  // one copy per wave (less atomic contention on hot superbins)
@@ -1622,13 +1634,14 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, double* __res
     for (int u = 0; u < kGqUnroll; ++u) {
       const int64_t i = i0 + u * stride;
       if (i >= p.n) break;
-      const double k = -(ta[u] - tg[u]);  // greedy_myopic_controller.py:79
-      key[i] = k;
+      const double k = -(ta[u] - tg[u]);  // gq_key_of
+      const uint32_t c = gq_code(k, kmin, scale, cl[u]);
+      code[i] = c;
       if (k == k) {
         lo = fmin(lo, k);
         hi = fmax(hi, k);
       }
-      atomicAdd(&s_sh[(threadIdx.x >> 6) * kGqSupStride + gq_super(k, kmin, scale) * 4 + (cl[u] & 3u)], 1u);
+      atomicAdd(&s_sh[(threadIdx.x >> 6) * kGqSupStride + (c >> 8) * 4 + (c & 3u)], 1u);
     }
   }
   __syncthreads();
@@ -1652,9 +1665,10 @@ __device__ __forceinline__ void gq_block_scan(double& x, unsigned long long& xc,
 
 // K2: every block first finds the crossing superbin itself (the cumulative P where it reaches S;
 // the same arithmetic in every block, so every block agrees), block 0 records it and the next
-// call's key range and zeroes the current count slab (compact and finish fill it); then the class
-// counts of the bins of superbins sb and sb + 1 (the crossing superbin and the room after it)
-__global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const double* __restrict__ key,
+// call's key range and zeroes the current count slab (compact and select fill it) and the window
+// allocator; then the class counts of the bins of superbins sb and sb + 1 (the crossing superbin
+// and the room after it).  The block's codes are loaded first: they stay in flight through the scan.
+__global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_t* __restrict__ code,
                                                         unsigned* __restrict__ hist, const double* __restrict__ part,
                                                         int nparts, double S, GqSel* __restrict__ sel,
                                                         unsigned long long* __restrict__ slab) {
@@ -1665,6 +1679,14 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const double*
   __shared__ unsigned long long s_wc[NW];
   __shared__ int s_first;
   const int tid = threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i00 = (int64_t)blockIdx.x * blockDim.x + tid;
+  uint32_t cd[kGqUnroll];
+#pragma unroll
+  for (int u = 0; u < kGqUnroll; ++u) {
+    const int64_t i = i00 + u * stride;
+    cd[u] = i < p.n ? code[i] : ~0u;  // (~0u: a bin past kGqBins, never counted)
+  }
   double p_on[kWinCap];
 #pragma unroll
   for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
@@ -1692,6 +1714,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const double*
       sel->sb = sb;
       sel->all = sb >= kGqSupN;
       sel->overflow = sb == kGqSuper;  // the crossing among NaN keys: the fallback orders them by house
+      sel->wcount = 0u;
     }
     // the next call's range: (min, max) of this call's finite keys
     double lo = INFINITY, hi = -INFINITY;
@@ -1717,24 +1740,21 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const double*
   for (int e = tid; e < NW * NB * 4; e += blockDim.x) (&s_h[0][0])[e] = 0u;
   __syncthreads();
   const int bb = sb * (kGqBins / kGqSuper);
-  const double kmin = sel->kmin, scale = sel->scale;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + tid; i0 < p.n; i0 += kGqUnroll * stride) {
-    double kk[kGqUnroll];
-    unsigned cl[kGqUnroll];
+  auto add = [&](uint32_t cc) {
+    const uint32_t b = cc >> 2;  // (NaN keys: kGqBins, past every band)
+    if (b < (uint32_t)kGqBins && b >= (uint32_t)bb && b < (uint32_t)(bb + NB))
+      atomicAdd(&s_h[tid >> 6][(b - bb) * 4 + (cc & 3u)], 1u);
+  };
+#pragma unroll
+  for (int u = 0; u < kGqUnroll; ++u) add(cd[u]);
+  for (int64_t i0 = i00 + kGqUnroll * stride; i0 < p.n; i0 += kGqUnroll * stride) {  // (n > one pass)
 #pragma unroll
     for (int u = 0; u < kGqUnroll; ++u) {
       const int64_t i = i0 + u * stride;
-      kk[u] = i < p.n ? key[i] : NAN;
-      cl[u] = i < p.n ? p.cap_idx[i] : 0u;
+      cd[u] = i < p.n ? code[i] : ~0u;
     }
 #pragma unroll
-    for (int u = 0; u < kGqUnroll; ++u) {
-      const double k = kk[u];
-      if (k != k) continue;
-      const int b = gq_bin(k, kmin, scale) - bb;
-      if (b >= 0 && b < NB) atomicAdd(&s_h[tid >> 6][b * 4 + (cl[u] & 3u)], 1u);
-    }
+    for (int u = 0; u < kGqUnroll; ++u) add(cd[u]);
   }
   __syncthreads();
   for (int e = tid; e < NB * 4; e += blockDim.x) {
@@ -1748,27 +1768,39 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const double*
 // K3: every block finds the crossing bin inside superbin sb (lane l = its bin l) and the candidate
 // window [b*, b_end] over the next 64 bins (the same arithmetic in every block; block 0 records it
 // and zeroes the superbin histograms); then every house of a bin below b* is taken, the rest start
-// as not taken (k_gq_finish sets the window's), the window's houses are staged per block of
-// kGqStage houses (okey, house << 2 | class, FSM word), and the ON houses of the decided (non-
-// window) houses are counted into the slab
-__global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const double* __restrict__ key,
+// as not taken (k_gq_select sets the window's), the window's houses go to win[] as (okey,
+// house << 2 | class, FSM word) at slots from one allocator atomic per block (unordered: select
+// orders them), and the ON houses of the decided (non-window) houses are counted into the slab
+__global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint32_t* __restrict__ code,
                                                            unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
-                                                           uint4* __restrict__ stage, unsigned* __restrict__ bcnt,
-                                                           uint8_t* __restrict__ action,
+                                                           uint4* __restrict__ win, uint8_t* __restrict__ action,
                                                            unsigned long long* __restrict__ slab) {
   static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
   static_assert(kGqCopies * 512 <= kGqBins * 4, "the bin copies fit below the superbin copies");
+  constexpr int NW = kGqThreads / 64;
   __shared__ unsigned s_c[128];
-  __shared__ int s_l0, s_le, s_n;
+  __shared__ int s_l0, s_le;
   __shared__ double s_base;
   __shared__ unsigned long long s_basec;
   __shared__ unsigned s_cnt[kWinCap];
-  const int tid = threadIdx.x, lane = tid & 63;
+  __shared__ unsigned s_wt[NW];
+  __shared__ unsigned s_wbase;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // this block's houses first (every load before the selection reads: they stay in flight)
+  const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
+  constexpr int U = kGqStage / kGqThreads;
+  uint32_t cd[U], hw[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = b0 + u * kGqThreads + tid;
+    cd[u] = i < p.n ? code[i] : 0u;
+    hw[u] = i < p.n ? p.hvac[i] : 0u;
+  }
   const bool all = sel->all, ovf = sel->overflow;
   const bool on = !all && !ovf;
   const int bb = sel->sb * 64;
   if (tid < kWinCap) s_cnt[tid] = 0u;
-  if (tid == 0) { s_n = 0; s_l0 = 0; s_le = 0; }
+  if (tid == 0) { s_l0 = 0; s_le = 0; }
   if (blockIdx.x == 0)  // (k_gq_bins read them; the next producer fills them again)
     for (int e = tid; e < kGqCopies * kGqSupStride; e += blockDim.x) hist[kGqBins * 4 + e] = 0u;
   if (on && tid < 128) {
@@ -1801,7 +1833,6 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const doub
     }
   }
   __syncthreads();
-  bool wovf = false;
   if (on && tid < 64) {  // the window: bins l0 .. l0 + 63 of the 128 loaded
     const int l0 = s_l0;
     const int li = l0 + lane;
@@ -1821,7 +1852,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const doub
     else if (enough) le = __ffsll((long long)enough) - 1;
     else le = 63 - __clzll((long long)fit);
     const int cnt = (int)__shfl(pre, le);
-    wovf = !(fit & 1ull);
+    const bool wovf = !(fit & 1ull);
     if (lane == 0) s_le = wovf ? -1 : le;
     if (lane == 0 && blockIdx.x == 0) {
       if (wovf) sel->overflow = 1;
@@ -1833,51 +1864,64 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const doub
     }
   }
   __syncthreads();
-  if (ovf || s_le < 0) {  // the fallback in k_gq_finish decides every house (block-uniform)
-    if (tid == 0) bcnt[blockIdx.x] = 0u;
-    return;
-  }
+  if (ovf || s_le < 0) return;  // the fallback in k_gq_select decides every house (block-uniform)
   const int bs = bb + s_l0, be = bb + s_l0 + s_le;
-  const double kmin = sel->kmin, scale = sel->scale;
-  const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
-  constexpr int U = kGqStage / kGqThreads;
-  double kk[U];
-  uint32_t hw[U];
-  unsigned cl[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {  // (every load before the first use)
-    const int64_t i = b0 + u * kGqThreads + tid;
-    kk[u] = i < p.n ? key[i] : 0.0;
-    hw[u] = i < p.n ? p.hvac[i] : 0u;
-    cl[u] = i < p.n ? p.cap_idx[i] : 0u;
-  }
   unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
+  bool inw[U];
+  unsigned mine = 0u;
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     const int64_t i = b0 + u * kGqThreads + tid;
+    const int b = (int)(cd[u] >> 2);
+    const unsigned cl = cd[u] & 3u;
     bool dec = false, take = false;  // dec: decided here (outside the window)
+    inw[u] = false;
     if (i < p.n) {
-      const double k = kk[u];
-      const int b = k == k ? gq_bin(k, kmin, scale) : kGqBins;
       take = all || b < bs;
       action[i] = take ? 1 : 0;
       dec = all || b < bs || b > be;
-      if (!dec) {
-        const unsigned slot = atomicAdd(&s_n, 1u);
-        const uint64_t ok = gq_okey(k);
-        stage[b0 + slot] = make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), ((uint32_t)i << 2) | (cl[u] & 3u), hw[u]);
-      }
+      inw[u] = !dec;
     }
+    mine += inw[u] ? 1u : 0u;
     const bool on1 = dec && hv_on(hvac_fsm(hw[u], take, p.dt, p.L));
 #pragma unroll
-    for (int c = 0; c < kWinCap; ++c) oncnt[c] += (unsigned)__popcll(__ballot(on1 && (cl[u] & 3u) == (unsigned)c));
+    for (int c = 0; c < kWinCap; ++c) oncnt[c] += (unsigned)__popcll(__ballot(on1 && cl == (unsigned)c));
   }
+  // the window houses' exact keys (issued before the allocator's round trip)
+  double kk[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) kk[u] = inw[u] ? gq_key_of(p, b0 + u * kGqThreads + tid) : 0.0;
+  unsigned x = mine;  // this lane's slots: a wave prefix, the wave's offset in the block, the block's base
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_wt[wv] = x;
   if (lane == 0)
 #pragma unroll
     for (int c = 0; c < kWinCap; ++c)
       if (oncnt[c]) atomicAdd(&s_cnt[c], oncnt[c]);
   __syncthreads();
-  if (tid == 0) bcnt[blockIdx.x] = s_n;
+  if (tid == 0) {
+    unsigned tot = 0u;
+    for (int w = 0; w < NW; ++w) {
+      const unsigned t = s_wt[w];
+      s_wt[w] = tot;
+      tot += t;
+    }
+    s_wbase = tot ? atomicAdd(&sel->wcount, tot) : 0u;
+  }
+  __syncthreads();
+  unsigned j = s_wbase + s_wt[wv] + (x - mine);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (!inw[u]) continue;
+    const uint32_t i = (uint32_t)(b0 + u * kGqThreads + tid);
+    const uint64_t ok = gq_okey(kk[u]);
+    if (j < (unsigned)kGqCap) win[j] = make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), (i << 2) | (cd[u] & 3u), hw[u]);
+    ++j;
+  }
   if (tid < p.n_cap && s_cnt[tid])
     atomicAdd(&slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)s_cnt[tid]);
 }
@@ -1885,82 +1929,6 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const doub
 __device__ __forceinline__ bool gq_less(const uint4& a, const uint4& b) {
   const uint64_t ka = ((uint64_t)a.y << 32) | a.x, kb = ((uint64_t)b.y << 32) | b.x;
   return ka < kb || (ka == kb && a.z < b.z);  // (z = house << 2 | class: house order on equal keys)
-}
-
-// K4: stage block b copies its window houses to win[offset_b ..) (offset_b: the counts of the
-// stage blocks before it), so the window becomes one contiguous array; block 0 zeroes the bin
-// histograms (k_gq_compact read them)
-__global__ void __launch_bounds__(256) k_gq_gather(const uint4* __restrict__ stage, const unsigned* __restrict__ bcnt,
-                                                   const GqSel* __restrict__ sel, uint4* __restrict__ win,
-                                                   unsigned* __restrict__ hist) {
-  __shared__ unsigned s_w[4];
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (b == 0)
-    for (int e = tid; e < kGqCopies * 512; e += blockDim.x) hist[e] = 0u;
-  if (sel->all || sel->overflow) return;
-  const unsigned c = bcnt[b];
-  if (c == 0u) return;  // (block-uniform)
-  unsigned o = 0;
-  for (int q = tid; q < b; q += blockDim.x) o += bcnt[q];
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) o += __shfl_xor(o, off);
-  if (lane == 0) s_w[wv] = o;
-  __syncthreads();
-  o = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-  for (unsigned e = tid; e < c; e += blockDim.x) win[o + e] = stage[(int64_t)b * kGqStage + e];
-}
-
-// K5 (kGqRankBlocks workgroups): the window into LDS; one wave per house computes its rank (how
-// many window houses precede it in (key, house) order, the lanes splitting the comparisons) and
-// writes it to sorted[rank]
-__global__ void __launch_bounds__(kGqRankThreads) k_gq_rank(const uint4* __restrict__ win, const GqSel* __restrict__ sel,
-                                                 uint4* __restrict__ sorted) {
-  __shared__ uint4 s_e[kGqCap];
-  if (sel->all || sel->overflow) return;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nth = blockDim.x;
-  const int ncand = sel->ncand;
-  {
-    constexpr int U = kGqCap / kGqRankThreads;  // (every load issued before the LDS stores)
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = tid + u * kGqRankThreads;
-      if (e < ncand) v[u] = win[e];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = tid + u * kGqRankThreads;
-      if (e < ncand) s_e[e] = v[u];
-    }
-  }
-  __syncthreads();
-  // each wave ranks EPW houses at once (one LDS read of a window house serves all EPW comparisons);
-  // 16 waves per CU hide the LDS latency of the comparison loop
-  constexpr int EPW = kGqCap / (kGqRankBlocks * (kGqRankThreads / 64));
-  static_assert(EPW >= 1 && EPW * kGqRankBlocks * (kGqRankThreads / 64) == kGqCap, "the launch covers the window");
-  const int nwv = (int)gridDim.x * (nth >> 6);
-  const int e0 = (int)blockIdx.x * (nth >> 6) + wv;
-  if (e0 >= ncand) return;  // (wave-uniform; no barrier follows)
-  uint4 me[EPW];
-  unsigned r[EPW];
-#pragma unroll
-  for (int j = 0; j < EPW; ++j) {
-    const int e = e0 + j * nwv;
-    me[j] = e < ncand ? s_e[e] : make_uint4(0u, 0u, 0u, 0u);
-    r[j] = 0u;
-  }
-#pragma unroll 2
-  for (int f = lane; f < ncand; f += 64) {
-    const uint4 o = s_e[f];
-#pragma unroll
-    for (int j = 0; j < EPW; ++j) r[j] += gq_less(o, me[j]) ? 1u : 0u;
-  }
-#pragma unroll
-  for (int j = 0; j < EPW; ++j) {
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) r[j] += __shfl_xor(r[j], off);
-    if (lane == 0 && e0 + j * nwv < ncand) sorted[r[j]] = me[j];
-  }
 }
 
 // the greedy take rule at one house (greedy_myopic_controller.py:93-101)
@@ -2004,8 +1972,8 @@ __device__ __forceinline__ bool gq_prefix_eq(const GqKey& c, const GqKey& pre, i
 // until the gap admits no class; (3) every house's action and the ON counts of the decided actions.
 // ~15 passes over the keys by one CU: milliseconds, for inputs the window form cannot take (a NaN
 // crossing, a crossing bin of more than kGqCap houses, a walk past the window).
-__device__ void gq_exact(const KParams& p, const double* __restrict__ key, double S, double pmin,
-                         uint8_t* __restrict__ action, unsigned long long* __restrict__ slab) {
+__device__ void gq_exact(const KParams& p, double S, double pmin, uint8_t* __restrict__ action,
+                         unsigned long long* __restrict__ slab) {
   __shared__ unsigned s_h[256 * 4];
   __shared__ double s_w[16];
   __shared__ unsigned long long s_wc[16];
@@ -2020,7 +1988,7 @@ __device__ void gq_exact(const KParams& p, const double* __restrict__ key, doubl
   double p_on[kWinCap];
 #pragma unroll
   for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
-  auto key_of = [&](int64_t i) { return GqKey{gq_okey(key[i]), (uint32_t)i}; };
+  auto key_of = [&](int64_t i) { return GqKey{gq_okey(gq_key_of(p, i)), (uint32_t)i}; };
   GqKey pre{0ull, 0u};
   double base = 0.0;
   if (tid == 0) { s_all = 0; s_ntake = 0; }
@@ -2131,15 +2099,13 @@ __device__ void gq_exact(const KParams& p, const double* __restrict__ key, doubl
   if (tid < p.n_cap) slab[tid] = s_cnt[tid];  // (shard 0; the others stay zero)
 }
 
-// K6 (one workgroup of 1024): the sorted window into LDS, the exact crossing position from
-// base_tot, the window's prefix taken, then the gap walk (k_greedy_walk's rule); the ON counts of
-// the window's decided actions; what the window cannot decide goes to gq_exact; finally this
-// call's key range becomes the next call's quantisation
-__global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __restrict__ sorted,
-                                                    const double* __restrict__ key, double S, double pmin,
-                                                    GqSel* __restrict__ sel, uint8_t* __restrict__ action,
-                                                    unsigned long long* __restrict__ slab) {
-  __shared__ uint4 s_e[kGqCap];
+// The decision on the sorted window (k_gq_select's last block): the window into LDS, the exact
+// crossing position from base_tot, the window's prefix taken, then the gap walk (k_greedy_walk's
+// rule); the ON counts of the window's decided actions; what the window cannot decide goes to
+// gq_exact; finally this call's key range becomes the next call's quantisation
+__device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, double S, double pmin,
+                          GqSel* __restrict__ sel, uint8_t* __restrict__ action,
+                          unsigned long long* __restrict__ slab, uint4* s_e) {
   __shared__ uint8_t s_tk[kGqCap];
   __shared__ double s_w[16];
   __shared__ double s_tot;
@@ -2247,13 +2213,83 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint4* __re
       if (tid < p.n_cap && s_cnt[tid]) atomicAdd(&slab[tid], (unsigned long long)s_cnt[tid]);
     }
   }
-  if (ovf) gq_exact(p, key, S, pmin, action, slab);
+  if (ovf) gq_exact(p, S, pmin, action, slab);
   if (tid == 0) {
     if (ovf) sel->fallbacks += 1;
     sel->overflow = 0;       // (the next call starts clear, with this call's key range)
     sel->kmin = sel->nkmin;  // (every kernel of this call has read the quantisation)
     sel->scale = sel->nscale;
+    sel->ticket = 0u;        // (every block of this launch has taken its ticket)
   }
+}
+
+
+// K4 (kGqSelBlocks workgroups of 1024): every block loads compact's unordered window win[0, ncand)
+// into LDS and ranks kGqCap / (kGqSelBlocks * 16) of its houses per wave (how many window houses
+// precede it in (key, house) order, the lanes splitting the comparisons; one LDS read serves all of
+// the wave's houses) into sorted[rank]; the last block to take a ticket (after a device-scope
+// fence, so every block's sorted[] is visible) then decides (gq_decide).  Block 0 zeroes the bin
+// histograms (k_gq_compact read them).
+__global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __restrict__ win, uint4* __restrict__ sorted,
+                                                    double S, double pmin, GqSel* __restrict__ sel,
+                                                    uint8_t* __restrict__ action, unsigned long long* __restrict__ slab,
+                                                    unsigned* __restrict__ hist) {
+  __shared__ uint4 s_e[kGqCap];
+  __shared__ unsigned s_last;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (blockIdx.x == 0)
+    for (int e = tid; e < kGqCopies * 512; e += blockDim.x) hist[e] = 0u;
+  const bool live = !sel->all && !sel->overflow;
+  const int ncand = sel->ncand;
+  if (live) {
+    constexpr int U = kGqCap / 1024;  // (every load issued before the LDS stores)
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + u * 1024;
+      if (e < ncand) v[u] = win[e];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + u * 1024;
+      if (e < ncand) s_e[e] = v[u];
+    }
+    __syncthreads();
+    constexpr int EPW = kGqCap / (kGqSelBlocks * 16);
+    static_assert(EPW >= 1 && EPW * kGqSelBlocks * 16 == kGqCap, "the launch covers the window");
+    constexpr int nwv = kGqSelBlocks * 16;  // (gridDim.x == kGqSelBlocks, blockDim.x == 1024)
+    const int e0 = (int)blockIdx.x * 16 + wv;
+    if (e0 < ncand) {  // (wave-uniform)
+      uint4 me[EPW];
+      unsigned r[EPW];
+#pragma unroll
+      for (int j = 0; j < EPW; ++j) {
+        const int e = e0 + j * nwv;
+        me[j] = e < ncand ? s_e[e] : make_uint4(~0u, ~0u, ~0u, 0u);
+        r[j] = 0u;
+      }
+#pragma unroll 2
+      for (int f = lane; f < ncand; f += 64) {
+        const uint4 o = s_e[f];
+#pragma unroll
+        for (int j = 0; j < EPW; ++j) r[j] += gq_less(o, me[j]) ? 1u : 0u;
+      }
+#pragma unroll
+      for (int j = 0; j < EPW; ++j) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) r[j] += __shfl_xor(r[j], off);
+        if (lane == 0 && e0 + j * nwv < ncand && r[j] < (unsigned)kGqCap) sorted[r[j]] = me[j];
+      }
+    }
+  }
+  __threadfence();  // this block's sorted[] before its ticket
+  __syncthreads();
+  if (tid == 0) s_last = atomicAdd(&sel->ticket, 1u) == gridDim.x - 1u ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;  // (block-uniform)
+  __threadfence();      // every block's sorted[] after the tickets
+  __syncthreads();
+  gq_decide(p, sorted, S, pmin, sel, action, slab, s_e);
 }
 
 // sharded greedy (mdr_greedy_inputs / mdr_greedy_select): this shard's (key, P, lockout) rows, and

@@ -75,41 +75,61 @@ def make_critic(num_state: int, layers=(100, 100)):
     return Critic()
 
 
-def discounted_returns(reward, done, gamma: float):
-    """G_i = r_i + gamma * (0 if done_i else G_{i+1}) over a 1-D float64 device tensor (the
-    reference's reversed loop, mappo.py:135-140), as a blocked parallel scan: a reverse recurrence
-    inside blocks of ~sqrt(L), the blocks' carries chained on the host, one fix-up pass."""
+def _suffix_affine(r, c):
+    """G_i = r_i + c_i * G_{i+1} with G_L = 0, over 1-D float64 tensors, without a host round trip:
+    a reverse recurrence inside ~sqrt(L) blocks of ~sqrt(L), the blocks' carries by the same scan one
+    level down (G entering block b is itself a suffix recurrence over the blocks), one fix-up pass."""
     torch = _torch()
-    L = reward.numel()
-    if L == 0:
-        return reward.clone()
-    M = max(1, int(np.ceil(np.sqrt(L))))
+    L = r.numel()
+    if L <= 64:
+        g = torch.empty_like(r)
+        nxt = r.new_zeros(())
+        for j in range(L - 1, -1, -1):
+            nxt = r[j] + c[j] * nxt
+            g[j] = nxt
+        return g
+    M = int(np.ceil(np.sqrt(L)))
     B = -(-L // M)
-    pad = B * M - L
-    r = torch.cat([reward.double(), reward.new_zeros(pad, dtype=torch.float64)]).view(B, M)
-    c = gamma * (1.0 - torch.cat([done.double(), done.new_ones(pad, dtype=torch.float64)])).view(B, M)
-    g = torch.empty_like(r)
-    nxt = torch.zeros(B, dtype=torch.float64, device=r.device)
+    pad = B * M - L  # (padding after the end: r = c = 0, so G stays 0 there)
+    r2 = torch.cat([r, r.new_zeros(pad)]).view(B, M)
+    c2 = torch.cat([c, c.new_zeros(pad)]).view(B, M)
+    g = torch.empty_like(r2)
+    nxt = r.new_zeros(B)
     for j in range(M - 1, -1, -1):  # local returns, each block as if it ended the buffer
-        nxt = r[:, j] + c[:, j] * nxt
+        nxt = r2[:, j] + c2[:, j] * nxt
         g[:, j] = nxt
-    suf = torch.flip(torch.cumprod(torch.flip(c, [1]), 1), [1])  # prod_{k >= j} c_k within the block
-    g0, s0 = g[:, 0].cpu().numpy(), suf[:, 0].cpu().numpy()
-    carry = np.zeros(B)
-    for b in range(B - 2, -1, -1):  # the return entering block b from block b + 1
-        carry[b] = g0[b + 1] + s0[b + 1] * carry[b + 1]
-    g = g + suf * torch.from_numpy(carry).to(g.device)[:, None]
-    return g.reshape(-1)[:L]
+    suf = torch.flip(torch.cumprod(torch.flip(c2, [1]), 1), [1])  # prod_{k >= j} c_k within the block
+    # carry[b] = G at the first element of block b + 1 = g[b+1, 0] + suf[b+1, 0] * carry[b+1]
+    carry = torch.cat([_suffix_affine(g[1:, 0].contiguous(), suf[1:, 0].contiguous()), r.new_zeros(1)])
+    return (g + suf * carry[:, None]).reshape(-1)[:L]
+
+
+def discounted_returns(reward, done, gamma: float):
+    """G_i = r_i + gamma * (0 if done_i else G_{i+1}) over a 1-D device tensor (the reference's
+    reversed loop, mappo.py:135-140), as the blocked scan of _suffix_affine: float64, on the
+    tensor's device, no host synchronisation."""
+    torch = _torch()
+    if reward.numel() == 0:
+        return reward.double().clone()
+    return _suffix_affine(reward.double(), gamma * (1.0 - done.double()))
 
 
 class DeviceMAPPO:
     """MAPPO with device actor rollouts, device transition storage and the PPO update on the GPU."""
 
     def __init__(self, env, config: Optional[MAPPOConfig] = None, num_action: int = 2, seed: int = 1,
-                 precision: str = "bf16x3", returns: str = "reference"):
+                 precision: str = "bf16x3", returns: str = "reference", sampler: str = "auto"):
+        """``sampler``: the minibatch permutation of each PPO epoch — "reference" draws it from the
+        global torch CPU generator exactly as the reference's SubsetRandomSampler does, "device"
+        draws it on the GPU (torch.randperm on the device generator: no L-element host permutation
+        and copy per epoch at C5's N x T transitions), "auto" = "reference" up to 2^20 transitions
+        and "device" beyond."""
         torch = _torch()
         if returns not in ("reference", "per_agent"):
             raise ValueError("returns must be 'reference' (the reference's buffer order) or 'per_agent'")
+        if sampler not in ("auto", "reference", "device"):
+            raise ValueError("sampler must be 'auto', 'reference' or 'device'")
+        self.sampler = sampler
         self.cfg = config or MAPPOConfig()
         self.env = env
         self.returns = returns
@@ -124,7 +144,7 @@ class DeviceMAPPO:
         self.actor_optimizer = torch.optim.Adam(self.actor_net.parameters(), self.cfg.lr_actor)
         self.critic_net_optimizer = torch.optim.Adam(self.critic_net.parameters(), self.cfg.lr_critic)
         self.device_actor = DeviceActor(env, self.actor_net, precision=precision)
-        self.buffer = []  # per tick: (state, action, prob, reward, next_state, done)
+        self.buffer = []  # per tick: (state, action, prob, reward, done)
         self.counter = 0
         self.training_step = 0
         self.last_actions = None
@@ -139,10 +159,11 @@ class DeviceMAPPO:
         return a
 
     def store_transition(self, observations, next_observations, rewards, done: bool) -> None:
-        """mappo.py:105-126 for all houses at once: device tensors obs / next_obs float32 [N, F],
-        rewards float [N] (the last select_actions' actions and probabilities)."""
+        """mappo.py:105-126 for all houses at once: device tensors obs float32 [N, F], rewards float
+        [N] (the last select_actions' actions and probabilities).  ``next_observations`` is accepted
+        for the reference's signature but not kept: update never reads it (mappo.py:128-217)."""
         self.buffer.append((observations, self.last_actions.clone(), self.last_probs.clone(),
-                            rewards.clone(), next_observations, bool(done)))
+                            rewards.clone(), bool(done)))
         self.counter += observations.shape[0]
 
     def __len__(self) -> int:
@@ -182,14 +203,15 @@ class DeviceMAPPO:
             self.env._comm.allreduce_sum(self.env.shard, tot)
         others = ((tot - acts) / max(n_glob - 1, 1)).float().reshape(-1, 1)  # mean of the other houses' actions
         reward = torch.stack([b[3] for b in self.buffer])  # [T, N]
-        done = torch.tensor([b[5] for b in self.buffer], dtype=torch.float64, device=reward.device)
+        done = torch.tensor([b[4] for b in self.buffer], dtype=torch.float64, device=reward.device)
         done_rows = done[:, None].expand(-1, n)
         Gt = self._returns(reward, done_rows, n).float()
         critic_in = torch.cat([state, others], 1)
+        on_device = self.sampler == "device" or (self.sampler == "auto" and L > (1 << 20))
         for _ in range(cfg.ppo_update_time):
-            # SubsetRandomSampler + BatchSampler(drop_last=False): a permutation of the global CPU
-            # generator, cut in order into batch_size chunks
-            perm = torch.randperm(L).to(state.device)
+            # SubsetRandomSampler + BatchSampler(drop_last=False): a permutation (the global CPU
+            # generator's, or the device generator's — see sampler), cut in order into batch_size chunks
+            perm = torch.randperm(L, device=state.device) if on_device else torch.randperm(L).to(state.device)
             for k in range(0, L, cfg.batch_size):
                 idx = perm[k:k + cfg.batch_size]
                 Gt_index = Gt[idx].view(-1, 1)

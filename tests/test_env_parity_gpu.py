@@ -320,7 +320,7 @@ def test_greedy_key_runs_vs_oracle(torch_gpu, form):
         ref = O.greedy(np.full(n, 23.0), np.full(n, 22.0), caps, cop, lock, S)
         np.testing.assert_array_equal(out.cpu().numpy().astype(bool), ref, err_msg=f"equal keys S={S}")
     if form == "select":
-        # the n identical keys make one bin of n houses > the window: decided by k_gq_finish's exact
+        # the n identical keys make one bin of n houses > the window: decided by k_gq_select's exact
         # in-kernel fallback (S = 1e12 takes everything: decided by the superbins)
         assert sh.greedy_fallbacks() == f0 + 1
 
@@ -487,7 +487,7 @@ def test_greedy_loop_keys_epilogue_and_counts(torch_gpu):
 
 @pytest.mark.parametrize("case", ["nan_crossing", "nan_after", "identical_crossing"])
 def test_greedy_exact_fallback(torch_gpu, case):
-    """Inputs the candidate window cannot decide go to k_gq_finish's exact in-kernel radix select
+    """Inputs the candidate window cannot decide go to k_gq_select's exact in-kernel radix select
     (no host synchronisation): a crossing among NaN keys (NaN temperatures sort last, in house order,
     as numpy's stable argsort and pandas' na_position='last' put them), NaN keys after the crossing,
     10,000 identical keys around the crossing; actions and the counted cluster power == the oracle."""

@@ -8,13 +8,13 @@ from mdr_amd.mappo import discounted_returns
 
 
 def _loop(r, d, g):
-    R, out = 0.0, []
+    R, out = 0.0, np.empty(len(r))
     for i in reversed(range(len(r))):
         if d[i]:
             R = 0.0
         R = r[i] + g * R
-        out.insert(0, R)
-    return np.array(out)
+        out[i] = R
+    return out
 
 
 def test_returns_golden_buffer():
@@ -27,7 +27,7 @@ def test_returns_golden_buffer():
 
 def test_returns_long_random():
     rs = np.random.RandomState(0)
-    for L in (1, 2, 17, 1000, 12345):
+    for L in (1, 2, 17, 65, 1000, 12345, 300001):  # (300,001: three levels of block carries)
         r = rs.normal(size=L)
         d = rs.rand(L) < 0.01
         got = discounted_returns(torch.from_numpy(r), torch.from_numpy(d), 0.97).numpy()

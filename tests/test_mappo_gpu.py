@@ -46,9 +46,11 @@ def test_mappo_update_matches_reference():
                                        err_msg=f"final {tag} {k}")
 
 
-def test_training_loop_runs_on_device():
+@pytest.mark.parametrize("sampler", ["reference", "device"])
+def test_training_loop_runs_on_device(sampler):
     """TrainingManager-style loop (training_manager.py:183-263) at 4,099 houses: select_actions ->
-    step -> store_transition -> update every epoch; the update runs and the policy moves."""
+    step -> store_transition -> update every epoch; the update runs and the policy moves (minibatch
+    permutations from the CPU generator, as the reference, or from the device generator)."""
     import torch
 
     from mdr_amd.environment import Environment
@@ -57,7 +59,7 @@ def test_training_loop_runs_on_device():
     props = gu.props_from_overrides({"cluster_prop.nb_agents": 4099,
                                      "power_grid_prop.signal_properties.mode": "sinusoidals"})
     env = Environment(props, rng=random.Random(2), population="synthetic", seed=3)
-    agent = DeviceMAPPO(env, MAPPOConfig(batch_size=4096, ppo_update_time=2))
+    agent = DeviceMAPPO(env, MAPPOConfig(batch_size=4096, ppo_update_time=2), sampler=sampler)
     w0 = agent.actor_net.fc[0].weight.detach().clone()
     obs = env.obs_tensor().clone()
     for t in range(6):
