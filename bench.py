@@ -536,6 +536,10 @@ def main():
                                      "signal) on the post-step state, then env.step, every tick")
         out["config"]["action_mode"] = "greedy_myopic"
         out["roofline"]["timing"] = "HIP events around 20 greedy+step ticks after the timed region"
+        gd = sh.greedy_diag()  # (after every timed call: it synchronises)
+        out["greedy_select"] = {"calls": gd["calls"], "fallbacks": gd["fallbacks"],
+                                "mean_window_houses": gd["window_sum"] / max(gd["calls"] - gd["fallbacks"], 1),
+                                "last_window_houses": gd["window_last"]}
     if dactor is not None:
         a = dactor.actor
         flops_house = 2 * sum(l.in_features * l.out_features for l in a.fc)  # 30,400 at F = 50

@@ -317,8 +317,34 @@ int mdr_cluster_stats(mdr_ctx* ctx, const double* reward, double* out, void* str
  * houses, e.g. identical keys; a walk past the window) the last kernel decides exactly itself.
  * With more than 4 capacity classes (or MDR_OPT_GREEDY_SORT) the full-sort form runs. */
 int mdr_ctrl_greedy(mdr_ctx* ctx, double budget, uint8_t* action, void* stream);
-/* Diagnostics (synchronises): mdr_ctrl_greedy calls decided by the exact in-kernel fallback. */
+/* Diagnostics (synchronises): mdr_ctrl_greedy calls decided by the exact in-kernel fallback;
+ * mdr_greedy_diag: out[4] = {fallbacks, histogram-select calls, sum of their candidate-window
+ * sizes, the last call's window size}. */
 int mdr_greedy_fallbacks(mdr_ctx* ctx, uint64_t* count);
+int mdr_greedy_diag(mdr_ctx* ctx, uint64_t* out);
+
+/* Sharded greedy, histogram form (per-rank work O(N/G + window)): the same
+ * select as mdr_ctrl_greedy with the caller's collectives between its stages, every rank deciding
+ * the same window:
+ *   mdr_gq_shard_begin      this shard's key codes, superbin histogram and (min, -max) key range
+ *   [caller] sum-allreduce the superbin histogram (uint32, n_super) and min-allreduce the range (2 f64)
+ *   mdr_gq_shard_bins       the crossing superbin, the next key map; this shard's bin counts
+ *   [caller] sum-allreduce the bin histogram (uint32, n_bin)
+ *   mdr_gq_shard_compact    this shard's actions below the crossing bin and its window houses:
+ *                           window = {count, 0, 0, 0} + count 16-B entries (window_bytes in all)
+ *   [caller] all-gather the ranks' windows (window_bytes each) in rank order
+ *   mdr_gq_shard_select     order the gathered window, decide it, write this shard's window actions
+ *   mdr_gq_shard_fallback   (synchronises) 1 = the window could not decide this call (a crossing
+ *                           among NaN keys or inside one bin of > 4,096 houses, a walk past the
+ *                           window): decide it with the all-gather form below instead.
+ * mdr_gq_shard_buffers exposes the device buffers the collectives work on (valid after begin). */
+int mdr_gq_shard_begin(mdr_ctx* ctx, void* stream);
+int mdr_gq_shard_buffers(mdr_ctx* ctx, void** super_hist, int64_t* n_super, void** bin_hist, int64_t* n_bin,
+                         void** range, void** window, int64_t* window_bytes);
+int mdr_gq_shard_bins(mdr_ctx* ctx, double budget, void* stream);
+int mdr_gq_shard_compact(mdr_ctx* ctx, double budget, uint8_t* action, void* stream);
+int mdr_gq_shard_select(mdr_ctx* ctx, double budget, const void* gathered, int world, uint8_t* action, void* stream);
+int mdr_gq_shard_fallback(mdr_ctx* ctx, int* need, void* stream);
 
 /* Sharded greedy (the all-gather form): mdr_greedy_inputs writes this shard's
  * rows key = -(T - target), P = cooling capacity / cop, lockout (u8); the caller all-gathers them
@@ -410,8 +436,11 @@ int mdr_interp_sum(const double* vals, int n, double multi_factor, double* out, 
 /* ncclUniqueId is 128 bytes; rank 0 creates it, the caller broadcasts it (torch.distributed). */
 int mdr_rccl_unique_id(uint8_t* id128);
 int mdr_rccl_init(mdr_ctx* ctx, const uint8_t* id128, int world, int rank);
-/* in-place allreduce on `stream`: dtype 0 = int64 sum, 1 = double sum, 2 = double max */
+/* in-place allreduce on `stream`: dtype 0 = int64 sum, 1 = double sum, 2 = double max,
+ * 3 = uint32 sum, 4 = double min */
 int mdr_rccl_allreduce(mdr_ctx* ctx, void* buf, int64_t count, int dtype, void* stream);
+/* all-gather of `bytes` per rank into recv (world x bytes, rank order) on `stream` */
+int mdr_rccl_allgather(mdr_ctx* ctx, const void* send, void* recv, int64_t bytes, void* stream);
 /* sharded multi-tick rollout, RCCL allreduce of the count slab inside the loop:
  * per tick  [phase 1 if BUFFER] -> allreduce(counts) -> phase 2 (with lookahead when possible) */
 int mdr_rollout_sharded(mdr_ctx* ctx, int n_ticks, const mdr_tick* ticks, const uint8_t* action,

@@ -101,6 +101,7 @@ struct mdr_ctx {
   size_t onb_bytes = 0, wah_bytes = 0;
   bool coef_dirty = true;
   int* d_flags = nullptr;                // [0] params_bad
+  unsigned* d_tickets = nullptr;         // k_count_window's grid_last_block counters (zero between uses)
   // rollout tick drivers
   TickArgs* d_ticks = nullptr;
   int ticks_cap = 0;
@@ -119,6 +120,9 @@ struct mdr_ctx {
   unsigned* g_hist = nullptr;
   GqSel* g_sel = nullptr;
   uint4* g_win = nullptr;                // the candidate window, unordered (k_gq_compact)
+  uint32_t* g_map = nullptr;             // the key -> bin map's cells (gq_bin; k_gq_bins writes the next)
+  unsigned* g_tickets = nullptr;         // k_gq_select's grid_last_block counters
+  double* g_range = nullptr;             // sharded select: this shard's (min, -max) key range (k_gq_range)
   uint4* g_sorted = nullptr;             // the window in (key, house) order (k_gq_select)
   int gq_parts_cap = 0;                  // g_part capacity in (min, max) pairs
   bool gq_keys_ready = false;            // keys + superbin histogram of the current state are in place
@@ -237,7 +241,7 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
     // partials buffer holds this grid
     const bool epi = gq && hot_buffer && (int)nb <= c->gq_parts_cap;
     GqOut go{};
-    if (epi) go = GqOut{gq_codes(c), c->g_part, c->g_hist, c->g_sel};
+    if (epi) go = GqOut{gq_codes(c), c->g_part, c->g_hist, c->g_sel, c->g_map};
 #define MDR_LAUNCH_PIPE(T, A, LA, G)                                                                     \
   hipLaunchKernelGGL((k_step_pipe<T, A, LA, G>), grid, dim3(256), 0, st, kp, action, tk, tkp, cur, reward, \
                      p_out, nxt, zer, go)
@@ -358,6 +362,9 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   k.q_on = c->d_tables;
   k.p_on = c->d_tables + MDR_MAX_CAP;
   if (hipMalloc(&c->d_flags, 16) != hipSuccess) return cleanup(fail(MDR_ENOMEM, "flags"));
+  if (hipMalloc(&c->d_tickets, kTicketWords * sizeof(unsigned)) != hipSuccess ||
+      hipMemset(c->d_tickets, 0, kTicketWords * sizeof(unsigned)) != hipSuccess)
+    return cleanup(fail(MDR_ENOMEM, "tickets"));
   k.params_bad = c->d_flags;
   {
     // the fast division is provably exact for dt < 2^20 s and |q_on| < 2^40 W (mdr_device.h)
@@ -444,7 +451,8 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
   hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_win);
-  hipFree(c->g_sorted);
+  hipFree(c->g_sorted); hipFree(c->g_map); hipFree(c->g_range); hipFree(c->g_tickets);
+  hipFree(c->d_tickets);
   if (c->comm) ncclCommDestroy(c->comm);
   delete c;
   return MDR_OK;
@@ -663,13 +671,16 @@ static unsigned win_grid(const mdr_ctx* c) { return blocks(blocks(c->kp.n, 64 * 
 
 // the first window's FSM count: ticks from tk (staged) or tick0 + j (tk == nullptr), from the
 // state's FSM words (w_in == nullptr) or from the end words of the previous window
+// p_only: the count kernel's last block also does the window's P-only reduce (win_reduce_last),
+// for a first window whose drivers ride on the step launch and whose shards need no allreduce
 static int launch_count(mdr_ctx* c, int mode, const uint8_t* action, int64_t act_stride, const TickArgs* tk,
                         uint64_t tick0, int K, unsigned long long* slot, uint64_t* onb, uint32_t* wah,
-                        const uint32_t* w_in, hipStream_t st) {
+                        const uint32_t* w_in, hipStream_t st, bool p_only = false) {
   const unsigned grid = win_grid(c);
+  unsigned* ticket = p_only ? c->d_tickets : nullptr;
 #define MDR_COUNT(A)                                                                                  \
   hipLaunchKernelGGL((k_count_window<A, kWinHpt>), dim3(grid), dim3(256), 0, st, c->kp, action, act_stride, tk, \
-                     tick0, K, slot, onb, wah, w_in)
+                     tick0, K, slot, onb, wah, w_in, ticket)
   if (mode == MDR_ACT_RANDOM) MDR_COUNT(MDR_ACT_RANDOM);
   else if (mode == MDR_ACT_ALWAYS_ON) MDR_COUNT(MDR_ACT_ALWAYS_ON);
   else MDR_COUNT(MDR_ACT_BUFFER);
@@ -792,12 +803,15 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     return MDR_OK;
   }
   if (!counted) {  // (counted: mdr_rollout_begin launched the count and its P-only reduce already)
+    // host_ticks: the P-only reduce of the first window (the drivers come with the step) — in the
+    // count kernel's last block on one GPU, after the shards' allreduce when sharded
     if (int rc = launch_count(c, mode, action, act_stride, host_ticks ? nullptr : tk,
-                              host_ticks ? host_ticks[0].tick : 0, wsz(0), slot(0), c->d_onb, c->d_wah, nullptr, st))
+                              host_ticks ? host_ticks[0].tick : 0, wsz(0), slot(0), c->d_onb, c->d_wah, nullptr, st,
+                              host_ticks && !comm))
       return rc;
     if (host_ticks && comm)
       RCCL_TRY(ncclAllReduce(slot(0), slot(0), (size_t)wsz(0) * kCountShards * ncap, ncclUint64, ncclSum, comm, st));
-    if (host_ticks) {  // the P-only reduce of the first window (the drivers come with the step)
+    if (host_ticks && comm) {
       hipLaunchKernelGGL(k_win_reduce, dim3(wsz(0)), dim3(64 * ncap), 0, st, kp, slot(0), wsz(0),
                          (const TickArgs*)nullptr, (double*)nullptr);
       LAUNCH_CHECK("k_win_reduce (P only)");
@@ -988,16 +1002,19 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   const int nw = (n + c->win - 1) / c->win;
   const int k0 = n / nw + (n % nw ? 1 : 0);  // window_launches' first window
   c->wslab_dirty = true;
-  rc = launch_count(c, mode, action, act_stride, nullptr, tick0, k0, c->d_wslab, c->d_onb, c->d_wah, nullptr, st);
+  // the window's P (the counts need no drivers): the matching direct mdr_rollout then launches the
+  // step kernel with the drivers as arguments (k_step_window<..., KA>), nothing in between — on one
+  // GPU the count kernel's last block reduces; sharded, the reduce follows the counts' allreduce
+  rc = launch_count(c, mode, action, act_stride, nullptr, tick0, k0, c->d_wslab, c->d_onb, c->d_wah, nullptr, st,
+                    !sharded);
   if (rc) return rc;
-  if (sharded)  // every rank's sharded per-tick class counts, summed (exact integers)
+  if (sharded) {  // every rank's sharded per-tick class counts, summed (exact integers)
     RCCL_TRY(ncclAllReduce(c->d_wslab, c->d_wslab, (size_t)k0 * kCountShards * c->kp.n_cap, ncclUint64, ncclSum,
                            c->comm, st));
-  // the window's P (the counts need no drivers): the matching direct mdr_rollout then launches the
-  // step kernel with the drivers as arguments (k_step_window<..., KA>), nothing in between
-  hipLaunchKernelGGL(k_win_reduce, dim3(k0), dim3(64 * c->kp.n_cap), 0, st, c->kp, c->d_wslab, k0,
-                     (const TickArgs*)nullptr, (double*)nullptr);
-  LAUNCH_CHECK("k_win_reduce (P only)");
+    hipLaunchKernelGGL(k_win_reduce, dim3(k0), dim3(64 * c->kp.n_cap), 0, st, c->kp, c->d_wslab, k0,
+                       (const TickArgs*)nullptr, (double*)nullptr);
+    LAUNCH_CHECK("k_win_reduce (P only)");
+  }
   c->wslab_dirty = false;
   c->begun.sharded = sharded;
   c->begun.on = true;
@@ -1145,7 +1162,8 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
   hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_win);
-  hipFree(c->g_sorted);
+  hipFree(c->g_sorted); hipFree(c->g_map); hipFree(c->g_range); hipFree(c->g_tickets);
+  c->g_map = nullptr; c->g_range = nullptr; c->g_tickets = nullptr;
   c->g_part = nullptr; c->g_hist = nullptr; c->g_sel = nullptr; c->g_win = nullptr;
   c->g_sorted = nullptr;
   c->gq_keys_ready = false;
@@ -1165,12 +1183,18 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_hist, kGqHistWords * sizeof(unsigned)));
   HIP_TRY(hipMemset(c->g_hist, 0, kGqHistWords * sizeof(unsigned)));  // (the kernels re-zero what they read)
   HIP_TRY(hipMalloc(&c->g_sel, 128));
+  HIP_TRY(hipMalloc(&c->g_map, kGqCells * sizeof(uint32_t)));
   {
     unsigned char init[128] = {};
-    gq_sel_init(init);
+    uint32_t map[kGqCells];
+    gq_sel_init(init, map);
     HIP_TRY(hipMemcpy(c->g_sel, init, 128, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->g_map, map, sizeof(map), hipMemcpyHostToDevice));
   }
-  HIP_TRY(hipMalloc(&c->g_win, kGqCap * sizeof(uint4)));
+  HIP_TRY(hipMalloc(&c->g_win, (kGqCap + 1) * sizeof(uint4)));  // (sharded: [0] = the count header)
+  HIP_TRY(hipMalloc(&c->g_range, 2 * sizeof(double)));
+  HIP_TRY(hipMalloc(&c->g_tickets, kTicketWords * sizeof(unsigned)));
+  HIP_TRY(hipMemset(c->g_tickets, 0, kTicketWords * sizeof(unsigned)));
   HIP_TRY(hipMalloc(&c->g_sorted, kGqCap * sizeof(uint4)));
   size_t b1 = 0, b2 = 0;
   HIP_TRY(greedy_sort(nullptr, b1, c->g_key, c->g_key2, c->g_idx, c->g_idx2, n, nullptr));
@@ -1184,7 +1208,7 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
 // the keys and superbin histogram of the current state (when no step epilogue prepared them)
 int launch_gq_keys(mdr_ctx* c, hipStream_t st) {
   hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_part, c->g_hist,
-                     c->g_sel);
+                     c->g_sel, c->g_map);
   LAUNCH_CHECK("k_gq_keys");
   c->gq_nparts = kGqParts;
   return MDR_OK;
@@ -1213,14 +1237,14 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
     if (!keys_ready)
       if (int rc2 = launch_gq_keys(c, st)) return rc2;
     hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, c->g_part,
-                       c->gq_nparts, budget, c->g_sel, slab);
+                       c->gq_nparts, budget, c->g_sel, slab, c->g_map);
     LAUNCH_CHECK("k_gq_bins");
     const int nstage = (n + kGqStage - 1) / kGqStage;
     hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
                        c->g_sel, c->g_win, action, slab);
     LAUNCH_CHECK("k_gq_compact");
     hipLaunchKernelGGL(k_gq_select, dim3(kGqSelBlocks), dim3(1024), 0, st, c->kp, c->g_win, c->g_sorted, budget, pmin,
-                       c->g_sel, action, slab, c->g_hist);
+                       c->g_sel, action, slab, c->g_hist, (const uint4*)nullptr, 0, c->g_tickets);
     LAUNCH_CHECK("k_gq_select");
     c->counts_ready = true;
     return MDR_OK;
@@ -1247,13 +1271,112 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   return MDR_OK;
 }
 
-int mdr_greedy_fallbacks(mdr_ctx* c, uint64_t* count) {
-  if (!c || !count) return fail(MDR_EARG, "mdr_greedy_fallbacks: null argument");
-  *count = 0;
+int mdr_greedy_diag(mdr_ctx* c, uint64_t* out) {
+  if (!c || !out) return fail(MDR_EARG, "mdr_greedy_diag: null argument");
+  for (int k = 0; k < 4; ++k) out[k] = 0;
   if (!c->g_sel) return MDR_OK;
   unsigned char h[128];
   HIP_TRY(hipMemcpy(h, c->g_sel, 128, hipMemcpyDeviceToHost));
-  *count = gq_fallbacks_of(h);
+  gq_diag_of(h, out);
+  return MDR_OK;
+}
+
+int mdr_greedy_fallbacks(mdr_ctx* c, uint64_t* count) {
+  if (!c || !count) return fail(MDR_EARG, "mdr_greedy_fallbacks: null argument");
+  uint64_t d[4];
+  if (int rc = mdr_greedy_diag(c, d)) return rc;
+  *count = d[0];
+  return MDR_OK;
+}
+
+// ---- sharded histogram select (the stages between the caller's collectives; mdr.h)
+static double greedy_pmin(const mdr_ctx* c) {
+  double pmin = INFINITY;
+  for (int k = 0; k < c->cfg.n_cap; ++k) pmin = fmin(pmin, c->cfg.cap_table[k] / c->cfg.cop);
+  return pmin;
+}
+
+int mdr_gq_shard_begin(mdr_ctx* c, void* stream) {
+  if (!c) return fail(MDR_EARG, "mdr_gq_shard_begin: null context");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_gq_shard_begin: context not bound");
+  if (c->kp.n_cap > 4) return fail(MDR_EARG, "mdr_gq_shard_begin: more than 4 capacity classes (use the all-gather form)");
+  const bool keys_ready = c->gq_keys_ready && c->g_cap >= c->kp.n;
+  drop_begun(c);
+  c->gq_keys_ready = false;
+  if (int rc = greedy_scratch(c, c->kp.n)) return rc;
+  hipStream_t st = S(stream);
+  if (!keys_ready)
+    if (int rc = launch_gq_keys(c, st)) return rc;
+  hipLaunchKernelGGL(k_gq_range, dim3(1), dim3(256), 0, st, c->g_part, c->gq_nparts, c->g_range);
+  LAUNCH_CHECK("k_gq_range");
+  return MDR_OK;
+}
+
+int mdr_gq_shard_buffers(mdr_ctx* c, void** super_hist, int64_t* n_super, void** bin_hist, int64_t* n_bin,
+                         void** range, void** window, int64_t* window_bytes) {
+  if (!c || !super_hist || !n_super || !bin_hist || !n_bin || !range || !window || !window_bytes)
+    return fail(MDR_EARG, "mdr_gq_shard_buffers: null argument");
+  if (!c->g_sel) return fail(MDR_ESTATE, "mdr_gq_shard_buffers: call mdr_gq_shard_begin first");
+  *super_hist = c->g_hist + kGqBins * 4;
+  *n_super = (int64_t)kGqCopies * (kGqSuper + 1) * 4;
+  *bin_hist = c->g_hist;
+  *n_bin = (int64_t)kGqCopies * 512;
+  *range = c->g_range;
+  *window = c->g_win;
+  *window_bytes = (int64_t)(kGqCap + 1) * (int64_t)sizeof(uint4);
+  return MDR_OK;
+}
+
+int mdr_gq_shard_bins(mdr_ctx* c, double budget, void* stream) {
+  if (!c || !c->g_sel) return fail(MDR_ESTATE, "mdr_gq_shard_bins: call mdr_gq_shard_begin first");
+  hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, S(stream), c->kp, gq_codes(c), c->g_hist,
+                     (const double*)c->g_range, -1, budget, c->g_sel, (unsigned long long*)nullptr, c->g_map);
+  LAUNCH_CHECK("k_gq_bins (sharded)");
+  return MDR_OK;
+}
+
+int mdr_gq_shard_compact(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
+  if (!c || !action) return fail(MDR_EARG, "mdr_gq_shard_compact: null argument");
+  if (!c->g_sel) return fail(MDR_ESTATE, "mdr_gq_shard_compact: call mdr_gq_shard_begin first");
+  hipStream_t st = S(stream);
+  const int nstage = (int)((c->kp.n + kGqStage - 1) / kGqStage);
+  hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
+                     c->g_sel, c->g_win + 1, action, (unsigned long long*)nullptr);
+  LAUNCH_CHECK("k_gq_compact (sharded)");
+  // the window's header {count, 0, 0, 0}: the allocator's final count
+  HIP_TRY(hipMemsetAsync(c->g_win, 0, sizeof(uint4), st));
+  HIP_TRY(hipMemcpyAsync(c->g_win, reinterpret_cast<const unsigned char*>(c->g_sel) + gq_wcount_offset(),
+                         sizeof(unsigned), hipMemcpyDeviceToDevice, st));
+  return MDR_OK;
+}
+
+int mdr_gq_shard_select(mdr_ctx* c, double budget, const void* gathered, int world, uint8_t* action, void* stream) {
+  if (!c || !gathered || !action) return fail(MDR_EARG, "mdr_gq_shard_select: null argument");
+  if (world < 1 || world > kGqMaxRanks) return fail(MDR_EARG, "mdr_gq_shard_select: 1 <= world <= 64");
+  if (!c->g_sel) return fail(MDR_ESTATE, "mdr_gq_shard_select: call mdr_gq_shard_begin first");
+  hipLaunchKernelGGL(k_gq_select, dim3(kGqSelBlocks), dim3(1024), 0, S(stream), c->kp, (const uint4*)nullptr,
+                     c->g_sorted, budget, greedy_pmin(c), c->g_sel, action, (unsigned long long*)nullptr, c->g_hist,
+                     static_cast<const uint4*>(gathered), world, c->g_tickets);
+  LAUNCH_CHECK("k_gq_select (sharded)");
+  return MDR_OK;
+}
+
+int mdr_gq_shard_fallback(mdr_ctx* c, int* need, void* stream) {
+  if (!c || !need) return fail(MDR_EARG, "mdr_gq_shard_fallback: null argument");
+  if (!c->g_sel) return fail(MDR_ESTATE, "mdr_gq_shard_fallback: call mdr_gq_shard_begin first");
+  unsigned v = 0;
+  hipStream_t st = S(stream);
+  HIP_TRY(hipMemcpyAsync(&v, reinterpret_cast<const unsigned char*>(c->g_sel) + gq_need_fb_offset(), sizeof(v),
+                         hipMemcpyDeviceToHost, st));
+  HIP_TRY(hipStreamSynchronize(st));
+  *need = v ? 1 : 0;
+  return MDR_OK;
+}
+
+int mdr_rccl_allgather(mdr_ctx* c, const void* send, void* recv, int64_t bytes, void* stream) {
+  if (!c || !send || !recv || bytes < 0) return fail(MDR_EARG, "mdr_rccl_allgather: bad argument");
+  if (!c->comm) return fail(MDR_ESTATE, "mdr_rccl_allgather: RCCL not initialised");
+  RCCL_TRY(ncclAllGather(send, recv, (size_t)bytes, ncclUint8, c->comm, S(stream)));
   return MDR_OK;
 }
 
@@ -1317,8 +1440,8 @@ int mdr_rccl_init(mdr_ctx* c, const uint8_t* id128, int world, int rank) {
 int mdr_rccl_allreduce(mdr_ctx* c, void* buf, int64_t count, int dtype, void* stream) {
   if (!c || !buf || count < 0) return fail(MDR_EARG, "mdr_rccl_allreduce: bad argument");
   if (!c->comm) return fail(MDR_ESTATE, "mdr_rccl_allreduce: RCCL not initialised");
-  ncclDataType_t t = dtype == 0 ? ncclInt64 : ncclFloat64;
-  ncclRedOp_t op = dtype == 2 ? ncclMax : ncclSum;
+  ncclDataType_t t = dtype == 0 ? ncclInt64 : dtype == 3 ? ncclUint32 : ncclFloat64;
+  ncclRedOp_t op = dtype == 2 ? ncclMax : dtype == 4 ? ncclMin : ncclSum;
   RCCL_TRY(ncclAllReduce(buf, buf, (size_t)count, t, op, c->comm, S(stream)));
   return MDR_OK;
 }

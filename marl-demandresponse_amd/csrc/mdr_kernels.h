@@ -8,6 +8,8 @@
 namespace mdr {
 
 constexpr int kCountShards = 64;  // atomic shards for the per-class ON counts
+constexpr int kTicketGroups = 64; // grid_last_block: group counters (+ 1 top), 32 words apart
+constexpr int kTicketWords = 32 * (kTicketGroups + 1);
 constexpr int kSlabs = 4;         // count slabs: ring of 3 (step path) / 4 (overlapped pipeline)
 constexpr int kObsBlock = 128;    // houses per obs tile
 constexpr int kActBangBang = 16;  // internal action modes: controller evaluated on the loaded state
@@ -85,7 +87,8 @@ struct GqOut {
   uint32_t* code;    // [n] the house's key bin << 2 | capacity class (gq_code)
   double* part;      // [grid][2] per-block (min, max) of the finite keys
   unsigned* hist;    // g_hist (the superbin copies follow its kGqBins * 4 bin words)
-  const GqSel* sel;  // this call's quantisation
+  const GqSel* sel;  // this call's key map: the cell grid (GqSel.kmin, .scale) ...
+  const uint32_t* map;  // ... and the cells' bin ranges (gq_bin)
 };
 template <int TPW, int ACT, int LA, bool GQ = false>
 __global__ void k_step_pipe(KParams p, const uint8_t* action, TickArgs tk, const TickArgs* tkp,
@@ -118,7 +121,7 @@ __global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const 
 template <int ACT, int HPT>
 __global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp,
                                uint64_t tick0, int nt, unsigned long long* slot, uint64_t* onb, uint32_t* wah,
-                               const uint32_t* w_in);
+                               const uint32_t* w_in, unsigned* ticket);
 __global__ void k_probe_stream(KParams p, double* reward);
 __global__ void k_refresh(KParams p, int* params_bad);
 __global__ void k_div_check(const double* a, const double* b, int64_t n, unsigned long long* mismatches);
@@ -152,17 +155,24 @@ constexpr int kGqCopies = 8;    // copies of the global superbin / bin histogram
 constexpr int kGqUnroll = 4;    // houses per thread per pass of k_gq_keys / k_gq_bins
 constexpr int kGqSuper = 256;   // superbins (64 bins each) of the select's first pass (+ 1 for NaN keys)
 constexpr int kGqHistWords = kGqBins * 4 + kGqCopies * (kGqSuper + 1) * 4;  // g_hist: bin copies | superbin copies
-constexpr int kGqSelBlocks = 64;  // k_gq_select grid (1024 threads each)
+constexpr int kGqCells = 256;   // cells of the key -> bin map (gq_bin)
+constexpr int kGqSelBlocks = 256;
+constexpr int kGqMaxRanks = 64;   // sharded histogram select: ranks whose windows k_gq_select gathers  // k_gq_select grid (1024 threads each: one window house per wave)
 struct GqSel;
-void gq_sel_init(void* sel128);            // host: the first call's quantisation (keys in [-32, 32])
-unsigned gq_fallbacks_of(const void* sel128);  // host: GqSel.fallbacks of a copied-back selection
-__global__ void k_gq_keys(KParams p, uint32_t* code, double* part, unsigned* hist, const GqSel* sel);
+void gq_sel_init(void* sel128, uint32_t* map);  // host: the first call's key map (uniform over [-32, 32])
+void gq_diag_of(const void* sel128, uint64_t* out);
+size_t gq_wcount_offset();   // host: byte offsets of GqSel.wcount / .need_fb (sharded select)
+size_t gq_need_fb_offset();  // host: [fallbacks, calls, sum of window sizes, last window]
+__global__ void k_gq_keys(KParams p, uint32_t* code, double* part, unsigned* hist, const GqSel* sel,
+                          const uint32_t* map);
 __global__ void k_gq_bins(KParams p, const uint32_t* code, unsigned* hist, const double* part, int nparts, double S,
-                          GqSel* sel, unsigned long long* slab);
+                          GqSel* sel, unsigned long long* slab, uint32_t* map);
 __global__ void k_gq_compact(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel, uint4* win,
                              uint8_t* action, unsigned long long* slab);
 __global__ void k_gq_select(KParams p, const uint4* win, uint4* sorted, double S, double pmin, GqSel* sel,
-                            uint8_t* action, unsigned long long* slab, unsigned* hist);
+                            uint8_t* action, unsigned long long* slab, unsigned* hist, const uint4* gathered,
+                            int world, unsigned* tickets);
+__global__ void k_gq_range(const double* part, int nparts, double* range);
 __global__ void k_greedy_inputs(KParams p, double* key, double* power, uint8_t* lock);
 __global__ void k_greedy_iota(int64_t n, int* idx);
 __global__ void k_greedy_gather_rows(int64_t n, const int* perm, const double* power, const uint8_t* lock,

@@ -88,22 +88,32 @@ __global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* 
 // ---- greedy selection state and key-histogram helpers (the k_gq_* kernels below; k_step_pipe
 // writes the keys in its GQ epilogue)
 struct GqSel {
-  double kmin, scale;            // this call's quantisation (the previous call's key range)
-  double nkmin, nscale;          // the range of this call's keys, for the next call
+  double kmin, scale;            // the key map's cell grid: cell = (k - kmin) * scale (gq_code)
   double base_tot;               // P of the houses before the window (exact for integer P)
   unsigned long long base_cnt, total;
   int sb, bstar, bend, all, overflow, more_after, ncand;
   unsigned fallbacks;            // calls decided by the exact fallback (gq_exact; diagnostics)
   unsigned wcount;               // k_gq_compact's window allocator (zeroed by k_gq_bins)
-  unsigned ticket;               // k_gq_select's block ticket (the last block resets it)
+  unsigned calls;                // diagnostics: decisions made, and the sum of their window sizes
+  unsigned need_fb;              // sharded: the window could not decide this call (host falls back)
+  unsigned long long ncand_sum;
 };
 static_assert(sizeof(GqSel) <= 128, "GqSel fits the 128-B sel buffer");
-void gq_sel_init(void* sel128) {
+void gq_sel_init(void* sel128, uint32_t* map) {
   GqSel* g = static_cast<GqSel*>(sel128);  // (a zeroed 128-B host buffer)
-  g->kmin = -32.0;
-  g->scale = (double)kGqBins / 64.0;
+  g->kmin = -32.0;                          // the first call: uniform bins over keys in [-32, 32]
+  g->scale = (double)kGqCells / 64.0;
+  for (int c = 0; c < kGqCells; ++c) map[c] = ((uint32_t)(c * (kGqBins / kGqCells)) << 16) | (uint32_t)(kGqBins / kGqCells);
 }
-unsigned gq_fallbacks_of(const void* sel128) { return static_cast<const GqSel*>(sel128)->fallbacks; }
+size_t gq_wcount_offset() { return offsetof(GqSel, wcount); }
+size_t gq_need_fb_offset() { return offsetof(GqSel, need_fb); }
+void gq_diag_of(const void* sel128, uint64_t* out) {
+  const GqSel* g = static_cast<const GqSel*>(sel128);
+  out[0] = g->fallbacks;
+  out[1] = g->calls;
+  out[2] = g->ncand_sum;
+  out[3] = (uint64_t)(int64_t)g->ncand;
+}
 
 constexpr int kGqSupN = kGqSuper + 1;  // superbins + one for NaN keys (sorted last, pandas' na_position)
 constexpr int kGqSupStride = kGqSupN * 4;
@@ -115,16 +125,25 @@ __device__ __forceinline__ uint64_t gq_okey(double k) {
   const uint64_t b = (uint64_t)__double_as_longlong(k + 0.0);
   return (b >> 63) ? ~b : (b | 0x8000000000000000ull);
 }
-// monotone non-decreasing in k for ANY (kmin, scale >= 0) — keys outside the range clamp to the end
-// bins — so a stale range (the previous call's) only costs window size, never exactness
-__device__ __forceinline__ int gq_bin(double k, double kmin, double scale) {
-  const double d = (k - kmin) * scale;
-  return d >= (double)(kGqBins - 1) ? kGqBins - 1 : (d > 0.0 ? (int)d : 0);
+// The key -> bin map (equi-depth, piecewise linear): kGqCells uniform cells over the previous
+// call's key range, cell c owning bins [B0_c, B0_c + W_c) (map[c] = B0_c << 16 | W_c, W_c >= 1,
+// the W_c summing to kGqBins) in proportion to the houses the previous call had there (k_gq_bins
+// builds the next map from this call's superbin histogram), so dense key ranges get many narrow
+// bins and the candidate window stays small.  The bin is monotone non-decreasing in k for ANY map,
+// range and scale >= 0 (keys outside the range clamp into the end cells), so a stale map only
+// costs window size, never exactness.
+__device__ __forceinline__ int gq_bin(double k, double kmin, double scale, const uint32_t* map) {
+  const double u = (k - kmin) * scale;
+  const int c = u >= (double)(kGqCells - 1) ? kGqCells - 1 : (u > 0.0 ? (int)u : 0);
+  const uint32_t m = map[c];
+  const int w = (int)(m & 0xFFFFu);
+  const double f = (u - (double)c) * (double)w;
+  return (int)(m >> 16) + (f >= (double)(w - 1) ? w - 1 : (f > 0.0 ? (int)f : 0));
 }
 // a house's code: its key bin (kGqBins for a NaN key) << 2 | its capacity class; the superbin is
 // code >> 8 (kGqBins / kGqSuper = 64 bins each; NaN keys land in superbin kGqSuper)
-__device__ __forceinline__ uint32_t gq_code(double k, double kmin, double scale, unsigned cls) {
-  return ((uint32_t)(k != k ? kGqBins : gq_bin(k, kmin, scale)) << 2) | (cls & 3u);
+__device__ __forceinline__ uint32_t gq_code(double k, double kmin, double scale, const uint32_t* map, unsigned cls) {
+  return ((uint32_t)(k != k ? kGqBins : gq_bin(k, kmin, scale, map)) << 2) | (cls & 3u);
 }
 __device__ __forceinline__ double gq_key_of(const KParams& p, int64_t i) {
   return -(p.t_air[i] - p.target[i]);  // greedy_myopic_controller.py:79
@@ -450,11 +469,14 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
   constexpr bool AB = ACT == MDR_ACT_BUFFER;
   __shared__ unsigned hist[MDR_MAX_CAP];
   __shared__ unsigned s_gq[GQ ? 4 * kGqSupStride : 1];
+  __shared__ uint32_t s_map[GQ ? kGqCells : 1];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   if (tid < p.n_cap) hist[tid] = 0;
-  if (GQ)
+  if (GQ) {
     for (int e = tid; e < 4 * kGqSupStride; e += blockDim.x) s_gq[e] = 0u;
+    for (int e = tid; e < kGqCells; e += blockDim.x) s_map[e] = gq.map[e];
+  }
   double gq_lo = INFINITY, gq_hi = -INFINITY;
   const double gq_kmin = GQ ? gq.sel->kmin : 0.0, gq_scale = GQ ? gq.sel->scale : 0.0;
   if (zero_slab && blockIdx.x == 0)
@@ -568,8 +590,8 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
     }
     if (GQ) {  // greedy_myopic_controller.py:79 on the post-step state (gq_key_of)
       const double k0 = -(Tn[0] - tg[0]), k1 = -(Tn[1] - tg[1]);
-      const uint32_t c0 = gq_code(k0, gq_kmin, gq_scale, (unsigned)cls[0]);
-      const uint32_t c1 = gq_code(k1, gq_kmin, gq_scale, (unsigned)cls[1]);
+      const uint32_t c0 = gq_code(k0, gq_kmin, gq_scale, s_map, (unsigned)cls[0]);
+      const uint32_t c1 = gq_code(k1, gq_kmin, gq_scale, s_map, (unsigned)cls[1]);
       if (valid[1]) sto(gq.code, i0 * 4u, make_uint2(c0, c1));
       else if (valid[0]) gq.code[i0] = c0;
 #pragma unroll
@@ -689,10 +711,10 @@ static_assert(kCountShards == 64, "k_win_reduce reduces the shards with one wave
 
 // Window count slot (u64 units): [slab: kWinMax][kCountShards][n_cap] | [red: kWinMax][n_cap] |
 // [rec: kWinMax][kWinRec] (double).  Producers accumulate block histograms into the sharded slab;
-// k_win_reduce (the next graph node: the kernel boundary makes every producer atomic visible — an
-// in-kernel last-block reduction would need an agent-scope release fence per block, i.e. an L2
-// write-back on this multi-XCD chip) sums the shards into red, zeroes the shards for the slot's
-// next use, and writes the tick records.
+// k_win_reduce (the next graph node: the kernel boundary makes every producer atomic visible) sums
+// the shards into red, zeroes the shards for the slot's next use, and writes the tick records; the
+// first window's P-only reduce runs instead in k_count_window's last block (win_reduce_last: the
+// shard adds are 8-B agent-scope atomics, so the hand-off needs no L2 write-back fence).
 __device__ __forceinline__ unsigned long long* win_red(unsigned long long* slot, int n_cap) {
   return slot + (size_t)kWinMax * kCountShards * n_cap;
 }
@@ -769,6 +791,83 @@ __device__ __forceinline__ void win_reduce_body(const KParams& p, unsigned long 
 __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long long* __restrict__ slot, int nt,
                                                     const TickArgs* __restrict__ tkp, double* p_out) {
   win_reduce_body(p, slot, nt, tkp ? tkp + blockIdx.x : nullptr, p_out);
+}
+
+// True in exactly one block of the grid: the last to arrive, after every block's earlier vector
+// memory operations have completed (each wave drains them, vmcnt(0), before the workgroup barrier).
+// Two-level ticket: block b adds to the counter of group b % G (G = min(grid, kTicketGroups), each
+// counter on its own 128-B line), the group's last arrival adds to one top counter, and the top's
+// last arrival is the answer; every counter is reset by the block that saw it complete.  (One
+// counter for a 2048-block grid serialises 2048 same-address atomics: ~25 us on MI355X.)
+// tickets: (kTicketGroups + 1) x 32 words, zero between launches.
+__device__ bool grid_last_block(unsigned* __restrict__ tickets) {
+  __shared__ unsigned s_last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned G = gridDim.x < (unsigned)kTicketGroups ? gridDim.x : (unsigned)kTicketGroups;
+    const unsigned g = blockIdx.x % G;
+    const unsigned gsize = (gridDim.x - g + G - 1) / G;
+    unsigned last = 0u;
+    if (__hip_atomic_fetch_add(&tickets[32 * g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u) {
+      __hip_atomic_store(&tickets[32 * g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      unsigned* top = &tickets[32 * kTicketGroups];
+      if (__hip_atomic_fetch_add(top, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == G - 1u) {
+        __hip_atomic_store(top, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        last = 1u;
+      }
+    }
+    s_last = last;
+  }
+  __syncthreads();
+  return s_last != 0u;
+}
+
+// The P-only reduce of a counted window by the count kernel's LAST block, in place of a k_win_reduce
+// launch (single GPU: no allreduce sits between the count and the reduce).  Hand-off per
+// cdna_hip_programming.md Guideline 16 / MI355X_MICROARCH.md Valid forms ("8-B agent atomics both
+// sides"): every block's shard adds (win_flush) are 8-B agent-scope atomics, drained by each wave
+// (vmcnt(0)) before the workgroup barrier and the block's agent-scope ticket add (grid_last_block);
+// the last block reads the shards only with 8-B agent-scope (sc1) loads.
+__device__ void win_reduce_last(const KParams& p, unsigned long long* __restrict__ slot, int nt,
+                                unsigned* __restrict__ ticket) {
+  __shared__ unsigned long long s_red[kWinMax * kWinCap];
+  if (!grid_last_block(ticket)) return;  // (block-uniform)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only: the loads below are sc1)
+  const int ncap = p.n_cap, ne = nt * ncap, q = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int NW = 4;  // (blockDim 256)
+  constexpr int E = kWinMax * kWinCap / NW;
+  unsigned long long v[E];
+#pragma unroll
+  for (int k = 0; k < E; ++k) {  // every load issued before the first use
+    const int e = wv + NW * k;
+    v[k] = 0ull;
+    if (e < ne) {
+      const int j = e / ncap, c = e - j * ncap;
+      v[k] = __hip_atomic_load(&slot[((size_t)j * kCountShards + q) * ncap + c], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < E; ++k) {
+    const int e = wv + NW * k;
+    if (e >= ne) break;  // (wave-uniform)
+    const int j = e / ncap, c = e - j * ncap;
+    __hip_atomic_store(&slot[((size_t)j * kCountShards + q) * ncap + c], 0ull, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);  // (the slot's next count adds into zeros)
+    unsigned long long x = v[k];
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    if (q == 0) s_red[e] = x;
+  }
+  __syncthreads();
+  for (int e = threadIdx.x; e < ne; e += blockDim.x) win_red(slot, ncap)[e] = s_red[e];
+  if ((int)threadIdx.x < nt) {
+    double p_on[kWinCap];
+#pragma unroll
+    for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < ncap ? k : 0];
+    win_rec(slot, ncap)[threadIdx.x * kWinRec] = win_power(p, s_red + threadIdx.x * ncap, p_on);
+  }
 }
 
 // the wave tile: 64 * HPT consecutive houses, house slot h of lane l = i0 + 64 h
@@ -934,7 +1033,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
                                                       int64_t act_stride, const TickArgs* __restrict__ tkp,
                                                       uint64_t tick0, int nt, unsigned long long* __restrict__ slot,
                                                       uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
-                                                      const uint32_t* __restrict__ w_in) {
+                                                      const uint32_t* __restrict__ w_in, unsigned* __restrict__ ticket) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
@@ -954,6 +1053,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
     if (t.v[h]) wah[t.i0 + 64u * h] = w[h];
   __syncthreads();
   win_flush(p, nt, s_cnt, slot);
+  if (ticket) win_reduce_last(p, slot, nt, ticket);  // (ticket: the P-only reduce, see win_reduce_last)
 }
 
 // Per-window affine transition of one house (FORM = MDR_THERMAL_AFFINE).  The reference's update
@@ -1221,7 +1321,8 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
   MDR_INST_WIN_F(A, true, false, MDR_THERMAL_AFFINE) MDR_INST_WIN_F(A, false, false, MDR_THERMAL_AFFINE)        \
   MDR_INST_WIN_F(A, true, true, MDR_THERMAL_AFFINE) MDR_INST_WIN_F(A, false, true, MDR_THERMAL_AFFINE)          \
   template __global__ void k_count_window<A, kWinHpt>(KParams, const uint8_t*, int64_t, const TickArgs*, uint64_t, \
-                                                      int, unsigned long long*, uint64_t*, uint32_t*, const uint32_t*);
+                                                      int, unsigned long long*, uint64_t*, uint32_t*, const uint32_t*, \
+                                                      unsigned*);
 MDR_INST_WIN(MDR_ACT_RANDOM)
 MDR_INST_WIN(MDR_ACT_ALWAYS_ON)
 MDR_INST_WIN(MDR_ACT_BUFFER)
@@ -1610,10 +1711,13 @@ __global__ void __launch_bounds__(256) k_greedy_walk(int64_t n, const double* __
 // per superbin (kGqBins / kGqSuper consecutive bins; NaN keys in their own) under this call's
 // quantisation
 __global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, uint32_t* __restrict__ code, double* __restrict__ part,
-                                                        unsigned* __restrict__ hist, const GqSel* __restrict__ sel) {
+                                                        unsigned* __restrict__ hist, const GqSel* __restrict__ sel,
+                                                        const uint32_t* __restrict__ map) {
   constexpr int NW = kGqThreads / 64;
   __shared__ unsigned s_sh[NW * kGqSupStride];  // one copy per wave (less atomic contention on hot superbins)
+  __shared__ uint32_t s_map[kGqCells];
   for (int e = threadIdx.x; e < NW * kGqSupStride; e += blockDim.x) s_sh[e] = 0u;
+  for (int e = threadIdx.x; e < kGqCells; e += blockDim.x) s_map[e] = map[e];
   __syncthreads();
   const double kmin = sel->kmin, scale = sel->scale;
   double lo = INFINITY, hi = -INFINITY;
@@ -1635,7 +1739,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, uint32_t* __r
       const int64_t i = i0 + u * stride;
       if (i >= p.n) break;
       const double k = -(ta[u] - tg[u]);  // gq_key_of
-      const uint32_t c = gq_code(k, kmin, scale, cl[u]);
+      const uint32_t c = gq_code(k, kmin, scale, s_map, cl[u]);
       code[i] = c;
       if (k == k) {
         lo = fmin(lo, k);
@@ -1646,6 +1750,28 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, uint32_t* __r
   }
   __syncthreads();
   gq_flush(s_sh, NW, hist, lo, hi, part);
+}
+
+// sharded histogram select: this shard's finite key range from the producer's per-block parts, as
+// (min, -max), so ONE min-allreduce gives the cluster's (k_gq_bins with nparts < 0); one block
+__global__ void __launch_bounds__(256) k_gq_range(const double* __restrict__ part, int nparts, double* __restrict__ range) {
+  __shared__ double s_lo[4], s_hi[4];
+  double lo = INFINITY, hi = -INFINITY;
+  for (int b = threadIdx.x; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, off));
+    hi = fmax(hi, __shfl_xor(hi, off));
+  }
+  if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 4; ++w) { lo = fmin(lo, s_lo[w]); hi = fmax(hi, s_hi[w]); }
+    lo = fmin(lo, s_lo[0]);
+    hi = fmax(hi, s_hi[0]);
+    range[0] = lo;
+    range[1] = -hi;
+  }
 }
 
 // a block-wide inclusive scan of (double P, u64 count) over the first n <= blockDim.x threads
@@ -1665,15 +1791,15 @@ __device__ __forceinline__ void gq_block_scan(double& x, unsigned long long& xc,
 
 // K2: every block first finds the crossing superbin itself (the cumulative P where it reaches S;
 // the same arithmetic in every block, so every block agrees), block 0 records it and the next
-// call's key range and zeroes the current count slab (compact and select fill it) and the window
-// allocator; then the class counts of the bins of superbins sb and sb + 1 (the crossing superbin
+// call's key map (gq_bin) and zeroes the current count slab (compact and select fill it) and the
+// window allocator; then the class counts of the bins of superbins sb and sb + 1 (the crossing superbin
 // and the room after it).  The block's codes are loaded first: they stay in flight through the scan.
 __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_t* __restrict__ code,
                                                         unsigned* __restrict__ hist, const double* __restrict__ part,
                                                         int nparts, double S, GqSel* __restrict__ sel,
-                                                        unsigned long long* __restrict__ slab) {
+                                                        unsigned long long* __restrict__ slab, uint32_t* __restrict__ map) {
   constexpr int NB = 2 * (kGqBins / kGqSuper), NW = kGqThreads / 64;
-  static_assert(kGqSupN <= kGqThreads, "one superbin per thread");
+  static_assert(kGqSupN <= kGqThreads && kGqCells < kGqThreads, "one superbin / cell edge per thread");
   __shared__ unsigned s_h[NW][NB * 4];
   __shared__ double s_w[NW];
   __shared__ unsigned long long s_wc[NW];
@@ -1715,26 +1841,66 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_
       sel->all = sb >= kGqSupN;
       sel->overflow = sb == kGqSuper;  // the crossing among NaN keys: the fallback orders them by house
       sel->wcount = 0u;
+      sel->need_fb = 0u;
     }
-    // the next call's range: (min, max) of this call's finite keys
+    // the next call's map: cells over this call's finite key range [min, max], each cell's bins in
+    // proportion to this call's houses there — the superbin CDF (linear inside a superbin) at the
+    // cell edges, read through this call's map
+    __shared__ double s_lo[NW], s_hi[NW], s_rng[2];
+    __shared__ double s_pre[kGqSuper], s_cnt[kGqSuper], s_C[kGqCells + 1];
+    __shared__ uint32_t s_map[kGqCells];
+    if (tid < kGqSuper) { s_pre[tid] = (double)(xc - cs); s_cnt[tid] = (double)cs; }
+    if (tid < kGqCells) s_map[tid] = map[tid];
     double lo = INFINITY, hi = -INFINITY;
-    for (int b = tid; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
+    if (nparts < 0) {  // sharded: the cluster's range, allreduced as (min, -max) (k_gq_range)
+      if (tid == 0) { lo = part[0]; hi = -part[1]; }
+    } else {
+      for (int b = tid; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
+    }
 #pragma unroll
     for (int off = 32; off > 0; off >>= 1) {
       lo = fmin(lo, __shfl_xor(lo, off));
       hi = fmax(hi, __shfl_xor(hi, off));
     }
-    __shared__ double s_lo[NW], s_hi[NW];
     if ((tid & 63) == 0) { s_lo[tid >> 6] = lo; s_hi[tid >> 6] = hi; }
     __syncthreads();
     if (tid == 0) {
       double kmin = s_lo[0], kmax = s_hi[0];
       for (int w = 1; w < NW; ++w) { kmin = fmin(kmin, s_lo[w]); kmax = fmax(kmax, s_hi[w]); }
       const double range = kmax - kmin;
-      sel->nkmin = kmin == kmin && kmin < INFINITY ? kmin : 0.0;
-      sel->nscale = range > 0.0 && range < INFINITY ? (double)kGqBins / range : 0.0;
+      s_rng[0] = kmin == kmin && kmin < INFINITY ? kmin : 0.0;
+      s_rng[1] = range > 0.0 && range < INFINITY ? (double)kGqCells / range : 0.0;
     }
-    for (int e = tid; e < kCountShards * p.n_cap; e += blockDim.x) slab[e] = 0ull;
+    __syncthreads();
+    const double okmin = sel->kmin, oscale = sel->scale, nkmin = s_rng[0], nscale = s_rng[1];
+    if (tid <= kGqCells) {
+      double C = 0.0;
+      if (nscale > 0.0) {
+        const double u = (nkmin + (double)tid / nscale - okmin) * oscale;  // the edge, in this call's cells
+        const int c = u >= (double)(kGqCells - 1) ? kGqCells - 1 : (u > 0.0 ? (int)u : 0);
+        const uint32_t m = s_map[c];
+        const double f = fmin(fmax(u - (double)c, 0.0), 1.0);
+        const double sp = ((double)(m >> 16) + f * (double)(m & 0xFFFFu)) / (double)(kGqBins / kGqSuper);
+        const int sc = sp >= (double)(kGqSuper - 1) ? kGqSuper - 1 : (sp > 0.0 ? (int)sp : 0);
+        C = s_pre[sc] + fmin(fmax(sp - (double)sc, 0.0), 1.0) * s_cnt[sc];
+      }
+      s_C[tid] = C;
+    }
+    __syncthreads();
+    if (tid < kGqCells) {  // B0_g = g + floor(K (C_g - C_0) / (C_G - C_0)): non-decreasing in g, so W_g >= 1
+      constexpr int K = kGqBins - kGqCells;
+      const double T = s_C[kGqCells] - s_C[0];
+      auto edge = [&](int g) {
+        if (g >= kGqCells) return kGqBins;
+        if (!(T > 0.0)) return g * (kGqBins / kGqCells);  // (no spread seen: uniform cells)
+        return g + min(K, (int)((double)K * ((s_C[g] - s_C[0]) / T)));
+      };
+      const int b0 = edge(tid), b1 = edge(tid + 1);
+      map[tid] = ((uint32_t)b0 << 16) | (uint32_t)(b1 - b0);
+    }
+    if (tid == 0) { sel->kmin = nkmin; sel->scale = nscale; }  // (no later kernel of this call maps keys)
+    if (slab)
+      for (int e = tid; e < kCountShards * p.n_cap; e += blockDim.x) slab[e] = 0ull;
   }
   if (sb >= kGqSuper) return;  // everything taken, or a NaN crossing (block-uniform)
   for (int e = tid; e < NW * NB * 4; e += blockDim.x) (&s_h[0][0])[e] = 0u;
@@ -1917,13 +2083,26 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (!inw[u]) continue;
-    const uint32_t i = (uint32_t)(b0 + u * kGqThreads + tid);
+    const uint32_t i = (uint32_t)(p.goff + b0 + u * kGqThreads + tid);  // (global id: the order's tie-break)
     const uint64_t ok = gq_okey(kk[u]);
     if (j < (unsigned)kGqCap) win[j] = make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), (i << 2) | (cd[u] & 3u), hw[u]);
     ++j;
   }
-  if (tid < p.n_cap && s_cnt[tid])
+  if (slab && tid < p.n_cap && s_cnt[tid])
     atomicAdd(&slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)s_cnt[tid]);
+}
+
+// 16-B window entries handed between workgroups of one launch as two 8-B agent-scope (sc1) accesses
+__device__ __forceinline__ void gq_store_sc1(uint4* d, const uint4& v) {
+  unsigned long long* q = reinterpret_cast<unsigned long long*>(d);
+  __hip_atomic_store(q, ((unsigned long long)v.y << 32) | v.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(q + 1, ((unsigned long long)v.w << 32) | v.z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ uint4 gq_load_sc1(const uint4* s) {
+  const unsigned long long* q = reinterpret_cast<const unsigned long long*>(s);
+  const unsigned long long a = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const unsigned long long b = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  return make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)b, (uint32_t)(b >> 32));
 }
 
 __device__ __forceinline__ bool gq_less(const uint4& a, const uint4& b) {
@@ -2102,10 +2281,11 @@ __device__ void gq_exact(const KParams& p, double S, double pmin, uint8_t* __res
 // The decision on the sorted window (k_gq_select's last block): the window into LDS, the exact
 // crossing position from base_tot, the window's prefix taken, then the gap walk (k_greedy_walk's
 // rule); the ON counts of the window's decided actions; what the window cannot decide goes to
-// gq_exact; finally this call's key range becomes the next call's quantisation
+// gq_exact (sharded: to the host, GqSel.need_fb — one shard cannot order the whole cluster).  The
+// window carries global house ids: only this shard's houses are written (offset p.goff).
 __device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, double S, double pmin,
                           GqSel* __restrict__ sel, uint8_t* __restrict__ action,
-                          unsigned long long* __restrict__ slab, uint4* s_e) {
+                          unsigned long long* __restrict__ slab, uint4* s_e, bool sharded, bool ovf0) {
   __shared__ uint8_t s_tk[kGqCap];
   __shared__ double s_w[16];
   __shared__ double s_tot;
@@ -2121,7 +2301,7 @@ __device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restr
     return cl == 0u ? pon[0] : cl == 1u ? pon[1] : cl == 2u ? pon[2] : pon[3];
   };
   const bool all = sel->all;
-  bool ovf = sel->overflow;
+  bool ovf = ovf0;
   if (!all && !ovf) {
     const int ncand = sel->ncand;
     {
@@ -2130,7 +2310,7 @@ __device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restr
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = tid + u * 1024;
-        if (e < ncand) v[u] = sorted[e];
+        if (e < ncand) v[u] = gq_load_sc1(sorted + e);  // (sc1: written by other workgroups of this launch)
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -2198,7 +2378,8 @@ __device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restr
         if (j < ncand) {
           const uint4 e = s_e[j];
           const bool take = s_tk[j] != 0;
-          if (take) action[e.z >> 2] = 1;
+          const int64_t li = (int64_t)(e.z >> 2) - p.goff;
+          if (take && li >= 0 && li < p.n) action[li] = 1;
           cl = e.z & 3u;
           on1 = hv_on(hvac_fsm(e.w, take, p.dt, p.L));
         }
@@ -2210,16 +2391,16 @@ __device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restr
         for (int c = 0; c < kWinCap; ++c)
           if (oncnt[c]) atomicAdd(&s_cnt[c], oncnt[c]);
       __syncthreads();
-      if (tid < p.n_cap && s_cnt[tid]) atomicAdd(&slab[tid], (unsigned long long)s_cnt[tid]);
+      if (slab && tid < p.n_cap && s_cnt[tid]) atomicAdd(&slab[tid], (unsigned long long)s_cnt[tid]);
     }
   }
-  if (ovf) gq_exact(p, S, pmin, action, slab);
+  if (ovf && !sharded) gq_exact(p, S, pmin, action, slab);
   if (tid == 0) {
     if (ovf) sel->fallbacks += 1;
-    sel->overflow = 0;       // (the next call starts clear, with this call's key range)
-    sel->kmin = sel->nkmin;  // (every kernel of this call has read the quantisation)
-    sel->scale = sel->nscale;
-    sel->ticket = 0u;        // (every block of this launch has taken its ticket)
+    if (ovf && sharded) sel->need_fb = 1u;
+    sel->overflow = 0;       // (the next call starts clear)
+    sel->calls += 1u;
+    if (!all && !ovf) sel->ncand_sum += (unsigned long long)sel->ncand;
   }
 }
 
@@ -2227,27 +2408,53 @@ __device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restr
 // K4 (kGqSelBlocks workgroups of 1024): every block loads compact's unordered window win[0, ncand)
 // into LDS and ranks kGqCap / (kGqSelBlocks * 16) of its houses per wave (how many window houses
 // precede it in (key, house) order, the lanes splitting the comparisons; one LDS read serves all of
-// the wave's houses) into sorted[rank]; the last block to take a ticket (after a device-scope
-// fence, so every block's sorted[] is visible) then decides (gq_decide).  Block 0 zeroes the bin
-// histograms (k_gq_compact read them).
+// the wave's houses) into sorted[rank]; the last block to take a ticket (sc1 hand-off below: every
+// block's sorted[] is visible to it) then decides (gq_decide).  Block 0 zeroes the bin
+// histograms (k_gq_compact read them).  Sharded (gathered != null): the window is the ranks'
+// all-gathered windows, rank r's at gathered[r * (kGqCap + 1)]: {count, -, -, -} then its entries.
 __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __restrict__ win, uint4* __restrict__ sorted,
                                                     double S, double pmin, GqSel* __restrict__ sel,
                                                     uint8_t* __restrict__ action, unsigned long long* __restrict__ slab,
-                                                    unsigned* __restrict__ hist) {
+                                                    unsigned* __restrict__ hist, const uint4* __restrict__ gathered,
+                                                    int world, unsigned* __restrict__ tickets) {
   __shared__ uint4 s_e[kGqCap];
-  __shared__ unsigned s_last;
+  __shared__ int s_off[kGqMaxRanks + 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   if (blockIdx.x == 0)
     for (int e = tid; e < kGqCopies * 512; e += blockDim.x) hist[e] = 0u;
-  const bool live = !sel->all && !sel->overflow;
+  bool ovf0 = sel->overflow;
+  bool live = !sel->all && !ovf0;
   const int ncand = sel->ncand;
+  if (gathered) {  // the ranks' window offsets (the counts must add up to the cluster's ncand)
+    if (tid == 0) {
+      int o = 0;
+      for (int r = 0; r < world; ++r) {
+        s_off[r] = o;
+        o += (int)gathered[(size_t)r * (kGqCap + 1)].x;
+      }
+      s_off[world] = o;
+    }
+    __syncthreads();
+    if (live && s_off[world] != ncand) {  // (block-uniform; cannot happen with consistent histograms)
+      live = false;
+      ovf0 = true;  // (decided by the host's fallback)
+    }
+  }
   if (live) {
     constexpr int U = kGqCap / 1024;  // (every load issued before the LDS stores)
     uint4 v[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int e = tid + u * 1024;
-      if (e < ncand) v[u] = win[e];
+      if (e < ncand) {
+        if (gathered) {
+          int r = 0;
+          while (r + 1 < world && s_off[r + 1] <= e) ++r;
+          v[u] = gathered[(size_t)r * (kGqCap + 1) + 1 + (e - s_off[r])];
+        } else {
+          v[u] = win[e];
+        }
+      }
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -2278,18 +2485,17 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
       for (int j = 0; j < EPW; ++j) {
 #pragma unroll
         for (int off = 32; off > 0; off >>= 1) r[j] += __shfl_xor(r[j], off);
-        if (lane == 0 && e0 + j * nwv < ncand && r[j] < (unsigned)kGqCap) sorted[r[j]] = me[j];
+        if (lane == 0 && e0 + j * nwv < ncand && r[j] < (unsigned)kGqCap) gq_store_sc1(sorted + r[j], me[j]);
       }
     }
   }
-  __threadfence();  // this block's sorted[] before its ticket
-  __syncthreads();
-  if (tid == 0) s_last = atomicAdd(&sel->ticket, 1u) == gridDim.x - 1u ? 1u : 0u;
-  __syncthreads();
-  if (!s_last) return;  // (block-uniform)
-  __threadfence();      // every block's sorted[] after the tickets
-  __syncthreads();
-  gq_decide(p, sorted, S, pmin, sel, action, slab, s_e);
+  // the hand-off to the last block (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md
+  // Valid forms): every sorted[] store is sc1 and drained by its wave before the workgroup barrier
+  // and the block's agent-scope ticket add (grid_last_block); the last block loads sorted[] only
+  // with sc1 loads (gq_decide), so no fence is needed
+  if (!grid_last_block(tickets)) return;  // (block-uniform)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only)
+  gq_decide(p, sorted, S, pmin, sel, action, slab, s_e, gathered != nullptr, ovf0);
 }
 
 // sharded greedy (mdr_greedy_inputs / mdr_greedy_select): this shard's (key, P, lockout) rows, and

@@ -130,8 +130,15 @@ SIGNATURES = {
     "mdr_msg_pack": (I, [VP, P(mdr_obs_spec), VP, VP]),
     "mdr_ctrl_greedy": (I, [VP, D, VP, VP]),
     "mdr_greedy_fallbacks": (I, [VP, VP]),
+    "mdr_greedy_diag": (I, [VP, VP]),
     "mdr_greedy_inputs": (I, [VP, VP, VP, VP, VP]),
     "mdr_greedy_select": (I, [VP, I64, VP, VP, VP, D, VP, VP]),
+    "mdr_gq_shard_begin": (I, [VP, VP]),
+    "mdr_gq_shard_buffers": (I, [VP, VP, VP, VP, VP, VP, VP, VP]),
+    "mdr_gq_shard_bins": (I, [VP, D, VP]),
+    "mdr_gq_shard_compact": (I, [VP, D, VP, VP]),
+    "mdr_gq_shard_select": (I, [VP, D, VP, I, VP, VP]),
+    "mdr_gq_shard_fallback": (I, [VP, VP, VP]),
     "mdr_cluster_stats": (I, [VP, VP, VP, VP]),
     "mdr_actor_load": (I, [VP, P(mdr_actor_spec), VP, VP, VP, VP, VP, VP, VP]),
     "mdr_actor_act": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, U64, VP, VP, VP, VP, I, VP]),
@@ -145,6 +152,7 @@ SIGNATURES = {
     "mdr_rccl_unique_id": (I, [VP]),
     "mdr_rccl_init": (I, [VP, VP, I, I]),
     "mdr_rccl_allreduce": (I, [VP, VP, I64, I, VP]),
+    "mdr_rccl_allgather": (I, [VP, VP, VP, I64, VP]),
     "mdr_rollout_sharded": (I, [VP, I, VP, VP, I64, I, VP, I64, VP, VP]),
     "mdr_rollout_sharded_mode": (I, [VP, P(I), P(I)]),
     "mdr_probe_stream": (I, [VP, VP, VP]),

@@ -71,6 +71,23 @@ class RcclComm:
         """In-place double max over ranks of a device tensor."""
         L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, L.ptr(t), t.numel(), 2, shard.stream()), "allreduce max")
 
+    def allreduce_min(self, shard, t) -> None:
+        """In-place double min over ranks of a device tensor."""
+        L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, L.ptr(t), t.numel(), 4, shard.stream()), "allreduce min")
+
+    def allreduce_count32(self, shard, t) -> None:
+        """In-place sum over ranks of a 32-bit count tensor (uint32 counts viewed as int32)."""
+        L.check(shard.lib.mdr_rccl_allreduce(shard.ctx, L.ptr(t), t.numel(), 3, shard.stream()), "allreduce u32")
+
+    def allgather_bytes(self, shard, t):
+        """The ranks' equal-size uint8 device tensors, concatenated in rank order."""
+        import torch
+
+        out = torch.empty(self.world * t.numel(), dtype=torch.uint8, device=shard.device)
+        L.check(shard.lib.mdr_rccl_allgather(shard.ctx, L.ptr(t), L.ptr(out), t.numel(), shard.stream()),
+                "allgather")
+        return out
+
     def rollout(self, shard, ticks, actions, mode, rewards, rew_stride) -> None:
         n = shard.n
         L.check(shard.lib.mdr_rollout_sharded(shard.ctx, len(ticks), ticks.ptr(), L.ptr(actions),
@@ -174,6 +191,19 @@ class TorchComm(RcclComm):
 
     def allreduce_max(self, shard, t) -> None:
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+
+    def allreduce_min(self, shard, t) -> None:
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+
+    def allreduce_count32(self, shard, t) -> None:
+        self.dist.all_reduce(t)
+
+    def allgather_bytes(self, shard, t):
+        import torch
+
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t.contiguous())
+        return torch.cat(parts)
 
     def pipeline(self, shard) -> dict:
         return {"mode": "torch.distributed per-step"}

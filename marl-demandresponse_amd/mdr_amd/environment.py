@@ -189,6 +189,8 @@ class Environment:
         if world > 1 and comm is None:
             raise ValueError("a multi-shard Environment needs a comm (mdr_amd.distributed)")
         self._comm = comm
+        self._gq_shard_fallbacks = 0  # sharded histogram-select calls decided by the all-gather form
+        self._gq_force_sharded = False  # tests: the sharded greedy stages at world 1 (RCCL to self)
         self._device = device
         self._shard_factory = _shard_factory
         self._shard: Optional[HipShard] = None
@@ -618,10 +620,25 @@ class Environment:
         sh = self._shard
         if out is None:
             out = torch.empty(self._n_local, dtype=torch.uint8, device=sh.device)
-        if self.world > 1:
-            # the cluster-wide order needs every house: all-gather this shard's (key, P, lockout)
-            # rows in global order, the same selection on every rank, keep this shard's slice
-            # 
+        if self.world > 1 or (self._gq_force_sharded and self._comm is not None):
+            if self._hist_greedy_ok():
+                # histogram select with the cluster's histograms: every rank
+                # decides the same ≤ 4,096-house window, per-rank work O(N/G + window)
+                S = float(self.power_grid.current_signal)
+                v = sh.gq_shard_begin()
+                self._comm.allreduce_count32(sh, v["super"])
+                self._comm.allreduce_min(sh, v["range"])
+                sh.gq_shard_bins(S)
+                self._comm.allreduce_count32(sh, v["bins"])
+                sh.gq_shard_compact(S, out)
+                gathered = self._comm.allgather_bytes(sh, v["window"])
+                sh.gq_shard_select(S, gathered, self.world, out)
+                if not sh.gq_shard_fallback():
+                    return out
+                self._gq_shard_fallbacks += 1
+            # the all-gather form (and the histogram form's fallback): all-gather this shard's
+            # (key, P, lockout) rows in global order, the same selection on every rank, keep this
+            # shard's slice
             nl = self._n_local
             key = torch.empty(nl, dtype=torch.float64, device=sh.device)
             pw = torch.empty(nl, dtype=torch.float64, device=sh.device)
@@ -636,6 +653,12 @@ class Environment:
         sh.greedy(float(self.power_grid.current_signal), out)
         self._counts_ready = ("greedy", out.data_ptr())
         return out
+
+    def _hist_greedy_ok(self) -> bool:
+        """The sharded histogram select applies: ≤ 4 capacity classes, ≤ 64 ranks, and a shard and
+        comm that implement its stages."""
+        return (self.world <= 64 and len(self._cap_values) <= 4 and hasattr(self._shard, "gq_shard_begin")
+                and hasattr(self._comm, "allgather_bytes"))
 
     def rollout_stream(self):
         """Stream the step launches of ``rollout`` are issued on (for HIP-event timing)."""

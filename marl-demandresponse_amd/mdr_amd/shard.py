@@ -220,11 +220,51 @@ class HipShard:
         L.check(self.lib.mdr_ctrl_greedy(self.ctx, float(budget), L.ptr(action), self.stream()),
                 "mdr_ctrl_greedy")
 
+    # ---- sharded histogram select (mdr_gq_shard_*): the stages between the comm's collectives
+    def gq_shard_begin(self) -> dict:
+        """This shard's key codes, superbin histogram and key range; returns zero-copy views of the
+        buffers the collectives work on: super / bins (int32 views of the uint32 class-count
+        histograms: sum-allreduce), range ((min, -max): min-allreduce), window (uint8: all-gather)."""
+        from .distributed import device_view
+
+        L.check(self.lib.mdr_gq_shard_begin(self.ctx, self.stream()), "mdr_gq_shard_begin")
+        sp, bp, rp, wp = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+        ns, nb, wb = C.c_int64(), C.c_int64(), C.c_int64()
+        L.check(self.lib.mdr_gq_shard_buffers(self.ctx, C.byref(sp), C.byref(ns), C.byref(bp), C.byref(nb),
+                                              C.byref(rp), C.byref(wp), C.byref(wb)), "mdr_gq_shard_buffers")
+        return {"super": device_view(sp.value, ns.value, "<i4", self.device),
+                "bins": device_view(bp.value, nb.value, "<i4", self.device),
+                "range": device_view(rp.value, 2, "<f8", self.device),
+                "window": device_view(wp.value, wb.value, "|u1", self.device)}
+
+    def gq_shard_bins(self, budget: float):
+        L.check(self.lib.mdr_gq_shard_bins(self.ctx, float(budget), self.stream()), "mdr_gq_shard_bins")
+
+    def gq_shard_compact(self, budget: float, action):
+        L.check(self.lib.mdr_gq_shard_compact(self.ctx, float(budget), L.ptr(action), self.stream()),
+                "mdr_gq_shard_compact")
+
+    def gq_shard_select(self, budget: float, gathered, world: int, action):
+        L.check(self.lib.mdr_gq_shard_select(self.ctx, float(budget), L.ptr(gathered), int(world), L.ptr(action),
+                                             self.stream()), "mdr_gq_shard_select")
+
+    def gq_shard_fallback(self) -> bool:
+        """True when this call's window could not decide (synchronises): use the all-gather form."""
+        v = C.c_int()
+        L.check(self.lib.mdr_gq_shard_fallback(self.ctx, C.byref(v), self.stream()), "mdr_gq_shard_fallback")
+        return bool(v.value)
+
     def greedy_fallbacks(self) -> int:
         """mdr_ctrl_greedy calls whose histogram select fell back to the full sort (mdr_greedy_fallbacks)."""
         v = C.c_uint64()
         L.check(self.lib.mdr_greedy_fallbacks(self.ctx, C.byref(v)), "mdr_greedy_fallbacks")
         return int(v.value)
+
+    def greedy_diag(self) -> dict:
+        """Histogram-select diagnostics (mdr_greedy_diag; synchronises)."""
+        v = (C.c_uint64 * 4)()
+        L.check(self.lib.mdr_greedy_diag(self.ctx, v), "mdr_greedy_diag")
+        return {"fallbacks": int(v[0]), "calls": int(v[1]), "window_sum": int(v[2]), "window_last": int(v[3])}
 
     def obs(self, spec, scalars, out, use_p_dev=True):
         L.check(self.lib.mdr_obs(self.ctx, C.byref(spec), C.byref(scalars),

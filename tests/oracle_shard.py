@@ -157,6 +157,121 @@ class OracleShard:
                 act[i] = 1
         action.copy_(torch.from_numpy(act))
 
+    # ---- the sharded histogram select's stages (the protocol of HipShard.gq_shard_*: what is
+    # allreduced and gathered between them), restated with NumPy: uniform bins over the previous
+    # call's cluster key range, 32 superbins of 32 bins (+ a NaN superbin), class counts
+    GQ_SUP, GQ_BPS, GQ_CAP, GQ_AFTER = 32, 32, 4096, 256
+
+    def _gq_bins_of(self, k):
+        lo, hi = self._gq_range
+        nb = self.GQ_SUP * self.GQ_BPS
+        sc = nb / (hi - lo) if hi > lo else 0.0
+        with np.errstate(invalid="ignore"):
+            b = np.clip(np.floor((k - lo) * sc), 0, nb - 1)
+        return np.where(np.isnan(k), nb, b).astype(np.int64)
+
+    def gq_shard_begin(self):
+        if not hasattr(self, "_gq_range"):
+            self._gq_range = (-32.0, 32.0)
+        k = -(self.t_air.numpy() - self.target.numpy())
+        self._gq_k, self._gq_b = k, self._gq_bins_of(k)
+        cls = self.cap_idx.numpy().astype(np.int64)
+        sup = np.zeros((self.GQ_SUP + 1, 4), np.int32)
+        np.add.at(sup, (np.minimum(self._gq_b // self.GQ_BPS, self.GQ_SUP), cls), 1)
+        fin = k[~np.isnan(k)]
+        rng = np.array([fin.min() if fin.size else np.inf, -fin.max() if fin.size else np.inf])
+        self._gq = {"super": torch.from_numpy(sup.reshape(-1).copy()), "bins": torch.zeros(2 * self.GQ_BPS * 4, dtype=torch.int32),
+                    "range": torch.from_numpy(rng), "window": torch.zeros(1 + 4 * self.GQ_CAP, dtype=torch.float64)}
+        return self._gq
+
+    def _gq_p(self):
+        hv = self.props.cluster_prop.house_prop.hvac_prop
+        return np.asarray(self.cap_values) / hv.cop
+
+    def gq_shard_bins(self, budget):
+        sup = self._gq["super"].numpy().reshape(-1, 4).astype(np.int64)
+        p = self._gq_p()
+        Pc = (sup[:, :len(p)] * p).sum(1)
+        cum = np.cumsum(Pc)
+        cnt = sup.sum(1)
+        hit = np.nonzero((cnt > 0) & ~(cum < budget))[0]
+        self._gq_sb = int(hit[0]) if hit.size else self.GQ_SUP + 1
+        self._gq_base = float(cum[self._gq_sb - 1]) if 0 < self._gq_sb <= self.GQ_SUP else 0.0
+        self._gq_basec = int(cnt[:self._gq_sb].sum())
+        self._gq_total = int(cnt.sum())
+        lo, mhi = self._gq["range"].tolist()
+        self._gq_next = (lo, -mhi) if np.isfinite(lo) else (0.0, 0.0)
+        bins = np.zeros((2 * self.GQ_BPS, 4), np.int32)
+        if self._gq_sb < self.GQ_SUP:
+            rel = self._gq_b - self._gq_sb * self.GQ_BPS
+            m = (rel >= 0) & (rel < 2 * self.GQ_BPS) & (self._gq_b < self.GQ_SUP * self.GQ_BPS)
+            np.add.at(bins, (rel[m], self.cap_idx.numpy()[m].astype(np.int64)), 1)
+        self._gq["bins"].copy_(torch.from_numpy(bins.reshape(-1)))
+
+    def gq_shard_compact(self, budget, action):
+        self._gq_range = self._gq_next
+        act = np.zeros(self.n, np.uint8)
+        sb, n_sup = self._gq_sb, self.GQ_SUP
+        self._gq_fb = sb == n_sup  # a NaN crossing: the all-gather form decides
+        win = self._gq["window"].numpy()
+        win[0] = 0
+        if sb > n_sup:  # everything fits the budget
+            act[:] = 1
+        elif not self._gq_fb:
+            bins = self._gq["bins"].numpy().reshape(-1, 4).astype(np.int64)
+            p = self._gq_p()
+            Pb = (bins[:, :len(p)] * p).sum(1)
+            cb = bins.sum(1)
+            cum = self._gq_base + np.cumsum(Pb)
+            l0 = int(np.nonzero((cb > 0) & ~(cum < budget))[0][0])
+            pre = np.cumsum(cb[l0:])
+            ok = np.nonzero(pre <= self.GQ_CAP)[0]
+            if ok.size == 0:
+                self._gq_fb = True
+            else:
+                enough = ok[pre[ok] >= cb[l0] + self.GQ_AFTER]
+                le = int(enough[0]) if enough.size else int(ok[-1])
+                bs = sb * self.GQ_BPS + l0
+                be = bs + le
+                self._gq_wbase = float(cum[l0] - Pb[l0])
+                self._gq_more = self._gq_basec + int(cb[:l0].sum()) + int(pre[le]) < self._gq_total
+                self._gq_ncand = int(pre[le])
+                act[self._gq_b < bs] = 1
+                inw = np.nonzero((self._gq_b >= bs) & (self._gq_b <= be))[0]
+                _, lk, _ = decode_hvac(self.hvac.numpy().copy())
+                pw = self._gq_p()[self.cap_idx.numpy()]
+                win[0] = inw.size
+                rows = np.stack([self._gq_k[inw], (inw + self.offset).astype(np.float64), pw[inw],
+                                 lk[inw].astype(np.float64)], 1)
+                win[1:1 + 4 * inw.size] = rows.reshape(-1)
+        action.copy_(torch.from_numpy(act))
+
+    def gq_shard_select(self, budget, gathered, world, action):
+        if self._gq_fb or self._gq_sb > self.GQ_SUP:
+            return
+        g = gathered.numpy().reshape(world, -1)
+        rows = np.concatenate([g[r, 1:1 + 4 * int(g[r, 0])].reshape(-1, 4) for r in range(world)])
+        if rows.shape[0] != self._gq_ncand:
+            self._gq_fb = True
+            return
+        order = np.lexsort((rows[:, 1], rows[:, 0]))  # (key, global house), as the stable sort
+        tot, take = self._gq_wbase, np.zeros(rows.shape[0], bool)
+        for j in order:  # greedy_myopic_controller.py:93-101 from the P taken before the window
+            pj, lk = rows[j, 2], rows[j, 3] != 0
+            if pj + tot < budget or (abs(pj + tot - budget) < abs(tot - budget) and not lk):
+                take[j], tot = True, tot + pj
+        if self._gq_more and not (not tot < budget or 2.0 * (budget - tot) < self._gq_p().min() * (1 - 1e-9)):
+            self._gq_fb = True  # the walk could continue past the window
+            return
+        act = action.numpy()
+        for j in np.nonzero(take)[0]:
+            li = int(rows[j, 1]) - self.offset
+            if 0 <= li < self.n:
+                act[li] = 1
+
+    def gq_shard_fallback(self):
+        return bool(self._gq_fb)
+
     def host_state(self):
         on, lock, sso = decode_hvac(self.hvac.numpy().copy())
         return {"T": self.t_air.numpy().copy(), "Tm": self.t_mass.numpy().copy(), "on": on,
@@ -191,6 +306,17 @@ class GlooComm:
 
     def allreduce_max(self, shard, t):
         self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX)
+
+    def allreduce_min(self, shard, t):
+        self.dist.all_reduce(t, op=self.dist.ReduceOp.MIN)
+
+    def allreduce_count32(self, shard, t):
+        self.dist.all_reduce(t)
+
+    def allgather_bytes(self, shard, t):
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t.contiguous())
+        return torch.cat(parts)
 
     def allgather_cat(self, shard, t, sizes):
         m = max(sizes)

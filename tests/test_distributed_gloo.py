@@ -117,14 +117,18 @@ def _greedy_worker(rank, world, port, overrides, seed, T, out_dir):
         acts.append(a.numpy().copy())
         env.step_tensor(a)
         Ts.append(env.shard.host_state()["T"])
-    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), lo=env._offset, acts=np.array(acts), T=np.array(Ts))
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), lo=env._offset, acts=np.array(acts), T=np.array(Ts),
+             fallbacks=env._gq_shard_fallbacks)
     dist.destroy_process_group()
 
 
-def test_sharded_greedy_equals_oracle(tmp_path):
-    """Sharded GreedyMyopic (all-gather of the shards' key / P / lockout rows, the same selection
-    on every rank, each keeps its slice) == the single-process oracle's greedy + step."""
-    world, T, seed, n = 2, 6, 9, 75
+@pytest.mark.parametrize("n", [75, 3001])
+def test_sharded_greedy_equals_oracle(tmp_path, n):
+    """Sharded GreedyMyopic — the histogram form: the shards' superbin / bin histograms and key
+    range allreduced, the candidate windows all-gathered, the same window decision on every rank,
+    each keeps its slice (the all-gather form decides what the window cannot) — == the
+    single-process oracle's greedy + step."""
+    world, T, seed = 2, 6, 9
     overrides = {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals"}
     mp.start_processes(_greedy_worker, args=(world, _free_port(), overrides, seed, T, str(tmp_path)),
                        nprocs=world, join=True, start_method="spawn")
@@ -140,3 +144,4 @@ def test_sharded_greedy_equals_oracle(tmp_path):
         assert 0 < got.sum() < n or t > 0
         o, _ = ora.step(ref)
         np.testing.assert_array_equal(np.concatenate([p["T"][t] for p in parts]), o["T"])
+    assert all(int(p["fallbacks"]) <= 1 for p in parts), [int(p["fallbacks"]) for p in parts]  # the window decided

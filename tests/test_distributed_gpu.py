@@ -53,7 +53,7 @@ def _run(env, n_total, torch, dev):
     for t in range(T_BUF):
         a = np.random.RandomState(100 + t).randint(0, 2, n_total).astype(np.uint8)[lo:lo + nl]
         rewards.append(env.step_tensor(torch.from_numpy(a).to(dev)).cpu().numpy().copy())
-    for t in range(T_GREEDY):  # GreedyMyopic over the whole cluster (sharded: all-gathered rows)
+    for t in range(T_GREEDY):  # GreedyMyopic over the whole cluster (sharded: the histogram form)
         rewards.append(env.step_tensor(env.greedy_actions()).cpu().numpy().copy())
     if env.shard.penalty_mode == 0:
         r = env.rollout(T_ROLL, action_mode="random")
@@ -63,7 +63,7 @@ def _run(env, n_total, torch, dev):
     st = env.shard.host_state()
     obs = env.obs_tensor().cpu().numpy().copy()
     return {"rewards": np.array(rewards), "T": st["T"], "Tm": st["Tm"], "on": st["on"], "lock": st["lock"],
-            "sso": st["sso"], "P": env._cluster_power(), "obs": obs}
+            "sso": st["sso"], "P": env._cluster_power(), "obs": obs, "gq_fb": env._gq_shard_fallbacks}
 
 
 def _variant(env, kind):
@@ -99,6 +99,8 @@ def _worker(rank, world, port, backend, kind, n, mode, out_dir):
                       population="synthetic", seed=77, rank=rank, world=world,
                       comm=make_comm("rccl" if kind.startswith("rccl") else kind))
     _variant(env, kind)
+    if kind.startswith("rccl"):  # world 1: the sharded greedy stages with RCCL collectives to self
+        env._gq_force_sharded = True
     res = _run(env, n, torch, dev)
     res["lo"] = env._offset
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
@@ -152,6 +154,7 @@ def test_sharded_equals_single(tmp_path, backend, kind, world, n, mode):
         np.testing.assert_allclose(got_r, ref["rewards"], rtol=1e-12, atol=1e-15)
     for p in parts:
         assert float(p["P"]) == ref["P"]
+        assert int(p["gq_fb"]) == 0  # the sharded histogram select decided every greedy tick
     obs = np.concatenate([p["obs"] for p in parts])
     np.testing.assert_array_equal(obs, ref["obs"])
 
