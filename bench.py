@@ -501,8 +501,12 @@ def main():
         "vs_baseline": None,
         "dtype": "f64",
         "data": "synthetic (device Philox population, reference noise model; fused Philox random actions)",
-        "config": {"workload": "1M houses per GPU, random actions, fused FSM+thermal+reward step, every "
-                               "tick's reward row written (BASELINE metric at 1M houses; configs[1]'s controller)",
+        "config": {"workload": (f"C4: {n_total:,} houses sharded over {world} GPUs ({n_loc:,} per GPU), random "
+                                "actions, fused FSM+thermal+reward step, every tick's reward row written, one "
+                                "allreduce of the window's power counts per window"
+                                if world > 1 and args.scaling == "strong" else
+                                f"{n_loc:,} houses per GPU, random actions, fused FSM+thermal+reward step, every "
+                                "tick's reward row written (BASELINE metric at 1M houses; configs[1]'s controller)"),
                    "houses_per_gpu": n_loc, "houses_total": n_total, "dt_s": props.time_step.seconds,
                    "signal": "sinusoidals", "penalty": "individual_L2", "action_mode": args.mode,
                    "chunk_ticks": chunk, "window_ticks": window,

@@ -152,13 +152,15 @@ int mdr_params_changed(mdr_ctx* ctx);
  *   MDR_OPT_GREEDY_SORT     1 = mdr_ctrl_greedy always runs the full-sort form
  *   MDR_OPT_FORCE_HALO      1 = mdr_actor_rollout_sharded exchanges the ring halo even at world 1
  *                           (send/recv to self: the one-GPU check of the multi-GPU exchange)
+ *   MDR_OPT_ACTOR_PINGPONG  k_actor: 1 = the two waves of a SIMD alternate MFMA and VALU stages
+ *                           between block barriers, 0 = free-running waves (default)
  *   MDR_OPT_WINDOW_THERMAL  k_step_window's per-tick thermal update: MDR_THERMAL_AFFINE (default)
  *                           = the reference's update as a per-house affine transition formed once
  *                           per window (4 FMAs per temperature per tick; ~1e-13 K per tick from the
  *                           reference order), MDR_THERMAL_EXACT = the reference's expression in its
  *                           operation order every tick (bit-identical to the one-tick kernels) */
 enum { MDR_OPT_STEP_TPW = 1, MDR_OPT_FASTDIV = 2, MDR_OPT_WINDOW_PIPELINE = 3, MDR_OPT_SHARDED_OVERLAP = 4,
-       MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7 };
+       MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7, MDR_OPT_ACTOR_PINGPONG = 8 };
 enum { MDR_THERMAL_EXACT = 0, MDR_THERMAL_AFFINE = 1 };
 int mdr_set_option(mdr_ctx* ctx, int option, int64_t value);
 
@@ -322,6 +324,10 @@ int mdr_ctrl_greedy(mdr_ctx* ctx, double budget, uint8_t* action, void* stream);
  * sizes, the last call's window size}. */
 int mdr_greedy_fallbacks(mdr_ctx* ctx, uint64_t* count);
 int mdr_greedy_diag(mdr_ctx* ctx, uint64_t* out);
+/* The select state after the last stage run (synchronises): out[12] = mdr_greedy_diag's 4 values,
+ * then {crossing superbin, crossing bin b*, window end bin, all taken, overflow, houses after the
+ * window, window allocator count, sharded need-fallback flag}. */
+int mdr_greedy_state(mdr_ctx* ctx, uint64_t* out);
 
 /* Sharded greedy, histogram form (per-rank work O(N/G + window)): the same
  * select as mdr_ctrl_greedy with the caller's collectives between its stages, every rank deciding

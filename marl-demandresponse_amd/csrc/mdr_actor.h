@@ -4,22 +4,34 @@
 
 namespace mdr {
 
-constexpr int kActorMB = 4;       // 32-row MFMA blocks per hidden layer (hidden width <= 128)
-constexpr int kActorRows = 32 * kActorMB;
+constexpr int kActorRB = 16;      // rows (neurons) per MFMA row block (v_mfma_f32_16x16x32_bf16)
+constexpr int kActorMaxMB = 8;    // row blocks per hidden layer (hidden width <= 128)
+constexpr int kActorRows = kActorRB * kActorMaxMB;
 constexpr int kActorNA = 2;       // actions: on / off (MAPPO num_action = 2, mappo.py:38)
-constexpr int kActorMaxIn = 128;  // obs features (8 k-steps of 16)
+constexpr int kActorMaxIn = 128;  // obs features
+constexpr int kActorMaxSlots = 128;  // feature slots of the chunked row layout (4 k-steps of 32)
+constexpr int kActorKS2 = kActorMaxMB / 2;  // layer-2 k-steps of 32 (hidden rows 0 .. 127)
 
-// Shapes + byte offsets of the packed weight image (identical in global memory and in LDS) and
-// of the per-block LDS work areas.  Filled by the host (mdr_capi.hip actor_layout).
+// Shapes, the obs row's slot layout, byte offsets of the packed weight image (identical in global
+// memory and in LDS) and of the per-block LDS work areas.  Filled by the host (mdr_capi.hip
+// actor_layout).
+//
+// Slot layout: the K dimension of layer 1 is the obs row in 4-float chunks, [own features (n_own,
+// zero padded to own4) | message 0 | ... | message K-1 (M each, zero padded to m4)]; the packed W1
+// columns follow the same order.  LDS rows (per wave, stride rs floats, an odd multiple of 4):
+//   ring:  one row per message source s (house b0 - lo + s): [message (m4) | own (own4)]
+//   table: one row per tile house: [own (own4) | message 0 .. K-1 (m4 each)]
 struct ActorDims {
   int n_in, h1, h2, n_act;
-  int ks1, ks2;  // k-steps of layer 1 (ceil(n_in/16)) and layer 2 (ceil(h1/16))
-  int fs;        // LDS obs row stride (floats): >= n_in, multiple of 4, odd multiple of 4 words
-  int nf;        // bf16 fragments per (row block, k-step): 2 = (hi, lo), 3 = (hi, mid, lo) for MDR_PREC_FP32
+  int mb;         // row blocks of both hidden layers (ceil(max(h1, h2) / 16), 7 or 8)
+  int ks1;        // layer-1 k-steps of 32 (ceil(nslot / 32))
+  int nf;         // bf16 fragments per (row block, k-step): 2 = (hi, lo), 3 = (hi, mid, lo) for MDR_PREC_FP32
+  int n_own, own4, msg_w, m4, n_comm, lo, ring, nslot, rs, nrows;
   int off_w1, off_w2, off_tail, off_end;  // packed image: W1 / W2 fragments, fp32 tail
   int lds_cf, lds_hist, lds_wave, wave_stride;  // block LDS: obs consts, count histogram, wave slices
-  int w_msg, w_hw, w_cls;                        // offsets inside a wave slice (rows at 0)
+  int w_zero, w_hw, w_cls;                       // offsets inside a wave slice (rows at 0)
   int lds_total;
+  int pp;  // ping-pong schedule (8 waves: MDR_OPT_ACTOR_PINGPONG)
 };
 
 struct ActorOut {
@@ -33,7 +45,7 @@ struct ActorOut {
 
 __global__ void k_actor_pack(ActorDims d, const float* w1, const float* b1, const float* w2,
                              const float* b2, const float* w3, const float* b3, unsigned char* out);
-template <int PREC, bool PROF>
+template <int PREC, bool PROF, int MB>
 __global__ void k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
                         const unsigned char* wpack, ActorOut out, uint64_t tick, const TickArgs* tkp);
 

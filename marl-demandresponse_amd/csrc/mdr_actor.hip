@@ -4,11 +4,12 @@
 // softmax(fc2(relu(fc1(relu(fc0(x)))))) over the norm_state_dict vector (server/app/utils/norm.py:
 // 178-218), sampled per agent with Categorical (server/app/core/agents/trainables/mappo.py:83-97).
 // The reference runs N batch-1 forwards on the CPU; here one persistent launch builds each house's
-// observation row in LDS (never written to HBM unless asked), runs the two hidden layers as MFMA
-// tiles (houses on the 32 columns of v_mfma_f32_32x32x16_bf16, neurons on the rows), the output
-// layer + softmax + sampling on the VALU, and writes action (u8) and the chosen action's
-// probability (f32).  Optionally it also counts the ON houses per capacity class the new actions
-// produce (the next k_step's cluster power), so a policy tick + env tick is two launches.
+// observation on chip (never written to HBM unless asked), runs the two hidden layers as MFMA tiles
+// (v_mfma_f32_16x16x32_bf16: neurons on the 16 rows of a row block, houses on the 16 columns; a
+// wave's tile is 32 houses = two column blocks sharing every weight fragment it reads from LDS),
+// the 2-wide output layer + softmax + sampling on the VALU, and writes action (u8) and the chosen
+// action's probability (f32).  Optionally it also counts the ON houses per capacity class the new
+// actions produce (the next k_step's cluster power), so a policy tick + env tick is two launches.
 //
 // Precision (mdr_actor_spec.precision):
 //   MDR_PREC_BF16X3 — every fp32 operand x is split x = hi + lo (hi = bf16(x), lo = bf16(x - hi))
@@ -18,20 +19,46 @@
 //                     significand) and a·b ≈ ah·bh + ah·bm + am·bh + ah·bl + al·bh + am·bm (the dropped
 //                     terms are <= 2^-24 relative): fp32-faithful, 6 MFMAs per term.
 //   MDR_PREC_BF16   — one bf16 product per term.
-// Bias adds, ReLU, the output layer, softmax and sampling are fp32.
+// The biases enter as each layer's first accumulator (the MFMA's C operand); ReLU, the output
+// layer, softmax and sampling are fp32.
 //
-// Fragment maps (gfx950, 32x32x16 bf16; lane l, r = l & 31, h = l >> 5, element j = 0..7):
-//   A[row r][k = 8h + j], B[k = 8h + j][col r], C/D reg g: col r, row (g & 3) + 8 (g >> 2) + 4h.
-// Layer 2 takes layer 1's accumulator registers 8s .. 8s+7 of row block kb directly as its B
-// fragment for k-step q = 2 kb + s: element j is hidden row 16q + 8 (j >> 2) + 4h + (j & 3); the
-// packed W2 fragments use that same k order (k_actor_pack), so no lane movement is needed.
+// Observation rows.  The rows live in LDS in the chunked slot layout of ActorDims (own features,
+// then each message padded to a multiple of 4 floats): in the ring topology one LDS row per message
+// source holds that house's message and, for the tile's houses, its own features, so a house's
+// message is computed once for the (up to 10) houses that receive it and no row is ever assembled —
+// every lane reads its B-fragment chunks with ds_read_b128 straight from the source rows (the
+// chunk offsets are per-lane constants).  Table topologies (closed groups, random) gather each
+// house's K messages into its own row.
+//
+// Fragment maps (gfx950, 16x16x32 bf16; lane l, c = l & 15, g = l >> 4, element j = 0..7):
+//   A[row c][k = 8g + j], B[k = 8g + j][col c], C/D reg i: col c, row 4g + i.
+// Layer 2 takes layer 1's accumulators of row blocks 2q and 2q + 1 directly as its B fragment for
+// k-step q: element j is hidden row 32q + 16 (j >> 2) + 4g + (j & 3); the packed W2 fragments use
+// that same k order (k_actor_pack), so no lane movement is needed.
 #include "mdr_actor.h"
 #include "mdr_obs_dev.h"
 
 namespace mdr {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// --------------------------------------------------------------------------------------- slots
+// The feature behind layer-1 slot s (-1: a padding slot)
+__device__ __forceinline__ int actor_feat_of_slot(const ActorDims& d, int s) {
+  if (s < d.own4) return s < d.n_own ? s : -1;
+  const int t = s - d.own4;
+  if (t >= d.n_comm * d.m4) return -1;
+  const int k = t / d.m4, m = t - k * d.m4;
+  return m < d.msg_w ? d.n_own + k * d.msg_w + m : -1;
+}
+// Float offset of slot s's value for tile house r, relative to r * rs (-1: padding past the row)
+__device__ __forceinline__ int actor_slot_off(const ActorDims& d, int s) {
+  if (s >= d.nslot) return -1;
+  if (s < d.own4) return d.ring ? d.lo * d.rs + d.m4 + s : s;
+  const int t = s - d.own4, k = t / d.m4, m = t - k * d.m4;
+  return d.ring ? (k + (k >= d.lo ? 1 : 0)) * d.rs + m : d.own4 + t;
+}
 
 // --------------------------------------------------------------------------------------- pack
 // One thread per (fragment, lane): 8 weights -> bf16 hi (and lo) in fragment order.
@@ -72,29 +99,29 @@ __global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const fl
                              const float* __restrict__ w2, const float* __restrict__ b2,
                              const float* __restrict__ w3, const float* __restrict__ b3,
                              unsigned char* __restrict__ out) {
-  const int nf1 = kActorMB * d.ks1, nf2 = kActorMB * d.ks2;
-  const int g = blockIdx.x * blockDim.x + threadIdx.x;
-  const int lane = g & 63, f = g >> 6;
-  const int r = lane & 31, h = lane >> 5;
+  const int nf1 = d.mb * d.ks1, nf2 = d.mb * kActorKS2;
+  const int gid = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = gid & 63, f = gid >> 6;
+  const int c = lane & 15, g = lane >> 4;
   float v[8];
-  // fragments are stored k-step-major (f = k-step * kActorMB + mb), so the kernel's unrolled
-  // (k-step, mb) loops address them with compile-time LDS offsets whatever ks1 / ks2 are
-  if (f < nf1) {  // W1 [H1][n_in], fragment (mb, ks)
-    const int ks = f / kActorMB, mb = f % kActorMB;
-    const int row = 32 * mb + r;
+  // fragments are stored k-step-major (f = k-step * mb + row block), so the kernel's unrolled
+  // (k-step, row block) loops address them with compile-time LDS offsets
+  if (f < nf1) {  // W1 [H1][n_in], columns in slot order
+    const int ks = f / d.mb, mb = f % d.mb;
+    const int row = kActorRB * mb + c;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = 16 * ks + 8 * h + j;
-      v[j] = (row < d.h1 && k < d.n_in) ? w1[row * d.n_in + k] : 0.f;
+      const int fe = actor_feat_of_slot(d, 32 * ks + 8 * g + j);
+      v[j] = (row < d.h1 && fe >= 0) ? w1[row * d.n_in + fe] : 0.f;
     }
     pack_frags(d, v, out + d.off_w1, f, lane);
   } else if (f < nf1 + nf2) {  // W2 [H2][H1], fragment (mb, q) in the accumulator k order
     const int f2 = f - nf1;
-    const int q = f2 / kActorMB, mb = f2 % kActorMB;
-    const int row = 32 * mb + r;
+    const int q = f2 / d.mb, mb = f2 % d.mb;
+    const int row = kActorRB * mb + c;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
-      const int k = 16 * q + 8 * (j >> 2) + 4 * h + (j & 3);
+      const int k = 32 * q + 16 * (j >> 2) + 4 * g + (j & 3);
       v[j] = (row < d.h2 && k < d.h1) ? w2[row * d.h1 + k] : 0.f;
     }
     pack_frags(d, v, out + d.off_w2, f2, lane);
@@ -128,19 +155,56 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
-// Persistent, wave-independent: every wave of the block shares the LDS weight image but owns its
-// own 32-house tiles (rows, ring messages, FSM words in a private LDS slice), so waves never wait
-// for each other inside the loop and one wave's obs build / memory phase overlaps another's MFMAs
-// on the same SIMD.  Each lane prefetches one obs source of the wave's NEXT tile into registers
-// before the current tile's MFMAs.
-template <int PREC, bool PROF>
+__device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+}
+
+// acc = C + A·B over the split operands (PREC 1: hi·hi; 3: + lo terms; 6: + mid terms), smallest
+// terms first; a[e] / b[e] = (hi, lo) or (hi, mid, lo)
+template <int PREC>
+__device__ __forceinline__ f32x4 mfma_split(const bf16x8* a, const bf16x8* b, f32x4 acc) {
+  if constexpr (PREC == 6) {
+    acc = mfma16(a[1], b[1], acc);  // mid·mid
+    acc = mfma16(a[2], b[0], acc);  // lo·hi
+    acc = mfma16(a[0], b[2], acc);  // hi·lo
+    acc = mfma16(a[1], b[0], acc);  // mid·hi
+    acc = mfma16(a[0], b[1], acc);  // hi·mid
+  } else if constexpr (PREC == 3) {
+    acc = mfma16(a[1], b[0], acc);  // lo·hi
+    acc = mfma16(a[0], b[1], acc);  // hi·lo
+  }
+  return mfma16(a[0], b[0], acc);
+}
+
+template <int PREC>
+__device__ __forceinline__ void split_operand(const float* v, bf16x8* s) {
+  if constexpr (PREC == 6) split8x3(v, s[0], s[1], s[2]);
+  else if constexpr (PREC == 3) split8(v, s[0], s[1]);
+  else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s[0][j] = (__bf16)v[j];
+  }
+}
+
+// Persistent: every wave of the block shares the LDS weight image but owns its own 32-house tiles
+// (source rows, FSM words in a private LDS slice).  A tile runs as three stages — build (its LDS
+// rows from sources prefetched into registers), X (layers 1 and 2 on the MFMA pipe; the next tile's
+// sources go in flight first) and Y (output layer, softmax, sampling, stores on the VALU) — and the
+// two waves of each SIMD run them in ping-pong (the schedule at the end of the kernel), so the
+// SIMD's matrix pipe and its VALU are busy at the same time.  MB: row blocks of the hidden layers
+// (compile-time LDS offsets).
+template <int PREC, bool PROF, int MB>
 __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
                                                const unsigned char* __restrict__ wpack, ActorOut out,
                                                uint64_t tick0, const TickArgs* tkp) {
+  static_assert(MB >= 1 && MB <= kActorMaxMB, "row blocks");
+  constexpr int NS = PREC == 6 ? 3 : PREC == 3 ? 2 : 1;  // operand splits
+  constexpr int NF = PREC == 6 ? 3 : 2;                   // packed fragments per (row block, k-step)
+  constexpr int KS2 = (MB + 1) / 2;
   const uint64_t tick = tkp ? tkp->tick : tick0;
   // diagnostics (out.prof): shader cycles per phase, accumulated by lane 0 of every wave:
-  // [0] weight fill + block barrier, [1] obs build + message copy, [2] prefetch issue + obs_out,
-  // [3] layer 1, [4] split + layer 2, [5] output layer + softmax + stores, [6] -, [7] tiles
+  // [0] weight fill + block barrier, [1] obs build, [2] prefetch issue + obs_out,
+  // [3] layer 1, [4] split + layer 2, [5] output layer + softmax + stores, [6] barrier waits, [7] tiles
   unsigned long long pacc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   unsigned long long plast = PROF ? clock64() : 0ull;
 #define PSTAMP(k)                                \
@@ -154,13 +218,14 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int nthr = blockDim.x, nw = nthr >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const int F = o.n_feat, FS = d.fs;
-  constexpr int NF = PREC == 6 ? 3 : 2;  // packed fragments per (row block, k-step)
+  const int cc = lane & 15, g = lane >> 4;
+  const int F = o.n_feat;
   const int K = o.n_comm, M = o.msg_w;
-  const bool ring = o.comm_mode == MDR_COMM_RING && K > 0;
-  const int lo = ring ? K / 2 : 0, hi = ring ? (K + 1) / 2 : 0;
+  const bool ring = d.ring != 0;
+  const int lo = d.lo, hi = ring ? (K + 1) / 2 : 0;
+  const int RS = d.rs;
   const bool thermal = obs_needs_thermal(o);
+  const ObsDiv dv = obs_div(p);
 
   // LDS: [weights image | obs consts | count histogram | per-wave slices]
   const unsigned char* s_w1 = smem;
@@ -169,8 +234,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
   float* s_cf = reinterpret_cast<float*>(smem + d.lds_cf);
   unsigned* s_hist = reinterpret_cast<unsigned*>(smem + d.lds_hist);
   unsigned char* wbase = smem + d.lds_wave + wv * d.wave_stride;
-  float* w_obs = reinterpret_cast<float*>(wbase);                  // [32][FS] + 16 ks1 overrun
-  float* w_msg = reinterpret_cast<float*>(wbase + d.w_msg);        // [lo + 32 + hi][M]
+  float* w_row = reinterpret_cast<float*>(wbase);                  // [nrows][RS]
   uint32_t* w_hw = reinterpret_cast<uint32_t*>(wbase + d.w_hw);    // [32] hvac words
   uint8_t* w_cls = wbase + d.w_cls;                                // [32] capacity classes
 
@@ -182,7 +246,8 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
       if (PREC == 1 && q < d.off_tail / 16 && ((q >> 6) & 1)) continue;  // bf16: no lo fragments (nf = 2)
       dst[q] = src[q];
     }
-    for (int q = lane; q < 32 * FS + 16 * d.ks1; q += 64) w_obs[q] = 0.f;
+    // the wave's slice: rows and the zero chunk (padding slots stay zero: the builds write features only)
+    for (int q = lane; q < d.w_hw / 4; q += 64) w_row[q] = 0.f;
     if (tid < MDR_MAX_CAP) s_hist[tid] = 0u;
     if (o.sc_dev) { o.s = o.sc_dev[1]; o.solar = o.sc_dev[2]; o.t_od = o.sc_dev[3]; }  // mdr_obs_scalars row
     obs_consts(p, o, p_dev ? *p_dev : o.p, s_cf, tid, nthr);
@@ -194,204 +259,214 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
   const float* w3 = s_tail + 2 * kActorRows;
   const float* b3 = s_tail + (2 + kActorNA) * kActorRows;
 
+  // this lane's B-fragment chunk addresses (floats into w_row) for column block 0: layer-1 k-step
+  // ks reads slots 32 ks + 8 g .. + 7 = two chunks; padding chunks read the wave's zero chunk
+  int xoff[4][2], xstep[4][2];  // column block cb reads xoff + cb * xstep
+#pragma unroll
+  for (int ks = 0; ks < 4; ++ks)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int off = actor_slot_off(d, 32 * ks + 8 * g + 4 * e);
+      xoff[ks][e] = off < 0 ? d.w_zero / 4 : cc * RS + off;
+      xstep[ks][e] = off < 0 ? 0 : 16 * RS;
+    }
+
   const uint32_t n = (uint32_t)p.n;
   const uint32_t ntile = (n + 31u) / 32u;
   const uint32_t stride = gridDim.x * (uint32_t)nw;
-  const int nsrc_max = lo + 32 + hi;
+  const int nsrc_max = ring ? lo + 32 + hi : 32;
   HouseRegs src{};
   int src_kind = 0;  // 0 none, 1 house, 2 halo
+  // source s of tile tl: ring = house b0 - lo + s (message source), table = house b0 + s (s < 32)
   auto source_of = [&](uint32_t tl, int s, HouseRegs& rg) -> int {
     const uint32_t b0 = tl * 32u;
     const int nb = (int)min(32u, n - b0);
     if (s >= lo + nb + hi) return 0;
     int64_t j = (int64_t)b0 - lo + s;
     if (o.halo_msg && (j < 0 || j >= (int64_t)n)) return 2;
-    j %= (int64_t)n;
-    if (j < 0) j += n;
+    if (n >= 64u) {  // j in [-lo, n + 32 + hi): one wrap at most (lo, hi <= 32)
+      j = j < 0 ? j + n : (j >= (int64_t)n ? j - n : j);
+    } else {
+      j %= (int64_t)n;
+      if (j < 0) j += n;
+    }
     house_load(p, j, thermal, rg);
     return 1;
   };
   auto build = [&](uint32_t b0, int nb, int s, int kind, const HouseRegs& rg) {
+    float* row = w_row + s * RS;
     if (kind == 2) {
       const int64_t j = (int64_t)b0 - lo + s;
       const int hh = j < 0 ? (int)(j + lo) : (int)(lo + (j - (int64_t)n));
-      for (int m = 0; m < M; ++m) w_msg[s * M + m] = o.halo_msg[hh * M + m];
+      for (int m = 0; m < M; ++m) row[m] = o.halo_msg[hh * M + m];
     } else if (kind == 1) {
-      if (ring) msg_from_regs(p, o, rg, s_cf, w_msg + s * M);
       const int t = s - lo;
+      if (ring) {
+        msg_from_regs(p, o, rg, s_cf, row, dv);
+        if (t >= 0 && t < nb) row_scalars(p, o, rg, s_cf, row + d.m4, dv);
+      } else {
+        row_scalars(p, o, rg, s_cf, row, dv);
+      }
       if (t >= 0 && t < nb) {
-        float* row = w_obs + t * FS;
-        const int f = row_scalars(p, o, rg, s_cf, row);
-        if (!ring) row_messages(p, o, (int64_t)b0 + t, t, s_cf, w_msg, row, f);  // TABLE gathers / none
-        for (int q = F; q < FS; ++q) row[q] = 0.f;
         w_hw[t] = rg.w;
         w_cls[t] = (uint8_t)rg.cls;
       }
     }
   };
-  uint32_t tile = blockIdx.x * (uint32_t)nw + (uint32_t)wv;
-  if (tile < ntile) src_kind = source_of(tile, lane, src);
-
-  for (; tile < ntile; tile += stride) {
-    const uint32_t b0 = tile * 32u;
+  // ---- the stages of a tile (mdr_actor.hip header: the ping-pong schedule below)
+  f32x4 acc2[MB][2];  // layer 2 of the tile between its X and Y stages
+  // build: the tile's LDS rows from the prefetched sources (+ the table topologies' gathers)
+  auto stage_build = [&](uint32_t tl) {
+    const uint32_t b0 = tl * 32u;
     const int nb = (int)min(32u, n - b0);
-    if (PROF && lane == 0) pacc[7] += 1;
-    wave_sync();  // this wave's previous MFMA reads of w_obs are done (compiler ordering)
+    wave_sync();  // this wave's previous MFMA-operand reads of the rows are done (compiler ordering)
     build(b0, nb, lane, src_kind, src);
     if (nsrc_max > 64 && lane + 64 < lo + nb + hi) {  // rings wider than 32 neighbours
       HouseRegs r2;
-      const int k2 = source_of(tile, lane + 64, r2);
+      const int k2 = source_of(tl, lane + 64, r2);
       build(b0, nb, lane + 64, k2, r2);
     }
-    wave_sync();
-    if (ring) {  // messages into the rows: lanes r and r + 32 each copy half of row r's K messages
-      const int base = F - K * M;
-      const int kh = (K + 1) / 2;
+    if (!ring && K > 0) {  // table topologies: lanes r and r + 32 gather half of house r's messages each
+      const int r = lane & 31, hh = lane >> 5, kh = (K + 1) / 2;
       if (r < nb) {
-        for (int k = h * kh; k < min(K, (h + 1) * kh); ++k) {
-          const int sidx = k < lo ? (r + k) : (r + k + 1);
-          float* dst = w_obs + r * FS + base + k * M;
-          const float* sp = w_msg + sidx * M;
-          for (int m = 0; m < M; ++m) dst[m] = sp[m];
+        const int64_t i = (int64_t)b0 + r;
+        float* row = w_row + r * RS + d.own4;
+        for (int k = hh * kh; k < min(K, (hh + 1) * kh); ++k) {
+          const int64_t j = o.comm_table[i * K + k];
+          if (o.msg_all) {  // sharded: the all-gathered rows, global ids
+            for (int m = 0; m < M; ++m) row[k * d.m4 + m] = o.msg_all[j * M + m];
+          } else {
+            msg_features(p, o, j, s_cf, row + k * d.m4, dv);
+          }
         }
       }
-      wave_sync();
     }
+    wave_sync();
     PSTAMP(1);
-    if (tile + stride < ntile) src_kind = source_of(tile + stride, lane, src);  // in flight during the MFMAs
-    else src_kind = 0;
-    if (out.obs) {  // optional obs rows to HBM (training buffers)
+  };
+  // X: the next tile's sources go in flight, then layers 1 and 2 on the MFMA pipe
+  auto stage_x = [&](uint32_t tl, uint32_t next) {
+    const uint32_t b0 = tl * 32u;
+    const int nb = (int)min(32u, n - b0);
+    src_kind = next < ntile ? source_of(next, lane, src) : 0;  // (in flight during the MFMAs)
+    if (out.obs) {  // optional obs rows to HBM in the reference's feature order (training buffers)
       float* dst = out.obs + (size_t)b0 * F;
       for (int q = lane; q < nb * F; q += 64) {
-        const int rr = q / F;
-        dst[q] = w_obs[rr * FS + (q - rr * F)];
+        const int rr = q / F, f = q - rr * F;
+        const int s = f < d.n_own ? f : d.own4 + ((f - d.n_own) / M) * d.m4 + (f - d.n_own) % M;
+        dst[q] = w_row[rr * RS + actor_slot_off(d, s)];
       }
     }
     PSTAMP(2);
-
-    // ---- layer 1: acc1[mb] = b1 + W1 · X  (X^T columns = this wave's 32 houses)
-    // (the wave in its MFMA phases gets issue priority over the SIMD's other wave, which is then
-    // building observations or running the output layer on the VALU: C5 actor 151 -> 141 us at 1M)
-    __builtin_amdgcn_s_setprio(3);
-    const float* xrow = w_obs + r * FS + 8 * h;
-    f32x16 acc1[kActorMB];
+    // (the wave in its MFMA stage gets VALU issue priority over the SIMD's other wave, which is then
+    // building observations or running the output layer)
+    __builtin_amdgcn_s_setprio(2);
+    // ---- layer 1: acc1[mb][cb] = b1 + W1 · X  (X^T columns = this wave's 32 houses, two column blocks)
+    f32x4 acc1[MB][2];
 #pragma unroll
-    for (int mb = 0; mb < kActorMB; ++mb)
+    for (int ks = 0; ks < 4; ++ks) {
+      if (ks >= d.ks1) break;  // (uniform; unrolled so the prefetch loads stay in flight)
+      bf16x8 xs[2][NS];
 #pragma unroll
-      for (int g = 0; g < 16; ++g) acc1[mb][g] = b1[32 * mb + (g & 3) + 8 * (g >> 2) + 4 * h];
-    // k-steps unrolled with uniform guards (a loop here makes the compiler drain the prefetch
-    // loads, vmcnt(0), at its header)
+      for (int cb = 0; cb < 2; ++cb) {
+        float xv[8];
 #pragma unroll
-    for (int ks = 0; ks < kActorMaxIn / 16; ++ks) {
-      if (ks >= d.ks1) break;
-      const float4 x0 = *reinterpret_cast<const float4*>(xrow + 16 * ks);
-      const float4 x1 = *reinterpret_cast<const float4*>(xrow + 16 * ks + 4);
-      const float xv[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-      bf16x8 xh, xl, xm;
-      if (PREC == 6) split8x3(xv, xh, xm, xl);
-      else split8(xv, xh, xl);
-      bf16x8 ah[kActorMB], al[kActorMB], am[kActorMB];
-#pragma unroll
-      for (int mb = 0; mb < kActorMB; ++mb) {
-        const int f = ks * kActorMB + mb;
-        ah[mb] = lds_frag(s_w1, NF * f, lane);
-        if (PREC == 3) al[mb] = lds_frag(s_w1, NF * f + 1, lane);
-        if (PREC == 6) { am[mb] = lds_frag(s_w1, NF * f + 1, lane); al[mb] = lds_frag(s_w1, NF * f + 2, lane); }
-      }
-      if (PREC == 6) {  // smallest terms first
-#pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mb], xm, acc1[mb], 0, 0, 0);
-#pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mb], xh, acc1[mb], 0, 0, 0);
-#pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], xl, acc1[mb], 0, 0, 0);
-#pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mb], xh, acc1[mb], 0, 0, 0);
-#pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], xm, acc1[mb], 0, 0, 0);
-      }
-      if (PREC == 3) {
-#pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mb], xh, acc1[mb], 0, 0, 0);
-#pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], xl, acc1[mb], 0, 0, 0);
+        for (int e = 0; e < 2; ++e) {
+          const int a = xoff[ks][e] + cb * xstep[ks][e];
+          const float4 x = *reinterpret_cast<const float4*>(w_row + a);
+          xv[4 * e] = x.x; xv[4 * e + 1] = x.y; xv[4 * e + 2] = x.z; xv[4 * e + 3] = x.w;
+        }
+        split_operand<PREC>(xv, xs[cb]);
       }
 #pragma unroll
-      for (int mb = 0; mb < kActorMB; ++mb) acc1[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], xh, acc1[mb], 0, 0, 0);
+      for (int mb = 0; mb < MB; ++mb) {
+        bf16x8 as[NS];
+        const int f = ks * MB + mb;
+#pragma unroll
+        for (int e = 0; e < NS; ++e) as[e] = lds_frag(s_w1, NF * f + e, lane);
+        if (ks == 0) {
+          const f32x4 bias = *reinterpret_cast<const f32x4*>(b1 + kActorRB * mb + 4 * g);
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) acc1[mb][cb] = mfma_split<PREC>(as, xs[cb], bias);
+        } else {
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) acc1[mb][cb] = mfma_split<PREC>(as, xs[cb], acc1[mb][cb]);
+        }
+      }
     }
     PSTAMP(3);
-
     // ---- ReLU + split: layer 1's accumulators become layer 2's B fragments in place
-    bf16x8 hh[2 * kActorMB], hl[2 * kActorMB], hm[PREC == 6 ? 2 * kActorMB : 1];
+    bf16x8 hs[KS2][2][NS];
 #pragma unroll
-    for (int q = 0; q < 2 * kActorMB; ++q) {
-      float v[8];
+    for (int q = 0; q < KS2; ++q)
 #pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = fmaxf(acc1[q >> 1][8 * (q & 1) + j], 0.f);
-      if constexpr (PREC == 6) split8x3(v, hh[q], hm[q], hl[q]);
-      else split8(v, hh[q], hl[q]);
-    }
-
-    // ---- layer 2: acc2[mb] = b2 + W2 · relu(H1)
-    f32x16 acc2[kActorMB];
+      for (int cb = 0; cb < 2; ++cb) {
+        float v[8];
 #pragma unroll
-    for (int mb = 0; mb < kActorMB; ++mb)
-#pragma unroll
-      for (int g = 0; g < 16; ++g) acc2[mb][g] = b2[32 * mb + (g & 3) + 8 * (g >> 2) + 4 * h];
-#pragma unroll
-    for (int q = 0; q < 2 * kActorMB; ++q) {
-      if (q >= d.ks2) break;
-      bf16x8 ah[kActorMB], al[kActorMB], am[kActorMB];
-#pragma unroll
-      for (int mb = 0; mb < kActorMB; ++mb) {
-        const int f = q * kActorMB + mb;
-        ah[mb] = lds_frag(s_w2, NF * f, lane);
-        if (PREC == 3) al[mb] = lds_frag(s_w2, NF * f + 1, lane);
-        if (PREC == 6) { am[mb] = lds_frag(s_w2, NF * f + 1, lane); al[mb] = lds_frag(s_w2, NF * f + 2, lane); }
+        for (int j = 0; j < 4; ++j) {
+          v[j] = fmaxf(acc1[2 * q][cb][j], 0.f);
+          v[4 + j] = 2 * q + 1 < MB ? fmaxf(acc1[2 * q + 1][cb][j], 0.f) : 0.f;
+        }
+        split_operand<PREC>(v, hs[q][cb]);
       }
-      if constexpr (PREC == 6) {  // smallest terms first
+    // ---- layer 2: acc2[mb][cb] = b2 + W2 · relu(H1)
 #pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mb], hm[q], acc2[mb], 0, 0, 0);
+    for (int q = 0; q < KS2; ++q) {
 #pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mb], hh[q], acc2[mb], 0, 0, 0);
+      for (int mb = 0; mb < MB; ++mb) {
+        bf16x8 as[NS];
+        const int f = q * MB + mb;
 #pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], hl[q], acc2[mb], 0, 0, 0);
+        for (int e = 0; e < NS; ++e) as[e] = lds_frag(s_w2, NF * f + e, lane);
+        if (q == 0) {
+          const f32x4 bias = *reinterpret_cast<const f32x4*>(b2 + kActorRB * mb + 4 * g);
 #pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(am[mb], hh[q], acc2[mb], 0, 0, 0);
+          for (int cb = 0; cb < 2; ++cb) acc2[mb][cb] = mfma_split<PREC>(as, hs[q][cb], bias);
+        } else {
 #pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], hm[q], acc2[mb], 0, 0, 0);
+          for (int cb = 0; cb < 2; ++cb) acc2[mb][cb] = mfma_split<PREC>(as, hs[q][cb], acc2[mb][cb]);
+        }
       }
-      if (PREC == 3) {
-#pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[mb], hh[q], acc2[mb], 0, 0, 0);
-#pragma unroll
-        for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], hl[q], acc2[mb], 0, 0, 0);
-      }
-#pragma unroll
-      for (int mb = 0; mb < kActorMB; ++mb) acc2[mb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[mb], hh[q], acc2[mb], 0, 0, 0);
     }
     __builtin_amdgcn_s_setprio(0);
     PSTAMP(4);
-
-    // ---- output layer (fp32 VALU): this lane's 64 hidden rows, then the partner half's
-    float z0 = 0.f, z1 = 0.f;
+  };
+  // Y: output layer (fp32 VALU) + softmax + sampling + stores (+ the ON counts of the new actions)
+  auto stage_y = [&](uint32_t tl) {
+    const uint32_t b0 = tl * 32u;
+    const int nb = (int)min(32u, n - b0);
+    float z[2][kActorNA] = {{0.f, 0.f}, {0.f, 0.f}};
     {
 #pragma clang fp contract(fast)
 #pragma unroll
-      for (int mb = 0; mb < kActorMB; ++mb)
+      for (int mb = 0; mb < MB; ++mb) {
+        const float* wr = w3 + (kActorRB * mb + 4 * g) * kActorNA;  // rows 4g .. 4g + 3, both actions
+        const float4 wa = *reinterpret_cast<const float4*>(wr);
+        const float4 wb = *reinterpret_cast<const float4*>(wr + 4);
+        const float w0[4] = {wa.x, wa.z, wb.x, wb.z}, w1v[4] = {wa.y, wa.w, wb.y, wb.w};
 #pragma unroll
-        for (int g = 0; g < 16; ++g) {
-          const int row = 32 * mb + (g & 3) + 8 * (g >> 2) + 4 * h;
-          const float x = fmaxf(acc2[mb][g], 0.f);
-          const float2 w = *reinterpret_cast<const float2*>(w3 + row * kActorNA);
-          z0 += w.x * x;
-          z1 += w.y * x;
-        }
+        for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float x = fmaxf(acc2[mb][cb][i], 0.f);
+            z[cb][0] += w0[i] * x;
+            z[cb][1] += w1v[i] * x;
+          }
+      }
     }
-    z0 = z0 + __shfl_xor(z0, 32) + b3[0];
-    z1 = z1 + __shfl_xor(z1, 32) + b3[1];
-
-    // ---- softmax over the 2 actions (fp32, max-subtracted like torch) + Categorical sample
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+      for (int a = 0; a < kActorNA; ++a) {
+        z[cb][a] += __shfl_xor(z[cb][a], 16);
+        z[cb][a] += __shfl_xor(z[cb][a], 32);
+      }
+    // lane l < 32 takes house l (column block l >> 4, column l & 15)
+    const int r = lane & 31;
+    const bool upper = (lane & 16) != 0;
+    const float z0 = (upper ? z[1][0] : z[0][0]) + b3[0];
+    const float z1 = (upper ? z[1][1] : z[0][1]) + b3[1];
+    // softmax over the 2 actions (fp32, max-subtracted like torch) + Categorical sample
     const float zmax = fmaxf(z0, z1);
     const float e0 = expf(z0 - zmax), e1 = expf(z1 - zmax);
     const float se = e0 + e1;
@@ -402,14 +477,15 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     const float u = philox_u01f(p.seed, (uint64_t)p.goff + i, tick);
     const int act = u < p0 ? 0 : 1;
     const float pa = act ? p1 : p0;
-    if (valid && h == 0) {
+    const bool writer = valid && lane < 32;
+    if (writer) {
       if (out.probs) *reinterpret_cast<float2*>(out.probs + 2 * (size_t)i) = make_float2(p0, p1);
       if (out.action) out.action[i] = (uint8_t)act;
       if (out.prob) out.prob[i] = pa;
     }
     if (out.count_next) {
       // the ON houses the new actions produce (hvac.py:43-64 on action != 0), per capacity class
-      const bool on1 = valid && h == 0 && hv_on(hvac_fsm(w_hw[r], act != 0, p.dt, p.L));
+      const bool on1 = writer && hv_on(hvac_fsm(w_hw[r], act != 0, p.dt, p.L));
       const int cls = valid ? w_cls[r] : 0;
       for (int k = 0; k < p.n_cap; ++k) {
         const unsigned long long m = __ballot(on1 && cls == k);
@@ -417,6 +493,44 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
       }
     }
     PSTAMP(5);
+  };
+
+  // ---- ping-pong schedule.  The block's 8 waves are two halves (waves 0-3 and 4-7, one wave of
+  // each half per SIMD); between block barriers one half runs an X stage (MFMA pipe) while the
+  // other runs Y + build stages (VALU), so each SIMD's matrix pipe and VALU work at the same time
+  // instead of in turn.  Wave sequence: build(t0) | X(t0) | Y(t0) + build(t1) | X(t1) | ... |
+  // Y(t_last); the second half starts one interval later.  Every wave passes the same number of
+  // barriers (the block's largest tile count decides), and nothing in LDS is shared across waves
+  // (the barrier only paces them).  Fewer than 8 waves (LDS-limited layouts): no pairing, no barrier.
+  const bool pp = d.pp != 0 && nw == 8;
+  const int half = pp ? wv >> 2 : 0;
+  const uint32_t tile0 = blockIdx.x * (uint32_t)nw + (uint32_t)wv;
+  const uint32_t first0 = blockIdx.x * (uint32_t)nw;  // wave 0's first tile: the block's largest count
+  const int n_my = tile0 < ntile ? (int)((ntile - 1u - tile0) / stride + 1u) : 0;
+  const int n_max = first0 < ntile ? (int)((ntile - 1u - first0) / stride + 1u) : 0;
+  if (n_my > 0) src_kind = source_of(tile0, lane, src);
+  const int n_int = pp ? 2 * n_max + 2 : 2 * n_my + 1;
+  for (int I = 0; I < n_int; ++I) {
+    const int L = I - half;  // this wave's stage: 0 build(t0), 2j + 1 X(t_j), 2j + 2 Y(t_j) + build(t_j+1)
+    if (L >= 0 && L <= 2 * n_my) {
+      if (L == 0) {
+        if (n_my > 0) stage_build(tile0);
+      } else {
+        const int j = (L - 1) >> 1;
+        const uint32_t tj = tile0 + (uint32_t)j * stride;
+        if (L & 1) {
+          if (PROF && lane == 0) pacc[7] += 1;
+          stage_x(tj, tj + stride);
+        } else {
+          stage_y(tj);
+          if (j + 1 < n_my) stage_build(tj + stride);
+        }
+      }
+    }
+    if (pp) {
+      __builtin_amdgcn_s_barrier();
+      PSTAMP(6);
+    }
   }
   if (PROF && lane == 0) {
     for (int k = 0; k < 8; ++k) out.prof[(blockIdx.x * nw + wv) * 8 + k] = pacc[k];
@@ -429,14 +543,17 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
 #undef PSTAMP
 }
 
-#define MDR_INST_ACTOR(P, F)                                                                   \
-  template __global__ void k_actor<P, F>(KParams, ObsArgs, ActorDims, const double*, const unsigned char*, \
-                                         ActorOut, uint64_t, const TickArgs*);
-MDR_INST_ACTOR(1, false)
-MDR_INST_ACTOR(3, false)
-MDR_INST_ACTOR(6, false)
-MDR_INST_ACTOR(1, true)
-MDR_INST_ACTOR(3, true)
-MDR_INST_ACTOR(6, true)
+#define MDR_INST_ACTOR(P, F, MB)                                                                   \
+  template __global__ void k_actor<P, F, MB>(KParams, ObsArgs, ActorDims, const double*, const unsigned char*, \
+                                             ActorOut, uint64_t, const TickArgs*);
+#define MDR_INST_ACTOR_MB(MB) \
+  MDR_INST_ACTOR(1, false, MB) \
+  MDR_INST_ACTOR(3, false, MB) \
+  MDR_INST_ACTOR(6, false, MB) \
+  MDR_INST_ACTOR(1, true, MB)  \
+  MDR_INST_ACTOR(3, true, MB)  \
+  MDR_INST_ACTOR(6, true, MB)
+MDR_INST_ACTOR_MB(7)
+MDR_INST_ACTOR_MB(8)
 
 }  // namespace mdr

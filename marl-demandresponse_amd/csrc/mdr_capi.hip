@@ -88,7 +88,8 @@ struct mdr_ctx {
   bool win_pipe = true;                  // MDR_OPT_WINDOW_PIPELINE: sharded count-ahead window pipeline
   bool tick_overlap = true;              // MDR_OPT_SHARDED_OVERLAP: per-tick sharded two-stream pipeline
   bool greedy_sort = false;              // MDR_OPT_GREEDY_SORT: the full-sort greedy form only
-  bool force_halo = false;               // MDR_OPT_FORCE_HALO: sharded actor halo exchange at world 1
+  bool force_halo = false;
+  bool actor_pp = false;                 // MDR_OPT_ACTOR_PINGPONG: k_actor's paired-wave schedule               // MDR_OPT_FORCE_HALO: sharded actor halo exchange at world 1
   int thermal = MDR_THERMAL_AFFINE;      // MDR_OPT_WINDOW_THERMAL: k_step_window's per-tick update
   int win = kWindowMax;                  // ticks per k_step_window launch (0: one-tick path)
   unsigned long long* d_wslab = nullptr; // 3 window count slots (mdr_kernels.hip K1W: slab | red | rec)
@@ -146,6 +147,9 @@ struct mdr_ctx {
   // MA-PPO actor (row P): packed weight image, per-tick obs scalars of actor rollouts
   unsigned char* d_actor = nullptr;
   size_t actor_cap = 0;
+  float* d_actor_raw = nullptr;  // the loaded fp32 weights (w1 b1 w2 b2 w3 b3), packed per obs layout
+  size_t actor_raw_cap = 0;
+  std::vector<int> actor_key;    // the slot layout + precision d_actor is packed for (empty: stale)
   mdr_actor_spec actor{};
   bool actor_ready = false;
   int n_cu = 0;
@@ -422,6 +426,7 @@ int mdr_destroy(mdr_ctx* c) {
   hipDeviceSynchronize();
   destroy_graphs(c);
   hipFree(c->d_actor);
+  hipFree(c->d_actor_raw);
   hipFree(c->d_interp);
   hipFree(c->d_act);
   hipFree(c->d_halo);
@@ -471,6 +476,7 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_SHARDED_OVERLAP: c->tick_overlap = value != 0; break;
     case MDR_OPT_GREEDY_SORT: c->greedy_sort = value != 0; break;
     case MDR_OPT_FORCE_HALO: c->force_halo = value != 0; break;
+    case MDR_OPT_ACTOR_PINGPONG: c->actor_pp = value != 0; break;
     case MDR_OPT_WINDOW_THERMAL:
       if (value != MDR_THERMAL_EXACT && value != MDR_THERMAL_AFFINE)
         return fail(MDR_EARG, "mdr_set_option: WINDOW_THERMAL must be MDR_THERMAL_EXACT or _AFFINE");
@@ -1281,6 +1287,16 @@ int mdr_greedy_diag(mdr_ctx* c, uint64_t* out) {
   return MDR_OK;
 }
 
+int mdr_greedy_state(mdr_ctx* c, uint64_t* out) {
+  if (!c || !out) return fail(MDR_EARG, "mdr_greedy_state: null argument");
+  for (int k = 0; k < 12; ++k) out[k] = 0;
+  if (!c->g_sel) return MDR_OK;
+  unsigned char h[128];
+  HIP_TRY(hipMemcpy(h, c->g_sel, 128, hipMemcpyDeviceToHost));
+  gq_state_of(h, out);
+  return MDR_OK;
+}
+
 int mdr_greedy_fallbacks(mdr_ctx* c, uint64_t* count) {
   if (!c || !count) return fail(MDR_EARG, "mdr_greedy_fallbacks: null argument");
   uint64_t d[4];
@@ -1642,27 +1658,37 @@ namespace {
 
 int align16(int x) { return (x + 15) & ~15; }
 
-// Packed-image offsets + the LDS plan of k_actor for `nw` waves per block.
+// Packed-image offsets, the obs row's slot layout and the LDS plan of k_actor for `nw` waves per
+// block (mdr_actor.h ActorDims).
 ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw) {
   ActorDims d{};
   d.n_in = a.n_in; d.h1 = a.h1; d.h2 = a.h2; d.n_act = a.n_act;
-  d.ks1 = (a.n_in + 15) / 16;
-  d.ks2 = (a.h1 + 15) / 16;
-  int fs = (a.n_in + 3) & ~3;
-  if (((fs / 4) & 1) == 0) fs += 4;  // odd multiple of 16 B: conflict-free ds_read_b128 rows
-  d.fs = fs;
+  const int mbn = (std::max(a.h1, a.h2) + kActorRB - 1) / kActorRB;
+  d.mb = mbn <= 7 ? 7 : 8;  // (the kernel's instantiations)
   d.nf = a.precision == MDR_PREC_FP32 ? 3 : 2;
+  const int K = sp->n_comm, M = mdr_msg_width(sp);
+  d.n_comm = K;
+  d.msg_w = M;
+  d.n_own = a.n_in - K * M;
+  d.own4 = (d.n_own + 3) & ~3;
+  d.m4 = (M + 3) & ~3;
+  d.ring = sp->comm_mode == MDR_COMM_RING && K > 0;
+  d.lo = d.ring ? K / 2 : 0;
+  d.nslot = d.own4 + K * d.m4;
+  d.ks1 = (d.nslot + 31) / 32;
+  int rs = d.ring ? d.m4 + d.own4 : d.nslot;
+  if (((rs / 4) & 1) == 0) rs += 4;  // odd multiple of 16 B: conflict-free ds_read_b128 of 16 rows
+  d.rs = rs;
+  d.nrows = d.ring ? d.lo + 32 + (K + 1) / 2 : 32;
   d.off_w1 = 0;
-  d.off_w2 = kActorMB * d.ks1 * d.nf * 1024;
-  d.off_tail = d.off_w2 + kActorMB * d.ks2 * d.nf * 1024;
+  d.off_w2 = d.mb * d.ks1 * d.nf * 1024;
+  d.off_tail = d.off_w2 + d.mb * kActorKS2 * d.nf * 1024;
   d.off_end = align16(d.off_tail + ((2 + kActorNA) * kActorRows + kActorNA) * 4);
-  const int K = sp ? sp->n_comm : 0, M = sp ? mdr_msg_width(sp) : 0;
-  const bool ring = sp && sp->comm_mode == MDR_COMM_RING && K > 0;
   d.lds_cf = d.off_end;
   d.lds_hist = d.lds_cf + align16(kObsConst * 4);
   d.lds_wave = d.lds_hist + MDR_MAX_CAP * 4;
-  d.w_msg = align16((32 * fs + 16 * d.ks1) * 4);
-  d.w_hw = d.w_msg + align16((ring ? (K / 2 + 32 + (K + 1) / 2) * M : 0) * 4);
+  d.w_zero = align16(d.nrows * rs * 4);
+  d.w_hw = d.w_zero + 16;
   d.w_cls = d.w_hw + 32 * 4;
   d.wave_stride = align16(d.w_cls + 32);
   d.lds_total = d.lds_wave + nw * d.wave_stride;
@@ -1670,6 +1696,9 @@ ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw) 
 }
 
 int actor_plan(const mdr_ctx* c, const mdr_obs_spec* sp, ActorDims* d, int* nw) {
+  *d = actor_layout(c->actor, sp, 1);
+  if (d->n_own < 0 || d->nslot > kActorMaxSlots)
+    return fail(MDR_EARG, "mdr_actor: obs row wider than the actor's 128 feature slots");
   for (int w = 8; w >= 1; --w) {
     *d = actor_layout(c->actor, sp, w);
     if (d->lds_total <= 160 * 1024) { *nw = w; return MDR_OK; }
@@ -1677,23 +1706,67 @@ int actor_plan(const mdr_ctx* c, const mdr_obs_spec* sp, ActorDims* d, int* nw) 
   return fail(MDR_EARG, "mdr_actor: weights + obs rows exceed the 160 KiB LDS of a CU");
 }
 
+// The packed weight image for this obs layout (k_actor_pack from the loaded fp32 weights): packed
+// again only when the slot layout or the precision changes.  Called by every actor entry point
+// before it launches or captures anything.
+int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
+  ActorDims d;
+  int nw = 0;
+  if (int rc = actor_plan(c, sp, &d, &nw)) return rc;
+  const std::vector<int> key{d.n_own, d.own4, d.msg_w, d.m4, d.n_comm, d.mb, d.ks1, d.nf, d.ring, d.lo,
+                             c->actor.precision};
+  if (key == c->actor_key) return MDR_OK;
+  if ((size_t)d.off_end > c->actor_cap) {
+    HIP_TRY(hipStreamSynchronize(st));
+    hipFree(c->d_actor);
+    c->d_actor = nullptr;
+    HIP_TRY(hipMalloc(&c->d_actor, d.off_end));
+    c->actor_cap = d.off_end;
+    for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
+    c->actor_graphs.clear();
+  }
+  const mdr_actor_spec& a = c->actor;
+  const float* w1 = c->d_actor_raw;
+  const float* b1 = w1 + (size_t)a.h1 * a.n_in;
+  const float* w2 = b1 + a.h1;
+  const float* b2 = w2 + (size_t)a.h2 * a.h1;
+  const float* w3 = b2 + a.h2;
+  const float* b3 = w3 + (size_t)kActorNA * a.h2;
+  const int nthreads = (d.mb * (d.ks1 + kActorKS2) + 1) * 64;
+  hipLaunchKernelGGL(k_actor_pack, dim3(blocks(nthreads, 256)), dim3(256), 0, st, d, w1, b1, w2, b2, w3, b3,
+                     c->d_actor);
+  LAUNCH_CHECK("k_actor_pack");
+  c->actor_key = key;
+  return MDR_OK;
+}
+
+#define MDR_ACTOR_KERNELS(MB)                                                                        \
+  (const void*)k_actor<1, false, MB>, (const void*)k_actor<3, false, MB>, (const void*)k_actor<6, false, MB>, \
+      (const void*)k_actor<1, true, MB>, (const void*)k_actor<3, true, MB>, (const void*)k_actor<6, true, MB>
+
 int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const double* p_dev, uint64_t tick,
                  const TickArgs* tkp, const ActorOut& out, hipStream_t st) {
   ActorDims d;
   int nw = 0;
   if (int rc = actor_plan(c, sp, &d, &nw)) return rc;
+  d.pp = c->actor_pp && nw == 8;
   const int64_t ntile = (c->kp.n + 32 * nw - 1) / (32 * nw);  // blocks with at least one tile per wave
   const unsigned grid = (unsigned)std::min<int64_t>(ntile, (int64_t)c->n_cu);
   static bool lds_attr = false;  // > 64 KiB of dynamic LDS must be opted into per kernel
   if (!lds_attr) {
-    for (const void* k : {(const void*)k_actor<1, false>, (const void*)k_actor<3, false>, (const void*)k_actor<6, false>,
-                          (const void*)k_actor<1, true>, (const void*)k_actor<3, true>, (const void*)k_actor<6, true>})
+    for (const void* k : {MDR_ACTOR_KERNELS(7), MDR_ACTOR_KERNELS(8)})
       HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     lds_attr = true;
   }
-#define MDR_LAUNCH_ACTOR(P, F)                                                                      \
-  hipLaunchKernelGGL((k_actor<P, F>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
-                     c->d_actor, out, tick, tkp)
+#define MDR_LAUNCH_ACTOR(P, F)                                                                              \
+  do {                                                                                                      \
+    if (d.mb == 7)                                                                                          \
+      hipLaunchKernelGGL((k_actor<P, F, 7>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
+                         c->d_actor, out, tick, tkp);                                                       \
+    else                                                                                                    \
+      hipLaunchKernelGGL((k_actor<P, F, 8>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
+                         c->d_actor, out, tick, tkp);                                                       \
+  } while (0)
   const int prec = c->actor.precision;
   if (out.prof) {
     if (prec == MDR_PREC_BF16) MDR_LAUNCH_ACTOR(1, true);
@@ -1709,11 +1782,13 @@ int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const dou
   return MDR_OK;
 }
 
-int check_actor_obs(const mdr_ctx* c, const mdr_obs_spec* sp, const char* who) {
+// the spec is valid for the loaded actor; the weights are packed for its slot layout (before any
+// launch or graph capture of the caller)
+int check_actor_obs(mdr_ctx* c, const mdr_obs_spec* sp, const char* who, hipStream_t st) {
   if (!c->actor_ready) return fail(MDR_ESTATE, std::string(who) + ": no actor loaded (mdr_actor_load)");
   if (int rc = check_obs_spec(sp, who)) return rc;
   if (sp->n_feat != c->actor.n_in) return fail(MDR_EARG, std::string(who) + ": obs n_feat != actor n_in");
-  return MDR_OK;
+  return actor_ensure_packed(c, sp, st);
 }
 
 }  // namespace
@@ -1728,20 +1803,26 @@ int mdr_actor_load(mdr_ctx* c, const mdr_actor_spec* a, const float* w1, const f
     return fail(MDR_EARG, "mdr_actor_load: shape outside n_in <= 128, hidden <= 128, n_act == 2");
   if (a->precision != MDR_PREC_BF16 && a->precision != MDR_PREC_BF16X3 && a->precision != MDR_PREC_FP32)
     return fail(MDR_EARG, "mdr_actor_load: bad precision");
-  const ActorDims d = actor_layout(*a, nullptr, 2);
-  if ((size_t)d.off_end > c->actor_cap) {
+  // the fp32 weights, kept on device: the packed image depends on the obs layout, so it is made
+  // by the first actor call of each layout (actor_ensure_packed)
+  const size_t nraw = (size_t)a->h1 * a->n_in + a->h1 + (size_t)a->h2 * a->h1 + a->h2 + (size_t)kActorNA * a->h2 +
+                      kActorNA;
+  if (nraw * sizeof(float) > c->actor_raw_cap) {
     HIP_TRY(hipStreamSynchronize(S(stream)));
-    hipFree(c->d_actor);
-    c->d_actor = nullptr;
-    HIP_TRY(hipMalloc(&c->d_actor, d.off_end));
-    c->actor_cap = d.off_end;
-    for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
-    c->actor_graphs.clear();
+    hipFree(c->d_actor_raw);
+    c->d_actor_raw = nullptr;
+    HIP_TRY(hipMalloc(&c->d_actor_raw, nraw * sizeof(float)));
+    c->actor_raw_cap = nraw * sizeof(float);
   }
-  const int nthreads = (kActorMB * (d.ks1 + d.ks2) + 1) * 64;
-  hipLaunchKernelGGL(k_actor_pack, dim3(blocks(nthreads, 256)), dim3(256), 0, S(stream), d, w1, b1, w2, b2, w3,
-                     b3, c->d_actor);
-  LAUNCH_CHECK("k_actor_pack");
+  float* r = c->d_actor_raw;
+  const std::pair<const float*, size_t> parts[6] = {{w1, (size_t)a->h1 * a->n_in}, {b1, (size_t)a->h1},
+                                                    {w2, (size_t)a->h2 * a->h1}, {b2, (size_t)a->h2},
+                                                    {w3, (size_t)kActorNA * a->h2}, {b3, (size_t)kActorNA}};
+  for (const auto& pt : parts) {
+    HIP_TRY(hipMemcpyAsync(r, pt.first, pt.second * sizeof(float), hipMemcpyDeviceToDevice, S(stream)));
+    r += pt.second;
+  }
+  c->actor_key.clear();
   c->actor = *a;
   c->actor_ready = true;
   return MDR_OK;
@@ -1753,7 +1834,7 @@ int mdr_actor_act(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc,
   drop_begun(c);
   if (!c || !sp || !sc) return fail(MDR_EARG, "mdr_actor_act: null argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_act: context not bound");
-  if (int rc = check_actor_obs(c, sp, "mdr_actor_act")) return rc;
+  if (int rc = check_actor_obs(c, sp, "mdr_actor_act", S(stream))) return rc;
   hipStream_t st = S(stream);
   ActorOut out{action, prob, probs, obs_out, nullptr, nullptr};
   if (count_next) {
@@ -1770,7 +1851,7 @@ int mdr_actor_profile(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars*
                       double* cycles_out, void* stream) {
   if (!c || !sp || !sc || !cycles_out) return fail(MDR_EARG, "mdr_actor_profile: null argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_profile: context not bound");
-  if (int rc = check_actor_obs(c, sp, "mdr_actor_profile")) return rc;
+  if (int rc = check_actor_obs(c, sp, "mdr_actor_profile", S(stream))) return rc;
   hipStream_t st = S(stream);
   const int nb = c->n_cu * 8;  // waves (at most 8 per block, one block per CU)
   unsigned long long* d = nullptr;
@@ -1803,7 +1884,7 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
   drop_begun(c);
   if (!c || !ticks || !osc || !sp || !reward || !p_dev || n < 1) return fail(MDR_EARG, "mdr_actor_rollout: bad argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_rollout: context not bound");
-  if (int rc = check_actor_obs(c, sp, "mdr_actor_rollout")) return rc;
+  if (int rc = check_actor_obs(c, sp, "mdr_actor_rollout", S(stream))) return rc;
   if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
     return fail(MDR_EARG, "mdr_actor_rollout: common penalty modes need the per-step API");
   hipStream_t st = S(stream);
@@ -1868,7 +1949,7 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
     return fail(MDR_EARG, "mdr_actor_rollout_sharded: bad argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_rollout_sharded: context not bound");
   if (!c->comm) return fail(MDR_ESTATE, "mdr_actor_rollout_sharded: RCCL not initialised");
-  if (int rc = check_actor_obs(c, sp, "mdr_actor_rollout_sharded")) return rc;
+  if (int rc = check_actor_obs(c, sp, "mdr_actor_rollout_sharded", S(stream))) return rc;
   if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
     return fail(MDR_EARG, "mdr_actor_rollout_sharded: common penalty modes need the per-step API");
   const int K = sp->n_comm, M = mdr_msg_width(sp);

@@ -161,6 +161,7 @@ constexpr int kGqMaxRanks = 64;   // sharded histogram select: ranks whose windo
 struct GqSel;
 void gq_sel_init(void* sel128, uint32_t* map);  // host: the first call's key map (uniform over [-32, 32])
 void gq_diag_of(const void* sel128, uint64_t* out);
+void gq_state_of(const void* sel128, uint64_t* out);  // gq_diag_of + {sb, bstar, bend, all, overflow, more_after, wcount, need_fb}
 size_t gq_wcount_offset();   // host: byte offsets of GqSel.wcount / .need_fb (sharded select)
 size_t gq_need_fb_offset();  // host: [fallbacks, calls, sum of window sizes, last window]
 __global__ void k_gq_keys(KParams p, uint32_t* code, double* part, unsigned* hist, const GqSel* sel,

@@ -92,6 +92,7 @@ struct GqSel {
   double base_tot;               // P of the houses before the window (exact for integer P)
   unsigned long long base_cnt, total;
   int sb, bstar, bend, all, overflow, more_after, ncand;
+  int whole;                     // the cluster fits the window (<= kGqCap houses): every house is a candidate
   unsigned fallbacks;            // calls decided by the exact fallback (gq_exact; diagnostics)
   unsigned wcount;               // k_gq_compact's window allocator (zeroed by k_gq_bins)
   unsigned calls;                // diagnostics: decisions made, and the sum of their window sizes
@@ -101,8 +102,8 @@ struct GqSel {
 static_assert(sizeof(GqSel) <= 128, "GqSel fits the 128-B sel buffer");
 void gq_sel_init(void* sel128, uint32_t* map) {
   GqSel* g = static_cast<GqSel*>(sel128);  // (a zeroed 128-B host buffer)
-  g->kmin = -32.0;                          // the first call: uniform bins over keys in [-32, 32]
-  g->scale = (double)kGqCells / 64.0;
+  g->kmin = -4.0;                           // the first call: uniform bins over keys in [-4, 4] (K from
+  g->scale = (double)kGqCells / 8.0;        // the target; keys outside clamp into the end cells)
   for (int c = 0; c < kGqCells; ++c) map[c] = ((uint32_t)(c * (kGqBins / kGqCells)) << 16) | (uint32_t)(kGqBins / kGqCells);
 }
 size_t gq_wcount_offset() { return offsetof(GqSel, wcount); }
@@ -113,6 +114,12 @@ void gq_diag_of(const void* sel128, uint64_t* out) {
   out[1] = g->calls;
   out[2] = g->ncand_sum;
   out[3] = (uint64_t)(int64_t)g->ncand;
+}
+void gq_state_of(const void* sel128, uint64_t* out) {
+  const GqSel* g = static_cast<const GqSel*>(sel128);
+  gq_diag_of(sel128, out);
+  const int v[8] = {g->sb, g->bstar, g->bend, g->all, g->overflow, g->more_after, (int)g->wcount, (int)g->need_fb};
+  for (int k = 0; k < 8; ++k) out[4 + k] = (uint64_t)(int64_t)v[k];
 }
 
 constexpr int kGqSupN = kGqSuper + 1;  // superbins + one for NaN keys (sorted last, pandas' na_position)
@@ -139,6 +146,12 @@ __device__ __forceinline__ int gq_bin(double k, double kmin, double scale, const
   const int w = (int)(m & 0xFFFFu);
   const double f = (u - (double)c) * (double)w;
   return (int)(m >> 16) + (f >= (double)(w - 1) ? w - 1 : (f > 0.0 ? (int)f : 0));
+}
+// bins the key map spreads over for a cluster of n houses: about 8 houses per bin at most, so a
+// window of 64 bins holds a few hundred houses however small the cluster (a multiple of 64, >= 1024)
+__host__ __device__ __forceinline__ int gq_bins_eff(int64_t n) {
+  const int64_t b = (n / 8) & ~(int64_t)63;
+  return b >= kGqBins ? kGqBins : (b < 1024 ? 1024 : (int)b);
 }
 // a house's code: its key bin (kGqBins for a NaN key) << 2 | its capacity class; the superbin is
 // code >> 8 (kGqBins / kGqSuper = 64 bins each; NaN keys land in superbin kGqSuper)
@@ -1567,10 +1580,11 @@ __global__ void __launch_bounds__(kObsBlock) k_obs(KParams p, ObsArgs o, const d
   __shared__ float cf[kObsConst];
   obs_consts(p, o, p_dev ? *p_dev : o.p, cf, threadIdx.x, kObsBlock);
   __syncthreads();
-  obs_stage_ring(p, o, b0, nb, cf, msg, threadIdx.x, kObsBlock);
+  const ObsDiv dv = obs_div(p);
+  obs_stage_ring(p, o, b0, nb, cf, msg, threadIdx.x, kObsBlock, dv);
   __syncthreads();
   const int t = threadIdx.x;
-  if (t < nb) obs_build_row(p, o, b0 + t, t, cf, msg, tile + t * F);
+  if (t < nb) obs_build_row(p, o, b0 + t, t, cf, msg, tile + t * F, dv);
   __syncthreads();
   // coalesced flush of the contiguous tile obs[b0 .. b0+nb) rows
   const int64_t nflt = (int64_t)nb * F;
@@ -1593,11 +1607,12 @@ __global__ void k_halo_pack(KParams p, ObsArgs o, int lo, int hi, float* out) {
   __shared__ float cf[kObsConst];
   obs_consts(p, o, o.p, cf, t, blockDim.x);  // (the message features use only cf[8..] and P_max/R)
   __syncthreads();
-  if (t < hi) msg_features(p, o, t % p.n, cf, out + t * M);
+  const ObsDiv dv = obs_div(p);
+  if (t < hi) msg_features(p, o, t % p.n, cf, out + t * M, dv);
   else if (t < hi + lo) {
     int64_t j = p.n - lo + (t - hi);
     if (j < 0) j = ((j % p.n) + p.n) % p.n;
-    msg_features(p, o, j, cf, out + t * M);
+    msg_features(p, o, j, cf, out + t * M, dv);
   }
 }
 
@@ -1607,7 +1622,7 @@ __global__ void k_msg_pack(KParams p, ObsArgs o, float* out) {
   obs_consts(p, o, o.p, cf, threadIdx.x, blockDim.x);  // (messages use only cf[8..] and P_max/R)
   __syncthreads();
   const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < p.n) msg_features(p, o, i, cf, out + i * o.msg_w);
+  if (i < p.n) msg_features(p, o, i, cf, out + i * o.msg_w, obs_div(p));
 }
 
 // --------------------------------------------------------------------------------------- greedy
@@ -1804,6 +1819,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_
   __shared__ double s_w[NW];
   __shared__ unsigned long long s_wc[NW];
   __shared__ int s_first;
+  __shared__ unsigned long long s_total;
   const int tid = threadIdx.x;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int64_t i00 = (int64_t)blockIdx.x * blockDim.x + tid;
@@ -1831,15 +1847,19 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_
   gq_block_scan(x, xc, s_w, s_wc);
   const double before = x - ps;
   if (tid < kGqSupN && cs > 0 && !(before + ps < S)) atomicMin(&s_first, tid);  // (the first: a non-empty superbin)
+  if (tid == kGqSupN - 1) s_total = xc;
   __syncthreads();
   const int sb = s_first;
+  // a cluster of <= kGqCap houses is one window (the select orders all of it, NaN keys included)
+  const bool whole = sb < kGqSupN && s_total <= (unsigned long long)kGqCap;
   if (blockIdx.x == 0) {
     if (tid == sb) { sel->base_tot = before; sel->base_cnt = xc - cs; }
     if (tid == kGqSupN - 1) sel->total = xc;
     if (tid == 0) {
       sel->sb = sb;
       sel->all = sb >= kGqSupN;
-      sel->overflow = sb == kGqSuper;  // the crossing among NaN keys: the fallback orders them by house
+      sel->overflow = sb == kGqSuper && !whole;  // the crossing among NaN keys: the fallback orders them by house
+      sel->whole = whole;
       sel->wcount = 0u;
       sel->need_fb = 0u;
     }
@@ -1888,11 +1908,11 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_
     }
     __syncthreads();
     if (tid < kGqCells) {  // B0_g = g + floor(K (C_g - C_0) / (C_G - C_0)): non-decreasing in g, so W_g >= 1
-      constexpr int K = kGqBins - kGqCells;
+      const int NBE = gq_bins_eff(p.n_global), K = NBE - kGqCells;
       const double T = s_C[kGqCells] - s_C[0];
       auto edge = [&](int g) {
-        if (g >= kGqCells) return kGqBins;
-        if (!(T > 0.0)) return g * (kGqBins / kGqCells);  // (no spread seen: uniform cells)
+        if (g >= kGqCells) return NBE;
+        if (!(T > 0.0)) return g * (NBE / kGqCells);  // (no spread seen: uniform cells)
         return g + min(K, (int)((double)K * ((s_C[g] - s_C[0]) / T)));
       };
       const int b0 = edge(tid), b1 = edge(tid + 1);
@@ -1902,7 +1922,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_
     if (slab)
       for (int e = tid; e < kCountShards * p.n_cap; e += blockDim.x) slab[e] = 0ull;
   }
-  if (sb >= kGqSuper) return;  // everything taken, or a NaN crossing (block-uniform)
+  if (sb >= kGqSuper || whole) return;  // everything taken, a NaN crossing, or one window (block-uniform)
   for (int e = tid; e < NW * NB * 4; e += blockDim.x) (&s_h[0][0])[e] = 0u;
   __syncthreads();
   const int bb = sb * (kGqBins / kGqSuper);
@@ -1962,8 +1982,8 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     cd[u] = i < p.n ? code[i] : 0u;
     hw[u] = i < p.n ? p.hvac[i] : 0u;
   }
-  const bool all = sel->all, ovf = sel->overflow;
-  const bool on = !all && !ovf;
+  const bool all = sel->all, ovf = sel->overflow, whole = sel->whole;
+  const bool on = !all && !ovf && !whole;
   const int bb = sel->sb * 64;
   if (tid < kWinCap) s_cnt[tid] = 0u;
   if (tid == 0) { s_l0 = 0; s_le = 0; }
@@ -2029,9 +2049,16 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
       sel->ncand = cnt;
     }
   }
+  if (whole && blockIdx.x == 0 && tid == 0) {  // every house is in the window
+    sel->bstar = 0;
+    sel->bend = kGqBins;
+    sel->base_tot = 0.0;
+    sel->more_after = 0;
+    sel->ncand = (int)sel->total;
+  }
   __syncthreads();
   if (ovf || s_le < 0) return;  // the fallback in k_gq_select decides every house (block-uniform)
-  const int bs = bb + s_l0, be = bb + s_l0 + s_le;
+  const int bs = whole ? -1 : bb + s_l0, be = whole ? kGqBins : bb + s_l0 + s_le;
   unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
   bool inw[U];
   unsigned mine = 0u;

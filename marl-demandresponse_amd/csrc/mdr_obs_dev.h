@@ -62,17 +62,42 @@ __device__ __forceinline__ void obs_consts(const KParams& p, const ObsArgs& o, d
   for (int k = tid; k < p.n_cap; k += nthr) cf[kObsPmr + k] = (float)(p.p_on[k] / R);
 }
 
-// int(sso / L) of norm.py: for 0 <= sso < 2^30 and L >= 1 the float64 quotient never rounds up to
-// the next integer, so truncating it equals the integer quotient
-__device__ __forceinline__ float sso_ratio(uint32_t w, int L) { return (float)(hv_sso(w) / (uint32_t)L); }
+// The divisions of the row expressions, set up once per kernel: x / 5.0 as the shared-reciprocal
+// sequence (mdr_device.h Recip: bit-identical to the IEEE quotient; the operator for zero,
+// non-finite or extreme x), and int(sso / L) as a multiply by the float64 reciprocal of L with one
+// correction (for sso < 2^30 the product is within 2^-52 relative of sso / L, so its truncation is
+// the quotient or one less; exact multiples are corrected up).
+struct ObsDiv {
+  Recip r5;
+  double rL;
+  uint32_t L;
+};
+__device__ __forceinline__ ObsDiv obs_div(const KParams& p) {
+  ObsDiv d;
+  d.r5 = recip(5.0);
+  d.L = p.L < 1 ? 1u : (uint32_t)p.L;
+  d.rL = 1.0 / (double)d.L;
+  return d;
+}
+__device__ __forceinline__ double div5(double a, const ObsDiv& dv) {
+  return div_safe(a) ? div_by(a, dv.r5) : a / 5.0;
+}
+// int(sso / L) of norm.py (sso < 2^30: the float64 quotient never rounds up to the next integer,
+// so truncating it equals the integer quotient)
+__device__ __forceinline__ float sso_ratio(uint32_t w, const ObsDiv& dv) {
+  const uint32_t a = hv_sso(w);
+  uint32_t q = (uint32_t)((double)a * dv.rL);
+  q += a - q * dv.L >= dv.L ? 1u : 0u;
+  return (float)q;
+}
 
 // Message a house sends (Building.message, building.py:101-139, normalised by norm.py:60-110):
 // (T - target)/5, int(sso/L), P/R, P_max/R [, Ua, Ca, Cm, Hm ratios][, cop, lcf, cap]
 __device__ __forceinline__ void msg_from_regs(const KParams& p, const ObsArgs& o, const HouseRegs& r,
-                                              const float* cf, float* dst) {
+                                              const float* cf, float* dst, const ObsDiv& dv) {
   const float pmr = cf[kObsPmr + r.cls];
-  dst[0] = (float)((r.T - r.tg) / 5.0);
-  dst[1] = sso_ratio(r.w, p.L);
+  dst[0] = (float)div5(r.T - r.tg, dv);
+  dst[1] = sso_ratio(r.w, dv);
   dst[2] = hv_on(r.w) ? pmr : 0.f;  // (0.0 / R) == +0
   dst[3] = pmr;
   int f = 4;
@@ -90,27 +115,27 @@ __device__ __forceinline__ void msg_from_regs(const KParams& p, const ObsArgs& o
 }
 
 __device__ __forceinline__ void msg_features(const KParams& p, const ObsArgs& o, int64_t j, const float* cf,
-                                             float* dst) {
+                                             float* dst, const ObsDiv& dv) {
   HouseRegs r;
   house_load(p, j, o.msg_thermal != 0, r);
-  msg_from_regs(p, o, r, cf, dst);
+  msg_from_regs(p, o, r, cf, dst, dv);
 }
 
 // The house's own features (everything before the messages); returns how many were written.
 __device__ __forceinline__ int row_scalars(const KParams& p, const ObsArgs& o, const HouseRegs& r,
-                                           const float* cf, float* row) {
+                                           const float* cf, float* row, const ObsDiv& dv) {
   int f = 0;
   row[f++] = hv_on(r.w) ? 1.f : 0.f;
   row[f++] = hv_lock(r.w) ? 1.f : 0.f;
-  row[f++] = sso_ratio(r.w, p.L);
+  row[f++] = sso_ratio(r.w, dv);
   row[f++] = cf[0];
   if (o.hvac_state) { row[f++] = cf[1]; row[f++] = cf[2]; }
   row[f++] = cf[3];
   row[f++] = cf[4];
   row[f++] = cf[5];
-  row[f++] = (float)((r.T - 20.0) / 5.0);
-  row[f++] = (float)((r.Tm - 20.0) / 5.0);
-  row[f++] = (float)((r.tg - 20.0) / 5.0);
+  row[f++] = (float)div5(r.T - 20.0, dv);
+  row[f++] = (float)div5(r.Tm - 20.0, dv);
+  row[f++] = (float)div5(r.tg - 20.0, dv);
   if (o.solar_state) row[f++] = cf[6];
   if (o.thermal_state) {
     row[f++] = (float)(r.ua / o.cfg_ua);
@@ -125,7 +150,7 @@ __device__ __forceinline__ int row_scalars(const KParams& p, const ObsArgs& o, c
 // RING topology: message sources of the houses [b0, b0 + nb) are [b0 - lo, b0 + nb + hi);
 // their features go to msg[(s) * M] for s = 0 .. lo + nb + hi.  Threads tid, tid + nthr, ...
 __device__ __forceinline__ void obs_stage_ring(const KParams& p, const ObsArgs& o, int64_t b0, int nb,
-                                               const float* cf, float* msg, int tid, int nthr) {
+                                               const float* cf, float* msg, int tid, int nthr, const ObsDiv& dv) {
   const int K = o.n_comm, M = o.msg_w;
   if (o.comm_mode != MDR_COMM_RING || K <= 0) return;
   const int lo = K / 2, hi = (K + 1) / 2;
@@ -139,14 +164,15 @@ __device__ __forceinline__ void obs_stage_ring(const KParams& p, const ObsArgs& 
     } else {
       j %= p.n;
       if (j < 0) j += p.n;
-      msg_features(p, o, j, cf, msg + s * M);
+      msg_features(p, o, j, cf, msg + s * M, dv);
     }
   }
 }
 
 // Messages of local house i (row index t in the block tile) appended at row[f ..).
 __device__ __forceinline__ void row_messages(const KParams& p, const ObsArgs& o, int64_t i, int t,
-                                             const float* cf, const float* msg, float* row, int f) {
+                                             const float* cf, const float* msg, float* row, int f,
+                                             const ObsDiv& dv) {
   const int M = o.msg_w, K = o.n_comm;
   const int lo = K / 2;
   if (K <= 0) return;
@@ -164,7 +190,7 @@ __device__ __forceinline__ void row_messages(const KParams& p, const ObsArgs& o,
         for (int m = 0; m < M; ++m) row[f++] = o.msg_all[j * M + m];
         continue;
       }
-      msg_features(p, o, j, cf, tmp);
+      msg_features(p, o, j, cf, tmp, dv);
       for (int m = 0; m < M; ++m) row[f++] = tmp[m];
     }
   }
@@ -173,11 +199,12 @@ __device__ __forceinline__ void row_messages(const KParams& p, const ObsArgs& o,
 // The F-wide row of local house i (= b0 + t) into row[0 .. F); cf: obs_consts of the tick.
 // The hvac word is returned (callers that need the FSM state reuse the load).
 __device__ __forceinline__ uint32_t obs_build_row(const KParams& p, const ObsArgs& o, int64_t i, int t,
-                                                  const float* cf, const float* msg, float* row) {
+                                                  const float* cf, const float* msg, float* row,
+                                                  const ObsDiv& dv) {
   HouseRegs r;
   house_load(p, i, o.thermal_state != 0, r);
-  const int f = row_scalars(p, o, r, cf, row);
-  row_messages(p, o, i, t, cf, msg, row, f);
+  const int f = row_scalars(p, o, r, cf, row, dv);
+  row_messages(p, o, i, t, cf, msg, row, f, dv);
   return r.w;
 }
 

@@ -266,6 +266,14 @@ class HipShard:
         L.check(self.lib.mdr_greedy_diag(self.ctx, v), "mdr_greedy_diag")
         return {"fallbacks": int(v[0]), "calls": int(v[1]), "window_sum": int(v[2]), "window_last": int(v[3])}
 
+    def greedy_state(self) -> dict:
+        """The select's state after its last stage (mdr_greedy_state; synchronises)."""
+        v = (C.c_uint64 * 12)()
+        L.check(self.lib.mdr_greedy_state(self.ctx, v), "mdr_greedy_state")
+        names = ("fallbacks", "calls", "window_sum", "window_last", "sb", "bstar", "bend", "all", "overflow",
+                 "more_after", "wcount", "need_fb")
+        return {k: C.c_int64(v[i]).value for i, k in enumerate(names)}
+
     def obs(self, spec, scalars, out, use_p_dev=True):
         L.check(self.lib.mdr_obs(self.ctx, C.byref(spec), C.byref(scalars),
                                  L.ptr(self.p_dev) if use_p_dev else 0, L.ptr(out), self.stream()),

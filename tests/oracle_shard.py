@@ -172,7 +172,7 @@ class OracleShard:
 
     def gq_shard_begin(self):
         if not hasattr(self, "_gq_range"):
-            self._gq_range = (-32.0, 32.0)
+            self._gq_range = (-4.0, 4.0)
         k = -(self.t_air.numpy() - self.target.numpy())
         self._gq_k, self._gq_b = k, self._gq_bins_of(k)
         cls = self.cap_idx.numpy().astype(np.int64)
@@ -212,11 +212,21 @@ class OracleShard:
         self._gq_range = self._gq_next
         act = np.zeros(self.n, np.uint8)
         sb, n_sup = self._gq_sb, self.GQ_SUP
-        self._gq_fb = sb == n_sup  # a NaN crossing: the all-gather form decides
+        whole = sb <= n_sup and self._gq_total <= self.GQ_CAP  # a cluster that fits the window is the window
+        self._gq_fb = sb == n_sup and not whole  # a NaN crossing: the all-gather form decides
         win = self._gq["window"].numpy()
         win[0] = 0
         if sb > n_sup:  # everything fits the budget
             act[:] = 1
+        elif whole:
+            self._gq_wbase, self._gq_more, self._gq_ncand = 0.0, False, self._gq_total
+            inw = np.arange(self.n)
+            _, lk, _ = decode_hvac(self.hvac.numpy().copy())
+            pw = self._gq_p()[self.cap_idx.numpy()]
+            win[0] = inw.size
+            rows = np.stack([self._gq_k[inw], (inw + self.offset).astype(np.float64), pw[inw],
+                             lk[inw].astype(np.float64)], 1)
+            win[1:1 + 4 * inw.size] = rows.reshape(-1)
         elif not self._gq_fb:
             bins = self._gq["bins"].numpy().reshape(-1, 4).astype(np.int64)
             p = self._gq_p()
