@@ -806,6 +806,13 @@ __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long lon
   win_reduce_body(p, slot, nt, tkp ? tkp + blockIdx.x : nullptr, p_out);
 }
 
+// LDS written by some lanes of a wave and read by others (the wave's LDS operations execute in
+// issue order: a wavefront-scope fence orders the compiler and waits lgkmcnt)
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+}
+
 // True in exactly one block of the grid: the last to arrive, after every block's earlier vector
 // memory operations have completed (each wave drains them, vmcnt(0), before the workgroup barrier).
 // Two-level ticket: block b adds to the counter of group b % G (G = min(grid, kTicketGroups), each
@@ -844,37 +851,62 @@ __device__ bool grid_last_block(unsigned* __restrict__ tickets) {
 // the last block reads the shards only with 8-B agent-scope (sc1) loads.
 __device__ void win_reduce_last(const KParams& p, unsigned long long* __restrict__ slot, int nt,
                                 unsigned* __restrict__ ticket) {
+  constexpr int NW = 4;                  // (blockDim 256)
+  constexpr int JW = kWinMax / NW;       // ticks per wave: j = wave + 4 k
+  constexpr int KR = 2;                  // ticks per transpose round (KR * kWinCap entries of 64 shards)
+  __shared__ unsigned s_t[NW][KR * kWinCap][kCountShards];  // a round's shard values, transposed for the sums
   __shared__ unsigned long long s_red[kWinMax * kWinCap];
   if (!grid_last_block(ticket)) return;  // (block-uniform)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only: the loads below are sc1)
-  const int ncap = p.n_cap, ne = nt * ncap, q = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  constexpr int NW = 4;  // (blockDim 256)
-  constexpr int E = kWinMax * kWinCap / NW;
-  unsigned long long v[E];
+  const int ncap = p.n_cap, q = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  // lane q reads shard q of the wave's (tick, class) entries: the low words of the 8-B shard counters
+  // (a shard's count < 2^32: the clusters have < 2^29 houses), every load issued before the first use
+  unsigned v[JW][kWinCap];
 #pragma unroll
-  for (int k = 0; k < E; ++k) {  // every load issued before the first use
-    const int e = wv + NW * k;
-    v[k] = 0ull;
-    if (e < ne) {
-      const int j = e / ncap, c = e - j * ncap;
-      v[k] = __hip_atomic_load(&slot[((size_t)j * kCountShards + q) * ncap + c], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < JW; ++k)
+#pragma unroll
+    for (int c = 0; c < kWinCap; ++c) {
+      const int j = wv + NW * k;
+      v[k][c] = 0u;
+      if (j < nt && c < ncap)
+        v[k][c] = __hip_atomic_load(reinterpret_cast<unsigned*>(&slot[((size_t)j * kCountShards + q) * ncap + c]),
+                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-  }
 #pragma unroll
-  for (int k = 0; k < E; ++k) {
-    const int e = wv + NW * k;
-    if (e >= ne) break;  // (wave-uniform)
-    const int j = e / ncap, c = e - j * ncap;
-    __hip_atomic_store(&slot[((size_t)j * kCountShards + q) * ncap + c], 0ull, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);  // (the slot's next count adds into zeros)
-    unsigned long long x = v[k];
+  for (int k = 0; k < JW; ++k)
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-    if (q == 0) s_red[e] = x;
+    for (int c = 0; c < kWinCap; ++c) {
+      const int j = wv + NW * k;
+      if (j < nt && c < ncap)  // (the slot's next count adds into zeros)
+        __hip_atomic_store(&slot[((size_t)j * kCountShards + q) * ncap + c], 0ull, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+  // rounds of KR ticks: the wave writes its lanes' values transposed, lane e sums entry e's 64 shards
+#pragma unroll
+  for (int r = 0; r < JW / KR; ++r) {
+    if (wv + NW * KR * r >= nt) break;  // (wave-uniform)
+#pragma unroll
+    for (int kk = 0; kk < KR; ++kk)
+#pragma unroll
+      for (int c = 0; c < kWinCap; ++c) s_t[wv][kk * kWinCap + c][q] = v[KR * r + kk][c];
+    wave_lds_sync();
+    if (q < KR * kWinCap) {
+      const int c = q % kWinCap, j = wv + NW * (KR * r + q / kWinCap);
+      if (j < nt && c < ncap) {
+        const uint4* rd = reinterpret_cast<const uint4*>(s_t[wv][q]);
+        unsigned long long x = 0ull;
+#pragma unroll
+        for (int i = 0; i < kCountShards / 4; ++i) {
+          const uint4 u = rd[i];
+          x += (unsigned long long)u.x + u.y + u.z + u.w;
+        }
+        s_red[j * ncap + c] = x;
+      }
+    }
+    wave_lds_sync();
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < ne; e += blockDim.x) win_red(slot, ncap)[e] = s_red[e];
+  for (int e = threadIdx.x; e < nt * ncap; e += blockDim.x) win_red(slot, ncap)[e] = s_red[e];
   if ((int)threadIdx.x < nt) {
     double p_on[kWinCap];
 #pragma unroll
