@@ -238,6 +238,12 @@ template <typename V>
 __device__ __forceinline__ void sto(void* base, uint32_t off, V v) {
   *reinterpret_cast<V*>(reinterpret_cast<char*>(base) + off) = v;
 }
+// reward rows: written once, never re-read by the step kernels — non-temporal stores keep them from
+// evicting the state and parameters the next launch reads (the Infinity Cache holds them at 1M houses)
+__device__ __forceinline__ void sto_nt(void* base, uint32_t off, double2 v) {
+  typedef double d2 __attribute__((ext_vector_type(2)));
+  __builtin_nontemporal_store(d2{v.x, v.y}, reinterpret_cast<d2*>(reinterpret_cast<char*>(base) + off));
+}
 
 template <int HPT, bool FAST, int ACT, int LA>
 __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __restrict__ action,
@@ -376,13 +382,13 @@ __global__ void __launch_bounds__(256) k_step_t(KParams p, const uint8_t* __rest
     sto(p.t_air, o8, make_double2(Tn[0], Tn[HPT - 1]));
     sto(p.t_mass, o8, make_double2(Tmn[0], Tmn[HPT - 1]));
     sto(p.hvac, i0 * 4u, make_uint2(w[0], w[HPT - 1]));
-    if (write_rew) sto(reward, o8, make_double2(rw[0], rw[HPT - 1]));
+    if (write_rew) sto_nt(reward, o8, make_double2(rw[0], rw[HPT - 1]));
   } else {
 #pragma unroll
     for (int h = 0; h < HPT; ++h)
       if (valid[h]) {
         p.t_air[i0 + h] = Tn[h]; p.t_mass[i0 + h] = Tmn[h]; p.hvac[i0 + h] = w[h];
-        if (write_rew) reward[i0 + h] = rw[h];
+        if (write_rew) __builtin_nontemporal_store(rw[h], reward + i0 + h);
       }
   }
   if (ctrl != MDR_CTRL_NONE && ctrl_out) {
@@ -596,10 +602,10 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
       sto(p.t_air, o8, make_double2(Tn[0], Tn[1]));
       sto(p.t_mass, o8, make_double2(Tmn[0], Tmn[1]));
       sto(p.hvac, i0 * 4u, make_uint2(w[0], w[1]));
-      if (counts) sto(reward, o8, make_double2(rw[0], rw[1]));
+      if (counts) sto_nt(reward, o8, make_double2(rw[0], rw[1]));
     } else if (valid[0]) {
       p.t_air[i0] = Tn[0]; p.t_mass[i0] = Tmn[0]; p.hvac[i0] = w[0];
-      if (counts) reward[i0] = rw[0];
+      if (counts) __builtin_nontemporal_store(rw[0], reward + i0);
     }
     if (GQ) {  // greedy_myopic_controller.py:79 on the post-step state (gq_key_of)
       const double k0 = -(Tn[0] - tg[0]), k1 = -(Tn[1] - tg[1]);
@@ -1295,7 +1301,7 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
           tk[h] = tkn;
           tmk[h] = tmkn;
           const double r = reward_of(h, tkn - 273.0, tkn, fast_c);  // (Celsius unused on the SIMPLE fast path)
-          if (t.v[h]) *reinterpret_cast<double*>(rrow + (rb + 512u * h)) = r;
+          if (t.v[h]) __builtin_nontemporal_store(r, reinterpret_cast<double*>(rrow + (rb + 512u * h)));
         }
       };
       if (win_finite && tick_ok) houses(std::true_type());
@@ -1318,7 +1324,7 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
           T[h] = Tn;
           Tm[h] = Tmn;
           const double r = reward_of(h, Tn, 0.0, fast_c);
-          if (t.v[h]) *reinterpret_cast<double*>(rrow + (rb + 512u * h)) = r;
+          if (t.v[h]) __builtin_nontemporal_store(r, reinterpret_cast<double*>(rrow + (rb + 512u * h)));
         }
       };
       if (fast) houses(std::true_type());
