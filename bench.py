@@ -564,6 +564,8 @@ def main():
                            "step_share": {"what": "launch-stream time per tick minus k_actor's time: the step "
                                                   "kernel's share of a tick (not a kernel duration)",
                                           "us_per_tick": kern_ms * 1e3}}
+    out["build"] = {"lib": os.path.relpath(L.LIB_PATH, os.path.dirname(os.path.abspath(__file__))),
+                    "src_hash": L.build_id(), "checked_against_tree": L.source_hash() == L.build_id()}
     if cpu is not None:
         out["cpu_baseline"] = cpu
     if rank == 0:

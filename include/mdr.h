@@ -123,6 +123,9 @@ typedef struct mdr_ctx mdr_ctx;
 
 /* ---- lifecycle ------------------------------------------------------------------------- */
 int mdr_abi_version(void);
+/* "MDR_SRC_HASH:<16 hex>": sha256 of the sources and build flags the library was built from
+ * (build_ext.py src_hash); the Python binding refuses a library whose hash differs from its tree's. */
+const char* mdr_build_id(void);
 /* sizeof of the ABI structs, for binding checks: out[0..7] = mdr_config, mdr_soa, mdr_tick,
  * mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars, mdr_actor_spec, mdr_interp_spec; returns the number
  * written */

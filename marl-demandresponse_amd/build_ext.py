@@ -6,7 +6,9 @@ operation with its own rounding) and no fast-math (correctly rounded fp64 divisi
 """
 from __future__ import annotations
 
+import hashlib
 import os
+import re
 import shutil
 import subprocess
 import sys
@@ -31,11 +33,29 @@ def hipcc() -> str:
     raise RuntimeError("hipcc not found")
 
 
+def src_hash() -> str:
+    """sha256 (16 hex digits) of the library's sources, headers and build flags: stamped into the
+    library at build time (mdr_build_id) and checked by mdr_amd._lib.load, so a library that was
+    not built from the sources next to it is refused."""
+    h = hashlib.sha256(" ".join(FLAGS).encode())
+    for p in SRC + HDR:
+        h.update(os.path.basename(p).encode() + b"\0")
+        with open(p, "rb") as f:
+            h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def lib_hash(path: str = OUT) -> str | None:
+    """The source hash stamped into a built library (None if absent or unstamped)."""
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        m = re.search(rb"MDR_SRC_HASH:([0-9a-f]{16})", f.read())
+    return m.group(1).decode() if m else None
+
+
 def up_to_date() -> bool:
-    if not os.path.exists(OUT):
-        return False
-    t = os.path.getmtime(OUT)
-    return all(os.path.getmtime(s) <= t for s in SRC + HDR + [__file__])
+    return lib_hash(OUT) == src_hash()
 
 
 HOST_SRC = os.path.join(HERE, "csrc", "mdr_host.c")
@@ -74,8 +94,8 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
     if not force and out == OUT and up_to_date():
         return out
     tmp = out + ".tmp"
-    cmd = [hipcc()] + FLAGS + ["-D" + d for d in defines] + SRC + ["-o", tmp, "-L/opt/rocm/lib", "-lrccl",
-                                                                    "-Wl,-rpath,/opt/rocm/lib"]
+    cmd = [hipcc()] + FLAGS + ["-D" + d for d in defines] + [f"-DMDR_SRC_HASH=\"{src_hash()}\""] + SRC + [
+        "-o", tmp, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

@@ -307,6 +307,11 @@ static void drop_begun(mdr_ctx* c) {
   if (c) c->gq_keys_ready = false;  // (every such entry point may change the state)
 }
 
+#ifndef MDR_SRC_HASH
+#define MDR_SRC_HASH "unstamped0000000"
+#endif
+const char* mdr_build_id(void) { return "MDR_SRC_HASH:" MDR_SRC_HASH; }
+
 int mdr_abi_version(void) { return MDR_ABI_VERSION; }
 
 int mdr_abi_sizes(int64_t* out, int n) {

@@ -132,6 +132,7 @@ SIGNATURES = {
     "mdr_greedy_fallbacks": (I, [VP, VP]),
     "mdr_greedy_diag": (I, [VP, VP]),
     "mdr_greedy_state": (I, [VP, VP]),
+    "mdr_build_id": (C.c_char_p, []),
     "mdr_greedy_inputs": (I, [VP, VP, VP, VP, VP]),
     "mdr_greedy_select": (I, [VP, I64, VP, VP, VP, D, VP, VP]),
     "mdr_gq_shard_begin": (I, [VP, VP]),
@@ -166,6 +167,29 @@ _lock = threading.Lock()
 _lib = None
 
 
+def build_id(lib=None) -> str | None:
+    """The source hash the loaded library was built from (mdr_build_id)."""
+    lib = lib if lib is not None else _lib
+    s = lib.mdr_build_id().decode()
+    return s.split(":", 1)[1] if s.startswith("MDR_SRC_HASH:") else None
+
+
+def source_hash() -> str | None:
+    """build_ext.src_hash() of the sources in this tree (None when they are not next to the
+    package, e.g. an installed copy)."""
+    import importlib.util
+
+    be = os.path.join(os.path.dirname(HERE), "build_ext.py")
+    if not os.path.exists(be):
+        return None
+    spec = importlib.util.spec_from_file_location("_mdr_build_ext", be)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    if not all(os.path.exists(p) for p in m.SRC + m.HDR):
+        return None
+    return m.src_hash()
+
+
 def load(path: str = LIB_PATH):
     """Load libmdr_hip.so (after torch, so one HIP runtime serves both) and bind SIGNATURES."""
     global _lib
@@ -188,6 +212,11 @@ def load(path: str = LIB_PATH):
             fn.argtypes = args
         if lib.mdr_abi_version() != ABI_VERSION:
             raise MdrLibraryError("libmdr_hip.so ABI version mismatch; rebuild it")
+        want_id = source_hash()
+        have_id = build_id(lib)
+        if want_id is not None and have_id != want_id:
+            raise MdrLibraryError(f"{path} was built from other sources (library {have_id}, tree {want_id}): "
+                                  "rebuild it with __graft_entry__.build()")
         sizes = (C.c_int64 * len(ABI_STRUCTS))()
         lib.mdr_abi_sizes(sizes, len(ABI_STRUCTS))
         want = [C.sizeof(t) for t in ABI_STRUCTS]
