@@ -91,9 +91,9 @@ def parse():
                     help="seconds of non-environment device work before the timed region (GPU clock ramp; "
                          "off by default: measured to slow the host side of a short timed region ~3x, "
                          "profiles/r02c_bench20_trace.log)")
-    ap.add_argument("--host-spin-ms", type=float, default=3.0,
-                    help="milliseconds of an idle host busy-loop right before the clock starts (no environment "
-                         "or device work: keeps the core out of a low-power state after the GPU sync)")
+    ap.add_argument("--host-spin-ms", type=float, default=0.0,
+                    help="milliseconds of an idle host busy-loop right before the clock starts (diagnostics; measured "
+                         "to slow a short timed call, so off by default)")
     ap.add_argument("--gc-off", action="store_true", help="diagnostics: disable Python's cyclic GC in the timed region")
     ap.add_argument("--min-warmup-calls", type=int, default=3,
                     help="warmup runs at least W steps AND at least this many rollout calls of the timed chunk "
@@ -110,7 +110,7 @@ def parse():
                     help="step: env.step with fused random actions (the BASELINE metric); actor: "
                          "config C5, MA-PPO actor select_actions fused with the obs, then env.step; "
                          "greedy: config C3, device greedy-myopic controller then env.step")
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "bf16"],
+    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32", "bf16"],
                     help="actor MFMA precision (--workload actor)")
     ap.add_argument("--comm", default="default", choices=["default", "none", "rccl", "torch"],
                     help="exchange for the sharded path (default: rccl when WORLD_SIZE > 1); "

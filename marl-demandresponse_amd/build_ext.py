@@ -37,7 +37,7 @@ def src_hash() -> str:
     """sha256 (16 hex digits) of the library's sources, headers and build flags: stamped into the
     library at build time (mdr_build_id) and checked by mdr_amd._lib.load, so a library that was
     not built from the sources next to it is refused."""
-    h = hashlib.sha256(" ".join(FLAGS).encode())
+    h = hashlib.sha256(" ".join(f for f in FLAGS if not f.startswith("-I")).encode())  # (no paths: the tree moves)
     for p in SRC + HDR:
         h.update(os.path.basename(p).encode() + b"\0")
         with open(p, "rb") as f:

@@ -11,6 +11,9 @@
  * module calls them; IEEE double adds), so the mdr_tick rows are bit-identical to the Python loop
  * (tests/test_driver_window.py).  Compiled with -ffp-contract=off.
  *
+ * rollout1(begin, rollout, ctx, stream, reward, rew_stride, p_dev, mode, <the driver arguments>):
+ *   the same loop between mdr_rollout_begin and mdr_rollout (below).
+ *
  * drivers(rng, random, sigma, n, s, dts, od_tab, sig_tab, solar_tab, month, day, window_area,
  *         shading_coeff, terms, tod, sig, sol, tick0, out) -> (k, s, tod, sig, sol)
  *   rng       the generator instance (its gauss_next attribute is read and written)
@@ -62,35 +65,47 @@ static double solar_minute(long month, long day, long hour, long minute, double 
   return wa * shc * load;
 }
 
-static PyObject* drivers(PyObject* self, PyObject* args) {
+/* The driver loop of drivers() / rollout1(): parses the 19 driver arguments from `args` starting at
+ * index `first`, fills `out`, and on success stores (k, s, tod, sig, sol) in *res. */
+typedef struct {
+  Py_ssize_t k, n;
+  long long s;
+  double tod, sig, sol;
+  unsigned long long tick0;
+  double* out;
+} drv_res;
+
+static int drivers_run(PyObject* args, Py_ssize_t first, drv_res* res) {
   PyObject *rng, *rnd, *od_o, *sig_o, *sol_o, *terms_o, *out_o;
   double sigma, tod, sig, sol, wa, shc;
   Py_ssize_t n;
   long long s, dts;
   long month, day;
   unsigned long long tick0;
-  (void)self;
-  if (!PyArg_ParseTuple(args, "OOdnLLOOOllddOdddKO", &rng, &rnd, &sigma, &n, &s, &dts, &od_o, &sig_o, &sol_o, &month,
-                        &day, &wa, &shc, &terms_o, &tod, &sig, &sol, &tick0, &out_o))
-    return NULL;
+  PyObject* sub = PyTuple_GetSlice(args, first, PyTuple_GET_SIZE(args));
+  if (!sub) return -1;
+  const int ok = PyArg_ParseTuple(sub, "OOdnLLOOOllddOdddKO", &rng, &rnd, &sigma, &n, &s, &dts, &od_o, &sig_o, &sol_o,
+                                  &month, &day, &wa, &shc, &terms_o, &tod, &sig, &sol, &tick0, &out_o);
+  Py_DECREF(sub);  /* (the parsed objects stay alive: `args` holds them) */
+  if (!ok) return -1;
   if (n < 0 || dts <= 0 || dts >= 86400 || s < -dts || s >= 86400) {
     PyErr_SetString(PyExc_ValueError, "drivers: bad tick count, time step or second of day");
-    return NULL;
+    return -1;
   }
   Py_buffer terms_b, od_b, sig_b, sol_b, out_b;
   const int solar_on = sol_o != Py_None;
-  if (get_buf(terms_o, &terms_b, 3, 0, "terms") < 0) return NULL;
-  if (get_buf(od_o, &od_b, 1440, 0, "od_tab") < 0) { PyBuffer_Release(&terms_b); return NULL; }
+  if (get_buf(terms_o, &terms_b, 3, 0, "terms") < 0) return -1;
+  if (get_buf(od_o, &od_b, 1440, 0, "od_tab") < 0) { PyBuffer_Release(&terms_b); return -1; }
   if (get_buf(sig_o, &sig_b, 86400, 0, "sig_tab") < 0) {
-    PyBuffer_Release(&terms_b); PyBuffer_Release(&od_b); return NULL;
+    PyBuffer_Release(&terms_b); PyBuffer_Release(&od_b); return -1;
   }
   if (solar_on && get_buf(sol_o, &sol_b, 1440, 1, "solar_tab") < 0) {
-    PyBuffer_Release(&terms_b); PyBuffer_Release(&od_b); PyBuffer_Release(&sig_b); return NULL;
+    PyBuffer_Release(&terms_b); PyBuffer_Release(&od_b); PyBuffer_Release(&sig_b); return -1;
   }
   if (get_buf(out_o, &out_b, 4 * n, 1, "out") < 0) {
     PyBuffer_Release(&terms_b); PyBuffer_Release(&od_b); PyBuffer_Release(&sig_b);
     if (solar_on) PyBuffer_Release(&sol_b);
-    return NULL;
+    return -1;
   }
   const double* terms = (const double*)terms_b.buf;
   const Py_ssize_t nterms = terms_b.len / 24;
@@ -103,6 +118,7 @@ static PyObject* drivers(PyObject* self, PyObject* args) {
   /* the cached second normal deviate of random.gauss (None or a float) */
   double z = 0.0;
   int have_z = 0, err = 0;
+  Py_ssize_t k = 0;
   PyObject* gn = PyObject_GetAttrString(rng, "gauss_next");
   if (!gn) { err = 1; goto done; }
   if (gn != Py_None) {
@@ -112,7 +128,6 @@ static PyObject* drivers(PyObject* self, PyObject* args) {
   }
   Py_DECREF(gn);
 
-  Py_ssize_t k = 0;
   for (; k < n; ++k) {
     if (s + dts >= 86400) break;  /* the next tick is on the next day: the caller switches tables */
     s += dts;
@@ -165,12 +180,78 @@ done:
   PyBuffer_Release(&sig_b);
   if (solar_on) PyBuffer_Release(&sol_b);
   PyBuffer_Release(&out_b);
-  if (err) return NULL;
-  return Py_BuildValue("nLddd", k, s, tod, sig, sol);
+  if (err) return -1;
+  res->k = k;
+  res->n = n;
+  res->s = s;
+  res->tod = tod;
+  res->sig = sig;
+  res->sol = sol;
+  res->tick0 = tick0;
+  res->out = out;  /* (the caller's array, alive while `args` is) */
+  return 0;
+}
+
+static PyObject* drivers(PyObject* self, PyObject* args) {
+  (void)self;
+  drv_res r;
+  if (drivers_run(args, 0, &r) < 0) return NULL;
+  return Py_BuildValue("nLddd", r.k, r.s, r.tod, r.sig, r.sol);
+}
+
+/* rollout1(begin, rollout, ctx, stream, reward, rew_stride, p_dev, mode, <the 19 driver arguments>)
+ *   -> (rc_begin, rc_rollout, k, s, tod, sig, sol)
+ * One short direct rollout (Environment.rollout's default sequence) without Python between its
+ * steps: mdr_rollout_begin (the first window's count, before the drivers exist), the driver loop
+ * into `out`, and — when the window did not stop at midnight (k == n) — mdr_rollout with those
+ * ticks (no action buffer, no graph).  begin / rollout are the library's entry points (addresses
+ * from ctypes); rc_rollout = -1 when it was not called (begin failed, or k < n: the caller finishes
+ * the driver window for the next day and launches itself). */
+typedef int (*begin_fn)(void* ctx, int n, uint64_t tick0, const uint8_t* action, int64_t act_stride, int mode,
+                        void* stream);
+typedef int (*rollout_fn)(void* ctx, int n, const void* ticks, const uint8_t* action, int64_t act_stride, int mode,
+                          double* reward, int64_t rew_stride, double* p_out, int use_graph, void* stream);
+
+static PyObject* rollout1(PyObject* self, PyObject* args) {
+  (void)self;
+  if (PyTuple_GET_SIZE(args) != 8 + 19) {
+    PyErr_SetString(PyExc_TypeError, "rollout1: 8 launch arguments + 19 driver arguments");
+    return NULL;
+  }
+  unsigned long long a[8];
+  for (int i = 0; i < 8; ++i) {
+    a[i] = PyLong_AsUnsignedLongLongMask(PyTuple_GET_ITEM(args, i));
+    if (PyErr_Occurred()) return NULL;
+  }
+  const begin_fn begin = (begin_fn)(uintptr_t)a[0];
+  const rollout_fn roll = (rollout_fn)(uintptr_t)a[1];
+  void* ctx = (void*)(uintptr_t)a[2];
+  void* stream = (void*)(uintptr_t)a[3];
+  double* reward = (double*)(uintptr_t)a[4];
+  const int64_t rew_stride = (int64_t)a[5];
+  double* p_dev = (double*)(uintptr_t)a[6];
+  const int mode = (int)(int64_t)a[7];
+  PyObject* n_o = PyTuple_GET_ITEM(args, 8 + 3);
+  PyObject* t0_o = PyTuple_GET_ITEM(args, 8 + 17);
+  const Py_ssize_t n = PyLong_AsSsize_t(n_o);
+  const unsigned long long tick0 = PyLong_AsUnsignedLongLongMask(t0_o);
+  if (PyErr_Occurred()) return NULL;
+  if (!begin || !roll || !ctx || n < 1 || n > 0x7fffffff) {
+    PyErr_SetString(PyExc_ValueError, "rollout1: bad launch arguments");
+    return NULL;
+  }
+  const int rc_b = begin(ctx, (int)n, (uint64_t)tick0, NULL, 0, mode, stream);
+  if (rc_b != 0) return Py_BuildValue("iinLddd", rc_b, -1, (Py_ssize_t)0, 0LL, 0.0, 0.0, 0.0);
+  drv_res r;
+  if (drivers_run(args, 8, &r) < 0) return NULL;
+  int rc_r = -1;
+  if (r.k == r.n) rc_r = roll(ctx, (int)n, r.out, NULL, 0, mode, reward, rew_stride, p_dev, 0, stream);
+  return Py_BuildValue("iinLddd", rc_b, rc_r, r.k, r.s, r.tod, r.sig, r.sol);
 }
 
 static PyMethodDef methods[] = {
     {"drivers", drivers, METH_VARARGS, "per-tick rollout drivers (see mdr_host.c)"},
+    {"rollout1", rollout1, METH_VARARGS, "begin + drivers + mdr_rollout of one short rollout (see mdr_host.c)"},
     {NULL, NULL, 0, NULL},
 };
 

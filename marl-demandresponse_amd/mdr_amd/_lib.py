@@ -167,6 +167,17 @@ _lock = threading.Lock()
 _lib = None
 
 
+_fn_addrs = {}
+
+
+def fn_addr(name: str) -> int:
+    """Address of a library entry point (for the host-driver extension's fused rollout call)."""
+    a = _fn_addrs.get(name)
+    if a is None:
+        a = _fn_addrs[name] = C.cast(getattr(load(), name), C.c_void_p).value
+    return a
+
+
 def build_id(lib=None) -> str | None:
     """The source hash the loaded library was built from (mdr_build_id)."""
     lib = lib if lib is not None else _lib

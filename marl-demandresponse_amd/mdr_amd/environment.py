@@ -417,10 +417,13 @@ class Environment:
         st = self.init_props.time_step
         return self.power_grid.series_ok() and st.microseconds == 0 and st.days == 0 and 0 < st.seconds < 86400
 
-    def _driver_window_vec(self, n: int) -> "TickWindow":
+    def _driver_window_vec(self, n: int, launch=None):
         """driver_window for a constant base power and a flat / sinusoidal / regular-steps signal:
         the host-driver extension (csrc/mdr_host.c) when it is built, else the Python loop below
-        (the same values bit for bit: tests/test_driver_window.py)."""
+        (the same values bit for bit: tests/test_driver_window.py).  ``launch`` (Environment.rollout's
+        direct sequence): the first day's ticks go through ``_host.rollout1``, which issues
+        mdr_rollout_begin, computes them and — when the window ends that day — launches
+        mdr_rollout itself; returns (TickWindow, launched) then."""
         if _host is None or not _host_gauss_ok(self.rng):
             return self._driver_window_vec_py(n)
         p = self.init_props
@@ -439,9 +442,18 @@ class Environment:
             dd = d0 + _dt.timedelta(days=day_off) if day_off else d0
             sig_tab = grid.day_table(dd)  # (the tick's new datetime: its signal)
             sol_tab = drivers.solar_day_table(dd.month, dd.day, wa, shc) if solar_on else None
-            k, s, tod, sig, sol = _host.drivers(rng, rng.random, tp.temp_std, n - done, s, dts, od_tab, sig_tab,
-                                                sol_tab, dd.month, dd.day, wa, shc, drivers.SOLAR_TERMS_ARRAY,
-                                                tod, sig, sol, tick0 + done, buf[done:])
+            if launch is not None and done == 0:
+                rc_b, rc_r, k, s, tod, sig, sol = _host.rollout1(
+                    *launch, rng, rng.random, tp.temp_std, n, s, dts, od_tab, sig_tab, sol_tab, dd.month, dd.day,
+                    wa, shc, drivers.SOLAR_TERMS_ARRAY, tod, sig, sol, tick0, buf)
+                L.check(rc_b, "mdr_rollout_begin")
+                if rc_r > 0:
+                    L.check(rc_r, "mdr_rollout")
+                launched = rc_r == 0
+            else:
+                k, s, tod, sig, sol = _host.drivers(rng, rng.random, tp.temp_std, n - done, s, dts, od_tab, sig_tab,
+                                                    sol_tab, dd.month, dd.day, wa, shc, drivers.SOLAR_TERMS_ARRAY,
+                                                    tod, sig, sol, tick0 + done, buf[done:])
             done += k
             if done == n:
                 break
@@ -452,7 +464,7 @@ class Environment:
         self._tod_prev, self._s_prev = buf[n - 1, 0], buf[n - 1, 2]
         self.current_od_temp = np.float64(tod)
         grid.current_signal = np.float64(sig)
-        return TickWindow(buf)
+        return TickWindow(buf) if launch is None else (TickWindow(buf), launched)
 
     def _driver_window_vec_py(self, n: int) -> "TickWindow":
         """driver_window for a constant base power and a flat / sinusoidal / regular-steps signal:
@@ -587,6 +599,19 @@ class Environment:
             rewards = torch.empty((n_ticks, self._n_local), dtype=torch.float64, device=sh.device)
         rew_stride = 0 if rewards.dim() == 1 else self._n_local  # 1-D: every tick overwrites it
         drivers_whole = self.power_grid.interp is None and self._links is not None  # one driver window
+        if (drivers_whole and not use_graph and self._comm is None and actions is None and n_ticks >= 2
+                and self._vector_drivers_ok() and _host is not None and _host_gauss_ok(self.rng)
+                and not self._grid_pending):
+            # one C call: mdr_rollout_begin, the host drivers, mdr_rollout (no Python between them)
+            launch = (L.fn_addr("mdr_rollout_begin"), L.fn_addr("mdr_rollout"), sh.ctx.value, sh.stream(),
+                      rewards.data_ptr(), rew_stride, sh.p_dev.data_ptr(), mode)
+            ticks, launched = self._driver_window_vec(n_ticks, launch)
+            if not launched:  # (the window crossed midnight: the drivers were finished in Python)
+                sh.rollout(ticks, None, 0, mode, rewards, rew_stride, False)
+            self._P_dev_valid = True
+            self.finish_grid_step()
+            self._counts_ready = 0
+            return rewards
         if drivers_whole and not use_graph and (self._comm is None or getattr(self._comm, "native", False)):
             # the first window's count (sharded: + its allreduce) and P, before the drivers exist
             sh.rollout_begin(n_ticks, self._tick, actions, self._n_local if actions is not None else 0, mode)

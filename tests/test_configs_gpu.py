@@ -79,17 +79,18 @@ def _assert_state(got, ref, msg=""):
 
 
 def _recording(env):
-    """Wrap env.driver_window so every TickWindow a rollout computes is kept (its rows are the
-    drivers the kernels consumed)."""
+    """Wrap env._driver_window_vec (the vectorised drivers of driver_window and of rollout's one-C-call
+    sequence) so every TickWindow a rollout computes is kept (its rows are the drivers the kernels
+    consumed)."""
     rec = []
-    orig = env.driver_window
+    orig = env._driver_window_vec
 
-    def dw(k):
-        w = orig(k)
-        rec.append(w.a.copy())
-        return w
+    def dwv(n, launch=None):
+        out = orig(n) if launch is None else orig(n, launch)
+        rec.append((out[0] if isinstance(out, tuple) else out).a.copy())
+        return out
 
-    env.driver_window = dw
+    env._driver_window_vec = dwv
     return rec
 
 

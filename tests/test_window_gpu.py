@@ -291,3 +291,34 @@ def test_rollout_direct_kernarg_drivers(torch_gpu, mode, deadband):
         _same_state(torch, e1, e2)
         assert torch.equal(r1[:k], r2[:k]), k
         assert float(e1.shard.p_dev.item()) == float(e2.shard.p_dev.item())
+
+
+@pytest.mark.parametrize("start", [(23, 58, 30), (23, 58, 40), (0, 0, 0)])
+def test_rollout_fused_call_across_midnight(torch_gpu, start):
+    """Environment.rollout's one-C-call sequence (_mdr_host.rollout1: mdr_rollout_begin, the host
+    drivers, mdr_rollout) when the window crosses midnight: the first day's ticks come from that
+    call, which then leaves the launch to Python (the next day's tables); equal to a
+    graph-replayed twin that stages every driver first (rewards, state, P ==).  Starts 22 ticks
+    before midnight, exactly 20 ticks before it (the window ends on the last tick of the day), and
+    at midnight."""
+    import datetime as dt
+
+    torch = torch_gpu
+    from mdr_amd import _lib as L
+
+    n = 5000
+    e1, e2 = _pair(n)
+    for e in (e1, e2):
+        e.date_time = e.date_time.replace(hour=start[0], minute=start[1], second=start[2])
+    r1 = torch.empty((40, n), dtype=torch.float64, device="cuda")
+    r2 = torch.empty_like(r1)
+    for k in (40, 20, 33):
+        e1.rollout(k, action_mode="random", rewards=r1[:k])
+        ticks = e2.driver_window(k)
+        e2.shard.rollout(ticks, None, 0, L.ACT_RANDOM, r2[:k], n, True)
+        e2._P_dev_valid = True
+        e2.finish_grid_step()
+        _same_state(torch, e1, e2)
+        assert torch.equal(r1[:k], r2[:k]), k
+        assert e1.date_time == e2.date_time and e1._tick == e2._tick
+        assert float(e1.shard.p_dev.item()) == float(e2.shard.p_dev.item())
