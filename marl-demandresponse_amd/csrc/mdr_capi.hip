@@ -684,6 +684,11 @@ static unsigned win_grid(const mdr_ctx* c) { return blocks(blocks(c->kp.n, 64 * 
 // state's FSM words (w_in == nullptr) or from the end words of the previous window
 // p_only: the count kernel's last block also does the window's P-only reduce (win_reduce_last),
 // for a first window whose drivers ride on the step launch and whose shards need no allreduce
+// the reduced per-tick class counts of a window slot (after its kWindowMax x 64 x n_cap shards)
+static unsigned long long* win_red_ptr(const mdr_ctx* c, unsigned long long* slot) {
+  return slot + (size_t)kWindowMax * kCountShards * c->kp.n_cap;
+}
+
 static int launch_count(mdr_ctx* c, int mode, const uint8_t* action, int64_t act_stride, const TickArgs* tk,
                         uint64_t tick0, int K, unsigned long long* slot, uint64_t* onb, uint32_t* wah,
                         const uint32_t* w_in, hipStream_t st, bool p_only = false) {
@@ -792,17 +797,19 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
       // comm stream: count(w) + allreduce; count(w) reuses the buffers step(w - 2) read
       if (w >= 2) HIP_TRY(hipStreamWaitEvent(cs, c->ev_k1[(w - 2) % kSlabs], 0));
       const uint8_t* a = action ? action + (int64_t)t0 * act_stride : nullptr;
+      // (the count kernel's last block sums its shards: one allreduce of K x n_cap totals, <= 1 KiB)
       if (int rc = launch_count(c, mode, a, act_stride, tk + t0, 0, K, slot(w), onbs[w % 2], wahs[w % 2],
-                                w == 0 ? nullptr : wahs[(w - 1) % 2], cs))
+                                w == 0 ? nullptr : wahs[(w - 1) % 2], cs, true))
         return rc;
       if (comm)
-        RCCL_TRY(ncclAllReduce(slot(w), slot(w), (size_t)K * kCountShards * ncap, ncclUint64, ncclSum, comm, cs));
+        RCCL_TRY(ncclAllReduce(win_red_ptr(c, slot(w)), win_red_ptr(c, slot(w)), (size_t)K * ncap, ncclUint64,
+                               ncclSum, comm, cs));
       HIP_TRY(hipEventRecord(c->ev_ar[w % kSlabs], cs));
-      // compute stream: reduce + step (no lookahead)
+      // compute stream: the tick records + step (no lookahead)
       HIP_TRY(hipStreamWaitEvent(st, c->ev_ar[w % kSlabs], 0));
-      hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0,
+      hipLaunchKernelGGL(k_win_records, dim3(1), dim3(kWindowMax), 0, st, kp, slot(w), K, tk + t0,
                          w == nw - 1 ? p_out : nullptr);
-      LAUNCH_CHECK("k_win_reduce");
+      LAUNCH_CHECK("k_win_records");
       if (int rc = launch_step_window(c, mode, false, a, act_stride, tk + t0, K, 0, rec(w),
                                       reward + (int64_t)t0 * rew_stride, rew_stride, onbs[w % 2], wahs[w % 2],
                                       slot(w), WinDrv{}, st))
@@ -1017,14 +1024,14 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   // step kernel with the drivers as arguments (k_step_window<..., KA>), nothing in between — on one
   // GPU the count kernel's last block reduces; sharded, the reduce follows the counts' allreduce
   rc = launch_count(c, mode, action, act_stride, nullptr, tick0, k0, c->d_wslab, c->d_onb, c->d_wah, nullptr, st,
-                    !sharded);
+                    true);
   if (rc) return rc;
-  if (sharded) {  // every rank's sharded per-tick class counts, summed (exact integers)
-    RCCL_TRY(ncclAllReduce(c->d_wslab, c->d_wslab, (size_t)k0 * kCountShards * c->kp.n_cap, ncclUint64, ncclSum,
-                           c->comm, st));
-    hipLaunchKernelGGL(k_win_reduce, dim3(k0), dim3(64 * c->kp.n_cap), 0, st, c->kp, c->d_wslab, k0,
+  if (sharded) {  // every rank's per-tick class totals (its count kernel's last block), summed
+    RCCL_TRY(ncclAllReduce(win_red_ptr(c, c->d_wslab), win_red_ptr(c, c->d_wslab), (size_t)k0 * c->kp.n_cap,
+                           ncclUint64, ncclSum, c->comm, st));
+    hipLaunchKernelGGL(k_win_records, dim3(1), dim3(kWindowMax), 0, st, c->kp, c->d_wslab, k0,
                        (const TickArgs*)nullptr, (double*)nullptr);
-    LAUNCH_CHECK("k_win_reduce (P only)");
+    LAUNCH_CHECK("k_win_records (P only)");
   }
   c->wslab_dirty = false;
   c->begun.sharded = sharded;

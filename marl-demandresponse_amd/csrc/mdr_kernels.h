@@ -118,6 +118,7 @@ __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stri
                               int la_K, const double* rec, double* reward, int64_t rew_stride, uint64_t* onb,
                               uint32_t* wah, unsigned long long* next_slot, WinDrv dv);
 __global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
+__global__ void k_win_records(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
 template <int ACT, int HPT>
 __global__ void k_count_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp,
                                uint64_t tick0, int nt, unsigned long long* slot, uint64_t* onb, uint32_t* wah,

@@ -812,6 +812,23 @@ __global__ void __launch_bounds__(256) k_win_reduce(KParams p, unsigned long lon
   win_reduce_body(p, slot, nt, tkp ? tkp + blockIdx.x : nullptr, p_out);
 }
 
+// Sharded windows: the tick records from the slot's reduced counts `red` once they hold the
+// cluster's totals (every rank's count kernel reduced its own shards in its last block, then one
+// sum-allreduce of the K x n_cap totals): thread j writes tick j's record (tkp: the full record;
+// null: P only, the drivers come later as kernel arguments).  One block of kWinMax threads.
+__global__ void __launch_bounds__(kWinMax) k_win_records(KParams p, unsigned long long* __restrict__ slot, int nt,
+                                                         const TickArgs* __restrict__ tkp, double* p_out) {
+  const int j = threadIdx.x, ncap = p.n_cap;
+  if (j >= nt) return;
+  double p_on[kWinCap];
+#pragma unroll
+  for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < ncap ? k : 0];
+  const unsigned long long* cnt = win_red(slot, ncap) + j * ncap;
+  double* rec = win_rec(slot, ncap) + j * kWinRec;
+  if (tkp) win_tick_record(p, cnt, tkp[j], p_on, rec, j == nt - 1 ? p_out : nullptr);
+  else rec[0] = win_power(p, cnt, p_on);
+}
+
 // LDS written by some lanes of a wave and read by others (the wave's LDS operations execute in
 // issue order: a wavefront-scope fence orders the compiler and waits lgkmcnt)
 __device__ __forceinline__ void wave_lds_sync() {
