@@ -361,29 +361,42 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     // (the wave in its MFMA stage gets VALU issue priority over the SIMD's other wave, which is then
     // building observations or running the output layer)
     __builtin_amdgcn_s_setprio(2);
-    // ---- layer 1: acc1[mb][cb] = b1 + W1 · X  (X^T columns = this wave's 32 houses, two column blocks)
+    // ---- layer 1: acc1[mb][cb] = b1 + W1 · X  (X^T columns = this wave's 32 houses, two column blocks).
+    // The (k-step, row block) fragments are step s = ks * MB + mb of the packed image; each step's
+    // weight fragments are read from LDS two steps ahead (a ring of three), so the MFMAs of one wave
+    // do not wait out the LDS latency.
+    constexpr int PF = 2;  // prefetch distance (steps)
     f32x4 acc1[MB][2];
+    {
+      const int total = d.ks1 * MB;
+      bf16x8 ring[PF + 1][NS];
 #pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      if (ks >= d.ks1) break;  // (uniform; unrolled so the prefetch loads stay in flight)
+      for (int q = 0; q < PF; ++q)
+        if (q < total)
+#pragma unroll
+          for (int e = 0; e < NS; ++e) ring[q][e] = lds_frag(s_w1, NF * q + e, lane);
       bf16x8 xs[2][NS];
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        float xv[8];
+      for (int st = 0; st < 4 * MB; ++st) {
+        if (st < total) {  // (uniform; a guard, not a break: every step keeps compile-time ring indices)
+        const int ks = st / MB, mb = st % MB;
+        if (mb == 0) {
 #pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const int a = xoff[ks][e] + cb * xstep[ks][e];
-          const float4 x = *reinterpret_cast<const float4*>(w_row + a);
-          xv[4 * e] = x.x; xv[4 * e + 1] = x.y; xv[4 * e + 2] = x.z; xv[4 * e + 3] = x.w;
+          for (int cb = 0; cb < 2; ++cb) {
+            float xv[8];
+#pragma unroll
+            for (int e = 0; e < 2; ++e) {
+              const int a = xoff[ks][e] + cb * xstep[ks][e];
+              const float4 x = *reinterpret_cast<const float4*>(w_row + a);
+              xv[4 * e] = x.x; xv[4 * e + 1] = x.y; xv[4 * e + 2] = x.z; xv[4 * e + 3] = x.w;
+            }
+            split_operand<PREC>(xv, xs[cb]);
+          }
         }
-        split_operand<PREC>(xv, xs[cb]);
-      }
+        if (st + PF < total)
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        bf16x8 as[NS];
-        const int f = ks * MB + mb;
-#pragma unroll
-        for (int e = 0; e < NS; ++e) as[e] = lds_frag(s_w1, NF * f + e, lane);
+          for (int e = 0; e < NS; ++e) ring[(st + PF) % (PF + 1)][e] = lds_frag(s_w1, NF * (st + PF) + e, lane);
+        const bf16x8* as = ring[st % (PF + 1)];
         if (ks == 0) {
           const f32x4 bias = *reinterpret_cast<const f32x4*>(b1 + kActorRB * mb + 4 * g);
 #pragma unroll
@@ -392,9 +405,11 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) acc1[mb][cb] = mfma_split<PREC>(as, xs[cb], acc1[mb][cb]);
         }
+        }
       }
     }
     PSTAMP(3);
+
     // ---- ReLU + split: layer 1's accumulators become layer 2's B fragments in place
     bf16x8 hs[KS2][2][NS];
 #pragma unroll
@@ -409,15 +424,22 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
         }
         split_operand<PREC>(v, hs[q][cb]);
       }
-    // ---- layer 2: acc2[mb][cb] = b2 + W2 · relu(H1)
+
+    // ---- layer 2: acc2[mb][cb] = b2 + W2 · relu(H1), steps st = q * MB + mb, fragments prefetched
+    {
+      constexpr int TOT = KS2 * MB;
+      bf16x8 ring[PF + 1][NS];
 #pragma unroll
-    for (int q = 0; q < KS2; ++q) {
+      for (int q = 0; q < PF; ++q)
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        bf16x8 as[NS];
-        const int f = q * MB + mb;
+        for (int e = 0; e < NS; ++e) ring[q][e] = lds_frag(s_w2, NF * q + e, lane);
 #pragma unroll
-        for (int e = 0; e < NS; ++e) as[e] = lds_frag(s_w2, NF * f + e, lane);
+      for (int st = 0; st < TOT; ++st) {
+        const int q = st / MB, mb = st % MB;
+        if (st + PF < TOT)
+#pragma unroll
+          for (int e = 0; e < NS; ++e) ring[(st + PF) % (PF + 1)][e] = lds_frag(s_w2, NF * (st + PF) + e, lane);
+        const bf16x8* as = ring[st % (PF + 1)];
         if (q == 0) {
           const f32x4 bias = *reinterpret_cast<const f32x4*>(b2 + kActorRB * mb + 4 * g);
 #pragma unroll
