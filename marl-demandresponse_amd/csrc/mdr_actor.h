@@ -24,7 +24,8 @@ constexpr int kActorKS2 = kActorMaxMB / 2;  // layer-2 k-steps of 32 (hidden row
 struct ActorDims {
   int n_in, h1, h2, n_act;
   int mb;         // row blocks of both hidden layers (ceil(max(h1, h2) / 16), 7 or 8)
-  int ks1;        // layer-1 k-steps of 32 (ceil(nslot / 32))
+  int ks1;        // layer-1 k-steps of 32: max(2, ceil(nslot / 32)) (the kernel's instantiations;
+                  // a padding k-step reads zero weights and the zero chunk)
   int nf;         // bf16 fragments per (row block, k-step): 2 = (hi, lo), 3 = (hi, mid, lo) for MDR_PREC_FP32
   int n_own, own4, msg_w, m4, n_comm, lo, ring, nslot, rs, nrows;
   int off_w1, off_w2, off_tail, off_end;  // packed image: W1 / W2 fragments, fp32 tail
@@ -45,7 +46,7 @@ struct ActorOut {
 
 __global__ void k_actor_pack(ActorDims d, const float* w1, const float* b1, const float* w2,
                              const float* b2, const float* w3, const float* b3, unsigned char* out);
-template <int PREC, bool PROF, int MB>
+template <int PREC, bool PROF, int MB, int KS1>
 __global__ void k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
                         const unsigned char* wpack, ActorOut out, uint64_t tick, const TickArgs* tkp);
 

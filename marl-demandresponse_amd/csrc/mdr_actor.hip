@@ -42,6 +42,7 @@ namespace mdr {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // --------------------------------------------------------------------------------------- slots
 // The feature behind layer-1 slot s (-1: a padding slot)
@@ -155,6 +156,13 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_wave_barrier();
 }
 
+// max(x, 0) as one v_max_i32 on the bits (fmaxf in IEEE mode adds a quieting v_max per operand):
+// every negative float is a negative integer, so it becomes +0; -0 becomes +0; a NaN passes
+// through (torch.relu(nan) = nan)
+__device__ __forceinline__ float relu(float x) {
+  return __int_as_float(max(__float_as_int(x), 0));
+}
+
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
@@ -189,15 +197,16 @@ __device__ __forceinline__ void split_operand(const float* v, bf16x8* s) {
 // Persistent: every wave of the block shares the LDS weight image but owns its own 32-house tiles
 // (source rows, FSM words in a private LDS slice).  A tile runs as three stages — build (its LDS
 // rows from sources prefetched into registers), X (layers 1 and 2 on the MFMA pipe; the next tile's
-// sources go in flight first) and Y (output layer, softmax, sampling, stores on the VALU) — and the
-// two waves of each SIMD run them in ping-pong (the schedule at the end of the kernel), so the
-// SIMD's matrix pipe and its VALU are busy at the same time.  MB: row blocks of the hidden layers
-// (compile-time LDS offsets).
-template <int PREC, bool PROF, int MB>
+// sources go in flight first) and Y (output layer, softmax, sampling, stores on the VALU); the
+// waves run them free, or (d.pp) the two waves of each SIMD in ping-pong (the schedule at the end
+// of the kernel).  MB: row blocks of the hidden layers (compile-time LDS offsets); KS1: layer-1
+// k-steps (d.ks1, 2 to 4; no per-step guards in the MFMA loop).
+template <int PREC, bool PROF, int MB, int KS1>
 __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
                                                const unsigned char* __restrict__ wpack, ActorOut out,
                                                uint64_t tick0, const TickArgs* tkp) {
   static_assert(MB >= 1 && MB <= kActorMaxMB, "row blocks");
+  static_assert(KS1 >= 1 && KS1 <= kActorMaxSlots / 32, "layer-1 k-steps");
   constexpr int NS = PREC == 6 ? 3 : PREC == 3 ? 2 : 1;  // operand splits
   constexpr int NF = PREC == 6 ? 3 : 2;                   // packed fragments per (row block, k-step)
   constexpr int KS2 = (MB + 1) / 2;
@@ -261,9 +270,9 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
 
   // this lane's B-fragment chunk addresses (floats into w_row) for column block 0: layer-1 k-step
   // ks reads slots 32 ks + 8 g .. + 7 = two chunks; padding chunks read the wave's zero chunk
-  int xoff[4][2], xstep[4][2];  // column block cb reads xoff + cb * xstep
+  int xoff[KS1][2], xstep[KS1][2];  // column block cb reads xoff + cb * xstep
 #pragma unroll
-  for (int ks = 0; ks < 4; ++ks)
+  for (int ks = 0; ks < KS1; ++ks)
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int off = actor_slot_off(d, 32 * ks + 8 * g + 4 * e);
@@ -368,17 +377,15 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     constexpr int PF = 2;  // prefetch distance (steps)
     f32x4 acc1[MB][2];
     {
-      const int total = d.ks1 * MB;
+      constexpr int total = KS1 * MB;
       bf16x8 ring[PF + 1][NS];
 #pragma unroll
       for (int q = 0; q < PF; ++q)
-        if (q < total)
 #pragma unroll
-          for (int e = 0; e < NS; ++e) ring[q][e] = lds_frag(s_w1, NF * q + e, lane);
+        for (int e = 0; e < NS; ++e) ring[q][e] = lds_frag(s_w1, NF * q + e, lane);
       bf16x8 xs[2][NS];
 #pragma unroll
-      for (int st = 0; st < 4 * MB; ++st) {
-        if (st < total) {  // (uniform; a guard, not a break: every step keeps compile-time ring indices)
+      for (int st = 0; st < total; ++st) {
         const int ks = st / MB, mb = st % MB;
         if (mb == 0) {
 #pragma unroll
@@ -405,7 +412,6 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) acc1[mb][cb] = mfma_split<PREC>(as, xs[cb], acc1[mb][cb]);
         }
-        }
       }
     }
     PSTAMP(3);
@@ -419,8 +425,8 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
         float v[8];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          v[j] = fmaxf(acc1[2 * q][cb][j], 0.f);
-          v[4 + j] = 2 * q + 1 < MB ? fmaxf(acc1[2 * q + 1][cb][j], 0.f) : 0.f;
+          v[j] = relu(acc1[2 * q][cb][j]);
+          v[4 + j] = 2 * q + 1 < MB ? relu(acc1[2 * q + 1][cb][j]) : 0.f;
         }
         split_operand<PREC>(v, hs[q][cb]);
       }
@@ -454,27 +460,32 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     PSTAMP(4);
   };
   // Y: output layer (fp32 VALU) + softmax + sampling + stores (+ the ON counts of the new actions)
-  auto stage_y = [&](uint32_t tl) {
+  float u_next = 0.f;  // the sampling uniforms of this wave's next tile (stage_y, odd tiles)
+  auto stage_y = [&](uint32_t tl, bool fresh) {
     const uint32_t b0 = tl * 32u;
     const int nb = (int)min(32u, n - b0);
-    float z[2][kActorNA] = {{0.f, 0.f}, {0.f, 0.f}};
+    float z[2][kActorNA];
     {
+      // both actions' sums as one packed pair (v_pk_fma_f32): (z0, z1) += (w0, w1) * (x, x), the
+      // same fused multiply-adds in the same order as two scalar chains
 #pragma clang fp contract(fast)
+      f32x2 zz[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
 #pragma unroll
       for (int mb = 0; mb < MB; ++mb) {
-        const float* wr = w3 + (kActorRB * mb + 4 * g) * kActorNA;  // rows 4g .. 4g + 3, both actions
-        const float4 wa = *reinterpret_cast<const float4*>(wr);
-        const float4 wb = *reinterpret_cast<const float4*>(wr + 4);
-        const float w0[4] = {wa.x, wa.z, wb.x, wb.z}, w1v[4] = {wa.y, wa.w, wb.y, wb.w};
+        const f32x2* wr = reinterpret_cast<const f32x2*>(w3 + (kActorRB * mb + 4 * g) * kActorNA);  // rows 4g .. 4g + 3
+        f32x2 w[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = wr[i];
 #pragma unroll
         for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
           for (int i = 0; i < 4; ++i) {
-            const float x = fmaxf(acc2[mb][cb][i], 0.f);
-            z[cb][0] += w0[i] * x;
-            z[cb][1] += w1v[i] * x;
+            const float x = relu(acc2[mb][cb][i]);
+            zz[cb] = __builtin_elementwise_fma(w[i], f32x2{x, x}, zz[cb]);
           }
       }
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) { z[cb][0] = zz[cb].x; z[cb][1] = zz[cb].y; }
     }
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
@@ -488,15 +499,25 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     const bool upper = (lane & 16) != 0;
     const float z0 = (upper ? z[1][0] : z[0][0]) + b3[0];
     const float z1 = (upper ? z[1][1] : z[0][1]) + b3[1];
-    // softmax over the 2 actions (fp32, max-subtracted like torch) + Categorical sample
+    // softmax over the 2 actions (fp32, max-subtracted like torch; one reciprocal of the sum, as
+    // ATen's vectorised softmax) + Categorical sample
     const float zmax = fmaxf(z0, z1);
-    const float e0 = expf(z0 - zmax), e1 = expf(z1 - zmax);
-    const float se = e0 + e1;
-    const float p0 = e0 / se, p1 = e1 / se;
+    const float e0 = __expf(z0 - zmax), e1 = __expf(z1 - zmax);
+    const float rse = 1.f / (e0 + e1);
+    const float p0 = e0 * rse, p1 = e1 * rse;
     const bool valid = r < nb;
     const uint32_t i = b0 + (uint32_t)r;
-    // Categorical(probs).sample(): action 0 iff u < p0
-    const float u = philox_u01f(p.seed, (uint64_t)p.goff + i, tick);
+    // Categorical(probs).sample(): action 0 iff u < p0.  The uniform of house i is
+    // philox(seed, goff + i, tick); every other tile, lanes 32..63 draw the next tile's (the same
+    // counters: one Philox pass per two tiles), kept in u_next
+    float u;
+    if (fresh) {
+      const uint32_t ih = (lane < 32 ? b0 : b0 + stride * 32u) + (uint32_t)r;
+      u = philox_u01f(p.seed, (uint64_t)p.goff + ih, tick);
+      u_next = __shfl(u, r + 32);
+    } else {
+      u = u_next;
+    }
     const int act = u < p0 ? 0 : 1;
     const float pa = act ? p1 : p0;
     const bool writer = valid && lane < 32;
@@ -544,7 +565,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
           if (PROF && lane == 0) pacc[7] += 1;
           stage_x(tj, tj + stride);
         } else {
-          stage_y(tj);
+          stage_y(tj, (j & 1) == 0);
           if (j + 1 < n_my) stage_build(tj + stride);
         }
       }
@@ -565,17 +586,21 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
 #undef PSTAMP
 }
 
-#define MDR_INST_ACTOR(P, F, MB)                                                                   \
-  template __global__ void k_actor<P, F, MB>(KParams, ObsArgs, ActorDims, const double*, const unsigned char*, \
-                                             ActorOut, uint64_t, const TickArgs*);
-#define MDR_INST_ACTOR_MB(MB) \
-  MDR_INST_ACTOR(1, false, MB) \
-  MDR_INST_ACTOR(3, false, MB) \
-  MDR_INST_ACTOR(6, false, MB) \
-  MDR_INST_ACTOR(1, true, MB)  \
-  MDR_INST_ACTOR(3, true, MB)  \
-  MDR_INST_ACTOR(6, true, MB)
-MDR_INST_ACTOR_MB(7)
-MDR_INST_ACTOR_MB(8)
+#define MDR_INST_ACTOR(P, F, MB, KS)                                                                \
+  template __global__ void k_actor<P, F, MB, KS>(KParams, ObsArgs, ActorDims, const double*,              \
+                                                 const unsigned char*, ActorOut, uint64_t, const TickArgs*);
+#define MDR_INST_ACTOR_SHAPE(MB, KS) \
+  MDR_INST_ACTOR(1, false, MB, KS) \
+  MDR_INST_ACTOR(3, false, MB, KS) \
+  MDR_INST_ACTOR(6, false, MB, KS) \
+  MDR_INST_ACTOR(1, true, MB, KS)  \
+  MDR_INST_ACTOR(3, true, MB, KS)  \
+  MDR_INST_ACTOR(6, true, MB, KS)
+MDR_INST_ACTOR_SHAPE(7, 2)
+MDR_INST_ACTOR_SHAPE(7, 3)
+MDR_INST_ACTOR_SHAPE(7, 4)
+MDR_INST_ACTOR_SHAPE(8, 2)
+MDR_INST_ACTOR_SHAPE(8, 3)
+MDR_INST_ACTOR_SHAPE(8, 4)
 
 }  // namespace mdr

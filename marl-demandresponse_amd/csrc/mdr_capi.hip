@@ -1687,7 +1687,7 @@ ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw) 
   d.ring = sp->comm_mode == MDR_COMM_RING && K > 0;
   d.lo = d.ring ? K / 2 : 0;
   d.nslot = d.own4 + K * d.m4;
-  d.ks1 = (d.nslot + 31) / 32;
+  d.ks1 = std::max(2, (d.nslot + 31) / 32);  // (the kernel's instantiations: 2, 3, 4; a padding k-step is zero)
   int rs = d.ring ? d.m4 + d.own4 : d.nslot;
   if (((rs / 4) & 1) == 0) rs += 4;  // odd multiple of 16 B: conflict-free ds_read_b128 of 16 rows
   d.rs = rs;
@@ -1752,9 +1752,10 @@ int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
   return MDR_OK;
 }
 
-#define MDR_ACTOR_KERNELS(MB)                                                                        \
-  (const void*)k_actor<1, false, MB>, (const void*)k_actor<3, false, MB>, (const void*)k_actor<6, false, MB>, \
-      (const void*)k_actor<1, true, MB>, (const void*)k_actor<3, true, MB>, (const void*)k_actor<6, true, MB>
+#define MDR_ACTOR_KERNELS(MB, KS)                                                                      \
+  (const void*)k_actor<1, false, MB, KS>, (const void*)k_actor<3, false, MB, KS>,                         \
+      (const void*)k_actor<6, false, MB, KS>, (const void*)k_actor<1, true, MB, KS>,                      \
+      (const void*)k_actor<3, true, MB, KS>, (const void*)k_actor<6, true, MB, KS>
 
 int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const double* p_dev, uint64_t tick,
                  const TickArgs* tkp, const ActorOut& out, hipStream_t st) {
@@ -1766,18 +1767,22 @@ int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const dou
   const unsigned grid = (unsigned)std::min<int64_t>(ntile, (int64_t)c->n_cu);
   static bool lds_attr = false;  // > 64 KiB of dynamic LDS must be opted into per kernel
   if (!lds_attr) {
-    for (const void* k : {MDR_ACTOR_KERNELS(7), MDR_ACTOR_KERNELS(8)})
+    for (const void* k : {MDR_ACTOR_KERNELS(7, 2), MDR_ACTOR_KERNELS(7, 3), MDR_ACTOR_KERNELS(7, 4),
+                          MDR_ACTOR_KERNELS(8, 2), MDR_ACTOR_KERNELS(8, 3), MDR_ACTOR_KERNELS(8, 4)})
       HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     lds_attr = true;
   }
-#define MDR_LAUNCH_ACTOR(P, F)                                                                              \
-  do {                                                                                                      \
-    if (d.mb == 7)                                                                                          \
-      hipLaunchKernelGGL((k_actor<P, F, 7>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
-                         c->d_actor, out, tick, tkp);                                                       \
-    else                                                                                                    \
-      hipLaunchKernelGGL((k_actor<P, F, 8>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
-                         c->d_actor, out, tick, tkp);                                                       \
+#define MDR_LAUNCH_ACTOR_S(P, F, MB, KS)                                                                     \
+  hipLaunchKernelGGL((k_actor<P, F, MB, KS>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
+                     c->d_actor, out, tick, tkp)
+#define MDR_LAUNCH_ACTOR(P, F)                                 \
+  do {                                                         \
+    if (d.mb == 7 && d.ks1 == 2) MDR_LAUNCH_ACTOR_S(P, F, 7, 2); \
+    else if (d.mb == 7 && d.ks1 == 3) MDR_LAUNCH_ACTOR_S(P, F, 7, 3); \
+    else if (d.mb == 7) MDR_LAUNCH_ACTOR_S(P, F, 7, 4);          \
+    else if (d.ks1 == 2) MDR_LAUNCH_ACTOR_S(P, F, 8, 2);         \
+    else if (d.ks1 == 3) MDR_LAUNCH_ACTOR_S(P, F, 8, 3);         \
+    else MDR_LAUNCH_ACTOR_S(P, F, 8, 4);                         \
   } while (0)
   const int prec = c->actor.precision;
   if (out.prof) {
@@ -1790,6 +1795,7 @@ int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const dou
     else MDR_LAUNCH_ACTOR(3, false);
   }
 #undef MDR_LAUNCH_ACTOR
+#undef MDR_LAUNCH_ACTOR_S
   LAUNCH_CHECK("k_actor");
   return MDR_OK;
 }
