@@ -1254,15 +1254,16 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
     // synchronisation; k_gq_select decides exactly what the candidate window cannot
     if (!keys_ready)
       if (int rc2 = launch_gq_keys(c, st)) return rc2;
-    hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, c->g_part,
-                       c->gq_nparts, budget, c->g_sel, slab, c->g_map);
+    hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
+                       c->g_sel, slab);
     LAUNCH_CHECK("k_gq_bins");
     const int nstage = (n + kGqStage - 1) / kGqStage;
     hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
                        c->g_sel, c->g_win, action, slab);
     LAUNCH_CHECK("k_gq_compact");
     hipLaunchKernelGGL(k_gq_select, dim3(kGqSelBlocks), dim3(1024), 0, st, c->kp, c->g_win, c->g_sorted, budget, pmin,
-                       c->g_sel, action, slab, c->g_hist, (const uint4*)nullptr, 0, c->g_tickets);
+                       c->g_sel, action, slab, c->g_hist, (const uint4*)nullptr, 0, c->g_tickets,
+                       (const double*)c->g_part, c->gq_nparts, c->g_map);
     LAUNCH_CHECK("k_gq_select");
     c->counts_ready = true;
     return MDR_OK;
@@ -1358,7 +1359,7 @@ int mdr_gq_shard_buffers(mdr_ctx* c, void** super_hist, int64_t* n_super, void**
 int mdr_gq_shard_bins(mdr_ctx* c, double budget, void* stream) {
   if (!c || !c->g_sel) return fail(MDR_ESTATE, "mdr_gq_shard_bins: call mdr_gq_shard_begin first");
   hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, S(stream), c->kp, gq_codes(c), c->g_hist,
-                     (const double*)c->g_range, -1, budget, c->g_sel, (unsigned long long*)nullptr, c->g_map);
+                     budget, c->g_sel, (unsigned long long*)nullptr);
   LAUNCH_CHECK("k_gq_bins (sharded)");
   return MDR_OK;
 }
@@ -1384,7 +1385,8 @@ int mdr_gq_shard_select(mdr_ctx* c, double budget, const void* gathered, int wor
   if (!c->g_sel) return fail(MDR_ESTATE, "mdr_gq_shard_select: call mdr_gq_shard_begin first");
   hipLaunchKernelGGL(k_gq_select, dim3(kGqSelBlocks), dim3(1024), 0, S(stream), c->kp, (const uint4*)nullptr,
                      c->g_sorted, budget, greedy_pmin(c), c->g_sel, action, (unsigned long long*)nullptr, c->g_hist,
-                     static_cast<const uint4*>(gathered), world, c->g_tickets);
+                     static_cast<const uint4*>(gathered), world, c->g_tickets, (const double*)c->g_range, -1,
+                     c->g_map);
   LAUNCH_CHECK("k_gq_select (sharded)");
   return MDR_OK;
 }

@@ -167,13 +167,13 @@ size_t gq_wcount_offset();   // host: byte offsets of GqSel.wcount / .need_fb (s
 size_t gq_need_fb_offset();  // host: [fallbacks, calls, sum of window sizes, last window]
 __global__ void k_gq_keys(KParams p, uint32_t* code, double* part, unsigned* hist, const GqSel* sel,
                           const uint32_t* map);
-__global__ void k_gq_bins(KParams p, const uint32_t* code, unsigned* hist, const double* part, int nparts, double S,
-                          GqSel* sel, unsigned long long* slab, uint32_t* map);
+__global__ void k_gq_bins(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel,
+                          unsigned long long* slab);
 __global__ void k_gq_compact(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel, uint4* win,
                              uint8_t* action, unsigned long long* slab);
 __global__ void k_gq_select(KParams p, const uint4* win, uint4* sorted, double S, double pmin, GqSel* sel,
                             uint8_t* action, unsigned long long* slab, unsigned* hist, const uint4* gathered,
-                            int world, unsigned* tickets);
+                            int world, unsigned* tickets, const double* part, int nparts, uint32_t* map);
 __global__ void k_gq_range(const double* part, int nparts, double* range);
 __global__ void k_greedy_inputs(KParams p, double* key, double* power, uint8_t* lock);
 __global__ void k_greedy_iota(int64_t n, int* idx);

@@ -1860,14 +1860,14 @@ __device__ __forceinline__ void gq_block_scan(double& x, unsigned long long& xc,
 }
 
 // K2: every block first finds the crossing superbin itself (the cumulative P where it reaches S;
-// the same arithmetic in every block, so every block agrees), block 0 records it and the next
-// call's key map (gq_bin) and zeroes the current count slab (compact and select fill it) and the
-// window allocator; then the class counts of the bins of superbins sb and sb + 1 (the crossing superbin
-// and the room after it).  The block's codes are loaded first: they stay in flight through the scan.
+// the same arithmetic in every block, so every block agrees), block 0 records it and zeroes the
+// current count slab (compact and select fill it) and the window allocator; then the class counts
+// of the bins of superbins sb and sb + 1 (the crossing superbin and the room after it).  The
+// block's codes are loaded first: they stay in flight through the scan.  (The next call's key map
+// is k_gq_select's: gq_next_map.)
 __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_t* __restrict__ code,
-                                                        unsigned* __restrict__ hist, const double* __restrict__ part,
-                                                        int nparts, double S, GqSel* __restrict__ sel,
-                                                        unsigned long long* __restrict__ slab, uint32_t* __restrict__ map) {
+                                                        unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
+                                                        unsigned long long* __restrict__ slab) {
   constexpr int NB = 2 * (kGqBins / kGqSuper), NW = kGqThreads / 64;
   static_assert(kGqSupN <= kGqThreads && kGqCells < kGqThreads, "one superbin / cell edge per thread");
   __shared__ unsigned s_h[NW][NB * 4];
@@ -1918,62 +1918,6 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_
       sel->wcount = 0u;
       sel->need_fb = 0u;
     }
-    // the next call's map: cells over this call's finite key range [min, max], each cell's bins in
-    // proportion to this call's houses there — the superbin CDF (linear inside a superbin) at the
-    // cell edges, read through this call's map
-    __shared__ double s_lo[NW], s_hi[NW], s_rng[2];
-    __shared__ double s_pre[kGqSuper], s_cnt[kGqSuper], s_C[kGqCells + 1];
-    __shared__ uint32_t s_map[kGqCells];
-    if (tid < kGqSuper) { s_pre[tid] = (double)(xc - cs); s_cnt[tid] = (double)cs; }
-    if (tid < kGqCells) s_map[tid] = map[tid];
-    double lo = INFINITY, hi = -INFINITY;
-    if (nparts < 0) {  // sharded: the cluster's range, allreduced as (min, -max) (k_gq_range)
-      if (tid == 0) { lo = part[0]; hi = -part[1]; }
-    } else {
-      for (int b = tid; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) {
-      lo = fmin(lo, __shfl_xor(lo, off));
-      hi = fmax(hi, __shfl_xor(hi, off));
-    }
-    if ((tid & 63) == 0) { s_lo[tid >> 6] = lo; s_hi[tid >> 6] = hi; }
-    __syncthreads();
-    if (tid == 0) {
-      double kmin = s_lo[0], kmax = s_hi[0];
-      for (int w = 1; w < NW; ++w) { kmin = fmin(kmin, s_lo[w]); kmax = fmax(kmax, s_hi[w]); }
-      const double range = kmax - kmin;
-      s_rng[0] = kmin == kmin && kmin < INFINITY ? kmin : 0.0;
-      s_rng[1] = range > 0.0 && range < INFINITY ? (double)kGqCells / range : 0.0;
-    }
-    __syncthreads();
-    const double okmin = sel->kmin, oscale = sel->scale, nkmin = s_rng[0], nscale = s_rng[1];
-    if (tid <= kGqCells) {
-      double C = 0.0;
-      if (nscale > 0.0) {
-        const double u = (nkmin + (double)tid / nscale - okmin) * oscale;  // the edge, in this call's cells
-        const int c = u >= (double)(kGqCells - 1) ? kGqCells - 1 : (u > 0.0 ? (int)u : 0);
-        const uint32_t m = s_map[c];
-        const double f = fmin(fmax(u - (double)c, 0.0), 1.0);
-        const double sp = ((double)(m >> 16) + f * (double)(m & 0xFFFFu)) / (double)(kGqBins / kGqSuper);
-        const int sc = sp >= (double)(kGqSuper - 1) ? kGqSuper - 1 : (sp > 0.0 ? (int)sp : 0);
-        C = s_pre[sc] + fmin(fmax(sp - (double)sc, 0.0), 1.0) * s_cnt[sc];
-      }
-      s_C[tid] = C;
-    }
-    __syncthreads();
-    if (tid < kGqCells) {  // B0_g = g + floor(K (C_g - C_0) / (C_G - C_0)): non-decreasing in g, so W_g >= 1
-      const int NBE = gq_bins_eff(p.n_global), K = NBE - kGqCells;
-      const double T = s_C[kGqCells] - s_C[0];
-      auto edge = [&](int g) {
-        if (g >= kGqCells) return NBE;
-        if (!(T > 0.0)) return g * (NBE / kGqCells);  // (no spread seen: uniform cells)
-        return g + min(K, (int)((double)K * ((s_C[g] - s_C[0]) / T)));
-      };
-      const int b0 = edge(tid), b1 = edge(tid + 1);
-      map[tid] = ((uint32_t)b0 << 16) | (uint32_t)(b1 - b0);
-    }
-    if (tid == 0) { sel->kmin = nkmin; sel->scale = nscale; }  // (no later kernel of this call maps keys)
     if (slab)
       for (int e = tid; e < kCountShards * p.n_cap; e += blockDim.x) slab[e] = 0ull;
   }
@@ -2004,6 +1948,91 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_
     for (int w = 0; w < NW; ++w) v += s_h[w][e];
     if (v) atomicAdd(&hist[(blockIdx.x % kGqCopies) * (NB * 4) + e], v);
   }
+}
+
+// The next call's key map (gq_bin): cells over this call's finite key range [min, max] (the
+// producer's per-block parts, or the allreduced (min, -max) when nparts < 0), each cell's bins in
+// proportion to this call's houses there — the superbin CDF (linear inside a superbin) at the cell
+// edges, read through this call's map; then the superbin copies are zeroed for the next producer.
+// One whole block of kGqThreads (k_gq_select's map block: off the decision's critical path); its
+// LDS work areas are carved from `lds` (>= kGqMapLds bytes, free: the caller's window array).
+constexpr int kGqMapLds = (3 * (kGqThreads / 64) + 2 + 2 * kGqSuper + kGqCells + 1) * 8 + kGqCells * 4 +
+                          (kGqThreads / 64) * 8;
+__device__ __forceinline__ void gq_next_map(const KParams& p, unsigned* __restrict__ hist, const double* __restrict__ part,
+                            int nparts, GqSel* __restrict__ sel, uint32_t* __restrict__ map, unsigned char* lds) {
+  constexpr int NW = kGqThreads / 64;
+  double* s_w = reinterpret_cast<double*>(lds);
+  double* s_lo = s_w + NW;
+  double* s_hi = s_lo + NW;
+  double* s_rng = s_hi + NW;
+  double* s_pre = s_rng + 2;
+  double* s_cnt = s_pre + kGqSuper;
+  double* s_C = s_cnt + kGqSuper;
+  unsigned long long* s_wc = reinterpret_cast<unsigned long long*>(s_C + kGqCells + 1);
+  uint32_t* s_map = reinterpret_cast<uint32_t*>(s_wc + NW);
+  const int tid = threadIdx.x;
+  unsigned long long cs = 0ull;  // this superbin's houses (tid < kGqSupN), over the copies
+  if (tid < kGqSupN)
+#pragma unroll
+    for (int q = 0; q < kGqCopies; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4*>(hist + kGqBins * 4 + q * kGqSupStride + tid * 4);
+      cs += (unsigned long long)v.x + v.y + v.z + v.w;
+    }
+  double x = 0.0;
+  unsigned long long xc = cs;
+  gq_block_scan(x, xc, s_w, s_wc);
+  if (tid < kGqSuper) { s_pre[tid] = (double)(xc - cs); s_cnt[tid] = (double)cs; }
+  if (tid < kGqCells) s_map[tid] = map[tid];
+  double lo = INFINITY, hi = -INFINITY;
+  if (nparts < 0) {  // sharded: the cluster's range, allreduced as (min, -max) (k_gq_range)
+    if (tid == 0) { lo = part[0]; hi = -part[1]; }
+  } else {
+    for (int b = tid; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, off));
+    hi = fmax(hi, __shfl_xor(hi, off));
+  }
+  if ((tid & 63) == 0) { s_lo[tid >> 6] = lo; s_hi[tid >> 6] = hi; }
+  __syncthreads();
+  if (tid == 0) {
+    double kmin = s_lo[0], kmax = s_hi[0];
+    for (int w = 1; w < NW; ++w) { kmin = fmin(kmin, s_lo[w]); kmax = fmax(kmax, s_hi[w]); }
+    const double range = kmax - kmin;
+    s_rng[0] = kmin == kmin && kmin < INFINITY ? kmin : 0.0;
+    s_rng[1] = range > 0.0 && range < INFINITY ? (double)kGqCells / range : 0.0;
+  }
+  __syncthreads();
+  const double okmin = sel->kmin, oscale = sel->scale, nkmin = s_rng[0], nscale = s_rng[1];
+  if (tid <= kGqCells) {
+    double C = 0.0;
+    if (nscale > 0.0) {
+      const double u = (nkmin + (double)tid / nscale - okmin) * oscale;  // the edge, in this call's cells
+      const int c = u >= (double)(kGqCells - 1) ? kGqCells - 1 : (u > 0.0 ? (int)u : 0);
+      const uint32_t m = s_map[c];
+      const double f = fmin(fmax(u - (double)c, 0.0), 1.0);
+      const double sp = ((double)(m >> 16) + f * (double)(m & 0xFFFFu)) / (double)(kGqBins / kGqSuper);
+      const int sc = sp >= (double)(kGqSuper - 1) ? kGqSuper - 1 : (sp > 0.0 ? (int)sp : 0);
+      C = s_pre[sc] + fmin(fmax(sp - (double)sc, 0.0), 1.0) * s_cnt[sc];
+    }
+    s_C[tid] = C;
+  }
+  __syncthreads();
+  if (tid < kGqCells) {  // B0_g = g + floor(K (C_g - C_0) / (C_G - C_0)): non-decreasing in g, so W_g >= 1
+    const int NBE = gq_bins_eff(p.n_global), K = NBE - kGqCells;
+    const double T = s_C[kGqCells] - s_C[0];
+    auto edge = [&](int g) {
+      if (g >= kGqCells) return NBE;
+      if (!(T > 0.0)) return g * (NBE / kGqCells);  // (no spread seen: uniform cells)
+      return g + min(K, (int)((double)K * ((s_C[g] - s_C[0]) / T)));
+    };
+    const int b0 = edge(tid), b1 = edge(tid + 1);
+    map[tid] = ((uint32_t)b0 << 16) | (uint32_t)(b1 - b0);
+  }
+  if (tid == 0) { sel->kmin = nkmin; sel->scale = nscale; }  // (no later kernel of this call maps keys)
+  __syncthreads();  // (every thread has read the superbin copies and the old map)
+  for (int e = tid; e < kGqCopies * kGqSupStride; e += blockDim.x) hist[kGqBins * 4 + e] = 0u;
 }
 
 // K3: every block finds the crossing bin inside superbin sb (lane l = its bin l) and the candidate
@@ -2042,8 +2071,6 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
   const int bb = sel->sb * 64;
   if (tid < kWinCap) s_cnt[tid] = 0u;
   if (tid == 0) { s_l0 = 0; s_le = 0; }
-  if (blockIdx.x == 0)  // (k_gq_bins read them; the next producer fills them again)
-    for (int e = tid; e < kGqCopies * kGqSupStride; e += blockDim.x) hist[kGqBins * 4 + e] = 0u;
   if (on && tid < 128) {
     double p_on[kWinCap];
 #pragma unroll
@@ -2498,7 +2525,8 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
                                                     double S, double pmin, GqSel* __restrict__ sel,
                                                     uint8_t* __restrict__ action, unsigned long long* __restrict__ slab,
                                                     unsigned* __restrict__ hist, const uint4* __restrict__ gathered,
-                                                    int world, unsigned* __restrict__ tickets) {
+                                                    int world, unsigned* __restrict__ tickets,
+                                                    const double* __restrict__ part, int nparts, uint32_t* __restrict__ map) {
   __shared__ uint4 s_e[kGqCap];
   __shared__ int s_off[kGqMaxRanks + 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -2575,9 +2603,17 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
   // Valid forms): every sorted[] store is sc1 and drained by its wave before the workgroup barrier
   // and the block's agent-scope ticket add (grid_last_block); the last block loads sorted[] only
   // with sc1 loads (gq_decide), so no fence is needed
-  if (!grid_last_block(tickets)) return;  // (block-uniform)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only)
-  gq_decide(p, sorted, S, pmin, sel, action, slab, s_e, gathered != nullptr, ovf0);
+  if (grid_last_block(tickets)) {  // (block-uniform)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only)
+    gq_decide(p, sorted, S, pmin, sel, action, slab, s_e, gathered != nullptr, ovf0);
+  }
+  // the next call's key map, by block 0 (dispatched first, it is rarely the last to take a ticket:
+  // the map's ~2 us run beside the decision instead of before it, as they did in k_gq_bins)
+  static_assert(kGqMapLds <= (int)sizeof(s_e), "the map's work areas fit the window array");
+  if (blockIdx.x == 0) {
+    __syncthreads();  // (a decision by this block has finished with s_e)
+    gq_next_map(p, hist, part, nparts, sel, map, reinterpret_cast<unsigned char*>(s_e));
+  }
 }
 
 // sharded greedy (mdr_greedy_inputs / mdr_greedy_select): this shard's (key, P, lockout) rows, and
