@@ -38,7 +38,25 @@ def main():
     for _ in range(20):
         env.rollout(n, action_mode="random", rewards=rew)
     torch.cuda.synchronize()
-    res = {k: [] for k in ("rollout (whole call)", "rollout_begin", "driver_window", "shard.rollout", "sync")}
+    res = {k: [] for k in ("rollout (whole call)", "rollout_begin", "driver_window", "shard.rollout", "sync",
+                           "python before the fused C call", "fused C call", "python after the fused C call")}
+    # the fused path (Environment.rollout -> _host.rollout1): stamp the C call's entry and exit
+    import mdr_amd.environment as E
+
+    host = E._host
+    stamps = []
+
+    class _Shim:
+        drivers = staticmethod(host.drivers)
+
+        @staticmethod
+        def rollout1(*args):
+            stamps.append(time.perf_counter())
+            r = host.rollout1(*args)
+            stamps.append(time.perf_counter())
+            return r
+
+    E._host = _Shim
     def idle():
         if a.idle == "spin":
             t = time.perf_counter()
@@ -51,12 +69,17 @@ def main():
         torch.cuda.synchronize()
         idle()
         t0 = time.perf_counter()
+        stamps.clear()
         env.rollout(n, action_mode="random", rewards=rew)
         t1 = time.perf_counter()
         torch.cuda.synchronize()
         t2 = time.perf_counter()
         res["rollout (whole call)"].append(t1 - t0)
         res["sync"].append(t2 - t1)
+        if len(stamps) == 2:
+            res["python before the fused C call"].append(stamps[0] - t0)
+            res["fused C call"].append(stamps[1] - stamps[0])
+            res["python after the fused C call"].append(t1 - stamps[1])
         # the pieces, as Environment.rollout issues them
         torch.cuda.synchronize()
         idle()
@@ -74,6 +97,8 @@ def main():
         res["shard.rollout"].append(t3 - t2)
     torch.cuda.synchronize()
     for k, v in res.items():
+        if not v:
+            continue
         print(f"{k:>22s}: min {1e6 * min(v):7.1f} us  median {1e6 * statistics.median(v):7.1f} us")
 
 
