@@ -573,6 +573,11 @@ def main():
     if comm is not None:
         import torch.distributed as dist
 
+        # deterministic teardown: every rank past its last collective, then the library's RCCL
+        # communicator (mdr_destroy -> ncclCommDestroy) on every rank, then torch's process group
+        torch.cuda.synchronize()
+        dist.barrier()
+        sh.close()
         dist.destroy_process_group()
 
 
