@@ -156,6 +156,52 @@ def test_actor_vs_torch_sizes(torch_gpu, n, precision):
     np.testing.assert_array_equal(prob.cpu().numpy(), p[np.arange(n), a])
 
 
+LAYOUTS = {
+    # 2 neighbours: 18 features, 20 slots -> one k-step of 32, run as KS1 = 2 with a zero k-step
+    "ks1_padded": {"cluster_prop.agents_comm_prop.max_nb_agents_communication": 2},
+    # every own-state feature + hvac messages: 88 features, 100 slots -> KS1 = 4
+    "ks1_4": {"cluster_prop.message_prop.hvac": True, "state_prop.hvac": True, "state_prop.solar_gain": True,
+              "state_prop.thermal": True},
+}
+
+
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("layout", sorted(LAYOUTS))
+def test_actor_layer1_ksteps(torch_gpu, layout, precision):
+    """The layer-1 k-step instantiations at their edges (mdr_actor.hip KS1): probabilities vs torch
+    fp32 on the same obs rows, at 3,001 houses (a ragged last tile)."""
+    from mdr_amd.actor import DeviceActor
+
+    torch = torch_gpu
+    n = 3001
+    ov = {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals"}
+    ov.update(LAYOUTS[layout])
+    env = make_env(gu.props_from_overrides(ov), 5)
+    rs = np.random.RandomState(7)
+    for _ in range(5):
+        env.step_tensor(torch.from_numpy(rs.randint(0, 2, n).astype(np.uint8)).to("cuda"))
+    F = env.obs_spec().n_feat
+    assert F == {"ks1_padded": 18, "ks1_4": 88}[layout]
+    actor = scaled_actor(torch, F, 2.0, seed=5)
+    probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
+    obs = torch.empty((n, F), dtype=torch.float32, device="cuda")
+    if layout == "ks1_4" and precision == "fp32":
+        # three bf16 planes of W1 (7 x 4 k-steps) and W2 (7 x 4) are 168 KiB: more than a CU's LDS
+        from mdr_amd._lib import MdrError
+
+        with pytest.raises(MdrError, match="160 KiB LDS"):
+            DeviceActor(env, actor, precision=precision).select_actions(probs=probs, obs_out=obs,
+                                                                        count_next=False)
+        return
+    da = DeviceActor(env, actor, precision=precision)
+    da.select_actions(probs=probs, obs_out=obs, count_next=False)
+    with torch.no_grad():
+        tp = actor(obs).cpu().numpy()
+    err = float(np.abs(probs.cpu().numpy() - tp).max())
+    print(f"{layout} {precision}: max |p - p_torch| = {err:.3g}")
+    assert err < (4e-6 if precision == "fp32" else PROB_ATOL[precision])
+
+
 def test_actor_sampling_statistics(torch_gpu):
     """Categorical sampling: the fraction of houses turning on matches the mean probability."""
     from mdr_amd.actor import DeviceActor
