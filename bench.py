@@ -560,7 +560,7 @@ def main():
                            "frac": tfs / BF16_PEAK_TFS, "traffic": None, "kernel": "mdr::k_actor",
                            "kernel_avg_us": actor_ms * 1e3, "launches_timed": launches,
                            "algorithmic_flops_per_launch": flops_launch, "flops_per_house": flops_house,
-                           "mfma_products_per_mac": 3 if args.precision == "bf16x3" else 1,
+                           "mfma_products_per_mac": {"bf16": 1, "bf16x3": 3, "fp32": 6}[args.precision],
                            "step_share": {"what": "launch-stream time per tick minus k_actor's time: the step "
                                                   "kernel's share of a tick (not a kernel duration)",
                                           "us_per_tick": kern_ms * 1e3}}

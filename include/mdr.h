@@ -448,6 +448,21 @@ int mdr_rccl_init(mdr_ctx* ctx, const uint8_t* id128, int world, int rank);
 /* in-place allreduce on `stream`: dtype 0 = int64 sum, 1 = double sum, 2 = double max,
  * 3 = uint32 sum, 4 = double min */
 int mdr_rccl_allreduce(mdr_ctx* ctx, void* buf, int64_t count, int dtype, void* stream);
+/* Host collectives: the same sharded C loops (mdr_rollout_begin / mdr_rollout_sharded /
+ * mdr_actor_rollout_sharded) with their exchanges handed to the caller instead of the library
+ * RCCL communicator — e.g. torch.distributed over gloo, so several ranks can share one GPU (how the
+ * world > 2 sharded paths are tested on a 1-GPU box).  Before each callback the library
+ * synchronises the stream the exchange is ordered on; the callback completes the exchange on the
+ * device buffers before it returns (0 = OK).  allreduce: in place, `op` = the mdr_rccl_allreduce
+ * dtype codes.  sendrecv: `send_bytes` from dev_send to rank dst and `recv_bytes` from rank src
+ * into dev_recv, as one paired exchange; `tag` tells the two ring directions apart (1: to the next
+ * rank, 2: to the previous).  Replaces SURVEY §8(e)'s RCCL calls one for one (environment.py:72-108
+ * exchange points). */
+typedef int (*mdr_host_allreduce_fn)(void* user, void* dev_buf, int64_t count, int op);
+typedef int (*mdr_host_sendrecv_fn)(void* user, const void* dev_send, int64_t send_bytes, int dst, void* dev_recv,
+                                    int64_t recv_bytes, int src, int tag);
+int mdr_comm_host(mdr_ctx* ctx, int world, int rank, mdr_host_allreduce_fn allreduce, mdr_host_sendrecv_fn sendrecv,
+                  void* user);
 /* all-gather of `bytes` per rank into recv (world x bytes, rank order) on `stream` */
 int mdr_rccl_allgather(mdr_ctx* ctx, const void* send, void* recv, int64_t bytes, void* stream);
 /* sharded multi-tick rollout, RCCL allreduce of the count slab inside the loop:

@@ -67,17 +67,41 @@ def host_out() -> str:
     return os.path.join(HERE, "mdr_amd", "_mdr_host" + sysconfig.get_config_var("EXT_SUFFIX"))
 
 
-def build_host(force: bool = False, verbose: bool = False) -> str:
-    """The rollout host drivers (csrc/mdr_host.c) as a CPython extension next to the package."""
+HOST_FLAGS = ["-O2", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-Wall"]
+
+
+def host_src_hash() -> str:
+    """sha256 (16 hex digits) of csrc/mdr_host.c and its build flags: stamped into _mdr_host
+    (build_id()) and checked when mdr_amd.environment imports it, so a stale extension is refused."""
+    h = hashlib.sha256(" ".join(HOST_FLAGS).encode())
+    with open(HOST_SRC, "rb") as f:
+        h.update(f.read())
+    return h.hexdigest()[:16]
+
+
+def host_hash(path: str | None = None) -> str | None:
+    """The source hash stamped into a built _mdr_host (None if absent or unstamped)."""
+    path = path or host_out()
+    if not os.path.exists(path):
+        return None
+    with open(path, "rb") as f:
+        m = re.search(rb"MDR_HOST_SRC_HASH:([0-9a-f]{16})", f.read())
+    return m.group(1).decode() if m else None
+
+
+def build_host(force: bool = False, verbose: bool = False, sanitize: bool = False, out: str | None = None) -> str:
+    """The rollout host drivers (csrc/mdr_host.c) as a CPython extension next to the package
+    (``sanitize``: an AddressSanitizer + UBSan build for the host tests, written to ``out``)."""
     import sysconfig
 
-    out = host_out()
-    if not force and os.path.exists(out) and os.path.getmtime(out) >= max(os.path.getmtime(HOST_SRC),
-                                                                          os.path.getmtime(__file__)):
+    out = out or host_out()
+    if not force and not sanitize and host_hash(out) == host_src_hash():
         return out
     cc = os.environ.get("CC", "gcc")
-    cmd = [cc, "-O2", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math", "-Wall",
-           "-I" + sysconfig.get_paths()["include"], HOST_SRC, "-o", out + ".tmp", "-lm"]
+    san = ["-g", "-O1", "-fno-omit-frame-pointer", "-fsanitize=address,undefined", "-fno-sanitize-recover=all"] \
+        if sanitize else []
+    cmd = [cc] + HOST_FLAGS + san + [f"-DMDR_HOST_SRC_HASH=\"{host_src_hash()}\"",
+                                     "-I" + sysconfig.get_paths()["include"], HOST_SRC, "-o", out + ".tmp", "-lm"]
     if verbose:
         print(" ".join(cmd), flush=True)
     r = subprocess.run(cmd, capture_output=True, text=True)

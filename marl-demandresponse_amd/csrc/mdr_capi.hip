@@ -130,6 +130,11 @@ struct mdr_ctx {
   int gq_nparts = 0;                     //   (from the last step's epilogue: its grid's partials)
   // multi-GPU
   ncclComm_t comm = nullptr;
+  struct {                               // mdr_comm_host: the caller's collectives instead of RCCL
+    mdr_host_allreduce_fn allreduce = nullptr;
+    mdr_host_sendrecv_fn sendrecv = nullptr;
+    void* user = nullptr;
+  } host;
   int world = 1, rank = 0;
   hipStream_t comm_stream = nullptr;     // per-tick / per-window allreduces of the overlapped pipelines
   hipStream_t cap_stream = nullptr;      // graph capture (graphs are replayed on the caller's stream)
@@ -167,6 +172,54 @@ struct mdr_ctx {
 };
 
 namespace {
+
+// the context has a communicator (the library's RCCL one, or the caller's host collectives)
+bool has_comm(const mdr_ctx* c) { return c->comm != nullptr || c->host.allreduce != nullptr; }
+
+// in-place allreduce ordered on st (op: the mdr_rccl_allreduce dtype codes; 0 = 64-bit sum, which
+// the unsigned count slabs use: the same bits for sums below 2^63)
+int comm_allreduce(mdr_ctx* c, void* buf, size_t count, int op, hipStream_t st) {
+  if (c->comm) {
+    const ncclDataType_t t = op == 0 ? ncclInt64 : op == 3 ? ncclUint32 : ncclFloat64;
+    const ncclRedOp_t o = op == 2 ? ncclMax : op == 4 ? ncclMin : ncclSum;
+    RCCL_TRY(ncclAllReduce(buf, buf, count, t, o, c->comm, st));
+    return MDR_OK;
+  }
+  if (!c->host.allreduce) return fail(MDR_ESTATE, "no communicator (mdr_rccl_init / mdr_comm_host)");
+  HIP_TRY(hipStreamSynchronize(st));
+  if (int r = c->host.allreduce(c->host.user, buf, (int64_t)count, op))
+    return fail(MDR_ERCCL, "host allreduce callback failed (" + std::to_string(r) + ")");
+  return MDR_OK;
+}
+
+// the 'neighbours' ring halo of a sharded obs: this shard's last lo rows (mine[hi, hi+lo)) to the
+// next rank, its first hi rows to the previous one; recv = [lo rows of prev | hi rows of next]
+int comm_halo(mdr_ctx* c, float* mine, float* recv, int lo, int hi, int M, hipStream_t st) {
+  const int prev = (c->rank + c->world - 1) % c->world, next = (c->rank + 1) % c->world;
+  if (c->comm) {
+    RCCL_TRY(ncclGroupStart());
+    if (lo) {
+      RCCL_TRY(ncclSend(mine + (size_t)hi * M, (size_t)lo * M, ncclFloat32, next, c->comm, st));
+      RCCL_TRY(ncclRecv(recv, (size_t)lo * M, ncclFloat32, prev, c->comm, st));
+    }
+    if (hi) {
+      RCCL_TRY(ncclSend(mine, (size_t)hi * M, ncclFloat32, prev, c->comm, st));
+      RCCL_TRY(ncclRecv(recv + (size_t)lo * M, (size_t)hi * M, ncclFloat32, next, c->comm, st));
+    }
+    RCCL_TRY(ncclGroupEnd());
+    return MDR_OK;
+  }
+  if (!c->host.sendrecv) return fail(MDR_ESTATE, "no communicator for the ring halo");
+  HIP_TRY(hipStreamSynchronize(st));
+  const int64_t b = (int64_t)sizeof(float) * M;
+  if (lo)
+    if (int r = c->host.sendrecv(c->host.user, mine + (size_t)hi * M, lo * b, next, recv, lo * b, prev, 1))
+      return fail(MDR_ERCCL, "host sendrecv callback failed (" + std::to_string(r) + ")");
+  if (hi)
+    if (int r = c->host.sendrecv(c->host.user, mine, hi * b, prev, recv + (size_t)lo * M, hi * b, next, 2))
+      return fail(MDR_ERCCL, "host sendrecv callback failed (" + std::to_string(r) + ")");
+  return MDR_OK;
+}
 
 unsigned long long* slab_at(mdr_ctx* c, int r) { return c->d_slab + (size_t)((r % 3 + 3) % 3) * c->slab_len; }
 
@@ -772,7 +825,7 @@ static int launch_step_window(mdr_ctx* c, int mode, bool ka, const uint8_t* acti
 // stream's reduce + step (which then has no lookahead): the allreduce latency hides behind the
 // step kernels.  Two sets of ON-mask / end-word buffers alternate; events order the reuse.
 static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t* action, int64_t act_stride,
-                           int mode, double* reward, int64_t rew_stride, double* p_out, ncclComm_t comm,
+                           int mode, double* reward, int64_t rew_stride, double* p_out, bool shd,
                            hipStream_t st, bool counted = false, bool pipe = false,
                            const mdr_tick* host_ticks = nullptr) {
   const int nw = (n + c->win - 1) / c->win;
@@ -801,9 +854,8 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
       if (int rc = launch_count(c, mode, a, act_stride, tk + t0, 0, K, slot(w), onbs[w % 2], wahs[w % 2],
                                 w == 0 ? nullptr : wahs[(w - 1) % 2], cs, true))
         return rc;
-      if (comm)
-        RCCL_TRY(ncclAllReduce(win_red_ptr(c, slot(w)), win_red_ptr(c, slot(w)), (size_t)K * ncap, ncclUint64,
-                               ncclSum, comm, cs));
+      if (shd)
+        if (int rc = comm_allreduce(c, win_red_ptr(c, slot(w)), (size_t)K * ncap, 0, cs)) return rc;
       HIP_TRY(hipEventRecord(c->ev_ar[w % kSlabs], cs));
       // compute stream: the tick records + step (no lookahead)
       HIP_TRY(hipStreamWaitEvent(st, c->ev_ar[w % kSlabs], 0));
@@ -825,11 +877,11 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     // count kernel's last block on one GPU, after the shards' allreduce when sharded
     if (int rc = launch_count(c, mode, action, act_stride, host_ticks ? nullptr : tk,
                               host_ticks ? host_ticks[0].tick : 0, wsz(0), slot(0), c->d_onb, c->d_wah, nullptr, st,
-                              host_ticks && !comm))
+                              host_ticks && !shd))
       return rc;
-    if (host_ticks && comm)
-      RCCL_TRY(ncclAllReduce(slot(0), slot(0), (size_t)wsz(0) * kCountShards * ncap, ncclUint64, ncclSum, comm, st));
-    if (host_ticks && comm) {
+    if (host_ticks && shd)
+      if (int rc = comm_allreduce(c, slot(0), (size_t)wsz(0) * kCountShards * ncap, 0, st)) return rc;
+    if (host_ticks && shd) {
       hipLaunchKernelGGL(k_win_reduce, dim3(wsz(0)), dim3(64 * ncap), 0, st, kp, slot(0), wsz(0),
                          (const TickArgs*)nullptr, (double*)nullptr);
       LAUNCH_CHECK("k_win_reduce (P only)");
@@ -861,8 +913,8 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
     }
     // sharded: every rank's sharded per-tick class counts are summed first (exact integers; the
     // slot's shard part, K x 64 x n_cap values), so one reduce kernel yields the global counts
-    if (comm)
-      RCCL_TRY(ncclAllReduce(slot(w), slot(w), (size_t)K * kCountShards * ncap, ncclUint64, ncclSum, comm, st));
+    if (shd)
+      if (int rc = comm_allreduce(c, slot(w), (size_t)K * kCountShards * ncap, 0, st)) return rc;
     hipLaunchKernelGGL(k_win_reduce, dim3(K), dim3(64 * ncap), 0, st, kp, slot(w), K, tk + t0,
                        w == nw - 1 ? p_out : nullptr);
     LAUNCH_CHECK("k_win_reduce");
@@ -895,7 +947,7 @@ static bool pipe_buffers(mdr_ctx* c) {
 static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t act_stride, int mode,
                             double* reward, int64_t rew_stride, double* p_out, hipStream_t st) {
   if (window_ok(c, mode))
-    return window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st);
+    return window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, false, st);
   if (mode == MDR_ACT_BANGBANG || mode == MDR_ACT_DEADBAND_BANGBANG)
     return fail(MDR_EARG, "rollout: bang-bang sources need the per-step API (mdr_step with a lookahead)");
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
@@ -960,7 +1012,7 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
     rc = ensure_ticks(c, n);
     if (!rc) rc = wslab_clean(c, st);
     if (!rc)
-      rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st, counted,
+      rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, false, st, counted,
                            false, ticks);
     c->counts_ready = false;
     return rc;
@@ -1011,7 +1063,7 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   if (!window_ok(c, mode)) return MDR_OK;
   // a sharded context (RCCL attached): single-window rollouts only, counts allreduced here, so
   // the matching mdr_rollout_sharded launches just the KA step kernel
-  const bool sharded = c->comm != nullptr;
+  const bool sharded = has_comm(c);
   if (sharded && n > c->win) return MDR_OK;
   hipStream_t st = S(stream);
   int rc = refresh_if_dirty(c, st);
@@ -1027,8 +1079,7 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
                     true);
   if (rc) return rc;
   if (sharded) {  // every rank's per-tick class totals (its count kernel's last block), summed
-    RCCL_TRY(ncclAllReduce(win_red_ptr(c, c->d_wslab), win_red_ptr(c, c->d_wslab), (size_t)k0 * c->kp.n_cap,
-                           ncclUint64, ncclSum, c->comm, st));
+    if (int rc2 = comm_allreduce(c, win_red_ptr(c, c->d_wslab), (size_t)k0 * c->kp.n_cap, 0, st)) return rc2;
     hipLaunchKernelGGL(k_win_records, dim3(1), dim3(kWindowMax), 0, st, c->kp, c->d_wslab, k0,
                        (const TickArgs*)nullptr, (double*)nullptr);
     LAUNCH_CHECK("k_win_records (P only)");
@@ -1457,11 +1508,27 @@ int mdr_rccl_unique_id(uint8_t* id128) {
 
 int mdr_rccl_init(mdr_ctx* c, const uint8_t* id128, int world, int rank) {
   if (!c || !id128 || world < 1 || rank < 0 || rank >= world) return fail(MDR_EARG, "mdr_rccl_init: bad argument");
+  if (c->host.allreduce) return fail(MDR_ESTATE, "mdr_rccl_init: the context already has host collectives");
   HIP_TRY(hipSetDevice(c->cfg.device));
   ncclUniqueId id;
   memcpy(&id, id128, 128);
   RCCL_TRY(ncclCommInitRank(&c->comm, world, id, rank));
   if (!c->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+  c->world = world;
+  c->rank = rank;
+  return MDR_OK;
+}
+
+int mdr_comm_host(mdr_ctx* c, int world, int rank, mdr_host_allreduce_fn allreduce, mdr_host_sendrecv_fn sendrecv,
+                  void* user) {
+  if (!c || !allreduce || !sendrecv || world < 1 || rank < 0 || rank >= world)
+    return fail(MDR_EARG, "mdr_comm_host: bad argument");
+  if (c->comm) return fail(MDR_ESTATE, "mdr_comm_host: the context already has an RCCL communicator");
+  HIP_TRY(hipSetDevice(c->cfg.device));
+  if (!c->comm_stream) HIP_TRY(hipStreamCreateWithFlags(&c->comm_stream, hipStreamNonBlocking));
+  c->host.allreduce = allreduce;
+  c->host.sendrecv = sendrecv;
+  c->host.user = user;
   c->world = world;
   c->rank = rank;
   return MDR_OK;
@@ -1498,7 +1565,7 @@ int rollout_sharded_overlap(mdr_ctx* c, const TickArgs* ticks, int n, int mode, 
   for (int t = 0; t < n; ++t) {
     // comm stream: counts of tick t are complete once K(t-1) (or phase 1) has finished
     HIP_TRY(hipStreamWaitEvent(cs, t == 0 ? c->ev_pc : c->ev_k1[(t - 1) % kSlabs], 0));
-    RCCL_TRY(ncclAllReduce(slab(t), slab(t), c->slab_len, ncclUint64, ncclSum, c->comm, cs));
+    if (int rc = comm_allreduce(c, slab(t), c->slab_len, 0, cs)) return rc;
     HIP_TRY(hipEventRecord(c->ev_ar[t % kSlabs], cs));
     // compute stream: K(t) needs the allreduced counts of tick t-1 for that tick's reward
     if (t >= 1) HIP_TRY(hipStreamWaitEvent(st, c->ev_ar[(t - 1) % kSlabs], 0));
@@ -1534,8 +1601,7 @@ int rollout_sharded_serial(mdr_ctx* c, const TickArgs* ticks, int n, const uint8
                          (uint64_t)0, ticks + t, slab_at(c, c->ring));
       LAUNCH_CHECK("k_power_counts");
     }
-    RCCL_TRY(ncclAllReduce(slab_at(c, c->ring), slab_at(c, c->ring), c->slab_len, ncclUint64, ncclSum,
-                           c->comm, st));
+    if (int rc = comm_allreduce(c, slab_at(c, c->ring), c->slab_len, 0, st)) return rc;
     int rc = launch_step(c, a, mode, TickArgs{}, ticks + t, reward + (int64_t)t * rew_stride,
                          la ? mode : 0, MDR_CTRL_NONE, nullptr, t == n - 1 ? p_out : nullptr, st);
     if (rc) return rc;
@@ -1554,21 +1620,21 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
   if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout_sharded: bad argument");
   // a single window begun by mdr_rollout_begin on this sharded context (count, allreduce, P-only
   // reduce already issued): only the KA step kernel is left, with these drivers as its arguments
-  if (c->begun.on && c->begun.sharded && c->comm && c->begun.n == n && c->begun.mode == mode &&
+  if (c->begun.on && c->begun.sharded && has_comm(c) && c->begun.n == n && c->begun.mode == mode &&
       c->begun.tick0 == ticks[0].tick && c->begun.action == action && c->begun.act_stride == act_stride &&
       window_ok(c, mode) && n <= c->win && consecutive(ticks, n)) {
     c->begun.on = false;
     hipStream_t st = S(stream);
     int rc = ensure_ticks(c, n);
     if (!rc)
-      rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, nullptr, st, true,
+      rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, false, st, true,
                            false, ticks);
     c->counts_ready = false;
     return rc;
   }
   drop_begun(c);
   if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout_sharded: context not bound");
-  if (!c->comm) return fail(MDR_ESTATE, "mdr_rollout_sharded: RCCL not initialised");
+  if (!has_comm(c)) return fail(MDR_ESTATE, "mdr_rollout_sharded: no communicator (mdr_rccl_init / mdr_comm_host)");
   if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout_sharded: bad action source");
   if (mode == MDR_ACT_BANGBANG || mode == MDR_ACT_DEADBAND_BANGBANG)
     return fail(MDR_EARG, "mdr_rollout_sharded: bang-bang sources need the per-step API");
@@ -1583,7 +1649,7 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
     rc = wslab_clean(c, st);
     if (rc) return rc;
     const bool pipe = c->win_pipe && c->comm_stream && pipe_buffers(c);
-    rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, c->comm, st, false,
+    rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, true, st, false,
                          pipe);
     c->counts_ready = false;
     return rc;
@@ -1968,7 +2034,7 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
   if (!c || !ticks || !osc || !sp || !reward || !p_dev || n < 1)
     return fail(MDR_EARG, "mdr_actor_rollout_sharded: bad argument");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_rollout_sharded: context not bound");
-  if (!c->comm) return fail(MDR_ESTATE, "mdr_actor_rollout_sharded: RCCL not initialised");
+  if (!has_comm(c)) return fail(MDR_ESTATE, "mdr_actor_rollout_sharded: no communicator (mdr_rccl_init / mdr_comm_host)");
   if (int rc = check_actor_obs(c, sp, "mdr_actor_rollout_sharded", S(stream))) return rc;
   if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
     return fail(MDR_EARG, "mdr_actor_rollout_sharded: common penalty modes need the per-step API");
@@ -1999,31 +2065,21 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
   mdr_obs_spec spec = *sp;
   spec.halo_msg = halo ? recv : nullptr;
   const ObsArgs o = obs_args(c, &spec, &osc[0]);
-  const int prev = (c->rank + c->world - 1) % c->world, next = (c->rank + 1) % c->world;
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
   c->ring = 0;
   for (int t = 0; t < n; ++t) {
     if (halo) {
       hipLaunchKernelGGL(k_halo_pack, dim3(1), dim3(64), 0, st, c->kp, o, lo, hi, mine);
       LAUNCH_CHECK("k_halo_pack");
-      RCCL_TRY(ncclGroupStart());
       // the previous rank's last lo houses come first in the halo, the next rank's first hi after
-      if (lo) {
-        RCCL_TRY(ncclSend(mine + (size_t)hi * M, (size_t)lo * M, ncclFloat32, next, c->comm, st));
-        RCCL_TRY(ncclRecv(recv, (size_t)lo * M, ncclFloat32, prev, c->comm, st));
-      }
-      if (hi) {
-        RCCL_TRY(ncclSend(mine, (size_t)hi * M, ncclFloat32, prev, c->comm, st));
-        RCCL_TRY(ncclRecv(recv + (size_t)lo * M, (size_t)hi * M, ncclFloat32, next, c->comm, st));
-      }
-      RCCL_TRY(ncclGroupEnd());
+      if (int rc = comm_halo(c, mine, recv, lo, hi, M, st)) return rc;
     }
     ObsArgs ot = o;
     ot.sc_dev = c->d_obs_sc + 4 * t;
     ActorOut out{action ? action + (int64_t)t * act_stride : c->d_act,
                  prob ? prob + (int64_t)t * prob_stride : nullptr, nullptr, nullptr, slab_at(c, c->ring), nullptr};
     if (int rc = launch_actor(c, &spec, ot, p_dev, 0, c->d_ticks + t, out, st)) return rc;
-    RCCL_TRY(ncclAllReduce(slab_at(c, c->ring), slab_at(c, c->ring), c->slab_len, ncclUint64, ncclSum, c->comm, st));
+    if (int rc = comm_allreduce(c, slab_at(c, c->ring), c->slab_len, 0, st)) return rc;
     if (int rc = launch_step(c, out.action, MDR_ACT_BUFFER, TickArgs{}, c->d_ticks + t,
                              reward + (int64_t)t * rew_stride, 0, MDR_CTRL_NONE, nullptr, p_dev, st))
       return rc;

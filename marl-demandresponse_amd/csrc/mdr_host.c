@@ -205,8 +205,10 @@ static PyObject* drivers(PyObject* self, PyObject* args) {
  * steps: mdr_rollout_begin (the first window's count, before the drivers exist), the driver loop
  * into `out`, and — when the window did not stop at midnight (k == n) — mdr_rollout with those
  * ticks (no action buffer, no graph).  begin / rollout are the library's entry points (addresses
- * from ctypes); rc_rollout = -1 when it was not called (begin failed, or k < n: the caller finishes
- * the driver window for the next day and launches itself). */
+ * from ctypes); rc_rollout = ROLLOUT_NOT_CALLED (1: no library status is positive) when it was not
+ * called (begin failed, or k < n: the caller finishes the driver window for the next day and
+ * launches itself); any other value is mdr_rollout's own status (0, or a negative MDR_E*). */
+#define ROLLOUT_NOT_CALLED 1
 typedef int (*begin_fn)(void* ctx, int n, uint64_t tick0, const uint8_t* action, int64_t act_stride, int mode,
                         void* stream);
 typedef int (*rollout_fn)(void* ctx, int n, const void* ticks, const uint8_t* action, int64_t act_stride, int mode,
@@ -241,15 +243,26 @@ static PyObject* rollout1(PyObject* self, PyObject* args) {
     return NULL;
   }
   const int rc_b = begin(ctx, (int)n, (uint64_t)tick0, NULL, 0, mode, stream);
-  if (rc_b != 0) return Py_BuildValue("iinLddd", rc_b, -1, (Py_ssize_t)0, 0LL, 0.0, 0.0, 0.0);
+  if (rc_b != 0) return Py_BuildValue("iinLddd", rc_b, ROLLOUT_NOT_CALLED, (Py_ssize_t)0, 0LL, 0.0, 0.0, 0.0);
   drv_res r;
   if (drivers_run(args, 8, &r) < 0) return NULL;
-  int rc_r = -1;
+  int rc_r = ROLLOUT_NOT_CALLED;
   if (r.k == r.n) rc_r = roll(ctx, (int)n, r.out, NULL, 0, mode, reward, rew_stride, p_dev, 0, stream);
   return Py_BuildValue("iinLddd", rc_b, rc_r, r.k, r.s, r.tod, r.sig, r.sol);
 }
 
+#ifndef MDR_HOST_SRC_HASH
+#define MDR_HOST_SRC_HASH "unstamped"
+#endif
+/* build_id() -> the source hash build_ext.py stamped in (checked against the tree at import) */
+static PyObject* build_id(PyObject* self, PyObject* args) {
+  (void)self;
+  (void)args;
+  return PyUnicode_FromString("MDR_HOST_SRC_HASH:" MDR_HOST_SRC_HASH);
+}
+
 static PyMethodDef methods[] = {
+    {"build_id", build_id, METH_NOARGS, "the source hash this extension was built from"},
     {"drivers", drivers, METH_VARARGS, "per-tick rollout drivers (see mdr_host.c)"},
     {"rollout1", rollout1, METH_VARARGS, "begin + drivers + mdr_rollout of one short rollout (see mdr_host.c)"},
     {NULL, NULL, 0, NULL},

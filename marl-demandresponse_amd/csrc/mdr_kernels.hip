@@ -89,7 +89,9 @@ __global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* 
 // writes the keys in its GQ epilogue)
 struct GqSel {
   double kmin, scale;            // the key map's cell grid: cell = (k - kmin) * scale (gq_code)
-  double base_tot;               // P of the houses before the window (exact for integer P)
+  double base_tot;               // P of the houses before the crossing superbin (k_gq_bins; read by every k_gq_compact block)
+  double win_tot;                // P of the houses before the window (k_gq_compact block 0 -> k_gq_select; a field of its
+                                 // own: overwriting base_tot raced with the compact blocks still reading it)
   unsigned long long base_cnt, total;
   int sb, bstar, bend, all, overflow, more_after, ncand;
   int whole;                     // the cluster fits the window (<= kGqCap houses): every house is a candidate
@@ -2126,7 +2128,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
       if (wovf) sel->overflow = 1;
       sel->bstar = bb + l0;
       sel->bend = bb + l0 + le;
-      sel->base_tot = s_base;
+      sel->win_tot = s_base;
       sel->more_after = s_basec + (unsigned long long)cnt < sel->total;
       sel->ncand = cnt;
     }
@@ -2134,7 +2136,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
   if (whole && blockIdx.x == 0 && tid == 0) {  // every house is in the window
     sel->bstar = 0;
     sel->bend = kGqBins;
-    sel->base_tot = 0.0;
+    sel->win_tot = 0.0;
     sel->more_after = 0;
     sel->ncand = (int)sel->total;
   }
@@ -2388,7 +2390,7 @@ __device__ void gq_exact(const KParams& p, double S, double pmin, uint8_t* __res
 }
 
 // The decision on the sorted window (k_gq_select's last block): the window into LDS, the exact
-// crossing position from base_tot, the window's prefix taken, then the gap walk (k_greedy_walk's
+// crossing position from win_tot, the window's prefix taken, then the gap walk (k_greedy_walk's
 // rule); the ON counts of the window's decided actions; what the window cannot decide goes to
 // gq_exact (sharded: to the host, GqSel.need_fb — one shard cannot order the whole cluster).  The
 // window carries global house ids: only this shard's houses are written (offset p.goff).
@@ -2427,7 +2429,7 @@ __device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restr
         if (e < ncand) { s_e[e] = v[u]; s_tk[e] = 0; }
       }
     }
-    if (tid == 0) { s_tot = sel->base_tot; s_k = -1; }
+    if (tid == 0) { s_tot = sel->win_tot; s_k = -1; }
     if (tid < kWinCap) s_cnt[tid] = 0u;
     __syncthreads();
     for (int c0 = 0; c0 < ncand; c0 += nth) {

@@ -103,6 +103,10 @@ ABI_STRUCTS = (mdr_config, mdr_soa, mdr_tick, mdr_pop_spec, mdr_obs_spec, mdr_ob
 
 P, VP, I, I64, U64, D = C.POINTER, C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_double
 
+# mdr_comm_host callbacks (include/mdr.h mdr_host_allreduce_fn / mdr_host_sendrecv_fn)
+HOST_ALLREDUCE_FN = C.CFUNCTYPE(I, VP, VP, I64, I)
+HOST_SENDRECV_FN = C.CFUNCTYPE(I, VP, VP, I64, I, VP, I64, I, I)
+
 # name -> (restype, argtypes); every symbol declared in include/mdr.h
 SIGNATURES = {
     "mdr_abi_version": (I, []),
@@ -155,6 +159,7 @@ SIGNATURES = {
     "mdr_rccl_init": (I, [VP, VP, I, I]),
     "mdr_rccl_allreduce": (I, [VP, VP, I64, I, VP]),
     "mdr_rccl_allgather": (I, [VP, VP, VP, I64, VP]),
+    "mdr_comm_host": (I, [VP, I, I, VP, VP, VP]),
     "mdr_rollout_sharded": (I, [VP, I, VP, VP, I64, I, VP, I64, VP, VP]),
     "mdr_rollout_sharded_mode": (I, [VP, P(I), P(I)]),
     "mdr_probe_stream": (I, [VP, VP, VP]),
@@ -199,6 +204,31 @@ def source_hash() -> str | None:
     if not all(os.path.exists(p) for p in m.SRC + m.HDR):
         return None
     return m.src_hash()
+
+
+def _build_ext():
+    import importlib.util
+
+    be = os.path.join(os.path.dirname(HERE), "build_ext.py")
+    if not os.path.exists(be):
+        return None
+    spec = importlib.util.spec_from_file_location("_mdr_build_ext", be)
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def check_host_ext(mod) -> None:
+    """Refuse a _mdr_host extension that was not built from csrc/mdr_host.c as it is in this tree
+    (its stamped build_id() against build_ext.host_src_hash(); skipped when the source is absent)."""
+    m = _build_ext()
+    if m is None or not os.path.exists(m.HOST_SRC):
+        return
+    want = m.host_src_hash()
+    have = mod.build_id().split(":", 1)[1]
+    if have != want:
+        raise MdrLibraryError(f"_mdr_host was built from other sources (extension {have}, tree {want}): "
+                              "rebuild it with __graft_entry__.build()")
 
 
 def load(path: str = LIB_PATH):

@@ -208,6 +208,39 @@ class TorchComm(RcclComm):
     def pipeline(self, shard) -> dict:
         return {"mode": "torch.distributed per-step"}
 
+    def ring_halo(self, shard, spec):
+        """Point-to-point ring halo, paired exactly as the library's RCCL exchange
+        (mdr_capi.hip mdr_actor_rollout_sharded): this shard's last lo houses go to rank r+1 and its
+        first hi houses to rank r-1; the halo is [lo rows from r-1 | hi rows from r+1].  Distinct
+        tags keep the two directions apart when r-1 == r+1 (world 2).  gloo has no device
+        send/recv, so its messages are staged through host memory (one copy each way)."""
+        import torch
+
+        k = spec.n_comm
+        lo, hi = k // 2, (k + 1) // 2
+        m = shard.lib.mdr_msg_width(C.byref(spec))
+        if shard.n < max(lo, hi):
+            raise NotImplementedError("shards smaller than the ring half-width")
+        mine = torch.empty((hi + lo, m), dtype=torch.float32, device=shard.device)
+        shard.halo_pack(spec, mine)
+        if self.world == 1:  # the local wrap-around (the RCCL path's send/recv to self)
+            return torch.cat([mine[hi:hi + lo], mine[:hi]]).contiguous()
+        host = self.dist.get_backend() == "gloo" and mine.is_cuda
+        src = mine.cpu() if host else mine
+        recv = torch.empty((lo + hi, m), dtype=torch.float32, device="cpu" if host else mine.device)
+        prev, nxt = (self.rank - 1) % self.world, (self.rank + 1) % self.world
+        P2P = self.dist.P2POp
+        ops = []
+        if lo:
+            ops += [P2P(self.dist.isend, src[hi:hi + lo].contiguous(), nxt, tag=1),
+                    P2P(self.dist.irecv, recv[:lo], prev, tag=1)]
+        if hi:
+            ops += [P2P(self.dist.isend, src[:hi].contiguous(), prev, tag=2),
+                    P2P(self.dist.irecv, recv[lo:], nxt, tag=2)]
+        for r in self.dist.batch_isend_irecv(ops):
+            r.wait()
+        return recv.to(shard.device) if host else recv
+
     def rollout(self, shard, ticks, actions, mode, rewards, rew_stride) -> None:
         for t in range(len(ticks)):
             tk = ticks.struct(t)
@@ -217,12 +250,82 @@ class TorchComm(RcclComm):
             shard.step(a, mode, tk, reward=rewards[t] if rew_stride else rewards)
 
 
+class HostComm(TorchComm):
+    """The library's sharded C loops (mdr_rollout_begin / mdr_rollout_sharded /
+    mdr_actor_rollout_sharded: count-ahead window pipeline, per-tick loops, actor + ring halo)
+    with their exchanges handed to ``torch.distributed`` through mdr_comm_host callbacks instead of
+    the library's RCCL communicator.  Over gloo several ranks share one GPU, so the C loops run at
+    world 3..8 on a 1-GPU box exactly as they run over RCCL, one collective call for one RCCL call
+    (the library synchronises the stream first; the callback finishes the exchange before it
+    returns).  Python-level exchanges (greedy stages, table obs, dict obs) are TorchComm's."""
+
+    native = True
+
+    def attach(self, shard) -> None:
+        if getattr(shard, "_host_comm", None) is self:
+            return
+        import torch
+
+        dist = self.dist
+        gloo = dist.get_backend() == "gloo"
+        dev = shard.device
+        ops = {0: ("<i8", dist.ReduceOp.SUM), 1: ("<f8", dist.ReduceOp.SUM), 2: ("<f8", dist.ReduceOp.MAX),
+               3: ("<u4", dist.ReduceOp.SUM), 4: ("<f8", dist.ReduceOp.MIN)}
+
+        def finish(t, host):
+            if host is not None:
+                t.copy_(host)
+            torch.cuda.synchronize(dev)
+
+        def allreduce(user, buf, count, op):
+            try:
+                typ, rop = ops[op]
+                t = device_view(buf, count, typ if typ != "<u4" else "<i4", dev)
+                h = t.cpu() if gloo else None
+                dist.all_reduce(h if gloo else t, op=rop)
+                finish(t, h)
+                return 0
+            except Exception as e:  # noqa: BLE001  (an exception must not cross the C frame)
+                self.error = e
+                return -1
+
+        def sendrecv(user, send, sbytes, dst, recv, rbytes, src, tag):
+            try:
+                s_t = device_view(send, sbytes, "|u1", dev)
+                r_t = device_view(recv, rbytes, "|u1", dev)
+                s_h = s_t.cpu() if gloo else s_t
+                r_h = torch.empty(rbytes, dtype=torch.uint8) if gloo else r_t
+                for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, s_h, dst, tag=tag),
+                                                 dist.P2POp(dist.irecv, r_h, src, tag=tag)]):
+                    w.wait()
+                finish(r_t, r_h if gloo else None)
+                return 0
+            except Exception as e:  # noqa: BLE001
+                self.error = e
+                return -1
+
+        self._cbs = (L.HOST_ALLREDUCE_FN(allreduce), L.HOST_SENDRECV_FN(sendrecv))  # (kept alive)
+        self.error = None
+        L.check(shard.lib.mdr_comm_host(shard.ctx, self.world, self.rank, self._cbs[0], self._cbs[1], None),
+                "mdr_comm_host")
+        shard._host_comm = self
+
+    def rollout(self, shard, ticks, actions, mode, rewards, rew_stride) -> None:
+        RcclComm.rollout(self, shard, ticks, actions, mode, rewards, rew_stride)
+
+    def pipeline(self, shard) -> dict:
+        return RcclComm.pipeline(self, shard)
+
+
 def make_comm(kind: str = "auto"):
     """Communicator for a sharded Environment: 'rccl' (libmdr_hip's own RCCL communicator, per-tick
-    allreduces issued from C), 'torch' (torch.distributed collectives), or 'auto' (rccl, falling
+    allreduces issued from C), 'torch' (torch.distributed collectives), 'host' (the library's C
+    loops with torch.distributed collectives as callbacks), or 'auto' (rccl, falling
     back to torch with a warning if the library communicator cannot be created)."""
     if kind == "torch":
         return TorchComm()
+    if kind == "host":
+        return HostComm()
     if kind == "rccl":
         return RcclComm()
     if kind != "auto":

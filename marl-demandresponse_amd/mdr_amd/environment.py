@@ -35,6 +35,9 @@ try:  # the rollout host drivers in C (csrc/mdr_host.c, built by build_ext.py); 
     from . import _mdr_host as _host
 except ImportError:  # pragma: no cover - the Python loop computes the same values
     _host = None
+if _host is not None:
+    L.check_host_ext(_host)  # (a stale build is refused, as libmdr_hip.so is)
+_HOST_ROLLOUT_NOT_CALLED = 1  # rollout1's rc_rollout when it did not call mdr_rollout (mdr_host.c)
 
 ACTION_MODES = {"buffer": L.ACT_BUFFER, "random": L.ACT_RANDOM, "always_on": L.ACT_ALWAYS_ON,
                 "bangbang": L.ACT_BANGBANG, "deadband_bangbang": L.ACT_DEADBAND_BANGBANG}
@@ -447,7 +450,9 @@ class Environment:
                     *launch, rng, rng.random, tp.temp_std, n, s, dts, od_tab, sig_tab, sol_tab, dd.month, dd.day,
                     wa, shc, drivers.SOLAR_TERMS_ARRAY, tod, sig, sol, tick0, buf)
                 L.check(rc_b, "mdr_rollout_begin")
-                if rc_r > 0:
+                # rc_r: mdr_rollout's status (0 or a negative MDR_E*), or 1 = not called (the
+                # window crossed midnight: the caller launches once the next day's drivers exist)
+                if rc_r != _HOST_ROLLOUT_NOT_CALLED:
                     L.check(rc_r, "mdr_rollout")
                 launched = rc_r == 0
             else:

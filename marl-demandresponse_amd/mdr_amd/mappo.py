@@ -118,18 +118,21 @@ class DeviceMAPPO:
     """MAPPO with device actor rollouts, device transition storage and the PPO update on the GPU."""
 
     def __init__(self, env, config: Optional[MAPPOConfig] = None, num_action: int = 2, seed: int = 1,
-                 precision: str = "bf16x3", returns: str = "reference", sampler: str = "auto"):
-        """``sampler``: the minibatch permutation of each PPO epoch — "reference" draws it from the
-        global torch CPU generator exactly as the reference's SubsetRandomSampler does, "device"
-        draws it on the GPU (torch.randperm on the device generator: no L-element host permutation
-        and copy per epoch at C5's N x T transitions), "auto" = "reference" up to 2^20 transitions
-        and "device" beyond."""
+                 precision: str = "bf16x3", returns: str = "reference", sampler: str = "reference"):
+        """``sampler``: the minibatch permutation of each PPO epoch — "reference" (default) draws it
+        from the global torch CPU generator exactly as the reference's SubsetRandomSampler does, so
+        reference-seeded runs keep the reference's minibatch order and later CPU draws at any size;
+        "device" (explicit opt-in) draws it on the GPU (torch.randperm on the device generator: no
+        L-element host permutation and copy per epoch at C5's N x T transitions; another order);
+        "auto" = "reference" up to 2^20 transitions and "device" beyond.  ``last_sampler`` records
+        which one the last update used."""
         torch = _torch()
         if returns not in ("reference", "per_agent"):
             raise ValueError("returns must be 'reference' (the reference's buffer order) or 'per_agent'")
         if sampler not in ("auto", "reference", "device"):
             raise ValueError("sampler must be 'auto', 'reference' or 'device'")
         self.sampler = sampler
+        self.last_sampler = None
         self.cfg = config or MAPPOConfig()
         self.env = env
         self.returns = returns
@@ -208,6 +211,7 @@ class DeviceMAPPO:
         Gt = self._returns(reward, done_rows, n).float()
         critic_in = torch.cat([state, others], 1)
         on_device = self.sampler == "device" or (self.sampler == "auto" and L > (1 << 20))
+        self.last_sampler = "device" if on_device else "reference"
         for _ in range(cfg.ppo_update_time):
             # SubsetRandomSampler + BatchSampler(drop_last=False): a permutation (the global CPU
             # generator's, or the device generator's — see sampler), cut in order into batch_size chunks

@@ -11,11 +11,11 @@ rand_vec.RandVec, tools.sample_vector / hasher / fade) as we know it:
   ``uniform(-1, 1)`` from a Mersenne Twister seeded with ``hasher([k]) * seed`` — hasher([k]) =
   max(1, int(|k| + 1)) and ``seed`` is the float ``random.random()`` SignalCalculator passes
   (signal_calculator.py:24-31), so ``random.seed`` hashes the float;
-* a lattice point contributes ``fade(1 - |xs - k|) * g * (xs - k)`` with fade(t) = 6 t**5 -
-  15 t**4 + 10 t**3 (evaluated here with products, t**3 = t*t*t, t**4 = t**3*t, t**5 = t**4*t, so
-  the scalar and the vectorised forms below agree bit for bit; the package's ``**`` may differ by an
-  ulp), and the contributions are summed with Python's ``sum`` (from int 0), in the order of
-  ``itertools.product``.
+* a lattice point contributes ``fade(1 - |xs - k|) * g * (xs - k)`` with fade(t) = 6 * t ** 5 -
+  15 * t ** 4 + 10 * t ** 3, the package's expression with Python float ``**`` (libm pow); the
+  vectorised form evaluates that same scalar expression once per distinct t, so both forms equal
+  the package's operations bit for bit; the contributions are summed with Python's ``sum`` (from
+  int 0), in the order of ``itertools.product``.
 
 The package draws the gradient by reseeding the GLOBAL ``random`` module; releases from 1.12 save
 and restore the global state around it, earlier ones leave it reseeded (the reference's later
@@ -33,12 +33,19 @@ import random
 import numpy as np
 
 
-def _fade(t):
-    # tools.fade: the package rejects t outside [-0.1, 1.1]; 1 - |d| with |d| <= 1 never is.
-    # Products (not **): the same IEEE operations for a float and for a float64 array
-    t3 = t * t * t
-    t4 = t3 * t
-    return 6 * (t4 * t) - 15 * t4 + 10 * t3
+def _fade(t: float) -> float:
+    # tools.fade: the package rejects t outside [-0.1, 1.1]; 1 - |d| with |d| <= 1 never is
+    return 6 * t ** 5 - 15 * t ** 4 + 10 * t ** 3
+
+
+_fade_py = np.frompyfunc(_fade, 1, 1)
+
+
+def _fade_array(t: np.ndarray) -> np.ndarray:
+    """_fade of every element through the scalar expression (Python float ``**``, not NumPy's
+    power, whose rounding may differ by an ulp), once per distinct value."""
+    u, inv = np.unique(t, return_inverse=True)
+    return _fade_py(u).astype(np.float64)[inv.reshape(t.shape)]
 
 
 def _hasher(k: int) -> int:
@@ -89,7 +96,7 @@ class _GradientNoise1D:
             ks = np.unique(k)
             g = np.array([self._grad(int(v)) for v in ks], np.float64)[np.searchsorted(ks, k)]
             d = xs - k
-            total = total + _fade(1 - np.abs(d)) * (g * d)
+            total = total + _fade_array(1 - np.abs(d)) * (g * d)
         return total
 
 

@@ -5,8 +5,9 @@ signal_calculator.py:24-31,100-115) sums octaves of the third-party ``perlin_noi
 (``perlin_noise==1.*``, server/requirements.txt:11), which is absent here and has no reference
 fixture.  This is the package's published 1-D algorithm (PerlinNoise.noise with its fade, hasher
 and per-lattice-point seeded ``random.uniform(-1, 1)`` gradient), written independently of
-``mdr_amd/perlin.py`` and in the package's own operation forms (``t ** 5``), so a test comparing the
-two checks the product's tabulated signal to the rounding of the power (an ulp), not bit for bit.
+``mdr_amd/perlin.py`` and in the package's own operation forms (``t ** 5``, Python float pow);
+the product evaluates the same expressions, so the two agree bit for bit
+(tests/test_host_logic.py::test_perlin_array_equals_oracle).
 Used by the oracle (oracle/env_np.py) when ``signal_properties.mode == "perlin"``.
 """
 from __future__ import annotations

@@ -76,3 +76,32 @@ def from_epoch(x: float) -> dt.datetime:
 
 TRAJ_NAMES = ("c1_sin_dbbc", "c1_flat_random", "fixed_steps_bbc", "n400_random_common",
               "n64_mixture_2d", "n30_maxerr_groups_hvacmsg", "interp_sin_random", "interp_flat_dbbc_nosolar")
+
+
+def calibrated_actor(n_feat: int, obs_absmax, seed: int = 1, gain: float = 3.0, layers=(100, 100)):
+    """The reference Actor (``make_actor``, torch seed ``seed``) with its first layer's columns
+    divided by max(1, |feature|max) (``obs_absmax``: float [n_feat]) and the output layer scaled by
+    ``gain``: the observation's normalisation folded into the weights, so that at any cluster size
+    (the cluster-power feature is ~0.4 N, norm.py:145) the policy stays away from saturation and a
+    probability check compares real numbers, not 1.0 with 1.0."""
+    import torch
+
+    from mdr_amd.actor import make_actor
+
+    a = make_actor(n_feat, 2, list(layers), seed=seed)
+    s = torch.as_tensor(np.maximum(1.0, np.asarray(obs_absmax, np.float64)), dtype=torch.float32)
+    with torch.no_grad():
+        a.fc[0].weight.div_(s[None, :])
+        a.fc[-1].weight.mul_(gain)
+        a.fc[-1].bias.mul_(gain)
+    return a
+
+
+def assert_not_saturated(probs, actions=None, lo: float = 0.05, hi: float = 0.95, frac: float = 0.5):
+    """At least ``frac`` of the sampled probabilities lie in (lo, hi), and both actions occur."""
+    p = np.asarray(probs, np.float64).ravel()
+    inside = float(np.mean((p > lo) & (p < hi)))
+    assert inside >= frac, f"only {inside:.3f} of the probabilities are in ({lo}, {hi})"
+    if actions is not None:
+        a = np.asarray(actions).ravel()
+        assert a.min() == 0 and a.max() == 1, "both actions must occur"

@@ -182,7 +182,9 @@ def test_actor_layer1_ksteps(torch_gpu, layout, precision):
         env.step_tensor(torch.from_numpy(rs.randint(0, 2, n).astype(np.uint8)).to("cuda"))
     F = env.obs_spec().n_feat
     assert F == {"ks1_padded": 18, "ks1_4": 88}[layout]
-    actor = scaled_actor(torch, F, 2.0, seed=5)
+    # (the obs normalisation folded into layer 1: probabilities away from saturation, so the
+    # check compares real numbers — r03's scaled actor saturated at 88 features)
+    actor = gu.calibrated_actor(F, env.obs_tensor().abs().amax(0).double().cpu().numpy(), seed=5).to("cuda")
     probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
     obs = torch.empty((n, F), dtype=torch.float32, device="cuda")
     if layout == "ks1_4" and precision == "fp32":
@@ -200,6 +202,7 @@ def test_actor_layer1_ksteps(torch_gpu, layout, precision):
     err = float(np.abs(probs.cpu().numpy() - tp).max())
     print(f"{layout} {precision}: max |p - p_torch| = {err:.3g}")
     assert err < (4e-6 if precision == "fp32" else PROB_ATOL[precision])
+    gu.assert_not_saturated(tp[:, 1])
 
 
 def test_actor_sampling_statistics(torch_gpu):

@@ -214,13 +214,18 @@ def test_c4_rank_rccl_window_rollout_vs_oracle(tmp_path, pipeline):
 
 
 # ------------------------------------------------------------------------------------- C5 @ 1M
-def test_c5_actor_rollout_1m(torch_gpu):
+@pytest.mark.parametrize("precision,atol", [("bf16x3", 1e-4), ("fp32", 4e-6)])
+def test_c5_actor_rollout_1m(torch_gpu, precision, atol):
     """C5's actor path at 1,048,576 houses: DeviceActor.rollout (actor -> step per tick, one graph)
     == the select_actions / step_tensor loop over 4 ticks (actions, probabilities, rewards, state);
     at every tick the loop's obs rows are within 2 float32 ulps of the oracle's norm_vector on
-    8,192 sampled houses (incl. both ring ends) and its probabilities within 1e-4 of torch fp32."""
+    8,192 sampled houses (incl. both ring ends) and its probabilities within ``atol`` of torch fp32
+    (bf16x3 1e-4, fp32 4e-6).  The actor is the seed-1 reference actor with the obs normalisation
+    folded into layer 1 (golden_util.calibrated_actor): at 1M houses the raw seed-1 policy
+    saturates (the cluster-power feature is ~0.4 N, norm.py:145), and a probability check would
+    compare 1.0 with 1.0; here most probabilities lie in (0.05, 0.95) and both actions occur."""
     torch = torch_gpu
-    from mdr_amd.actor import DeviceActor, make_actor
+    from mdr_amd.actor import DeviceActor
     from mdr_amd.environment import Environment
 
     n, T = 1 << 20, 4
@@ -228,8 +233,8 @@ def test_c5_actor_rollout_1m(torch_gpu):
     ea = Environment(props, rng=random.Random(BENCH_RNG), population="synthetic", seed=BENCH_SEED)
     eb = Environment(props, rng=random.Random(BENCH_RNG), population="synthetic", seed=BENCH_SEED)
     F = ea.obs_spec().n_feat
-    actor = make_actor(F, 2, [100, 100], seed=1).to("cuda")
-    da, db = DeviceActor(ea, actor), DeviceActor(eb, actor)
+    actor = gu.calibrated_actor(F, ea.obs_tensor().abs().amax(0).double().cpu().numpy(), seed=1).to("cuda")
+    da, db = DeviceActor(ea, actor, precision=precision), DeviceActor(eb, actor, precision=precision)
     rew = torch.empty((T, n), dtype=torch.float64, device="cuda")
     acts = torch.empty((T, n), dtype=torch.uint8, device="cuda")
     probs = torch.empty((T, n), dtype=torch.float32, device="cuda")
@@ -255,7 +260,9 @@ def test_c5_actor_rollout_1m(torch_gpu):
         np.testing.assert_array_max_ulp(got, ref.astype(np.float32), maxulp=2)
         with torch.no_grad():
             tp = actor(obs[torch.from_numpy(sample).to("cuda")]).cpu().numpy()
-        assert float(np.abs(pr.cpu().numpy()[sample] - tp).max()) < 1e-4, t
+        got_p = pr.cpu().numpy()[sample]
+        assert float(np.abs(got_p - tp).max()) < atol, (t, float(np.abs(got_p - tp).max()))
+        gu.assert_not_saturated(got_p[:, 1])
         r = eb.step_tensor(a)
         assert torch.equal(a, acts[t]), t
         assert torch.equal(p, probs[t]), t
@@ -263,6 +270,4 @@ def test_c5_actor_rollout_1m(torch_gpu):
     for key in ("t_air", "t_mass", "hvac"):
         assert torch.equal(getattr(ea.shard, key), getattr(eb.shard, key)), key
     assert ea._cluster_power() == eb._cluster_power()
-    # (at 1M houses the obs feature cluster_hvac_power / R is ~1e6 — the reference divides the
-    # cluster power by R only, norm.py:145 — so the seed-1 policy saturates: every house samples 1)
-    assert set(np.unique(acts.cpu().numpy())) <= {0, 1}
+    gu.assert_not_saturated(probs.cpu().numpy(), acts.cpu().numpy())

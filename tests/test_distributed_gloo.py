@@ -65,12 +65,14 @@ def _free_port():
 INTERP = {gu.BPP + "mode": "interpolation", gu.BPP + "interp_update_period": 8, gu.BPP + "interp_nb_agents": 30}
 
 
-@pytest.mark.parametrize("mode,n,extra", [("individual_L2", 101, {}), ("common_L2", 64, {}), ("mixture", 37, {}),
-                                          ("individual_L2", 101, INTERP)])
-def test_sharded_env_equals_oracle(tmp_path, mode, n, extra):
-    """Sharded orchestration (2 ranks, gloo) == the oracle; the interpolation case draws its
-    sampled houses on every rank and sums the per-rank sample values (base power every 2 ticks)."""
-    world, T, seed = 2, 12, 21
+@pytest.mark.parametrize("mode,n,extra,world", [("individual_L2", 101, {}, 2), ("common_L2", 64, {}, 2),
+                                                ("mixture", 37, {}, 2), ("individual_L2", 101, INTERP, 2),
+                                                ("individual_L2", 101, {}, 3), ("mixture", 37, {}, 3)])
+def test_sharded_env_equals_oracle(tmp_path, mode, n, extra, world):
+    """Sharded orchestration (2 or 3 ranks, gloo) == the oracle; the interpolation case draws its
+    sampled houses on every rank and sums the per-rank sample values (base power every 2 ticks).
+    World 3: uneven shards, and the previous and next rank on the ring are different processes."""
+    T, seed = 12, 21
     overrides = {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals",
                  "reward_prop.penalty_props.mode": mode, "reward_prop.penalty_props.alpha_common_max": 0.5,
                  "cluster_prop.house_prop.deadband": 0.3, **extra}
@@ -122,13 +124,13 @@ def _greedy_worker(rank, world, port, overrides, seed, T, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n", [75, 3001])
-def test_sharded_greedy_equals_oracle(tmp_path, n):
+@pytest.mark.parametrize("n,world", [(75, 2), (3001, 2), (3001, 3)])
+def test_sharded_greedy_equals_oracle(tmp_path, n, world):
     """Sharded GreedyMyopic — the histogram form: the shards' superbin / bin histograms and key
     range allreduced, the candidate windows all-gathered, the same window decision on every rank,
     each keeps its slice (the all-gather form decides what the window cannot) — == the
     single-process oracle's greedy + step."""
-    world, T, seed = 2, 6, 9
+    T, seed = 6, 9
     overrides = {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals"}
     mp.start_processes(_greedy_worker, args=(world, _free_port(), overrides, seed, T, str(tmp_path)),
                        nprocs=world, join=True, start_method="spawn")
@@ -145,3 +147,56 @@ def test_sharded_greedy_equals_oracle(tmp_path, n):
         o, _ = ora.step(ref)
         np.testing.assert_array_equal(np.concatenate([p["T"][t] for p in parts]), o["T"])
     assert all(int(p["fallbacks"]) == 0 for p in parts), [int(p["fallbacks"]) for p in parts]  # the window decided
+
+
+def _halo_worker(rank, world, port, n, k, m, out_dir):
+    import torch
+    import torch.distributed as dist
+
+    sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "marl-demandresponse_amd"), os.path.dirname(HERE)]
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    from types import SimpleNamespace
+
+    from mdr_amd.distributed import TorchComm
+    from mdr_amd.environment import shard_range
+
+    lo_h, hi_h = k // 2, (k + 1) // 2
+    off, nl = shard_range(n, rank, world)
+
+    class FakeShard:  # halo_pack's row layout (mdr.h): [first hi houses | last lo houses], row = gid * m + col
+        device = torch.device("cpu")
+        lib = SimpleNamespace(mdr_msg_width=lambda spec: m)
+
+        def __init__(self):
+            self.n = nl
+
+        def halo_pack(self, spec, out):
+            ids = list(range(off, off + hi_h)) + list(range(off + nl - lo_h, off + nl))
+            out.copy_(torch.tensor([[g * m + c for c in range(m)] for g in ids], dtype=torch.float32))
+
+    from mdr_amd import _lib as L
+
+    spec = L.mdr_obs_spec()
+    spec.n_comm = k
+    halo = TorchComm().ring_halo(FakeShard(), spec)
+    np.save(os.path.join(out_dir, f"halo{rank}.npy"), halo.numpy())
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n", [(2, 41), (3, 41), (4, 64)])
+def test_torchcomm_p2p_ring_halo(tmp_path, world, n):
+    """TorchComm.ring_halo's point-to-point pairing (the library's RCCL send/recv order): rank r
+    receives rank r-1's last 5 houses and rank r+1's first 5, in global ring order, for distinct
+    left and right peers (world 3, 4) and for r-1 == r+1 (world 2)."""
+    from mdr_amd.environment import shard_range
+
+    k, m = 10, 3
+    mp.start_processes(_halo_worker, args=(world, _free_port(), n, k, m, str(tmp_path)), nprocs=world, join=True,
+                       start_method="spawn")
+    for r in range(world):
+        off, nl = shard_range(n, r, world)
+        want = [(off - 5 + j) % n for j in range(5)] + [(off + nl + j) % n for j in range(5)]
+        got = np.load(tmp_path / f"halo{r}.npy")
+        np.testing.assert_array_equal(got, np.array([[g * m + c for c in range(m)] for g in want], np.float32))

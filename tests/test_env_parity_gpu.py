@@ -394,6 +394,38 @@ def test_greedy_one_million_vs_oracle(torch_gpu):
         assert env.cluster.current_power_consumption == o["P"]
 
 
+def test_greedy_four_million_vs_oracle(torch_gpu):
+    """4,194,304 houses: k_gq_compact runs 1,024 blocks of 1,024 threads, more than the chip holds
+    at once, so later blocks start after block 0 has published the window (r03's race: block 0
+    overwrote the crossing base those blocks still read, and they cut a different window).  The
+    device greedy + step == the oracle's over 3 ticks, every call decided by the window (no exact
+    fallback)."""
+    from mdr_amd.environment import Environment
+
+    n = 1 << 22
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env = Environment(props, rng=random.Random(23), population="synthetic", seed=23)
+    prm = env.shard.host_params()
+    caps = np.array(env._cap_values, np.float64)[prm["cap_idx"]]
+    pop = {"Ua": prm["ua"], "Ca": prm["ca"], "Cm": prm["cm"], "Hm": prm["hm"], "target": prm["target"], "cap": caps}
+    ora = O.OracleEnv(props, random.Random(23), population=pop)
+    hv = props.cluster_prop.house_prop.hvac_prop
+    for t in range(3):
+        a = env.greedy_actions().cpu().numpy().astype(bool)
+        ref = O.greedy(ora.T, ora.pop["target"], caps, hv.cop, ora.lock, float(ora.S))
+        np.testing.assert_array_equal(a, ref, err_msg=f"greedy t={t}")
+        r = env.step_tensor(torch_gpu.from_numpy(a.astype(np.uint8)).to("cuda")).cpu().numpy()
+        o, rr = ora.step(a)
+        np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12)
+        assert env.cluster.current_power_consumption == o["P"]
+    st = env.shard.host_state()
+    for k in ("on", "lock", "sso"):
+        np.testing.assert_array_equal(st[k], o[k], err_msg=k)
+    d = env.shard.greedy_state()
+    assert d["calls"] == 3 and d["fallbacks"] == 0, d
+
+
 @pytest.mark.parametrize("path", ["step", "rollout"])
 def test_perlin_trajectory_vs_oracle(torch_gpu, path):
     """Perlin signal mode (the MARLconfig default) on the GPU path, against the

@@ -166,6 +166,22 @@ def test_perlin_published_algorithm():
     assert pn.calculate_noise(x) == 1 * (0 + n[0] / 1 + n[1] / 2 + n[2] / 7)
 
 
+def test_perlin_array_equals_oracle():
+    """The tabulated (array) perlin noise == the scalar form == the oracle's independent scalar
+    restatement, bit for bit: all three evaluate the package's fade with Python float ``**``
+    (r03's product form could differ from the package's ``**`` by an ulp)."""
+    from mdr_amd.perlin import Perlin
+    from oracle.perlin_np import PerlinSignal
+
+    seed = 0.61803
+    pn, ora = Perlin(1, 5, 5, 300, seed), PerlinSignal(5, 5, 300, seed)
+    xs = np.concatenate([np.arange(0, 86400, 4.0), np.arange(0.5, 3000, 0.37)])
+    arr = pn.calculate_noise_array(xs)
+    scal = np.array([pn.calculate_noise(float(x)) for x in xs[::7]])
+    np.testing.assert_array_equal(arr[::7], scal)
+    np.testing.assert_array_equal(scal, [ora.calculate_noise(float(x)) for x in xs[::7]])
+
+
 def test_actor_init_matches_reference_mappo():
     """make_actor(seed=1) reproduces MAPPO's actor initialisation (mappo.py:41-50) and forward:
     the reference's own weights and probabilities in tests/golden/policy.npz."""
