@@ -47,7 +47,7 @@
 extern "C" {
 #endif
 
-#define MDR_ABI_VERSION 4
+#define MDR_ABI_VERSION 5
 #define MDR_MAX_CAP 64
 
 enum {
@@ -126,9 +126,9 @@ int mdr_abi_version(void);
 /* "MDR_SRC_HASH:<16 hex>": sha256 of the sources and build flags the library was built from
  * (build_ext.py src_hash); the Python binding refuses a library whose hash differs from its tree's. */
 const char* mdr_build_id(void);
-/* sizeof of the ABI structs, for binding checks: out[0..7] = mdr_config, mdr_soa, mdr_tick,
- * mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars, mdr_actor_spec, mdr_interp_spec; returns the number
- * written */
+/* sizeof of the ABI structs, for binding checks: out[0..8] = mdr_config, mdr_soa, mdr_tick,
+ * mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars, mdr_actor_spec, mdr_interp_spec, mdr_actor_net;
+ * returns the number written */
 int mdr_abi_sizes(int64_t* out, int n);
 const char* mdr_last_error(void);
 int mdr_create(mdr_ctx** out, const mdr_config* cfg);
@@ -155,15 +155,14 @@ int mdr_params_changed(mdr_ctx* ctx);
  *   MDR_OPT_GREEDY_SORT     1 = mdr_ctrl_greedy always runs the full-sort form
  *   MDR_OPT_FORCE_HALO      1 = mdr_actor_rollout_sharded exchanges the ring halo even at world 1
  *                           (send/recv to self: the one-GPU check of the multi-GPU exchange)
- *   MDR_OPT_ACTOR_PINGPONG  k_actor: 1 = the two waves of a SIMD alternate MFMA and VALU stages
- *                           between block barriers, 0 = free-running waves (default)
  *   MDR_OPT_WINDOW_THERMAL  k_step_window's per-tick thermal update: MDR_THERMAL_AFFINE (default)
  *                           = the reference's update as a per-house affine transition formed once
  *                           per window (4 FMAs per temperature per tick; ~1e-13 K per tick from the
  *                           reference order), MDR_THERMAL_EXACT = the reference's expression in its
  *                           operation order every tick (bit-identical to the one-tick kernels) */
 enum { MDR_OPT_STEP_TPW = 1, MDR_OPT_FASTDIV = 2, MDR_OPT_WINDOW_PIPELINE = 3, MDR_OPT_SHARDED_OVERLAP = 4,
-       MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7, MDR_OPT_ACTOR_PINGPONG = 8 };
+       MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7 };
+/* (8 was MDR_OPT_ACTOR_PINGPONG, a k_actor schedule measured slower and retired in r04: rejected) */
 enum { MDR_THERMAL_EXACT = 0, MDR_THERMAL_AFFINE = 1 };
 int mdr_set_option(mdr_ctx* ctx, int option, int64_t value);
 
@@ -376,8 +375,8 @@ enum { MDR_PREC_BF16 = 1,   /* bf16 products, fp32 accumulate (~4e-3 relative) *
                                fp32-faithful (~1e-7), the reference Actor's precision */ };
 
 typedef struct mdr_actor_spec {
-  int32_t n_in;      /* obs features (= mdr_obs_spec.n_feat), <= 128 */
-  int32_t h1, h2;    /* hidden widths (actor_layers), each <= 128 */
+  int32_t n_in;      /* obs features (= mdr_obs_spec.n_feat) */
+  int32_t h1, h2;    /* hidden widths (actor_layers) */
   int32_t n_act;     /* actions (num_action): 2, the on/off decision */
   int32_t precision; /* MDR_PREC_* */
 } mdr_actor_spec;
@@ -387,6 +386,21 @@ typedef struct mdr_actor_spec {
  * reference Actor's fc.0 / fc.1 / fc.2).  They are packed into MFMA fragment order on `stream`. */
 int mdr_actor_load(mdr_ctx* ctx, const mdr_actor_spec* spec, const float* w1, const float* b1,
                    const float* w2, const float* b2, const float* w3, const float* b3, void* stream);
+/* The general actor: any number of hidden layers (actor_layers, network.py:14-33) of any widths,
+ * over any obs row.  w[l] / b[l], l = 0 .. n_hidden: device fp32 nn.Linear weights [out][in] and
+ * biases of fc.l (the last one the output layer, [n_act][hidden[n_hidden-1]]).  A net of two
+ * hidden layers <= 128 wide whose obs row (<= 128 feature slots) and weight planes fit a CU's LDS
+ * runs the fused k_actor; any other runs the chain k_obs -> k_dense per hidden layer ->
+ * k_actor_head (the same precisions and sampling stream). */
+#define MDR_ACTOR_MAX_LAYERS 8
+typedef struct mdr_actor_net {
+  int32_t n_in, n_hidden, n_act, precision;
+  int32_t hidden[MDR_ACTOR_MAX_LAYERS];
+} mdr_actor_net;
+int mdr_actor_load_net(mdr_ctx* ctx, const mdr_actor_net* net, const float* const* w, const float* const* b,
+                       void* stream);
+/* 1 when the loaded actor runs the fused kernel for this obs layout, 0 when it runs the chain. */
+int mdr_actor_fused(mdr_ctx* ctx, const mdr_obs_spec* obs);
 /* One select_actions over the shard.  Outputs (device, any may be NULL): action u8 [n_local],
  * prob f32 [n_local] (probability of the sampled action, MAPPO.last_probs), probs f32
  * [n_local][n_act], obs_out f32 [n_local][n_in].  Sampling: Philox4x32-10(seed, global house id,

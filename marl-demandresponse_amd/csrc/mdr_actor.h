@@ -32,7 +32,6 @@ struct ActorDims {
   int lds_cf, lds_hist, lds_wave, wave_stride;  // block LDS: obs consts, count histogram, wave slices
   int w_zero, w_hw, w_cls;                       // offsets inside a wave slice (rows at 0)
   int lds_total;
-  int pp;  // ping-pong schedule (8 waves: MDR_OPT_ACTOR_PINGPONG)
 };
 
 struct ActorOut {
@@ -49,5 +48,12 @@ __global__ void k_actor_pack(ActorDims d, const float* w1, const float* b1, cons
 template <int PREC, bool PROF, int MB, int KS1>
 __global__ void k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
                         const unsigned char* wpack, ActorOut out, uint64_t tick, const TickArgs* tkp);
+
+// the general chain (mdr_actor.hip "chain"): one dense layer over fp32 rows, then the head
+template <int PREC>
+__global__ void k_dense(const float* X, int ldx, int K, int64_t n, const float* W, const float* b, int out, float* Y,
+                        int ldy, int relu_on);
+__global__ void k_actor_head(KParams p, const float* X, int ldx, int K, const float* W3, const float* b3,
+                             uint64_t tick0, const TickArgs* tkp, ActorOut out);
 
 }  // namespace mdr

@@ -198,8 +198,8 @@ __device__ __forceinline__ void split_operand(const float* v, bf16x8* s) {
 // (source rows, FSM words in a private LDS slice).  A tile runs as three stages — build (its LDS
 // rows from sources prefetched into registers), X (layers 1 and 2 on the MFMA pipe; the next tile's
 // sources go in flight first) and Y (output layer, softmax, sampling, stores on the VALU); the
-// waves run them free, or (d.pp) the two waves of each SIMD in ping-pong (the schedule at the end
-// of the kernel).  MB: row blocks of the hidden layers (compile-time LDS offsets); KS1: layer-1
+// waves run them free (a ping-pong schedule of the two waves of a SIMD, tried in r03, was slower:
+// DESIGN.md §3.4).  MB: row blocks of the hidden layers (compile-time LDS offsets); KS1: layer-1
 // k-steps (d.ks1, 2 to 4; no per-step guards in the MFMA loop).
 template <int PREC, bool PROF, int MB, int KS1>
 __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
@@ -538,42 +538,19 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     PSTAMP(5);
   };
 
-  // ---- ping-pong schedule.  The block's 8 waves are two halves (waves 0-3 and 4-7, one wave of
-  // each half per SIMD); between block barriers one half runs an X stage (MFMA pipe) while the
-  // other runs Y + build stages (VALU), so each SIMD's matrix pipe and VALU work at the same time
-  // instead of in turn.  Wave sequence: build(t0) | X(t0) | Y(t0) + build(t1) | X(t1) | ... |
-  // Y(t_last); the second half starts one interval later.  Every wave passes the same number of
-  // barriers (the block's largest tile count decides), and nothing in LDS is shared across waves
-  // (the barrier only paces them).  Fewer than 8 waves (LDS-limited layouts): no pairing, no barrier.
-  const bool pp = d.pp != 0 && nw == 8;
-  const int half = pp ? wv >> 2 : 0;
+  // ---- the wave's tiles: build(t0) | X(t0) | Y(t0) + build(t1) | X(t1) | ... | Y(t_last)
   const uint32_t tile0 = blockIdx.x * (uint32_t)nw + (uint32_t)wv;
-  const uint32_t first0 = blockIdx.x * (uint32_t)nw;  // wave 0's first tile: the block's largest count
   const int n_my = tile0 < ntile ? (int)((ntile - 1u - tile0) / stride + 1u) : 0;
-  const int n_max = first0 < ntile ? (int)((ntile - 1u - first0) / stride + 1u) : 0;
-  if (n_my > 0) src_kind = source_of(tile0, lane, src);
-  const int n_int = pp ? 2 * n_max + 2 : 2 * n_my + 1;
-  for (int I = 0; I < n_int; ++I) {
-    const int L = I - half;  // this wave's stage: 0 build(t0), 2j + 1 X(t_j), 2j + 2 Y(t_j) + build(t_j+1)
-    if (L >= 0 && L <= 2 * n_my) {
-      if (L == 0) {
-        if (n_my > 0) stage_build(tile0);
-      } else {
-        const int j = (L - 1) >> 1;
-        const uint32_t tj = tile0 + (uint32_t)j * stride;
-        if (L & 1) {
-          if (PROF && lane == 0) pacc[7] += 1;
-          stage_x(tj, tj + stride);
-        } else {
-          stage_y(tj, (j & 1) == 0);
-          if (j + 1 < n_my) stage_build(tj + stride);
-        }
-      }
-    }
-    if (pp) {
-      __builtin_amdgcn_s_barrier();
-      PSTAMP(6);
-    }
+  if (n_my > 0) {
+    src_kind = source_of(tile0, lane, src);
+    stage_build(tile0);
+  }
+  for (int j = 0; j < n_my; ++j) {
+    const uint32_t tj = tile0 + (uint32_t)j * stride;
+    if (PROF && lane == 0) pacc[7] += 1;
+    stage_x(tj, tj + stride);
+    stage_y(tj, (j & 1) == 0);
+    if (j + 1 < n_my) stage_build(tj + stride);
   }
   if (PROF && lane == 0) {
     for (int k = 0; k < 8; ++k) out.prof[(blockIdx.x * nw + wv) * 8 + k] = pacc[k];
@@ -585,6 +562,119 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
   }
 #undef PSTAMP
 }
+
+// --------------------------------------------------------------------------------------- chain
+// The general actor (any number of hidden layers, any widths, any obs row; and the fp32 mode where
+// the fused kernel's three weight planes do not fit the LDS): the reference Actor.forward
+// (network.py:29-33) as a chain of launches over fp32 rows in HBM — the obs rows (k_obs), one
+// k_dense per hidden layer, then k_actor_head (output layer, softmax, sampling, ON counts).  The
+// same split-bf16 MFMA products per precision as k_actor, the same sampling stream.
+
+// Y[i][o] = act(b[o] + sum_k W[o][k] X[i][k]) for houses i < n and neurons o < out (row-major fp32,
+// leading dimensions ldx / ldy).  A block of 4 waves covers 64 houses x 64 neurons; wave w owns
+// neurons 16 w .. 16 w + 15 (the rows of one 16x16x32 MFMA) against four column blocks of 16
+// houses; k-steps of 32 with zero-filled edges.  The bias is the first MFMA's C operand.
+template <int PREC>
+__global__ void __launch_bounds__(256) k_dense(const float* __restrict__ X, int ldx, int K, int64_t n,
+                                               const float* __restrict__ W, const float* __restrict__ b, int out,
+                                               float* __restrict__ Y, int ldy, int relu_on) {
+  constexpr int NS = PREC == 6 ? 3 : PREC == 3 ? 2 : 1;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int c = lane & 15, g = lane >> 4;
+  const int64_t h0 = (int64_t)blockIdx.x * 64;
+  const int o0 = ((int)blockIdx.y * 4 + wv) * kActorRB;
+  if (o0 >= out) return;  // (wave-uniform)
+  const int orow = o0 + c;
+  f32x4 bias;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) bias[i] = o0 + 4 * g + i < out ? b[o0 + 4 * g + i] : 0.f;
+  f32x4 acc[4] = {bias, bias, bias, bias};
+  for (int k0 = 0; k0 < K; k0 += 32) {
+    float av[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int k = k0 + 8 * g + j;
+      av[j] = orow < out && k < K ? W[(int64_t)orow * K + k] : 0.f;
+    }
+    bf16x8 as[NS];
+    split_operand<PREC>(av, as);
+#pragma unroll
+    for (int cb = 0; cb < 4; ++cb) {
+      const int64_t hi = h0 + 16 * cb + c;
+      float xv[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        const int k = k0 + 8 * g + j;
+        xv[j] = hi < n && k < K ? X[hi * ldx + k] : 0.f;
+      }
+      bf16x8 xs[NS];
+      split_operand<PREC>(xv, xs);
+      acc[cb] = mfma_split<PREC>(as, xs, acc[cb]);
+    }
+  }
+#pragma unroll
+  for (int cb = 0; cb < 4; ++cb) {
+    const int64_t hi = h0 + 16 * cb + c;
+    if (hi >= n) continue;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int o = o0 + 4 * g + i;
+      if (o < out) Y[hi * ldy + o] = relu_on ? relu(acc[cb][i]) : acc[cb][i];
+    }
+  }
+}
+
+// The output layer (fp32 FMAs over the last hidden layer, W3 [2][K] row-major, b3 [2]), softmax and
+// Categorical sampling of k_actor's stage Y — the same uniform philox(seed, goff + i, tick) per
+// house — the stores, and the ON counts of the new actions; one thread per house.
+__global__ void __launch_bounds__(256) k_actor_head(KParams p, const float* __restrict__ X, int ldx, int K,
+                                                    const float* __restrict__ W3, const float* __restrict__ b3,
+                                                    uint64_t tick0, const TickArgs* tkp, ActorOut out) {
+  __shared__ unsigned s_hist[MDR_MAX_CAP];
+  if (threadIdx.x < MDR_MAX_CAP) s_hist[threadIdx.x] = 0u;
+  __syncthreads();
+  const uint64_t tick = tkp ? tkp->tick : tick0;
+  const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool valid = i < p.n;
+  float z0 = 0.f, z1 = 0.f;
+  if (valid) {
+    const float* x = X + i * ldx;
+    for (int k = 0; k < K; ++k) {
+      const float v = x[k];
+      z0 = fmaf(W3[k], v, z0);
+      z1 = fmaf(W3[K + k], v, z1);
+    }
+  }
+  z0 += b3[0];
+  z1 += b3[1];
+  const float zmax = fmaxf(z0, z1);
+  const float e0 = __expf(z0 - zmax), e1 = __expf(z1 - zmax);
+  const float rse = 1.f / (e0 + e1);
+  const float p0 = e0 * rse, p1 = e1 * rse;
+  const float u = philox_u01f(p.seed, (uint64_t)p.goff + (uint64_t)(valid ? i : 0), tick);
+  const int act = u < p0 ? 0 : 1;
+  if (valid) {
+    if (out.probs) *reinterpret_cast<float2*>(out.probs + 2 * (size_t)i) = make_float2(p0, p1);
+    if (out.action) out.action[i] = (uint8_t)act;
+    if (out.prob) out.prob[i] = act ? p1 : p0;
+  }
+  if (out.count_next) {
+    const bool on1 = valid && hv_on(hvac_fsm(p.hvac[i], act != 0, p.dt, p.L));
+    const int cls = valid ? p.cap_idx[i] : 0;
+    for (int k = 0; k < p.n_cap; ++k) {
+      const unsigned long long m = __ballot(on1 && cls == k);
+      if ((threadIdx.x & 63) == 0 && m) atomicAdd(&s_hist[k], (unsigned)__popcll(m));
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < p.n_cap && s_hist[threadIdx.x])
+      atomicAdd(&out.count_next[(blockIdx.x % kCountShards) * p.n_cap + threadIdx.x],
+                (unsigned long long)s_hist[threadIdx.x]);
+  }
+}
+
+template __global__ void k_dense<1>(const float*, int, int, int64_t, const float*, const float*, int, float*, int, int);
+template __global__ void k_dense<3>(const float*, int, int, int64_t, const float*, const float*, int, float*, int, int);
+template __global__ void k_dense<6>(const float*, int, int, int64_t, const float*, const float*, int, float*, int, int);
 
 #define MDR_INST_ACTOR(P, F, MB, KS)                                                                \
   template __global__ void k_actor<P, F, MB, KS>(KParams, ObsArgs, ActorDims, const double*,              \

@@ -88,8 +88,7 @@ struct mdr_ctx {
   bool win_pipe = true;                  // MDR_OPT_WINDOW_PIPELINE: sharded count-ahead window pipeline
   bool tick_overlap = true;              // MDR_OPT_SHARDED_OVERLAP: per-tick sharded two-stream pipeline
   bool greedy_sort = false;              // MDR_OPT_GREEDY_SORT: the full-sort greedy form only
-  bool force_halo = false;
-  bool actor_pp = false;                 // MDR_OPT_ACTOR_PINGPONG: k_actor's paired-wave schedule               // MDR_OPT_FORCE_HALO: sharded actor halo exchange at world 1
+  bool force_halo = false;               // MDR_OPT_FORCE_HALO: sharded actor halo exchange at world 1
   int thermal = MDR_THERMAL_AFFINE;      // MDR_OPT_WINDOW_THERMAL: k_step_window's per-tick update
   int win = kWindowMax;                  // ticks per k_step_window launch (0: one-tick path)
   unsigned long long* d_wslab = nullptr; // 3 window count slots (mdr_kernels.hip K1W: slab | red | rec)
@@ -155,8 +154,11 @@ struct mdr_ctx {
   float* d_actor_raw = nullptr;  // the loaded fp32 weights (w1 b1 w2 b2 w3 b3), packed per obs layout
   size_t actor_raw_cap = 0;
   std::vector<int> actor_key;    // the slot layout + precision d_actor is packed for (empty: stale)
-  mdr_actor_spec actor{};
+  mdr_actor_spec actor{};                // (the two-hidden-layer view the fused kernel packs from)
+  mdr_actor_net net{};                   // the loaded actor: layers, widths, precision
   bool actor_ready = false;
+  float* d_chain = nullptr;              // the chain's rows: obs [n][F] | hidden ping-pong 2 x [n][wmax4]
+  size_t chain_cap = 0;
   int n_cu = 0;
   double* d_obs_sc = nullptr;  // [ticks_cap][4]
   uint8_t* d_act = nullptr;    // [n_local] actor actions when the caller keeps none
@@ -368,12 +370,12 @@ const char* mdr_build_id(void) { return "MDR_SRC_HASH:" MDR_SRC_HASH; }
 int mdr_abi_version(void) { return MDR_ABI_VERSION; }
 
 int mdr_abi_sizes(int64_t* out, int n) {
-  const int64_t v[8] = {(int64_t)sizeof(mdr_config), (int64_t)sizeof(mdr_soa), (int64_t)sizeof(mdr_tick),
+  const int64_t v[9] = {(int64_t)sizeof(mdr_config), (int64_t)sizeof(mdr_soa), (int64_t)sizeof(mdr_tick),
                         (int64_t)sizeof(mdr_pop_spec), (int64_t)sizeof(mdr_obs_spec),
                         (int64_t)sizeof(mdr_obs_scalars), (int64_t)sizeof(mdr_actor_spec),
-                        (int64_t)sizeof(mdr_interp_spec)};
+                        (int64_t)sizeof(mdr_interp_spec), (int64_t)sizeof(mdr_actor_net)};
   int k = 0;
-  for (; out && k < n && k < 8; ++k) out[k] = v[k];
+  for (; out && k < n && k < 9; ++k) out[k] = v[k];
   return k;
 }
 
@@ -485,6 +487,7 @@ int mdr_destroy(mdr_ctx* c) {
   destroy_graphs(c);
   hipFree(c->d_actor);
   hipFree(c->d_actor_raw);
+  hipFree(c->d_chain);
   hipFree(c->d_interp);
   hipFree(c->d_act);
   hipFree(c->d_halo);
@@ -534,7 +537,6 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_SHARDED_OVERLAP: c->tick_overlap = value != 0; break;
     case MDR_OPT_GREEDY_SORT: c->greedy_sort = value != 0; break;
     case MDR_OPT_FORCE_HALO: c->force_halo = value != 0; break;
-    case MDR_OPT_ACTOR_PINGPONG: c->actor_pp = value != 0; break;
     case MDR_OPT_WINDOW_THERMAL:
       if (value != MDR_THERMAL_EXACT && value != MDR_THERMAL_AFFINE)
         return fail(MDR_EARG, "mdr_set_option: WINDOW_THERMAL must be MDR_THERMAL_EXACT or _AFFINE");
@@ -714,11 +716,12 @@ static bool win_simple(const mdr_ctx* c) {
          c->kp.alpha_sig >= 0.0 && !std::signbit(c->kp.alpha_sig) && c->kp.norm_sig > 0.0;
 }
 
-// (the lookahead's FSM runs on unsaturated seconds-since-off: L <= 2^30 - 1 and 33 ticks of dt
-// from a saturated value stay below 2^32 — mdr_kernels.hip win_run)
+// (the lookahead's FSM runs on unsaturated seconds-since-off in a signed offset form: L <= 2^30 - 1,
+// dt <= 2^25, so a saturated value plus 33 ticks of dt and L - 32 dt stay inside int32 —
+// mdr_kernels.hip win_run_t)
 static bool window_ok(const mdr_ctx* c, int mode) {
   return c->win > 0 && c->d_wslab && c->kp.n_cap <= kWindowCap && c->kp.penalty_mode == MDR_PEN_INDIVIDUAL_L2 &&
-         c->kp.L < (1 << 30) && c->kp.dt <= (1 << 26) &&
+         c->kp.L < (1 << 30) && c->kp.dt >= 0 && c->kp.dt <= (1 << 25) &&
          (mode == MDR_ACT_RANDOM || mode == MDR_ACT_ALWAYS_ON || mode == MDR_ACT_BUFFER);
 }
 
@@ -1786,10 +1789,56 @@ int actor_plan(const mdr_ctx* c, const mdr_obs_spec* sp, ActorDims* d, int* nw) 
   return fail(MDR_EARG, "mdr_actor: weights + obs rows exceed the 160 KiB LDS of a CU");
 }
 
+// the loaded net takes the fused k_actor for this obs layout (two hidden layers <= 128 wide, the obs
+// row within 128 slots, weights + rows within the LDS); otherwise the chain runs it
+bool actor_fused_ok(const mdr_ctx* c, const mdr_obs_spec* sp) {
+  const mdr_actor_net& a = c->net;
+  if (a.n_hidden != 2 || a.hidden[0] > kActorRows || a.hidden[1] > kActorRows || a.n_in > kActorMaxIn) return false;
+  ActorDims d;
+  int nw = 0;
+  const std::string keep = g_err;
+  const bool ok = actor_plan(c, sp, &d, &nw) == MDR_OK;
+  g_err = keep;
+  return ok;
+}
+
+// offsets of layer l's weights in the loaded fp32 image [w0 b0 w1 b1 ... wL bL]
+size_t net_w_off(const mdr_actor_net& a, int l) {
+  size_t o = 0;
+  int in = a.n_in;
+  for (int k = 0; k < l; ++k) {
+    const int out = k < a.n_hidden ? a.hidden[k] : a.n_act;
+    o += (size_t)out * in + out;
+    in = out;
+  }
+  return o;
+}
+int net_width(const mdr_actor_net& a) {
+  int w = 0;
+  for (int l = 0; l < a.n_hidden; ++l) w = std::max(w, a.hidden[l]);
+  return w;
+}
+
+// the chain's row buffers for n houses and an F-feature obs row (allocated before any capture)
+int chain_ensure(mdr_ctx* c, int F, hipStream_t st) {
+  const size_t w4 = (size_t)((net_width(c->net) + 3) & ~3);
+  const size_t need = ((size_t)F + 2 * w4) * (size_t)c->kp.n * sizeof(float);
+  if (need <= c->chain_cap) return MDR_OK;
+  HIP_TRY(hipStreamSynchronize(st));
+  hipFree(c->d_chain);
+  c->d_chain = nullptr;
+  HIP_TRY(hipMalloc(&c->d_chain, need));
+  c->chain_cap = need;
+  for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
+  c->actor_graphs.clear();
+  return MDR_OK;
+}
+
 // The packed weight image for this obs layout (k_actor_pack from the loaded fp32 weights): packed
 // again only when the slot layout or the precision changes.  Called by every actor entry point
-// before it launches or captures anything.
+// before it launches or captures anything.  (The chain needs no packing: its row buffers.)
 int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
+  if (!actor_fused_ok(c, sp)) return chain_ensure(c, sp->n_feat, st);
   ActorDims d;
   int nw = 0;
   if (int rc = actor_plan(c, sp, &d, &nw)) return rc;
@@ -1825,12 +1874,54 @@ int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
       (const void*)k_actor<6, false, MB, KS>, (const void*)k_actor<1, true, MB, KS>,                      \
       (const void*)k_actor<3, true, MB, KS>, (const void*)k_actor<6, true, MB, KS>
 
+// The general actor as a chain of launches (mdr_actor.hip "chain"): obs rows (into out.obs when the
+// caller keeps them), one k_dense per hidden layer (ping-pong row buffers), k_actor_head.
+int launch_actor_chain(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const double* p_dev, uint64_t tick,
+                       const TickArgs* tkp, const ActorOut& out, hipStream_t st) {
+  if (out.prof) return fail(MDR_EARG, "mdr_actor_profile: the chained actor has no phase profile");
+  const mdr_actor_net& a = c->net;
+  const int64_t n = c->kp.n;
+  const int F = sp->n_feat;
+  const int w4 = (net_width(a) + 3) & ~3;
+  float* x0 = out.obs ? out.obs : c->d_chain;
+  float* hb[2] = {c->d_chain + (size_t)F * n, c->d_chain + ((size_t)F + w4) * n};
+  const int lo = sp->n_comm / 2, hi = (sp->n_comm + 1) / 2;
+  const size_t tile = ((size_t)kObsBlock * F + 3) & ~(size_t)3;
+  const size_t bytes = (tile + (size_t)(lo + kObsBlock + hi) * o.msg_w) * sizeof(float);
+  if (bytes > 160 * 1024) return fail(MDR_EARG, "mdr_actor: obs row too wide for one LDS tile");
+  hipLaunchKernelGGL(k_obs, dim3(blocks(n, kObsBlock)), dim3(kObsBlock), bytes, st, c->kp, o, p_dev, x0);
+  LAUNCH_CHECK("k_obs (actor chain)");
+  const float* x = x0;
+  int ld = F, K = F;
+  const float* raw = c->d_actor_raw;
+  const int prec = a.precision;
+  for (int l = 0; l < a.n_hidden; ++l) {
+    const int out_w = a.hidden[l];
+    const float* W = raw + net_w_off(a, l);
+    const float* b = W + (size_t)out_w * K;
+    float* y = hb[l & 1];
+    const dim3 grid(blocks(n, 64), blocks(out_w, 64));
+    if (prec == MDR_PREC_BF16) hipLaunchKernelGGL(k_dense<1>, grid, dim3(256), 0, st, x, ld, K, n, W, b, out_w, y, w4, 1);
+    else if (prec == MDR_PREC_FP32) hipLaunchKernelGGL(k_dense<6>, grid, dim3(256), 0, st, x, ld, K, n, W, b, out_w, y, w4, 1);
+    else hipLaunchKernelGGL(k_dense<3>, grid, dim3(256), 0, st, x, ld, K, n, W, b, out_w, y, w4, 1);
+    LAUNCH_CHECK("k_dense");
+    x = y;
+    ld = w4;
+    K = out_w;
+  }
+  const float* W3 = raw + net_w_off(a, a.n_hidden);
+  hipLaunchKernelGGL(k_actor_head, dim3(blocks(n, 256)), dim3(256), 0, st, c->kp, x, ld, K, W3, W3 + (size_t)kActorNA * K,
+                     tick, tkp, out);
+  LAUNCH_CHECK("k_actor_head");
+  return MDR_OK;
+}
+
 int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const double* p_dev, uint64_t tick,
                  const TickArgs* tkp, const ActorOut& out, hipStream_t st) {
+  if (!actor_fused_ok(c, sp)) return launch_actor_chain(c, sp, o, p_dev, tick, tkp, out, st);
   ActorDims d;
   int nw = 0;
   if (int rc = actor_plan(c, sp, &d, &nw)) return rc;
-  d.pp = c->actor_pp && nw == 8;
   const int64_t ntile = (c->kp.n + 32 * nw - 1) / (32 * nw);  // blocks with at least one tile per wave
   const unsigned grid = (unsigned)std::min<int64_t>(ntile, (int64_t)c->n_cu);
   static bool lds_attr = false;  // > 64 KiB of dynamic LDS must be opted into per kernel
@@ -1881,18 +1972,27 @@ int check_actor_obs(mdr_ctx* c, const mdr_obs_spec* sp, const char* who, hipStre
 
 extern "C" {
 
-int mdr_actor_load(mdr_ctx* c, const mdr_actor_spec* a, const float* w1, const float* b1, const float* w2,
-                   const float* b2, const float* w3, const float* b3, void* stream) {
-  if (!c || !a || !w1 || !b1 || !w2 || !b2 || !w3 || !b3) return fail(MDR_EARG, "mdr_actor_load: null argument");
-  if (a->n_in < 1 || a->n_in > kActorMaxIn || a->h1 < 1 || a->h1 > kActorRows || a->h2 < 1 ||
-      a->h2 > kActorRows || a->n_act != kActorNA)
-    return fail(MDR_EARG, "mdr_actor_load: shape outside n_in <= 128, hidden <= 128, n_act == 2");
+int mdr_actor_load_net(mdr_ctx* c, const mdr_actor_net* a, const float* const* w, const float* const* b,
+                       void* stream) {
+  if (!c || !a || !w || !b) return fail(MDR_EARG, "mdr_actor_load_net: null argument");
+  if (a->n_in < 1 || a->n_in > 4096 || a->n_hidden < 1 || a->n_hidden > MDR_ACTOR_MAX_LAYERS || a->n_act != kActorNA)
+    return fail(MDR_EARG, "mdr_actor_load_net: shape outside 1 <= n_in <= 4096, 1..8 hidden layers, n_act == 2");
+  for (int l = 0; l < a->n_hidden; ++l)
+    if (a->hidden[l] < 1 || a->hidden[l] > 4096) return fail(MDR_EARG, "mdr_actor_load_net: hidden width outside 1..4096");
   if (a->precision != MDR_PREC_BF16 && a->precision != MDR_PREC_BF16X3 && a->precision != MDR_PREC_FP32)
-    return fail(MDR_EARG, "mdr_actor_load: bad precision");
-  // the fp32 weights, kept on device: the packed image depends on the obs layout, so it is made
-  // by the first actor call of each layout (actor_ensure_packed)
-  const size_t nraw = (size_t)a->h1 * a->n_in + a->h1 + (size_t)a->h2 * a->h1 + a->h2 + (size_t)kActorNA * a->h2 +
-                      kActorNA;
+    return fail(MDR_EARG, "mdr_actor_load_net: bad precision");
+  for (int l = 0; l <= a->n_hidden; ++l)
+    if (!w[l] || !b[l]) return fail(MDR_EARG, "mdr_actor_load_net: null layer");
+  // the fp32 weights, kept on device: the fused kernel's packed image depends on the obs layout, so
+  // it is made by the first actor call of each layout (actor_ensure_packed)
+  const size_t nraw = net_w_off(*a, a->n_hidden + 1);
+  // captured actor graphs hold the chain's weight pointers and the fused / chain choice: they stay
+  // valid while the buffer and the net's shape do (a PPO update reloads weights of the same shape)
+  const bool same = c->actor_ready && memcmp(&c->net, a, sizeof(mdr_actor_net)) == 0;
+  if (!same || nraw * sizeof(float) > c->actor_raw_cap) {
+    for (auto& g : c->actor_graphs) hipGraphExecDestroy(g.second);
+    c->actor_graphs.clear();
+  }
   if (nraw * sizeof(float) > c->actor_raw_cap) {
     HIP_TRY(hipStreamSynchronize(S(stream)));
     hipFree(c->d_actor_raw);
@@ -1901,17 +2001,41 @@ int mdr_actor_load(mdr_ctx* c, const mdr_actor_spec* a, const float* w1, const f
     c->actor_raw_cap = nraw * sizeof(float);
   }
   float* r = c->d_actor_raw;
-  const std::pair<const float*, size_t> parts[6] = {{w1, (size_t)a->h1 * a->n_in}, {b1, (size_t)a->h1},
-                                                    {w2, (size_t)a->h2 * a->h1}, {b2, (size_t)a->h2},
-                                                    {w3, (size_t)kActorNA * a->h2}, {b3, (size_t)kActorNA}};
-  for (const auto& pt : parts) {
-    HIP_TRY(hipMemcpyAsync(r, pt.first, pt.second * sizeof(float), hipMemcpyDeviceToDevice, S(stream)));
-    r += pt.second;
+  int in = a->n_in;
+  for (int l = 0; l <= a->n_hidden; ++l) {
+    const int out = l < a->n_hidden ? a->hidden[l] : a->n_act;
+    HIP_TRY(hipMemcpyAsync(r, w[l], (size_t)out * in * sizeof(float), hipMemcpyDeviceToDevice, S(stream)));
+    r += (size_t)out * in;
+    HIP_TRY(hipMemcpyAsync(r, b[l], (size_t)out * sizeof(float), hipMemcpyDeviceToDevice, S(stream)));
+    r += out;
+    in = out;
   }
   c->actor_key.clear();
-  c->actor = *a;
+  c->net = *a;
+  c->actor = mdr_actor_spec{a->n_in, a->hidden[0], a->n_hidden > 1 ? a->hidden[1] : 0, a->n_act, a->precision};
   c->actor_ready = true;
   return MDR_OK;
+}
+
+int mdr_actor_load(mdr_ctx* c, const mdr_actor_spec* a, const float* w1, const float* b1, const float* w2,
+                   const float* b2, const float* w3, const float* b3, void* stream) {
+  if (!c || !a || !w1 || !b1 || !w2 || !b2 || !w3 || !b3) return fail(MDR_EARG, "mdr_actor_load: null argument");
+  mdr_actor_net net{};
+  net.n_in = a->n_in;
+  net.n_hidden = 2;
+  net.n_act = a->n_act;
+  net.precision = a->precision;
+  net.hidden[0] = a->h1;
+  net.hidden[1] = a->h2;
+  const float* w[3] = {w1, w2, w3};
+  const float* b[3] = {b1, b2, b3};
+  return mdr_actor_load_net(c, &net, w, b, stream);
+}
+
+int mdr_actor_fused(mdr_ctx* c, const mdr_obs_spec* sp) {
+  if (!c || !sp) return fail(MDR_EARG, "mdr_actor_fused: null argument");
+  if (!c->actor_ready) return fail(MDR_ESTATE, "mdr_actor_fused: no actor loaded");
+  return actor_fused_ok(c, sp) ? 1 : 0;
 }
 
 int mdr_actor_act(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars* sc, const double* p_dev,
@@ -1998,7 +2122,10 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
     return MDR_OK;
   };
   if (!action && !c->d_act) HIP_TRY(hipMalloc(&c->d_act, c->kp.n));  // context-owned action row
-  if (!use_graph) {
+  // the layer chain runs as direct launches: replays of its captured graph after the first gave
+  // wrong counts for the first two ticks on ROCm 7.2 (tools/chain_debug.py; direct launches and
+  // the fused kernel's graph are exact), so it is not captured
+  if (!use_graph || !actor_fused_ok(c, sp)) {
     const int rc = launches(st);
     c->counts_ready = false;
     return rc;

@@ -8,6 +8,8 @@
 namespace mdr {
 
 constexpr int kCountShards = 64;  // atomic shards for the per-class ON counts
+constexpr int kWinShards = 16;    // the shards a window count flush uses (the first 16 of kCountShards:
+                                  // 128 adds per counter at 2048 blocks, one quarter of the reads to sum)
 constexpr int kTicketGroups = 64; // grid_last_block: group counters (+ 1 top), 32 words apart
 constexpr int kTicketWords = 32 * (kTicketGroups + 1);
 constexpr int kSlabs = 4;         // count slabs: ring of 3 (step path) / 4 (overlapped pipeline)

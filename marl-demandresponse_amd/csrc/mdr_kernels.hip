@@ -873,65 +873,43 @@ __device__ bool grid_last_block(unsigned* __restrict__ tickets) {
 // cdna_hip_programming.md Guideline 16 / MI355X_MICROARCH.md Valid forms ("8-B agent atomics both
 // sides"): every block's shard adds (win_flush) are 8-B agent-scope atomics, drained by each wave
 // (vmcnt(0)) before the workgroup barrier and the block's agent-scope ticket add (grid_last_block);
-// the last block reads the shards only with 8-B agent-scope (sc1) loads.
+// the last block reads the shards only with 8-B agent-scope (sc1) loads.  Thread t takes shard
+// t % 16 of entries (tick, class) e = t / 16 + 16 k: every load issued first (one round trip), the
+// 16 shards of an entry summed across a 16-lane group (shuffles), the shards zeroed behind.
 __device__ void win_reduce_last(const KParams& p, unsigned long long* __restrict__ slot, int nt,
                                 unsigned* __restrict__ ticket) {
-  constexpr int NW = 4;                  // (blockDim 256)
-  constexpr int JW = kWinMax / NW;       // ticks per wave: j = wave + 4 k
-  constexpr int KR = 2;                  // ticks per transpose round (KR * kWinCap entries of 64 shards)
-  __shared__ unsigned s_t[NW][KR * kWinCap][kCountShards];  // a round's shard values, transposed for the sums
+  static_assert(kWinShards == 16, "one 16-lane group per entry");
+  constexpr int EPT = kWinMax * kWinCap * kWinShards / 256;  // loads per thread (blockDim 256)
   __shared__ unsigned long long s_red[kWinMax * kWinCap];
   if (!grid_last_block(ticket)) return;  // (block-uniform)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only: the loads below are sc1)
-  const int ncap = p.n_cap, q = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  // lane q reads shard q of the wave's (tick, class) entries: the low words of the 8-B shard counters
-  // (a shard's count < 2^32: the clusters have < 2^29 houses), every load issued before the first use
-  unsigned v[JW][kWinCap];
+  const int ncap = p.n_cap, E = nt * ncap, sh = threadIdx.x & 15;
+  unsigned long long v[EPT];
 #pragma unroll
-  for (int k = 0; k < JW; ++k)
-#pragma unroll
-    for (int c = 0; c < kWinCap; ++c) {
-      const int j = wv + NW * k;
-      v[k][c] = 0u;
-      if (j < nt && c < ncap)
-        v[k][c] = __hip_atomic_load(reinterpret_cast<unsigned*>(&slot[((size_t)j * kCountShards + q) * ncap + c]),
-                                    __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < EPT; ++k) {
+    const int e = (int)(threadIdx.x >> 4) + 16 * k;
+    v[k] = 0ull;
+    if (e < E) {
+      const int j = e / ncap, c = e - j * ncap;
+      v[k] = __hip_atomic_load(&slot[((size_t)j * kCountShards + sh) * ncap + c], __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
 #pragma unroll
-  for (int k = 0; k < JW; ++k)
-#pragma unroll
-    for (int c = 0; c < kWinCap; ++c) {
-      const int j = wv + NW * k;
-      if (j < nt && c < ncap)  // (the slot's next count adds into zeros)
-        __hip_atomic_store(&slot[((size_t)j * kCountShards + q) * ncap + c], 0ull, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < EPT; ++k) {
+    const int e = (int)(threadIdx.x >> 4) + 16 * k;
+    if (e < E) {  // (the slot's next count adds into zeros)
+      const int j = e / ncap, c = e - j * ncap;
+      __hip_atomic_store(&slot[((size_t)j * kCountShards + sh) * ncap + c], 0ull, __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
     }
-  // rounds of KR ticks: the wave writes its lanes' values transposed, lane e sums entry e's 64 shards
+    unsigned long long x = v[k];
 #pragma unroll
-  for (int r = 0; r < JW / KR; ++r) {
-    if (wv + NW * KR * r >= nt) break;  // (wave-uniform)
-#pragma unroll
-    for (int kk = 0; kk < KR; ++kk)
-#pragma unroll
-      for (int c = 0; c < kWinCap; ++c) s_t[wv][kk * kWinCap + c][q] = v[KR * r + kk][c];
-    wave_lds_sync();
-    if (q < KR * kWinCap) {
-      const int c = q % kWinCap, j = wv + NW * (KR * r + q / kWinCap);
-      if (j < nt && c < ncap) {
-        const uint4* rd = reinterpret_cast<const uint4*>(s_t[wv][q]);
-        unsigned long long x = 0ull;
-#pragma unroll
-        for (int i = 0; i < kCountShards / 4; ++i) {
-          const uint4 u = rd[i];
-          x += (unsigned long long)u.x + u.y + u.z + u.w;
-        }
-        s_red[j * ncap + c] = x;
-      }
-    }
-    wave_lds_sync();
+    for (int off = 8; off > 0; off >>= 1) x += __shfl_xor(x, off);
+    if (sh == 0 && e < E) s_red[e] = x;
   }
   __syncthreads();
-  for (int e = threadIdx.x; e < nt * ncap; e += blockDim.x) win_red(slot, ncap)[e] = s_red[e];
+  for (int e = threadIdx.x; e < E; e += blockDim.x) win_red(slot, ncap)[e] = s_red[e];
   if ((int)threadIdx.x < nt) {
     double p_on[kWinCap];
 #pragma unroll
@@ -980,14 +958,16 @@ __device__ __forceinline__ uint32_t writelane_u32(uint32_t old, uint32_t val, in
 
 // FSM-only run of nt <= kWinMax ticks (HVAC.step, hvac.py:43-64; the transitions of hvac_fsm) from
 // the words w[h]; tkp / action: the run's first tick.  The booleans (on, can, action) are wave lane
-// masks carried in scalar registers, and the loop carries s1 = the seconds-since-off after the
-// tick's "if not on: sso += dt" instead of sso itself: tick j+1's s1 is 0 for a house turned on at
-// tick j and s1 + dt otherwise, so the per-house work of a tick is one compare, one add and one
-// select.  Tick j's ON masks are written into lane j of per-wave VGPRs (v_writelane); at the end
-// lane t counts tick t's ON houses per capacity class into cnt[t][kWinCap], stores the masks to
-// onb[t][HPT] (this wave's rows, read by the next window's thermal loop) and w[h] becomes the FSM
-// word after the run.  Transitions use the unsaturated seconds-since-off (window_ok guarantees
-// L < 2^30 and sso + (kWinMax + 1) dt < 2^32), so saturating once at the end gives the
+// masks carried in scalar registers.  The seconds-since-off are carried in a per-house offset form:
+// s1_j (the seconds-since-off at tick j after its "if not on: sso += dt") = c + j dt, with c constant
+// while the house stays off and c = -(j + 1) dt when it is ON at tick j (so s1_{j+1} = 0).  A tick is
+// then one compare of c against the wave-uniform L - j dt (straight into a lane mask) and one select
+// of the wave-uniform -(j + 1) dt — no per-house add.  Tick j's ON masks are written into lane j of
+// per-wave VGPRs (v_writelane); at the end lane t counts tick t's ON houses per capacity class into
+// cnt[t][kWinCap], stores the masks to onb[t][HPT] (this wave's rows, read by the next window's
+// thermal loop) and w[h] becomes the FSM word after the run.  Transitions use the unsaturated
+// seconds-since-off (window_ok guarantees L < 2^30 and sso + (kWinMax + 1) dt < 2^31, dt < 2^25, so
+// c and L - j dt fit a signed 32-bit compare), so saturating once at the end gives the
 // per-tick-saturated value; the lock bit comes from the last tick.  SH: the tile starts off a
 // 64-house group boundary (sharded runs), so a random action mask is spliced from two words.
 template <int ACT, int HPT, bool SH>
@@ -995,14 +975,15 @@ __device__ __forceinline__ void win_run_t(const KParams& p, uint32_t* w, const u
                                           const WinTile<HPT>& t, const TickArgs* tkp, uint64_t tick0, int nt,
                                           const uint8_t* action, int64_t act_stride, unsigned* cnt, uint64_t* onb) {
   const int lane = threadIdx.x & 63;
-  const uint32_t Lu = p.L < 0 ? 0u : (uint32_t)p.L, dt = (uint32_t)p.dt;
+  const int Li = p.L < 0 ? 0 : p.L, dt = p.dt;
   uint64_t on_m[HPT], can_m[HPT];
-  uint32_t s1[HPT], mlo[HPT], mhi[HPT];
+  int32_t c[HPT];
+  uint32_t mlo[HPT], mhi[HPT];
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
     on_m[h] = __ballot((w[h] & kOnBit) != 0);
-    const uint32_t sso = w[h] & kSsoMask;
-    s1[h] = __builtin_amdgcn_inverse_ballot_w64(on_m[h]) ? sso : sso + dt;  // if not on: sso += dt
+    const int32_t sso = (int32_t)(w[h] & kSsoMask);
+    c[h] = __builtin_amdgcn_inverse_ballot_w64(on_m[h]) ? sso : sso + dt;  // s1_0: if not on, sso += dt
     can_m[h] = 0ull;
     mlo[h] = mhi[h] = 0u;
   }
@@ -1025,15 +1006,17 @@ __device__ __forceinline__ void win_run_t(const KParams& p, uint32_t* w, const u
       if constexpr (G > 2) W[2] = readlane_u64(wb_lo, wb_hi, j);
     }
     const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)j * act_stride : nullptr;
+    const int32_t thr = Li - j * dt;        // s1_j >= L  <=>  c >= L - j dt
+    const int32_t c_on = -(j + 1) * dt;     // ON at tick j: s1_{j+1} = 0
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
       uint64_t a;  // the actions as a lane mask
       if (ACT == MDR_ACT_RANDOM) a = SH ? (W[h] >> t.sh) | (W[h + 1] << (64 - t.sh)) : W[h];
       else if (ACT == MDR_ACT_ALWAYS_ON) a = ~0ull;
       else a = __ballot(arow[t.idx[h]] != 0);
-      can_m[h] = on_m[h] | __ballot(s1[h] >= Lu);  // not locked
+      can_m[h] = on_m[h] | __ballot(c[h] >= thr);  // not locked
       on_m[h] = can_m[h] & a;
-      s1[h] = __builtin_amdgcn_inverse_ballot_w64(on_m[h]) ? 0u : s1[h] + dt;  // the next tick's s1
+      c[h] = __builtin_amdgcn_inverse_ballot_w64(on_m[h]) ? c_on : c[h];
       mlo[h] = writelane_u32(mlo[h], (uint32_t)on_m[h], j);
       mhi[h] = writelane_u32(mhi[h], (uint32_t)(on_m[h] >> 32), j);
     }
@@ -1041,11 +1024,11 @@ __device__ __forceinline__ void win_run_t(const KParams& p, uint32_t* w, const u
 #pragma unroll
   for (int h = 0; h < HPT; ++h) {
     // the last tick's lockout (hvac.py:58-63): locked before the decision, or turned off with too
-    // little time to finish the lockout (for a house left off, s1 now holds that tick's s1 + dt);
-    // its seconds-since-off: 0 if turned on, else the last tick's s1 (= s1 - dt)
+    // little time to finish the lockout (s1_nt = c + nt dt < L); its seconds-since-off: 0 if turned
+    // on, else the last tick's s1 = c + (nt - 1) dt
     const bool on = __builtin_amdgcn_inverse_ballot_w64(on_m[h]);
-    const uint64_t lock_m = nt > 0 ? ~can_m[h] | (~on_m[h] & __ballot(s1[h] < Lu)) : 0ull;
-    const uint32_t sso = nt > 0 ? (on ? 0u : s1[h] - dt) : w[h] & kSsoMask;
+    const uint64_t lock_m = nt > 0 ? ~can_m[h] | (~on_m[h] & __ballot(c[h] < Li - nt * dt)) : 0ull;
+    const uint32_t sso = nt > 0 ? (on ? 0u : (uint32_t)(c[h] + (nt - 1) * dt)) : w[h] & kSsoMask;
     const uint32_t s = sso < kSsoMask ? sso : kSsoMask;
     w[h] = s | (__builtin_amdgcn_inverse_ballot_w64(lock_m) ? kLockBit : 0u) | (on ? kOnBit : 0u);
   }
@@ -1056,10 +1039,10 @@ __device__ __forceinline__ void win_run_t(const KParams& p, uint32_t* w, const u
       const uint64_t m = ((uint64_t)mhi[h] << 32) | mlo[h];
       onb[lane * HPT + h] = m;
 #pragma unroll
-      for (int c = 0; c < kWinCap; ++c) k[c] += (unsigned)__popcll(m & cm[h][c]);
+      for (int cc = 0; cc < kWinCap; ++cc) k[cc] += (unsigned)__popcll(m & cm[h][cc]);
     }
 #pragma unroll
-    for (int c = 0; c < kWinCap; ++c) cnt[lane * kWinCap + c] = k[c];
+    for (int cc = 0; cc < kWinCap; ++cc) cnt[lane * kWinCap + cc] = k[cc];
   }
 }
 
@@ -1081,7 +1064,7 @@ __device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsign
     const int j = e / ncap, c = e - j * ncap;
     const unsigned v = cnt[0][j * kWinCap + c] + cnt[1][j * kWinCap + c] + cnt[2][j * kWinCap + c] +
                        cnt[3][j * kWinCap + c];
-    if (v) atomicAdd(&slot[((size_t)j * kCountShards + blockIdx.x % kCountShards) * ncap + c],
+    if (v) atomicAdd(&slot[((size_t)j * kCountShards + blockIdx.x % kWinShards) * ncap + c],
                      (unsigned long long)v);
   }
 }
@@ -1095,6 +1078,17 @@ __device__ __forceinline__ void win_classes(const WinTile<HPT>& t, const int* cl
     for (int c = 0; c < kWinCap; ++c) cm[h][c] = __ballot(t.v[h] && cls[h] == c);
 }
 
+#ifdef MDR_COUNT_TIMING
+// measurement build only (tools/count_timing.py, a variant library): per block of k_count_window
+// the constant 100 MHz clock at entry, after the state loads were consumed, after the shard flush,
+// and after the ticket (the last block: after its reduce)
+__device__ unsigned long long g_cw_ts[16384 * 4];
+#define MDR_CW_TS(k) \
+  do { if (threadIdx.x == 0 && blockIdx.x < 16384) g_cw_ts[blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define MDR_CW_TS(k) do {} while (0)
+#endif
+
 // First window of a rollout: ON counts, ON lane masks and end-of-window FSM words of ticks
 // 0 .. nt-1 from the current state (hvac itself is not changed).  Tick ids from the staged drivers,
 // or tick0 + t when tkp is null (mdr_rollout_begin: launched before the host computes the drivers).
@@ -1105,6 +1099,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
                                                       uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
                                                       const uint32_t* __restrict__ w_in, unsigned* __restrict__ ticket) {
   __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
+  MDR_CW_TS(0);
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
   uint32_t w[HPT];
@@ -1116,6 +1111,7 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
   }
   uint64_t cm[HPT][kWinCap];
   win_classes<HPT>(t, cls, cm);
+  MDR_CW_TS(1);
   win_run<ACT, HPT>(p, w, cm, t, tkp, tick0, nt, action, act_stride, s_cnt[wv],
                     onb + (size_t)t.tile * HPT * kWinMax);
 #pragma unroll
@@ -1123,7 +1119,9 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
     if (t.v[h]) wah[t.i0 + 64u * h] = w[h];
   __syncthreads();
   win_flush(p, nt, s_cnt, slot);
+  MDR_CW_TS(2);
   if (ticket) win_reduce_last(p, slot, nt, ticket);  // (ticket: the P-only reduce, see win_reduce_last)
+  MDR_CW_TS(3);
 }
 
 // Per-window affine transition of one house (FORM = MDR_THERMAL_AFFINE).  The reference's update
@@ -1381,6 +1379,13 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
   }
 }
 
+#ifdef MDR_COUNT_TIMING
+extern "C" int mdr_count_timing(unsigned long long* out, int n) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cw_ts), (size_t)n * 4 * sizeof(unsigned long long), 0,
+                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+#endif
+
 #define MDR_INST_WIN_F(A, SI, KA_, FO)                                                                         \
   template __global__ void k_step_window<A, kWinHpt, SI, KA_, FO>(KParams, const uint8_t*, int64_t, const TickArgs*, \
                                                                   int, int, const double*, double*, int64_t,   \
@@ -1629,6 +1634,7 @@ __global__ void __launch_bounds__(256) k_populate(KParams p, PopArgs a) {
 __global__ void __launch_bounds__(kObsBlock) k_obs(KParams p, ObsArgs o, const double* p_dev,
                                                    float* __restrict__ obs) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  if (o.sc_dev) { o.s = o.sc_dev[1]; o.solar = o.sc_dev[2]; o.t_od = o.sc_dev[3]; }  // (per-tick rows of rollouts)
   const int F = o.n_feat;
   const int64_t b0 = (int64_t)blockIdx.x * kObsBlock;
   const int nb = (int)min((int64_t)kObsBlock, p.n - b0);

@@ -12,7 +12,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("MDR_LIB", os.path.join(HERE, "libmdr_hip.so"))
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MAX_CAP = 64
 
 # enums (mdr.h)
@@ -22,7 +22,7 @@ COMM_RING, COMM_TABLE = 0, 1
 PEN_MODES = {"individual_L2": 0, "common_L2": 1, "common_max_error": 2, "mixture": 3}
 ERRORS = {-1: "MDR_EARG", -2: "MDR_EHIP", -3: "MDR_ERCCL", -4: "MDR_ENOMEM", -5: "MDR_ESTATE"}
 # mdr_set_option (mdr.h): alternative launch forms of the same computation
-OPTIONS = {"step_tpw": 1, "fastdiv": 2, "window_pipeline": 3, "sharded_overlap": 4, "greedy_sort": 5, "actor_pingpong": 8,
+OPTIONS = {"step_tpw": 1, "fastdiv": 2, "window_pipeline": 3, "sharded_overlap": 4, "greedy_sort": 5,
            "force_halo": 6, "window_thermal": 7}
 THERMAL_EXACT, THERMAL_AFFINE = 0, 1
 
@@ -86,6 +86,14 @@ class mdr_actor_spec(C.Structure):
                 ("precision", C.c_int32)]
 
 
+ACTOR_MAX_LAYERS = 8
+
+
+class mdr_actor_net(C.Structure):
+    _fields_ = [("n_in", C.c_int32), ("n_hidden", C.c_int32), ("n_act", C.c_int32), ("precision", C.c_int32),
+                ("hidden", C.c_int32 * ACTOR_MAX_LAYERS)]
+
+
 INTERP_AXES = 10
 
 
@@ -99,7 +107,7 @@ PRECISIONS = {"bf16": PREC_BF16, "bf16x3": PREC_BF16X3, "fp32": PREC_FP32}
 
 # the structs mdr_abi_sizes reports, in its order
 ABI_STRUCTS = (mdr_config, mdr_soa, mdr_tick, mdr_pop_spec, mdr_obs_spec, mdr_obs_scalars, mdr_actor_spec,
-               mdr_interp_spec)
+               mdr_interp_spec, mdr_actor_net)
 
 P, VP, I, I64, U64, D = C.POINTER, C.c_void_p, C.c_int, C.c_int64, C.c_uint64, C.c_double
 
@@ -147,6 +155,8 @@ SIGNATURES = {
     "mdr_gq_shard_fallback": (I, [VP, VP, VP]),
     "mdr_cluster_stats": (I, [VP, VP, VP, VP]),
     "mdr_actor_load": (I, [VP, P(mdr_actor_spec), VP, VP, VP, VP, VP, VP, VP]),
+    "mdr_actor_load_net": (I, [VP, P(mdr_actor_net), VP, VP, VP]),
+    "mdr_actor_fused": (I, [VP, P(mdr_obs_spec)]),
     "mdr_actor_act": (I, [VP, P(mdr_obs_spec), P(mdr_obs_scalars), VP, U64, VP, VP, VP, VP, I, VP]),
     "mdr_actor_rollout": (I, [VP, I, VP, VP, P(mdr_obs_spec), VP, I64, VP, I64,
                               VP, I64, VP, I, VP]),

@@ -62,8 +62,8 @@ class DeviceActor:
     def __init__(self, env, actor, precision: str = "bf16x3"):
         if precision not in L.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(L.PRECISIONS)}")
-        if len(actor.layers) != 2:
-            raise NotImplementedError("the fused actor kernel takes two hidden layers (actor_layers = [h1, h2])")
+        if not 1 <= len(actor.layers) <= L.ACTOR_MAX_LAYERS:
+            raise ValueError(f"1 to {L.ACTOR_MAX_LAYERS} hidden layers (actor_layers)")
         self.env = env
         self.actor = actor
         self.precision = precision
@@ -76,14 +76,20 @@ class DeviceActor:
         torch = _torch()
         sh = self.env.shard
         dev = sh.device
-        ws = []
-        for lin in self.actor.fc:
-            ws.append(lin.weight.detach().to(device=dev, dtype=torch.float32).contiguous())
-            ws.append(lin.bias.detach().to(device=dev, dtype=torch.float32).contiguous())
-        spec = L.mdr_actor_spec(self.n_in, self.actor.fc[0].out_features, self.actor.fc[1].out_features,
-                                self.n_act, L.PRECISIONS[self.precision])
-        sh.actor_load(spec, *ws)
-        torch.cuda.current_stream(dev).synchronize()  # the packed image is read by later launches only
+        ws = [lin.weight.detach().to(device=dev, dtype=torch.float32).contiguous() for lin in self.actor.fc]
+        bs = [lin.bias.detach().to(device=dev, dtype=torch.float32).contiguous() for lin in self.actor.fc]
+        hidden = [lin.out_features for lin in self.actor.fc[:-1]]
+        net = L.mdr_actor_net(self.n_in, len(hidden), self.n_act, L.PRECISIONS[self.precision])
+        for i, h in enumerate(hidden):
+            net.hidden[i] = h
+        sh.actor_load_net(net, ws, bs)
+        torch.cuda.current_stream(dev).synchronize()  # (the copies are read by later launches only)
+
+    def fused(self) -> bool:
+        """True when this actor runs the fused obs + MLP kernel (k_actor) for the env's obs layout:
+        two hidden layers <= 128 wide, <= 128 feature slots, weights within the LDS; otherwise the
+        layer chain (k_obs -> k_dense per layer -> k_actor_head)."""
+        return self.env.shard.actor_fused(self.env.obs_spec())
 
     def _check_obs(self, spec):
         if spec.n_feat != self.n_in:
@@ -111,15 +117,17 @@ class DeviceActor:
         return action, prob
 
     def rollout(self, n_ticks: int, rewards=None, actions=None, probs=None, use_graph: bool = True):
-        """n_ticks of (select_actions -> env.step) in one graph-captured C call (single shard,
-        individual_L2).  ``rewards`` float64 [n_ticks, N] (or [N], overwritten each tick);
-        ``actions`` u8 / ``probs`` f32 [n_ticks, N] (or [N]) optional outputs."""
+        """n_ticks of (select_actions -> env.step) in one graph-captured C call (individual_L2;
+        sharded: the library's C loop).  The common penalty modes (common_L2, common_max_error,
+        mixture: rewards_calculator.py:29-203) need the cluster's penalty sum / max between the
+        step and the reward, so they run tick by tick (select_actions -> step_tensor, whose penalty
+        reduce — and allreduce when sharded — finishes every tick's rewards).  ``rewards`` float64
+        [n_ticks, N] (or [N], overwritten each tick); ``actions`` u8 / ``probs`` f32 [n_ticks, N]
+        (or [N]) optional outputs."""
         torch = _torch()
         env = self.env
         sh = env.shard
-        if sh.penalty_mode != 0:
-            raise NotImplementedError("actor rollouts support individual_L2; use step_tensor")
-        if env.world > 1 and not getattr(env._comm, "native", False):
+        if sh.penalty_mode != 0 or (env.world > 1 and not getattr(env._comm, "native", False)):
             return self._rollout_stepwise(n_ticks, rewards, actions, probs)
         sharded = env.world > 1
         spec, _sc, keep = env.bound_obs_spec() if not sharded else (env.obs_spec(), None, [])
@@ -162,9 +170,10 @@ class DeviceActor:
 
 
     def _rollout_stepwise(self, n_ticks, rewards, actions, probs):
-        """Sharded rollout over a torch.distributed communicator (e.g. gloo): per tick
-        select_actions (ring halo all-gather, ON counts of the actions) then step_tensor (count
-        allreduce, step) from Python — the same launches and exchanges as the C loop."""
+        """Per tick select_actions (sharded: the ring halo, ON counts of the actions) then
+        step_tensor (count allreduce, step, and for the common penalty modes the penalty reduce +
+        reward finalize) from Python — the same launches and exchanges as the C loop, plus the
+        penalty stages the C loops do not have."""
         torch = _torch()
         env = self.env
         sh = env.shard

@@ -284,6 +284,21 @@ class HipShard:
         L.check(self.lib.mdr_actor_load(self.ctx, C.byref(spec), *(L.ptr(t) for t in (w1, b1, w2, b2, w3, b3)),
                                         self.stream()), "mdr_actor_load")
 
+    def actor_load_net(self, net, weights, biases):
+        """mdr_actor_load_net: any number of hidden layers (weights / biases: device fp32 tensors,
+        fc.0 .. fc.L in order)."""
+        n = len(weights)
+        w = (C.c_void_p * n)(*[L.ptr(t) for t in weights])
+        b = (C.c_void_p * n)(*[L.ptr(t) for t in biases])
+        L.check(self.lib.mdr_actor_load_net(self.ctx, C.byref(net), w, b, self.stream()), "mdr_actor_load_net")
+
+    def actor_fused(self, spec) -> bool:
+        """True when the loaded actor runs the fused k_actor for this obs layout (else the chain)."""
+        r = self.lib.mdr_actor_fused(self.ctx, C.byref(spec))
+        if r < 0:
+            L.check(r, "mdr_actor_fused")
+        return r == 1
+
     def actor_act(self, spec, scalars, tick, action, prob, probs, obs_out, count_next, use_p_dev=True):
         L.check(self.lib.mdr_actor_act(self.ctx, C.byref(spec), C.byref(scalars),
                                        L.ptr(self.p_dev) if use_p_dev else 0, int(tick), L.ptr(action),

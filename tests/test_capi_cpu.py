@@ -34,12 +34,12 @@ def test_abi_struct_sizes_and_version():
 
     lib = _lib.load()
     assert lib.mdr_abi_version() == _lib.ABI_VERSION
-    sizes = (C.c_int64 * 8)()
-    assert lib.mdr_abi_sizes(sizes, 8) == 8
+    sizes = (C.c_int64 * 9)()
+    assert lib.mdr_abi_sizes(sizes, 9) == 9
     assert list(sizes) == [C.sizeof(t) for t in (_lib.mdr_config, _lib.mdr_soa, _lib.mdr_tick,
                                                  _lib.mdr_pop_spec, _lib.mdr_obs_spec, _lib.mdr_obs_scalars,
-                                                 _lib.mdr_actor_spec, _lib.mdr_interp_spec)]
-    assert _lib.ABI_STRUCTS[-1] is _lib.mdr_interp_spec
+                                                 _lib.mdr_actor_spec, _lib.mdr_interp_spec, _lib.mdr_actor_net)]
+    assert _lib.ABI_STRUCTS[-1] is _lib.mdr_actor_net
 
 
 def test_argument_errors_without_gpu():

@@ -189,7 +189,7 @@ def test_sharded_equals_single(tmp_path, backend, kind, world, n, mode):
 T_ACT = 12
 
 
-def _actor_run(env, torch, dist=None):
+def _actor_run(env, torch, dist=None, layers=(100, 100)):
     from mdr_amd.actor import DeviceActor
 
     # the seed-1 reference actor with the obs normalisation folded into layer 1 (not saturated at
@@ -198,7 +198,7 @@ def _actor_run(env, torch, dist=None):
     if dist is not None:
         dist.all_reduce(m, op=dist.ReduceOp.MAX)
     m = m.cpu().numpy()
-    da = DeviceActor(env, gu.calibrated_actor(env.obs_spec().n_feat, m, seed=1).to(env.shard.device))
+    da = DeviceActor(env, gu.calibrated_actor(env.obs_spec().n_feat, m, seed=1, layers=layers).to(env.shard.device))
     nl = env.n_local
     A = torch.zeros((T_ACT, nl), dtype=torch.uint8, device=env.shard.device)
     Pr = torch.zeros((T_ACT, nl), dtype=torch.float32, device=env.shard.device)
@@ -209,7 +209,7 @@ def _actor_run(env, torch, dist=None):
             "T": st["T"], "on": st["on"], "sso": st["sso"], "P": env._cluster_power()}
 
 
-def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo):
+def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo, layers):
     sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "marl-demandresponse_amd"), os.path.dirname(HERE)]
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -229,33 +229,34 @@ def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo):
                       population="synthetic", seed=77, rank=rank, world=world, comm=make_comm(kind))
     if force_halo:
         env.shard.set_option("force_halo", 1)
-    res = _actor_run(env, torch, dist)
+    res = _actor_run(env, torch, dist, layers)
     res["lo"] = env._offset
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("backend,kind,world,force_halo,n", [
-    ("nccl", "rccl", 1, False, 3001),   # C loop: actor -> RCCL count allreduce -> step
-    ("nccl", "rccl", 1, True, 3001),    # + the ring-halo pack / ncclSend / ncclRecv (to self)
-    ("gloo", "torch", 2, False, 3001),  # two shards on cuda:0, per-tick Python loop, P2P halo
-    ("gloo", "torch", 3, False, 3001),  # distinct left / right peers
-    ("gloo", "host", 3, False, 3001),   # the C loop (halo pack -> paired send/recv -> actor -> allreduce -> step)
-    ("gloo", "host", 8, False, 8 * 131072),  # C5: the 1,048,576-house cluster on 8 ranks
+@pytest.mark.parametrize("backend,kind,world,force_halo,n,layers", [
+    ("nccl", "rccl", 1, False, 3001, (100, 100)),   # C loop: actor -> RCCL count allreduce -> step
+    ("nccl", "rccl", 1, True, 3001, (100, 100)),    # + the ring-halo pack / ncclSend / ncclRecv (to self)
+    ("gloo", "torch", 2, False, 3001, (100, 100)),  # two shards on cuda:0, per-tick Python loop, P2P halo
+    ("gloo", "torch", 3, False, 3001, (100, 100)),  # distinct left / right peers
+    ("gloo", "host", 3, False, 3001, (100, 100)),   # the C loop (halo pack -> send/recv -> actor -> allreduce -> step)
+    ("gloo", "host", 3, False, 3001, (64, 64, 64)),  # the layer chain (k_obs reads the halo) in the C loop
+    ("gloo", "host", 8, False, 8 * 131072, (100, 100)),  # C5: the 1,048,576-house cluster on 8 ranks
 ])
-def test_sharded_actor_rollout_equals_single(tmp_path, backend, kind, world, force_halo, n):
+def test_sharded_actor_rollout_equals_single(tmp_path, backend, kind, world, force_halo, n, layers):
     """Sharded MA-PPO rollout (config C5) == the single-process graph rollout: actions, sampled
     probabilities, rewards, state and P bit for bit."""
     import torch
 
     from mdr_amd.environment import Environment
 
-    mp.start_processes(_actor_worker, args=(world, _free_port(), backend, kind, n, str(tmp_path), force_halo),
+    mp.start_processes(_actor_worker, args=(world, _free_port(), backend, kind, n, str(tmp_path), force_halo, layers),
                        nprocs=world, join=True, start_method="spawn")
     parts = sorted((np.load(tmp_path / f"rank{r}.npz") for r in range(world)), key=lambda p: int(p["lo"]))
     env = Environment(gu.props_from_overrides(_overrides(n, "individual_L2")), device=torch.device("cuda", 0),
                       rng=random.Random(4), population="synthetic", seed=77)
-    ref = _actor_run(env, torch)
+    ref = _actor_run(env, torch, layers=layers)
     for key in ("actions", "probs", "rewards"):
         np.testing.assert_array_equal(np.concatenate([p[key] for p in parts], axis=1), ref[key], err_msg=key)
     for key in ("T", "on", "sso"):

@@ -18,7 +18,6 @@ def main():
     ap.add_argument("--houses", type=int, default=1 << 20)
     ap.add_argument("--precision", default="bf16x3")
     ap.add_argument("--reps", type=int, default=20)
-    ap.add_argument("--pingpong", type=int, default=0, help="MDR_OPT_ACTOR_PINGPONG")
     a = ap.parse_args()
     import torch
 
@@ -29,7 +28,6 @@ def main():
     env = Environment(bench.env_props(a.houses), device="cuda:0", rng=random.Random(4), population="synthetic",
                       seed=1234)
     actor = make_actor(env.obs_spec().n_feat, 2, [100, 100], seed=1)
-    env.shard.set_option("actor_pingpong", a.pingpong)
     da = DeviceActor(env, actor, precision=a.precision)
     n = env.n_local
     act = torch.empty(n, dtype=torch.uint8, device="cuda:0")
@@ -45,7 +43,7 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / a.reps
     flops = 2 * sum(l.in_features * l.out_features for l in actor.fc) * n
-    print(f"houses={n} precision={a.precision} pingpong={a.pingpong}: k_actor {us:.1f} us/launch, {flops / us / 1e6:.1f} TFLOP/s "
+    print(f"houses={n} precision={a.precision}: k_actor {us:.1f} us/launch, {flops / us / 1e6:.1f} TFLOP/s "
           f"algorithmic ({flops / us / 1e6 / bench.BF16_PEAK_TFS:.3f} of dense bf16 peak)", flush=True)
 
 

@@ -20,7 +20,9 @@ REPS = 20
 
 
 def groups():
-    return [(m, t) for m in MODES for t in TICKS]
+    ticks = [int(x) for x in os.environ.get("CP_TICKS", ",".join(map(str, TICKS))).split(",")]
+    modes = os.environ.get("CP_MODES", ",".join(MODES)).split(",")
+    return [(m, t) for m in modes for t in ticks]
 
 
 def run(houses):
