@@ -100,6 +100,9 @@ def parse():
                          "size (graph capture + 2 replays: the first replay of a graph and of the host path is "
                          "2-3x slower than the steady state, profiles/r02e_bench20_warmup.log)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--above-mall-houses", type=int, default=16 << 20,
+                    help="roofline.above_mall: the same step kernel timed alone at this many houses (working set "
+                         "well above the 256 MB Infinity Cache, SURVEY 8(d) LLC caveat); 0 = skip")
     ap.add_argument("--trace", action="store_true",
                     help="print host phase timestamps of the timed region to stderr (diagnostics)")
     ap.add_argument("--graph", default="off", choices=["on", "off"],
@@ -147,7 +150,22 @@ def _cpu_run(job):
 
     cfg, n, seconds = job
     os.environ.setdefault("OMP_NUM_THREADS", "1")
-    if cfg == "C1":  # 50 houses, deadband bang-bang, reference population + RNG stream
+    if cfg == "C5":  # MA-PPO: the oracle's norm_state_dict rows -> torch fp32 actor (batched) -> Categorical
+        import torch
+
+        from mdr_amd.actor import make_actor
+
+        torch.set_num_threads(1)
+        props = env_props(n)
+        ora = O.OracleEnv(props, random.Random(1), population=_synthetic_pop(props, n, 0))
+        actor = make_actor(ora.norm_vector().shape[1], 2, [100, 100], seed=1)
+        gen = torch.Generator().manual_seed(3)
+
+        def act():
+            with torch.no_grad():
+                p = actor(torch.from_numpy(ora.norm_vector()).float())
+            return torch.multinomial(p, 1, generator=gen).squeeze(1).numpy().astype(bool)
+    elif cfg == "C1":  # 50 houses, deadband bang-bang, reference population + RNG stream
         props = env_props(n)
         ora = O.OracleEnv(props, random.Random(4))
         hp = props.cluster_prop.house_prop
@@ -215,6 +233,16 @@ def cpu_baseline(budget_s: float):
     out["configs"][f"C2_65536_random_{procs}cores"] = {"value": c2_all, "procs": procs}
     hs, el = _cpu_run(("C3", 1 << 20, 0.2 * b))
     out["configs"]["C3_1048576_greedy_1core"] = {"value": hs / el, "ticks": hs // (1 << 20)}
+    hs, el = _cpu_run(("C5", 65536, 0.15 * b))
+    out["configs"]["C5_65536_mappo_actor_1core"] = {
+        "value": hs / el, "ticks": hs // 65536,
+        "what": "oracle norm_vector rows -> torch fp32 Actor (batched forward, 1 thread) -> Categorical sample -> "
+                "oracle step; the reference does N batch-1 forwards per tick (mappo.py:83-97), so this port is "
+                "faster than the reference's own loop"}
+    out["reference_itself"] = {"C1_50_deadband_bbc_1core": 31752, "unit": "house-steps/s",
+                               "where": "the reference env (single-thread Python) in the survey container, "
+                                        "Xeon 1 core (BASELINE.md:30, SURVEY.md section 6); it cannot run on the "
+                                        "GPU box (the reference does not travel)"}
     out.update({"value": c2_all, "unit": "house-steps/s", "cores": procs, "kind": "port",
                 "sample": f"oracle/env_np.py (NumPy fp64 restatement, 1 thread per process) on {procs} "
                           f"processes x 65,536 houses, random actions, {0.3 * b:.1f} s each "
@@ -261,6 +289,39 @@ def valu_roofline(kernel: str, houses: int, kern_ms: float):
             "valu_instr_per_launch": inst,
             "source": "SQ_INSTS_VALU per launch (profiles/pmc_traffic.json) / kernel_avg_us; peak = 1024 SIMDs x "
                       "2.4 GHz / 4 cycles (the clock under this fp64 load is ~1.75 GHz, GRBM_GUI_ACTIVE)"}
+
+
+def above_mall(houses: int, args, kern_1m: str) -> dict:
+    """The dominant kernel timed ALONE at `houses` (16M by default: ~1.6 GB of state + parameters,
+    ~6x the 256 MB Infinity Cache, so the fraction is HBM-honest), as for the 1M line: untimed
+    warm ticks, then hipExtLaunchKernel events around every 32-tick k_step_window launch
+    (mdr_time_step_kernels); traffic = the committed PMC record at that size."""
+    import torch
+
+    from mdr_amd import _lib as L
+    from mdr_amd.environment import Environment
+
+    env = Environment(env_props(houses), device="cuda:0", rng=random.Random(4), population="synthetic", seed=1234)
+    sh = env.shard
+    kt = 32
+    kern = step_kernel_name(houses, "random", 32, True, args.thermal)
+    buf = torch.empty((kt, houses), dtype=torch.float64, device="cuda:0")
+    for _ in range(4):  # warm: clock and caches in the state the timed launches see
+        sh.rollout(env.driver_window(kt), None, 0, L.ACT_RANDOM, buf, houses, True)
+    ms, launches = 0.0, 0
+    for _ in range(8):
+        m, l = sh.time_step_kernels(env.driver_window(kt), None, 0, L.ACT_RANDOM, buf, houses)
+        ms += m
+        launches += l
+    kern_ms = ms / launches
+    b = window_bytes(houses, kt, "random")
+    achieved = b / (kern_ms * 1e-3) / 1e9
+    del buf, env
+    torch.cuda.empty_cache()
+    return {"houses": houses, "kernel": kern, "same_kernel_as_1m": kern == kern_1m, "kernel_avg_us": kern_ms * 1e3,
+            "launches_timed": launches, "algorithmic_bytes_per_launch": b, "achieved": achieved,
+            "frac": achieved / HBM_PEAK_GBS, "traffic": pmc_traffic(kern, houses),
+            "timing": "hipExtLaunchKernel events around each 32-tick launch, 8 calls after 4 untimed ones"}
 
 
 def main():
@@ -564,9 +625,20 @@ def main():
                            "step_share": {"what": "launch-stream time per tick minus k_actor's time: the step "
                                                   "kernel's share of a tick (not a kernel duration)",
                                           "us_per_tick": kern_ms * 1e3}}
+    if (dactor is None and g_act is None and rank == 0 and window > 0 and args.above_mall_houses > 0
+            and args.mode == "random"):
+        out["roofline"]["above_mall"] = above_mall(args.above_mall_houses, args, kern)
     out["build"] = {"lib": os.path.relpath(L.LIB_PATH, os.path.dirname(os.path.abspath(__file__))),
                     "src_hash": L.build_id(), "checked_against_tree": L.source_hash() == L.build_id()}
     if cpu is not None:
+        # the headline CPU number of the line's own config: C2 (step), C3 (greedy), C5 (actor)
+        key = {"greedy": "C3_1048576_greedy_1core", "actor": "C5_65536_mappo_actor_1core"}.get(args.workload)
+        if key is not None:
+            c = cpu["configs"][key]
+            cpu = dict(cpu, value=c["value"], cores=1,
+                       sample=(f"{key}: oracle/env_np.py (NumPy fp64, 1 thread)" +
+                               (" + torch fp32 actor" if args.workload == "actor" else "") +
+                               f", {c['ticks']} ticks; host {cpu['cpu_model']}"))
         out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -41,11 +41,13 @@ struct ActorOut {
   float* obs;                    // [n][n_in] the observation rows, or null
   unsigned long long* count_next;  // count slab of the tick these actions drive, or null
   unsigned long long* prof;        // diagnostics: [grid][8] per-phase shader cycles, or null
+  int tiles;                       // 32-house tiles to run: 0 all, 1 interior (not the first or last), 2 the
+                                   // first and last (the sharded ring halo's readers; mdr_actor_rollout_sharded)
 };
 
 __global__ void k_actor_pack(ActorDims d, const float* w1, const float* b1, const float* w2,
                              const float* b2, const float* w3, const float* b3, unsigned char* out);
-template <int PREC, bool PROF, int MB, int KS1>
+template <int PREC, bool PROF, int MB, int KS1, bool DEF>
 __global__ void k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
                         const unsigned char* wpack, ActorOut out, uint64_t tick, const TickArgs* tkp);
 

@@ -200,11 +200,19 @@ __device__ __forceinline__ void split_operand(const float* v, bf16x8* s) {
 // sources go in flight first) and Y (output layer, softmax, sampling, stores on the VALU); the
 // waves run them free (a ping-pong schedule of the two waves of a SIMD, tried in r03, was slower:
 // DESIGN.md §3.4).  MB: row blocks of the hidden layers (compile-time LDS offsets); KS1: layer-1
-// k-steps (d.ks1, 2 to 4; no per-step guards in the MFMA loop).
-template <int PREC, bool PROF, int MB, int KS1>
+// k-steps (d.ks1, 2 to 4; no per-step guards in the MFMA loop).  DEF: the reference's default obs
+// layout (the 'neighbours' ring, 4-float messages, no optional state or message features), fixed at
+// compile time: the optional features' branches and their uniform operands leave the kernel (the
+// generic form spills ~127 SGPRs into VGPR lanes, reloaded by v_readlane in the tile loop; DEF 19).
+template <int PREC, bool PROF, int MB, int KS1, bool DEF>
 __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
                                                const unsigned char* __restrict__ wpack, ActorOut out,
                                                uint64_t tick0, const TickArgs* tkp) {
+  if (DEF) {  // (the host launches DEF only for this layout: mdr_capi.hip actor_def_layout)
+    o.hvac_state = 0; o.solar_state = 0; o.thermal_state = 0; o.msg_thermal = 0; o.msg_hvac = 0;
+    o.comm_mode = MDR_COMM_RING; o.msg_w = 4; o.comm_table = nullptr; o.msg_all = nullptr;
+    d.ring = 1; d.m4 = 4; d.msg_w = 4; d.n_own = 10; d.own4 = 12; d.nf = PREC == 6 ? 3 : 2;
+  }
   static_assert(MB >= 1 && MB <= kActorMaxMB, "row blocks");
   static_assert(KS1 >= 1 && KS1 <= kActorMaxSlots / 32, "layer-1 k-steps");
   constexpr int NS = PREC == 6 ? 3 : PREC == 3 ? 2 : 1;  // operand splits
@@ -283,6 +291,12 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
   const uint32_t n = (uint32_t)p.n;
   const uint32_t ntile = (n + 31u) / 32u;
   const uint32_t stride = gridDim.x * (uint32_t)nw;
+  // the launch's tiles as virtual indices v < nv (out.tiles: all, the interior ones, or the first and
+  // last — the sharded tick runs the interior while the ring halo is in flight)
+  const uint32_t nv = out.tiles == 1 ? ntile - 2u : out.tiles == 2 ? 2u : ntile;
+  auto real_tile = [&](uint32_t v) -> uint32_t {
+    return out.tiles == 1 ? v + 1u : out.tiles == 2 ? (v == 0u ? 0u : ntile - 1u) : v;
+  };
   const int nsrc_max = ring ? lo + 32 + hi : 32;
   HouseRegs src{};
   int src_kind = 0;  // 0 none, 1 house, 2 halo
@@ -353,7 +367,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     wave_sync();
     PSTAMP(1);
   };
-  // X: the next tile's sources go in flight, then layers 1 and 2 on the MFMA pipe
+  // X: the next tile's sources go in flight, then layers 1 and 2 on the MFMA pipe (next >= ntile: none)
   auto stage_x = [&](uint32_t tl, uint32_t next) {
     const uint32_t b0 = tl * 32u;
     const int nb = (int)min(32u, n - b0);
@@ -461,7 +475,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
   };
   // Y: output layer (fp32 VALU) + softmax + sampling + stores (+ the ON counts of the new actions)
   float u_next = 0.f;  // the sampling uniforms of this wave's next tile (stage_y, odd tiles)
-  auto stage_y = [&](uint32_t tl, bool fresh) {
+  auto stage_y = [&](uint32_t tl, uint32_t next, bool fresh) {
     const uint32_t b0 = tl * 32u;
     const int nb = (int)min(32u, n - b0);
     float z[2][kActorNA];
@@ -512,7 +526,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     // counters: one Philox pass per two tiles), kept in u_next
     float u;
     if (fresh) {
-      const uint32_t ih = (lane < 32 ? b0 : b0 + stride * 32u) + (uint32_t)r;
+      const uint32_t ih = (lane < 32 ? b0 : next * 32u) + (uint32_t)r;
       u = philox_u01f(p.seed, (uint64_t)p.goff + ih, tick);
       u_next = __shfl(u, r + 32);
     } else {
@@ -539,18 +553,20 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
   };
 
   // ---- the wave's tiles: build(t0) | X(t0) | Y(t0) + build(t1) | X(t1) | ... | Y(t_last)
-  const uint32_t tile0 = blockIdx.x * (uint32_t)nw + (uint32_t)wv;
-  const int n_my = tile0 < ntile ? (int)((ntile - 1u - tile0) / stride + 1u) : 0;
+  const uint32_t v0 = blockIdx.x * (uint32_t)nw + (uint32_t)wv;
+  const int n_my = v0 < nv ? (int)((nv - 1u - v0) / stride + 1u) : 0;
   if (n_my > 0) {
-    src_kind = source_of(tile0, lane, src);
-    stage_build(tile0);
+    src_kind = source_of(real_tile(v0), lane, src);
+    stage_build(real_tile(v0));
   }
   for (int j = 0; j < n_my; ++j) {
-    const uint32_t tj = tile0 + (uint32_t)j * stride;
+    const uint32_t vj = v0 + (uint32_t)j * stride;
+    const uint32_t tj = real_tile(vj);
+    const uint32_t next = vj + stride < nv ? real_tile(vj + stride) : ntile;  // (ntile: none)
     if (PROF && lane == 0) pacc[7] += 1;
-    stage_x(tj, tj + stride);
-    stage_y(tj, (j & 1) == 0);
-    if (j + 1 < n_my) stage_build(tj + stride);
+    stage_x(tj, next);
+    stage_y(tj, next, (j & 1) == 0);
+    if (j + 1 < n_my) stage_build(next);
   }
   if (PROF && lane == 0) {
     for (int k = 0; k < 8; ++k) out.prof[(blockIdx.x * nw + wv) * 8 + k] = pacc[k];
@@ -676,9 +692,10 @@ template __global__ void k_dense<1>(const float*, int, int, int64_t, const float
 template __global__ void k_dense<3>(const float*, int, int, int64_t, const float*, const float*, int, float*, int, int);
 template __global__ void k_dense<6>(const float*, int, int, int64_t, const float*, const float*, int, float*, int, int);
 
-#define MDR_INST_ACTOR(P, F, MB, KS)                                                                \
-  template __global__ void k_actor<P, F, MB, KS>(KParams, ObsArgs, ActorDims, const double*,              \
-                                                 const unsigned char*, ActorOut, uint64_t, const TickArgs*);
+#define MDR_INST_ACTOR_D(P, F, MB, KS, DF)                                                            \
+  template __global__ void k_actor<P, F, MB, KS, DF>(KParams, ObsArgs, ActorDims, const double*,          \
+                                                     const unsigned char*, ActorOut, uint64_t, const TickArgs*);
+#define MDR_INST_ACTOR(P, F, MB, KS) MDR_INST_ACTOR_D(P, F, MB, KS, false)
 #define MDR_INST_ACTOR_SHAPE(MB, KS) \
   MDR_INST_ACTOR(1, false, MB, KS) \
   MDR_INST_ACTOR(3, false, MB, KS) \
@@ -692,5 +709,11 @@ MDR_INST_ACTOR_SHAPE(7, 4)
 MDR_INST_ACTOR_SHAPE(8, 2)
 MDR_INST_ACTOR_SHAPE(8, 3)
 MDR_INST_ACTOR_SHAPE(8, 4)
+#define MDR_INST_ACTOR_DEF(MB)                                                                      \
+  MDR_INST_ACTOR_D(1, false, MB, 2, true) MDR_INST_ACTOR_D(3, false, MB, 2, true)                   \
+  MDR_INST_ACTOR_D(6, false, MB, 2, true) MDR_INST_ACTOR_D(1, true, MB, 2, true)                    \
+  MDR_INST_ACTOR_D(3, true, MB, 2, true) MDR_INST_ACTOR_D(6, true, MB, 2, true)
+MDR_INST_ACTOR_DEF(7)
+MDR_INST_ACTOR_DEF(8)
 
 }  // namespace mdr

@@ -89,6 +89,7 @@ struct mdr_ctx {
   bool tick_overlap = true;              // MDR_OPT_SHARDED_OVERLAP: per-tick sharded two-stream pipeline
   bool greedy_sort = false;              // MDR_OPT_GREEDY_SORT: the full-sort greedy form only
   bool force_halo = false;               // MDR_OPT_FORCE_HALO: sharded actor halo exchange at world 1
+  bool halo_overlap = true;              // MDR_OPT_HALO_OVERLAP: sharded actor tick, halo beside the interior tiles
   int thermal = MDR_THERMAL_AFFINE;      // MDR_OPT_WINDOW_THERMAL: k_step_window's per-tick update
   int win = kWindowMax;                  // ticks per k_step_window launch (0: one-tick path)
   unsigned long long* d_wslab = nullptr; // 3 window count slots (mdr_kernels.hip K1W: slab | red | rec)
@@ -537,6 +538,7 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_SHARDED_OVERLAP: c->tick_overlap = value != 0; break;
     case MDR_OPT_GREEDY_SORT: c->greedy_sort = value != 0; break;
     case MDR_OPT_FORCE_HALO: c->force_halo = value != 0; break;
+    case MDR_OPT_HALO_OVERLAP: c->halo_overlap = value != 0; break;
     case MDR_OPT_WINDOW_THERMAL:
       if (value != MDR_THERMAL_EXACT && value != MDR_THERMAL_AFFINE)
         return fail(MDR_EARG, "mdr_set_option: WINDOW_THERMAL must be MDR_THERMAL_EXACT or _AFFINE");
@@ -1312,13 +1314,11 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
                        c->g_sel, slab);
     LAUNCH_CHECK("k_gq_bins");
     const int nstage = (n + kGqStage - 1) / kGqStage;
-    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
-                       c->g_sel, c->g_win, action, slab);
-    LAUNCH_CHECK("k_gq_compact");
-    hipLaunchKernelGGL(k_gq_select, dim3(kGqSelBlocks), dim3(1024), 0, st, c->kp, c->g_win, c->g_sorted, budget, pmin,
-                       c->g_sel, action, slab, c->g_hist, (const uint4*)nullptr, 0, c->g_tickets,
-                       (const double*)c->g_part, c->gq_nparts, c->g_map);
-    LAUNCH_CHECK("k_gq_select");
+    // compact + (its last block) the select and decision: two launches per decision
+    hipLaunchKernelGGL(k_gq_compact<true>, dim3(nstage), dim3(kGqThreads), kGqCap * sizeof(uint4), st, c->kp,
+                       gq_codes(c), c->g_hist, budget, c->g_sel, c->g_win, action, slab, pmin, c->g_sorted,
+                       c->g_tickets, (const double*)c->g_part, c->gq_nparts, c->g_map);
+    LAUNCH_CHECK("k_gq_compact (fused select)");
     c->counts_ready = true;
     return MDR_OK;
   }
@@ -1423,8 +1423,9 @@ int mdr_gq_shard_compact(mdr_ctx* c, double budget, uint8_t* action, void* strea
   if (!c->g_sel) return fail(MDR_ESTATE, "mdr_gq_shard_compact: call mdr_gq_shard_begin first");
   hipStream_t st = S(stream);
   const int nstage = (int)((c->kp.n + kGqStage - 1) / kGqStage);
-  hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
-                     c->g_sel, c->g_win + 1, action, (unsigned long long*)nullptr);
+  hipLaunchKernelGGL(k_gq_compact<false>, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist,
+                     budget, c->g_sel, c->g_win + 1, action, (unsigned long long*)nullptr, 0.0, (uint4*)nullptr,
+                     (unsigned*)nullptr, (const double*)nullptr, 0, (uint32_t*)nullptr);
   LAUNCH_CHECK("k_gq_compact (sharded)");
   // the window's header {count, 0, 0, 0}: the allocator's final count
   HIP_TRY(hipMemsetAsync(c->g_win, 0, sizeof(uint4), st));
@@ -1869,10 +1870,19 @@ int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
   return MDR_OK;
 }
 
-#define MDR_ACTOR_KERNELS(MB, KS)                                                                      \
-  (const void*)k_actor<1, false, MB, KS>, (const void*)k_actor<3, false, MB, KS>,                         \
-      (const void*)k_actor<6, false, MB, KS>, (const void*)k_actor<1, true, MB, KS>,                      \
-      (const void*)k_actor<3, true, MB, KS>, (const void*)k_actor<6, true, MB, KS>
+#define MDR_ACTOR_KERNELS_D(MB, KS, D)                                                                 \
+  (const void*)k_actor<1, false, MB, KS, D>, (const void*)k_actor<3, false, MB, KS, D>,                   \
+      (const void*)k_actor<6, false, MB, KS, D>, (const void*)k_actor<1, true, MB, KS, D>,                \
+      (const void*)k_actor<3, true, MB, KS, D>, (const void*)k_actor<6, true, MB, KS, D>
+#define MDR_ACTOR_KERNELS(MB, KS) MDR_ACTOR_KERNELS_D(MB, KS, false)
+
+// the obs layout k_actor<..., DEF = true> fixes at compile time: the reference's defaults (the
+// 'neighbours' ring, messages of 4 features, no hvac / solar / thermal state features), <= 64 slots
+static bool actor_def_layout(const mdr_obs_spec* sp, const ActorDims& d) {
+  return sp->comm_mode == MDR_COMM_RING && sp->n_comm > 0 && !sp->hvac_state && !sp->solar_state &&
+         !sp->thermal_state && !sp->msg_thermal && !sp->msg_hvac && d.ring && d.msg_w == 4 && d.n_own == 10 &&
+         d.ks1 == 2;
+}
 
 // The general actor as a chain of launches (mdr_actor.hip "chain"): obs rows (into out.obs when the
 // caller keeps them), one k_dense per hidden layer (ping-pong row buffers), k_actor_head.
@@ -1922,21 +1932,30 @@ int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const dou
   ActorDims d;
   int nw = 0;
   if (int rc = actor_plan(c, sp, &d, &nw)) return rc;
-  const int64_t ntile = (c->kp.n + 32 * nw - 1) / (32 * nw);  // blocks with at least one tile per wave
-  const unsigned grid = (unsigned)std::min<int64_t>(ntile, (int64_t)c->n_cu);
+  const int64_t ntile_all = (c->kp.n + 31) / 32;
+  const int64_t nv = out.tiles == 1 ? ntile_all - 2 : out.tiles == 2 ? 2 : ntile_all;  // (ActorOut.tiles)
+  const int64_t ntile = (nv + nw - 1) / nw;  // blocks with at least one tile per wave
+  const unsigned grid = (unsigned)std::max<int64_t>(1, std::min<int64_t>(ntile, (int64_t)c->n_cu));
   static bool lds_attr = false;  // > 64 KiB of dynamic LDS must be opted into per kernel
   if (!lds_attr) {
     for (const void* k : {MDR_ACTOR_KERNELS(7, 2), MDR_ACTOR_KERNELS(7, 3), MDR_ACTOR_KERNELS(7, 4),
-                          MDR_ACTOR_KERNELS(8, 2), MDR_ACTOR_KERNELS(8, 3), MDR_ACTOR_KERNELS(8, 4)})
+                          MDR_ACTOR_KERNELS(8, 2), MDR_ACTOR_KERNELS(8, 3), MDR_ACTOR_KERNELS(8, 4),
+                          MDR_ACTOR_KERNELS_D(7, 2, true), MDR_ACTOR_KERNELS_D(8, 2, true)})
       HIP_TRY(hipFuncSetAttribute(k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     lds_attr = true;
   }
 #define MDR_LAUNCH_ACTOR_S(P, F, MB, KS)                                                                     \
-  hipLaunchKernelGGL((k_actor<P, F, MB, KS>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
+  hipLaunchKernelGGL((k_actor<P, F, MB, KS, false>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
                      c->d_actor, out, tick, tkp)
+#define MDR_LAUNCH_ACTOR_DEF(P, F, MB)                                                                        \
+  hipLaunchKernelGGL((k_actor<P, F, MB, 2, true>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
+                     c->d_actor, out, tick, tkp)
+  const bool def = actor_def_layout(sp, d);
 #define MDR_LAUNCH_ACTOR(P, F)                                 \
   do {                                                         \
-    if (d.mb == 7 && d.ks1 == 2) MDR_LAUNCH_ACTOR_S(P, F, 7, 2); \
+    if (def && d.mb == 7) MDR_LAUNCH_ACTOR_DEF(P, F, 7);         \
+    else if (def) MDR_LAUNCH_ACTOR_DEF(P, F, 8);                 \
+    else if (d.mb == 7 && d.ks1 == 2) MDR_LAUNCH_ACTOR_S(P, F, 7, 2); \
     else if (d.mb == 7 && d.ks1 == 3) MDR_LAUNCH_ACTOR_S(P, F, 7, 3); \
     else if (d.mb == 7) MDR_LAUNCH_ACTOR_S(P, F, 7, 4);          \
     else if (d.ks1 == 2) MDR_LAUNCH_ACTOR_S(P, F, 8, 2);         \
@@ -1955,6 +1974,7 @@ int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const dou
   }
 #undef MDR_LAUNCH_ACTOR
 #undef MDR_LAUNCH_ACTOR_S
+#undef MDR_LAUNCH_ACTOR_DEF
   LAUNCH_CHECK("k_actor");
   return MDR_OK;
 }
@@ -2194,17 +2214,35 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
   const ObsArgs o = obs_args(c, &spec, &osc[0]);
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
   c->ring = 0;
+  // overlap (fused actor, >= 4 tiles, a comm stream): per tick the halo is packed and exchanged on the
+  // comm stream while the interior tiles' actor runs on the compute stream; the first and last
+  // tile (the only readers of the halo: lo, hi <= 32) follow once it has landed
+  const bool overlap = halo && c->halo_overlap && c->comm_stream && actor_fused_ok(c, &spec) &&
+                       (c->kp.n + 31) / 32 >= 4;
+  hipStream_t cs = c->comm_stream;
   for (int t = 0; t < n; ++t) {
-    if (halo) {
+    ObsArgs ot = o;
+    ot.sc_dev = c->d_obs_sc + 4 * t;
+    ActorOut out{action ? action + (int64_t)t * act_stride : c->d_act,
+                 prob ? prob + (int64_t)t * prob_stride : nullptr, nullptr, nullptr, slab_at(c, c->ring), nullptr};
+    if (overlap) {
+      HIP_TRY(hipEventRecord(c->ev_pc, st));  // the state after the previous step
+      HIP_TRY(hipStreamWaitEvent(cs, c->ev_pc, 0));
+      hipLaunchKernelGGL(k_halo_pack, dim3(1), dim3(64), 0, cs, c->kp, o, lo, hi, mine);
+      LAUNCH_CHECK("k_halo_pack");
+      ActorOut in = out;
+      in.tiles = 1;  // (issued before the exchange: host collectives block in comm_halo)
+      if (int rc = launch_actor(c, &spec, ot, p_dev, 0, c->d_ticks + t, in, st)) return rc;
+      if (int rc = comm_halo(c, mine, recv, lo, hi, M, cs)) return rc;
+      HIP_TRY(hipEventRecord(c->ev_ar[0], cs));
+      HIP_TRY(hipStreamWaitEvent(st, c->ev_ar[0], 0));
+      out.tiles = 2;
+    } else if (halo) {
       hipLaunchKernelGGL(k_halo_pack, dim3(1), dim3(64), 0, st, c->kp, o, lo, hi, mine);
       LAUNCH_CHECK("k_halo_pack");
       // the previous rank's last lo houses come first in the halo, the next rank's first hi after
       if (int rc = comm_halo(c, mine, recv, lo, hi, M, st)) return rc;
     }
-    ObsArgs ot = o;
-    ot.sc_dev = c->d_obs_sc + 4 * t;
-    ActorOut out{action ? action + (int64_t)t * act_stride : c->d_act,
-                 prob ? prob + (int64_t)t * prob_stride : nullptr, nullptr, nullptr, slab_at(c, c->ring), nullptr};
     if (int rc = launch_actor(c, &spec, ot, p_dev, 0, c->d_ticks + t, out, st)) return rc;
     if (int rc = comm_allreduce(c, slab_at(c, c->ring), c->slab_len, 0, st)) return rc;
     if (int rc = launch_step(c, out.action, MDR_ACT_BUFFER, TickArgs{}, c->d_ticks + t,

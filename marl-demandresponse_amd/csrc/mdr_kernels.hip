@@ -2049,10 +2049,31 @@ __device__ __forceinline__ void gq_next_map(const KParams& p, unsigned* __restri
 // as not taken (k_gq_select sets the window's), the window's houses go to win[] as (okey,
 // house << 2 | class, FSM word) at slots from one allocator atomic per block (unordered: select
 // orders them), and the ON houses of the decided (non-window) houses are counted into the slab
+__device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, double S, double pmin,
+                          GqSel* __restrict__ sel, uint8_t* __restrict__ action, unsigned long long* __restrict__ slab,
+                          uint4* s_e, bool sharded, bool ovf0, bool all, int ncand, double win_tot, bool more_after,
+                          bool in_lds);
+__device__ __forceinline__ void gq_store_sc1(uint4* d, const uint4& v);
+__device__ __forceinline__ uint4 gq_load_sc1(const uint4* s);
+__device__ __forceinline__ bool gq_less(const uint4& a, const uint4& b);
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* d, T v) { __hip_atomic_store(d, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* s) { return __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+__device__ void gq_compact_tail(const KParams& p, double S, double pmin, GqSel* __restrict__ sel,
+                                const uint4* __restrict__ win, uint4* __restrict__ sorted, uint8_t* __restrict__ action,
+                                unsigned long long* __restrict__ slab, unsigned* __restrict__ tickets,
+                                unsigned* __restrict__ hist, const double* __restrict__ part, int nparts,
+                                uint32_t* __restrict__ map);
+
+template <bool FUSED>
 __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint32_t* __restrict__ code,
                                                            unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
                                                            uint4* __restrict__ win, uint8_t* __restrict__ action,
-                                                           unsigned long long* __restrict__ slab) {
+                                                           unsigned long long* __restrict__ slab, double pmin,
+                                                           uint4* __restrict__ sorted, unsigned* __restrict__ tickets,
+                                                           const double* __restrict__ part, int nparts,
+                                                           uint32_t* __restrict__ map) {
   static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
   static_assert(kGqCopies * 512 <= kGqBins * 4, "the bin copies fit below the superbin copies");
   constexpr int NW = kGqThreads / 64;
@@ -2130,24 +2151,27 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     const int cnt = (int)__shfl(pre, le);
     const bool wovf = !(fit & 1ull);
     if (lane == 0) s_le = wovf ? -1 : le;
-    if (lane == 0 && blockIdx.x == 0) {
-      if (wovf) sel->overflow = 1;
-      sel->bstar = bb + l0;
-      sel->bend = bb + l0 + le;
-      sel->win_tot = s_base;
-      sel->more_after = s_basec + (unsigned long long)cnt < sel->total;
-      sel->ncand = cnt;
+    if (lane == 0 && blockIdx.x == 0) {  // (sc1: the fused form's last block reads them in this launch)
+      if (wovf) st_sc1(&sel->overflow, 1);
+      st_sc1(&sel->bstar, bb + l0);
+      st_sc1(&sel->bend, bb + l0 + le);
+      st_sc1(&sel->win_tot, s_base);
+      st_sc1(&sel->more_after, s_basec + (unsigned long long)cnt < sel->total ? 1 : 0);
+      st_sc1(&sel->ncand, cnt);
     }
   }
   if (whole && blockIdx.x == 0 && tid == 0) {  // every house is in the window
-    sel->bstar = 0;
-    sel->bend = kGqBins;
-    sel->win_tot = 0.0;
-    sel->more_after = 0;
-    sel->ncand = (int)sel->total;
+    st_sc1(&sel->bstar, 0);
+    st_sc1(&sel->bend, kGqBins);
+    st_sc1(&sel->win_tot, 0.0);
+    st_sc1(&sel->more_after, 0);
+    st_sc1(&sel->ncand, (int)sel->total);
   }
   __syncthreads();
-  if (ovf || s_le < 0) return;  // the fallback in k_gq_select decides every house (block-uniform)
+  if (ovf || s_le < 0) {  // the fallback (gq_exact) decides every house (block-uniform)
+    if (FUSED) gq_compact_tail(p, S, pmin, sel, win, sorted, action, slab, tickets, hist, part, nparts, map);
+    return;
+  }
   const int bs = whole ? -1 : bb + s_l0, be = whole ? kGqBins : bb + s_l0 + s_le;
   unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
   bool inw[U];
@@ -2202,11 +2226,13 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     if (!inw[u]) continue;
     const uint32_t i = (uint32_t)(p.goff + b0 + u * kGqThreads + tid);  // (global id: the order's tie-break)
     const uint64_t ok = gq_okey(kk[u]);
-    if (j < (unsigned)kGqCap) win[j] = make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), (i << 2) | (cd[u] & 3u), hw[u]);
+    // (sc1: the fused form's last block loads them in this launch)
+    if (j < (unsigned)kGqCap) gq_store_sc1(win + j, make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), (i << 2) | (cd[u] & 3u), hw[u]));
     ++j;
   }
   if (slab && tid < p.n_cap && s_cnt[tid])
     atomicAdd(&slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)s_cnt[tid]);
+  if (FUSED) gq_compact_tail(p, S, pmin, sel, win, sorted, action, slab, tickets, hist, part, nparts, map);
 }
 
 // 16-B window entries handed between workgroups of one launch as two 8-B agent-scope (sc1) accesses
@@ -2400,9 +2426,10 @@ __device__ void gq_exact(const KParams& p, double S, double pmin, uint8_t* __res
 // rule); the ON counts of the window's decided actions; what the window cannot decide goes to
 // gq_exact (sharded: to the host, GqSel.need_fb — one shard cannot order the whole cluster).  The
 // window carries global house ids: only this shard's houses are written (offset p.goff).
-__device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, double S, double pmin,
-                          GqSel* __restrict__ sel, uint8_t* __restrict__ action,
-                          unsigned long long* __restrict__ slab, uint4* s_e, bool sharded, bool ovf0) {
+__device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, double S, double pmin,
+                          GqSel* __restrict__ sel, uint8_t* __restrict__ action, unsigned long long* __restrict__ slab,
+                          uint4* s_e, bool sharded, bool ovf0, bool all, int ncand, double win_tot, bool more_after,
+                          bool in_lds) {
   __shared__ uint8_t s_tk[kGqCap];
   __shared__ double s_w[16];
   __shared__ double s_tot;
@@ -2417,25 +2444,28 @@ __device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restr
     const uint32_t cl = z & 3u;
     return cl == 0u ? pon[0] : cl == 1u ? pon[1] : cl == 2u ? pon[2] : pon[3];
   };
-  const bool all = sel->all;
   bool ovf = ovf0;
   if (!all && !ovf) {
-    const int ncand = sel->ncand;
     {
       constexpr int U = kGqCap / 1024;  // (blockDim 1024: every load issued before the LDS stores)
       uint4 v[U];
+      if (!in_lds) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = tid + u * 1024;
-        if (e < ncand) v[u] = gq_load_sc1(sorted + e);  // (sc1: written by other workgroups of this launch)
+        for (int u = 0; u < U; ++u) {
+          const int e = tid + u * 1024;
+          if (e < ncand) v[u] = gq_load_sc1(sorted + e);  // (sc1: written by other workgroups of this launch)
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int e = tid + u * 1024;
-        if (e < ncand) { s_e[e] = v[u]; s_tk[e] = 0; }
+        if (e < ncand) {
+          if (!in_lds) s_e[e] = v[u];
+          s_tk[e] = 0;
+        }
       }
     }
-    if (tid == 0) { s_tot = sel->win_tot; s_k = -1; }
+    if (tid == 0) { s_tot = win_tot; s_k = -1; }
     if (tid < kWinCap) s_cnt[tid] = 0u;
     __syncthreads();
     for (int c0 = 0; c0 < ncand; c0 += nth) {
@@ -2480,7 +2510,7 @@ __device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restr
             tot += pj;
           }
         }
-        if (j >= ncand && sel->more_after && !gq_walk_over(tot, S, pmin)) o = 1;
+        if (j >= ncand && more_after && !gq_walk_over(tot, S, pmin)) o = 1;
       }
       s_ovf = o;
     }
@@ -2517,10 +2547,81 @@ __device__ __forceinline__ void gq_decide(const KParams& p, const uint4* __restr
     if (ovf && sharded) sel->need_fb = 1u;
     sel->overflow = 0;       // (the next call starts clear)
     sel->calls += 1u;
-    if (!all && !ovf) sel->ncand_sum += (unsigned long long)sel->ncand;
+    if (!all && !ovf) sel->ncand_sum += (unsigned long long)ncand;
   }
 }
 
+
+
+// The single-GPU select inside k_gq_compact<true> (mdr_ctrl_greedy: two launches per decision, no
+// k_gq_select): the LAST compact block to take a ticket loads the window into LDS, ranks it in
+// (key, house) order (a wave per four entries, its lanes splitting the comparisons) into sorted[],
+// and decides (gq_decide); it then zeroes the bin copies every compact block has read.  Block 0,
+// after its own work, builds the next call's key map beside the decision.  Hand-off (MI355X_MICROARCH.md
+// Valid forms, row 1): every window entry and the sel fields read here were stored sc1 by their
+// block before that block's drained ticket add, and are loaded here with sc1 loads only.
+__device__ void gq_compact_tail(const KParams& p, double S, double pmin, GqSel* __restrict__ sel,
+                                const uint4* __restrict__ win, uint4* __restrict__ sorted, uint8_t* __restrict__ action,
+                                unsigned long long* __restrict__ slab, unsigned* __restrict__ tickets,
+                                unsigned* __restrict__ hist, const double* __restrict__ part, int nparts,
+                                uint32_t* __restrict__ map) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char gq_dyn[];  // kGqCap entries (dynamic LDS)
+  uint4* s_e = reinterpret_cast<uint4*>(gq_dyn);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (grid_last_block(tickets)) {  // (block-uniform)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only: the loads below are sc1)
+    const bool all = ld_sc1(&sel->all) != 0, ovf0 = ld_sc1(&sel->overflow) != 0;
+    const int ncand = ld_sc1(&sel->ncand);
+    const double wt = ld_sc1(&sel->win_tot);
+    const bool more = ld_sc1(&sel->more_after) != 0;
+    if (!all && !ovf0) {
+      constexpr int U = kGqCap / kGqThreads;
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kGqThreads;
+        if (e < ncand) v[u] = gq_load_sc1(win + e);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int e = tid + u * kGqThreads;
+        if (e < ncand) s_e[e] = v[u];
+      }
+      __syncthreads();
+      constexpr int B = 4, NW = kGqThreads / 64;
+      for (int e0 = wv * B; e0 < ncand; e0 += NW * B) {  // (wave-uniform)
+        uint4 me[B];
+        unsigned rk[B];
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+          me[b] = e0 + b < ncand ? s_e[e0 + b] : make_uint4(~0u, ~0u, ~0u, 0u);
+          rk[b] = 0u;
+        }
+        for (int f = lane; f < ncand; f += 64) {
+          const uint4 o = s_e[f];
+#pragma unroll
+          for (int b = 0; b < B; ++b) rk[b] += gq_less(o, me[b]) ? 1u : 0u;
+        }
+#pragma unroll
+        for (int b = 0; b < B; ++b) {
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) rk[b] += __shfl_xor(rk[b], off);
+          if (lane == 0 && e0 + b < ncand && rk[b] < (unsigned)kGqCap) gq_store_sc1(sorted + rk[b], me[b]);
+        }
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this block's sorted[] stores, before gq_decide's loads)
+      __syncthreads();
+    }
+    gq_decide(p, sorted, S, pmin, sel, action, slab, s_e, false, ovf0, all, ncand, wt, more, false);
+    __syncthreads();
+    for (int e = tid; e < kGqCopies * 512; e += blockDim.x) hist[e] = 0u;  // (read by every compact block)
+  }
+  static_assert(kGqMapLds <= kGqCap * 16, "the map's work areas fit the window array");
+  if (blockIdx.x == 0) {
+    __syncthreads();  // (a decision by this block has finished with s_e)
+    gq_next_map(p, hist, part, nparts, sel, map, gq_dyn);
+  }
+}
 
 // K4 (kGqSelBlocks workgroups of 1024): every block loads compact's unordered window win[0, ncand)
 // into LDS and ranks kGqCap / (kGqSelBlocks * 16) of its houses per wave (how many window houses
@@ -2613,7 +2714,8 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
   // with sc1 loads (gq_decide), so no fence is needed
   if (grid_last_block(tickets)) {  // (block-uniform)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only)
-    gq_decide(p, sorted, S, pmin, sel, action, slab, s_e, gathered != nullptr, ovf0);
+    gq_decide(p, sorted, S, pmin, sel, action, slab, s_e, gathered != nullptr, ovf0, sel->all != 0, ncand,
+              sel->win_tot, sel->more_after != 0, false);
   }
   // the next call's key map, by block 0 (dispatched first, it is rarely the last to take a ticket:
   // the map's ~2 us run beside the decision instead of before it, as they did in k_gq_bins)
@@ -2623,6 +2725,11 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
     gq_next_map(p, hist, part, nparts, sel, map, reinterpret_cast<unsigned char*>(s_e));
   }
 }
+
+template __global__ void k_gq_compact<true>(KParams, const uint32_t*, unsigned*, double, GqSel*, uint4*, uint8_t*,
+                                             unsigned long long*, double, uint4*, unsigned*, const double*, int, uint32_t*);
+template __global__ void k_gq_compact<false>(KParams, const uint32_t*, unsigned*, double, GqSel*, uint4*, uint8_t*,
+                                              unsigned long long*, double, uint4*, unsigned*, const double*, int, uint32_t*);
 
 // sharded greedy (mdr_greedy_inputs / mdr_greedy_select): this shard's (key, P, lockout) rows, and
 // the generic gather / iota for the cluster-wide selection over the gathered rows

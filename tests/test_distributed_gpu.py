@@ -226,9 +226,11 @@ def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo, laye
     from mdr_amd.environment import Environment
 
     env = Environment(g.props_from_overrides(_overrides(n, "individual_L2")), device=dev, rng=random.Random(4),
-                      population="synthetic", seed=77, rank=rank, world=world, comm=make_comm(kind))
+                      population="synthetic", seed=77, rank=rank, world=world, comm=make_comm(_comm_kind(kind)))
     if force_halo:
         env.shard.set_option("force_halo", 1)
+    if kind.endswith("-serialhalo"):  # MDR_OPT_HALO_OVERLAP off: halo, then one k_actor per tick
+        env.shard.set_option("halo_overlap", 0)
     res = _actor_run(env, torch, dist, layers)
     res["lo"] = env._offset
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
@@ -240,7 +242,8 @@ def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo, laye
     ("nccl", "rccl", 1, True, 3001, (100, 100)),    # + the ring-halo pack / ncclSend / ncclRecv (to self)
     ("gloo", "torch", 2, False, 3001, (100, 100)),  # two shards on cuda:0, per-tick Python loop, P2P halo
     ("gloo", "torch", 3, False, 3001, (100, 100)),  # distinct left / right peers
-    ("gloo", "host", 3, False, 3001, (100, 100)),   # the C loop (halo pack -> send/recv -> actor -> allreduce -> step)
+    ("gloo", "host", 3, False, 3001, (100, 100)),   # the C loop: halo on the side stream beside the interior tiles
+    ("gloo", "host-serialhalo", 3, False, 3001, (100, 100)),  # halo pack -> send/recv -> actor -> allreduce -> step
     ("gloo", "host", 3, False, 3001, (64, 64, 64)),  # the layer chain (k_obs reads the halo) in the C loop
     ("gloo", "host", 8, False, 8 * 131072, (100, 100)),  # C5: the 1,048,576-house cluster on 8 ranks
 ])
