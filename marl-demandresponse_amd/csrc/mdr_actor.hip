@@ -205,13 +205,13 @@ __device__ __forceinline__ void split_operand(const float* v, bf16x8* s) {
 // compile time: the optional features' branches and their uniform operands leave the kernel (the
 // generic form spills ~127 SGPRs into VGPR lanes, reloaded by v_readlane in the tile loop; DEF 19).
 template <int PREC, bool PROF, int MB, int KS1, bool DEF>
-__global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
+__global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KParams p, ObsArgs o, ActorDims d, const double* p_dev,
                                                const unsigned char* __restrict__ wpack, ActorOut out,
                                                uint64_t tick0, const TickArgs* tkp) {
   if (DEF) {  // (the host launches DEF only for this layout: mdr_capi.hip actor_def_layout)
     o.hvac_state = 0; o.solar_state = 0; o.thermal_state = 0; o.msg_thermal = 0; o.msg_hvac = 0;
     o.comm_mode = MDR_COMM_RING; o.msg_w = 4; o.comm_table = nullptr; o.msg_all = nullptr;
-    d.ring = 1; d.m4 = 4; d.msg_w = 4; d.n_own = 10; d.own4 = 12; d.nf = PREC == 6 ? 3 : 2;
+    d.ring = 1; d.m4 = 4; d.msg_w = 4; d.n_own = 10; d.own4 = 12; d.rs = 20; d.nf = PREC == 6 ? 3 : 2;
   }
   static_assert(MB >= 1 && MB <= kActorMaxMB, "row blocks");
   static_assert(KS1 >= 1 && KS1 <= kActorMaxSlots / 32, "layer-1 k-steps");
@@ -337,7 +337,7 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     }
   };
   // ---- the stages of a tile (mdr_actor.hip header: the ping-pong schedule below)
-  f32x4 acc2[MB][2];  // layer 2 of the tile between its X and Y stages
+  f32x2 zz[2];  // the tile's two logits per column block (partial over this lane's rows) between X and Y
   // build: the tile's LDS rows from the prefetched sources (+ the table topologies' gathers)
   auto stage_build = [&](uint32_t tl) {
     const uint32_t b0 = tl * 32u;
@@ -384,89 +384,114 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     // (the wave in its MFMA stage gets VALU issue priority over the SIMD's other wave, which is then
     // building observations or running the output layer)
     __builtin_amdgcn_s_setprio(2);
-    // ---- layer 1: acc1[mb][cb] = b1 + W1 · X  (X^T columns = this wave's 32 houses, two column blocks).
-    // The (k-step, row block) fragments are step s = ks * MB + mb of the packed image; each step's
-    // weight fragments are read from LDS two steps ahead (a ring of three), so the MFMAs of one wave
-    // do not wait out the LDS latency.
+    // ---- layer 1: acc1 = b1 + W1 · X  (X^T columns = this wave's 32 houses, two column blocks), row
+    // block by row block (mb-major: one block's accumulators live at a time); each pair of finished
+    // blocks (2q, 2q + 1) becomes layer 2's B fragment of k-step q at once (ReLU + split, VALU work
+    // that overlaps the next block's MFMAs).  Weight fragments (packed k-step-major: step (ks, mb) =
+    // fragment ks * MB + mb) are read from LDS two steps ahead (a ring of three), so the MFMAs of one
+    // wave do not wait out the LDS latency.
     constexpr int PF = 2;  // prefetch distance (steps)
-    f32x4 acc1[MB][2];
+    bf16x8 hs[KS2][2][NS];
     {
+      bf16x8 xs[KS1][2][NS];
+#pragma unroll
+      for (int ks = 0; ks < KS1; ++ks)
+#pragma unroll
+        for (int cb = 0; cb < 2; ++cb) {
+          float xv[8];
+#pragma unroll
+          for (int e = 0; e < 2; ++e) {
+            const int a = xoff[ks][e] + cb * xstep[ks][e];
+            const float4 x = *reinterpret_cast<const float4*>(w_row + a);
+            xv[4 * e] = x.x; xv[4 * e + 1] = x.y; xv[4 * e + 2] = x.z; xv[4 * e + 3] = x.w;
+          }
+          split_operand<PREC>(xv, xs[ks][cb]);
+        }
       constexpr int total = KS1 * MB;
+      auto frag1 = [&](int s, int e) { return lds_frag(s_w1, NF * ((s % KS1) * MB + s / KS1) + e, lane); };
       bf16x8 ring[PF + 1][NS];
 #pragma unroll
       for (int q = 0; q < PF; ++q)
 #pragma unroll
-        for (int e = 0; e < NS; ++e) ring[q][e] = lds_frag(s_w1, NF * q + e, lane);
-      bf16x8 xs[2][NS];
+        for (int e = 0; e < NS; ++e) ring[q][e] = frag1(q, e);
+      f32x4 acc1[2][2];  // row blocks 2q, 2q + 1 of the pair in progress
 #pragma unroll
       for (int st = 0; st < total; ++st) {
-        const int ks = st / MB, mb = st % MB;
-        if (mb == 0) {
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) {
-            float xv[8];
-#pragma unroll
-            for (int e = 0; e < 2; ++e) {
-              const int a = xoff[ks][e] + cb * xstep[ks][e];
-              const float4 x = *reinterpret_cast<const float4*>(w_row + a);
-              xv[4 * e] = x.x; xv[4 * e + 1] = x.y; xv[4 * e + 2] = x.z; xv[4 * e + 3] = x.w;
-            }
-            split_operand<PREC>(xv, xs[cb]);
-          }
-        }
+        const int mb = st / KS1, ks = st % KS1;
         if (st + PF < total)
 #pragma unroll
-          for (int e = 0; e < NS; ++e) ring[(st + PF) % (PF + 1)][e] = lds_frag(s_w1, NF * (st + PF) + e, lane);
+          for (int e = 0; e < NS; ++e) ring[(st + PF) % (PF + 1)][e] = frag1(st + PF, e);
         const bf16x8* as = ring[st % (PF + 1)];
+        f32x4* a1 = acc1[mb & 1];
         if (ks == 0) {
           const f32x4 bias = *reinterpret_cast<const f32x4*>(b1 + kActorRB * mb + 4 * g);
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc1[mb][cb] = mfma_split<PREC>(as, xs[cb], bias);
+          for (int cb = 0; cb < 2; ++cb) a1[cb] = mfma_split<PREC>(as, xs[ks][cb], bias);
         } else {
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc1[mb][cb] = mfma_split<PREC>(as, xs[cb], acc1[mb][cb]);
+          for (int cb = 0; cb < 2; ++cb) a1[cb] = mfma_split<PREC>(as, xs[ks][cb], a1[cb]);
+        }
+        if (ks == KS1 - 1 && ((mb & 1) || mb == MB - 1)) {  // the pair (or the odd last block) is done
+          const int q = mb >> 1;
+          const bool pair = (mb & 1) != 0;
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb) {
+            float v[8];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+              v[j] = relu(acc1[0][cb][j]);
+              v[4 + j] = pair ? relu(acc1[1][cb][j]) : 0.f;
+            }
+            split_operand<PREC>(v, hs[q][cb]);
+          }
         }
       }
     }
     PSTAMP(3);
 
-    // ---- ReLU + split: layer 1's accumulators become layer 2's B fragments in place
-    bf16x8 hs[KS2][2][NS];
-#pragma unroll
-    for (int q = 0; q < KS2; ++q)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        float v[8];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          v[j] = relu(acc1[2 * q][cb][j]);
-          v[4 + j] = 2 * q + 1 < MB ? relu(acc1[2 * q + 1][cb][j]) : 0.f;
-        }
-        split_operand<PREC>(v, hs[q][cb]);
-      }
-
-    // ---- layer 2: acc2[mb][cb] = b2 + W2 · relu(H1), steps st = q * MB + mb, fragments prefetched
+    // ---- layer 2 (acc2 = b2 + W2 · relu(H1)) fused with the output layer, row block by row block:
+    // as soon as a block's four k-steps are done its ReLU'd rows enter the two logits (fp32 VALU;
+    // (z0, z1) += (w0, w1) * (x, x) as one v_pk_fma_f32, in the block / row order of two scalar
+    // chains) while the next block's MFMAs run
     {
       constexpr int TOT = KS2 * MB;
+      auto frag2 = [&](int s, int e) { return lds_frag(s_w2, NF * ((s % KS2) * MB + s / KS2) + e, lane); };
       bf16x8 ring[PF + 1][NS];
 #pragma unroll
       for (int q = 0; q < PF; ++q)
 #pragma unroll
-        for (int e = 0; e < NS; ++e) ring[q][e] = lds_frag(s_w2, NF * q + e, lane);
+        for (int e = 0; e < NS; ++e) ring[q][e] = frag2(q, e);
+      f32x4 acc2[2];
+      zz[0] = f32x2{0.f, 0.f};
+      zz[1] = f32x2{0.f, 0.f};
 #pragma unroll
       for (int st = 0; st < TOT; ++st) {
-        const int q = st / MB, mb = st % MB;
+        const int mb = st / KS2, q = st % KS2;
         if (st + PF < TOT)
 #pragma unroll
-          for (int e = 0; e < NS; ++e) ring[(st + PF) % (PF + 1)][e] = lds_frag(s_w2, NF * (st + PF) + e, lane);
+          for (int e = 0; e < NS; ++e) ring[(st + PF) % (PF + 1)][e] = frag2(st + PF, e);
         const bf16x8* as = ring[st % (PF + 1)];
         if (q == 0) {
           const f32x4 bias = *reinterpret_cast<const f32x4*>(b2 + kActorRB * mb + 4 * g);
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc2[mb][cb] = mfma_split<PREC>(as, hs[q][cb], bias);
+          for (int cb = 0; cb < 2; ++cb) acc2[cb] = mfma_split<PREC>(as, hs[q][cb], bias);
         } else {
 #pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc2[mb][cb] = mfma_split<PREC>(as, hs[q][cb], acc2[mb][cb]);
+          for (int cb = 0; cb < 2; ++cb) acc2[cb] = mfma_split<PREC>(as, hs[q][cb], acc2[cb]);
+        }
+        if (q == KS2 - 1) {
+#pragma clang fp contract(fast)
+          const f32x2* wr = reinterpret_cast<const f32x2*>(w3 + (kActorRB * mb + 4 * g) * kActorNA);  // rows 4g .. 4g + 3
+          f32x2 w[4];
+#pragma unroll
+          for (int i = 0; i < 4; ++i) w[i] = wr[i];
+#pragma unroll
+          for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+              const float x = relu(acc2[cb][i]);
+              zz[cb] = __builtin_elementwise_fma(w[i], f32x2{x, x}, zz[cb]);
+            }
         }
       }
     }
@@ -479,28 +504,8 @@ __global__ void __launch_bounds__(512) k_actor(KParams p, ObsArgs o, ActorDims d
     const uint32_t b0 = tl * 32u;
     const int nb = (int)min(32u, n - b0);
     float z[2][kActorNA];
-    {
-      // both actions' sums as one packed pair (v_pk_fma_f32): (z0, z1) += (w0, w1) * (x, x), the
-      // same fused multiply-adds in the same order as two scalar chains
-#pragma clang fp contract(fast)
-      f32x2 zz[2] = {f32x2{0.f, 0.f}, f32x2{0.f, 0.f}};
 #pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        const f32x2* wr = reinterpret_cast<const f32x2*>(w3 + (kActorRB * mb + 4 * g) * kActorNA);  // rows 4g .. 4g + 3
-        f32x2 w[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = wr[i];
-#pragma unroll
-        for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            const float x = relu(acc2[mb][cb][i]);
-            zz[cb] = __builtin_elementwise_fma(w[i], f32x2{x, x}, zz[cb]);
-          }
-      }
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) { z[cb][0] = zz[cb].x; z[cb][1] = zz[cb].y; }
-    }
+    for (int cb = 0; cb < 2; ++cb) { z[cb][0] = zz[cb].x; z[cb][1] = zz[cb].y; }
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll

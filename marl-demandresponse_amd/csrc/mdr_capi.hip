@@ -1779,11 +1779,20 @@ ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw) 
   return d;
 }
 
+// the obs layout k_actor<..., DEF = true> fixes at compile time: the reference's defaults (the
+// 'neighbours' ring, messages of 4 features, no hvac / solar / thermal state features), <= 64 slots, rows of 20 floats
+bool actor_def_layout(const mdr_obs_spec* sp, const ActorDims& d) {
+  return sp->comm_mode == MDR_COMM_RING && sp->n_comm > 0 && !sp->hvac_state && !sp->solar_state &&
+         !sp->thermal_state && !sp->msg_thermal && !sp->msg_hvac && d.ring && d.msg_w == 4 && d.n_own == 10 &&
+         d.ks1 == 2 && d.rs == 20;
+}
+
 int actor_plan(const mdr_ctx* c, const mdr_obs_spec* sp, ActorDims* d, int* nw) {
   *d = actor_layout(c->actor, sp, 1);
   if (d->n_own < 0 || d->nslot > kActorMaxSlots)
     return fail(MDR_EARG, "mdr_actor: obs row wider than the actor's 128 feature slots");
-  for (int w = 8; w >= 1; --w) {
+  const int prec = c->actor.precision == MDR_PREC_FP32 ? 6 : c->actor.precision == MDR_PREC_BF16 ? 1 : 3;
+  for (int w = actor_max_waves(prec, actor_def_layout(sp, *d)); w >= 1; --w) {
     *d = actor_layout(c->actor, sp, w);
     if (d->lds_total <= 160 * 1024) { *nw = w; return MDR_OK; }
   }
@@ -1876,13 +1885,6 @@ int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
       (const void*)k_actor<3, true, MB, KS, D>, (const void*)k_actor<6, true, MB, KS, D>
 #define MDR_ACTOR_KERNELS(MB, KS) MDR_ACTOR_KERNELS_D(MB, KS, false)
 
-// the obs layout k_actor<..., DEF = true> fixes at compile time: the reference's defaults (the
-// 'neighbours' ring, messages of 4 features, no hvac / solar / thermal state features), <= 64 slots
-static bool actor_def_layout(const mdr_obs_spec* sp, const ActorDims& d) {
-  return sp->comm_mode == MDR_COMM_RING && sp->n_comm > 0 && !sp->hvac_state && !sp->solar_state &&
-         !sp->thermal_state && !sp->msg_thermal && !sp->msg_hvac && d.ring && d.msg_w == 4 && d.n_own == 10 &&
-         d.ks1 == 2;
-}
 
 // The general actor as a chain of launches (mdr_actor.hip "chain"): obs rows (into out.obs when the
 // caller keeps them), one k_dense per hidden layer (ping-pong row buffers), k_actor_head.
@@ -2083,7 +2085,7 @@ int mdr_actor_profile(mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_scalars*
   if (!c->bound) return fail(MDR_ESTATE, "mdr_actor_profile: context not bound");
   if (int rc = check_actor_obs(c, sp, "mdr_actor_profile", S(stream))) return rc;
   hipStream_t st = S(stream);
-  const int nb = c->n_cu * 8;  // waves (at most 8 per block, one block per CU)
+  const int nb = c->n_cu * 16;  // waves (at most 16 per block, one block per CU)
   unsigned long long* d = nullptr;
   HIP_TRY(hipMalloc(&d, (size_t)nb * 8 * sizeof(unsigned long long)));
   HIP_TRY(hipMemsetAsync(d, 0, (size_t)nb * 8 * sizeof(unsigned long long), st));

@@ -10,7 +10,9 @@ for t in 20 1; do
 done
 timeout -k 10 1500 python -u -m pytest -v --timeout 400 --timeout-method thread -m gpu tests > $O/pytest.log 2>&1; rc=$?
 tail -3 $O/pytest.log; grep -E "FAILED|ERROR" $O/pytest.log | head -20
-[ $rc -ge 2 ] && exit $rc
+[ $rc -ge 2 ] && timeout -k 10 180 python tools/actor_profile.py > $O/actor_prof.log 2>&1 || exit 1
+cat $O/actor_prof.log
+exit $rc
 for i in 1 2 3; do
   timeout -k 10 300 python bench.py --steps 20 --warmup 5 --no-cpu-baseline > $O/bench20_$i.log 2>&1 || exit 1
   python3 -c "import json,sys; d=json.loads(open('$O/bench20_$i.log').read().strip().splitlines()[-1]); r=d['roofline']; am=r.get('above_mall') or {}; print('bench20', round(d['value']/1e11,3), 'e11 k', round(r['kernel_avg_us'],1), 'frac', round(r['frac'],3), '16M k', round(am.get('kernel_avg_us',0),1), 'frac', round(am.get('frac',0),3))"
@@ -19,4 +21,6 @@ timeout -k 10 300 python bench.py --workload greedy --steps 50 --warmup 5 --no-c
 python3 -c "import json; d=json.loads(open('$O/greedy.log').read().strip().splitlines()[-1]); print('greedy', round(d['ms_per_step']*1e3,2), 'us/tick; kernel', round(d['roofline']['kernel_avg_us'],2), d.get('greedy_select'))"
 timeout -k 10 300 python bench.py --workload actor --steps 50 --warmup 5 --no-cpu-baseline > $O/actor.log 2>&1 || exit 1
 python3 -c "import json; d=json.loads(open('$O/actor.log').read().strip().splitlines()[-1]); print('actor', '%.3e' % d['value'], 'k_actor us', round(d['roofline']['kernel_avg_us'],1))"
+timeout -k 10 180 python tools/actor_profile.py > $O/actor_prof.log 2>&1 || exit 1
+cat $O/actor_prof.log
 exit $rc
