@@ -184,10 +184,41 @@ __device__ __forceinline__ f32x4 mfma_split(const bf16x8* a, const bf16x8* b, f3
   return mfma16(a[0], b[0], acc);
 }
 
+// scalar f32 ops the SLP vectorizer cannot pair into v_pk_* (beside MFMAs a v_pk_add_f32 / v_pk_fma_f32
+// costs ~22 cycles more than its two scalar halves: MI355X_MICROARCH.md, filler prices)
+__device__ __forceinline__ float sub_s(float a, float b) {
+  float d;
+  asm("v_sub_f32 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+  return d;
+}
+__device__ __forceinline__ float fma_s(float a, float b, float c) {
+  float d;
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
+
+// The per-tile activation split of the bf16x3 form: hi = x with its low 16 bits cleared (a bf16
+// value, so its conversion is exact), lo = bf16(x - hi) (the difference is exact).  Truncation
+// instead of rounding for hi: two VALU ops per value besides the (co-issued) packing conversions,
+// against 2.5 with a rounded hi; |lo| < 2^-7 |x| instead of 2^-8, which leaves the dropped lo·lo
+// product below 2^-16 of the term (bf16x3 stays within its 1e-4 probability tolerance).
+__device__ __forceinline__ void split8_trunc(const float* v, bf16x8& hi, bf16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float h = __uint_as_float(__float_as_uint(v[j]) & 0xffff0000u);
+    hi[j] = (__bf16)h;
+    lo[j] = (__bf16)sub_s(v[j], h);
+  }
+}
+
 template <int PREC>
 __device__ __forceinline__ void split_operand(const float* v, bf16x8* s) {
   if constexpr (PREC == 6) split8x3(v, s[0], s[1], s[2]);
+#ifdef MDR_ACTOR_RNE_SPLIT  // (A/B builds: the rounded-hi split of r03)
   else if constexpr (PREC == 3) split8(v, s[0], s[1]);
+#else
+  else if constexpr (PREC == 3) split8_trunc(v, s[0], s[1]);
+#endif
   else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[0][j] = (__bf16)v[j];
@@ -450,9 +481,8 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     PSTAMP(3);
 
     // ---- layer 2 (acc2 = b2 + W2 · relu(H1)) fused with the output layer, row block by row block:
-    // as soon as a block's four k-steps are done its ReLU'd rows enter the two logits (fp32 VALU;
-    // (z0, z1) += (w0, w1) * (x, x) as one v_pk_fma_f32, in the block / row order of two scalar
-    // chains) while the next block's MFMAs run
+    // as soon as a block's four k-steps are done its ReLU'd rows enter the two logits (scalar fp32
+    // FMAs in block / row order) while the next block's MFMAs run
     {
       constexpr int TOT = KS2 * MB;
       auto frag2 = [&](int s, int e) { return lds_frag(s_w2, NF * ((s % KS2) * MB + s / KS2) + e, lane); };
@@ -480,7 +510,6 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
           for (int cb = 0; cb < 2; ++cb) acc2[cb] = mfma_split<PREC>(as, hs[q][cb], acc2[cb]);
         }
         if (q == KS2 - 1) {
-#pragma clang fp contract(fast)
           const f32x2* wr = reinterpret_cast<const f32x2*>(w3 + (kActorRB * mb + 4 * g) * kActorNA);  // rows 4g .. 4g + 3
           f32x2 w[4];
 #pragma unroll
@@ -490,7 +519,8 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const float x = relu(acc2[cb][i]);
-              zz[cb] = __builtin_elementwise_fma(w[i], f32x2{x, x}, zz[cb]);
+              zz[cb].x = fma_s(w[i].x, x, zz[cb].x);
+              zz[cb].y = fma_s(w[i].y, x, zz[cb].y);
             }
         }
       }

@@ -89,6 +89,7 @@ struct mdr_ctx {
   bool tick_overlap = true;              // MDR_OPT_SHARDED_OVERLAP: per-tick sharded two-stream pipeline
   bool greedy_sort = false;              // MDR_OPT_GREEDY_SORT: the full-sort greedy form only
   bool force_halo = false;               // MDR_OPT_FORCE_HALO: sharded actor halo exchange at world 1
+  bool actor_generic = false;            // MDR_OPT_ACTOR_GENERIC: no default-layout k_actor form
   bool halo_overlap = true;              // MDR_OPT_HALO_OVERLAP: sharded actor tick, halo beside the interior tiles
   int thermal = MDR_THERMAL_AFFINE;      // MDR_OPT_WINDOW_THERMAL: k_step_window's per-tick update
   int win = kWindowMax;                  // ticks per k_step_window launch (0: one-tick path)
@@ -539,6 +540,7 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_GREEDY_SORT: c->greedy_sort = value != 0; break;
     case MDR_OPT_FORCE_HALO: c->force_halo = value != 0; break;
     case MDR_OPT_HALO_OVERLAP: c->halo_overlap = value != 0; break;
+    case MDR_OPT_ACTOR_GENERIC: c->actor_generic = value != 0; break;
     case MDR_OPT_WINDOW_THERMAL:
       if (value != MDR_THERMAL_EXACT && value != MDR_THERMAL_AFFINE)
         return fail(MDR_EARG, "mdr_set_option: WINDOW_THERMAL must be MDR_THERMAL_EXACT or _AFFINE");
@@ -1781,8 +1783,8 @@ ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw) 
 
 // the obs layout k_actor<..., DEF = true> fixes at compile time: the reference's defaults (the
 // 'neighbours' ring, messages of 4 features, no hvac / solar / thermal state features), <= 64 slots, rows of 20 floats
-bool actor_def_layout(const mdr_obs_spec* sp, const ActorDims& d) {
-  return sp->comm_mode == MDR_COMM_RING && sp->n_comm > 0 && !sp->hvac_state && !sp->solar_state &&
+bool actor_def_layout(const mdr_ctx* c, const mdr_obs_spec* sp, const ActorDims& d) {
+  return !c->actor_generic && sp->comm_mode == MDR_COMM_RING && sp->n_comm > 0 && !sp->hvac_state && !sp->solar_state &&
          !sp->thermal_state && !sp->msg_thermal && !sp->msg_hvac && d.ring && d.msg_w == 4 && d.n_own == 10 &&
          d.ks1 == 2 && d.rs == 20;
 }
@@ -1792,7 +1794,7 @@ int actor_plan(const mdr_ctx* c, const mdr_obs_spec* sp, ActorDims* d, int* nw) 
   if (d->n_own < 0 || d->nslot > kActorMaxSlots)
     return fail(MDR_EARG, "mdr_actor: obs row wider than the actor's 128 feature slots");
   const int prec = c->actor.precision == MDR_PREC_FP32 ? 6 : c->actor.precision == MDR_PREC_BF16 ? 1 : 3;
-  for (int w = actor_max_waves(prec, actor_def_layout(sp, *d)); w >= 1; --w) {
+  for (int w = actor_max_waves(prec, actor_def_layout(c, sp, *d)); w >= 1; --w) {
     *d = actor_layout(c->actor, sp, w);
     if (d->lds_total <= 160 * 1024) { *nw = w; return MDR_OK; }
   }
@@ -1952,7 +1954,7 @@ int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const dou
 #define MDR_LAUNCH_ACTOR_DEF(P, F, MB)                                                                        \
   hipLaunchKernelGGL((k_actor<P, F, MB, 2, true>), dim3(grid), dim3(64 * nw), d.lds_total, st, c->kp, o, d, p_dev, \
                      c->d_actor, out, tick, tkp)
-  const bool def = actor_def_layout(sp, d);
+  const bool def = actor_def_layout(c, sp, d);
 #define MDR_LAUNCH_ACTOR(P, F)                                 \
   do {                                                         \
     if (def && d.mb == 7) MDR_LAUNCH_ACTOR_DEF(P, F, 7);         \

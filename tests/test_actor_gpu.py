@@ -200,6 +200,39 @@ def test_actor_layer1_ksteps(torch_gpu, layout, precision):
     gu.assert_not_saturated(tp[:, 1])
 
 
+@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16"])
+def test_actor_default_layout_form_equals_generic(torch_gpu, precision):
+    """The k_actor form specialised for the reference's default obs layout (mdr_actor.hip DEF: its
+    layout fixed at compile time, 12 / 16 waves per block) == the generic form on the same inputs,
+    bit for bit: probabilities, actions, chosen probabilities and obs rows (MDR_OPT_ACTOR_GENERIC
+    switches between them; the ON counts of the new actions come from the same FSM code and are
+    checked on the default form by test_actor_count_next_equals_power_counts)."""
+    from mdr_amd.actor import DeviceActor
+
+    torch = torch_gpu
+    n = 40_000
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env = make_env(props, 13)
+    rs = np.random.RandomState(3)
+    for _ in range(4):
+        env.step_tensor(torch.from_numpy(rs.randint(0, 2, n).astype(np.uint8)).to("cuda"))
+    F = env.obs_spec().n_feat
+    actor = gu.calibrated_actor(F, env.obs_tensor().abs().amax(0).double().cpu().numpy(), seed=9).to("cuda")
+    da = DeviceActor(env, actor, precision=precision)
+    res = []
+    for generic in (0, 1):
+        env.shard.set_option("actor_generic", generic)
+        probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
+        obs = torch.empty((n, F), dtype=torch.float32, device="cuda")
+        act, prob = da.select_actions(probs=probs, obs_out=obs, count_next=False)
+        res.append((probs, obs, act.clone(), prob.clone()))
+    env.shard.set_option("actor_generic", 0)
+    for k, (x, y) in enumerate(zip(*res)):
+        assert torch.equal(x, y), k
+    gu.assert_not_saturated(res[0][0][:, 1].cpu().numpy(), res[0][2].cpu().numpy())
+
+
 def test_actor_sampling_statistics(torch_gpu):
     """Categorical sampling: the fraction of houses turning on matches the mean probability."""
     from mdr_amd.actor import DeviceActor
