@@ -738,7 +738,7 @@ static int wslab_clean(mdr_ctx* c, hipStream_t st) {
   return MDR_OK;
 }
 
-static unsigned win_grid(const mdr_ctx* c) { return blocks(blocks(c->kp.n, 64 * kWinHpt), 4); }  // a tile per wave
+static unsigned win_grid(const mdr_ctx* c, int waves = 4) { return blocks(blocks(c->kp.n, 64 * kWinHpt), waves); }  // a tile per wave
 
 // the first window's FSM count: ticks from tk (staged) or tick0 + j (tk == nullptr), from the
 // state's FSM words (w_in == nullptr) or from the end words of the previous window
@@ -752,10 +752,10 @@ static unsigned long long* win_red_ptr(const mdr_ctx* c, unsigned long long* slo
 static int launch_count(mdr_ctx* c, int mode, const uint8_t* action, int64_t act_stride, const TickArgs* tk,
                         uint64_t tick0, int K, unsigned long long* slot, uint64_t* onb, uint32_t* wah,
                         const uint32_t* w_in, hipStream_t st, bool p_only = false) {
-  const unsigned grid = win_grid(c);
+  const unsigned grid = win_grid(c, kCountWaves);
   unsigned* ticket = p_only ? c->d_tickets : nullptr;
 #define MDR_COUNT(A)                                                                                  \
-  hipLaunchKernelGGL((k_count_window<A, kWinHpt>), dim3(grid), dim3(256), 0, st, c->kp, action, act_stride, tk, \
+  hipLaunchKernelGGL((k_count_window<A, kWinHpt>), dim3(grid), dim3(64 * kCountWaves), 0, st, c->kp, action, act_stride, tk, \
                      tick0, K, slot, onb, wah, w_in, ticket)
   if (mode == MDR_ACT_RANDOM) MDR_COUNT(MDR_ACT_RANDOM);
   else if (mode == MDR_ACT_ALWAYS_ON) MDR_COUNT(MDR_ACT_ALWAYS_ON);
@@ -1309,18 +1309,27 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   unsigned long long* slab = slab_at(c, c->ring);  // the counts of the actions decided here
   if (c->kp.n_cap <= 4 && !c->greedy_sort) {
     // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster, no host
-    // synchronisation; k_gq_select decides exactly what the candidate window cannot
+    // synchronisation; k_gq_select1 decides exactly what the candidate window cannot
     if (!keys_ready)
       if (int rc2 = launch_gq_keys(c, st)) return rc2;
     hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
                        c->g_sel, slab);
     LAUNCH_CHECK("k_gq_bins");
     const int nstage = (n + kGqStage - 1) / kGqStage;
-    // compact + (its last block) the select and decision: two launches per decision
-    hipLaunchKernelGGL(k_gq_compact<true>, dim3(nstage), dim3(kGqThreads), kGqCap * sizeof(uint4), st, c->kp,
-                       gq_codes(c), c->g_hist, budget, c->g_sel, c->g_win, action, slab, pmin, c->g_sorted,
-                       c->g_tickets, (const double*)c->g_part, c->gq_nparts, c->g_map);
-    LAUNCH_CHECK("k_gq_compact (fused select)");
+    hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
+                       c->g_sel, c->g_win, action, slab);
+    LAUNCH_CHECK("k_gq_compact");
+    // the select: block 0 ranks the window and decides, block 1 builds the next call's key map
+    static bool lds_attr = false;  // (> 64 KiB of dynamic LDS is opted into per kernel)
+    if (!lds_attr) {
+      HIP_TRY(hipFuncSetAttribute((const void*)k_gq_select1, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  2 * kGqCap * (int)sizeof(uint4)));
+      lds_attr = true;
+    }
+    hipLaunchKernelGGL(k_gq_select1, dim3(2), dim3(kGqThreads), 2 * kGqCap * sizeof(uint4), st, c->kp,
+                       (const uint4*)c->g_win, budget, pmin, c->g_sel, action, slab, c->g_hist,
+                       (const double*)c->g_part, c->gq_nparts, c->g_map);
+    LAUNCH_CHECK("k_gq_select1");
     c->counts_ready = true;
     return MDR_OK;
   }
@@ -1425,9 +1434,8 @@ int mdr_gq_shard_compact(mdr_ctx* c, double budget, uint8_t* action, void* strea
   if (!c->g_sel) return fail(MDR_ESTATE, "mdr_gq_shard_compact: call mdr_gq_shard_begin first");
   hipStream_t st = S(stream);
   const int nstage = (int)((c->kp.n + kGqStage - 1) / kGqStage);
-  hipLaunchKernelGGL(k_gq_compact<false>, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist,
-                     budget, c->g_sel, c->g_win + 1, action, (unsigned long long*)nullptr, 0.0, (uint4*)nullptr,
-                     (unsigned*)nullptr, (const double*)nullptr, 0, (uint32_t*)nullptr);
+  hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist,
+                     budget, c->g_sel, c->g_win + 1, action, (unsigned long long*)nullptr);
   LAUNCH_CHECK("k_gq_compact (sharded)");
   // the window's header {count, 0, 0, 0}: the allocator's final count
   HIP_TRY(hipMemsetAsync(c->g_win, 0, sizeof(uint4), st));

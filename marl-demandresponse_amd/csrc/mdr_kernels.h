@@ -10,6 +10,11 @@ namespace mdr {
 constexpr int kCountShards = 64;  // atomic shards for the per-class ON counts
 constexpr int kWinShards = 16;    // the shards a window count flush uses (the first 16 of kCountShards:
                                   // 128 adds per counter at 2048 blocks, one quarter of the reads to sum)
+// waves per k_count_window block (a tile of 64 * kWinHpt houses per wave; MDR_COUNT_WAVES: A/B builds)
+#ifndef MDR_COUNT_WAVES
+#define MDR_COUNT_WAVES 4
+#endif
+constexpr int kCountWaves = MDR_COUNT_WAVES;
 constexpr int kTicketGroups = 64; // grid_last_block: group counters (+ 1 top), 32 words apart
 constexpr int kTicketWords = 32 * (kTicketGroups + 1);
 constexpr int kSlabs = 4;         // count slabs: ring of 3 (step path) / 4 (overlapped pipeline)
@@ -171,10 +176,10 @@ __global__ void k_gq_keys(KParams p, uint32_t* code, double* part, unsigned* his
                           const uint32_t* map);
 __global__ void k_gq_bins(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel,
                           unsigned long long* slab);
-template <bool FUSED>
 __global__ void k_gq_compact(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel, uint4* win,
-                             uint8_t* action, unsigned long long* slab, double pmin, uint4* sorted, unsigned* tickets,
-                             const double* part, int nparts, uint32_t* map);
+                             uint8_t* action, unsigned long long* slab);
+__global__ void k_gq_select1(KParams p, const uint4* win, double S, double pmin, GqSel* sel, uint8_t* action,
+                             unsigned long long* slab, unsigned* hist, const double* part, int nparts, uint32_t* map);
 __global__ void k_gq_select(KParams p, const uint4* win, uint4* sorted, double S, double pmin, GqSel* sel,
                             uint8_t* action, unsigned long long* slab, unsigned* hist, const uint4* gathered,
                             int world, unsigned* tickets, const double* part, int nparts, uint32_t* map);

@@ -876,10 +876,12 @@ __device__ bool grid_last_block(unsigned* __restrict__ tickets) {
 // the last block reads the shards only with 8-B agent-scope (sc1) loads.  Thread t takes shard
 // t % 16 of entries (tick, class) e = t / 16 + 16 k: every load issued first (one round trip), the
 // 16 shards of an entry summed across a 16-lane group (shuffles), the shards zeroed behind.
+template <int NTH>
 __device__ void win_reduce_last(const KParams& p, unsigned long long* __restrict__ slot, int nt,
                                 unsigned* __restrict__ ticket) {
   static_assert(kWinShards == 16, "one 16-lane group per entry");
-  constexpr int EPT = kWinMax * kWinCap * kWinShards / 256;  // loads per thread (blockDim 256)
+  constexpr int EPT = kWinMax * kWinCap * kWinShards / NTH;  // loads per thread (blockDim NTH)
+  constexpr int EPK = NTH / 16;                               // entries per k
   __shared__ unsigned long long s_red[kWinMax * kWinCap];
   if (!grid_last_block(ticket)) return;  // (block-uniform)
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only: the loads below are sc1)
@@ -887,7 +889,7 @@ __device__ void win_reduce_last(const KParams& p, unsigned long long* __restrict
   unsigned long long v[EPT];
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
-    const int e = (int)(threadIdx.x >> 4) + 16 * k;
+    const int e = (int)(threadIdx.x >> 4) + EPK * k;
     v[k] = 0ull;
     if (e < E) {
       const int j = e / ncap, c = e - j * ncap;
@@ -897,7 +899,7 @@ __device__ void win_reduce_last(const KParams& p, unsigned long long* __restrict
   }
 #pragma unroll
   for (int k = 0; k < EPT; ++k) {
-    const int e = (int)(threadIdx.x >> 4) + 16 * k;
+    const int e = (int)(threadIdx.x >> 4) + EPK * k;
     if (e < E) {  // (the slot's next count adds into zeros)
       const int j = e / ncap, c = e - j * ncap;
       __hip_atomic_store(&slot[((size_t)j * kCountShards + sh) * ncap + c], 0ull, __ATOMIC_RELAXED,
@@ -1056,14 +1058,16 @@ __device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uin
     win_run_t<ACT, HPT, false>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb);
 }
 
-// sum the block's per-wave rows cnt[4][kWinMax][kWinCap] and add them to this block's slab shard
+// sum the block's per-wave rows cnt[R][kWinMax][kWinCap] and add them to this block's slab shard
+template <int R = 4>
 __device__ __forceinline__ void win_flush(const KParams& p, int nt, const unsigned (*cnt)[kWinMax * kWinCap],
                                           unsigned long long* slot) {
   const int ncap = p.n_cap;
   for (int e = threadIdx.x; e < nt * ncap; e += blockDim.x) {
     const int j = e / ncap, c = e - j * ncap;
-    const unsigned v = cnt[0][j * kWinCap + c] + cnt[1][j * kWinCap + c] + cnt[2][j * kWinCap + c] +
-                       cnt[3][j * kWinCap + c];
+    unsigned v = 0u;
+#pragma unroll
+    for (int r = 0; r < R; ++r) v += cnt[r][j * kWinCap + c];
     if (v) atomicAdd(&slot[((size_t)j * kCountShards + blockIdx.x % kWinShards) * ncap + c],
                      (unsigned long long)v);
   }
@@ -1093,12 +1097,12 @@ __device__ unsigned long long g_cw_ts[16384 * 4];
 // 0 .. nt-1 from the current state (hvac itself is not changed).  Tick ids from the staged drivers,
 // or tick0 + t when tkp is null (mdr_rollout_begin: launched before the host computes the drivers).
 template <int ACT, int HPT>
-__global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* __restrict__ action,
+__global__ void __launch_bounds__(64 * kCountWaves) k_count_window(KParams p, const uint8_t* __restrict__ action,
                                                       int64_t act_stride, const TickArgs* __restrict__ tkp,
                                                       uint64_t tick0, int nt, unsigned long long* __restrict__ slot,
                                                       uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
                                                       const uint32_t* __restrict__ w_in, unsigned* __restrict__ ticket) {
-  __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
+  __shared__ unsigned s_cnt[kCountWaves][kWinMax * kWinCap];
   MDR_CW_TS(0);
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
@@ -1118,9 +1122,9 @@ __global__ void __launch_bounds__(256) k_count_window(KParams p, const uint8_t* 
   for (int h = 0; h < HPT; ++h)
     if (t.v[h]) wah[t.i0 + 64u * h] = w[h];
   __syncthreads();
-  win_flush(p, nt, s_cnt, slot);
+  win_flush<kCountWaves>(p, nt, s_cnt, slot);
   MDR_CW_TS(2);
-  if (ticket) win_reduce_last(p, slot, nt, ticket);  // (ticket: the P-only reduce, see win_reduce_last)
+  if (ticket) win_reduce_last<64 * kCountWaves>(p, slot, nt, ticket);  // (ticket: the P-only reduce, see win_reduce_last)
   MDR_CW_TS(3);
 }
 
@@ -2060,20 +2064,11 @@ template <typename T>
 __device__ __forceinline__ void st_sc1(T* d, T v) { __hip_atomic_store(d, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 template <typename T>
 __device__ __forceinline__ T ld_sc1(const T* s) { return __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-__device__ void gq_compact_tail(const KParams& p, double S, double pmin, GqSel* __restrict__ sel,
-                                const uint4* __restrict__ win, uint4* __restrict__ sorted, uint8_t* __restrict__ action,
-                                unsigned long long* __restrict__ slab, unsigned* __restrict__ tickets,
-                                unsigned* __restrict__ hist, const double* __restrict__ part, int nparts,
-                                uint32_t* __restrict__ map);
 
-template <bool FUSED>
 __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint32_t* __restrict__ code,
                                                            unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
                                                            uint4* __restrict__ win, uint8_t* __restrict__ action,
-                                                           unsigned long long* __restrict__ slab, double pmin,
-                                                           uint4* __restrict__ sorted, unsigned* __restrict__ tickets,
-                                                           const double* __restrict__ part, int nparts,
-                                                           uint32_t* __restrict__ map) {
+                                                           unsigned long long* __restrict__ slab) {
   static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
   static_assert(kGqCopies * 512 <= kGqBins * 4, "the bin copies fit below the superbin copies");
   constexpr int NW = kGqThreads / 64;
@@ -2151,7 +2146,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     const int cnt = (int)__shfl(pre, le);
     const bool wovf = !(fit & 1ull);
     if (lane == 0) s_le = wovf ? -1 : le;
-    if (lane == 0 && blockIdx.x == 0) {  // (sc1: the fused form's last block reads them in this launch)
+    if (lane == 0 && blockIdx.x == 0) {
       if (wovf) st_sc1(&sel->overflow, 1);
       st_sc1(&sel->bstar, bb + l0);
       st_sc1(&sel->bend, bb + l0 + le);
@@ -2168,10 +2163,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     st_sc1(&sel->ncand, (int)sel->total);
   }
   __syncthreads();
-  if (ovf || s_le < 0) {  // the fallback (gq_exact) decides every house (block-uniform)
-    if (FUSED) gq_compact_tail(p, S, pmin, sel, win, sorted, action, slab, tickets, hist, part, nparts, map);
-    return;
-  }
+  if (ovf || s_le < 0) return;  // the fallback (gq_exact) decides every house (block-uniform)
   const int bs = whole ? -1 : bb + s_l0, be = whole ? kGqBins : bb + s_l0 + s_le;
   unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
   bool inw[U];
@@ -2226,13 +2218,11 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     if (!inw[u]) continue;
     const uint32_t i = (uint32_t)(p.goff + b0 + u * kGqThreads + tid);  // (global id: the order's tie-break)
     const uint64_t ok = gq_okey(kk[u]);
-    // (sc1: the fused form's last block loads them in this launch)
     if (j < (unsigned)kGqCap) gq_store_sc1(win + j, make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), (i << 2) | (cd[u] & 3u), hw[u]));
     ++j;
   }
   if (slab && tid < p.n_cap && s_cnt[tid])
     atomicAdd(&slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)s_cnt[tid]);
-  if (FUSED) gq_compact_tail(p, S, pmin, sel, win, sorted, action, slab, tickets, hist, part, nparts, map);
 }
 
 // 16-B window entries handed between workgroups of one launch as two 8-B agent-scope (sc1) accesses
@@ -2553,74 +2543,72 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
 
 
 
-// The single-GPU select inside k_gq_compact<true> (mdr_ctrl_greedy: two launches per decision, no
-// k_gq_select): the LAST compact block to take a ticket loads the window into LDS, ranks it in
-// (key, house) order (a wave per four entries, its lanes splitting the comparisons) into sorted[],
-// and decides (gq_decide); it then zeroes the bin copies every compact block has read.  Block 0,
-// after its own work, builds the next call's key map beside the decision.  Hand-off (MI355X_MICROARCH.md
-// Valid forms, row 1): every window entry and the sel fields read here were stored sc1 by their
-// block before that block's drained ticket add, and are loaded here with sc1 loads only.
-__device__ void gq_compact_tail(const KParams& p, double S, double pmin, GqSel* __restrict__ sel,
-                                const uint4* __restrict__ win, uint4* __restrict__ sorted, uint8_t* __restrict__ action,
-                                unsigned long long* __restrict__ slab, unsigned* __restrict__ tickets,
-                                unsigned* __restrict__ hist, const double* __restrict__ part, int nparts,
-                                uint32_t* __restrict__ map) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char gq_dyn[];  // kGqCap entries (dynamic LDS)
-  uint4* s_e = reinterpret_cast<uint4*>(gq_dyn);
+// The single-GPU select (mdr_ctrl_greedy: k_gq_bins -> k_gq_compact -> this launch of two blocks).
+// Block 0 loads compact's unordered window into LDS, ranks it in (key, house) order (a wave per
+// four entries, its lanes splitting the comparisons) into a second LDS array and decides on it
+// (gq_decide); block 1 zeroes the bin copies compact read and builds the next call's key map
+// (gq_next_map) beside the decision.  Dynamic LDS: two window arrays (2 x kGqCap x 16 B).  The
+// sharded form (k_gq_select below) ranks across 256 blocks because its window is the ranks'
+// gathered windows; r04 also tried the select as the last block of k_gq_compact (one launch
+// fewer): compact's register budget grew (85 VGPRs, 59 spilled SGPRs) and the launch took 30.9 us
+// against 9.2 + 11.0 for the two launches of r03 (profiles/r04g_greedy_kernel_stats.csv).
+__global__ void __launch_bounds__(kGqThreads) k_gq_select1(KParams p, const uint4* __restrict__ win, double S,
+                                                           double pmin, GqSel* __restrict__ sel,
+                                                           uint8_t* __restrict__ action,
+                                                           unsigned long long* __restrict__ slab,
+                                                           unsigned* __restrict__ hist, const double* __restrict__ part,
+                                                           int nparts, uint32_t* __restrict__ map) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char gq_dyn[];
+  uint4* s_w = reinterpret_cast<uint4*>(gq_dyn);  // [kGqCap] the window as compact wrote it
+  uint4* s_s = s_w + kGqCap;                      // [kGqCap] in (key, house) order
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (grid_last_block(tickets)) {  // (block-uniform)
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only: the loads below are sc1)
-    const bool all = ld_sc1(&sel->all) != 0, ovf0 = ld_sc1(&sel->overflow) != 0;
-    const int ncand = ld_sc1(&sel->ncand);
-    const double wt = ld_sc1(&sel->win_tot);
-    const bool more = ld_sc1(&sel->more_after) != 0;
-    if (!all && !ovf0) {
-      constexpr int U = kGqCap / kGqThreads;
-      uint4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = tid + u * kGqThreads;
-        if (e < ncand) v[u] = gq_load_sc1(win + e);
-      }
-#pragma unroll
-      for (int u = 0; u < U; ++u) {
-        const int e = tid + u * kGqThreads;
-        if (e < ncand) s_e[e] = v[u];
-      }
-      __syncthreads();
-      constexpr int B = 4, NW = kGqThreads / 64;
-      for (int e0 = wv * B; e0 < ncand; e0 += NW * B) {  // (wave-uniform)
-        uint4 me[B];
-        unsigned rk[B];
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-          me[b] = e0 + b < ncand ? s_e[e0 + b] : make_uint4(~0u, ~0u, ~0u, 0u);
-          rk[b] = 0u;
-        }
-        for (int f = lane; f < ncand; f += 64) {
-          const uint4 o = s_e[f];
-#pragma unroll
-          for (int b = 0; b < B; ++b) rk[b] += gq_less(o, me[b]) ? 1u : 0u;
-        }
-#pragma unroll
-        for (int b = 0; b < B; ++b) {
-#pragma unroll
-          for (int off = 32; off > 0; off >>= 1) rk[b] += __shfl_xor(rk[b], off);
-          if (lane == 0 && e0 + b < ncand && rk[b] < (unsigned)kGqCap) gq_store_sc1(sorted + rk[b], me[b]);
-        }
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (this block's sorted[] stores, before gq_decide's loads)
-      __syncthreads();
-    }
-    gq_decide(p, sorted, S, pmin, sel, action, slab, s_e, false, ovf0, all, ncand, wt, more, false);
-    __syncthreads();
-    for (int e = tid; e < kGqCopies * 512; e += blockDim.x) hist[e] = 0u;  // (read by every compact block)
-  }
   static_assert(kGqMapLds <= kGqCap * 16, "the map's work areas fit the window array");
-  if (blockIdx.x == 0) {
-    __syncthreads();  // (a decision by this block has finished with s_e)
+  if (blockIdx.x == 1) {
+    for (int e = tid; e < kGqCopies * 512; e += blockDim.x) hist[e] = 0u;  // (read by every compact block)
     gq_next_map(p, hist, part, nparts, sel, map, gq_dyn);
+    return;
   }
+  const bool all = sel->all != 0, ovf0 = sel->overflow != 0;
+  const int ncand = sel->ncand;
+  if (!all && !ovf0) {
+    constexpr int U = kGqCap / kGqThreads;
+    uint4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + u * kGqThreads;
+      if (e < ncand) v[u] = win[e];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int e = tid + u * kGqThreads;
+      if (e < ncand) s_w[e] = v[u];
+    }
+    __syncthreads();
+    constexpr int B = 4, NW = kGqThreads / 64;
+    for (int e0 = wv * B; e0 < ncand; e0 += NW * B) {  // (wave-uniform)
+      uint4 me[B];
+      unsigned rk[B];
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+        me[b] = e0 + b < ncand ? s_w[e0 + b] : make_uint4(~0u, ~0u, ~0u, 0u);
+        rk[b] = 0u;
+      }
+      for (int f = lane; f < ncand; f += 64) {
+        const uint4 o = s_w[f];
+#pragma unroll
+        for (int b = 0; b < B; ++b) rk[b] += gq_less(o, me[b]) ? 1u : 0u;
+      }
+#pragma unroll
+      for (int b = 0; b < B; ++b) {
+#pragma unroll
+        for (int off = 32; off > 0; off >>= 1) rk[b] += __shfl_xor(rk[b], off);
+        if (lane == 0 && e0 + b < ncand && rk[b] < (unsigned)kGqCap) s_s[rk[b]] = me[b];
+      }
+    }
+    __syncthreads();
+  }
+  gq_decide(p, nullptr, S, pmin, sel, action, slab, s_s, false, ovf0, all, ncand, sel->win_tot, sel->more_after != 0,
+            true);
 }
 
 // K4 (kGqSelBlocks workgroups of 1024): every block loads compact's unordered window win[0, ncand)
@@ -2726,10 +2714,6 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
   }
 }
 
-template __global__ void k_gq_compact<true>(KParams, const uint32_t*, unsigned*, double, GqSel*, uint4*, uint8_t*,
-                                             unsigned long long*, double, uint4*, unsigned*, const double*, int, uint32_t*);
-template __global__ void k_gq_compact<false>(KParams, const uint32_t*, unsigned*, double, GqSel*, uint4*, uint8_t*,
-                                              unsigned long long*, double, uint4*, unsigned*, const double*, int, uint32_t*);
 
 // sharded greedy (mdr_greedy_inputs / mdr_greedy_select): this shard's (key, P, lockout) rows, and
 // the generic gather / iota for the cluster-wide selection over the gathered rows

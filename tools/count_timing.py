@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--houses", type=int, default=1 << 20)
     ap.add_argument("--ticks", type=int, default=20)
     ap.add_argument("--reps", type=int, default=10)
+    ap.add_argument("--waves", type=int, default=4, help="waves per count block (the library's MDR_COUNT_WAVES)")
     a = ap.parse_args()
     import torch
 
@@ -35,7 +36,8 @@ def main():
     lib = L.load()
     fn = lib.mdr_count_timing
     fn.argtypes = [C.c_void_p, C.c_int]
-    nb = (a.houses + 511) // 512
+    hpb = 128 * a.waves  # houses per block
+    nb = (a.houses + hpb - 1) // hpb
     buf = np.zeros(nb * 4, np.uint64)
     rows = []
     for r in range(a.reps + 2):
