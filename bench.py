@@ -575,11 +575,13 @@ def main():
                    "parallelism": f"house-sharded x{world} ({kind} allreduce of "
                                   "per-window power counts)" if comm is not None else "1 GPU"},
         "timed_region": {"wall_s": elapsed, "launch_stream_event_ms": gpu_ms,
-                         "includes": "host drivers (OD-temperature RNG, solar, signal) + tick staging + "
-                                     "graph launches + device work",
+                         "includes": "host drivers (OD-temperature RNG, solar, signal) + kernel launches ("
+                                     + ("staged drivers, hipGraph replay" if args.graph == "on" else
+                                        "direct: the first window's count, its drivers as step-kernel arguments, "
+                                        "the later windows' drivers staged") + ") + device work",
                          "before": f"{warm_steps} warmup steps (>= the {args.warmup} requested and >= "
-                                   f"{args.min_warmup_calls} rollout calls: graph capture of every chunk size, "
-                                   "then replays until the host path is in steady state)" +
+                                   f"{args.min_warmup_calls} rollout calls of the timed chunk size, until the "
+                                   "host path is in steady state)" +
                                    (f" and {args.clock_warmup:.2f} s of non-environment device work"
                                     if args.clock_warmup > 0 else "") +
                                    (f"; a {args.host_spin_ms:g} ms idle host busy-loop" if args.host_spin_ms > 0 else "")},

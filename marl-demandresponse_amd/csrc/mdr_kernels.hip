@@ -2423,7 +2423,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
   __shared__ uint8_t s_tk[kGqCap];
   __shared__ double s_w[16];
   __shared__ double s_tot;
-  __shared__ int s_k, s_first, s_ovf;
+  __shared__ int s_k, s_first, s_ovf, s_pick;
   __shared__ unsigned long long s_bal[16];
   __shared__ unsigned s_cnt[kWinCap];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nth = blockDim.x;
@@ -2487,22 +2487,37 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
     }
     const int k = s_k;  // >= 0: the crossing lies in bin b*, inside the window
     for (int j = tid; j < (k < 0 ? ncand : k); j += nth) s_tk[j] = 1;
-    if (tid == 0) {
-      int o = k < 0;
-      if (!o) {
-        double tot = s_tot;
-        int j = k;
-        for (; j < ncand; ++j) {
-          if (gq_walk_over(tot, S, pmin)) break;
-          const double pj = P_of(s_e[j].z);
-          if (gq_take(pj, tot, S, hv_lock(s_e[j].w))) {
-            s_tk[j] = 1;
-            tot += pj;
-          }
+    if (k < 0) {
+      if (tid == 0) s_ovf = 1;
+    } else {
+      // the gap walk from the crossing (k_greedy_walk's rule, in the reference's order): tot changes
+      // only at a take, so each step is one block-wide search for the first house after the last
+      // take that the rule admits (r03: one thread stepping house by house, ~20 us at a window of
+      // ~370 houses).  Every thread carries the same tot and pick: the sums happen in take order.
+      double tot = s_tot;
+      int j0 = k;
+      bool over = false;
+      for (;;) {
+        if (gq_walk_over(tot, S, pmin)) {
+          over = true;
+          break;
         }
-        if (j >= ncand && more_after && !gq_walk_over(tot, S, pmin)) o = 1;
+        if (tid == 0) s_pick = 0x7fffffff;
+        __syncthreads();
+        for (int e = j0 + tid; e < ncand; e += nth)
+          if (gq_take(P_of(s_e[e].z), tot, S, hv_lock(s_e[e].w))) {
+            atomicMin(&s_pick, e);
+            break;
+          }
+        __syncthreads();
+        const int f = s_pick;
+        __syncthreads();  // (every thread has read it before the next step resets it)
+        if (f == 0x7fffffff) break;  // no house left in the window: the walk reaches its end
+        if (tid == 0) s_tk[f] = 1;
+        tot += P_of(s_e[f].z);
+        j0 = f + 1;
       }
-      s_ovf = o;
+      if (tid == 0) s_ovf = (!over && more_after && !gq_walk_over(tot, S, pmin)) ? 1 : 0;
     }
     __syncthreads();
     ovf = s_ovf != 0;

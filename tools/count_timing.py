@@ -23,7 +23,7 @@ def main():
     ap.add_argument("--houses", type=int, default=1 << 20)
     ap.add_argument("--ticks", type=int, default=20)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--waves", type=int, default=4, help="waves per count block (the library's MDR_COUNT_WAVES)")
+    ap.add_argument("--waves", type=int, default=16, help="waves per count block (the library's MDR_COUNT_WAVES)")
     a = ap.parse_args()
     import torch
 

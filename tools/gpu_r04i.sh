@@ -24,4 +24,6 @@ for r in 1 2; do for v in hip cw16; do
   MDR_LIB=marl-demandresponse_amd/mdr_amd/libmdr_$v.so timeout -k 10 200 python bench.py --steps 20 --warmup 5 --no-cpu-baseline --above-mall-houses 0 > $O/b20_${v}_$r.log 2>&1 || exit 1
   python3 -c "import json; d=json.loads(open('$O/b20_${v}_$r.log').read().strip().splitlines()[-1]); print('$v bench20', round(d['value']/1e11,3), 'e11')"
 done; done
+timeout -k 10 60 ./tools/bin/mfma_probe > $O/mfma_probe.log 2>&1 || exit 1
+cat $O/mfma_probe.log
 exit 0
