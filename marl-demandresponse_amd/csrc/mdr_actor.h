@@ -11,13 +11,6 @@ constexpr int kActorNA = 2;       // actions: on / off (MAPPO num_action = 2, ma
 constexpr int kActorMaxIn = 128;  // obs features
 constexpr int kActorMaxSlots = 128;  // feature slots of the chunked row layout (4 k-steps of 32)
 constexpr int kActorKS2 = kActorMaxMB / 2;  // layer-2 k-steps of 32 (hidden rows 0 .. 127)
-// the last layer-2 k-step of an odd row-block count (hidden rows 16 MB .. 16 MB + 15 are padding)
-// as v_mfma_f32_16x16x16_bf16 (MDR_ACTOR_NO_K16: the K = 32 form, for A/B builds)
-#ifdef MDR_ACTOR_NO_K16
-constexpr bool kActorK16 = false;
-#else
-constexpr bool kActorK16 = true;
-#endif
 // waves per block of k_actor (one block per CU: the block shares the LDS weight image).  The
 // default-layout (DEF) forms fit more waves per SIMD: bf16 4 (<= 128 VGPRs), bf16x3 3 (<= 168); the
 // generic forms and the fp32-faithful form (three operand planes) 2.  (MDR_ACTOR_MAXW caps it, for

@@ -41,7 +41,6 @@
 namespace mdr {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
-typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -168,30 +167,21 @@ __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const 
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
 
-// the K = 16 form on the low halves of K = 32 fragments (elements 0..3: k = 4g + j, the same k map):
-// a k-step whose upper 16 rows are zero padding
-__device__ __forceinline__ f32x4 mfma16h(const bf16x8& a, const bf16x8& b, const f32x4& c) {
-  const bf16x4 a4 = __builtin_shufflevector(a, a, 0, 1, 2, 3), b4 = __builtin_shufflevector(b, b, 0, 1, 2, 3);
-  return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(a4, b4, c, 0, 0, 0);
-}
-
 // acc = C + A·B over the split operands (PREC 1: hi·hi; 3: + lo terms; 6: + mid terms), smallest
-// terms first; a[e] / b[e] = (hi, lo) or (hi, mid, lo).  HALF: only k = 0..15 of the k-step
-// (v_mfma_f32_16x16x16_bf16 on the fragments' low halves; the upper halves are zero)
-template <int PREC, bool HALF = false>
+// terms first; a[e] / b[e] = (hi, lo) or (hi, mid, lo)
+template <int PREC>
 __device__ __forceinline__ f32x4 mfma_split(const bf16x8* a, const bf16x8* b, f32x4 acc) {
-  auto mm = [](const bf16x8& x, const bf16x8& y, const f32x4& c) { return HALF ? mfma16h(x, y, c) : mfma16(x, y, c); };
   if constexpr (PREC == 6) {
-    acc = mm(a[1], b[1], acc);  // mid·mid
-    acc = mm(a[2], b[0], acc);  // lo·hi
-    acc = mm(a[0], b[2], acc);  // hi·lo
-    acc = mm(a[1], b[0], acc);  // mid·hi
-    acc = mm(a[0], b[1], acc);  // hi·mid
+    acc = mfma16(a[1], b[1], acc);  // mid·mid
+    acc = mfma16(a[2], b[0], acc);  // lo·hi
+    acc = mfma16(a[0], b[2], acc);  // hi·lo
+    acc = mfma16(a[1], b[0], acc);  // mid·hi
+    acc = mfma16(a[0], b[1], acc);  // hi·mid
   } else if constexpr (PREC == 3) {
-    acc = mm(a[1], b[0], acc);  // lo·hi
-    acc = mm(a[0], b[1], acc);  // hi·lo
+    acc = mfma16(a[1], b[0], acc);  // lo·hi
+    acc = mfma16(a[0], b[1], acc);  // hi·lo
   }
-  return mm(a[0], b[0], acc);
+  return mfma16(a[0], b[0], acc);
 }
 
 // scalar f32 ops the SLP vectorizer cannot pair into v_pk_* (beside MFMAs a v_pk_add_f32 / v_pk_fma_f32
@@ -511,15 +501,10 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
 #pragma unroll
           for (int e = 0; e < NS; ++e) ring[(st + PF) % (PF + 1)][e] = frag2(st + PF, e);
         const bf16x8* as = ring[st % (PF + 1)];
-        // an odd MB leaves the last k-step's upper 16 rows (block MB) zero: K = 16 there
-        constexpr bool kHalfLast = (MB & 1) != 0 && kActorK16;
         if (q == 0) {
           const f32x4 bias = *reinterpret_cast<const f32x4*>(b2 + kActorRB * mb + 4 * g);
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) acc2[cb] = mfma_split<PREC>(as, hs[q][cb], bias);
-        } else if (kHalfLast && q == KS2 - 1) {
-#pragma unroll
-          for (int cb = 0; cb < 2; ++cb) acc2[cb] = mfma_split<PREC, true>(as, hs[q][cb], acc2[cb]);
         } else {
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) acc2[cb] = mfma_split<PREC>(as, hs[q][cb], acc2[cb]);

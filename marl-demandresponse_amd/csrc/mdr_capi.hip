@@ -447,7 +447,11 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   if (cfg->n_cap <= kWindowCap) {
     // a window count slot: sharded slab | reduced counts (mdr_kernels.hip)
     c->wslab_len = kWindowMax * kCountShards * cfg->n_cap + kWindowMax * cfg->n_cap + kWindowMax * kWindowRec;
-    const size_t tiles64 = ((size_t)cfg->n_local + 63) / 64 + 1;  // 64-house lane groups
+    // 64-house lane groups of every wave tile a count / step-window grid launches: the grids round
+    // the tiles up to whole blocks (up to kCountWaves tiles per block), and the waves of a ragged
+    // last block store and load the mask rows of their (empty) tiles too
+    const size_t tiles = ((size_t)cfg->n_local + 64 * kWinHpt - 1) / (64 * kWinHpt);
+    const size_t tiles64 = (tiles + kCountWaves) / kCountWaves * kCountWaves * kWinHpt + 1;
     c->onb_bytes = tiles64 * kWindowMax * sizeof(uint64_t);
     c->wah_bytes = ((size_t)cfg->n_local + 1) * sizeof(uint32_t);
     if (hipMalloc(&c->d_wslab, 3 * sizeof(unsigned long long) * c->wslab_len) != hipSuccess ||

@@ -1093,6 +1093,17 @@ __device__ unsigned long long g_cw_ts[16384 * 4];
 #define MDR_CW_TS(k) do {} while (0)
 #endif
 
+#ifdef MDR_GQ_TIMING
+// measurement build only (tools/gq_timing.py, a variant library): the 100 MHz clock at the phases of
+// the select launch ([0..5] block 0: entry, window loaded, ranked, crossing found, walk done, end;
+// [6..7] block 1: entry, map done)
+__device__ unsigned long long g_gq_ts[8];
+#define MDR_GQ_TS(k) \
+  do { if (threadIdx.x == 0) g_gq_ts[(k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#else
+#define MDR_GQ_TS(k) do {} while (0)
+#endif
+
 // First window of a rollout: ON counts, ON lane masks and end-of-window FSM words of ticks
 // 0 .. nt-1 from the current state (hvac itself is not changed).  Tick ids from the staged drivers,
 // or tick0 + t when tkp is null (mdr_rollout_begin: launched before the host computes the drivers).
@@ -1387,6 +1398,12 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
 extern "C" int mdr_count_timing(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cw_ts), (size_t)n * 4 * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
+}
+#endif
+#ifdef MDR_GQ_TIMING
+extern "C" int mdr_gq_timing(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gq_ts), 8 * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost) ==
+                 hipSuccess ? 0 : -2;
 }
 #endif
 
@@ -2486,6 +2503,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
       if (f >= 0) break;
     }
     const int k = s_k;  // >= 0: the crossing lies in bin b*, inside the window
+    MDR_GQ_TS(3);
     for (int j = tid; j < (k < 0 ? ncand : k); j += nth) s_tk[j] = 1;
     if (k < 0) {
       if (tid == 0) s_ovf = 1;
@@ -2520,6 +2538,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
       if (tid == 0) s_ovf = (!over && more_after && !gq_walk_over(tot, S, pmin)) ? 1 : 0;
     }
     __syncthreads();
+    MDR_GQ_TS(4);
     ovf = s_ovf != 0;
     if (!ovf) {  // the window's actions and the ON counts they produce
       unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
@@ -2558,6 +2577,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
 
 
 
+
 // The single-GPU select (mdr_ctrl_greedy: k_gq_bins -> k_gq_compact -> this launch of two blocks).
 // Block 0 loads compact's unordered window into LDS, ranks it in (key, house) order (a wave per
 // four entries, its lanes splitting the comparisons) into a second LDS array and decides on it
@@ -2579,10 +2599,13 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_select1(KParams p, const uint
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   static_assert(kGqMapLds <= kGqCap * 16, "the map's work areas fit the window array");
   if (blockIdx.x == 1) {
+    MDR_GQ_TS(6);
     for (int e = tid; e < kGqCopies * 512; e += blockDim.x) hist[e] = 0u;  // (read by every compact block)
     gq_next_map(p, hist, part, nparts, sel, map, gq_dyn);
+    MDR_GQ_TS(7);
     return;
   }
+  MDR_GQ_TS(0);
   const bool all = sel->all != 0, ovf0 = sel->overflow != 0;
   const int ncand = sel->ncand;
   if (!all && !ovf0) {
@@ -2599,6 +2622,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_select1(KParams p, const uint
       if (e < ncand) s_w[e] = v[u];
     }
     __syncthreads();
+    MDR_GQ_TS(1);
     constexpr int B = 4, NW = kGqThreads / 64;
     for (int e0 = wv * B; e0 < ncand; e0 += NW * B) {  // (wave-uniform)
       uint4 me[B];
@@ -2622,8 +2646,10 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_select1(KParams p, const uint
     }
     __syncthreads();
   }
+  MDR_GQ_TS(2);
   gq_decide(p, nullptr, S, pmin, sel, action, slab, s_s, false, ovf0, all, ncand, sel->win_tot, sel->more_after != 0,
             true);
+  MDR_GQ_TS(5);
 }
 
 // K4 (kGqSelBlocks workgroups of 1024): every block loads compact's unordered window win[0, ncand)
