@@ -100,6 +100,8 @@ def parse():
                          "size (graph capture + 2 replays: the first replay of a graph and of the host path is "
                          "2-3x slower than the steady state, profiles/r02e_bench20_warmup.log)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--step-tpw", type=int, default=None,
+                    help="per-tick step kernel tiles per wave (MDR_OPT_STEP_TPW; default: the library's choice)")
     ap.add_argument("--above-mall-houses", type=int, default=16 << 20,
                     help="roofline.above_mall: the same step kernel timed alone at this many houses (working set "
                          "well above the 256 MB Infinity Cache, SURVEY 8(d) LLC caveat); 0 = skip")
@@ -380,6 +382,8 @@ def main():
         if world > 1:
             raise SystemExit("--workload greedy runs on one GPU (config C3)")
         g_act = torch.empty(n_loc, dtype=torch.uint8, device=dev)
+    if args.step_tpw is not None:  # (A/B of the per-tick step kernel's tiles per wave, MDR_OPT_STEP_TPW)
+        env.shard.set_option("step_tpw", args.step_tpw)
 
     use_graph = args.graph == "on"
 

@@ -2085,7 +2085,8 @@ __device__ __forceinline__ T ld_sc1(const T* s) { return __hip_atomic_load(s, __
 __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint32_t* __restrict__ code,
                                                            unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
                                                            uint4* __restrict__ win, uint8_t* __restrict__ action,
-                                                           unsigned long long* __restrict__ slab) {
+                                                           unsigned long long* __restrict__ slab,
+                                                           unsigned* __restrict__ wbin) {
   static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
   static_assert(kGqCopies * 512 <= kGqBins * 4, "the bin copies fit below the superbin copies");
   constexpr int NW = kGqThreads / 64;
@@ -2096,6 +2097,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
   __shared__ unsigned s_cnt[kWinCap];
   __shared__ unsigned s_wt[NW];
   __shared__ unsigned s_wbase;
+  __shared__ unsigned s_boff[64];  // binned window (wbin): the first slot of each window bin
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // this block's houses first (every load before the selection reads: they stay in flight)
   const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
@@ -2163,6 +2165,11 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     const int cnt = (int)__shfl(pre, le);
     const bool wovf = !(fit & 1ull);
     if (lane == 0) s_le = wovf ? -1 : le;
+    if (wbin && !wovf) {  // bin l0 + lane's slots start at the exclusive prefix (every block: the same counts)
+      s_boff[lane] = (unsigned)(pre - c2);
+      if (blockIdx.x == 0 && lane <= le) wbin[64 + lane] = (unsigned)(pre - c2);
+      if (blockIdx.x == 0 && lane == le) wbin[64 + le + 1] = (unsigned)pre;
+    }
     if (lane == 0 && blockIdx.x == 0) {
       if (wovf) st_sc1(&sel->overflow, 1);
       st_sc1(&sel->bstar, bb + l0);
@@ -2230,12 +2237,16 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
   }
   __syncthreads();
   unsigned j = s_wbase + s_wt[wv] + (x - mine);
+  const bool binned = wbin && !whole;  // (block-uniform)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (!inw[u]) continue;
     const uint32_t i = (uint32_t)(p.goff + b0 + u * kGqThreads + tid);  // (global id: the order's tie-break)
     const uint64_t ok = gq_okey(kk[u]);
-    if (j < (unsigned)kGqCap) gq_store_sc1(win + j, make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), (i << 2) | (cd[u] & 3u), hw[u]));
+    // binned: the house's slot among its bin's (k_gq_select1 then orders each bin on its own)
+    const int g = (int)(cd[u] >> 2) - bs;
+    const unsigned slot = binned ? s_boff[g] + atomicAdd(&wbin[g], 1u) : j;
+    if (slot < (unsigned)kGqCap) gq_store_sc1(win + slot, make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), (i << 2) | (cd[u] & 3u), hw[u]));
     ++j;
   }
   if (slab && tid < p.n_cap && s_cnt[tid])
@@ -2592,7 +2603,9 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_select1(KParams p, const uint
                                                            uint8_t* __restrict__ action,
                                                            unsigned long long* __restrict__ slab,
                                                            unsigned* __restrict__ hist, const double* __restrict__ part,
-                                                           int nparts, uint32_t* __restrict__ map) {
+                                                           int nparts, uint32_t* __restrict__ map,
+                                                           unsigned* __restrict__ wbin) {
+  __shared__ unsigned s_bo[66];
   extern __shared__ __attribute__((aligned(16))) unsigned char gq_dyn[];
   uint4* s_w = reinterpret_cast<uint4*>(gq_dyn);  // [kGqCap] the window as compact wrote it
   uint4* s_s = s_w + kGqCap;                      // [kGqCap] in (key, house) order
@@ -2623,28 +2636,24 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_select1(KParams p, const uint
     }
     __syncthreads();
     MDR_GQ_TS(1);
-    constexpr int B = 4, NW = kGqThreads / 64;
-    for (int e0 = wv * B; e0 < ncand; e0 += NW * B) {  // (wave-uniform)
-      uint4 me[B];
-      unsigned rk[B];
-#pragma unroll
-      for (int b = 0; b < B; ++b) {
-        me[b] = e0 + b < ncand ? s_w[e0 + b] : make_uint4(~0u, ~0u, ~0u, 0u);
-        rk[b] = 0u;
+    // the window arrives grouped by bin (k_gq_compact's binned slots; bins are monotone in the key):
+    // an entry's rank is its bin's first slot plus the entries of its own bin before it
+    const int ngrp = sel->bend - sel->bstar + 1;
+    for (int g = tid; g <= ngrp; g += blockDim.x) s_bo[g] = wbin[64 + g];
+    __syncthreads();
+    for (int e = tid; e < ncand; e += blockDim.x) {
+      const uint4 me = s_w[e];
+      int lo = 0, hi = ngrp - 1;  // the last group whose first slot is <= e
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_bo[mid] <= (unsigned)e) lo = mid; else hi = mid - 1;
       }
-      for (int f = lane; f < ncand; f += 64) {
-        const uint4 o = s_w[f];
-#pragma unroll
-        for (int b = 0; b < B; ++b) rk[b] += gq_less(o, me[b]) ? 1u : 0u;
-      }
-#pragma unroll
-      for (int b = 0; b < B; ++b) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) rk[b] += __shfl_xor(rk[b], off);
-        if (lane == 0 && e0 + b < ncand && rk[b] < (unsigned)kGqCap) s_s[rk[b]] = me[b];
-      }
+      unsigned r = s_bo[lo];
+      for (unsigned f = s_bo[lo]; f < s_bo[lo + 1]; ++f) r += gq_less(s_w[f], me) ? 1u : 0u;
+      if (r < (unsigned)kGqCap) s_s[r] = me;
     }
     __syncthreads();
+    if (tid < 64) wbin[tid] = 0u;  // (every compact block has allocated: the next call's counters)
   }
   MDR_GQ_TS(2);
   gq_decide(p, nullptr, S, pmin, sel, action, slab, s_s, false, ovf0, all, ncand, sel->win_tot, sel->more_after != 0,
