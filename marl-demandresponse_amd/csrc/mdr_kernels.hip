@@ -1097,9 +1097,14 @@ __device__ unsigned long long g_cw_ts[16384 * 4];
 // measurement build only (tools/gq_timing.py, a variant library): the 100 MHz clock at the phases of
 // the select launch ([0..5] block 0: entry, window loaded, ranked, crossing found, walk done, end;
 // [6..7] block 1: entry, map done)
-__device__ unsigned long long g_gq_ts[8];
-#define MDR_GQ_TS(k) \
-  do { if (threadIdx.x == 0) g_gq_ts[(k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+__device__ unsigned long long g_gq_ts[16];  // [k]: 100 MHz clock, [8 + k]: shader clock (s_memtime)
+#define MDR_GQ_TS(k)                                                    \
+  do {                                                                  \
+    if (threadIdx.x == 0) {                                             \
+      g_gq_ts[(k)] = __builtin_amdgcn_s_memrealtime();                  \
+      g_gq_ts[8 + (k)] = __builtin_amdgcn_s_memtime();                  \
+    }                                                                   \
+  } while (0)
 #else
 #define MDR_GQ_TS(k) do {} while (0)
 #endif
@@ -1402,7 +1407,7 @@ extern "C" int mdr_count_timing(unsigned long long* out, int n) {
 #endif
 #ifdef MDR_GQ_TIMING
 extern "C" int mdr_gq_timing(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gq_ts), 8 * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost) ==
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gq_ts), 16 * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost) ==
                  hipSuccess ? 0 : -2;
 }
 #endif

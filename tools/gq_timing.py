@@ -32,7 +32,7 @@ def main():
     lib = L.load()
     fn = lib.mdr_gq_timing
     fn.argtypes = [C.c_void_p]
-    buf = np.zeros(8, np.uint64)
+    buf = np.zeros(16, np.uint64)
     n = env.n_local
     act = torch.empty(n, dtype=torch.uint8, device="cuda:0")
     rew = torch.empty(n, dtype=torch.float64, device="cuda:0")
@@ -43,7 +43,8 @@ def main():
         assert fn(buf.ctypes.data) == 0
         ts = buf.astype(np.int64)
         base = ts[[0, 6]].min()
-        rows.append((ts - base) * 10)  # ns
+        clk = [(ts[8 + 5] - ts[8]) / max(1, ts[5] - ts[0]) * 0.1, (ts[8 + 7] - ts[8 + 6]) / max(1, ts[7] - ts[6]) * 0.1]
+        rows.append(list((ts[:8] - base) * 10) + clk)  # ns, GHz
         env.step_tensor(act, rewards=rew, ctrl="greedy_keys")
     r = np.array(rows[3:], np.float64) / 1e3
     names = ["block 0 entry", "window loaded", "ranked", "crossing found", "walk done", "block 0 end",
@@ -51,6 +52,9 @@ def main():
     print(f"k_gq_select1, {a.houses} houses: us after the earlier block's entry (median over {a.ticks} calls)")
     for i, nm in enumerate(names):
         print(f"  {nm:22s} {np.median(r[:, i]):7.2f}  (min {r[:, i].min():.2f}, max {r[:, i].max():.2f})")
+    r2 = np.array(rows[3:], np.float64)
+    for i, nm in enumerate(["block 0 shader clock", "block 1 shader clock"]):
+        print(f"  {nm:22s} {np.median(r2[:, 8 + i]):7.2f} GHz  (min {r2[:, 8 + i].min():.2f}, max {r2[:, 8 + i].max():.2f})")
 
 
 if __name__ == "__main__":
