@@ -1325,7 +1325,11 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
     const int nstage = (n + kGqStage - 1) / kGqStage;
     // a cluster that fits the window (<= kGqCap houses, GqSel.whole) is ordered whole by k_gq_select's
     // 256 blocks; otherwise compact writes the window grouped by bin and k_gq_select1 orders each bin
+#ifdef MDR_GQ_SELECT256  // (A/B builds: every call through k_gq_select's 256 blocks, as r03)
+    const bool whole = true;
+#else
     const bool whole = c->kp.n_global <= kGqCap;
+#endif
     hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
                        c->g_sel, c->g_win, action, slab, whole ? nullptr : c->g_wbin);
     LAUNCH_CHECK("k_gq_compact");
