@@ -126,7 +126,6 @@ struct mdr_ctx {
   unsigned* g_tickets = nullptr;         // k_gq_select's grid_last_block counters
   double* g_range = nullptr;             // sharded select: this shard's (min, -max) key range (k_gq_range)
   uint4* g_sorted = nullptr;             // the window in (key, house) order (k_gq_select)
-  unsigned* g_wbin = nullptr;            // binned window: [0, 64) slot counters, [64, 130) bin offsets
   int gq_parts_cap = 0;                  // g_part capacity in (min, max) pairs
   bool gq_keys_ready = false;            // keys + superbin histogram of the current state are in place
   int gq_nparts = 0;                     //   (from the last step's epilogue: its grid's partials)
@@ -1243,8 +1242,8 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   hipFree(c->g_idx); hipFree(c->g_idx2); hipFree(c->g_ls); hipFree(c->g_tmp);
   hipFree(c->g_kpos); hipFree(c->g_extra);
   hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_win);
-  hipFree(c->g_sorted); hipFree(c->g_map); hipFree(c->g_range); hipFree(c->g_tickets); hipFree(c->g_wbin);
-  c->g_map = nullptr; c->g_range = nullptr; c->g_tickets = nullptr; c->g_wbin = nullptr;
+  hipFree(c->g_sorted); hipFree(c->g_map); hipFree(c->g_range); hipFree(c->g_tickets);
+  c->g_map = nullptr; c->g_range = nullptr; c->g_tickets = nullptr;
   c->g_part = nullptr; c->g_hist = nullptr; c->g_sel = nullptr; c->g_win = nullptr;
   c->g_sorted = nullptr;
   c->gq_keys_ready = false;
@@ -1277,8 +1276,6 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_tickets, kTicketWords * sizeof(unsigned)));
   HIP_TRY(hipMemset(c->g_tickets, 0, kTicketWords * sizeof(unsigned)));
   HIP_TRY(hipMalloc(&c->g_sorted, kGqCap * sizeof(uint4)));
-  HIP_TRY(hipMalloc(&c->g_wbin, 256 * sizeof(unsigned)));
-  HIP_TRY(hipMemset(c->g_wbin, 0, 256 * sizeof(unsigned)));  // (k_gq_select1 re-zeroes the counters it consumed)
   size_t b1 = 0, b2 = 0;
   HIP_TRY(greedy_sort(nullptr, b1, c->g_key, c->g_key2, c->g_idx, c->g_idx2, n, nullptr));
   HIP_TRY(hipcub::DeviceScan::InclusiveSum(nullptr, b2, c->g_ps, c->g_incl, (int)n));
@@ -1316,42 +1313,22 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   unsigned long long* slab = slab_at(c, c->ring);  // the counts of the actions decided here
   if (c->kp.n_cap <= 4 && !c->greedy_sort) {
     // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster, no host
-    // synchronisation; k_gq_select1 decides exactly what the candidate window cannot
+    // synchronisation; k_gq_select decides exactly what the candidate window cannot
     if (!keys_ready)
       if (int rc2 = launch_gq_keys(c, st)) return rc2;
     hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
                        c->g_sel, slab);
     LAUNCH_CHECK("k_gq_bins");
     const int nstage = (n + kGqStage - 1) / kGqStage;
-    // a cluster that fits the window (<= kGqCap houses, GqSel.whole) is ordered whole by k_gq_select's
-    // 256 blocks; otherwise compact writes the window grouped by bin and k_gq_select1 orders each bin
-#ifdef MDR_GQ_SELECT256  // (A/B builds: every call through k_gq_select's 256 blocks, as r03)
-    const bool whole = true;
-#else
-    const bool whole = c->kp.n_global <= kGqCap;
-#endif
     hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
-                       c->g_sel, c->g_win, action, slab, whole ? nullptr : c->g_wbin);
+                       c->g_sel, c->g_win, action, slab);
     LAUNCH_CHECK("k_gq_compact");
-    if (whole) {
-      hipLaunchKernelGGL(k_gq_select, dim3(kGqSelBlocks), dim3(1024), 0, st, c->kp, (const uint4*)c->g_win,
-                         c->g_sorted, budget, pmin, c->g_sel, action, slab, c->g_hist, (const uint4*)nullptr, 0,
-                         c->g_tickets, (const double*)c->g_part, c->gq_nparts, c->g_map);
-      LAUNCH_CHECK("k_gq_select");
-      c->counts_ready = true;
-      return MDR_OK;
-    }
-    // the select: block 0 ranks the window and decides, block 1 builds the next call's key map
-    static bool lds_attr = false;  // (> 64 KiB of dynamic LDS is opted into per kernel)
-    if (!lds_attr) {
-      HIP_TRY(hipFuncSetAttribute((const void*)k_gq_select1, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  2 * kGqCap * (int)sizeof(uint4)));
-      lds_attr = true;
-    }
-    hipLaunchKernelGGL(k_gq_select1, dim3(2), dim3(kGqThreads), 2 * kGqCap * sizeof(uint4), st, c->kp,
-                       (const uint4*)c->g_win, budget, pmin, c->g_sel, action, slab, c->g_hist,
-                       (const double*)c->g_part, c->gq_nparts, c->g_map, c->g_wbin);
-    LAUNCH_CHECK("k_gq_select1");
+    // the window ranked by 256 blocks, the last of them decides (a one-block select measured slower:
+    // DESIGN.md §3.3)
+    hipLaunchKernelGGL(k_gq_select, dim3(kGqSelBlocks), dim3(1024), 0, st, c->kp, (const uint4*)c->g_win,
+                       c->g_sorted, budget, pmin, c->g_sel, action, slab, c->g_hist, (const uint4*)nullptr, 0,
+                       c->g_tickets, (const double*)c->g_part, c->gq_nparts, c->g_map);
+    LAUNCH_CHECK("k_gq_select");
     c->counts_ready = true;
     return MDR_OK;
   }
@@ -1457,7 +1434,7 @@ int mdr_gq_shard_compact(mdr_ctx* c, double budget, uint8_t* action, void* strea
   hipStream_t st = S(stream);
   const int nstage = (int)((c->kp.n + kGqStage - 1) / kGqStage);
   hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist,
-                     budget, c->g_sel, c->g_win + 1, action, (unsigned long long*)nullptr, (unsigned*)nullptr);
+                     budget, c->g_sel, c->g_win + 1, action, (unsigned long long*)nullptr);
   LAUNCH_CHECK("k_gq_compact (sharded)");
   // the window's header {count, 0, 0, 0}: the allocator's final count
   HIP_TRY(hipMemsetAsync(c->g_win, 0, sizeof(uint4), st));

@@ -178,10 +178,7 @@ __global__ void k_gq_keys(KParams p, uint32_t* code, double* part, unsigned* his
 __global__ void k_gq_bins(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel,
                           unsigned long long* slab);
 __global__ void k_gq_compact(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel, uint4* win,
-                             uint8_t* action, unsigned long long* slab, unsigned* wbin);
-__global__ void k_gq_select1(KParams p, const uint4* win, double S, double pmin, GqSel* sel, uint8_t* action,
-                             unsigned long long* slab, unsigned* hist, const double* part, int nparts, uint32_t* map,
-                             unsigned* wbin);
+                             uint8_t* action, unsigned long long* slab);
 __global__ void k_gq_select(KParams p, const uint4* win, uint4* sorted, double S, double pmin, GqSel* sel,
                             uint8_t* action, unsigned long long* slab, unsigned* hist, const uint4* gathered,
                             int world, unsigned* tickets, const double* part, int nparts, uint32_t* map);

@@ -1093,21 +1093,6 @@ __device__ unsigned long long g_cw_ts[16384 * 4];
 #define MDR_CW_TS(k) do {} while (0)
 #endif
 
-#ifdef MDR_GQ_TIMING
-// measurement build only (tools/gq_timing.py, a variant library): the 100 MHz clock at the phases of
-// the select launch ([0..5] block 0: entry, window loaded, ranked, crossing found, walk done, end;
-// [6..7] block 1: entry, map done)
-__device__ unsigned long long g_gq_ts[16];  // [k]: 100 MHz clock, [8 + k]: shader clock (s_memtime)
-#define MDR_GQ_TS(k)                                                    \
-  do {                                                                  \
-    if (threadIdx.x == 0) {                                             \
-      g_gq_ts[(k)] = __builtin_amdgcn_s_memrealtime();                  \
-      g_gq_ts[8 + (k)] = __builtin_amdgcn_s_memtime();                  \
-    }                                                                   \
-  } while (0)
-#else
-#define MDR_GQ_TS(k) do {} while (0)
-#endif
 
 // First window of a rollout: ON counts, ON lane masks and end-of-window FSM words of ticks
 // 0 .. nt-1 from the current state (hvac itself is not changed).  Tick ids from the staged drivers,
@@ -1403,12 +1388,6 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
 extern "C" int mdr_count_timing(unsigned long long* out, int n) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cw_ts), (size_t)n * 4 * sizeof(unsigned long long), 0,
                              hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
-}
-#endif
-#ifdef MDR_GQ_TIMING
-extern "C" int mdr_gq_timing(unsigned long long* out) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_gq_ts), 16 * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost) ==
-                 hipSuccess ? 0 : -2;
 }
 #endif
 
@@ -2090,8 +2069,7 @@ __device__ __forceinline__ T ld_sc1(const T* s) { return __hip_atomic_load(s, __
 __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint32_t* __restrict__ code,
                                                            unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
                                                            uint4* __restrict__ win, uint8_t* __restrict__ action,
-                                                           unsigned long long* __restrict__ slab,
-                                                           unsigned* __restrict__ wbin) {
+                                                           unsigned long long* __restrict__ slab) {
   static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
   static_assert(kGqCopies * 512 <= kGqBins * 4, "the bin copies fit below the superbin copies");
   constexpr int NW = kGqThreads / 64;
@@ -2102,7 +2080,6 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
   __shared__ unsigned s_cnt[kWinCap];
   __shared__ unsigned s_wt[NW];
   __shared__ unsigned s_wbase;
-  __shared__ unsigned s_boff[64];  // binned window (wbin): the first slot of each window bin
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   // this block's houses first (every load before the selection reads: they stay in flight)
   const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
@@ -2170,11 +2147,6 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     const int cnt = (int)__shfl(pre, le);
     const bool wovf = !(fit & 1ull);
     if (lane == 0) s_le = wovf ? -1 : le;
-    if (wbin && !wovf) {  // bin l0 + lane's slots start at the exclusive prefix (every block: the same counts)
-      s_boff[lane] = (unsigned)(pre - c2);
-      if (blockIdx.x == 0 && lane <= le) wbin[64 + lane] = (unsigned)(pre - c2);
-      if (blockIdx.x == 0 && lane == le) wbin[64 + le + 1] = (unsigned)pre;
-    }
     if (lane == 0 && blockIdx.x == 0) {
       if (wovf) st_sc1(&sel->overflow, 1);
       st_sc1(&sel->bstar, bb + l0);
@@ -2242,16 +2214,12 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
   }
   __syncthreads();
   unsigned j = s_wbase + s_wt[wv] + (x - mine);
-  const bool binned = wbin && !whole;  // (block-uniform)
 #pragma unroll
   for (int u = 0; u < U; ++u) {
     if (!inw[u]) continue;
     const uint32_t i = (uint32_t)(p.goff + b0 + u * kGqThreads + tid);  // (global id: the order's tie-break)
     const uint64_t ok = gq_okey(kk[u]);
-    // binned: the house's slot among its bin's (k_gq_select1 then orders each bin on its own)
-    const int g = (int)(cd[u] >> 2) - bs;
-    const unsigned slot = binned ? s_boff[g] + atomicAdd(&wbin[g], 1u) : j;
-    if (slot < (unsigned)kGqCap) gq_store_sc1(win + slot, make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), (i << 2) | (cd[u] & 3u), hw[u]));
+    if (j < (unsigned)kGqCap) gq_store_sc1(win + j, make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), (i << 2) | (cd[u] & 3u), hw[u]));
     ++j;
   }
   if (slab && tid < p.n_cap && s_cnt[tid])
@@ -2519,7 +2487,6 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
       if (f >= 0) break;
     }
     const int k = s_k;  // >= 0: the crossing lies in bin b*, inside the window
-    MDR_GQ_TS(3);
     for (int j = tid; j < (k < 0 ? ncand : k); j += nth) s_tk[j] = 1;
     if (k < 0) {
       if (tid == 0) s_ovf = 1;
@@ -2554,7 +2521,6 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
       if (tid == 0) s_ovf = (!over && more_after && !gq_walk_over(tot, S, pmin)) ? 1 : 0;
     }
     __syncthreads();
-    MDR_GQ_TS(4);
     ovf = s_ovf != 0;
     if (!ovf) {  // the window's actions and the ON counts they produce
       unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
@@ -2593,78 +2559,6 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
 
 
 
-
-// The single-GPU select (mdr_ctrl_greedy: k_gq_bins -> k_gq_compact -> this launch of two blocks).
-// Block 0 loads compact's unordered window into LDS, ranks it in (key, house) order (a wave per
-// four entries, its lanes splitting the comparisons) into a second LDS array and decides on it
-// (gq_decide); block 1 zeroes the bin copies compact read and builds the next call's key map
-// (gq_next_map) beside the decision.  Dynamic LDS: two window arrays (2 x kGqCap x 16 B).  The
-// sharded form (k_gq_select below) ranks across 256 blocks because its window is the ranks'
-// gathered windows; r04 also tried the select as the last block of k_gq_compact (one launch
-// fewer): compact's register budget grew (85 VGPRs, 59 spilled SGPRs) and the launch took 30.9 us
-// against 9.2 + 11.0 for the two launches of r03 (profiles/r04g_greedy_kernel_stats.csv).
-__global__ void __launch_bounds__(kGqThreads) k_gq_select1(KParams p, const uint4* __restrict__ win, double S,
-                                                           double pmin, GqSel* __restrict__ sel,
-                                                           uint8_t* __restrict__ action,
-                                                           unsigned long long* __restrict__ slab,
-                                                           unsigned* __restrict__ hist, const double* __restrict__ part,
-                                                           int nparts, uint32_t* __restrict__ map,
-                                                           unsigned* __restrict__ wbin) {
-  __shared__ unsigned s_bo[66];
-  extern __shared__ __attribute__((aligned(16))) unsigned char gq_dyn[];
-  uint4* s_w = reinterpret_cast<uint4*>(gq_dyn);  // [kGqCap] the window as compact wrote it
-  uint4* s_s = s_w + kGqCap;                      // [kGqCap] in (key, house) order
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  static_assert(kGqMapLds <= kGqCap * 16, "the map's work areas fit the window array");
-  if (blockIdx.x == 1) {
-    MDR_GQ_TS(6);
-    for (int e = tid; e < kGqCopies * 512; e += blockDim.x) hist[e] = 0u;  // (read by every compact block)
-    gq_next_map(p, hist, part, nparts, sel, map, gq_dyn);
-    MDR_GQ_TS(7);
-    return;
-  }
-  MDR_GQ_TS(0);
-  const bool all = sel->all != 0, ovf0 = sel->overflow != 0;
-  const int ncand = sel->ncand;
-  if (!all && !ovf0) {
-    constexpr int U = kGqCap / kGqThreads;
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = tid + u * kGqThreads;
-      if (e < ncand) v[u] = win[e];
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = tid + u * kGqThreads;
-      if (e < ncand) s_w[e] = v[u];
-    }
-    __syncthreads();
-    MDR_GQ_TS(1);
-    // the window arrives grouped by bin (k_gq_compact's binned slots; bins are monotone in the key):
-    // an entry's rank is its bin's first slot plus the entries of its own bin before it
-    const int ngrp = sel->bend - sel->bstar + 1;
-    for (int g = tid; g <= ngrp; g += blockDim.x) s_bo[g] = wbin[64 + g];
-    __syncthreads();
-    for (int e = tid; e < ncand; e += blockDim.x) {
-      const uint4 me = s_w[e];
-      int lo = 0, hi = ngrp - 1;  // the last group whose first slot is <= e
-      while (lo < hi) {
-        const int mid = (lo + hi + 1) >> 1;
-        if (s_bo[mid] <= (unsigned)e) lo = mid; else hi = mid - 1;
-      }
-      unsigned r = s_bo[lo];
-      for (unsigned f = s_bo[lo]; f < s_bo[lo + 1]; ++f) r += gq_less(s_w[f], me) ? 1u : 0u;
-      if (r < (unsigned)kGqCap) s_s[r] = me;
-    }
-    __syncthreads();
-    if (tid < 64) wbin[tid] = 0u;  // (every compact block has allocated: the next call's counters)
-  }
-  MDR_GQ_TS(2);
-  gq_decide(p, nullptr, S, pmin, sel, action, slab, s_s, false, ovf0, all, ncand, sel->win_tot, sel->more_after != 0,
-            true);
-  MDR_GQ_TS(5);
-}
 
 // K4 (kGqSelBlocks workgroups of 1024): every block loads compact's unordered window win[0, ncand)
 // into LDS and ranks kGqCap / (kGqSelBlocks * 16) of its houses per wave (how many window houses
