@@ -756,7 +756,7 @@ static unsigned long long* win_red_ptr(const mdr_ctx* c, unsigned long long* slo
 static int launch_count(mdr_ctx* c, int mode, const uint8_t* action, int64_t act_stride, const TickArgs* tk,
                         uint64_t tick0, int K, unsigned long long* slot, uint64_t* onb, uint32_t* wah,
                         const uint32_t* w_in, hipStream_t st, bool p_only = false) {
-  const unsigned grid = win_grid(c, kCountWaves * kCountTPW);
+  const unsigned grid = win_grid(c, kCountWaves);
   unsigned* ticket = p_only ? c->d_tickets : nullptr;
 #define MDR_COUNT(A)                                                                                  \
   hipLaunchKernelGGL((k_count_window<A, kWinHpt>), dim3(grid), dim3(64 * kCountWaves), 0, st, c->kp, action, act_stride, tk, \

@@ -16,12 +16,6 @@ constexpr int kWinShards = 16;    // the shards a window count flush uses (the f
 #define MDR_COUNT_WAVES 16
 #endif
 constexpr int kCountWaves = MDR_COUNT_WAVES;
-// tiles per wave of k_count_window (1: one tile per wave, the grid covers the tiles; > 1: A/B builds,
-// MDR_COUNT_TPW — a grid of ceil(tiles / (waves x TPW)) blocks whose waves loop over their tiles)
-#ifndef MDR_COUNT_TPW
-#define MDR_COUNT_TPW 1
-#endif
-constexpr int kCountTPW = MDR_COUNT_TPW;
 constexpr int kTicketGroups = 64; // grid_last_block: group counters (+ 1 top), 32 words apart
 constexpr int kTicketWords = 32 * (kTicketGroups + 1);
 constexpr int kSlabs = 4;         // count slabs: ring of 3 (step path) / 4 (overlapped pipeline)

@@ -928,11 +928,10 @@ struct WinTile {
   bool v[HPT];
   uint64_t g0;        // first 64-house group of global ids the tile touches
   int sh;             // global id of the tile's first house mod 64 (0 when the shard offset is aligned)
-  __device__ __forceinline__ WinTile(const KParams& p)
-      : WinTile(p, blockIdx.x * (blockDim.x >> 6) + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {}
-  __device__ __forceinline__ WinTile(const KParams& p, uint32_t tile_) {
+  __device__ __forceinline__ WinTile(const KParams& p) {
     const uint32_t n = (uint32_t)p.n;
-    tile = tile_;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    tile = blockIdx.x * (blockDim.x >> 6) + wv;
     i0 = tile * (64u * HPT) + (uint32_t)(threadIdx.x & 63);
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
@@ -973,7 +972,7 @@ __device__ __forceinline__ uint32_t writelane_u32(uint32_t old, uint32_t val, in
 // c and L - j dt fit a signed 32-bit compare), so saturating once at the end gives the
 // per-tick-saturated value; the lock bit comes from the last tick.  SH: the tile starts off a
 // 64-house group boundary (sharded runs), so a random action mask is spliced from two words.
-template <int ACT, int HPT, bool SH, bool ACC>
+template <int ACT, int HPT, bool SH>
 __device__ __forceinline__ void win_run_t(const KParams& p, uint32_t* w, const uint64_t (*cm)[kWinCap],
                                           const WinTile<HPT>& t, const TickArgs* tkp, uint64_t tick0, int nt,
                                           const uint8_t* action, int64_t act_stride, unsigned* cnt, uint64_t* onb) {
@@ -1045,19 +1044,18 @@ __device__ __forceinline__ void win_run_t(const KParams& p, uint32_t* w, const u
       for (int cc = 0; cc < kWinCap; ++cc) k[cc] += (unsigned)__popcll(m & cm[h][cc]);
     }
 #pragma unroll
-    for (int cc = 0; cc < kWinCap; ++cc) cnt[lane * kWinCap + cc] = ACC ? cnt[lane * kWinCap + cc] + k[cc] : k[cc];
+    for (int cc = 0; cc < kWinCap; ++cc) cnt[lane * kWinCap + cc] = k[cc];
   }
 }
 
-// ACC: add the tile's counts to cnt (a wave running several tiles) instead of writing them
-template <int ACT, int HPT, bool ACC = false>
+template <int ACT, int HPT>
 __device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uint64_t (*cm)[kWinCap],
                                         const WinTile<HPT>& t, const TickArgs* tkp, uint64_t tick0, int nt,
                                         const uint8_t* action, int64_t act_stride, unsigned* cnt, uint64_t* onb) {
   if (ACT == MDR_ACT_RANDOM && t.sh != 0)
-    win_run_t<ACT, HPT, true, ACC>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb);
+    win_run_t<ACT, HPT, true>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb);
   else
-    win_run_t<ACT, HPT, false, ACC>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb);
+    win_run_t<ACT, HPT, false>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb);
 }
 
 // sum the block's per-wave rows cnt[R][kWinMax][kWinCap] and add them to this block's slab shard
@@ -1108,32 +1106,22 @@ __global__ void __launch_bounds__(64 * kCountWaves) k_count_window(KParams p, co
   __shared__ unsigned s_cnt[kCountWaves][kWinMax * kWinCap];
   MDR_CW_TS(0);
   const int wv = threadIdx.x >> 6;
-  auto tile_run = [&](const WinTile<HPT>& t, auto acc) {
-    uint32_t w[HPT];
-    int cls[HPT];
+  const WinTile<HPT> t(p);
+  uint32_t w[HPT];
+  int cls[HPT];
 #pragma unroll
-    for (int h = 0; h < HPT; ++h) {
-      w[h] = w_in ? w_in[t.idx[h]] : p.hvac[t.idx[h]];
-      cls[h] = p.cap_idx[t.idx[h]];
-    }
-    uint64_t cm[HPT][kWinCap];
-    win_classes<HPT>(t, cls, cm);
-    MDR_CW_TS(1);
-    win_run<ACT, HPT, decltype(acc)::value>(p, w, cm, t, tkp, tick0, nt, action, act_stride, s_cnt[wv],
-                                            onb + (size_t)t.tile * HPT * kWinMax);
-#pragma unroll
-    for (int h = 0; h < HPT; ++h)
-      if (t.v[h]) wah[t.i0 + 64u * h] = w[h];
-  };
-  if (kCountTPW == 1) {
-    tile_run(WinTile<HPT>(p), std::false_type{});
-  } else {  // (A/B builds) the wave's tiles tile0, tile0 + G, ...: G = every wave of the grid
-    for (int e = threadIdx.x & 63; e < kWinMax * kWinCap; e += 64) s_cnt[wv][e] = 0u;
-    const uint32_t ntiles = (uint32_t)((p.n + 64 * HPT - 1) / (64 * HPT));
-    const uint32_t G = gridDim.x * (uint32_t)kCountWaves;
-    for (uint32_t tl = blockIdx.x * (uint32_t)kCountWaves + (uint32_t)wv; tl < ntiles; tl += G)  // (wave-uniform)
-      tile_run(WinTile<HPT>(p, tl), std::true_type{});
+  for (int h = 0; h < HPT; ++h) {
+    w[h] = w_in ? w_in[t.idx[h]] : p.hvac[t.idx[h]];
+    cls[h] = p.cap_idx[t.idx[h]];
   }
+  uint64_t cm[HPT][kWinCap];
+  win_classes<HPT>(t, cls, cm);
+  MDR_CW_TS(1);
+  win_run<ACT, HPT>(p, w, cm, t, tkp, tick0, nt, action, act_stride, s_cnt[wv],
+                    onb + (size_t)t.tile * HPT * kWinMax);
+#pragma unroll
+  for (int h = 0; h < HPT; ++h)
+    if (t.v[h]) wah[t.i0 + 64u * h] = w[h];
   __syncthreads();
   win_flush<kCountWaves>(p, nt, s_cnt, slot);
   MDR_CW_TS(2);
