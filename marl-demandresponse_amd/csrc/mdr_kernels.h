@@ -157,8 +157,14 @@ __global__ void k_greedy_apply(int64_t n, const int* perm, const int64_t* kpos, 
 constexpr int kGqBins = 16384;  // histogram-select greedy: key bins
 constexpr int kGqCap = 4096;    // candidate window capacity (LDS, 16 B per house)
 constexpr int kGqAfter = 256;   // window houses past the crossing bin (the gap walk's room)
-constexpr int kGqStage = 4096;  // houses per k_gq_compact block
-constexpr int kGqParts = 256;   // k_gq_keys / k_gq_bins grid (one block per CU)
+#ifndef MDR_GQ_STAGE
+#define MDR_GQ_STAGE 4096
+#endif
+#ifndef MDR_GQ_PARTS
+#define MDR_GQ_PARTS 256
+#endif
+constexpr int kGqStage = MDR_GQ_STAGE;  // houses per k_gq_compact block (MDR_GQ_STAGE: A/B builds)
+constexpr int kGqParts = MDR_GQ_PARTS;  // k_gq_keys / k_gq_bins grid (one block per CU; MDR_GQ_PARTS: A/B)
 constexpr int kGqThreads = 1024; // k_gq_keys / k_gq_bins / k_gq_compact block size
 constexpr int kGqCopies = 8;    // copies of the global superbin / bin histograms (blockIdx % kGqCopies)
 constexpr int kGqUnroll = 4;    // houses per thread per pass of k_gq_keys / k_gq_bins
