@@ -117,9 +117,10 @@ def parse():
                          "greedy: config C3, device greedy-myopic controller then env.step")
     ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32", "bf16"],
                     help="actor MFMA precision (--workload actor)")
-    ap.add_argument("--comm", default="default", choices=["default", "none", "rccl", "torch"],
+    ap.add_argument("--comm", default="default", choices=["default", "none", "rccl", "torch", "host"],
                     help="exchange for the sharded path (default: rccl when WORLD_SIZE > 1); "
-                         "'rccl' at world 1 exercises the sharded C loop on one GPU")
+                         "'rccl' at world 1 exercises the sharded C loop on one GPU; 'host' = the same C loops "
+                         "with gloo collectives (ranks may share one GPU: a rehearsal of the multi-GPU line)")
     return ap.parse_args()
 
 
@@ -338,6 +339,8 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.cpu_seconds)  # before this process touches the GPU
+    if args.comm == "host":  # (rehearsal: the ranks may share the visible GPUs)
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     comm = None
@@ -349,7 +352,10 @@ def main():
 
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         os.environ.setdefault("MASTER_PORT", "29511")
-        dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
+        if kind == "host":
+            dist.init_process_group("gloo", rank=rank, world_size=world)
+        else:
+            dist.init_process_group("nccl", device_id=dev, rank=rank, world_size=world)
         from mdr_amd.distributed import make_comm
 
         comm = make_comm(kind)
@@ -477,7 +483,7 @@ def main():
     if comm is not None:
         import torch.distributed as dist
 
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        t = torch.tensor([elapsed], dtype=torch.float64, device="cpu" if kind == "host" else dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     value = n_total * args.steps / elapsed

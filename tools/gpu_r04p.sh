@@ -14,4 +14,9 @@ for v in hip gs2kp512; do
 done
 MDR_LIB=marl-demandresponse_amd/mdr_amd/libmdr_gs2kp512.so timeout -k 10 400 python -u -m pytest -q --timeout 200 --timeout-method thread -m gpu tests/test_env_parity_gpu.py tests/test_distributed_gpu.py -k greedy > $O/pytest_gs2kp512.log 2>&1; rc=$?
 tail -n 1 $O/pytest_gs2kp512.log
+# rehearsal of the driver's multi-GPU bench line: 2 ranks sharing cuda:0 over gloo + the library's C loops
+for sc in weak strong; do
+  timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29533 bench.py --gpus 2 --comm host --scaling $sc --steps 20 --warmup 5 --no-cpu-baseline --above-mall-houses 0 > $O/bench_w2_$sc.log 2>&1; echo "w2 $sc rc=$?"
+  grep '^{' $O/bench_w2_$sc.log | tail -n 1 | cut -c1-400
+done
 exit $rc
