@@ -166,12 +166,18 @@ constexpr int kGqAfter = 256;   // window houses past the crossing bin (the gap 
 constexpr int kGqStage = MDR_GQ_STAGE;  // houses per k_gq_compact block (MDR_GQ_STAGE: A/B builds)
 constexpr int kGqParts = MDR_GQ_PARTS;  // k_gq_keys / k_gq_bins grid (one block per CU; MDR_GQ_PARTS: A/B)
 constexpr int kGqThreads = 1024; // k_gq_keys / k_gq_bins / k_gq_compact block size
-constexpr int kGqCopies = 8;    // copies of the global superbin / bin histograms (blockIdx % kGqCopies)
+#ifndef MDR_GQ_COPIES
+#define MDR_GQ_COPIES 8
+#endif
+constexpr int kGqCopies = MDR_GQ_COPIES;  // copies of the global superbin / bin histograms (blockIdx % kGqCopies)
 constexpr int kGqUnroll = 4;    // houses per thread per pass of k_gq_keys / k_gq_bins
 constexpr int kGqSuper = 256;   // superbins (64 bins each) of the select's first pass (+ 1 for NaN keys)
 constexpr int kGqHistWords = kGqBins * 4 + kGqCopies * (kGqSuper + 1) * 4;  // g_hist: bin copies | superbin copies
 constexpr int kGqCells = 256;   // cells of the key -> bin map (gq_bin)
-constexpr int kGqSelBlocks = 256;
+#ifndef MDR_GQ_SEL_BLOCKS
+#define MDR_GQ_SEL_BLOCKS 256
+#endif
+constexpr int kGqSelBlocks = MDR_GQ_SEL_BLOCKS;  // (MDR_GQ_SEL_BLOCKS: A/B builds)
 constexpr int kGqMaxRanks = 64;   // sharded histogram select: ranks whose windows k_gq_select gathers  // k_gq_select grid (1024 threads each: one window house per wave)
 struct GqSel;
 void gq_sel_init(void* sel128, uint32_t* map);  // host: the first call's key map (uniform over [-32, 32])
