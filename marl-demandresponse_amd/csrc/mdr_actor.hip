@@ -368,11 +368,7 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     }
   };
   // ---- the stages of a tile (mdr_actor.hip header: the ping-pong schedule below)
-#ifdef MDR_ACTOR_OUT_F64
-  double zz[2][kActorNA];  // the tile's two logits per column block (partial over this lane's rows), X -> Y
-#else
   f32x2 zz[2];  // the tile's two logits per column block (partial over this lane's rows) between X and Y
-#endif
   // build: the tile's LDS rows from the prefetched sources (+ the table topologies' gathers)
   auto stage_build = [&](uint32_t tl) {
     const uint32_t b0 = tl * 32u;
@@ -496,12 +492,8 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
 #pragma unroll
         for (int e = 0; e < NS; ++e) ring[q][e] = frag2(q, e);
       f32x4 acc2[2];
-#ifdef MDR_ACTOR_OUT_F64
-      zz[0][0] = zz[0][1] = zz[1][0] = zz[1][1] = 0.0;
-#else
       zz[0] = f32x2{0.f, 0.f};
       zz[1] = f32x2{0.f, 0.f};
-#endif
 #pragma unroll
       for (int st = 0; st < TOT; ++st) {
         const int mb = st / KS2, q = st % KS2;
@@ -527,14 +519,8 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
               const float x = relu(acc2[cb][i]);
-#ifdef MDR_ACTOR_OUT_F64  // (fp64 FMAs issue beside the MFMAs; one rounding to f32 at the end)
-              const double xd = (double)x;
-              zz[cb][0] = __builtin_fma((double)w[i].x, xd, zz[cb][0]);
-              zz[cb][1] = __builtin_fma((double)w[i].y, xd, zz[cb][1]);
-#else
               zz[cb].x = fma_s(w[i].x, x, zz[cb].x);
               zz[cb].y = fma_s(w[i].y, x, zz[cb].y);
-#endif
             }
         }
       }
@@ -547,15 +533,9 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
   auto stage_y = [&](uint32_t tl, uint32_t next, bool fresh) {
     const uint32_t b0 = tl * 32u;
     const int nb = (int)min(32u, n - b0);
-#ifdef MDR_ACTOR_OUT_F64
-    double z[2][kActorNA];
-#pragma unroll
-    for (int cb = 0; cb < 2; ++cb) { z[cb][0] = zz[cb][0]; z[cb][1] = zz[cb][1]; }
-#else
     float z[2][kActorNA];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) { z[cb][0] = zz[cb].x; z[cb][1] = zz[cb].y; }
-#endif
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -566,13 +546,8 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     // lane l < 32 takes house l (column block l >> 4, column l & 15)
     const int r = lane & 31;
     const bool upper = (lane & 16) != 0;
-#ifdef MDR_ACTOR_OUT_F64
-    const float z0 = (float)((upper ? z[1][0] : z[0][0]) + (double)b3[0]);
-    const float z1 = (float)((upper ? z[1][1] : z[0][1]) + (double)b3[1]);
-#else
     const float z0 = (upper ? z[1][0] : z[0][0]) + b3[0];
     const float z1 = (upper ? z[1][1] : z[0][1]) + b3[1];
-#endif
     // softmax over the 2 actions (fp32, max-subtracted like torch; one reciprocal of the sum, as
     // ATen's vectorised softmax) + Categorical sample
     const float zmax = fmaxf(z0, z1);
