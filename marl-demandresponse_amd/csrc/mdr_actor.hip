@@ -410,6 +410,10 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
         const int s = f < d.n_own ? f : d.own4 + ((f - d.n_own) / M) * d.m4 + (f - d.n_own) % M;
         dst[q] = w_row[rr * RS + actor_slot_off(d, s)];
       }
+      // (these stores' data registers are reused below: without a wait here the compiler's wait-count
+      // pass, merging this branch with the path that skips it, put an s_waitcnt vmcnt(0) in front of
+      // layer 1 on EVERY tile — which also waited out the next tile's prefetch loads just issued)
+      __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), on this path only
     }
     PSTAMP(2);
     // (the wave in its MFMA stage gets VALU issue priority over the SIMD's other wave, which is then
@@ -594,6 +598,11 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     src_kind = source_of(real_tile(v0), lane, src);
     stage_build(real_tile(v0));
   }
+  // the first build's loads have all landed (on every path): the compiler's wait-count pass otherwise
+  // carries them, pending on the lanes that skipped the build, into the tile loop and puts an
+  // s_waitcnt vmcnt(0) in front of layer 1 on EVERY tile — which also waits out the next tile's
+  // prefetch loads just issued (an HBM latency per tile instead of loads landing beside the MFMAs)
+  __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
   for (int j = 0; j < n_my; ++j) {
     const uint32_t vj = v0 + (uint32_t)j * stride;
     const uint32_t tj = real_tile(vj);
