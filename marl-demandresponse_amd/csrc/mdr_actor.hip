@@ -367,7 +367,7 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
       }
     }
   };
-  // ---- the stages of a tile (mdr_actor.hip header: the ping-pong schedule below)
+  // ---- the stages of a tile (build, X, Y: the comment above k_actor)
   f32x2 zz[2];  // the tile's two logits per column block (partial over this lane's rows) between X and Y
   // build: the tile's LDS rows from the prefetched sources (+ the table topologies' gathers)
   auto stage_build = [&](uint32_t tl) {

@@ -24,7 +24,6 @@ def main():
     ap.add_argument("--ticks", type=int, default=20)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--waves", type=int, default=16, help="waves per count block (the library's MDR_COUNT_WAVES)")
-    ap.add_argument("--tpw", type=int, default=1, help="tiles per wave (the library's MDR_COUNT_TPW)")
     a = ap.parse_args()
     import torch
 
@@ -37,7 +36,7 @@ def main():
     lib = L.load()
     fn = lib.mdr_count_timing
     fn.argtypes = [C.c_void_p, C.c_int]
-    hpb = 128 * a.waves * a.tpw  # houses per block
+    hpb = 128 * a.waves  # houses per block
     nb = (a.houses + hpb - 1) // hpb
     buf = np.zeros(nb * 4, np.uint64)
     rows = []

@@ -19,15 +19,9 @@ timeout -k 10 200 python bench.py --workload actor --steps 50 --warmup 5 --no-cp
 python3 -c "import json; d=json.loads(open('$O/actor.log').read().strip().splitlines()[-1]); print('actor', '%.3e' % d['value'], 'k_actor us', round(d['roofline']['kernel_avg_us'],1))"
 timeout -k 10 120 python tools/actor_profile.py > $O/actor_prof.log 2>&1 || exit 1
 cat $O/actor_prof.log
-# k_actor A/B on this box: the default build, 8 waves per block (aw8), the rounded-hi split (arne)
-for r in 1 2; do for v in hip aw8 arne; do
-  MDR_LIB=marl-demandresponse_amd/mdr_amd/libmdr_$v.so timeout -k 10 120 python tools/actor_kbench.py --reps 20 > $O/akb_${v}_$r.log 2>&1 || exit 1
-  echo "$v: $(tail -n 1 $O/akb_${v}_$r.log)"
-done; done
-for v in hip aw8; do
-  MDR_LIB=marl-demandresponse_amd/mdr_amd/libmdr_$v.so timeout -k 10 120 python tools/actor_kbench.py --reps 20 --precision bf16 > $O/akb16_${v}.log 2>&1 || exit 1
-  echo "$v: $(tail -n 1 $O/akb16_${v}.log)"
-done
+# (the r04f run also timed A/B builds — 8 waves per block, the rounded-hi split — built with
+#  python marl-demandresponse_amd/build_ext.py --variant aw8 MDR_ACTOR_MAXW=8 / --variant arne MDR_ACTOR_RNE_SPLIT;
+#  results in profiles/r04f_actor_ab.log)
 timeout -k 10 700 python -u -m pytest -v --timeout 300 --timeout-method thread -m gpu tests > $O/pytest.log 2>&1; rc=$?
 tail -3 $O/pytest.log; grep -E "FAILED|ERROR" $O/pytest.log | head -20
 exit $rc
