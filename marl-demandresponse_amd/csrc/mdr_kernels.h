@@ -177,8 +177,8 @@ constexpr int kGqCells = 256;   // cells of the key -> bin map (gq_bin)
 #ifndef MDR_GQ_SEL_BLOCKS
 #define MDR_GQ_SEL_BLOCKS 256
 #endif
-constexpr int kGqSelBlocks = MDR_GQ_SEL_BLOCKS;  // (MDR_GQ_SEL_BLOCKS: A/B builds)
-constexpr int kGqMaxRanks = 64;   // sharded histogram select: ranks whose windows k_gq_select gathers  // k_gq_select grid (1024 threads each: one window house per wave)
+constexpr int kGqSelBlocks = MDR_GQ_SEL_BLOCKS;  // k_gq_select grid, 1024 threads each (MDR_GQ_SEL_BLOCKS: A/B builds)
+constexpr int kGqMaxRanks = 64;   // sharded histogram select: ranks whose windows k_gq_select gathers
 struct GqSel;
 void gq_sel_init(void* sel128, uint32_t* map);  // host: the first call's key map (uniform over [-32, 32])
 void gq_diag_of(const void* sel128, uint64_t* out);

@@ -1872,31 +1872,31 @@ __device__ __forceinline__ void gq_block_scan(double& x, unsigned long long& xc,
   for (int w = 0; w < wv; ++w) { x += s_w[w]; xc += s_wc[w]; }  // (fixed order: the same sums in every block)
 }
 
-// K2: every block first finds the crossing superbin itself (the cumulative P where it reaches S;
-// the same arithmetic in every block, so every block agrees), block 0 records it and zeroes the
-// current count slab (compact and select fill it) and the window allocator; then the class counts
-// of the bins of superbins sb and sb + 1 (the crossing superbin and the room after it).  The
-// block's codes are loaded first: they stay in flight through the scan.  (The next call's key map
-// is k_gq_select's: gq_next_map.)
-__global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_t* __restrict__ code,
-                                                        unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
-                                                        unsigned long long* __restrict__ slab) {
-  constexpr int NB = 2 * (kGqBins / kGqSuper), NW = kGqThreads / 64;
+// relaxed agent-scope (sc1) stores and loads: write-through / L2-served, for data other workgroups of
+// the same launch read (MI355X_MICROARCH.md, Valid forms)
+template <typename T>
+__device__ __forceinline__ void st_sc1(T* d, T v) { __hip_atomic_store(d, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+template <typename T>
+__device__ __forceinline__ T ld_sc1(const T* s) { return __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// The crossing superbin (k_gq_bins): every block scans the superbin class counts
+// itself (the cumulative P where it reaches S; the same arithmetic in every block, so every block
+// agrees), block 0 records it and zeroes the current count slab (compact and select fill it) and the
+// window allocator.  Returns the superbin, the P and houses before it and the cluster's houses.
+struct GqSuper {
+  int sb;
+  bool whole;  // a cluster of <= kGqCap houses is one window (the select orders all of it, NaN keys included)
+  double before;
+  unsigned long long before_cnt, total;
+};
+__device__ __forceinline__ GqSuper gq_super_find(const KParams& p, const unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
+                                 unsigned long long* __restrict__ slab) {
+  constexpr int NW = kGqThreads / 64;
   static_assert(kGqSupN <= kGqThreads && kGqCells < kGqThreads, "one superbin / cell edge per thread");
-  __shared__ unsigned s_h[NW][NB * 4];
-  __shared__ double s_w[NW];
-  __shared__ unsigned long long s_wc[NW];
+  __shared__ double s_w[NW], s_bt;
+  __shared__ unsigned long long s_wc[NW], s_total, s_bc;
   __shared__ int s_first;
-  __shared__ unsigned long long s_total;
   const int tid = threadIdx.x;
-  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  const int64_t i00 = (int64_t)blockIdx.x * blockDim.x + tid;
-  uint32_t cd[kGqUnroll];
-#pragma unroll
-  for (int u = 0; u < kGqUnroll; ++u) {
-    const int64_t i = i00 + u * stride;
-    cd[u] = i < p.n ? code[i] : ~0u;  // (~0u: a bin past kGqBins, never counted)
-  }
   double p_on[kWinCap];
 #pragma unroll
   for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
@@ -1911,15 +1911,15 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_
   const unsigned long long cs = c[0] + c[1] + c[2] + c[3];
   double x = ps;
   unsigned long long xc = cs;
-  if (tid == 0) s_first = kGqSupN;
+  if (tid == 0) { s_first = kGqSupN; s_bt = 0.0; s_bc = 0ull; }
   gq_block_scan(x, xc, s_w, s_wc);
   const double before = x - ps;
   if (tid < kGqSupN && cs > 0 && !(before + ps < S)) atomicMin(&s_first, tid);  // (the first: a non-empty superbin)
   if (tid == kGqSupN - 1) s_total = xc;
   __syncthreads();
   const int sb = s_first;
-  // a cluster of <= kGqCap houses is one window (the select orders all of it, NaN keys included)
   const bool whole = sb < kGqSupN && s_total <= (unsigned long long)kGqCap;
+  if (tid == sb) { s_bt = before; s_bc = xc - cs; }
   if (blockIdx.x == 0) {
     if (tid == sb) { sel->base_tot = before; sel->base_cnt = xc - cs; }
     if (tid == kGqSupN - 1) sel->total = xc;
@@ -1934,33 +1934,67 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_
     if (slab)
       for (int e = tid; e < kCountShards * p.n_cap; e += blockDim.x) slab[e] = 0ull;
   }
-  if (sb >= kGqSuper || whole) return;  // everything taken, a NaN crossing, or one window (block-uniform)
-  for (int e = tid; e < NW * NB * 4; e += blockDim.x) (&s_h[0][0])[e] = 0u;
   __syncthreads();
-  const int bb = sb * (kGqBins / kGqSuper);
-  auto add = [&](uint32_t cc) {
-    const uint32_t b = cc >> 2;  // (NaN keys: kGqBins, past every band)
-    if (b < (uint32_t)kGqBins && b >= (uint32_t)bb && b < (uint32_t)(bb + NB))
-      atomicAdd(&s_h[tid >> 6][(b - bb) * 4 + (cc & 3u)], 1u);
-  };
+  return GqSuper{sb, whole, s_bt, s_bc, s_total};
+}
+
+// The class counts of the bins of superbins sb and sb + 1 (the crossing superbin and the room after
+// it) over a block's codes: per-wave LDS copies s_h (NW x 128 bins x 4 classes, zeroed here), then
+// one add per non-zero entry into copy blockIdx % kGqCopies of the global bin histograms
+constexpr int kGqBinBand = 2 * (kGqBins / kGqSuper);  // bins of two superbins
+template <int NC>
+__device__ __forceinline__ void gq_bins_add(const uint32_t* cd, int bb, unsigned* s_h) {
+  const uint32_t b0 = (uint32_t)bb;
 #pragma unroll
-  for (int u = 0; u < kGqUnroll; ++u) add(cd[u]);
+  for (int u = 0; u < NC; ++u) {
+    const uint32_t b = cd[u] >> 2;  // (NaN keys: kGqBins, past every band; ~0u: no house)
+    if (b < (uint32_t)kGqBins && b >= b0 && b < b0 + kGqBinBand)
+      atomicAdd(&s_h[(threadIdx.x >> 6) * (kGqBinBand * 4) + (b - b0) * 4 + (cd[u] & 3u)], 1u);
+  }
+}
+__device__ __forceinline__ void gq_bins_flush(const unsigned* s_h, unsigned* __restrict__ hist) {
+  constexpr int NW = kGqThreads / 64;
+  for (int e = threadIdx.x; e < kGqBinBand * 4; e += blockDim.x) {
+    unsigned v = 0u;
+#pragma unroll
+    for (int w = 0; w < NW; ++w) v += s_h[w * (kGqBinBand * 4) + e];
+    if (v) atomicAdd(&hist[(blockIdx.x % kGqCopies) * (kGqBinBand * 4) + e], v);
+  }
+}
+
+// K2: the crossing superbin (gq_super_find), then the class counts of its bins and the next
+// superbin's (gq_bins_add).  The block's codes are loaded first: they stay in flight through the
+// scan.  (The next call's key map is k_gq_select's: gq_next_map.)
+__global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_t* __restrict__ code,
+                                                        unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
+                                                        unsigned long long* __restrict__ slab) {
+  constexpr int NW = kGqThreads / 64;
+  __shared__ unsigned s_h[NW * kGqBinBand * 4];
+  const int tid = threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  const int64_t i00 = (int64_t)blockIdx.x * blockDim.x + tid;
+  uint32_t cd[kGqUnroll];
+#pragma unroll
+  for (int u = 0; u < kGqUnroll; ++u) {
+    const int64_t i = i00 + u * stride;
+    cd[u] = i < p.n ? code[i] : ~0u;  // (~0u: a bin past kGqBins, never counted)
+  }
+  const GqSuper g = gq_super_find(p, hist, S, sel, slab);
+  if (g.sb >= kGqSuper || g.whole) return;  // everything taken, a NaN crossing, or one window (block-uniform)
+  for (int e = tid; e < NW * kGqBinBand * 4; e += blockDim.x) s_h[e] = 0u;
+  __syncthreads();
+  const int bb = g.sb * (kGqBins / kGqSuper);
+  gq_bins_add<kGqUnroll>(cd, bb, s_h);
   for (int64_t i0 = i00 + kGqUnroll * stride; i0 < p.n; i0 += kGqUnroll * stride) {  // (n > one pass)
 #pragma unroll
     for (int u = 0; u < kGqUnroll; ++u) {
       const int64_t i = i0 + u * stride;
       cd[u] = i < p.n ? code[i] : ~0u;
     }
-#pragma unroll
-    for (int u = 0; u < kGqUnroll; ++u) add(cd[u]);
+    gq_bins_add<kGqUnroll>(cd, bb, s_h);
   }
   __syncthreads();
-  for (int e = tid; e < NB * 4; e += blockDim.x) {
-    unsigned v = 0u;
-#pragma unroll
-    for (int w = 0; w < NW; ++w) v += s_h[w][e];
-    if (v) atomicAdd(&hist[(blockIdx.x % kGqCopies) * (NB * 4) + e], v);
-  }
+  gq_bins_flush(s_h, hist);
 }
 
 // The next call's key map (gq_bin): cells over this call's finite key range [min, max] (the
@@ -2061,53 +2095,44 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
 __device__ __forceinline__ void gq_store_sc1(uint4* d, const uint4& v);
 __device__ __forceinline__ uint4 gq_load_sc1(const uint4* s);
 __device__ __forceinline__ bool gq_less(const uint4& a, const uint4& b);
-template <typename T>
-__device__ __forceinline__ void st_sc1(T* d, T v) { __hip_atomic_store(d, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
-template <typename T>
-__device__ __forceinline__ T ld_sc1(const T* s) { return __hip_atomic_load(s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
-__global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint32_t* __restrict__ code,
-                                                           unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
-                                                           uint4* __restrict__ win, uint8_t* __restrict__ action,
-                                                           unsigned long long* __restrict__ slab) {
+// The candidate window from the bin counts of the crossing superbin sb and the next (k_gq_compact):
+// the crossing bin b*
+// (lane l = bin l), the window [b*, b_end] over the next 64 bins, the P and houses before it.  Every
+// block runs the same arithmetic; block 0 records it in sel.  ovf: the fallback decides this call
+// (a NaN crossing found by gq_super_find, or a crossing bin alone over kGqCap houses).
+struct GqWin {
+  int bs, be;          // houses of bins < bs are taken, of bins in [bs, be] are candidates
+  bool ovf;
+  int ncand;
+  double win_tot;      // P before the window
+  bool more_after;     // houses after the window
+};
+__device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
+                           int sb, bool all, bool ovf, bool whole, double base_tot, unsigned long long base_cnt,
+                           unsigned long long total) {
   static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
   static_assert(kGqCopies * 512 <= kGqBins * 4, "the bin copies fit below the superbin copies");
-  constexpr int NW = kGqThreads / 64;
   __shared__ unsigned s_c[128];
-  __shared__ int s_l0, s_le;
+  __shared__ int s_l0, s_le, s_cnt;
   __shared__ double s_base;
   __shared__ unsigned long long s_basec;
-  __shared__ unsigned s_cnt[kWinCap];
-  __shared__ unsigned s_wt[NW];
-  __shared__ unsigned s_wbase;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // this block's houses first (every load before the selection reads: they stay in flight)
-  const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
-  constexpr int U = kGqStage / kGqThreads;
-  uint32_t cd[U], hw[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t i = b0 + u * kGqThreads + tid;
-    cd[u] = i < p.n ? code[i] : 0u;
-    hw[u] = i < p.n ? p.hvac[i] : 0u;
-  }
-  const bool all = sel->all, ovf = sel->overflow, whole = sel->whole;
+  const int tid = threadIdx.x, lane = tid & 63;
   const bool on = !all && !ovf && !whole;
-  const int bb = sel->sb * 64;
-  if (tid < kWinCap) s_cnt[tid] = 0u;
-  if (tid == 0) { s_l0 = 0; s_le = 0; }
+  const int bb = sb * 64;
+  if (tid == 0) { s_l0 = 0; s_le = 0; s_cnt = 0; s_base = 0.0; s_basec = 0ull; }
   if (on && tid < 128) {
     double p_on[kWinCap];
 #pragma unroll
     for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
     unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
 #pragma unroll
-    for (int q = 0; q < kGqCopies; ++q) {  // (k_gq_bins' copies, 128 bins x 4 classes each)
+    for (int q = 0; q < kGqCopies; ++q) {  // (gq_bins_flush's copies, 128 bins x 4 classes each)
       const uint4 v = *reinterpret_cast<const uint4*>(hist + q * 512 + tid * 4);
       c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] += v.w;
     }
     s_c[tid] = (unsigned)(c[0] + c[1] + c[2] + c[3]);
-    if (tid < 64) {  // wave 0: the crossing bin of superbin sb (it crosses: k_gq_bins)
+    if (tid < 64) {  // wave 0: the crossing bin of superbin sb (it crosses: gq_super_find)
       const double pb = win_power(p, c, p_on);
       const unsigned long long cb = c[0] + c[1] + c[2] + c[3];
       double xb = pb;
@@ -2118,8 +2143,8 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
         const unsigned long long yc = __shfl_up(xcb, off);
         if (lane >= off) { xb += y; xcb += yc; }
       }
-      const double bef = sel->base_tot + (xb - pb);
-      const unsigned long long befc = sel->base_cnt + (xcb - cb);
+      const double bef = base_tot + (xb - pb);
+      const unsigned long long befc = base_cnt + (xcb - cb);
       const unsigned long long m = __ballot(cb > 0 && !(bef + pb < S));
       const int l0 = m ? __ffsll((long long)m) - 1 : 63;
       if (lane == l0) { s_l0 = l0; s_base = bef; s_basec = befc; }
@@ -2146,13 +2171,13 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     else le = 63 - __clzll((long long)fit);
     const int cnt = (int)__shfl(pre, le);
     const bool wovf = !(fit & 1ull);
-    if (lane == 0) s_le = wovf ? -1 : le;
+    if (lane == 0) { s_le = wovf ? -1 : le; s_cnt = cnt; }
     if (lane == 0 && blockIdx.x == 0) {
       if (wovf) st_sc1(&sel->overflow, 1);
       st_sc1(&sel->bstar, bb + l0);
       st_sc1(&sel->bend, bb + l0 + le);
       st_sc1(&sel->win_tot, s_base);
-      st_sc1(&sel->more_after, s_basec + (unsigned long long)cnt < sel->total ? 1 : 0);
+      st_sc1(&sel->more_after, s_basec + (unsigned long long)cnt < total ? 1 : 0);
       st_sc1(&sel->ncand, cnt);
     }
   }
@@ -2161,11 +2186,37 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     st_sc1(&sel->bend, kGqBins);
     st_sc1(&sel->win_tot, 0.0);
     st_sc1(&sel->more_after, 0);
-    st_sc1(&sel->ncand, (int)sel->total);
+    st_sc1(&sel->ncand, (int)total);
   }
   __syncthreads();
-  if (ovf || s_le < 0) return;  // the fallback (gq_exact) decides every house (block-uniform)
-  const int bs = whole ? -1 : bb + s_l0, be = whole ? kGqBins : bb + s_l0 + s_le;
+  GqWin w;
+  w.ovf = ovf || s_le < 0;
+  w.bs = whole ? -1 : bb + s_l0;
+  w.be = whole ? kGqBins : bb + s_l0 + s_le;
+  w.ncand = whole ? (int)total : s_cnt;
+  w.win_tot = whole ? 0.0 : s_base;
+  w.more_after = !whole && s_basec + (unsigned long long)s_cnt < total;
+  return w;
+}
+
+// A block's houses against the window (k_gq_compact): every house of a bin below bs is
+// taken, the rest start as not taken (the select sets the window's), the window's houses go to win[]
+// as (okey, house << 2 | class, FSM word) at slots from one allocator atomic per block (unordered:
+// the select orders them), and the ON houses of the decided (non-window) houses are counted into the
+// slab.  House i = b0 + u * kGqThreads + tid.
+template <int U>
+__device__ __forceinline__ void gq_compact_houses(const KParams& p, const uint32_t* cd, const uint32_t* hw, int64_t b0,
+                                                  bool all, const GqWin& w, GqSel* __restrict__ sel,
+                                                  uint4* __restrict__ win, uint8_t* __restrict__ action,
+                                                  unsigned long long* __restrict__ slab) {
+  constexpr int NW = kGqThreads / 64;
+  __shared__ unsigned s_cnt[kWinCap];
+  __shared__ unsigned s_wt[NW];
+  __shared__ unsigned s_wbase;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  if (tid < kWinCap) s_cnt[tid] = 0u;
+  __syncthreads();
+  const int bs = w.bs, be = w.be;
   unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
   bool inw[U];
   unsigned mine = 0u;
@@ -2190,7 +2241,8 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
   // the window houses' exact keys (issued before the allocator's round trip)
   double kk[U];
 #pragma unroll
-  for (int u = 0; u < U; ++u) kk[u] = inw[u] ? gq_key_of(p, b0 + u * kGqThreads + tid) : 0.0;
+  for (int u = 0; u < U; ++u)
+    kk[u] = inw[u] ? gq_key_of(p, b0 + u * kGqThreads + tid) : 0.0;
   unsigned x = mine;  // this lane's slots: a wave prefix, the wave's offset in the block, the block's base
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -2205,9 +2257,9 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
   __syncthreads();
   if (tid == 0) {
     unsigned tot = 0u;
-    for (int w = 0; w < NW; ++w) {
-      const unsigned t = s_wt[w];
-      s_wt[w] = tot;
+    for (int k = 0; k < NW; ++k) {
+      const unsigned t = s_wt[k];
+      s_wt[k] = tot;
       tot += t;
     }
     s_wbase = tot ? atomicAdd(&sel->wcount, tot) : 0u;
@@ -2224,6 +2276,27 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
   }
   if (slab && tid < p.n_cap && s_cnt[tid])
     atomicAdd(&slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)s_cnt[tid]);
+}
+
+__global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint32_t* __restrict__ code,
+                                                           unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
+                                                           uint4* __restrict__ win, uint8_t* __restrict__ action,
+                                                           unsigned long long* __restrict__ slab) {
+  // this block's houses first (every load before the selection reads: they stay in flight)
+  const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
+  constexpr int U = kGqStage / kGqThreads;
+  uint32_t cd[U], hw[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = b0 + u * kGqThreads + threadIdx.x;
+    cd[u] = i < p.n ? code[i] : 0u;
+    hw[u] = i < p.n ? p.hvac[i] : 0u;
+  }
+  const bool all = sel->all;
+  const GqWin w = gq_window(p, hist, S, sel, sel->sb, all, sel->overflow != 0, sel->whole != 0, sel->base_tot,
+                                   sel->base_cnt, sel->total);
+  if (w.ovf) return;  // the fallback (gq_exact) decides every house (block-uniform)
+  gq_compact_houses<U>(p, cd, hw, b0, all, w, sel, win, action, slab);
 }
 
 // 16-B window entries handed between workgroups of one launch as two 8-B agent-scope (sc1) accesses
@@ -2560,6 +2633,24 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
 
 
 
+// The window's houses ranked by the launch's waves (k_gq_select): wave w of the grid
+// takes entries w, w + waves, ... of s_e[0, ncand) (the window in LDS) and counts how many entries
+// precede each in (key, house) order, the lanes splitting the comparisons (one LDS read serves all
+// of the wave's entries); the entry goes to sorted[rank] (sc1: read by the deciding block)
+__device__ void gq_rank(const uint4* s_e, int ncand, uint4* __restrict__ sorted) {
+  const int lane = threadIdx.x & 63, wpb = (int)(blockDim.x >> 6);
+  const int nwv = (int)gridDim.x * wpb;
+  for (int e = (int)blockIdx.x * wpb + (int)(threadIdx.x >> 6); e < ncand; e += nwv) {  // (wave-uniform)
+    const uint4 me = s_e[e];
+    unsigned r = 0u;
+#pragma unroll 2
+    for (int f = lane; f < ncand; f += 64) r += gq_less(s_e[f], me) ? 1u : 0u;
+#pragma unroll
+    for (int off = 32; off > 0; off >>= 1) r += __shfl_xor(r, off);
+    if (lane == 0 && r < (unsigned)kGqCap) gq_store_sc1(sorted + r, me);
+  }
+}
+
 // K4 (kGqSelBlocks workgroups of 1024): every block loads compact's unordered window win[0, ncand)
 // into LDS and ranks kGqCap / (kGqSelBlocks * 16) of its houses per wave (how many window houses
 // precede it in (key, house) order, the lanes splitting the comparisons; one LDS read serves all of
@@ -2618,32 +2709,7 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
       if (e < ncand) s_e[e] = v[u];
     }
     __syncthreads();
-    constexpr int EPW = kGqCap / (kGqSelBlocks * 16);
-    static_assert(EPW >= 1 && EPW * kGqSelBlocks * 16 == kGqCap, "the launch covers the window");
-    constexpr int nwv = kGqSelBlocks * 16;  // (gridDim.x == kGqSelBlocks, blockDim.x == 1024)
-    const int e0 = (int)blockIdx.x * 16 + wv;
-    if (e0 < ncand) {  // (wave-uniform)
-      uint4 me[EPW];
-      unsigned r[EPW];
-#pragma unroll
-      for (int j = 0; j < EPW; ++j) {
-        const int e = e0 + j * nwv;
-        me[j] = e < ncand ? s_e[e] : make_uint4(~0u, ~0u, ~0u, 0u);
-        r[j] = 0u;
-      }
-#pragma unroll 2
-      for (int f = lane; f < ncand; f += 64) {
-        const uint4 o = s_e[f];
-#pragma unroll
-        for (int j = 0; j < EPW; ++j) r[j] += gq_less(o, me[j]) ? 1u : 0u;
-      }
-#pragma unroll
-      for (int j = 0; j < EPW; ++j) {
-#pragma unroll
-        for (int off = 32; off > 0; off >>= 1) r[j] += __shfl_xor(r[j], off);
-        if (lane == 0 && e0 + j * nwv < ncand && r[j] < (unsigned)kGqCap) gq_store_sc1(sorted + r[j], me[j]);
-      }
-    }
+    gq_rank(s_e, ncand, sorted);
   }
   // the hand-off to the last block (cdna_hip_programming.md Guideline 16, MI355X_MICROARCH.md
   // Valid forms): every sorted[] store is sc1 and drained by its wave before the workgroup barrier
