@@ -296,15 +296,17 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
   if (pipe_ok) {
     int tpw = c->tpw >= 8 ? 8 : c->tpw >= 4 ? 4 : c->tpw >= 2 ? 2 : 1;
     if (hot_buffer) tpw = tpw >= 4 ? 4 : 2;  // the instantiated buffer variants
-    const unsigned nb = blocks(blocks(kp.n, 128), 4 * tpw);  // every tile covered: ceil(tiles / (4 waves x tpw))
+    // the greedy controller's keys in the epilogue (buffer actions: the C3 loop; blocks of
+    // kStepGqWaves waves), when its partials buffer holds this grid
+    const unsigned nbg = blocks(blocks(kp.n, 128), kStepGqWaves * tpw);
+    const bool epi = gq && hot_buffer && (int)nbg <= c->gq_parts_cap;
+    const int nwv = epi ? kStepGqWaves : 4;
+    const unsigned nb = blocks(blocks(kp.n, 128), nwv * tpw);  // every tile covered: ceil(tiles / (waves x tpw))
     const dim3 grid(nb);
-    // the greedy controller's keys in the epilogue (buffer actions: the C3 loop), when its
-    // partials buffer holds this grid
-    const bool epi = gq && hot_buffer && (int)nb <= c->gq_parts_cap;
     GqOut go{};
     if (epi) go = GqOut{gq_codes(c), c->g_part, c->g_hist, c->g_sel, c->g_map};
 #define MDR_LAUNCH_PIPE(T, A, LA, G)                                                                     \
-  hipLaunchKernelGGL((k_step_pipe<T, A, LA, G>), grid, dim3(256), 0, st, kp, action, tk, tkp, cur, reward, \
+  hipLaunchKernelGGL((k_step_pipe<T, A, LA, G>), grid, dim3(64 * nwv), 0, st, kp, action, tk, tkp, cur, reward, \
                      p_out, nxt, zer, go)
     if (hot_random) {
       if (tpw == 8) MDR_LAUNCH_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false);
@@ -1257,7 +1259,7 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_kpos, 2 * sizeof(int64_t)));
   HIP_TRY(hipMalloc(&c->g_extra, 64 * sizeof(int64_t)));
   // (min, max) partials: k_gq_keys' grid, or the grid of the step kernel whose epilogue writes the
-  // keys (k_step_pipe: a block per 4 x tpw x 128 houses, tpw >= 2)
+  // keys (k_step_pipe: a block per kStepGqWaves x tpw x 128 houses, tpw >= 2)
   c->gq_parts_cap = (int)std::max<int64_t>(kGqParts, (n + 1023) / 1024);
   HIP_TRY(hipMalloc(&c->g_part, 2 * (size_t)c->gq_parts_cap * sizeof(double)));
   HIP_TRY(hipMalloc(&c->g_hist, kGqHistWords * sizeof(unsigned)));

@@ -98,6 +98,12 @@ struct GqOut {
   const GqSel* sel;  // this call's key map: the cell grid (GqSel.kmin, .scale) ...
   const uint32_t* map;  // ... and the cells' bin ranges (gq_bin)
 };
+#ifndef MDR_GQ_STEP_WAVES
+#define MDR_GQ_STEP_WAVES 16
+#endif
+// waves per block of k_step_pipe with the GQ epilogue (4 without): fewer, larger blocks share one LDS
+// superbin histogram, so fewer global flushes (MDR_GQ_STEP_WAVES: A/B builds)
+constexpr int kStepGqWaves = MDR_GQ_STEP_WAVES;
 template <int TPW, int ACT, int LA, bool GQ = false>
 __global__ void k_step_pipe(KParams p, const uint8_t* action, TickArgs tk, const TickArgs* tkp,
                             const unsigned long long* counts, double* reward, double* p_out,

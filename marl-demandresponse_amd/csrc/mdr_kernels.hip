@@ -165,10 +165,11 @@ __device__ __forceinline__ double gq_key_of(const KParams& p, int64_t i) {
 }
 
 // the keys' producer side, shared by k_gq_keys and the step kernel's epilogue: a block's houses go
-// into per-wave LDS superbin histograms, then one flush per block (spread over kGqCopies copies)
-// and the block's (min, max) of the finite keys into part[]
-__device__ __forceinline__ void gq_flush(const unsigned* s_sh, int nw, unsigned* hist, double lo, double hi,
+// into ncopy LDS superbin histograms (wave w into copy w % ncopy), then one flush per block (spread
+// over kGqCopies global copies) and the block's (min, max) of the finite keys into part[]
+__device__ __forceinline__ void gq_flush(const unsigned* s_sh, int ncopy, unsigned* hist, double lo, double hi,
                                          double* part) {
+  const int nw = (int)(blockDim.x >> 6);
   __shared__ double s_lo[16], s_hi[16];
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -185,7 +186,7 @@ __device__ __forceinline__ void gq_flush(const unsigned* s_sh, int nw, unsigned*
   }
   for (int e = threadIdx.x; e < kGqSupStride; e += blockDim.x) {
     unsigned v = 0u;
-    for (int w = 0; w < nw; ++w) v += s_sh[w * kGqSupStride + e];
+    for (int w = 0; w < ncopy; ++w) v += s_sh[w * kGqSupStride + e];
     if (v) atomicAdd(&hist[kGqBins * 4 + (blockIdx.x % kGqCopies) * kGqSupStride + e], v);
   }
 }
@@ -479,9 +480,9 @@ __device__ __forceinline__ void load_tile2(const KParams& p, const uint8_t* acti
 
 // GQ: the greedy controller's keys of the post-step state, their superbin histogram and the
 // block's key range (k_gq_keys' outputs, gq_flush) as an epilogue, so the next mdr_ctrl_greedy
-// skips its key pass
+// skips its key pass; blocks of kStepGqWaves waves (4 LDS histogram copies) instead of 4
 template <int TPW, int ACT, int LA, bool GQ>
-__global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __restrict__ action, TickArgs tk0,
+__global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KParams p, const uint8_t* __restrict__ action, TickArgs tk0,
                                                    const TickArgs* tkp, const unsigned long long* __restrict__ counts,
                                                    double* __restrict__ reward, double* p_out,
                                                    unsigned long long* next_slab, unsigned long long* zero_slab,
@@ -624,7 +625,7 @@ __global__ void __launch_bounds__(256) k_step_pipe(KParams p, const uint8_t* __r
           gq_hi = fmax(gq_hi, k);
         }
         const uint32_t c = h ? c1 : c0;
-        atomicAdd(&s_gq[(tid >> 6) * kGqSupStride + (c >> 8) * 4 + (c & 3u)], 1u);
+        atomicAdd(&s_gq[((tid >> 6) & 3) * kGqSupStride + (c >> 8) * 4 + (c & 3u)], 1u);
       }
     }
     if (LA) {
