@@ -131,6 +131,9 @@ const char* mdr_build_id(void);
  * returns the number written */
 int mdr_abi_sizes(int64_t* out, int n);
 const char* mdr_last_error(void);
+/* Graph cache diagnostics: out[0..3] = cached rollout graphs, cached actor-rollout graphs,
+ * hipGraphLaunch calls of mdr_rollout, of mdr_actor_rollout; returns the number written. */
+int mdr_graph_info(mdr_ctx* ctx, int64_t* out, int n);
 int mdr_create(mdr_ctx** out, const mdr_config* cfg);
 int mdr_destroy(mdr_ctx* ctx);
 /* Bind the caller-owned SoA arrays (Environment.reset, environment.py:49-70). */
@@ -171,6 +174,16 @@ enum { MDR_OPT_STEP_TPW = 1, MDR_OPT_FASTDIV = 2, MDR_OPT_WINDOW_PIPELINE = 3, M
 /* (8 was MDR_OPT_ACTOR_PINGPONG, a k_actor schedule measured slower and retired in r04: rejected) */
 enum { MDR_THERMAL_EXACT = 0, MDR_THERMAL_AFFINE = 1 };
 int mdr_set_option(mdr_ctx* ctx, int option, int64_t value);
+
+/* ---- launch geometry (no reference counterpart) ---------------------------------------- */
+/* Bytes of the window ON-mask rows ([tiles][HPT][32] u64) that a window launch over n_local houses
+ * with `waves` waves per block touches (every wave of a ragged last block stores and loads the rows
+ * of its tile): the count launches use the build's kCountWaves, the step launches 4. */
+size_t mdr_window_onb_bytes(int64_t n_local, int waves);
+/* MDR_OK when ON-mask rows of onb_bytes and end words of wah_bytes cover every count and step
+ * window launch over n_local houses; MDR_EARG otherwise.  Every k_count_window / k_step_window
+ * launch checks its context's buffers with it, so a new launch geometry cannot overrun them. */
+int mdr_window_geometry_check(int64_t n_local, size_t onb_bytes, size_t wah_bytes);
 
 /* ---- population ------------------------------------------------------------------------ */
 /* Synthetic population drawn on device from Philox4x32-10(seed, global house id): the reference

@@ -117,15 +117,36 @@ def build(force: bool = False, verbose: bool = False, out: str = OUT, defines=()
     ``out=mdr_amd/libmdr_w4.so, defines=["MDR_WIN_WAVES=4"]``, loaded with MDR_LIB=...)."""
     if not force and out == OUT and up_to_date():
         return out
+    import tempfile
+
     tmp = out + ".tmp"
-    cmd = [hipcc()] + FLAGS + ["-D" + d for d in defines] + [f"-DMDR_SRC_HASH=\"{src_hash()}\""] + SRC + [
-        "-o", tmp, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
-    if verbose:
-        print(" ".join(cmd), flush=True)
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        sys.stderr.write(r.stdout + r.stderr)
-        raise RuntimeError(f"hipcc failed ({r.returncode})")
+    # one hipcc per translation unit, in parallel (each carries its own device code), then one link
+    cflags = [f for f in FLAGS if f != "-shared"] + ["-D" + d for d in defines] + [f"-DMDR_SRC_HASH=\"{src_hash()}\""]
+    with tempfile.TemporaryDirectory(prefix="mdr_build_") as td:
+        objs, procs = [], []
+        for src in SRC:
+            obj = os.path.join(td, os.path.basename(src) + ".o")
+            cmd = [hipcc()] + cflags + ["-c", src, "-o", obj]
+            if verbose:
+                print(" ".join(cmd), flush=True)
+            objs.append(obj)
+            procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True))
+        failed = []
+        for src, pr in zip(SRC, procs):
+            log = pr.communicate()[0]
+            if pr.returncode != 0:
+                failed.append(os.path.basename(src))
+                sys.stderr.write(log)
+        if failed:
+            raise RuntimeError(f"hipcc failed: {failed}")
+        cmd = [hipcc(), "-shared", "-fPIC", f"--offload-arch={ARCH}"] + objs + [
+            "-o", tmp, "-L/opt/rocm/lib", "-lrccl", "-Wl,-rpath,/opt/rocm/lib"]
+        if verbose:
+            print(" ".join(cmd), flush=True)
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stdout + r.stderr)
+            raise RuntimeError(f"hipcc link failed ({r.returncode})")
     os.replace(tmp, out)
     return out
 

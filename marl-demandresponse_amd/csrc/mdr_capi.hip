@@ -168,6 +168,7 @@ struct mdr_ctx {
   double* d_stats = nullptr;   // k_cluster_stats block partials
   size_t halo_bytes = 0;
   std::map<std::vector<int64_t>, hipGraphExec_t> actor_graphs;
+  int64_t graph_launches[2] = {0, 0};  // hipGraphLaunch calls: rollout graphs, actor rollout graphs
   // interpolated base power (row a10): grid | table | capacities
   double* d_interp = nullptr;
   size_t interp_bytes = 0;
@@ -226,6 +227,18 @@ int comm_halo(mdr_ctx* c, float* mine, float* recv, int lo, int hi, int M, hipSt
 }
 
 unsigned long long* slab_at(mdr_ctx* c, int r) { return c->d_slab + (size_t)((r % 3 + 3) % 3) * c->slab_len; }
+
+// All count slabs to zero with a kernel, never hipMemsetAsync: these launch sequences are captured
+// into graphs (mdr_rollout, mdr_actor_rollout), and on ROCm 7.2 a captured memset node wrote
+// non-zero words (host stack addresses, 0x7fff....) into the slabs on every replay after the
+// first (profiles/r05b_graph_memset_bisect.log: the slab only the memset touches, with every other
+// node of the graph removed in turn; tools/graph_memset_repro.hip), which the chained actor's
+// rollout read as counts of ~1e14 W in its first two ticks
+int zero_slabs(mdr_ctx* c, hipStream_t st) {
+  hipLaunchKernelGGL(k_zero_u64, dim3(1), dim3(256), 0, st, c->d_slab, (int64_t)kSlabs * c->slab_len);
+  LAUNCH_CHECK("k_zero_u64");
+  return MDR_OK;
+}
 
 int check_mode(int m) {
   return m == MDR_ACT_BUFFER || m == MDR_ACT_RANDOM || m == MDR_ACT_ALWAYS_ON ||
@@ -384,6 +397,15 @@ int mdr_abi_sizes(int64_t* out, int n) {
 }
 
 const char* mdr_last_error(void) { return g_err.c_str(); }
+
+int mdr_graph_info(mdr_ctx* c, int64_t* out, int n) {
+  if (!c || !out || n < 0) return fail(MDR_EARG, "mdr_graph_info: bad argument");
+  const int64_t v[4] = {(int64_t)c->graphs.size(), (int64_t)c->actor_graphs.size(), c->graph_launches[0],
+                        c->graph_launches[1]};
+  int k = 0;
+  for (; k < n && k < 4; ++k) out[k] = v[k];
+  return k;
+}
 
 int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   if (!out || !cfg) return fail(MDR_EARG, "mdr_create: null argument");
@@ -746,6 +768,23 @@ static int wslab_clean(mdr_ctx* c, hipStream_t st) {
 
 static unsigned win_grid(const mdr_ctx* c, int waves = 4) { return blocks(blocks(c->kp.n, 64 * kWinHpt), waves); }  // a tile per wave
 
+extern "C" size_t mdr_window_onb_bytes(int64_t n_local, int waves) {
+  if (n_local < 0 || waves < 1) return 0;
+  const size_t tiles = ((size_t)n_local + 64 * kWinHpt - 1) / (64 * kWinHpt);
+  return (tiles + waves - 1) / waves * waves * kWinHpt * kWindowMax * sizeof(uint64_t);
+}
+
+extern "C" int mdr_window_geometry_check(int64_t n_local, size_t onb_bytes, size_t wah_bytes) {
+  if (n_local < 1) return fail(MDR_EARG, "window launch: no houses");
+  const size_t need = std::max(mdr_window_onb_bytes(n_local, kCountWaves), mdr_window_onb_bytes(n_local, 4));
+  if (onb_bytes < need)
+    return fail(MDR_EARG, "window launch: ON-mask rows of " + std::to_string(onb_bytes) + " B, the launch geometry touches " +
+                              std::to_string(need) + " B");
+  if (wah_bytes < (size_t)n_local * sizeof(uint32_t))
+    return fail(MDR_EARG, "window launch: end-word buffer shorter than the shard");
+  return MDR_OK;
+}
+
 // the first window's FSM count: ticks from tk (staged) or tick0 + j (tk == nullptr), from the
 // state's FSM words (w_in == nullptr) or from the end words of the previous window
 // p_only: the count kernel's last block also does the window's P-only reduce (win_reduce_last),
@@ -758,6 +797,7 @@ static unsigned long long* win_red_ptr(const mdr_ctx* c, unsigned long long* slo
 static int launch_count(mdr_ctx* c, int mode, const uint8_t* action, int64_t act_stride, const TickArgs* tk,
                         uint64_t tick0, int K, unsigned long long* slot, uint64_t* onb, uint32_t* wah,
                         const uint32_t* w_in, hipStream_t st, bool p_only = false) {
+  if (int rc = mdr_window_geometry_check(c->kp.n, c->onb_bytes, c->wah_bytes)) return rc;
   const unsigned grid = win_grid(c, kCountWaves);
   unsigned* ticket = p_only ? c->d_tickets : nullptr;
 #define MDR_COUNT(A)                                                                                  \
@@ -777,6 +817,7 @@ static int launch_step_window(mdr_ctx* c, int mode, bool ka, const uint8_t* acti
                               const TickArgs* tk, int K, int la_K, const double* rec, double* reward,
                               int64_t rew_stride, uint64_t* onb, uint32_t* wah, unsigned long long* next_slot,
                               const WinDrv& dv, hipStream_t st) {
+  if (int rc = mdr_window_geometry_check(c->kp.n, c->onb_bytes, c->wah_bytes)) return rc;
   const unsigned grid = win_grid(c);
   hipEvent_t t0 = nullptr, t1 = nullptr;
   if (c->step_events) {
@@ -963,7 +1004,7 @@ static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t ac
     return window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, false, st);
   if (mode == MDR_ACT_BANGBANG || mode == MDR_ACT_DEADBAND_BANGBANG)
     return fail(MDR_EARG, "rollout: bang-bang sources need the per-step API (mdr_step with a lookahead)");
-  HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
+  if (int rc = zero_slabs(c, st)) return rc;
   c->ring = 0;
   const bool la = lookahead_ok(mode);
   for (int t = 0; t < n; ++t) {
@@ -1055,6 +1096,7 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
     c->wslab_dirty = true;
     return fail(MDR_EHIP, "mdr_rollout: hipGraphLaunch");
   }
+  ++c->graph_launches[0];
   c->ring = it->second.second;
   c->counts_ready = false;
   return MDR_OK;
@@ -2138,7 +2180,7 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
 
   ObsArgs o = obs_args(c, sp, &osc[0]);
   auto launches = [&](hipStream_t ls) -> int {
-    HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), ls));
+    if (int rc = zero_slabs(c, ls)) return rc;
     c->ring = 0;
     for (int t = 0; t < n; ++t) {
       // the current slab is zero here: the memset above (t = 0), then the previous two steps
@@ -2155,10 +2197,7 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
     return MDR_OK;
   };
   if (!action && !c->d_act) HIP_TRY(hipMalloc(&c->d_act, c->kp.n));  // context-owned action row
-  // the layer chain runs as direct launches: replays of its captured graph after the first gave
-  // wrong counts for the first two ticks on ROCm 7.2 (tools/chain_debug.py; direct launches and
-  // the fused kernel's graph are exact), so it is not captured
-  if (!use_graph || !actor_fused_ok(c, sp)) {
+  if (!use_graph) {
     const int rc = launches(st);
     c->counts_ready = false;
     return rc;
@@ -2176,6 +2215,7 @@ int mdr_actor_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const mdr_obs_sc
     c->ring = n % 3;
   }
   HIP_TRY(hipGraphLaunch(it->second, st));
+  ++c->graph_launches[1];
   c->counts_ready = false;
   return MDR_OK;
 }
@@ -2229,9 +2269,12 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
   c->ring = 0;
   // overlap (fused actor, >= 4 tiles, a comm stream): per tick the halo is packed and exchanged on the
   // comm stream while the interior tiles' actor runs on the compute stream; the first and last
-  // tile (the only readers of the halo: lo, hi <= 32) follow once it has landed
+  // tile follow once it has landed.  They are the only readers of the halo when lo, hi <= 32 and
+  // the last tile holds no house whose ring reaches past it: tile ntile-2 reads houses up to
+  // 32 (ntile-1) + hi - 1, beyond the shard when the last tile is short, n % 32 in 1 .. hi-1
+  const int64_t rag = c->kp.n % 32;
   const bool overlap = halo && c->halo_overlap && c->comm_stream && actor_fused_ok(c, &spec) &&
-                       (c->kp.n + 31) / 32 >= 4;
+                       (c->kp.n + 31) / 32 >= 4 && lo <= 32 && hi <= 32 && (rag == 0 || rag >= hi);
   hipStream_t cs = c->comm_stream;
   for (int t = 0; t < n; ++t) {
     ObsArgs ot = o;

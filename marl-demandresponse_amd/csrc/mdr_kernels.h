@@ -80,6 +80,7 @@ struct ObsArgs {
 };
 
 __global__ void k_stage32(StagePack pk, int n, Rec32* dst);
+__global__ void k_zero_u64(unsigned long long* dst, int64_t n);
 constexpr int kPcHouses = 4;  // chunks of 256 houses per k_power_counts block (grid: blocks(n, 256 * kPcHouses))
 __global__ void k_power_counts(KParams p, const uint8_t* action, int action_mode, uint64_t tick,
                                const TickArgs* tkp, unsigned long long* slab);

@@ -38,6 +38,13 @@ __global__ void k_stage32(StagePack pk, int n, Rec32* __restrict__ dst) {
   if (i < n) dst[i] = pk.r[i];
 }
 
+// n 64-bit zeros from a kernel (the count slabs inside captured launch sequences: see
+// mdr_capi.hip zero_u64)
+__global__ void k_zero_u64(unsigned long long* __restrict__ dst, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    dst[i] = 0ull;
+}
+
 // --------------------------------------------------------------------------------------- K0
 // Phase 1: FSM only -> ON count per capacity class (cluster.py:82-88).  Reads 6 B per house.
 __global__ void __launch_bounds__(256) k_power_counts(KParams p, const uint8_t* __restrict__ action,

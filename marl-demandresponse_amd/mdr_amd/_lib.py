@@ -120,12 +120,15 @@ SIGNATURES = {
     "mdr_abi_version": (I, []),
     "mdr_abi_sizes": (I, [P(I64), I]),
     "mdr_last_error": (C.c_char_p, []),
+    "mdr_graph_info": (I, [VP, P(I64), I]),
     "mdr_create": (I, [P(VP), P(mdr_config)]),
     "mdr_destroy": (I, [VP]),
     "mdr_bind": (I, [VP, P(mdr_soa)]),
     "mdr_params_changed": (I, [VP]),
     "mdr_set_rollout_window": (I, [VP, I]),
     "mdr_set_option": (I, [VP, I, I64]),
+    "mdr_window_onb_bytes": (C.c_size_t, [I64, I]),
+    "mdr_window_geometry_check": (I, [I64, C.c_size_t, C.c_size_t]),
     "mdr_time_step_kernels": (I, [VP, I, VP, VP, I64, I, VP, I64, VP, P(C.c_float), P(I)]),
     "mdr_rollout_begin": (I, [VP, I, U64, VP, I64, I, VP]),
     "mdr_populate": (I, [VP, P(mdr_pop_spec), VP]),

@@ -146,6 +146,14 @@ class HipShard:
         L.check(self.lib.mdr_power_counts(self.ctx, L.ptr(action), mode, tick, self.stream()),
                 "mdr_power_counts")
 
+    def graph_info(self):
+        """{rollout_graphs, actor_graphs, rollout_launches, actor_launches}: cached graphs and
+        hipGraphLaunch calls (mdr_graph_info)."""
+        out = (C.c_int64 * 4)()
+        rc = self.lib.mdr_graph_info(self.ctx, out, 4)
+        L.check(0 if rc == 4 else rc, "mdr_graph_info")
+        return dict(zip(("rollout_graphs", "actor_graphs", "rollout_launches", "actor_launches"), list(out)))
+
     def counts_buffer(self):
         p = C.c_void_p()
         n = C.c_int()

@@ -89,26 +89,35 @@ def test_actor_layouts_vs_torch(torch_gpu, layout, precision):
     gu.assert_not_saturated(tp[:, 1], a)
 
 
-@pytest.mark.parametrize("layout", ["three_layers", "msg_thermal_hvac"])
-def test_chain_rollout_equals_loop(torch_gpu, layout):
-    """The chain inside DeviceActor.rollout's captured graph (actor chain -> step per tick, replayed
-    twice) == select_actions / step_tensor, with the counts of the sampled actions from
-    k_actor_head."""
+@pytest.mark.parametrize("layout,T", [("three_layers", 6), ("msg_thermal_hvac", 6), ("three_layers", 1),
+                                      ("default", 6)])
+def test_chain_rollout_equals_loop(torch_gpu, layout, T):
+    """DeviceActor.rollout's captured graph (actor -> step per tick), launched three times (the
+    first launch after capture, then two replays), == select_actions / step_tensor, with the counts
+    of the sampled actions from k_actor_head (the chain) or k_actor (default: the fused kernel).
+    r04 ran the chain uncaptured because its replays read counts of ~1e14 W in ticks 0-1: the
+    graph's leading hipMemsetAsync node wrote host stack addresses into the count slabs on every
+    replay after the first (ROCm 7.2; tools/chain_bisect.py, tools/graph_memset_repro.hip).  The
+    slabs are now zeroed by a kernel node; graph_info asserts that every call replayed the graph."""
     from mdr_amd.actor import DeviceActor
 
     torch = torch_gpu
     extra, layers, _ = LAYOUTS[layout]
-    n, T = 2049, 6
+    n = 2049
     env_a, env_b = _env(n, extra, 8), _env(n, extra, 8)
     m = env_a.obs_tensor().abs().amax(0).double().cpu().numpy()
     actor = gu.calibrated_actor(env_a.obs_spec().n_feat, m, seed=2, layers=layers).to("cuda")
     da, db = DeviceActor(env_a, actor), DeviceActor(env_b, actor)
-    assert not da.fused()
+    assert da.fused() == (layout == "default")
     rew = torch.empty((T, n), dtype=torch.float64, device="cuda")
     acts = torch.empty((T, n), dtype=torch.uint8, device="cuda")
     probs = torch.empty((T, n), dtype=torch.float32, device="cuda")
-    for rep in range(2):
+    g0 = env_a.shard.graph_info()
+    for rep in range(3):
         da.rollout(T, rewards=rew, actions=acts, probs=probs)
+        gi = env_a.shard.graph_info()
+        assert gi["actor_launches"] == g0["actor_launches"] + rep + 1, gi
+        assert gi["actor_graphs"] == 1, gi
         for t in range(T):
             a, p = db.select_actions(count_next=True)
             r = env_b.step_tensor(a)

@@ -13,7 +13,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 def declared_symbols():
     with open(os.path.join(ROOT, "include", "mdr.h")) as f:
         src = f.read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(mdr_\w+)\s*\(", src, re.M)))
+    return sorted(set(re.findall(r"^(?:int|size_t|const char\*)\s+(mdr_\w+)\s*\(", src, re.M)))
 
 
 def test_header_symbols_exported():
@@ -66,6 +66,30 @@ def test_argument_errors_without_gpu():
     assert lib.mdr_interp_load(None, None) == -1
     assert lib.mdr_interp_values(None, None, 1, 0.0, 0.0, 0.0, None, None) == -1
     assert lib.mdr_interp_sum(None, -1, 1.0, None, None) == -1
+
+
+def test_window_geometry_guard():
+    """The host-side check every k_count_window / k_step_window launch makes (the
+    r04j overrun of the ON-mask rows by a ragged 16-wave count block): buffers sized by mdr_create
+    pass at every shard size, and a buffer one byte short of what the launch geometry touches, or
+    an end-word buffer shorter than the shard, is refused with MDR_EARG before anything launches."""
+    from mdr_amd import _lib
+
+    lib = _lib.load()
+    hpt, kmax = 2, 32  # kWinHpt, kWindowMax (mdr_kernels.h)
+    for n in (1, 63, 64, 128, 129, 2049, 65536, 131071, 1 << 20, (1 << 20) + 7):
+        tiles = (n + 64 * hpt - 1) // (64 * hpt)
+        need = max(lib.mdr_window_onb_bytes(n, w) for w in (4, 16))
+        assert need >= tiles * hpt * kmax * 8  # every real tile's rows
+        assert lib.mdr_window_onb_bytes(n, 16) == (tiles + 15) // 16 * 16 * hpt * kmax * 8
+        # the allocation of mdr_create (mdr_capi.hip: whole count blocks + one row)
+        alloc = ((tiles + 16) // 16 * 16 * hpt + 1) * kmax * 8
+        assert lib.mdr_window_geometry_check(n, alloc, (n + 1) * 4) == 0, lib.mdr_last_error()
+        assert lib.mdr_window_geometry_check(n, need, n * 4) == 0
+        assert lib.mdr_window_geometry_check(n, need - 1, n * 4) == -1
+        assert b"ON-mask" in lib.mdr_last_error()
+        assert lib.mdr_window_geometry_check(n, need, n * 4 - 1) == -1
+    assert lib.mdr_window_geometry_check(0, 1 << 20, 1 << 20) == -1
 
 
 def test_environment_fails_loudly_without_gpu():

@@ -245,6 +245,13 @@ def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo, laye
     ("gloo", "host", 3, False, 3001, (100, 100)),   # the C loop: halo on the side stream beside the interior tiles
     ("gloo", "host-serialhalo", 3, False, 3001, (100, 100)),  # halo pack -> send/recv -> actor -> allreduce -> step
     ("gloo", "host", 3, False, 3001, (64, 64, 64)),  # the layer chain (k_obs reads the halo) in the C loop
+    # ragged shards around the interior / edge tile split: 994 = 32 * 31 + 2 houses per rank (the
+    # second-to-last tile's ring reaches the next shard, so the halo overlap must stay off), 992
+    # (whole tiles), 101 = 32 * 3 + 5 (four tiles, the last one holding hi houses)
+    ("gloo", "host", 3, False, 3 * 994, (100, 100)),
+    ("gloo", "host-serialhalo", 3, False, 3 * 994, (100, 100)),
+    ("gloo", "host", 3, False, 3 * 992, (100, 100)),
+    ("gloo", "host", 3, False, 3 * 101, (100, 100)),
     ("gloo", "host", 8, False, 8 * 131072, (100, 100)),  # C5: the 1,048,576-house cluster on 8 ranks
 ])
 def test_sharded_actor_rollout_equals_single(tmp_path, backend, kind, world, force_halo, n, layers):

@@ -123,6 +123,65 @@ def test_affine_form_long_run(torch_gpu, n):
     print(f"n={n}: after 2000 ticks max rel |T_affine - T_exact| = {rel:.3g}, max |dr| = {worst:.3g}")
 
 
+C2_TICKS = 10000  # 64k houses x T = 10,000
+
+
+def test_affine_form_c2_horizon_vs_exact(torch_gpu):
+    """C2's whole horizon, 65,536 houses x 10,000 ticks (313 windows), of the default AFFINE form
+    against the EXACT form (bit-identical to the one-tick kernels, which the reference goldens pin):
+    ON masks, lockout, seconds-since-off and P `==` after every 1,000-tick call; temperatures and
+    rewards within the north star's 1e-5 relative at every call (measured drift printed)."""
+    torch = torch_gpu
+    from mdr_amd import _lib as L
+
+    e1, e2 = _pair(65536)
+    e2.shard.set_option("window_thermal", L.THERMAL_EXACT)
+    worst_r = worst_t = 0.0
+    for c in range(C2_TICKS // 1000):
+        r1 = e1.rollout(1000, action_mode="random")
+        r2 = e2.rollout(1000, action_mode="random")
+        _close_state(torch, e1, e2, 1e-5)
+        rel = ((r1 - r2).abs() / r2.abs().clamp_min(1e-3)).max().item()
+        assert rel <= 1e-5, (c, rel)
+        worst_r = max(worst_r, rel)
+        s1, s2 = e1.shard.host_state(), e2.shard.host_state()
+        worst_t = max(worst_t, float(np.max(np.abs(s1["T"] - s2["T"]) / np.abs(s2["T"]))))
+    assert e1._tick == e2._tick
+    print(f"65,536 x {C2_TICKS} ticks: max rel |T_affine - T_exact| = {worst_t:.3g}, "
+          f"max rel reward difference = {worst_r:.3g}")
+
+
+def test_affine_form_c2_horizon_vs_oracle(torch_gpu):
+    """The benched form (AFFINE, random actions) over C2's 10,000-tick horizon against the oracle
+    stepping the same Philox actions (4,096 houses, so the NumPy oracle finishes in seconds):
+    on / lock / sso and P `==` at the last tick, T, Tm and the last tick's rewards within 1e-5
+    relative (north star)."""
+    from mdr_amd.environment import Environment
+
+    n, seed = 4096, 4
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env = Environment(props, rng=random.Random(seed), seed=1234)
+    ora = O.OracleEnv(props, random.Random(seed))
+    tick0 = env._tick
+    rows = []
+    for c in range(C2_TICKS // 1000):
+        rows.append(env.rollout(1000, action_mode="random")[-1].cpu().numpy())
+    gids = np.arange(n, dtype=np.uint64)
+    for t in range(C2_TICKS):
+        o, rr = ora.step(PX.random_actions(1234, gids, tick0 + t))
+        if t % 1000 == 999:
+            np.testing.assert_allclose(rows[t // 1000], rr, rtol=1e-5, atol=1e-8, err_msg=f"reward t={t}")
+    st = env.shard.host_state()
+    for k in ("on", "lock", "sso"):
+        np.testing.assert_array_equal(st[k], o[k], err_msg=k)
+    np.testing.assert_allclose(st["T"], o["T"], rtol=1e-5, atol=0)
+    np.testing.assert_allclose(st["Tm"], o["Tm"], rtol=1e-5, atol=0)
+    assert env.cluster.current_power_consumption == o["P"]
+    rel = float(np.max(np.abs(st["T"] - o["T"]) / np.abs(o["T"])))
+    print(f"4,096 x {C2_TICKS} ticks vs the oracle: max rel |T - T_oracle| = {rel:.3g}")
+
+
 def test_window_options_validated(torch_gpu):
     """mdr_set_option rejects unknown options and out-of-range values (MDR_EARG)."""
     from mdr_amd import _lib as L

@@ -1,4 +1,5 @@
-"""Debug probe: the chained actor's rollout graph vs the select_actions / step_tensor loop."""
+"""Debug probe: the chained actor's rollout graph vs the select_actions / step_tensor loop, with the
+three per-tick count slabs dumped before and after every graph launch."""
 import os
 import random
 import sys
@@ -9,6 +10,7 @@ import torch  # noqa: E402
 
 import golden_util as gu  # noqa: E402
 from mdr_amd.actor import DeviceActor  # noqa: E402
+from mdr_amd.distributed import device_view  # noqa: E402
 from mdr_amd.environment import Environment  # noqa: E402
 
 
@@ -18,8 +20,17 @@ def env(n, seed):
                        rng=random.Random(seed))
 
 
-for layers, graph in (((64, 64, 64), True), ((64, 64, 64), False), ((100, 100), True)):
-    n, T = 2049, 6
+def slabs(e, T):
+    """The three count slabs [3][64][n_cap] (the library's ring is at T % 3 after a rollout of T)."""
+    ptr, ln = e.shard.counts_buffer()
+    base = ptr - (T % 3) * ln * 8
+    torch.cuda.synchronize()
+    v = device_view(base, 3 * ln, "<i8", "cuda").clone().cpu().reshape(3, ln)
+    return [(int(v[k].sum()), int(v[k].max())) for k in range(3)]
+
+
+for layers, T in (((64, 64, 64), 1), ((64, 64, 64), 2), ((64, 64, 64), 6), ((100, 100), 6)):
+    n = 2049
     ea, eb = env(n, 8), env(n, 8)
     m = ea.obs_tensor().abs().amax(0).double().cpu().numpy()
     actor = gu.calibrated_actor(ea.obs_spec().n_feat, m, seed=2, layers=layers).to("cuda")
@@ -27,12 +38,14 @@ for layers, graph in (((64, 64, 64), True), ((64, 64, 64), False), ((100, 100), 
     rew = torch.empty((T, n), dtype=torch.float64, device="cuda")
     acts = torch.empty((T, n), dtype=torch.uint8, device="cuda")
     for rep in range(3):
-        da.rollout(T, rewards=rew, actions=acts, use_graph=graph)
+        before = slabs(ea, 0 if rep == 0 else T)
+        da.rollout(T, rewards=rew, actions=acts, use_graph=True)
+        after = slabs(ea, T)
         bad = []
         for t in range(T):
             a, p = db.select_actions(count_next=True)
             r = eb.step_tensor(a)
             if not (torch.equal(a, acts[t]) and torch.equal(r, rew[t])):
                 bad.append((t, int((a != acts[t]).sum()), float(rew[t][0]), float(r[0])))
-        print(layers, "graph" if graph else "direct", "rep", rep, "fused", da.fused(), "P", ea._cluster_power(),
-              eb._cluster_power(), "bad", bad, flush=True)
+        print(layers, "T", T, "rep", rep, "fused", da.fused(), "slabs before", before, "after", after,
+              "bad", bad, flush=True)
