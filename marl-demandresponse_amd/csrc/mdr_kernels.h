@@ -132,6 +132,22 @@ template <int ACT, int HPT, bool SIMPLE, bool KA, int FORM>
 __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int K,
                               int la_K, const double* rec, double* reward, int64_t rew_stride, uint64_t* onb,
                               uint32_t* wah, unsigned long long* next_slot, WinDrv dv);
+// One-launch single-window rollout (k_window_rs, mdr_kernels.hip): count blocks and thermal blocks
+// of one launch, the thermal blocks waiting for the count blocks' published penalties.  The count
+// shards and tickets are self-cleaning (the last count block zeroes them after reading); the
+// published penalties carry the launch's epoch, so no flag needs a reset between launches.
+struct FuseSync {
+  unsigned long long* shards;  // [kWindowMax][kCountShards][n_cap] (the first kWinShards shards used), then
+                               // the published penalties: 8 copies x 64 words (flag = epoch | K values)
+  unsigned* arrive;            // grid_last_block tickets of the count blocks (kTicketWords, zero between launches)
+  unsigned* err;               // flag-wait timeouts (never expected: a diagnostic, mdr_graph_info)
+  unsigned long long* prof;    // diagnostics: [grid][8] phase stamps (100 MHz clock), or null
+};
+constexpr int kRsCountTiles = 8;  // tiles per count wave of k_window_rs (the host sizes the count blocks)
+template <int ACT, int HPT, bool SIMPLE>
+__global__ void k_window_rs(KParams p, const uint8_t* action, int64_t act_stride, int K, double* reward,
+                            int64_t rew_stride, uint64_t* onb, uint32_t* wah, WinDrv dv, FuseSync fs, uint32_t nC,
+                            uint32_t ntile, uint32_t epoch);
 __global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
 __global__ void k_win_records(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
 template <int ACT, int HPT>
