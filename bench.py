@@ -110,9 +110,6 @@ def parse():
     ap.add_argument("--graph", default="off", choices=["on", "off"],
                     help="rollout launch policy: off = Environment.rollout's default (direct launches, the first "
                          "window's drivers as kernel arguments), on = staged drivers + hipGraph replay")
-    ap.add_argument("--fused", default="on", choices=["on", "off"],
-                    help="single-window calls as one persistent launch (k_window_fused, MDR_OPT_WINDOW_FUSED) "
-                         "or the count + step kernel pair")
     ap.add_argument("--mode", default="random", choices=["random", "buffer"])
     ap.add_argument("--workload", default="step", choices=["step", "actor", "greedy"],
                     help="step: env.step with fused random actions (the BASELINE metric); actor: "
@@ -374,7 +371,6 @@ def main():
     window = min(max(args.window, 0), 32)
     sh.set_rollout_window(window)
     sh.set_option("window_thermal", L.THERMAL_AFFINE if args.thermal == "affine" else L.THERMAL_EXACT)
-    sh.set_option("window_fused", 1 if args.fused == "on" else 0)
     chunk = min(args.chunk, args.steps)
     chunks = [chunk] * (args.steps // chunk) + ([args.steps % chunk] if args.steps % chunk else [])
     acts = None

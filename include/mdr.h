@@ -131,15 +131,9 @@ const char* mdr_build_id(void);
  * returns the number written */
 int mdr_abi_sizes(int64_t* out, int n);
 const char* mdr_last_error(void);
-/* Launch diagnostics: out[0..5] = cached rollout graphs, cached actor-rollout graphs,
- * hipGraphLaunch calls of mdr_rollout, of mdr_actor_rollout, k_window_rs launches, and (n > 5:
- * synchronises the device) k_window_rs flag-wait timeouts; returns the number written. */
+/* Graph cache diagnostics: out[0..3] = cached rollout graphs, cached actor-rollout graphs,
+ * hipGraphLaunch calls of mdr_rollout, of mdr_actor_rollout; returns the number written. */
 int mdr_graph_info(mdr_ctx* ctx, int64_t* out, int n);
-/* Diagnostics: the next k_window_rs launches write per-block phase stamps (the 100 MHz clock at
- * entry; count blocks: after the count flush, after the publish; thermal blocks: after the
- * coefficients, after the flag, at the end: 8 words per block) into dev_buf (device memory of
- * n_words u64; the launch fails with MDR_EARG when shorter than 8 x its grid); NULL / 0 stops. */
-int mdr_fused_stamps(mdr_ctx* ctx, unsigned long long* dev_buf, int64_t n_words);
 int mdr_create(mdr_ctx** out, const mdr_config* cfg);
 int mdr_destroy(mdr_ctx* ctx);
 /* Bind the caller-owned SoA arrays (Environment.reset, environment.py:49-70). */
@@ -169,9 +163,6 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           k_actor runs, then the first and last tile; 0 = halo, then one k_actor
  *   MDR_OPT_ACTOR_GENERIC   1 = k_actor runs its generic form for the reference's default obs layout too
  *                           (0, default: that layout runs the form specialised for it, mdr_actor.hip DEF)
- *   MDR_OPT_WINDOW_FUSED    1 (default) = a single-window rollout on one GPU (AFFINE form) runs as ONE
- *                           launch (k_window_rs: count blocks, then thermal blocks that wait for their
- *                           published penalties); 0 = the count kernel + step kernel pair
  *   MDR_OPT_WINDOW_THERMAL  k_step_window's per-tick thermal update: MDR_THERMAL_AFFINE (default)
  *                           = the reference's update as a per-house affine transition formed once
  *                           per window (4 FMAs per temperature per tick; ~1e-13 K per tick from the
@@ -179,7 +170,7 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           operation order every tick (bit-identical to the one-tick kernels) */
 enum { MDR_OPT_STEP_TPW = 1, MDR_OPT_FASTDIV = 2, MDR_OPT_WINDOW_PIPELINE = 3, MDR_OPT_SHARDED_OVERLAP = 4,
        MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7,
-       MDR_OPT_HALO_OVERLAP = 9, MDR_OPT_ACTOR_GENERIC = 10, MDR_OPT_WINDOW_FUSED = 11 };
+       MDR_OPT_HALO_OVERLAP = 9, MDR_OPT_ACTOR_GENERIC = 10 };
 /* (8 was MDR_OPT_ACTOR_PINGPONG, a k_actor schedule measured slower and retired in r04: rejected) */
 enum { MDR_THERMAL_EXACT = 0, MDR_THERMAL_AFFINE = 1 };
 int mdr_set_option(mdr_ctx* ctx, int option, int64_t value);

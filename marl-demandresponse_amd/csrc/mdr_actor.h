@@ -13,14 +13,8 @@ constexpr int kActorMaxSlots = 128;  // feature slots of the chunked row layout 
 constexpr int kActorKS2 = kActorMaxMB / 2;  // layer-2 k-steps of 32 (hidden rows 0 .. 127)
 // waves per block of k_actor (one block per CU: the block shares the LDS weight image).  The
 // default-layout (DEF) forms fit more waves per SIMD: bf16 4 (<= 128 VGPRs), bf16x3 3 (<= 168); the
-// generic forms and the fp32-faithful form (three operand planes) 2.  (MDR_ACTOR_MAXW caps it, for
-// measurements.)
-#ifndef MDR_ACTOR_MAXW
-#define MDR_ACTOR_MAXW 16
-#endif
-constexpr int actor_max_waves(int prec, bool def) {
-  return !def || prec == 6 ? 8 : (prec == 1 ? 16 : 12) < MDR_ACTOR_MAXW ? (prec == 1 ? 16 : 12) : MDR_ACTOR_MAXW;
-}
+// generic forms and the fp32-faithful form (three operand planes) 2.
+constexpr int actor_max_waves(int prec, bool def) { return !def || prec == 6 ? 8 : prec == 1 ? 16 : 12; }
 
 // Shapes, the obs row's slot layout, byte offsets of the packed weight image (identical in global
 // memory and in LDS) and of the per-block LDS work areas.  Filled by the host (mdr_capi.hip

@@ -104,12 +104,6 @@ struct mdr_ctx {
   bool coef_dirty = true;
   int* d_flags = nullptr;                // [0] params_bad
   unsigned* d_tickets = nullptr;         // k_count_window's grid_last_block counters (zero between uses)
-  unsigned long long* d_fuse = nullptr;  // k_window_rs: count shards | published penalties | tickets | err
-  bool fuse_on = true;                   // MDR_OPT_WINDOW_FUSED
-  int64_t fuse_launches = 0;
-  uint32_t fuse_epoch = 0;               // the launch's id in the published flags (never 0)
-  unsigned long long* fuse_prof = nullptr;  // mdr_fused_stamps: phase stamps of the next launches
-  int64_t fuse_prof_words = 0;
   // rollout tick drivers
   TickArgs* d_ticks = nullptr;
   int ticks_cap = 0;
@@ -233,13 +227,6 @@ int comm_halo(mdr_ctx* c, float* mine, float* recv, int lo, int hi, int M, hipSt
 }
 
 unsigned long long* slab_at(mdr_ctx* c, int r) { return c->d_slab + (size_t)((r % 3 + 3) % 3) * c->slab_len; }
-
-// k_window_fused's buffer (u64 words): [kWindowMax][kCountShards][n_cap] count shards | published
-// penalties (kFuseCopies x kFuseCopyWords) | grid_last_block tickets (kTicketWords u32) | err (128 B)
-size_t fuse_shard_words(int n_cap) { return (size_t)kWindowMax * kCountShards * n_cap; }
-size_t fuse_ticket_off(int n_cap) { return fuse_shard_words(n_cap) + 8 * 64; }  // (u64 words)
-size_t fuse_err_off(int n_cap) { return fuse_ticket_off(n_cap) + kTicketWords / 2; }
-size_t fuse_bytes(int n_cap) { return (fuse_err_off(n_cap) + 16) * sizeof(unsigned long long); }
 
 // All count slabs to zero with a kernel, never hipMemsetAsync: these launch sequences are captured
 // into graphs (mdr_rollout, mdr_actor_rollout), and on ROCm 7.2 a captured memset node wrote
@@ -411,25 +398,12 @@ int mdr_abi_sizes(int64_t* out, int n) {
 
 const char* mdr_last_error(void) { return g_err.c_str(); }
 
-int mdr_fused_stamps(mdr_ctx* c, unsigned long long* dev_buf, int64_t n_words) {
-  if (!c || n_words < 0 || (n_words > 0 && !dev_buf)) return fail(MDR_EARG, "mdr_fused_stamps: bad argument");
-  c->fuse_prof = n_words > 0 ? dev_buf : nullptr;
-  c->fuse_prof_words = n_words;
-  return MDR_OK;
-}
-
 int mdr_graph_info(mdr_ctx* c, int64_t* out, int n) {
   if (!c || !out || n < 0) return fail(MDR_EARG, "mdr_graph_info: bad argument");
-  int64_t v[6] = {(int64_t)c->graphs.size(), (int64_t)c->actor_graphs.size(), c->graph_launches[0],
-                  c->graph_launches[1], c->fuse_launches, 0};
-  if (n > 5 && c->d_fuse) {  // k_window_rs flag-wait timeouts (synchronises)
-    unsigned err = 0;
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(&err, c->d_fuse + fuse_err_off(c->kp.n_cap), sizeof(unsigned), hipMemcpyDeviceToHost));
-    v[5] = err;
-  }
+  const int64_t v[4] = {(int64_t)c->graphs.size(), (int64_t)c->actor_graphs.size(), c->graph_launches[0],
+                        c->graph_launches[1]};
   int k = 0;
-  for (; k < n && k < 6; ++k) out[k] = v[k];
+  for (; k < n && k < 4; ++k) out[k] = v[k];
   return k;
 }
 
@@ -478,10 +452,6 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   k.q_on = c->d_tables;
   k.p_on = c->d_tables + MDR_MAX_CAP;
   if (hipMalloc(&c->d_flags, 16) != hipSuccess) return cleanup(fail(MDR_ENOMEM, "flags"));
-  if (cfg->n_cap <= kWindowCap &&
-      (hipMalloc(&c->d_fuse, fuse_bytes(cfg->n_cap)) != hipSuccess ||
-       hipMemset(c->d_fuse, 0, fuse_bytes(cfg->n_cap)) != hipSuccess))
-    return cleanup(fail(MDR_ENOMEM, "fused window counts"));
   if (hipMalloc(&c->d_tickets, kTicketWords * sizeof(unsigned)) != hipSuccess ||
       hipMemset(c->d_tickets, 0, kTicketWords * sizeof(unsigned)) != hipSuccess)
     return cleanup(fail(MDR_ENOMEM, "tickets"));
@@ -579,7 +549,6 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_win);
   hipFree(c->g_sorted); hipFree(c->g_map); hipFree(c->g_range); hipFree(c->g_tickets);
   hipFree(c->d_tickets);
-  hipFree(c->d_fuse);
   if (c->comm) ncclCommDestroy(c->comm);
   delete c;
   return MDR_OK;
@@ -600,7 +569,6 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_FORCE_HALO: c->force_halo = value != 0; break;
     case MDR_OPT_HALO_OVERLAP: c->halo_overlap = value != 0; break;
     case MDR_OPT_ACTOR_GENERIC: c->actor_generic = value != 0; break;
-    case MDR_OPT_WINDOW_FUSED: c->fuse_on = value != 0; break;
     case MDR_OPT_WINDOW_THERMAL:
       if (value != MDR_THERMAL_EXACT && value != MDR_THERMAL_AFFINE)
         return fail(MDR_EARG, "mdr_set_option: WINDOW_THERMAL must be MDR_THERMAL_EXACT or _AFFINE");
@@ -1065,70 +1033,6 @@ static int rollout_launches(mdr_ctx* c, int n, const uint8_t* action, int64_t ac
   return MDR_OK;
 }
 
-// ---- one-launch single-window rollout (k_window_rs, mdr_kernels.hip)
-// An n-tick rollout as one launch of count blocks + thermal blocks: one GPU (the whole cluster on
-// this context: the counts need no allreduce), the default AFFINE form, one window.  Otherwise
-// (false) the count kernel + step kernel pair runs.
-static bool fused_plan(const mdr_ctx* c, int n, int mode) {
-  return c->fuse_on && c->d_fuse && window_ok(c, mode) && c->thermal == MDR_THERMAL_AFFINE && n >= 1 && n <= c->win &&
-         n <= kWindowMax && !has_comm(c) && c->kp.n == c->kp.n_global && c->kp.goff == 0;
-}
-
-static int launch_fused(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action, int64_t act_stride,
-                        int mode, double* reward, int64_t rew_stride, double* p_out, hipStream_t st) {
-  if (int rc = mdr_window_geometry_check(c->kp.n, c->onb_bytes, c->wah_bytes)) return rc;
-  WinDrv dv{};
-  for (int j = 0; j < n; ++j) {
-    const mdr_tick& h = ticks[j];
-    dv.od_k[j] = h.t_od_prev + 273.0;  // (k_win_reduce's rec[0]: the same IEEE addition)
-    dv.solar[j] = h.solar;
-    dv.s_prev[j] = h.s_prev;
-    if (fabs(h.t_od_prev) < 1048576.0 && fabs(h.solar) < 1099511627776.0) dv.ok |= 1u << j;  // (win_tick_record)
-  }
-  dv.tick0 = ticks[0].tick;
-  dv.p_out = p_out;
-  const int ncap = c->kp.n_cap;
-  const bool prof = c->fuse_prof != nullptr;
-  FuseSync fs{c->d_fuse, reinterpret_cast<unsigned*>(c->d_fuse + fuse_ticket_off(ncap)),
-              reinterpret_cast<unsigned*>(c->d_fuse + fuse_err_off(ncap)), prof ? c->fuse_prof : nullptr};
-  const uint32_t ntile = (uint32_t)((c->kp.n + 64 * kWinHpt - 1) / (64 * kWinHpt));
-  // count blocks: MDR_RS_COUNT_PER_CU per CU (fewer for small clusters: at least a tile per count wave;
-  // more for large ones: at most kRsCountTiles tiles per count wave)
-  const int64_t per_cu = getenv("MDR_RS_COUNT_PER_CU") ? atoi(getenv("MDR_RS_COUNT_PER_CU")) : 1;
-  const uint32_t nC = (uint32_t)std::max<int64_t>(
-      std::max<int64_t>(1, std::min<int64_t>(per_cu * c->n_cu, (ntile + 3) / 4)),
-      (ntile + 4 * kRsCountTiles - 1) / (4 * kRsCountTiles));
-  const uint32_t grid = nC + (ntile + 3) / 4;
-  if (prof && c->fuse_prof_words < (int64_t)grid * 8) return fail(MDR_EARG, "mdr_fused_stamps: buffer shorter than 8 x grid");
-  if (++c->fuse_epoch == 0) c->fuse_epoch = 1;
-  const uint32_t epoch = c->fuse_epoch;
-  const KParams kp = c->kp;
-  const bool si = win_simple(c);
-  hipEvent_t t0 = nullptr, t1 = nullptr;
-  if (c->step_events) {
-    HIP_TRY(hipEventCreate(&t0));
-    c->step_events->push_back(t0);
-    HIP_TRY(hipEventCreate(&t1));
-    c->step_events->push_back(t1);
-  }
-#define MDR_RS(A, SI)                                                                                          \
-  do {                                                                                                         \
-    if (t0)                                                                                                    \
-      hipExtLaunchKernelGGL((k_window_rs<A, kWinHpt, SI>), dim3(grid), dim3(256), 0, st, t0, t1, 0, kp, action, act_stride, \
-                            n, reward, rew_stride, c->d_onb, c->d_wah, dv, fs, nC, ntile, epoch);             \
-    else                                                                                                       \
-      hipLaunchKernelGGL((k_window_rs<A, kWinHpt, SI>), dim3(grid), dim3(256), 0, st, kp, action, act_stride, n, \
-                         reward, rew_stride, c->d_onb, c->d_wah, dv, fs, nC, ntile, epoch);                   \
-  } while (0)
-  if (mode == MDR_ACT_RANDOM) { if (si) MDR_RS(MDR_ACT_RANDOM, true); else MDR_RS(MDR_ACT_RANDOM, false); }
-  else if (mode == MDR_ACT_ALWAYS_ON) { if (si) MDR_RS(MDR_ACT_ALWAYS_ON, true); else MDR_RS(MDR_ACT_ALWAYS_ON, false); }
-  else { if (si) MDR_RS(MDR_ACT_BUFFER, true); else MDR_RS(MDR_ACT_BUFFER, false); }
-#undef MDR_RS
-  LAUNCH_CHECK("k_window_rs");
-  ++c->fuse_launches;
-  return MDR_OK;
-}
-
 static bool consecutive(const mdr_tick* ticks, int n) {
   for (int i = 1; i < n; ++i)
     if (ticks[i].tick != ticks[0].tick + (uint64_t)i) return false;
@@ -1156,12 +1060,6 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
   c->begun.on = false;
   int rc = refresh_if_dirty(c, st);
   if (rc) return rc;
-  if (!counted && win && !use_graph && consec && fused_plan(c, n, mode)) {
-    // one window on one GPU: count blocks and thermal blocks in one launch
-    rc = launch_fused(c, n, ticks, action, act_stride, mode, reward, rew_stride, p_out, st);
-    c->counts_ready = false;
-    return rc;
-  }
   if (counted || (win && !use_graph && consec)) {
     // direct launches of the windowed path: the first window's drivers travel as kernel arguments
     // of its step kernel (window_launches host_ticks)
@@ -1222,7 +1120,6 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
   // the matching mdr_rollout_sharded launches just the KA step kernel
   const bool sharded = has_comm(c);
   if (sharded && n > c->win) return MDR_OK;
-  if (fused_plan(c, n, mode)) return MDR_OK;  // (one launch: mdr_rollout counts inside it)
   hipStream_t st = S(stream);
   int rc = refresh_if_dirty(c, st);
   if (!rc) rc = wslab_clean(c, st);

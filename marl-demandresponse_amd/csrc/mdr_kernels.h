@@ -10,12 +10,9 @@ namespace mdr {
 constexpr int kCountShards = 64;  // atomic shards for the per-class ON counts
 constexpr int kWinShards = 16;    // the shards a window count flush uses (the first 16 of kCountShards:
                                   // 128 adds per counter at 2048 blocks, one quarter of the reads to sum)
-// waves per k_count_window block (a tile of 64 * kWinHpt houses per wave; MDR_COUNT_WAVES: A/B builds):
+// waves per k_count_window block (a tile of 64 * kWinHpt houses per wave):
 // 16 (512 blocks at 1M houses) against 4: 15.6 vs 17.3 us for 20 ticks, 8.9 vs 14.5 for 1 (r04i)
-#ifndef MDR_COUNT_WAVES
-#define MDR_COUNT_WAVES 16
-#endif
-constexpr int kCountWaves = MDR_COUNT_WAVES;
+constexpr int kCountWaves = 16;
 constexpr int kTicketGroups = 64; // grid_last_block: group counters (+ 1 top), 32 words apart
 constexpr int kTicketWords = 32 * (kTicketGroups + 1);
 constexpr int kSlabs = 4;         // count slabs: ring of 3 (step path) / 4 (overlapped pipeline)
@@ -99,12 +96,9 @@ struct GqOut {
   const GqSel* sel;  // this call's key map: the cell grid (GqSel.kmin, .scale) ...
   const uint32_t* map;  // ... and the cells' bin ranges (gq_bin)
 };
-#ifndef MDR_GQ_STEP_WAVES
-#define MDR_GQ_STEP_WAVES 16
-#endif
 // waves per block of k_step_pipe with the GQ epilogue (4 without): fewer, larger blocks share one LDS
-// superbin histogram, so fewer global flushes (MDR_GQ_STEP_WAVES: A/B builds)
-constexpr int kStepGqWaves = MDR_GQ_STEP_WAVES;
+// superbin histogram, so fewer global flushes
+constexpr int kStepGqWaves = 16;
 template <int TPW, int ACT, int LA, bool GQ = false>
 __global__ void k_step_pipe(KParams p, const uint8_t* action, TickArgs tk, const TickArgs* tkp,
                             const unsigned long long* counts, double* reward, double* p_out,
@@ -132,22 +126,6 @@ template <int ACT, int HPT, bool SIMPLE, bool KA, int FORM>
 __global__ void k_step_window(KParams p, const uint8_t* action, int64_t act_stride, const TickArgs* tkp, int K,
                               int la_K, const double* rec, double* reward, int64_t rew_stride, uint64_t* onb,
                               uint32_t* wah, unsigned long long* next_slot, WinDrv dv);
-// One-launch single-window rollout (k_window_rs, mdr_kernels.hip): count blocks and thermal blocks
-// of one launch, the thermal blocks waiting for the count blocks' published penalties.  The count
-// shards and tickets are self-cleaning (the last count block zeroes them after reading); the
-// published penalties carry the launch's epoch, so no flag needs a reset between launches.
-struct FuseSync {
-  unsigned long long* shards;  // [kWindowMax][kCountShards][n_cap] (the first kWinShards shards used), then
-                               // the published penalties: 8 copies x 64 words (flag = epoch | K values)
-  unsigned* arrive;            // grid_last_block tickets of the count blocks (kTicketWords, zero between launches)
-  unsigned* err;               // flag-wait timeouts (never expected: a diagnostic, mdr_graph_info)
-  unsigned long long* prof;    // diagnostics: [grid][8] phase stamps (100 MHz clock), or null
-};
-constexpr int kRsCountTiles = 8;  // tiles per count wave of k_window_rs (the host sizes the count blocks)
-template <int ACT, int HPT, bool SIMPLE>
-__global__ void k_window_rs(KParams p, const uint8_t* action, int64_t act_stride, int K, double* reward,
-                            int64_t rew_stride, uint64_t* onb, uint32_t* wah, WinDrv dv, FuseSync fs, uint32_t nC,
-                            uint32_t ntile, uint32_t epoch);
 __global__ void k_win_reduce(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
 __global__ void k_win_records(KParams p, unsigned long long* slot, int nt, const TickArgs* tkp, double* p_out);
 template <int ACT, int HPT>
@@ -180,27 +158,15 @@ __global__ void k_greedy_apply(int64_t n, const int* perm, const int64_t* kpos, 
 constexpr int kGqBins = 16384;  // histogram-select greedy: key bins
 constexpr int kGqCap = 4096;    // candidate window capacity (LDS, 16 B per house)
 constexpr int kGqAfter = 256;   // window houses past the crossing bin (the gap walk's room)
-#ifndef MDR_GQ_STAGE
-#define MDR_GQ_STAGE 4096
-#endif
-#ifndef MDR_GQ_PARTS
-#define MDR_GQ_PARTS 256
-#endif
-constexpr int kGqStage = MDR_GQ_STAGE;  // houses per k_gq_compact block (MDR_GQ_STAGE: A/B builds)
-constexpr int kGqParts = MDR_GQ_PARTS;  // k_gq_keys / k_gq_bins grid (one block per CU; MDR_GQ_PARTS: A/B)
+constexpr int kGqStage = 4096;  // houses per k_gq_compact block
+constexpr int kGqParts = 256;  // k_gq_keys / k_gq_bins grid (one block per CU)
 constexpr int kGqThreads = 1024; // k_gq_keys / k_gq_bins / k_gq_compact block size
-#ifndef MDR_GQ_COPIES
-#define MDR_GQ_COPIES 8
-#endif
-constexpr int kGqCopies = MDR_GQ_COPIES;  // copies of the global superbin / bin histograms (blockIdx % kGqCopies)
+constexpr int kGqCopies = 8;  // copies of the global superbin / bin histograms (blockIdx % kGqCopies)
 constexpr int kGqUnroll = 4;    // houses per thread per pass of k_gq_keys / k_gq_bins
 constexpr int kGqSuper = 256;   // superbins (64 bins each) of the select's first pass (+ 1 for NaN keys)
 constexpr int kGqHistWords = kGqBins * 4 + kGqCopies * (kGqSuper + 1) * 4;  // g_hist: bin copies | superbin copies
 constexpr int kGqCells = 256;   // cells of the key -> bin map (gq_bin)
-#ifndef MDR_GQ_SEL_BLOCKS
-#define MDR_GQ_SEL_BLOCKS 256
-#endif
-constexpr int kGqSelBlocks = MDR_GQ_SEL_BLOCKS;  // k_gq_select grid, 1024 threads each (MDR_GQ_SEL_BLOCKS: A/B builds)
+constexpr int kGqSelBlocks = 256;  // k_gq_select grid, 1024 threads each
 constexpr int kGqMaxRanks = 64;   // sharded histogram select: ranks whose windows k_gq_select gathers
 struct GqSel;
 void gq_sel_init(void* sel128, uint32_t* map);  // host: the first call's key map (uniform over [-32, 32])

@@ -853,16 +853,14 @@ __device__ __forceinline__ void wave_lds_sync() {
 // last arrival is the answer; every counter is reset by the block that saw it complete.  (One
 // counter for a 2048-block grid serialises 2048 same-address atomics: ~25 us on MI355X.)
 // tickets: (kTicketGroups + 1) x 32 words, zero between launches.
-// (nblk: the blocks taking part, ids 0 .. nblk-1; default the whole grid)
-__device__ bool grid_last_block(unsigned* __restrict__ tickets, unsigned nblk = 0u) {
+__device__ bool grid_last_block(unsigned* __restrict__ tickets) {
   __shared__ unsigned s_last;
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned nb = nblk ? nblk : gridDim.x;
-    const unsigned G = nb < (unsigned)kTicketGroups ? nb : (unsigned)kTicketGroups;
+    const unsigned G = gridDim.x < (unsigned)kTicketGroups ? gridDim.x : (unsigned)kTicketGroups;
     const unsigned g = blockIdx.x % G;
-    const unsigned gsize = (nb - g + G - 1) / G;
+    const unsigned gsize = (gridDim.x - g + G - 1) / G;
     unsigned last = 0u;
     if (__hip_atomic_fetch_add(&tickets[32 * g], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gsize - 1u) {
       __hip_atomic_store(&tickets[32 * g], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -938,13 +936,10 @@ struct WinTile {
   bool v[HPT];
   uint64_t g0;        // first 64-house group of global ids the tile touches
   int sh;             // global id of the tile's first house mod 64 (0 when the shard offset is aligned)
-  // the launch's tile of this wave (one tile per wave)
-  __device__ __forceinline__ WinTile(const KParams& p)
-      : WinTile(p, blockIdx.x * (blockDim.x >> 6) + (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6))) {}
-  // tile tl (wave-uniform)
-  __device__ __forceinline__ WinTile(const KParams& p, uint32_t tl) {
+  __device__ __forceinline__ WinTile(const KParams& p) {
     const uint32_t n = (uint32_t)p.n;
-    tile = tl;
+    const uint32_t wv = (uint32_t)__builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    tile = blockIdx.x * (blockDim.x >> 6) + wv;
     i0 = tile * (64u * HPT) + (uint32_t)(threadIdx.x & 63);
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
@@ -985,13 +980,10 @@ __device__ __forceinline__ uint32_t writelane_u32(uint32_t old, uint32_t val, in
 // c and L - j dt fit a signed 32-bit compare), so saturating once at the end gives the
 // per-tick-saturated value; the lock bit comes from the last tick.  SH: the tile starts off a
 // 64-house group boundary (sharded runs), so a random action mask is spliced from two words.
-// FUSED (k_window_fused): the masks stay in registers (mlo_out / mhi_out: lane j = tick j's mask
-// words) instead of onb rows, and the counts ADD to the wave's rows (a wave runs several tiles).
-template <int ACT, int HPT, bool SH, bool FUSED = false>
+template <int ACT, int HPT, bool SH>
 __device__ __forceinline__ void win_run_t(const KParams& p, uint32_t* w, const uint64_t (*cm)[kWinCap],
                                           const WinTile<HPT>& t, const TickArgs* tkp, uint64_t tick0, int nt,
-                                          const uint8_t* action, int64_t act_stride, unsigned* cnt, uint64_t* onb,
-                                          uint32_t* mlo_out = nullptr, uint32_t* mhi_out = nullptr) {
+                                          const uint8_t* action, int64_t act_stride, unsigned* cnt, uint64_t* onb) {
   const int lane = threadIdx.x & 63;
   const int Li = p.L < 0 ? 0 : p.L, dt = p.dt;
   uint64_t on_m[HPT], can_m[HPT];
@@ -1014,16 +1006,14 @@ __device__ __forceinline__ void win_run_t(const KParams& p, uint32_t* w, const u
     const int jj = lane & 31;  // (tick ids: the staged drivers', or consecutive from tick0 before staging)
     const uint64_t tick = tkp ? tkp[jj < nt ? jj : 0].tick : tick0 + (uint64_t)(jj < nt ? jj : 0);
     philox_words(p.seed, t.g0 + (uint64_t)(lane >> 5), tick, wa_lo, wa_hi);
-    if constexpr (G > 2) philox_words(p.seed, t.g0 + 2u + (uint64_t)(lane >> 5), tick, wb_lo, wb_hi);
+    if constexpr (G > 2) philox_words(p.seed, t.g0 + 2u, tick, wb_lo, wb_hi);
   }
-  static_assert(G <= 4, "at most four 64-house groups per tile");
   for (int j = 0; j < nt; ++j) {
     uint64_t W[G];
     if (ACT == MDR_ACT_RANDOM) {
       W[0] = readlane_u64(wa_lo, wa_hi, j);
       if constexpr (G > 1) W[1] = readlane_u64(wa_lo, wa_hi, j + 32);
       if constexpr (G > 2) W[2] = readlane_u64(wb_lo, wb_hi, j);
-      if constexpr (G > 3) W[3] = readlane_u64(wb_lo, wb_hi, j + 32);
     }
     const uint8_t* arow = ACT == MDR_ACT_BUFFER ? action + (int64_t)j * act_stride : nullptr;
     const int32_t thr = Li - j * dt;        // s1_j >= L  <=>  c >= L - j dt
@@ -1052,44 +1042,28 @@ __device__ __forceinline__ void win_run_t(const KParams& p, uint32_t* w, const u
     const uint32_t s = sso < kSsoMask ? sso : kSsoMask;
     w[h] = s | (__builtin_amdgcn_inverse_ballot_w64(lock_m) ? kLockBit : 0u) | (on ? kOnBit : 0u);
   }
-  if constexpr (FUSED) {
-#pragma unroll
-    for (int h = 0; h < HPT; ++h) {
-      mlo_out[h] = mlo[h];
-      mhi_out[h] = mhi[h];
-    }
-  }
   if (lane < nt) {
     unsigned k[kWinCap] = {};
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
       const uint64_t m = ((uint64_t)mhi[h] << 32) | mlo[h];
-      if constexpr (!FUSED) onb[lane * HPT + h] = m;
+      onb[lane * HPT + h] = m;
 #pragma unroll
       for (int cc = 0; cc < kWinCap; ++cc) k[cc] += (unsigned)__popcll(m & cm[h][cc]);
     }
 #pragma unroll
-    for (int cc = 0; cc < kWinCap; ++cc) {
-      if constexpr (FUSED) cnt[lane * kWinCap + cc] += k[cc];  // (lane-exclusive rows)
-      else cnt[lane * kWinCap + cc] = k[cc];
-    }
+    for (int cc = 0; cc < kWinCap; ++cc) cnt[lane * kWinCap + cc] = k[cc];
   }
 }
 
-template <int ACT, int HPT, bool FUSED = false>
+template <int ACT, int HPT>
 __device__ __forceinline__ void win_run(const KParams& p, uint32_t* w, const uint64_t (*cm)[kWinCap],
                                         const WinTile<HPT>& t, const TickArgs* tkp, uint64_t tick0, int nt,
-                                        const uint8_t* action, int64_t act_stride, unsigned* cnt, uint64_t* onb,
-                                        uint32_t* mlo_out = nullptr, uint32_t* mhi_out = nullptr) {
-  // (a tile off a 64-house group boundary only occurs on sharded contexts; the fused kernel's
-  // 256-house tiles (HPT 4) only run on unsharded ones, mdr_capi.hip fused_plan)
-  if constexpr (HPT <= 2) {
-    if (ACT == MDR_ACT_RANDOM && t.sh != 0) {
-      win_run_t<ACT, HPT, true, FUSED>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb, mlo_out, mhi_out);
-      return;
-    }
-  }
-  win_run_t<ACT, HPT, false, FUSED>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb, mlo_out, mhi_out);
+                                        const uint8_t* action, int64_t act_stride, unsigned* cnt, uint64_t* onb) {
+  if (ACT == MDR_ACT_RANDOM && t.sh != 0)
+    win_run_t<ACT, HPT, true>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb);
+  else
+    win_run_t<ACT, HPT, false>(p, w, cm, t, tkp, tick0, nt, action, act_stride, cnt, onb);
 }
 
 // sum the block's per-wave rows cnt[R][kWinMax][kWinCap] and add them to this block's slab shard
@@ -1116,16 +1090,6 @@ __device__ __forceinline__ void win_classes(const WinTile<HPT>& t, const int* cl
     for (int c = 0; c < kWinCap; ++c) cm[h][c] = __ballot(t.v[h] && cls[h] == c);
 }
 
-#ifdef MDR_COUNT_TIMING
-// measurement build only (tools/count_timing.py, a variant library): per block of k_count_window
-// the constant 100 MHz clock at entry, after the state loads were consumed, after the shard flush,
-// and after the ticket (the last block: after its reduce)
-__device__ unsigned long long g_cw_ts[16384 * 4];
-#define MDR_CW_TS(k) \
-  do { if (threadIdx.x == 0 && blockIdx.x < 16384) g_cw_ts[blockIdx.x * 4 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-#else
-#define MDR_CW_TS(k) do {} while (0)
-#endif
 
 
 // First window of a rollout: ON counts, ON lane masks and end-of-window FSM words of ticks
@@ -1138,7 +1102,6 @@ __global__ void __launch_bounds__(64 * kCountWaves) k_count_window(KParams p, co
                                                       uint64_t* __restrict__ onb, uint32_t* __restrict__ wah,
                                                       const uint32_t* __restrict__ w_in, unsigned* __restrict__ ticket) {
   __shared__ unsigned s_cnt[kCountWaves][kWinMax * kWinCap];
-  MDR_CW_TS(0);
   const int wv = threadIdx.x >> 6;
   const WinTile<HPT> t(p);
   uint32_t w[HPT];
@@ -1150,7 +1113,6 @@ __global__ void __launch_bounds__(64 * kCountWaves) k_count_window(KParams p, co
   }
   uint64_t cm[HPT][kWinCap];
   win_classes<HPT>(t, cls, cm);
-  MDR_CW_TS(1);
   win_run<ACT, HPT>(p, w, cm, t, tkp, tick0, nt, action, act_stride, s_cnt[wv],
                     onb + (size_t)t.tile * HPT * kWinMax);
 #pragma unroll
@@ -1158,9 +1120,7 @@ __global__ void __launch_bounds__(64 * kCountWaves) k_count_window(KParams p, co
     if (t.v[h]) wah[t.i0 + 64u * h] = w[h];
   __syncthreads();
   win_flush<kCountWaves>(p, nt, s_cnt, slot);
-  MDR_CW_TS(2);
   if (ticket) win_reduce_last<64 * kCountWaves>(p, slot, nt, ticket);  // (ticket: the P-only reduce, see win_reduce_last)
-  MDR_CW_TS(3);
 }
 
 // Per-window affine transition of one house (FORM = MDR_THERMAL_AFFINE).  The reference's update
@@ -1204,42 +1164,6 @@ __device__ __forceinline__ AffWin aff_window(double ua, double ca, double cm, do
   w.qt = w.tq * qc;
   w.qm = w.mq * qc;
   return w;
-}
-
-// one AFFINE tick of one house: the Kelvin state (tk, tmk) advanced by the window's transition
-// (k_step_window and k_window_fused share it, so both forms give the same bits)
-__device__ __forceinline__ void aff_tick(const AffWin& a, bool on, double od_k, double solar, double& tk, double& tmk) {
-  const double ut = __builtin_fma(a.to, od_k, __builtin_fma(a.tq, solar, on ? a.qt : 0.0));
-  const double um = __builtin_fma(a.mo, od_k, __builtin_fma(a.mq, solar, on ? a.qm : 0.0));
-  const double tkn = __builtin_fma(a.tt, tk, __builtin_fma(a.tm, tmk, ut));
-  const double tmkn = __builtin_fma(a.mt, tk, __builtin_fma(a.mm, tmk, um));
-  tk = tkn;
-  tmk = tmkn;
-}
-
-// the individual_L2 reward of a house at the new Celsius temperature Tn (Kelvin tkn and threshold hk
-// on the affine path), nsig = the tick's NEGATED signal penalty (rewards_calculator.py:29-203)
-template <bool SIMPLE, bool AFF, bool F>
-__device__ __forceinline__ double win_reward(const KParams& p, double Tn, double tkn, double hk, double hi_tg,
-                                             double lo_tg, double nalpha, double nsig) {
-  if (SIMPLE) {  // deadband 0, norm_temp 1 (the defaults): no branches, no division
-    // on the fast path Tn is finite, so the reference's two comparisons reduce to x * x (x = 0
-    // gives +0 either way); off it a NaN gives 0.  -(a * pen + s) == (-a) * pen + (-s) bit for
-    // bit: negation is exact and rounding is symmetric, and with a, s >= +0 (mdr_capi checks
-    // the signs for SIMPLE) the only zero sum is +0 + +0, whose negation is -0 either way
-    if (AFF && F) {
-      const double x = tkn - hk;
-      return __builtin_fma(nalpha, x * x, nsig);
-    }
-    const double x = Tn - hi_tg;
-    const double pen = F ? x * x : deadband_l2_0(hi_tg, Tn);
-    return nalpha * pen + nsig;
-  }
-  double pen = 0.0;
-  if (hi_tg < Tn) { const double x = Tn - hi_tg; pen = x * x; }
-  else if (lo_tg > Tn) { const double x = lo_tg - Tn; pen = x * x; }
-  const double tpen = p.alpha_temp * pen;
-  return -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + -nsig);
 }
 
 // One window of K ticks.  slot: this window's slot (red counts are folded into its tick records);
@@ -1360,14 +1284,39 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
     // the reward from the new Celsius temperature Tn (Kelvin tkn on the affine path)
     auto reward_of = [&](int h, double Tn, double tkn, auto fast_c) {
       constexpr bool F = decltype(fast_c)::value;
-      return win_reward<SIMPLE, AFF, F>(p, Tn, tkn, AFF ? hk[h] : 0.0, hi_tg[h], lo_tg[h], nalpha, nsig);
+      if (SIMPLE) {  // deadband 0, norm_temp 1 (the defaults): no branches, no division
+        // on the fast path Tn is finite, so the reference's two comparisons reduce to x * x (x = 0
+        // gives +0 either way); off it a NaN gives 0.  -(a * pen + s) == (-a) * pen + (-s) bit for
+        // bit: negation is exact and rounding is symmetric, and with a, s >= +0 (mdr_capi checks
+        // the signs for SIMPLE) the only zero sum is +0 + +0, whose negation is -0 either way
+        if (AFF && F) {
+          const double x = tkn - hk[h];
+          return __builtin_fma(nalpha, x * x, nsig);
+        }
+        const double x = Tn - hi_tg[h];
+        const double pen = F ? x * x : deadband_l2_0(hi_tg[h], Tn);
+        return nalpha * pen + nsig;
+      }
+      double pen = 0.0;
+      if (hi_tg[h] < Tn) { const double x = Tn - hi_tg[h]; pen = x * x; }
+      else if (lo_tg[h] > Tn) { const double x = lo_tg[h] - Tn; pen = x * x; }
+      const double tpen = p.alpha_temp * pen;
+      return -((p.norm_temp == 1.0 ? tpen : tpen / p.norm_temp) + -nsig);
     };
     if constexpr (AFF) {
       auto houses = [&](auto fast_c) {
+        constexpr bool F = decltype(fast_c)::value;
 #pragma unroll
         for (int h = 0; h < HPT; ++h) {
-          aff_tick(aw[h], __builtin_amdgcn_inverse_ballot_w64(on_m[h]), od_k, solar, tk[h], tmk[h]);
-          const double r = reward_of(h, tk[h] - 273.0, tk[h], fast_c);  // (Celsius unused on the SIMPLE fast path)
+          const AffWin& a = aw[h];
+          const bool on = __builtin_amdgcn_inverse_ballot_w64(on_m[h]);
+          const double ut = __builtin_fma(a.to, od_k, __builtin_fma(a.tq, solar, on ? a.qt : 0.0));
+          const double um = __builtin_fma(a.mo, od_k, __builtin_fma(a.mq, solar, on ? a.qm : 0.0));
+          const double tkn = __builtin_fma(a.tt, tk[h], __builtin_fma(a.tm, tmk[h], ut));
+          const double tmkn = __builtin_fma(a.mt, tk[h], __builtin_fma(a.mm, tmk[h], um));
+          tk[h] = tkn;
+          tmk[h] = tmkn;
+          const double r = reward_of(h, tkn - 273.0, tkn, fast_c);  // (Celsius unused on the SIMPLE fast path)
           if (t.v[h]) __builtin_nontemporal_store(r, reinterpret_cast<double*>(rrow + (rb + 512u * h)));
         }
       };
@@ -1429,267 +1378,6 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
   }
 }
 
-// ------------------------------------------------------------------ one-launch single window
-// k_window_rs: the count kernel and the KA step kernel of a single-window rollout (the driver's
-// 20-tick bench call) as ONE launch with two block roles.
-//   count role (blocks 0 .. nC-1, dispatched first, never waiting on anyone): the FSM of the window
-//      for every tile (tile c, c + 4 nC, ... per wave; win_run), the ON lane masks and end-of-window
-//      FSM words written through (sc1) to the onb / wah rows, the class counts added to 16 shards;
-//      the last count block (grid ticket over the count blocks) sums the shards, zeroes them, forms
-//      each tick's P and negated signal penalty (the reduce's expressions) and publishes them to
-//      kFuseCopies copies, then the launch's epoch into each copy's flag (after vmcnt(0));
-//   thermal role (blocks nC ..): one 128-house tile per wave, exactly k_step_window<..., KA, AFFINE>
-//      (the same helpers), except that the penalties, ON masks and end words come from the count
-//      role: the block loads its state and parameters and forms the window's coefficients, THEN
-//      waits for the flag (thread 0 polls its copy with sc1 loads + s_sleep), so the first round of
-//      thermal blocks overlaps its state loads and coefficient math with the count, and the later
-//      rounds, scheduled by the hardware as usual, find the flag set.
-// Deadlock-free by dispatch order: the count blocks have the lowest ids, are dispatched first and
-// wait for nothing; a thermal block only waits for them (2 s timeout: a diagnostic, never expected).
-// What it removes from a 20-tick call: the count -> step kernel boundary, the count kernel's late
-// block starts, and the first round's state loads and coefficient math from the critical path.
-constexpr uint64_t kFuseTimeout = 200000000ull;  // s_memrealtime ticks (100 MHz): 2 s, then give up
-constexpr int kFuseCopies = 8;
-constexpr int kFuseCopyWords = 64;  // per copy: [0] flag (epoch), [32 ..] the K negated penalties (u64)
-// phase stamps (fs.prof, diagnostics): per block the 100 MHz clock at entry, after its count flush
-// (count blocks) / its coefficients (thermal blocks), after the flag, at the end (thread 0)
-#define MDR_FUSE_TS(k) \
-  do { if (fs.prof && threadIdx.x == 0) fs.prof[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-
-// the count role's last block: shard sums -> P, penalties published (see above)
-__device__ void rs_publish(const KParams& p, const FuseSync& fs, int K, uint32_t epoch, const WinDrv& dv,
-                           uint32_t nC) {
-  __shared__ unsigned long long s_red[kWinMax * kWinCap];
-  const int ncap = p.n_cap, E = K * ncap;
-  unsigned long long* pub = fs.shards + (size_t)kWinMax * kCountShards * ncap;  // kFuseCopies x kFuseCopyWords
-  if (!grid_last_block(fs.arrive, nC)) return;  // (block-uniform; the tickets are reset inside)
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering: the loads below are sc1)
-  for (int e = threadIdx.x; e < E; e += blockDim.x) {
-    const int j = e / ncap, c = e - j * ncap;
-    unsigned long long v[kWinShards];
-#pragma unroll
-    for (int q = 0; q < kWinShards; ++q)
-      v[q] = __hip_atomic_load(&fs.shards[((size_t)j * kCountShards + q) * ncap + c], __ATOMIC_RELAXED,
-                               __HIP_MEMORY_SCOPE_AGENT);
-    unsigned long long x = 0ull;
-#pragma unroll
-    for (int q = 0; q < kWinShards; ++q) {
-      x += v[q];
-      __hip_atomic_store(&fs.shards[((size_t)j * kCountShards + q) * ncap + c], 0ull, __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-    s_red[e] = x;
-  }
-  __syncthreads();
-  if ((int)threadIdx.x < K) {
-    const int j = threadIdx.x;
-    double p_on[kWinCap];
-#pragma unroll
-    for (int c = 0; c < kWinCap; ++c) p_on[c] = p.p_on[c < ncap ? c : 0];
-    const double P = win_power(p, s_red + j * ncap, p_on);
-    const double ns = win_nsig(p, P, dv.s_prev[j]);
-    if (dv.p_out && j == K - 1) *dv.p_out = P;
-#pragma unroll
-    for (int x = 0; x < kFuseCopies; ++x)
-      __hip_atomic_store(&pub[x * kFuseCopyWords + 32 + j], (unsigned long long)__double_as_longlong(ns),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if ((int)threadIdx.x < kFuseCopies)
-    __hip_atomic_store(&pub[threadIdx.x * kFuseCopyWords], (unsigned long long)epoch, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int ACT, int HPT, bool SIMPLE>
-__global__ void __launch_bounds__(256) k_window_rs(KParams p, const uint8_t* __restrict__ action,
-                                                   int64_t act_stride, int K, double* __restrict__ reward,
-                                                   int64_t rew_stride, uint64_t* __restrict__ onb,
-                                                   uint32_t* __restrict__ wah, WinDrv dv, FuseSync fs, uint32_t nC,
-                                                   uint32_t ntile, uint32_t epoch) {
-  MDR_FUSE_TS(0);
-  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  if (blockIdx.x < nC) {
-    // ---- count role
-    __shared__ unsigned s_cnt[4][kWinMax * kWinCap];
-    if (lane < kWinMax) {
-#pragma unroll
-      for (int cc = 0; cc < kWinCap; ++cc) s_cnt[wv][lane * kWinCap + cc] = 0u;
-    }
-    // the wave's tiles c, c + 4 nC, ... (at most kRsCountTiles, mdr_capi.hip launch_fused): every
-    // tile's FSM words and classes are loaded first (one memory round trip under the thermal
-    // blocks' load traffic, not one per tile), then the FSM runs tile by tile
-    const uint32_t ncw = nC * 4u;
-    const uint32_t c0 = blockIdx.x * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(wv);
-    uint32_t wi[kRsCountTiles][HPT];
-    uint8_t ci[kRsCountTiles][HPT];
-#pragma unroll
-    for (int k = 0; k < kRsCountTiles; ++k) {
-      const uint32_t tl = c0 + (uint32_t)k * ncw;
-#pragma unroll
-      for (int h = 0; h < HPT; ++h) {
-        wi[k][h] = 0u;
-        ci[k][h] = 0;
-      }
-      if (tl < ntile) {
-        const WinTile<HPT> t(p, tl);
-#pragma unroll
-        for (int h = 0; h < HPT; ++h) {
-          wi[k][h] = p.hvac[t.idx[h]];
-          ci[k][h] = p.cap_idx[t.idx[h]];
-        }
-      }
-    }
-#pragma unroll
-    for (int k = 0; k < kRsCountTiles; ++k) {
-      const uint32_t tl = c0 + (uint32_t)k * ncw;
-      if (tl >= ntile) break;  // (wave-uniform)
-      const WinTile<HPT> t(p, tl);
-      uint32_t w[HPT], mlo[HPT], mhi[HPT];
-      int cls[HPT];
-#pragma unroll
-      for (int h = 0; h < HPT; ++h) {
-        w[h] = wi[k][h];
-        cls[h] = ci[k][h];
-      }
-      uint64_t cm[HPT][kWinCap];
-      win_classes<HPT>(t, cls, cm);
-      win_run<ACT, HPT, true>(p, w, cm, t, nullptr, dv.tick0, K, action, act_stride, s_cnt[wv], nullptr, mlo, mhi);
-      uint64_t* rows = onb + (size_t)tl * HPT * kWinMax;
-      if (lane < K) {
-#pragma unroll
-        for (int h = 0; h < HPT; ++h)
-          __hip_atomic_store(&rows[lane * HPT + h], ((uint64_t)mhi[h] << 32) | mlo[h], __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_AGENT);
-      }
-#pragma unroll
-      for (int h = 0; h < HPT; ++h)
-        if (t.v[h]) __hip_atomic_store(&wah[t.i0 + 64u * h], w[h], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    win_flush(p, K, s_cnt, fs.shards);
-    MDR_FUSE_TS(1);
-    rs_publish(p, fs, K, epoch, dv, nC);  // (drains every store above before the block's ticket)
-    MDR_FUSE_TS(2);
-    return;
-  }
-
-  // ---- thermal role: k_step_window<ACT, HPT, SIMPLE, KA, AFFINE> on tile (block - nC) * 4 + wave
-  const WinTile<HPT> t(p, (blockIdx.x - nC) * 4u + (uint32_t)__builtin_amdgcn_readfirstlane(wv));
-  double T[HPT], Tm[HPT], ua[HPT], hm[HPT], tg[HPT], ca[HPT], cm[HPT];
-  int cls[HPT];
-  const bool params_ok = !*p.params_bad && p.fast_tick_ok;
-#pragma unroll
-  for (int h = 0; h < HPT; ++h) {
-    const uint32_t i = t.idx[h];
-    T[h] = p.t_air[i]; Tm[h] = p.t_mass[i]; ua[h] = p.ua[i]; hm[h] = p.hm[i]; tg[h] = p.target[i];
-    ca[h] = p.ca[i]; cm[h] = p.cm[i];
-    cls[h] = p.cap_idx[i];
-  }
-  double q_on[kWinCap];
-#pragma unroll
-  for (int c = 0; c < kWinCap; ++c) q_on[c] = p.q_on[c < p.n_cap ? c : 0];
-  AffWin aw[HPT];
-  double tk[HPT], tmk[HPT], hk[HPT], hi_tg[HPT], lo_tg[HPT];
-  bool win_finite = true;
-#pragma unroll
-  for (int h = 0; h < HPT; ++h) {
-    double qc = q_on[0];
-#pragma unroll
-    for (int c = 1; c < kWinCap; ++c) qc = cls[h] == c ? q_on[c] : qc;
-    hi_tg[h] = tg[h] + p.deadband / 2.0;
-    lo_tg[h] = tg[h] - p.deadband / 2.0;
-    aw[h] = aff_window(ua[h], ca[h], cm[h], hm[h], (double)p.dt, qc, params_ok);
-    tk[h] = T[h] + 273.0;
-    tmk[h] = Tm[h] + 273.0;
-    hk[h] = hi_tg[h] + 273.0;
-    const AffWin& a = aw[h];
-    const double z = a.tt + a.tm + a.tq + a.to + a.qt + a.mt + a.mm + a.mq + a.mo + a.qm + tk[h] + tmk[h] + hk[h];
-    win_finite = win_finite && (z - z == 0.0);
-  }
-  win_finite = __all(win_finite);
-  MDR_FUSE_TS(1);
-  // the count role's results
-  const unsigned long long* cp =
-      fs.shards + (size_t)kWinMax * kCountShards * p.n_cap + (blockIdx.x % kFuseCopies) * kFuseCopyWords;
-  if (threadIdx.x == 0) {
-    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(&cp[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != (unsigned long long)epoch) {
-      __builtin_amdgcn_s_sleep(1);
-      if (__builtin_amdgcn_s_memrealtime() - t0 > kFuseTimeout) {
-        __hip_atomic_fetch_add(fs.err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        break;
-      }
-    }
-  }
-  __syncthreads();
-  MDR_FUSE_TS(2);
-  uint32_t ns_lo = 0, ns_hi = 0;
-  {
-    const unsigned long long nb = __hip_atomic_load(&cp[32 + (lane < K ? lane : 0)], __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-    ns_lo = (uint32_t)nb;
-    ns_hi = (uint32_t)(nb >> 32);
-  }
-  uint32_t w_end[HPT];
-#pragma unroll
-  for (int h = 0; h < HPT; ++h)
-    w_end[h] = __hip_atomic_load(&wah[t.idx[h]], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  auto lane_nsig = [&](int j) { return __longlong_as_double((long long)readlane_u64(ns_lo, ns_hi, j)); };
-  const uint64_t* onb_w = onb + (size_t)t.tile * HPT * kWinMax;  // this wave's rows [kWinMax][HPT]
-  uint64_t r_on[HPT];
-#pragma unroll
-  for (int h = 0; h < HPT; ++h) r_on[h] = onb_w[h];
-  const uint32_t rb = t.i0 * 8u;  // byte offset of the lane's house in a reward row (n < 2^29)
-  const double nalpha = -p.alpha_temp;
-  for (int j = 0; j < K; ++j) {
-    const double od_k = dv.od_k[j], solar = dv.solar[j], nsig = lane_nsig(j);
-    const bool tick_ok = ((dv.ok >> j) & 1u) != 0u;
-    uint64_t on_m[HPT];
-#pragma unroll
-    for (int h = 0; h < HPT; ++h) on_m[h] = r_on[h];
-    const int jn = j + 1 < K ? j + 1 : j;
-#pragma unroll
-    for (int h = 0; h < HPT; ++h) r_on[h] = onb_w[jn * HPT + h];
-    char* rrow = reinterpret_cast<char*>(reward + (int64_t)j * rew_stride);
-    auto houses = [&](auto fast_c) {
-      constexpr bool F = decltype(fast_c)::value;
-#pragma unroll
-      for (int h = 0; h < HPT; ++h) {
-        aff_tick(aw[h], __builtin_amdgcn_inverse_ballot_w64(on_m[h]), od_k, solar, tk[h], tmk[h]);
-        const double r = win_reward<SIMPLE, true, F>(p, tk[h] - 273.0, tk[h], hk[h], hi_tg[h], lo_tg[h], nalpha, nsig);
-        if (t.v[h]) __builtin_nontemporal_store(r, reinterpret_cast<double*>(rrow + (rb + 512u * h)));
-      }
-    };
-    if (win_finite && tick_ok) houses(std::true_type());
-    else houses(std::false_type());
-  }
-#pragma unroll
-  for (int h = 0; h < HPT; ++h)
-    if (t.v[h]) {
-      const uint32_t i = t.i0 + 64u * h;
-      p.t_air[i] = tk[h] - 273.0; p.t_mass[i] = tmk[h] - 273.0; p.hvac[i] = w_end[h];
-    }
-  MDR_FUSE_TS(3);
-}
-
-#define MDR_INST_RS(A, SI)                                                                                      \
-  template __global__ void k_window_rs<A, kWinHpt, SI>(KParams, const uint8_t*, int64_t, int, double*, int64_t,    \
-                                                       uint64_t*, uint32_t*, WinDrv, FuseSync, uint32_t, uint32_t, \
-                                                       uint32_t);
-MDR_INST_RS(MDR_ACT_RANDOM, true)
-MDR_INST_RS(MDR_ACT_RANDOM, false)
-MDR_INST_RS(MDR_ACT_ALWAYS_ON, true)
-MDR_INST_RS(MDR_ACT_ALWAYS_ON, false)
-MDR_INST_RS(MDR_ACT_BUFFER, true)
-MDR_INST_RS(MDR_ACT_BUFFER, false)
-
-#ifdef MDR_COUNT_TIMING
-extern "C" int mdr_count_timing(unsigned long long* out, int n) {
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cw_ts), (size_t)n * 4 * sizeof(unsigned long long), 0,
-                             hipMemcpyDeviceToHost) == hipSuccess ? 0 : -2;
-}
-#endif
 
 #define MDR_INST_WIN_F(A, SI, KA_, FO)                                                                         \
   template __global__ void k_step_window<A, kWinHpt, SI, KA_, FO>(KParams, const uint8_t*, int64_t, const TickArgs*, \

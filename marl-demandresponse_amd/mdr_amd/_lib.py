@@ -23,7 +23,7 @@ PEN_MODES = {"individual_L2": 0, "common_L2": 1, "common_max_error": 2, "mixture
 ERRORS = {-1: "MDR_EARG", -2: "MDR_EHIP", -3: "MDR_ERCCL", -4: "MDR_ENOMEM", -5: "MDR_ESTATE"}
 # mdr_set_option (mdr.h): alternative launch forms of the same computation
 OPTIONS = {"step_tpw": 1, "fastdiv": 2, "window_pipeline": 3, "sharded_overlap": 4, "greedy_sort": 5, "halo_overlap": 9, "actor_generic": 10,
-           "force_halo": 6, "window_thermal": 7, "window_fused": 11}
+           "force_halo": 6, "window_thermal": 7}
 THERMAL_EXACT, THERMAL_AFFINE = 0, 1
 
 
@@ -121,7 +121,6 @@ SIGNATURES = {
     "mdr_abi_sizes": (I, [P(I64), I]),
     "mdr_last_error": (C.c_char_p, []),
     "mdr_graph_info": (I, [VP, P(I64), I]),
-    "mdr_fused_stamps": (I, [VP, VP, I64]),
     "mdr_create": (I, [P(VP), P(mdr_config)]),
     "mdr_destroy": (I, [VP]),
     "mdr_bind": (I, [VP, P(mdr_soa)]),

@@ -146,16 +146,13 @@ class HipShard:
         L.check(self.lib.mdr_power_counts(self.ctx, L.ptr(action), mode, tick, self.stream()),
                 "mdr_power_counts")
 
-    def graph_info(self, sync: bool = False):
-        """{rollout_graphs, actor_graphs, rollout_launches, actor_launches, fused_launches}: cached
-        graphs, hipGraphLaunch calls and k_window_fused launches (mdr_graph_info); ``sync`` also
-        reads k_window_fused's grid-wait timeout count (fused_timeouts; synchronises the device)."""
-        k = 6 if sync else 5
-        out = (C.c_int64 * k)()
-        rc = self.lib.mdr_graph_info(self.ctx, out, k)
-        L.check(0 if rc == k else rc, "mdr_graph_info")
-        return dict(zip(("rollout_graphs", "actor_graphs", "rollout_launches", "actor_launches", "fused_launches",
-                         "fused_timeouts"), list(out)))
+    def graph_info(self):
+        """{rollout_graphs, actor_graphs, rollout_launches, actor_launches}: cached graphs and
+        hipGraphLaunch calls (mdr_graph_info)."""
+        out = (C.c_int64 * 4)()
+        rc = self.lib.mdr_graph_info(self.ctx, out, 4)
+        L.check(0 if rc == 4 else rc, "mdr_graph_info")
+        return dict(zip(("rollout_graphs", "actor_graphs", "rollout_launches", "actor_launches"), list(out)))
 
     def counts_buffer(self):
         p = C.c_void_p()

@@ -123,52 +123,6 @@ def test_affine_form_long_run(torch_gpu, n):
     print(f"n={n}: after 2000 ticks max rel |T_affine - T_exact| = {rel:.3g}, max |dr| = {worst:.3g}")
 
 
-@pytest.mark.parametrize("n,ticks", [(1, 1), (2, 20), (129, 7), (4099, 32), (131072, 20), (1 << 20, 20),
-                                     (1572864, 20), (1 << 22, 32)])
-@pytest.mark.parametrize("mode", ["random", "always_on", "buffer"])
-@pytest.mark.parametrize("deadband", [0.0, 0.5])
-def test_window_fused_equals_pair(torch_gpu, n, ticks, mode, deadband):
-    """A single-window rollout as ONE launch (k_window_rs: count blocks, then thermal blocks that
-    wait for the published penalties) == the count kernel + KA step kernel pair
-    (MDR_OPT_WINDOW_FUSED 0), bit for bit: rewards, state, P, over three consecutive calls (the
-    count shards and tickets clean themselves up).  1M houses is the driver's 20-step bench call;
-    4M thermal blocks run in several rounds; deadband 0.5 takes the non-SIMPLE reward."""
-    torch = torch_gpu
-    extra = {"reward_prop.penalty_props.deadband": deadband} if deadband else None
-    e1, e2 = _pair(n, extra=extra)
-    e2.shard.set_option("window_fused", 0)
-    acts = None
-    if mode == "buffer":
-        g = torch.Generator(device="cuda").manual_seed(n)
-        acts = (torch.rand((ticks, n), device="cuda", generator=g) < 0.5).to(torch.uint8)
-    f0 = e1.shard.graph_info()["fused_launches"]
-    for rep in range(3):
-        r1 = e1.rollout(ticks, actions=acts, action_mode=mode)
-        r2 = e2.rollout(ticks, actions=acts, action_mode=mode)
-        assert torch.equal(r1, r2), rep
-        _same_state(torch, e1, e2)
-    gi = e1.shard.graph_info(sync=True)
-    assert gi["fused_launches"] == f0 + 3, gi
-    assert gi["fused_timeouts"] == 0, gi
-    assert e2.shard.graph_info()["fused_launches"] == 0
-
-
-def test_window_fused_not_taken(torch_gpu):
-    """Calls the fused launch does not take run the pair: more ticks than one window, the EXACT
-    form, a graph-captured rollout."""
-    from mdr_amd import _lib as L
-
-    e1, _ = _pair(4099)
-    e1.rollout(33, action_mode="random")
-    e1.rollout(20, action_mode="random", use_graph=True)
-    e1.shard.set_option("window_thermal", L.THERMAL_EXACT)
-    e1.rollout(20, action_mode="random")
-    assert e1.shard.graph_info()["fused_launches"] == 0
-    e1.shard.set_option("window_thermal", L.THERMAL_AFFINE)
-    e1.rollout(20, action_mode="random")
-    assert e1.shard.graph_info()["fused_launches"] == 1
-
-
 C2_TICKS = 10000  # SURVEY §8(d) C2: 64k houses x T = 10,000
 
 
