@@ -648,9 +648,13 @@ def main():
         if key is not None:
             c = cpu["configs"][key]
             cpu = dict(cpu, value=c["value"], cores=1,
+                       basis=("single core: the line's own config on 1 thread (the step line's value is C2 on 16 "
+                              "processes; its 1-core C2 figure is configs.C2_65536_random_1core)"),
                        sample=(f"{key}: oracle/env_np.py (NumPy fp64, 1 thread)" +
                                (" + torch fp32 actor" if args.workload == "actor" else "") +
                                f", {c['ticks']} ticks; host {cpu['cpu_model']}"))
+        else:
+            cpu = dict(cpu, basis="16 processes x 1 thread of C2 (the 1-core figure: configs.C2_65536_random_1core)")
         out["cpu_baseline"] = cpu
     if rank == 0:
         print(json.dumps(out), flush=True)
