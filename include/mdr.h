@@ -161,6 +161,10 @@ int mdr_params_changed(mdr_ctx* ctx);
  *   MDR_OPT_HALO_OVERLAP    mdr_actor_rollout_sharded: 1 (default) = each tick's ring halo is packed and
  *                           exchanged on the communicator's side stream while the interior tiles'
  *                           k_actor runs, then the first and last tile; 0 = halo, then one k_actor
+ *   MDR_OPT_HALO_IN_COUNTS  mdr_actor_rollout_sharded: 1 (default) = ONE collective per tick: the edge
+ *                           houses' post-step message rows (the next tick's ring halo) are computed
+ *                           before the step and summed into the count allreduce; 0 = a ring-halo
+ *                           send/recv per tick plus the count allreduce (MDR_OPT_HALO_OVERLAP applies)
  *   MDR_OPT_ACTOR_GENERIC   1 = k_actor runs its generic form for the reference's default obs layout too
  *                           (0, default: that layout runs the form specialised for it, mdr_actor.hip DEF)
  *   MDR_OPT_WINDOW_THERMAL  k_step_window's per-tick thermal update: MDR_THERMAL_AFFINE (default)
@@ -170,7 +174,7 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           operation order every tick (bit-identical to the one-tick kernels) */
 enum { MDR_OPT_STEP_TPW = 1, MDR_OPT_FASTDIV = 2, MDR_OPT_WINDOW_PIPELINE = 3, MDR_OPT_SHARDED_OVERLAP = 4,
        MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7,
-       MDR_OPT_HALO_OVERLAP = 9, MDR_OPT_ACTOR_GENERIC = 10 };
+       MDR_OPT_HALO_OVERLAP = 9, MDR_OPT_ACTOR_GENERIC = 10, MDR_OPT_HALO_IN_COUNTS = 12 };
 /* (8 was MDR_OPT_ACTOR_PINGPONG, a k_actor schedule measured slower and retired in r04: rejected) */
 enum { MDR_THERMAL_EXACT = 0, MDR_THERMAL_AFFINE = 1 };
 int mdr_set_option(mdr_ctx* ctx, int option, int64_t value);

@@ -352,7 +352,8 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     if (kind == 2) {
       const int64_t j = (int64_t)b0 - lo + s;
       const int hh = j < 0 ? (int)(j + lo) : (int)(lo + (j - (int64_t)n));
-      for (int m = 0; m < M; ++m) row[m] = o.halo_msg[hh * M + m];
+      const float* src = o.halo_next && hh >= lo ? o.halo_next + (size_t)(hh - lo) * M : o.halo_msg + (size_t)hh * M;
+      for (int m = 0; m < M; ++m) row[m] = src[m];
     } else if (kind == 1) {
       const int t = s - lo;
       if (ring) {

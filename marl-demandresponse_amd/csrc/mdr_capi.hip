@@ -91,6 +91,9 @@ struct mdr_ctx {
   bool force_halo = false;               // MDR_OPT_FORCE_HALO: sharded actor halo exchange at world 1
   bool actor_generic = false;            // MDR_OPT_ACTOR_GENERIC: no default-layout k_actor form
   bool halo_overlap = true;              // MDR_OPT_HALO_OVERLAP: sharded actor tick, halo beside the interior tiles
+  bool halo_in_counts = true;            // MDR_OPT_HALO_IN_COUNTS: the next tick's ring halo rides in the count allreduce
+  unsigned long long* d_c5 = nullptr;    // that path's ring of 3 x [count slab | world x halo rows]
+  size_t c5_bytes = 0;
   int thermal = MDR_THERMAL_AFFINE;      // MDR_OPT_WINDOW_THERMAL: k_step_window's per-tick update
   int win = kWindowMax;                  // ticks per k_step_window launch (0: one-tick path)
   unsigned long long* d_wslab = nullptr; // 3 window count slots (mdr_kernels.hip K1W: slab | red | rec)
@@ -549,6 +552,7 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_win);
   hipFree(c->g_sorted); hipFree(c->g_map); hipFree(c->g_range); hipFree(c->g_tickets);
   hipFree(c->d_tickets);
+  hipFree(c->d_c5);
   if (c->comm) ncclCommDestroy(c->comm);
   delete c;
   return MDR_OK;
@@ -568,6 +572,7 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_GREEDY_SORT: c->greedy_sort = value != 0; break;
     case MDR_OPT_FORCE_HALO: c->force_halo = value != 0; break;
     case MDR_OPT_HALO_OVERLAP: c->halo_overlap = value != 0; break;
+    case MDR_OPT_HALO_IN_COUNTS: c->halo_in_counts = value != 0; break;
     case MDR_OPT_ACTOR_GENERIC: c->actor_generic = value != 0; break;
     case MDR_OPT_WINDOW_THERMAL:
       if (value != MDR_THERMAL_EXACT && value != MDR_THERMAL_AFFINE)
@@ -1198,6 +1203,7 @@ static ObsArgs obs_args(const mdr_ctx* c, const mdr_obs_spec* sp, const mdr_obs_
   o.msg_hvac = sp->msg_hvac;
   o.comm_table = sp->comm_table;
   o.halo_msg = sp->halo_msg;
+  o.halo_next = nullptr;
   o.msg_all = sp->msg_all;
   o.norm_reg_sig = sp->norm_reg_sig;
   o.cfg_ua = sp->cfg_ua;
@@ -2265,6 +2271,51 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
   mdr_obs_spec spec = *sp;
   spec.halo_msg = halo ? recv : nullptr;
   const ObsArgs o = obs_args(c, &spec, &osc[0]);
+  if (halo && c->halo_in_counts) {
+    // ONE collective per tick: the count slab and every rank's post-step edge rows of tick t (the
+    // halo of tick t + 1) in one integer sum-allreduce (k_halo_step_pack); tick 0's halo (of the
+    // current state) is exchanged once before the loop
+    const int W = lo + hi;
+    const size_t rows_words = ((size_t)c->world * W * M + 1) / 2;  // floats, two per u64 word
+    const size_t words = c->slab_len + rows_words;
+    if (3 * words * sizeof(unsigned long long) > c->c5_bytes) {
+      HIP_TRY(hipStreamSynchronize(st));
+      hipFree(c->d_c5);
+      c->d_c5 = nullptr;
+      HIP_TRY(hipMalloc(&c->d_c5, 3 * words * sizeof(unsigned long long)));
+      c->c5_bytes = 3 * words * sizeof(unsigned long long);
+    }
+    auto buf = [&](int t) { return c->d_c5 + (size_t)(t % 3) * words; };
+    auto rows = [&](int t) { return reinterpret_cast<float*>(buf(t) + c->slab_len); };
+    hipLaunchKernelGGL(k_zero_u64, dim3(1), dim3(256), 0, st, c->d_c5, (int64_t)(3 * words));
+    LAUNCH_CHECK("k_zero_u64");
+    hipLaunchKernelGGL(k_halo_pack, dim3(1), dim3(64), 0, st, c->kp, o, lo, hi, mine);
+    LAUNCH_CHECK("k_halo_pack");
+    if (int rc = comm_halo(c, mine, recv, lo, hi, M, st)) return rc;
+    const int prev = (c->rank + c->world - 1) % c->world, next = (c->rank + 1) % c->world;
+    for (int t = 0; t < n; ++t) {
+      ObsArgs ot = o;
+      ot.sc_dev = c->d_obs_sc + 4 * t;
+      if (t > 0) {  // the previous tick's allreduced rows: rank prev's last lo, rank next's first hi
+        ot.halo_msg = rows(t - 1) + (size_t)prev * W * M + (size_t)hi * M;
+        ot.halo_next = rows(t - 1) + (size_t)next * W * M;
+      }
+      ActorOut out{action ? action + (int64_t)t * act_stride : c->d_act,
+                   prob ? prob + (int64_t)t * prob_stride : nullptr, nullptr, nullptr, buf(t), nullptr};
+      if (int rc = launch_actor(c, &spec, ot, p_dev, 0, c->d_ticks + t, out, st)) return rc;
+      hipLaunchKernelGGL(k_halo_step_pack, dim3(1), dim3(256), 0, st, c->kp, ot, (const uint8_t*)out.action,
+                         (const TickArgs*)(c->d_ticks + t), lo, hi, c->rank, c->world, rows(t));
+      LAUNCH_CHECK("k_halo_step_pack");
+      if (int rc = comm_allreduce(c, buf(t), words, 0, st)) return rc;
+      c->gq_keys_ready = false;
+      if (int rc = launch_step_on(c, out.action, MDR_ACT_BUFFER, TickArgs{}, c->d_ticks + t,
+                                  reward + (int64_t)t * rew_stride, 0, MDR_CTRL_NONE, nullptr, p_dev, buf(t),
+                                  buf(t + 1), buf(t + 2), 0, st))
+        return rc;
+    }
+    c->counts_ready = false;
+    return MDR_OK;
+  }
   HIP_TRY(hipMemsetAsync(c->d_slab, 0, kSlabs * c->slab_len * sizeof(unsigned long long), st));
   c->ring = 0;
   // overlap (fused actor, >= 4 tiles, a comm stream): per tick the halo is packed and exchanged on the

@@ -69,7 +69,8 @@ struct ObsArgs {
   int n_feat, msg_w, n_comm, comm_mode;
   int hvac_state, solar_state, thermal_state, msg_thermal, msg_hvac;
   const int32_t* comm_table;
-  const float* halo_msg;  // [lo + hi][msg_w] or null
+  const float* halo_msg;  // [lo + hi][msg_w] or null (halo_next set: only the lo rows before the shard)
+  const float* halo_next; // the hi rows after the shard when they live apart from the lo rows, or null
   const float* msg_all;   // TABLE, sharded: [n_global][msg_w] (comm_table ids are global) or null
   double norm_reg_sig, cfg_ua, cfg_ca, cfg_cm, cfg_hm, cfg_cop, cfg_lcf, cfg_cap;
   double p, s, solar, t_od;
@@ -147,6 +148,8 @@ __global__ void k_cluster_stats(KParams p, const double* reward, double* partial
 __global__ void k_cluster_stats_final(const double* partial, int nblk, double* out);
 __global__ void k_obs(KParams p, ObsArgs o, const double* p_dev, float* obs);
 __global__ void k_halo_pack(KParams p, ObsArgs o, int lo, int hi, float* out);
+__global__ void k_halo_step_pack(KParams p, ObsArgs o, const uint8_t* action, const TickArgs* tkp, int lo, int hi,
+                                 int rank, int world, float* rows);
 __global__ void k_msg_pack(KParams p, ObsArgs o, float* out);
 __global__ void k_greedy_keys(KParams p, double* key, int* idx);
 __global__ void k_greedy_gather(KParams p, const int* perm, double* psorted, uint8_t* lsorted);

@@ -1672,6 +1672,41 @@ __global__ void k_halo_pack(KParams p, ObsArgs o, int lo, int hi, float* out) {
   }
 }
 
+// The sharded MA-PPO tick's one collective (mdr_actor_rollout_sharded): the ring halo of tick t + 1
+// needs the POST-step message features of this shard's first hi and last lo houses, and those need
+// only the houses' own state, the actions just sampled and the tick's drivers — not the cluster
+// power — so they are computed here, before the step (the same FSM and one-tick RC expressions as
+// the step kernels: bit-identical to the state the step will write), and packed into this rank's
+// slot of `rows` [world][hi + lo][msg_w] (rows 0..hi: first hi houses, hi..hi+lo: last lo), every
+// other slot zeroed: summed with the count slab in one integer allreduce, the slots become every
+// rank's rows (x + 0 is exact on the bit patterns).  One block.
+__global__ void k_halo_step_pack(KParams p, ObsArgs o, const uint8_t* __restrict__ action,
+                                 const TickArgs* __restrict__ tkp, int lo, int hi, int rank, int world,
+                                 float* __restrict__ rows) {
+  const int M = o.msg_w, tid = threadIdx.x, slot = (hi + lo) * M;
+  __shared__ float cf[kObsConst];
+  obs_consts(p, o, o.p, cf, tid, blockDim.x);  // (messages use only cf[8..] and P_max/R)
+  for (int e = tid; e < world * slot; e += blockDim.x)
+    if (e / slot != rank) rows[e] = 0.f;
+  __syncthreads();
+  const ObsDiv dv = obs_div(p);
+  const TickArgs tk = *tkp;
+  for (int t = tid; t < hi + lo; t += blockDim.x) {
+    int64_t j = t < hi ? t % p.n : p.n - lo + (t - hi);
+    if (j < 0) j = ((j % p.n) + p.n) % p.n;
+    HouseRegs r;
+    house_load(p, j, true, r);
+    r.w = hvac_fsm(r.w, action[j] != 0, p.dt, p.L);
+    const double q = hv_on(r.w) ? p.q_on[r.cls] : 0.0;
+    const RcCoef kc = rc_coeffs_t<false>(r.ua, r.ca, r.cm, r.hm, (double)p.dt);
+    double Tn, Tmn;
+    rc_apply_t<false>(r.T, r.Tm, r.ua, r.ca, r.hm, kc, q, tk.solar, tk.t_od_prev, Tn, Tmn);
+    r.T = Tn;
+    r.Tm = Tmn;
+    msg_from_regs(p, o, r, cf, rows + (size_t)rank * slot + (size_t)t * M, dv);
+  }
+}
+
 // message features of every local house (sharded table comm modes: all-gathered into msg_all)
 __global__ void k_msg_pack(KParams p, ObsArgs o, float* out) {
   __shared__ float cf[kObsConst];

@@ -160,7 +160,8 @@ __device__ __forceinline__ void obs_stage_ring(const KParams& p, const ObsArgs& 
     if (o.halo_msg && (j < 0 || j >= p.n)) {
       // multi-GPU ring: [0, lo) = houses before the shard, [lo, lo+hi) = houses after it
       const int h = j < 0 ? (int)(j + lo) : (int)(lo + (j - p.n));
-      for (int m = 0; m < M; ++m) msg[s * M + m] = o.halo_msg[h * M + m];
+      const float* src = o.halo_next && h >= lo ? o.halo_next + (size_t)(h - lo) * M : o.halo_msg + (size_t)h * M;
+      for (int m = 0; m < M; ++m) msg[s * M + m] = src[m];
     } else {
       j %= p.n;
       if (j < 0) j += p.n;

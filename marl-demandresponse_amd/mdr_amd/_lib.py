@@ -23,7 +23,7 @@ PEN_MODES = {"individual_L2": 0, "common_L2": 1, "common_max_error": 2, "mixture
 ERRORS = {-1: "MDR_EARG", -2: "MDR_EHIP", -3: "MDR_ERCCL", -4: "MDR_ENOMEM", -5: "MDR_ESTATE"}
 # mdr_set_option (mdr.h): alternative launch forms of the same computation
 OPTIONS = {"step_tpw": 1, "fastdiv": 2, "window_pipeline": 3, "sharded_overlap": 4, "greedy_sort": 5, "halo_overlap": 9, "actor_generic": 10,
-           "force_halo": 6, "window_thermal": 7}
+           "force_halo": 6, "window_thermal": 7, "halo_in_counts": 12}
 THERMAL_EXACT, THERMAL_AFFINE = 0, 1
 
 

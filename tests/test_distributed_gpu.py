@@ -229,7 +229,9 @@ def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo, laye
                       population="synthetic", seed=77, rank=rank, world=world, comm=make_comm(_comm_kind(kind)))
     if force_halo:
         env.shard.set_option("force_halo", 1)
-    if kind.endswith("-serialhalo"):  # MDR_OPT_HALO_OVERLAP off: halo, then one k_actor per tick
+    if "-twocoll" in kind:  # MDR_OPT_HALO_IN_COUNTS off: a ring-halo send/recv + the count allreduce per tick
+        env.shard.set_option("halo_in_counts", 0)
+    if kind.endswith("-serialhalo"):  # (two collectives) MDR_OPT_HALO_OVERLAP off: halo, then one k_actor per tick
         env.shard.set_option("halo_overlap", 0)
     res = _actor_run(env, torch, dist, layers)
     res["lo"] = env._offset
@@ -239,20 +241,30 @@ def _actor_worker(rank, world, port, backend, kind, n, out_dir, force_halo, laye
 
 @pytest.mark.parametrize("backend,kind,world,force_halo,n,layers", [
     ("nccl", "rccl", 1, False, 3001, (100, 100)),   # C loop: actor -> RCCL count allreduce -> step
-    ("nccl", "rccl", 1, True, 3001, (100, 100)),    # + the ring-halo pack / ncclSend / ncclRecv (to self)
+    # + the halo: the edge rows of the next tick summed into the count allreduce (to self), and the
+    # two-collective form (ring-halo pack / ncclSend / ncclRecv to self, then the allreduce)
+    ("nccl", "rccl", 1, True, 3001, (100, 100)),
+    ("nccl", "rccl-twocoll", 1, True, 3001, (100, 100)),
     ("gloo", "torch", 2, False, 3001, (100, 100)),  # two shards on cuda:0, per-tick Python loop, P2P halo
     ("gloo", "torch", 3, False, 3001, (100, 100)),  # distinct left / right peers
-    ("gloo", "host", 3, False, 3001, (100, 100)),   # the C loop: halo on the side stream beside the interior tiles
-    ("gloo", "host-serialhalo", 3, False, 3001, (100, 100)),  # halo pack -> send/recv -> actor -> allreduce -> step
+    # the C loop, ONE collective per tick: actor -> edge rows of the post-step state (k_halo_step_pack)
+    # -> allreduce of [count slab | every rank's rows] -> step
+    ("gloo", "host", 3, False, 3001, (100, 100)),
     ("gloo", "host", 3, False, 3001, (64, 64, 64)),  # the layer chain (k_obs reads the halo) in the C loop
+    # the two-collective C loop: halo on the side stream beside the interior tiles, or serial
+    ("gloo", "host-twocoll", 3, False, 3001, (100, 100)),
+    ("gloo", "host-twocoll-serialhalo", 3, False, 3001, (100, 100)),
+    ("gloo", "host-twocoll", 3, False, 3001, (64, 64, 64)),
     # ragged shards around the interior / edge tile split: 994 = 32 * 31 + 2 houses per rank (the
     # second-to-last tile's ring reaches the next shard, so the halo overlap must stay off), 992
     # (whole tiles), 101 = 32 * 3 + 5 (four tiles, the last one holding hi houses)
     ("gloo", "host", 3, False, 3 * 994, (100, 100)),
-    ("gloo", "host-serialhalo", 3, False, 3 * 994, (100, 100)),
-    ("gloo", "host", 3, False, 3 * 992, (100, 100)),
-    ("gloo", "host", 3, False, 3 * 101, (100, 100)),
+    ("gloo", "host-twocoll", 3, False, 3 * 994, (100, 100)),
+    ("gloo", "host-twocoll-serialhalo", 3, False, 3 * 994, (100, 100)),
+    ("gloo", "host-twocoll", 3, False, 3 * 992, (100, 100)),
+    ("gloo", "host-twocoll", 3, False, 3 * 101, (100, 100)),
     ("gloo", "host", 8, False, 8 * 131072, (100, 100)),  # C5: the 1,048,576-house cluster on 8 ranks
+    ("gloo", "host-twocoll", 8, False, 8 * 131072, (100, 100)),
 ])
 def test_sharded_actor_rollout_equals_single(tmp_path, backend, kind, world, force_halo, n, layers):
     """Sharded MA-PPO rollout (config C5) == the single-process graph rollout: actions, sampled
