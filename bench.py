@@ -100,6 +100,8 @@ def parse():
                          "size (graph capture + 2 replays: the first replay of a graph and of the host path is "
                          "2-3x slower than the steady state, profiles/r02e_bench20_warmup.log)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--gq-band", type=int, default=None, choices=[0, 1],
+                    help="greedy: A/B of the predicted band (MDR_OPT_GQ_BAND; default on)")
     ap.add_argument("--step-tpw", type=int, default=None,
                     help="per-tick step kernel tiles per wave (MDR_OPT_STEP_TPW; default: the library's choice)")
     ap.add_argument("--above-mall-houses", type=int, default=16 << 20,
@@ -388,6 +390,8 @@ def main():
         if world > 1:
             raise SystemExit("--workload greedy runs on one GPU (config C3)")
         g_act = torch.empty(n_loc, dtype=torch.uint8, device=dev)
+    if args.gq_band is not None:
+        env.shard.set_option("gq_band", args.gq_band)
     if args.step_tpw is not None:  # (A/B of the per-tick step kernel's tiles per wave, MDR_OPT_STEP_TPW)
         env.shard.set_option("step_tpw", args.step_tpw)
 
@@ -396,10 +400,8 @@ def main():
     def run(n):
         if dactor is not None:
             dactor.rollout(n, rewards=rew[:n])
-        elif g_act is not None:  # C3: controller on the post-step state -> step, every tick
-            for t in range(n):  # (the step's epilogue writes the next greedy call's keys)
-                env.greedy_actions(out=g_act)
-                env.step_tensor(g_act, rewards=rew[t], ctrl="greedy_keys")
+        elif g_act is not None:  # C3: controller on the post-step state -> step, every tick, one C
+            env.greedy_rollout(n, actions=g_act, rewards=rew[:n])  # call (the step writes the next keys)
         else:  # (whole buffers when the chunk fills them: no tensor views built per call)
             env.rollout(n, actions=None if acts is None else (acts if n == chunk else acts[:n]),
                         action_mode=args.mode, rewards=rew if n == chunk else rew[:n], use_graph=use_graph)
@@ -526,19 +528,18 @@ def main():
         bytes_launch = window_bytes(n_loc, k_win, args.mode) if window > 0 else BYTES_PER_HOUSE_STEP * n_loc
         steps_launch = k_win
     elif g_act is not None:
-        K = 20
+        K = min(20, rew.shape[0])
+        gt = env.driver_window(K)  # (the drivers first: the events bracket the device work)
         torch.cuda.synchronize()
         ev0.record(cur)
-        for t in range(K):
-            env.greedy_actions(out=g_act)
-            env.step_tensor(g_act, rewards=rew[t % rew.shape[0]], ctrl="greedy_keys")
+        sh.greedy_rollout(gt, g_act, 0, rew[:K], n_loc)
         ev1.record(cur)
         torch.cuda.synchronize()
         launches, kern_ms = K, ev0.elapsed_time(ev1) / K
         bytes_launch = (BYTES_PER_HOUSE_STEP + GREEDY_EXTRA) * n_loc
         steps_launch = 1
-        kern = ("greedy tick: histogram select (k_gq_bins, k_gq_compact, k_gq_select; "
-                "codes from the previous k_step_pipe's epilogue) + k_step_pipe")
+        kern = ("greedy tick: histogram select (k_gq_binsc, k_gq_compact, k_gq_select; codes, superbin "
+                "and predicted-band bin counts from the previous k_step_pipe's epilogue) + k_step_pipe")
     else:
         # the actor rollout graph interleaves k_actor and k_step: time the actor alone
         K = 50
@@ -612,11 +613,14 @@ def main():
         out["config"]["workload"] = ("C3: 1M houses, device GreedyMyopic (sort by -(T - target), budget = "
                                      "signal) on the post-step state, then env.step, every tick")
         out["config"]["action_mode"] = "greedy_myopic"
-        out["roofline"]["timing"] = "HIP events around 20 greedy+step ticks after the timed region"
+        out["roofline"]["timing"] = ("HIP events around one mdr_greedy_rollout call of 20 greedy+step ticks after "
+                                     "the timed region (drivers computed before the first event)")
         gd = sh.greedy_diag()  # (after every timed call: it synchronises)
         out["greedy_select"] = {"calls": gd["calls"], "fallbacks": gd["fallbacks"],
                                 "mean_window_houses": gd["window_sum"] / max(gd["calls"] - gd["fallbacks"], 1),
                                 "last_window_houses": gd["window_last"]}
+        bd = sh.greedy_band()  # the predicted band: calls whose bins pass k_gq_binsc skipped, and the misses
+        out["greedy_select"]["band"] = {"skips": bd["skips"], "misses": bd["misses"], "band_base": bd["band_base"]}
     if dactor is not None:
         a = dactor.actor
         flops_house = 2 * sum(l.in_features * l.out_features for l in a.fc)  # 30,400 at F = 50

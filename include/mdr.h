@@ -165,6 +165,9 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           houses' post-step message rows (the next tick's ring halo) are computed
  *                           before the step and summed into the count allreduce; 0 = a ring-halo
  *                           send/recv per tick plus the count allreduce (MDR_OPT_HALO_OVERLAP applies)
+ *   MDR_OPT_GQ_BAND         mdr_ctrl_greedy: 1 (default) = k_gq_binsc cuts the window from the step
+ *                           epilogue's predicted band when it holds the crossing (no bins pass); 0 = the
+ *                           bins pass every call (k_gq_bins)
  *   MDR_OPT_ACTOR_GENERIC   1 = k_actor runs its generic form for the reference's default obs layout too
  *                           (0, default: that layout runs the form specialised for it, mdr_actor.hip DEF)
  *   MDR_OPT_WINDOW_THERMAL  k_step_window's per-tick thermal update: MDR_THERMAL_AFFINE (default)
@@ -174,7 +177,8 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           operation order every tick (bit-identical to the one-tick kernels) */
 enum { MDR_OPT_STEP_TPW = 1, MDR_OPT_FASTDIV = 2, MDR_OPT_WINDOW_PIPELINE = 3, MDR_OPT_SHARDED_OVERLAP = 4,
        MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7,
-       MDR_OPT_HALO_OVERLAP = 9, MDR_OPT_ACTOR_GENERIC = 10, MDR_OPT_HALO_IN_COUNTS = 12 };
+       MDR_OPT_HALO_OVERLAP = 9, MDR_OPT_ACTOR_GENERIC = 10, MDR_OPT_HALO_IN_COUNTS = 12,
+       MDR_OPT_GQ_BAND = 13 };
 /* (8 was MDR_OPT_ACTOR_PINGPONG, a k_actor schedule measured slower and retired in r04: rejected) */
 enum { MDR_THERMAL_EXACT = 0, MDR_THERMAL_AFFINE = 1 };
 int mdr_set_option(mdr_ctx* ctx, int option, int64_t value);
@@ -351,8 +355,20 @@ int mdr_greedy_fallbacks(mdr_ctx* ctx, uint64_t* count);
 int mdr_greedy_diag(mdr_ctx* ctx, uint64_t* out);
 /* The select state after the last stage run (synchronises): out[12] = mdr_greedy_diag's 4 values,
  * then {crossing superbin, crossing bin b*, window end bin, all taken, overflow, houses after the
- * window, window allocator count, sharded need-fallback flag}. */
+ * window, window allocator count (zero again once the select has run), sharded need-fallback flag}. */
 int mdr_greedy_state(mdr_ctx* ctx, uint64_t* out);
+/* Config C3's loop: n ticks of {mdr_ctrl_greedy with budget ticks[t].s_prev (the
+ * signal before the tick's step, the one the observation carries) into action + t * act_stride,
+ * then mdr_step of those actions with MDR_CTRL_GREEDY_KEYS (reward + t * rew_stride; common
+ * penalty modes: + mdr_penalty_partials / mdr_reward_finalize)}; strides 0 = every tick overwrites.
+ * Replaces the per-tick Python loop GreedyMyopic.get_action -> Environment.step
+ * (greedy_myopic_controller.py:67-104, environment.py:86-106). */
+int mdr_greedy_rollout(mdr_ctx* ctx, int n, const mdr_tick* ticks, uint8_t* action, int64_t act_stride,
+                       double* reward, int64_t rew_stride, double* p_out, void* stream);
+/* The predicted band (synchronises): out[3] = {mdr_ctrl_greedy calls that skipped the bins pass
+ * (the step epilogue's band held the crossing, or no bins were needed), histogram-select calls,
+ * the first superbin of the band the next GQ step counts}.  Misses = calls - skips. */
+int mdr_greedy_band(mdr_ctx* ctx, uint64_t* out);
 
 /* Sharded greedy, histogram form (per-rank work O(N/G + window)): the same
  * select as mdr_ctrl_greedy with the caller's collectives between its stages, every rank deciding

@@ -131,6 +131,8 @@ struct mdr_ctx {
   uint4* g_sorted = nullptr;             // the window in (key, house) order (k_gq_select)
   int gq_parts_cap = 0;                  // g_part capacity in (min, max) pairs
   bool gq_keys_ready = false;            // keys + superbin histogram of the current state are in place
+  bool gq_hist_dirty = false;            // a producer added counts to g_hist that no select has consumed
+  bool gq_band = true;                   // MDR_OPT_GQ_BAND: k_gq_binsc (the predicted band) vs k_gq_bins
   int gq_nparts = 0;                     //   (from the last step's epilogue: its grid's partials)
   // multi-GPU
   ncclComm_t comm = nullptr;
@@ -280,7 +282,8 @@ int refresh_if_dirty(mdr_ctx* c, hipStream_t st) {
 }
 
 int greedy_scratch(mdr_ctx* c, int64_t n);
-int launch_gq_keys(mdr_ctx* c, hipStream_t st);
+int launch_gq_keys(mdr_ctx* c, hipStream_t st, unsigned long long* slab);
+int gq_hist_produce(mdr_ctx* c, hipStream_t st);
 // the histogram select's per-house codes (gq_code, 4 B) live in the sort form's key buffer
 uint32_t* gq_codes(mdr_ctx* c) { return reinterpret_cast<uint32_t*>(c->g_key); }
 
@@ -320,7 +323,10 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
     const unsigned nb = blocks(blocks(kp.n, 128), nwv * tpw);  // every tile covered: ceil(tiles / (waves x tpw))
     const dim3 grid(nb);
     GqOut go{};
-    if (epi) go = GqOut{gq_codes(c), c->g_part, c->g_hist, c->g_sel, c->g_map};
+    if (epi) {
+      if (int rc = gq_hist_produce(c, st)) return rc;
+      go = GqOut{gq_codes(c), c->g_part, c->g_hist, c->g_sel, c->g_map};
+    }
 #define MDR_LAUNCH_PIPE(T, A, LA, G)                                                                     \
   hipLaunchKernelGGL((k_step_pipe<T, A, LA, G>), grid, dim3(64 * nwv), 0, st, kp, action, tk, tkp, cur, reward, \
                      p_out, nxt, zer, go)
@@ -338,7 +344,7 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
     }
 #undef MDR_LAUNCH_PIPE
     LAUNCH_CHECK("k_step_pipe");
-    if (gq && !epi) return launch_gq_keys(c, st);
+    if (gq && !epi) return launch_gq_keys(c, st, nxt);
     if (epi) c->gq_nparts = (int)nb;
     return MDR_OK;
   }
@@ -351,7 +357,7 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
   }
 #undef MDR_LAUNCH_STEP
   LAUNCH_CHECK("k_step");
-  if (gq) return launch_gq_keys(c, st);
+  if (gq) return launch_gq_keys(c, st, nxt);
   return MDR_OK;
 }
 
@@ -573,6 +579,7 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_FORCE_HALO: c->force_halo = value != 0; break;
     case MDR_OPT_HALO_OVERLAP: c->halo_overlap = value != 0; break;
     case MDR_OPT_HALO_IN_COUNTS: c->halo_in_counts = value != 0; break;
+    case MDR_OPT_GQ_BAND: c->gq_band = value != 0; break;
     case MDR_OPT_ACTOR_GENERIC: c->actor_generic = value != 0; break;
     case MDR_OPT_WINDOW_THERMAL:
       if (value != MDR_THERMAL_EXACT && value != MDR_THERMAL_AFFINE)
@@ -1297,6 +1304,7 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   c->g_part = nullptr; c->g_hist = nullptr; c->g_sel = nullptr; c->g_win = nullptr;
   c->g_sorted = nullptr;
   c->gq_keys_ready = false;
+  c->gq_hist_dirty = false;
   HIP_TRY(hipMalloc(&c->g_key, n * sizeof(double)));
   HIP_TRY(hipMalloc(&c->g_key2, n * sizeof(double)));
   HIP_TRY(hipMalloc(&c->g_ps, n * sizeof(double)));
@@ -1312,13 +1320,13 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   HIP_TRY(hipMalloc(&c->g_part, 2 * (size_t)c->gq_parts_cap * sizeof(double)));
   HIP_TRY(hipMalloc(&c->g_hist, kGqHistWords * sizeof(unsigned)));
   HIP_TRY(hipMemset(c->g_hist, 0, kGqHistWords * sizeof(unsigned)));  // (the kernels re-zero what they read)
-  HIP_TRY(hipMalloc(&c->g_sel, 128));
+  HIP_TRY(hipMalloc(&c->g_sel, kGqSelBytes));
   HIP_TRY(hipMalloc(&c->g_map, kGqCells * sizeof(uint32_t)));
   {
-    unsigned char init[128] = {};
+    unsigned char init[kGqSelBytes] = {};
     uint32_t map[kGqCells];
     gq_sel_init(init, map);
-    HIP_TRY(hipMemcpy(c->g_sel, init, 128, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->g_sel, init, kGqSelBytes, hipMemcpyHostToDevice));
     HIP_TRY(hipMemcpy(c->g_map, map, sizeof(map), hipMemcpyHostToDevice));
   }
   HIP_TRY(hipMalloc(&c->g_win, (kGqCap + 1) * sizeof(uint4)));  // (sharded: [0] = the count header)
@@ -1335,10 +1343,25 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   return MDR_OK;
 }
 
-// the keys and superbin histogram of the current state (when no step epilogue prepared them)
-int launch_gq_keys(mdr_ctx* c, hipStream_t st) {
+// before a producer (k_gq_keys, the step's GQ epilogue) adds to g_hist: counts an earlier producer
+// left unconsumed (two GQ steps with no greedy call between, or keys dropped by a state change)
+// are zeroed first, so the select never sees the sum of two states
+int gq_hist_produce(mdr_ctx* c, hipStream_t st) {
+  if (c->gq_hist_dirty) {
+    hipLaunchKernelGGL(k_zero_u64, dim3(64), dim3(256), 0, st, reinterpret_cast<unsigned long long*>(c->g_hist),
+                       (int64_t)(kGqHistWords / 2));
+    LAUNCH_CHECK("k_zero_u64 (g_hist)");
+  }
+  c->gq_hist_dirty = true;
+  return MDR_OK;
+}
+
+// the keys and superbin histogram of the current state (when no step epilogue prepared them);
+// slab: zeroed for the decisions' counts (nullptr: none)
+int launch_gq_keys(mdr_ctx* c, hipStream_t st, unsigned long long* slab) {
+  if (int rc = gq_hist_produce(c, st)) return rc;
   hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_part, c->g_hist,
-                     c->g_sel, c->g_map);
+                     c->g_sel, c->g_map, slab);
   LAUNCH_CHECK("k_gq_keys");
   c->gq_nparts = kGqParts;
   return MDR_OK;
@@ -1365,11 +1388,18 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
     // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster, no host
     // synchronisation; k_gq_select decides exactly what the candidate window cannot
     if (!keys_ready)
-      if (int rc2 = launch_gq_keys(c, st)) return rc2;
-    hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
-                       c->g_sel, slab);
-    LAUNCH_CHECK("k_gq_bins");
+      if (int rc2 = launch_gq_keys(c, st, slab)) return rc2;
+    // the slab was zeroed by the codes' producer (k_gq_keys, or the GQ step: its next slab is this)
     const int nstage = (n + kGqStage - 1) / kGqStage;
+    if (c->gq_band) {
+      hipLaunchKernelGGL(k_gq_binsc, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
+                         c->g_sel, c->g_win, action, slab);
+      LAUNCH_CHECK("k_gq_binsc");
+    } else {
+      hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
+                         c->g_sel, slab);
+      LAUNCH_CHECK("k_gq_bins");
+    }
     hipLaunchKernelGGL(k_gq_compact, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
                        c->g_sel, c->g_win, action, slab);
     LAUNCH_CHECK("k_gq_compact");
@@ -1379,6 +1409,7 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
                        c->g_sorted, budget, pmin, c->g_sel, action, slab, c->g_hist, (const uint4*)nullptr, 0,
                        c->g_tickets, (const double*)c->g_part, c->gq_nparts, c->g_map);
     LAUNCH_CHECK("k_gq_select");
+    c->gq_hist_dirty = false;
     c->counts_ready = true;
     return MDR_OK;
   }
@@ -1408,8 +1439,8 @@ int mdr_greedy_diag(mdr_ctx* c, uint64_t* out) {
   if (!c || !out) return fail(MDR_EARG, "mdr_greedy_diag: null argument");
   for (int k = 0; k < 4; ++k) out[k] = 0;
   if (!c->g_sel) return MDR_OK;
-  unsigned char h[128];
-  HIP_TRY(hipMemcpy(h, c->g_sel, 128, hipMemcpyDeviceToHost));
+  unsigned char h[kGqSelBytes];
+  HIP_TRY(hipMemcpy(h, c->g_sel, kGqSelBytes, hipMemcpyDeviceToHost));
   gq_diag_of(h, out);
   return MDR_OK;
 }
@@ -1418,9 +1449,45 @@ int mdr_greedy_state(mdr_ctx* c, uint64_t* out) {
   if (!c || !out) return fail(MDR_EARG, "mdr_greedy_state: null argument");
   for (int k = 0; k < 12; ++k) out[k] = 0;
   if (!c->g_sel) return MDR_OK;
-  unsigned char h[128];
-  HIP_TRY(hipMemcpy(h, c->g_sel, 128, hipMemcpyDeviceToHost));
+  unsigned char h[kGqSelBytes];
+  HIP_TRY(hipMemcpy(h, c->g_sel, kGqSelBytes, hipMemcpyDeviceToHost));
   gq_state_of(h, out);
+  return MDR_OK;
+}
+
+// config C3's loop in one call: per tick, GreedyMyopic on the current state with the tick's
+// pre-step signal as budget (greedy_myopic_controller.py:67-104; the signal the obs carries), then
+// the step with those actions (environment.py:86-106), whose epilogue writes the next call's keys
+// — Environment.greedy_actions + step_tensor(ctrl='greedy_keys') per tick, without a host round
+// trip between them
+int mdr_greedy_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, uint8_t* action, int64_t act_stride,
+                       double* reward, int64_t rew_stride, double* p_out, void* stream) {
+  if (!c || (n > 0 && (!ticks || !action || !reward))) return fail(MDR_EARG, "mdr_greedy_rollout: null argument");
+  if (n < 0 || act_stride < 0 || rew_stride < 0) return fail(MDR_EARG, "mdr_greedy_rollout: negative size");
+  if (!c->bound) return fail(MDR_ESTATE, "mdr_greedy_rollout: context not bound");
+  hipStream_t st = S(stream);
+  for (int t = 0; t < n; ++t) {
+    uint8_t* a = action + (int64_t)t * act_stride;
+    double* r = reward + (int64_t)t * rew_stride;
+    if (int rc = mdr_ctrl_greedy(c, ticks[t].s_prev, a, stream)) return rc;
+    if (int rc = launch_step(c, a, MDR_ACT_BUFFER, to_tick(&ticks[t]), nullptr, r, 0, MDR_CTRL_GREEDY_KEYS, nullptr,
+                             p_out, st))
+      return rc;
+    if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2) {  // (Environment.step_tensor's common-penalty tail)
+      if (int rc = mdr_penalty_partials(c, stream)) return rc;
+      if (int rc = mdr_reward_finalize(c, &ticks[t], r, stream)) return rc;
+    }
+  }
+  return MDR_OK;
+}
+
+int mdr_greedy_band(mdr_ctx* c, uint64_t* out) {
+  if (!c || !out) return fail(MDR_EARG, "mdr_greedy_band: null argument");
+  for (int k = 0; k < 3; ++k) out[k] = 0;
+  if (!c->g_sel) return MDR_OK;
+  unsigned char h[kGqSelBytes];
+  HIP_TRY(hipMemcpy(h, c->g_sel, kGqSelBytes, hipMemcpyDeviceToHost));
+  gq_band_of(h, out);
   return MDR_OK;
 }
 
@@ -1449,7 +1516,7 @@ int mdr_gq_shard_begin(mdr_ctx* c, void* stream) {
   if (int rc = greedy_scratch(c, c->kp.n)) return rc;
   hipStream_t st = S(stream);
   if (!keys_ready)
-    if (int rc = launch_gq_keys(c, st)) return rc;
+    if (int rc = launch_gq_keys(c, st, nullptr)) return rc;
   hipLaunchKernelGGL(k_gq_range, dim3(1), dim3(256), 0, st, c->g_part, c->gq_nparts, c->g_range);
   LAUNCH_CHECK("k_gq_range");
   return MDR_OK;
@@ -1502,6 +1569,7 @@ int mdr_gq_shard_select(mdr_ctx* c, double budget, const void* gathered, int wor
                      static_cast<const uint4*>(gathered), world, c->g_tickets, (const double*)c->g_range, -1,
                      c->g_map);
   LAUNCH_CHECK("k_gq_select (sharded)");
+  c->gq_hist_dirty = false;
   return MDR_OK;
 }
 

@@ -94,7 +94,7 @@ struct GqOut {
   uint32_t* code;    // [n] the house's key bin << 2 | capacity class (gq_code)
   double* part;      // [grid][2] per-block (min, max) of the finite keys
   unsigned* hist;    // g_hist (the superbin copies follow its kGqBins * 4 bin words)
-  const GqSel* sel;  // this call's key map: the cell grid (GqSel.kmin, .scale) ...
+  GqSel* sel;        // this call's key map: the cell grid (GqSel.kmin, .scale) ...; the band (band_base, band_valid)
   const uint32_t* map;  // ... and the cells' bin ranges (gq_bin)
 };
 // waves per block of k_step_pipe with the GQ epilogue (4 without): fewer, larger blocks share one LDS
@@ -168,21 +168,33 @@ constexpr int kGqCopies = 8;  // copies of the global superbin / bin histograms 
 constexpr int kGqUnroll = 4;    // houses per thread per pass of k_gq_keys / k_gq_bins
 constexpr int kGqSuper = 256;   // superbins (64 bins each) of the select's first pass (+ 1 for NaN keys)
 constexpr int kGqHistWords = kGqBins * 4 + kGqCopies * (kGqSuper + 1) * 4;  // g_hist: bin copies | superbin copies
+// the predicted band: the bin class counts of kGqBand superbins around the previous call's crossing,
+// counted by the step kernel's GQ epilogue (its kGqCopies copies sit after the bin copies, inside the
+// first kGqBins * 4 words of g_hist); a call whose crossing lands inside skips the bins pass
+constexpr int kGqBand = 16;
+constexpr int kGqBandWords = kGqBand * 64 * 4;
+constexpr int kGqBandOff = kGqCopies * 512;
+static_assert(kGqBandOff + kGqCopies * kGqBandWords <= kGqBins * 4, "the band copies fit below the superbin copies");
+static_assert(kGqHistWords % 2 == 0, "g_hist is zeroed as 64-bit words");
 constexpr int kGqCells = 256;   // cells of the key -> bin map (gq_bin)
 constexpr int kGqSelBlocks = 256;  // k_gq_select grid, 1024 threads each
 constexpr int kGqMaxRanks = 64;   // sharded histogram select: ranks whose windows k_gq_select gathers
 struct GqSel;
-void gq_sel_init(void* sel128, uint32_t* map);  // host: the first call's key map (uniform over [-32, 32])
-void gq_diag_of(const void* sel128, uint64_t* out);
-void gq_state_of(const void* sel128, uint64_t* out);  // gq_diag_of + {sb, bstar, bend, all, overflow, more_after, wcount, need_fb}
+constexpr int kGqSelBytes = 256;  // g_sel: the GqSel record
+void gq_sel_init(void* sel, uint32_t* map);  // host: the first call's key map (uniform over [-32, 32])
+void gq_diag_of(const void* sel, uint64_t* out);
+void gq_state_of(const void* sel, uint64_t* out);  // gq_diag_of + {sb, bstar, bend, all, overflow, more_after, wcount, need_fb}
 size_t gq_wcount_offset();   // host: byte offsets of GqSel.wcount / .need_fb (sharded select)
 size_t gq_need_fb_offset();  // host: [fallbacks, calls, sum of window sizes, last window]
-__global__ void k_gq_keys(KParams p, uint32_t* code, double* part, unsigned* hist, const GqSel* sel,
-                          const uint32_t* map);
+__global__ void k_gq_keys(KParams p, uint32_t* code, double* part, unsigned* hist, GqSel* sel,
+                          const uint32_t* map, unsigned long long* slab);
 __global__ void k_gq_bins(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel,
                           unsigned long long* slab);
 __global__ void k_gq_compact(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel, uint4* win,
                              uint8_t* action, unsigned long long* slab);
+__global__ void k_gq_binsc(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel, uint4* win,
+                           uint8_t* action, unsigned long long* slab);
+void gq_band_of(const void* sel, uint64_t* out);  // host: {calls that skipped the bins pass, calls, band base}
 __global__ void k_gq_select(KParams p, const uint4* win, uint4* sorted, double S, double pmin, GqSel* sel,
                             uint8_t* action, unsigned long long* slab, unsigned* hist, const uint4* gathered,
                             int world, unsigned* tickets, const double* part, int nparts, uint32_t* map);

@@ -103,30 +103,47 @@ struct GqSel {
   int sb, bstar, bend, all, overflow, more_after, ncand;
   int whole;                     // the cluster fits the window (<= kGqCap houses): every house is a candidate
   unsigned fallbacks;            // calls decided by the exact fallback (gq_exact; diagnostics)
-  unsigned wcount;               // k_gq_compact's window allocator (zeroed by k_gq_bins)
+  unsigned wcount;               // k_gq_compact's window allocator (zeroed by gq_decide for the next call; k_gq_bins)
   unsigned calls;                // diagnostics: decisions made, and the sum of their window sizes
   unsigned need_fb;              // sharded: the window could not decide this call (host falls back)
   unsigned long long ncand_sum;
+  int band_base;                 // the first superbin of the predicted band the GQ epilogue counts bins of
+                                 // (gq_next_map: centred on where this call's crossing lands in the next map)
+  unsigned xcnt;                 // the houses before the crossing bin (gq_window block 0 -> gq_next_map)
+  unsigned xprev;                // the previous call's xcnt + 1 (0: none), for the band's trend
+  int sb_raw;                    // this call's crossing superbin as the last call predicted it (-1: none)
+  int sb_bias;                   // the last prediction's error (actual - predicted superbin)
+  int band_valid;                // the band copies hold this call's counts (the GQ epilogue sets it)
+  int hit;                       // k_gq_binsc skipped the bins pass (k_gq_compact then exits)
+  unsigned hits;                 // diagnostics: calls whose bins pass was skipped
 };
-static_assert(sizeof(GqSel) <= 128, "GqSel fits the 128-B sel buffer");
-void gq_sel_init(void* sel128, uint32_t* map) {
-  GqSel* g = static_cast<GqSel*>(sel128);  // (a zeroed 128-B host buffer)
+static_assert(sizeof(GqSel) <= kGqSelBytes, "GqSel fits the g_sel buffer");
+void gq_sel_init(void* sel, uint32_t* map) {
+  GqSel* g = static_cast<GqSel*>(sel);  // (a zeroed host buffer of kGqSelBytes)
   g->kmin = -4.0;                           // the first call: uniform bins over keys in [-4, 4] (K from
   g->scale = (double)kGqCells / 8.0;        // the target; keys outside clamp into the end cells)
   for (int c = 0; c < kGqCells; ++c) map[c] = ((uint32_t)(c * (kGqBins / kGqCells)) << 16) | (uint32_t)(kGqBins / kGqCells);
+  g->band_base = kGqSuper / 2 - kGqBand / 2;
+  g->sb_raw = -1;
+}
+void gq_band_of(const void* sel, uint64_t* out) {
+  const GqSel* g = static_cast<const GqSel*>(sel);
+  out[0] = g->hits;
+  out[1] = g->calls;
+  out[2] = (uint64_t)(int64_t)g->band_base;
 }
 size_t gq_wcount_offset() { return offsetof(GqSel, wcount); }
 size_t gq_need_fb_offset() { return offsetof(GqSel, need_fb); }
-void gq_diag_of(const void* sel128, uint64_t* out) {
-  const GqSel* g = static_cast<const GqSel*>(sel128);
+void gq_diag_of(const void* sel, uint64_t* out) {
+  const GqSel* g = static_cast<const GqSel*>(sel);
   out[0] = g->fallbacks;
   out[1] = g->calls;
   out[2] = g->ncand_sum;
   out[3] = (uint64_t)(int64_t)g->ncand;
 }
-void gq_state_of(const void* sel128, uint64_t* out) {
-  const GqSel* g = static_cast<const GqSel*>(sel128);
-  gq_diag_of(sel128, out);
+void gq_state_of(const void* sel, uint64_t* out) {
+  const GqSel* g = static_cast<const GqSel*>(sel);
+  gq_diag_of(sel, out);
   const int v[8] = {g->sb, g->bstar, g->bend, g->all, g->overflow, g->more_after, (int)g->wcount, (int)g->need_fb};
   for (int k = 0; k < 8; ++k) out[4 + k] = (uint64_t)(int64_t)v[k];
 }
@@ -498,18 +515,26 @@ __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KPar
   constexpr bool AB = ACT == MDR_ACT_BUFFER;
   __shared__ unsigned hist[MDR_MAX_CAP];
   __shared__ unsigned s_gq[GQ ? 4 * kGqSupStride : 1];
+  __shared__ unsigned s_band[GQ ? kGqBandWords : 1];  // (one copy: ~kGqBand / kGqSuper of the houses land in it)
   __shared__ uint32_t s_map[GQ ? kGqCells : 1];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   if (tid < p.n_cap) hist[tid] = 0;
+  int gq_band0 = 0;  // the band's first bin
   if (GQ) {
     for (int e = tid; e < 4 * kGqSupStride; e += blockDim.x) s_gq[e] = 0u;
+    for (int e = tid; e < kGqBandWords; e += blockDim.x) s_band[e] = 0u;
     for (int e = tid; e < kGqCells; e += blockDim.x) s_map[e] = gq.map[e];
+    gq_band0 = gq.sel->band_base * 64;
   }
   double gq_lo = INFINITY, gq_hi = -INFINITY;
   const double gq_kmin = GQ ? gq.sel->kmin : 0.0, gq_scale = GQ ? gq.sel->scale : 0.0;
   if (zero_slab && blockIdx.x == 0)
     for (int j = tid; j < kCountShards * p.n_cap; j += blockDim.x) zero_slab[j] = 0ull;
+  // GQ (no lookahead): the greedy call that follows counts its decisions into next_slab, and its
+  // one-pass form (k_gq_binsc) cannot zero it itself
+  if (GQ && !LA && next_slab && blockIdx.x == 0)
+    for (int j = tid; j < kCountShards * p.n_cap; j += blockDim.x) next_slab[j] = 0ull;
   const uint32_t n = (uint32_t)p.n;
   const uint32_t ntiles = (n + 64u * HPT - 1u) / (64u * HPT);
   const uint32_t nwaves = gridDim.x * (blockDim.x >> 6);
@@ -633,6 +658,8 @@ __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KPar
         }
         const uint32_t c = h ? c1 : c0;
         atomicAdd(&s_gq[((tid >> 6) & 3) * kGqSupStride + (c >> 8) * 4 + (c & 3u)], 1u);
+        const uint32_t bo = (c >> 2) - (uint32_t)gq_band0;  // (NaN keys: bin kGqBins, past any band)
+        if (bo < (uint32_t)(kGqBand * 64)) atomicAdd(&s_band[bo * 4 + (c & 3u)], 1u);
       }
     }
     if (LA) {
@@ -656,6 +683,11 @@ __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KPar
   if (GQ) {
     __syncthreads();
     gq_flush(s_gq, 4, gq.hist, gq_lo, gq_hi, gq.part);
+    for (int e = threadIdx.x; e < kGqBandWords; e += blockDim.x) {
+      const unsigned v = s_band[e];
+      if (v) atomicAdd(&gq.hist[kGqBandOff + (blockIdx.x % kGqCopies) * kGqBandWords + e], v);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) gq.sel->band_valid = 1;
   }
 }
 
@@ -1816,14 +1848,20 @@ __global__ void __launch_bounds__(256) k_greedy_walk(int64_t n, const double* __
 // K1: codes, per-block (min, max) of the finite keys (the next call's range), and the class counts
 // per superbin (kGqBins / kGqSuper consecutive bins; NaN keys in their own) under this call's
 // quantisation
+// (no band counts: band_valid = 0); block 0 zeroes the slab the decisions are counted into
 __global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, uint32_t* __restrict__ code, double* __restrict__ part,
-                                                        unsigned* __restrict__ hist, const GqSel* __restrict__ sel,
-                                                        const uint32_t* __restrict__ map) {
+                                                        unsigned* __restrict__ hist, GqSel* __restrict__ sel,
+                                                        const uint32_t* __restrict__ map, unsigned long long* __restrict__ slab) {
   constexpr int NW = kGqThreads / 64;
   __shared__ unsigned s_sh[NW * kGqSupStride];  // one copy per wave (less atomic contention on hot superbins)
   __shared__ uint32_t s_map[kGqCells];
   for (int e = threadIdx.x; e < NW * kGqSupStride; e += blockDim.x) s_sh[e] = 0u;
   for (int e = threadIdx.x; e < kGqCells; e += blockDim.x) s_map[e] = map[e];
+  if (blockIdx.x == 0) {
+    if (threadIdx.x == 0) sel->band_valid = 0;
+    if (slab)
+      for (int e = threadIdx.x; e < kCountShards * p.n_cap; e += blockDim.x) slab[e] = 0ull;
+  }
   __syncthreads();
   const double kmin = sel->kmin, scale = sel->scale;
   double lo = INFINITY, hi = -INFINITY;
@@ -1913,7 +1951,7 @@ struct GqSuper {
   unsigned long long before_cnt, total;
 };
 __device__ __forceinline__ GqSuper gq_super_find(const KParams& p, const unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
-                                 unsigned long long* __restrict__ slab) {
+                                 unsigned long long* __restrict__ slab, bool reset_alloc = true) {
   constexpr int NW = kGqThreads / 64;
   static_assert(kGqSupN <= kGqThreads && kGqCells < kGqThreads, "one superbin / cell edge per thread");
   __shared__ double s_w[NW], s_bt;
@@ -1951,8 +1989,10 @@ __device__ __forceinline__ GqSuper gq_super_find(const KParams& p, const unsigne
       sel->all = sb >= kGqSupN;
       sel->overflow = sb == kGqSuper && !whole;  // the crossing among NaN keys: the fallback orders them by house
       sel->whole = whole;
-      sel->wcount = 0u;
-      sel->need_fb = 0u;
+      if (reset_alloc) {  // (k_gq_binsc: other blocks of its launch may already allocate)
+        sel->wcount = 0u;
+        sel->need_fb = 0u;
+      }
     }
     if (slab)
       for (int e = tid; e < kCountShards * p.n_cap; e += blockDim.x) slab[e] = 0ull;
@@ -2099,7 +2139,25 @@ __device__ __forceinline__ void gq_next_map(const KParams& p, unsigned* __restri
     };
     const int b0 = edge(tid), b1 = edge(tid + 1);
     map[tid] = ((uint32_t)b0 << 16) | (uint32_t)(b1 - b0);
+    // the band the next producer counts: centred on the superbin the next call's crossing falls
+    // into under the new map if it moves as it did since the last call (xcnt houses before it now,
+    // the signal's trend: the sinusoid moves it by up to ~2 superbins a tick, tools/band_probe.py)
+    // and shifted by the last prediction's error: the keys move between this call and the next
+    // (the taken houses cool, the others warm), which the map of this call's keys cannot see
+    const double X1 = (double)sel->xcnt, X0 = sel->xprev ? (double)(sel->xprev - 1u) : X1;
+    const double X = fmin(fmax(2.0 * X1 - X0, 0.0), s_C[kGqCells]), c0 = s_C[tid], c1 = s_C[tid + 1];
+    if (T > 0.0 && X >= c0 && (X < c1 || tid == kGqCells - 1)) {
+      const double f = c1 > c0 ? fmin((X - c0) / (c1 - c0), 1.0) : 0.0;
+      const int sbp = (b0 + (int)(f * (double)(b1 - b0))) / (kGqBins / kGqSuper);
+      const int sb = sel->sb;
+      const int bias = sel->sb_raw >= 0 && sb < kGqSuper ? sb - sel->sb_raw : sel->sb_bias;
+      sel->sb_bias = bias;
+      sel->sb_raw = sbp;
+      sel->band_base = min(max(sbp + bias - (kGqBand / 2 - 1), 0), kGqSuper - kGqBand);
+    }
   }
+  __syncthreads();  // (every thread has read xprev)
+  if (tid == 0) sel->xprev = sel->xcnt + 1u;
   if (tid == 0) { sel->kmin = nkmin; sel->scale = nscale; }  // (no later kernel of this call maps keys)
   __syncthreads();  // (every thread has read the superbin copies and the old map)
   for (int e = tid; e < kGqCopies * kGqSupStride; e += blockDim.x) hist[kGqBins * 4 + e] = 0u;
@@ -2131,9 +2189,11 @@ struct GqWin {
   double win_tot;      // P before the window
   bool more_after;     // houses after the window
 };
-__device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
-                           int sb, bool all, bool ovf, bool whole, double base_tot, unsigned long long base_cnt,
-                           unsigned long long total) {
+// bins: the class counts of superbin sb's first bin in copy 0 (128 bins x 4 classes follow), the
+// other copies at multiples of cstride: gq_bins_flush's (g_hist, 512) or the band's (k_gq_binsc).
+__device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __restrict__ bins, int cstride, double S,
+                           GqSel* __restrict__ sel, int sb, bool all, bool ovf, bool whole, double base_tot,
+                           unsigned long long base_cnt, unsigned long long total) {
   static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
   static_assert(kGqCopies * 512 <= kGqBins * 4, "the bin copies fit below the superbin copies");
   __shared__ unsigned s_c[128];
@@ -2150,8 +2210,8 @@ __device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __r
     for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
     unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
 #pragma unroll
-    for (int q = 0; q < kGqCopies; ++q) {  // (gq_bins_flush's copies, 128 bins x 4 classes each)
-      const uint4 v = *reinterpret_cast<const uint4*>(hist + q * 512 + tid * 4);
+    for (int q = 0; q < kGqCopies; ++q) {
+      const uint4 v = *reinterpret_cast<const uint4*>(bins + q * cstride + tid * 4);
       c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] += v.w;
     }
     s_c[tid] = (unsigned)(c[0] + c[1] + c[2] + c[3]);
@@ -2202,8 +2262,10 @@ __device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __r
       st_sc1(&sel->win_tot, s_base);
       st_sc1(&sel->more_after, s_basec + (unsigned long long)cnt < total ? 1 : 0);
       st_sc1(&sel->ncand, cnt);
+      st_sc1(&sel->xcnt, (unsigned)s_basec);
     }
   }
+  if (!on && !whole && blockIdx.x == 0 && tid == 0) st_sc1(&sel->xcnt, (unsigned)(all ? total : base_cnt));
   if (whole && blockIdx.x == 0 && tid == 0) {  // every house is in the window
     st_sc1(&sel->bstar, 0);
     st_sc1(&sel->bend, kGqBins);
@@ -2305,6 +2367,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
                                                            unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
                                                            uint4* __restrict__ win, uint8_t* __restrict__ action,
                                                            unsigned long long* __restrict__ slab) {
+  if (sel->hit) return;  // k_gq_binsc compacted (block-uniform)
   // this block's houses first (every load before the selection reads: they stay in flight)
   const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
   constexpr int U = kGqStage / kGqThreads;
@@ -2316,10 +2379,56 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
     hw[u] = i < p.n ? p.hvac[i] : 0u;
   }
   const bool all = sel->all;
-  const GqWin w = gq_window(p, hist, S, sel, sel->sb, all, sel->overflow != 0, sel->whole != 0, sel->base_tot,
-                                   sel->base_cnt, sel->total);
+  const GqWin w = gq_window(p, hist, 512, S, sel, sel->sb, all, sel->overflow != 0, sel->whole != 0, sel->base_tot,
+                            sel->base_cnt, sel->total);
   if (w.ovf) return;  // the fallback (gq_exact) decides every house (block-uniform)
   gq_compact_houses<U>(p, cd, hw, b0, all, w, sel, win, action, slab);
+}
+
+// K2+K3 in one pass when the prediction holds (the single-GPU call, k_gq_compact's grid): every
+// block finds the crossing superbin (gq_super_find); when the step epilogue's band holds it and
+// the next superbin (band_valid; the band: gq_next_map's prediction), or no bins are needed (all
+// taken, a NaN crossing, one window), the block cuts the window from the band and compacts its
+// houses at once and k_gq_compact returns; otherwise it counts its houses' bins of the crossing
+// superbin and the next (k_gq_bins' work on this grid) and k_gq_compact cuts the window.  The
+// slab was zeroed by the codes' producer and the allocator by the previous call's gq_decide.
+__global__ void __launch_bounds__(kGqThreads) k_gq_binsc(KParams p, const uint32_t* __restrict__ code,
+                                                         unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
+                                                         uint4* __restrict__ win, uint8_t* __restrict__ action,
+                                                         unsigned long long* __restrict__ slab) {
+  constexpr int NW = kGqThreads / 64;
+  constexpr int U = kGqStage / kGqThreads;
+  __shared__ unsigned s_h[NW * kGqBinBand * 4];
+  const int tid = threadIdx.x;
+  const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
+  uint32_t cd[U], hw[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = b0 + u * kGqThreads + tid;
+    cd[u] = i < p.n ? code[i] : ~0u;  // (~0u: a bin past kGqBins, never counted)
+    hw[u] = i < p.n ? p.hvac[i] : 0u;
+  }
+  const int pb = sel->band_base;
+  const bool band = sel->band_valid != 0;
+  const GqSuper g = gq_super_find(p, hist, S, sel, nullptr, false);
+  const bool all = g.sb >= kGqSupN, ovf = g.sb == kGqSuper && !g.whole;
+  const bool inband = band && g.sb >= pb && g.sb + 1 < pb + kGqBand;
+  if (all || ovf || g.whole || inband) {  // (block-uniform)
+    const unsigned* bins = inband ? hist + kGqBandOff + (g.sb - pb) * 64 * 4 : hist;
+    const GqWin w = gq_window(p, bins, kGqBandWords, S, sel, g.sb, all, ovf, g.whole, g.before, g.before_cnt, g.total);
+    if (blockIdx.x == 0 && tid == 0) {
+      sel->hit = 1;
+      sel->hits += 1u;
+    }
+    if (w.ovf) return;  // the fallback (gq_exact) decides every house
+    gq_compact_houses<U>(p, cd, hw, b0, all, w, sel, win, action, slab);
+    return;
+  }
+  for (int e = tid; e < NW * kGqBinBand * 4; e += blockDim.x) s_h[e] = 0u;
+  __syncthreads();
+  gq_bins_add<U>(cd, g.sb * (kGqBins / kGqSuper), s_h);
+  __syncthreads();
+  gq_bins_flush(s_h, hist);
 }
 
 // 16-B window entries handed between workgroups of one launch as two 8-B agent-scope (sc1) accesses
@@ -2648,6 +2757,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
     if (ovf) sel->fallbacks += 1;
     if (ovf && sharded) sel->need_fb = 1u;
     sel->overflow = 0;       // (the next call starts clear)
+    sel->wcount = 0u;
     sel->calls += 1u;
     if (!all && !ovf) sel->ncand_sum += (unsigned long long)ncand;
   }
@@ -2690,8 +2800,14 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
   __shared__ uint4 s_e[kGqCap];
   __shared__ int s_off[kGqMaxRanks + 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (blockIdx.x == 0)
-    for (int e = tid; e < kGqCopies * 512; e += blockDim.x) hist[e] = 0u;
+  if (blockIdx.x == 0) {  // the bin copies and the band copies after them (read by compact / binsc)
+    static_assert(kGqBandOff == kGqCopies * 512, "the band copies follow the bin copies");
+    for (int e = tid; e < kGqBandOff + kGqCopies * kGqBandWords; e += blockDim.x) hist[e] = 0u;
+    if (tid == 0) {
+      sel->hit = 0;
+      sel->band_valid = 0;
+    }
+  }
   bool ovf0 = sel->overflow;
   bool live = !sel->all && !ovf0;
   const int ncand = sel->ncand;

@@ -23,7 +23,8 @@ PEN_MODES = {"individual_L2": 0, "common_L2": 1, "common_max_error": 2, "mixture
 ERRORS = {-1: "MDR_EARG", -2: "MDR_EHIP", -3: "MDR_ERCCL", -4: "MDR_ENOMEM", -5: "MDR_ESTATE"}
 # mdr_set_option (mdr.h): alternative launch forms of the same computation
 OPTIONS = {"step_tpw": 1, "fastdiv": 2, "window_pipeline": 3, "sharded_overlap": 4, "greedy_sort": 5, "halo_overlap": 9, "actor_generic": 10,
-           "force_halo": 6, "window_thermal": 7, "halo_in_counts": 12}
+           "force_halo": 6, "window_thermal": 7, "halo_in_counts": 12,
+           "gq_band": 13}
 THERMAL_EXACT, THERMAL_AFFINE = 0, 1
 
 
@@ -147,6 +148,8 @@ SIGNATURES = {
     "mdr_greedy_fallbacks": (I, [VP, VP]),
     "mdr_greedy_diag": (I, [VP, VP]),
     "mdr_greedy_state": (I, [VP, VP]),
+    "mdr_greedy_band": (I, [VP, VP]),
+    "mdr_greedy_rollout": (I, [VP, I, VP, VP, I64, VP, I64, VP, VP]),
     "mdr_build_id": (C.c_char_p, []),
     "mdr_greedy_inputs": (I, [VP, VP, VP, VP, VP]),
     "mdr_greedy_select": (I, [VP, I64, VP, VP, VP, D, VP, VP]),

@@ -639,6 +639,44 @@ class Environment:
         self._counts_ready = 0
         return rewards
 
+    def greedy_rollout(self, n_ticks: int, actions=None, rewards=None):
+        """Config C3's loop for n_ticks: ``greedy_actions`` then ``step_tensor(actions,
+        ctrl='greedy_keys')`` every tick, as one C call per driver window (mdr_greedy_rollout: no
+        Python between the ticks).  ``actions``: uint8 [n_ticks, N] (every tick's decisions) or a
+        1-D [N] buffer every tick overwrites (allocated if None); ``rewards`` likewise (float64).
+        Sharded, or a comm mode that draws per tick: the per-tick loop.  Returns (actions, rewards)."""
+        import torch
+
+        sh = self._shard
+        n = self._n_local
+        if actions is None:
+            actions = torch.empty(n, dtype=torch.uint8, device=sh.device)
+        if rewards is None:
+            rewards = torch.empty((n_ticks, n), dtype=torch.float64, device=sh.device)
+        for buf, dt, name in ((actions, torch.uint8, "actions"), (rewards, torch.float64, "rewards")):
+            if buf.dtype != dt or buf.shape[-1] != n or not buf.is_contiguous() or buf.dim() not in (1, 2) or (
+                    buf.dim() == 2 and buf.shape[0] < n_ticks):
+                raise ValueError(f"{name}: a contiguous {dt} tensor [n_ticks, {n}] or [{n}]")
+        a_st = n if actions.dim() == 2 else 0
+        r_st = n if rewards.dim() == 2 else 0
+        if self.world > 1 or self._links is None or self._grid_pending:
+            for t in range(n_ticks):
+                a = actions[t] if a_st else actions
+                self.greedy_actions(out=a)
+                self.step_tensor(a, rewards=rewards[t] if r_st else rewards, ctrl="greedy_keys")
+            return actions, rewards
+        done = 0
+        while done < n_ticks:  # one window unless interpolation ends it early (driver_window)
+            ticks = self.driver_window(n_ticks - done)
+            k = len(ticks)
+            sh.greedy_rollout(ticks, actions[done:] if a_st else actions, a_st,
+                              rewards[done:] if r_st else rewards, r_st)
+            self._P_dev_valid = True
+            self.finish_grid_step()
+            done += k
+        self._counts_ready = 0
+        return actions, rewards
+
     def greedy_actions(self, out=None):
         """GreedyMyopic.get_action (greedy_myopic_controller.py:67-104) on device: the next tick's
         actions from the current state, budget = the current regulation signal (obs reg_signal).

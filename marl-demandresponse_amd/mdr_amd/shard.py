@@ -228,6 +228,12 @@ class HipShard:
         L.check(self.lib.mdr_ctrl_greedy(self.ctx, float(budget), L.ptr(action), self.stream()),
                 "mdr_ctrl_greedy")
 
+    def greedy_rollout(self, ticks, action, act_stride, reward, rew_stride):
+        """mdr_greedy_rollout: config C3's greedy -> step loop over a TickWindow in one C call."""
+        L.check(self.lib.mdr_greedy_rollout(self.ctx, len(ticks), ticks.ptr(), L.ptr(action), act_stride,
+                                            L.ptr(reward), rew_stride, L.ptr(self.p_dev), self.stream()),
+                "mdr_greedy_rollout")
+
     # ---- sharded histogram select (mdr_gq_shard_*): the stages between the comm's collectives
     def gq_shard_begin(self) -> dict:
         """This shard's key codes, superbin histogram and key range; returns zero-copy views of the
@@ -281,6 +287,13 @@ class HipShard:
         names = ("fallbacks", "calls", "window_sum", "window_last", "sb", "bstar", "bend", "all", "overflow",
                  "more_after", "wcount", "need_fb")
         return {k: C.c_int64(v[i]).value for i, k in enumerate(names)}
+
+    def greedy_band(self) -> dict:
+        """The predicted band's record (mdr_greedy_band; synchronises): calls whose bins pass the
+        band let k_gq_binsc skip, calls, misses, and the band the next GQ step counts."""
+        v = (C.c_uint64 * 3)()
+        L.check(self.lib.mdr_greedy_band(self.ctx, v), "mdr_greedy_band")
+        return {"skips": int(v[0]), "calls": int(v[1]), "misses": int(v[1]) - int(v[0]), "band_base": int(v[2])}
 
     def obs(self, spec, scalars, out, use_p_dev=True):
         L.check(self.lib.mdr_obs(self.ctx, C.byref(spec), C.byref(scalars),

@@ -515,6 +515,94 @@ def test_greedy_loop_keys_epilogue_and_counts(torch_gpu):
     st = a.shard.host_state()
     np.testing.assert_array_equal(st["on"], o["on"])
     np.testing.assert_allclose(st["T"], o["T"], rtol=TEMP_RTOL, atol=0)
+    bd = a.shard.greedy_band()
+    assert bd["calls"] == 12 and bd["skips"] >= 1, bd  # (the twin never skips: its keys are k_gq_keys')
+    assert b.shard.greedy_band()["skips"] == 0
+
+
+@pytest.mark.parametrize("strided", [False, True])
+def test_greedy_rollout_matches_loop(torch_gpu, strided):
+    """Environment.greedy_rollout (mdr_greedy_rollout: config C3's loop in one C call, drivers from
+    driver_window) == the per-tick Python loop greedy_actions -> step_tensor(ctrl='greedy_keys') on a
+    twin: every tick's actions and rewards bit for bit, the state, clock and signal after; 13 ticks
+    at 200,003 houses (ragged tiles), per-tick buffers ('strided') or one overwritten buffer."""
+    torch = torch_gpu
+    n, T = 200_003, 13
+    _, a = _greedy_env(n, 29)
+    _, b = _greedy_env(n, 29)
+    if strided:
+        acts, rews = a.greedy_rollout(T, actions=torch.empty((T, n), dtype=torch.uint8, device="cuda"))
+    else:
+        acts, rews = a.greedy_rollout(T, rewards=torch.empty(n, dtype=torch.float64, device="cuda"))
+    ga = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for t in range(T):
+        ab = b.greedy_actions(out=ga)
+        rb = b.step_tensor(ab, ctrl="greedy_keys")
+        if strided:
+            assert torch.equal(acts[t], ab), t
+            assert torch.equal(rews[t], rb), t
+    if not strided:
+        assert torch.equal(acts, ab) and torch.equal(rews, rb)
+    sa, sb = a.shard.host_state(), b.shard.host_state()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    assert a.date_time == b.date_time and a._tick == b._tick
+    assert float(a.power_grid.current_signal) == float(b.power_grid.current_signal)
+    assert float(a.current_od_temp) == float(b.current_od_temp)
+    assert a.cluster.current_power_consumption == b.cluster.current_power_consumption
+
+
+def test_greedy_band_skips_and_misses(torch_gpu):
+    """The predicted band (k_gq_binsc): config C3's loop at 1,048,576 houses, 16 ticks, against the
+    oracle's greedy + step every tick, through every way a call meets the band: predicted ticks
+    (the window cut from the step epilogue's band, no bins pass), a forced miss (tick 6 decides a
+    budget at 10% of the cluster's cumulative power, far outside the band: the bins pass runs), the
+    tick after it (the band re-centred on the miss), and two GQ steps with no greedy call between
+    (tick 11: the first step's histograms are zeroed before the second's epilogue adds its own)."""
+    torch = torch_gpu
+    n = 1 << 20
+    props, env = _greedy_env(n, 41)
+    sh = env.shard
+    prm = sh.host_params()
+    caps = np.array(env._cap_values, np.float64)[prm["cap_idx"]]
+    pop = {"Ua": prm["ua"], "Ca": prm["ca"], "Cm": prm["cm"], "Hm": prm["hm"], "target": prm["target"], "cap": caps}
+    ora = O.OracleEnv(props, random.Random(41), population=pop)
+    cop = props.cluster_prop.house_prop.hvac_prop.cop
+    ga = torch.empty(n, dtype=torch.uint8, device="cuda")
+    log = []
+    for t in range(16):
+        before = sh.greedy_band()["skips"] if t in (6, 7) else None
+        if t == 6:
+            key = -(ora.T - ora.pop["target"])
+            order = np.argsort(key, kind="stable")
+            S = float(np.cumsum((caps / cop)[order])[n // 10]) + 0.25
+            sh.greedy(S, ga)
+            aa = ga
+        else:
+            S = float(ora.S)
+            aa = env.greedy_actions(out=ga)
+        ref = O.greedy(ora.T, ora.pop["target"], caps, cop, ora.lock, S)
+        np.testing.assert_array_equal(aa.cpu().numpy().astype(bool), ref, err_msg=f"greedy t={t}")
+        if t == 6:
+            assert sh.greedy_band()["skips"] == before, "a budget outside the band must run the bins pass"
+        r = env.step_tensor(aa, ctrl="greedy_keys").cpu().numpy()
+        o, rr = ora.step(ref)
+        np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12, err_msg=f"reward t={t}")
+        assert env.cluster.current_power_consumption == o["P"], t
+        if t == 11:  # a second GQ step before the next greedy call
+            z = torch.zeros(n, dtype=torch.uint8, device="cuda")
+            r = env.step_tensor(z, ctrl="greedy_keys").cpu().numpy()
+            o, rr = ora.step(np.zeros(n, bool))
+            np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12)
+        log.append(sh.greedy_band())
+    st = sh.host_state()
+    for k in ("on", "lock", "sso"):
+        np.testing.assert_array_equal(st[k], o[k], err_msg=k)
+    np.testing.assert_allclose(st["T"], o["T"], rtol=TEMP_RTOL, atol=0)
+    bd = sh.greedy_band()
+    print("band", bd, [d["band_base"] for d in log])
+    assert bd["calls"] == 16, bd
+    assert bd["skips"] >= 8, (bd, log)  # (ticks 0, 6 and 7 cannot skip; 12 may not)
 
 
 @pytest.mark.parametrize("case", ["nan_crossing", "nan_after", "identical_crossing"])
