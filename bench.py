@@ -553,6 +553,19 @@ def main():
         ev1.record(cur)
         torch.cuda.synchronize()
         actor_ms = ev0.elapsed_time(ev1) / K
+        actor_fp32_ms = None
+        if args.precision != "fp32":  # the reference's own precision, timed beside the headline form
+            from mdr_amd.actor import DeviceActor
+
+            d32 = DeviceActor(env, dactor.actor, precision="fp32")
+            d32.select_actions(action=act_buf, prob=prob_buf, count_next=False)
+            torch.cuda.synchronize()
+            ev0.record(cur)
+            for _ in range(K):
+                d32.select_actions(action=act_buf, prob=prob_buf, count_next=False)
+            ev1.record(cur)
+            torch.cuda.synchronize()
+            actor_fp32_ms = ev0.elapsed_time(ev1) / K
         launches = K
         kern_ms = max(gpu_ms / args.steps - actor_ms, 1e-6)  # the step kernel's share of a tick
         bytes_launch = BYTES_PER_HOUSE_STEP * n_loc
@@ -641,6 +654,12 @@ def main():
                            "step_share": {"what": "launch-stream time per tick minus k_actor's time: the step "
                                                   "kernel's share of a tick (not a kernel duration)",
                                           "us_per_tick": kern_ms * 1e3}}
+        if actor_fp32_ms is not None:
+            out["roofline"]["fp32_mode"] = {
+                "what": "the same k_actor launches in fp32-faithful mode (MFMA fp32 emulated by 6 bf16 products; "
+                        "the reference's own precision), timed the same way",
+                "kernel_avg_us": actor_fp32_ms * 1e3,
+                "achieved_tflops": flops_launch / (actor_fp32_ms * 1e-3) / 1e12}
     if (dactor is None and g_act is None and rank == 0 and window > 0 and args.above_mall_houses > 0
             and args.mode == "random"):
         out["roofline"]["above_mall"] = above_mall(args.above_mall_houses, args, kern)

@@ -365,9 +365,10 @@ int mdr_greedy_state(mdr_ctx* ctx, uint64_t* out);
  * (greedy_myopic_controller.py:67-104, environment.py:86-106). */
 int mdr_greedy_rollout(mdr_ctx* ctx, int n, const mdr_tick* ticks, uint8_t* action, int64_t act_stride,
                        double* reward, int64_t rew_stride, double* p_out, void* stream);
-/* The predicted band (synchronises): out[3] = {mdr_ctrl_greedy calls that skipped the bins pass
+/* The predicted band (synchronises): out[4] = {mdr_ctrl_greedy calls that skipped the bins pass
  * (the step epilogue's band held the crossing, or no bins were needed), histogram-select calls,
- * the first superbin of the band the next GQ step counts}.  Misses = calls - skips. */
+ * the first superbin of the band the next GQ step counts, the band's width in superbins}.
+ * Misses = calls - skips. */
 int mdr_greedy_band(mdr_ctx* ctx, uint64_t* out);
 
 /* Sharded greedy, histogram form (per-rank work O(N/G + window)): the same

@@ -1483,7 +1483,7 @@ int mdr_greedy_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, uint8_t* action
 
 int mdr_greedy_band(mdr_ctx* c, uint64_t* out) {
   if (!c || !out) return fail(MDR_EARG, "mdr_greedy_band: null argument");
-  for (int k = 0; k < 3; ++k) out[k] = 0;
+  for (int k = 0; k < 4; ++k) out[k] = 0;
   if (!c->g_sel) return MDR_OK;
   unsigned char h[kGqSelBytes];
   HIP_TRY(hipMemcpy(h, c->g_sel, kGqSelBytes, hipMemcpyDeviceToHost));

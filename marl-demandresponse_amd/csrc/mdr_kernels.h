@@ -171,7 +171,7 @@ constexpr int kGqHistWords = kGqBins * 4 + kGqCopies * (kGqSuper + 1) * 4;  // g
 // the predicted band: the bin class counts of kGqBand superbins around the previous call's crossing,
 // counted by the step kernel's GQ epilogue (its kGqCopies copies sit after the bin copies, inside the
 // first kGqBins * 4 words of g_hist); a call whose crossing lands inside skips the bins pass
-constexpr int kGqBand = 16;
+constexpr int kGqBand = 8;
 constexpr int kGqBandWords = kGqBand * 64 * 4;
 constexpr int kGqBandOff = kGqCopies * 512;
 static_assert(kGqBandOff + kGqCopies * kGqBandWords <= kGqBins * 4, "the band copies fit below the superbin copies");
@@ -194,7 +194,7 @@ __global__ void k_gq_compact(KParams p, const uint32_t* code, unsigned* hist, do
                              uint8_t* action, unsigned long long* slab);
 __global__ void k_gq_binsc(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel, uint4* win,
                            uint8_t* action, unsigned long long* slab);
-void gq_band_of(const void* sel, uint64_t* out);  // host: {calls that skipped the bins pass, calls, band base}
+void gq_band_of(const void* sel, uint64_t* out);  // host: {calls that skipped the bins pass, calls, band base, band width}
 __global__ void k_gq_select(KParams p, const uint4* win, uint4* sorted, double S, double pmin, GqSel* sel,
                             uint8_t* action, unsigned long long* slab, unsigned* hist, const uint4* gathered,
                             int world, unsigned* tickets, const double* part, int nparts, uint32_t* map);

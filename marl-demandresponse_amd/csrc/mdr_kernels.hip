@@ -131,6 +131,7 @@ void gq_band_of(const void* sel, uint64_t* out) {
   out[0] = g->hits;
   out[1] = g->calls;
   out[2] = (uint64_t)(int64_t)g->band_base;
+  out[3] = (uint64_t)kGqBand;
 }
 size_t gq_wcount_offset() { return offsetof(GqSel, wcount); }
 size_t gq_need_fb_offset() { return offsetof(GqSel, need_fb); }

@@ -291,9 +291,10 @@ class HipShard:
     def greedy_band(self) -> dict:
         """The predicted band's record (mdr_greedy_band; synchronises): calls whose bins pass the
         band let k_gq_binsc skip, calls, misses, and the band the next GQ step counts."""
-        v = (C.c_uint64 * 3)()
+        v = (C.c_uint64 * 4)()
         L.check(self.lib.mdr_greedy_band(self.ctx, v), "mdr_greedy_band")
-        return {"skips": int(v[0]), "calls": int(v[1]), "misses": int(v[1]) - int(v[0]), "band_base": int(v[2])}
+        return {"skips": int(v[0]), "calls": int(v[1]), "misses": int(v[1]) - int(v[0]), "band_base": int(v[2]),
+                "band_width": int(v[3])}
 
     def obs(self, spec, scalars, out, use_p_dev=True):
         L.check(self.lib.mdr_obs(self.ctx, C.byref(spec), C.byref(scalars),

@@ -21,6 +21,7 @@ def main():
     sh = env.shard
     act = torch.empty(n, dtype=torch.uint8, device="cuda:0")
     rows = []
+    kband = sh.greedy_band()["band_width"]
     for t in range(ticks):
         b0 = sh.greedy_band()
         env.greedy_actions(out=act)
@@ -28,7 +29,7 @@ def main():
         st = sh.greedy_state()
         env.step_tensor(act, ctrl="greedy_keys")
         rows.append((t, b0["band_base"], st["sb"], st["bstar"], b1["skips"] - b0["skips"], st["window_last"]))
-        print("t=%3d band=[%3d,%3d) sb=%3d bstar=%5d skip=%d window=%d" % (t, rows[-1][1], rows[-1][1] + 16,
+        print("t=%3d band=[%3d,%3d) sb=%3d bstar=%5d skip=%d window=%d" % (t, rows[-1][1], rows[-1][1] + kband,
                                                                           *rows[-1][2:]), flush=True)
     d = [r[2] - r[1] for r in rows[1:]]
     print("sb - band_base: min %d max %d mean %.2f; skips %d of %d" % (min(d), max(d), sum(d) / len(d),
