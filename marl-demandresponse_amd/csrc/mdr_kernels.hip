@@ -516,17 +516,17 @@ __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KPar
   constexpr bool AB = ACT == MDR_ACT_BUFFER;
   __shared__ unsigned hist[MDR_MAX_CAP];
   __shared__ unsigned s_gq[GQ ? 4 * kGqSupStride : 1];
-  __shared__ unsigned s_band[GQ ? kGqBandWords : 1];  // (one copy: ~kGqBand / kGqSuper of the houses land in it)
   __shared__ uint32_t s_map[GQ ? kGqCells : 1];
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   if (tid < p.n_cap) hist[tid] = 0;
   int gq_band0 = 0;  // the band's first bin
+  unsigned* gq_band = nullptr;  // this block's copy of the band's class counts
   if (GQ) {
     for (int e = tid; e < 4 * kGqSupStride; e += blockDim.x) s_gq[e] = 0u;
-    for (int e = tid; e < kGqBandWords; e += blockDim.x) s_band[e] = 0u;
     for (int e = tid; e < kGqCells; e += blockDim.x) s_map[e] = gq.map[e];
     gq_band0 = gq.sel->band_base * 64;
+    gq_band = gq.hist + kGqBandOff + (blockIdx.x % kGqCopies) * kGqBandWords;
   }
   double gq_lo = INFINITY, gq_hi = -INFINITY;
   const double gq_kmin = GQ ? gq.sel->kmin : 0.0, gq_scale = GQ ? gq.sel->scale : 0.0;
@@ -659,8 +659,11 @@ __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KPar
         }
         const uint32_t c = h ? c1 : c0;
         atomicAdd(&s_gq[((tid >> 6) & 3) * kGqSupStride + (c >> 8) * 4 + (c & 3u)], 1u);
-        const uint32_t bo = (c >> 2) - (uint32_t)gq_band0;  // (NaN keys: bin kGqBins, past any band)
-        if (bo < (uint32_t)(kGqBand * 64)) atomicAdd(&s_band[bo * 4 + (c & 3u)], 1u);
+        // the band's houses (~kGqBand / kGqSuper of them) add to the global copy at once: a few lanes
+        // per wave-instruction, issued inside the HBM-bound loop instead of a flush at the blocks'
+        // common end (NaN keys: bin kGqBins, past any band)
+        const uint32_t bo = (c >> 2) - (uint32_t)gq_band0;
+        if (bo < (uint32_t)(kGqBand * 64)) atomicAdd(&gq_band[bo * 4 + (c & 3u)], 1u);
       }
     }
     if (LA) {
@@ -684,10 +687,6 @@ __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KPar
   if (GQ) {
     __syncthreads();
     gq_flush(s_gq, 4, gq.hist, gq_lo, gq_hi, gq.part);
-    for (int e = threadIdx.x; e < kGqBandWords; e += blockDim.x) {
-      const unsigned v = s_band[e];
-      if (v) atomicAdd(&gq.hist[kGqBandOff + (blockIdx.x % kGqCopies) * kGqBandWords + e], v);
-    }
     if (blockIdx.x == 0 && threadIdx.x == 0) gq.sel->band_valid = 1;
   }
 }
@@ -2801,13 +2800,15 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
   __shared__ uint4 s_e[kGqCap];
   __shared__ int s_off[kGqMaxRanks + 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  if (blockIdx.x == 0) {  // the bin copies and the band copies after them (read by compact / binsc)
-    static_assert(kGqBandOff == kGqCopies * 512, "the band copies follow the bin copies");
-    for (int e = tid; e < kGqBandOff + kGqCopies * kGqBandWords; e += blockDim.x) hist[e] = 0u;
-    if (tid == 0) {
-      sel->hit = 0;
-      sel->band_valid = 0;
-    }
+  // the bin copies and the band copies after them (read by compact / binsc), a slice per block (a
+  // whole-region loop in block 0 made it the ticket's last arrival and delayed the decision)
+  static_assert(kGqBandOff == kGqCopies * 512, "the band copies follow the bin copies");
+  for (int e = (int)blockIdx.x * (int)blockDim.x + tid; e < kGqBandOff + kGqCopies * kGqBandWords;
+       e += (int)(gridDim.x * blockDim.x))
+    hist[e] = 0u;
+  if (blockIdx.x == 0 && tid == 0) {
+    sel->hit = 0;
+    sel->band_valid = 0;
   }
   bool ovf0 = sel->overflow;
   bool live = !sel->all && !ovf0;

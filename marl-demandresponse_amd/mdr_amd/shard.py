@@ -122,7 +122,7 @@ class HipShard:
     def set_option(self, name: str, value: int):
         """mdr_set_option: an alternative launch form of the same computation (mdr.h MDR_OPT_*:
         step_tpw, fastdiv, window_pipeline, sharded_overlap, greedy_sort, force_halo, halo_overlap,
-        actor_generic, window_thermal)."""
+        actor_generic, window_thermal, halo_in_counts, gq_band)."""
         L.check(self.lib.mdr_set_option(self.ctx, L.OPTIONS[name], int(value)), f"mdr_set_option({name})")
 
     def params_changed(self):

@@ -399,7 +399,8 @@ def test_greedy_four_million_vs_oracle(torch_gpu):
     at once, so later blocks start after block 0 has published the window (r03's race: block 0
     overwrote the crossing base those blocks still read, and they cut a different window).  The
     device greedy + step == the oracle's over 3 ticks, every call decided by the window (no exact
-    fallback)."""
+    fallback); the steps write the next call's keys (ctrl='greedy_keys'), so calls 2 and 3 may cut
+    their window from the predicted band in k_gq_binsc's 1,024 blocks."""
     from mdr_amd.environment import Environment
 
     n = 1 << 22
@@ -415,7 +416,7 @@ def test_greedy_four_million_vs_oracle(torch_gpu):
         a = env.greedy_actions().cpu().numpy().astype(bool)
         ref = O.greedy(ora.T, ora.pop["target"], caps, hv.cop, ora.lock, float(ora.S))
         np.testing.assert_array_equal(a, ref, err_msg=f"greedy t={t}")
-        r = env.step_tensor(torch_gpu.from_numpy(a.astype(np.uint8)).to("cuda")).cpu().numpy()
+        r = env.step_tensor(torch_gpu.from_numpy(a.astype(np.uint8)).to("cuda"), ctrl="greedy_keys").cpu().numpy()
         o, rr = ora.step(a)
         np.testing.assert_allclose(r, rr, rtol=1e-9, atol=1e-12)
         assert env.cluster.current_power_consumption == o["P"]
@@ -424,6 +425,7 @@ def test_greedy_four_million_vs_oracle(torch_gpu):
         np.testing.assert_array_equal(st[k], o[k], err_msg=k)
     d = env.shard.greedy_state()
     assert d["calls"] == 3 and d["fallbacks"] == 0, d
+    print("band", env.shard.greedy_band())
 
 
 @pytest.mark.parametrize("path", ["step", "rollout"])
