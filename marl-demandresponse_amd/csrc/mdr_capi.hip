@@ -1392,9 +1392,18 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
     // the slab was zeroed by the codes' producer (k_gq_keys, or the GQ step: its next slab is this)
     const int nstage = (n + kGqStage - 1) / kGqStage;
     if (c->gq_band) {
+      // the band's two launches: binsc (window from the band and compaction, or the bins), finish
+      // (rank + decide, or on a miss window + compaction + decide)
       hipLaunchKernelGGL(k_gq_binsc, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
                          c->g_sel, c->g_win, action, slab);
       LAUNCH_CHECK("k_gq_binsc");
+      hipLaunchKernelGGL(k_gq_finish, dim3(kGqSelBlocks), dim3(1024), 0, st, c->kp, (const uint32_t*)gq_codes(c),
+                         c->g_win, c->g_sorted, budget, pmin, c->g_sel, action, slab, c->g_hist, c->g_tickets,
+                         (const double*)c->g_part, c->gq_nparts, c->g_map);
+      LAUNCH_CHECK("k_gq_finish");
+      c->gq_hist_dirty = false;
+      c->counts_ready = true;
+      return MDR_OK;
     } else {
       hipLaunchKernelGGL(k_gq_bins, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
                          c->g_sel, slab);

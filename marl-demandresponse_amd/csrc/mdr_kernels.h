@@ -195,6 +195,9 @@ __global__ void k_gq_compact(KParams p, const uint32_t* code, unsigned* hist, do
 __global__ void k_gq_binsc(KParams p, const uint32_t* code, unsigned* hist, double S, GqSel* sel, uint4* win,
                            uint8_t* action, unsigned long long* slab);
 void gq_band_of(const void* sel, uint64_t* out);  // host: {calls that skipped the bins pass, calls, band base, band width}
+__global__ void k_gq_finish(KParams p, const uint32_t* code, uint4* win, uint4* sorted, double S, double pmin,
+                            GqSel* sel, uint8_t* action, unsigned long long* slab, unsigned* hist, unsigned* tickets,
+                            const double* part, int nparts, uint32_t* map);
 __global__ void k_gq_select(KParams p, const uint4* win, uint4* sorted, double S, double pmin, GqSel* sel,
                             uint8_t* action, unsigned long long* slab, unsigned* hist, const uint4* gathered,
                             int world, unsigned* tickets, const double* part, int nparts, uint32_t* map);

@@ -114,7 +114,7 @@ struct GqSel {
   int sb_raw;                    // this call's crossing superbin as the last call predicted it (-1: none)
   int sb_bias;                   // the last prediction's error (actual - predicted superbin)
   int band_valid;                // the band copies hold this call's counts (the GQ epilogue sets it)
-  int hit;                       // k_gq_binsc skipped the bins pass (k_gq_compact then exits)
+  int hit;                       // k_gq_binsc compacted from the band (k_gq_finish ranks; reset by its decider)
   unsigned hits;                 // diagnostics: calls whose bins pass was skipped
 };
 static_assert(sizeof(GqSel) <= kGqSelBytes, "GqSel fits the g_sel buffer");
@@ -2144,7 +2144,8 @@ __device__ __forceinline__ void gq_next_map(const KParams& p, unsigned* __restri
     // the signal's trend: the sinusoid moves it by up to ~2 superbins a tick, tools/band_probe.py)
     // and shifted by the last prediction's error: the keys move between this call and the next
     // (the taken houses cool, the others warm), which the map of this call's keys cannot see
-    const double X1 = (double)sel->xcnt, X0 = sel->xprev ? (double)(sel->xprev - 1u) : X1;
+    // (xcnt: sc1 — k_gq_finish's block 0 may have just written it, past this CU's L1)
+    const double X1 = (double)ld_sc1(&sel->xcnt), X0 = sel->xprev ? (double)(sel->xprev - 1u) : X1;
     const double X = fmin(fmax(2.0 * X1 - X0, 0.0), s_C[kGqCells]), c0 = s_C[tid], c1 = s_C[tid + 1];
     if (T > 0.0 && X >= c0 && (X < c1 || tid == kGqCells - 1)) {
       const double f = c1 > c0 ? fmin((X - c0) / (c1 - c0), 1.0) : 0.0;
@@ -2157,7 +2158,7 @@ __device__ __forceinline__ void gq_next_map(const KParams& p, unsigned* __restri
     }
   }
   __syncthreads();  // (every thread has read xprev)
-  if (tid == 0) sel->xprev = sel->xcnt + 1u;
+  if (tid == 0) sel->xprev = ld_sc1(&sel->xcnt) + 1u;
   if (tid == 0) { sel->kmin = nkmin; sel->scale = nscale; }  // (no later kernel of this call maps keys)
   __syncthreads();  // (every thread has read the superbin copies and the old map)
   for (int e = tid; e < kGqCopies * kGqSupStride; e += blockDim.x) hist[kGqBins * 4 + e] = 0u;
@@ -2367,7 +2368,6 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
                                                            unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
                                                            uint4* __restrict__ win, uint8_t* __restrict__ action,
                                                            unsigned long long* __restrict__ slab) {
-  if (sel->hit) return;  // k_gq_binsc compacted (block-uniform)
   // this block's houses first (every load before the selection reads: they stay in flight)
   const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
   constexpr int U = kGqStage / kGqThreads;
@@ -2389,9 +2389,9 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_compact(KParams p, const uint
 // block finds the crossing superbin (gq_super_find); when the step epilogue's band holds it and
 // the next superbin (band_valid; the band: gq_next_map's prediction), or no bins are needed (all
 // taken, a NaN crossing, one window), the block cuts the window from the band and compacts its
-// houses at once and k_gq_compact returns; otherwise it counts its houses' bins of the crossing
-// superbin and the next (k_gq_bins' work on this grid) and k_gq_compact cuts the window.  The
-// slab was zeroed by the codes' producer and the allocator by the previous call's gq_decide.
+// houses at once (GqSel.hit); otherwise it counts its houses' bins of the crossing superbin and
+// the next (k_gq_bins' work on this grid) and k_gq_finish cuts the window and compacts.  The slab
+// was zeroed by the codes' producer and the allocator by the previous call's gq_decide.
 __global__ void __launch_bounds__(kGqThreads) k_gq_binsc(KParams p, const uint32_t* __restrict__ code,
                                                          unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
                                                          uint4* __restrict__ win, uint8_t* __restrict__ action,
@@ -2766,6 +2766,16 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
 
 
 
+// the bin copies and the band copies after them (read by compact / binsc), a slice per block of
+// the launch (a whole-region loop in block 0 made it the ticket's last arrival and delayed the
+// decision); only where no block of the launch reads them
+__device__ __forceinline__ void gq_zero_bins_sliced(unsigned* __restrict__ hist) {
+  static_assert(kGqBandOff == kGqCopies * 512, "the band copies follow the bin copies");
+  for (int e = (int)(blockIdx.x * blockDim.x + threadIdx.x); e < kGqBandOff + kGqCopies * kGqBandWords;
+       e += (int)(gridDim.x * blockDim.x))
+    hist[e] = 0u;
+}
+
 // The window's houses ranked by the launch's waves (k_gq_select): wave w of the grid
 // takes entries w, w + waves, ... of s_e[0, ncand) (the window in LDS) and counts how many entries
 // precede each in (key, house) order, the lanes splitting the comparisons (one LDS read serves all
@@ -2800,16 +2810,8 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
   __shared__ uint4 s_e[kGqCap];
   __shared__ int s_off[kGqMaxRanks + 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  // the bin copies and the band copies after them (read by compact / binsc), a slice per block (a
-  // whole-region loop in block 0 made it the ticket's last arrival and delayed the decision)
-  static_assert(kGqBandOff == kGqCopies * 512, "the band copies follow the bin copies");
-  for (int e = (int)blockIdx.x * (int)blockDim.x + tid; e < kGqBandOff + kGqCopies * kGqBandWords;
-       e += (int)(gridDim.x * blockDim.x))
-    hist[e] = 0u;
-  if (blockIdx.x == 0 && tid == 0) {
-    sel->hit = 0;
-    sel->band_valid = 0;
-  }
+  gq_zero_bins_sliced(hist);
+  if (blockIdx.x == 0 && tid == 0) sel->band_valid = 0;
   bool ovf0 = sel->overflow;
   bool live = !sel->all && !ovf0;
   const int ncand = sel->ncand;
@@ -2864,6 +2866,102 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
   // the next call's key map, by block 0 (dispatched first, it is rarely the last to take a ticket:
   // the map's ~2 us run beside the decision instead of before it, as they did in k_gq_bins)
   static_assert(kGqMapLds <= (int)sizeof(s_e), "the map's work areas fit the window array");
+  if (blockIdx.x == 0) {
+    __syncthreads();  // (a decision by this block has finished with s_e)
+    gq_next_map(p, hist, part, nparts, sel, map, reinterpret_cast<unsigned char*>(s_e));
+  }
+}
+
+// K3 of the single-GPU call after k_gq_binsc, in place of k_gq_compact + k_gq_select (one launch
+// fewer on every call: the host cannot know whether binsc compacted).  GqSel.hit (binsc cut the window
+// from the band and compacted): the blocks rank the window as k_gq_select does and the last block
+// decides.  Otherwise (a band miss: binsc counted the bins): every block cuts the window from the bin
+// copies (gq_window, as k_gq_compact) and compacts its stages blockIdx, blockIdx + grid, ...; the last
+// block then ranks the whole window alone (one thread per house against the window in LDS: a miss is
+// rare) and decides.  Every block reads hit / the window state before its ticket; only the last block
+// (after every ticket) resets them.  Block 0 builds the next call's key map after its ticket.
+__global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint32_t* __restrict__ code,
+                                                    uint4* __restrict__ win, uint4* __restrict__ sorted, double S,
+                                                    double pmin, GqSel* __restrict__ sel, uint8_t* __restrict__ action,
+                                                    unsigned long long* __restrict__ slab, unsigned* __restrict__ hist,
+                                                    unsigned* __restrict__ tickets, const double* __restrict__ part,
+                                                    int nparts, uint32_t* __restrict__ map) {
+  static_assert(kGqThreads == 1024, "the miss path compacts with gq_compact_houses' block shape");
+  __shared__ uint4 s_e[kGqCap];
+  const int tid = threadIdx.x;
+  const bool hit = sel->hit != 0;
+  const bool all = sel->all != 0;
+  bool ovf;
+  int ncand;
+  double win_tot;
+  bool more_after;
+  if (hit) {
+    gq_zero_bins_sliced(hist);  // (nobody reads the bins or the band on this path)
+    ovf = sel->overflow != 0;
+    ncand = sel->ncand;
+    win_tot = sel->win_tot;
+    more_after = sel->more_after != 0;
+    if (!all && !ovf) {
+      constexpr int U = kGqCap / 1024;  // (every load issued before the LDS stores)
+      uint4 v[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (tid + u * 1024 < ncand) v[u] = win[tid + u * 1024];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (tid + u * 1024 < ncand) s_e[tid + u * 1024] = v[u];
+      __syncthreads();
+      gq_rank(s_e, ncand, sorted);
+    }
+  } else {
+    const GqWin w = gq_window(p, hist, 512, S, sel, sel->sb, all, sel->overflow != 0, sel->whole != 0,
+                              sel->base_tot, sel->base_cnt, sel->total);
+    ovf = w.ovf;
+    ncand = w.ncand;
+    win_tot = w.win_tot;
+    more_after = w.more_after;
+    if (!ovf) {
+      constexpr int U = kGqStage / kGqThreads;
+      const int nstage = (int)((p.n + kGqStage - 1) / kGqStage);
+      for (int b = (int)blockIdx.x; b < nstage; b += (int)gridDim.x) {  // (block-uniform)
+        const int64_t b0 = (int64_t)b * kGqStage;
+        uint32_t cd[U], hw[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int64_t i = b0 + u * kGqThreads + tid;
+          cd[u] = i < p.n ? code[i] : 0u;
+          hw[u] = i < p.n ? p.hvac[i] : 0u;
+        }
+        gq_compact_houses<U>(p, cd, hw, b0, all, w, sel, win, action, slab);
+        __syncthreads();  // (gq_compact_houses' LDS is reused by the next stage)
+      }
+    }
+  }
+  // hand-offs to the last block: sorted[] (hit) or win[] (miss), every store sc1 and drained before
+  // the ticket (grid_last_block), every load of them there sc1
+  if (grid_last_block(tickets)) {  // (block-uniform)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only)
+    if (!hit) {
+      if (!all && !ovf) {
+        for (int e = tid; e < ncand; e += (int)blockDim.x) s_e[e] = gq_load_sc1(win + e);
+        __syncthreads();
+        for (int e = tid; e < ncand; e += (int)blockDim.x) {
+          const uint4 me = s_e[e];
+          unsigned r = 0u;
+          for (int f = 0; f < ncand; ++f) r += gq_less(s_e[f], me) ? 1u : 0u;  // (one broadcast read a step)
+          if (r < (unsigned)kGqCap) gq_store_sc1(sorted + r, me);
+        }
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+      }
+      for (int e = tid; e < kGqBandOff + kGqCopies * kGqBandWords; e += (int)blockDim.x) hist[e] = 0u;
+    }
+    if (tid == 0) {
+      sel->hit = 0;
+      sel->band_valid = 0;
+    }
+    gq_decide(p, sorted, S, pmin, sel, action, slab, s_e, false, ovf, all, ncand, win_tot, more_after, false);
+  }
   if (blockIdx.x == 0) {
     __syncthreads();  // (a decision by this block has finished with s_e)
     gq_next_map(p, hist, part, nparts, sel, map, reinterpret_cast<unsigned char*>(s_e));
