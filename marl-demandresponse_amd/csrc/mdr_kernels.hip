@@ -1950,8 +1950,23 @@ struct GqSuper {
   double before;
   unsigned long long before_cnt, total;
 };
-__device__ __forceinline__ GqSuper gq_super_find(const KParams& p, const unsigned* __restrict__ hist, double S, GqSel* __restrict__ sel,
-                                 unsigned long long* __restrict__ slab, bool reset_alloc = true) {
+// the superbin copies of thread tid (< kGqSupN) as loaded values, issued before a caller's other loads
+// (gq_super_find's scan then waits only for these: vmcnt counts in issue order)
+struct GqSupLoad {
+  uint4 v[kGqCopies];
+};
+__device__ __forceinline__ GqSupLoad gq_super_load(const unsigned* __restrict__ hist) {
+  GqSupLoad l;
+  const int tid = threadIdx.x;
+  // (one branch around all the loads: per-load conditions made the compiler wait after every pair)
+  const int t = tid < kGqSupN ? tid : 0;
+  const uint4* src = reinterpret_cast<const uint4*>(hist + kGqBins * 4 + t * 4);
+#pragma unroll
+  for (int q = 0; q < kGqCopies; ++q) l.v[q] = src[q * (kGqSupStride / 4)];
+  return l;  // (threads >= kGqSupN hold superbin 0's counts: gq_super_find ignores them)
+}
+__device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLoad& l, double S, GqSel* __restrict__ sel,
+                                 unsigned long long* __restrict__ slab, bool reset_alloc) {
   constexpr int NW = kGqThreads / 64;
   static_assert(kGqSupN <= kGqThreads && kGqCells < kGqThreads, "one superbin / cell edge per thread");
   __shared__ double s_w[NW], s_bt;
@@ -1965,8 +1980,7 @@ __device__ __forceinline__ GqSuper gq_super_find(const KParams& p, const unsigne
   if (tid < kGqSupN)
 #pragma unroll
     for (int q = 0; q < kGqCopies; ++q) {
-      const uint4 v = *reinterpret_cast<const uint4*>(hist + kGqBins * 4 + q * kGqSupStride + tid * 4);
-      c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] += v.w;
+      c[0] += l.v[q].x; c[1] += l.v[q].y; c[2] += l.v[q].z; c[3] += l.v[q].w;
     }
   const double ps = win_power(p, c, p_on);
   const unsigned long long cs = c[0] + c[1] + c[2] + c[3];
@@ -1999,6 +2013,11 @@ __device__ __forceinline__ GqSuper gq_super_find(const KParams& p, const unsigne
   }
   __syncthreads();
   return GqSuper{sb, whole, s_bt, s_bc, s_total};
+}
+__device__ __forceinline__ GqSuper gq_super_find(const KParams& p, const unsigned* __restrict__ hist, double S,
+                                                 GqSel* __restrict__ sel, unsigned long long* __restrict__ slab,
+                                                 bool reset_alloc = true) {
+  return gq_super_scan(p, gq_super_load(hist), S, sel, slab, reset_alloc);
 }
 
 // The class counts of the bins of superbins sb and sb + 1 (the crossing superbin and the room after
@@ -2210,10 +2229,12 @@ __device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __r
 #pragma unroll
     for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
     unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
+    uint4 v[kGqCopies];  // (every copy's load issued before the first sum)
+#pragma unroll
+    for (int q = 0; q < kGqCopies; ++q) v[q] = *reinterpret_cast<const uint4*>(bins + q * cstride + tid * 4);
 #pragma unroll
     for (int q = 0; q < kGqCopies; ++q) {
-      const uint4 v = *reinterpret_cast<const uint4*>(bins + q * cstride + tid * 4);
-      c[0] += v.x; c[1] += v.y; c[2] += v.z; c[3] += v.w;
+      c[0] += v[q].x; c[1] += v[q].y; c[2] += v[q].z; c[3] += v[q].w;
     }
     s_c[tid] = (unsigned)(c[0] + c[1] + c[2] + c[3]);
     if (tid < 64) {  // wave 0: the crossing bin of superbin sb (it crosses: gq_super_find)
@@ -2328,7 +2349,21 @@ __device__ __forceinline__ void gq_compact_houses(const KParams& p, const uint32
   double kk[U];
 #pragma unroll
   for (int u = 0; u < U; ++u)
-    kk[u] = inw[u] ? gq_key_of(p, b0 + u * kGqThreads + tid) : 0.0;
+    kk[u] = 0.0;
+  // (the loads of every u first, the subtractions after: a use right behind each conditional load
+  // made the compiler wait out each pair's round trip in turn)
+  double ta[U], tg[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    ta[u] = tg[u] = 0.0;
+    if (inw[u]) {
+      ta[u] = p.t_air[b0 + u * kGqThreads + tid];
+      tg[u] = p.target[b0 + u * kGqThreads + tid];
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u)
+    if (inw[u]) kk[u] = -(ta[u] - tg[u]);  // gq_key_of
   unsigned x = mine;  // this lane's slots: a wave prefix, the wave's offset in the block, the block's base
 #pragma unroll
   for (int off = 1; off < 64; off <<= 1) {
@@ -2401,16 +2436,23 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_binsc(KParams p, const uint32
   __shared__ unsigned s_h[NW * kGqBinBand * 4];
   const int tid = threadIdx.x;
   const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
-  uint32_t cd[U], hw[U];
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int64_t i = b0 + u * kGqThreads + tid;
-    cd[u] = i < p.n ? code[i] : ~0u;  // (~0u: a bin past kGqBins, never counted)
-    hw[u] = i < p.n ? p.hvac[i] : 0u;
-  }
+  // the superbin counts and this block's houses, all issued before the scan's first wait (r05: the
+  // per-load conditions of the old form made the compiler wait after every pair of superbin loads,
+  // four serialised round trips)
+  const GqSupLoad sup = gq_super_load(hist);
   const int pb = sel->band_base;
   const bool band = sel->band_valid != 0;
-  const GqSuper g = gq_super_find(p, hist, S, sel, nullptr, false);
+  uint32_t cd[U], hw[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {  // (unconditional, clamped: no branch, nothing waits on them yet)
+    const int64_t i = b0 + u * kGqThreads + tid, ic = i < p.n ? i : p.n - 1;
+    cd[u] = code[ic];
+    hw[u] = p.hvac[ic];
+  }
+  const GqSuper g = gq_super_scan(p, sup, S, sel, nullptr, false);
+#pragma unroll
+  for (int u = 0; u < U; ++u)  // (~0u: a bin past kGqBins, never counted; gq_compact_houses checks i)
+    if (b0 + u * kGqThreads + tid >= p.n) cd[u] = ~0u;
   const bool all = g.sb >= kGqSupN, ovf = g.sb == kGqSuper && !g.whole;
   const bool inband = band && g.sb >= pb && g.sb + 1 < pb + kGqBand;
   if (all || ovf || g.whole || inband) {  // (block-uniform)
@@ -2418,7 +2460,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_binsc(KParams p, const uint32
     const GqWin w = gq_window(p, bins, kGqBandWords, S, sel, g.sb, all, ovf, g.whole, g.before, g.before_cnt, g.total);
     if (blockIdx.x == 0 && tid == 0) {
       sel->hit = 1;
-      sel->hits += 1u;
+      atomicAdd(&sel->hits, 1u);  // (no load to wait for: a += stalled block 0 a round trip)
     }
     if (w.ovf) return;  // the fallback (gq_exact) decides every house
     gq_compact_houses<U>(p, cd, hw, b0, all, w, sel, win, action, slab);
@@ -2831,25 +2873,14 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
     }
   }
   if (live) {
-    constexpr int U = kGqCap / 1024;  // (every load issued before the LDS stores)
-    uint4 v[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = tid + u * 1024;
-      if (e < ncand) {
-        if (gathered) {
-          int r = 0;
-          while (r + 1 < world && s_off[r + 1] <= e) ++r;
-          v[u] = gathered[(size_t)r * (kGqCap + 1) + 1 + (e - s_off[r])];
-        } else {
-          v[u] = win[e];
-        }
+    for (int e = tid; e < ncand; e += (int)blockDim.x) {  // (one load per thread up to 1,024 houses)
+      if (gathered) {
+        int r = 0;
+        while (r + 1 < world && s_off[r + 1] <= e) ++r;
+        s_e[e] = gathered[(size_t)r * (kGqCap + 1) + 1 + (e - s_off[r])];
+      } else {
+        s_e[e] = win[e];
       }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int e = tid + u * 1024;
-      if (e < ncand) s_e[e] = v[u];
     }
     __syncthreads();
     gq_rank(s_e, ncand, sorted);
@@ -2902,14 +2933,9 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint32_t* _
     win_tot = sel->win_tot;
     more_after = sel->more_after != 0;
     if (!all && !ovf) {
-      constexpr int U = kGqCap / 1024;  // (every load issued before the LDS stores)
-      uint4 v[U];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (tid + u * 1024 < ncand) v[u] = win[tid + u * 1024];
-#pragma unroll
-      for (int u = 0; u < U; ++u)
-        if (tid + u * 1024 < ncand) s_e[tid + u * 1024] = v[u];
+      // (a plain loop: one load per thread for a window of <= 1,024 houses; the array form of
+      // k_gq_select spilled to scratch)
+      for (int e = tid; e < ncand; e += (int)blockDim.x) s_e[e] = win[e];
       __syncthreads();
       gq_rank(s_e, ncand, sorted);
     }
