@@ -214,11 +214,7 @@ __device__ __forceinline__ void split8_trunc(const float* v, bf16x8& hi, bf16x8&
 template <int PREC>
 __device__ __forceinline__ void split_operand(const float* v, bf16x8* s) {
   if constexpr (PREC == 6) split8x3(v, s[0], s[1], s[2]);
-#ifdef MDR_ACTOR_RNE_SPLIT  // (A/B builds: the rounded-hi split of r03)
-  else if constexpr (PREC == 3) split8(v, s[0], s[1]);
-#else
-  else if constexpr (PREC == 3) split8_trunc(v, s[0], s[1]);
-#endif
+  else if constexpr (PREC == 3) split8_trunc(v, s[0], s[1]);  // (r03's rounded-hi split: DESIGN.md §3.4)
   else {
 #pragma unroll
     for (int j = 0; j < 8; ++j) s[0][j] = (__bf16)v[j];
