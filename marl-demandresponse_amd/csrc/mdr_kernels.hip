@@ -2920,6 +2920,9 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint32_t* _
   static_assert(kGqThreads == 1024, "the miss path compacts with gq_compact_houses' block shape");
   __shared__ uint4 s_e[kGqCap];
   const int tid = threadIdx.x;
+  // the window's first 1,024 slots are loaded before the window's size is known (beside the GqSel
+  // reads: one round trip instead of two; slots past the size are never used)
+  const uint4 w0 = win[tid];
   const bool hit = sel->hit != 0;
   const bool all = sel->all != 0;
   bool ovf;
@@ -2933,9 +2936,8 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint32_t* _
     win_tot = sel->win_tot;
     more_after = sel->more_after != 0;
     if (!all && !ovf) {
-      // (a plain loop: one load per thread for a window of <= 1,024 houses; the array form of
-      // k_gq_select spilled to scratch)
-      for (int e = tid; e < ncand; e += (int)blockDim.x) s_e[e] = win[e];
+      if (tid < ncand) s_e[tid] = w0;
+      for (int e = tid + (int)blockDim.x; e < ncand; e += (int)blockDim.x) s_e[e] = win[e];  // (> 1,024)
       __syncthreads();
       gq_rank(s_e, ncand, sorted);
     }
