@@ -554,6 +554,39 @@ def test_greedy_rollout_matches_loop(torch_gpu, strided):
     assert a.cluster.current_power_consumption == b.cluster.current_power_consumption
 
 
+@pytest.mark.parametrize("n", [200_003, 1 << 20])
+def test_greedy_band_forms_agree(torch_gpu, n):
+    """The band's two launches (k_gq_binsc + k_gq_finish) against the r04 three (MDR_OPT_GQ_BAND 0)
+    on twin environments: 24 ticks of C3's loop (mostly band hits), then 12 calls at budgets drawn
+    at random across the cluster's cumulative power (mostly misses: k_gq_finish cuts the window,
+    compacts and ranks it in its last block), each followed by a GQ step; actions and rewards bit
+    for bit, the same state after."""
+    torch = torch_gpu
+    props, a = _greedy_env(n, 37)
+    _, b = _greedy_env(n, 37)
+    b.shard.set_option("gq_band", 0)
+    ra, rb = a.greedy_rollout(24)[1], b.greedy_rollout(24)[1]
+    assert torch.equal(ra, rb)
+    prm = a.shard.host_params()
+    p_all = float(np.sum(np.array(a._cap_values, np.float64)[prm["cap_idx"]]) /
+                  props.cluster_prop.house_prop.hvac_prop.cop)
+    rs = np.random.RandomState(5)
+    ga = torch.empty(n, dtype=torch.uint8, device="cuda")
+    gb = torch.empty(n, dtype=torch.uint8, device="cuda")
+    for t in range(12):
+        S = p_all * float(rs.uniform(0.02, 0.98))
+        a.shard.greedy(S, ga)
+        b.shard.greedy(S, gb)
+        assert torch.equal(ga, gb), t
+        r1 = a.step_tensor(ga, ctrl="greedy_keys")
+        r2 = b.step_tensor(gb, ctrl="greedy_keys")
+        assert torch.equal(r1, r2), t
+    sa, sb = a.shard.host_state(), b.shard.host_state()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    print("band", a.shard.greedy_band())
+
+
 def test_greedy_band_skips_and_misses(torch_gpu):
     """The predicted band (k_gq_binsc): config C3's loop at 1,048,576 houses, 16 ticks, against the
     oracle's greedy + step every tick, through every way a call meets the band: predicted ticks
