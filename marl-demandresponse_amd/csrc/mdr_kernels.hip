@@ -2671,7 +2671,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
   __shared__ uint8_t s_tk[kGqCap];
   __shared__ double s_w[16];
   __shared__ double s_tot;
-  __shared__ int s_k, s_first, s_ovf, s_pick;
+  __shared__ int s_k, s_first, s_ovf;
   __shared__ unsigned long long s_bal[16];
   __shared__ unsigned s_cnt[kWinCap];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nth = blockDim.x;
@@ -2739,33 +2739,36 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
       if (tid == 0) s_ovf = 1;
     } else {
       // the gap walk from the crossing (k_greedy_walk's rule, in the reference's order): tot changes
-      // only at a take, so each step is one block-wide search for the first house after the last
-      // take that the rule admits (r03: one thread stepping house by house, ~20 us at a window of
-      // ~370 houses).  Every thread carries the same tot and pick: the sums happen in take order.
-      double tot = s_tot;
-      int j0 = k;
-      bool over = false;
-      for (;;) {
-        if (gq_walk_over(tot, S, pmin)) {
-          over = true;
-          break;
-        }
-        if (tid == 0) s_pick = 0x7fffffff;
-        __syncthreads();
-        for (int e = j0 + tid; e < ncand; e += nth)
-          if (gq_take(P_of(s_e[e].z), tot, S, hv_lock(s_e[e].w))) {
-            atomicMin(&s_pick, e);
+      // only at a take, so each step is a search for the first house after the last take that the
+      // rule admits — by wave 0 alone, 64 houses a ballot, no block barrier per step (r04: block-wide
+      // searches, three barriers a take; r03: one thread stepping house by house).  Every lane
+      // carries the same tot: the sums happen in take order.
+      if (wv == 0) {
+        double tot = s_tot;
+        int j0 = k;
+        bool over = false;
+        for (;;) {
+          if (gq_walk_over(tot, S, pmin)) {
+            over = true;
             break;
           }
-        __syncthreads();
-        const int f = s_pick;
-        __syncthreads();  // (every thread has read it before the next step resets it)
-        if (f == 0x7fffffff) break;  // no house left in the window: the walk reaches its end
-        if (tid == 0) s_tk[f] = 1;
-        tot += P_of(s_e[f].z);
-        j0 = f + 1;
+          int f = -1;
+          for (int c = j0; c < ncand; c += 64) {  // (wave-uniform)
+            const int e = c + lane;
+            const bool ok = e < ncand && gq_take(P_of(s_e[e].z), tot, S, hv_lock(s_e[e].w));
+            const unsigned long long m = __ballot(ok);
+            if (m) {
+              f = c + __ffsll((long long)m) - 1;
+              break;
+            }
+          }
+          if (f < 0) break;  // no house left in the window: the walk reaches its end
+          if (lane == 0) s_tk[f] = 1;
+          tot += P_of(s_e[f].z);
+          j0 = f + 1;
+        }
+        if (lane == 0) s_ovf = (!over && more_after && !gq_walk_over(tot, S, pmin)) ? 1 : 0;
       }
-      if (tid == 0) s_ovf = (!over && more_after && !gq_walk_over(tot, S, pmin)) ? 1 : 0;
     }
     __syncthreads();
     ovf = s_ovf != 0;
@@ -2822,10 +2825,14 @@ __device__ __forceinline__ void gq_zero_bins_sliced(unsigned* __restrict__ hist)
 // takes entries w, w + waves, ... of s_e[0, ncand) (the window in LDS) and counts how many entries
 // precede each in (key, house) order, the lanes splitting the comparisons (one LDS read serves all
 // of the wave's entries); the entry goes to sorted[rank] (sc1: read by the deciding block)
+// Block 0 ranks nothing when the grid has others: it takes its ticket first and builds the next
+// call's map beside the decision (as the deciding block it would run the map after the decision).
 __device__ void gq_rank(const uint4* s_e, int ncand, uint4* __restrict__ sorted) {
   const int lane = threadIdx.x & 63, wpb = (int)(blockDim.x >> 6);
-  const int nwv = (int)gridDim.x * wpb;
-  for (int e = (int)blockIdx.x * wpb + (int)(threadIdx.x >> 6); e < ncand; e += nwv) {  // (wave-uniform)
+  const int b0 = gridDim.x > 1 ? 1 : 0;
+  if ((int)blockIdx.x < b0) return;
+  const int nwv = ((int)gridDim.x - b0) * wpb;
+  for (int e = ((int)blockIdx.x - b0) * wpb + (int)(threadIdx.x >> 6); e < ncand; e += nwv) {  // (wave-uniform)
     const uint4 me = s_e[e];
     unsigned r = 0u;
 #pragma unroll 2
