@@ -2798,13 +2798,13 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
     }
   }
   if (ovf && !sharded) gq_exact(p, S, pmin, action, slab);
-  if (tid == 0) {
-    if (ovf) sel->fallbacks += 1;
+  if (tid == 0) {  // (counters as atomics: a += would hold the launch's end behind a load's round trip)
+    if (ovf) atomicAdd(&sel->fallbacks, 1u);
     if (ovf && sharded) sel->need_fb = 1u;
     sel->overflow = 0;       // (the next call starts clear)
     sel->wcount = 0u;
-    sel->calls += 1u;
-    if (!all && !ovf) sel->ncand_sum += (unsigned long long)ncand;
+    atomicAdd(&sel->calls, 1u);
+    if (!all && !ovf) atomicAdd(&sel->ncand_sum, (unsigned long long)ncand);
   }
 }
 
