@@ -2669,10 +2669,8 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
                           uint4* s_e, bool sharded, bool ovf0, bool all, int ncand, double win_tot, bool more_after,
                           bool in_lds) {
   __shared__ uint8_t s_tk[kGqCap];
-  __shared__ double s_w[16];
   __shared__ double s_tot;
-  __shared__ int s_k, s_first, s_ovf;
-  __shared__ unsigned long long s_bal[16];
+  __shared__ int s_k, s_ovf;
   __shared__ unsigned s_cnt[kWinCap];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, nth = blockDim.x;
   double pon[4];
@@ -2703,36 +2701,38 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
         }
       }
     }
-    if (tid == 0) { s_tot = win_tot; s_k = -1; }
     if (tid < kWinCap) s_cnt[tid] = 0u;
     __syncthreads();
-    for (int c0 = 0; c0 < ncand; c0 += nth) {
-      const int j = c0 + tid;
-      const double pj = j < ncand ? P_of(s_e[j].z) : 0.0;
-      double x = pj;
+    // the crossing: the first house whose running P reaches S, by wave 0 alone, 64 houses a wave
+    // prefix with the running total carried between them (r04: block-wide prefixes, four barriers a
+    // round); sums of integer-valued P are exact in any order
+    if (wv == 0) {
+      double tot = win_tot;
+      int kk = -1;
+      for (int c0 = 0; c0 < ncand; c0 += 64) {  // (wave-uniform)
+        const int j = c0 + lane;
+        const double pj = j < ncand ? P_of(s_e[j].z) : 0.0;
+        double x = pj;
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const double y = __shfl_up(x, off);
-        if (lane >= off) x += y;
+        for (int off = 1; off < 64; off <<= 1) {
+          const double y = __shfl_up(x, off);
+          if (lane >= off) x += y;
+        }
+        const unsigned long long bl = __ballot(j < ncand && !(tot + x < S));
+        if (bl) {
+          const int f = __ffsll((long long)bl) - 1;
+          kk = c0 + f;
+          tot = tot + (__shfl(x, f) - __shfl(pj, f));  // (exclusive: the P before house kk)
+          break;
+        }
+        tot = tot + __shfl(x, 63);  // the round's total (houses past ncand add 0)
       }
-      if (lane == 63) s_w[wv] = x;
-      __syncthreads();
-      for (int w = 0; w < wv; ++w) x += s_w[w];
-      const double tot = s_tot;
-      const unsigned long long bl = __ballot(j < ncand && !(tot + x < S));
-      if (lane == 0) s_bal[wv] = bl;
-      if (tid == 0) s_first = -1;
-      __syncthreads();
-      if (tid == 0)
-        for (int w = 0; w < 16; ++w)
-          if (s_bal[w]) { s_first = w * 64 + __ffsll((long long)s_bal[w]) - 1; break; }
-      __syncthreads();
-      const int f = s_first;
-      if (f >= 0 && tid == f) { s_k = c0 + f; s_tot = tot + (x - pj); }  // (exclusive: exact for integer P)
-      if (f < 0 && tid == nth - 1) s_tot = tot + x;                     // the round's total
-      __syncthreads();
-      if (f >= 0) break;
+      if (lane == 0) {
+        s_k = kk;
+        s_tot = tot;
+      }
     }
+    __syncthreads();
     const int k = s_k;  // >= 0: the crossing lies in bin b*, inside the window
     for (int j = tid; j < (k < 0 ? ncand : k); j += nth) s_tk[j] = 1;
     if (k < 0) {
