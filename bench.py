@@ -538,8 +538,8 @@ def main():
         launches, kern_ms = K, ev0.elapsed_time(ev1) / K
         bytes_launch = (BYTES_PER_HOUSE_STEP + GREEDY_EXTRA) * n_loc
         steps_launch = 1
-        kern = ("greedy tick: histogram select (k_gq_binsc, k_gq_compact, k_gq_select; codes, superbin "
-                "and predicted-band bin counts from the previous k_step_pipe's epilogue) + k_step_pipe")
+        kern = ("greedy tick: histogram select (k_gq_binsc, k_gq_finish; codes, superbin and predicted-band "
+                "bin counts from the previous k_step_pipe's epilogue) + k_step_pipe")
     else:
         # the actor rollout graph interleaves k_actor and k_step: time the actor alone
         K = 50

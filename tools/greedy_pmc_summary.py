@@ -1,9 +1,10 @@
 """Sum the HBM bytes of one greedy + step tick (config C3) from the rocprofv3 counter passes of
-tools/gpu_r04u.sh: per kernel the mean per-dispatch FETCH_SIZE (x 2: gfx950 counts half the bytes of
-wide coalesced reads, MI355X_MICROARCH.md) + WRITE_SIZE, summed over the tick's four kernels, and
-recorded in profiles/pmc_traffic.json under the greedy line's kernel name at 1,048,576 houses.
+tools/pmc_greedy.sh: per kernel the mean per-dispatch FETCH_SIZE (x 2: gfx950 counts half the bytes of
+wide coalesced reads, MI355X_MICROARCH.md) + WRITE_SIZE, summed over the tick's three kernels, and
+recorded in profiles/pmc_traffic.json under the greedy line's kernel name at 1,048,576 houses
+(round 5: the band's two launches after the step, tools/pmc_greedy.sh).
 
-    python tools/greedy_pmc_summary.py TAG gpurun_out/r04u
+    python tools/greedy_pmc_summary.py TAG gpurun_out/pmc_greedy
 """
 import csv
 import glob
@@ -14,9 +15,9 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ["k_step_pipe<2, 0, 0, true>", "k_gq_bins", "k_gq_compact", "k_gq_select"]
-LINE_KERNEL = ("greedy tick: histogram select (k_gq_bins, k_gq_compact, k_gq_select; "
-               "codes from the previous k_step_pipe's epilogue) + k_step_pipe")
+KERNELS = ["k_step_pipe<2, 0, 0, true>", "k_gq_binsc", "k_gq_finish"]
+LINE_KERNEL = ("greedy tick: histogram select (k_gq_binsc, k_gq_finish; codes, superbin and predicted-band "
+               "bin counts from the previous k_step_pipe's epilogue) + k_step_pipe")
 
 
 def main():
