@@ -166,13 +166,18 @@ __device__ __forceinline__ uint64_t gq_okey(double k) {
 // bins and the candidate window stays small.  The bin is monotone non-decreasing in k for ANY map,
 // range and scale >= 0 (keys outside the range clamp into the end cells), so a stale map only
 // costs window size, never exactness.
+// In float32: every step (the conversion of k, the subtraction of kmin, the product with the
+// positive scale, the truncations) is monotone non-decreasing in k, and a cell's bins end where the
+// next cell's begin, so the bin is monotone in the key — all the histogram select needs (the window
+// orders its houses by their exact float64 keys; NaN keys never come here).  Every producer of codes
+// uses this one function.  (Float64 arithmetic here cost the GQ step kernel's fp64 VALU pipe.)
 __device__ __forceinline__ int gq_bin(double k, double kmin, double scale, const uint32_t* map) {
-  const double u = (k - kmin) * scale;
-  const int c = u >= (double)(kGqCells - 1) ? kGqCells - 1 : (u > 0.0 ? (int)u : 0);
+  const float u = ((float)k - (float)kmin) * (float)scale;
+  const int c = u >= (float)(kGqCells - 1) ? kGqCells - 1 : (u > 0.0f ? (int)u : 0);
   const uint32_t m = map[c];
   const int w = (int)(m & 0xFFFFu);
-  const double f = (u - (double)c) * (double)w;
-  return (int)(m >> 16) + (f >= (double)(w - 1) ? w - 1 : (f > 0.0 ? (int)f : 0));
+  const float f = (u - (float)c) * (float)w;
+  return (int)(m >> 16) + (f >= (float)(w - 1) ? w - 1 : (f > 0.0f ? (int)f : 0));
 }
 // bins the key map spreads over for a cluster of n houses: about 8 houses per bin at most, so a
 // window of 64 bins holds a few hundred houses however small the cluster (a multiple of 64, >= 1024)
