@@ -2983,16 +2983,28 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint32_t* _
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only)
     if (!hit) {
       if (!all && !ovf) {
-        for (int e = tid; e < ncand; e += (int)blockDim.x) s_e[e] = gq_load_sc1(win + e);
+        // the window sorted in LDS by this block alone: a bitonic network over the next power of
+        // two (sentinels past ncand sort last), log2(P)(log2(P)+1)/2 barriers — bounded at any window
+        // size, where a rank by counting is quadratic in it
+        int np2 = 1;
+        while (np2 < ncand) np2 <<= 1;
+        for (int e = tid; e < np2; e += (int)blockDim.x)
+          s_e[e] = e < ncand ? gq_load_sc1(win + e) : make_uint4(~0u, ~0u, ~0u, ~0u);
         __syncthreads();
-        for (int e = tid; e < ncand; e += (int)blockDim.x) {
-          const uint4 me = s_e[e];
-          unsigned r = 0u;
-          for (int f = 0; f < ncand; ++f) r += gq_less(s_e[f], me) ? 1u : 0u;  // (one broadcast read a step)
-          if (r < (unsigned)kGqCap) gq_store_sc1(sorted + r, me);
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
+        for (int k2 = 2; k2 <= np2; k2 <<= 1)
+          for (int j = k2 >> 1; j > 0; j >>= 1) {
+            for (int i = tid; i < np2; i += (int)blockDim.x) {
+              const int l = i ^ j;
+              if (l > i) {
+                const uint4 a = s_e[i], b = s_e[l];
+                if ((i & k2) == 0 ? gq_less(b, a) : gq_less(a, b)) {
+                  s_e[i] = b;
+                  s_e[l] = a;
+                }
+              }
+            }
+            __syncthreads();
+          }
       }
       for (int e = tid; e < kGqBandOff + kGqCopies * kGqBandWords; e += (int)blockDim.x) hist[e] = 0u;
     }
@@ -3000,7 +3012,8 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint32_t* _
       sel->hit = 0;
       sel->band_valid = 0;
     }
-    gq_decide(p, sorted, S, pmin, sel, action, slab, s_e, false, ovf, all, ncand, win_tot, more_after, false);
+    // (a hit's window is in sorted[], ranked by every block; a miss's is in s_e, sorted here)
+    gq_decide(p, sorted, S, pmin, sel, action, slab, s_e, false, ovf, all, ncand, win_tot, more_after, !hit);
   }
   if (blockIdx.x == 0) {
     __syncthreads();  // (a decision by this block has finished with s_e)
