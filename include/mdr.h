@@ -166,8 +166,10 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           before the step and summed into the count allreduce; 0 = a ring-halo
  *                           send/recv per tick plus the count allreduce (MDR_OPT_HALO_OVERLAP applies)
  *   MDR_OPT_GQ_BAND         mdr_ctrl_greedy: 1 (default) = k_gq_binsc cuts the window from the step
- *                           epilogue's predicted band when it holds the crossing (no bins pass); 0 = the
- *                           bins pass every call (k_gq_bins)
+ *                           epilogue's predicted band when it holds the crossing (no bins pass) and
+ *                           k_gq_finish ranks and decides; 0 = the bins pass every call (k_gq_bins,
+ *                           k_gq_compact, k_gq_select: faster when the budget jumps across the cluster
+ *                           every call)
  *   MDR_OPT_ACTOR_GENERIC   1 = k_actor runs its generic form for the reference's default obs layout too
  *                           (0, default: that layout runs the form specialised for it, mdr_actor.hip DEF)
  *   MDR_OPT_WINDOW_THERMAL  k_step_window's per-tick thermal update: MDR_THERMAL_AFFINE (default)
