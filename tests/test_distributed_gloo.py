@@ -99,7 +99,7 @@ def test_sharded_env_equals_oracle(tmp_path, mode, n, extra, world):
     np.testing.assert_array_equal(msgs, ref)
 
 
-def _greedy_worker(rank, world, port, overrides, seed, T, out_dir):
+def _greedy_worker(rank, world, port, overrides, seed, T, out_dir, via_rollout=False):
     import torch.distributed as dist
 
     sys.path[:0] = [HERE, os.path.join(os.path.dirname(HERE), "marl-demandresponse_amd"), os.path.dirname(HERE)]
@@ -114,7 +114,14 @@ def _greedy_worker(rank, world, port, overrides, seed, T, out_dir):
     env = Environment(g.props_from_overrides(overrides), rng=random.Random(seed), rank=rank, world=world,
                       comm=GlooComm(), _shard_factory=OracleShard)
     acts, Ts = [], []
-    for _ in range(T):
+    if via_rollout:  # Environment.greedy_rollout (sharded: its per-tick loop), every tick's actions kept
+        import torch
+
+        buf = torch.empty((T, env.n_local), dtype=torch.uint8)
+        env.greedy_rollout(T, actions=buf)
+        acts = list(buf.numpy().copy())
+        Ts = [env.shard.host_state()["T"]] * T  # (only the last tick's state is compared)
+    for _ in range(0 if via_rollout else T):
         a = env.greedy_actions()
         acts.append(a.numpy().copy())
         env.step_tensor(a)
@@ -124,15 +131,16 @@ def _greedy_worker(rank, world, port, overrides, seed, T, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("n,world", [(75, 2), (3001, 2), (3001, 3)])
-def test_sharded_greedy_equals_oracle(tmp_path, n, world):
+@pytest.mark.parametrize("n,world,via_rollout", [(75, 2, False), (3001, 2, False), (3001, 3, False),
+                                                 (3001, 2, True)])
+def test_sharded_greedy_equals_oracle(tmp_path, n, world, via_rollout):
     """Sharded GreedyMyopic — the histogram form: the shards' superbin / bin histograms and key
     range allreduced, the candidate windows all-gathered, the same window decision on every rank,
     each keeps its slice (the all-gather form decides what the window cannot) — == the
-    single-process oracle's greedy + step."""
+    single-process oracle's greedy + step; also through Environment.greedy_rollout (via_rollout)."""
     T, seed = 6, 9
     overrides = {"cluster_prop.nb_agents": n, "power_grid_prop.signal_properties.mode": "sinusoidals"}
-    mp.start_processes(_greedy_worker, args=(world, _free_port(), overrides, seed, T, str(tmp_path)),
+    mp.start_processes(_greedy_worker, args=(world, _free_port(), overrides, seed, T, str(tmp_path), via_rollout),
                        nprocs=world, join=True, start_method="spawn")
     parts = sorted((np.load(tmp_path / f"rank{r}.npz") for r in range(world)), key=lambda p: int(p["lo"]))
     props = gu.props_from_overrides(overrides)
@@ -145,7 +153,8 @@ def test_sharded_greedy_equals_oracle(tmp_path, n, world):
         np.testing.assert_array_equal(got, ref, err_msg=f"t={t}")
         assert 0 < got.sum() < n or t > 0
         o, _ = ora.step(ref)
-        np.testing.assert_array_equal(np.concatenate([p["T"][t] for p in parts]), o["T"])
+        if not via_rollout or t == T - 1:
+            np.testing.assert_array_equal(np.concatenate([p["T"][t] for p in parts]), o["T"])
     assert all(int(p["fallbacks"]) == 0 for p in parts), [int(p["fallbacks"]) for p in parts]  # the window decided
 
 
