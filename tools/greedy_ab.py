@@ -1,7 +1,7 @@
 """A/B of the greedy select's launch forms on config C3 (1M houses, bench.py's population): HIP
 events around mdr_greedy_rollout calls of 100 ticks, alternating MDR_OPT_GQ_BAND 1 / 0 on one
 context (the drivers are computed before each call's first event).  Prints per-tick medians and the
-band's skip / miss counts.  Usage: python tools/greedy_ab.py [reps]"""
+band's skip / miss counts.  Usage: python tools/greedy_ab.py [reps] [step_tpw]"""
 import os
 import random
 import statistics
@@ -21,6 +21,8 @@ def main():
     n, K = 1 << 20, 100
     env = Environment(env_props(n), device="cuda:0", rng=random.Random(4), population="synthetic", seed=1234)
     sh = env.shard
+    if len(sys.argv) > 2:
+        sh.set_option("step_tpw", int(sys.argv[2]))
     act = torch.empty(n, dtype=torch.uint8, device="cuda:0")
     rew = torch.empty(n, dtype=torch.float64, device="cuda:0")
     env.greedy_rollout(150, actions=act, rewards=rew)  # warm: keys, map, band in steady state
