@@ -131,9 +131,16 @@ const char* mdr_build_id(void);
  * returns the number written */
 int mdr_abi_sizes(int64_t* out, int n);
 const char* mdr_last_error(void);
-/* Graph cache diagnostics: out[0..3] = cached rollout graphs, cached actor-rollout graphs,
- * hipGraphLaunch calls of mdr_rollout, of mdr_actor_rollout; returns the number written. */
+/* Graph cache diagnostics: out[0..5] = cached rollout graphs, cached actor-rollout graphs,
+ * hipGraphLaunch calls of mdr_rollout, of mdr_actor_rollout, captured graphs the memset guard
+ * walked (every capture fails with MDR_EHIP on a memset node), their nodes; returns the number
+ * written. */
 int mdr_graph_info(mdr_ctx* ctx, int64_t* out, int n);
+/* Diagnostic (synchronises, overwrites the count slabs): captures hipMemsetAsync of the count slabs
+ * to zero in this context and reports out[13] = {nodes, memset nodes, dst == the slabs, value,
+ * elementSize, width, height, pitch, bytes passed, non-zero 64-bit words after replays 1..3 (slabs
+ * pre-filled with 0xA5 before replays 1 and 2), non-zero words after the kernel zeroing}. */
+int mdr_graph_memset_probe(mdr_ctx* ctx, int64_t* out, int n, void* stream);
 int mdr_create(mdr_ctx** out, const mdr_config* cfg);
 int mdr_destroy(mdr_ctx* ctx);
 /* Bind the caller-owned SoA arrays (Environment.reset, environment.py:49-70). */
@@ -172,6 +179,11 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           every call)
  *   MDR_OPT_ACTOR_GENERIC   1 = k_actor runs its generic form for the reference's default obs layout too
  *                           (0, default: that layout runs the form specialised for it, mdr_actor.hip DEF)
+ *   MDR_OPT_ACTOR_FP32_FORM the fused actor's MDR_PREC_FP32 arithmetic: MDR_FP32_F16_SPLIT (default) =
+ *                           fp16 hi/lo operands on the fp16 MFMA, 3 products per term, power-of-two
+ *                           per-layer weight scales (activations must stay inside fp16's range:
+ *                           mdr_actor_status counts the tiles that did not); MDR_FP32_BF16_SPLIT3 =
+ *                           three-way bf16 operands, 6 products per term, no range limit
  *   MDR_OPT_WINDOW_THERMAL  k_step_window's per-tick thermal update: MDR_THERMAL_AFFINE (default)
  *                           = the reference's update as a per-house affine transition formed once
  *                           per window (4 FMAs per temperature per tick; ~1e-13 K per tick from the
@@ -180,7 +192,8 @@ int mdr_params_changed(mdr_ctx* ctx);
 enum { MDR_OPT_STEP_TPW = 1, MDR_OPT_FASTDIV = 2, MDR_OPT_WINDOW_PIPELINE = 3, MDR_OPT_SHARDED_OVERLAP = 4,
        MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7,
        MDR_OPT_HALO_OVERLAP = 9, MDR_OPT_ACTOR_GENERIC = 10, MDR_OPT_HALO_IN_COUNTS = 12,
-       MDR_OPT_GQ_BAND = 13 };
+       MDR_OPT_GQ_BAND = 13, MDR_OPT_ACTOR_FP32_FORM = 14 };
+enum { MDR_FP32_F16_SPLIT = 0, MDR_FP32_BF16_SPLIT3 = 1 };
 /* (8 was MDR_OPT_ACTOR_PINGPONG, a k_actor schedule measured slower and retired in r04: rejected) */
 enum { MDR_THERMAL_EXACT = 0, MDR_THERMAL_AFFINE = 1 };
 int mdr_set_option(mdr_ctx* ctx, int option, int64_t value);
@@ -364,7 +377,8 @@ int mdr_greedy_state(mdr_ctx* ctx, uint64_t* out);
  * then mdr_step of those actions with MDR_CTRL_GREEDY_KEYS (reward + t * rew_stride; common
  * penalty modes: + mdr_penalty_partials / mdr_reward_finalize)}; strides 0 = every tick overwrites.
  * Replaces the per-tick Python loop GreedyMyopic.get_action -> Environment.step
- * (greedy_myopic_controller.py:67-104, environment.py:86-106). */
+ * (greedy_myopic_controller.py:67-104, environment.py:86-106).  Single GPU only: a sharded context
+ * (world > 1) returns MDR_ESTATE (its decision needs the caller's collectives: mdr_gq_shard_*). */
 int mdr_greedy_rollout(mdr_ctx* ctx, int n, const mdr_tick* ticks, uint8_t* action, int64_t act_stride,
                        double* reward, int64_t rew_stride, double* p_out, void* stream);
 /* The predicted band (synchronises): out[4] = {mdr_ctrl_greedy calls that skipped the bins pass
@@ -413,8 +427,10 @@ int mdr_greedy_select(mdr_ctx* ctx, int64_t n, const double* key, const double* 
  * row on chip, runs both hidden layers on MFMA, softmax + Categorical sampling in fp32. */
 enum { MDR_PREC_BF16 = 1,   /* bf16 products, fp32 accumulate (~4e-3 relative) */
        MDR_PREC_BF16X3 = 3, /* split-bf16 (hi*hi + hi*lo + lo*hi), fp32 accumulate (~1e-5) */
-       MDR_PREC_FP32 = 6    /* three-way split-bf16 (24 significant bits, 6 products), fp32 accumulate:
-                               fp32-faithful (~1e-7), the reference Actor's precision */ };
+       MDR_PREC_FP32 = 6    /* fp32-faithful (~1e-7), the reference Actor's precision: fp16 hi/lo split
+                               (22 significand bits, 3 products on the fp16 MFMA) or, with
+                               MDR_OPT_ACTOR_FP32_FORM, three-way split-bf16 (24 bits, 6 products);
+                               fp32 accumulate.  The layer chain runs the three-way split. */ };
 
 typedef struct mdr_actor_spec {
   int32_t n_in;      /* obs features (= mdr_obs_spec.n_feat) */
@@ -441,6 +457,11 @@ typedef struct mdr_actor_net {
 } mdr_actor_net;
 int mdr_actor_load_net(mdr_ctx* ctx, const mdr_actor_net* net, const float* const* w, const float* const* b,
                        void* stream);
+/* Synchronises: out[0] = tiles of the fused fp16-split form (MDR_PREC_FP32, MDR_FP32_F16_SPLIT) that met
+ * a non-finite logit since the last call (an activation outside fp16's range; zeroed by this call),
+ * out[1] = the fused kernel's arithmetic (1 bf16, 3 bf16x3, 4 the fp16 split, 6 the three-way bf16
+ * split; 0 without an actor). */
+int mdr_actor_status(mdr_ctx* ctx, int64_t* out, int n, void* stream);
 /* 1 when the loaded actor runs the fused kernel for this obs layout, 0 when it runs the chain. */
 int mdr_actor_fused(mdr_ctx* ctx, const mdr_obs_spec* obs);
 /* One select_actions over the shard.  Outputs (device, any may be NULL): action u8 [n_local],

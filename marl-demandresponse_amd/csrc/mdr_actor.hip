@@ -15,9 +15,17 @@
 //   MDR_PREC_BF16X3 — every fp32 operand x is split x = hi + lo (hi = bf16(x), lo = bf16(x - hi))
 //                     and a·b ≈ ah·bh + ah·bl + al·bh, accumulated in fp32: ~1e-5 relative to the
 //                     fp32 reference (bf16 alone: ~4e-3).
-//   MDR_PREC_FP32   — three-way split x = hi + mid + lo (24 significant bits: the whole fp32
-//                     significand) and a·b ≈ ah·bh + ah·bm + am·bh + ah·bl + al·bh + am·bm (the dropped
-//                     terms are <= 2^-24 relative): fp32-faithful, 6 MFMAs per term.
+//   MDR_PREC_FP32   — fp32-faithful.  Default form (kernel PREC 4): an fp16 hi/lo split on
+//                     v_mfma_f32_16x16x32_f16 (the bf16 rate): x = hi + lo with hi = fp16(x), lo =
+//                     fp16(x - hi) — 11 + 11 significand bits against bf16's 8 + 8 — and a·b ≈ ah·bh +
+//                     ah·bl + al·bh (3 MFMAs per term, the dropped al·bl and lo's rounding <= 2^-22
+//                     relative).  fp16's range is kept by power-of-two per-layer weight scales chosen
+//                     at pack time (exact: they fold into the biases and the fp32 output layer), so
+//                     small weights' lo parts stay out of fp16 subnormals; an activation beyond fp16's
+//                     range makes a non-finite logit, which the kernel counts (ActorOut.ovf,
+//                     mdr_actor_status).  MDR_OPT_ACTOR_FP32_FORM = 1 (kernel PREC 6): the three-way
+//                     bf16 split x = hi + mid + lo (24 significant bits) and a·b ≈ ah·bh + ah·bm + am·bh
+//                     + ah·bl + al·bh + am·bm, 6 MFMAs per term, no range limit.
 //   MDR_PREC_BF16   — one bf16 product per term.
 // The biases enter as each layer's first accumulator (the MFMA's C operand); ReLU, the output
 // layer, softmax and sampling are fp32.
@@ -41,6 +49,10 @@
 namespace mdr {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+// the MFMA operand fragment of a kernel precision: fp16 for the fp16-split form (PREC 4), bf16 otherwise
+template <int PREC> struct FragOf { using T = bf16x8; };
+template <> struct FragOf<4> { using T = f16x8; };
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 
@@ -81,8 +93,29 @@ __device__ __forceinline__ void split8x3(const float* v, bf16x8& hi, bf16x8& mid
   }
 }
 
-// the packed fragments of one (row block, k-step): nf = 2 (hi, lo) or 3 (hi, mid, lo)
-__device__ __forceinline__ void pack_frags(const ActorDims& d, const float* v, unsigned char* base, int f, int lane) {
+__device__ __forceinline__ bool actor_uniform_feat(const ActorFold& fo, int fe) {
+  for (int u = 0; u < fo.nu; ++u)
+    if (fo.feat[u] == fe) return true;
+  return false;
+}
+
+// the packed fragments of one (row block, k-step): nf = 2 (hi, lo) or 3 (hi, mid, lo); d.f16: fp16
+// (hi, lo) of the values times the layer's scale (a power of two: exact)
+__device__ __forceinline__ void pack_frags(const ActorDims& d, const float* v, unsigned char* base, int f, int lane,
+                                           float scale = 1.f) {
+  if (d.f16) {
+    f16x8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float x = v[j] * scale;
+      h[j] = (_Float16)x;
+      l[j] = (_Float16)(x - (float)h[j]);  // (the difference is exact in fp32)
+    }
+    f16x8* o = reinterpret_cast<f16x8*>(base);
+    o[2 * f * 64 + lane] = h;
+    o[(2 * f + 1) * 64 + lane] = l;
+    return;
+  }
   bf16x8 hi, mid, lo;
   if (d.nf == 3) split8x3(v, hi, mid, lo);
   else split8(v, hi, lo);
@@ -96,11 +129,44 @@ __device__ __forceinline__ void pack_frags(const ActorDims& d, const float* v, u
   }
 }
 
-__global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const float* __restrict__ b1,
+__global__ void k_actor_pack(ActorDims d, ActorFold fo, const float* __restrict__ w1, const float* __restrict__ b1,
                              const float* __restrict__ w2, const float* __restrict__ b2,
                              const float* __restrict__ w3, const float* __restrict__ b3,
                              unsigned char* __restrict__ out) {
   const int nf1 = d.mb * d.ks1, nf2 = d.mb * kActorKS2;
+  // fp16 form: the per-layer power-of-two weight scales s1, s2 (every block reduces max |W| itself:
+  // ~23k floats).  s = 2^(kActorF16Exp - e) with max |W| < 2^e, so every scaled weight is below
+  // 2^kActorF16Exp and weights down to 2^-(kActorF16Exp + 11) of the largest keep their lo part out of
+  // fp16 subnormals.  The layer-1 accumulator is then s1 x the reference's, layer 2's s1 s2 x: b1 and
+  // b2 are packed scaled alike and W3 by 1 / (s1 s2), so the logits are the reference's.  Layer 2's
+  // fp16 operand is relu(layer 1) x s1: s1 is also capped so that max |b1| s1 < 2^kActorF16Bias, which
+  // leaves that operand inside fp16's range while sum |x| over the obs row stays below
+  // (65504 - 2^kActorF16Bias) / 2^kActorF16Exp (~3,800).
+  float s1 = 1.f, s2 = 1.f;
+  if (d.f16) {
+    __shared__ float red[3][256];
+    float m1 = 0.f, m2 = 0.f, mb = 0.f;
+    for (int i = threadIdx.x; i < d.h1 * d.n_in; i += blockDim.x)
+      if (!actor_uniform_feat(fo, i % d.n_in)) m1 = fmaxf(m1, fabsf(w1[i]));  // (folded columns: fp32)
+    for (int i = threadIdx.x; i < d.h2 * d.h1; i += blockDim.x) m2 = fmaxf(m2, fabsf(w2[i]));
+    for (int i = threadIdx.x; i < d.h1; i += blockDim.x) mb = fmaxf(mb, fabsf(b1[i]));
+    red[0][threadIdx.x] = m1;
+    red[1][threadIdx.x] = m2;
+    red[2][threadIdx.x] = mb;
+    __syncthreads();
+    for (int h = blockDim.x / 2; h > 0; h >>= 1) {
+      if ((int)threadIdx.x < h)
+        for (int k = 0; k < 3; ++k) red[k][threadIdx.x] = fmaxf(red[k][threadIdx.x], red[k][threadIdx.x + h]);
+      __syncthreads();
+    }
+    int e;
+    if (red[0][0] > 0.f && red[0][0] < INFINITY) { frexpf(red[0][0], &e); s1 = ldexpf(1.f, kActorF16Exp - e); }
+    if (red[2][0] > 0.f && red[2][0] < INFINITY) {
+      frexpf(red[2][0], &e);
+      s1 = fminf(s1, ldexpf(1.f, kActorF16Bias - e));
+    }
+    if (red[1][0] > 0.f && red[1][0] < INFINITY) { frexpf(red[1][0], &e); s2 = ldexpf(1.f, kActorF16Exp - e); }
+  }
   const int gid = blockIdx.x * blockDim.x + threadIdx.x;
   const int lane = gid & 63, f = gid >> 6;
   const int c = lane & 15, g = lane >> 4;
@@ -113,9 +179,9 @@ __global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const fl
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int fe = actor_feat_of_slot(d, 32 * ks + 8 * g + j);
-      v[j] = (row < d.h1 && fe >= 0) ? w1[row * d.n_in + fe] : 0.f;
+      v[j] = (row < d.h1 && fe >= 0 && !(d.f16 && actor_uniform_feat(fo, fe))) ? w1[row * d.n_in + fe] : 0.f;
     }
-    pack_frags(d, v, out + d.off_w1, f, lane);
+    pack_frags(d, v, out + d.off_w1, f, lane, s1);
   } else if (f < nf1 + nf2) {  // W2 [H2][H1], fragment (mb, q) in the accumulator k order
     const int f2 = f - nf1;
     const int q = f2 / d.mb, mb = f2 % d.mb;
@@ -125,21 +191,33 @@ __global__ void k_actor_pack(ActorDims d, const float* __restrict__ w1, const fl
       const int k = 32 * q + 16 * (j >> 2) + 4 * g + (j & 3);
       v[j] = (row < d.h2 && k < d.h1) ? w2[row * d.h1 + k] : 0.f;
     }
-    pack_frags(d, v, out + d.off_w2, f2, lane);
+    pack_frags(d, v, out + d.off_w2, f2, lane, s2);
   } else if (f == nf1 + nf2) {  // fp32 tail: b1, b2 [128], W3^T [128][2] (row-interleaved), b3 [2]
     float* t = reinterpret_cast<float*>(out + d.off_tail);
+    const float s12 = s1 * s2, r12 = 1.f / s12;  // (powers of two: exact)
     for (int i = lane; i < kActorRows; i += 64) {
-      t[i] = i < d.h1 ? b1[i] : 0.f;
-      t[kActorRows + i] = i < d.h2 ? b2[i] : 0.f;
-      for (int a = 0; a < kActorNA; ++a) t[2 * kActorRows + i * kActorNA + a] = i < d.h2 ? w3[a * d.h2 + i] : 0.f;
+      t[i] = i < d.h1 ? b1[i] * s1 : 0.f;
+      t[kActorRows + i] = i < d.h2 ? b2[i] * s12 : 0.f;
+      for (int a = 0; a < kActorNA; ++a) t[2 * kActorRows + i * kActorNA + a] = i < d.h2 ? w3[a * d.h2 + i] * r12 : 0.f;
     }
     if (lane < kActorNA) t[(2 + kActorNA) * kActorRows + lane] = b3[lane];
+    if (lane == 0) t[kActorTailS1] = s1;
+    int* tf = reinterpret_cast<int*>(t + kActorTailFold);  // the folded features (ActorFold)
+    if (lane == 0) {
+      tf[0] = d.f16 ? fo.nu : 0;
+      tf[1] = d.f16 ? fo.nu_own : 0;
+    }
+    for (int u = lane; u < kActorMaxU; u += 64) {
+      tf[2 + u] = fo.feat[u];
+      tf[2 + kActorMaxU + u] = fo.cf[u];
+    }
   }
 }
 
 // --------------------------------------------------------------------------------------- forward
-__device__ __forceinline__ bf16x8 lds_frag(const unsigned char* base, int frag, int lane) {
-  return reinterpret_cast<const bf16x8*>(base)[frag * 64 + lane];
+template <typename T = bf16x8>
+__device__ __forceinline__ T lds_frag(const unsigned char* base, int frag, int lane) {
+  return reinterpret_cast<const T*>(base)[frag * 64 + lane];
 }
 
 __device__ __forceinline__ float philox_u01f(uint64_t seed, uint64_t gid, uint64_t tick) {
@@ -166,18 +244,21 @@ __device__ __forceinline__ float relu(float x) {
 __device__ __forceinline__ f32x4 mfma16(const bf16x8& a, const bf16x8& b, const f32x4& c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
 }
+__device__ __forceinline__ f32x4 mfma16(const f16x8& a, const f16x8& b, const f32x4& c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
 
-// acc = C + A·B over the split operands (PREC 1: hi·hi; 3: + lo terms; 6: + mid terms), smallest
-// terms first; a[e] / b[e] = (hi, lo) or (hi, mid, lo)
-template <int PREC>
-__device__ __forceinline__ f32x4 mfma_split(const bf16x8* a, const bf16x8* b, f32x4 acc) {
+// acc = C + A·B over the split operands (PREC 1: hi·hi; 3 and 4: + lo terms; 6: + mid terms),
+// smallest terms first; a[e] / b[e] = (hi, lo) or (hi, mid, lo)
+template <int PREC, typename T>
+__device__ __forceinline__ f32x4 mfma_split(const T* a, const T* b, f32x4 acc) {
   if constexpr (PREC == 6) {
     acc = mfma16(a[1], b[1], acc);  // mid·mid
     acc = mfma16(a[2], b[0], acc);  // lo·hi
     acc = mfma16(a[0], b[2], acc);  // hi·lo
     acc = mfma16(a[1], b[0], acc);  // mid·hi
     acc = mfma16(a[0], b[1], acc);  // hi·mid
-  } else if constexpr (PREC == 3) {
+  } else if constexpr (PREC == 3 || PREC == 4) {
     acc = mfma16(a[1], b[0], acc);  // lo·hi
     acc = mfma16(a[0], b[1], acc);  // hi·lo
   }
@@ -211,9 +292,21 @@ __device__ __forceinline__ void split8_trunc(const float* v, bf16x8& hi, bf16x8&
   }
 }
 
-template <int PREC>
-__device__ __forceinline__ void split_operand(const float* v, bf16x8* s) {
-  if constexpr (PREC == 6) split8x3(v, s[0], s[1], s[2]);
+// The fp16-split form's activation split (PREC 4): hi = fp16(x) rounded to nearest, lo = fp16(x - hi)
+// (the difference is exact in fp32; |lo| <= 2^-11 |x|, its rounding <= 2^-23 |x|).
+__device__ __forceinline__ void split8_f16(const float* v, f16x8& hi, f16x8& lo) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const _Float16 h = (_Float16)v[j];
+    hi[j] = h;
+    lo[j] = (_Float16)sub_s(v[j], (float)h);
+  }
+}
+
+template <int PREC, typename T>
+__device__ __forceinline__ void split_operand(const float* v, T* s) {
+  if constexpr (PREC == 4) split8_f16(v, s[0], s[1]);
+  else if constexpr (PREC == 6) split8x3(v, s[0], s[1], s[2]);
   else if constexpr (PREC == 3) split8_trunc(v, s[0], s[1]);  // (r03's rounded-hi split: DESIGN.md §3.4)
   else {
 #pragma unroll
@@ -239,12 +332,14 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     o.hvac_state = 0; o.solar_state = 0; o.thermal_state = 0; o.msg_thermal = 0; o.msg_hvac = 0;
     o.comm_mode = MDR_COMM_RING; o.msg_w = 4; o.comm_table = nullptr; o.msg_all = nullptr;
     d.ring = 1; d.m4 = 4; d.msg_w = 4; d.n_own = 10; d.own4 = 12; d.rs = 20; d.nf = PREC == 6 ? 3 : 2;
+    d.f16 = PREC == 4;
   }
   static_assert(MB >= 1 && MB <= kActorMaxMB, "row blocks");
   static_assert(KS1 >= 1 && KS1 <= kActorMaxSlots / 32, "layer-1 k-steps");
-  constexpr int NS = PREC == 6 ? 3 : PREC == 3 ? 2 : 1;  // operand splits
+  constexpr int NS = PREC == 6 ? 3 : PREC == 3 || PREC == 4 ? 2 : 1;  // operand splits
   constexpr int NF = PREC == 6 ? 3 : 2;                   // packed fragments per (row block, k-step)
   constexpr int KS2 = (MB + 1) / 2;
+  using FragT = typename FragOf<PREC>::T;
   const uint64_t tick = tkp ? tkp->tick : tick0;
   // diagnostics (out.prof): shader cycles per phase, accumulated by lane 0 of every wave:
   // [0] weight fill + block barrier, [1] obs build, [2] prefetch issue + obs_out,
@@ -297,8 +392,26 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     obs_consts(p, o, p_dev ? *p_dev : o.p, s_cf, tid, nthr);
   }
   __syncthreads();
-  PSTAMP(0);
+  // fp16-split form: the layer-1 bias with the house-independent features' contribution (the obs
+  // rows hold 0 in their slots), s1 x (b1 + sum_u W1[i][f_u] cf_u) in fp32 from the raw weights
   const float* b1 = s_tail;
+  if (PREC == 4) {
+    float* s_b1 = reinterpret_cast<float*>(smem + d.lds_b1);
+    const float s1 = s_tail[kActorTailS1];
+    const int* tf = reinterpret_cast<const int*>(s_tail + kActorTailFold);
+    const int nu = tf[0];
+    for (int i = tid; i < kActorRows; i += nthr) {
+      float u = 0.f;
+      if (i < d.h1) {
+        const float* wr = d.w1raw + (size_t)i * d.n_in;
+        for (int k = 0; k < nu; ++k) u = fmaf(wr[tf[2 + k]], s_cf[tf[2 + kActorMaxU + k]], u);
+      }
+      s_b1[i] = s_tail[i] + s1 * u;
+    }
+    __syncthreads();
+    b1 = s_b1;
+  }
+  PSTAMP(0);
   const float* b2 = s_tail + kActorRows;
   const float* w3 = s_tail + 2 * kActorRows;
   const float* b3 = s_tail + (2 + kActorNA) * kActorRows;
@@ -354,9 +467,9 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
       const int t = s - lo;
       if (ring) {
         msg_from_regs(p, o, rg, s_cf, row, dv);
-        if (t >= 0 && t < nb) row_scalars(p, o, rg, s_cf, row + d.m4, dv);
+        if (t >= 0 && t < nb) row_scalars(p, o, rg, s_cf, row + d.m4, dv, PREC == 4);
       } else {
-        row_scalars(p, o, rg, s_cf, row, dv);
+        row_scalars(p, o, rg, s_cf, row, dv, PREC == 4);
       }
       if (t >= 0 && t < nb) {
         w_hw[t] = rg.w;
@@ -366,6 +479,7 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
   };
   // ---- the stages of a tile (build, X, Y: the comment above k_actor)
   f32x2 zz[2];  // the tile's two logits per column block (partial over this lane's rows) between X and Y
+  float zsc = 1.f;  // (PREC 4) their scale back: 1 / the tile's layer-1 input scale
   // build: the tile's LDS rows from the prefetched sources (+ the table topologies' gathers)
   auto stage_build = [&](uint32_t tl) {
     const uint32_t b0 = tl * 32u;
@@ -405,7 +519,13 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
       for (int q = lane; q < nb * F; q += 64) {
         const int rr = q / F, f = q - rr * F;
         const int s = f < d.n_own ? f : d.own4 + ((f - d.n_own) / M) * d.m4 + (f - d.n_own) % M;
-        dst[q] = w_row[rr * RS + actor_slot_off(d, s)];
+        float v = w_row[rr * RS + actor_slot_off(d, s)];
+        if (PREC == 4 && f < d.n_own) {  // (the folded own features' slots hold 0: their values)
+          const int* tf = reinterpret_cast<const int*>(s_tail + kActorTailFold);
+          for (int k = 0; k < tf[1]; ++k)
+            if (tf[2 + k] == f) v = s_cf[tf[2 + kActorMaxU + k]];
+        }
+        dst[q] = v;
       }
       // (these stores' data registers are reused below: the wait here keeps the compiler's wait-count
       // pass from putting one in front of layer 1 on the paths without obs rows)
@@ -422,9 +542,18 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     // fragment ks * MB + mb) are read from LDS two steps ahead (a ring of three), so the MFMAs of one
     // wave do not wait out the LDS latency.
     constexpr int PF = 2;  // prefetch distance (steps)
-    bf16x8 hs[KS2][2][NS];
-    {
-      bf16x8 xs[KS1][2][NS];
+    FragT hs[KS2][2][NS];
+    // fp16-split form (PREC 4): layer 2's operand relu(layer 1) must stay inside fp16's range.  The
+    // first pass tracks its maximum (on the bits: non-negative floats order as integers); when a lane
+    // holds a value >= 2^15 (ballot: rare) the tile's layer 1 runs again with its inputs and bias
+    // scaled by sig = 2^-k (exact), which brings the maximum below 2^15, and stage Y scales the logits
+    // back by 1 / sig.  A second pass still out of range, or a non-finite value (an obs feature
+    // beyond fp16), is counted in out.ovf (mdr_actor_status).
+    float sig = 1.f;
+#pragma unroll 1
+    for (int attempt = 0; attempt < (PREC == 4 ? 2 : 1); ++attempt) {
+      uint32_t mbits = 0u;
+      FragT xs[KS1][2][NS];
 #pragma unroll
       for (int ks = 0; ks < KS1; ++ks)
 #pragma unroll
@@ -436,11 +565,14 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
             const float4 x = *reinterpret_cast<const float4*>(w_row + a);
             xv[4 * e] = x.x; xv[4 * e + 1] = x.y; xv[4 * e + 2] = x.z; xv[4 * e + 3] = x.w;
           }
+          if (PREC == 4 && attempt)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) xv[j] *= sig;
           split_operand<PREC>(xv, xs[ks][cb]);
         }
       constexpr int total = KS1 * MB;
-      auto frag1 = [&](int s, int e) { return lds_frag(s_w1, NF * ((s % KS1) * MB + s / KS1) + e, lane); };
-      bf16x8 ring[PF + 1][NS];
+      auto frag1 = [&](int s, int e) { return lds_frag<FragT>(s_w1, NF * ((s % KS1) * MB + s / KS1) + e, lane); };
+      FragT ring[PF + 1][NS];
 #pragma unroll
       for (int q = 0; q < PF; ++q)
 #pragma unroll
@@ -452,10 +584,11 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
         if (st + PF < total)
 #pragma unroll
           for (int e = 0; e < NS; ++e) ring[(st + PF) % (PF + 1)][e] = frag1(st + PF, e);
-        const bf16x8* as = ring[st % (PF + 1)];
+        const FragT* as = ring[st % (PF + 1)];
         f32x4* a1 = acc1[mb & 1];
         if (ks == 0) {
-          const f32x4 bias = *reinterpret_cast<const f32x4*>(b1 + kActorRB * mb + 4 * g);
+          f32x4 bias = *reinterpret_cast<const f32x4*>(b1 + kActorRB * mb + 4 * g);
+          if (PREC == 4 && attempt) bias *= sig;
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) a1[cb] = mfma_split<PREC>(as, xs[ks][cb], bias);
         } else {
@@ -473,11 +606,26 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
               v[j] = relu(acc1[0][cb][j]);
               v[4 + j] = pair ? relu(acc1[1][cb][j]) : 0.f;
             }
+            if (PREC == 4)
+#pragma unroll
+              for (int j = 0; j < 8; j += 2)
+                mbits = max(mbits, max(__float_as_uint(v[j]), __float_as_uint(v[j + 1])));
             split_operand<PREC>(v, hs[q][cb]);
           }
         }
       }
+      if constexpr (PREC == 4) {
+        if (!__ballot(mbits >= 0x47000000u)) break;  // (every value < 2^15 = 32768.0f)
+        uint32_t m = mbits;
+        for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+        if (attempt || m >= 0x7f800000u) {
+          if (lane == 0 && out.ovf) atomicAdd(out.ovf, 1u);
+          break;
+        }
+        sig = ldexpf(1.f, 14 - ((int)(m >> 23) - 127));  // max x sig < 2^15
+      }
     }
+    zsc = PREC == 4 ? 1.f / sig : 1.f;  // (a power of two: exact)
     PSTAMP(3);
 
     // ---- layer 2 (acc2 = b2 + W2 · relu(H1)) fused with the output layer, row block by row block:
@@ -485,8 +633,8 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     // FMAs in block / row order) while the next block's MFMAs run
     {
       constexpr int TOT = KS2 * MB;
-      auto frag2 = [&](int s, int e) { return lds_frag(s_w2, NF * ((s % KS2) * MB + s / KS2) + e, lane); };
-      bf16x8 ring[PF + 1][NS];
+      auto frag2 = [&](int s, int e) { return lds_frag<FragT>(s_w2, NF * ((s % KS2) * MB + s / KS2) + e, lane); };
+      FragT ring[PF + 1][NS];
 #pragma unroll
       for (int q = 0; q < PF; ++q)
 #pragma unroll
@@ -500,7 +648,7 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
         if (st + PF < TOT)
 #pragma unroll
           for (int e = 0; e < NS; ++e) ring[(st + PF) % (PF + 1)][e] = frag2(st + PF, e);
-        const bf16x8* as = ring[st % (PF + 1)];
+        const FragT* as = ring[st % (PF + 1)];
         if (q == 0) {
           const f32x4 bias = *reinterpret_cast<const f32x4*>(b2 + kActorRB * mb + 4 * g);
 #pragma unroll
@@ -536,6 +684,9 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     float z[2][kActorNA];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) { z[cb][0] = zz[cb].x; z[cb][1] = zz[cb].y; }
+    if (PREC == 4)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) { z[cb][0] *= zsc; z[cb][1] *= zsc; }
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -570,6 +721,10 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     const int act = u < p0 ? 0 : 1;
     const float pa = act ? p1 : p0;
     const bool writer = valid && lane < 32;
+    if (PREC == 4 && out.ovf) {  // a non-finite logit (mdr_actor_status)
+      const bool bad = writer && !(__builtin_isfinite(z0) && __builtin_isfinite(z1));
+      if (__ballot(bad) && lane == 0) atomicAdd(out.ovf, 1u);
+    }
     if (writer) {
       if (out.probs) *reinterpret_cast<float2*>(out.probs + 2 * (size_t)i) = make_float2(p0, p1);
       if (out.action) out.action[i] = (uint8_t)act;
@@ -740,9 +895,11 @@ template __global__ void k_dense<6>(const float*, int, int, int64_t, const float
 #define MDR_INST_ACTOR_SHAPE(MB, KS) \
   MDR_INST_ACTOR(1, false, MB, KS) \
   MDR_INST_ACTOR(3, false, MB, KS) \
+  MDR_INST_ACTOR(4, false, MB, KS) \
   MDR_INST_ACTOR(6, false, MB, KS) \
   MDR_INST_ACTOR(1, true, MB, KS)  \
   MDR_INST_ACTOR(3, true, MB, KS)  \
+  MDR_INST_ACTOR(4, true, MB, KS)  \
   MDR_INST_ACTOR(6, true, MB, KS)
 MDR_INST_ACTOR_SHAPE(7, 2)
 MDR_INST_ACTOR_SHAPE(7, 3)
@@ -752,8 +909,9 @@ MDR_INST_ACTOR_SHAPE(8, 3)
 MDR_INST_ACTOR_SHAPE(8, 4)
 #define MDR_INST_ACTOR_DEF(MB)                                                                      \
   MDR_INST_ACTOR_D(1, false, MB, 2, true) MDR_INST_ACTOR_D(3, false, MB, 2, true)                   \
-  MDR_INST_ACTOR_D(6, false, MB, 2, true) MDR_INST_ACTOR_D(1, true, MB, 2, true)                    \
-  MDR_INST_ACTOR_D(3, true, MB, 2, true) MDR_INST_ACTOR_D(6, true, MB, 2, true)
+  MDR_INST_ACTOR_D(4, false, MB, 2, true) MDR_INST_ACTOR_D(6, false, MB, 2, true)                   \
+  MDR_INST_ACTOR_D(1, true, MB, 2, true) MDR_INST_ACTOR_D(3, true, MB, 2, true)                     \
+  MDR_INST_ACTOR_D(4, true, MB, 2, true) MDR_INST_ACTOR_D(6, true, MB, 2, true)
 MDR_INST_ACTOR_DEF(7)
 MDR_INST_ACTOR_DEF(8)
 

@@ -90,6 +90,7 @@ struct mdr_ctx {
   bool greedy_sort = false;              // MDR_OPT_GREEDY_SORT: the full-sort greedy form only
   bool force_halo = false;               // MDR_OPT_FORCE_HALO: sharded actor halo exchange at world 1
   bool actor_generic = false;            // MDR_OPT_ACTOR_GENERIC: no default-layout k_actor form
+  bool actor_fp32_bf16 = false;          // MDR_OPT_ACTOR_FP32_FORM: the three-way bf16 fp32 form (kernel PREC 6)
   bool halo_overlap = true;              // MDR_OPT_HALO_OVERLAP: sharded actor tick, halo beside the interior tiles
   bool halo_in_counts = true;            // MDR_OPT_HALO_IN_COUNTS: the next tick's ring halo rides in the count allreduce
   unsigned long long* d_c5 = nullptr;    // that path's ring of 3 x [count slab | world x halo rows]
@@ -132,6 +133,8 @@ struct mdr_ctx {
   int gq_parts_cap = 0;                  // g_part capacity in (min, max) pairs
   bool gq_keys_ready = false;            // keys + superbin histogram of the current state are in place
   bool gq_hist_dirty = false;            // a producer added counts to g_hist that no select has consumed
+  bool gq_slab_zeroed = false;           // the codes' producer zeroed the slab the decisions count into
+                                         // (not when its step counted a lookahead there)
   bool gq_band = true;                   // MDR_OPT_GQ_BAND: k_gq_binsc (the predicted band) vs k_gq_bins
   int gq_nparts = 0;                     //   (from the last step's epilogue: its grid's partials)
   // multi-GPU
@@ -174,6 +177,8 @@ struct mdr_ctx {
   size_t halo_bytes = 0;
   std::map<std::vector<int64_t>, hipGraphExec_t> actor_graphs;
   int64_t graph_launches[2] = {0, 0};  // hipGraphLaunch calls: rollout graphs, actor rollout graphs
+  int64_t graphs_guarded = 0;            // captured graphs the memset guard walked (graph_memset_guard)
+  int64_t graph_nodes_checked = 0;       //   and their nodes
   // interpolated base power (row a10): grid | table | capacities
   double* d_interp = nullptr;
   size_t interp_bytes = 0;
@@ -344,8 +349,12 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
     }
 #undef MDR_LAUNCH_PIPE
     LAUNCH_CHECK("k_step_pipe");
-    if (gq && !epi) return launch_gq_keys(c, st, nxt);
-    if (epi) c->gq_nparts = (int)nb;
+    // (a lookahead's counts are in nxt: k_gq_keys leaves them, mdr_ctrl_greedy zeroes the slab)
+    if (gq && !epi) return launch_gq_keys(c, st, lookahead ? nullptr : nxt);
+    if (epi) {
+      c->gq_nparts = (int)nb;
+      c->gq_slab_zeroed = true;  // (the GQ epilogue zeroes its next slab; epi implies no lookahead)
+    }
     return MDR_OK;
   }
   if (c->fastdiv) {
@@ -357,7 +366,7 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
   }
 #undef MDR_LAUNCH_STEP
   LAUNCH_CHECK("k_step");
-  if (gq) return launch_gq_keys(c, st, nxt);
+  if (gq) return launch_gq_keys(c, st, lookahead ? nullptr : nxt);
   return MDR_OK;
 }
 
@@ -409,11 +418,79 @@ const char* mdr_last_error(void) { return g_err.c_str(); }
 
 int mdr_graph_info(mdr_ctx* c, int64_t* out, int n) {
   if (!c || !out || n < 0) return fail(MDR_EARG, "mdr_graph_info: bad argument");
-  const int64_t v[4] = {(int64_t)c->graphs.size(), (int64_t)c->actor_graphs.size(), c->graph_launches[0],
-                        c->graph_launches[1]};
+  const int64_t v[6] = {(int64_t)c->graphs.size(), (int64_t)c->actor_graphs.size(), c->graph_launches[0],
+                        c->graph_launches[1], c->graphs_guarded, c->graph_nodes_checked};
   int k = 0;
-  for (; k < n && k < 4; ++k) out[k] = v[k];
+  for (; k < n && k < 6; ++k) out[k] = v[k];
   return k;
+}
+
+// the parameters of a memset node captured in this library's context, against
+// what was passed, and what its replays leave in the slabs.  Captures hipMemsetAsync(d_slab, 0, all
+// slabs) exactly as the r04 rollouts did, outside capture_graph (whose guard refuses memset nodes).
+// out[0..12] = {nodes, memset nodes, dst == d_slab, value, elementSize, width, height, pitch,
+// bytes passed, non-zero 64-bit words after replay 1 (slabs pre-filled with 0xA5), after replay 2
+// (re-filled), after replay 3 (not re-filled), non-zero words after a kernel (k_zero_u64) zeroing}
+int mdr_graph_memset_probe(mdr_ctx* c, int64_t* out, int n, void* stream) {
+  drop_begun(c);
+  if (!c || !out || n < 13) return fail(MDR_EARG, "mdr_graph_memset_probe: need out[13]");
+  c->counts_ready = false;  // (the slabs are overwritten)
+  for (int k = 0; k < n; ++k) out[k] = 0;
+  hipStream_t st = S(stream);
+  HIP_TRY(hipStreamSynchronize(st));
+  if (!c->cap_stream) HIP_TRY(hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking));
+  const size_t bytes = (size_t)kSlabs * c->slab_len * sizeof(unsigned long long);
+  const size_t words = bytes / 8;
+  hipGraph_t g;
+  HIP_TRY(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal));
+  hipError_t e = hipMemsetAsync(c->d_slab, 0, bytes, c->cap_stream);
+  hipError_t e2 = hipStreamEndCapture(c->cap_stream, &g);
+  if (e != hipSuccess || e2 != hipSuccess) return fail(MDR_EHIP, "memset probe: capture failed");
+  size_t nn = 0;
+  hipGraphGetNodes(g, nullptr, &nn);
+  std::vector<hipGraphNode_t> nodes(nn);
+  if (nn) hipGraphGetNodes(g, nodes.data(), &nn);
+  out[0] = (int64_t)nn;
+  for (size_t i = 0; i < nn; ++i) {
+    hipGraphNodeType t;
+    if (hipGraphNodeGetType(nodes[i], &t) != hipSuccess || t != hipGraphNodeTypeMemset) continue;
+    out[1] += 1;
+    hipMemsetParams mp{};
+    if (hipGraphMemsetNodeGetParams(nodes[i], &mp) == hipSuccess) {
+      out[2] = mp.dst == (void*)c->d_slab;
+      out[3] = (int64_t)mp.value;
+      out[4] = (int64_t)mp.elementSize;
+      out[5] = (int64_t)mp.width;
+      out[6] = (int64_t)mp.height;
+      out[7] = (int64_t)mp.pitch;
+    }
+  }
+  out[8] = (int64_t)bytes;
+  hipGraphExec_t ex;
+  e = hipGraphInstantiate(&ex, g, nullptr, nullptr, 0);
+  hipGraphDestroy(g);
+  if (e != hipSuccess) return fail(MDR_EHIP, std::string("memset probe: instantiate: ") + hipGetErrorString(e));
+  std::vector<unsigned long long> h(words);
+  auto nonzero = [&](int64_t* o) -> int {
+    HIP_TRY(hipStreamSynchronize(st));
+    HIP_TRY(hipMemcpy(h.data(), c->d_slab, bytes, hipMemcpyDeviceToHost));
+    int64_t z = 0;
+    for (size_t i = 0; i < words; ++i) z += h[i] != 0ull;
+    *o = z;
+    return MDR_OK;
+  };
+  int rc = MDR_OK;
+  for (int r = 0; r < 3 && !rc; ++r) {
+    if (r < 2) {
+      hipMemsetAsync(c->d_slab, 0xA5, bytes, st);
+    }
+    if (hipGraphLaunch(ex, st) != hipSuccess) rc = fail(MDR_EHIP, "memset probe: launch");
+    else rc = nonzero(&out[9 + r]);
+  }
+  hipGraphExecDestroy(ex);
+  if (rc) return rc;
+  if ((rc = zero_slabs(c, st))) return rc;
+  return nonzero(&out[12]);
 }
 
 int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
@@ -460,7 +537,8 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
     return cleanup(fail(MDR_EHIP, "tables copy"));
   k.q_on = c->d_tables;
   k.p_on = c->d_tables + MDR_MAX_CAP;
-  if (hipMalloc(&c->d_flags, 16) != hipSuccess) return cleanup(fail(MDR_ENOMEM, "flags"));
+  if (hipMalloc(&c->d_flags, 16) != hipSuccess || hipMemset(c->d_flags, 0, 16) != hipSuccess)
+    return cleanup(fail(MDR_ENOMEM, "flags"));  // [0] params_bad, [1] the actor's fp16-range count
   if (hipMalloc(&c->d_tickets, kTicketWords * sizeof(unsigned)) != hipSuccess ||
       hipMemset(c->d_tickets, 0, kTicketWords * sizeof(unsigned)) != hipSuccess)
     return cleanup(fail(MDR_ENOMEM, "tickets"));
@@ -581,6 +659,12 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_HALO_IN_COUNTS: c->halo_in_counts = value != 0; break;
     case MDR_OPT_GQ_BAND: c->gq_band = value != 0; break;
     case MDR_OPT_ACTOR_GENERIC: c->actor_generic = value != 0; break;
+    case MDR_OPT_ACTOR_FP32_FORM:
+      if (value != MDR_FP32_F16_SPLIT && value != MDR_FP32_BF16_SPLIT3)
+        return fail(MDR_EARG, "mdr_set_option: ACTOR_FP32_FORM must be MDR_FP32_F16_SPLIT or MDR_FP32_BF16_SPLIT3");
+      c->actor_fp32_bf16 = value == MDR_FP32_BF16_SPLIT3;
+      c->actor_key.clear();  // (packed again for the form)
+      break;
     case MDR_OPT_WINDOW_THERMAL:
       if (value != MDR_THERMAL_EXACT && value != MDR_THERMAL_AFFINE)
         return fail(MDR_EARG, "mdr_set_option: WINDOW_THERMAL must be MDR_THERMAL_EXACT or _AFFINE");
@@ -731,6 +815,25 @@ static int stage_ticks(mdr_ctx* c, int n, const mdr_tick* ticks, hipStream_t st)
   return stage_recs(ticks, n, c->d_ticks, st);
 }
 
+// every node of a captured graph must be a kernel (the launch sequences hold nothing else); a memset
+// node fails the capture with MDR_EHIP.  Counts the graphs checked (mdr_graph_info[4]).
+static int graph_memset_guard(mdr_ctx* c, hipGraph_t g) {
+  size_t nn = 0;
+  HIP_TRY(hipGraphGetNodes(g, nullptr, &nn));
+  std::vector<hipGraphNode_t> nodes(nn);
+  if (nn) HIP_TRY(hipGraphGetNodes(g, nodes.data(), &nn));
+  for (size_t i = 0; i < nn; ++i) {
+    hipGraphNodeType t;
+    HIP_TRY(hipGraphNodeGetType(nodes[i], &t));
+    if (t == hipGraphNodeTypeMemset)
+      return fail(MDR_EHIP, "capture: graph node " + std::to_string(i) + " of " + std::to_string(nn) +
+                                " is a memset (captured launch sequences must zero with kernels)");
+  }
+  c->graphs_guarded += 1;
+  c->graph_nodes_checked += (int64_t)nn;
+  return MDR_OK;
+}
+
 // Capture a launch sequence into an executable graph on the context's own capture stream (the
 // capture executes nothing), so the graph can then be launched on ANY caller stream — the null
 // stream included — with no cross-stream synchronisation around each replay.
@@ -743,6 +846,12 @@ static int capture_graph(mdr_ctx* c, F&& launches, hipGraphExec_t* out) {
   hipError_t e = hipStreamEndCapture(c->cap_stream, &g);
   if (rc) return rc;
   if (e != hipSuccess) return fail(MDR_EHIP, std::string("capture: ") + hipGetErrorString(e));
+  // memset guard: a captured hipMemsetAsync node left non-zero words in the count slabs on every
+  // replay after the first (zero_slabs) — no captured graph may contain one
+  if (int grc = graph_memset_guard(c, g)) {
+    hipGraphDestroy(g);
+    return grc;
+  }
   e = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
   hipGraphDestroy(g);
   if (e != hipSuccess) return fail(MDR_EHIP, std::string("instantiate: ") + hipGetErrorString(e));
@@ -1364,6 +1473,7 @@ int launch_gq_keys(mdr_ctx* c, hipStream_t st, unsigned long long* slab) {
                      c->g_sel, c->g_map, slab);
   LAUNCH_CHECK("k_gq_keys");
   c->gq_nparts = kGqParts;
+  c->gq_slab_zeroed = slab != nullptr;
   return MDR_OK;
 }
 
@@ -1387,8 +1497,13 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   if (c->kp.n_cap <= 4 && !c->greedy_sort) {
     // histogram select (mdr_kernels.hip k_gq_*): no sort of the whole cluster, no host
     // synchronisation; k_gq_select decides exactly what the candidate window cannot
-    if (!keys_ready)
+    if (!keys_ready) {
       if (int rc2 = launch_gq_keys(c, st, slab)) return rc2;
+    } else if (!c->gq_slab_zeroed) {
+      // the producing step counted a lookahead into this slab: the decisions replace those counts
+      hipLaunchKernelGGL(k_zero_u64, dim3(1), dim3(256), 0, st, slab, (int64_t)c->slab_len);
+      LAUNCH_CHECK("k_zero_u64 (decision slab)");
+    }
     // the slab was zeroed by the codes' producer (k_gq_keys, or the GQ step: its next slab is this)
     const int nstage = (n + kGqStage - 1) / kGqStage;
     if (c->gq_band) {
@@ -1474,6 +1589,8 @@ int mdr_greedy_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, uint8_t* action
   if (!c || (n > 0 && (!ticks || !action || !reward))) return fail(MDR_EARG, "mdr_greedy_rollout: null argument");
   if (n < 0 || act_stride < 0 || rew_stride < 0) return fail(MDR_EARG, "mdr_greedy_rollout: negative size");
   if (!c->bound) return fail(MDR_ESTATE, "mdr_greedy_rollout: context not bound");
+  if (c->world > 1)  // (a shard-local decision and step would use shard-local counts: per-tick loop)
+    return fail(MDR_ESTATE, "mdr_greedy_rollout: single-GPU only (sharded contexts: the per-tick greedy + step loop)");
   hipStream_t st = S(stream);
   for (int t = 0; t < n; ++t) {
     uint8_t* a = action + (int64_t)t * act_stride;
@@ -1880,12 +1997,20 @@ int align16(int x) { return (x + 15) & ~15; }
 
 // Packed-image offsets, the obs row's slot layout and the LDS plan of k_actor for `nw` waves per
 // block (mdr_actor.h ActorDims).
-ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw) {
+// the fused kernel's PREC for the loaded actor: 1 bf16, 3 bf16x3, fp32: 4 (the fp16 split, default) or
+// 6 (the three-way bf16 split, MDR_OPT_ACTOR_FP32_FORM)
+int actor_kprec(const mdr_ctx* c) {
+  const int p = c->actor.precision;
+  return p == MDR_PREC_BF16 ? 1 : p == MDR_PREC_FP32 ? (c->actor_fp32_bf16 ? 6 : 4) : 3;
+}
+
+ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw, int kprec) {
   ActorDims d{};
   d.n_in = a.n_in; d.h1 = a.h1; d.h2 = a.h2; d.n_act = a.n_act;
   const int mbn = (std::max(a.h1, a.h2) + kActorRB - 1) / kActorRB;
   d.mb = mbn <= 7 ? 7 : 8;  // (the kernel's instantiations)
-  d.nf = a.precision == MDR_PREC_FP32 ? 3 : 2;
+  d.nf = kprec == 6 ? 3 : 2;
+  d.f16 = kprec == 4;
   const int K = sp->n_comm, M = mdr_msg_width(sp);
   d.n_comm = K;
   d.msg_w = M;
@@ -1903,10 +2028,12 @@ ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw) 
   d.off_w1 = 0;
   d.off_w2 = d.mb * d.ks1 * d.nf * 1024;
   d.off_tail = d.off_w2 + d.mb * kActorKS2 * d.nf * 1024;
-  d.off_end = align16(d.off_tail + ((2 + kActorNA) * kActorRows + kActorNA) * 4);
+  d.off_end = align16(d.off_tail + kActorTailEnd * 4);
   d.lds_cf = d.off_end;
   d.lds_hist = d.lds_cf + align16(kObsConst * 4);
-  d.lds_wave = d.lds_hist + MDR_MAX_CAP * 4;
+  d.lds_b1 = d.lds_hist + MDR_MAX_CAP * 4;
+  d.lds_wave = d.lds_b1 + (d.f16 ? kActorRows * 4 : 0);
+
   d.w_zero = align16(d.nrows * rs * 4);
   d.w_hw = d.w_zero + 16;
   d.w_cls = d.w_hw + 32 * 4;
@@ -1924,12 +2051,13 @@ bool actor_def_layout(const mdr_ctx* c, const mdr_obs_spec* sp, const ActorDims&
 }
 
 int actor_plan(const mdr_ctx* c, const mdr_obs_spec* sp, ActorDims* d, int* nw) {
-  *d = actor_layout(c->actor, sp, 1);
+  const int prec = actor_kprec(c);
+  *d = actor_layout(c->actor, sp, 1, prec);
   if (d->n_own < 0 || d->nslot > kActorMaxSlots)
     return fail(MDR_EARG, "mdr_actor: obs row wider than the actor's 128 feature slots");
-  const int prec = c->actor.precision == MDR_PREC_FP32 ? 6 : c->actor.precision == MDR_PREC_BF16 ? 1 : 3;
   for (int w = actor_max_waves(prec, actor_def_layout(c, sp, *d)); w >= 1; --w) {
-    *d = actor_layout(c->actor, sp, w);
+    *d = actor_layout(c->actor, sp, w, prec);
+    d->w1raw = c->d_actor_raw;
     if (d->lds_total <= 160 * 1024) { *nw = w; return MDR_OK; }
   }
   return fail(MDR_EARG, "mdr_actor: weights + obs rows exceed the 160 KiB LDS of a CU");
@@ -1989,7 +2117,7 @@ int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
   int nw = 0;
   if (int rc = actor_plan(c, sp, &d, &nw)) return rc;
   const std::vector<int> key{d.n_own, d.own4, d.msg_w, d.m4, d.n_comm, d.mb, d.ks1, d.nf, d.ring, d.lo,
-                             c->actor.precision};
+                             c->actor.precision, d.f16};
   if (key == c->actor_key) return MDR_OK;
   if ((size_t)d.off_end > c->actor_cap) {
     HIP_TRY(hipStreamSynchronize(st));
@@ -2007,8 +2135,21 @@ int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
   const float* b2 = w2 + (size_t)a.h2 * a.h1;
   const float* w3 = b2 + a.h2;
   const float* b3 = w3 + (size_t)kActorNA * a.h2;
+  ActorFold fo{};
+  if (d.f16) {  // the folded features (mdr_actor.h ActorFold)
+    int off[3], mk[3];
+    int u = obs_uniform_own(sp->hvac_state, sp->solar_state, sp->thermal_state, fo.feat, fo.cf);
+    fo.nu_own = u;
+    const int um = obs_uniform_msg(sp->msg_thermal, sp->msg_hvac, off, mk);
+    for (int k = 0; k < d.n_comm; ++k)
+      for (int j = 0; j < um && u < kActorMaxU; ++j) {
+        fo.feat[u] = d.n_own + k * d.msg_w + off[j];
+        fo.cf[u++] = mk[j];
+      }
+    fo.nu = u;
+  }
   const int nthreads = (d.mb * (d.ks1 + kActorKS2) + 1) * 64;
-  hipLaunchKernelGGL(k_actor_pack, dim3(blocks(nthreads, 256)), dim3(256), 0, st, d, w1, b1, w2, b2, w3, b3,
+  hipLaunchKernelGGL(k_actor_pack, dim3(blocks(nthreads, 256)), dim3(256), 0, st, d, fo, w1, b1, w2, b2, w3, b3,
                      c->d_actor);
   LAUNCH_CHECK("k_actor_pack");
   c->actor_key = key;
@@ -2017,8 +2158,9 @@ int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
 
 #define MDR_ACTOR_KERNELS_D(MB, KS, D)                                                                 \
   (const void*)k_actor<1, false, MB, KS, D>, (const void*)k_actor<3, false, MB, KS, D>,                   \
-      (const void*)k_actor<6, false, MB, KS, D>, (const void*)k_actor<1, true, MB, KS, D>,                \
-      (const void*)k_actor<3, true, MB, KS, D>, (const void*)k_actor<6, true, MB, KS, D>
+      (const void*)k_actor<4, false, MB, KS, D>, (const void*)k_actor<6, false, MB, KS, D>,               \
+      (const void*)k_actor<1, true, MB, KS, D>, (const void*)k_actor<3, true, MB, KS, D>,                 \
+      (const void*)k_actor<4, true, MB, KS, D>, (const void*)k_actor<6, true, MB, KS, D>
 #define MDR_ACTOR_KERNELS(MB, KS) MDR_ACTOR_KERNELS_D(MB, KS, false)
 
 
@@ -2065,8 +2207,10 @@ int launch_actor_chain(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, con
 }
 
 int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const double* p_dev, uint64_t tick,
-                 const TickArgs* tkp, const ActorOut& out, hipStream_t st) {
-  if (!actor_fused_ok(c, sp)) return launch_actor_chain(c, sp, o, p_dev, tick, tkp, out, st);
+                 const TickArgs* tkp, const ActorOut& out_in, hipStream_t st) {
+  if (!actor_fused_ok(c, sp)) return launch_actor_chain(c, sp, o, p_dev, tick, tkp, out_in, st);
+  ActorOut out = out_in;
+  out.ovf = reinterpret_cast<unsigned*>(c->d_flags) + 1;  // (mdr_actor_status; read by the fp16 form only)
   ActorDims d;
   int nw = 0;
   if (int rc = actor_plan(c, sp, &d, &nw)) return rc;
@@ -2100,14 +2244,16 @@ int launch_actor(mdr_ctx* c, const mdr_obs_spec* sp, const ObsArgs& o, const dou
     else if (d.ks1 == 3) MDR_LAUNCH_ACTOR_S(P, F, 8, 3);         \
     else MDR_LAUNCH_ACTOR_S(P, F, 8, 4);                         \
   } while (0)
-  const int prec = c->actor.precision;
+  const int prec = actor_kprec(c);
   if (out.prof) {
-    if (prec == MDR_PREC_BF16) MDR_LAUNCH_ACTOR(1, true);
-    else if (prec == MDR_PREC_FP32) MDR_LAUNCH_ACTOR(6, true);
+    if (prec == 1) MDR_LAUNCH_ACTOR(1, true);
+    else if (prec == 4) MDR_LAUNCH_ACTOR(4, true);
+    else if (prec == 6) MDR_LAUNCH_ACTOR(6, true);
     else MDR_LAUNCH_ACTOR(3, true);
   } else {
-    if (prec == MDR_PREC_BF16) MDR_LAUNCH_ACTOR(1, false);
-    else if (prec == MDR_PREC_FP32) MDR_LAUNCH_ACTOR(6, false);
+    if (prec == 1) MDR_LAUNCH_ACTOR(1, false);
+    else if (prec == 4) MDR_LAUNCH_ACTOR(4, false);
+    else if (prec == 6) MDR_LAUNCH_ACTOR(6, false);
     else MDR_LAUNCH_ACTOR(3, false);
   }
 #undef MDR_LAUNCH_ACTOR
@@ -2188,6 +2334,18 @@ int mdr_actor_load(mdr_ctx* c, const mdr_actor_spec* a, const float* w1, const f
   const float* w[3] = {w1, w2, w3};
   const float* b[3] = {b1, b2, b3};
   return mdr_actor_load_net(c, &net, w, b, stream);
+}
+
+int mdr_actor_status(mdr_ctx* c, int64_t* out, int n, void* stream) {
+  if (!c || !out || n < 2) return fail(MDR_EARG, "mdr_actor_status: need out[2]");
+  unsigned v = 0;
+  HIP_TRY(hipStreamSynchronize(S(stream)));
+  HIP_TRY(hipMemcpy(&v, c->d_flags + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
+  const unsigned z = 0;
+  HIP_TRY(hipMemcpy(c->d_flags + 1, &z, sizeof(unsigned), hipMemcpyHostToDevice));
+  out[0] = (int64_t)v;
+  out[1] = c->actor_ready ? actor_kprec(c) : 0;
+  return MDR_OK;
 }
 
 int mdr_actor_fused(mdr_ctx* c, const mdr_obs_spec* sp) {

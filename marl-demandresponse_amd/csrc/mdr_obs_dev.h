@@ -114,6 +114,16 @@ __device__ __forceinline__ void msg_from_regs(const KParams& p, const ObsArgs& o
   }
 }
 
+// The house-independent features of a message in msg_from_regs' order (the hvac constants cf[8..10]):
+// off[u] = the offset inside the message, cfk[u] = the obs_consts entry; returns how many (<= 3).
+// Keep in step with msg_from_regs.
+__host__ __device__ inline int obs_uniform_msg(int msg_thermal, int msg_hvac, int* off, int* cfk) {
+  if (!msg_hvac) return 0;
+  const int f = 4 + (msg_thermal ? 4 : 0);
+  for (int u = 0; u < 3; ++u) { off[u] = f + u; cfk[u] = 8 + u; }
+  return 3;
+}
+
 __device__ __forceinline__ void msg_features(const KParams& p, const ObsArgs& o, int64_t j, const float* cf,
                                              float* dst, const ObsDiv& dv) {
   HouseRegs r;
@@ -122,29 +132,48 @@ __device__ __forceinline__ void msg_features(const KParams& p, const ObsArgs& o,
 }
 
 // The house's own features (everything before the messages); returns how many were written.
+// zu: the house-independent ones (the cf[k] entries, obs_uniform_own) written as 0 — the fp16-split
+// actor adds their contribution to its layer-1 bias once per block instead (mdr_actor.hip)
 __device__ __forceinline__ int row_scalars(const KParams& p, const ObsArgs& o, const HouseRegs& r,
-                                           const float* cf, float* row, const ObsDiv& dv) {
+                                           const float* cf, float* row, const ObsDiv& dv, bool zu = false) {
   int f = 0;
   row[f++] = hv_on(r.w) ? 1.f : 0.f;
   row[f++] = hv_lock(r.w) ? 1.f : 0.f;
   row[f++] = sso_ratio(r.w, dv);
-  row[f++] = cf[0];
-  if (o.hvac_state) { row[f++] = cf[1]; row[f++] = cf[2]; }
-  row[f++] = cf[3];
-  row[f++] = cf[4];
-  row[f++] = cf[5];
+  row[f++] = zu ? 0.f : cf[0];
+  if (o.hvac_state) { row[f++] = zu ? 0.f : cf[1]; row[f++] = zu ? 0.f : cf[2]; }
+  row[f++] = zu ? 0.f : cf[3];
+  row[f++] = zu ? 0.f : cf[4];
+  row[f++] = zu ? 0.f : cf[5];
   row[f++] = (float)div5(r.T - 20.0, dv);
   row[f++] = (float)div5(r.Tm - 20.0, dv);
   row[f++] = (float)div5(r.tg - 20.0, dv);
-  if (o.solar_state) row[f++] = cf[6];
+  if (o.solar_state) row[f++] = zu ? 0.f : cf[6];
   if (o.thermal_state) {
     row[f++] = (float)(r.ua / o.cfg_ua);
     row[f++] = (float)(r.ca / o.cfg_ca);
     row[f++] = (float)(r.cm / o.cfg_cm);
     row[f++] = (float)(r.hm / o.cfg_hm);
-    row[f++] = cf[7];
+    row[f++] = zu ? 0.f : cf[7];
   }
   return f;
+}
+
+// The house-independent own features of row_scalars' order: feat[u] = the feature index, cfk[u] = the
+// obs_consts entry it holds; returns how many (<= kObsUniformMax).  Keep in step with row_scalars.
+constexpr int kObsUniformMax = 8;
+__host__ __device__ inline int obs_uniform_own(int hvac_state, int solar_state, int thermal_state, int* feat,
+                                               int* cfk) {
+  int f = 3, u = 0;  // (on, lock, sso ratio first)
+  feat[u] = f++; cfk[u++] = 0;
+  if (hvac_state) { feat[u] = f++; cfk[u++] = 1; feat[u] = f++; cfk[u++] = 2; }
+  feat[u] = f++; cfk[u++] = 3;
+  feat[u] = f++; cfk[u++] = 4;
+  feat[u] = f++; cfk[u++] = 5;
+  f += 3;  // (T, Tm, target)
+  if (solar_state) { feat[u] = f++; cfk[u++] = 6; }
+  if (thermal_state) { f += 4; feat[u] = f++; cfk[u++] = 7; }
+  return u;
 }
 
 // RING topology: message sources of the houses [b0, b0 + nb) are [b0 - lo, b0 + nb + hi);

@@ -59,9 +59,18 @@ def make_actor(num_state: int, num_action: int = 2, layers=(100, 100), seed: Opt
 class DeviceActor:
     """``MAPPO.select_actions`` for every house of an Environment shard in one launch."""
 
-    def __init__(self, env, actor, precision: str = "bf16x3"):
+    def __init__(self, env, actor, precision: str = "bf16x3", fp32_form: str = "f16_split"):
+        """precision: "fp32" (the reference Actor's), "bf16x3" or "bf16".  fp32_form: the fused kernel's
+        fp32 arithmetic — "f16_split" (fp16 hi/lo operands, 3 MFMAs per term, per-layer power-of-two
+        weight scales; ``status()`` counts tiles whose activations left fp16's range) or "bf16_split3"
+        (three-way bf16 operands, 6 MFMAs per term, no range limit)."""
         if precision not in L.PRECISIONS:
             raise ValueError(f"precision must be one of {sorted(L.PRECISIONS)}")
+        forms = {"f16_split": L.FP32_F16_SPLIT, "bf16_split3": L.FP32_BF16_SPLIT3}
+        if fp32_form not in forms:
+            raise ValueError(f"fp32_form must be one of {sorted(forms)}")
+        env.shard.set_option("actor_fp32_form", forms[fp32_form])
+        self.fp32_form = fp32_form
         if not 1 <= len(actor.layers) <= L.ACTOR_MAX_LAYERS:
             raise ValueError(f"1 to {L.ACTOR_MAX_LAYERS} hidden layers (actor_layers)")
         self.env = env
@@ -84,6 +93,10 @@ class DeviceActor:
             net.hidden[i] = h
         sh.actor_load_net(net, ws, bs)
         torch.cuda.current_stream(dev).synchronize()  # (the copies are read by later launches only)
+
+    def status(self):
+        """mdr_actor_status (synchronises): {range_faults, kernel_prec} — see ``Shard.actor_status``."""
+        return self.env.shard.actor_status()
 
     def fused(self) -> bool:
         """True when this actor runs the fused obs + MLP kernel (k_actor) for the env's obs layout:

@@ -659,7 +659,8 @@ class Environment:
                 raise ValueError(f"{name}: a contiguous {dt} tensor [n_ticks, {n}] or [{n}]")
         a_st = n if actions.dim() == 2 else 0
         r_st = n if rewards.dim() == 2 else 0
-        if self.world > 1 or self._links is None or self._grid_pending:
+        if (self.world > 1 or (self._gq_force_sharded and self._comm is not None) or self._links is None
+                or self._grid_pending):
             for t in range(n_ticks):
                 a = actions[t] if a_st else actions
                 self.greedy_actions(out=a)

@@ -122,7 +122,7 @@ class HipShard:
     def set_option(self, name: str, value: int):
         """mdr_set_option: an alternative launch form of the same computation (mdr.h MDR_OPT_*:
         step_tpw, fastdiv, window_pipeline, sharded_overlap, greedy_sort, force_halo, halo_overlap,
-        actor_generic, window_thermal, halo_in_counts, gq_band)."""
+        actor_generic, window_thermal, halo_in_counts, gq_band, actor_fp32_form)."""
         L.check(self.lib.mdr_set_option(self.ctx, L.OPTIONS[name], int(value)), f"mdr_set_option({name})")
 
     def params_changed(self):
@@ -147,12 +147,22 @@ class HipShard:
                 "mdr_power_counts")
 
     def graph_info(self):
-        """{rollout_graphs, actor_graphs, rollout_launches, actor_launches}: cached graphs and
-        hipGraphLaunch calls (mdr_graph_info)."""
-        out = (C.c_int64 * 4)()
-        rc = self.lib.mdr_graph_info(self.ctx, out, 4)
-        L.check(0 if rc == 4 else rc, "mdr_graph_info")
-        return dict(zip(("rollout_graphs", "actor_graphs", "rollout_launches", "actor_launches"), list(out)))
+        """{rollout_graphs, actor_graphs, rollout_launches, actor_launches, guarded, guarded_nodes}:
+        cached graphs, hipGraphLaunch calls, and the captures the memset guard walked (mdr_graph_info)."""
+        out = (C.c_int64 * 6)()
+        rc = self.lib.mdr_graph_info(self.ctx, out, 6)
+        L.check(0 if rc == 6 else rc, "mdr_graph_info")
+        return dict(zip(("rollout_graphs", "actor_graphs", "rollout_launches", "actor_launches", "guarded",
+                         "guarded_nodes"), list(out)))
+
+    def graph_memset_probe(self):
+        """mdr_graph_memset_probe: a memset node captured in this context, its parameters and what
+        its replays leave in the count slabs (diagnostic; synchronises and overwrites the slabs)."""
+        out = (C.c_int64 * 13)()
+        L.check(self.lib.mdr_graph_memset_probe(self.ctx, out, 13, self.stream()), "mdr_graph_memset_probe")
+        keys = ("nodes", "memset_nodes", "dst_ok", "value", "element_size", "width", "height", "pitch", "bytes",
+                "nonzero_replay1", "nonzero_replay2", "nonzero_replay3", "nonzero_kernel_zero")
+        return dict(zip(keys, list(out)))
 
     def counts_buffer(self):
         p = C.c_void_p()
@@ -313,6 +323,13 @@ class HipShard:
         w = (C.c_void_p * n)(*[L.ptr(t) for t in weights])
         b = (C.c_void_p * n)(*[L.ptr(t) for t in biases])
         L.check(self.lib.mdr_actor_load_net(self.ctx, C.byref(net), w, b, self.stream()), "mdr_actor_load_net")
+
+    def actor_status(self):
+        """mdr_actor_status (synchronises): {range_faults: fused fp16-split tiles that met a non-finite
+        logit since the last call, kernel_prec: 1 bf16 / 3 bf16x3 / 4 fp16 split / 6 three-way bf16}."""
+        out = (C.c_int64 * 2)()
+        L.check(self.lib.mdr_actor_status(self.ctx, out, 2, self.stream()), "mdr_actor_status")
+        return {"range_faults": int(out[0]), "kernel_prec": int(out[1])}
 
     def actor_fused(self, spec) -> bool:
         """True when the loaded actor runs the fused k_actor for this obs layout (else the chain)."""

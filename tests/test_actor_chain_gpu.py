@@ -18,7 +18,7 @@ import golden_util as gu
 
 pytestmark = pytest.mark.gpu
 
-ATOL = {"fp32": 4e-6, "bf16x3": 1e-4, "bf16": 3e-2}
+ATOL = {"fp32": 4e-6, "fp32_bf16": 4e-6, "bf16x3": 1e-4, "bf16": 3e-2}
 
 # (env overrides, actor_layers, runs fused?)
 LAYOUTS = {
@@ -28,7 +28,8 @@ LAYOUTS = {
     "three_layers": ({}, (64, 64, 64), False),
     "wide_256": ({}, (256, 256), False),
     "one_layer": ({}, (48,), False),
-    # 88 features (KS1 = 4): bf16x3 fits the fused kernel, fp32's three weight planes do not
+    # 88 features (KS1 = 4): bf16x3 and the fp16-split fp32 form fit the fused kernel, the three-way
+    # bf16 fp32 form's three weight planes do not
     "ks1_4": ({"cluster_prop.message_prop.hvac": True, "state_prop.hvac": True, "state_prop.solar_gain": True,
                "state_prop.thermal": True}, (100, 100), None),
     "default": ({}, (100, 100), True),
@@ -58,7 +59,7 @@ def _warm(env, torch, ticks=5, seed=7):
         env.step_tensor(torch.from_numpy(rs.randint(0, 2, env.n_local).astype(np.uint8)).to("cuda"))
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32_bf16", "bf16x3", "bf16"])
 @pytest.mark.parametrize("layout", sorted(LAYOUTS))
 def test_actor_layouts_vs_torch(torch_gpu, layout, precision):
     from mdr_amd.actor import DeviceActor
@@ -71,8 +72,11 @@ def test_actor_layouts_vs_torch(torch_gpu, layout, precision):
     F = env.obs_spec().n_feat
     ref_obs = env.obs_tensor().clone()
     actor = gu.calibrated_actor(F, ref_obs.abs().amax(0).double().cpu().numpy(), seed=5, layers=layers).to("cuda")
-    da = DeviceActor(env, actor, precision=precision)
-    want_fused = fused if fused is not None else precision != "fp32"
+    if precision == "fp32_bf16":  # (the fp32 precision in its three-way bf16 form)
+        da = DeviceActor(env, actor, precision="fp32", fp32_form="bf16_split3")
+    else:
+        da = DeviceActor(env, actor, precision=precision)
+    want_fused = fused if fused is not None else precision != "fp32_bf16"
     assert da.fused() == want_fused
     probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
     obs = torch.empty((n, F), dtype=torch.float32, device="cuda")

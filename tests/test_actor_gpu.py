@@ -5,7 +5,9 @@ initialisation (mappo.py:41-50), on norm_state_dict vectors (norm.py:178-218); g
 ``tests/golden/policy.npz`` (reference probabilities on reference obs vectors).
 
 Tolerances on action probabilities (the kernel's documented precision, mdr.h MDR_PREC_*):
-  fp32   (three-way split-bf16 MFMA, 6 products, fp32 accumulate)  atol 1e-6 against torch fp32
+  fp32   (fp16 hi/lo split on the fp16 MFMA, 3 products, per-layer power-of-two weight scales, fp32
+         accumulate: the default fp32 form)  atol 1e-6 against torch fp32
+  fp32_bf16 (the fp32 precision in its three-way split-bf16 form, 6 products)  atol 1e-6
   bf16x3 (split-bf16 MFMA, fp32 accumulate)  atol 1e-4 against torch fp32 on the same obs
   bf16   (one bf16 product per term)         atol 3e-2
 Obs rows: within 2 float32 ulps of the reference (as tests/test_env_parity_gpu.py); bit-identical
@@ -21,7 +23,17 @@ import golden_util as gu
 
 pytestmark = pytest.mark.gpu
 
-PROB_ATOL = {"fp32": 1e-6, "bf16x3": 1e-4, "bf16": 3e-2}
+PROB_ATOL = {"fp32": 1e-6, "fp32_bf16": 1e-6, "bf16x3": 1e-4, "bf16": 3e-2}
+FP32S = ("fp32", "fp32_bf16")
+
+
+def device_actor(env, actor, precision):
+    """DeviceActor for a test precision: 'fp32_bf16' = precision fp32 in its three-way bf16 form."""
+    from mdr_amd.actor import DeviceActor
+
+    if precision == "fp32_bf16":
+        return DeviceActor(env, actor, precision="fp32", fp32_form="bf16_split3")
+    return DeviceActor(env, actor, precision=precision)
 POLICY_CASES = {"c1": ("c1_sin_dbbc", (0, 1, 50)), "wide": ("n30_maxerr_groups_hvacmsg", (0, 50))}
 
 
@@ -53,7 +65,7 @@ def make_env(props, rng_seed, resets=1, **kw):
     return env
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32_bf16", "bf16x3", "bf16"])
 @pytest.mark.parametrize("case", sorted(POLICY_CASES))
 def test_actor_golden(torch_gpu, case, precision):
     """Reference actor weights + reference trajectory state: obs rows and probabilities."""
@@ -65,7 +77,7 @@ def test_actor_golden(torch_gpu, case, precision):
     d, meta = gu.traj(name)
     props = gu.props_from_overrides(meta["overrides"])
     env = make_env(props, meta["seed"], meta["resets"])
-    da = DeviceActor(env, actor, precision=precision)
+    da = device_actor(env, actor, precision)
     N, F = meta["N"], pol[f"{case}_obs"].shape[1]
     ref_obs = pol[f"{case}_obs"].reshape(len(ticks), N, F)
     ref_probs = pol[f"{case}_probs"].reshape(len(ticks), N, 2)
@@ -87,12 +99,13 @@ def test_actor_golden(torch_gpu, case, precision):
             assert err < PROB_ATOL[precision], (t, err)
             # (the golden holds the reference's CPU probabilities: torch's CPU and GPU fp32 GEMMs
             # accumulate in other orders, ~1e-7)
-            assert np.abs(p - ref_probs[k]).max() < PROB_ATOL[precision] + (1e-6 if precision == "fp32" else 1e-5)
+            assert np.abs(p - ref_probs[k]).max() < PROB_ATOL[precision] + (1e-6 if precision in FP32S else 1e-5)
             a = act.cpu().numpy()
             np.testing.assert_array_equal(prob.cpu().numpy(), p[np.arange(N), a])
         if t < max(ticks):
             env.step_tensor(torch.from_numpy(d["actions"][t]).to("cuda"))
     print(f"{case} {precision}: max |p - p_torch| = {worst:.3g}")
+    assert da.status()["range_faults"] == 0
 
 
 def scaled_actor(torch, n_in, scale, seed=3):
@@ -116,7 +129,7 @@ def _forward64(actor, x):
     return x
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32_bf16", "bf16x3", "bf16"])
 @pytest.mark.parametrize("n", [1, 37, 300, 4099])
 def test_actor_vs_torch_sizes(torch_gpu, n, precision):
     """Ragged sizes, spread-out logits (weights x3): probabilities vs torch fp32 on the same obs."""
@@ -131,7 +144,7 @@ def test_actor_vs_torch_sizes(torch_gpu, n, precision):
         env.step_tensor(torch.from_numpy(rs.randint(0, 2, n).astype(np.uint8)).to("cuda"))
     F = env.obs_spec().n_feat
     actor = scaled_actor(torch, F, 3.0)
-    da = DeviceActor(env, actor, precision=precision)
+    da = device_actor(env, actor, precision)
     probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
     obs = torch.empty((n, F), dtype=torch.float32, device="cuda")
     act, prob = da.select_actions(probs=probs, obs_out=obs, count_next=False)
@@ -140,7 +153,7 @@ def test_actor_vs_torch_sizes(torch_gpu, n, precision):
     p = probs.cpu().numpy()
     err = float(np.abs(p - tp).max())
     print(f"n={n} {precision}: max |p - p_torch| = {err:.3g}, p1 spread {tp[:, 1].min():.3f}..{tp[:, 1].max():.3f}")
-    if precision == "fp32":
+    if precision in FP32S:
         # fp32-faithful: no further from the float64 forward than torch's own fp32 GEMMs are (other
         # accumulation orders; at weights x3 the logits reach tens, so both sit at a few 1e-7 .. 1e-6)
         with torch.no_grad():
@@ -165,7 +178,7 @@ LAYOUTS = {
 }
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32_bf16", "bf16x3"])
 @pytest.mark.parametrize("layout", sorted(LAYOUTS))
 def test_actor_layer1_ksteps(torch_gpu, layout, precision):
     """The layer-1 k-step instantiations at their edges (mdr_actor.hip KS1): probabilities vs torch
@@ -187,20 +200,21 @@ def test_actor_layer1_ksteps(torch_gpu, layout, precision):
     actor = gu.calibrated_actor(F, env.obs_tensor().abs().amax(0).double().cpu().numpy(), seed=5).to("cuda")
     probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
     obs = torch.empty((n, F), dtype=torch.float32, device="cuda")
-    da = DeviceActor(env, actor, precision=precision)
-    # (ks1_4 in fp32: three bf16 planes of W1 (7 x 4 k-steps) and W2 (7 x 4) are 168 KiB, more than a
-    # CU's LDS, so that layout runs the layer chain; tests/test_actor_chain_gpu.py)
-    assert da.fused() == (layout != "ks1_4" or precision != "fp32")
+    da = device_actor(env, actor, precision)
+    # (ks1_4 in the three-way bf16 fp32 form: three planes of W1 (7 x 4 k-steps) and W2 (7 x 4) are
+    # 168 KiB, more than a CU's LDS, so that layout runs the layer chain, tests/test_actor_chain_gpu.py;
+    # the fp16-split form has two planes, like bf16x3, and runs fused)
+    assert da.fused() == (layout != "ks1_4" or precision != "fp32_bf16")
     da.select_actions(probs=probs, obs_out=obs, count_next=False)
     with torch.no_grad():
         tp = actor(obs).cpu().numpy()
     err = float(np.abs(probs.cpu().numpy() - tp).max())
     print(f"{layout} {precision}: max |p - p_torch| = {err:.3g}")
-    assert err < (4e-6 if precision == "fp32" else PROB_ATOL[precision])
+    assert err < (4e-6 if precision in FP32S else PROB_ATOL[precision])
     gu.assert_not_saturated(tp[:, 1])
 
 
-@pytest.mark.parametrize("precision", ["fp32", "bf16x3", "bf16"])
+@pytest.mark.parametrize("precision", ["fp32", "fp32_bf16", "bf16x3", "bf16"])
 def test_actor_default_layout_form_equals_generic(torch_gpu, precision):
     """The k_actor form specialised for the reference's default obs layout (mdr_actor.hip DEF: its
     layout fixed at compile time, 12 / 16 waves per block) == the generic form on the same inputs,
@@ -219,7 +233,7 @@ def test_actor_default_layout_form_equals_generic(torch_gpu, precision):
         env.step_tensor(torch.from_numpy(rs.randint(0, 2, n).astype(np.uint8)).to("cuda"))
     F = env.obs_spec().n_feat
     actor = gu.calibrated_actor(F, env.obs_tensor().abs().amax(0).double().cpu().numpy(), seed=9).to("cuda")
-    da = DeviceActor(env, actor, precision=precision)
+    da = device_actor(env, actor, precision)
     res = []
     for generic in (0, 1):
         env.shard.set_option("actor_generic", generic)
@@ -303,18 +317,17 @@ def test_actor_rollout_equals_loop(torch_gpu):
         assert torch.equal(a, acts[t]) and torch.equal(r, rew[t]), t
 
 
-def test_actor_fp32_rollout_equals_loop(torch_gpu):
-    """The fp32-faithful precision through the fused rollout graph == its select_actions /
-    step_tensor loop (the same kernel in both)."""
-    from mdr_amd.actor import DeviceActor
-
+@pytest.mark.parametrize("precision", FP32S)
+def test_actor_fp32_rollout_equals_loop(torch_gpu, precision):
+    """The fp32-faithful precision (both forms) through the fused rollout graph == its select_actions
+    / step_tensor loop (the same kernel in both)."""
     torch = torch_gpu
     n, T = 2049, 6
     props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
                                      "power_grid_prop.signal_properties.mode": "sinusoidals"})
     env_a, env_b = make_env(props, 8), make_env(props, 8)
     actor = scaled_actor(torch, env_a.obs_spec().n_feat, 2.0)
-    da, db = DeviceActor(env_a, actor, precision="fp32"), DeviceActor(env_b, actor, precision="fp32")
+    da, db = device_actor(env_a, actor, precision), device_actor(env_b, actor, precision)
     rew = torch.empty((T, n), dtype=torch.float64, device="cuda")
     acts = torch.empty((T, n), dtype=torch.uint8, device="cuda")
     da.rollout(T, rewards=rew, actions=acts)
@@ -322,3 +335,42 @@ def test_actor_fp32_rollout_equals_loop(torch_gpu):
         a, _ = db.select_actions(count_next=True)
         r = env_b.step_tensor(a)
         assert torch.equal(a, acts[t]) and torch.equal(r, rew[t]), t
+
+
+def test_actor_fp16_split_range(torch_gpu):
+    """The fp16-split fp32 form's range limit is visible, not silent: houses whose seconds-since-off
+    ratio (an obs feature, sso / L) exceeds fp16's 65504 cannot be represented, and
+    mdr_actor_status counts their tiles; the three-way bf16 form has no such limit and matches torch
+    fp32 there.  Every other house's probabilities stay within the fp32 tolerance in both forms —
+    including the tiles whose hidden activations the large features push beyond fp16 (k_actor runs
+    their layer 1 again at a power-of-two scale)."""
+    torch = torch_gpu
+    n = 3001
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    env = make_env(props, 5)
+    for _ in range(3):
+        env.step_tensor(torch.zeros(n, dtype=torch.uint8, device="cuda"))
+    # houses 100..131 (one tile) off for ~34 years: sso saturated at 2^30 - 1 (hvac bits 0-29)
+    env.shard.hvac[100:132] = 0x3FFFFFFF
+    F = env.obs_spec().n_feat
+    obs = env.obs_tensor().clone()
+    assert float(obs[100:132].abs().max()) > 65504.0
+    actor = gu.calibrated_actor(F, np.ones(F), seed=4).to("cuda")
+    with torch.no_grad():
+        tp = actor(obs).cpu().numpy()
+    ok = np.ones(n, bool)
+    ok[95:137] = False  # (the saturated houses and the houses whose ring messages carry them)
+    for precision in FP32S:
+        da = device_actor(env, actor, precision)
+        da.status()  # (clear)
+        probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
+        da.select_actions(probs=probs, count_next=False)
+        st = da.status()
+        p = probs.cpu().numpy()
+        assert np.abs(p[ok] - tp[ok]).max() < 4e-6, precision
+        if precision == "fp32":
+            assert st["kernel_prec"] == 4 and st["range_faults"] >= 1, st
+        else:
+            assert st["kernel_prec"] == 6 and st["range_faults"] == 0, st
+            assert np.all(np.isfinite(p)) and np.abs(p - tp).max() < 4e-6

@@ -214,13 +214,14 @@ def test_c4_rank_rccl_window_rollout_vs_oracle(tmp_path, pipeline):
 
 
 # ------------------------------------------------------------------------------------- C5 @ 1M
-@pytest.mark.parametrize("precision,atol", [("bf16x3", 1e-4), ("fp32", 4e-6)])
+@pytest.mark.parametrize("precision,atol", [("bf16x3", 1e-4), ("fp32", 4e-6), ("fp32_bf16", 4e-6)])
 def test_c5_actor_rollout_1m(torch_gpu, precision, atol):
     """C5's actor path at 1,048,576 houses: DeviceActor.rollout (actor -> step per tick, one graph)
     == the select_actions / step_tensor loop over 4 ticks (actions, probabilities, rewards, state);
     at every tick the loop's obs rows are within 2 float32 ulps of the oracle's norm_vector on
     8,192 sampled houses (incl. both ring ends) and its probabilities within ``atol`` of torch fp32
-    (bf16x3 1e-4, fp32 4e-6).  The actor is the seed-1 reference actor with the obs normalisation
+    (bf16x3 1e-4, fp32 4e-6 in both its forms: the fp16 split, default, and the three-way bf16
+    split, 'fp32_bf16').  The actor is the seed-1 reference actor with the obs normalisation
     folded into layer 1 (golden_util.calibrated_actor): at 1M houses the raw seed-1 policy
     saturates (the cluster-power feature is ~0.4 N, norm.py:145), and a probability check would
     compare 1.0 with 1.0; here most probabilities lie in (0.05, 0.95) and both actions occur."""
@@ -234,7 +235,8 @@ def test_c5_actor_rollout_1m(torch_gpu, precision, atol):
     eb = Environment(props, rng=random.Random(BENCH_RNG), population="synthetic", seed=BENCH_SEED)
     F = ea.obs_spec().n_feat
     actor = gu.calibrated_actor(F, ea.obs_tensor().abs().amax(0).double().cpu().numpy(), seed=1).to("cuda")
-    da, db = DeviceActor(ea, actor, precision=precision), DeviceActor(eb, actor, precision=precision)
+    kw = {"precision": "fp32", "fp32_form": "bf16_split3"} if precision == "fp32_bf16" else {"precision": precision}
+    da, db = DeviceActor(ea, actor, **kw), DeviceActor(eb, actor, **kw)
     rew = torch.empty((T, n), dtype=torch.float64, device="cuda")
     acts = torch.empty((T, n), dtype=torch.uint8, device="cuda")
     probs = torch.empty((T, n), dtype=torch.float32, device="cuda")
@@ -271,3 +273,4 @@ def test_c5_actor_rollout_1m(torch_gpu, precision, atol):
         assert torch.equal(getattr(ea.shard, key), getattr(eb.shard, key)), key
     assert ea._cluster_power() == eb._cluster_power()
     gu.assert_not_saturated(probs.cpu().numpy(), acts.cpu().numpy())
+    assert da.status()["range_faults"] == 0 and db.status()["range_faults"] == 0

@@ -112,6 +112,18 @@ def _worker(rank, world, port, backend, kind, n, mode, out_dir):
         env._gq_force_sharded = True
     res = _run(env, n, torch, dev)
     res["lo"] = env._offset
+    if world > 1 and _comm_kind(kind) == "host":
+        #  config C3's one-call loop refuses a sharded context: a shard-local decision
+        # and step would use shard-local counts (Environment.greedy_rollout takes the per-tick loop)
+        from mdr_amd._lib import MdrError
+
+        a = torch.empty(env.n_local, dtype=torch.uint8, device=dev)
+        r = torch.empty(env.n_local, dtype=torch.float64, device=dev)
+        try:
+            env.shard.greedy_rollout(env.driver_window(1), a, 0, r, 0)
+            res["gr_guard"] = 0
+        except MdrError as e:
+            res["gr_guard"] = int("single-GPU only" in str(e))
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
     torch.cuda.synchronize()
     dist.destroy_process_group()
@@ -181,6 +193,8 @@ def test_sharded_equals_single(tmp_path, backend, kind, world, n, mode):
         # either way); r03's occasional hand-off to the all-gather form was a race in
         # k_gq_compact (block 0 overwrote the crossing base the other blocks were still reading)
         assert int(p["gq_fb"]) == 0, int(p["gq_fb"])
+        if world > 1 and _comm_kind(kind) == "host":
+            assert int(p["gr_guard"]) == 1
     obs = np.concatenate([p["obs"] for p in parts])
     np.testing.assert_array_equal(obs, ref["obs"])
 

@@ -325,6 +325,44 @@ def test_greedy_key_runs_vs_oracle(torch_gpu, form):
         assert sh.greedy_fallbacks() == f0 + 1
 
 
+@pytest.mark.parametrize("n", [3001, 200_003])
+def test_greedy_keys_with_lookahead_keeps_counts(torch_gpu, n):
+    """a step with a lookahead AND ctrl='greedy_keys' must keep the lookahead's counts
+    (k_gq_keys used to zero that slab, so the next non-greedy step ran with P = 0), and a greedy call
+    after such a step must still count only its own decisions.  Twins: the same seeds with and
+    without the keys; everything compared with ==."""
+    torch = torch_gpu
+    from mdr_amd.environment import Environment
+
+    props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
+                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+    a = Environment(props, rng=random.Random(5), population="synthetic", seed=5)
+    b = Environment(props, rng=random.Random(5), population="synthetic", seed=5)
+    for _ in range(3):
+        ra = a.step_tensor(None, action_mode="random", lookahead="random", ctrl="greedy_keys").clone()
+        rb = b.step_tensor(None, action_mode="random", lookahead="random").clone()
+        assert torch.equal(ra, rb)
+    ra = a.step_tensor(None, action_mode="random").clone()  # (the counts the keys' step looked ahead)
+    rb = b.step_tensor(None, action_mode="random").clone()
+    assert torch.equal(ra, rb)
+    assert a.cluster.current_power_consumption == b.cluster.current_power_consumption > 0
+    sa, sb = a.shard.host_state(), b.shard.host_state()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    # keys + lookahead, then the greedy decision and its step: the decisions' counts alone
+    a.step_tensor(None, action_mode="random", lookahead="random", ctrl="greedy_keys")
+    b.step_tensor(None, action_mode="random", lookahead="random")
+    ga, gb = a.greedy_actions(), b.greedy_actions()
+    assert torch.equal(ga, gb)
+    ra, rb = a.step_tensor(ga).clone(), b.step_tensor(gb).clone()
+    assert torch.equal(ra, rb)
+    prm = a.shard.host_params()
+    caps = np.array(a._cap_values, np.float64)[prm["cap_idx"]]
+    on = a.shard.host_state()["on"]
+    P = float(np.sum(np.where(on, caps / props.cluster_prop.house_prop.hvac_prop.cop, 0.0)))
+    assert a.cluster.current_power_consumption == b.cluster.current_power_consumption == P
+
+
 def test_one_million_houses_properties(torch_gpu):
     """Full-size (1,048,576 houses) size-independent checks: FSM bit-exact vs the oracle on the
     same input state, temperatures within tolerance, P == sum of ON power (exact integers)."""

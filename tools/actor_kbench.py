@@ -2,7 +2,7 @@
 around K launches: the per-launch time and achieved TFLOP/s on the algorithmic FLOPs; the program
 rocprofv3 --pmc passes profile (tools/pmc_actor.sh).
 
-    python tools/actor_kbench.py [--houses 1048576] [--precision bf16x3] [--reps 20]
+    python tools/actor_kbench.py [--houses 1048576] [--precision bf16x3] [--reps 20] [--fp32-form f16_split]
 """
 import argparse
 import os
@@ -18,6 +18,7 @@ def main():
     ap.add_argument("--houses", type=int, default=1 << 20)
     ap.add_argument("--precision", default="bf16x3")
     ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--fp32-form", default="f16_split", choices=["f16_split", "bf16_split3"])
     a = ap.parse_args()
     import torch
 
@@ -28,7 +29,7 @@ def main():
     env = Environment(bench.env_props(a.houses), device="cuda:0", rng=random.Random(4), population="synthetic",
                       seed=1234)
     actor = make_actor(env.obs_spec().n_feat, 2, [100, 100], seed=1)
-    da = DeviceActor(env, actor, precision=a.precision)
+    da = DeviceActor(env, actor, precision=a.precision, fp32_form=a.fp32_form)
     n = env.n_local
     act = torch.empty(n, dtype=torch.uint8, device="cuda:0")
     prob = torch.empty(n, dtype=torch.float32, device="cuda:0")
@@ -43,7 +44,8 @@ def main():
     torch.cuda.synchronize()
     us = e0.elapsed_time(e1) * 1e3 / a.reps
     flops = 2 * sum(l.in_features * l.out_features for l in actor.fc) * n
-    print(f"houses={n} precision={a.precision}: k_actor {us:.1f} us/launch, {flops / us / 1e6:.1f} TFLOP/s "
+    st = da.status()
+    print(f"houses={n} precision={a.precision} kernel_prec={st['kernel_prec']} range_faults={st['range_faults']}: k_actor {us:.1f} us/launch, {flops / us / 1e6:.1f} TFLOP/s "
           f"algorithmic ({flops / us / 1e6 / bench.BF16_PEAK_TFS:.3f} of dense bf16 peak)", flush=True)
 
 
