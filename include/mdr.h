@@ -457,11 +457,13 @@ typedef struct mdr_actor_net {
 } mdr_actor_net;
 int mdr_actor_load_net(mdr_ctx* ctx, const mdr_actor_net* net, const float* const* w, const float* const* b,
                        void* stream);
-/* Synchronises: out[0] = tiles of the fused fp16-split form (MDR_PREC_FP32, MDR_FP32_F16_SPLIT) that met
- * a non-finite logit since the last call (an activation outside fp16's range; zeroed by this call),
- * out[1] = the fused kernel's arithmetic (1 bf16, 3 bf16x3, 4 the fp16 split, 6 the three-way bf16
- * split; 0 without an actor). */
-int mdr_actor_status(mdr_ctx* ctx, int64_t* out, int n, void* stream);
+/* Synchronises; counts since the last call (zeroed by it).  out[0] = 32-house tiles of the fused
+ * fp16-split form (MDR_PREC_FP32, MDR_FP32_F16_SPLIT) that met a non-finite logit, out[1] = the fused
+ * kernel's arithmetic (1 bf16, 3 bf16x3, 4 the fp16 split, 6 the three-way bf16 split; 0 without an
+ * actor), out[2] = tiles of the fp16 split whose values left fp16's range (a hidden activation >= 2^15
+ * x the layer's weight scale, or an sso ratio >= 2^15 in the tile's rows) and whose logits were
+ * computed in scalar fp32 instead. */
+int mdr_actor_status(mdr_ctx* ctx, int64_t* out, int n, void* stream);  /* out[3] */
 /* 1 when the loaded actor runs the fused kernel for this obs layout, 0 when it runs the chain. */
 int mdr_actor_fused(mdr_ctx* ctx, const mdr_obs_spec* obs);
 /* One select_actions over the shard.  Outputs (device, any may be NULL): action u8 [n_local],

@@ -17,9 +17,9 @@ constexpr int kActorKS2 = kActorMaxMB / 2;  // layer-2 k-steps of 32 (hidden row
 // (prec: the kernel's PREC — 1 bf16, 3 bf16x3, 4 the fp16-split fp32 form, 6 the three-way bf16 fp32 form)
 constexpr int actor_max_waves(int prec, bool def) { return !def || prec == 6 ? 8 : prec == 1 ? 16 : 12; }
 // the fp16-split form's per-layer weight scale: every scaled weight below 2^kActorF16Exp (k_actor_pack)
-constexpr int kActorF16Exp = 4;
+constexpr int kActorF16Exp = 0;
 // ... and max |b1| s1 below 2^kActorF16Bias (layer 2's fp16 operand relu(layer 1) s1 stays in range)
-constexpr int kActorF16Bias = 12;
+constexpr int kActorF16Bias = 13;
 // the packed tail: b1 [kActorRows] | b2 [kActorRows] | W3^T [kActorRows][kActorNA] | b3 [kActorNA] | s1
 constexpr int kActorMaxU = 64;  // folded features (<= 8 own + 3 per message; <= 128 slots: <= 8 + 3 x 15)
 constexpr int kActorTailS1 = (2 + kActorNA) * kActorRows + kActorNA;
@@ -44,6 +44,7 @@ constexpr int kActorTailEnd = kActorTailFold + 2 + 2 * kActorMaxU;
 struct ActorFold {
   int nu, nu_own;
   int feat[kActorMaxU], cf[kActorMaxU];
+  float cfmax[kActorMaxU];  // a bound on |cf| (the cluster power's: n_global max P_on / R; constants exact)
 };
 struct ActorDims {
   int n_in, h1, h2, n_act;
@@ -53,7 +54,7 @@ struct ActorDims {
   int nf;         // fragments per (row block, k-step): 2 = (hi, lo), 3 = (hi, mid, lo) for the bf16 fp32 form
   int f16;        // 1: fp16 fragments (the fp16-split fp32 form, kernel PREC 4), scaled per layer
   const float* w1raw;  // the loaded fp32 W1 [h1][n_in] (the fp16-split form's folded features, ActorFold)
-  int lds_b1;          // block LDS: that bias, [kActorRows] floats
+  int lds_b1;          // block LDS: that bias and b2, both times the launch's layer-1 scale, [2][kActorRows] floats
   int n_own, own4, msg_w, m4, n_comm, lo, ring, nslot, rs, nrows;
   int off_w1, off_w2, off_tail, off_end;  // packed image: W1 / W2 fragments, fp32 tail
   int lds_cf, lds_hist, lds_wave, wave_stride;  // block LDS: obs consts, count histogram, wave slices
@@ -70,7 +71,8 @@ struct ActorOut {
   unsigned long long* prof;        // diagnostics: [grid][8] per-phase shader cycles, or null
   int tiles;                       // 32-house tiles to run: 0 all, 1 interior (not the first or last), 2 the
                                    // first and last (the sharded ring halo's readers; mdr_actor_rollout_sharded)
-  unsigned* ovf;                   // fp16-split form: launches whose tiles met a non-finite logit (or null)
+  unsigned* ovf;                   // fp16-split form: [0] tiles that met a non-finite logit, [1] tiles whose
+                                   // logits came from the scalar fp32 fallback (actor_tile_fp32), or null
 };
 
 __global__ void k_actor_pack(ActorDims d, ActorFold fo, const float* w1, const float* b1, const float* w2,

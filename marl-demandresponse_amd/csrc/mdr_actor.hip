@@ -139,9 +139,10 @@ __global__ void k_actor_pack(ActorDims d, ActorFold fo, const float* __restrict_
   // 2^kActorF16Exp and weights down to 2^-(kActorF16Exp + 11) of the largest keep their lo part out of
   // fp16 subnormals.  The layer-1 accumulator is then s1 x the reference's, layer 2's s1 s2 x: b1 and
   // b2 are packed scaled alike and W3 by 1 / (s1 s2), so the logits are the reference's.  Layer 2's
-  // fp16 operand is relu(layer 1) x s1: s1 is also capped so that max |b1| s1 < 2^kActorF16Bias, which
-  // leaves that operand inside fp16's range while sum |x| over the obs row stays below
-  // (65504 - 2^kActorF16Bias) / 2^kActorF16Exp (~3,800).
+  // fp16 operand is relu(layer 1) x s1: s1 is also capped so that the folded bias (b1 + the folded
+  // features' contribution, bounded by ActorFold.cfmax) stays below 2^kActorF16Bias, which leaves that
+  // operand inside fp16's range while sum |x| over the rest of the obs row stays below
+  // (2^15 - 2^kActorF16Bias) / 2^kActorF16Exp; k_actor checks (tile_exact).
   float s1 = 1.f, s2 = 1.f;
   if (d.f16) {
     __shared__ float red[3][256];
@@ -149,7 +150,11 @@ __global__ void k_actor_pack(ActorDims d, ActorFold fo, const float* __restrict_
     for (int i = threadIdx.x; i < d.h1 * d.n_in; i += blockDim.x)
       if (!actor_uniform_feat(fo, i % d.n_in)) m1 = fmaxf(m1, fabsf(w1[i]));  // (folded columns: fp32)
     for (int i = threadIdx.x; i < d.h2 * d.h1; i += blockDim.x) m2 = fmaxf(m2, fabsf(w2[i]));
-    for (int i = threadIdx.x; i < d.h1; i += blockDim.x) mb = fmaxf(mb, fabsf(b1[i]));
+    for (int i = threadIdx.x; i < d.h1; i += blockDim.x) {  // the folded bias' bound, row i
+      float b = fabsf(b1[i]);
+      for (int u = 0; u < fo.nu; ++u) b += fabsf(w1[(size_t)i * d.n_in + fo.feat[u]]) * fo.cfmax[u];
+      mb = fmaxf(mb, b);
+    }
     red[0][threadIdx.x] = m1;
     red[1][threadIdx.x] = m2;
     red[2][threadIdx.x] = mb;
@@ -314,6 +319,66 @@ __device__ __forceinline__ void split_operand(const float* v, T* s) {
   }
 }
 
+// The fp16-split form's fallback for a tile whose values leave fp16's range: the logits (without
+// b3) of the tile's houses in scalar fp32 from the raw weights [w1 b1 w2 b2 w3 b3] (d.w1raw), the obs
+// rows from the tile's LDS rows, one house at a time across the wave — lane j holds hidden neurons j
+// and j + 64 of both layers, each a sequential fmaf chain over its inputs (the layer-2 inputs by
+// wave broadcast), the logits a wave sum.  The folded features (ActorFold, the packed tail) enter
+// through b1f = s1 (b1 + their contribution) / s1 (exact), their row slots / columns skipped.
+// Returns house `lane`'s logits on lanes < nb.  Rare (tools: mdr_actor_status 'exact'): ~20 us a tile.
+__device__ float2 actor_tile_fp32(const ActorDims& d, const float* w_row, const float* b1f, float s1b,
+                                               const float* s_tail, int lane, int nb) {
+  const float* W1 = d.w1raw;
+  const float* W2 = W1 + (size_t)d.h1 * d.n_in + d.h1;
+  const float* B2 = W2 + (size_t)d.h2 * d.h1;
+  const float* W3 = B2 + d.h2;
+  const int* tf = reinterpret_cast<const int*>(s_tail + kActorTailFold);
+  const int nu = tf[0];
+  float2 mine = make_float2(0.f, 0.f);
+  for (int r = 0; r < nb; ++r) {
+    float h1[2], h2[2];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int i = lane + 64 * q;
+      float a = i < d.h1 ? b1f[i] / s1b : 0.f;
+      if (i < d.h1)
+        for (int f = 0; f < d.n_in; ++f) {
+          bool folded = false;
+          for (int k = 0; k < nu; ++k) folded = folded || tf[2 + k] == f;
+          if (folded) continue;
+          const int s = f < d.n_own ? f : d.own4 + ((f - d.n_own) / d.msg_w) * d.m4 + (f - d.n_own) % d.msg_w;
+          a = fmaf(W1[(size_t)i * d.n_in + f], w_row[r * d.rs + actor_slot_off(d, s)], a);
+        }
+      h1[q] = fmaxf(a, 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j = lane + 64 * q;
+      float a = j < d.h2 ? B2[j] : 0.f;
+      for (int i = 0; i < d.h1; ++i) {
+        const float hv = __shfl(h1[i >> 6], i & 63);
+        if (j < d.h2) a = fmaf(W2[(size_t)j * d.h1 + i], hv, a);
+      }
+      h2[q] = fmaxf(a, 0.f);
+    }
+    float z0 = 0.f, z1 = 0.f;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const int j = lane + 64 * q;
+      if (j < d.h2) {
+        z0 = fmaf(W3[j], h2[q], z0);
+        z1 = fmaf(W3[d.h2 + j], h2[q], z1);
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      z0 += __shfl_xor(z0, off);
+      z1 += __shfl_xor(z1, off);
+    }
+    if (lane == r) mine = make_float2(z0, z1);
+  }
+  return mine;
+}
+
 // Persistent: every wave of the block shares the LDS weight image but owns its own 32-house tiles
 // (source rows, FSM words in a private LDS slice).  A tile runs as three stages — build (its LDS
 // rows from sources prefetched into registers), X (layers 1 and 2 on the MFMA pipe; the next tile's
@@ -393,11 +458,13 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
   }
   __syncthreads();
   // fp16-split form: the layer-1 bias with the house-independent features' contribution (the obs
-  // rows hold 0 in their slots), s1 x (b1 + sum_u W1[i][f_u] cf_u) in fp32 from the raw weights
+  // rows hold 0 in their slots), s1 x (b1 + sum_u W1[i][f_u] cf_u) in fp32 from the raw weights (s1
+  // keeps it below 2^kActorF16Bias for the features' bounds: k_actor_pack)
   const float* b1 = s_tail;
+  const float* b2 = s_tail + kActorRows;
+  const float s1b = PREC == 4 ? s_tail[kActorTailS1] : 1.f;  // (the layer-1 accumulator's scale)
   if (PREC == 4) {
     float* s_b1 = reinterpret_cast<float*>(smem + d.lds_b1);
-    const float s1 = s_tail[kActorTailS1];
     const int* tf = reinterpret_cast<const int*>(s_tail + kActorTailFold);
     const int nu = tf[0];
     for (int i = tid; i < kActorRows; i += nthr) {
@@ -406,13 +473,12 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
         const float* wr = d.w1raw + (size_t)i * d.n_in;
         for (int k = 0; k < nu; ++k) u = fmaf(wr[tf[2 + k]], s_cf[tf[2 + kActorMaxU + k]], u);
       }
-      s_b1[i] = s_tail[i] + s1 * u;
+      s_b1[i] = s_tail[i] + s1b * u;
     }
     __syncthreads();
     b1 = s_b1;
   }
   PSTAMP(0);
-  const float* b2 = s_tail + kActorRows;
   const float* w3 = s_tail + 2 * kActorRows;
   const float* b3 = s_tail + (2 + kActorNA) * kActorRows;
 
@@ -440,6 +506,11 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
   const int nsrc_max = ring ? lo + 32 + hi : 32;
   HouseRegs src{};
   int src_kind = 0;  // 0 none, 1 house, 2 halo
+  // (PREC 4) a row of this lane's current tile holds a seconds-since-off ratio int(sso / L) >= 2^15
+  // (a house off for more than 2^15 L seconds: beyond what fp16 carries with room to spare)
+  bool xbig = false;
+  const uint32_t xthr = dv.L <= 131071u ? 32768u * dv.L : 0xFFFFFFFFu;
+
   // source s of tile tl: ring = house b0 - lo + s (message source), table = house b0 + s (s < 32)
   auto source_of = [&](uint32_t tl, int s, HouseRegs& rg) -> int {
     const uint32_t b0 = tl * 32u;
@@ -463,7 +534,9 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
       const int hh = j < 0 ? (int)(j + lo) : (int)(lo + (j - (int64_t)n));
       const float* src = o.halo_next && hh >= lo ? o.halo_next + (size_t)(hh - lo) * M : o.halo_msg + (size_t)hh * M;
       for (int m = 0; m < M; ++m) row[m] = src[m];
+      if (PREC == 4) xbig = xbig || src[1] >= 32768.f;  // (a message's sso ratio, msg_from_regs)
     } else if (kind == 1) {
+      if (PREC == 4) xbig = xbig || hv_sso(rg.w) >= xthr;
       const int t = s - lo;
       if (ring) {
         msg_from_regs(p, o, rg, s_cf, row, dv);
@@ -479,12 +552,13 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
   };
   // ---- the stages of a tile (build, X, Y: the comment above k_actor)
   f32x2 zz[2];  // the tile's two logits per column block (partial over this lane's rows) between X and Y
-  float zsc = 1.f;  // (PREC 4) their scale back: 1 / the tile's layer-1 input scale
+  bool tile_exact = false;  // (PREC 4) the tile's values left fp16's range: its outputs come from the fallback pass
   // build: the tile's LDS rows from the prefetched sources (+ the table topologies' gathers)
   auto stage_build = [&](uint32_t tl) {
     const uint32_t b0 = tl * 32u;
     const int nb = (int)min(32u, n - b0);
     wave_sync();  // this wave's previous MFMA-operand reads of the rows are done (compiler ordering)
+    xbig = false;
     build(b0, nb, lane, src_kind, src);
     if (nsrc_max > 64 && lane + 64 < lo + nb + hi) {  // rings wider than 32 neighbours
       HouseRegs r2;
@@ -503,6 +577,7 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
           } else {
             msg_features(p, o, j, s_cf, row + k * d.m4, dv);
           }
+          if (PREC == 4) xbig = xbig || row[k * d.m4 + 1] >= 32768.f;  // (the message's sso ratio)
         }
       }
     }
@@ -543,15 +618,11 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     // wave do not wait out the LDS latency.
     constexpr int PF = 2;  // prefetch distance (steps)
     FragT hs[KS2][2][NS];
-    // fp16-split form (PREC 4): layer 2's operand relu(layer 1) must stay inside fp16's range.  The
-    // first pass tracks its maximum (on the bits: non-negative floats order as integers); when a lane
-    // holds a value >= 2^15 (ballot: rare) the tile's layer 1 runs again with its inputs and bias
-    // scaled by sig = 2^-k (exact), which brings the maximum below 2^15, and stage Y scales the logits
-    // back by 1 / sig.  A second pass still out of range, or a non-finite value (an obs feature
-    // beyond fp16), is counted in out.ovf (mdr_actor_status).
-    float sig = 1.f;
-#pragma unroll 1
-    for (int attempt = 0; attempt < (PREC == 4 ? 2 : 1); ++attempt) {
+    // fp16-split form (PREC 4): layer 2's operand relu(layer 1) must stay inside fp16's range.  Layer 1
+    // tracks its maximum (on the bits: non-negative floats order as integers); a tile holding a value
+    // >= 2^15, or an input beyond it (xbig), has its logits computed again in scalar fp32 from the raw
+    // weights (actor_tile_fp32: rare), which stage Y uses instead (tile_exact).
+    {
       uint32_t mbits = 0u;
       FragT xs[KS1][2][NS];
 #pragma unroll
@@ -565,9 +636,6 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
             const float4 x = *reinterpret_cast<const float4*>(w_row + a);
             xv[4 * e] = x.x; xv[4 * e + 1] = x.y; xv[4 * e + 2] = x.z; xv[4 * e + 3] = x.w;
           }
-          if (PREC == 4 && attempt)
-#pragma unroll
-            for (int j = 0; j < 8; ++j) xv[j] *= sig;
           split_operand<PREC>(xv, xs[ks][cb]);
         }
       constexpr int total = KS1 * MB;
@@ -587,8 +655,7 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
         const FragT* as = ring[st % (PF + 1)];
         f32x4* a1 = acc1[mb & 1];
         if (ks == 0) {
-          f32x4 bias = *reinterpret_cast<const f32x4*>(b1 + kActorRB * mb + 4 * g);
-          if (PREC == 4 && attempt) bias *= sig;
+          const f32x4 bias = *reinterpret_cast<const f32x4*>(b1 + kActorRB * mb + 4 * g);
 #pragma unroll
           for (int cb = 0; cb < 2; ++cb) a1[cb] = mfma_split<PREC>(as, xs[ks][cb], bias);
         } else {
@@ -615,23 +682,16 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
         }
       }
       if constexpr (PREC == 4) {
-        if (!__ballot(mbits >= 0x47000000u)) break;  // (every value < 2^15 = 32768.0f)
-        uint32_t m = mbits;
-        for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
-        if (attempt || m >= 0x7f800000u) {
-          if (lane == 0 && out.ovf) atomicAdd(out.ovf, 1u);
-          break;
-        }
-        sig = ldexpf(1.f, 14 - ((int)(m >> 23) - 127));  // max x sig < 2^15
+        tile_exact = __ballot(xbig || mbits >= 0x47000000u) != 0ull;  // (>= 2^15 = 32768.0f)
+        // (such a tile's outputs are written after the wave's other tiles: the fallback pass below)
       }
     }
-    zsc = PREC == 4 ? 1.f / sig : 1.f;  // (a power of two: exact)
     PSTAMP(3);
 
     // ---- layer 2 (acc2 = b2 + W2 · relu(H1)) fused with the output layer, row block by row block:
     // as soon as a block's four k-steps are done its ReLU'd rows enter the two logits (scalar fp32
-    // FMAs in block / row order) while the next block's MFMAs run
-    {
+    // FMAs in block / row order) while the next block's MFMAs run (not for a tile_exact tile)
+    if (!(PREC == 4 && tile_exact)) {
       constexpr int TOT = KS2 * MB;
       auto frag2 = [&](int s, int e) { return lds_frag<FragT>(s_w2, NF * ((s % KS2) * MB + s / KS2) + e, lane); };
       FragT ring[PF + 1][NS];
@@ -678,15 +738,16 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
   };
   // Y: output layer (fp32 VALU) + softmax + sampling + stores (+ the ON counts of the new actions)
   float u_next = 0.f;  // the sampling uniforms of this wave's next tile (stage_y, odd tiles)
-  auto stage_y = [&](uint32_t tl, uint32_t next, bool fresh) {
+  // skip: the tile's outputs come later (a tile_exact tile in the main loop; its uniforms for the next
+  // tile are still drawn)
+  // exact: the logits are zx (the fallback pass), lanes < 32 (house = lane)
+  auto stage_y = [&](uint32_t tl, uint32_t next, bool fresh, bool skip, bool exact, float2 zx) {
     const uint32_t b0 = tl * 32u;
     const int nb = (int)min(32u, n - b0);
     float z[2][kActorNA];
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) { z[cb][0] = zz[cb].x; z[cb][1] = zz[cb].y; }
-    if (PREC == 4)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) { z[cb][0] *= zsc; z[cb][1] *= zsc; }
+
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
@@ -697,8 +758,8 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     // lane l < 32 takes house l (column block l >> 4, column l & 15)
     const int r = lane & 31;
     const bool upper = (lane & 16) != 0;
-    const float z0 = (upper ? z[1][0] : z[0][0]) + b3[0];
-    const float z1 = (upper ? z[1][1] : z[0][1]) + b3[1];
+    const float z0 = (PREC == 4 && exact ? zx.x : upper ? z[1][0] : z[0][0]) + b3[0];
+    const float z1 = (PREC == 4 && exact ? zx.y : upper ? z[1][1] : z[0][1]) + b3[1];
     // softmax over the 2 actions (fp32, max-subtracted like torch; one reciprocal of the sum, as
     // ATen's vectorised softmax) + Categorical sample
     const float zmax = fmaxf(z0, z1);
@@ -720,7 +781,7 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
     }
     const int act = u < p0 ? 0 : 1;
     const float pa = act ? p1 : p0;
-    const bool writer = valid && lane < 32;
+    const bool writer = valid && lane < 32 && !skip;
     if (PREC == 4 && out.ovf) {  // a non-finite logit (mdr_actor_status)
       const bool bad = writer && !(__builtin_isfinite(z0) && __builtin_isfinite(z1));
       if (__ballot(bad) && lane == 0) atomicAdd(out.ovf, 1u);
@@ -755,15 +816,33 @@ __global__ void __launch_bounds__(64 * actor_max_waves(PREC, DEF)) k_actor(KPara
   // prefetch loads just issued (measured: no change of the kernel time, 117.9 vs 118.7-119.4 us —
   // the other waves of the SIMD cover that wait; kept because the wait has no purpose)
   __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+  uint64_t exact_tiles = 0ull;  // (PREC 4) the wave's tiles j left to the fallback pass (bit j)
   for (int j = 0; j < n_my; ++j) {
     const uint32_t vj = v0 + (uint32_t)j * stride;
     const uint32_t tj = real_tile(vj);
     const uint32_t next = vj + stride < nv ? real_tile(vj + stride) : ntile;  // (ntile: none)
     if (PROF && lane == 0) pacc[7] += 1;
     stage_x(tj, next);
-    stage_y(tj, next, (j & 1) == 0);
+    const bool defer = PREC == 4 && tile_exact && j < 64;
+    if (PREC == 4 && tile_exact && !defer && lane == 0 && out.ovf) atomicAdd(out.ovf, 1u);  // (> 64 tiles a wave)
+    if (defer) exact_tiles |= 1ull << j;
+    stage_y(tj, next, (j & 1) == 0, defer, false, make_float2(0.f, 0.f));
     if (j + 1 < n_my) stage_build(next);
   }
+  // (PREC 4) the fallback pass: each deferred tile's rows built again, its logits in scalar fp32 from
+  // the raw weights (actor_tile_fp32), then stage Y with fresh uniforms.  After the tile loop, so
+  // the loop's registers are free for it.
+  if (PREC == 4)
+    while (exact_tiles) {  // (wave-uniform)
+      const int j = __ffsll((long long)exact_tiles) - 1;
+      exact_tiles &= exact_tiles - 1ull;
+      const uint32_t tj = real_tile(v0 + (uint32_t)j * stride);
+      src_kind = source_of(tj, lane, src);
+      stage_build(tj);
+      const float2 zx = actor_tile_fp32(d, w_row, b1, s1b, s_tail, lane, (int)min(32u, n - tj * 32u));
+      stage_y(tj, ntile, true, false, true, zx);
+      if (lane == 0 && out.ovf) atomicAdd(out.ovf + 1, 1u);  // (mdr_actor_status 'exact')
+    }
   if (PROF && lane == 0) {
     for (int k = 0; k < 8; ++k) out.prof[(blockIdx.x * nw + wv) * 8 + k] = pacc[k];
   }

@@ -538,7 +538,7 @@ int mdr_create(mdr_ctx** out, const mdr_config* cfg) {
   k.q_on = c->d_tables;
   k.p_on = c->d_tables + MDR_MAX_CAP;
   if (hipMalloc(&c->d_flags, 16) != hipSuccess || hipMemset(c->d_flags, 0, 16) != hipSuccess)
-    return cleanup(fail(MDR_ENOMEM, "flags"));  // [0] params_bad, [1] the actor's fp16-range count
+    return cleanup(fail(MDR_ENOMEM, "flags"));  // [0] params_bad, [1..2] the actor's fp16-range counts
   if (hipMalloc(&c->d_tickets, kTicketWords * sizeof(unsigned)) != hipSuccess ||
       hipMemset(c->d_tickets, 0, kTicketWords * sizeof(unsigned)) != hipSuccess)
     return cleanup(fail(MDR_ENOMEM, "tickets"));
@@ -2032,7 +2032,7 @@ ActorDims actor_layout(const mdr_actor_spec& a, const mdr_obs_spec* sp, int nw, 
   d.lds_cf = d.off_end;
   d.lds_hist = d.lds_cf + align16(kObsConst * 4);
   d.lds_b1 = d.lds_hist + MDR_MAX_CAP * 4;
-  d.lds_wave = d.lds_b1 + (d.f16 ? kActorRows * 4 : 0);
+  d.lds_wave = d.lds_b1 + (d.f16 ? 2 * kActorRows * 4 + 16 : 0);  // (b1, b2, max of the fp16 split: mdr_actor.hip)
 
   d.w_zero = align16(d.nrows * rs * 4);
   d.w_hw = d.w_zero + 16;
@@ -2136,7 +2136,7 @@ int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
   const float* w3 = b2 + a.h2;
   const float* b3 = w3 + (size_t)kActorNA * a.h2;
   ActorFold fo{};
-  if (d.f16) {  // the folded features (mdr_actor.h ActorFold)
+  if (d.f16) {  // the folded features (mdr_actor.h ActorFold) and bounds on their values (obs_consts)
     int off[3], mk[3];
     int u = obs_uniform_own(sp->hvac_state, sp->solar_state, sp->thermal_state, fo.feat, fo.cf);
     fo.nu_own = u;
@@ -2147,6 +2147,18 @@ int actor_ensure_packed(mdr_ctx* c, const mdr_obs_spec* sp, hipStream_t st) {
         fo.cf[u++] = mk[j];
       }
     fo.nu = u;
+    double pmax = 0.0;
+    for (int k = 0; k < c->cfg.n_cap; ++k) pmax = std::max(pmax, fabs(c->cfg.cap_table[k] / c->cfg.cop));
+    const double R = sp->norm_reg_sig != 0.0 ? fabs(sp->norm_reg_sig) : 1.0;
+    for (int j = 0; j < u; ++j) {
+      const int k = fo.cf[j];
+      // P / R <= n_global P_on,max / R (every house on); the signal, solar, deadband and OD features
+      // are O(1) after norm.py's scaling (64 is a bound for the scale choice only: a value beyond it
+      // is still exact, k_actor's range check sends its tile to the fp32 fallback)
+      const double b = k == 3 ? (double)c->kp.n_global * pmax / R : k <= 2 ? 1.0 : k == 8 ? fabs(c->cfg.cop)
+                       : k == 9 ? fabs(c->cfg.lcf) : k == 10 ? fabs(sp->cfg_cap) : 64.0;
+      fo.cfmax[j] = (float)std::min(b, 3.0e38);
+    }
   }
   const int nthreads = (d.mb * (d.ks1 + kActorKS2) + 1) * 64;
   hipLaunchKernelGGL(k_actor_pack, dim3(blocks(nthreads, 256)), dim3(256), 0, st, d, fo, w1, b1, w2, b2, w3, b3,
@@ -2337,14 +2349,15 @@ int mdr_actor_load(mdr_ctx* c, const mdr_actor_spec* a, const float* w1, const f
 }
 
 int mdr_actor_status(mdr_ctx* c, int64_t* out, int n, void* stream) {
-  if (!c || !out || n < 2) return fail(MDR_EARG, "mdr_actor_status: need out[2]");
-  unsigned v = 0;
+  if (!c || !out || n < 3) return fail(MDR_EARG, "mdr_actor_status: need out[3]");
+  unsigned v[2] = {0u, 0u};
   HIP_TRY(hipStreamSynchronize(S(stream)));
-  HIP_TRY(hipMemcpy(&v, c->d_flags + 1, sizeof(unsigned), hipMemcpyDeviceToHost));
-  const unsigned z = 0;
-  HIP_TRY(hipMemcpy(c->d_flags + 1, &z, sizeof(unsigned), hipMemcpyHostToDevice));
-  out[0] = (int64_t)v;
+  HIP_TRY(hipMemcpy(v, c->d_flags + 1, sizeof(v), hipMemcpyDeviceToHost));
+  const unsigned z[2] = {0u, 0u};
+  HIP_TRY(hipMemcpy(c->d_flags + 1, z, sizeof(z), hipMemcpyHostToDevice));
+  out[0] = (int64_t)v[0];
   out[1] = c->actor_ready ? actor_kprec(c) : 0;
+  out[2] = (int64_t)v[1];
   return MDR_OK;
 }
 

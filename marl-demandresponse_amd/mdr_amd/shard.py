@@ -325,11 +325,12 @@ class HipShard:
         L.check(self.lib.mdr_actor_load_net(self.ctx, C.byref(net), w, b, self.stream()), "mdr_actor_load_net")
 
     def actor_status(self):
-        """mdr_actor_status (synchronises): {range_faults: fused fp16-split tiles that met a non-finite
-        logit since the last call, kernel_prec: 1 bf16 / 3 bf16x3 / 4 fp16 split / 6 three-way bf16}."""
-        out = (C.c_int64 * 2)()
-        L.check(self.lib.mdr_actor_status(self.ctx, out, 2, self.stream()), "mdr_actor_status")
-        return {"range_faults": int(out[0]), "kernel_prec": int(out[1])}
+        """mdr_actor_status (synchronises; counts since the last call): {range_faults: fused fp16-split
+        tiles that met a non-finite logit, kernel_prec: 1 bf16 / 3 bf16x3 / 4 fp16 split / 6 three-way
+        bf16, exact: tiles whose values left fp16's range, their logits computed in scalar fp32}."""
+        out = (C.c_int64 * 3)()
+        L.check(self.lib.mdr_actor_status(self.ctx, out, 3, self.stream()), "mdr_actor_status")
+        return {"range_faults": int(out[0]), "kernel_prec": int(out[1]), "exact": int(out[2])}
 
     def actor_fused(self, spec) -> bool:
         """True when the loaded actor runs the fused k_actor for this obs layout (else the chain)."""

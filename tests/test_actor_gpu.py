@@ -338,12 +338,11 @@ def test_actor_fp32_rollout_equals_loop(torch_gpu, precision):
 
 
 def test_actor_fp16_split_range(torch_gpu):
-    """The fp16-split fp32 form's range limit is visible, not silent: houses whose seconds-since-off
-    ratio (an obs feature, sso / L) exceeds fp16's 65504 cannot be represented, and
-    mdr_actor_status counts their tiles; the three-way bf16 form has no such limit and matches torch
-    fp32 there.  Every other house's probabilities stay within the fp32 tolerance in both forms —
-    including the tiles whose hidden activations the large features push beyond fp16 (k_actor runs
-    their layer 1 again at a power-of-two scale)."""
+    """The fp16-split fp32 form beyond fp16's range: houses off for ~34 years (sso saturated at
+    2^30 - 1 s: a seconds-since-off ratio of ~2.7e7, beyond fp16's 65504, in their own rows and their
+    ring neighbours' messages) make k_actor compute their tiles' logits in scalar fp32 from the raw
+    weights (mdr_actor_status 'exact'); every house's probabilities then match torch fp32 within the
+    fp32 tolerance, as the three-way bf16 form's do.  A normal state needs no such tile."""
     torch = torch_gpu
     n = 3001
     props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
@@ -351,26 +350,25 @@ def test_actor_fp16_split_range(torch_gpu):
     env = make_env(props, 5)
     for _ in range(3):
         env.step_tensor(torch.zeros(n, dtype=torch.uint8, device="cuda"))
-    # houses 100..131 (one tile) off for ~34 years: sso saturated at 2^30 - 1 (hvac bits 0-29)
-    env.shard.hvac[100:132] = 0x3FFFFFFF
     F = env.obs_spec().n_feat
-    obs = env.obs_tensor().clone()
-    assert float(obs[100:132].abs().max()) > 65504.0
-    actor = gu.calibrated_actor(F, np.ones(F), seed=4).to("cuda")
-    with torch.no_grad():
-        tp = actor(obs).cpu().numpy()
-    ok = np.ones(n, bool)
-    ok[95:137] = False  # (the saturated houses and the houses whose ring messages carry them)
-    for precision in FP32S:
-        da = device_actor(env, actor, precision)
-        da.status()  # (clear)
-        probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
-        da.select_actions(probs=probs, count_next=False)
-        st = da.status()
-        p = probs.cpu().numpy()
-        assert np.abs(p[ok] - tp[ok]).max() < 4e-6, precision
-        if precision == "fp32":
-            assert st["kernel_prec"] == 4 and st["range_faults"] >= 1, st
-        else:
-            assert st["kernel_prec"] == 6 and st["range_faults"] == 0, st
-            assert np.all(np.isfinite(p)) and np.abs(p - tp).max() < 4e-6
+    actor = gu.calibrated_actor(F, env.obs_tensor().abs().amax(0).double().cpu().numpy(), seed=4).to("cuda")
+    for big in (False, True):
+        if big:  # houses 100..131 off for ~34 years (hvac bits 0-29 saturated)
+            env.shard.hvac[100:132] = 0x3FFFFFFF
+        obs = env.obs_tensor().clone()
+        assert (float(obs[100:132].abs().max()) > 65504.0) == big
+        with torch.no_grad():
+            tp = actor(obs).cpu().numpy()
+        for precision in FP32S:
+            da = device_actor(env, actor, precision)
+            da.status()  # (clear)
+            probs = torch.empty((n, 2), dtype=torch.float32, device="cuda")
+            da.select_actions(probs=probs, count_next=False)
+            st = da.status()
+            p = probs.cpu().numpy()
+            assert np.all(np.isfinite(p)) and np.abs(p - tp).max() < 4e-6, (big, precision, np.abs(p - tp).max())
+            assert st["range_faults"] == 0, st
+            if precision == "fp32":
+                assert st["kernel_prec"] == 4 and (st["exact"] >= 1) == big, st
+            else:
+                assert st["kernel_prec"] == 6 and st["exact"] == 0, st

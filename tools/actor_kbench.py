@@ -45,7 +45,7 @@ def main():
     us = e0.elapsed_time(e1) * 1e3 / a.reps
     flops = 2 * sum(l.in_features * l.out_features for l in actor.fc) * n
     st = da.status()
-    print(f"houses={n} precision={a.precision} kernel_prec={st['kernel_prec']} range_faults={st['range_faults']}: k_actor {us:.1f} us/launch, {flops / us / 1e6:.1f} TFLOP/s "
+    print(f"houses={n} precision={a.precision} kernel_prec={st['kernel_prec']} range_faults={st['range_faults']} exact_tiles={st['exact']}: k_actor {us:.1f} us/launch, {flops / us / 1e6:.1f} TFLOP/s "
           f"algorithmic ({flops / us / 1e6 / bench.BF16_PEAK_TFS:.3f} of dense bf16 peak)", flush=True)
 
 
