@@ -117,8 +117,10 @@ def parse():
                     help="step: env.step with fused random actions (the BASELINE metric); actor: "
                          "config C5, MA-PPO actor select_actions fused with the obs, then env.step; "
                          "greedy: config C3, device greedy-myopic controller then env.step")
-    ap.add_argument("--precision", default="bf16x3", choices=["bf16x3", "fp32", "bf16"],
-                    help="actor MFMA precision (--workload actor)")
+    ap.add_argument("--precision", default="fp32", choices=["bf16x3", "fp32", "bf16"],
+                    help="actor MFMA precision (--workload actor; fp32 = the reference Actor's)")
+    ap.add_argument("--fp32-form", default="f16_split", choices=["f16_split", "bf16_split3"],
+                    help="the fp32 precision's arithmetic (MDR_OPT_ACTOR_FP32_FORM)")
     ap.add_argument("--comm", default="default", choices=["default", "none", "rccl", "torch", "host"],
                     help="exchange for the sharded path (default: rccl when WORLD_SIZE > 1); "
                          "'rccl' at world 1 exercises the sharded C loop on one GPU; 'host' = the same C loops "
@@ -384,7 +386,7 @@ def main():
         from mdr_amd.actor import DeviceActor, make_actor
 
         dactor = DeviceActor(env, make_actor(env.obs_spec().n_feat, 2, [100, 100], seed=1),
-                             precision=args.precision)
+                             precision=args.precision, fp32_form=args.fp32_form)
     g_act = None
     if args.workload == "greedy":
         if world > 1:
@@ -553,19 +555,28 @@ def main():
         ev1.record(cur)
         torch.cuda.synchronize()
         actor_ms = ev0.elapsed_time(ev1) / K
-        actor_fp32_ms = None
-        if args.precision != "fp32":  # the reference's own precision, timed beside the headline form
-            from mdr_amd.actor import DeviceActor
+        actor_status = dactor.status()  # (the headline launches: tiles left to the fp32 fallback, faults)
+        # the other precisions / forms, timed the same way beside the headline one
+        from mdr_amd.actor import DeviceActor
 
-            d32 = DeviceActor(env, dactor.actor, precision="fp32")
-            d32.select_actions(action=act_buf, prob=prob_buf, count_next=False)
+        beside = {}
+        for name, kw in (("fp32_f16_split", {"precision": "fp32", "fp32_form": "f16_split"}),
+                         ("fp32_bf16_split3", {"precision": "fp32", "fp32_form": "bf16_split3"}),
+                         ("bf16x3", {"precision": "bf16x3"})):
+            if kw["precision"] == args.precision and kw.get("fp32_form", args.fp32_form) == args.fp32_form:
+                continue
+            dx = DeviceActor(env, dactor.actor, **kw)
+            dx.select_actions(action=act_buf, prob=prob_buf, count_next=False)
             torch.cuda.synchronize()
             ev0.record(cur)
             for _ in range(K):
-                d32.select_actions(action=act_buf, prob=prob_buf, count_next=False)
+                dx.select_actions(action=act_buf, prob=prob_buf, count_next=False)
             ev1.record(cur)
             torch.cuda.synchronize()
-            actor_fp32_ms = ev0.elapsed_time(ev1) / K
+            beside[name] = ev0.elapsed_time(ev1) / K
+        # (each DeviceActor loaded its weights into the shard: the headline actor again)
+        env.shard.set_option("actor_fp32_form", L.FP32_F16_SPLIT if args.fp32_form == "f16_split" else L.FP32_BF16_SPLIT3)
+        dactor.load_weights()
         launches = K
         kern_ms = max(gpu_ms / args.steps - actor_ms, 1e-6)  # the step kernel's share of a tick
         bytes_launch = BYTES_PER_HOUSE_STEP * n_loc
@@ -639,27 +650,32 @@ def main():
         flops_house = 2 * sum(l.in_features * l.out_features for l in a.fc)  # 30,400 at F = 50
         flops_launch = flops_house * n_loc
         tfs = flops_launch / (actor_ms * 1e-3) / 1e12
-        out["dtype"] = f"f64 env step + {args.precision} MFMA actor (fp32 accumulate)"
+        prec_name = ("fp32 (fp16 hi/lo split, 3 products on v_mfma_f32_16x16x32_f16)" if args.precision == "fp32"
+                     and args.fp32_form == "f16_split" else "fp32 (three-way bf16 split, 6 products)"
+                     if args.precision == "fp32" else args.precision)
+        out["dtype"] = f"f64 env step + {prec_name} MFMA actor (fp32 accumulate)"
         out["data"] = ("synthetic (device Philox population, reference noise model); actor = the "
                        "reference MAPPO init (torch seed 1), actions sampled on device")
         out["config"]["workload"] = ("C5: 1M houses, MA-PPO actor select_actions fused with the obs "
                                      "(one launch) -> env.step (one launch) per tick, hipGraph chunks")
         out["config"]["action_mode"] = "mappo_actor"
-        out["config"]["actor"] = {"layers": [a.fc[0].in_features, 100, 100, 2], "precision": args.precision}
+        out["config"]["actor"] = {"layers": [a.fc[0].in_features, 100, 100, 2], "precision": args.precision,
+                                  "fp32_form": args.fp32_form if args.precision == "fp32" else None,
+                                  "status": actor_status}
         out["roofline"] = {"bound": "mfma", "achieved": tfs, "peak": BF16_PEAK_TFS, "unit": "TFLOP/s",
                            "frac": tfs / BF16_PEAK_TFS, "traffic": None, "kernel": "mdr::k_actor",
                            "kernel_avg_us": actor_ms * 1e3, "launches_timed": launches,
                            "algorithmic_flops_per_launch": flops_launch, "flops_per_house": flops_house,
-                           "mfma_products_per_mac": {"bf16": 1, "bf16x3": 3, "fp32": 6}[args.precision],
+                           "mfma_products_per_mac": {"bf16": 1, "bf16x3": 3,
+                                                     "fp32": 3 if args.fp32_form == "f16_split" else 6}[args.precision],
                            "step_share": {"what": "launch-stream time per tick minus k_actor's time: the step "
                                                   "kernel's share of a tick (not a kernel duration)",
                                           "us_per_tick": kern_ms * 1e3}}
-        if actor_fp32_ms is not None:
-            out["roofline"]["fp32_mode"] = {
-                "what": "the same k_actor launches in fp32-faithful mode (MFMA fp32 emulated by 6 bf16 products; "
-                        "the reference's own precision), timed the same way",
-                "kernel_avg_us": actor_fp32_ms * 1e3,
-                "achieved_tflops": flops_launch / (actor_fp32_ms * 1e-3) / 1e12}
+        out["roofline"]["beside"] = {
+            name: {"kernel_avg_us": ms * 1e3, "achieved_tflops": flops_launch / (ms * 1e-3) / 1e12}
+            for name, ms in beside.items()}
+        out["roofline"]["beside"]["what"] = ("the same k_actor launches in the other arithmetic forms, timed the "
+                                             "same way (fp32 = the reference Actor's precision)")
     if (dactor is None and g_act is None and rank == 0 and window > 0 and args.above_mall_houses > 0
             and args.mode == "random"):
         out["roofline"]["above_mall"] = above_mall(args.above_mall_houses, args, kern)

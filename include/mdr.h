@@ -177,6 +177,10 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           k_gq_finish ranks and decides; 0 = the bins pass every call (k_gq_bins,
  *                           k_gq_compact, k_gq_select: faster when the budget jumps across the cluster
  *                           every call)
+ *   MDR_OPT_GQ_FUSED        mdr_greedy_rollout: 1 (default) = the fused tick, one decision launch per tick
+ *                           (k_gq_decide2: the previous step's epilogue counted the keys and the band's
+ *                           houses, the step applies the decision from the pre-step keys); 0 = the
+ *                           mdr_ctrl_greedy + mdr_step tick (bit-identical)
  *   MDR_OPT_ACTOR_GENERIC   1 = k_actor runs its generic form for the reference's default obs layout too
  *                           (0, default: that layout runs the form specialised for it, mdr_actor.hip DEF)
  *   MDR_OPT_ACTOR_FP32_FORM the fused actor's MDR_PREC_FP32 arithmetic: MDR_FP32_F16_SPLIT (default) =
@@ -192,7 +196,7 @@ int mdr_params_changed(mdr_ctx* ctx);
 enum { MDR_OPT_STEP_TPW = 1, MDR_OPT_FASTDIV = 2, MDR_OPT_WINDOW_PIPELINE = 3, MDR_OPT_SHARDED_OVERLAP = 4,
        MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7,
        MDR_OPT_HALO_OVERLAP = 9, MDR_OPT_ACTOR_GENERIC = 10, MDR_OPT_HALO_IN_COUNTS = 12,
-       MDR_OPT_GQ_BAND = 13, MDR_OPT_ACTOR_FP32_FORM = 14 };
+       MDR_OPT_GQ_BAND = 13, MDR_OPT_ACTOR_FP32_FORM = 14, MDR_OPT_GQ_FUSED = 15 };
 enum { MDR_FP32_F16_SPLIT = 0, MDR_FP32_BF16_SPLIT3 = 1 };
 /* (8 was MDR_OPT_ACTOR_PINGPONG, a k_actor schedule measured slower and retired in r04: rejected) */
 enum { MDR_THERMAL_EXACT = 0, MDR_THERMAL_AFFINE = 1 };
@@ -386,6 +390,14 @@ int mdr_greedy_rollout(mdr_ctx* ctx, int n, const mdr_tick* ticks, uint8_t* acti
  * the first superbin of the band the next GQ step counts, the band's width in superbins}.
  * Misses = calls - skips. */
 int mdr_greedy_band(mdr_ctx* ctx, uint64_t* out);
+/* The fused tick's counters (synchronises): out[6] = {decisions, band hits, misses (the decision's own
+ * pass over the cluster), exact decisions (gq_exact), the last decision's mode (0 window, 1 all taken,
+ * 2 every house's byte), the last window's houses}. */
+int mdr_greedy_fused_diag(mdr_ctx* ctx, uint64_t* out);
+/* Diagnostics: on != 0 makes the following fused decisions record each block's phase clocks (the
+ * 100 MHz constant clock; [kGqSelBlocks = 256][16] words, slot 10 = 1 in the deciding block); out, when
+ * non-NULL, receives the current record (synchronises); on = 0 stops. */
+int mdr_greedy_fused_stamps(mdr_ctx* ctx, int on, uint64_t* out);
 
 /* Sharded greedy, histogram form (per-rank work O(N/G + window)): the same
  * select as mdr_ctrl_greedy with the caller's collectives between its stages, every rank deciding

@@ -136,6 +136,12 @@ struct mdr_ctx {
   bool gq_slab_zeroed = false;           // the codes' producer zeroed the slab the decisions count into
                                          // (not when its step counted a lookahead there)
   bool gq_band = true;                   // MDR_OPT_GQ_BAND: k_gq_binsc (the predicted band) vs k_gq_bins
+  // the fused greedy tick (mdr_greedy_rollout; mdr_kernels.h GqfBufs)
+  bool gq_fused = true;                  // MDR_OPT_GQ_FUSED
+  GqfBufs fz{};
+  int64_t fz_cap_n = 0;                  // the cluster size fz is allocated for
+  int fz_par = 0;                        // the parity the last producer wrote
+  bool fz_ready = false;                 // ... for the current state (the last step's GQ = 2 epilogue)
   int gq_nparts = 0;                     //   (from the last step's epilogue: its grid's partials)
   // multi-GPU
   ncclComm_t comm = nullptr;
@@ -330,22 +336,22 @@ int launch_step_on(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, con
     GqOut go{};
     if (epi) {
       if (int rc = gq_hist_produce(c, st)) return rc;
-      go = GqOut{gq_codes(c), c->g_part, c->g_hist, c->g_sel, c->g_map};
+      go = GqOut{nullptr, gq_codes(c), c->g_part, c->g_hist, c->g_sel, c->g_map};
     }
 #define MDR_LAUNCH_PIPE(T, A, LA, G)                                                                     \
   hipLaunchKernelGGL((k_step_pipe<T, A, LA, G>), grid, dim3(64 * nwv), 0, st, kp, action, tk, tkp, cur, reward, \
-                     p_out, nxt, zer, go)
+                     p_out, nxt, zer, go, GqfBufs{}, 0)
     if (hot_random) {
-      if (tpw == 8) MDR_LAUNCH_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false);
-      else if (tpw == 4) MDR_LAUNCH_PIPE(4, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false);
-      else if (tpw == 2) MDR_LAUNCH_PIPE(2, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false);
-      else MDR_LAUNCH_PIPE(1, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false);
+      if (tpw == 8) MDR_LAUNCH_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM, 0);
+      else if (tpw == 4) MDR_LAUNCH_PIPE(4, MDR_ACT_RANDOM, MDR_ACT_RANDOM, 0);
+      else if (tpw == 2) MDR_LAUNCH_PIPE(2, MDR_ACT_RANDOM, MDR_ACT_RANDOM, 0);
+      else MDR_LAUNCH_PIPE(1, MDR_ACT_RANDOM, MDR_ACT_RANDOM, 0);
     } else if (epi) {
-      if (tpw >= 4) MDR_LAUNCH_PIPE(4, MDR_ACT_BUFFER, 0, true);
-      else MDR_LAUNCH_PIPE(2, MDR_ACT_BUFFER, 0, true);
+      if (tpw >= 4) MDR_LAUNCH_PIPE(4, MDR_ACT_BUFFER, 0, 1);
+      else MDR_LAUNCH_PIPE(2, MDR_ACT_BUFFER, 0, 1);
     } else {
-      if (tpw >= 4) MDR_LAUNCH_PIPE(4, MDR_ACT_BUFFER, 0, false);
-      else MDR_LAUNCH_PIPE(2, MDR_ACT_BUFFER, 0, false);
+      if (tpw >= 4) MDR_LAUNCH_PIPE(4, MDR_ACT_BUFFER, 0, 0);
+      else MDR_LAUNCH_PIPE(2, MDR_ACT_BUFFER, 0, 0);
     }
 #undef MDR_LAUNCH_PIPE
     LAUNCH_CHECK("k_step_pipe");
@@ -374,6 +380,7 @@ int launch_step(mdr_ctx* c, const uint8_t* action, int mode, TickArgs tk, const 
                 double* reward, int lookahead, int ctrl, uint8_t* ctrl_out, double* p_out,
                 hipStream_t st) {
   c->gq_keys_ready = false;
+  c->fz_ready = false;
   int rc = launch_step_on(c, action, mode, tk, tkp, reward, lookahead, ctrl, ctrl_out, p_out,
                           slab_at(c, c->ring), slab_at(c, c->ring + 1), slab_at(c, c->ring + 2), 0, st);
   if (rc) return rc;
@@ -394,7 +401,10 @@ static void drop_begun(mdr_ctx* c) {
     c->begun.on = false;
     c->wslab_dirty = true;
   }
-  if (c) c->gq_keys_ready = false;  // (every such entry point may change the state)
+  if (c) {
+    c->gq_keys_ready = false;  // (every such entry point may change the state)
+    c->fz_ready = false;
+  }
 }
 
 #ifndef MDR_SRC_HASH
@@ -636,6 +646,9 @@ int mdr_destroy(mdr_ctx* c) {
   hipFree(c->g_part); hipFree(c->g_hist); hipFree(c->g_sel); hipFree(c->g_win);
   hipFree(c->g_sorted); hipFree(c->g_map); hipFree(c->g_range); hipFree(c->g_tickets);
   hipFree(c->d_tickets);
+  hipFree(c->fz.par[0]); hipFree(c->fz.bkt[0]); hipFree(c->fz.mbkt); hipFree(c->fz.map[0]); hipFree(c->fz.sel);
+  hipFree(c->fz.dec);
+  hipFree(c->fz.stamps);
   hipFree(c->d_c5);
   if (c->comm) ncclCommDestroy(c->comm);
   delete c;
@@ -658,6 +671,7 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_HALO_OVERLAP: c->halo_overlap = value != 0; break;
     case MDR_OPT_HALO_IN_COUNTS: c->halo_in_counts = value != 0; break;
     case MDR_OPT_GQ_BAND: c->gq_band = value != 0; break;
+    case MDR_OPT_GQ_FUSED: c->gq_fused = value != 0; break;
     case MDR_OPT_ACTOR_GENERIC: c->actor_generic = value != 0; break;
     case MDR_OPT_ACTOR_FP32_FORM:
       if (value != MDR_FP32_F16_SPLIT && value != MDR_FP32_BF16_SPLIT3)
@@ -1002,7 +1016,7 @@ static int launch_step_window(mdr_ctx* c, int mode, bool ka, const uint8_t* acti
 static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t* action, int64_t act_stride,
                            int mode, double* reward, int64_t rew_stride, double* p_out, bool shd,
                            hipStream_t st, bool counted = false, bool pipe = false,
-                           const mdr_tick* host_ticks = nullptr) {
+                           const mdr_tick* host_ticks = nullptr, bool ka_red = false) {
   const int nw = (n + c->win - 1) / c->win;
   const int base = n / nw, rem = n % nw;
   auto wsz = [&](int w) { return base + (w < rem ? 1 : 0); };
@@ -1078,6 +1092,7 @@ static int window_launches(mdr_ctx* c, int n, const TickArgs* tk, const uint8_t*
       }
       dv.tick0 = host_ticks[0].tick;
       if (nw == 1) dv.p_out = p_out;
+      if (ka_red) dv.red = win_red_ptr(c, slot(0));  // (sharded, begun: P from the allreduced totals)
       if (int rc = launch_step_window(c, mode, true, a, act_stride, tk, K, la, rec(0), reward, rew_stride, c->d_onb,
                                       c->d_wah, slot(1), dv, st))
         return rc;
@@ -1164,6 +1179,7 @@ int mdr_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t* action,
                 int mode, double* reward, int64_t rew_stride, double* p_out, int use_graph, void* stream) {
   if (!c || !ticks || !reward || n < 1) return fail(MDR_EARG, "mdr_rollout: bad argument");
   c->gq_keys_ready = false;
+  c->fz_ready = false;
   if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout: context not bound");
   if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout: bad action source");
   if (c->kp.penalty_mode != MDR_PEN_INDIVIDUAL_L2)
@@ -1232,6 +1248,7 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
                       void* stream) {
   if (!c || n < 1) return fail(MDR_EARG, "mdr_rollout_begin: bad argument");
   c->gq_keys_ready = false;
+  c->fz_ready = false;
   if (!c->bound) return fail(MDR_ESTATE, "mdr_rollout_begin: context not bound");
   if (!check_mode(mode) || (mode == MDR_ACT_BUFFER && !action)) return fail(MDR_EARG, "mdr_rollout_begin: bad action source");
   if (c->begun.on) c->wslab_dirty = true;  // a previous early count that no rollout consumed
@@ -1255,10 +1272,8 @@ int mdr_rollout_begin(mdr_ctx* c, int n, uint64_t tick0, const uint8_t* action, 
                     true);
   if (rc) return rc;
   if (sharded) {  // every rank's per-tick class totals (its count kernel's last block), summed
+    // (the KA step derives each tick's P from these totals itself: no k_win_records launch, r06)
     if (int rc2 = comm_allreduce(c, win_red_ptr(c, c->d_wslab), (size_t)k0 * c->kp.n_cap, 0, st)) return rc2;
-    hipLaunchKernelGGL(k_win_records, dim3(1), dim3(kWindowMax), 0, st, c->kp, c->d_wslab, k0,
-                       (const TickArgs*)nullptr, (double*)nullptr);
-    LAUNCH_CHECK("k_win_records (P only)");
   }
   c->wslab_dirty = false;
   c->begun.sharded = sharded;
@@ -1413,6 +1428,7 @@ int greedy_scratch(mdr_ctx* c, int64_t n) {
   c->g_part = nullptr; c->g_hist = nullptr; c->g_sel = nullptr; c->g_win = nullptr;
   c->g_sorted = nullptr;
   c->gq_keys_ready = false;
+  c->fz_ready = false;
   c->gq_hist_dirty = false;
   HIP_TRY(hipMalloc(&c->g_key, n * sizeof(double)));
   HIP_TRY(hipMalloc(&c->g_key2, n * sizeof(double)));
@@ -1487,6 +1503,7 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
   const bool keys_ready = c->gq_keys_ready && c->g_cap >= c->kp.n;  // (the last step's epilogue wrote them)
   drop_begun(c);
   c->gq_keys_ready = false;  // (the histogram is consumed below)
+  c->fz_ready = false;
   int rc = greedy_scratch(c, c->kp.n);
   if (rc) return rc;
   hipStream_t st = S(stream);
@@ -1584,6 +1601,107 @@ int mdr_greedy_state(mdr_ctx* c, uint64_t* out) {
 // the step with those actions (environment.py:86-106), whose epilogue writes the next call's keys
 // — Environment.greedy_actions + step_tensor(ctrl='greedy_keys') per tick, without a host round
 // trip between them
+}  // extern "C"
+
+namespace {
+// the fused tick's buffers (mdr_kernels.h GqfBufs), for a cluster of n houses
+int gqf_scratch(mdr_ctx* c, int64_t n) {
+  if (c->fz_cap_n >= n && c->fz.par[0]) return MDR_OK;
+  HIP_TRY(hipDeviceSynchronize());
+  hipFree(c->fz.par[0]); hipFree(c->fz.bkt[0]); hipFree(c->fz.mbkt); hipFree(c->fz.map[0]); hipFree(c->fz.sel);
+  hipFree(c->fz.dec);
+  unsigned long long* keep_stamps = c->fz.stamps;
+  c->fz = GqfBufs{};
+  c->fz.stamps = keep_stamps;
+  c->fz_ready = false;
+  // bucket capacity: 4x the houses a (copy, bin) holds on average under an equi-depth map, >= 32
+  const int64_t avg = (n + (int64_t)gq_bins_eff(c->kp.n_global) * kGqCopies - 1) / ((int64_t)gq_bins_eff(c->kp.n_global) * kGqCopies);
+  const int cap = (int)std::max<int64_t>(32, 4 * avg);
+  unsigned* regions = nullptr;
+  HIP_TRY(hipMalloc(&regions, (2 * (size_t)kGqfParWords + kGqfMissWords) * sizeof(unsigned)));
+  HIP_TRY(hipMemset(regions, 0, (2 * (size_t)kGqfParWords + kGqfMissWords) * sizeof(unsigned)));
+  c->fz.par[0] = regions;
+  c->fz.par[1] = regions + kGqfParWords;
+  c->fz.miss = regions + 2 * kGqfParWords;
+  uint4* bk = nullptr;
+  const size_t nb = (size_t)kGqCopies * kGqBand * 64 * cap;
+  HIP_TRY(hipMalloc(&bk, 2 * nb * sizeof(uint4)));
+  c->fz.bkt[0] = bk;
+  c->fz.bkt[1] = bk + nb;
+  HIP_TRY(hipMalloc(&c->fz.mbkt, (size_t)kGqCopies * 128 * cap * sizeof(uint4)));
+  c->fz.cap = cap;
+  c->fz.mcap = cap;
+  uint32_t* maps = nullptr;
+  HIP_TRY(hipMalloc(&maps, 2 * kGqCells * sizeof(uint32_t)));
+  c->fz.map[0] = maps;
+  c->fz.map[1] = maps + kGqCells;
+  HIP_TRY(hipMalloc(&c->fz.sel, kGqSelBytes));
+  {
+    unsigned char init[kGqSelBytes] = {};
+    uint32_t map[kGqCells];
+    gqf_sel_init(init, map);
+    HIP_TRY(hipMemcpy(c->fz.sel, init, kGqSelBytes, hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->fz.map[0], map, sizeof(map), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->fz.map[1], map, sizeof(map), hipMemcpyHostToDevice));
+  }
+  HIP_TRY(hipMalloc(&c->fz.dec, (size_t)n));
+  c->fz_cap_n = n;
+  c->fz_par = 0;
+  return MDR_OK;
+}
+
+// the fused tick's step: k_step_pipe<..., GQ = 2> applying the decision of parity par, producing 1 - par
+int launch_step_fused(mdr_ctx* c, const TickArgs& tk, double* reward, uint8_t* act_out, double* p_out, int par,
+                      hipStream_t st) {
+  const KParams kp = c->kp;
+  const int tpw = c->tpw >= 4 ? 4 : 2;
+  const unsigned nb = blocks(blocks(kp.n, 128), kStepGqWaves * tpw);
+  if ((int)nb > c->gq_parts_cap) return fail(MDR_ESTATE, "fused greedy: the step grid exceeds the partials buffer");
+  GqOut go{act_out, nullptr, c->g_part, nullptr, nullptr, nullptr};
+  unsigned long long *cur = slab_at(c, c->ring), *nxt = slab_at(c, c->ring + 1), *zer = slab_at(c, c->ring + 2);
+  if (tpw >= 4)
+    hipLaunchKernelGGL((k_step_pipe<4, MDR_ACT_BUFFER, 0, 2>), dim3(nb), dim3(64 * kStepGqWaves), 0, st, kp,
+                       (const uint8_t*)c->fz.dec, tk, (const TickArgs*)nullptr, cur, reward, p_out, nxt, zer, go, c->fz, par);
+  else
+    hipLaunchKernelGGL((k_step_pipe<2, MDR_ACT_BUFFER, 0, 2>), dim3(nb), dim3(64 * kStepGqWaves), 0, st, kp,
+                       (const uint8_t*)c->fz.dec, tk, (const TickArgs*)nullptr, cur, reward, p_out, nxt, zer, go, c->fz, par);
+  LAUNCH_CHECK("k_step_pipe (fused greedy)");
+  c->gq_nparts = (int)nb;
+  c->ring = (c->ring + 1) % 3;
+  return MDR_OK;
+}
+}  // namespace
+
+extern "C" {
+
+// diagnostics: record k_gq_decide2's per-block phase clocks (100 MHz) of the following calls into a
+// device buffer of kGqSelBlocks x kGqfStampWords words (n = 0: stop); read it back with mdr_greedy_fused_stamps
+int mdr_greedy_fused_stamps(mdr_ctx* c, int on, uint64_t* out) {
+  if (!c) return fail(MDR_EARG, "mdr_greedy_fused_stamps: null ctx");
+  if (out && c->fz.stamps)
+    HIP_TRY(hipMemcpy(out, c->fz.stamps, kGqSelBlocks * kGqfStampWords * sizeof(uint64_t), hipMemcpyDeviceToHost));
+  if (on && !c->fz.stamps) {
+    HIP_TRY(hipMalloc(&c->fz.stamps, kGqSelBlocks * kGqfStampWords * sizeof(uint64_t)));
+    HIP_TRY(hipMemset(c->fz.stamps, 0, kGqSelBlocks * kGqfStampWords * sizeof(uint64_t)));
+  }
+  if (!on && c->fz.stamps) {
+    HIP_TRY(hipDeviceSynchronize());
+    hipFree(c->fz.stamps);
+    c->fz.stamps = nullptr;
+  }
+  return MDR_OK;
+}
+
+int mdr_greedy_fused_diag(mdr_ctx* c, uint64_t* out) {
+  if (!c || !out) return fail(MDR_EARG, "mdr_greedy_fused_diag: null argument");
+  for (int k = 0; k < 6; ++k) out[k] = 0;
+  if (!c->fz.sel) return MDR_OK;
+  unsigned char h[kGqSelBytes];
+  HIP_TRY(hipMemcpy(h, c->fz.sel, kGqSelBytes, hipMemcpyDeviceToHost));
+  gqf_diag_of(h, out);
+  return MDR_OK;
+}
+
 int mdr_greedy_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, uint8_t* action, int64_t act_stride,
                        double* reward, int64_t rew_stride, double* p_out, void* stream) {
   if (!c || (n > 0 && (!ticks || !action || !reward))) return fail(MDR_EARG, "mdr_greedy_rollout: null argument");
@@ -1592,6 +1710,41 @@ int mdr_greedy_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, uint8_t* action
   if (c->world > 1)  // (a shard-local decision and step would use shard-local counts: per-tick loop)
     return fail(MDR_ESTATE, "mdr_greedy_rollout: single-GPU only (sharded contexts: the per-tick greedy + step loop)");
   hipStream_t st = S(stream);
+  // the fused tick (MDR_OPT_GQ_FUSED): individual_L2 on the software-pipelined step, <= 4 classes
+  const bool fused = c->gq_fused && !c->greedy_sort && c->kp.n_cap <= 4 && c->tpw >= 1 && c->fastdiv &&
+                     c->kp.penalty_mode == MDR_PEN_INDIVIDUAL_L2 && n > 0;
+  if (fused) {
+    const bool ready = c->fz_ready && c->fz_cap_n >= c->kp.n;  // (the last step produced this state's counts)
+    drop_begun(c);
+    if (int rc = refresh_if_dirty(c, st)) return rc;
+    if (int rc = greedy_scratch(c, c->kp.n)) return rc;  // (the partials, tickets and sorted window)
+    if (int rc = gqf_scratch(c, c->kp.n)) return rc;
+    double pmin = INFINITY;
+    for (int k = 0; k < c->cfg.n_cap; ++k) pmin = fmin(pmin, c->cfg.cap_table[k] / c->cfg.cop);
+    int par = c->fz_par;
+    if (!ready) {  // the current state's keys: the producer without a step, into parity par
+      hipLaunchKernelGGL(k_zero_u64, dim3(64), dim3(256), 0, st, reinterpret_cast<unsigned long long*>(c->fz.par[par]),
+                         (int64_t)(kGqfParWords / 2));
+      LAUNCH_CHECK("k_zero_u64 (fused producer region)");
+      const unsigned g = blocks(c->kp.n, kGqStage);
+      hipLaunchKernelGGL(k_gq_keys2, dim3(g), dim3(kGqThreads), 0, st, c->kp, c->fz, par, c->g_part, slab_at(c, c->ring));
+      LAUNCH_CHECK("k_gq_keys2");
+      c->gq_nparts = (int)g;
+    }
+    for (int t = 0; t < n; ++t) {
+      hipLaunchKernelGGL(k_gq_decide2, dim3(kGqSelBlocks), dim3(1024), 0, st, c->kp, c->fz, par, ticks[t].s_prev, pmin,
+                         slab_at(c, c->ring), c->g_tickets, (const double*)c->g_part, c->gq_nparts);
+      LAUNCH_CHECK("k_gq_decide2");
+      if (int rc = launch_step_fused(c, to_tick(&ticks[t]), reward + (int64_t)t * rew_stride,
+                                     action ? action + (int64_t)t * act_stride : nullptr, p_out, par, st))
+        return rc;
+      par = 1 - par;
+    }
+    c->fz_par = par;
+    c->fz_ready = true;
+    c->counts_ready = false;
+    return MDR_OK;
+  }
   for (int t = 0; t < n; ++t) {
     uint8_t* a = action + (int64_t)t * act_stride;
     double* r = reward + (int64_t)t * rew_stride;
@@ -1639,6 +1792,7 @@ int mdr_gq_shard_begin(mdr_ctx* c, void* stream) {
   const bool keys_ready = c->gq_keys_ready && c->g_cap >= c->kp.n;
   drop_begun(c);
   c->gq_keys_ready = false;
+  c->fz_ready = false;
   if (int rc = greedy_scratch(c, c->kp.n)) return rc;
   hipStream_t st = S(stream);
   if (!keys_ready)
@@ -1885,7 +2039,7 @@ int mdr_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const uint8_t*
     int rc = ensure_ticks(c, n);
     if (!rc)
       rc = window_launches(c, n, c->d_ticks, action, act_stride, mode, reward, rew_stride, p_out, false, st, true,
-                           false, ticks);
+                           false, ticks, true);
     c->counts_ready = false;
     return rc;
   }
@@ -2556,6 +2710,7 @@ int mdr_actor_rollout_sharded(mdr_ctx* c, int n, const mdr_tick* ticks, const md
       LAUNCH_CHECK("k_halo_step_pack");
       if (int rc = comm_allreduce(c, buf(t), words, 0, st)) return rc;
       c->gq_keys_ready = false;
+      c->fz_ready = false;
       if (int rc = launch_step_on(c, out.action, MDR_ACT_BUFFER, TickArgs{}, c->d_ticks + t,
                                   reward + (int64_t)t * rew_stride, 0, MDR_CTRL_NONE, nullptr, p_dev, buf(t),
                                   buf(t + 1), buf(t + 2), 0, st))

@@ -11,7 +11,7 @@
  * module calls them; IEEE double adds), so the mdr_tick rows are bit-identical to the Python loop
  * (tests/test_driver_window.py).  Compiled with -ffp-contract=off.
  *
- * rollout1(begin, rollout, ctx, stream, reward, rew_stride, p_dev, mode, <the driver arguments>):
+ * rollout1(begin, rollout, ctx, stream, reward, rew_stride, p_dev, mode, sharded, <the driver arguments>):
  *   the same loop between mdr_rollout_begin and mdr_rollout (below).
  *
  * drivers(rng, random, sigma, n, s, dts, od_tab, sig_tab, solar_tab, month, day, window_area,
@@ -199,7 +199,7 @@ static PyObject* drivers(PyObject* self, PyObject* args) {
   return Py_BuildValue("nLddd", r.k, r.s, r.tod, r.sig, r.sol);
 }
 
-/* rollout1(begin, rollout, ctx, stream, reward, rew_stride, p_dev, mode, <the 19 driver arguments>)
+/* rollout1(begin, rollout, ctx, stream, reward, rew_stride, p_dev, mode, sharded, <the 19 driver arguments>)
  *   -> (rc_begin, rc_rollout, k, s, tod, sig, sol)
  * One short direct rollout (Environment.rollout's default sequence) without Python between its
  * steps: mdr_rollout_begin (the first window's count, before the drivers exist), the driver loop
@@ -207,21 +207,25 @@ static PyObject* drivers(PyObject* self, PyObject* args) {
  * ticks (no action buffer, no graph).  begin / rollout are the library's entry points (addresses
  * from ctypes); rc_rollout = ROLLOUT_NOT_CALLED (1: no library status is positive) when it was not
  * called (begin failed, or k < n: the caller finishes the driver window for the next day and
- * launches itself); any other value is mdr_rollout's own status (0, or a negative MDR_E*). */
+ * launches itself); any other value is mdr_rollout's own status (0, or a negative MDR_E*).
+ * sharded != 0: `rollout` is mdr_rollout_sharded (a context with a communicator: begin also
+ * allreduced the count, the KA step kernel is all that is left), called without use_graph. */
 #define ROLLOUT_NOT_CALLED 1
 typedef int (*begin_fn)(void* ctx, int n, uint64_t tick0, const uint8_t* action, int64_t act_stride, int mode,
                         void* stream);
 typedef int (*rollout_fn)(void* ctx, int n, const void* ticks, const uint8_t* action, int64_t act_stride, int mode,
                           double* reward, int64_t rew_stride, double* p_out, int use_graph, void* stream);
+typedef int (*rollout_sharded_fn)(void* ctx, int n, const void* ticks, const uint8_t* action, int64_t act_stride,
+                                  int mode, double* reward, int64_t rew_stride, double* p_out, void* stream);
 
 static PyObject* rollout1(PyObject* self, PyObject* args) {
   (void)self;
-  if (PyTuple_GET_SIZE(args) != 8 + 19) {
-    PyErr_SetString(PyExc_TypeError, "rollout1: 8 launch arguments + 19 driver arguments");
+  if (PyTuple_GET_SIZE(args) != 9 + 19) {
+    PyErr_SetString(PyExc_TypeError, "rollout1: 9 launch arguments + 19 driver arguments");
     return NULL;
   }
-  unsigned long long a[8];
-  for (int i = 0; i < 8; ++i) {
+  unsigned long long a[9];
+  for (int i = 0; i < 9; ++i) {
     a[i] = PyLong_AsUnsignedLongLongMask(PyTuple_GET_ITEM(args, i));
     if (PyErr_Occurred()) return NULL;
   }
@@ -233,8 +237,9 @@ static PyObject* rollout1(PyObject* self, PyObject* args) {
   const int64_t rew_stride = (int64_t)a[5];
   double* p_dev = (double*)(uintptr_t)a[6];
   const int mode = (int)(int64_t)a[7];
-  PyObject* n_o = PyTuple_GET_ITEM(args, 8 + 3);
-  PyObject* t0_o = PyTuple_GET_ITEM(args, 8 + 17);
+  const int sharded = a[8] != 0;
+  PyObject* n_o = PyTuple_GET_ITEM(args, 9 + 3);
+  PyObject* t0_o = PyTuple_GET_ITEM(args, 9 + 17);
   const Py_ssize_t n = PyLong_AsSsize_t(n_o);
   const unsigned long long tick0 = PyLong_AsUnsignedLongLongMask(t0_o);
   if (PyErr_Occurred()) return NULL;
@@ -245,9 +250,11 @@ static PyObject* rollout1(PyObject* self, PyObject* args) {
   const int rc_b = begin(ctx, (int)n, (uint64_t)tick0, NULL, 0, mode, stream);
   if (rc_b != 0) return Py_BuildValue("iinLddd", rc_b, ROLLOUT_NOT_CALLED, (Py_ssize_t)0, 0LL, 0.0, 0.0, 0.0);
   drv_res r;
-  if (drivers_run(args, 8, &r) < 0) return NULL;
+  if (drivers_run(args, 9, &r) < 0) return NULL;
   int rc_r = ROLLOUT_NOT_CALLED;
-  if (r.k == r.n) rc_r = roll(ctx, (int)n, r.out, NULL, 0, mode, reward, rew_stride, p_dev, 0, stream);
+  if (r.k == r.n)
+    rc_r = sharded ? ((rollout_sharded_fn)(uintptr_t)a[1])(ctx, (int)n, r.out, NULL, 0, mode, reward, rew_stride, p_dev, stream)
+                   : roll(ctx, (int)n, r.out, NULL, 0, mode, reward, rew_stride, p_dev, 0, stream);
   return Py_BuildValue("iinLddd", rc_b, rc_r, r.k, r.s, r.tod, r.sig, r.sol);
 }
 

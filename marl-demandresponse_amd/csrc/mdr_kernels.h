@@ -91,6 +91,7 @@ __global__ void k_step_t(KParams p, const uint8_t* action, int action_mode, Tick
 struct GqSel;
 // the greedy controller's key outputs of a step kernel's epilogue (k_step_pipe GQ; k_gq_keys' outputs)
 struct GqOut {
+  uint8_t* act_out;  // (the fused tick, GQ = 2) every house's applied action, or null
   uint32_t* code;    // [n] the house's key bin << 2 | capacity class (gq_code)
   double* part;      // [grid][2] per-block (min, max) of the finite keys
   unsigned* hist;    // g_hist (the superbin copies follow its kGqBins * 4 bin words)
@@ -100,10 +101,47 @@ struct GqOut {
 // waves per block of k_step_pipe with the GQ epilogue (4 without): fewer, larger blocks share one LDS
 // superbin histogram, so fewer global flushes
 constexpr int kStepGqWaves = 16;
-template <int TPW, int ACT, int LA, bool GQ = false>
+// The fused greedy tick (mdr_greedy_rollout: producer -> k_gq_decide2 -> k_step_pipe<..., 2>).  The
+// producer (the previous tick's step epilogue, or k_gq_keys2) writes, under the key map of its parity
+// par, into parity region par: the superbin class counts of every house (C) and of the houses that
+// can turn on at the next step (A: not locked out, hvac.py:43-64), the class counts (C, A) of the
+// predicted band's bins, and the band's houses themselves as window entries in per-(copy, bin)
+// buckets.  The decision needs no pass over the cluster when the band holds the crossing; the step
+// applies it from the pre-step keys (the same bins under the same map) and the window houses' bytes.
+constexpr int kGqfSup = 8 * 257 * 4;             // words: superbin class counts, kGqCopies x kGqSupN x 4
+constexpr int kGqfBand = 8 * 8 * 64 * 4;         // words: band bin class counts, kGqCopies x band bins x 4
+constexpr int kGqfBandN = 8 * 8 * 64;            // words: band bucket allocators, kGqCopies x band bins
+constexpr int kGqfParWords = 2 * kGqfSup + 2 * kGqfBand + kGqfBandN + 64;  // + flags (64 words)
+constexpr int kGqfMissC = 8 * 128 * 4;           // miss path: the bins of superbins sb, sb + 1 (C, A)
+constexpr int kGqfMissN = 8 * 128;
+constexpr int kGqfMissWords = 2 * kGqfMissC + kGqfMissN + 64;
+// parity region offsets (words)
+// (kGqfOffASum: the A summary, kGqCopies x {A_lo[4], A_all[4]}; the rest of its kGqfSup words unused)
+constexpr int kGqfOffASum = kGqfSup, kGqfOffBandC = 2 * kGqfSup, kGqfOffBandA = 2 * kGqfSup + kGqfBand;
+// the miss region's A_lo (the houses below the crossing superbin, per class) after its overflow flag
+constexpr int kGqfOffMissALo = 2 * kGqfMissC + kGqfMissN + 1;
+constexpr int kGqfOffBandN = 2 * kGqfSup + 2 * kGqfBand, kGqfOffFlags = kGqfOffBandN + kGqfBandN;
+// decision modes (GqSel.fmode): the band / miss window's bins (take below bs, the window's bytes in
+// [bs, be], nothing above), every house taken, every house's byte written (gq_exact)
+enum { kGqfBandMode = 0, kGqfAll = 1, kGqfFull = 2 };
+constexpr int kGqfList = 1024;  // a GQ = 2 step block's band houses, staged in LDS before their buckets
+constexpr int kGqfStampWords = 32;  // phase stamps per block (mdr_greedy_fused_stamps)
+struct GqfBufs {
+  unsigned* par[2];      // the parity regions (kGqfParWords each)
+  unsigned* miss;        // kGqfMissWords
+  uint4* bkt[2];         // band buckets per parity: [kGqCopies][band bins][cap] window entries
+  uint4* mbkt;           // miss buckets [kGqCopies][128][mcap]
+  uint32_t* map[2];      // the key maps of the two parities (gq_bin)
+  GqSel* sel;            // the fused path's own select record (fkmin / fscale per parity, the decision)
+  uint8_t* dec;          // the decision bytes: window houses (band mode) or every house (full mode)
+  int cap, mcap;         // bucket capacities (entries per copy and bin)
+  unsigned long long* stamps;  // diagnostics (mdr_greedy_fused_stamps): k_gq_decide2's phase times, or null
+};
+template <int TPW, int ACT, int LA, int GQ = 0>
 __global__ void k_step_pipe(KParams p, const uint8_t* action, TickArgs tk, const TickArgs* tkp,
                             const unsigned long long* counts, double* reward, double* p_out,
-                            unsigned long long* next_slab, unsigned long long* zero_slab, GqOut gq);
+                            unsigned long long* next_slab, unsigned long long* zero_slab, GqOut gq,
+                            GqfBufs fz, int fpar);
 constexpr int kPipeMaxCap = 4;
 constexpr int kWindowMax = 32;  // = kWinMax: ticks per k_step_window launch
 constexpr int kWindowCap = 4;   // = kWinCap: capacity classes the window kernel supports
@@ -119,6 +157,8 @@ struct WinDrv {
   uint64_t tick0;             // the window's first tick id (ids are consecutive)
   double* p_out;              // last window: <- P of its last tick
   uint32_t ok;                // bit j: tick j's drivers are in the fast-division ranges
+  const unsigned long long* red;  // sharded KA: the allreduced K x n_cap class totals — each lane's P
+                                  // from them (win_power), in place of rec (no k_win_records launch)
 };
 // SIMPLE: deadband 0 and norm_temp 1 (reward without branches / division); FORM: the per-tick
 // thermal update, MDR_THERMAL_EXACT (the reference's expression) or MDR_THERMAL_AFFINE (its
@@ -177,6 +217,15 @@ constexpr int kGqBandOff = kGqCopies * 512;
 static_assert(kGqBandOff + kGqCopies * kGqBandWords <= kGqBins * 4, "the band copies fit below the superbin copies");
 static_assert(kGqHistWords % 2 == 0, "g_hist is zeroed as 64-bit words");
 constexpr int kGqCells = 256;   // cells of the key -> bin map (gq_bin)
+// bins the key map spreads over for a cluster of n houses: about 8 houses per bin at most, so a
+// window of 64 bins holds a few hundred houses however small the cluster (a multiple of 64, >= 1024)
+__host__ __device__ __forceinline__ int gq_bins_eff(int64_t n) {
+  const int64_t b = (n / 8) & ~(int64_t)63;
+  return b >= kGqBins ? kGqBins : (b < 1024 ? 1024 : (int)b);
+}
+static_assert(kGqfSup == kGqCopies * (kGqSuper + 1) * 4 && kGqfBand == kGqCopies * kGqBandWords &&
+              kGqfBandN == kGqCopies * kGqBand * 64 && kGqfMissN == kGqCopies * 128,
+              "the fused greedy's region sizes (declared before the histogram constants)");
 constexpr int kGqSelBlocks = 256;  // k_gq_select grid, 1024 threads each
 constexpr int kGqMaxRanks = 64;   // sharded histogram select: ranks whose windows k_gq_select gathers
 struct GqSel;
@@ -202,6 +251,12 @@ __global__ void k_gq_select(KParams p, const uint4* win, uint4* sorted, double S
                             uint8_t* action, unsigned long long* slab, unsigned* hist, const uint4* gathered,
                             int world, unsigned* tickets, const double* part, int nparts, uint32_t* map);
 __global__ void k_gq_range(const double* part, int nparts, double* range);
+// the fused tick: the producer without a step (the state's first decision), and the decision
+__global__ void k_gq_keys2(KParams p, GqfBufs fz, int par, double* part, unsigned long long* slab);
+__global__ void k_gq_decide2(KParams p, GqfBufs fz, int par, double S, double pmin, unsigned long long* slab,
+                             unsigned* tickets, const double* part, int nparts);
+void gqf_sel_init(void* sel, uint32_t* map);  // host: the fused record (both parities' cells = gq_sel_init's)
+void gqf_diag_of(const void* sel, uint64_t* out);  // host: {calls, band hits, misses, exact, last mode, last window}
 __global__ void k_greedy_inputs(KParams p, double* key, double* power, uint8_t* lock);
 __global__ void k_greedy_iota(int64_t n, int* idx);
 __global__ void k_greedy_gather_rows(int64_t n, const int* perm, const double* power, const uint8_t* lock,

@@ -116,6 +116,13 @@ struct GqSel {
   int band_valid;                // the band copies hold this call's counts (the GQ epilogue sets it)
   int hit;                       // k_gq_binsc compacted from the band (k_gq_finish ranks; reset by its decider)
   unsigned hits;                 // diagnostics: calls whose bins pass was skipped
+  // the fused tick (k_gq_decide2; its own record): the cell grids of the two parities' key maps, the
+  // decision the step applies, diagnostics
+  double fkmin[2], fscale[2];
+  int fmode, fbs, fbe;           // kGqfBandMode: take bins < fbs, the bytes of [fbs, fbe]; kGqfAll; kGqfFull
+  int fband[2];                  // the band_base of each parity's producer (decide2(par) writes fband[1 - par]:
+                                 // a block of the same launch may still read fband[par])
+  unsigned fcalls, fhits, fmisses, fexact, fwin;
 };
 static_assert(sizeof(GqSel) <= kGqSelBytes, "GqSel fits the g_sel buffer");
 void gq_sel_init(void* sel, uint32_t* map) {
@@ -125,6 +132,24 @@ void gq_sel_init(void* sel, uint32_t* map) {
   for (int c = 0; c < kGqCells; ++c) map[c] = ((uint32_t)(c * (kGqBins / kGqCells)) << 16) | (uint32_t)(kGqBins / kGqCells);
   g->band_base = kGqSuper / 2 - kGqBand / 2;
   g->sb_raw = -1;
+}
+void gqf_sel_init(void* sel, uint32_t* map) {
+  gq_sel_init(sel, map);
+  GqSel* g = static_cast<GqSel*>(sel);
+  for (int q = 0; q < 2; ++q) {
+    g->fkmin[q] = g->kmin;
+    g->fscale[q] = g->scale;
+    g->fband[q] = g->band_base;
+  }
+}
+void gqf_diag_of(const void* sel, uint64_t* out) {
+  const GqSel* g = static_cast<const GqSel*>(sel);
+  out[0] = g->fcalls;
+  out[1] = g->fhits;
+  out[2] = g->fmisses;
+  out[3] = g->fexact;
+  out[4] = (uint64_t)(int64_t)g->fmode;
+  out[5] = g->fwin;
 }
 void gq_band_of(const void* sel, uint64_t* out) {
   const GqSel* g = static_cast<const GqSel*>(sel);
@@ -179,12 +204,6 @@ __device__ __forceinline__ int gq_bin(double k, double kmin, double scale, const
   const float f = (u - (float)c) * (float)w;
   return (int)(m >> 16) + (f >= (float)(w - 1) ? w - 1 : (f > 0.0f ? (int)f : 0));
 }
-// bins the key map spreads over for a cluster of n houses: about 8 houses per bin at most, so a
-// window of 64 bins holds a few hundred houses however small the cluster (a multiple of 64, >= 1024)
-__host__ __device__ __forceinline__ int gq_bins_eff(int64_t n) {
-  const int64_t b = (n / 8) & ~(int64_t)63;
-  return b >= kGqBins ? kGqBins : (b < 1024 ? 1024 : (int)b);
-}
 // a house's code: its key bin (kGqBins for a NaN key) << 2 | its capacity class; the superbin is
 // code >> 8 (kGqBins / kGqSuper = 64 bins each; NaN keys land in superbin kGqSuper)
 __device__ __forceinline__ uint32_t gq_code(double k, double kmin, double scale, const uint32_t* map, unsigned cls) {
@@ -218,6 +237,66 @@ __device__ __forceinline__ void gq_flush(const unsigned* s_sh, int ncopy, unsign
     unsigned v = 0u;
     for (int w = 0; w < ncopy; ++w) v += s_sh[w * kGqSupStride + e];
     if (v) atomicAdd(&hist[kGqBins * 4 + (blockIdx.x % kGqCopies) * kGqSupStride + e], v);
+  }
+}
+
+// The fused tick's A summary (the houses that can turn on at the next step, per class): of the houses
+// below the band's first superbin (A_lo) and of every house (A_all) — the decision's ON counts of the
+// houses it takes outside the window (A_lo plus the band's A bins below the window, or A_all when every
+// house is taken); per-superbin A counts are not kept (r06: their flush atomics cost ~1.7 us a step).
+// Per lane: 16-bit fields (classes 0/1 and 2/3), summed over the wave at the block's end.
+struct GqfAcnt {
+  uint32_t lo01, lo23, al01, al23;
+};
+__device__ __forceinline__ void gqf_acount(GqfAcnt& a, bool canon, bool below, unsigned cls) {
+  const uint32_t inc = canon ? 1u << (16u * (cls & 1u)) : 0u;
+  const uint32_t il = below ? inc : 0u;
+  if (cls < 2u) { a.al01 += inc; a.lo01 += il; }
+  else { a.al23 += inc; a.lo23 += il; }
+}
+// the wave's sums into s_acnt[8] (A_lo[4], A_all[4]; LDS, zeroed by the caller before a barrier)
+__device__ __forceinline__ void gqf_acount_wave(GqfAcnt a, unsigned* s_acnt) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    a.lo01 += __shfl_xor(a.lo01, off);
+    a.lo23 += __shfl_xor(a.lo23, off);
+    a.al01 += __shfl_xor(a.al01, off);
+    a.al23 += __shfl_xor(a.al23, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    const uint32_t v[8] = {a.lo01 & 0xFFFFu, a.lo01 >> 16, a.lo23 & 0xFFFFu, a.lo23 >> 16,
+                           a.al01 & 0xFFFFu, a.al01 >> 16, a.al23 & 0xFFFFu, a.al23 >> 16};
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (v[k]) atomicAdd(&s_acnt[k], v[k]);
+  }
+}
+// the fused tick's producer flush: the LDS copies of the superbin C counts into the parity region's
+// copy blockIdx % kGqCopies, the block's A summary (s_acnt, complete after this function's barrier)
+// into the copy's 8 summary words, and the block's (min, max) of the finite keys
+__device__ __forceinline__ void gqf_flush(const unsigned* s_sh, int ncopy, unsigned* par, double lo, double hi,
+                                          double* part, const unsigned* s_acnt) {
+  const int nw = (int)(blockDim.x >> 6);
+  __shared__ double s_lo[16], s_hi[16];
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, off));
+    hi = fmax(hi, __shfl_xor(hi, off));
+  }
+  if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double l = s_lo[0], h = s_hi[0];
+    for (int w = 1; w < nw; ++w) { l = fmin(l, s_lo[w]); h = fmax(h, s_hi[w]); }
+    part[2 * blockIdx.x] = l;
+    part[2 * blockIdx.x + 1] = h;
+  }
+  const int cp = (int)(blockIdx.x % kGqCopies);
+  if (threadIdx.x < 8 && s_acnt[threadIdx.x]) atomicAdd(&par[kGqfOffASum + cp * 8 + threadIdx.x], s_acnt[threadIdx.x]);
+  for (int e = threadIdx.x; e < kGqSupStride; e += blockDim.x) {
+    unsigned v = 0u;
+    for (int w = 0; w < ncopy; ++w) v += s_sh[w * kGqSupStride + e];
+    if (v) atomicAdd(&par[cp * kGqSupStride + e], v);
   }
 }
 
@@ -508,33 +587,75 @@ __device__ __forceinline__ void load_tile2(const KParams& p, const uint8_t* acti
   }
 }
 
-// GQ: the greedy controller's keys of the post-step state, their superbin histogram and the
+// GQ = 1: the greedy controller's keys of the post-step state, their superbin histogram and the
 // block's key range (k_gq_keys' outputs, gq_flush) as an epilogue, so the next mdr_ctrl_greedy
-// skips its key pass; blocks of kStepGqWaves waves (4 LDS histogram copies) instead of 4
-template <int TPW, int ACT, int LA, bool GQ>
+// skips its key pass; blocks of kStepGqWaves waves (4 LDS histogram copies) instead of 4.
+// GQ = 2, the fused tick (mdr_greedy_rollout; mdr_kernels.h GqfBufs): the actions are the decision of
+// k_gq_decide2 applied here — the pre-step key's bin under the decision's map (parity fpar: the same
+// bin the producer counted) below fbs taken, in [fbs, fbe] the house's byte (action = fz.dec), above
+// not — and the epilogue is the producer of the next decision (parity 1 - fpar): superbin C and A
+// counts (packed C | A << 16 in the LDS copies), the band's C / A bin counts and its houses as window
+// entries in their (copy, bin) buckets; no codes are stored
+template <int TPW, int ACT, int LA, int GQ>
 __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KParams p, const uint8_t* __restrict__ action, TickArgs tk0,
                                                    const TickArgs* tkp, const unsigned long long* __restrict__ counts,
                                                    double* __restrict__ reward, double* p_out,
                                                    unsigned long long* next_slab, unsigned long long* zero_slab,
-                                                   GqOut gq) {
+                                                   GqOut gq, GqfBufs fz, int fpar) {
   constexpr int HPT = 2;
   constexpr bool AB = ACT == MDR_ACT_BUFFER;
   __shared__ unsigned hist[MDR_MAX_CAP];
   __shared__ unsigned s_gq[GQ ? 4 * kGqSupStride : 1];
   __shared__ uint32_t s_map[GQ ? kGqCells : 1];
+  __shared__ uint32_t s_mapd[GQ == 2 ? kGqCells : 1];  // (GQ 2) the decision's map
+  // (GQ 2) the block's band houses: entries, (bin << 16 | rank in the block's bin), per-bin counts and
+  // bucket bases — one returning global atomic per non-empty bin at the block's end, not per house
+  __shared__ uint4 s_bl[GQ == 2 ? kGqfList : 1];
+  __shared__ uint32_t s_blr[GQ == 2 ? kGqfList : 1];
+  __shared__ unsigned s_bcnt[GQ == 2 ? kGqBand * 64 : 1];
+  __shared__ unsigned s_blen;
+  __shared__ unsigned s_acnt[8];  // (GQ 2) the block's A summary
   const int tid = threadIdx.x;
   const int lane = tid & 63;
   if (tid < p.n_cap) hist[tid] = 0;
   int gq_band0 = 0;  // the band's first bin
   unsigned* gq_band = nullptr;  // this block's copy of the band's class counts
-  if (GQ) {
+  const int npar = 1 - fpar;    // (GQ 2) the parity this epilogue produces
+  unsigned* fz_band_a = nullptr;
+  unsigned* fz_band_n = nullptr;
+  uint4* fz_bkt = nullptr;
+  double d_kmin = 0.0, d_scale = 0.0;
+  int f_mode = 0, f_bs = 0, f_be = 0;
+  if (GQ == 1) {
     for (int e = tid; e < 4 * kGqSupStride; e += blockDim.x) s_gq[e] = 0u;
     for (int e = tid; e < kGqCells; e += blockDim.x) s_map[e] = gq.map[e];
     gq_band0 = gq.sel->band_base * 64;
     gq_band = gq.hist + kGqBandOff + (blockIdx.x % kGqCopies) * kGqBandWords;
+  } else if (GQ == 2) {
+    for (int e = tid; e < 4 * kGqSupStride; e += blockDim.x) s_gq[e] = 0u;
+    for (int e = tid; e < kGqCells; e += blockDim.x) {
+      s_map[e] = fz.map[npar][e];
+      s_mapd[e] = fz.map[fpar][e];
+    }
+    for (int e = tid; e < kGqBand * 64; e += blockDim.x) s_bcnt[e] = 0u;
+    if (tid == 0) s_blen = 0u;
+    if (tid < 8) s_acnt[tid] = 0u;
+    gq_band0 = fz.sel->fband[npar] * 64;
+    const int cp = (int)(blockIdx.x % kGqCopies);
+    gq_band = fz.par[npar] + kGqfOffBandC + cp * kGqBandWords;
+    fz_band_a = fz.par[npar] + kGqfOffBandA + cp * kGqBandWords;
+    fz_band_n = fz.par[npar] + kGqfOffBandN + cp * (kGqBand * 64);
+    fz_bkt = fz.bkt[npar] + (size_t)cp * (kGqBand * 64) * fz.cap;
+    d_kmin = fz.sel->fkmin[fpar];
+    d_scale = fz.sel->fscale[fpar];
+    f_mode = fz.sel->fmode;
+    f_bs = fz.sel->fbs;
+    f_be = fz.sel->fbe;
   }
   double gq_lo = INFINITY, gq_hi = -INFINITY;
-  const double gq_kmin = GQ ? gq.sel->kmin : 0.0, gq_scale = GQ ? gq.sel->scale : 0.0;
+  GqfAcnt gq_a{0u, 0u, 0u, 0u};
+  const double gq_kmin = GQ == 1 ? gq.sel->kmin : GQ == 2 ? fz.sel->fkmin[npar] : 0.0;
+  const double gq_scale = GQ == 1 ? gq.sel->scale : GQ == 2 ? fz.sel->fscale[npar] : 0.0;
   if (zero_slab && blockIdx.x == 0)
     for (int j = tid; j < kCountShards * p.n_cap; j += blockDim.x) zero_slab[j] = 0ull;
   // GQ (no lookahead): the greedy call that follows counts its decisions into next_slab, and its
@@ -607,11 +728,27 @@ __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KPar
 
     double Tn[2], Tmn[2], rw[2];
     uint32_t w[2];
-    bool on1[2];
+    bool on1[2], act_ap[2];
 #pragma unroll
     for (int h = 0; h < HPT; ++h) {
-      const bool a = valid[h] && (AB ? ((in.act >> (8 * h)) & 0xFFu) != 0u
-                                     : pick_action(ACT, action, i0 + h, rnd[h], T[h], tg[h], p.deadband, w0[h]));
+      bool a;
+      if (GQ == 2) {  // the fused decision (GqSel.fmode; the byte: fz.dec, loaded as the action row)
+        const bool byte = ((in.act >> (8 * h)) & 0xFFu) != 0u;
+        if (f_mode == kGqfAll) {
+          a = true;
+        } else if (f_mode == kGqfFull) {
+          a = byte;
+        } else {
+          const double k = -(T[h] - tg[h]);  // gq_key_of, pre-step: the key the decision ordered
+          const int b = k != k ? kGqBins : gq_bin(k, d_kmin, d_scale, s_mapd);
+          a = b < f_bs || (b <= f_be && byte);
+        }
+        a = valid[h] && a;
+        act_ap[h] = a;
+      } else {
+        a = valid[h] && (AB ? ((in.act >> (8 * h)) & 0xFFu) != 0u
+                            : pick_action(ACT, action, i0 + h, rnd[h], T[h], tg[h], p.deadband, w0[h]));
+      }
       w[h] = hvac_fsm(w0[h], a, p.dt, p.L);
       const bool on = hv_on(w[h]);
       double qc = q_on[0];
@@ -638,6 +775,14 @@ __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KPar
         on1[h] = valid[h] && hv_on(hvac_fsm(w[h], an, p.dt, p.L));
       }
     }
+    if (GQ == 2 && gq.act_out) {  // (the fused tick: the applied actions, when the caller keeps them)
+      if (valid[1] && ((uintptr_t)gq.act_out & 1u) == 0u) {
+        sto(gq.act_out, i0, (unsigned short)((act_ap[0] ? 1u : 0u) | (act_ap[1] ? 256u : 0u)));
+      } else {  // (an odd row start: per-tick rows of an odd cluster size)
+        if (valid[0]) gq.act_out[i0] = act_ap[0] ? 1 : 0;
+        if (valid[1]) gq.act_out[i0 + 1] = act_ap[1] ? 1 : 0;
+      }
+    }
     if (valid[1]) {
       const uint32_t o8 = i0 * 8u;
       sto(p.t_air, o8, make_double2(Tn[0], Tn[1]));
@@ -648,7 +793,44 @@ __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KPar
       p.t_air[i0] = Tn[0]; p.t_mass[i0] = Tmn[0]; p.hvac[i0] = w[0];
       if (counts) __builtin_nontemporal_store(rw[0], reward + i0);
     }
-    if (GQ) {  // greedy_myopic_controller.py:79 on the post-step state (gq_key_of)
+    if (GQ == 2) {  // the next decision's producer (gq_key_of of the post-step state)
+      const uint32_t Lu = p.L < 0 ? 0u : (uint32_t)p.L;
+#pragma unroll
+      for (int h = 0; h < HPT; ++h) {
+        const double k = -(Tn[h] - tg[h]);
+        const uint32_t c = gq_code(k, gq_kmin, gq_scale, s_map, (unsigned)cls[h]);
+        if (valid[h] && k == k) {
+          gq_lo = fmin(gq_lo, k);
+          gq_hi = fmax(gq_hi, k);
+        }
+        // A: the house can turn on at the next step (hvac_fsm: not locked out)
+        const bool canon = hv_on(w[h]) || hv_sso(w[h]) + (uint32_t)p.dt >= Lu;
+        if (valid[h]) atomicAdd(&s_gq[((tid >> 6) & 3) * kGqSupStride + (c >> 8) * 4 + (c & 3u)], 1u);
+        gqf_acount(gq_a, valid[h] && canon, (c >> 2) < (uint32_t)gq_band0, c & 3u);
+        const uint32_t bo = (c >> 2) - (uint32_t)gq_band0;
+        const bool inb = valid[h] && bo < (uint32_t)(kGqBand * 64);
+        // the list slots: one LDS atomic per wave (same-address LDS atomics serialise), then by lane rank
+        const unsigned long long m = __ballot(inb);
+        unsigned lbase = 0u;
+        if (m) {  // (wave-uniform)
+          const int lead = __ffsll((long long)m) - 1;
+          if (lane == lead) lbase = atomicAdd(&s_blen, (unsigned)__popcll(m));
+          lbase = __shfl(lbase, lead);
+        }
+        if (inb) {
+          atomicAdd(&gq_band[bo * 4 + (c & 3u)], 1u);
+          if (canon) atomicAdd(&fz_band_a[bo * 4 + (c & 3u)], 1u);
+          const unsigned li = lbase + (unsigned)__popcll(m & ((1ull << lane) - 1ull));
+          const unsigned lr = atomicAdd(&s_bcnt[bo], 1u);  // (LDS)
+          const uint64_t ok = gq_okey(k);
+          if (li < (unsigned)kGqfList) {
+            s_bl[li] = make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), (uint32_t)((p.goff + i0 + h) << 2) | (c & 3u), w[h]);
+            s_blr[li] = (bo << 16) | lr;
+          }
+        }
+      }
+    }
+    if (GQ == 1) {  // greedy_myopic_controller.py:79 on the post-step state (gq_key_of)
       const double k0 = -(Tn[0] - tg[0]), k1 = -(Tn[1] - tg[1]);
       const uint32_t c0 = gq_code(k0, gq_kmin, gq_scale, s_map, (unsigned)cls[0]);
       const uint32_t c1 = gq_code(k1, gq_kmin, gq_scale, s_map, (unsigned)cls[1]);
@@ -689,10 +871,31 @@ __global__ void __launch_bounds__(GQ ? 64 * kStepGqWaves : 256) k_step_pipe(KPar
     if (tid < p.n_cap && hist[tid])
       atomicAdd(&next_slab[(blockIdx.x % kCountShards) * p.n_cap + tid], (unsigned long long)hist[tid]);
   }
-  if (GQ) {
+  if (GQ == 1) {
     __syncthreads();
     gq_flush(s_gq, 4, gq.hist, gq_lo, gq_hi, gq.part);
     if (blockIdx.x == 0 && threadIdx.x == 0) gq.sel->band_valid = 1;
+  } else if (GQ == 2) {
+    gqf_acount_wave(gq_a, s_acnt);
+    __syncthreads();
+    // the band houses into their buckets: a base per non-empty bin (one returning atomic each, in
+    // parallel), then each house at base + its rank in the block's bin
+    if (s_blen > (unsigned)kGqfList && tid == 0) atomicOr(&fz.par[npar][kGqfOffFlags], 1u);
+    // (the returning atomics' latency overlaps the flush: their values go to LDS after it)
+    static_assert(kGqBand * 64 <= 64 * kStepGqWaves, "a thread per band bin");
+    unsigned bbase = 0u;
+    if (tid < kGqBand * 64 && s_bcnt[tid]) bbase = atomicAdd(&fz_band_n[tid], s_bcnt[tid]);
+    gqf_flush(s_gq, 4, fz.par[npar], gq_lo, gq_hi, gq.part, s_acnt);
+    unsigned* s_bbase = s_bcnt;  // (in place: each thread owns its bin's entry)
+    if (tid < kGqBand * 64) s_bbase[tid] = bbase;
+    __syncthreads();
+    const unsigned nl = s_blen < (unsigned)kGqfList ? s_blen : (unsigned)kGqfList;
+    for (unsigned e = tid; e < nl; e += blockDim.x) {
+      const uint32_t br = s_blr[e], bo = br >> 16;
+      const unsigned slot = s_bbase[bo] + (br & 0xFFFFu);
+      if (slot < (unsigned)fz.cap) fz_bkt[(size_t)bo * fz.cap + slot] = s_bl[e];
+      else atomicOr(&fz.par[npar][kGqfOffFlags], 1u);  // (a full bucket: the band is not usable)
+    }
   }
 }
 
@@ -1229,10 +1432,20 @@ __global__ void __launch_bounds__(256) k_step_window(KParams p, const uint8_t* _
   uint32_t ns_lo = 0, ns_hi = 0;
   if (KA) {
     const int l = (int)(threadIdx.x & 63) < K ? (int)(threadIdx.x & 63) : 0;
-    const double ns = win_nsig(p, rec[l * kWinRec], dv.s_prev[l]);
+    double P;
+    if (dv.red) {  // (k_win_records' P, in place: the same win_power on the same totals)
+      double p_on[kWinCap];
+#pragma unroll
+      for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
+      P = win_power(p, dv.red + l * p.n_cap, p_on);
+      if (dv.p_out && blockIdx.x == 0 && (int)threadIdx.x == K - 1) *dv.p_out = P;
+    } else {
+      P = rec[l * kWinRec];
+      if (dv.p_out && blockIdx.x == 0 && threadIdx.x == 0) *dv.p_out = rec[(K - 1) * kWinRec];  // (last window)
+    }
+    const double ns = win_nsig(p, P, dv.s_prev[l]);
     ns_lo = (uint32_t)__double_as_longlong(ns);
     ns_hi = (uint32_t)((uint64_t)__double_as_longlong(ns) >> 32);
-    if (dv.p_out && blockIdx.x == 0 && threadIdx.x == 0) *dv.p_out = rec[(K - 1) * kWinRec];  // (last window)
   }
 
   // ---- state + parameters, once per window
@@ -1435,15 +1648,17 @@ MDR_INST_WIN(MDR_ACT_BUFFER)
 #define MDR_INST_PIPE(T, A, LA, G)                                                                    \
   template __global__ void k_step_pipe<T, A, LA, G>(KParams, const uint8_t*, TickArgs, const TickArgs*, \
                                                     const unsigned long long*, double*, double*,         \
-                                                    unsigned long long*, unsigned long long*, GqOut);
-MDR_INST_PIPE(1, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false)
-MDR_INST_PIPE(2, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false)
-MDR_INST_PIPE(4, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false)
-MDR_INST_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM, false)
-MDR_INST_PIPE(2, MDR_ACT_BUFFER, 0, false)
-MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0, false)
-MDR_INST_PIPE(2, MDR_ACT_BUFFER, 0, true)
-MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0, true)
+                                                    unsigned long long*, unsigned long long*, GqOut, GqfBufs, int);
+MDR_INST_PIPE(1, MDR_ACT_RANDOM, MDR_ACT_RANDOM, 0)
+MDR_INST_PIPE(2, MDR_ACT_RANDOM, MDR_ACT_RANDOM, 0)
+MDR_INST_PIPE(4, MDR_ACT_RANDOM, MDR_ACT_RANDOM, 0)
+MDR_INST_PIPE(8, MDR_ACT_RANDOM, MDR_ACT_RANDOM, 0)
+MDR_INST_PIPE(2, MDR_ACT_BUFFER, 0, 0)
+MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0, 0)
+MDR_INST_PIPE(2, MDR_ACT_BUFFER, 0, 1)
+MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0, 1)
+MDR_INST_PIPE(2, MDR_ACT_BUFFER, 0, 2)
+MDR_INST_PIPE(4, MDR_ACT_BUFFER, 0, 2)
 
 #define MDR_INST_STEP(F, A, LA)                                                                  \
   template __global__ void k_step_t<2, F, A, LA>(                                                \
@@ -1960,15 +2175,19 @@ struct GqSuper {
 struct GqSupLoad {
   uint4 v[kGqCopies];
 };
-__device__ __forceinline__ GqSupLoad gq_super_load(const unsigned* __restrict__ hist) {
+// sup: the superbin copies (kGqCopies x kGqSupStride words; g_hist + kGqBins * 4, or a fused parity's)
+__device__ __forceinline__ GqSupLoad gq_super_load_at(const unsigned* __restrict__ sup) {
   GqSupLoad l;
   const int tid = threadIdx.x;
   // (one branch around all the loads: per-load conditions made the compiler wait after every pair)
   const int t = tid < kGqSupN ? tid : 0;
-  const uint4* src = reinterpret_cast<const uint4*>(hist + kGqBins * 4 + t * 4);
+  const uint4* src = reinterpret_cast<const uint4*>(sup + t * 4);
 #pragma unroll
   for (int q = 0; q < kGqCopies; ++q) l.v[q] = src[q * (kGqSupStride / 4)];
   return l;  // (threads >= kGqSupN hold superbin 0's counts: gq_super_find ignores them)
+}
+__device__ __forceinline__ GqSupLoad gq_super_load(const unsigned* __restrict__ hist) {
+  return gq_super_load_at(hist + kGqBins * 4);
 }
 __device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLoad& l, double S, GqSel* __restrict__ sel,
                                  unsigned long long* __restrict__ slab, bool reset_alloc) {
@@ -1994,7 +2213,11 @@ __device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLo
   if (tid == 0) { s_first = kGqSupN; s_bt = 0.0; s_bc = 0ull; }
   gq_block_scan(x, xc, s_w, s_wc);
   const double before = x - ps;
-  if (tid < kGqSupN && cs > 0 && !(before + ps < S)) atomicMin(&s_first, tid);  // (the first: a non-empty superbin)
+  {  // the first non-empty superbin where the P reaches S: one LDS atomic per wave (same-address LDS
+     // atomics serialise: one per thread cost ~4 us here, r06 phase stamps)
+    const unsigned long long m = __ballot(tid < kGqSupN && cs > 0 && !(before + ps < S));
+    if (m && (tid & 63) == 0) atomicMin(&s_first, (tid & ~63) + __ffsll((long long)m) - 1);
+  }
   if (tid == kGqSupN - 1) s_total = xc;
   __syncthreads();
   const int sb = s_first;
@@ -2092,8 +2315,23 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_bins(KParams p, const uint32_
 // LDS work areas are carved from `lds` (>= kGqMapLds bytes, free: the caller's window array).
 constexpr int kGqMapLds = (3 * (kGqThreads / 64) + 2 + 2 * kGqSuper + kGqCells + 1) * 8 + kGqCells * 4 +
                           (kGqThreads / 64) * 8;
+// The core over explicit buffers (the fused tick: the superbin copies and maps of its parities):
+// sup = the superbin copies, map_in / (okmin, oscale) the map they were counted under, map_out /
+// (*kmin_out, *scale_out) the next map (may alias map_in); zero_sup: zero the copies after
+__device__ void gq_next_map_core(const KParams& p, unsigned* __restrict__ sup, const double* __restrict__ part,
+                                 int nparts, GqSel* __restrict__ sel, const uint32_t* map_in, double okmin,
+                                 double oscale, uint32_t* map_out, double* kmin_out, double* scale_out,
+                                 unsigned char* lds, bool zero_sup, int sb_now, unsigned xcnt_now, int* band_out);
 __device__ __forceinline__ void gq_next_map(const KParams& p, unsigned* __restrict__ hist, const double* __restrict__ part,
                             int nparts, GqSel* __restrict__ sel, uint32_t* __restrict__ map, unsigned char* lds) {
+  // (xcnt: sc1 — k_gq_finish's block 0 may have just written it, past this CU's L1)
+  gq_next_map_core(p, hist + kGqBins * 4, part, nparts, sel, map, sel->kmin, sel->scale, map, &sel->kmin, &sel->scale,
+                   lds, true, sel->sb, ld_sc1(&sel->xcnt), &sel->band_base);
+}
+__device__ void gq_next_map_core(const KParams& p, unsigned* __restrict__ sup, const double* __restrict__ part,
+                                 int nparts, GqSel* __restrict__ sel, const uint32_t* map_in, double okmin,
+                                 double oscale, uint32_t* map_out, double* kmin_out, double* scale_out,
+                                 unsigned char* lds, bool zero_sup, int sb_now, unsigned xcnt_now, int* band_out) {
   constexpr int NW = kGqThreads / 64;
   double* s_w = reinterpret_cast<double*>(lds);
   double* s_lo = s_w + NW;
@@ -2109,14 +2347,14 @@ __device__ __forceinline__ void gq_next_map(const KParams& p, unsigned* __restri
   if (tid < kGqSupN)
 #pragma unroll
     for (int q = 0; q < kGqCopies; ++q) {
-      const uint4 v = *reinterpret_cast<const uint4*>(hist + kGqBins * 4 + q * kGqSupStride + tid * 4);
+      const uint4 v = *reinterpret_cast<const uint4*>(sup + q * kGqSupStride + tid * 4);
       cs += (unsigned long long)v.x + v.y + v.z + v.w;
     }
   double x = 0.0;
   unsigned long long xc = cs;
   gq_block_scan(x, xc, s_w, s_wc);
   if (tid < kGqSuper) { s_pre[tid] = (double)(xc - cs); s_cnt[tid] = (double)cs; }
-  if (tid < kGqCells) s_map[tid] = map[tid];
+  if (tid < kGqCells) s_map[tid] = map_in[tid];
   double lo = INFINITY, hi = -INFINITY;
   if (nparts < 0) {  // sharded: the cluster's range, allreduced as (min, -max) (k_gq_range)
     if (tid == 0) { lo = part[0]; hi = -part[1]; }
@@ -2138,7 +2376,7 @@ __device__ __forceinline__ void gq_next_map(const KParams& p, unsigned* __restri
     s_rng[1] = range > 0.0 && range < INFINITY ? (double)kGqCells / range : 0.0;
   }
   __syncthreads();
-  const double okmin = sel->kmin, oscale = sel->scale, nkmin = s_rng[0], nscale = s_rng[1];
+  const double nkmin = s_rng[0], nscale = s_rng[1];
   if (tid <= kGqCells) {
     double C = 0.0;
     if (nscale > 0.0) {
@@ -2162,30 +2400,31 @@ __device__ __forceinline__ void gq_next_map(const KParams& p, unsigned* __restri
       return g + min(K, (int)((double)K * ((s_C[g] - s_C[0]) / T)));
     };
     const int b0 = edge(tid), b1 = edge(tid + 1);
-    map[tid] = ((uint32_t)b0 << 16) | (uint32_t)(b1 - b0);
+    map_out[tid] = ((uint32_t)b0 << 16) | (uint32_t)(b1 - b0);
     // the band the next producer counts: centred on the superbin the next call's crossing falls
     // into under the new map if it moves as it did since the last call (xcnt houses before it now,
     // the signal's trend: the sinusoid moves it by up to ~2 superbins a tick, tools/band_probe.py)
     // and shifted by the last prediction's error: the keys move between this call and the next
     // (the taken houses cool, the others warm), which the map of this call's keys cannot see
-    // (xcnt: sc1 — k_gq_finish's block 0 may have just written it, past this CU's L1)
-    const double X1 = (double)ld_sc1(&sel->xcnt), X0 = sel->xprev ? (double)(sel->xprev - 1u) : X1;
+    // (sb_now / xcnt_now: this call's crossing superbin and the houses before its crossing bin)
+    const double X1 = (double)xcnt_now, X0 = sel->xprev ? (double)(sel->xprev - 1u) : X1;
     const double X = fmin(fmax(2.0 * X1 - X0, 0.0), s_C[kGqCells]), c0 = s_C[tid], c1 = s_C[tid + 1];
     if (T > 0.0 && X >= c0 && (X < c1 || tid == kGqCells - 1)) {
       const double f = c1 > c0 ? fmin((X - c0) / (c1 - c0), 1.0) : 0.0;
       const int sbp = (b0 + (int)(f * (double)(b1 - b0))) / (kGqBins / kGqSuper);
-      const int sb = sel->sb;
+      const int sb = sb_now;
       const int bias = sel->sb_raw >= 0 && sb < kGqSuper ? sb - sel->sb_raw : sel->sb_bias;
       sel->sb_bias = bias;
       sel->sb_raw = sbp;
-      sel->band_base = min(max(sbp + bias - (kGqBand / 2 - 1), 0), kGqSuper - kGqBand);
+      *band_out = min(max(sbp + bias - (kGqBand / 2 - 1), 0), kGqSuper - kGqBand);
     }
   }
   __syncthreads();  // (every thread has read xprev)
-  if (tid == 0) sel->xprev = ld_sc1(&sel->xcnt) + 1u;
-  if (tid == 0) { sel->kmin = nkmin; sel->scale = nscale; }  // (no later kernel of this call maps keys)
+  if (tid == 0) sel->xprev = xcnt_now + 1u;
+  if (tid == 0) { *kmin_out = nkmin; *scale_out = nscale; }  // (no later kernel of this call maps keys)
   __syncthreads();  // (every thread has read the superbin copies and the old map)
-  for (int e = tid; e < kGqCopies * kGqSupStride; e += blockDim.x) hist[kGqBins * 4 + e] = 0u;
+  if (zero_sup)
+    for (int e = tid; e < kGqCopies * kGqSupStride; e += blockDim.x) sup[e] = 0u;
 }
 
 // K3: every block finds the crossing bin inside superbin sb (lane l = its bin l) and the candidate
@@ -2194,10 +2433,10 @@ __device__ __forceinline__ void gq_next_map(const KParams& p, unsigned* __restri
 // as not taken (k_gq_select sets the window's), the window's houses go to win[] as (okey,
 // house << 2 | class, FSM word) at slots from one allocator atomic per block (unordered: select
 // orders them), and the ON houses of the decided (non-window) houses are counted into the slab
-__device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, double S, double pmin,
+__device__ bool gq_decide(const KParams& p, const uint4* __restrict__ sorted, double S, double pmin,
                           GqSel* __restrict__ sel, uint8_t* __restrict__ action, unsigned long long* __restrict__ slab,
                           uint4* s_e, bool sharded, bool ovf0, bool all, int ncand, double win_tot, bool more_after,
-                          bool in_lds);
+                          bool in_lds, const unsigned* a_add = nullptr, unsigned long long* st = nullptr);
 __device__ __forceinline__ void gq_store_sc1(uint4* d, const uint4& v);
 __device__ __forceinline__ uint4 gq_load_sc1(const uint4* s);
 __device__ __forceinline__ bool gq_less(const uint4& a, const uint4& b);
@@ -2213,32 +2452,44 @@ struct GqWin {
   int ncand;
   double win_tot;      // P before the window
   bool more_after;     // houses after the window
+  unsigned abelow[4];  // (abins given) the A class counts of superbin sb's bins below bs
+  unsigned xcnt;       // the houses before the crossing bin (GqSel.xcnt, the band's prediction)
 };
 // bins: the class counts of superbin sb's first bin in copy 0 (128 bins x 4 classes follow), the
 // other copies at multiples of cstride: gq_bins_flush's (g_hist, 512) or the band's (k_gq_binsc).
+// abins (the fused tick): the A class counts in the layout of bins; GqWin.abelow = their sums over
+// superbin sb's bins below bs.
+template <int NC = kGqCopies>  // (NC: the copies to sum; 1: counts summed by the caller)
 __device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __restrict__ bins, int cstride, double S,
                            GqSel* __restrict__ sel, int sb, bool all, bool ovf, bool whole, double base_tot,
-                           unsigned long long base_cnt, unsigned long long total) {
+                           unsigned long long base_cnt, unsigned long long total,
+                           const unsigned* __restrict__ abins = nullptr) {
   static_assert(kGqBins / kGqSuper == 64, "one bin per lane");
   static_assert(kGqCopies * 512 <= kGqBins * 4, "the bin copies fit below the superbin copies");
   __shared__ unsigned s_c[128];
   __shared__ int s_l0, s_le, s_cnt;
   __shared__ double s_base;
   __shared__ unsigned long long s_basec;
+  __shared__ unsigned s_ab[4];
   const int tid = threadIdx.x, lane = tid & 63;
   const bool on = !all && !ovf && !whole;
   const int bb = sb * 64;
   if (tid == 0) { s_l0 = 0; s_le = 0; s_cnt = 0; s_base = 0.0; s_basec = 0ull; }
+  if (tid < 4) s_ab[tid] = 0u;
   if (on && tid < 128) {
     double p_on[kWinCap];
 #pragma unroll
     for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
     unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
-    uint4 v[kGqCopies];  // (every copy's load issued before the first sum)
+    uint4 v[NC];  // (every copy's load issued before the first sum)
 #pragma unroll
-    for (int q = 0; q < kGqCopies; ++q) v[q] = *reinterpret_cast<const uint4*>(bins + q * cstride + tid * 4);
+    for (int q = 0; q < NC; ++q) v[q] = *reinterpret_cast<const uint4*>(bins + q * cstride + tid * 4);
+    uint4 va[NC];
+    if (abins && tid < 64)
 #pragma unroll
-    for (int q = 0; q < kGqCopies; ++q) {
+      for (int q = 0; q < NC; ++q) va[q] = *reinterpret_cast<const uint4*>(abins + q * cstride + tid * 4);
+#pragma unroll
+    for (int q = 0; q < NC; ++q) {
       c[0] += v[q].x; c[1] += v[q].y; c[2] += v[q].z; c[3] += v[q].w;
     }
     s_c[tid] = (unsigned)(c[0] + c[1] + c[2] + c[3]);
@@ -2258,6 +2509,19 @@ __device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __r
       const unsigned long long m = __ballot(cb > 0 && !(bef + pb < S));
       const int l0 = m ? __ffsll((long long)m) - 1 : 63;
       if (lane == l0) { s_l0 = l0; s_base = bef; s_basec = befc; }
+      if (abins) {  // the A counts of the bins below the crossing bin
+        unsigned a[4] = {0u, 0u, 0u, 0u};
+        if (lane < l0)
+#pragma unroll
+          for (int q = 0; q < NC; ++q) { a[0] += va[q].x; a[1] += va[q].y; a[2] += va[q].z; a[3] += va[q].w; }
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) a[k] += __shfl_xor(a[k], off);
+        if (lane == 0)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) s_ab[k] = a[k];
+      }
     }
   }
   __syncthreads();
@@ -2308,6 +2572,9 @@ __device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __r
   w.ncand = whole ? (int)total : s_cnt;
   w.win_tot = whole ? 0.0 : s_base;
   w.more_after = !whole && s_basec + (unsigned long long)s_cnt < total;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) w.abelow[k] = s_ab[k];
+  w.xcnt = (unsigned)(on ? s_basec : (all ? total : base_cnt));
   return w;
 }
 
@@ -2575,7 +2842,10 @@ __device__ void gq_exact(const KParams& p, double S, double pmin, uint8_t* __res
     unsigned long long xc = cd;
     if (tid == 0) s_d = 256;
     gq_block_scan(x, xc, s_w, s_wc);
-    if (tid < 256 && cd > 0 && !(base + (x - pd) + pd < S)) atomicMin(&s_d, tid);
+    {  // (one LDS atomic per wave: same-address LDS atomics serialise)
+      const unsigned long long m = __ballot(tid < 256 && cd > 0 && !(base + (x - pd) + pd < S));
+      if (m && (tid & 63) == 0) atomicMin(&s_d, (tid & ~63) + __ffsll((long long)m) - 1);
+    }
     __syncthreads();
     const int d = s_d;
     if (d >= 256) {  // (L = 0 only: the whole cluster's P stays below S) everything is taken
@@ -2669,11 +2939,16 @@ __device__ void gq_exact(const KParams& p, double S, double pmin, uint8_t* __res
 // rule); the ON counts of the window's decided actions; what the window cannot decide goes to
 // gq_exact (sharded: to the host, GqSel.need_fb — one shard cannot order the whole cluster).  The
 // window carries global house ids: only this shard's houses are written (offset p.goff).
-__device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, double S, double pmin,
+// a_add (the fused tick): every window house's byte is written (0 or 1: the step reads the window's
+// bytes only), and a_add[k] (the ON houses of the decided houses outside the window) joins class k's count
+// (returns true when the window could not decide: gq_exact decided, or sharded, the host must)
+__device__ bool gq_decide(const KParams& p, const uint4* __restrict__ sorted, double S, double pmin,
                           GqSel* __restrict__ sel, uint8_t* __restrict__ action, unsigned long long* __restrict__ slab,
                           uint4* s_e, bool sharded, bool ovf0, bool all, int ncand, double win_tot, bool more_after,
-                          bool in_lds) {
+                          bool in_lds, const unsigned* a_add, unsigned long long* st) {
   __shared__ uint8_t s_tk[kGqCap];
+#define GQD_STAMP(k) \
+  do { if (st && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
   __shared__ double s_tot;
   __shared__ int s_k, s_ovf;
   __shared__ unsigned s_cnt[kWinCap];
@@ -2708,6 +2983,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
     }
     if (tid < kWinCap) s_cnt[tid] = 0u;
     __syncthreads();
+    GQD_STAMP(0);
     // the crossing: the first house whose running P reaches S, by wave 0 alone, 64 houses a wave
     // prefix with the running total carried between them (r04: block-wide prefixes, four barriers a
     // round); sums of integer-valued P are exact in any order
@@ -2738,6 +3014,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
       }
     }
     __syncthreads();
+    GQD_STAMP(1);
     const int k = s_k;  // >= 0: the crossing lies in bin b*, inside the window
     for (int j = tid; j < (k < 0 ? ncand : k); j += nth) s_tk[j] = 1;
     if (k < 0) {
@@ -2776,6 +3053,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
       }
     }
     __syncthreads();
+    GQD_STAMP(2);
     ovf = s_ovf != 0;
     if (!ovf) {  // the window's actions and the ON counts they produce
       unsigned oncnt[kWinCap] = {0u, 0u, 0u, 0u};
@@ -2787,7 +3065,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
           const uint4 e = s_e[j];
           const bool take = s_tk[j] != 0;
           const int64_t li = (int64_t)(e.z >> 2) - p.goff;
-          if (take && li >= 0 && li < p.n) action[li] = 1;
+          if ((take || a_add) && li >= 0 && li < p.n) action[li] = take ? 1 : 0;
           cl = e.z & 3u;
           on1 = hv_on(hvac_fsm(e.w, take, p.dt, p.L));
         }
@@ -2799,9 +3077,12 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
         for (int c = 0; c < kWinCap; ++c)
           if (oncnt[c]) atomicAdd(&s_cnt[c], oncnt[c]);
       __syncthreads();
-      if (slab && tid < p.n_cap && s_cnt[tid]) atomicAdd(&slab[tid], (unsigned long long)s_cnt[tid]);
+      const unsigned add = tid < p.n_cap ? s_cnt[tid] + (a_add ? a_add[tid] : 0u) : 0u;
+      if (slab && tid < p.n_cap && add) atomicAdd(&slab[tid], (unsigned long long)add);
+      GQD_STAMP(3);
     }
   }
+#undef GQD_STAMP
   if (ovf && !sharded) gq_exact(p, S, pmin, action, slab);
   if (tid == 0) {  // (counters as atomics: a += would hold the launch's end behind a load's round trip)
     if (ovf) atomicAdd(&sel->fallbacks, 1u);
@@ -2811,6 +3092,7 @@ __device__ void gq_decide(const KParams& p, const uint4* __restrict__ sorted, do
     atomicAdd(&sel->calls, 1u);
     if (!all && !ovf) atomicAdd(&sel->ncand_sum, (unsigned long long)ncand);
   }
+  return ovf;
 }
 
 
@@ -2915,6 +3197,31 @@ __global__ void __launch_bounds__(1024) k_gq_select(KParams p, const uint4* __re
   }
 }
 
+// The window s_e[0, ncand) sorted in LDS by one block: a bitonic network over the next power of two
+// (sentinels past ncand sort last), log2(P)(log2(P)+1)/2 barriers — bounded at any window size, where a
+// rank by counting is quadratic in it.  (ncand <= kGqCap; the caller wrote s_e[0, ncand) before.)
+__device__ void gq_sort_lds(uint4* s_e, int ncand) {
+  const int tid = threadIdx.x;
+  int np2 = 1;
+  while (np2 < ncand) np2 <<= 1;
+  for (int e = ncand + tid; e < np2; e += (int)blockDim.x) s_e[e] = make_uint4(~0u, ~0u, ~0u, ~0u);
+  __syncthreads();
+  for (int k2 = 2; k2 <= np2; k2 <<= 1)
+    for (int j = k2 >> 1; j > 0; j >>= 1) {
+      for (int i = tid; i < np2; i += (int)blockDim.x) {
+        const int l = i ^ j;
+        if (l > i) {
+          const uint4 a = s_e[i], b = s_e[l];
+          if ((i & k2) == 0 ? gq_less(b, a) : gq_less(a, b)) {
+            s_e[i] = b;
+            s_e[l] = a;
+          }
+        }
+      }
+      __syncthreads();
+    }
+}
+
 // K3 of the single-GPU call after k_gq_binsc, in place of k_gq_compact + k_gq_select (one launch
 // fewer on every call: the host cannot know whether binsc compacted).  GqSel.hit (binsc cut the window
 // from the band and compacted): the blocks rank the window as k_gq_select does and the last block
@@ -2983,28 +3290,8 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint32_t* _
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only)
     if (!hit) {
       if (!all && !ovf) {
-        // the window sorted in LDS by this block alone: a bitonic network over the next power of
-        // two (sentinels past ncand sort last), log2(P)(log2(P)+1)/2 barriers — bounded at any window
-        // size, where a rank by counting is quadratic in it
-        int np2 = 1;
-        while (np2 < ncand) np2 <<= 1;
-        for (int e = tid; e < np2; e += (int)blockDim.x)
-          s_e[e] = e < ncand ? gq_load_sc1(win + e) : make_uint4(~0u, ~0u, ~0u, ~0u);
-        __syncthreads();
-        for (int k2 = 2; k2 <= np2; k2 <<= 1)
-          for (int j = k2 >> 1; j > 0; j >>= 1) {
-            for (int i = tid; i < np2; i += (int)blockDim.x) {
-              const int l = i ^ j;
-              if (l > i) {
-                const uint4 a = s_e[i], b = s_e[l];
-                if ((i & k2) == 0 ? gq_less(b, a) : gq_less(a, b)) {
-                  s_e[i] = b;
-                  s_e[l] = a;
-                }
-              }
-            }
-            __syncthreads();
-          }
+        for (int e = tid; e < ncand; e += (int)blockDim.x) s_e[e] = gq_load_sc1(win + e);
+        gq_sort_lds(s_e, ncand);
       }
       for (int e = tid; e < kGqBandOff + kGqCopies * kGqBandWords; e += (int)blockDim.x) hist[e] = 0u;
     }
@@ -3021,6 +3308,436 @@ __global__ void __launch_bounds__(1024) k_gq_finish(KParams p, const uint32_t* _
   }
 }
 
+
+// ---- the fused greedy tick (mdr_greedy_rollout; mdr_kernels.h GqfBufs)
+// A house's window entry: (okey, global id << 2 | class, FSM word) — gq_compact_houses' format.
+__device__ __forceinline__ uint4 gqf_entry(double k, int64_t gid, unsigned cls, uint32_t w) {
+  const uint64_t ok = gq_okey(k);
+  return make_uint4((uint32_t)ok, (uint32_t)(ok >> 32), ((uint32_t)gid << 2) | (cls & 3u), w);
+}
+// A: the house can turn on at the next step (hvac_fsm: not locked out after "if not on: sso += dt")
+__device__ __forceinline__ bool gqf_canon(uint32_t w, const KParams& p) {
+  const uint32_t Lu = p.L < 0 ? 0u : (uint32_t)p.L;
+  return hv_on(w) || hv_sso(w) + (uint32_t)p.dt >= Lu;
+}
+
+// The window's houses from (bin, copy) buckets into s_e[0, total), in (key, house) order: pair q = (bin
+// bi0 + q / kGqCopies, copy q % kGqCopies) holds cnt(q) entries at src(q); the pairs' exclusive offsets by
+// one block scan, then every thread fetches up to kGqCap / blockDim entries, each located by a binary
+// search over the offsets (all loads issued before the LDS stores).  The entries land bin-major, and a
+// bin's keys all precede the next bin's (gq_bin is monotone in the key), so each entry's rank is its
+// bin's offset plus the entries of its own bin that order before it (~tens of comparisons, not a sort
+// of the window); each thread then stores its entries at their ranks.  SC1: entries written by other
+// workgroups of this launch.  Returns the total (> kGqCap: nothing ordered, the caller falls back).
+template <bool SC1, typename CntF, typename SrcF>
+__device__ int gqf_gather(uint4* s_e, int npair, CntF cnt_of, SrcF src_of, unsigned long long* st = nullptr) {
+#define GQG_STAMP(k) \
+  do { if (st && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
+  constexpr int U = kGqCap / 1024;
+  __shared__ unsigned s_poff[kGqCopies * 64 + 1];
+  __shared__ unsigned s_ws[16];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const unsigned cnt = tid < npair ? cnt_of(tid) : 0u;
+  unsigned x = cnt;
+#pragma unroll
+  for (int off = 1; off < 64; off <<= 1) {
+    const unsigned y = __shfl_up(x, off);
+    if (lane >= off) x += y;
+  }
+  if (lane == 63) s_ws[tid >> 6] = x;
+  __syncthreads();
+  unsigned base = 0u;
+  for (int k = 0; k < (tid >> 6); ++k) base += s_ws[k];
+  if (tid < npair) s_poff[tid] = base + x - cnt;
+  if (tid == npair) s_poff[npair] = base + x - cnt;  // (the total: thread npair holds cnt 0)
+  __syncthreads();
+  const unsigned total = s_poff[npair];
+  GQG_STAMP(0);
+  if (st && threadIdx.x == 0) { st[3] = (unsigned long long)npair; st[4] = total; }
+  if (total > (unsigned)kGqCap) return (int)total;  // (block-uniform)
+  const int nf = (int)total;
+  uint4 v[U];
+  int q[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + u * (int)blockDim.x;
+    q[u] = 0;
+    if (e < nf) {
+      int lo = 0, hi = npair - 1;  // the last pair whose offset <= e
+      while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (s_poff[mid] <= (unsigned)e) lo = mid;
+        else hi = mid - 1;
+      }
+      q[u] = lo;
+      const uint4* src = src_of(lo) + (e - (int)s_poff[lo]);
+      v[u] = SC1 ? gq_load_sc1(src) : *src;
+    }
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + u * (int)blockDim.x;
+    if (e < nf) s_e[e] = v[u];
+  }
+  __syncthreads();
+  GQG_STAMP(1);
+  unsigned r[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + u * (int)blockDim.x;
+    r[u] = 0u;
+    if (e < nf) {
+      const int b0 = q[u] - q[u] % kGqCopies, b1 = min(b0 + kGqCopies, npair);
+      const int lo = (int)s_poff[b0], len = (int)s_poff[b1] - lo;
+      // the keys alone first (2 VALU a comparison: wave64 VALU is the bound here, r06 stamps), 8 LDS
+      // reads in flight a round, the rounds' tail by clamped re-reads of the bin's last entry counted
+      // once below; equal keys (the entry itself, or ties: rare) by house id in a second pass
+      uint32_t mx = v[u].x, my = v[u].y, mz = v[u].z;
+      asm volatile("" : "+v"(mx), "+v"(my), "+v"(mz));
+      const uint64_t mk = ((uint64_t)my << 32) | mx;
+      const uint64_t* kb = reinterpret_cast<const uint64_t*>(s_e + lo);  // (the key: the entry's first 8 bytes)
+      unsigned lt = 0u, eq = 0u;
+      const int full8 = len & ~7;
+      for (int f0 = 0; f0 < full8; f0 += 8) {
+        uint64_t t[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) t[j] = kb[2 * (f0 + j)];
+        __builtin_amdgcn_sched_barrier(0);  // (all 8 reads issued before the first compare waits)
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          lt += t[j] < mk ? 1u : 0u;
+          eq += t[j] == mk ? 1u : 0u;
+        }
+      }
+      for (int f = full8; f < len; ++f) {
+        const uint64_t t = kb[2 * f];
+        lt += t < mk ? 1u : 0u;
+        eq += t == mk ? 1u : 0u;
+      }
+      unsigned k = (unsigned)lo + lt;
+      if (eq > 1u)  // (ties: the house order among the equal keys)
+        for (int f = 0; f < len; ++f) {
+          const uint4 t = s_e[lo + f];
+          k += (((uint64_t)t.y << 32) | t.x) == mk && t.z < mz ? 1u : 0u;
+        }
+      r[u] = k;
+    }
+  }
+  GQG_STAMP(5);
+  __syncthreads();
+  GQG_STAMP(6);
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int e = tid + u * (int)blockDim.x;
+    if (e < nf) s_e[r[u]] = v[u];
+  }
+  __syncthreads();
+  GQG_STAMP(2);
+#undef GQG_STAMP
+  return (int)total;
+}
+
+// The producer without a step (a rollout's first decision, or after the state changed): the current
+// state's keys under parity par's map into parity region par (zeroed before, k_zero_u64), as the
+// GQ = 2 step epilogue writes them.  A block per kGqStage houses (its packed LDS counts < 2^16);
+// block 0 zeroes the slab the decision is counted into.
+__global__ void __launch_bounds__(kGqThreads) k_gq_keys2(KParams p, GqfBufs fz, int par, double* __restrict__ part,
+                                                         unsigned long long* __restrict__ slab) {
+  constexpr int U = kGqStage / kGqThreads;
+  __shared__ unsigned s_sh[4 * kGqSupStride];
+  __shared__ uint32_t s_map[kGqCells];
+  __shared__ unsigned s_acnt[8];
+  const int tid = threadIdx.x;
+  for (int e = tid; e < 4 * kGqSupStride; e += blockDim.x) s_sh[e] = 0u;
+  if (tid < 8) s_acnt[tid] = 0u;
+  for (int e = tid; e < kGqCells; e += blockDim.x) s_map[e] = fz.map[par][e];
+  if (blockIdx.x == 0 && slab)
+    for (int e = tid; e < kCountShards * p.n_cap; e += blockDim.x) slab[e] = 0ull;
+  __syncthreads();
+  const double kmin = fz.sel->fkmin[par], scale = fz.sel->fscale[par];
+  const uint32_t band0 = (uint32_t)fz.sel->fband[par] * 64u;
+  const int cp = (int)(blockIdx.x % kGqCopies);
+  unsigned* R = fz.par[par];
+  unsigned* bandC = R + kGqfOffBandC + cp * kGqBandWords;
+  unsigned* bandA = R + kGqfOffBandA + cp * kGqBandWords;
+  unsigned* bandN = R + kGqfOffBandN + cp * (kGqBand * 64);
+  uint4* bkt = fz.bkt[par] + (size_t)cp * (kGqBand * 64) * fz.cap;
+  double lo = INFINITY, hi = -INFINITY;
+  GqfAcnt acnt{0u, 0u, 0u, 0u};
+  const int64_t b0 = (int64_t)blockIdx.x * kGqStage;
+  double ta[U], tg[U];
+  uint32_t hw[U];
+  unsigned cl[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = b0 + u * kGqThreads + tid, ic = i < p.n ? i : p.n - 1;
+    ta[u] = p.t_air[ic];
+    tg[u] = p.target[ic];
+    hw[u] = p.hvac[ic];
+    cl[u] = p.cap_idx[ic];
+  }
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int64_t i = b0 + u * kGqThreads + tid;
+    if (i >= p.n) break;
+    const double k = -(ta[u] - tg[u]);  // gq_key_of
+    const uint32_t c = gq_code(k, kmin, scale, s_map, cl[u]);
+    if (k == k) {
+      lo = fmin(lo, k);
+      hi = fmax(hi, k);
+    }
+    const bool canon = gqf_canon(hw[u], p);
+    atomicAdd(&s_sh[((tid >> 6) & 3) * kGqSupStride + (c >> 8) * 4 + (c & 3u)], 1u);
+    gqf_acount(acnt, canon, (c >> 2) < band0, c & 3u);
+    const uint32_t bo = (c >> 2) - band0;
+    if (bo < (uint32_t)(kGqBand * 64)) {
+      atomicAdd(&bandC[bo * 4 + (c & 3u)], 1u);
+      if (canon) atomicAdd(&bandA[bo * 4 + (c & 3u)], 1u);
+      const unsigned slot = atomicAdd(&bandN[bo], 1u);
+      if (slot < (unsigned)fz.cap) bkt[(size_t)bo * fz.cap + slot] = gqf_entry(k, p.goff + i, c, hw[u]);
+      else atomicOr(&R[kGqfOffFlags], 1u);
+    }
+  }
+  gqf_acount_wave(acnt, s_acnt);
+  __syncthreads();
+  gqf_flush(s_sh, 4, R, lo, hi, part, s_acnt);
+}
+
+// The fused decision (kGqSelBlocks blocks of 1024): from parity par's counts (its producer: the
+// previous step's epilogue or k_gq_keys2) every block finds the crossing superbin (gq_super_scan); then
+//  * band hit (the producer's band holds superbins sb and sb + 1, no bucket overflowed): block 0 alone
+//    cuts the window from the band's bin counts (gq_window), gathers its houses from the band's buckets
+//    into LDS in (key, house) order (gqf_gather) and decides (gq_decide: the window houses' bytes into
+//    fz.dec, the ON counts of every decided house into the slab — the A counts below the window, from
+//    the A copies it loaded beside the C copies, plus the window's); no hand-off between workgroups;
+//  * miss: every block passes over its slice of the cluster, the keys under parity par's map, counting
+//    the bins of superbins sb and sb + 1 (C, A) and appending their houses to the miss buckets (sc1:
+//    read by the last block of this launch); the last block cuts the window, gathers it in order and
+//    decides, then zeroes the miss region;
+//  * everything taken (the cluster's P < S): block 0 takes every house, the ON counts = all A counts;
+//  * a NaN crossing, a cluster of <= kGqCap houses, a crossing bin over kGqCap houses, a full bucket
+//    or a walk past the window: gq_exact decides every house (kGqfFull), in block 0 (the last on a miss).
+// The decision (GqSel.fmode, fbs, fbe) is the step's (k_step_pipe GQ = 2).  Every block zeroes its
+// slice of the other parity's region (read by the previous call; the step after this call produces
+// into it).  The next map (parity 1 - par, its band in fband[1 - par]) is block 1's, beside block 0's
+// decision — on a miss the last block's, after the decision (the window's xcnt feeds the band).
+__global__ void __launch_bounds__(1024) k_gq_decide2(KParams p, GqfBufs fz, int par, double S, double pmin,
+                                                     unsigned long long* __restrict__ slab,
+                                                     unsigned* __restrict__ tickets, const double* __restrict__ part,
+                                                     int nparts) {
+  __shared__ uint4 s_e[kGqCap];
+  __shared__ unsigned s_apre[4], s_asum[8];
+  __shared__ int s_bad;
+  __shared__ uint32_t s_map[kGqCells];
+  __shared__ unsigned s_band[2][kGqBand * 64 * 4];  // (blocks 0, 1) the band's C and A bin counts
+  static_assert(2 * kGqBand * 64 == 1024 && kGqfBandN == 4 * 1024, "a thread per band bin and kind; 4 bucket counts each");
+  const int tid = threadIdx.x, lane = tid & 63;
+  GqSel* sel = fz.sel;
+  // diagnostics: the constant 100 MHz clock at the phases of this block (fz.stamps[block][kGqfStampWords])
+#define GQF_STAMP(k)                                                                              \
+  do {                                                                                            \
+    if (fz.stamps && tid == 0) fz.stamps[blockIdx.x * kGqfStampWords + (k)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+  GQF_STAMP(0);
+  unsigned* R = fz.par[par];
+  {  // the other parity's region, for the step after this decision
+    unsigned* Z = fz.par[1 - par];
+    for (int e = (int)(blockIdx.x * blockDim.x) + tid; e < kGqfParWords; e += (int)(gridDim.x * blockDim.x)) Z[e] = 0u;
+  }
+  const bool bovf = R[kGqfOffFlags] != 0u;
+  const int pb = sel->fband[par];
+  // the superbin copies, loaded only by the threads that own a superbin (every thread loading them
+  // made 256 blocks x 1024 threads read 33 MB of L2 per call: ~5 us; r06 phase stamps); block 0 (the
+  // decider unless the band misses) loads the A summary's copies beside them
+  GqSupLoad sup;
+#pragma unroll
+  for (int q = 0; q < kGqCopies; ++q) sup.v[q] = make_uint4(0u, 0u, 0u, 0u);
+  if (tid < kGqSupN)
+#pragma unroll
+    for (int q = 0; q < kGqCopies; ++q) sup.v[q] = *reinterpret_cast<const uint4*>(R + q * kGqSupStride + tid * 4);
+  const unsigned asv = blockIdx.x == 0 && tid < kGqCopies * 8 ? R[kGqfOffASum + tid] : 0u;
+  if (tid < 8) s_asum[tid] = 0u;
+  // blocks 0 and 1 (they cut the window unless the band misses): the band's C and A bin counts summed
+  // over the copies into LDS (a thread per bin and kind), and block 0 the band's bucket counts (into
+  // s_e: gqf_gather reads them before it stores an entry) — issued beside the superbin loads, so the
+  // window and the gather start without a round trip to memory
+  if (blockIdx.x <= 1 && !bovf) {
+    const int bn = tid & (kGqBand * 64 - 1), kind = tid / (kGqBand * 64);  // (kind 0: C, 1: A)
+    const unsigned* src = R + (kind ? kGqfOffBandA : kGqfOffBandC) + bn * 4;
+    uint4 bv[kGqCopies];
+#pragma unroll
+    for (int q = 0; q < kGqCopies; ++q) bv[q] = *reinterpret_cast<const uint4*>(src + q * kGqBandWords);
+    uint4 nv = make_uint4(0u, 0u, 0u, 0u);
+    if (blockIdx.x == 0) nv = *reinterpret_cast<const uint4*>(R + kGqfOffBandN + tid * 4);
+    uint4 t = bv[0];
+#pragma unroll
+    for (int q = 1; q < kGqCopies; ++q) { t.x += bv[q].x; t.y += bv[q].y; t.z += bv[q].z; t.w += bv[q].w; }
+    *reinterpret_cast<uint4*>(&s_band[kind][bn * 4]) = t;
+    if (blockIdx.x == 0) *reinterpret_cast<uint4*>(reinterpret_cast<unsigned*>(s_e) + tid * 4) = nv;
+  }
+  if (tid < 4) s_apre[tid] = 0u;
+  if (fz.stamps) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    GQF_STAMP(16);
+  }
+  const GqSuper g = gq_super_scan(p, sup, S, sel, nullptr, false);  // (ends with a block barrier)
+  GQF_STAMP(1);
+  const bool all = g.sb >= kGqSupN, nanx = g.sb == kGqSuper && !g.whole;
+  const bool hit = !all && !nanx && !g.whole && !bovf && g.sb >= pb && g.sb + 1 < pb + kGqBand;
+  // 0 band window, 1 miss, 2 everything taken, 3 gq_exact (the same in every block)
+  int path = all ? 2 : (nanx || g.whole) ? 3 : hit ? 0 : 1;
+  const int path0 = path;
+  GqWin w{};
+  if (path != 1) {
+    if (blockIdx.x > 1) return;  // (block-uniform: blocks 0 and 1 decide and map)
+    if (asv) atomicAdd(&s_asum[tid & 7], asv);  // (block 0: A_lo, A_all over the copies; zeroed before the scan's barriers)
+    const int off = hit ? (g.sb - pb) * 64 * 4 : 0;
+    w = gq_window<1>(p, s_band[0] + off, 0, S, sel, g.sb, path != 0, path == 3, g.whole, g.before, g.before_cnt,
+                     g.total, s_band[1] + off);
+    if (path == 0 && w.ovf) path = 3;  // (a crossing bin over kGqCap houses)
+    GQF_STAMP(3);
+    if (blockIdx.x == 1) {  // the next map, beside block 0's decision
+      gq_next_map_core(p, R, part, nparts, sel, fz.map[par], sel->fkmin[par], sel->fscale[par], fz.map[1 - par],
+                       &sel->fkmin[1 - par], &sel->fscale[1 - par], reinterpret_cast<unsigned char*>(s_e), false,
+                       g.sb, w.xcnt, &sel->fband[1 - par]);
+      GQF_STAMP(8);
+      return;
+    }
+    if (path == 0) {  // the band's A bins of its superbins below the crossing one: a wave sum, one LDS atomic per wave and class
+      unsigned a[4] = {0u, 0u, 0u, 0u};
+      if (tid < (g.sb - pb) * 64)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a[k] = s_band[1][tid * 4 + k];
+      if (tid < (kGqBand - 1) * 64) {  // (wave-uniform bound)
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+          for (int off = 32; off > 0; off >>= 1) a[k] += __shfl_xor(a[k], off);
+        if (lane == 0)
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (a[k]) atomicAdd(&s_apre[k], a[k]);
+      }
+    }
+  } else {  // the miss pass: this block's slice, the bins of superbins sb and sb + 1, and the A_lo of the houses below them
+    for (int e = tid; e < kGqCells; e += blockDim.x) s_map[e] = fz.map[par][e];
+    if (tid < 8) s_asum[tid] = 0u;
+    __syncthreads();
+    const double kmin = sel->fkmin[par], scale = sel->fscale[par];
+    const uint32_t bb = (uint32_t)g.sb * 64u;
+    const int cp = (int)(blockIdx.x % kGqCopies);
+    unsigned* M = fz.miss;
+    GqfAcnt acnt{0u, 0u, 0u, 0u};
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + tid; i < p.n; i += (int64_t)gridDim.x * blockDim.x) {
+      const double k = gq_key_of(p, i);
+      const uint32_t bin = (uint32_t)(k != k ? kGqBins : gq_bin(k, kmin, scale, s_map)), b = bin - bb;
+      const unsigned cls = p.cap_idx[i] & 3u;
+      const uint32_t hw = p.hvac[i];
+      const bool canon = gqf_canon(hw, p);
+      gqf_acount(acnt, canon, bin < bb, cls);
+      if (b < 128u) {
+        atomicAdd(&M[(cp * 128 + b) * 4 + cls], 1u);
+        if (canon) atomicAdd(&M[kGqfMissC + (cp * 128 + b) * 4 + cls], 1u);
+        const unsigned slot = atomicAdd(&M[2 * kGqfMissC + cp * 128 + b], 1u);
+        if (slot < (unsigned)fz.mcap) gq_store_sc1(fz.mbkt + ((size_t)(cp * 128 + b)) * fz.mcap + slot,
+                                                   gqf_entry(k, p.goff + i, cls, hw));
+        else atomicOr(&M[2 * kGqfMissC + kGqfMissN], 1u);
+      }
+    }
+    gqf_acount_wave(acnt, s_asum);
+    __syncthreads();
+    if (tid < 4 && s_asum[tid]) atomicAdd(&M[kGqfOffMissALo + tid], s_asum[tid]);
+    // hand-offs to the last block: the miss counts, A_lo and buckets (atomics, sc1 stores)
+    const bool last = grid_last_block(tickets);
+    GQF_STAMP(6);
+    if (!last) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // (compiler ordering only)
+    if (tid < 4) s_asum[tid] = ld_sc1(&M[kGqfOffMissALo + tid]);  // (the cluster's A_lo below sb, in place of the band's)
+  }
+  __syncthreads();  // (s_apre, s_asum)
+  GQF_STAMP(11);
+  // the deciding block (block 0, or the last on a miss)
+  int mode = kGqfBandMode, bs = w.bs, be = w.be;
+  bool ovf0 = path == 3, more_after = w.more_after;
+  int ncand = w.ncand;
+  double win_tot = w.win_tot;
+  unsigned xcnt = w.xcnt;
+  unsigned aadd[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) aadd[k] = s_asum[k] + s_apre[k] + w.abelow[k];
+  if (path == 0) {  // the window's houses from the band buckets: (bin, copy) pairs, bin-major
+    const int bi0 = w.bs - pb * 64, npair = (w.be - w.bs + 1) * kGqCopies;  // (<= 64 x 8)
+    const int np = gqf_gather<false>(
+        s_e, npair,
+        [&](int q) {  // (prefetched into s_e)
+          return reinterpret_cast<const unsigned*>(s_e)[(q % kGqCopies) * (kGqBand * 64) + bi0 + q / kGqCopies];
+        },
+        [&](int q) { return fz.bkt[par] + ((size_t)(q % kGqCopies) * (kGqBand * 64) + bi0 + q / kGqCopies) * fz.cap; },
+        fz.stamps ? fz.stamps + blockIdx.x * kGqfStampWords + 18 : nullptr);
+    ovf0 = np != w.ncand;  // (cannot happen: the buckets hold the counted houses)
+    GQF_STAMP(4);
+  } else if (path == 1) {
+    // the miss counts into LDS (sc1: other workgroups' atomics) — C and A behind the window array
+    unsigned* lc = reinterpret_cast<unsigned*>(s_e);
+    unsigned* M = fz.miss;
+    for (int e = tid; e < 2 * kGqfMissC; e += blockDim.x) lc[e] = ld_sc1(&M[e]);
+    if (tid == 0) s_bad = ld_sc1(&M[2 * kGqfMissC + kGqfMissN]) != 0u;
+    __syncthreads();
+    const GqWin wm = gq_window(p, lc, 512, S, sel, g.sb, false, false, false, g.before, g.before_cnt, g.total,
+                               lc + kGqfMissC);
+    xcnt = wm.xcnt;
+    __syncthreads();  // (done with lc: the window goes into s_e)
+    ovf0 = wm.ovf || s_bad;
+    if (!ovf0) {  // gather [bs, be] of the miss bins (bin-major, copies inside) in order
+      const int bi0 = wm.bs - g.sb * 64, npair = (wm.be - wm.bs + 1) * kGqCopies;
+      const int np = gqf_gather<true>(
+          s_e, npair, [&](int q) { return ld_sc1(&M[2 * kGqfMissC + (q % kGqCopies) * 128 + bi0 + q / kGqCopies]); },
+          [&](int q) { return fz.mbkt + ((size_t)(q % kGqCopies) * 128 + bi0 + q / kGqCopies) * fz.mcap; });
+      ovf0 = np != wm.ncand;
+      ncand = wm.ncand;
+      win_tot = wm.win_tot;
+      more_after = wm.more_after;
+      bs = wm.bs;
+      be = wm.be;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) aadd[k] = s_asum[k] + wm.abelow[k];
+    }
+    // the miss region back to zero for the next call (this block was its only reader)
+    for (int e = tid; e < kGqfMissWords; e += blockDim.x) M[e] = 0u;
+  }
+  bool full = false;
+  if (path == 2) {  // everything taken: the ON counts of every house (shard 0; the rest are zero)
+    mode = kGqfAll;
+    if (tid < p.n_cap) slab[tid] = s_asum[4 + tid];  // (A_all)
+  } else {
+    // (a walk past the window, or ovf0: gq_decide's own gq_exact decides every house)
+    full = gq_decide(p, nullptr, S, pmin, sel, fz.dec, slab, s_e, false, ovf0, false, ncand, win_tot, more_after,
+                     true, aadd, fz.stamps ? fz.stamps + blockIdx.x * kGqfStampWords + 12 : nullptr);
+    if (!full && tid == 0) sel->fwin = (unsigned)ncand;
+  }
+  if (full) mode = kGqfFull;
+  if (tid == 0) {
+    sel->fmode = mode;
+    sel->fbs = bs;
+    sel->fbe = be;
+    atomicAdd(&sel->fcalls, 1u);
+    if (path0 == 0 && path == 0) atomicAdd(&sel->fhits, 1u);
+    if (path0 == 1) atomicAdd(&sel->fmisses, 1u);
+    if (full) atomicAdd(&sel->fexact, 1u);
+    sel->overflow = 0;
+  }
+  GQF_STAMP(7);
+  if (fz.stamps && tid == 0) fz.stamps[blockIdx.x * kGqfStampWords + 10] = 1;  // (the deciding block)
+  if (path0 == 1) {  // the next map here, after the miss window's xcnt (see above)
+    __syncthreads();
+    gq_next_map_core(p, R, part, nparts, sel, fz.map[par], sel->fkmin[par], sel->fscale[par], fz.map[1 - par],
+                     &sel->fkmin[1 - par], &sel->fscale[1 - par], reinterpret_cast<unsigned char*>(s_e), false, g.sb,
+                     xcnt, &sel->fband[1 - par]);
+    GQF_STAMP(8);
+  }
+  GQF_STAMP(9);
+#undef GQF_STAMP
+}
 
 // sharded greedy (mdr_greedy_inputs / mdr_greedy_select): this shard's (key, P, lockout) rows, and
 // the generic gather / iota for the cluster-wide selection over the gathered rows

@@ -604,15 +604,21 @@ class Environment:
             rewards = torch.empty((n_ticks, self._n_local), dtype=torch.float64, device=sh.device)
         rew_stride = 0 if rewards.dim() == 1 else self._n_local  # 1-D: every tick overwrites it
         drivers_whole = self.power_grid.interp is None and self._links is not None  # one driver window
-        if (drivers_whole and not use_graph and self._comm is None and actions is None and n_ticks >= 2
+        native = self._comm is not None and getattr(self._comm, "native", False)
+        if (drivers_whole and not use_graph and (self._comm is None or native) and actions is None and n_ticks >= 2
                 and self._vector_drivers_ok() and _host is not None and _host_gauss_ok(self.rng)
                 and not self._grid_pending):
-            # one C call: mdr_rollout_begin, the host drivers, mdr_rollout (no Python between them)
-            launch = (L.fn_addr("mdr_rollout_begin"), L.fn_addr("mdr_rollout"), sh.ctx.value, sh.stream(),
-                      rewards.data_ptr(), rew_stride, sh.p_dev.data_ptr(), mode)
+            # one C call: mdr_rollout_begin, the host drivers, mdr_rollout / mdr_rollout_sharded (no
+            # Python between them: r06, the sharded call's Python driver loop cost ~50 us a call)
+            launch = (L.fn_addr("mdr_rollout_begin"), L.fn_addr("mdr_rollout_sharded" if native else "mdr_rollout"),
+                      sh.ctx.value, sh.stream(), rewards.data_ptr(), rew_stride, sh.p_dev.data_ptr(), mode,
+                      1 if native else 0)
             ticks, launched = self._driver_window_vec(n_ticks, launch)
             if not launched:  # (the window crossed midnight: the drivers were finished in Python)
-                sh.rollout(ticks, None, 0, mode, rewards, rew_stride, False)
+                if native:
+                    self._comm.rollout(sh, ticks, None, mode, rewards, rew_stride)
+                else:
+                    sh.rollout(ticks, None, 0, mode, rewards, rew_stride, False)
             self._P_dev_valid = True
             self.finish_grid_step()
             self._counts_ready = 0

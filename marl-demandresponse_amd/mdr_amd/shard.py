@@ -306,6 +306,14 @@ class HipShard:
         return {"skips": int(v[0]), "calls": int(v[1]), "misses": int(v[1]) - int(v[0]), "band_base": int(v[2]),
                 "band_width": int(v[3])}
 
+    def greedy_fused_diag(self) -> dict:
+        """The fused tick's counters (mdr_greedy_fused_diag; synchronises): decisions, band hits,
+        misses (the decision's own pass over the cluster), exact decisions, the last mode and window."""
+        v = (C.c_uint64 * 6)()
+        L.check(self.lib.mdr_greedy_fused_diag(self.ctx, v), "mdr_greedy_fused_diag")
+        return {"calls": int(v[0]), "hits": int(v[1]), "misses": int(v[2]), "exact": int(v[3]),
+                "last_mode": int(v[4]), "last_window": int(v[5])}
+
     def obs(self, spec, scalars, out, use_p_dev=True):
         L.check(self.lib.mdr_obs(self.ctx, C.byref(spec), C.byref(scalars),
                                  L.ptr(self.p_dev) if use_p_dev else 0, L.ptr(out), self.stream()),

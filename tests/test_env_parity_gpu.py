@@ -516,11 +516,11 @@ def test_perlin_trajectory_vs_oracle(torch_gpu, path):
 
 
 
-def _greedy_env(n, seed):
+def _greedy_env(n, seed, signal="sinusoidals"):
     from mdr_amd.environment import Environment
 
     props = gu.props_from_overrides({"cluster_prop.nb_agents": n,
-                                     "power_grid_prop.signal_properties.mode": "sinusoidals"})
+                                     "power_grid_prop.signal_properties.mode": signal})
     return props, Environment(props, rng=random.Random(seed), population="synthetic", seed=seed)
 
 
@@ -592,6 +592,115 @@ def test_greedy_rollout_matches_loop(torch_gpu, strided):
     assert a.cluster.current_power_consumption == b.cluster.current_power_consumption
 
 
+@pytest.mark.parametrize("n,signal,T", [(3001, "sinusoidals", 30), (200_003, "sinusoidals", 40),
+                                        (1 << 20, "sinusoidals", 40), (1 << 20, "regular_steps", 40),
+                                        (1 << 20, "perlin", 40), (1 << 22, "sinusoidals", 12)])
+def test_greedy_fused_matches_per_tick(torch_gpu, n, signal, T):
+    """The fused tick (MDR_OPT_GQ_FUSED: k_gq_decide2 -> k_step_pipe<..., GQ = 2>, the decision applied
+    from the pre-step keys) against the per-tick form (mdr_ctrl_greedy + mdr_step, itself pinned to
+    the oracle and to the Python loop) on twins: every tick's actions and rewards bit for bit, the
+    state after, for the sinusoidal, regular-steps (a budget jump at every step edge) and perlin
+    signals, ragged and 4M-house clusters; the fused counters (band hits, misses, exact) printed."""
+    torch = torch_gpu
+    _, a = _greedy_env(n, 53, signal)
+    _, b = _greedy_env(n, 53, signal)
+    b.shard.set_option("gq_fused", 0)
+    acts_a = torch.empty((T, n), dtype=torch.uint8, device="cuda")
+    acts_b = torch.empty((T, n), dtype=torch.uint8, device="cuda")
+    ra = a.greedy_rollout(T, actions=acts_a)[1]
+    rb = b.greedy_rollout(T, actions=acts_b)[1]
+    for t in range(T):
+        assert torch.equal(acts_a[t], acts_b[t]), t
+        assert torch.equal(ra[t], rb[t]), t
+    sa, sb = a.shard.host_state(), b.shard.host_state()
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    assert a.cluster.current_power_consumption == b.cluster.current_power_consumption
+    fd = a.shard.greedy_fused_diag()
+    print(signal, n, "fused", fd)
+    assert fd["calls"] == T
+
+
+@pytest.mark.parametrize("n", [200_003, 1 << 20])
+def test_greedy_fused_jumping_budgets(torch_gpu, n):
+    """The fused tick's miss path (the decision's own pass over the cluster, its last block sorting the
+    window) and its hit path after it: mdr_greedy_rollout over 32 ticks whose budgets jump at random
+    across the cluster's cumulative power every 4th tick and stay put in between, against the per-tick
+    form on a twin fed the same ticks; actions, rewards, state bit for bit."""
+    torch = torch_gpu
+    from mdr_amd.environment import TickWindow
+
+    props, a = _greedy_env(n, 59)
+    _, b = _greedy_env(n, 59)
+    b.shard.set_option("gq_fused", 0)
+    T = 32
+    ta = a.driver_window(T)
+    tb = TickWindow(ta.a.copy())
+    b.driver_window(T)  # (the twin's clock, unused)
+    prm = a.shard.host_params()
+    p_all = float(np.sum(np.array(a._cap_values, np.float64)[prm["cap_idx"]]) /
+                  props.cluster_prop.house_prop.hvac_prop.cop)
+    rs = np.random.RandomState(11)
+    S = p_all * np.repeat(rs.uniform(0.05, 0.95, T // 4), 4)
+    ta.s_prev[:] = S
+    tb.s_prev[:] = S
+    out = []
+    for e, tw in ((a, ta), (b, tb)):
+        acts = torch.empty((T, n), dtype=torch.uint8, device="cuda")
+        rews = torch.empty((T, n), dtype=torch.float64, device="cuda")
+        e.shard.greedy_rollout(tw, acts, n, rews, n)
+        out.append((acts, rews, e.shard.host_state()))
+    for t in range(T):
+        assert torch.equal(out[0][0][t], out[1][0][t]), t
+        assert torch.equal(out[0][1][t], out[1][1][t]), t
+    for k in out[0][2]:
+        np.testing.assert_array_equal(out[0][2][k], out[1][2][k], err_msg=k)
+    fd = a.shard.greedy_fused_diag()
+    print("jumping budgets", n, fd)
+    assert fd["calls"] == T and fd["misses"] + fd["exact"] >= 1
+
+
+@pytest.mark.parametrize("case", ["nan_crossing", "identical_crossing", "after_state_write"])
+def test_greedy_fused_exact_and_restart(torch_gpu, case):
+    """The fused tick where the window cannot decide (a crossing among NaN keys, 10,000 identical keys
+    around the crossing: gq_exact, kGqfFull) and after the state was rewritten between two rollouts
+    (the producer k_gq_keys2 runs again): == the per-tick form on a twin, 4 ticks."""
+    torch = torch_gpu
+    from mdr_amd.shard import encode_hvac
+
+    n = 60_000
+    envs = [_greedy_env(n, 31)[1], _greedy_env(n, 31)[1]]
+    envs[1].shard.set_option("gq_fused", 0)
+    outs = []
+    for e in envs:
+        sh = e.shard
+        prm = sh.host_params()
+        rs = np.random.RandomState(7)
+        tg = prm["target"].copy()
+        T = tg + rs.normal(0.0, 1.0, n)
+        lock = rs.rand(n) < 0.3
+        if case == "nan_crossing":
+            T[rs.choice(n, 40000, replace=False)] = np.nan
+        elif case == "identical_crossing":
+            T[:50000] = 24.0
+            tg[:50000] = 22.5
+        if case == "after_state_write":
+            e.greedy_rollout(3)
+        sh.t_air.copy_(torch.from_numpy(T).cuda())
+        sh.target.copy_(torch.from_numpy(tg).cuda())
+        sh.hvac.copy_(torch.from_numpy(encode_hvac(~lock & (rs.rand(n) < 0.5), lock, rs.randint(0, 60, n))).cuda())
+        sh.params_changed()
+        acts = torch.empty((4, n), dtype=torch.uint8, device="cuda")
+        r = e.greedy_rollout(4, actions=acts)[1]
+        outs.append((acts.clone(), r.clone(), sh.host_state()))
+    (aa, ra, sa), (ab, rb, sb) = outs
+    assert torch.equal(aa, ab)
+    assert torch.equal(ra, rb)
+    for k in sa:
+        np.testing.assert_array_equal(sa[k], sb[k], err_msg=k)
+    print(case, envs[0].shard.greedy_fused_diag())
+
+
 @pytest.mark.parametrize("n", [200_003, 1 << 20])
 def test_greedy_band_forms_agree(torch_gpu, n):
     """The band's two launches (k_gq_binsc + k_gq_finish) against the r04 three (MDR_OPT_GQ_BAND 0)
@@ -603,6 +712,8 @@ def test_greedy_band_forms_agree(torch_gpu, n):
     props, a = _greedy_env(n, 37)
     _, b = _greedy_env(n, 37)
     b.shard.set_option("gq_band", 0)
+    for e in (a, b):  # (the per-tick forms: mdr_ctrl_greedy + mdr_step, not the fused tick)
+        e.shard.set_option("gq_fused", 0)
     ra, rb = a.greedy_rollout(24)[1], b.greedy_rollout(24)[1]
     assert torch.equal(ra, rb)
     prm = a.shard.host_params()

@@ -28,6 +28,8 @@ PKG = os.path.join(ROOT, "marl-demandresponse_amd")
 BEGIN = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_uint64, C.c_void_p, C.c_int64, C.c_int, C.c_void_p)
 ROLL = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p,
                    C.c_int64, C.c_void_p, C.c_int, C.c_void_p)
+ROLL_SHARDED = C.CFUNCTYPE(C.c_int, C.c_void_p, C.c_int, C.c_void_p, C.c_void_p, C.c_int64, C.c_int, C.c_void_p,
+                           C.c_int64, C.c_void_p, C.c_void_p)
 
 
 def _env(start):
@@ -40,7 +42,7 @@ def _env(start):
     return Environment(props, rng=random.Random(3), _shard_factory=OracleShard)
 
 
-def _launch(rc_begin, rc_roll, calls):
+def _launch(rc_begin, rc_roll, calls, sharded=False):
     def begin(ctx, n, tick0, action, stride, mode, stream):
         calls.append(("begin", n, tick0, mode))
         return rc_begin
@@ -50,9 +52,14 @@ def _launch(rc_begin, rc_roll, calls):
         calls.append(("rollout", n, int(rows[0, 3:].view(np.uint64)[0]), mode))
         return rc_roll
 
-    cb = (BEGIN(begin), ROLL(roll))
+    def roll_sharded(ctx, n, ticks, action, stride, mode, reward, rew_stride, p_out, stream):
+        rows = np.ctypeslib.as_array(C.cast(ticks, C.POINTER(C.c_double)), shape=(n, 4)).copy()
+        calls.append(("rollout_sharded", n, int(rows[0, 3:].view(np.uint64)[0]), mode))
+        return rc_roll
+
+    cb = (BEGIN(begin), ROLL_SHARDED(roll_sharded) if sharded else ROLL(roll))
     addr = [C.cast(f, C.c_void_p).value for f in cb]
-    return cb, (addr[0], addr[1], 0x1000, 0, 0x2000, 10, 0x3000, 1)
+    return cb, (addr[0], addr[1], 0x1000, 0, 0x2000, 10, 0x3000, 1, 1 if sharded else 0)
 
 
 def rollout1_cases():
@@ -83,6 +90,16 @@ def rollout1_cases():
     cb, launch = _launch(0, 0, calls)
     w, launched = _env(dt.datetime(2021, 7, 4, 23, 59, 30))._driver_window_vec(20, launch)
     assert not launched and len(w) == 20 and [c[0] for c in calls] == ["begin"]
+    # 4. a sharded context (a communicator attached in the library): mdr_rollout_sharded's signature
+    calls = []
+    cb, launch = _launch(0, 0, calls, sharded=True)
+    w, launched = _env(noon)._driver_window_vec(20, launch)
+    assert launched and len(w) == 20 and calls[-1] == ("rollout_sharded", 20, 0, 1)
+    calls = []
+    cb, launch = _launch(0, -2, calls, sharded=True)
+    with pytest.raises(L.MdrError):
+        _env(noon)._driver_window_vec(20, launch)
+    assert [c[0] for c in calls] == ["begin", "rollout_sharded"]
     del cb
 
 

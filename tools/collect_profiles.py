@@ -1,4 +1,4 @@
-"""Copy a round's rocprofv3 outputs (gpurun_out/round, written by tools/profile_r02.sh) into
+"""Copy a round's rocprofv3 outputs (gpurun_out/round, written by tools/pmc.sh passes) into
 profiles/ under a round prefix and derive profiles/pmc_traffic.json: per kernel and shard size, the
 HBM bytes per launch and the SQ instruction / stall counters.
 
