@@ -177,10 +177,11 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           k_gq_finish ranks and decides; 0 = the bins pass every call (k_gq_bins,
  *                           k_gq_compact, k_gq_select: faster when the budget jumps across the cluster
  *                           every call)
- *   MDR_OPT_GQ_FUSED        mdr_greedy_rollout: 1 (default) = the fused tick, one decision launch per tick
+ *   MDR_OPT_GQ_FUSED        mdr_greedy_rollout: 1 = the fused tick, one decision launch per tick
  *                           (k_gq_decide2: the previous step's epilogue counted the keys and the band's
- *                           houses, the step applies the decision from the pre-step keys); 0 = the
- *                           mdr_ctrl_greedy + mdr_step tick (bit-identical)
+ *                           houses, the step applies the decision from the pre-step keys); 0 (default)
+ *                           = the mdr_ctrl_greedy + mdr_step tick (bit-identical; faster at 1M houses,
+ *                           DESIGN.md §3.3)
  *   MDR_OPT_ACTOR_GENERIC   1 = k_actor runs its generic form for the reference's default obs layout too
  *                           (0, default: that layout runs the form specialised for it, mdr_actor.hip DEF)
  *   MDR_OPT_ACTOR_FP32_FORM the fused actor's MDR_PREC_FP32 arithmetic: MDR_FP32_F16_SPLIT (default) =

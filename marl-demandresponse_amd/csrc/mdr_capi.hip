@@ -137,7 +137,7 @@ struct mdr_ctx {
                                          // (not when its step counted a lookahead there)
   bool gq_band = true;                   // MDR_OPT_GQ_BAND: k_gq_binsc (the predicted band) vs k_gq_bins
   // the fused greedy tick (mdr_greedy_rollout; mdr_kernels.h GqfBufs)
-  bool gq_fused = true;                  // MDR_OPT_GQ_FUSED
+  bool gq_fused = false;                 // MDR_OPT_GQ_FUSED (r06: slower than the band form)
   GqfBufs fz{};
   int64_t fz_cap_n = 0;                  // the cluster size fz is allocated for
   int fz_par = 0;                        // the parity the last producer wrote

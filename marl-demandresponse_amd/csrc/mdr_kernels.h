@@ -201,6 +201,10 @@ __global__ void k_greedy_apply(int64_t n, const int* perm, const int64_t* kpos, 
 constexpr int kGqBins = 16384;  // histogram-select greedy: key bins
 constexpr int kGqCap = 4096;    // candidate window capacity (LDS, 16 B per house)
 constexpr int kGqAfter = 256;   // window houses past the crossing bin (the gap walk's room)
+// the fused tick's room: a walk past the window falls back to gq_exact (one block over the cluster,
+// ~7 ms at 1M houses, r06); with 256 the walk escaped on ~1 tick in 100 (most houses after the
+// crossing locked out), the in-bin ranking costs what the bins hold, not the window
+constexpr int kGqfAfter = 1024;
 constexpr int kGqStage = 4096;  // houses per k_gq_compact block
 constexpr int kGqParts = 256;  // k_gq_keys / k_gq_bins grid (one block per CU)
 constexpr int kGqThreads = 1024; // k_gq_keys / k_gq_bins / k_gq_compact block size

@@ -2459,7 +2459,8 @@ struct GqWin {
 // other copies at multiples of cstride: gq_bins_flush's (g_hist, 512) or the band's (k_gq_binsc).
 // abins (the fused tick): the A class counts in the layout of bins; GqWin.abelow = their sums over
 // superbin sb's bins below bs.
-template <int NC = kGqCopies>  // (NC: the copies to sum; 1: counts summed by the caller)
+// (NC: the copies to sum, 1: counts summed by the caller; AFTER: the houses the window holds past the crossing bin)
+template <int NC = kGqCopies, int AFTER = kGqAfter>
 __device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __restrict__ bins, int cstride, double S,
                            GqSel* __restrict__ sel, int sb, bool all, bool ovf, bool whole, double base_tot,
                            unsigned long long base_cnt, unsigned long long total,
@@ -2538,7 +2539,7 @@ __device__ __forceinline__ GqWin gq_window(const KParams& p, const unsigned* __r
     }
     const unsigned long long c0 = __shfl(c2, 0);
     const unsigned long long fit = __ballot(valid && pre <= (unsigned long long)kGqCap);
-    const unsigned long long enough = __ballot(valid && pre >= c0 + kGqAfter) & fit;
+    const unsigned long long enough = __ballot(valid && pre >= c0 + AFTER) & fit;
     int le;
     if (!(fit & 1ull)) le = 0;  // the crossing bin alone overflows the window
     else if (enough) le = __ffsll((long long)enough) - 1;
@@ -3592,8 +3593,8 @@ __global__ void __launch_bounds__(1024) k_gq_decide2(KParams p, GqfBufs fz, int 
     if (blockIdx.x > 1) return;  // (block-uniform: blocks 0 and 1 decide and map)
     if (asv) atomicAdd(&s_asum[tid & 7], asv);  // (block 0: A_lo, A_all over the copies; zeroed before the scan's barriers)
     const int off = hit ? (g.sb - pb) * 64 * 4 : 0;
-    w = gq_window<1>(p, s_band[0] + off, 0, S, sel, g.sb, path != 0, path == 3, g.whole, g.before, g.before_cnt,
-                     g.total, s_band[1] + off);
+    w = gq_window<1, kGqfAfter>(p, s_band[0] + off, 0, S, sel, g.sb, path != 0, path == 3, g.whole, g.before,
+                                g.before_cnt, g.total, s_band[1] + off);
     if (path == 0 && w.ovf) path = 3;  // (a crossing bin over kGqCap houses)
     GQF_STAMP(3);
     if (blockIdx.x == 1) {  // the next map, beside block 0's decision
@@ -3683,8 +3684,8 @@ __global__ void __launch_bounds__(1024) k_gq_decide2(KParams p, GqfBufs fz, int 
     for (int e = tid; e < 2 * kGqfMissC; e += blockDim.x) lc[e] = ld_sc1(&M[e]);
     if (tid == 0) s_bad = ld_sc1(&M[2 * kGqfMissC + kGqfMissN]) != 0u;
     __syncthreads();
-    const GqWin wm = gq_window(p, lc, 512, S, sel, g.sb, false, false, false, g.before, g.before_cnt, g.total,
-                               lc + kGqfMissC);
+    const GqWin wm = gq_window<kGqCopies, kGqfAfter>(p, lc, 512, S, sel, g.sb, false, false, false, g.before,
+                                                     g.before_cnt, g.total, lc + kGqfMissC);
     xcnt = wm.xcnt;
     __syncthreads();  // (done with lc: the window goes into s_e)
     ovf0 = wm.ovf || s_bad;

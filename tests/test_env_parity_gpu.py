@@ -604,6 +604,7 @@ def test_greedy_fused_matches_per_tick(torch_gpu, n, signal, T):
     torch = torch_gpu
     _, a = _greedy_env(n, 53, signal)
     _, b = _greedy_env(n, 53, signal)
+    a.shard.set_option("gq_fused", 1)
     b.shard.set_option("gq_fused", 0)
     acts_a = torch.empty((T, n), dtype=torch.uint8, device="cuda")
     acts_b = torch.empty((T, n), dtype=torch.uint8, device="cuda")
@@ -632,6 +633,7 @@ def test_greedy_fused_jumping_budgets(torch_gpu, n):
 
     props, a = _greedy_env(n, 59)
     _, b = _greedy_env(n, 59)
+    a.shard.set_option("gq_fused", 1)
     b.shard.set_option("gq_fused", 0)
     T = 32
     ta = a.driver_window(T)
@@ -670,6 +672,7 @@ def test_greedy_fused_exact_and_restart(torch_gpu, case):
 
     n = 60_000
     envs = [_greedy_env(n, 31)[1], _greedy_env(n, 31)[1]]
+    envs[0].shard.set_option("gq_fused", 1)
     envs[1].shard.set_option("gq_fused", 0)
     outs = []
     for e in envs:

@@ -45,6 +45,9 @@ def run_signal(signal, reps, K, n=1 << 20):
         for form, opts in FORMS.items():
             for k, v in opts.items():
                 sh.set_option(k, v)
+            # a form switch restarts the form's key map from its last call's (stale: the state moved
+            # on under the other forms; the first call may fall back to gq_exact): re-warm untimed
+            env.greedy_rollout(8, actions=act, rewards=rew)
             ticks = env.driver_window(K)
             b0, f0, g0 = sh.greedy_band(), sh.greedy_fused_diag(), sh.greedy_diag()
             torch.cuda.synchronize()

@@ -32,6 +32,7 @@ def main():
     env = Environment(props, rng=random.Random(53), population="synthetic", seed=53)
     sh = env.shard
     lib = sh.lib
+    sh.set_option("gq_fused", 1)
     env.greedy_rollout(30)
     L.check(lib.mdr_greedy_fused_stamps(sh.ctx, 1, None), "stamps on")
     names = ["entry", "super_scan", "A_prefix", "window", "gather", "rank", "ticket", "decided", "next_map", "exit",
