@@ -2190,7 +2190,10 @@ __device__ __forceinline__ GqSupLoad gq_super_load(const unsigned* __restrict__ 
   return gq_super_load_at(hist + kGqBins * 4);
 }
 __device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLoad& l, double S, GqSel* __restrict__ sel,
-                                 unsigned long long* __restrict__ slab, bool reset_alloc) {
+                                 unsigned long long* __restrict__ slab, bool reset_alloc,
+                                 unsigned long long* st = nullptr) {
+#define GQS_STAMP(k) \
+  do { if (st && threadIdx.x == 0) st[k] = __builtin_amdgcn_s_memrealtime(); } while (0)
   constexpr int NW = kGqThreads / 64;
   static_assert(kGqSupN <= kGqThreads && kGqCells < kGqThreads, "one superbin / cell edge per thread");
   __shared__ double s_w[NW], s_bt;
@@ -2206,12 +2209,14 @@ __device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLo
     for (int q = 0; q < kGqCopies; ++q) {
       c[0] += l.v[q].x; c[1] += l.v[q].y; c[2] += l.v[q].z; c[3] += l.v[q].w;
     }
+  GQS_STAMP(0);
   const double ps = win_power(p, c, p_on);
   const unsigned long long cs = c[0] + c[1] + c[2] + c[3];
   double x = ps;
   unsigned long long xc = cs;
   if (tid == 0) { s_first = kGqSupN; s_bt = 0.0; s_bc = 0ull; }
   gq_block_scan(x, xc, s_w, s_wc);
+  GQS_STAMP(1);
   const double before = x - ps;
   {  // the first non-empty superbin where the P reaches S: one LDS atomic per wave (same-address LDS
      // atomics serialise: one per thread cost ~4 us here, r06 phase stamps)
@@ -2220,6 +2225,7 @@ __device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLo
   }
   if (tid == kGqSupN - 1) s_total = xc;
   __syncthreads();
+  GQS_STAMP(2);
   const int sb = s_first;
   const bool whole = sb < kGqSupN && s_total <= (unsigned long long)kGqCap;
   if (tid == sb) { s_bt = before; s_bc = xc - cs; }
@@ -2240,6 +2246,8 @@ __device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLo
       for (int e = tid; e < kCountShards * p.n_cap; e += blockDim.x) slab[e] = 0ull;
   }
   __syncthreads();
+  GQS_STAMP(3);
+#undef GQS_STAMP
   return GqSuper{sb, whole, s_bt, s_bc, s_total};
 }
 __device__ __forceinline__ GqSuper gq_super_find(const KParams& p, const unsigned* __restrict__ hist, double S,
@@ -3581,7 +3589,8 @@ __global__ void __launch_bounds__(1024) k_gq_decide2(KParams p, GqfBufs fz, int 
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     GQF_STAMP(16);
   }
-  const GqSuper g = gq_super_scan(p, sup, S, sel, nullptr, false);  // (ends with a block barrier)
+  const GqSuper g = gq_super_scan(p, sup, S, sel, nullptr, false,
+                                  fz.stamps ? fz.stamps + blockIdx.x * kGqfStampWords + 27 : nullptr);  // (ends with a block barrier)
   GQF_STAMP(1);
   const bool all = g.sb >= kGqSupN, nanx = g.sb == kGqSuper && !g.whole;
   const bool hit = !all && !nanx && !g.whole && !bovf && g.sb >= pb && g.sb + 1 < pb + kGqBand;

@@ -36,7 +36,7 @@ def main():
     env.greedy_rollout(30)
     L.check(lib.mdr_greedy_fused_stamps(sh.ctx, 1, None), "stamps on")
     names = ["entry", "super_scan", "A_prefix", "window", "gather", "rank", "ticket", "decided", "next_map", "exit",
-             "lastflag", "apre_done", "d_loaded", "d_cross", "d_walk", "d_counts", "sup_loaded", "A_loaded", "g_counts", "g_loaded", "g_ranked", "-", "-", "t0_ranked", "t0_bar", "-", "-", "bar16_start", "bar16_end", "lds16_end"]
+             "lastflag", "apre_done", "d_loaded", "d_cross", "d_walk", "d_counts", "sup_loaded", "A_loaded", "g_counts", "g_loaded", "g_ranked", "-", "-", "t0_ranked", "t0_bar", "-", "-", "scan_summed", "scan_blockscan", "scan_first", "scan_end"]
     per = {k: [] for k in names}
     lastb, blk0 = {k: [] for k in names}, {k: [] for k in names}
     for _ in range(a.calls):

@@ -1,6 +1,4 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06t
+O=gpurun_out/r06u
 bash tools/gpu_steps.sh $O \
- "1000|gputests|python -u -m pytest tests -m gpu -x -q -p no:cacheprovider --timeout 300 --timeout-method thread" \
- "200|smoke|python -u -c 'import __graft_entry__ as g; g.smoke(); print(\"smoke ok\")'" \
- "300|bench|python -u bench.py"
+ "120|probe|python -u tools/greedy_fused_probe.py"
