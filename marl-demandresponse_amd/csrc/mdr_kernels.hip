@@ -2140,17 +2140,23 @@ __global__ void __launch_bounds__(256) k_gq_range(const double* __restrict__ par
 
 // a block-wide inclusive scan of (double P, u64 count) over the first n <= blockDim.x threads
 // (wave shuffles, then the wave totals through LDS); returns the inclusive values
-__device__ __forceinline__ void gq_block_scan(double& x, unsigned long long& xc, double* s_w, unsigned long long* s_wc) {
+// (nwd: the waves holding data — the superbin and digit scans fill the first 257 / 256 threads; the
+// other waves skip both halves, so the longest serial sum of wave totals is nwd - 1 reads, not 15)
+__device__ __forceinline__ void gq_block_scan(double& x, unsigned long long& xc, double* s_w, unsigned long long* s_wc,
+                                              int nwd = kGqThreads / 64) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (wv < nwd) {
 #pragma unroll
-  for (int off = 1; off < 64; off <<= 1) {
-    const double y = __shfl_up(x, off);
-    const unsigned long long yc = __shfl_up(xc, off);
-    if (lane >= off) { x += y; xc += yc; }
+    for (int off = 1; off < 64; off <<= 1) {
+      const double y = __shfl_up(x, off);
+      const unsigned long long yc = __shfl_up(xc, off);
+      if (lane >= off) { x += y; xc += yc; }
+    }
+    if (lane == 63) { s_w[wv] = x; s_wc[wv] = xc; }
   }
-  if (lane == 63) { s_w[wv] = x; s_wc[wv] = xc; }
   __syncthreads();
-  for (int w = 0; w < wv; ++w) { x += s_w[w]; xc += s_wc[w]; }  // (fixed order: the same sums in every block)
+  if (wv < nwd)
+    for (int w = 0; w < wv; ++w) { x += s_w[w]; xc += s_wc[w]; }  // (fixed order: the same sums in every block)
 }
 
 // relaxed agent-scope (sc1) stores and loads: write-through / L2-served, for data other workgroups of
@@ -2174,10 +2180,16 @@ struct GqSuper {
 // (gq_super_find's scan then waits only for these: vmcnt counts in issue order)
 struct GqSupLoad {
   uint4 v[kGqCopies];
+  double pon[kWinCap];  // the classes' P (issued beside the copies: a scalar load waited for after them cost ~1 us)
 };
+__device__ __forceinline__ void gq_pon_load(const KParams& p, double* pon) {
+#pragma unroll
+  for (int k = 0; k < kWinCap; ++k) pon[k] = p.p_on[k < p.n_cap ? k : 0];
+}
 // sup: the superbin copies (kGqCopies x kGqSupStride words; g_hist + kGqBins * 4, or a fused parity's)
-__device__ __forceinline__ GqSupLoad gq_super_load_at(const unsigned* __restrict__ sup) {
+__device__ __forceinline__ GqSupLoad gq_super_load_at(const KParams& p, const unsigned* __restrict__ sup) {
   GqSupLoad l;
+  gq_pon_load(p, l.pon);
   const int tid = threadIdx.x;
   // (one branch around all the loads: per-load conditions made the compiler wait after every pair)
   const int t = tid < kGqSupN ? tid : 0;
@@ -2186,8 +2198,8 @@ __device__ __forceinline__ GqSupLoad gq_super_load_at(const unsigned* __restrict
   for (int q = 0; q < kGqCopies; ++q) l.v[q] = src[q * (kGqSupStride / 4)];
   return l;  // (threads >= kGqSupN hold superbin 0's counts: gq_super_find ignores them)
 }
-__device__ __forceinline__ GqSupLoad gq_super_load(const unsigned* __restrict__ hist) {
-  return gq_super_load_at(hist + kGqBins * 4);
+__device__ __forceinline__ GqSupLoad gq_super_load(const KParams& p, const unsigned* __restrict__ hist) {
+  return gq_super_load_at(p, hist + kGqBins * 4);
 }
 __device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLoad& l, double S, GqSel* __restrict__ sel,
                                  unsigned long long* __restrict__ slab, bool reset_alloc,
@@ -2200,9 +2212,7 @@ __device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLo
   __shared__ unsigned long long s_wc[NW], s_total, s_bc;
   __shared__ int s_first;
   const int tid = threadIdx.x;
-  double p_on[kWinCap];
-#pragma unroll
-  for (int k = 0; k < kWinCap; ++k) p_on[k] = p.p_on[k < p.n_cap ? k : 0];
+  const double* p_on = l.pon;
   unsigned long long c[kWinCap] = {0ull, 0ull, 0ull, 0ull};
   if (tid < kGqSupN)
 #pragma unroll
@@ -2215,7 +2225,7 @@ __device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLo
   double x = ps;
   unsigned long long xc = cs;
   if (tid == 0) { s_first = kGqSupN; s_bt = 0.0; s_bc = 0ull; }
-  gq_block_scan(x, xc, s_w, s_wc);
+  gq_block_scan(x, xc, s_w, s_wc, (kGqSupN + 63) / 64);
   GQS_STAMP(1);
   const double before = x - ps;
   {  // the first non-empty superbin where the P reaches S: one LDS atomic per wave (same-address LDS
@@ -2253,7 +2263,7 @@ __device__ __forceinline__ GqSuper gq_super_scan(const KParams& p, const GqSupLo
 __device__ __forceinline__ GqSuper gq_super_find(const KParams& p, const unsigned* __restrict__ hist, double S,
                                                  GqSel* __restrict__ sel, unsigned long long* __restrict__ slab,
                                                  bool reset_alloc = true) {
-  return gq_super_scan(p, gq_super_load(hist), S, sel, slab, reset_alloc);
+  return gq_super_scan(p, gq_super_load(p, hist), S, sel, slab, reset_alloc);
 }
 
 // The class counts of the bins of superbins sb and sb + 1 (the crossing superbin and the room after
@@ -2360,7 +2370,7 @@ __device__ void gq_next_map_core(const KParams& p, unsigned* __restrict__ sup, c
     }
   double x = 0.0;
   unsigned long long xc = cs;
-  gq_block_scan(x, xc, s_w, s_wc);
+  gq_block_scan(x, xc, s_w, s_wc, (kGqSupN + 63) / 64);
   if (tid < kGqSuper) { s_pre[tid] = (double)(xc - cs); s_cnt[tid] = (double)cs; }
   if (tid < kGqCells) s_map[tid] = map_in[tid];
   double lo = INFINITY, hi = -INFINITY;
@@ -2720,7 +2730,7 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_binsc(KParams p, const uint32
   // the superbin counts and this block's houses, all issued before the scan's first wait (r05: the
   // per-load conditions of the old form made the compiler wait after every pair of superbin loads,
   // four serialised round trips)
-  const GqSupLoad sup = gq_super_load(hist);
+  const GqSupLoad sup = gq_super_load(p, hist);
   const int pb = sel->band_base;
   const bool band = sel->band_valid != 0;
   uint32_t cd[U], hw[U];
@@ -2850,7 +2860,7 @@ __device__ void gq_exact(const KParams& p, double S, double pmin, uint8_t* __res
     double x = pd;
     unsigned long long xc = cd;
     if (tid == 0) s_d = 256;
-    gq_block_scan(x, xc, s_w, s_wc);
+    gq_block_scan(x, xc, s_w, s_wc, 256 / 64);
     {  // (one LDS atomic per wave: same-address LDS atomics serialise)
       const unsigned long long m = __ballot(tid < 256 && cd > 0 && !(base + (x - pd) + pd < S));
       if (m && (tid & 63) == 0) atomicMin(&s_d, (tid & ~63) + __ffsll((long long)m) - 1);
@@ -3559,6 +3569,7 @@ __global__ void __launch_bounds__(1024) k_gq_decide2(KParams p, GqfBufs fz, int 
   // made 256 blocks x 1024 threads read 33 MB of L2 per call: ~5 us; r06 phase stamps); block 0 (the
   // decider unless the band misses) loads the A summary's copies beside them
   GqSupLoad sup;
+  gq_pon_load(p, sup.pon);
 #pragma unroll
   for (int q = 0; q < kGqCopies; ++q) sup.v[q] = make_uint4(0u, 0u, 0u, 0u);
   if (tid < kGqSupN)

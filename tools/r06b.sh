@@ -1,4 +1,4 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06u
+O=gpurun_out/r06v
 bash tools/gpu_steps.sh $O \
- "120|probe|python -u tools/greedy_fused_probe.py"
+ "600|greedy|python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread -k 'greedy or gq'"
