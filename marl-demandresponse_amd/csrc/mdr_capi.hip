@@ -137,6 +137,7 @@ struct mdr_ctx {
                                          // (not when its step counted a lookahead there)
   bool gq_band = true;                   // MDR_OPT_GQ_BAND: k_gq_binsc (the predicted band) vs k_gq_bins
   // the fused greedy tick (mdr_greedy_rollout; mdr_kernels.h GqfBufs)
+  bool gq_map_stale = true;              // the state was written since the key maps were last built (k_gq_remap)
   bool gq_fused = false;                 // MDR_OPT_GQ_FUSED (r06: slower than the band form)
   GqfBufs fz{};
   int64_t fz_cap_n = 0;                  // the cluster size fz is allocated for
@@ -293,7 +294,7 @@ int refresh_if_dirty(mdr_ctx* c, hipStream_t st) {
 }
 
 int greedy_scratch(mdr_ctx* c, int64_t n);
-int launch_gq_keys(mdr_ctx* c, hipStream_t st, unsigned long long* slab);
+int launch_gq_keys(mdr_ctx* c, hipStream_t st, unsigned long long* slab, bool local_map = true);
 int gq_hist_produce(mdr_ctx* c, hipStream_t st);
 // the histogram select's per-house codes (gq_code, 4 B) live in the sort form's key buffer
 uint32_t* gq_codes(mdr_ctx* c) { return reinterpret_cast<uint32_t*>(c->g_key); }
@@ -710,6 +711,7 @@ int mdr_bind(mdr_ctx* c, const mdr_soa* s) {
   c->bound = true;
   c->counts_ready = false;
   c->coef_dirty = true;
+  c->gq_map_stale = true;
   for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
   c->graphs.clear();
   return MDR_OK;
@@ -729,6 +731,7 @@ int mdr_populate(mdr_ctx* c, const mdr_pop_spec* sp, void* stream) {
   LAUNCH_CHECK("k_populate");
   c->counts_ready = false;
   c->coef_dirty = true;
+  c->gq_map_stale = true;
   return MDR_OK;
 }
 
@@ -1483,11 +1486,23 @@ int gq_hist_produce(mdr_ctx* c, hipStream_t st) {
 
 // the keys and superbin histogram of the current state (when no step epilogue prepared them);
 // slab: zeroed for the decisions' counts (nullptr: none)
-int launch_gq_keys(mdr_ctx* c, hipStream_t st, unsigned long long* slab) {
+int launch_gq_keys(mdr_ctx* c, hipStream_t st, unsigned long long* slab, bool local_map) {
   if (int rc = gq_hist_produce(c, st)) return rc;
   hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_part, c->g_hist,
                      c->g_sel, c->g_map, slab);
   LAUNCH_CHECK("k_gq_keys");
+  // (sharded, local_map = false: every rank's map must stay the one built from the allreduced range)
+  if (c->gq_map_stale && local_map) {  // (a written state: cells over its key range, then the codes again)
+    unsigned char* sel = reinterpret_cast<unsigned char*>(c->g_sel);
+    hipLaunchKernelGGL(k_gq_remap, dim3(1), dim3(256), 0, st, c->kp, (const double*)c->g_part, (int)kGqParts,
+                       c->g_hist + kGqBins * 4, c->g_sel, c->g_map,
+                       reinterpret_cast<double*>(sel + gq_kmin_offset(-1)), reinterpret_cast<double*>(sel + gq_scale_offset(-1)));
+    LAUNCH_CHECK("k_gq_remap");
+    hipLaunchKernelGGL(k_gq_keys, dim3(kGqParts), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_part, c->g_hist,
+                       c->g_sel, c->g_map, slab);
+    LAUNCH_CHECK("k_gq_keys (remapped)");
+    c->gq_map_stale = false;
+  }
   c->gq_nparts = kGqParts;
   c->gq_slab_zeroed = slab != nullptr;
   return MDR_OK;
@@ -1729,6 +1744,19 @@ int mdr_greedy_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, uint8_t* action
       const unsigned g = blocks(c->kp.n, kGqStage);
       hipLaunchKernelGGL(k_gq_keys2, dim3(g), dim3(kGqThreads), 0, st, c->kp, c->fz, par, c->g_part, slab_at(c, c->ring));
       LAUNCH_CHECK("k_gq_keys2");
+      if (c->gq_map_stale) {  // (a written state: parity par's cells over its key range, then the producer again)
+        unsigned char* fs = reinterpret_cast<unsigned char*>(c->fz.sel);
+        hipLaunchKernelGGL(k_gq_remap, dim3(1), dim3(256), 0, st, c->kp, (const double*)c->g_part, (int)g, c->fz.par[par],
+                           c->fz.sel, c->fz.map[par], reinterpret_cast<double*>(fs + gq_kmin_offset(par)),
+                           reinterpret_cast<double*>(fs + gq_scale_offset(par)));
+        LAUNCH_CHECK("k_gq_remap (fused)");
+        hipLaunchKernelGGL(k_zero_u64, dim3(64), dim3(256), 0, st, reinterpret_cast<unsigned long long*>(c->fz.par[par]),
+                           (int64_t)(kGqfParWords / 2));
+        LAUNCH_CHECK("k_zero_u64 (fused producer region, remapped)");
+        hipLaunchKernelGGL(k_gq_keys2, dim3(g), dim3(kGqThreads), 0, st, c->kp, c->fz, par, c->g_part, slab_at(c, c->ring));
+        LAUNCH_CHECK("k_gq_keys2 (remapped)");
+        c->gq_map_stale = false;
+      }
       c->gq_nparts = (int)g;
     }
     for (int t = 0; t < n; ++t) {
@@ -1796,7 +1824,7 @@ int mdr_gq_shard_begin(mdr_ctx* c, void* stream) {
   if (int rc = greedy_scratch(c, c->kp.n)) return rc;
   hipStream_t st = S(stream);
   if (!keys_ready)
-    if (int rc = launch_gq_keys(c, st, nullptr)) return rc;
+    if (int rc = launch_gq_keys(c, st, nullptr, false)) return rc;
   hipLaunchKernelGGL(k_gq_range, dim3(1), dim3(256), 0, st, c->g_part, c->gq_nparts, c->g_range);
   LAUNCH_CHECK("k_gq_range");
   return MDR_OK;
@@ -2106,6 +2134,7 @@ int mdr_params_changed(mdr_ctx* c) {
   drop_begun(c);
   if (!c) return fail(MDR_EARG, "mdr_params_changed: null ctx");
   c->coef_dirty = true;
+  c->gq_map_stale = true;
   return MDR_OK;
 }
 

@@ -238,6 +238,8 @@ void gq_sel_init(void* sel, uint32_t* map);  // host: the first call's key map (
 void gq_diag_of(const void* sel, uint64_t* out);
 void gq_state_of(const void* sel, uint64_t* out);  // gq_diag_of + {sb, bstar, bend, all, overflow, more_after, wcount, need_fb}
 size_t gq_wcount_offset();   // host: byte offsets of GqSel.wcount / .need_fb (sharded select)
+size_t gq_kmin_offset(int fpar);   // host: GqSel.kmin / .scale (fpar < 0), or the fused parity's fkmin / fscale
+size_t gq_scale_offset(int fpar);
 size_t gq_need_fb_offset();  // host: [fallbacks, calls, sum of window sizes, last window]
 __global__ void k_gq_keys(KParams p, uint32_t* code, double* part, unsigned* hist, GqSel* sel,
                           const uint32_t* map, unsigned long long* slab);
@@ -259,6 +261,8 @@ __global__ void k_gq_range(const double* part, int nparts, double* range);
 __global__ void k_gq_keys2(KParams p, GqfBufs fz, int par, double* part, unsigned long long* slab);
 __global__ void k_gq_decide2(KParams p, GqfBufs fz, int par, double S, double pmin, unsigned long long* slab,
                              unsigned* tickets, const double* part, int nparts);
+__global__ void k_gq_remap(KParams p, const double* part, int nparts, unsigned* sup, GqSel* sel, uint32_t* map,
+                           double* kmin_out, double* scale_out);
 void gqf_sel_init(void* sel, uint32_t* map);  // host: the fused record (both parities' cells = gq_sel_init's)
 void gqf_diag_of(const void* sel, uint64_t* out);  // host: {calls, band hits, misses, exact, last mode, last window}
 __global__ void k_greedy_inputs(KParams p, double* key, double* power, uint8_t* lock);

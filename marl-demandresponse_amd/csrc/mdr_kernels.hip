@@ -159,6 +159,8 @@ void gq_band_of(const void* sel, uint64_t* out) {
   out[3] = (uint64_t)kGqBand;
 }
 size_t gq_wcount_offset() { return offsetof(GqSel, wcount); }
+size_t gq_kmin_offset(int fpar) { return fpar < 0 ? offsetof(GqSel, kmin) : offsetof(GqSel, fkmin) + fpar * sizeof(double); }
+size_t gq_scale_offset(int fpar) { return fpar < 0 ? offsetof(GqSel, scale) : offsetof(GqSel, fscale) + fpar * sizeof(double); }
 size_t gq_need_fb_offset() { return offsetof(GqSel, need_fb); }
 void gq_diag_of(const void* sel, uint64_t* out) {
   const GqSel* g = static_cast<const GqSel*>(sel);
@@ -2114,6 +2116,46 @@ __global__ void __launch_bounds__(kGqThreads) k_gq_keys(KParams p, uint32_t* __r
   }
   __syncthreads();
   gq_flush(s_sh, NW, hist, lo, hi, part);
+}
+
+// A fresh key map after the state was written (reset, populate, parameter writes): the keys may lie
+// far outside the map the last call built, so a code pass under it clamps most houses into its end cells
+// and the crossing bin overflows the window (gq_exact: one block over the cluster, ~7 ms at 1M houses).
+// From a first pass's per-block key ranges: cells uniform over the cluster's [min, max] (the calls after
+// rebuild them equi-depth), the superbin copies that pass counted zeroed, the band prediction reset; the
+// caller runs the code pass again.  One block.  map / kmin / scale: the parity's (fused) or the select's.
+__global__ void __launch_bounds__(256) k_gq_remap(KParams p, const double* __restrict__ part, int nparts,
+                                                  unsigned* __restrict__ sup, GqSel* __restrict__ sel,
+                                                  uint32_t* __restrict__ map, double* __restrict__ kmin_out,
+                                                  double* __restrict__ scale_out) {
+  __shared__ double s_lo[4], s_hi[4], s_rng[2];
+  double lo = INFINITY, hi = -INFINITY;
+  for (int b = threadIdx.x; b < nparts; b += blockDim.x) { lo = fmin(lo, part[2 * b]); hi = fmax(hi, part[2 * b + 1]); }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    lo = fmin(lo, __shfl_xor(lo, off));
+    hi = fmax(hi, __shfl_xor(hi, off));
+  }
+  if ((threadIdx.x & 63) == 0) { s_lo[threadIdx.x >> 6] = lo; s_hi[threadIdx.x >> 6] = hi; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double kmin = s_lo[0], kmax = s_hi[0];
+    for (int w = 1; w < 4; ++w) { kmin = fmin(kmin, s_lo[w]); kmax = fmax(kmax, s_hi[w]); }
+    const double range = kmax - kmin;
+    s_rng[0] = kmin == kmin && kmin < INFINITY ? kmin : 0.0;  // (gq_next_map_core's rules)
+    s_rng[1] = range > 0.0 && range < INFINITY ? (double)kGqCells / range : 0.0;
+    *kmin_out = s_rng[0];
+    *scale_out = s_rng[1];
+    sel->band_valid = 0;
+    sel->sb_raw = -1;
+    sel->xprev = 0u;
+  }
+  const int NBE = gq_bins_eff(p.n_global);
+  for (int c = threadIdx.x; c < kGqCells; c += blockDim.x) {
+    const int b0 = c * (NBE / kGqCells), b1 = (c + 1) * (NBE / kGqCells);
+    map[c] = ((uint32_t)b0 << 16) | (uint32_t)(b1 - b0);
+  }
+  for (int e = threadIdx.x; e < kGqCopies * kGqSupStride; e += blockDim.x) sup[e] = 0u;
 }
 
 // sharded histogram select: this shard's finite key range from the producer's per-block parts, as

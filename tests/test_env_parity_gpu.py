@@ -845,3 +845,44 @@ def test_greedy_exact_fallback(torch_gpu, case):
     env._counts_ready = ("greedy", out.data_ptr())
     env.step_tensor(out)
     assert env.cluster.current_power_consumption == float(np.sum(np.where(on, caps / cop, 0.0)))
+
+
+@pytest.mark.parametrize("form", ["band", "fused"])
+def test_greedy_state_write_remaps_keys(torch_gpu, form):
+    """A state write that moves every key far outside the key map the last calls built (here 9 K
+    warmer than target: keys near -9 against a map fitted around 0): the first call after it rebuilds
+    the cells over the new key range (k_gq_remap) instead of clamping the cluster into the map's end
+    cells, whose crossing bin would overflow the window and send the decision to gq_exact (one block
+    over the cluster, ~7 ms at 1M houses).  No exact fallback on that call, and the decisions equal the
+    sort form's (hipCUB radix sort + the reference's sequential rule) on a twin, actions and rewards
+    bit for bit."""
+    torch = torch_gpu
+    from mdr_amd.shard import encode_hvac
+
+    n = 300_017
+    _, a = _greedy_env(n, 71)
+    _, b = _greedy_env(n, 71)
+    a.shard.set_option("gq_fused", 1 if form == "fused" else 0)
+    b.shard.set_option("greedy_sort", 1)
+    outs = []
+    for e in (a, b):
+        e.greedy_rollout(10)
+        sh = e.shard
+        prm = sh.host_params()
+        rs = np.random.RandomState(13)
+        tg = prm["target"].copy()
+        T = tg + 9.0 + rs.normal(0.0, 1.0, n)
+        lock = rs.rand(n) < 0.3
+        sh.t_air.copy_(torch.from_numpy(T).cuda())
+        sh.hvac.copy_(torch.from_numpy(encode_hvac(~lock & (rs.rand(n) < 0.5), lock, rs.randint(0, 60, n))).cuda())
+        sh.params_changed()
+        d0 = (sh.greedy_diag()["fallbacks"], sh.greedy_fused_diag()["exact"])
+        acts = torch.empty((3, n), dtype=torch.uint8, device="cuda")
+        r = e.greedy_rollout(3, actions=acts)[1]
+        d1 = (sh.greedy_diag()["fallbacks"], sh.greedy_fused_diag()["exact"])
+        outs.append((acts.clone(), r.clone(), d1[0] - d0[0], d1[1] - d0[1]))
+    (aa, ra, fa, xa), (ab, rb, _, _) = outs
+    print(form, "exact fallbacks after the write:", fa, xa)
+    assert fa == 0 and xa == 0
+    assert torch.equal(aa, ab)
+    assert torch.equal(ra, rb)

@@ -1,4 +1,4 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06v
+O=gpurun_out/r06x
 bash tools/gpu_steps.sh $O \
- "600|greedy|python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread -k 'greedy or gq'"
+ "300|remapoff|python -u -m pytest tests -m gpu -q -s -p no:cacheprovider --timeout 200 --timeout-method thread -k 'remap'"
