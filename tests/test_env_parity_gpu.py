@@ -592,7 +592,8 @@ def test_greedy_rollout_matches_loop(torch_gpu, strided):
     assert a.cluster.current_power_consumption == b.cluster.current_power_consumption
 
 
-@pytest.mark.parametrize("n,signal,T", [(3001, "sinusoidals", 30), (200_003, "sinusoidals", 40),
+@pytest.mark.parametrize("n,signal,T", [(17, "sinusoidals", 10), (4097, "regular_steps", 20),
+                                        (3001, "sinusoidals", 30), (200_003, "sinusoidals", 40),
                                         (1 << 20, "sinusoidals", 40), (1 << 20, "regular_steps", 40),
                                         (1 << 20, "perlin", 40), (1 << 22, "sinusoidals", 12)])
 def test_greedy_fused_matches_per_tick(torch_gpu, n, signal, T):
