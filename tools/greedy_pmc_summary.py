@@ -15,7 +15,7 @@ import sys
 from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-KERNELS = ["k_step_pipe<2, 0, 0, true>", "k_gq_binsc", "k_gq_finish"]
+KERNELS = ["k_step_pipe<2, 0, 0, 1>", "k_gq_binsc", "k_gq_finish"]
 LINE_KERNEL = ("greedy tick: histogram select (k_gq_binsc, k_gq_finish; codes, superbin and predicted-band "
                "bin counts from the previous k_step_pipe's epilogue) + k_step_pipe")
 

@@ -1,4 +1,2 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06f
-bash tools/gpu_steps.sh $O \
- "300|fused|python -u -m pytest tests/test_env_parity_gpu.py -m gpu -q -s -p no:cacheprovider --timeout 200 --timeout-method thread -k 'fused_matches'"
+bash tools/pmc_greedy.sh gpurun_out/r06pmc
