@@ -300,12 +300,23 @@ __device__ __forceinline__ void split8_trunc(const float* v, bf16x8& hi, bf16x8&
 // The fp16-split form's activation split (PREC 4): hi = fp16(x) rounded to nearest, lo = fp16(x - hi)
 // (the difference is exact in fp32; |lo| <= 2^-11 |x|, its rounding <= 2^-23 |x|).
 __device__ __forceinline__ void split8_f16(const float* v, f16x8& hi, f16x8& lo) {
+  // per pair: hi = both values rounded to f16 in one v_cvt_pk_f16_f32 (RNE), each remainder x - hi as
+  // one mixed-precision FMA reading its half of the packed hi (v_fma_mix_f32: no conversion back to
+  // f32; exact, hi is representable in f32), the remainders packed by a second v_cvt_pk_f16_f32
+  uint32_t h[4], l[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const _Float16 h = (_Float16)v[j];
-    hi[j] = h;
-    lo[j] = (_Float16)sub_s(v[j], (float)h);
+  for (int q = 0; q < 4; ++q) {
+    uint32_t hp, lp;
+    float d0, d1;
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(hp) : "v"(v[2 * q]), "v"(v[2 * q + 1]));
+    asm("v_fma_mix_f32 %0, -1.0, %1, %2 op_sel_hi:[0,1,0]" : "=v"(d0) : "v"(hp), "v"(v[2 * q]));
+    asm("v_fma_mix_f32 %0, -1.0, %1, %2 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "=v"(d1) : "v"(hp), "v"(v[2 * q + 1]));
+    asm("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(lp) : "v"(d0), "v"(d1));
+    h[q] = hp;
+    l[q] = lp;
   }
+  hi = __builtin_bit_cast(f16x8, make_uint4(h[0], h[1], h[2], h[3]));
+  lo = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
 }
 
 template <int PREC, typename T>
