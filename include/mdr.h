@@ -182,6 +182,9 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           houses, the step applies the decision from the pre-step keys); 0 (default)
  *                           = the mdr_ctrl_greedy + mdr_step tick (bit-identical; faster at 1M houses,
  *                           DESIGN.md §3.3)
+ *   MDR_OPT_GQ_ADAPTIVE     mdr_greedy_rollout with the band form: 1 (default) = a tick whose budget change departs
+ *                           from the previous change by more than two superbins' worth of power runs the
+ *                           three-launch form (a band miss costs more); 0 = the band form on every tick
  *   MDR_OPT_ACTOR_GENERIC   1 = k_actor runs its generic form for the reference's default obs layout too
  *                           (0, default: that layout runs the form specialised for it, mdr_actor.hip DEF)
  *   MDR_OPT_ACTOR_FP32_FORM the fused actor's MDR_PREC_FP32 arithmetic: MDR_FP32_F16_SPLIT (default) =
@@ -197,7 +200,7 @@ int mdr_params_changed(mdr_ctx* ctx);
 enum { MDR_OPT_STEP_TPW = 1, MDR_OPT_FASTDIV = 2, MDR_OPT_WINDOW_PIPELINE = 3, MDR_OPT_SHARDED_OVERLAP = 4,
        MDR_OPT_GREEDY_SORT = 5, MDR_OPT_FORCE_HALO = 6, MDR_OPT_WINDOW_THERMAL = 7,
        MDR_OPT_HALO_OVERLAP = 9, MDR_OPT_ACTOR_GENERIC = 10, MDR_OPT_HALO_IN_COUNTS = 12,
-       MDR_OPT_GQ_BAND = 13, MDR_OPT_ACTOR_FP32_FORM = 14, MDR_OPT_GQ_FUSED = 15 };
+       MDR_OPT_GQ_BAND = 13, MDR_OPT_ACTOR_FP32_FORM = 14, MDR_OPT_GQ_FUSED = 15, MDR_OPT_GQ_ADAPTIVE = 16 };
 enum { MDR_FP32_F16_SPLIT = 0, MDR_FP32_BF16_SPLIT3 = 1 };
 /* (8 was MDR_OPT_ACTOR_PINGPONG, a k_actor schedule measured slower and retired in r04: rejected) */
 enum { MDR_THERMAL_EXACT = 0, MDR_THERMAL_AFFINE = 1 };

@@ -137,6 +137,9 @@ struct mdr_ctx {
                                          // (not when its step counted a lookahead there)
   bool gq_band = true;                   // MDR_OPT_GQ_BAND: k_gq_binsc (the predicted band) vs k_gq_bins
   // the fused greedy tick (mdr_greedy_rollout; mdr_kernels.h GqfBufs)
+  bool gq_adaptive = true;               // MDR_OPT_GQ_ADAPTIVE: mdr_greedy_rollout skips the band on budget jumps
+  bool gq_band_skip = false;             // (set around one mdr_ctrl_greedy call by mdr_greedy_rollout)
+  double gq_s1 = NAN, gq_s2 = NAN;       // the last two budgets mdr_greedy_rollout decided for
   bool gq_map_stale = true;              // the state was written since the key maps were last built (k_gq_remap)
   bool gq_fused = false;                 // MDR_OPT_GQ_FUSED (r06: slower than the band form)
   GqfBufs fz{};
@@ -673,6 +676,7 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_HALO_IN_COUNTS: c->halo_in_counts = value != 0; break;
     case MDR_OPT_GQ_BAND: c->gq_band = value != 0; break;
     case MDR_OPT_GQ_FUSED: c->gq_fused = value != 0; break;
+    case MDR_OPT_GQ_ADAPTIVE: c->gq_adaptive = value != 0; break;
     case MDR_OPT_ACTOR_GENERIC: c->actor_generic = value != 0; break;
     case MDR_OPT_ACTOR_FP32_FORM:
       if (value != MDR_FP32_F16_SPLIT && value != MDR_FP32_BF16_SPLIT3)
@@ -712,6 +716,7 @@ int mdr_bind(mdr_ctx* c, const mdr_soa* s) {
   c->counts_ready = false;
   c->coef_dirty = true;
   c->gq_map_stale = true;
+  c->gq_s1 = c->gq_s2 = NAN;
   for (auto& g : c->graphs) hipGraphExecDestroy(g.second.first);
   c->graphs.clear();
   return MDR_OK;
@@ -732,6 +737,7 @@ int mdr_populate(mdr_ctx* c, const mdr_pop_spec* sp, void* stream) {
   c->counts_ready = false;
   c->coef_dirty = true;
   c->gq_map_stale = true;
+  c->gq_s1 = c->gq_s2 = NAN;
   return MDR_OK;
 }
 
@@ -1538,7 +1544,7 @@ int mdr_ctrl_greedy(mdr_ctx* c, double budget, uint8_t* action, void* stream) {
     }
     // the slab was zeroed by the codes' producer (k_gq_keys, or the GQ step: its next slab is this)
     const int nstage = (n + kGqStage - 1) / kGqStage;
-    if (c->gq_band) {
+    if (c->gq_band && !c->gq_band_skip) {
       // the band's two launches: binsc (window from the band and compaction, or the bins), finish
       // (rank + decide, or on a miss window + compaction + decide)
       hipLaunchKernelGGL(k_gq_binsc, dim3(nstage), dim3(kGqThreads), 0, st, c->kp, gq_codes(c), c->g_hist, budget,
@@ -1773,10 +1779,25 @@ int mdr_greedy_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, uint8_t* action
     c->counts_ready = false;
     return MDR_OK;
   }
+  // the adaptive band (MDR_OPT_GQ_ADAPTIVE): the band is predicted from the crossing's
+  // trend, so a budget whose change departs from the last change by more than two superbins' worth of
+  // power (a regular-steps edge, the tick after it) would miss it — that tick runs the three-launch
+  // form (bins -> compact -> select, cheaper than a band miss), decided on the host from the budgets
+  double pavg = 0.0;
+  for (int k = 0; k < c->cfg.n_cap; ++k) pavg += c->cfg.cap_table[k] / c->cfg.cop;
+  pavg /= c->cfg.n_cap > 0 ? c->cfg.n_cap : 1;
+  const double jump = 2.0 * ((double)c->kp.n_global * 64.0 / (double)gq_bins_eff(c->kp.n_global)) * pavg;
   for (int t = 0; t < n; ++t) {
     uint8_t* a = action + (int64_t)t * act_stride;
     double* r = reward + (int64_t)t * rew_stride;
-    if (int rc = mdr_ctrl_greedy(c, ticks[t].s_prev, a, stream)) return rc;
+    const double sb = ticks[t].s_prev;
+    c->gq_band_skip = c->gq_adaptive && c->gq_s1 == c->gq_s1 && c->gq_s2 == c->gq_s2 &&
+                      !(fabs((sb - c->gq_s1) - (c->gq_s1 - c->gq_s2)) <= jump);
+    const int rc0 = mdr_ctrl_greedy(c, sb, a, stream);
+    c->gq_band_skip = false;
+    if (rc0) return rc0;
+    c->gq_s2 = c->gq_s1;
+    c->gq_s1 = sb;
     if (int rc = launch_step(c, a, MDR_ACT_BUFFER, to_tick(&ticks[t]), nullptr, r, 0, MDR_CTRL_GREEDY_KEYS, nullptr,
                              p_out, st))
       return rc;
@@ -2135,6 +2156,7 @@ int mdr_params_changed(mdr_ctx* c) {
   if (!c) return fail(MDR_EARG, "mdr_params_changed: null ctx");
   c->coef_dirty = true;
   c->gq_map_stale = true;
+  c->gq_s1 = c->gq_s2 = NAN;
   return MDR_OK;
 }
 

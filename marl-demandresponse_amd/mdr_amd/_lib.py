@@ -24,7 +24,7 @@ ERRORS = {-1: "MDR_EARG", -2: "MDR_EHIP", -3: "MDR_ERCCL", -4: "MDR_ENOMEM", -5:
 # mdr_set_option (mdr.h): alternative launch forms of the same computation
 OPTIONS = {"step_tpw": 1, "fastdiv": 2, "window_pipeline": 3, "sharded_overlap": 4, "greedy_sort": 5, "halo_overlap": 9, "actor_generic": 10,
            "force_halo": 6, "window_thermal": 7, "halo_in_counts": 12,
-           "gq_band": 13, "actor_fp32_form": 14, "gq_fused": 15}
+           "gq_band": 13, "actor_fp32_form": 14, "gq_fused": 15, "gq_adaptive": 16}
 THERMAL_EXACT, THERMAL_AFFINE = 0, 1
 FP32_F16_SPLIT, FP32_BF16_SPLIT3 = 0, 1  # MDR_OPT_ACTOR_FP32_FORM
 

@@ -5,6 +5,7 @@ bit-exact; temperatures, cluster power and rewards within 1e-5 relative — asse
 tighter (1e-10) since the kernels keep the reference's fp64 operation order; float32 observation
 vectors within 2 float32 ulps of the float64 reference values cast to float32.
 """
+import os
 import random
 
 import numpy as np
@@ -887,3 +888,41 @@ def test_greedy_state_write_remaps_keys(torch_gpu, form):
     assert fa == 0 and xa == 0
     assert torch.equal(aa, ab)
     assert torch.equal(ra, rb)
+
+
+def test_greedy_adaptive_band_on_budget_jumps(torch_gpu):
+    """MDR_OPT_GQ_ADAPTIVE on the regular-steps signal (a budget jump at every step edge,
+    signal_calculator.py:78-98): the ticks whose budget change departs from the last change run the
+    three-launch form instead of a band miss.  Three twins over 400 ticks at 1M houses — adaptive, the
+    band on every tick, the three-launch form on every tick — give the same actions and rewards bit
+    for bit; the adaptive twin skipped the band on some ticks (fewer bins-pass skips recorded than the
+    band-only twin) and never fell back to gq_exact."""
+    torch = torch_gpu
+    from mdr_amd.config import EnvironmentProperties
+    from mdr_amd.environment import Environment
+
+    n, T = 1 << 20, 400
+
+    def make():  # (bench.py's C3 configuration, the reference's marl_env_prop.json, regular-steps signal)
+        p = EnvironmentProperties.from_json(os.path.join(os.path.dirname(__file__), "golden", "marl_env_prop.json"))
+        p.cluster_prop.nb_agents = n
+        p.power_grid_prop.signal_properties.mode = "regular_steps"
+        return Environment(p, rng=random.Random(4), population="synthetic", seed=1234)
+
+    envs = [make() for _ in range(3)]
+    envs[0].shard.set_option("gq_adaptive", 1)
+    envs[1].shard.set_option("gq_adaptive", 0)
+    envs[2].shard.set_option("gq_band", 0)
+    outs = []
+    for e in envs:
+        b0, g0 = e.shard.greedy_band(), e.shard.greedy_diag()
+        acts = torch.empty((T, n), dtype=torch.uint8, device="cuda")
+        r = e.greedy_rollout(T, actions=acts)[1]
+        b1, g1 = e.shard.greedy_band(), e.shard.greedy_diag()
+        outs.append((acts, r, b1["skips"] - b0["skips"], g1["fallbacks"] - g0["fallbacks"]))
+    print("band skips (adaptive, band only):", outs[0][2], outs[1][2], "fallbacks:", [o[3] for o in outs])
+    for o in outs[1:]:
+        assert torch.equal(outs[0][0], o[0])
+        assert torch.equal(outs[0][1], o[1])
+    assert outs[0][2] < outs[1][2]
+    assert outs[0][3] == 0

@@ -3,7 +3,8 @@
 on one context per signal (the drivers are computed before each call's first event):
 
   fused   MDR_OPT_GQ_FUSED 1 (producer epilogue -> k_gq_decide2 -> k_step_pipe GQ 2)
-  band    MDR_OPT_GQ_FUSED 0, MDR_OPT_GQ_BAND 1 (k_gq_binsc skips its bins pass on a band hit)
+  band    MDR_OPT_GQ_FUSED 0, MDR_OPT_GQ_BAND 1, MDR_OPT_GQ_ADAPTIVE 0 (k_gq_binsc skips its bins pass on a hit)
+  adaptive  the band form, ticks with a budget jump on the three-launch form (MDR_OPT_GQ_ADAPTIVE 1)
   noband  MDR_OPT_GQ_FUSED 0, MDR_OPT_GQ_BAND 0 (bins -> compact -> select every tick)
 
 Prints per-tick medians, and the hit / miss counts of the band and of the fused decision.
@@ -24,7 +25,8 @@ import torch  # noqa: E402
 from bench import env_props  # noqa: E402
 from mdr_amd.environment import Environment  # noqa: E402
 
-FORMS = {"fused": {"gq_fused": 1}, "band": {"gq_fused": 0, "gq_band": 1}, "noband": {"gq_fused": 0, "gq_band": 0}}
+FORMS = {"fused": {"gq_fused": 1}, "band": {"gq_fused": 0, "gq_band": 1, "gq_adaptive": 0},
+         "adaptive": {"gq_fused": 0, "gq_band": 1, "gq_adaptive": 1}, "noband": {"gq_fused": 0, "gq_band": 0}}
 
 
 def run_signal(signal, reps, K, n=1 << 20):
@@ -63,7 +65,7 @@ def run_signal(signal, reps, K, n=1 << 20):
             res[form].append(us)
             if form == "fused":
                 h, m = f1["hits"] - f0["hits"], f1["misses"] - f0["misses"]
-            elif form == "band":
+            elif form in ("band", "adaptive"):
                 h, m = b1["skips"] - b0["skips"], (b1["calls"] - b0["calls"]) - (b1["skips"] - b0["skips"])
             else:
                 h, m = 0, 0
