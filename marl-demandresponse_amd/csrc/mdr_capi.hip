@@ -675,7 +675,10 @@ int mdr_set_option(mdr_ctx* c, int option, int64_t value) {
     case MDR_OPT_HALO_OVERLAP: c->halo_overlap = value != 0; break;
     case MDR_OPT_HALO_IN_COUNTS: c->halo_in_counts = value != 0; break;
     case MDR_OPT_GQ_BAND: c->gq_band = value != 0; break;
-    case MDR_OPT_GQ_FUSED: c->gq_fused = value != 0; break;
+    case MDR_OPT_GQ_FUSED:  // (the other form's key map was last fitted to an older state: re-fit it)
+      c->gq_map_stale = c->gq_map_stale || c->gq_fused != (value != 0);
+      c->gq_fused = value != 0;
+      break;
     case MDR_OPT_GQ_ADAPTIVE: c->gq_adaptive = value != 0; break;
     case MDR_OPT_ACTOR_GENERIC: c->actor_generic = value != 0; break;
     case MDR_OPT_ACTOR_FP32_FORM:

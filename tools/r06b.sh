@@ -1,4 +1,4 @@
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT
-O=gpurun_out/r06ae
+O=gpurun_out/r06ag
 bash tools/gpu_steps.sh $O \
- "300|adaptive|python -u -m pytest tests/test_env_parity_gpu.py -m gpu -q -s -p no:cacheprovider --timeout 200 --timeout-method thread -k 'adaptive'"
+ "600|greedy|python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 200 --timeout-method thread -k 'greedy or gq or remap'"
