@@ -183,7 +183,7 @@ int mdr_params_changed(mdr_ctx* ctx);
  *                           = the mdr_ctrl_greedy + mdr_step tick (bit-identical; faster at 1M houses,
  *                           DESIGN.md §3.3)
  *   MDR_OPT_GQ_ADAPTIVE     mdr_greedy_rollout with the band form: 1 (default) = a tick whose budget change departs
- *                           from the previous change by more than two superbins' worth of power runs the
+ *                           from the previous change by more than four superbins' worth of power runs the
  *                           three-launch form (a band miss costs more); 0 = the band form on every tick
  *   MDR_OPT_ACTOR_GENERIC   1 = k_actor runs its generic form for the reference's default obs layout too
  *                           (0, default: that layout runs the form specialised for it, mdr_actor.hip DEF)

@@ -1783,13 +1783,13 @@ int mdr_greedy_rollout(mdr_ctx* c, int n, const mdr_tick* ticks, uint8_t* action
     return MDR_OK;
   }
   // the adaptive band (MDR_OPT_GQ_ADAPTIVE): the band is predicted from the crossing's
-  // trend, so a budget whose change departs from the last change by more than two superbins' worth of
+  // trend, so a budget whose change departs from the last change by more than four superbins' worth of
   // power (a regular-steps edge, the tick after it) would miss it — that tick runs the three-launch
   // form (bins -> compact -> select, cheaper than a band miss), decided on the host from the budgets
   double pavg = 0.0;
   for (int k = 0; k < c->cfg.n_cap; ++k) pavg += c->cfg.cap_table[k] / c->cfg.cop;
   pavg /= c->cfg.n_cap > 0 ? c->cfg.n_cap : 1;
-  const double jump = 2.0 * ((double)c->kp.n_global * 64.0 / (double)gq_bins_eff(c->kp.n_global)) * pavg;
+  const double jump = 4.0 * ((double)c->kp.n_global * 64.0 / (double)gq_bins_eff(c->kp.n_global)) * pavg;
   for (int t = 0; t < n; ++t) {
     uint8_t* a = action + (int64_t)t * act_stride;
     double* r = reward + (int64_t)t * rew_stride;
