@@ -645,9 +645,10 @@ def main():
                                 "last_window_houses": gd["window_last"]}
         bd = sh.greedy_band()  # the predicted band: calls whose bins pass k_gq_binsc skipped, and the misses
         out["greedy_select"]["band"] = {"skips": bd["skips"], "misses": bd["misses"], "band_base": bd["band_base"]}
-        out["greedy_select"]["form"] = ("adaptive band (the predicted band's two launches; budget jumps the host sees "
-                                        "on bins -> compact -> select: MDR_OPT_GQ_ADAPTIVE); the fused one-launch "
-                                        "tick MDR_OPT_GQ_FUSED is off (slower, DESIGN.md 3.3.1)")
+        out["greedy_select"]["form"] = (
+            "bins -> compact -> select every tick (--gq-band 0)" if args.gq_band == 0 else
+            "adaptive band (the predicted band's two launches; budget jumps the host sees on bins -> compact -> "
+            "select: MDR_OPT_GQ_ADAPTIVE); the fused one-launch tick MDR_OPT_GQ_FUSED is off (slower, DESIGN.md 3.3.1)")
     if dactor is not None:
         a = dactor.actor
         flops_house = 2 * sum(l.in_features * l.out_features for l in a.fc)  # 30,400 at F = 50
