@@ -2709,14 +2709,16 @@ __device__ __forceinline__ void gq_compact_houses(const KParams& p, const uint32
     for (int c = 0; c < kWinCap; ++c)
       if (oncnt[c]) atomicAdd(&s_cnt[c], oncnt[c]);
   __syncthreads();
-  if (tid == 0) {
-    unsigned tot = 0u;
-    for (int k = 0; k < NW; ++k) {
-      const unsigned t = s_wt[k];
-      s_wt[k] = tot;
-      tot += t;
+  if (wv == 0) {  // the waves' offsets by one 16-lane scan (r05: a serial loop in thread 0), the block's base
+    const unsigned t = lane < NW ? s_wt[lane] : 0u;
+    unsigned y = t;
+#pragma unroll
+    for (int off = 1; off < NW; off <<= 1) {
+      const unsigned z = __shfl_up(y, off);
+      if (lane >= off) y += z;
     }
-    s_wbase = tot ? atomicAdd(&sel->wcount, tot) : 0u;
+    if (lane < NW) s_wt[lane] = y - t;
+    if (lane == NW - 1) s_wbase = y ? atomicAdd(&sel->wcount, y) : 0u;
   }
   __syncthreads();
   unsigned j = s_wbase + s_wt[wv] + (x - mine);
